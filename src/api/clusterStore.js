@@ -1,0 +1,342 @@
+/**
+ * ClusterStore — framework-agnostic data layer for the AMD GPU plugin.
+ *
+ * Replaces the reference's per-route React provider state
+ * (src/api/IntelGpuDataContext.tsx:96-254, SURVEY.md C3) with a store that:
+ *
+ *   * fetches the DeviceConfig CRD and the operator pods IN PARALLEL
+ *     (reference: 4 serial round-trips, :122-165) — refresh latency is
+ *     max(RTT) instead of Σ RTT;
+ *   * keeps the last good data visible while a refresh is in flight
+ *     (stale-while-revalidate) instead of swapping the page for a Loader;
+ *   * is shared across routes and detail views through `getSharedStore`, so
+ *     a route switch or a Node detail view reuses the cluster snapshot instead
+ *     of starting cold (reference Q7);
+ *   * clears its timeout timers (reference Q6) and drops responses from a
+ *     superseded refresh via a sequence number (the analog of the
+ *     reference's `cancelled` flag, :114/:187);
+ *   * computes GPU node/pod filters and the cluster index once per data
+ *     change (memoised on input identity), not once per render.
+ *
+ * Nodes and pods arrive from Headlamp's `useList` watch through
+ * `setNodes` / `setPods` (same two-track design as reference ADR 002);
+ * `loadLists()` fetches them directly for harnesses without Headlamp.
+ *
+ * The store exposes `subscribe` / `getSnapshot` for React 18's
+ * `useSyncExternalStore`; snapshots are immutable objects.
+ */
+
+import {
+  DEVICE_CONFIG_LIST_PATH,
+  PLUGIN_POD_QUERIES,
+  buildClusterIndex,
+  dedupePods,
+  filterAmdGpuNodes,
+  filterAmdGpuPluginPods,
+  filterGpuRequestingPods,
+  isDeviceConfig,
+  isKubeList,
+  unwrapAll,
+} from './amdgpu.js';
+
+export const DEFAULT_REQUEST_TIMEOUT_MS = 2000;
+
+const defaultClock = {
+  setTimeout: function (fn, ms) { return setTimeout(fn, ms); },
+  clearTimeout: function (h) { clearTimeout(h); },
+  now: function () { return Date.now(); },
+};
+
+/**
+ * Race `promise` against a timer; the timer is always cleared.
+ * @template T
+ * @param {Promise<T>} promise
+ * @param {number} ms
+ * @param {{setTimeout: Function, clearTimeout: Function}} [clock]
+ * @returns {Promise<T>}
+ */
+export function withTimeout(promise, ms, clock) {
+  const c = clock || defaultClock;
+  return new Promise(function (resolve, reject) {
+    let done = false;
+    const h = c.setTimeout(function () {
+      if (done) return;
+      done = true;
+      reject(new Error('Request timed out after ' + ms + 'ms'));
+    }, ms);
+    Promise.resolve(promise).then(
+      function (v) {
+        if (done) return;
+        done = true;
+        c.clearTimeout(h);
+        resolve(v);
+      },
+      function (e) {
+        if (done) return;
+        done = true;
+        c.clearTimeout(h);
+        reject(e);
+      }
+    );
+  });
+}
+
+/**
+ * @typedef {Object} ClusterSnapshot
+ * @property {any[]} deviceConfigs
+ * @property {boolean} pluginInstalled
+ * @property {any[]} gpuNodes
+ * @property {any[]} gpuPods
+ * @property {any[]} pluginPods
+ * @property {boolean} crdAvailable
+ * @property {boolean} loading      true until nodes, pods and the first CRD/pod fetch are in
+ * @property {boolean} refreshing   a refresh is in flight (data above is still valid)
+ * @property {string|null} error
+ * @property {ReturnType<typeof buildClusterIndex>} index
+ * @property {number|null} lastUpdated  ms epoch of the last committed refresh
+ * @property {number} version
+ */
+
+/**
+ * @param {{ request: (path: string) => Promise<any>, timeoutMs?: number,
+ *           clock?: {setTimeout: Function, clearTimeout: Function, now: Function},
+ *           crdPath?: string, pluginPodQueries?: string[],
+ *           onTrace?: (span: {name: string, path: string, start: number, end: number, ok: boolean}) => void }} opts
+ */
+export function createClusterStore(opts) {
+  if (!opts || typeof opts.request !== 'function') throw new Error('createClusterStore: request(path) is required');
+  const request = opts.request;
+  const timeoutMs = opts.timeoutMs || DEFAULT_REQUEST_TIMEOUT_MS;
+  const clock = opts.clock || defaultClock;
+  const crdPath = opts.crdPath || DEVICE_CONFIG_LIST_PATH;
+  const podQueries = opts.pluginPodQueries || PLUGIN_POD_QUERIES;
+  const onTrace = opts.onTrace || null;
+
+  const s = {
+    nodes: null,
+    nodeError: null,
+    pods: null,
+    podError: null,
+    deviceConfigs: [],
+    crdAvailable: false,
+    pluginPods: [],
+    asyncLoaded: false,
+    refreshing: false,
+    asyncError: null,
+    lastUpdated: null,
+  };
+  let seq = 0;
+  let inflight = null;
+  let version = 0;
+  const listeners = [];
+
+  // Memoised derivations keyed on input identity.
+  let memoNodesIn = undefined;
+  let memoGpuNodes = [];
+  let memoPodsIn = undefined;
+  let memoGpuPods = [];
+  let memoIndexKey = [null, null];
+  let memoIndex = buildClusterIndex([], []);
+  let snapshot = null;
+
+  function gpuNodes() {
+    if (s.nodes !== memoNodesIn) {
+      memoNodesIn = s.nodes;
+      memoGpuNodes = s.nodes ? filterAmdGpuNodes(s.nodes) : [];
+    }
+    return memoGpuNodes;
+  }
+  function gpuPods() {
+    if (s.pods !== memoPodsIn) {
+      memoPodsIn = s.pods;
+      memoGpuPods = s.pods ? filterGpuRequestingPods(s.pods) : [];
+    }
+    return memoGpuPods;
+  }
+  function index(n, p) {
+    if (memoIndexKey[0] !== n || memoIndexKey[1] !== p) {
+      memoIndexKey = [n, p];
+      memoIndex = buildClusterIndex(n, p);
+    }
+    return memoIndex;
+  }
+
+  function build() {
+    const n = gpuNodes();
+    const p = gpuPods();
+    const errors = [];
+    if (s.nodeError) errors.push(String(s.nodeError));
+    if (s.podError) errors.push(String(s.podError));
+    if (s.asyncError) errors.push(s.asyncError);
+    version++;
+    return Object.freeze({
+      deviceConfigs: s.deviceConfigs,
+      pluginInstalled: s.deviceConfigs.length > 0 || s.pluginPods.length > 0,
+      gpuNodes: n,
+      gpuPods: p,
+      pluginPods: s.pluginPods,
+      crdAvailable: s.crdAvailable,
+      loading: !s.asyncLoaded || s.nodes === null || s.pods === null,
+      refreshing: s.refreshing,
+      error: errors.length ? errors.join('; ') : null,
+      index: index(n, p),
+      lastUpdated: s.lastUpdated,
+      version: version,
+    });
+  }
+
+  function emit() {
+    snapshot = build();
+    const ls = listeners.slice();
+    for (let i = 0; i < ls.length; i++) ls[i]();
+  }
+
+  function traced(name, path) {
+    const start = clock.now();
+    const p = withTimeout(request(path), timeoutMs, clock);
+    if (!onTrace) return p;
+    return p.then(
+      function (v) {
+        onTrace({ name: name, path: path, start: start, end: clock.now(), ok: true });
+        return v;
+      },
+      function (e) {
+        onTrace({ name: name, path: path, start: start, end: clock.now(), ok: false });
+        throw e;
+      }
+    );
+  }
+
+  /**
+   * Re-fetch the DeviceConfig CRD and operator pods. Resolves once the new
+   * data is committed (or dropped because a newer refresh superseded it).
+   * @returns {Promise<void>}
+   */
+  function refresh() {
+    const my = ++seq;
+    s.refreshing = true;
+    emit();
+    const crd = traced('crd', crdPath).then(
+      function (list) {
+        return isKubeList(list) ? { ok: true, items: list.items.filter(isDeviceConfig) } : { ok: false, items: [] };
+      },
+      function () {
+        // Missing / forbidden / timed-out CRD degrades silently (reference ADR 003).
+        return { ok: false, items: [] };
+      }
+    );
+    const pods = podQueries.map(function (path, i) {
+      return traced('plugin-pods-' + i, path).then(
+        function (list) { return isKubeList(list) ? filterAmdGpuPluginPods(list.items) : []; },
+        function () { return []; }
+      );
+    });
+    const run = Promise.all([crd].concat(pods)).then(
+      function (results) {
+        if (my !== seq) return;
+        const c = results[0];
+        s.crdAvailable = c.ok;
+        s.deviceConfigs = c.items;
+        let found = [];
+        for (let i = 1; i < results.length; i++) found = found.concat(results[i]);
+        s.pluginPods = dedupePods(found);
+        s.asyncError = null;
+        s.asyncLoaded = true;
+        s.refreshing = false;
+        s.lastUpdated = clock.now();
+        emit();
+      },
+      function (err) {
+        if (my !== seq) return;
+        s.asyncError = err instanceof Error ? err.message : String(err);
+        s.asyncLoaded = true;
+        s.refreshing = false;
+        emit();
+      }
+    );
+    inflight = run;
+    return run;
+  }
+
+  /** Feed the Headlamp `useList()` result for nodes (wrappers are unwrapped here). */
+  function setNodes(items, error) {
+    const next = items ? unwrapAll(items) : null;
+    const err = error ? String(error) : null;
+    if (items === null && s.nodes === null && err === s.nodeError) return;
+    s.nodes = next;
+    s.nodeError = err;
+    emit();
+  }
+
+  function setPods(items, error) {
+    const next = items ? unwrapAll(items) : null;
+    const err = error ? String(error) : null;
+    if (items === null && s.pods === null && err === s.podError) return;
+    s.pods = next;
+    s.podError = err;
+    emit();
+  }
+
+  /**
+   * Fetch nodes and pods directly (harness / cold start without Headlamp
+   * hooks). Runs in parallel with nothing else; callers usually do
+   * `Promise.all([store.loadLists(), store.refresh()])`.
+   */
+  function loadLists() {
+    const nodesP = traced('nodes', '/api/v1/nodes').then(
+      function (l) { setNodes(isKubeList(l) ? l.items : [], null); },
+      function (e) { setNodes([], e instanceof Error ? e.message : String(e)); }
+    );
+    const podsP = traced('pods', '/api/v1/pods').then(
+      function (l) { setPods(isKubeList(l) ? l.items : [], null); },
+      function (e) { setPods([], e instanceof Error ? e.message : String(e)); }
+    );
+    return Promise.all([nodesP, podsP]).then(function () {});
+  }
+
+  function subscribe(fn) {
+    listeners.push(fn);
+    return function () {
+      const i = listeners.indexOf(fn);
+      if (i >= 0) listeners.splice(i, 1);
+    };
+  }
+
+  function getSnapshot() {
+    if (!snapshot) snapshot = build();
+    return snapshot;
+  }
+
+  return {
+    subscribe: subscribe,
+    getSnapshot: getSnapshot,
+    setNodes: setNodes,
+    setPods: setPods,
+    refresh: refresh,
+    loadLists: loadLists,
+    /** Promise of the most recent refresh (or a resolved promise). */
+    settled: function () { return inflight || Promise.resolve(); },
+    /** True once a CRD/pod fetch has committed at least once. */
+    hasLoaded: function () { return s.asyncLoaded; },
+  };
+}
+
+// ---------------------------------------------------------------------------
+// Shared stores (one per cluster) — survive route switches and detail views.
+// ---------------------------------------------------------------------------
+
+const shared = {};
+
+/**
+ * @param {string} key  cluster name
+ * @param {() => ReturnType<typeof createClusterStore>} factory
+ */
+export function getSharedStore(key, factory) {
+  const k = key || '__default__';
+  if (!shared[k]) shared[k] = factory();
+  return shared[k];
+}
+
+export function resetSharedStores() {
+  for (const k in shared) delete shared[k];
+}

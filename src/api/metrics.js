@@ -1,0 +1,475 @@
+/**
+ * MI355X telemetry from Prometheus, reached through the Kubernetes service proxy.
+ *
+ * Reference analog: src/api/metrics.ts (SURVEY.md C4), which finds
+ * Prometheus by probing three services serially with no timeout (:77-90),
+ * then runs four instant queries on i915 hwmon series and joins power by
+ * PCI `chip` only (:127-138, quirk Q1).
+ *
+ * This client:
+ *   * probes the candidate services IN PARALLEL with a timeout, keeps the
+ *     highest-priority success, and caches it (TTL) so steady-state
+ *     refreshes skip discovery entirely;
+ *   * reads AMD series — the AMD Device Metrics Exporter (`gpu_*`, per-GPU,
+ *     optionally pod-labelled) and, as a fallback, node-exporter's amdgpu
+ *     hwmon + DRM collectors — in ONE parallel wave, then remembers which
+ *     source answered so later waves only query that one;
+ *   * keys every GPU by (node, gpu index), never by PCI address alone;
+ *   * exposes power, HBM used/total, GFX and memory-controller activity,
+ *     temperature, and `query_range` time series (power / HBM per node);
+ *   * surfaces xGMI per-link throughput when the exporter publishes it.
+ *
+ * Metric and label names marked (verify) must be checked against the
+ * exporter release deployed on the cluster; they are all in `SERIES`.
+ */
+
+import { MI355X, isObject } from './amdgpu.js';
+import { withTimeout, DEFAULT_REQUEST_TIMEOUT_MS } from './clusterStore.js';
+
+/** Candidate Prometheus services, highest priority first (reference metrics.ts:61-65). */
+export const PROMETHEUS_SERVICES = [
+  { namespace: 'monitoring', service: 'kube-prometheus-stack-prometheus', port: '9090' },
+  { namespace: 'monitoring', service: 'prometheus-operated', port: '9090' },
+  { namespace: 'monitoring', service: 'prometheus', port: '9090' },
+];
+
+export function servicePath(svc) {
+  return '/api/v1/namespaces/' + svc.namespace + '/services/' + svc.service + ':' + svc.port + '/proxy';
+}
+
+/**
+ * Series names. Exporter names follow the AMD Device Metrics Exporter field
+ * list (lower-cased); node-exporter names follow its hwmon/drm collectors.
+ * (verify both against the deployed versions)
+ */
+export const SERIES = {
+  exporter: {
+    power: 'gpu_power_usage', // W
+    vramUsed: 'gpu_used_vram', // MiB (verify unit)
+    vramTotal: 'gpu_total_vram', // MiB
+    gfx: 'gpu_gfx_activity', // %
+    umc: 'gpu_umc_activity', // % — HBM controller busy
+    temp: 'gpu_junction_temperature', // °C
+    xgmiRe: 'xgmi_neighbor_[0-6]_tx_throughput', // bytes/s per neighbour
+  },
+  exporterVramUnitBytes: 1024 * 1024,
+  nodeExporter: {
+    chips: 'node_hwmon_chip_names{chip_name="amdgpu"}',
+    power: 'node_hwmon_power_average_watt',
+    powerCap: 'node_hwmon_power_cap_watt',
+    busy: 'node_drm_gpu_busy_percent',
+    vramUsed: 'node_drm_memory_vram_used_bytes',
+    vramTotal: 'node_drm_memory_vram_size_bytes',
+    uname: 'node_uname_info',
+  },
+};
+
+/** Discovery cache lifetime. Prometheus services move rarely. */
+export const DISCOVERY_TTL_MS = 5 * 60 * 1000;
+
+/**
+ * @typedef {Object} GpuTelemetry
+ * @property {string} nodeName
+ * @property {string} gpu            device index on the node ("0".."7")
+ * @property {string} instance
+ * @property {number|null} powerWatts
+ * @property {number|null} powerCapWatts
+ * @property {number|null} vramUsedBytes
+ * @property {number|null} vramTotalBytes
+ * @property {number|null} gfxActivityPct
+ * @property {number|null} memActivityPct
+ * @property {number|null} tempC
+ * @property {string|null} pod
+ * @property {string|null} namespace
+ *
+ * @typedef {Object} GpuMetrics
+ * @property {'amd-exporter'|'node-exporter'|null} source
+ * @property {GpuTelemetry[]} gpus
+ * @property {Record<string, Record<string, number>>} xgmi  node → "src-dst" → GB/s
+ * @property {string} fetchedAt
+ * @property {string} prometheusPath
+ */
+
+function num(v) {
+  const f = parseFloat(v);
+  return isFinite(f) ? f : null;
+}
+
+function emptyGpu(nodeName, gpu, instance) {
+  return {
+    nodeName: nodeName, gpu: gpu, instance: instance,
+    powerWatts: null, powerCapWatts: null, vramUsedBytes: null, vramTotalBytes: null,
+    gfxActivityPct: null, memActivityPct: null, tempC: null, pod: null, namespace: null,
+  };
+}
+
+/** Sort GPUs by node then numeric device index. */
+function byNodeGpu(a, b) {
+  if (a.nodeName !== b.nodeName) return a.nodeName < b.nodeName ? -1 : 1;
+  return parseInt(a.gpu, 10) - parseInt(b.gpu, 10);
+}
+
+/**
+ * Join AMD Device Metrics Exporter instant vectors into per-GPU telemetry.
+ * Keyed by (hostname, gpu_id). Exported for direct unit tests.
+ */
+export function joinExporterResults(r) {
+  const E = SERIES.exporter;
+  const map = {};
+  function slot(m) {
+    const node = m.hostname || m.node || m.instance || '';
+    const gpu = m.gpu_id !== undefined ? String(m.gpu_id) : '0';
+    const k = node + '\u0000' + gpu;
+    if (!map[k]) map[k] = emptyGpu(node, gpu, m.instance || '');
+    return map[k];
+  }
+  function each(list, fn) {
+    if (!Array.isArray(list)) return;
+    for (let i = 0; i < list.length; i++) {
+      const row = list[i];
+      if (!row || !isObject(row.metric) || !Array.isArray(row.value)) continue;
+      fn(slot(row.metric), num(row.value[1]), row.metric);
+    }
+  }
+  each(r[E.power], function (g, v, m) {
+    g.powerWatts = v;
+    if (m.pod) {
+      g.pod = m.pod;
+      g.namespace = m.namespace || null;
+    }
+  });
+  each(r[E.vramUsed], function (g, v) { g.vramUsedBytes = v === null ? null : v * SERIES.exporterVramUnitBytes; });
+  each(r[E.vramTotal], function (g, v) { g.vramTotalBytes = v === null ? null : v * SERIES.exporterVramUnitBytes; });
+  each(r[E.gfx], function (g, v) { g.gfxActivityPct = v; });
+  each(r[E.umc], function (g, v) { g.memActivityPct = v; });
+  each(r[E.temp], function (g, v) { g.tempC = v; });
+  const gpus = [];
+  for (const k in map) {
+    const g = map[k];
+    if (g.powerCapWatts === null) g.powerCapWatts = MI355X.tdpWatts;
+    gpus.push(g);
+  }
+  gpus.sort(byNodeGpu);
+
+  // xGMI: neighbour k of GPU i is the k-th peer in index order, skipping i (verify).
+  const xgmi = {};
+  const xr = r.__xgmi;
+  if (Array.isArray(xr)) {
+    for (let i = 0; i < xr.length; i++) {
+      const m = xr[i].metric || {};
+      const name = m.__name__ || '';
+      const mm = /^xgmi_neighbor_(\d)_tx_throughput$/.exec(name);
+      if (!mm) continue;
+      const src = parseInt(m.gpu_id, 10);
+      const k = parseInt(mm[1], 10);
+      const dst = k < src ? k : k + 1;
+      const node = m.hostname || m.instance || '';
+      if (!xgmi[node]) xgmi[node] = {};
+      const v = num(xr[i].value[1]);
+      if (v !== null) xgmi[node][src + '-' + dst] = v / 1e9;
+    }
+  }
+  return { gpus: gpus, xgmi: xgmi };
+}
+
+/**
+ * Join node-exporter hwmon (power, keyed by PCI chip) and DRM (busy %, VRAM,
+ * keyed by card) series. Within one instance the k-th amdgpu chip in PCI
+ * order is card k — DRM cards enumerate in PCI order on amdgpu (verify).
+ */
+export function joinNodeExporterResults(r) {
+  const N = SERIES.nodeExporter;
+  const instToNode = {};
+  const un = r[N.uname] || [];
+  for (let i = 0; i < un.length; i++) {
+    const m = un[i].metric || {};
+    if (m.instance) instToNode[m.instance] = m.nodename || m.node || m.instance;
+  }
+  const chipsByInst = {};
+  const chips = r[N.chips] || [];
+  for (let i = 0; i < chips.length; i++) {
+    const m = chips[i].metric || {};
+    if (!m.instance || !m.chip) continue;
+    if (!chipsByInst[m.instance]) chipsByInst[m.instance] = [];
+    if (chipsByInst[m.instance].indexOf(m.chip) < 0) chipsByInst[m.instance].push(m.chip);
+  }
+  const map = {};
+  const gpus = [];
+  for (const inst in chipsByInst) {
+    const list = chipsByInst[inst].sort();
+    for (let k = 0; k < list.length; k++) {
+      const g = emptyGpu(instToNode[inst] || inst, String(k), inst);
+      map[inst + '\u0000chip:' + list[k]] = g;
+      map[inst + '\u0000card:card' + k] = g;
+      gpus.push(g);
+    }
+  }
+  function each(list, keyFn, fn) {
+    if (!Array.isArray(list)) return;
+    for (let i = 0; i < list.length; i++) {
+      const m = list[i].metric || {};
+      const g = map[(m.instance || '') + '\u0000' + keyFn(m)];
+      if (g) fn(g, num(list[i].value[1]));
+    }
+  }
+  function chipKey(m) { return 'chip:' + (m.chip || ''); }
+  function cardKey(m) { return 'card:' + (m.card || ''); }
+  each(r[N.power], chipKey, function (g, v) { g.powerWatts = v; });
+  each(r[N.powerCap], chipKey, function (g, v) { g.powerCapWatts = v; });
+  each(r[N.busy], cardKey, function (g, v) { g.gfxActivityPct = v; });
+  each(r[N.vramUsed], cardKey, function (g, v) { g.vramUsedBytes = v; });
+  each(r[N.vramTotal], cardKey, function (g, v) { g.vramTotalBytes = v; });
+  gpus.sort(byNodeGpu);
+  return { gpus: gpus, xgmi: {} };
+}
+
+function exporterQueries() {
+  const E = SERIES.exporter;
+  return [
+    [E.power, E.power],
+    [E.vramUsed, E.vramUsed],
+    [E.vramTotal, E.vramTotal],
+    [E.gfx, E.gfx],
+    [E.umc, E.umc],
+    [E.temp, E.temp],
+    ['__xgmi', '{__name__=~"' + E.xgmiRe + '"}'],
+  ];
+}
+
+function nodeExporterQueries() {
+  const N = SERIES.nodeExporter;
+  return [
+    [N.chips, N.chips],
+    [N.power, N.power],
+    [N.powerCap, N.powerCap],
+    [N.busy, N.busy],
+    [N.vramUsed, N.vramUsed],
+    [N.vramTotal, N.vramTotal],
+    [N.uname, N.uname],
+  ];
+}
+
+/**
+ * @param {{ request: (path: string) => Promise<any>, timeoutMs?: number,
+ *           clock?: {setTimeout: Function, clearTimeout: Function, now: Function},
+ *           services?: Array<{namespace: string, service: string, port: string}>,
+ *           discoveryTtlMs?: number,
+ *           onTrace?: (span: {name: string, path: string, start: number, end: number, ok: boolean}) => void }} opts
+ */
+export function createMetricsSource(opts) {
+  const request = opts.request;
+  const timeoutMs = opts.timeoutMs || DEFAULT_REQUEST_TIMEOUT_MS;
+  const clock = opts.clock || { setTimeout: setTimeout, clearTimeout: clearTimeout, now: Date.now };
+  const services = opts.services || PROMETHEUS_SERVICES;
+  const ttl = opts.discoveryTtlMs === undefined ? DISCOVERY_TTL_MS : opts.discoveryTtlMs;
+  const onTrace = opts.onTrace || null;
+
+  let cachedPath = null;
+  let cachedAt = 0;
+  let discovering = null;
+  let source = null; // which exporter answered last time
+
+  function get(name, path) {
+    const start = clock.now();
+    const p = withTimeout(request(path), timeoutMs, clock);
+    if (!onTrace) return p;
+    return p.then(
+      function (v) { onTrace({ name: name, path: path, start: start, end: clock.now(), ok: true }); return v; },
+      function (e) { onTrace({ name: name, path: path, start: start, end: clock.now(), ok: false }); throw e; }
+    );
+  }
+
+  function probe(svc) {
+    const base = servicePath(svc);
+    return get('probe', base + '/api/v1/query?query=1').then(
+      function (raw) { return raw && raw.status === 'success' ? base : null; },
+      function () { return null; }
+    );
+  }
+
+  /** Base proxy path of a reachable Prometheus, or null. Parallel probes, cached. */
+  function discover() {
+    if (cachedPath && clock.now() - cachedAt < ttl) return Promise.resolve(cachedPath);
+    if (discovering) return discovering;
+    discovering = Promise.all(services.map(probe)).then(function (paths) {
+      discovering = null;
+      for (let i = 0; i < paths.length; i++) {
+        if (paths[i]) {
+          cachedPath = paths[i];
+          cachedAt = clock.now();
+          return cachedPath;
+        }
+      }
+      cachedPath = null;
+      return null;
+    });
+    return discovering;
+  }
+
+  function invalidate() {
+    cachedPath = null;
+    source = null;
+  }
+
+  function instant(base, q) {
+    return get('query', base + '/api/v1/query?query=' + encodeURIComponent(q)).then(function (raw) {
+      if (!raw || raw.status !== 'success' || !raw.data || !Array.isArray(raw.data.result)) return [];
+      return raw.data.result;
+    });
+  }
+
+  function runWave(base, pairs) {
+    return Promise.all(
+      pairs.map(function (p) {
+        return instant(base, p[1]).then(
+          function (res) { return [p[0], res, true]; },
+          function () { return [p[0], [], false]; }
+        );
+      })
+    ).then(function (rows) {
+      const out = {};
+      let anyOk = false;
+      for (let i = 0; i < rows.length; i++) {
+        out[rows[i][0]] = rows[i][1];
+        if (rows[i][2]) anyOk = true;
+      }
+      out.__anyOk = anyOk;
+      return out;
+    });
+  }
+
+  /**
+   * One metrics snapshot. Resolves to null when no Prometheus is reachable
+   * (the page's "Prometheus Unreachable" state).
+   * @returns {Promise<GpuMetrics|null>}
+   */
+  function fetchGpuMetrics() {
+    return discover().then(function (base) {
+      if (!base) return null;
+      const wantExp = source === null || source === 'amd-exporter';
+      const wantNe = source === null || source === 'node-exporter';
+      const waves = [
+        wantExp ? runWave(base, exporterQueries()) : Promise.resolve(null),
+        wantNe ? runWave(base, nodeExporterQueries()) : Promise.resolve(null),
+      ];
+      return Promise.all(waves).then(function (res) {
+        const exp = res[0];
+        const ne = res[1];
+        if ((!exp || !exp.__anyOk) && (!ne || !ne.__anyOk)) {
+          // Prometheus went away between discovery and query.
+          invalidate();
+          return null;
+        }
+        let joined = { gpus: [], xgmi: {} };
+        let src = null;
+        if (exp) {
+          const j = joinExporterResults(exp);
+          if (j.gpus.length) {
+            joined = j;
+            src = 'amd-exporter';
+          }
+        }
+        if (!src && ne) {
+          const j = joinNodeExporterResults(ne);
+          if (j.gpus.length) {
+            joined = j;
+            src = 'node-exporter';
+          }
+        }
+        source = src;
+        return {
+          source: src,
+          gpus: joined.gpus,
+          xgmi: joined.xgmi,
+          fetchedAt: new Date(clock.now()).toISOString(),
+          prometheusPath: base,
+        };
+      });
+    });
+  }
+
+  /**
+   * Per-node power and HBM-used time series over the last `rangeSec`.
+   * Server-side `sum by (hostname)` keeps the payload O(nodes × points).
+   * @returns {Promise<{ power: Record<string, Array<[number, number]>>, vram: Record<string, Array<[number, number]>> } | null>}
+   */
+  function fetchSeries(rangeSec, stepSec) {
+    const range = rangeSec || 1800;
+    const step = stepSec || 30;
+    return discover().then(function (base) {
+      if (!base) return null;
+      const end = Math.floor(clock.now() / 1000);
+      const start = end - range;
+      const E = SERIES.exporter;
+      const qs = [
+        ['power', 'sum by (hostname) (' + E.power + ')', 1],
+        ['vram', 'sum by (hostname) (' + E.vramUsed + ')', SERIES.exporterVramUnitBytes],
+      ];
+      return Promise.all(
+        qs.map(function (q) {
+          const path = base + '/api/v1/query_range?query=' + encodeURIComponent(q[1]) +
+            '&start=' + start + '&end=' + end + '&step=' + step;
+          return get('query_range', path).then(
+            function (raw) {
+              const out = {};
+              const res = raw && raw.status === 'success' && raw.data && Array.isArray(raw.data.result) ? raw.data.result : [];
+              for (let i = 0; i < res.length; i++) {
+                const node = (res[i].metric && (res[i].metric.hostname || res[i].metric.instance)) || 'cluster';
+                const vals = Array.isArray(res[i].values) ? res[i].values : [];
+                out[node] = vals.map(function (v) { return [v[0], (num(v[1]) || 0) * q[2]]; });
+              }
+              return [q[0], out];
+            },
+            function () { return [q[0], {}]; }
+          );
+        })
+      ).then(function (rows) {
+        const out = {};
+        for (let i = 0; i < rows.length; i++) out[rows[i][0]] = rows[i][1];
+        return out;
+      });
+    });
+  }
+
+  return {
+    discover: discover,
+    invalidate: invalidate,
+    fetchGpuMetrics: fetchGpuMetrics,
+    fetchSeries: fetchSeries,
+    source: function () { return source; },
+  };
+}
+
+/** Cluster totals for the summary box. */
+export function summarizeMetrics(m) {
+  let power = 0;
+  let cap = 0;
+  let vramUsed = 0;
+  let vramTotal = 0;
+  let gfx = 0;
+  let gfxN = 0;
+  let withPower = 0;
+  for (let i = 0; i < m.gpus.length; i++) {
+    const g = m.gpus[i];
+    if (g.powerWatts !== null) {
+      power += g.powerWatts;
+      withPower++;
+    }
+    if (g.powerCapWatts !== null) cap += g.powerCapWatts;
+    if (g.vramUsedBytes !== null) vramUsed += g.vramUsedBytes;
+    if (g.vramTotalBytes !== null) vramTotal += g.vramTotalBytes;
+    if (g.gfxActivityPct !== null) {
+      gfx += g.gfxActivityPct;
+      gfxN++;
+    }
+  }
+  return {
+    gpus: m.gpus.length,
+    withPower: withPower,
+    powerWatts: power,
+    powerCapWatts: cap,
+    vramUsedBytes: vramUsed,
+    vramTotalBytes: vramTotal,
+    avgGfxActivityPct: gfxN ? gfx / gfxN : null,
+  };
+}

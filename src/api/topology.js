@@ -1,0 +1,115 @@
+/**
+ * MI355X node topology: per-GPU allocation slots and the xGMI neighbour matrix.
+ *
+ * Not present in the reference (it has no topology concept — SURVEY.md §7.1
+ * "Topology | none"). An 8×MI355X node is a point-to-point xGMI full mesh:
+ * every GPU has 7 links, one to each peer, ≈153 GB/s per link (task brief /
+ * MI355X_MICROARCH.md). Ring collectives over that mesh are per-link bound,
+ * which is why the panel shows per-link figures rather than one node number.
+ *
+ * Kubernetes does not expose which device a pod holds. When the metrics
+ * exporter attaches `pod`/`namespace` labels to per-GPU series, slots are
+ * exact; otherwise they are filled in pod order and flagged `inferred`.
+ */
+
+import { MI355X, getNodeGpuCount, getPodGpuCount, get } from './amdgpu.js';
+
+/**
+ * @typedef {{ index: number, pod: string|null, namespace: string|null, inferred: boolean }} GpuSlot
+ */
+
+/**
+ * @param {any} node
+ * @param {any[]} podsOnNode  GPU pods bound to the node
+ * @param {Array<{gpu: string, pod?: string|null, namespace?: string|null}>} [perGpuOwners]
+ *        exporter-derived owners keyed by gpu index (as string)
+ * @returns {{ slots: GpuSlot[], exact: boolean }}
+ */
+export function buildGpuSlots(node, podsOnNode, perGpuOwners) {
+  const n = getNodeGpuCount(node) || 0;
+  const slots = [];
+  for (let i = 0; i < n; i++) slots.push({ index: i, pod: null, namespace: null, inferred: false });
+  if (perGpuOwners && perGpuOwners.length) {
+    for (let i = 0; i < perGpuOwners.length; i++) {
+      const o = perGpuOwners[i];
+      const idx = parseInt(o.gpu, 10);
+      if (idx >= 0 && idx < n && o.pod) {
+        slots[idx].pod = o.pod;
+        slots[idx].namespace = o.namespace || null;
+      }
+    }
+    return { slots: slots, exact: true };
+  }
+  let next = 0;
+  for (let p = 0; p < podsOnNode.length; p++) {
+    const pod = podsOnNode[p];
+    const phase = get(pod, ['status', 'phase'], '');
+    if (phase === 'Succeeded' || phase === 'Failed') continue;
+    const g = getPodGpuCount(pod);
+    for (let k = 0; k < g && next < n; k++, next++) {
+      slots[next].pod = pod.metadata.name;
+      slots[next].namespace = pod.metadata.namespace || null;
+      slots[next].inferred = true;
+    }
+  }
+  return { slots: slots, exact: false };
+}
+
+/**
+ * xGMI neighbour matrix for one node.
+ *
+ * @param {number} gpuCount
+ * @param {Record<string, number>} [measured]  `${src}-${dst}` → GB/s observed
+ *        (exporter xGMI throughput series), optional
+ * @param {Record<string, {type: string, hops: number}>} [probed]  `${src}-${dst}` →
+ *        link type/hops from the native probe (hipExtGetLinkTypeAndHopCount)
+ * @returns {{ size: number, cells: Array<Array<{ kind: 'self'|'xgmi'|'pcie'|'none', hops: number, peakGBs: number, measuredGBs: number|null }>>,
+ *             linksPerGpu: number, perGpuPeakGBs: number, ringBusGBs: number }}
+ */
+export function buildXgmiMatrix(gpuCount, measured, probed) {
+  const n = gpuCount > 0 ? gpuCount : 0;
+  const cells = [];
+  let linksPerGpu = 0;
+  for (let i = 0; i < n; i++) {
+    const row = [];
+    let links = 0;
+    for (let j = 0; j < n; j++) {
+      if (i === j) {
+        row.push({ kind: 'self', hops: 0, peakGBs: 0, measuredGBs: null });
+        continue;
+      }
+      const key = i + '-' + j;
+      let kind = 'xgmi';
+      let hops = 1;
+      if (probed && probed[key]) {
+        kind = probed[key].type === 'XGMI' ? 'xgmi' : probed[key].type === 'PCIE' ? 'pcie' : 'none';
+        hops = probed[key].hops;
+      }
+      const m = measured && typeof measured[key] === 'number' ? measured[key] : null;
+      if (kind === 'xgmi') links++;
+      row.push({ kind: kind, hops: hops, peakGBs: kind === 'xgmi' ? MI355X.xgmiLinkGBs : 0, measuredGBs: m });
+    }
+    if (links > linksPerGpu) linksPerGpu = links;
+    cells.push(row);
+  }
+  return {
+    size: n,
+    cells: cells,
+    linksPerGpu: linksPerGpu,
+    perGpuPeakGBs: linksPerGpu * MI355X.xgmiLinkGBs,
+    // A ring all-reduce moves each byte over one link per step, so its bus
+    // bandwidth is bounded by a single link, not by the sum of the mesh.
+    ringBusGBs: linksPerGpu > 0 ? MI355X.xgmiLinkGBs : 0,
+  };
+}
+
+/** True when the matrix is the full point-to-point mesh an 8×MI355X node should have. */
+export function isFullMesh(matrix) {
+  if (matrix.size < 2) return false;
+  for (let i = 0; i < matrix.size; i++) {
+    for (let j = 0; j < matrix.size; j++) {
+      if (i !== j && (matrix.cells[i][j].kind !== 'xgmi' || matrix.cells[i][j].hops !== 1)) return false;
+    }
+  }
+  return true;
+}

@@ -1,0 +1,141 @@
+/**
+ * View IR → static semantic HTML.
+ *
+ * Uses the same element mapping the reference's component tests use to mock
+ * Headlamp CommonComponents (src/components/OverviewPage.test.tsx:8-61):
+ * SectionBox → <section><h2>, SectionHeader → <h1>, NameValueTable → <dl>,
+ * SimpleTable → <table>, StatusLabel → <span data-status>, Loader →
+ * data-testid="loader", PercentageBar → data-testid="percentage-bar".
+ *
+ * Used by the Node-side tests and by the benchmark to measure "rows
+ * rendered" on real output; the shipped plugin renders the IR with React
+ * (src/components/View.tsx).
+ */
+
+function esc(s) {
+  return String(s)
+    .replace(/&/g, '&amp;')
+    .replace(/</g, '&lt;')
+    .replace(/>/g, '&gt;')
+    .replace(/"/g, '&quot;');
+}
+
+export function renderValue(v) {
+  if (v === null || v === undefined) return '';
+  if (typeof v === 'string' || typeof v === 'number') return esc(v);
+  switch (v.t) {
+    case 'status':
+      return '<span data-status="' + esc(v.status) + '">' + esc(v.text) + '</span>';
+    case 'bar':
+      return (
+        '<div class="bar"' + (v.pct === null ? '' : ' data-pct="' + v.pct + '"') + ' data-color="' + esc(v.color) + '">' +
+        '<span>' + esc(v.text) + '</span></div>'
+      );
+    case 'lines':
+      return v.lines
+        .map(function (l) {
+          return '<div>' + (l.label ? '<strong>' + esc(l.label) + '</strong>: ' : '') + esc(l.text) + '</div>';
+        })
+        .join('');
+    default:
+      return '';
+  }
+}
+
+function renderBlock(b) {
+  switch (b.t) {
+    case 'kv':
+      return (
+        '<dl>' +
+        b.rows.map(function (r) { return '<div><dt>' + esc(r.name) + '</dt><dd>' + renderValue(r.value) + '</dd></div>'; }).join('') +
+        '</dl>'
+      );
+    case 'table':
+      return (
+        '<table><thead><tr>' +
+        b.columns.map(function (c) { return '<th>' + esc(c) + '</th>'; }).join('') +
+        '</tr></thead><tbody>' +
+        b.rows
+          .map(function (r) { return '<tr>' + r.map(function (c) { return '<td>' + renderValue(c) + '</td>'; }).join('') + '</tr>'; })
+          .join('') +
+        '</tbody></table>'
+      );
+    case 'pctbar':
+      return (
+        '<div><div>' + esc(b.label) + '</div><div data-testid="percentage-bar" data-total="' + b.total + '">' +
+        b.data.map(function (d) { return '<i data-name="' + esc(d.name) + '" data-value="' + d.value + '"></i>'; }).join('') +
+        '</div></div>'
+      );
+    case 'slots':
+      return (
+        '<ol data-testid="gpu-slots" data-exact="' + (b.exact ? 'true' : 'false') + '">' +
+        b.slots
+          .map(function (s) {
+            return '<li data-gpu="' + s.index + '"' + (s.pod ? ' data-pod="' + esc(s.pod) + '"' : '') + '>' +
+              'GPU ' + s.index + ': ' + (s.pod ? esc(s.pod) + (s.inferred ? ' (inferred)' : '') : 'free') + '</li>';
+          })
+          .join('') +
+        '</ol>'
+      );
+    case 'matrix': {
+      const m = b.matrix;
+      let h = '<table data-testid="xgmi-matrix" data-full-mesh="' + (b.fullMesh ? 'true' : 'false') + '"><thead><tr><th></th>';
+      for (let j = 0; j < m.size; j++) h += '<th>GPU ' + j + '</th>';
+      h += '</tr></thead><tbody>';
+      for (let i = 0; i < m.size; i++) {
+        h += '<tr><th>GPU ' + i + '</th>';
+        for (let j = 0; j < m.size; j++) {
+          const c = m.cells[i][j];
+          h += '<td data-kind="' + c.kind + '">' + (c.kind === 'self' ? '—' : c.kind === 'xgmi'
+            ? (c.measuredGBs !== null ? c.measuredGBs.toFixed(1) + '/' : '') + c.peakGBs + ' GB/s'
+            : c.kind) + '</td>';
+        }
+        h += '</tr>';
+      }
+      return h + '</tbody></table>';
+    }
+    case 'series': {
+      const nodes = Object.keys(b.power || {});
+      return '<div data-testid="series" data-nodes="' + nodes.length + '">' +
+        nodes.map(function (n) { return '<div data-node="' + esc(n) + '" data-points="' + b.power[n].length + '"></div>'; }).join('') +
+        '</div>';
+    }
+    default:
+      return '';
+  }
+}
+
+export function renderSection(s) {
+  if (!s) return '';
+  return '<section><h2>' + esc(s.title) + '</h2>' + s.blocks.map(renderBlock).join('') + '</section>';
+}
+
+export function renderPage(vm) {
+  let h = '';
+  if (vm.title) {
+    h += '<header><h1>' + esc(vm.title) + '</h1>';
+    if (vm.refresh) {
+      h += '<button aria-label="' + esc(vm.refresh.ariaLabel) + '"' + (vm.refresh.disabled ? ' disabled' : '') + '>' +
+        esc(vm.refresh.label) + '</button>';
+    }
+    h += '</header>';
+  }
+  for (let i = 0; i < vm.items.length; i++) {
+    const it = vm.items[i];
+    if (it.t === 'loader') h += '<div data-testid="loader">' + esc(it.title) + '</div>';
+    else h += renderSection(it);
+  }
+  return h;
+}
+
+/** Visible text of rendered HTML (tags stripped, entities decoded). */
+export function textContent(html) {
+  return html
+    .replace(/<[^>]*>/g, ' ')
+    .replace(/&lt;/g, '<')
+    .replace(/&gt;/g, '>')
+    .replace(/&quot;/g, '"')
+    .replace(/&amp;/g, '&')
+    .replace(/\s+/g, ' ')
+    .trim();
+}

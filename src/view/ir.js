@@ -1,0 +1,159 @@
+/**
+ * View IR — the declarative page description every view-model returns.
+ *
+ * A page is a list of items (loaders and sections); a section holds blocks
+ * (name/value tables, simple tables, percentage bars, per-GPU slot strips,
+ * the xGMI matrix, time series). The TSX layer maps each node 1:1 onto a
+ * Headlamp CommonComponent (SectionBox, NameValueTable, SimpleTable,
+ * StatusLabel, PercentageBar, Loader); `html.js` maps it onto the same
+ * semantic HTML the reference's component tests mock those components with
+ * (src/components/OverviewPage.test.tsx:8-61), so the page logic is testable
+ * without React.
+ */
+
+/** @typedef {'success'|'warning'|'error'} Status */
+
+/** @param {Status} status @param {string|number} text */
+export function status(st, text) {
+  return { t: 'status', status: st, text: String(text) };
+}
+
+/** Inline allocation/power bar: text like "3/8 (38%)". */
+export function bar(used, total, pctValue, color, text) {
+  return { t: 'bar', used: used, total: total, pct: pctValue, color: color, text: text };
+}
+
+/** Multi-line cell: [{label, text}] rendered as "<strong>label</strong>: text". */
+export function lines(items) {
+  return { t: 'lines', lines: items };
+}
+
+export function kv(rows) {
+  return { t: 'kv', rows: rows };
+}
+
+export function row(name, value) {
+  return { name: name, value: value };
+}
+
+/** @param {string[]} columns @param {Array<Array<any>>} rows @param {string[]} [keys] */
+export function table(columns, rows, keys) {
+  return { t: 'table', columns: columns, rows: rows, keys: keys || null };
+}
+
+/** PercentageBar: data [{name, value, fill}] of `total`. */
+export function pctbar(label, data, total) {
+  return { t: 'pctbar', label: label, data: data, total: total };
+}
+
+export function section(title, blocks, key) {
+  return { t: 'section', title: title, key: key || title, blocks: blocks };
+}
+
+export function loader(title) {
+  return { t: 'loader', title: title };
+}
+
+/**
+ * @param {string|null} title  page header (null while the page is only a loader)
+ * @param {{label: string, ariaLabel: string, disabled: boolean}|null} refresh
+ * @param {any[]} items
+ */
+export function page(title, refresh, items) {
+  return { t: 'page', title: title, refresh: refresh, items: items };
+}
+
+// ---------------------------------------------------------------------------
+// Query helpers (tests, benchmark row counting)
+// ---------------------------------------------------------------------------
+
+export function sections(vm) {
+  const out = [];
+  if (!vm) return out;
+  const items = vm.t === 'section' ? [vm] : vm.items || [];
+  for (let i = 0; i < items.length; i++) if (items[i].t === 'section') out.push(items[i]);
+  return out;
+}
+
+export function sectionTitles(vm) {
+  return sections(vm).map(function (s) { return s.title; });
+}
+
+export function findSection(vm, title) {
+  const ss = sections(vm);
+  for (let i = 0; i < ss.length; i++) if (ss[i].title === title) return ss[i];
+  return null;
+}
+
+export function loaders(vm) {
+  if (!vm || !vm.items) return [];
+  return vm.items.filter(function (i) { return i.t === 'loader'; }).map(function (i) { return i.title; });
+}
+
+/** Value of the first kv row named `name` in a section (or whole page). */
+export function rowValue(scope, name) {
+  const ss = scope && scope.t === 'page' ? sections(scope) : [scope];
+  for (let s = 0; s < ss.length; s++) {
+    if (!ss[s]) continue;
+    const blocks = ss[s].blocks || [];
+    for (let b = 0; b < blocks.length; b++) {
+      if (blocks[b].t !== 'kv') continue;
+      const rows = blocks[b].rows;
+      for (let r = 0; r < rows.length; r++) if (rows[r].name === name) return rows[r].value;
+    }
+  }
+  return undefined;
+}
+
+export function rowNames(sec) {
+  const out = [];
+  if (!sec) return out;
+  for (let b = 0; b < sec.blocks.length; b++) {
+    if (sec.blocks[b].t !== 'kv') continue;
+    for (let r = 0; r < sec.blocks[b].rows.length; r++) out.push(sec.blocks[b].rows[r].name);
+  }
+  return out;
+}
+
+export function firstTable(sec) {
+  if (!sec) return null;
+  for (let b = 0; b < sec.blocks.length; b++) if (sec.blocks[b].t === 'table') return sec.blocks[b];
+  return null;
+}
+
+export function firstBlock(sec, t) {
+  if (!sec) return null;
+  for (let b = 0; b < sec.blocks.length; b++) if (sec.blocks[b].t === t) return sec.blocks[b];
+  return null;
+}
+
+/** Plain text of a cell value. */
+export function text(v) {
+  if (v === null || v === undefined) return '';
+  if (typeof v === 'string' || typeof v === 'number') return String(v);
+  if (v.t === 'status') return v.text;
+  if (v.t === 'bar') return v.text;
+  if (v.t === 'lines') return v.lines.map(function (l) { return l.label ? l.label + ': ' + l.text : l.text; }).join('\n');
+  return '';
+}
+
+/**
+ * Count what a page renders: table rows, name/value rows, sections, and
+ * per-GPU cells. This is the "rows rendered" half of the benchmark metric.
+ */
+export function countRows(vm) {
+  const c = { sections: 0, tableRows: 0, kvRows: 0, gpuCells: 0 };
+  const ss = sections(vm);
+  for (let s = 0; s < ss.length; s++) {
+    c.sections++;
+    const blocks = ss[s].blocks;
+    for (let b = 0; b < blocks.length; b++) {
+      const bl = blocks[b];
+      if (bl.t === 'table') c.tableRows += bl.rows.length;
+      else if (bl.t === 'kv') c.kvRows += bl.rows.length;
+      else if (bl.t === 'slots') c.gpuCells += bl.slots.length;
+      else if (bl.t === 'matrix') c.gpuCells += bl.matrix.size * bl.matrix.size;
+    }
+  }
+  return c;
+}

@@ -1,0 +1,860 @@
+/**
+ * Page view-models: snapshot → View IR. Pure functions, no React, no I/O.
+ *
+ * One function per reference page / integration (SURVEY.md C5–C12):
+ *   overviewView        ← src/components/OverviewPage.tsx
+ *   devicePluginsView   ← src/components/DevicePluginsPage.tsx
+ *   nodesView           ← src/components/NodesPage.tsx
+ *   podsView            ← src/components/PodsPage.tsx
+ *   metricsView         ← src/components/MetricsPage.tsx
+ *   nodeDetailView      ← src/components/NodeDetailSection.tsx
+ *   podDetailView       ← src/components/PodDetailSection.tsx
+ *   nodeColumns         ← src/components/integrations/NodeColumns.tsx
+ *
+ * Section titles, loader texts, empty states and refresh aria-labels keep
+ * the reference's wording with AMD vocabulary, so the reference's component
+ * assertions translate one-for-one. Behavioural differences are listed in
+ * each function's comment.
+ *
+ * `opts.now` (ms epoch) makes ages deterministic in tests.
+ */
+
+import {
+  AMD_GPU_OPERATOR_NAMESPACE,
+  AMD_GPU_RESOURCE,
+  BAR_COLORS,
+  MI355X,
+  OPERANDS,
+  containerGpuEntries,
+  countsToStatus,
+  countsToText,
+  deviceConfigStatus,
+  deviceConfigStatusText,
+  formatAge,
+  formatBytes,
+  formatComponent,
+  formatGpuModel,
+  formatGpuResourceName,
+  formatPercent,
+  formatPodGpuRequests,
+  formatSelector,
+  formatWatts,
+  get,
+  getGpuResources,
+  getNodeGpuCount,
+  getNodeGpuModel,
+  getPodGpuCount,
+  getPodRestarts,
+  gpuContainers,
+  gpuInitContainers,
+  isAmdGpuNode,
+  isGpuRequestingPod,
+  isNodeReady,
+  isPodReady,
+  labellerValue,
+  operandEnabled,
+  operandStatus,
+  pct,
+  pctToColor,
+  pctToStatus,
+  phaseToStatus,
+  pluginPodComponent,
+  podPhase,
+  podWaitingReason,
+  unwrapKubeObject,
+} from '../api/amdgpu.js';
+import { buildGpuSlots, buildXgmiMatrix, isFullMesh } from '../api/topology.js';
+import { PROMETHEUS_SERVICES, summarizeMetrics } from '../api/metrics.js';
+import { bar, kv, lines, loader, page, pctbar, row, section, status, table } from './ir.js';
+
+export const BRAND = 'AMD GPU';
+export const ACTIVE_PODS_LIMIT = 10;
+
+export const HELM_INSTALL =
+  'helm repo add rocm https://rocm.github.io/gpu-operator && ' +
+  'helm install amd-gpu-operator rocm/gpu-operator-charts --namespace ' + AMD_GPU_OPERATOR_NAMESPACE + ' --create-namespace';
+export const OPERATOR_DOCS = 'https://instinct.docs.amd.com/projects/gpu-operator/';
+
+function nowOf(opts) {
+  return opts && typeof opts.now === 'number' ? opts.now : Date.now();
+}
+
+function refreshButton(ariaLabel, busy) {
+  return { label: busy ? 'Refreshing…' : 'Refresh', ariaLabel: ariaLabel, disabled: !!busy };
+}
+
+function errorSection(err) {
+  return section('Error', [kv([row('Status', status('error', err))])]);
+}
+
+/** Inline allocation bar (reference NodesPage.tsx:35-63; 70/90 thresholds). */
+export function allocationBar(used, allocatable) {
+  if (!(allocatable > 0)) return '—';
+  const p = Math.min(100, pct(used, allocatable));
+  return bar(used, allocatable, p, pctToColor(p), used + '/' + allocatable + ' (' + p + '%)');
+}
+
+function podName(p) {
+  return p.metadata.name;
+}
+function podNs(p) {
+  return p.metadata.namespace || '—';
+}
+function podNode(p) {
+  return get(p, ['spec', 'nodeName'], '—');
+}
+
+function readyLabel(p) {
+  const r = isPodReady(p);
+  return status(r ? 'success' : 'warning', r ? 'Ready' : get(p, ['status', 'phase'], 'Unknown'));
+}
+
+function restartsCell(p) {
+  const n = getPodRestarts(p);
+  return n > 0 ? status('warning', n) : String(n);
+}
+
+// ---------------------------------------------------------------------------
+// Overview (reference OverviewPage.tsx:54-420)
+// ---------------------------------------------------------------------------
+
+/**
+ * Differences: the loader only replaces the page on the FIRST load — later
+ * refreshes keep the data (stale-while-revalidate). Aggregates come from
+ * the store's memoised index. In-use counts GPUs held by bound,
+ * non-terminated pods (the scheduler's view), and Free is clamped at 0.
+ */
+export function overviewView(ctx, opts) {
+  const now = nowOf(opts);
+  if (ctx.loading && !ctx.lastUpdated) return page(null, null, [loader('Loading ' + BRAND + ' data...')]);
+  const items = [];
+  const t = ctx.index.totals;
+
+  if (ctx.error) items.push(errorSection(ctx.error));
+
+  if (!ctx.pluginInstalled) {
+    items.push(
+      section('Plugin Not Detected', [
+        kv([
+          row('Status', status('warning', 'AMD GPU device plugin not found on this cluster')),
+          row('Install (Helm)', HELM_INSTALL),
+          row('Documentation', OPERATOR_DOCS),
+        ]),
+      ])
+    );
+  }
+
+  if (!ctx.crdAvailable && ctx.pluginInstalled) {
+    items.push(
+      section('Notice', [
+        kv([
+          row('CRD Status', status('warning', 'DeviceConfig CRD not found — limited visibility available')),
+          row(
+            'Note',
+            'Device plugin pods detected via DaemonSet labels. Install the AMD GPU Operator for DeviceConfig-based management.'
+          ),
+        ]),
+      ])
+    );
+  }
+
+  if (ctx.crdAvailable && ctx.deviceConfigs.length > 0) {
+    items.push(
+      section('Device Config Status', [
+        table(
+          ['Name', 'Namespace', 'Status', 'Metrics Exporter', 'Node Labeller', 'Selector', 'Age'],
+          ctx.deviceConfigs.map(function (dc) {
+            return [
+              dc.metadata.name,
+              dc.metadata.namespace || '—',
+              status(deviceConfigStatus(dc), deviceConfigStatusText(dc)),
+              operandEnabled(dc, 'metricsExporter') ? status('success', 'Enabled') : status('warning', 'Disabled'),
+              operandEnabled(dc, 'nodeLabeller') ? status('success', 'Enabled') : status('warning', 'Disabled'),
+              formatSelector(get(dc, ['spec', 'selector'], null)),
+              formatAge(dc.metadata.creationTimestamp, now),
+            ];
+          }),
+          ctx.deviceConfigs.map(function (dc) { return dc.metadata.uid || dc.metadata.name; })
+        ),
+      ])
+    );
+  }
+
+  if (ctx.pluginPods.length > 0) {
+    items.push(
+      section('Plugin Daemon Pods', [
+        table(
+          ['Name', 'Namespace', 'Component', 'Node', 'Status', 'Age'],
+          ctx.pluginPods.map(function (p) {
+            return [podName(p), podNs(p), formatComponent(pluginPodComponent(p)), podNode(p), readyLabel(p), formatAge(p.metadata.creationTimestamp, now)];
+          })
+        ),
+      ])
+    );
+  }
+
+  const nodeBlocks = [];
+  if (t.nodes > 0) {
+    nodeBlocks.push(
+      pctbar(
+        'Node Readiness',
+        [
+          { name: 'Ready', value: t.readyNodes, fill: BAR_COLORS.ok },
+          { name: 'Not Ready', value: t.nodes - t.readyNodes, fill: BAR_COLORS.mute },
+        ].filter(function (d) { return d.value > 0; }),
+        t.nodes
+      )
+    );
+  }
+  const nodeRows = [
+    row('Total GPU Nodes', status(t.nodes > 0 ? 'success' : 'warning', t.nodes)),
+    row('Ready Nodes', String(t.readyNodes)),
+  ];
+  if (t.nodes > 0) nodeRows.push(row('GPU Model', MI355X.product + ' (' + MI355X.arch + ')'));
+  if (t.capacity > 0) {
+    nodeRows.push(row('Total GPU Devices', String(t.capacity)));
+    nodeRows.push(row('Total HBM', formatBytes(t.capacity * MI355X.hbmBytes) + ' (' + MI355X.hbmLabel + ' per GPU)'));
+  }
+  if (t.partitions > 0) nodeRows.push(row('GPU Partitions', String(t.partitions)));
+  nodeBlocks.push(kv(nodeRows));
+  items.push(section('GPU Nodes', nodeBlocks));
+
+  if (t.capacity > 0) {
+    items.push(
+      section('GPU Allocation', [
+        pctbar(
+          'GPU Allocation (' + t.utilizationPct + '%)',
+          [
+            { name: 'In Use', value: t.inUse, fill: BAR_COLORS.ok },
+            { name: 'Available', value: t.free, fill: BAR_COLORS.track },
+          ],
+          t.allocatable
+        ),
+        kv([
+          row('Total Capacity (GPU devices)', String(t.capacity)),
+          row('Allocatable', String(t.allocatable)),
+          row('In Use', String(t.inUse)),
+          row('Free', status(t.free > 0 ? 'success' : 'warning', t.free)),
+          row('HBM Allocated', formatBytes(t.inUse * MI355X.hbmBytes)),
+        ]),
+      ])
+    );
+  }
+
+  const ph = ctx.index.phases;
+  const wl = [row('Total GPU Pods', String(ctx.gpuPods.length))];
+  if (ph.Running > 0) wl.push(row('Running', status('success', ph.Running)));
+  if (ph.Pending > 0) wl.push(row('Pending', status('warning', ph.Pending)));
+  if (ph.Failed > 0) wl.push(row('Failed', status('error', ph.Failed)));
+  items.push(section('GPU Workloads', [kv(wl)]));
+
+  const running = ctx.gpuPods.filter(function (p) { return podPhase(p) === 'Running'; });
+  if (running.length > 0) {
+    items.push(
+      section('Active GPU Pods', [
+        table(
+          ['Name', 'Namespace', 'Node', 'GPU Request', 'Age'],
+          running.slice(0, ACTIVE_PODS_LIMIT).map(function (p) {
+            return [podName(p), podNs(p), podNode(p), formatPodGpuRequests(p), formatAge(p.metadata.creationTimestamp, now)];
+          })
+        ),
+      ])
+    );
+  }
+
+  return page(BRAND + ' — Overview', refreshButton('Refresh AMD GPU data', ctx.refreshing), items);
+}
+
+// ---------------------------------------------------------------------------
+// Device Plugins (reference DevicePluginsPage.tsx:20-219)
+// ---------------------------------------------------------------------------
+
+function enabledCell(on, detail) {
+  return on ? status('success', detail ? 'Enabled — ' + detail : 'Enabled') : status('warning', 'Disabled');
+}
+
+/**
+ * One card per DeviceConfig (reference: one per GpuDevicePlugin). Per-operand
+ * DaemonSet counts replace the single desired/ready pair.
+ */
+export function devicePluginsView(ctx, opts) {
+  const now = nowOf(opts);
+  if (ctx.loading && !ctx.lastUpdated) return page(null, null, [loader('Loading device plugin data...')]);
+  const items = [];
+  if (ctx.error) items.push(errorSection(ctx.error));
+
+  if (!ctx.crdAvailable) {
+    items.push(
+      section('CRD Not Available', [
+        kv([
+          row('Status', status('warning', 'DeviceConfig CRD (amd.com/v1alpha1) is not installed')),
+          row(
+            'Note',
+            'Install the AMD GPU Operator to manage DeviceConfig resources. Device plugin daemon pods are shown below if detected.'
+          ),
+        ]),
+      ])
+    );
+  }
+
+  if (ctx.crdAvailable && ctx.deviceConfigs.length === 0) {
+    items.push(
+      section('No Device Configs', [
+        kv([
+          row('Status', status('warning', 'No DeviceConfig resources found on this cluster')),
+          row('Create', 'kubectl apply -f deviceconfig.yaml (see the AMD GPU Operator documentation)'),
+        ]),
+      ])
+    );
+  }
+
+  for (let i = 0; i < ctx.deviceConfigs.length; i++) {
+    const dc = ctx.deviceConfigs[i];
+    const dp = operandStatus(dc, 'devicePlugin');
+    const rows = [
+      row('Status', status(deviceConfigStatus(dc), deviceConfigStatusText(dc))),
+      row('Namespace', dc.metadata.namespace || '—'),
+      row('Device Plugin Image', get(dc, ['spec', 'devicePlugin', 'devicePluginImage'], '—')),
+      row(
+        'Driver',
+        enabledCell(operandEnabled(dc, 'driver'), get(dc, ['spec', 'driver', 'version'], null))
+      ),
+      row('Node Labeller', enabledCell(operandEnabled(dc, 'nodeLabeller'))),
+      row(
+        'Metrics Exporter',
+        enabledCell(
+          operandEnabled(dc, 'metricsExporter'),
+          get(dc, ['spec', 'metricsExporter', 'port'], null) !== null ? 'port ' + get(dc, ['spec', 'metricsExporter', 'port'], '') : null
+        )
+      ),
+      row('Desired Nodes', String(dp.desired)),
+      row('Ready Nodes', String(dp.available)),
+    ];
+    if (dp.unavailable > 0) rows.push(row('Unavailable Nodes', status('error', dp.unavailable)));
+    for (let k = 0; k < OPERANDS.length; k++) {
+      const op = OPERANDS[k];
+      if (op.key === 'devicePlugin' || !operandEnabled(dc, op.key)) continue;
+      const st = operandStatus(dc, op.key);
+      rows.push(row(op.label + ' Pods', status(countsToStatus(st.desired, st.available), countsToText(st.desired, st.available))));
+    }
+    rows.push(row('Node Selector', formatSelector(get(dc, ['spec', 'selector'], null))));
+    rows.push(row('Age', formatAge(dc.metadata.creationTimestamp, now)));
+    items.push(section('DeviceConfig: ' + dc.metadata.name, [kv(rows)], dc.metadata.uid || dc.metadata.name));
+  }
+
+  if (ctx.pluginPods.length > 0) {
+    items.push(
+      section('Plugin Daemon Pods', [
+        table(
+          ['Name', 'Namespace', 'Component', 'Node', 'Ready', 'Restarts', 'Age'],
+          ctx.pluginPods.map(function (p) {
+            return [
+              podName(p), podNs(p), formatComponent(pluginPodComponent(p)), podNode(p), readyLabel(p),
+              restartsCell(p), formatAge(p.metadata.creationTimestamp, now),
+            ];
+          })
+        ),
+      ])
+    );
+  }
+
+  return page(BRAND + ' — Device Plugins', refreshButton('Refresh device plugin data', ctx.refreshing), items);
+}
+
+// ---------------------------------------------------------------------------
+// Nodes (reference NodesPage.tsx:145-293)
+// ---------------------------------------------------------------------------
+
+/** Per-GPU allocation strip block. */
+export function slotsBlock(node, podsOnNode, owners) {
+  const s = buildGpuSlots(node, podsOnNode, owners);
+  return { t: 'slots', slots: s.slots, exact: s.exact };
+}
+
+/** xGMI neighbour matrix block. */
+export function matrixBlock(gpuCount, measured, probed) {
+  const m = buildXgmiMatrix(gpuCount, measured, probed);
+  return { t: 'matrix', matrix: m, fullMesh: isFullMesh(m) };
+}
+
+/** Owners per GPU from exporter pod labels, for one node (or undefined). */
+function ownersFor(metrics, nodeName) {
+  if (!metrics || !metrics.gpus) return undefined;
+  const out = [];
+  for (let i = 0; i < metrics.gpus.length; i++) {
+    const g = metrics.gpus[i];
+    if (g.nodeName === nodeName && g.pod) out.push({ gpu: g.gpu, pod: g.pod, namespace: g.namespace });
+  }
+  return out.length ? out : undefined;
+}
+
+function nodeCardRows(node, podsOnNode, stats, now) {
+  const model = getNodeGpuModel(node);
+  const ready = isNodeReady(node);
+  const count = getNodeGpuCount(node);
+  const cap = getGpuResources(get(node, ['status', 'capacity'], null));
+  const alloc = getGpuResources(get(node, ['status', 'allocatable'], null));
+  const rows = [
+    row('Status', status(ready ? 'success' : 'error', ready ? 'Ready' : 'Not Ready')),
+    row('GPU Model', model.product),
+  ];
+  if (count > 0) {
+    rows.push(row('GPU Devices (amd.com/gpu)', String(count)));
+    rows.push(row('HBM', formatBytes(count * MI355X.hbmBytes) + ' (' + count + ' × ' + model.vram + ')'));
+  }
+  for (const k in cap) rows.push(row(formatGpuResourceName(k) + ' (capacity)', cap[k]));
+  for (const k in alloc) rows.push(row(formatGpuResourceName(k) + ' (allocatable)', alloc[k]));
+  if (stats) rows.push(row('GPU Allocation', allocationBar(stats.inUse, stats.allocatable || count)));
+  if (model.computePartition || model.memoryPartition) rows.push(row('Partition Mode', formatGpuModel(model)));
+  const drv = labellerValue(node, 'driver-version');
+  if (drv) rows.push(row('amdgpu Driver', drv));
+  rows.push(row('GPU Workload Pods', podsOnNode.length > 0 ? podsOnNode.map(podName).join(', ') : '—'));
+  rows.push(row('OS Image', get(node, ['status', 'nodeInfo', 'osImage'], '—')));
+  rows.push(row('Kernel', get(node, ['status', 'nodeInfo', 'kernelVersion'], '—')));
+  rows.push(row('Kubelet', get(node, ['status', 'nodeInfo', 'kubeletVersion'], '—')));
+  rows.push(row('Age', formatAge(node.metadata.creationTimestamp, now)));
+  return rows;
+}
+
+/**
+ * Differences: Allocation = GPUs held / allocatable GPUs (reference used the
+ * pod count, quirk Q2); each node card adds HBM, the per-GPU allocation
+ * strip and the xGMI neighbour matrix. `metrics` (optional) supplies exact
+ * per-GPU owners and measured xGMI throughput.
+ */
+export function nodesView(ctx, opts) {
+  const now = nowOf(opts);
+  const metrics = opts && opts.metrics ? opts.metrics : null;
+  if (ctx.loading && !ctx.lastUpdated) return page(null, null, [loader('Loading GPU node data...')]);
+  const items = [];
+  if (ctx.error) items.push(errorSection(ctx.error));
+
+  if (ctx.gpuNodes.length === 0) {
+    items.push(
+      section('No GPU Nodes Found', [
+        kv([
+          row('Status', status('warning', 'No nodes with AMD GPU resources or labels were found')),
+          row(
+            'Note',
+            'Nodes appear here when they advertise amd.com/gpu or carry AMD node-feature-discovery / node-labeller labels. ' +
+              'Ensure the AMD GPU Operator (or the AMD k8s device plugin) and Node Feature Discovery are installed.'
+          ),
+        ]),
+      ])
+    );
+  }
+
+  const idx = ctx.index;
+  if (ctx.gpuNodes.length > 0) {
+    items.push(
+      section('GPU Node Summary', [
+        table(
+          ['Node', 'Ready', 'GPU Model', 'GPU Devices', 'Allocation', 'GPU Pods', 'Age'],
+          ctx.gpuNodes.map(function (n) {
+            const st = idx.nodeStats[n.metadata.name];
+            const count = getNodeGpuCount(n);
+            const ready = isNodeReady(n);
+            return [
+              n.metadata.name,
+              status(ready ? 'success' : 'error', ready ? 'Ready' : 'Not Ready'),
+              formatGpuModel(getNodeGpuModel(n)),
+              count > 0 ? String(count) : '—',
+              allocationBar(st ? st.inUse : 0, (st && st.allocatable) || count),
+              String(st ? st.pods : 0),
+              formatAge(n.metadata.creationTimestamp, now),
+            ];
+          }),
+          ctx.gpuNodes.map(function (n) { return n.metadata.uid || n.metadata.name; })
+        ),
+      ])
+    );
+  }
+
+  for (let i = 0; i < ctx.gpuNodes.length; i++) {
+    const n = ctx.gpuNodes[i];
+    const name = n.metadata.name;
+    const pods = idx.podsByNode[name] || [];
+    const blocks = [kv(nodeCardRows(n, pods, idx.nodeStats[name], now))];
+    const count = getNodeGpuCount(n);
+    if (count > 0) {
+      blocks.push(slotsBlock(n, pods, ownersFor(metrics, name)));
+      blocks.push(matrixBlock(count, metrics && metrics.xgmi ? metrics.xgmi[name] : undefined));
+    }
+    items.push(section(name, blocks, n.metadata.uid || name));
+  }
+
+  return page(BRAND + ' — Nodes', refreshButton('Refresh node data', ctx.refreshing), items);
+}
+
+// ---------------------------------------------------------------------------
+// Pods (reference PodsPage.tsx:94-270)
+// ---------------------------------------------------------------------------
+
+/** Per-container GPU lines (reference GpuContainerList, PodsPage.tsx:49-88), init containers included. */
+export function gpuContainerLines(pod) {
+  const out = [];
+  function add(c, init) {
+    const es = containerGpuEntries(c);
+    const parts = [];
+    for (let i = 0; i < es.length; i++) {
+      const e = es[i];
+      const label = formatGpuResourceName(e.key);
+      if (e.request !== null && e.limit !== null && e.request === e.limit) parts.push(label + ': ' + e.request);
+      else parts.push(label + ': req=' + (e.request === null ? '—' : e.request) + ' lim=' + (e.limit === null ? '—' : e.limit));
+    }
+    out.push({ label: c.name + (init ? ' (init)' : ''), text: parts.join(', ') });
+  }
+  const ics = gpuInitContainers(pod);
+  for (let i = 0; i < ics.length; i++) add(ics[i], true);
+  const cs = gpuContainers(pod);
+  for (let i = 0; i < cs.length; i++) add(cs[i], false);
+  return out.length ? lines(out) : '—';
+}
+
+export function podsView(ctx, opts) {
+  const now = nowOf(opts);
+  if (ctx.loading && !ctx.lastUpdated) return page(null, null, [loader('Loading GPU pod data...')]);
+  const items = [];
+  if (ctx.error) items.push(errorSection(ctx.error));
+  const pods = ctx.gpuPods;
+
+  if (pods.length === 0) {
+    items.push(
+      section('No GPU Pods Found', [
+        kv([
+          row('Status', status('warning', 'No pods requesting AMD GPU resources were found')),
+          row('Note', 'Pods appear here when they request resources like amd.com/gpu.'),
+        ]),
+      ])
+    );
+  }
+
+  const ph = ctx.index.phases;
+  const pending = pods.filter(function (p) { return podPhase(p) === 'Pending'; });
+  if (pods.length > 0) {
+    const rows = [row('Total GPU Pods', String(pods.length))];
+    if (ph.Running > 0) rows.push(row('Running', status('success', ph.Running)));
+    if (ph.Pending > 0) rows.push(row('Pending', status('warning', ph.Pending)));
+    if (ph.Failed > 0) rows.push(row('Failed', status('error', ph.Failed)));
+    let gpus = 0;
+    for (let i = 0; i < pods.length; i++) {
+      const phase = podPhase(pods[i]);
+      if (phase !== 'Succeeded' && phase !== 'Failed' && get(pods[i], ['spec', 'nodeName'], null)) gpus += getPodGpuCount(pods[i]);
+    }
+    rows.push(row('GPUs Held', String(gpus)));
+    items.push(section('Summary', [kv(rows)]));
+
+    items.push(
+      section('All GPU Pods', [
+        table(
+          ['Name', 'Namespace', 'Node', 'Phase', 'GPU Resources', 'Restarts', 'Age'],
+          pods.map(function (p) {
+            const phase = podPhase(p);
+            return [
+              podName(p), podNs(p), podNode(p), status(phaseToStatus(phase), phase), gpuContainerLines(p),
+              restartsCell(p), formatAge(p.metadata.creationTimestamp, now),
+            ];
+          }),
+          pods.map(function (p) { return p.metadata.uid || (p.metadata.namespace + '/' + p.metadata.name); })
+        ),
+      ])
+    );
+  }
+
+  if (pending.length > 0) {
+    items.push(
+      section('Attention: Pending GPU Pods', [
+        table(
+          ['Name', 'Namespace', 'GPU Resources', 'Waiting Reason', 'Age'],
+          pending.map(function (p) {
+            return [podName(p), podNs(p), formatPodGpuRequests(p), podWaitingReason(p) || '—', formatAge(p.metadata.creationTimestamp, now)];
+          })
+        ),
+      ])
+    );
+  }
+
+  return page(BRAND + ' — Pods', refreshButton('Refresh pod data', ctx.refreshing), items);
+}
+
+// ---------------------------------------------------------------------------
+// Metrics (reference MetricsPage.tsx:191-355)
+// ---------------------------------------------------------------------------
+
+/** Power bar: "X W / Y W (Z%)" with 70/90 colouring (reference PowerBar, MetricsPage.tsx:50-89). */
+export function powerBar(watts, capWatts) {
+  const hasCap = capWatts !== null && capWatts > 0;
+  const p = hasCap ? Math.min(100, pct(watts, capWatts)) : null;
+  const txt = formatWatts(watts) + (hasCap ? ' / ' + formatWatts(capWatts) + ' (' + formatPercent(watts, capWatts) + ')' : '');
+  return bar(watts, hasCap ? capWatts : null, p, p === null ? BAR_COLORS.ok : pctToColor(p), txt);
+}
+
+export function hbmBar(used, total) {
+  if (used === null) return '—';
+  if (total === null || !(total > 0)) return formatBytes(used);
+  const p = Math.min(100, pct(used, total));
+  return bar(used, total, p, pctToColor(p), formatBytes(used) + ' / ' + formatBytes(total) + ' (' + p + '%)');
+}
+
+function pctText(v) {
+  return v === null ? '—' : Math.round(v) + '%';
+}
+
+/** Static availability box (reference MetricRequirements, MetricsPage.tsx:125-185) — on AMD everything is available. */
+export function metricAvailabilitySection() {
+  return section('Metric Availability', [
+    kv([
+      row('Power (W)', lines([
+        { label: '', text: 'Available — gpu_power_usage (AMD Device Metrics Exporter) or amdgpu hwmon power1_average via node-exporter' },
+      ])),
+      row('HBM used / total', lines([
+        { label: '', text: 'Available — gpu_used_vram / gpu_total_vram, or node-exporter --collector.drm node_drm_memory_vram_* (288 GB HBM3E per MI355X)' },
+      ])),
+      row('GFX activity (%)', lines([{ label: '', text: 'Available — gpu_gfx_activity, or node_drm_gpu_busy_percent' }])),
+      row('HBM controller activity (%)', lines([{ label: '', text: 'Available — gpu_umc_activity (exporter only)' }])),
+      row('xGMI link throughput', lines([{ label: '', text: 'Available — xgmi_neighbor_N_tx_throughput (exporter only; 7 links per GPU)' }])),
+      row('Per-GPU pod owner', lines([{ label: '', text: 'Available when the exporter runs with pod association (pod / namespace labels)' }])),
+    ]),
+  ]);
+}
+
+/**
+ * @param {{gpuNodes: any[], loading: boolean}} ctx
+ * @param {{ metrics: any|null, fetchError: string|null, fetching: boolean, series?: any }} mstate
+ *
+ * Differences: one card per NODE with a per-GPU table (the reference renders
+ * one card per chip — 64 cards at 8 nodes); HBM, activity and temperature
+ * columns; per-node power/HBM series when range data is present.
+ */
+export function metricsView(ctx, mstate, opts) {
+  const now = nowOf(opts);
+  const items = [];
+  if (ctx.loading && !ctx.lastUpdated) items.push(loader('Loading ' + BRAND + ' data...'));
+  items.push(metricAvailabilitySection());
+  const m = mstate.metrics;
+  if (mstate.fetching && !m) items.push(loader('Querying Prometheus for GPU metrics...'));
+
+  if (mstate.fetchError) {
+    items.push(
+      section('Prometheus Unreachable', [
+        kv([
+          row('Error', status('error', mstate.fetchError)),
+          row(
+            'Checked services',
+            PROMETHEUS_SERVICES.map(function (s) { return s.service + ':' + s.port; }).join(', ') + ' (monitoring namespace)'
+          ),
+        ]),
+      ])
+    );
+  }
+
+  if (m && m.gpus.length === 0) {
+    items.push(
+      section('No AMD GPU Metrics in Prometheus', [
+        kv([
+          row('Status', status('warning', 'Prometheus reachable — no gpu_power_usage or amdgpu hwmon series found')),
+          row('GPU Nodes', ctx.gpuNodes.length > 0 ? ctx.gpuNodes.map(function (n) { return n.metadata.name; }).join(', ') : 'None detected'),
+          row(
+            'Likely cause',
+            'The AMD Device Metrics Exporter is not deployed (DeviceConfig spec.metricsExporter.enable) or not scraped, and node-exporter is not running on the GPU nodes.'
+          ),
+        ]),
+      ])
+    );
+  }
+
+  if (m && m.gpus.length > 0) {
+    const sum = summarizeMetrics(m);
+    items.push(
+      section('GPU Power Summary', [
+        kv([
+          row('GPUs Monitored', String(sum.gpus)),
+          row('Total Power', powerBar(sum.powerWatts, sum.powerCapWatts > 0 ? sum.powerCapWatts : null)),
+          row('HBM In Use', hbmBar(sum.vramUsedBytes, sum.vramTotalBytes > 0 ? sum.vramTotalBytes : null)),
+          row('Avg GFX Activity', pctText(sum.avgGfxActivityPct)),
+          row('Source', m.source === 'amd-exporter' ? 'AMD Device Metrics Exporter' : 'node-exporter (amdgpu hwmon + DRM)'),
+          row('Last Fetched', new Date(m.fetchedAt).toISOString().slice(11, 19) + ' UTC'),
+        ]),
+      ])
+    );
+
+    if (mstate.series && mstate.series.power) {
+      items.push(section('Power & HBM (last 30 min)', [{ t: 'series', power: mstate.series.power, vram: mstate.series.vram || {} }]));
+    }
+
+    const byNode = {};
+    const order = [];
+    for (let i = 0; i < m.gpus.length; i++) {
+      const g = m.gpus[i];
+      if (!byNode[g.nodeName]) {
+        byNode[g.nodeName] = [];
+        order.push(g.nodeName);
+      }
+      byNode[g.nodeName].push(g);
+    }
+    for (let i = 0; i < order.length; i++) {
+      const gs = byNode[order[i]];
+      items.push(
+        section(order[i] + ' — ' + gs.length + ' × ' + MI355X.shortName, [
+          table(
+            ['GPU', 'Power', 'HBM Used', 'GFX', 'HBM Activity', 'Temp', 'Pod'],
+            gs.map(function (g) {
+              return [
+                'GPU ' + g.gpu,
+                g.powerWatts !== null ? powerBar(g.powerWatts, g.powerCapWatts) : status('warning', 'No data'),
+                hbmBar(g.vramUsedBytes, g.vramTotalBytes),
+                pctText(g.gfxActivityPct),
+                pctText(g.memActivityPct),
+                g.tempC === null ? '—' : Math.round(g.tempC) + ' °C',
+                g.pod ? (g.namespace ? g.namespace + '/' : '') + g.pod : '—',
+              ];
+            }),
+            gs.map(function (g) { return g.nodeName + '-' + g.gpu; })
+          ),
+        ], order[i])
+      );
+    }
+  }
+
+  void now;
+  return page(BRAND + ' — Metrics', refreshButton('Refresh metrics', mstate.fetching || ctx.loading), items);
+}
+
+// ---------------------------------------------------------------------------
+// Node detail section (reference NodeDetailSection.tsx:36-138)
+// ---------------------------------------------------------------------------
+
+/**
+ * @param {any} resource  Headlamp KubeObject or raw Node
+ * @param {{gpuPods: any[], loading: boolean, index?: any}} ctx
+ * @returns {any|null}  a section, or null for non-GPU nodes
+ *
+ * Differences: in-use counts GPUs of every bound non-terminated pod
+ * including init containers (reference: running pods' regular containers
+ * only, quirk Q3); adds HBM, slots and the xGMI matrix.
+ */
+export function nodeDetailView(resource, ctx, opts) {
+  const raw = unwrapKubeObject(resource);
+  if (!isAmdGpuNode(raw)) return null;
+  const cap = getGpuResources(get(raw, ['status', 'capacity'], null));
+  const alloc = getGpuResources(get(raw, ['status', 'allocatable'], null));
+  if (Object.keys(cap).length === 0 && Object.keys(alloc).length === 0) return null;
+  const name = raw.metadata.name;
+  const podsOnNode = ctx.loading && !ctx.lastUpdated
+    ? []
+    : ctx.gpuPods.filter(function (p) { return get(p, ['spec', 'nodeName'], null) === name; });
+  const allocatable = parseInt(alloc[AMD_GPU_RESOURCE] || '0', 10) || 0;
+  let inUse = 0;
+  for (let i = 0; i < podsOnNode.length; i++) {
+    const ph = podPhase(podsOnNode[i]);
+    if (ph !== 'Succeeded' && ph !== 'Failed') inUse += getPodGpuCount(podsOnNode[i]);
+  }
+  const p = pct(inUse, allocatable);
+  const model = getNodeGpuModel(raw);
+  const rows = [row('GPU Model', model.product)];
+  for (const k in cap) rows.push(row(formatGpuResourceName(k) + ' (capacity)', cap[k]));
+  for (const k in alloc) rows.push(row(formatGpuResourceName(k) + ' (allocatable)', alloc[k]));
+  const count = getNodeGpuCount(raw);
+  if (count > 0) rows.push(row('HBM', formatBytes(count * MI355X.hbmBytes)));
+  if (allocatable > 0) rows.push(row('GPU Allocation', status(pctToStatus(p), inUse + '/' + allocatable + ' (' + p + '%)')));
+  rows.push(
+    row(
+      'GPU Workload Pods',
+      podsOnNode.length > 0 ? podsOnNode.map(podName).join(', ') : ctx.loading ? 'Loading…' : 'None'
+    )
+  );
+  const blocks = [kv(rows)];
+  if (count > 0) {
+    const metrics = opts && opts.metrics ? opts.metrics : null;
+    blocks.push(slotsBlock(raw, podsOnNode, ownersFor(metrics, name)));
+    blocks.push(matrixBlock(count, metrics && metrics.xgmi ? metrics.xgmi[name] : undefined));
+  }
+  return section('AMD GPU', blocks);
+}
+
+// ---------------------------------------------------------------------------
+// Pod detail section (reference PodDetailSection.tsx:25-114)
+// ---------------------------------------------------------------------------
+
+/**
+ * Self-contained (no store). Differences: init containers are listed too, so
+ * an init-only GPU pod renders (reference quirk Q3), and the effective GPU
+ * demand the scheduler uses is shown.
+ */
+export function podDetailView(resource) {
+  const raw = unwrapKubeObject(resource);
+  if (!isGpuRequestingPod(raw)) return null;
+  const ics = gpuInitContainers(raw);
+  const cs = gpuContainers(raw);
+  const all = ics.map(function (c) { return [c, true]; }).concat(cs.map(function (c) { return [c, false]; }));
+  if (all.length === 0) return null;
+  const rows = [];
+  for (let i = 0; i < all.length; i++) {
+    const c = all[i][0];
+    const cname = c.name + (all[i][1] ? ' (init)' : '');
+    const es = containerGpuEntries(c);
+    for (let j = 0; j < es.length; j++) {
+      const res = formatGpuResourceName(es[j].key);
+      rows.push(row(cname + ' → ' + res + ' request', es[j].request === null ? '—' : es[j].request));
+      if (es[j].limit !== null && es[j].limit !== es[j].request) rows.push(row(cname + ' → ' + res + ' limit', es[j].limit));
+    }
+  }
+  const phase = get(raw, ['status', 'phase'], null);
+  const phaseStatus = phase === 'Running' || phase === 'Succeeded' ? 'success' : phase === 'Pending' ? 'warning' : 'error';
+  const gpus = getPodGpuCount(raw);
+  return section('AMD GPU Resources', [
+    kv(
+      [
+        row('Phase', status(phaseStatus, phase || 'Unknown')),
+        row('Scheduled Node', get(raw, ['spec', 'nodeName'], '—')),
+        row('GPU Containers', String(all.length)),
+        row('GPUs (effective)', gpus > 0 ? gpus + ' × ' + MI355X.shortName + ' (' + formatBytes(gpus * MI355X.hbmBytes) + ' HBM)' : '—'),
+      ].concat(rows)
+    ),
+  ]);
+}
+
+// ---------------------------------------------------------------------------
+// Nodes-table columns (reference integrations/NodeColumns.tsx:17-48)
+// ---------------------------------------------------------------------------
+
+/**
+ * Column descriptors for the native `headlamp-nodes` table. Getters return
+ * IR cells; the TSX wrapper turns status cells into StatusLabels.
+ * Each getter unwraps and classifies the row once via a WeakMap cache, so
+ * N columns cost one `isAmdGpuNode` per row (reference re-ran it per column).
+ */
+export function nodeColumns() {
+  const cache = typeof WeakMap === 'function' ? new WeakMap() : null;
+  function info(resource) {
+    const key = resource && typeof resource === 'object' ? resource : null;
+    if (cache && key && cache.has(key)) return cache.get(key);
+    const raw = unwrapKubeObject(resource);
+    const v = isAmdGpuNode(raw) ? { raw: raw, count: getNodeGpuCount(raw), model: getNodeGpuModel(raw) } : null;
+    if (cache && key) cache.set(key, v);
+    return v;
+  }
+  return [
+    {
+      label: 'GPU Model',
+      getter: function (resource) {
+        const i = info(resource);
+        return i ? status('success', formatGpuModel(i.model)) : '—';
+      },
+    },
+    {
+      label: 'GPU Devices',
+      getter: function (resource) {
+        const i = info(resource);
+        return i && i.count > 0 ? String(i.count) : '—';
+      },
+    },
+    {
+      label: 'GPU HBM',
+      getter: function (resource) {
+        const i = info(resource);
+        return i && i.count > 0 ? formatBytes(i.count * MI355X.hbmBytes) : '—';
+      },
+    },
+  ];
+}

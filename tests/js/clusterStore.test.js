@@ -1,0 +1,280 @@
+/**
+ * Data-layer specs (analog of reference src/api/IntelGpuDataContext.test.tsx,
+ * 8 cases) plus the parallel-fetch, SWR, race and shared-cache behaviour the
+ * reference lacks.
+ */
+import { createClusterStore, getSharedStore, resetSharedStores, withTimeout } from '../../src/api/clusterStore.js';
+import { DEVICE_CONFIG_LIST_PATH, PLUGIN_POD_QUERIES } from '../../src/api/amdgpu.js';
+import { makeDeviceConfig, makeGpuNode, makeGpuPod, makeNode, makePlainPod, makePluginPod } from './fixtures.js';
+
+function deferred() {
+  let resolve;
+  let reject;
+  const promise = new Promise((a, b) => {
+    resolve = a;
+    reject = b;
+  });
+  return { promise, resolve, reject };
+}
+
+/** request() stub answering by path. */
+function router(table) {
+  return vi.fn((path) => {
+    const h = table[path];
+    if (h === undefined) return Promise.reject(new Error('404 ' + path));
+    return typeof h === 'function' ? h(path) : Promise.resolve(h);
+  });
+}
+
+function baseRoutes(extra) {
+  const r = {};
+  r[DEVICE_CONFIG_LIST_PATH] = { items: [makeDeviceConfig()] };
+  r[PLUGIN_POD_QUERIES[0]] = { items: [makePluginPod('dp-0'), makePluginPod('dp-1')] };
+  r[PLUGIN_POD_QUERIES[1]] = { items: [makePluginPod('dp-0'), makePlainPod('other')] };
+  r['/api/v1/nodes'] = { items: [makeGpuNode('mi355x-0'), makeNode('cpu-0')] };
+  r['/api/v1/pods'] = { items: [makeGpuPod('train-0'), makePlainPod('web')] };
+  return Object.assign(r, extra || {});
+}
+
+describe('withTimeout', () => {
+  it('resolves with the value and clears its timer', async () => {
+    vi.useFakeTimers();
+    const v = await withTimeout(Promise.resolve(7), 2000);
+    expect(v).toBe(7);
+    expect(vi.getTimerCount()).toBe(0);
+    vi.useRealTimers();
+  });
+  it('rejects after the deadline', async () => {
+    vi.useFakeTimers();
+    const p = withTimeout(new Promise(() => {}), 2000);
+    vi.advanceTimersByTime(2000);
+    await expect(p).rejects.toThrow('Request timed out after 2000ms');
+    vi.useRealTimers();
+  });
+});
+
+describe('createClusterStore', () => {
+  it('requires a request function', () => {
+    expect(() => createClusterStore({})).toThrow('request(path) is required');
+  });
+
+  it('is loading until nodes, pods and the first refresh arrive', async () => {
+    const store = createClusterStore({ request: router(baseRoutes()) });
+    expect(store.getSnapshot().loading).toBe(true);
+    store.setNodes([], null);
+    store.setPods([], null);
+    expect(store.getSnapshot().loading).toBe(true);
+    await store.refresh();
+    expect(store.getSnapshot().loading).toBe(false);
+  });
+
+  it('filters GPU nodes and pods from Headlamp KubeObject wrappers', async () => {
+    const store = createClusterStore({ request: router(baseRoutes()) });
+    store.setNodes([{ jsonData: makeGpuNode('g0') }, { jsonData: makeNode('c0') }], null);
+    store.setPods([{ jsonData: makeGpuPod('p0', { node: 'g0' }) }, { jsonData: makePlainPod('x') }], null);
+    const s = store.getSnapshot();
+    expect(s.gpuNodes.map((n) => n.metadata.name)).toEqual(['g0']);
+    expect(s.gpuPods.map((p) => p.metadata.name)).toEqual(['p0']);
+    expect(s.index.nodeStats.g0.inUse).toBe(1);
+  });
+
+  it('issues the CRD and every plugin-pod query concurrently', async () => {
+    const gates = {};
+    const request = vi.fn((path) => {
+      gates[path] = deferred();
+      return gates[path].promise;
+    });
+    const store = createClusterStore({ request });
+    const done = store.refresh();
+    // All three requests are in flight before any of them resolves.
+    expect(request).toHaveBeenCalledTimes(1 + PLUGIN_POD_QUERIES.length);
+    Object.keys(gates).forEach((k) => gates[k].resolve({ items: [] }));
+    await done;
+    expect(store.getSnapshot().crdAvailable).toBe(true);
+  });
+
+  it('sets crdAvailable and deviceConfigs from the CRD list', async () => {
+    const store = createClusterStore({ request: router(baseRoutes()) });
+    await store.refresh();
+    const s = store.getSnapshot();
+    expect(s.crdAvailable).toBe(true);
+    expect(s.deviceConfigs).toHaveLength(1);
+    expect(s.deviceConfigs[0].metadata.name).toBe('gpu-operator');
+    expect(s.pluginInstalled).toBe(true);
+  });
+
+  it('drops non-DeviceConfig items from the CRD list', async () => {
+    const r = baseRoutes();
+    r[DEVICE_CONFIG_LIST_PATH] = { items: [makeDeviceConfig(), { kind: 'Other', metadata: { name: 'x' } }] };
+    const store = createClusterStore({ request: router(r) });
+    await store.refresh();
+    expect(store.getSnapshot().deviceConfigs).toHaveLength(1);
+  });
+
+  it('degrades silently when the CRD is missing', async () => {
+    const r = baseRoutes();
+    delete r[DEVICE_CONFIG_LIST_PATH];
+    const store = createClusterStore({ request: router(r) });
+    await store.refresh();
+    const s = store.getSnapshot();
+    expect(s.crdAvailable).toBe(false);
+    expect(s.deviceConfigs).toHaveLength(0);
+    expect(s.error).toBeNull();
+    expect(s.pluginInstalled).toBe(true); // found via pods
+  });
+
+  it('treats a CRD timeout as missing and does not wait for it', async () => {
+    vi.useFakeTimers();
+    const r = baseRoutes();
+    r[DEVICE_CONFIG_LIST_PATH] = () => new Promise(() => {});
+    const store = createClusterStore({ request: router(r), timeoutMs: 2000 });
+    let settled = false;
+    const p = store.refresh().then(() => {
+      settled = true;
+    });
+    await vi.advanceTimersByTimeAsync(1999);
+    expect(settled).toBe(false);
+    await vi.advanceTimersByTimeAsync(1);
+    await p;
+    expect(store.getSnapshot().crdAvailable).toBe(false);
+    expect(vi.getTimerCount()).toBe(0);
+    vi.useRealTimers();
+  });
+
+  it('merges and dedupes plugin pods across queries', async () => {
+    const store = createClusterStore({ request: router(baseRoutes()) });
+    await store.refresh();
+    expect(store.getSnapshot().pluginPods.map((p) => p.metadata.name)).toEqual(['dp-0', 'dp-1']);
+  });
+
+  it('ignores failing plugin-pod queries', async () => {
+    const r = baseRoutes();
+    delete r[PLUGIN_POD_QUERIES[0]];
+    const store = createClusterStore({ request: router(r) });
+    await store.refresh();
+    expect(store.getSnapshot().pluginPods.map((p) => p.metadata.name)).toEqual(['dp-0']);
+    expect(store.getSnapshot().error).toBeNull();
+  });
+
+  it('reports pluginInstalled=false when nothing is found', async () => {
+    const store = createClusterStore({ request: router({}) });
+    await store.refresh();
+    expect(store.getSnapshot().pluginInstalled).toBe(false);
+  });
+
+  it('keeps data visible while a refresh is in flight (stale-while-revalidate)', async () => {
+    const store = createClusterStore({ request: router(baseRoutes()) });
+    store.setNodes([], null);
+    store.setPods([], null);
+    await store.refresh();
+    const p = store.refresh();
+    const mid = store.getSnapshot();
+    expect(mid.loading).toBe(false);
+    expect(mid.refreshing).toBe(true);
+    expect(mid.deviceConfigs).toHaveLength(1);
+    await p;
+    expect(store.getSnapshot().refreshing).toBe(false);
+  });
+
+  it('drops results of a superseded refresh', async () => {
+    const first = deferred();
+    let calls = 0;
+    const request = vi.fn((path) => {
+      if (path === DEVICE_CONFIG_LIST_PATH) {
+        calls++;
+        return calls === 1 ? first.promise : Promise.resolve({ items: [makeDeviceConfig('new')] });
+      }
+      return Promise.resolve({ items: [] });
+    });
+    const store = createClusterStore({ request });
+    const a = store.refresh();
+    const b = store.refresh();
+    await b;
+    first.resolve({ items: [makeDeviceConfig('old')] });
+    await a;
+    expect(store.getSnapshot().deviceConfigs[0].metadata.name).toBe('new');
+  });
+
+  it('refresh re-issues the imperative requests', async () => {
+    const request = router(baseRoutes());
+    const store = createClusterStore({ request });
+    await store.refresh();
+    const n = request.mock.calls.length;
+    await store.refresh();
+    expect(request.mock.calls.length).toBe(2 * n);
+  });
+
+  it('aggregates node, pod and async errors', async () => {
+    const store = createClusterStore({ request: router(baseRoutes()) });
+    store.setNodes(null, 'nodes forbidden');
+    store.setPods(null, 'pods forbidden');
+    expect(store.getSnapshot().error).toBe('nodes forbidden; pods forbidden');
+  });
+
+  it('memoises filters on input identity', () => {
+    const store = createClusterStore({ request: router({}) });
+    const nodes = [makeGpuNode('g')];
+    store.setNodes(nodes, null);
+    const a = store.getSnapshot().gpuNodes;
+    store.setPods([], null);
+    expect(store.getSnapshot().gpuNodes).toBe(a);
+  });
+
+  it('notifies subscribers and supports unsubscribe', async () => {
+    const store = createClusterStore({ request: router(baseRoutes()) });
+    const fn = vi.fn();
+    const off = store.subscribe(fn);
+    store.setNodes([], null);
+    expect(fn).toHaveBeenCalledTimes(1);
+    off();
+    store.setPods([], null);
+    expect(fn).toHaveBeenCalledTimes(1);
+  });
+
+  it('snapshots are immutable and versioned', () => {
+    const store = createClusterStore({ request: router({}) });
+    const a = store.getSnapshot();
+    store.setNodes([], null);
+    const b = store.getSnapshot();
+    expect(a).not.toBe(b);
+    expect(b.version).toBeGreaterThan(a.version);
+    expect(Object.isFrozen(b)).toBe(true);
+  });
+
+  it('loadLists fetches nodes and pods directly', async () => {
+    const store = createClusterStore({ request: router(baseRoutes()) });
+    await Promise.all([store.loadLists(), store.refresh()]);
+    const s = store.getSnapshot();
+    expect(s.loading).toBe(false);
+    expect(s.gpuNodes).toHaveLength(1);
+    expect(s.gpuPods).toHaveLength(1);
+  });
+
+  it('loadLists surfaces list errors', async () => {
+    const store = createClusterStore({ request: router({}) });
+    await store.loadLists();
+    expect(store.getSnapshot().error).toContain('404 /api/v1/nodes');
+  });
+
+  it('emits a trace span per request', async () => {
+    const spans = [];
+    const store = createClusterStore({ request: router(baseRoutes()), onTrace: (s) => spans.push(s) });
+    await store.refresh();
+    expect(spans.map((s) => s.name).sort()).toEqual(['crd', 'plugin-pods-0', 'plugin-pods-1']);
+    expect(spans.every((s) => s.end >= s.start && s.ok)).toBe(true);
+  });
+});
+
+describe('getSharedStore', () => {
+  it('returns one store per cluster key', () => {
+    resetSharedStores();
+    const f = vi.fn(() => createClusterStore({ request: router({}) }));
+    const a = getSharedStore('c1', f);
+    const b = getSharedStore('c1', f);
+    const c = getSharedStore('c2', f);
+    expect(a).toBe(b);
+    expect(a).not.toBe(c);
+    expect(f).toHaveBeenCalledTimes(2);
+    resetSharedStores();
+  });
+});

@@ -1,0 +1,195 @@
+/**
+ * Native-view integration specs: Node detail section (reference
+ * NodeDetailSection.test.tsx, 8 cases), Pod detail section
+ * (PodDetailSection.test.tsx, 10 cases), the Nodes-table columns (untested in
+ * the reference) and the topology model (new).
+ */
+import { nodeColumns, nodeDetailView, podDetailView } from '../../src/view/pages.js';
+import { findSection, firstBlock, rowNames, rowValue, text } from '../../src/view/ir.js';
+import { buildGpuSlots, buildXgmiMatrix, isFullMesh } from '../../src/api/topology.js';
+import { NOW, makeContext, makeGpuNode, makeGpuPod, makeNode, makePlainPod } from './fixtures.js';
+
+describe('nodeDetailView', () => {
+  const node = makeGpuNode('g0');
+  const ctx = makeContext({
+    nodes: [node],
+    pods: [makeGpuPod('a', { node: 'g0', gpus: 6 }), makeGpuPod('b', { node: 'g0', gpus: 1, phase: 'Succeeded' }), makeGpuPod('c', { node: 'other' })],
+  });
+
+  it('returns null for non-GPU nodes', () => {
+    expect(nodeDetailView(makeNode('cpu'), ctx)).toBeNull();
+  });
+  it('returns null for label-only nodes without AMD resources', () => {
+    expect(nodeDetailView(makeGpuNode('x', { capacity: false }), ctx)).toBeNull();
+  });
+  it('accepts a Headlamp KubeObject wrapper', () => {
+    expect(nodeDetailView({ jsonData: node }, ctx)).not.toBeNull();
+  });
+  it('renders the AMD GPU section with capacity and allocatable rows', () => {
+    const s = nodeDetailView(node, ctx);
+    expect(s.title).toBe('AMD GPU');
+    expect(rowValue(s, 'GPU (capacity)')).toBe('8');
+    expect(rowValue(s, 'GPU (allocatable)')).toBe('8');
+    expect(rowValue(s, 'GPU Model')).toBe('AMD Instinct MI355X');
+    expect(rowValue(s, 'HBM')).toBe('2.3 TB');
+  });
+  it('computes allocation from pods on this node with threshold status', () => {
+    const s = nodeDetailView(node, ctx);
+    expect(rowValue(s, 'GPU Allocation')).toEqual({ t: 'status', status: 'warning', text: '6/8 (75%)' });
+  });
+  it('escalates to error at 90%', () => {
+    const c2 = makeContext({ nodes: [node], pods: [makeGpuPod('a', { node: 'g0', gpus: 8 })] });
+    expect(rowValue(nodeDetailView(node, c2), 'GPU Allocation').status).toBe('error');
+  });
+  it('counts GPU init containers (reference quirk Q3)', () => {
+    const c2 = makeContext({ nodes: [node], pods: [makeGpuPod('a', { node: 'g0', gpus: 1, init: 4 })] });
+    expect(text(rowValue(nodeDetailView(node, c2), 'GPU Allocation'))).toBe('4/8 (50%)');
+  });
+  it('lists workload pods on the node', () => {
+    expect(rowValue(nodeDetailView(node, ctx), 'GPU Workload Pods')).toBe('a, b');
+  });
+  it('shows Loading… while the store loads', () => {
+    const c2 = makeContext({ loading: true, lastUpdated: null });
+    expect(rowValue(nodeDetailView(node, c2), 'GPU Workload Pods')).toBe('Loading…');
+  });
+  it('shows None when no pods use the node', () => {
+    expect(rowValue(nodeDetailView(node, makeContext({ nodes: [node] })), 'GPU Workload Pods')).toBe('None');
+  });
+  it('omits allocation when nothing is allocatable', () => {
+    const n = makeGpuNode('g0', { allocatable: 0 });
+    expect(rowNames(nodeDetailView(n, ctx))).not.toContain('GPU Allocation');
+  });
+  it('includes the per-GPU strip and xGMI matrix', () => {
+    const s = nodeDetailView(node, ctx);
+    expect(firstBlock(s, 'slots').slots).toHaveLength(8);
+    expect(firstBlock(s, 'matrix').fullMesh).toBe(true);
+  });
+});
+
+describe('podDetailView', () => {
+  it('returns null for CPU pods', () => {
+    expect(podDetailView(makePlainPod('x'))).toBeNull();
+  });
+  it('returns null for non-objects', () => {
+    expect(podDetailView(null)).toBeNull();
+  });
+  it('accepts a KubeObject wrapper', () => {
+    expect(podDetailView({ jsonData: makeGpuPod('p') })).not.toBeNull();
+  });
+  it('renders phase, node and container count', () => {
+    const s = podDetailView(makeGpuPod('p', { gpus: 2 }));
+    expect(s.title).toBe('AMD GPU Resources');
+    expect(rowValue(s, 'Phase')).toEqual({ t: 'status', status: 'success', text: 'Running' });
+    expect(rowValue(s, 'Scheduled Node')).toBe('mi355x-0');
+    expect(rowValue(s, 'GPU Containers')).toBe('1');
+    expect(rowValue(s, 'GPUs (effective)')).toBe('2 × MI355X (576 GB HBM)');
+  });
+  it('shows request rows and omits equal limits', () => {
+    const s = podDetailView(makeGpuPod('p', { gpus: 2 }));
+    expect(rowValue(s, 'trainer → GPU request')).toBe('2');
+    expect(rowNames(s)).not.toContain('trainer → GPU limit');
+  });
+  it('shows a limit row when it differs', () => {
+    const p = makeGpuPod('p', { gpus: 1 });
+    p.spec.containers[0].resources.limits['amd.com/gpu'] = '2';
+    expect(rowValue(podDetailView(p), 'trainer → GPU limit')).toBe('2');
+  });
+  it('shows — for a limits-only request', () => {
+    const s = podDetailView(makeGpuPod('p', { limitsOnly: true, gpus: 2 }));
+    expect(rowValue(s, 'trainer → GPU request')).toBe('—');
+    expect(rowValue(s, 'trainer → GPU limit')).toBe('2');
+  });
+  it('renders init-only GPU pods (reference quirk Q3)', () => {
+    const s = podDetailView(makeGpuPod('p', { gpus: 0, init: 1 }));
+    expect(s).not.toBeNull();
+    expect(rowValue(s, 'warmup (init) → GPU request')).toBe('1');
+  });
+  it('maps Pending to warning and unknown phases to error', () => {
+    expect(rowValue(podDetailView(makeGpuPod('p', { phase: 'Pending' })), 'Phase').status).toBe('warning');
+    expect(rowValue(podDetailView(makeGpuPod('p', { phase: 'Failed' })), 'Phase').status).toBe('error');
+    const p = makeGpuPod('p');
+    delete p.status.phase;
+    expect(rowValue(podDetailView(p), 'Phase')).toEqual({ t: 'status', status: 'error', text: 'Unknown' });
+  });
+  it('shows — for unscheduled pods', () => {
+    expect(rowValue(podDetailView(makeGpuPod('p', { node: null, phase: 'Pending' })), 'Scheduled Node')).toBe('—');
+  });
+  it('lists partition resources with their display name', () => {
+    const s = podDetailView(makeGpuPod('p', { resource: 'amd.com/cpx_nps4', gpus: 2 }));
+    expect(rowValue(s, 'trainer → GPU partition (CPX/NPS4) request')).toBe('2');
+  });
+});
+
+describe('nodeColumns', () => {
+  const cols = nodeColumns();
+  it('declares GPU Model, GPU Devices and GPU HBM', () => {
+    expect(cols.map((c) => c.label)).toEqual(['GPU Model', 'GPU Devices', 'GPU HBM']);
+  });
+  it('returns dashes for CPU nodes', () => {
+    const n = makeNode('c');
+    expect(cols.map((c) => c.getter(n))).toEqual(['—', '—', '—']);
+  });
+  it('renders the model as a success status', () => {
+    expect(cols[0].getter(makeGpuNode('g'))).toEqual({ t: 'status', status: 'success', text: 'MI355X' });
+  });
+  it('counts devices and HBM from KubeObject wrappers', () => {
+    const w = { jsonData: makeGpuNode('g', { gpus: 4 }) };
+    expect(cols[1].getter(w)).toBe('4');
+    expect(cols[2].getter(w)).toBe('1.2 TB');
+  });
+  it('shows — devices for label-only nodes', () => {
+    expect(cols[1].getter(makeGpuNode('g', { capacity: false }))).toBe('—');
+  });
+  it('classifies each row once across columns', () => {
+    const n = makeGpuNode('g');
+    cols[0].getter(n);
+    n.metadata.labels = {};
+    n.status.capacity = {};
+    // Cached classification from the first getter is reused.
+    expect(cols[1].getter(n)).toBe('8');
+  });
+});
+
+describe('topology', () => {
+  it('builds a full 8×8 xGMI mesh with 7 links per GPU', () => {
+    const m = buildXgmiMatrix(8);
+    expect(m.size).toBe(8);
+    expect(m.linksPerGpu).toBe(7);
+    expect(m.perGpuPeakGBs).toBe(7 * 153);
+    expect(m.ringBusGBs).toBe(153);
+    expect(isFullMesh(m)).toBe(true);
+    expect(m.cells[3][3].kind).toBe('self');
+  });
+  it('overlays measured throughput', () => {
+    const m = buildXgmiMatrix(8, { '0-1': 42.5 });
+    expect(m.cells[0][1].measuredGBs).toBe(42.5);
+    expect(m.cells[1][0].measuredGBs).toBeNull();
+  });
+  it('detects a non-mesh from probed link types', () => {
+    const m = buildXgmiMatrix(2, null, { '0-1': { type: 'PCIE', hops: 2 }, '1-0': { type: 'PCIE', hops: 2 } });
+    expect(isFullMesh(m)).toBe(false);
+    expect(m.cells[0][1].kind).toBe('pcie');
+  });
+  it('a single GPU is not a mesh', () => {
+    expect(isFullMesh(buildXgmiMatrix(1))).toBe(false);
+  });
+  it('fills inferred slots in pod order, skipping finished pods', () => {
+    const node = makeGpuNode('g', { gpus: 8 });
+    const s = buildGpuSlots(node, [makeGpuPod('a', { gpus: 2 }), makeGpuPod('done', { gpus: 4, phase: 'Succeeded' }), makeGpuPod('b', { gpus: 1 })]);
+    expect(s.exact).toBe(false);
+    expect(s.slots.map((x) => x.pod)).toEqual(['a', 'a', 'b', null, null, null, null, null]);
+    expect(s.slots[0].inferred).toBe(true);
+  });
+  it('never over-fills slots', () => {
+    const s = buildGpuSlots(makeGpuNode('g', { gpus: 2 }), [makeGpuPod('a', { gpus: 8 })]);
+    expect(s.slots).toHaveLength(2);
+  });
+  it('uses exporter owners when present', () => {
+    const s = buildGpuSlots(makeGpuNode('g'), [], [{ gpu: '7', pod: 'x', namespace: 'ns' }, { gpu: '9', pod: 'bad' }]);
+    expect(s.exact).toBe(true);
+    expect(s.slots[7]).toEqual({ index: 7, pod: 'x', namespace: 'ns', inferred: false });
+  });
+});
+
+void NOW;
+void findSection;

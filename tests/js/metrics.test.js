@@ -1,0 +1,245 @@
+/**
+ * Metrics-client specs. The reference has NO direct tests for
+ * src/api/metrics.ts (SURVEY.md §4 gaps); these cover discovery, the
+ * exporter and node-exporter joins, the per-(node, gpu) key, caching and
+ * range queries.
+ */
+import {
+  PROMETHEUS_SERVICES,
+  SERIES,
+  createMetricsSource,
+  joinExporterResults,
+  joinNodeExporterResults,
+  servicePath,
+  summarizeMetrics,
+} from '../../src/api/metrics.js';
+
+const BASE0 = servicePath(PROMETHEUS_SERVICES[0]);
+const BASE1 = servicePath(PROMETHEUS_SERVICES[1]);
+
+function vec(metric, v) {
+  return { metric, value: [1760000000, String(v)] };
+}
+function ok(result) {
+  return { status: 'success', data: { resultType: 'vector', result } };
+}
+
+/** Exporter series for `nodes` × 8 GPUs. */
+function exporterData(nodes) {
+  const d = {};
+  const E = SERIES.exporter;
+  [E.power, E.vramUsed, E.vramTotal, E.gfx, E.umc, E.temp].forEach((k) => (d[k] = []));
+  d.__xgmi = [];
+  nodes.forEach((node) => {
+    for (let g = 0; g < 8; g++) {
+      const m = { hostname: node, gpu_id: String(g), instance: node + ':5000' };
+      d[E.power].push(vec(Object.assign({ pod: g < 2 ? 'train-' + g : undefined, namespace: g < 2 ? 'ml' : undefined }, m), 700 + g));
+      d[E.vramUsed].push(vec(m, 1024 * (g + 1)));
+      d[E.vramTotal].push(vec(m, 288 * 1000 * 1000 * 1000 / (1024 * 1024)));
+      d[E.gfx].push(vec(m, 50));
+      d[E.umc].push(vec(m, 30));
+      d[E.temp].push(vec(m, 60));
+      d.__xgmi.push(vec(Object.assign({ __name__: 'xgmi_neighbor_0_tx_throughput' }, m), 50e9));
+    }
+  });
+  return d;
+}
+
+/** A fake proxy: answers probes on `up` services and queries from `data`. */
+function prom(opts) {
+  const o = Object.assign({ up: [BASE0], data: exporterData(['n0']), ne: null }, opts || {});
+  return vi.fn((path) => {
+    const base = o.up.find((b) => path.indexOf(b) === 0);
+    if (!base) return Promise.reject(new Error('503'));
+    const q = decodeURIComponent((path.split('query=')[1] || '').split('&')[0]);
+    if (q === '1') return Promise.resolve(ok([{ metric: {}, value: [0, '1'] }]));
+    if (path.indexOf('/query_range') >= 0) {
+      return Promise.resolve({
+        status: 'success',
+        data: { resultType: 'matrix', result: [{ metric: { hostname: 'n0' }, values: [[1, '100'], [2, '200']] }] },
+      });
+    }
+    if (q.indexOf('{__name__=~') === 0) return Promise.resolve(ok(o.data ? o.data.__xgmi || [] : []));
+    if (o.data && o.data[q]) return Promise.resolve(ok(o.data[q]));
+    if (o.ne && o.ne[q]) return Promise.resolve(ok(o.ne[q]));
+    return Promise.resolve(ok([]));
+  });
+}
+
+describe('discovery', () => {
+  it('probes all candidate services in parallel', async () => {
+    const request = prom();
+    const src = createMetricsSource({ request });
+    await src.discover();
+    const probes = request.mock.calls.filter((c) => c[0].indexOf('query=1') >= 0);
+    expect(probes).toHaveLength(PROMETHEUS_SERVICES.length);
+  });
+  it('prefers the highest-priority reachable service', async () => {
+    const src = createMetricsSource({ request: prom({ up: [BASE1, BASE0] }) });
+    expect(await src.discover()).toBe(BASE0);
+  });
+  it('falls back to a lower-priority service', async () => {
+    const src = createMetricsSource({ request: prom({ up: [BASE1] }) });
+    expect(await src.discover()).toBe(BASE1);
+  });
+  it('returns null when nothing answers', async () => {
+    const src = createMetricsSource({ request: prom({ up: [] }) });
+    expect(await src.discover()).toBeNull();
+  });
+  it('caches the discovered path', async () => {
+    const request = prom();
+    const src = createMetricsSource({ request });
+    await src.discover();
+    const n = request.mock.calls.length;
+    await src.discover();
+    expect(request.mock.calls.length).toBe(n);
+  });
+  it('re-discovers after the TTL', async () => {
+    let now = 0;
+    const request = prom();
+    const src = createMetricsSource({
+      request, discoveryTtlMs: 1000,
+      clock: { setTimeout, clearTimeout, now: () => now },
+    });
+    await src.discover();
+    const n = request.mock.calls.length;
+    now = 5000;
+    await src.discover();
+    expect(request.mock.calls.length).toBe(n + PROMETHEUS_SERVICES.length);
+  });
+  it('times out a hanging probe', async () => {
+    vi.useFakeTimers();
+    const request = vi.fn(() => new Promise(() => {}));
+    const src = createMetricsSource({ request, timeoutMs: 2000 });
+    const p = src.discover();
+    await vi.advanceTimersByTimeAsync(2000);
+    expect(await p).toBeNull();
+    vi.useRealTimers();
+  });
+});
+
+describe('fetchGpuMetrics', () => {
+  it('returns null when Prometheus is unreachable', async () => {
+    const src = createMetricsSource({ request: prom({ up: [] }) });
+    expect(await src.fetchGpuMetrics()).toBeNull();
+  });
+  it('joins exporter series per (node, gpu)', async () => {
+    const src = createMetricsSource({ request: prom({ data: exporterData(['n0', 'n1']) }) });
+    const m = await src.fetchGpuMetrics();
+    expect(m.source).toBe('amd-exporter');
+    expect(m.gpus).toHaveLength(16);
+    const g = m.gpus.find((x) => x.nodeName === 'n1' && x.gpu === '3');
+    expect(g.powerWatts).toBe(703);
+    expect(g.gfxActivityPct).toBe(50);
+    expect(g.vramUsedBytes).toBe(4 * 1024 * 1024 * 1024);
+  });
+  it('does not collide identical GPU ids across nodes (reference quirk Q1)', async () => {
+    const d = exporterData(['a', 'b']);
+    d[SERIES.exporter.power].forEach((r) => {
+      if (r.metric.hostname === 'b') r.value[1] = '111';
+    });
+    const src = createMetricsSource({ request: prom({ data: d }) });
+    const m = await src.fetchGpuMetrics();
+    expect(m.gpus.find((x) => x.nodeName === 'a' && x.gpu === '5').powerWatts).toBe(705);
+    expect(m.gpus.find((x) => x.nodeName === 'b' && x.gpu === '5').powerWatts).toBe(111);
+  });
+  it('captures pod ownership labels', async () => {
+    const src = createMetricsSource({ request: prom() });
+    const m = await src.fetchGpuMetrics();
+    expect(m.gpus[0].pod).toBe('train-0');
+    expect(m.gpus[0].namespace).toBe('ml');
+    expect(m.gpus[4].pod).toBeNull();
+  });
+  it('maps xGMI neighbour series onto peer indices', async () => {
+    const src = createMetricsSource({ request: prom() });
+    const m = await src.fetchGpuMetrics();
+    expect(m.xgmi.n0['0-1']).toBe(50);
+    expect(m.xgmi.n0['3-0']).toBe(50);
+  });
+  it('remembers the answering source and skips the other', async () => {
+    const request = prom();
+    const src = createMetricsSource({ request });
+    await src.fetchGpuMetrics();
+    const n = request.mock.calls.length;
+    await src.fetchGpuMetrics();
+    const second = request.mock.calls.slice(n).map((c) => decodeURIComponent(c[0]));
+    expect(second.some((p) => p.indexOf('node_hwmon') >= 0)).toBe(false);
+    expect(second).toHaveLength(7);
+  });
+  it('falls back to node-exporter amdgpu hwmon + DRM', async () => {
+    const N = SERIES.nodeExporter;
+    const ne = {};
+    ne[N.chips] = [
+      vec({ instance: '10.0.0.1:9100', chip: '0000:15:00_0', chip_name: 'amdgpu' }, 1),
+      vec({ instance: '10.0.0.1:9100', chip: '0000:05:00_0', chip_name: 'amdgpu' }, 1),
+    ];
+    ne[N.power] = [
+      vec({ instance: '10.0.0.1:9100', chip: '0000:05:00_0' }, 650),
+      vec({ instance: '10.0.0.1:9100', chip: '0000:15:00_0' }, 900),
+    ];
+    ne[N.busy] = [vec({ instance: '10.0.0.1:9100', card: 'card1' }, 88)];
+    ne[N.uname] = [vec({ instance: '10.0.0.1:9100', nodename: 'mi355x-0' }, 1)];
+    const src = createMetricsSource({ request: prom({ data: null, ne }) });
+    const m = await src.fetchGpuMetrics();
+    expect(m.source).toBe('node-exporter');
+    expect(m.gpus.map((g) => [g.nodeName, g.gpu, g.powerWatts])).toEqual([
+      ['mi355x-0', '0', 650],
+      ['mi355x-0', '1', 900],
+    ]);
+    expect(m.gpus[1].gfxActivityPct).toBe(88);
+  });
+  it('returns an empty GPU list when Prometheus has no AMD series', async () => {
+    const src = createMetricsSource({ request: prom({ data: null }) });
+    const m = await src.fetchGpuMetrics();
+    expect(m.gpus).toHaveLength(0);
+    expect(m.source).toBeNull();
+  });
+  it('fills the power cap with the MI355X board power when absent', async () => {
+    const src = createMetricsSource({ request: prom() });
+    const m = await src.fetchGpuMetrics();
+    expect(m.gpus[0].powerCapWatts).toBe(1400);
+  });
+});
+
+describe('joins (direct)', () => {
+  it('joinExporterResults tolerates malformed rows', () => {
+    const r = {};
+    r[SERIES.exporter.power] = [null, { metric: 'x' }, vec({ hostname: 'n', gpu_id: '0' }, 'NaN')];
+    const j = joinExporterResults(r);
+    expect(j.gpus).toHaveLength(1);
+    expect(j.gpus[0].powerWatts).toBeNull();
+  });
+  it('joinNodeExporterResults maps instance to nodename', () => {
+    const N = SERIES.nodeExporter;
+    const r = {};
+    r[N.chips] = [vec({ instance: 'i', chip: 'c' }, 1)];
+    r[N.uname] = [vec({ instance: 'i', nodename: 'node-x' }, 1)];
+    expect(joinNodeExporterResults(r).gpus[0].nodeName).toBe('node-x');
+  });
+});
+
+describe('fetchSeries', () => {
+  it('returns per-node power and HBM series', async () => {
+    const src = createMetricsSource({ request: prom() });
+    const s = await src.fetchSeries(600, 30);
+    expect(s.power.n0).toEqual([[1, 100], [2, 200]]);
+    expect(s.vram.n0[1][1]).toBe(200 * 1024 * 1024);
+  });
+  it('passes start/end/step to query_range', async () => {
+    const request = prom();
+    const src = createMetricsSource({ request, clock: { setTimeout, clearTimeout, now: () => 1000000 } });
+    await src.fetchSeries(600, 15);
+    const rq = request.mock.calls.map((c) => c[0]).find((p) => p.indexOf('query_range') >= 0);
+    expect(rq).toContain('&start=400&end=1000&step=15');
+  });
+});
+
+describe('summarizeMetrics', () => {
+  it('sums power, caps and HBM and averages activity', () => {
+    const s = summarizeMetrics(joinExporterResults(exporterData(['n0'])));
+    expect(s.gpus).toBe(8);
+    expect(s.powerWatts).toBe(700 * 8 + 28);
+    expect(s.powerCapWatts).toBe(8 * 1400);
+    expect(s.avgGfxActivityPct).toBe(50);
+  });
+});

@@ -1,0 +1,404 @@
+/**
+ * Page view-model specs — the analog of the reference's component tests
+ * (OverviewPage.test.tsx 9, DevicePluginsPage.test.tsx 6, NodesPage.test.tsx 5,
+ * PodsPage.test.tsx 6, MetricsPage.test.tsx 9). Assertions target section
+ * titles, row labels, status values and refresh aria-labels, as there.
+ */
+import {
+  overviewView,
+  devicePluginsView,
+  nodesView,
+  podsView,
+  metricsView,
+  allocationBar,
+  powerBar,
+  hbmBar,
+  gpuContainerLines,
+  ACTIVE_PODS_LIMIT,
+} from '../../src/view/pages.js';
+import { countRows, findSection, firstBlock, firstTable, loaders, rowNames, rowValue, sectionTitles, text } from '../../src/view/ir.js';
+import { renderPage, textContent } from '../../src/view/html.js';
+import { joinExporterResults, SERIES } from '../../src/api/metrics.js';
+import { NOW, makeContext, makeDeviceConfig, makeGpuNode, makeGpuPod, makeNode, makePlainPod, makePluginPod } from './fixtures.js';
+
+const opts = { now: NOW };
+
+// ---------------------------------------------------------------------------
+describe('overviewView', () => {
+  it('shows only the loader on first load', () => {
+    const vm = overviewView(makeContext({ loading: true, lastUpdated: null }), opts);
+    expect(loaders(vm)).toEqual(['Loading AMD GPU data...']);
+    expect(vm.title).toBeNull();
+  });
+
+  it('keeps content visible during a refresh (no loader swap)', () => {
+    const vm = overviewView(makeContext({ loading: true, refreshing: true, nodes: [makeGpuNode('g')] }), opts);
+    expect(loaders(vm)).toEqual([]);
+    expect(vm.refresh.label).toBe('Refreshing…');
+    expect(vm.refresh.disabled).toBe(true);
+  });
+
+  it('has the page header and refresh aria-label', () => {
+    const vm = overviewView(makeContext(), opts);
+    expect(vm.title).toBe('AMD GPU — Overview');
+    expect(vm.refresh.ariaLabel).toBe('Refresh AMD GPU data');
+  });
+
+  it('shows "Plugin Not Detected" with install instructions when nothing is installed', () => {
+    const vm = overviewView(makeContext(), opts);
+    const s = findSection(vm, 'Plugin Not Detected');
+    expect(s).not.toBeNull();
+    expect(text(rowValue(s, 'Install (Helm)'))).toContain('gpu-operator-charts');
+    expect(rowValue(s, 'Status').status).toBe('warning');
+  });
+
+  it('shows the CRD notice when plugin pods exist without the CRD', () => {
+    const vm = overviewView(makeContext({ pluginPods: [makePluginPod('dp')] }), opts);
+    expect(sectionTitles(vm)).toContain('Notice');
+    expect(sectionTitles(vm)).not.toContain('Plugin Not Detected');
+  });
+
+  it('renders the DeviceConfig status table when the CRD exists', () => {
+    const vm = overviewView(makeContext({ crdAvailable: true, deviceConfigs: [makeDeviceConfig('cfg', { desired: 4, available: 3 })] }), opts);
+    const t = firstTable(findSection(vm, 'Device Config Status'));
+    expect(t.columns).toEqual(['Name', 'Namespace', 'Status', 'Metrics Exporter', 'Node Labeller', 'Selector', 'Age']);
+    expect(t.rows[0][0]).toBe('cfg');
+    expect(t.rows[0][2]).toEqual({ t: 'status', status: 'warning', text: '3/4 ready' });
+    expect(t.rows[0][6]).toBe('3d');
+  });
+
+  it('lists plugin daemon pods with their component', () => {
+    const vm = overviewView(makeContext({ pluginPods: [makePluginPod('dp-0'), makePluginPod('lb-0', { label: 'amdgpu-labeller-ds', ready: false })] }), opts);
+    const t = firstTable(findSection(vm, 'Plugin Daemon Pods'));
+    expect(t.rows.map((r) => r[2])).toEqual(['Device Plugin', 'Node Labeller']);
+    expect(t.rows[1][4].status).toBe('warning');
+  });
+
+  it('summarises GPU nodes with MI355X model and HBM', () => {
+    const vm = overviewView(makeContext({ nodes: [makeGpuNode('a'), makeGpuNode('b', { ready: false })] }), opts);
+    const s = findSection(vm, 'GPU Nodes');
+    expect(rowValue(s, 'Total GPU Nodes')).toEqual({ t: 'status', status: 'success', text: '2' });
+    expect(rowValue(s, 'Ready Nodes')).toBe('1');
+    expect(rowValue(s, 'Total GPU Devices')).toBe('16');
+    expect(rowValue(s, 'Total HBM')).toContain('4.6 TB');
+    expect(text(rowValue(s, 'GPU Model'))).toContain('MI355X');
+  });
+
+  it('warns when there are zero GPU nodes', () => {
+    const vm = overviewView(makeContext({ nodes: [makeNode('cpu')] }), opts);
+    expect(rowValue(findSection(vm, 'GPU Nodes'), 'Total GPU Nodes').status).toBe('warning');
+    expect(findSection(vm, 'GPU Allocation')).toBeNull();
+  });
+
+  it('computes allocation from GPUs held', () => {
+    const ctx = makeContext({
+      nodes: [makeGpuNode('g0')],
+      pods: [makeGpuPod('a', { node: 'g0', gpus: 4 }), makeGpuPod('b', { node: 'g0', gpus: 2, phase: 'Succeeded' })],
+    });
+    const s = findSection(overviewView(ctx, opts), 'GPU Allocation');
+    expect(rowValue(s, 'In Use')).toBe('4');
+    expect(rowValue(s, 'Free')).toEqual({ t: 'status', status: 'success', text: '4' });
+    expect(firstBlock(s, 'pctbar').label).toBe('GPU Allocation (50%)');
+  });
+
+  it('warns when no GPU is free', () => {
+    const ctx = makeContext({ nodes: [makeGpuNode('g0', { gpus: 1 })], pods: [makeGpuPod('a', { node: 'g0', gpus: 1 })] });
+    expect(rowValue(findSection(overviewView(ctx, opts), 'GPU Allocation'), 'Free').status).toBe('warning');
+  });
+
+  it('counts workload phases', () => {
+    const ctx = makeContext({
+      nodes: [makeGpuNode('g0')],
+      pods: [makeGpuPod('a'), makeGpuPod('b', { phase: 'Pending' }), makeGpuPod('c', { phase: 'Failed' })],
+    });
+    const s = findSection(overviewView(ctx, opts), 'GPU Workloads');
+    expect(rowNames(s)).toEqual(['Total GPU Pods', 'Running', 'Pending', 'Failed']);
+    expect(rowValue(s, 'Failed').status).toBe('error');
+  });
+
+  it('caps Active GPU Pods at the first 10 running', () => {
+    const pods = [];
+    for (let i = 0; i < 15; i++) pods.push(makeGpuPod('p' + i));
+    pods.push(makeGpuPod('pending', { phase: 'Pending' }));
+    const t = firstTable(findSection(overviewView(makeContext({ nodes: [makeGpuNode('mi355x-0')], pods }), opts), 'Active GPU Pods'));
+    expect(t.rows).toHaveLength(ACTIVE_PODS_LIMIT);
+    expect(t.rows[0][3]).toBe('GPU: 1');
+  });
+
+  it('surfaces the aggregated error', () => {
+    const vm = overviewView(makeContext({ error: 'nodes forbidden' }), opts);
+    expect(rowValue(findSection(vm, 'Error'), 'Status')).toEqual({ t: 'status', status: 'error', text: 'nodes forbidden' });
+  });
+});
+
+// ---------------------------------------------------------------------------
+describe('devicePluginsView', () => {
+  it('shows the loader on first load', () => {
+    expect(loaders(devicePluginsView(makeContext({ loading: true, lastUpdated: null }), opts))).toEqual(['Loading device plugin data...']);
+  });
+  it('has header and aria-label', () => {
+    const vm = devicePluginsView(makeContext(), opts);
+    expect(vm.title).toBe('AMD GPU — Device Plugins');
+    expect(vm.refresh.ariaLabel).toBe('Refresh device plugin data');
+  });
+  it('shows "CRD Not Available" without the CRD', () => {
+    const s = findSection(devicePluginsView(makeContext(), opts), 'CRD Not Available');
+    expect(text(rowValue(s, 'Status'))).toContain('amd.com/v1alpha1');
+  });
+  it('shows "No Device Configs" when the CRD exists but is empty', () => {
+    const vm = devicePluginsView(makeContext({ crdAvailable: true }), opts);
+    expect(sectionTitles(vm)).toContain('No Device Configs');
+    expect(sectionTitles(vm)).not.toContain('CRD Not Available');
+  });
+  it('renders one card per DeviceConfig with operand rows', () => {
+    const vm = devicePluginsView(makeContext({ crdAvailable: true, deviceConfigs: [makeDeviceConfig('a'), makeDeviceConfig('b', { exporter: false })] }), opts);
+    const a = findSection(vm, 'DeviceConfig: a');
+    expect(rowValue(a, 'Status')).toEqual({ t: 'status', status: 'success', text: '2/2 ready' });
+    expect(rowValue(a, 'Metrics Exporter')).toEqual({ t: 'status', status: 'success', text: 'Enabled — port 5000' });
+    expect(rowNames(a)).toContain('Metrics Exporter Pods');
+    expect(rowValue(findSection(vm, 'DeviceConfig: b'), 'Metrics Exporter').status).toBe('warning');
+    expect(rowValue(a, 'Node Selector')).toBe('feature.node.kubernetes.io/amd-gpu=true');
+  });
+  it('shows Unavailable Nodes only when some are unavailable', () => {
+    const vm = devicePluginsView(makeContext({ crdAvailable: true, deviceConfigs: [makeDeviceConfig('a', { desired: 4, available: 1 })] }), opts);
+    expect(rowValue(findSection(vm, 'DeviceConfig: a'), 'Unavailable Nodes')).toEqual({ t: 'status', status: 'error', text: '3' });
+    const vm2 = devicePluginsView(makeContext({ crdAvailable: true, deviceConfigs: [makeDeviceConfig('a')] }), opts);
+    expect(rowNames(findSection(vm2, 'DeviceConfig: a'))).not.toContain('Unavailable Nodes');
+  });
+  it('lists daemon pods with restarts flagged', () => {
+    const vm = devicePluginsView(makeContext({ pluginPods: [makePluginPod('dp-0', { restarts: 3 }), makePluginPod('dp-1')] }), opts);
+    const t = firstTable(findSection(vm, 'Plugin Daemon Pods'));
+    expect(t.columns).toEqual(['Name', 'Namespace', 'Component', 'Node', 'Ready', 'Restarts', 'Age']);
+    expect(t.rows[0][5]).toEqual({ t: 'status', status: 'warning', text: '3' });
+    expect(t.rows[1][5]).toBe('0');
+  });
+  it('surfaces errors', () => {
+    expect(sectionTitles(devicePluginsView(makeContext({ error: 'x' }), opts))[0]).toBe('Error');
+  });
+});
+
+// ---------------------------------------------------------------------------
+describe('nodesView', () => {
+  it('shows the loader on first load', () => {
+    expect(loaders(nodesView(makeContext({ loading: true, lastUpdated: null }), opts))).toEqual(['Loading GPU node data...']);
+  });
+  it('shows "No GPU Nodes Found" on a CPU cluster', () => {
+    const vm = nodesView(makeContext({ nodes: [makeNode('c')] }), opts);
+    expect(sectionTitles(vm)).toEqual(['No GPU Nodes Found']);
+    expect(vm.refresh.ariaLabel).toBe('Refresh node data');
+  });
+  it('renders the summary table with GPU-based allocation', () => {
+    const ctx = makeContext({
+      nodes: [makeGpuNode('g0'), makeGpuNode('g1')],
+      pods: [makeGpuPod('a', { node: 'g0', gpus: 6 }), makeGpuPod('b', { node: 'g0', gpus: 1 }), makeGpuPod('c', { node: 'g1', gpus: 1 })],
+    });
+    const t = firstTable(findSection(nodesView(ctx, opts), 'GPU Node Summary'));
+    expect(t.columns).toEqual(['Node', 'Ready', 'GPU Model', 'GPU Devices', 'Allocation', 'GPU Pods', 'Age']);
+    expect(t.rows[0][4].text).toBe('7/8 (88%)');
+    expect(t.rows[0][4].color).toBe('#f57c00');
+    expect(t.rows[0][5]).toBe('2');
+    expect(t.rows[1][4].text).toBe('1/8 (13%)');
+  });
+  it('renders one card per node with HBM and workload pods', () => {
+    const ctx = makeContext({ nodes: [makeGpuNode('g0')], pods: [makeGpuPod('a', { node: 'g0', gpus: 2 })] });
+    const s = findSection(nodesView(ctx, opts), 'g0');
+    expect(rowValue(s, 'GPU Devices (amd.com/gpu)')).toBe('8');
+    expect(rowValue(s, 'HBM')).toBe('2.3 TB (8 × 288G)');
+    expect(rowValue(s, 'GPU Workload Pods')).toBe('a');
+    expect(rowValue(s, 'GPU (capacity)')).toBe('8');
+    expect(rowValue(s, 'Kubelet')).toBe('v1.31.2');
+  });
+  it('adds per-GPU slots and the xGMI matrix to each card', () => {
+    const ctx = makeContext({ nodes: [makeGpuNode('g0')], pods: [makeGpuPod('a', { node: 'g0', gpus: 3 })] });
+    const s = findSection(nodesView(ctx, opts), 'g0');
+    const slots = firstBlock(s, 'slots');
+    expect(slots.slots.filter((x) => x.pod === 'a')).toHaveLength(3);
+    expect(slots.exact).toBe(false);
+    const m = firstBlock(s, 'matrix');
+    expect(m.matrix.size).toBe(8);
+    expect(m.fullMesh).toBe(true);
+  });
+  it('uses exporter pod labels for exact slots when metrics are given', () => {
+    const E = SERIES.exporter;
+    const r = {};
+    r[E.power] = [{ metric: { hostname: 'g0', gpu_id: '5', pod: 'a', namespace: 'ml' }, value: [0, '700'] }];
+    const metrics = joinExporterResults(r);
+    const ctx = makeContext({ nodes: [makeGpuNode('g0')], pods: [makeGpuPod('a', { node: 'g0', gpus: 1 })] });
+    const slots = firstBlock(findSection(nodesView(ctx, { now: NOW, metrics }), 'g0'), 'slots');
+    expect(slots.exact).toBe(true);
+    expect(slots.slots[5].pod).toBe('a');
+    expect(slots.slots[0].pod).toBeNull();
+  });
+  it('marks not-ready nodes', () => {
+    const t = firstTable(findSection(nodesView(makeContext({ nodes: [makeGpuNode('g', { ready: false })] }), opts), 'GPU Node Summary'));
+    expect(t.rows[0][1]).toEqual({ t: 'status', status: 'error', text: 'Not Ready' });
+  });
+  it('shows partition mode on partitioned nodes', () => {
+    const s = findSection(nodesView(makeContext({ nodes: [makeGpuNode('g', { partition: 'cpx/nps4' })] }), opts), 'g');
+    expect(rowValue(s, 'Partition Mode')).toBe('MI355X (CPX/NPS4)');
+  });
+});
+
+// ---------------------------------------------------------------------------
+describe('podsView', () => {
+  it('shows the loader on first load', () => {
+    expect(loaders(podsView(makeContext({ loading: true, lastUpdated: null }), opts))).toEqual(['Loading GPU pod data...']);
+  });
+  it('shows "No GPU Pods Found"', () => {
+    const vm = podsView(makeContext({ pods: [makePlainPod('x')] }), opts);
+    expect(sectionTitles(vm)).toEqual(['No GPU Pods Found']);
+    expect(vm.refresh.ariaLabel).toBe('Refresh pod data');
+  });
+  it('summarises phases and GPUs held', () => {
+    const ctx = makeContext({
+      pods: [makeGpuPod('a', { gpus: 8 }), makeGpuPod('b', { phase: 'Pending', gpus: 2 }), makeGpuPod('c', { phase: 'Failed', gpus: 4 })],
+    });
+    const s = findSection(podsView(ctx, opts), 'Summary');
+    expect(rowValue(s, 'Total GPU Pods')).toBe('3');
+    expect(rowValue(s, 'Running').status).toBe('success');
+    expect(rowValue(s, 'GPUs Held')).toBe('10');
+  });
+  it('lists all GPU pods with phase status and restarts', () => {
+    const ctx = makeContext({ pods: [makeGpuPod('a', { restarts: 2 }), makeGpuPod('b', { phase: 'Failed' })] });
+    const t = firstTable(findSection(podsView(ctx, opts), 'All GPU Pods'));
+    expect(t.columns).toEqual(['Name', 'Namespace', 'Node', 'Phase', 'GPU Resources', 'Restarts', 'Age']);
+    expect(t.rows[0][3]).toEqual({ t: 'status', status: 'success', text: 'Running' });
+    expect(t.rows[1][3].status).toBe('error');
+    expect(t.rows[0][5].status).toBe('warning');
+    expect(text(t.rows[0][4])).toBe('trainer: GPU: 1');
+  });
+  it('shows the pending attention table with waiting reasons', () => {
+    const ctx = makeContext({ pods: [makeGpuPod('a'), makeGpuPod('b', { phase: 'Pending', waiting: 'ImagePullBackOff', gpus: 4 })] });
+    const t = firstTable(findSection(podsView(ctx, opts), 'Attention: Pending GPU Pods'));
+    expect(t.rows).toHaveLength(1);
+    expect(t.rows[0][2]).toBe('GPU: 4');
+    expect(t.rows[0][3]).toBe('ImagePullBackOff');
+  });
+  it('omits the pending table when nothing is pending', () => {
+    expect(sectionTitles(podsView(makeContext({ pods: [makeGpuPod('a')] }), opts))).not.toContain('Attention: Pending GPU Pods');
+  });
+  it('gpuContainerLines shows req/lim when they differ and marks init containers', () => {
+    const p = makeGpuPod('p', { gpus: 1, init: 2 });
+    p.spec.containers[0].resources.limits['amd.com/gpu'] = '2';
+    expect(text(gpuContainerLines(p))).toBe('warmup (init): GPU: 2\ntrainer: GPU: req=1 lim=2');
+  });
+  it('gpuContainerLines handles limits-only containers', () => {
+    expect(text(gpuContainerLines(makeGpuPod('p', { limitsOnly: true, gpus: 2 })))).toBe('trainer: GPU: req=— lim=2');
+  });
+});
+
+// ---------------------------------------------------------------------------
+describe('metricsView', () => {
+  const E = SERIES.exporter;
+  function metrics(nodes, gpusPer) {
+    const r = {};
+    r[E.power] = [];
+    r[E.vramUsed] = [];
+    r[E.vramTotal] = [];
+    nodes.forEach((n) => {
+      for (let g = 0; g < gpusPer; g++) {
+        const m = { hostname: n, gpu_id: String(g) };
+        r[E.power].push({ metric: m, value: [0, String(1300)] });
+        r[E.vramUsed].push({ metric: m, value: [0, String(100 * 1024)] });
+        r[E.vramTotal].push({ metric: m, value: [0, String(274658)] });
+      }
+    });
+    const j = joinExporterResults(r);
+    return { source: 'amd-exporter', gpus: j.gpus, xgmi: j.xgmi, fetchedAt: new Date(NOW).toISOString(), prometheusPath: '/p' };
+  }
+  const ctx = makeContext({ nodes: [makeGpuNode('n0')] });
+
+  it('always shows the availability box and header', () => {
+    const vm = metricsView(ctx, { metrics: null, fetchError: null, fetching: false }, opts);
+    expect(vm.title).toBe('AMD GPU — Metrics');
+    expect(sectionTitles(vm)).toEqual(['Metric Availability']);
+    expect(vm.refresh.ariaLabel).toBe('Refresh metrics');
+  });
+  it('shows the context loader while the store loads', () => {
+    const vm = metricsView(makeContext({ loading: true, lastUpdated: null }), { metrics: null, fetchError: null, fetching: false }, opts);
+    expect(loaders(vm)).toEqual(['Loading AMD GPU data...']);
+    expect(vm.refresh.disabled).toBe(true);
+  });
+  it('shows the query loader while fetching the first time', () => {
+    const vm = metricsView(ctx, { metrics: null, fetchError: null, fetching: true }, opts);
+    expect(loaders(vm)).toEqual(['Querying Prometheus for GPU metrics...']);
+    expect(vm.refresh.label).toBe('Refreshing…');
+  });
+  it('shows "Prometheus Unreachable" with the checked services', () => {
+    const vm = metricsView(ctx, { metrics: null, fetchError: 'Could not reach Prometheus', fetching: false }, opts);
+    const s = findSection(vm, 'Prometheus Unreachable');
+    expect(rowValue(s, 'Error').status).toBe('error');
+    expect(rowValue(s, 'Checked services')).toContain('kube-prometheus-stack-prometheus:9090');
+  });
+  it('shows "No AMD GPU Metrics" with the GPU node list', () => {
+    const vm = metricsView(ctx, { metrics: { source: null, gpus: [], xgmi: {}, fetchedAt: new Date(NOW).toISOString() }, fetchError: null, fetching: false }, opts);
+    expect(rowValue(findSection(vm, 'No AMD GPU Metrics in Prometheus'), 'GPU Nodes')).toBe('n0');
+  });
+  it('summarises power and HBM', () => {
+    const vm = metricsView(ctx, { metrics: metrics(['n0'], 8), fetchError: null, fetching: false }, opts);
+    const s = findSection(vm, 'GPU Power Summary');
+    expect(rowValue(s, 'GPUs Monitored')).toBe('8');
+    expect(rowValue(s, 'Total Power').text).toBe('10400.0 W / 11200.0 W (93%)');
+    expect(rowValue(s, 'Total Power').color).toBe('#d32f2f');
+    expect(rowValue(s, 'Source')).toBe('AMD Device Metrics Exporter');
+  });
+  it('renders one card per node with a per-GPU table', () => {
+    const vm = metricsView(ctx, { metrics: metrics(['n0', 'n1'], 8), fetchError: null, fetching: false }, opts);
+    const s = findSection(vm, 'n1 — 8 × MI355X');
+    expect(firstTable(s).rows).toHaveLength(8);
+    expect(firstTable(s).rows[0][0]).toBe('GPU 0');
+  });
+  it('adds the time-series section when range data exists', () => {
+    const vm = metricsView(ctx, { metrics: metrics(['n0'], 1), fetchError: null, fetching: false, series: { power: { n0: [[1, 2]] }, vram: {} } }, opts);
+    expect(sectionTitles(vm)).toContain('Power & HBM (last 30 min)');
+  });
+  it('powerBar without a cap shows watts only', () => {
+    expect(powerBar(512.25, null).text).toBe('512.3 W');
+    expect(powerBar(512.25, null).pct).toBeNull();
+  });
+  it('hbmBar formats used/total', () => {
+    expect(hbmBar(144e9, 288e9).text).toBe('144 GB / 288 GB (50%)');
+    expect(hbmBar(null, 288e9)).toBe('—');
+  });
+});
+
+// ---------------------------------------------------------------------------
+describe('allocationBar', () => {
+  it('returns a dash without allocatable GPUs', () => {
+    expect(allocationBar(1, 0)).toBe('—');
+  });
+  it('caps at 100% and colours by threshold', () => {
+    expect(allocationBar(10, 8).pct).toBe(100);
+    expect(allocationBar(10, 8).color).toBe('#d32f2f');
+    expect(allocationBar(1, 8).color).toBe('#ed1c24');
+  });
+});
+
+// ---------------------------------------------------------------------------
+describe('html rendering', () => {
+  it('renders sections, tables and status labels semantically', () => {
+    const ctx = makeContext({ nodes: [makeGpuNode('g0')], pods: [makeGpuPod('a', { node: 'g0' })] });
+    const html = renderPage(nodesView(ctx, opts));
+    expect(html).toContain('<h1>AMD GPU — Nodes</h1>');
+    expect(html).toContain('<button aria-label="Refresh node data">Refresh</button>');
+    expect(html).toContain('<h2>GPU Node Summary</h2>');
+    expect(html).toContain('<span data-status="success">Ready</span>');
+    expect(html).toContain('data-testid="xgmi-matrix" data-full-mesh="true"');
+  });
+  it('escapes user-controlled strings', () => {
+    const n = makeGpuNode('<script>');
+    const html = renderPage(nodesView(makeContext({ nodes: [n] }), opts));
+    expect(html).not.toContain('<script>');
+    expect(html).toContain('&lt;script&gt;');
+  });
+  it('textContent strips markup', () => {
+    const html = renderPage(overviewView(makeContext({ loading: true, lastUpdated: null }), opts));
+    expect(textContent(html)).toBe('Loading AMD GPU data...');
+  });
+  it('countRows counts table rows and GPU cells', () => {
+    const ctx = makeContext({ nodes: [makeGpuNode('g0'), makeGpuNode('g1')], pods: [makeGpuPod('a', { node: 'g0' })] });
+    const c = countRows(nodesView(ctx, opts));
+    expect(c.tableRows).toBe(2);
+    expect(c.gpuCells).toBe(2 * (8 + 64));
+  });
+});
