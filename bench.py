@@ -1,0 +1,194 @@
+#!/usr/bin/env python3
+"""Headline benchmark: p50 dashboard refresh + rows rendered on a synthetic MI355X cluster.
+
+    python bench.py --gpus N --steps K --warmup W
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+BASELINE.json metric: "p50 dashboard refresh (ms) + GPU nodes/pods rendered at
+1/2/4/8-node cluster". One rank per GPU; rank r plays node r of an N-node
+cluster of 8×MI355X nodes (weak scaling: per-node work is fixed as N grows).
+
+* rank 0 hosts the fake kube-apiserver + Prometheus (service proxy) with an
+  injected per-request round-trip latency (``--rtt-ms``, default 20 ms),
+  identical for both schedules measured;
+* every rank with a GPU runs a node agent that exports its MI355X's live
+  telemetry through the native probe, and (unless ``--no-burn``) a workload
+  "pod" running the MFMA GEMM + HBM triad kernels, so GPU 0 of every node
+  reports real power / HBM / activity; rank 0 scrapes the agents into the TSDB;
+* rank 0 drives the SHIPPED plugin data layer (src/, Node.js) over real HTTP:
+  the reference plugin's request schedule is replayed first as the measured
+  baseline (untimed), then the flagship schedule runs W warm-up refreshes and
+  EXACTLY K timed refreshes bracketed by barrier + torch.cuda.synchronize()
+  on every rank; ms_per_step is the MAX over ranks.
+
+A "refresh" = Refresh clicked → every dashboard page's data (DeviceConfigs,
+operator pods, per-GPU telemetry, power/HBM series) committed and all five
+page view-models + node/pod detail sections + Nodes-table columns rebuilt and
+rendered. Data is synthetic (no cluster, no network); say so in the JSON.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import socket
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "p50 dashboard refresh (ms) + GPU nodes/pods rendered at 1/2/4/8-node cluster"
+
+
+def parse_args(argv=None):
+    p = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    p.add_argument("--gpus", type=int, default=1, help="ranks / synthetic nodes (one GPU per rank)")
+    p.add_argument("--steps", type=int, default=30, help="timed refreshes")
+    p.add_argument("--warmup", type=int, default=5, help="untimed warm-up refreshes")
+    p.add_argument("--rtt-ms", type=float, default=20.0, help="injected per-request round trip")
+    p.add_argument("--nodes", type=int, default=None, help="override synthetic node count (default: --gpus)")
+    p.add_argument("--ref-steps", type=int, default=None, help="reference-schedule refreshes (default: --steps)")
+    p.add_argument("--no-burn", action="store_true", help="do not run the GPU workload pods")
+    p.add_argument("--no-live", action="store_true", help="synthetic telemetry only (no native probe)")
+    p.add_argument("--out", default=None, help="also write the full result JSON here")
+    return p.parse_args(argv)
+
+
+def main(argv=None) -> int:
+    args = parse_args(argv)
+    import torch
+
+    from headlamp_intel_gpu_plugin_amd.models.cluster import gpu_node_name
+    from headlamp_intel_gpu_plugin_amd.parallel import dist as D
+    from headlamp_intel_gpu_plugin_amd.utils.stats import summarize
+
+    info = D.init()
+    n_nodes = args.nodes if args.nodes is not None else max(args.gpus, info.world)
+    node_name = gpu_node_name(info.rank)
+    gpu = info.device is not None
+
+    # --- per-rank node agent + workload pod ---------------------------------
+    agent = burner = None
+    live_on = gpu and not args.no_live
+    if live_on:
+        from headlamp_intel_gpu_plugin_amd.ops import probe
+        from headlamp_intel_gpu_plugin_amd.parallel.agent import NodeAgent
+
+        if not probe.available():
+            raise RuntimeError("GPU present but the native probe sees no device: " + probe.native().last_error())
+        dev_index = info.device.index
+        agent = NodeAgent(node_name, lambda: probe.sample(dev_index)).start()
+    if gpu and not args.no_burn:
+        from headlamp_intel_gpu_plugin_amd.ops.workload import Burner
+
+        burner = Burner(device=info.device.index, size=4096, gemms=4, triad_mb=512).start()
+    targets = D.all_gather_object(info, (node_name, agent.url if agent else None))
+
+    result = None
+    elapsed = 0.0
+    if info.is_main:
+        from headlamp_intel_gpu_plugin_amd.parallel.agent import Scraper, live_series
+        from headlamp_intel_gpu_plugin_amd.sim.apiserver import ServerThread, make_fake
+        from headlamp_intel_gpu_plugin_amd.utils.nodebridge import Driver
+
+        live_targets = {n: u for n, u in targets if u}
+        live = live_series(list(live_targets)) if live_targets else None
+        fc = make_fake(n_nodes, source="both", latency_ms=args.rtt_ms, live=live)
+        scraper = Scraper(live_targets, live, interval=2.0).start() if live_targets else None
+        server = ServerThread(fc).start()
+        drv = Driver(server.url)
+        try:
+            ref_steps = args.ref_steps if args.ref_steps is not None else args.steps
+            # Measured baseline: the reference plugin's schedule (untimed region).
+            ref_cold = drv.call("cold", "reference", n=3)
+            drv.call("steps", "reference", n=max(1, args.warmup))
+            ref = drv.call("steps", "reference", n=ref_steps)
+            ref_switch = drv.call("switch", "reference", n=3)
+            # Flagship schedule.
+            amd_cold = drv.call("cold", "amd", n=3)
+            drv.call("steps", "amd", n=max(1, args.warmup))
+            D.barrier(info)
+            D.sync_device(info)
+            t0 = time.perf_counter()
+            amd = drv.call("steps", "amd", n=args.steps)
+            D.sync_device(info)
+            D.barrier(info)
+            elapsed = time.perf_counter() - t0
+            amd_switch = drv.call("switch", "amd", n=5)
+            result = {"ref": ref, "ref_cold": ref_cold, "ref_switch": ref_switch,
+                      "amd": amd, "amd_cold": amd_cold, "amd_switch": amd_switch,
+                      "server_requests": fc.stats(),
+                      "scrapes": scraper.scrapes if scraper else 0}
+        finally:
+            drv.close()
+            server.stop()
+            if scraper:
+                scraper.stop()
+    else:
+        # Agents serve scrapes while rank 0 measures; join its timed region.
+        D.barrier(info)
+        D.sync_device(info)
+        t0 = time.perf_counter()
+        D.sync_device(info)
+        D.barrier(info)
+        elapsed = time.perf_counter() - t0
+
+    ms_per_step = D.max_float(info, elapsed * 1000.0 / max(1, args.steps))
+    if burner:
+        burner.stop()
+    if agent:
+        agent.stop()
+
+    if info.is_main:
+        amd_s = summarize(result["amd"]["latencies"])
+        ref_s = summarize(result["ref"]["latencies"])
+        rows = result["amd"]["rows"]
+        value = amd_s["p50"]
+        line = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "ms",
+            "n_gpus": info.world if info.world > 1 else args.gpus,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": False,
+            "scaling": "weak",
+            "vs_baseline": round(value / ref_s["p50"], 4),
+            "dtype": "n/a (dashboard; GPU workload pods run bf16 MFMA)" if gpu else "n/a (dashboard)",
+            "data": "synthetic cluster + synthetic/live telemetry (no real cluster or network)",
+            "config": {
+                "model": "amd-gpu Headlamp plugin on a synthetic 8xMI355X-per-node cluster",
+                "nodes": n_nodes,
+                "gpus_per_node": 8,
+                "global_batch": None,
+                "seq_len": None,
+                "parallelism": f"rank-per-node x{info.world}",
+                "rtt_ms": args.rtt_ms,
+            },
+            "baseline": {"schedule": "reference plugin request schedule replayed on the same server",
+                         "p50_ms": round(ref_s["p50"], 3), "p95_ms": round(ref_s["p95"], 3),
+                         "requests_per_refresh": result["ref"]["requestsPerStep"]},
+            "p95_ms": round(amd_s["p95"], 3),
+            "requests_per_refresh": result["amd"]["requestsPerStep"],
+            "cold_open_p50_ms": {"amd": round(summarize(result["amd_cold"]["latencies"])["p50"], 3),
+                                 "reference": round(summarize(result["ref_cold"]["latencies"])["p50"], 3)},
+            "route_switch_p50_ms": {"amd": round(summarize(result["amd_switch"]["latencies"])["p50"], 3),
+                                    "reference": round(summarize(result["ref_switch"]["latencies"])["p50"], 3)},
+            "rendered": {"gpu_nodes": rows["gpuNodes"], "gpu_pods": rows["gpuPods"],
+                         "gpus_monitored": rows["gpusMonitored"], "gpu_cells": rows["gpuCells"],
+                         "pod_table_rows": rows["podTableRows"], "detail_sections": rows["detailSections"]},
+            "live_telemetry": bool(result["scrapes"]),
+            "host": socket.gethostname(),
+        }
+        print(json.dumps(line), flush=True)
+        if args.out:
+            with open(args.out, "w") as f:
+                json.dump({"line": line, "raw": result}, f)
+    D.shutdown(info)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,370 @@
+#!/usr/bin/env node
+/**
+ * Dashboard-refresh benchmark driver (runs the SHIPPED plugin data layer).
+ *
+ *   node bench/driver.js --url http://127.0.0.1:PORT --steps K --warmup W \
+ *        [--cold N] [--out result.json] [--schedule amd|reference|both]
+ *
+ * Talks HTTP to the fake control plane (headlamp_intel_gpu_plugin_amd.sim)
+ * through a keep-alive agent capped at 6 sockets — the per-origin HTTP/1.1
+ * connection limit of the browser Headlamp runs in.
+ *
+ * For each schedule it measures, in wall-clock ms:
+ *   refresh     warm page; Refresh clicked → every dashboard page's data
+ *               (DeviceConfigs, operator pods, GPU telemetry; for the amd
+ *               schedule also the power/HBM time series) committed and all
+ *               five page view-models + node/pod detail sections + Nodes-table
+ *               columns rebuilt and rendered to HTML;
+ *   cold        route mount on an empty cache (node + pod lists included);
+ *   switch      navigating to another plugin route after the first load
+ *               (shared store: cached render + background revalidate; the
+ *               reference mounts a fresh provider, i.e. a cold open).
+ * and the rows each view renders.
+ */
+
+import http from 'http';
+import fs from 'fs';
+import { createClusterStore } from '../src/api/clusterStore.js';
+import { createMetricsSource } from '../src/api/metrics.js';
+import {
+  overviewView, devicePluginsView, nodesView, podsView, metricsView,
+  nodeDetailView, podDetailView, nodeColumns,
+} from '../src/view/pages.js';
+import { countRows } from '../src/view/ir.js';
+import { renderPage, renderSection } from '../src/view/html.js';
+import { createReferenceSchedule } from './referenceSchedule.js';
+
+function parseArgs(argv) {
+  const a = { url: null, steps: 20, warmup: 3, cold: 5, out: null, schedule: 'both' };
+  for (let i = 0; i < argv.length; i++) {
+    const k = argv[i];
+    const v = argv[i + 1];
+    if (k === '--url') a.url = v;
+    else if (k === '--steps') a.steps = parseInt(v, 10);
+    else if (k === '--warmup') a.warmup = parseInt(v, 10);
+    else if (k === '--cold') a.cold = parseInt(v, 10);
+    else if (k === '--out') a.out = v;
+    else if (k === '--schedule') a.schedule = v;
+    else continue;
+    i++;
+  }
+  if (!a.url) throw new Error('--url is required');
+  return a;
+}
+
+function makeRequest(base, counter) {
+  const agent = new http.Agent({ keepAlive: true, maxSockets: 6 });
+  const u = new URL(base);
+  return function request(path) {
+    counter.n++;
+    return new Promise(function (resolve, reject) {
+      const req = http.get({ hostname: u.hostname, port: u.port, path: path, agent: agent, headers: { Accept: 'application/json' } }, function (res) {
+        const chunks = [];
+        res.on('data', function (c) { chunks.push(c); });
+        res.on('end', function () {
+          const body = Buffer.concat(chunks);
+          counter.bytes += body.length;
+          let json = null;
+          try {
+            json = JSON.parse(body.toString('utf8'));
+          } catch (e) {
+            reject(new Error('bad JSON from ' + path));
+            return;
+          }
+          if (res.statusCode >= 400) {
+            const err = new Error((json && json.message) || 'HTTP ' + res.statusCode);
+            err.status = res.statusCode;
+            // Prometheus answers 4xx with a JSON body the caller may want.
+            if (json && json.status === 'error') resolve(json);
+            else reject(err);
+            return;
+          }
+          resolve(json);
+        });
+      });
+      req.on('error', reject);
+    });
+  };
+}
+
+function ms(hr) {
+  return hr[0] * 1e3 + hr[1] / 1e6;
+}
+
+function stats(xs) {
+  const s = xs.slice().sort(function (a, b) { return a - b; });
+  const q = function (p) {
+    if (!s.length) return null;
+    const idx = (s.length - 1) * p;
+    const lo = Math.floor(idx);
+    const hi = Math.ceil(idx);
+    return s[lo] + (s[hi] - s[lo]) * (idx - lo);
+  };
+  const mean = s.reduce(function (a, b) { return a + b; }, 0) / (s.length || 1);
+  return { n: s.length, p50: q(0.5), p95: q(0.95), min: s[0], max: s[s.length - 1], mean: mean };
+}
+
+/** Build and render every dashboard view; returns the row counts. */
+function renderAll(ctx, mstate) {
+  const pages = {
+    overview: overviewView(ctx),
+    devicePlugins: devicePluginsView(ctx),
+    nodes: nodesView(ctx, { metrics: mstate.metrics }),
+    pods: podsView(ctx),
+    metrics: metricsView(ctx, mstate),
+  };
+  const rows = {};
+  let htmlBytes = 0;
+  for (const k in pages) {
+    rows[k] = countRows(pages[k]);
+    htmlBytes += renderPage(pages[k]).length;
+  }
+  let detailSections = 0;
+  for (let i = 0; i < ctx.gpuNodes.length; i++) {
+    const s = nodeDetailView(ctx.gpuNodes[i], ctx, { metrics: mstate.metrics });
+    if (s) {
+      detailSections++;
+      htmlBytes += renderSection(s).length;
+    }
+  }
+  for (let i = 0; i < ctx.gpuPods.length; i++) {
+    const s = podDetailView(ctx.gpuPods[i]);
+    if (s) {
+      detailSections++;
+      htmlBytes += renderSection(s).length;
+    }
+  }
+  const cols = nodeColumns();
+  let columnCells = 0;
+  for (let i = 0; i < ctx.gpuNodes.length; i++) {
+    for (let c = 0; c < cols.length; c++) {
+      cols[c].getter(ctx.gpuNodes[i]);
+      columnCells++;
+    }
+  }
+  return {
+    gpuNodes: ctx.gpuNodes.length,
+    gpuPods: ctx.gpuPods.length,
+    gpusMonitored: mstate.metrics ? mstate.metrics.gpus.length : 0,
+    nodeSummaryRows: rows.nodes.tableRows,
+    podTableRows: rows.pods.tableRows,
+    gpuCells: rows.nodes.gpuCells,
+    metricsRows: rows.metrics.tableRows,
+    detailSections: detailSections,
+    columnCells: columnCells,
+    htmlBytes: htmlBytes,
+  };
+}
+
+// ---------------------------------------------------------------------------
+// Schedules
+// ---------------------------------------------------------------------------
+
+function amdSchedule(request) {
+  const store = createClusterStore({ request: request });
+  const metrics = createMetricsSource({ request: request });
+  const mstate = { metrics: null, fetchError: null, fetching: false, series: null };
+  function fetchMetrics() {
+    return Promise.all([metrics.fetchGpuMetrics(), metrics.fetchSeries(1800, 30)]).then(function (r) {
+      mstate.metrics = r[0];
+      mstate.series = r[1];
+      mstate.fetchError = r[0] ? null : 'Could not reach Prometheus';
+    });
+  }
+  return {
+    coldOpen: function () {
+      return Promise.all([store.loadLists(), store.refresh(), fetchMetrics()]);
+    },
+    refresh: function () {
+      return Promise.all([store.refresh(), fetchMetrics()]);
+    },
+    /** Route switch: render from the shared store now, revalidate in the background. */
+    switchRoute: function () {
+      const bg = Promise.all([store.refresh(), fetchMetrics()]);
+      return { rendered: Promise.resolve(), background: bg };
+    },
+    ctx: function () { return store.getSnapshot(); },
+    mstate: function () { return mstate; },
+  };
+}
+
+function referenceSchedule(request) {
+  const r = createReferenceSchedule(request);
+  return {
+    coldOpen: r.coldOpen,
+    refresh: r.refresh,
+    switchRoute: function () {
+      const p = r.coldOpen();
+      return { rendered: p, background: p };
+    },
+    ctx: r.snapshot,
+    mstate: function () { return { metrics: r.metrics(), fetchError: r.metrics() ? null : 'unreachable', fetching: false }; },
+  };
+}
+
+async function measure(name, factory, base, a) {
+  const counter = { n: 0, bytes: 0 };
+  const request = makeRequest(base, counter);
+  const out = { schedule: name };
+
+  // Cold opens: fresh schedule each time.
+  const cold = [];
+  let coldRequests = 0;
+  for (let i = 0; i < a.cold; i++) {
+    const s = factory(makeRequest(base, counter));
+    const before = counter.n;
+    const t0 = process.hrtime();
+    await s.coldOpen();
+    renderAll(s.ctx(), s.mstate());
+    cold.push(ms(process.hrtime(t0)));
+    coldRequests = counter.n - before;
+  }
+  out.cold = stats(cold);
+  out.coldRequests = coldRequests;
+
+  // Warm refreshes on one long-lived page.
+  const s = factory(request);
+  await s.coldOpen();
+  for (let i = 0; i < a.warmup; i++) {
+    await s.refresh();
+    renderAll(s.ctx(), s.mstate());
+  }
+  const lat = [];
+  const reqBefore = counter.n;
+  const bytesBefore = counter.bytes;
+  let rows = null;
+  for (let i = 0; i < a.steps; i++) {
+    const t0 = process.hrtime();
+    await s.refresh();
+    rows = renderAll(s.ctx(), s.mstate());
+    lat.push(ms(process.hrtime(t0)));
+  }
+  out.refresh = stats(lat);
+  out.refreshSamples = lat;
+  out.requestsPerRefresh = (counter.n - reqBefore) / Math.max(1, a.steps);
+  out.bytesPerRefresh = (counter.bytes - bytesBefore) / Math.max(1, a.steps);
+  out.rows = rows;
+
+  // Route switches (time to first render with data).
+  const sw = [];
+  for (let i = 0; i < Math.max(3, Math.min(a.cold, 10)); i++) {
+    const t0 = process.hrtime();
+    const r = s.switchRoute();
+    await r.rendered;
+    renderAll(s.ctx(), s.mstate());
+    sw.push(ms(process.hrtime(t0)));
+    await r.background;
+  }
+  out.switch = stats(sw);
+  return out;
+}
+
+/**
+ * --serve: line-oriented JSON command loop on stdin/stdout so the Python
+ * harness can bracket exactly the timed steps with its own barrier / clock.
+ *   {"cmd":"cold","schedule":"amd","n":3}
+ *   {"cmd":"steps","schedule":"amd","n":K}      → per-step latencies
+ *   {"cmd":"switch","schedule":"amd","n":3}
+ *   {"cmd":"quit"}
+ */
+async function serve(a) {
+  const counter = { n: 0, bytes: 0 };
+  const live = {};
+  function get(name) {
+    if (!live[name]) {
+      const f = name === 'reference' ? referenceSchedule : amdSchedule;
+      live[name] = { s: f(makeRequest(a.url, counter)), opened: false };
+    }
+    return live[name];
+  }
+  const rl = (await import('readline')).createInterface({ input: process.stdin });
+  for await (const line of rl) {
+    if (!line.trim()) continue;
+    const c = JSON.parse(line);
+    const out = { cmd: c.cmd };
+    try {
+      if (c.cmd === 'quit') {
+        process.stdout.write(JSON.stringify(out) + '\n');
+        break;
+      }
+      const name = c.schedule || 'amd';
+      const n = c.n || 1;
+      if (c.cmd === 'cold') {
+        const lat = [];
+        let req = 0;
+        for (let i = 0; i < n; i++) {
+          const s = (name === 'reference' ? referenceSchedule : amdSchedule)(makeRequest(a.url, counter));
+          const before = counter.n;
+          const t0 = process.hrtime();
+          await s.coldOpen();
+          renderAll(s.ctx(), s.mstate());
+          lat.push(ms(process.hrtime(t0)));
+          req = counter.n - before;
+        }
+        out.latencies = lat;
+        out.requests = req;
+      } else if (c.cmd === 'steps') {
+        const L = get(name);
+        if (!L.opened) {
+          await L.s.coldOpen();
+          L.opened = true;
+        }
+        const lat = [];
+        const before = counter.n;
+        const bytesBefore = counter.bytes;
+        let rows = null;
+        for (let i = 0; i < n; i++) {
+          const t0 = process.hrtime();
+          await L.s.refresh();
+          rows = renderAll(L.s.ctx(), L.s.mstate());
+          lat.push(ms(process.hrtime(t0)));
+        }
+        out.latencies = lat;
+        out.requestsPerStep = (counter.n - before) / n;
+        out.bytesPerStep = (counter.bytes - bytesBefore) / n;
+        out.rows = rows;
+      } else if (c.cmd === 'switch') {
+        const L = get(name);
+        if (!L.opened) {
+          await L.s.coldOpen();
+          L.opened = true;
+        }
+        const lat = [];
+        for (let i = 0; i < n; i++) {
+          const t0 = process.hrtime();
+          const r = L.s.switchRoute();
+          await r.rendered;
+          renderAll(L.s.ctx(), L.s.mstate());
+          lat.push(ms(process.hrtime(t0)));
+          await r.background;
+        }
+        out.latencies = lat;
+      } else {
+        throw new Error('unknown cmd ' + c.cmd);
+      }
+    } catch (e) {
+      out.error = String(e && e.stack ? e.stack : e);
+    }
+    process.stdout.write(JSON.stringify(out) + '\n');
+  }
+}
+
+async function main() {
+  const argv = process.argv.slice(2);
+  const a = parseArgs(argv);
+  if (argv.indexOf('--serve') >= 0) return serve(a);
+  const res = { url: a.url, steps: a.steps, warmup: a.warmup, node: process.version, results: {} };
+  if (a.schedule === 'reference' || a.schedule === 'both') res.results.reference = await measure('reference', referenceSchedule, a.url, a);
+  if (a.schedule === 'amd' || a.schedule === 'both') res.results.amd = await measure('amd', amdSchedule, a.url, a);
+  const txt = JSON.stringify(res);
+  if (a.out) fs.writeFileSync(a.out, txt);
+  else process.stdout.write(txt + '\n');
+}
+
+main().then(
+  function () { process.exit(0); },
+  function (e) {
+    process.stderr.write(String(e && e.stack ? e.stack : e) + '\n');
+    process.exit(1);
+  }
+);

@@ -1,0 +1,585 @@
+"""A PromQL subset evaluator over an in-memory TSDB.
+
+Enough of the Prometheus HTTP API (``/api/v1/query``, ``/api/v1/query_range``)
+to serve every query the plugin and the reference-schedule replay issue:
+
+* vector selectors with ``= != =~ !~`` matchers, including ``__name__``;
+* range selectors ``x[5m]`` with ``rate irate increase avg_over_time
+  max_over_time min_over_time sum_over_time count_over_time last_over_time``;
+* aggregations ``sum avg max min count`` with ``by (...)`` / ``without (...)``
+  in either position;
+* binary arithmetic/comparison between scalars and vectors, with
+  ``on(...)`` / ``ignoring(...)`` and ``group_left(...)`` / ``group_right(...)``;
+* number literals (the reference's discovery probe is ``query=1``).
+
+Series are stored either as a deterministic function of time sampled on a
+fixed scrape grid (synthetic telemetry) or as explicit pushed samples (live
+GPU telemetry from the native probe). Staleness/lookback follow Prometheus'
+5-minute default.
+"""
+from __future__ import annotations
+
+import bisect
+import json
+import math
+import re
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+LOOKBACK_S = 300.0
+Labels = Dict[str, str]
+
+
+# ---------------------------------------------------------------------------
+# Storage
+# ---------------------------------------------------------------------------
+
+class Series:
+    """One time series: labels + samples.
+
+    Either ``fn(t)`` sampled every ``interval`` seconds (aligned to the grid),
+    or explicit samples appended with :meth:`push` (kept sorted, bounded).
+    """
+
+    __slots__ = ("labels", "fn", "interval", "ts", "vs", "cap", "_key", "_json")
+
+    def __init__(self, labels: Labels, fn: Optional[Callable[[float], float]] = None,
+                 interval: float = 15.0, cap: int = 4096):
+        self.labels = dict(labels)
+        self.fn = fn
+        self.interval = float(interval)
+        self.ts: List[float] = []
+        self.vs: List[float] = []
+        self.cap = cap
+        self._key = tuple(sorted(self.labels.items()))
+        self._json = None
+
+    def metric_json(self) -> str:
+        """JSON of the label set (cached — series labels never change once stored)."""
+        if self._json is None:
+            self._json = json.dumps(self.labels, separators=(",", ":"))
+        return self._json
+
+    def push(self, t: float, v: float) -> None:
+        if self.ts and t <= self.ts[-1]:
+            if t == self.ts[-1]:
+                self.vs[-1] = v
+            return
+        self.ts.append(t)
+        self.vs.append(v)
+        if len(self.ts) > self.cap:
+            drop = len(self.ts) - self.cap
+            del self.ts[:drop]
+            del self.vs[:drop]
+
+    def samples(self, start: float, end: float) -> List[Tuple[float, float]]:
+        """Samples with start < t <= end."""
+        if self.fn is not None:
+            iv = self.interval
+            k0 = math.floor(start / iv) + 1
+            k1 = math.floor(end / iv)
+            return [(k * iv, self.fn(k * iv)) for k in range(k0, k1 + 1)]
+        lo = bisect.bisect_right(self.ts, start)
+        hi = bisect.bisect_right(self.ts, end)
+        return list(zip(self.ts[lo:hi], self.vs[lo:hi]))
+
+    def at(self, t: float) -> Optional[Tuple[float, float]]:
+        """Latest sample within the lookback window ending at ``t``."""
+        if self.fn is not None:
+            k = math.floor(t / self.interval) * self.interval
+            return (k, self.fn(k))
+        i = bisect.bisect_right(self.ts, t) - 1
+        if i < 0 or t - self.ts[i] > LOOKBACK_S:
+            return None
+        return (self.ts[i], self.vs[i])
+
+
+class TSDB:
+    """Series indexed by metric name."""
+
+    def __init__(self) -> None:
+        self.by_name: Dict[str, List[Series]] = {}
+        self._index: Dict[tuple, Series] = {}
+        self._select_cache: Dict[tuple, List[Series]] = {}
+        self._by_labels_id: Dict[int, Series] = {}
+
+    def label_json(self, labels: Labels) -> str:
+        """JSON for a label set; cached when it is a stored series' own dict."""
+        s = self._by_labels_id.get(id(labels))
+        if s is not None and s.labels is labels:
+            return s.metric_json()
+        return json.dumps(labels, separators=(",", ":"))
+
+    def add(self, series: Series) -> Series:
+        key = series._key
+        if key in self._index:
+            return self._index[key]
+        self._index[key] = series
+        self.by_name.setdefault(series.labels.get("__name__", ""), []).append(series)
+        self._by_labels_id[id(series.labels)] = series
+        self._select_cache.clear()
+        return series
+
+    def get_or_create(self, labels: Labels) -> Series:
+        key = tuple(sorted(labels.items()))
+        s = self._index.get(key)
+        if s is None:
+            s = self.add(Series(labels))
+        return s
+
+    def select(self, matchers: Sequence["Matcher"]) -> List[Series]:
+        """Series matching every matcher. The series set only grows via
+        :meth:`add`, so results are cached per matcher signature."""
+        sig = tuple((m.label, m.op, m.value) for m in matchers)
+        hit = self._select_cache.get(sig)
+        if hit is not None:
+            return hit
+        names = [m for m in matchers if m.label == "__name__" and m.op == "="]
+        if names:
+            cands = self.by_name.get(names[0].value, [])
+        else:
+            name_re = [m for m in matchers if m.label == "__name__" and m.op == "=~"]
+            if name_re:
+                cands = [s for n, lst in self.by_name.items() if name_re[0].matches(n) for s in lst]
+            else:
+                cands = [s for lst in self.by_name.values() for s in lst]
+        out = [s for s in cands if all(m.matches(s.labels.get(m.label, "")) for m in matchers)]
+        self._select_cache[sig] = out
+        return out
+
+    def __len__(self) -> int:
+        return len(self._index)
+
+
+# ---------------------------------------------------------------------------
+# Lexer / parser
+# ---------------------------------------------------------------------------
+
+class PromQLError(ValueError):
+    pass
+
+
+_TOKEN_RE = re.compile(r"""
+    (?P<ws>\s+)
+  | (?P<num>(?:\d+\.\d*|\.\d+|\d+)(?:[eE][+-]?\d+)?)
+  | (?P<dur>\[\s*\d+[smhdw]\s*\])
+  | (?P<str>"(?:[^"\\]|\\.)*"|'(?:[^'\\]|\\.)*')
+  | (?P<op>=~|!~|!=|==|>=|<=|[-+*/%^(){},=<>])
+  | (?P<ident>[a-zA-Z_:][a-zA-Z0-9_:]*)
+""", re.X)
+
+_DUR = {"s": 1, "m": 60, "h": 3600, "d": 86400, "w": 604800}
+AGGREGATIONS = {"sum", "avg", "max", "min", "count"}
+RANGE_FUNCS = {"rate", "irate", "increase", "avg_over_time", "max_over_time", "min_over_time",
+               "sum_over_time", "count_over_time", "last_over_time"}
+BIN_PREC = {"+": 1, "-": 1, "*": 2, "/": 2, "%": 2, "==": 0, "!=": 0, ">": 0, "<": 0, ">=": 0, "<=": 0}
+
+
+def _tokenize(q: str) -> List[Tuple[str, str]]:
+    pos = 0
+    out = []
+    while pos < len(q):
+        m = _TOKEN_RE.match(q, pos)
+        if not m:
+            raise PromQLError(f"unexpected character {q[pos]!r} at {pos}")
+        pos = m.end()
+        kind = m.lastgroup
+        if kind == "ws":
+            continue
+        out.append((kind, m.group(kind)))
+    out.append(("eof", ""))
+    return out
+
+
+class Matcher:
+    __slots__ = ("label", "op", "value", "_re")
+
+    def __init__(self, label: str, op: str, value: str):
+        self.label, self.op, self.value = label, op, value
+        self._re = re.compile("^(?:" + value + ")$") if op in ("=~", "!~") else None
+
+    def matches(self, v: str) -> bool:
+        if self.op == "=":
+            return v == self.value
+        if self.op == "!=":
+            return v != self.value
+        ok = bool(self._re.match(v))
+        return ok if self.op == "=~" else not ok
+
+
+# AST nodes are tuples: ("num", v) ("sel", matchers, range_s|None) ("func", name, arg)
+# ("agg", op, by|None, without|None, expr) ("bin", op, lhs, rhs, matching)
+
+class _Parser:
+    def __init__(self, q: str):
+        self.toks = _tokenize(q)
+        self.i = 0
+
+    def peek(self, k: int = 0):
+        return self.toks[self.i + k]
+
+    def take(self, kind: Optional[str] = None, val: Optional[str] = None):
+        t = self.toks[self.i]
+        if (kind and t[0] != kind) or (val is not None and t[1] != val):
+            raise PromQLError(f"expected {val or kind}, got {t[1]!r}")
+        self.i += 1
+        return t
+
+    def parse(self):
+        e = self.expr(0)
+        self.take("eof")
+        return e
+
+    def expr(self, min_prec: int):
+        lhs = self.unary()
+        while True:
+            k, v = self.peek()
+            if k != "op" or v not in BIN_PREC or BIN_PREC[v] < min_prec:
+                return lhs
+            self.i += 1
+            matching = self.vector_matching()
+            rhs = self.expr(BIN_PREC[v] + 1)
+            lhs = ("bin", v, lhs, rhs, matching)
+
+    def vector_matching(self):
+        k, v = self.peek()
+        if k == "ident" and v in ("on", "ignoring"):
+            self.i += 1
+            labels = self.label_list()
+            group = None
+            k2, v2 = self.peek()
+            if k2 == "ident" and v2 in ("group_left", "group_right"):
+                self.i += 1
+                extra = self.label_list() if self.peek()[1] == "(" else []
+                group = (v2, extra)
+            return (v, labels, group)
+        return None
+
+    def label_list(self) -> List[str]:
+        self.take("op", "(")
+        out = []
+        while self.peek()[1] != ")":
+            out.append(self.take("ident")[1])
+            if self.peek()[1] == ",":
+                self.i += 1
+        self.take("op", ")")
+        return out
+
+    def unary(self):
+        k, v = self.peek()
+        if k == "op" and v == "-":
+            self.i += 1
+            return ("bin", "*", ("num", -1.0), self.unary(), None)
+        return self.primary()
+
+    def primary(self):
+        k, v = self.peek()
+        if k == "num":
+            self.i += 1
+            return ("num", float(v))
+        if k == "op" and v == "(":
+            self.i += 1
+            e = self.expr(0)
+            self.take("op", ")")
+            return e
+        if k == "op" and v == "{":
+            return self.selector(None)
+        if k == "ident":
+            if v in AGGREGATIONS and self.peek(1)[1] in ("(", "by", "without"):
+                return self.aggregation()
+            if v in RANGE_FUNCS and self.peek(1)[1] == "(":
+                self.i += 2
+                arg = self.expr(0)
+                self.take("op", ")")
+                if arg[0] != "sel" or arg[2] is None:
+                    raise PromQLError(f"{v}() expects a range vector")
+                return ("func", v, arg)
+            self.i += 1
+            return self.selector(v)
+        raise PromQLError(f"unexpected token {v!r}")
+
+    def aggregation(self):
+        op = self.take("ident")[1]
+        by = without = None
+        if self.peek()[1] in ("by", "without"):
+            kw = self.take("ident")[1]
+            lst = self.label_list()
+            by, without = (lst, None) if kw == "by" else (None, lst)
+        self.take("op", "(")
+        e = self.expr(0)
+        self.take("op", ")")
+        if self.peek()[1] in ("by", "without"):
+            kw = self.take("ident")[1]
+            lst = self.label_list()
+            by, without = (lst, None) if kw == "by" else (None, lst)
+        return ("agg", op, by, without, e)
+
+    def selector(self, name: Optional[str]):
+        matchers = []
+        if name:
+            matchers.append(Matcher("__name__", "=", name))
+        if self.peek()[1] == "{":
+            self.i += 1
+            while self.peek()[1] != "}":
+                label = self.take("ident")[1]
+                op = self.take("op")[1]
+                if op not in ("=", "!=", "=~", "!~"):
+                    raise PromQLError(f"bad matcher op {op}")
+                raw = self.take("str")[1]
+                matchers.append(Matcher(label, op, bytes(raw[1:-1], "utf-8").decode("unicode_escape")))
+                if self.peek()[1] == ",":
+                    self.i += 1
+            self.take("op", "}")
+        if not matchers:
+            raise PromQLError("empty selector")
+        rng = None
+        if self.peek()[0] == "dur":
+            d = self.take("dur")[1].strip("[] ")
+            rng = float(d[:-1]) * _DUR[d[-1]]
+        return ("sel", matchers, rng)
+
+
+def parse(q: str):
+    return _Parser(q).parse()
+
+
+# ---------------------------------------------------------------------------
+# Evaluation
+# ---------------------------------------------------------------------------
+
+def _drop_name(labels: Labels) -> Labels:
+    return {k: v for k, v in labels.items() if k != "__name__"}
+
+
+def _key(labels: Labels, on: Optional[List[str]] = None, ignoring: Optional[List[str]] = None) -> tuple:
+    if on is not None:
+        return tuple((k, labels.get(k, "")) for k in sorted(on))
+    ign = set(ignoring or []) | {"__name__"}
+    return tuple(sorted((k, v) for k, v in labels.items() if k not in ign))
+
+
+def _range_fn(name: str, samples: List[Tuple[float, float]], window: float) -> Optional[float]:
+    if name == "count_over_time":
+        return float(len(samples)) if samples else None
+    if not samples:
+        return None
+    vs = [v for _, v in samples]
+    if name == "avg_over_time":
+        return sum(vs) / len(vs)
+    if name == "max_over_time":
+        return max(vs)
+    if name == "min_over_time":
+        return min(vs)
+    if name == "sum_over_time":
+        return sum(vs)
+    if name == "last_over_time":
+        return vs[-1]
+    if len(samples) < 2:
+        return None
+    if name == "irate":
+        (t0, v0), (t1, v1) = samples[-2], samples[-1]
+        d = v1 - v0 if v1 >= v0 else v1
+        return d / (t1 - t0) if t1 > t0 else None
+    # rate / increase with counter-reset handling and extrapolation to the window
+    inc = 0.0
+    for (_, a), (_, b) in zip(samples, samples[1:]):
+        inc += b - a if b >= a else b
+    span = samples[-1][0] - samples[0][0]
+    if span <= 0:
+        return None
+    per_s = inc / span
+    return per_s if name == "rate" else per_s * window
+
+
+def _apply(op: str, a: float, b: float) -> Optional[float]:
+    if op == "+":
+        return a + b
+    if op == "-":
+        return a - b
+    if op == "*":
+        return a * b
+    if op == "/":
+        return a / b if b != 0 else (math.nan if a == 0 else math.copysign(math.inf, a))
+    if op == "%":
+        return math.fmod(a, b) if b != 0 else math.nan
+    cmp = {"==": a == b, "!=": a != b, ">": a > b, "<": a < b, ">=": a >= b, "<=": a <= b}[op]
+    return a if cmp else None
+
+
+class Evaluator:
+    def __init__(self, db: TSDB):
+        self.db = db
+
+    def instant(self, node, t: float):
+        """Returns ("scalar", v) or ("vector", [(labels, v), ...])."""
+        kind = node[0]
+        if kind == "num":
+            return ("scalar", node[1])
+        if kind == "sel":
+            if node[2] is not None:
+                raise PromQLError("range vector not allowed here")
+            out = []
+            for s in self.db.select(node[1]):
+                smp = s.at(t)
+                if smp is not None:
+                    out.append((s.labels, smp[1]))
+            return ("vector", out)
+        if kind == "func":
+            _, name, sel = node
+            out = []
+            for s in self.db.select(sel[1]):
+                v = _range_fn(name, s.samples(t - sel[2], t), sel[2])
+                if v is not None:
+                    out.append((_drop_name(s.labels), v))
+            return ("vector", out)
+        if kind == "agg":
+            _, op, by, without, e = node
+            typ, vec = self.instant(e, t)
+            if typ != "vector":
+                raise PromQLError("aggregation over scalar")
+            groups: Dict[tuple, List] = {}
+            glabels: Dict[tuple, Labels] = {}
+            for labels, v in vec:
+                if by is not None:
+                    gl = {k: labels[k] for k in by if k in labels}
+                elif without is not None:
+                    gl = {k: x for k, x in _drop_name(labels).items() if k not in without}
+                else:
+                    gl = {}
+                k = tuple(sorted(gl.items()))
+                groups.setdefault(k, []).append(v)
+                glabels[k] = gl
+            res = []
+            for k, vs in groups.items():
+                if op == "sum":
+                    r = sum(vs)
+                elif op == "avg":
+                    r = sum(vs) / len(vs)
+                elif op == "max":
+                    r = max(vs)
+                elif op == "min":
+                    r = min(vs)
+                else:
+                    r = float(len(vs))
+                res.append((glabels[k], r))
+            return ("vector", res)
+        if kind == "bin":
+            return self._binary(node, t)
+        raise PromQLError(f"cannot evaluate {kind}")
+
+    def _binary(self, node, t):
+        _, op, lhs, rhs, matching = node
+        lt, lv = self.instant(lhs, t)
+        rt, rv = self.instant(rhs, t)
+        is_cmp = op in ("==", "!=", ">", "<", ">=", "<=")
+        if lt == "scalar" and rt == "scalar":
+            r = _apply(op, lv, rv)
+            return ("scalar", r if r is not None else 0.0)
+        if lt == "scalar" or rt == "scalar":
+            out = []
+            vec, sc, vec_left = (rv, lv, False) if lt == "scalar" else (lv, rv, True)
+            for labels, v in vec:
+                r = _apply(op, v, sc) if vec_left else _apply(op, sc, v)
+                if r is None:
+                    continue
+                out.append((labels if is_cmp else _drop_name(labels), v if is_cmp else r))
+            return ("vector", out)
+        on = ignoring = None
+        group = None
+        if matching:
+            mode, labels, group = matching
+            if mode == "on":
+                on = labels
+            else:
+                ignoring = labels
+        # "one" side is indexed by key; group_left lets the left side be many.
+        if group and group[0] == "group_right":
+            many, one, many_is_left = rv, lv, False
+        else:
+            many, one, many_is_left = lv, rv, True
+        index: Dict[tuple, Tuple[Labels, float]] = {}
+        for labels, v in one:
+            k = _key(labels, on, ignoring)
+            if k in index and not group:
+                raise PromQLError("many-to-many matching not allowed")
+            index[k] = (labels, v)
+        out = []
+        seen = set()
+        for labels, v in many:
+            k = _key(labels, on, ignoring)
+            if k not in index:
+                continue
+            if not group:
+                if k in seen:
+                    raise PromQLError("multiple matches on the left side; use group_left")
+                seen.add(k)
+            olabels, ov = index[k]
+            a, b = (v, ov) if many_is_left else (ov, v)
+            r = _apply(op, a, b)
+            if r is None:
+                continue
+            if group:
+                res_labels = _drop_name(labels) if not is_cmp else dict(labels)
+                for extra in group[1]:
+                    if extra in olabels:
+                        res_labels[extra] = olabels[extra]
+            elif on is not None:
+                res_labels = {k2: labels[k2] for k2 in on if k2 in labels} if not is_cmp else dict(labels)
+            else:
+                res_labels = _drop_name(labels) if not is_cmp else dict(labels)
+            out.append((res_labels, a if is_cmp else r))
+        return ("vector", out)
+
+
+def _fmt(v: float) -> str:
+    if math.isnan(v):
+        return "NaN"
+    if math.isinf(v):
+        return "+Inf" if v > 0 else "-Inf"
+    r = repr(float(v))
+    return r[:-2] if r.endswith(".0") else r
+
+
+class RawJSON(str):
+    """A pre-encoded JSON response body (served as-is by the fake apiserver)."""
+
+
+def query(db: TSDB, q: str, t: float):
+    """Prometheus ``/api/v1/query`` response body (dict on error/scalar, RawJSON for vectors)."""
+    try:
+        typ, val = Evaluator(db).instant(parse(q), t)
+    except PromQLError as e:
+        return {"status": "error", "errorType": "bad_data", "error": str(e)}
+    if typ == "scalar":
+        return {"status": "success", "data": {"resultType": "scalar", "result": [t, _fmt(val)]}}
+    ts = repr(float(t))
+    parts = ['{"metric":' + db.label_json(l) + ',"value":[' + ts + ',"' + _fmt(v) + '"]}' for l, v in val]
+    return RawJSON('{"status":"success","data":{"resultType":"vector","result":[' + ",".join(parts) + "]}}")
+
+
+def query_range(db: TSDB, q: str, start: float, end: float, step: float):
+    """Prometheus ``/api/v1/query_range`` response body."""
+    if step <= 0 or end < start:
+        return {"status": "error", "errorType": "bad_data", "error": "invalid range"}
+    if (end - start) / step > 11000:
+        return {"status": "error", "errorType": "bad_data", "error": "exceeded maximum resolution of 11,000 points"}
+    try:
+        node = parse(q)
+        ev = Evaluator(db)
+        series: Dict[tuple, Tuple[Labels, List[str]]] = {}
+        n = int(math.floor((end - start) / step))
+        for i in range(n + 1):
+            t = start + i * step
+            typ, val = ev.instant(node, t)
+            if typ == "scalar":
+                val = [({}, val)]
+            tsr = repr(float(t))
+            for labels, v in val:
+                k = tuple(sorted(labels.items()))
+                ent = series.get(k)
+                if ent is None:
+                    ent = series[k] = (labels, [])
+                ent[1].append("[" + tsr + ',"' + _fmt(v) + '"]')
+    except PromQLError as e:
+        return {"status": "error", "errorType": "bad_data", "error": str(e)}
+    parts = ['{"metric":' + db.label_json(l) + ',"values":[' + ",".join(vs) + "]}" for l, vs in series.values()]
+    return RawJSON('{"status":"success","data":{"resultType":"matrix","result":[' + ",".join(parts) + "]}}")

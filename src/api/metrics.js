@@ -223,30 +223,44 @@ export function joinNodeExporterResults(r) {
   return { gpus: gpus, xgmi: {} };
 }
 
-function exporterQueries() {
+/**
+ * ONE instant query per source: a `__name__=~` selector returns every series
+ * the page needs in a single response (split client-side by `__name__`).
+ * A browser allows 6 concurrent HTTP/1.1 connections per origin, so a
+ * refresh that stays within 6 requests completes in one round-trip.
+ */
+export function exporterQuery() {
   const E = SERIES.exporter;
-  return [
-    [E.power, E.power],
-    [E.vramUsed, E.vramUsed],
-    [E.vramTotal, E.vramTotal],
-    [E.gfx, E.gfx],
-    [E.umc, E.umc],
-    [E.temp, E.temp],
-    ['__xgmi', '{__name__=~"' + E.xgmiRe + '"}'],
-  ];
+  return '{__name__=~"' + [E.power, E.vramUsed, E.vramTotal, E.gfx, E.umc, E.temp, E.xgmiRe].join('|') + '"}';
 }
 
-function nodeExporterQueries() {
+export function nodeExporterQuery() {
   const N = SERIES.nodeExporter;
-  return [
-    [N.chips, N.chips],
-    [N.power, N.power],
-    [N.powerCap, N.powerCap],
-    [N.busy, N.busy],
-    [N.vramUsed, N.vramUsed],
-    [N.vramTotal, N.vramTotal],
-    [N.uname, N.uname],
-  ];
+  const names = [N.chips.split('{')[0], N.power, N.powerCap, N.busy, N.vramUsed, N.vramTotal, N.uname];
+  return '{__name__=~"' + names.join('|') + '"}';
+}
+
+/** Split a combined result into `name → rows` (xGMI rows under `__xgmi`). */
+export function splitByName(result) {
+  const out = { __xgmi: [] };
+  const N = SERIES.nodeExporter;
+  const xre = new RegExp('^' + SERIES.exporter.xgmiRe + '$');
+  for (let i = 0; i < result.length; i++) {
+    const row = result[i];
+    const m = row && row.metric;
+    if (!isObject(m)) continue;
+    const name = m.__name__ || '';
+    if (xre.test(name)) {
+      out.__xgmi.push(row);
+      continue;
+    }
+    // The chip-name series is keyed by its full selector in SERIES.
+    const key = name === 'node_hwmon_chip_names' ? (m.chip_name === 'amdgpu' ? N.chips : null) : name;
+    if (!key) continue;
+    if (!out[key]) out[key] = [];
+    out[key].push(row);
+  }
+  return out;
 }
 
 /**
@@ -309,6 +323,7 @@ export function createMetricsSource(opts) {
   function invalidate() {
     cachedPath = null;
     source = null;
+    seriesCache = null;
   }
 
   function instant(base, q) {
@@ -318,24 +333,12 @@ export function createMetricsSource(opts) {
     });
   }
 
-  function runWave(base, pairs) {
-    return Promise.all(
-      pairs.map(function (p) {
-        return instant(base, p[1]).then(
-          function (res) { return [p[0], res, true]; },
-          function () { return [p[0], [], false]; }
-        );
-      })
-    ).then(function (rows) {
-      const out = {};
-      let anyOk = false;
-      for (let i = 0; i < rows.length; i++) {
-        out[rows[i][0]] = rows[i][1];
-        if (rows[i][2]) anyOk = true;
-      }
-      out.__anyOk = anyOk;
-      return out;
-    });
+  /** Run one combined query; resolves {rows: name → results, ok}. */
+  function combined(base, q) {
+    return instant(base, q).then(
+      function (res) { return { rows: splitByName(res), ok: true }; },
+      function () { return { rows: {}, ok: false }; }
+    );
   }
 
   /**
@@ -349,13 +352,13 @@ export function createMetricsSource(opts) {
       const wantExp = source === null || source === 'amd-exporter';
       const wantNe = source === null || source === 'node-exporter';
       const waves = [
-        wantExp ? runWave(base, exporterQueries()) : Promise.resolve(null),
-        wantNe ? runWave(base, nodeExporterQueries()) : Promise.resolve(null),
+        wantExp ? combined(base, exporterQuery()) : Promise.resolve(null),
+        wantNe ? combined(base, nodeExporterQuery()) : Promise.resolve(null),
       ];
       return Promise.all(waves).then(function (res) {
-        const exp = res[0];
-        const ne = res[1];
-        if ((!exp || !exp.__anyOk) && (!ne || !ne.__anyOk)) {
+        const exp = res[0] ? res[0].rows : null;
+        const ne = res[1] ? res[1].rows : null;
+        if ((!res[0] || !res[0].ok) && (!res[1] || !res[1].ok)) {
           // Prometheus went away between discovery and query.
           invalidate();
           return null;
@@ -388,9 +391,34 @@ export function createMetricsSource(opts) {
     });
   }
 
+  // Incremental range cache: step-aligned samples per series key.
+  let seriesCache = null; // { range, step, end, data: { power: {node: [[t,v]]}, vram: {...} } }
+
+  function rangeQuery(base, key, q, scale, start, end, step) {
+    const path = base + '/api/v1/query_range?query=' + encodeURIComponent(q) +
+      '&start=' + start + '&end=' + end + '&step=' + step;
+    return get('query_range', path).then(
+      function (raw) {
+        const out = {};
+        const res = raw && raw.status === 'success' && raw.data && Array.isArray(raw.data.result) ? raw.data.result : [];
+        for (let i = 0; i < res.length; i++) {
+          const node = (res[i].metric && (res[i].metric.hostname || res[i].metric.instance)) || 'cluster';
+          const vals = Array.isArray(res[i].values) ? res[i].values : [];
+          out[node] = vals.map(function (v) { return [Number(v[0]), (num(v[1]) || 0) * scale]; });
+        }
+        return [key, out, true];
+      },
+      function () { return [key, {}, false]; }
+    );
+  }
+
   /**
    * Per-node power and HBM-used time series over the last `rangeSec`.
    * Server-side `sum by (hostname)` keeps the payload O(nodes × points).
+   *
+   * Incremental: samples are aligned to `step`, and Prometheus never rewrites
+   * a past step, so after the first call only the steps newer than the cache
+   * are requested — and none at all until the next step boundary.
    * @returns {Promise<{ power: Record<string, Array<[number, number]>>, vram: Record<string, Array<[number, number]>> } | null>}
    */
   function fetchSeries(rangeSec, stepSec) {
@@ -398,35 +426,38 @@ export function createMetricsSource(opts) {
     const step = stepSec || 30;
     return discover().then(function (base) {
       if (!base) return null;
-      const end = Math.floor(clock.now() / 1000);
-      const start = end - range;
+      const end = Math.floor(clock.now() / 1000 / step) * step;
+      const fresh = !seriesCache || seriesCache.range !== range || seriesCache.step !== step ||
+        seriesCache.base !== base || end - seriesCache.end >= range;
+      const start = fresh ? end - range : seriesCache.end + step;
+      if (!fresh && start > end) return seriesCache.data;
       const E = SERIES.exporter;
       const qs = [
         ['power', 'sum by (hostname) (' + E.power + ')', 1],
         ['vram', 'sum by (hostname) (' + E.vramUsed + ')', SERIES.exporterVramUnitBytes],
       ];
       return Promise.all(
-        qs.map(function (q) {
-          const path = base + '/api/v1/query_range?query=' + encodeURIComponent(q[1]) +
-            '&start=' + start + '&end=' + end + '&step=' + step;
-          return get('query_range', path).then(
-            function (raw) {
-              const out = {};
-              const res = raw && raw.status === 'success' && raw.data && Array.isArray(raw.data.result) ? raw.data.result : [];
-              for (let i = 0; i < res.length; i++) {
-                const node = (res[i].metric && (res[i].metric.hostname || res[i].metric.instance)) || 'cluster';
-                const vals = Array.isArray(res[i].values) ? res[i].values : [];
-                out[node] = vals.map(function (v) { return [v[0], (num(v[1]) || 0) * q[2]]; });
-              }
-              return [q[0], out];
-            },
-            function () { return [q[0], {}]; }
-          );
-        })
+        qs.map(function (q) { return rangeQuery(base, q[0], q[1], q[2], start, end, step); })
       ).then(function (rows) {
-        const out = {};
-        for (let i = 0; i < rows.length; i++) out[rows[i][0]] = rows[i][1];
-        return out;
+        const data = {};
+        const cutoff = end - range;
+        let allOk = true;
+        for (let i = 0; i < rows.length; i++) {
+          const key = rows[i][0];
+          const got = rows[i][1];
+          if (!rows[i][2]) allOk = false;
+          const prev = fresh ? {} : seriesCache.data[key] || {};
+          const merged = {};
+          const nodes = Object.keys(Object.assign({}, prev, got));
+          for (let n = 0; n < nodes.length; n++) {
+            const pts = (prev[nodes[n]] || []).concat(got[nodes[n]] || []).filter(function (p) { return p[0] >= cutoff; });
+            if (pts.length) merged[nodes[n]] = pts;
+          }
+          data[key] = merged;
+        }
+        // Only advance the cache when every query answered; otherwise retry the window next time.
+        if (allOk) seriesCache = { range: range, step: step, end: end, base: base, data: data };
+        return data;
       });
     });
   }

@@ -24,45 +24,55 @@ function ok(result) {
   return { status: 'success', data: { resultType: 'vector', result } };
 }
 
-/** Exporter series for `nodes` × 8 GPUs. */
+/** Exporter series for `nodes` × 8 GPUs, as a name → rows map (rows carry __name__). */
 function exporterData(nodes) {
   const d = {};
   const E = SERIES.exporter;
   [E.power, E.vramUsed, E.vramTotal, E.gfx, E.umc, E.temp].forEach((k) => (d[k] = []));
   d.__xgmi = [];
+  const add = (name, m, v) => d[name].push(vec(Object.assign({ __name__: name }, m), v));
   nodes.forEach((node) => {
     for (let g = 0; g < 8; g++) {
       const m = { hostname: node, gpu_id: String(g), instance: node + ':5000' };
-      d[E.power].push(vec(Object.assign({ pod: g < 2 ? 'train-' + g : undefined, namespace: g < 2 ? 'ml' : undefined }, m), 700 + g));
-      d[E.vramUsed].push(vec(m, 1024 * (g + 1)));
-      d[E.vramTotal].push(vec(m, 288 * 1000 * 1000 * 1000 / (1024 * 1024)));
-      d[E.gfx].push(vec(m, 50));
-      d[E.umc].push(vec(m, 30));
-      d[E.temp].push(vec(m, 60));
+      add(E.power, Object.assign({}, m, g < 2 ? { pod: 'train-' + g, namespace: 'ml' } : {}), 700 + g);
+      add(E.vramUsed, m, 1024 * (g + 1));
+      add(E.vramTotal, m, 288 * 1000 * 1000 * 1000 / (1024 * 1024));
+      add(E.gfx, m, 50);
+      add(E.umc, m, 30);
+      add(E.temp, m, 60);
       d.__xgmi.push(vec(Object.assign({ __name__: 'xgmi_neighbor_0_tx_throughput' }, m), 50e9));
     }
   });
   return d;
 }
 
-/** A fake proxy: answers probes on `up` services and queries from `data`. */
+function flatten(d) {
+  const out = [];
+  if (!d) return out;
+  Object.keys(d).forEach((k) => d[k].forEach((r) => out.push(r)));
+  return out;
+}
+
+/** A fake proxy: answers probes on `up` services and `{__name__=~"a|b"}` queries from `data` / `ne`. */
 function prom(opts) {
   const o = Object.assign({ up: [BASE0], data: exporterData(['n0']), ne: null }, opts || {});
+  const rows = flatten(o.data).concat(flatten(o.ne));
   return vi.fn((path) => {
     const base = o.up.find((b) => path.indexOf(b) === 0);
     if (!base) return Promise.reject(new Error('503'));
     const q = decodeURIComponent((path.split('query=')[1] || '').split('&')[0]);
     if (q === '1') return Promise.resolve(ok([{ metric: {}, value: [0, '1'] }]));
     if (path.indexOf('/query_range') >= 0) {
+      const end = Number(/end=(\d+)/.exec(path)[1]);
       return Promise.resolve({
         status: 'success',
-        data: { resultType: 'matrix', result: [{ metric: { hostname: 'n0' }, values: [[1, '100'], [2, '200']] }] },
+        data: { resultType: 'matrix', result: [{ metric: { hostname: 'n0' }, values: [[end - 30, '100'], [end, '200']] }] },
       });
     }
-    if (q.indexOf('{__name__=~') === 0) return Promise.resolve(ok(o.data ? o.data.__xgmi || [] : []));
-    if (o.data && o.data[q]) return Promise.resolve(ok(o.data[q]));
-    if (o.ne && o.ne[q]) return Promise.resolve(ok(o.ne[q]));
-    return Promise.resolve(ok([]));
+    const m = /^\{__name__=~"(.*)"\}$/.exec(q);
+    if (!m) return Promise.resolve(ok([]));
+    const re = new RegExp('^(?:' + m[1] + ')$');
+    return Promise.resolve(ok(rows.filter((r) => re.test(r.metric.__name__ || ''))));
   });
 }
 
@@ -164,21 +174,23 @@ describe('fetchGpuMetrics', () => {
     await src.fetchGpuMetrics();
     const second = request.mock.calls.slice(n).map((c) => decodeURIComponent(c[0]));
     expect(second.some((p) => p.indexOf('node_hwmon') >= 0)).toBe(false);
-    expect(second).toHaveLength(7);
+    expect(second).toHaveLength(1);
   });
   it('falls back to node-exporter amdgpu hwmon + DRM', async () => {
-    const N = SERIES.nodeExporter;
-    const ne = {};
-    ne[N.chips] = [
-      vec({ instance: '10.0.0.1:9100', chip: '0000:15:00_0', chip_name: 'amdgpu' }, 1),
-      vec({ instance: '10.0.0.1:9100', chip: '0000:05:00_0', chip_name: 'amdgpu' }, 1),
-    ];
-    ne[N.power] = [
-      vec({ instance: '10.0.0.1:9100', chip: '0000:05:00_0' }, 650),
-      vec({ instance: '10.0.0.1:9100', chip: '0000:15:00_0' }, 900),
-    ];
-    ne[N.busy] = [vec({ instance: '10.0.0.1:9100', card: 'card1' }, 88)];
-    ne[N.uname] = [vec({ instance: '10.0.0.1:9100', nodename: 'mi355x-0' }, 1)];
+    const i = '10.0.0.1:9100';
+    const ne = {
+      chips: [
+        vec({ __name__: 'node_hwmon_chip_names', instance: i, chip: '0000:15:00_0', chip_name: 'amdgpu' }, 1),
+        vec({ __name__: 'node_hwmon_chip_names', instance: i, chip: '0000:05:00_0', chip_name: 'amdgpu' }, 1),
+        vec({ __name__: 'node_hwmon_chip_names', instance: i, chip: 'platform_coretemp_0', chip_name: 'coretemp' }, 1),
+      ],
+      power: [
+        vec({ __name__: 'node_hwmon_power_average_watt', instance: i, chip: '0000:05:00_0' }, 650),
+        vec({ __name__: 'node_hwmon_power_average_watt', instance: i, chip: '0000:15:00_0' }, 900),
+      ],
+      busy: [vec({ __name__: 'node_drm_gpu_busy_percent', instance: i, card: 'card1' }, 88)],
+      uname: [vec({ __name__: 'node_uname_info', instance: i, nodename: 'mi355x-0' }, 1)],
+    };
     const src = createMetricsSource({ request: prom({ data: null, ne }) });
     const m = await src.fetchGpuMetrics();
     expect(m.source).toBe('node-exporter');
@@ -187,6 +199,15 @@ describe('fetchGpuMetrics', () => {
       ['mi355x-0', '1', 900],
     ]);
     expect(m.gpus[1].gfxActivityPct).toBe(88);
+  });
+  it('issues one combined query per source on the first fetch', async () => {
+    const request = prom();
+    const src = createMetricsSource({ request });
+    await src.fetchGpuMetrics();
+    const qs = request.mock.calls.map((c) => decodeURIComponent(c[0])).filter((p) => p.indexOf('query=1') < 0);
+    expect(qs).toHaveLength(2);
+    expect(qs[0]).toContain('gpu_power_usage|gpu_used_vram');
+    expect(qs[1]).toContain('node_hwmon_chip_names|node_hwmon_power_average_watt');
   });
   it('returns an empty GPU list when Prometheus has no AMD series', async () => {
     const src = createMetricsSource({ request: prom({ data: null }) });
@@ -220,17 +241,53 @@ describe('joins (direct)', () => {
 
 describe('fetchSeries', () => {
   it('returns per-node power and HBM series', async () => {
-    const src = createMetricsSource({ request: prom() });
+    const src = createMetricsSource({ request: prom(), clock: { setTimeout, clearTimeout, now: () => 1000000 } });
     const s = await src.fetchSeries(600, 30);
-    expect(s.power.n0).toEqual([[1, 100], [2, 200]]);
+    expect(s.power.n0).toEqual([[960, 100], [990, 200]]);
     expect(s.vram.n0[1][1]).toBe(200 * 1024 * 1024);
+  });
+  it('fetches only new steps after the first call', async () => {
+    let now = 1000000;
+    const request = prom();
+    const src = createMetricsSource({ request, clock: { setTimeout, clearTimeout, now: () => now } });
+    await src.fetchSeries(600, 30);
+    const ranges = () => request.mock.calls.map((c) => c[0]).filter((p) => p.indexOf('query_range') >= 0);
+    expect(ranges()).toHaveLength(2);
+    now += 10000; // same 30 s step: served from cache, no request
+    await src.fetchSeries(600, 30);
+    expect(ranges()).toHaveLength(2);
+    now += 50000; // two steps later: only the new window is requested
+    await src.fetchSeries(600, 30);
+    expect(ranges()).toHaveLength(4);
+    const last = ranges()[3];
+    const startT = Number(/start=(\d+)/.exec(last)[1]);
+    const endT = Number(/end=(\d+)/.exec(last)[1]);
+    expect(endT - startT).toBe(30);
+  });
+  it('drops points that fall out of the window and keeps merged history', async () => {
+    let now = 1000000;
+    const request = vi.fn((path) => {
+      if (path.indexOf('query=1') >= 0) return Promise.resolve(ok([]));
+      const start = Number(/start=(\d+)/.exec(path)[1]);
+      const end = Number(/end=(\d+)/.exec(path)[1]);
+      const values = [];
+      for (let t = start; t <= end; t += 30) values.push([t, '1']);
+      return Promise.resolve({ status: 'success', data: { resultType: 'matrix', result: [{ metric: { hostname: 'n0' }, values }] } });
+    });
+    const src = createMetricsSource({ request, clock: { setTimeout, clearTimeout, now: () => now } });
+    const a = await src.fetchSeries(300, 30);
+    expect(a.power.n0).toHaveLength(11);
+    now += 90000;
+    const b = await src.fetchSeries(300, 30);
+    expect(b.power.n0).toHaveLength(11);
+    expect(b.power.n0[10][0]).toBe(Math.floor(now / 1000 / 30) * 30);
   });
   it('passes start/end/step to query_range', async () => {
     const request = prom();
     const src = createMetricsSource({ request, clock: { setTimeout, clearTimeout, now: () => 1000000 } });
     await src.fetchSeries(600, 15);
     const rq = request.mock.calls.map((c) => c[0]).find((p) => p.indexOf('query_range') >= 0);
-    expect(rq).toContain('&start=400&end=1000&step=15');
+    expect(rq).toContain('&start=390&end=990&step=15');
   });
 });
 
