@@ -94,7 +94,7 @@ export const MI355X = Object.freeze({
   product: 'AMD Instinct MI355X',
   shortName: 'MI355X',
   arch: 'gfx950 (CDNA4)',
-  hbmBytes: 288 * 1000 * 1000 * 1000,
+  hbmBytes: 288 * 1024 * 1024 * 1024, // 288 GiB: the device reports 309,220,868,096 B usable
   hbmLabel: '288 GB HBM3E',
   hbmPeakTBs: 8.0,
   computeUnits: 256,
@@ -749,14 +749,17 @@ export function formatGpuResourceName(key) {
   return key.indexOf(AMD_RESOURCE_PREFIX) === 0 ? key.slice(AMD_RESOURCE_PREFIX.length) : key;
 }
 
-/** Bytes → "288 GB" / "1.5 TB" (decimal units, as HBM capacity is quoted). */
+/**
+ * Bytes → "288 GiB" / "2.3 TiB". Binary units: the MI355X's "288 GB" of HBM3E
+ * is 288 GiB (measured on the device), and the exporter reports MiB.
+ */
 export function formatBytes(b) {
   if (!(b >= 0) || b === null) return '—';
-  const units = ['B', 'KB', 'MB', 'GB', 'TB', 'PB'];
+  const units = ['B', 'KiB', 'MiB', 'GiB', 'TiB', 'PiB'];
   let v = b;
   let u = 0;
-  while (v >= 1000 && u < units.length - 1) {
-    v /= 1000;
+  while (v >= 1024 && u < units.length - 1) {
+    v /= 1024;
     u++;
   }
   const digits = v >= 100 || u === 0 ? 0 : 1;

@@ -62,7 +62,7 @@ describe('constants', () => {
     expect(AMD_GPU_RESOURCE).toBe('amd.com/gpu');
   });
   it('describes an MI355X with 288 GB HBM and an 8-GPU xGMI mesh', () => {
-    expect(MI355X.hbmBytes).toBe(288e9);
+    expect(MI355X.hbmBytes).toBe(288 * 1024 * 1024 * 1024);
     expect(MI355X.gpusPerNode).toBe(8);
     expect(MI355X.xgmiLinksPerGpu).toBe(MI355X.gpusPerNode - 1);
     expect(MI355X.computeUnits).toBe(256);
@@ -407,8 +407,8 @@ describe('formatters', () => {
     expect(formatGpuResourceName('nvidia.com/gpu')).toBe('nvidia.com/gpu');
   });
   it('formatBytes uses decimal units', () => {
-    expect(formatBytes(288e9)).toBe('288 GB');
-    expect(formatBytes(8 * 288e9)).toBe('2.3 TB');
+    expect(formatBytes(288 * 1024 ** 3)).toBe('288 GiB');
+    expect(formatBytes(8 * 288 * 1024 ** 3)).toBe('2.3 TiB');
     expect(formatBytes(512)).toBe('512 B');
     expect(formatBytes(null)).toBe('—');
   });

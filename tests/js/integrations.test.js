@@ -31,7 +31,7 @@ describe('nodeDetailView', () => {
     expect(rowValue(s, 'GPU (capacity)')).toBe('8');
     expect(rowValue(s, 'GPU (allocatable)')).toBe('8');
     expect(rowValue(s, 'GPU Model')).toBe('AMD Instinct MI355X');
-    expect(rowValue(s, 'HBM')).toBe('2.3 TB');
+    expect(rowValue(s, 'HBM')).toBe('2.3 TiB');
   });
   it('computes allocation from pods on this node with threshold status', () => {
     const s = nodeDetailView(node, ctx);
@@ -82,7 +82,7 @@ describe('podDetailView', () => {
     expect(rowValue(s, 'Phase')).toEqual({ t: 'status', status: 'success', text: 'Running' });
     expect(rowValue(s, 'Scheduled Node')).toBe('mi355x-0');
     expect(rowValue(s, 'GPU Containers')).toBe('1');
-    expect(rowValue(s, 'GPUs (effective)')).toBe('2 × MI355X (576 GB HBM)');
+    expect(rowValue(s, 'GPUs (effective)')).toBe('2 × MI355X (576 GiB HBM)');
   });
   it('shows request rows and omits equal limits', () => {
     const s = podDetailView(makeGpuPod('p', { gpus: 2 }));
@@ -135,7 +135,7 @@ describe('nodeColumns', () => {
   it('counts devices and HBM from KubeObject wrappers', () => {
     const w = { jsonData: makeGpuNode('g', { gpus: 4 }) };
     expect(cols[1].getter(w)).toBe('4');
-    expect(cols[2].getter(w)).toBe('1.2 TB');
+    expect(cols[2].getter(w)).toBe('1.1 TiB');
   });
   it('shows — devices for label-only nodes', () => {
     expect(cols[1].getter(makeGpuNode('g', { capacity: false }))).toBe('—');

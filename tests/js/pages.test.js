@@ -80,7 +80,7 @@ describe('overviewView', () => {
     expect(rowValue(s, 'Total GPU Nodes')).toEqual({ t: 'status', status: 'success', text: '2' });
     expect(rowValue(s, 'Ready Nodes')).toBe('1');
     expect(rowValue(s, 'Total GPU Devices')).toBe('16');
-    expect(rowValue(s, 'Total HBM')).toContain('4.6 TB');
+    expect(rowValue(s, 'Total HBM')).toContain('4.5 TiB');
     expect(text(rowValue(s, 'GPU Model'))).toContain('MI355X');
   });
 
@@ -203,7 +203,7 @@ describe('nodesView', () => {
     const ctx = makeContext({ nodes: [makeGpuNode('g0')], pods: [makeGpuPod('a', { node: 'g0', gpus: 2 })] });
     const s = findSection(nodesView(ctx, opts), 'g0');
     expect(rowValue(s, 'GPU Devices (amd.com/gpu)')).toBe('8');
-    expect(rowValue(s, 'HBM')).toBe('2.3 TB (8 × 288G)');
+    expect(rowValue(s, 'HBM')).toBe('2.3 TiB (8 × 288G)');
     expect(rowValue(s, 'GPU Workload Pods')).toBe('a');
     expect(rowValue(s, 'GPU (capacity)')).toBe('8');
     expect(rowValue(s, 'Kubelet')).toBe('v1.31.2');
@@ -357,7 +357,7 @@ describe('metricsView', () => {
     expect(powerBar(512.25, null).pct).toBeNull();
   });
   it('hbmBar formats used/total', () => {
-    expect(hbmBar(144e9, 288e9).text).toBe('144 GB / 288 GB (50%)');
+    expect(hbmBar(144 * 1024 ** 3, 288 * 1024 ** 3).text).toBe('144 GiB / 288 GiB (50%)');
     expect(hbmBar(null, 288e9)).toBe('—');
   });
 });

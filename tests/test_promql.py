@@ -1,0 +1,171 @@
+"""PromQL-subset evaluator (sim/promql.py) against hand-computed expectations."""
+import json
+import math
+
+import pytest
+
+from headlamp_intel_gpu_plugin_amd.sim import promql
+from headlamp_intel_gpu_plugin_amd.sim.promql import TSDB, Series, parse, query, query_range
+
+
+@pytest.fixture()
+def db():
+    d = TSDB()
+    for node in ("n0", "n1"):
+        for g in range(2):
+            base = 100.0 * (1 if node == "n0" else 2) + g
+            d.add(Series({"__name__": "gpu_power_usage", "hostname": node, "gpu_id": str(g)}, fn=lambda t, b=base: b))
+            d.add(Series({"__name__": "gpu_gfx_activity", "hostname": node, "gpu_id": str(g)}, fn=lambda t: 50.0))
+    # counter increasing 2/s
+    d.add(Series({"__name__": "energy_total", "chip": "c0", "instance": "i0"}, fn=lambda t: 2.0 * t))
+    d.add(Series({"__name__": "chip_names", "chip": "c0", "instance": "i0", "chip_name": "amdgpu"}, fn=lambda t: 1.0))
+    d.add(Series({"__name__": "chip_names", "chip": "c1", "instance": "i0", "chip_name": "k10temp"}, fn=lambda t: 1.0))
+    return d
+
+
+def _vec(body):
+    if isinstance(body, str):
+        body = json.loads(body)
+    assert body["status"] == "success", body
+    return body["data"]["result"]
+
+
+def test_scalar_literal(db):
+    body = query(db, "1", 1000.0)
+    assert body["data"]["resultType"] == "scalar"
+    assert body["data"]["result"][1] == "1"
+
+
+def test_selector_by_name(db):
+    assert len(_vec(query(db, "gpu_power_usage", 1000.0))) == 4
+
+
+def test_label_matchers(db):
+    r = _vec(query(db, 'gpu_power_usage{hostname="n1",gpu_id!="0"}', 1000.0))
+    assert len(r) == 1 and r[0]["value"][1] == "201"
+
+
+def test_regex_name_selector(db):
+    r = _vec(query(db, '{__name__=~"gpu_power_usage|gpu_gfx_activity"}', 1000.0))
+    assert len(r) == 8
+    assert {x["metric"]["__name__"] for x in r} == {"gpu_power_usage", "gpu_gfx_activity"}
+
+
+def test_negative_regex(db):
+    r = _vec(query(db, 'chip_names{chip_name!~"k10.*"}', 1000.0))
+    assert [x["metric"]["chip"] for x in r] == ["c0"]
+
+
+def test_sum_by(db):
+    r = _vec(query(db, "sum by (hostname) (gpu_power_usage)", 1000.0))
+    got = {x["metric"]["hostname"]: float(x["value"][1]) for x in r}
+    assert got == {"n0": 201.0, "n1": 401.0}
+
+
+def test_aggregation_clause_after_body(db):
+    r = _vec(query(db, "max(gpu_power_usage) by (hostname)", 1000.0))
+    assert {x["metric"]["hostname"]: float(x["value"][1]) for x in r} == {"n0": 101.0, "n1": 201.0}
+
+
+def test_avg_count_min_without(db):
+    assert float(_vec(query(db, "avg(gpu_power_usage)", 1000.0))[0]["value"][1]) == pytest.approx(150.5)
+    assert float(_vec(query(db, "count(gpu_power_usage)", 1000.0))[0]["value"][1]) == 4
+    r = _vec(query(db, "min without (gpu_id) (gpu_power_usage)", 1000.0))
+    assert {x["metric"]["hostname"]: float(x["value"][1]) for x in r} == {"n0": 100.0, "n1": 200.0}
+
+
+def test_rate_of_counter(db):
+    r = _vec(query(db, "rate(energy_total[5m])", 1000.0))
+    assert float(r[0]["value"][1]) == pytest.approx(2.0)
+    assert "__name__" not in r[0]["metric"]
+
+
+def test_increase_and_irate(db):
+    assert float(_vec(query(db, "increase(energy_total[1m])", 1000.0))[0]["value"][1]) == pytest.approx(120.0)
+    assert float(_vec(query(db, "irate(energy_total[1m])", 1000.0))[0]["value"][1]) == pytest.approx(2.0)
+
+
+def test_over_time_functions(db):
+    assert float(_vec(query(db, "avg_over_time(gpu_gfx_activity[5m])", 1000.0))[0]["value"][1]) == 50.0
+    assert float(_vec(query(db, "count_over_time(gpu_gfx_activity[1m])", 1005.0))[0]["value"][1]) == 4
+
+
+def test_group_left_join(db):
+    q = 'rate(energy_total[5m]) * on(chip,instance) group_left(chip_name) chip_names{chip_name="amdgpu"}'
+    r = _vec(query(db, q, 1000.0))
+    assert len(r) == 1
+    assert r[0]["metric"]["chip_name"] == "amdgpu"
+    assert float(r[0]["value"][1]) == pytest.approx(2.0)
+
+
+def test_scalar_vector_arithmetic(db):
+    r = _vec(query(db, 'gpu_power_usage{hostname="n0",gpu_id="0"} / 2 + 1', 1000.0))
+    assert float(r[0]["value"][1]) == 51.0
+
+
+def test_comparison_filters(db):
+    r = _vec(query(db, "gpu_power_usage > 150", 1000.0))
+    assert {x["metric"]["hostname"] for x in r} == {"n1"}
+    assert all(x["metric"]["__name__"] == "gpu_power_usage" for x in r)
+
+
+def test_unary_minus(db):
+    assert float(_vec(query(db, '-gpu_power_usage{hostname="n0",gpu_id="1"}', 1000.0))[0]["value"][1]) == -101.0
+
+
+def test_many_to_many_is_an_error(db):
+    body = query(db, "gpu_power_usage * on(hostname) gpu_gfx_activity", 1000.0)
+    assert body["status"] == "error"
+
+
+def test_parse_errors_are_reported(db):
+    for bad in ("sum(", "gpu_power_usage{hostname=}", "rate(gpu_power_usage)", "@@"):
+        assert query(db, bad, 1000.0)["status"] == "error", bad
+
+
+def test_query_range_matrix(db):
+    body = json.loads(query_range(db, "sum by (hostname) (gpu_power_usage)", 1000.0, 1060.0, 30.0))
+    res = body["data"]["result"]
+    assert body["data"]["resultType"] == "matrix"
+    assert len(res) == 2 and all(len(r["values"]) == 3 for r in res)
+
+
+def test_query_range_rejects_bad_range(db):
+    assert query_range(db, "gpu_power_usage", 10.0, 0.0, 1.0)["status"] == "error"
+    assert query_range(db, "gpu_power_usage", 0.0, 1e9, 1.0)["status"] == "error"
+
+
+def test_pushed_series_lookback():
+    d = TSDB()
+    s = d.add(Series({"__name__": "live"}))
+    s.push(100.0, 1.0)
+    s.push(110.0, 2.0)
+    s.push(105.0, 9.0)  # out of order: dropped
+    assert _vec(query(d, "live", 120.0))[0]["value"][1] == "2"
+    assert _vec(query(d, "live", 110.0 + promql.LOOKBACK_S + 1)) == []
+
+
+def test_pushed_series_cap():
+    s = Series({"__name__": "x"}, cap=3)
+    for t in range(10):
+        s.push(float(t), float(t))
+    assert s.ts == [7.0, 8.0, 9.0]
+
+
+def test_select_cache_invalidated_on_add(db):
+    assert len(_vec(query(db, "gpu_power_usage", 1.0))) == 4
+    db.add(Series({"__name__": "gpu_power_usage", "hostname": "n2", "gpu_id": "0"}, fn=lambda t: 1.0))
+    assert len(_vec(query(db, "gpu_power_usage", 1.0))) == 5
+
+
+def test_nan_and_inf_formatting():
+    assert promql._fmt(math.nan) == "NaN"
+    assert promql._fmt(math.inf) == "+Inf"
+    assert promql._fmt(2.0) == "2"
+
+
+def test_parse_ast_shapes():
+    assert parse("1")[0] == "num"
+    node = parse("x[5m]")
+    assert node[0] == "sel" and node[2] == 300.0 and node[1][0].value == "x"
+    assert parse("sum by (a) (x)")[0] == "agg"
