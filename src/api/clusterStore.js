@@ -307,12 +307,25 @@ export function createClusterStore(opts) {
     return snapshot;
   }
 
+  /**
+   * Refresh unless a refresh is already in flight or the data is younger
+   * than `maxAgeMs` — what each mounting view calls, so N providers mounted
+   * together (a route + a Node detail section) cost one fetch, not N.
+   */
+  function revalidate(maxAgeMs) {
+    if (s.refreshing && inflight) return inflight;
+    const age = s.lastUpdated === null ? Infinity : clock.now() - s.lastUpdated;
+    if (age < (maxAgeMs === undefined ? 0 : maxAgeMs)) return Promise.resolve();
+    return refresh();
+  }
+
   return {
     subscribe: subscribe,
     getSnapshot: getSnapshot,
     setNodes: setNodes,
     setPods: setPods,
     refresh: refresh,
+    revalidate: revalidate,
     loadLists: loadLists,
     /** Promise of the most recent refresh (or a resolved promise). */
     settled: function () { return inflight || Promise.resolve(); },

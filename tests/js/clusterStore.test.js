@@ -265,6 +265,31 @@ describe('createClusterStore', () => {
   });
 });
 
+describe('revalidate', () => {
+  it('joins an in-flight refresh instead of starting another', async () => {
+    const request = router(baseRoutes());
+    const store = createClusterStore({ request });
+    const a = store.refresh();
+    const b = store.revalidate(0);
+    expect(b).toBe(a);
+    await a;
+    expect(request).toHaveBeenCalledTimes(1 + PLUGIN_POD_QUERIES.length);
+  });
+  it('skips when data is fresh and refreshes when stale', async () => {
+    let now = 1000;
+    const request = router(baseRoutes());
+    const store = createClusterStore({ request, clock: { setTimeout, clearTimeout, now: () => now } });
+    await store.revalidate(5000);
+    const n = request.mock.calls.length;
+    now += 1000;
+    await store.revalidate(5000);
+    expect(request.mock.calls.length).toBe(n);
+    now += 10000;
+    await store.revalidate(5000);
+    expect(request.mock.calls.length).toBe(2 * n);
+  });
+});
+
 describe('getSharedStore', () => {
   it('returns one store per cluster key', () => {
     resetSharedStores();

@@ -1,0 +1,59 @@
+"""bench.py honours the driver contract (one JSON line, required keys), on 1 rank and on 2 gloo ranks."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REQUIRED = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config"}
+
+
+def _json_lines(out):
+    return [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+
+
+def _check(line, n):
+    assert REQUIRED <= set(line)
+    assert line["metric"] == json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+    assert line["n_gpus"] == n and line["steps"] == 4 and line["warmup"] == 1
+    assert line["higher_is_better"] is False and line["scaling"] == "weak" and line["unit"] == "ms"
+    assert 0 < line["value"] < 1000
+    assert line["ms_per_step"] > 0
+    # The flagship schedule must beat the replayed reference schedule.
+    assert line["vs_baseline"] < 1.0
+    assert line["config"]["nodes"] == n
+    assert line["rendered"]["gpu_nodes"] == n
+    assert line["rendered"]["gpus_monitored"] == 8 * n
+
+
+def test_bench_single_rank():
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "4", "--warmup", "1", "--rtt-ms", "10"], cwd=ROOT,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    _check(lines[0], 1)
+
+
+def test_bench_two_ranks_gloo():
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29541", "bench.py", "--gpus", "2",
+                        "--steps", "4", "--warmup", "1", "--rtt-ms", "10"], cwd=ROOT, capture_output=True, text=True,
+                       timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    _check(lines[0], 2)
+
+
+@pytest.mark.parametrize("n", [4])
+def test_bench_node_override(n):
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "4", "--warmup", "1", "--rtt-ms", "10", "--nodes", str(n)],
+                       cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = _json_lines(r.stdout)[0]
+    assert line["config"]["nodes"] == n and line["rendered"]["gpu_nodes"] == n
