@@ -47,7 +47,9 @@ def parse_args(argv=None):
     p.add_argument("--steps", type=int, default=30, help="timed refreshes")
     p.add_argument("--warmup", type=int, default=5, help="untimed warm-up refreshes")
     p.add_argument("--rtt-ms", type=float, default=20.0, help="injected per-request round trip")
-    p.add_argument("--nodes", type=int, default=None, help="override synthetic node count (default: --gpus)")
+    p.add_argument("--nodes", type=int, default=None, help="override synthetic node count (default: --gpus; 0 = CPU-only)")
+    p.add_argument("--preset", default=None, choices=["cpu-only", "1x1", "1x8", "4x8", "8x8"],
+                   help="BASELINE.json config preset instead of N x 8 nodes")
     p.add_argument("--ref-steps", type=int, default=None, help="reference-schedule refreshes (default: --steps)")
     p.add_argument("--no-burn", action="store_true", help="do not run the GPU workload pods")
     p.add_argument("--no-live", action="store_true", help="synthetic telemetry only (no native probe)")
@@ -94,7 +96,8 @@ def main(argv=None) -> int:
 
         live_targets = {n: u for n, u in targets if u}
         live = live_series(list(live_targets)) if live_targets else None
-        fc = make_fake(n_nodes, source="both", latency_ms=args.rtt_ms, live=live)
+        fc = make_fake(n_nodes, source="both", latency_ms=args.rtt_ms, live=live, preset=args.preset)
+        n_nodes = len(fc.cluster.gpu_nodes)
         scraper = Scraper(live_targets, live, interval=2.0).start() if live_targets else None
         server = ServerThread(fc).start()
         drv = Driver(server.url)
@@ -161,7 +164,8 @@ def main(argv=None) -> int:
             "config": {
                 "model": "amd-gpu Headlamp plugin on a synthetic 8xMI355X-per-node cluster",
                 "nodes": n_nodes,
-                "gpus_per_node": 8,
+                "gpus_per_node": fc.cluster.spec.gpus_per_node,
+                "preset": args.preset,
                 "global_batch": None,
                 "seq_len": None,
                 "parallelism": f"rank-per-node x{info.world}",

@@ -326,12 +326,14 @@ class ServerThread:
 
 
 def make_fake(nodes: int, *, source: str = "amd-exporter", latency_ms: float = 20.0, crd_installed: bool = True,
-              prometheus_up=(DEFAULT_PROM_SERVICE,), live=None) -> FakeCluster:
-    """Convenience: synthetic cluster of ``nodes`` × 8 MI355X + telemetry + fake control plane."""
-    from ..models.cluster import SyntheticCluster, spec_for_nodes
+              prometheus_up=(DEFAULT_PROM_SERVICE,), live=None, preset: Optional[str] = None) -> FakeCluster:
+    """Convenience: synthetic cluster of ``nodes`` × 8 MI355X (or a BASELINE ``preset``) + telemetry + fake control plane."""
+    import copy
+
+    from ..models.cluster import PRESETS, SyntheticCluster, spec_for_nodes
     from ..models.telemetry import populate
 
-    cluster = SyntheticCluster(spec_for_nodes(nodes))
+    cluster = SyntheticCluster(copy.deepcopy(PRESETS[preset]) if preset else spec_for_nodes(nodes))
     db = promql.TSDB()
     # "both": a kube-prometheus-stack cluster scrapes node-exporter AND the AMD exporter.
     for src in (("amd-exporter", "node-exporter") if source == "both" else (source,)):

@@ -41,6 +41,27 @@ import {
 
 export const DEFAULT_REQUEST_TIMEOUT_MS = 2000;
 
+/**
+ * True when two lists hold the same Kubernetes objects at the same versions
+ * (uid + resourceVersion, falling back to a JSON comparison for objects
+ * without a resourceVersion).
+ */
+export function sameObjects(a, b) {
+  if (a === b) return true;
+  if (!a || !b || a.length !== b.length) return false;
+  for (let i = 0; i < a.length; i++) {
+    const ma = a[i] && a[i].metadata;
+    const mb = b[i] && b[i].metadata;
+    if (!ma || !mb) return false;
+    if (ma.resourceVersion && mb.resourceVersion) {
+      if (ma.uid !== mb.uid || ma.resourceVersion !== mb.resourceVersion) return false;
+    } else if (JSON.stringify(a[i]) !== JSON.stringify(b[i])) {
+      return false;
+    }
+  }
+  return true;
+}
+
 const defaultClock = {
   setTimeout: function (fn, ms) { return setTimeout(fn, ms); },
   clearTimeout: function (h) { clearTimeout(h); },
@@ -236,10 +257,13 @@ export function createClusterStore(opts) {
         if (my !== seq) return;
         const c = results[0];
         s.crdAvailable = c.ok;
-        s.deviceConfigs = c.items;
+        // Structural sharing: an unchanged list keeps its identity, so every
+        // memoised view (and React.memo'd section) downstream is reused.
+        s.deviceConfigs = sameObjects(s.deviceConfigs, c.items) ? s.deviceConfigs : c.items;
         let found = [];
         for (let i = 1; i < results.length; i++) found = found.concat(results[i]);
-        s.pluginPods = dedupePods(found);
+        const pods = dedupePods(found);
+        s.pluginPods = sameObjects(s.pluginPods, pods) ? s.pluginPods : pods;
         s.asyncError = null;
         s.asyncLoaded = true;
         s.refreshing = false;

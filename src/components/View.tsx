@@ -251,7 +251,7 @@ export function Block({ b }: { b: IR }): JSX.Element | null {
   }
 }
 
-export function Section({ s }: { s: IR }): JSX.Element | null {
+function SectionImpl({ s }: { s: IR }): JSX.Element | null {
   if (!s) return null;
   return (
     <SectionBox title={s.title}>
@@ -261,6 +261,13 @@ export function Section({ s }: { s: IR }): JSX.Element | null {
     </SectionBox>
   );
 }
+
+/**
+ * View-models return the same section object while its inputs are unchanged
+ * (src/view/pages.js memo + the store's structural sharing), so a memoised
+ * Section skips re-rendering unchanged parts of a page on refresh.
+ */
+export const Section = React.memo(SectionImpl);
 
 const buttonStyle = (disabled: boolean): React.CSSProperties => ({
   padding: '6px 16px',

@@ -105,9 +105,22 @@ function renderBlock(b) {
   }
 }
 
+const sectionCache = typeof WeakMap === 'function' ? new WeakMap() : null;
+
+/**
+ * Section → HTML, cached by section identity: the analog of `React.memo` on
+ * View.tsx's Section. View-models return the same section object when its
+ * inputs are unchanged, so an unchanged section is not re-rendered.
+ */
 export function renderSection(s) {
   if (!s) return '';
-  return '<section><h2>' + esc(s.title) + '</h2>' + s.blocks.map(renderBlock).join('') + '</section>';
+  if (sectionCache) {
+    const hit = sectionCache.get(s);
+    if (hit !== undefined) return hit;
+  }
+  const h = '<section><h2>' + esc(s.title) + '</h2>' + s.blocks.map(renderBlock).join('') + '</section>';
+  if (sectionCache) sectionCache.set(s, h);
+  return h;
 }
 
 export function renderPage(vm) {

@@ -64,6 +64,43 @@ export function page(title, refresh, items) {
 }
 
 // ---------------------------------------------------------------------------
+// Memoisation
+// ---------------------------------------------------------------------------
+
+/**
+ * Identity-keyed memo with a bounded number of slots. `memo(key, deps, fn)`
+ * returns the previous value for `key` when every dep is `===` to last time.
+ * The store keeps unchanged lists by identity (structural sharing), so
+ * sections whose inputs did not change are returned as the SAME IR objects —
+ * which `React.memo` (View.tsx) and `renderSection`'s cache then skip.
+ */
+export function createMemo(limit) {
+  const max = limit || 256;
+  const slots = new Map();
+  function memo(key, deps, compute) {
+    const e = slots.get(key);
+    if (e && e.deps.length === deps.length) {
+      let same = true;
+      for (let i = 0; i < deps.length; i++) {
+        if (e.deps[i] !== deps[i]) {
+          same = false;
+          break;
+        }
+      }
+      if (same) return e.value;
+    }
+    const value = compute();
+    slots.delete(key);
+    slots.set(key, { deps: deps, value: value });
+    if (slots.size > max) slots.delete(slots.keys().next().value);
+    return value;
+  }
+  memo.clear = function () { slots.clear(); };
+  memo.size = function () { return slots.size; };
+  return memo;
+}
+
+// ---------------------------------------------------------------------------
 // Query helpers (tests, benchmark row counting)
 // ---------------------------------------------------------------------------
 

@@ -65,9 +65,26 @@ import {
 } from '../api/amdgpu.js';
 import { buildGpuSlots, buildXgmiMatrix, isFullMesh } from '../api/topology.js';
 import { PROMETHEUS_SERVICES, summarizeMetrics } from '../api/metrics.js';
-import { bar, kv, lines, loader, page, pctbar, row, section, status, table } from './ir.js';
+import { bar, createMemo, kv, lines, loader, page, pctbar, row, section, status, table } from './ir.js';
 
 export const BRAND = 'AMD GPU';
+
+/**
+ * Section-level memo shared by all views. Deps are the snapshot fields a
+ * section reads plus the age clock (ages are shown with 1 s resolution), so a
+ * refresh that returns unchanged Kubernetes objects reuses the section IR.
+ */
+const memo = createMemo(512);
+const podDetailCache = typeof WeakMap === 'function' ? new WeakMap() : null;
+
+function ageKey(now) {
+  return Math.floor(now / 1000);
+}
+
+/** Drop memoised sections (tests; cluster switch). */
+export function clearViewMemo() {
+  memo.clear();
+}
 export const ACTIVE_PODS_LIMIT = 10;
 
 export const HELM_INSTALL =
@@ -127,6 +144,15 @@ function restartsCell(p) {
 export function overviewView(ctx, opts) {
   const now = nowOf(opts);
   if (ctx.loading && !ctx.lastUpdated) return page(null, null, [loader('Loading ' + BRAND + ' data...')]);
+  const items = memo(
+    'overview',
+    [ctx.deviceConfigs, ctx.pluginPods, ctx.pluginInstalled, ctx.crdAvailable, ctx.gpuNodes, ctx.gpuPods, ctx.index, ctx.error, ageKey(now)],
+    function () { return overviewItems(ctx, now); }
+  );
+  return page(BRAND + ' — Overview', refreshButton('Refresh AMD GPU data', ctx.refreshing), items);
+}
+
+function overviewItems(ctx, now) {
   const items = [];
   const t = ctx.index.totals;
 
@@ -262,7 +288,7 @@ export function overviewView(ctx, opts) {
     );
   }
 
-  return page(BRAND + ' — Overview', refreshButton('Refresh AMD GPU data', ctx.refreshing), items);
+  return items;
 }
 
 // ---------------------------------------------------------------------------
@@ -280,6 +306,15 @@ function enabledCell(on, detail) {
 export function devicePluginsView(ctx, opts) {
   const now = nowOf(opts);
   if (ctx.loading && !ctx.lastUpdated) return page(null, null, [loader('Loading device plugin data...')]);
+  const items = memo(
+    'device-plugins',
+    [ctx.deviceConfigs, ctx.pluginPods, ctx.crdAvailable, ctx.error, ageKey(now)],
+    function () { return devicePluginsItems(ctx, now); }
+  );
+  return page(BRAND + ' — Device Plugins', refreshButton('Refresh device plugin data', ctx.refreshing), items);
+}
+
+function devicePluginsItems(ctx, now) {
   const items = [];
   if (ctx.error) items.push(errorSection(ctx.error));
 
@@ -358,7 +393,7 @@ export function devicePluginsView(ctx, opts) {
     );
   }
 
-  return page(BRAND + ' — Device Plugins', refreshButton('Refresh device plugin data', ctx.refreshing), items);
+  return items;
 }
 
 // ---------------------------------------------------------------------------
@@ -375,17 +410,6 @@ export function slotsBlock(node, podsOnNode, owners) {
 export function matrixBlock(gpuCount, measured, probed) {
   const m = buildXgmiMatrix(gpuCount, measured, probed);
   return { t: 'matrix', matrix: m, fullMesh: isFullMesh(m) };
-}
-
-/** Owners per GPU from exporter pod labels, for one node (or undefined). */
-function ownersFor(metrics, nodeName) {
-  if (!metrics || !metrics.gpus) return undefined;
-  const out = [];
-  for (let i = 0; i < metrics.gpus.length; i++) {
-    const g = metrics.gpus[i];
-    if (g.nodeName === nodeName && g.pod) out.push({ gpu: g.gpu, pod: g.pod, namespace: g.namespace });
-  }
-  return out.length ? out : undefined;
 }
 
 function nodeCardRows(node, podsOnNode, stats, now) {
@@ -426,6 +450,58 @@ export function nodesView(ctx, opts) {
   const now = nowOf(opts);
   const metrics = opts && opts.metrics ? opts.metrics : null;
   if (ctx.loading && !ctx.lastUpdated) return page(null, null, [loader('Loading GPU node data...')]);
+  const age = ageKey(now);
+  const head = memo('nodes-head', [ctx.gpuNodes, ctx.index, ctx.error, age], function () {
+    return nodesHeadItems(ctx, now);
+  });
+  const items = head.slice();
+  const idx = ctx.index;
+  const owners = ownersByNode(metrics);
+  for (let i = 0; i < ctx.gpuNodes.length; i++) {
+    const n = ctx.gpuNodes[i];
+    const name = n.metadata.name;
+    const pods = idx.podsByNode[name] || [];
+    const stats = idx.nodeStats[name];
+    const own = owners[name];
+    const xg = metrics && metrics.xgmi ? metrics.xgmi[name] : undefined;
+    items.push(
+      memo('node-card:' + name, [n, pods, stats, keyOf(own), keyOf(xg), age], function () {
+        const blocks = [kv(nodeCardRows(n, pods, stats, now))];
+        const count = getNodeGpuCount(n);
+        if (count > 0) {
+          blocks.push(slotsBlock(n, pods, own));
+          blocks.push(matrixBlock(count, xg));
+        }
+        return section(name, blocks, n.metadata.uid || name);
+      })
+    );
+  }
+  return page(BRAND + ' — Nodes', refreshButton('Refresh node data', ctx.refreshing), items);
+}
+
+/** Stable string key of a small JSON value (undefined → ''). */
+function keyOf(v) {
+  return v === undefined || v === null ? '' : JSON.stringify(v);
+}
+
+const ownersCache = typeof WeakMap === 'function' ? new WeakMap() : null;
+
+/** node → [{gpu, pod, namespace}] from exporter pod labels, computed once per metrics object. */
+function ownersByNode(metrics) {
+  if (!metrics || !metrics.gpus) return {};
+  if (ownersCache && ownersCache.has(metrics)) return ownersCache.get(metrics);
+  const out = {};
+  for (let i = 0; i < metrics.gpus.length; i++) {
+    const g = metrics.gpus[i];
+    if (!g.pod) continue;
+    if (!out[g.nodeName]) out[g.nodeName] = [];
+    out[g.nodeName].push({ gpu: g.gpu, pod: g.pod, namespace: g.namespace });
+  }
+  if (ownersCache) ownersCache.set(metrics, out);
+  return out;
+}
+
+function nodesHeadItems(ctx, now) {
   const items = [];
   if (ctx.error) items.push(errorSection(ctx.error));
 
@@ -470,20 +546,7 @@ export function nodesView(ctx, opts) {
     );
   }
 
-  for (let i = 0; i < ctx.gpuNodes.length; i++) {
-    const n = ctx.gpuNodes[i];
-    const name = n.metadata.name;
-    const pods = idx.podsByNode[name] || [];
-    const blocks = [kv(nodeCardRows(n, pods, idx.nodeStats[name], now))];
-    const count = getNodeGpuCount(n);
-    if (count > 0) {
-      blocks.push(slotsBlock(n, pods, ownersFor(metrics, name)));
-      blocks.push(matrixBlock(count, metrics && metrics.xgmi ? metrics.xgmi[name] : undefined));
-    }
-    items.push(section(name, blocks, n.metadata.uid || name));
-  }
-
-  return page(BRAND + ' — Nodes', refreshButton('Refresh node data', ctx.refreshing), items);
+  return items;
 }
 
 // ---------------------------------------------------------------------------
@@ -514,6 +577,13 @@ export function gpuContainerLines(pod) {
 export function podsView(ctx, opts) {
   const now = nowOf(opts);
   if (ctx.loading && !ctx.lastUpdated) return page(null, null, [loader('Loading GPU pod data...')]);
+  const items = memo('pods', [ctx.gpuPods, ctx.index, ctx.error, ageKey(now)], function () {
+    return podsItems(ctx, now);
+  });
+  return page(BRAND + ' — Pods', refreshButton('Refresh pod data', ctx.refreshing), items);
+}
+
+function podsItems(ctx, now) {
   const items = [];
   if (ctx.error) items.push(errorSection(ctx.error));
   const pods = ctx.gpuPods;
@@ -574,7 +644,7 @@ export function podsView(ctx, opts) {
     );
   }
 
-  return page(BRAND + ' — Pods', refreshButton('Refresh pod data', ctx.refreshing), items);
+  return items;
 }
 
 // ---------------------------------------------------------------------------
@@ -740,9 +810,19 @@ export function nodeDetailView(resource, ctx, opts) {
   const alloc = getGpuResources(get(raw, ['status', 'allocatable'], null));
   if (Object.keys(cap).length === 0 && Object.keys(alloc).length === 0) return null;
   const name = raw.metadata.name;
-  const podsOnNode = ctx.loading && !ctx.lastUpdated
-    ? []
-    : ctx.gpuPods.filter(function (p) { return get(p, ['spec', 'nodeName'], null) === name; });
+  let podsOnNode;
+  if (ctx.loading && !ctx.lastUpdated) podsOnNode = [];
+  else if (ctx.index && ctx.index.podsByNode && ctx.index.podsByNode[name]) podsOnNode = ctx.index.podsByNode[name];
+  else podsOnNode = ctx.gpuPods.filter(function (p) { return get(p, ['spec', 'nodeName'], null) === name; });
+  const metrics = opts && opts.metrics ? opts.metrics : null;
+  const own = ownersByNode(metrics)[name];
+  const xg = metrics && metrics.xgmi ? metrics.xgmi[name] : undefined;
+  return memo('node-detail:' + name, [raw, podsOnNode, !!ctx.loading, keyOf(own), keyOf(xg)], function () {
+    return nodeDetailSection(raw, name, cap, alloc, podsOnNode, ctx.loading, own, xg);
+  });
+}
+
+function nodeDetailSection(raw, name, cap, alloc, podsOnNode, loading, own, xg) {
   const allocatable = parseInt(alloc[AMD_GPU_RESOURCE] || '0', 10) || 0;
   let inUse = 0;
   for (let i = 0; i < podsOnNode.length; i++) {
@@ -760,14 +840,13 @@ export function nodeDetailView(resource, ctx, opts) {
   rows.push(
     row(
       'GPU Workload Pods',
-      podsOnNode.length > 0 ? podsOnNode.map(podName).join(', ') : ctx.loading ? 'Loading…' : 'None'
+      podsOnNode.length > 0 ? podsOnNode.map(podName).join(', ') : loading ? 'Loading…' : 'None'
     )
   );
   const blocks = [kv(rows)];
   if (count > 0) {
-    const metrics = opts && opts.metrics ? opts.metrics : null;
-    blocks.push(slotsBlock(raw, podsOnNode, ownersFor(metrics, name)));
-    blocks.push(matrixBlock(count, metrics && metrics.xgmi ? metrics.xgmi[name] : undefined));
+    blocks.push(slotsBlock(raw, podsOnNode, own));
+    blocks.push(matrixBlock(count, xg));
   }
   return section('AMD GPU', blocks);
 }
@@ -783,6 +862,16 @@ export function nodeDetailView(resource, ctx, opts) {
  */
 export function podDetailView(resource) {
   const raw = unwrapKubeObject(resource);
+  if (podDetailCache && raw && typeof raw === 'object') {
+    if (podDetailCache.has(raw)) return podDetailCache.get(raw);
+    const s = podDetailSection(raw);
+    podDetailCache.set(raw, s);
+    return s;
+  }
+  return podDetailSection(raw);
+}
+
+function podDetailSection(raw) {
   if (!isGpuRequestingPod(raw)) return null;
   const ics = gpuInitContainers(raw);
   const cs = gpuContainers(raw);

@@ -1,0 +1,112 @@
+/**
+ * Structural sharing + view memoisation: unchanged inputs → identical IR
+ * objects (what React.memo and renderSection's cache rely on); changed
+ * inputs → recomputed sections.
+ */
+import { createMemo, sections } from '../../src/view/ir.js';
+import { clearViewMemo, nodesView, overviewView, podDetailView, podsView } from '../../src/view/pages.js';
+import { renderSection } from '../../src/view/html.js';
+import { createClusterStore, sameObjects } from '../../src/api/clusterStore.js';
+import { DEVICE_CONFIG_LIST_PATH, PLUGIN_POD_QUERIES } from '../../src/api/amdgpu.js';
+import { NOW, makeContext, makeDeviceConfig, makeGpuNode, makeGpuPod, makePluginPod } from './fixtures.js';
+
+describe('createMemo', () => {
+  it('returns the cached value while deps are identical', () => {
+    const memo = createMemo(4);
+    const a = {};
+    const f = vi.fn(() => ({ v: 1 }));
+    const x = memo('k', [a, 1], f);
+    expect(memo('k', [a, 1], f)).toBe(x);
+    expect(f).toHaveBeenCalledTimes(1);
+  });
+  it('recomputes when any dep changes', () => {
+    const memo = createMemo(4);
+    const f = vi.fn(() => ({}));
+    memo('k', [{}], f);
+    memo('k', [{}], f);
+    expect(f).toHaveBeenCalledTimes(2);
+  });
+  it('evicts the oldest slot beyond its limit', () => {
+    const memo = createMemo(2);
+    memo('a', [], () => 1);
+    memo('b', [], () => 2);
+    memo('c', [], () => 3);
+    expect(memo.size()).toBe(2);
+  });
+});
+
+describe('view memoisation', () => {
+  beforeEach(() => clearViewMemo());
+
+  it('overview returns the same sections for the same snapshot data', () => {
+    const ctx = makeContext({ nodes: [makeGpuNode('g0')], pods: [makeGpuPod('a', { node: 'g0' })] });
+    const a = overviewView(ctx, { now: NOW });
+    const b = overviewView(Object.assign({}, ctx, { refreshing: true }), { now: NOW + 200 });
+    expect(b.items).toBe(a.items);
+    expect(b.refresh.label).toBe('Refreshing…');
+  });
+
+  it('recomputes when the age clock ticks a second', () => {
+    const ctx = makeContext({ nodes: [makeGpuNode('g0')] });
+    const a = overviewView(ctx, { now: NOW });
+    expect(overviewView(ctx, { now: NOW + 1000 }).items).not.toBe(a.items);
+  });
+
+  it('recomputes when the pod list changes', () => {
+    const ctx = makeContext({ pods: [makeGpuPod('a')] });
+    const a = podsView(ctx, { now: NOW });
+    const ctx2 = makeContext({ pods: [makeGpuPod('a'), makeGpuPod('b')] });
+    expect(podsView(ctx2, { now: NOW }).items).not.toBe(a.items);
+  });
+
+  it('reuses unchanged node cards and rebuilds changed ones', () => {
+    const n0 = makeGpuNode('g0');
+    const n1 = makeGpuNode('g1');
+    const ctx = makeContext({ nodes: [n0, n1] });
+    const a = sections(nodesView(ctx, { now: NOW }));
+    const metrics = { gpus: [], xgmi: { g1: { '0-1': 12.5 } } };
+    const b = sections(nodesView(ctx, { now: NOW, metrics }));
+    const card = (ss, name) => ss.find((s) => s.title === name);
+    expect(card(b, 'g0')).toBe(card(a, 'g0'));
+    expect(card(b, 'g1')).not.toBe(card(a, 'g1'));
+  });
+
+  it('pod detail sections are cached per pod object', () => {
+    const p = makeGpuPod('p');
+    expect(podDetailView(p)).toBe(podDetailView({ jsonData: p }));
+  });
+
+  it('renderSection reuses HTML for the same section object', () => {
+    const s = podDetailView(makeGpuPod('q'));
+    const h = renderSection(s);
+    expect(renderSection(s)).toBe(h);
+  });
+});
+
+describe('structural sharing in the store', () => {
+  it('sameObjects compares uid + resourceVersion', () => {
+    const a = [{ metadata: { uid: 'x', resourceVersion: '1' } }];
+    expect(sameObjects(a, [{ metadata: { uid: 'x', resourceVersion: '1' } }])).toBe(true);
+    expect(sameObjects(a, [{ metadata: { uid: 'x', resourceVersion: '2' } }])).toBe(false);
+    expect(sameObjects(a, [])).toBe(false);
+  });
+  it('sameObjects falls back to deep comparison without resourceVersion', () => {
+    expect(sameObjects([makeDeviceConfig('a')], [makeDeviceConfig('a')])).toBe(true);
+    expect(sameObjects([makeDeviceConfig('a')], [makeDeviceConfig('b')])).toBe(false);
+  });
+  it('keeps list identity across refreshes that return unchanged objects', async () => {
+    const request = (path) => {
+      if (path === DEVICE_CONFIG_LIST_PATH) return Promise.resolve({ items: [makeDeviceConfig()] });
+      if (path === PLUGIN_POD_QUERIES[0]) return Promise.resolve({ items: [makePluginPod('dp')] });
+      return Promise.resolve({ items: [] });
+    };
+    const store = createClusterStore({ request });
+    await store.refresh();
+    const a = store.getSnapshot();
+    await store.refresh();
+    const b = store.getSnapshot();
+    expect(b).not.toBe(a);
+    expect(b.deviceConfigs).toBe(a.deviceConfigs);
+    expect(b.pluginPods).toBe(a.pluginPods);
+  });
+});
