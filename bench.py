@@ -183,7 +183,7 @@ def main(argv=None) -> int:
             "rendered": {"gpu_nodes": rows["gpuNodes"], "gpu_pods": rows["gpuPods"],
                          "gpus_monitored": rows["gpusMonitored"], "gpu_cells": rows["gpuCells"],
                          "pod_table_rows": rows["podTableRows"], "detail_sections": rows["detailSections"]},
-            "live_telemetry": bool(result["scrapes"]),
+            "live_telemetry": bool(result["scrapes"]) and n_nodes > 0,
             "host": socket.gethostname(),
         }
         print(json.dumps(line), flush=True)
