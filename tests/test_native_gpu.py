@@ -83,7 +83,9 @@ def _ref(a, b):
     return a.float() @ b.float().T
 
 
-@pytest.mark.parametrize("m,n,k", [(128, 128, 64), (256, 384, 192), (1024, 512, 2048), (384, 1152, 64)])
+@pytest.mark.parametrize("m,n,k", [(128, 128, 64), (256, 384, 192), (1024, 512, 2048), (384, 1152, 64),
+                                   # ≥128 tiles of 256² → the 8-wave 256×256 kernel
+                                   (2048, 4096, 320), (4096, 2048, 64)])
 def test_gemm_matches_fp32_reference(dev, m, n, k):
     g = torch.Generator(device=dev).manual_seed(m * 7 + n + k)
     a = torch.randn(m, k, device=dev, dtype=torch.bfloat16, generator=g)
@@ -110,12 +112,24 @@ def test_gemm_identity_with_asymmetric_b(dev):
     assert torch.equal(c.float(), bvals.T.contiguous())
 
 
-def test_gemm_multi_tile_exact_integers(dev):
-    m, n, k = 256, 256, 256
+@pytest.mark.parametrize("m,n,k", [(256, 256, 256), (4096, 2048, 128)])
+def test_gemm_multi_tile_exact_integers(dev, m, n, k):
+    # |sum| <= 2*1*k <= 256: exact in bf16, so any indexing error shows up exactly.
     a = (torch.arange(m * k, device=dev) % 5 - 2).reshape(m, k).to(torch.bfloat16)
-    b = (torch.arange(n * k, device=dev) % 3 - 1).reshape(n, k).to(torch.bfloat16)
+    b = ((torch.arange(n * k, device=dev) * 7) % 3 - 1).reshape(n, k).to(torch.bfloat16)
     c = workload.gemm_bf16_nt(a, b)
     assert torch.equal(c.float(), _ref(a, b))
+
+
+def test_gemm_big_tile_identity_asymmetric(dev):
+    # A = I (padded to 4096 rows) with an asymmetric B through the 256² kernel.
+    m, n, k = 4096, 2048, 256
+    a = torch.zeros(m, k, device=dev, dtype=torch.bfloat16)
+    a[:k, :k] = torch.eye(k, device=dev, dtype=torch.bfloat16)
+    bvals = (torch.arange(n * k, device=dev, dtype=torch.float32).reshape(n, k) % 61) - 30
+    c = workload.gemm_bf16_nt(a, bvals.to(torch.bfloat16))
+    assert torch.equal(c[:k].float(), bvals.T[:k].contiguous())
+    assert torch.count_nonzero(c[k:]) == 0
 
 
 def test_gemm_respects_stream(dev):
