@@ -1,0 +1,204 @@
+/**
+ * Typed shapes of the Kubernetes / AMD objects the plugin reads — the fields
+ * it actually uses, nothing more. Runtime narrowing from `unknown` happens in
+ * the `is*` guards of ./amdgpu.js; these interfaces describe what a value is
+ * once a guard has accepted it.
+ *
+ * Reference analog: src/api/k8s.ts:37-50 (KubeObjectMeta, KubeObject),
+ * :56-80 (CRD), :92-122 (Node), :209-247 (Pod), :315-318 (KubeList)
+ * — SURVEY.md C2.2, C2.3, C2.4, C2.8, C2.12.
+ */
+
+// ---------------------------------------------------------------------------
+// Generic
+// ---------------------------------------------------------------------------
+
+export interface KubeObjectMeta {
+  name: string;
+  namespace?: string;
+  uid?: string;
+  resourceVersion?: string;
+  creationTimestamp?: string;
+  labels?: Record<string, string>;
+  annotations?: Record<string, string>;
+}
+
+export interface KubeObject {
+  apiVersion?: string;
+  kind?: string;
+  metadata: KubeObjectMeta;
+}
+
+export interface KubeList<T> {
+  items: T[];
+  metadata?: { resourceVersion?: string };
+}
+
+/** Headlamp `useList()` returns class instances that keep the raw JSON here. */
+export interface KubeObjectWrapper<T> {
+  jsonData: T;
+}
+
+export type Status = 'success' | 'warning' | 'error';
+
+// ---------------------------------------------------------------------------
+// AMD GPU Operator DeviceConfig (amd.com/v1alpha1) — fields used, verify per release
+// ---------------------------------------------------------------------------
+
+export interface OperandStatus {
+  nodesMatchingSelectorNumber?: number;
+  desiredNumber?: number;
+  availableNumber?: number;
+}
+
+export interface DeviceConfigSpec {
+  driver?: { enable?: boolean; version?: string; image?: string };
+  devicePlugin?: { devicePluginImage?: string; nodeLabellerImage?: string; enableNodeLabeller?: boolean };
+  metricsExporter?: { enable?: boolean; port?: number; image?: string; serviceType?: string; nodePort?: number };
+  testRunner?: { enable?: boolean };
+  selector?: Record<string, string>;
+}
+
+export interface DeviceConfigStatus {
+  devicePlugin?: OperandStatus;
+  nodeLabeller?: OperandStatus;
+  metricsExporter?: OperandStatus;
+  driver?: OperandStatus;
+}
+
+export interface DeviceConfig extends KubeObject {
+  kind: 'DeviceConfig';
+  spec?: DeviceConfigSpec;
+  status?: DeviceConfigStatus;
+}
+
+// ---------------------------------------------------------------------------
+// Node
+// ---------------------------------------------------------------------------
+
+export type NodeResources = Record<string, string | undefined>;
+
+export interface NodeCondition {
+  type: string;
+  status: string;
+  reason?: string;
+  message?: string;
+  lastHeartbeatTime?: string;
+}
+
+export interface NodeStatus {
+  capacity?: NodeResources;
+  allocatable?: NodeResources;
+  conditions?: NodeCondition[];
+  nodeInfo?: {
+    kernelVersion?: string;
+    osImage?: string;
+    architecture?: string;
+    kubeletVersion?: string;
+    containerRuntimeVersion?: string;
+  };
+}
+
+export interface NodeSpec {
+  taints?: Array<{ key: string; effect: string; value?: string }>;
+  unschedulable?: boolean;
+}
+
+export interface AmdGpuNode extends KubeObject {
+  spec?: NodeSpec;
+  status?: NodeStatus;
+}
+
+/** Result of getNodeGpuModel(). */
+export interface GpuModel {
+  product: string;
+  shortName: string;
+  fromLabels: boolean;
+  computePartition: string | null;
+  memoryPartition: string | null;
+  vram: string;
+  cuCount: number;
+}
+
+// ---------------------------------------------------------------------------
+// Pod
+// ---------------------------------------------------------------------------
+
+export interface ResourceRequirements {
+  requests?: Record<string, string>;
+  limits?: Record<string, string>;
+}
+
+export interface ContainerSpec {
+  name: string;
+  image?: string;
+  resources?: ResourceRequirements;
+  /** `Always` marks a restartable (sidecar) init container. */
+  restartPolicy?: string;
+}
+
+export interface ContainerStatus {
+  name: string;
+  ready: boolean;
+  restartCount: number;
+  image?: string;
+  state?: {
+    running?: { startedAt?: string };
+    waiting?: { reason?: string; message?: string };
+    terminated?: { exitCode?: number; reason?: string };
+  };
+}
+
+export interface PodSpec {
+  nodeName?: string;
+  containers?: ContainerSpec[];
+  initContainers?: ContainerSpec[];
+}
+
+export interface PodStatus {
+  phase?: string;
+  conditions?: Array<{ type: string; status: string; reason?: string }>;
+  containerStatuses?: ContainerStatus[];
+  initContainerStatuses?: ContainerStatus[];
+}
+
+export interface AmdGpuPod extends KubeObject {
+  spec?: PodSpec;
+  status?: PodStatus;
+}
+
+/** One AMD resource entry of a container (containerGpuEntries()). */
+export interface ContainerGpuEntry {
+  key: string;
+  request: string | null;
+  limit: string | null;
+  effective: number;
+}
+
+// ---------------------------------------------------------------------------
+// Cluster index (buildClusterIndex())
+// ---------------------------------------------------------------------------
+
+export interface NodeStats {
+  capacity: number;
+  allocatable: number;
+  inUse: number;
+  pods: number;
+  ready: boolean;
+}
+
+export interface ClusterIndex {
+  podsByNode: Record<string, AmdGpuPod[]>;
+  nodeStats: Record<string, NodeStats>;
+  totals: {
+    nodes: number;
+    readyNodes: number;
+    capacity: number;
+    allocatable: number;
+    inUse: number;
+    free: number;
+    partitions: number;
+    utilizationPct: number;
+  };
+  phases: { Running: number; Pending: number; Succeeded: number; Failed: number; Other: number };
+}

@@ -152,6 +152,24 @@ export function overviewView(ctx, opts) {
   return page(BRAND + ' — Overview', refreshButton('Refresh AMD GPU data', ctx.refreshing), items);
 }
 
+const MODE_COLORS = ['#ed1c24', '#f06b6f', '#7a0c10', '#ff9e80', '#9e9e9e'];
+
+/** PercentageBar data: nodes per compute/memory partition mode ("SPX/NPS1" when unlabelled). */
+export function partitionModeDistribution(gpuNodes) {
+  const counts = {};
+  const order = [];
+  for (let i = 0; i < gpuNodes.length; i++) {
+    const m = getNodeGpuModel(gpuNodes[i]);
+    const k = (m.computePartition || 'SPX') + '/' + (m.memoryPartition || 'NPS1');
+    if (!(k in counts)) {
+      counts[k] = 0;
+      order.push(k);
+    }
+    counts[k]++;
+  }
+  return order.map(function (k, i) { return { name: k, value: counts[k], fill: MODE_COLORS[i % MODE_COLORS.length] }; });
+}
+
 function overviewItems(ctx, now) {
   const items = [];
   const t = ctx.index.totals;
@@ -231,6 +249,10 @@ function overviewItems(ctx, now) {
         t.nodes
       )
     );
+    // Analog of the reference's GPU-type distribution (OverviewPage.tsx:37-48):
+    // every GPU is an MI355X, so what varies between nodes is the partition mode.
+    const modes = partitionModeDistribution(ctx.gpuNodes);
+    if (modes.length > 0) nodeBlocks.push(pctbar('GPU Partition Modes', modes, t.nodes));
   }
   const nodeRows = [
     row('Total GPU Nodes', status(t.nodes > 0 ? 'success' : 'warning', t.nodes)),

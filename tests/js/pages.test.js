@@ -84,6 +84,14 @@ describe('overviewView', () => {
     expect(text(rowValue(s, 'GPU Model'))).toContain('MI355X');
   });
 
+  it('shows the partition-mode distribution of GPU nodes', () => {
+    const vm = overviewView(makeContext({ nodes: [makeGpuNode('a'), makeGpuNode('b', { partition: 'cpx/nps4' }), makeGpuNode('c')] }), opts);
+    const bars = findSection(vm, 'GPU Nodes').blocks.filter((b) => b.t === 'pctbar');
+    const modes = bars.find((b) => b.label === 'GPU Partition Modes');
+    expect(modes.data.map((d) => [d.name, d.value])).toEqual([['SPX/NPS1', 2], ['CPX/NPS4', 1]]);
+    expect(modes.total).toBe(3);
+  });
+
   it('warns when there are zero GPU nodes', () => {
     const vm = overviewView(makeContext({ nodes: [makeNode('cpu')] }), opts);
     expect(rowValue(findSection(vm, 'GPU Nodes'), 'Total GPU Nodes').status).toBe('warning');
