@@ -23,6 +23,7 @@ import { createClusterStore, getSharedStore } from './clusterStore.js';
 import { createMetricsSource } from './metrics.js';
 import type { GpuMetrics } from './metrics.js';
 import { clusterKey } from './cluster.js';
+import { createPoller, loadSettings, prometheusCandidates, seriesStepSec } from './settings.js';
 
 /** Data younger than this is served from the shared store on mount without re-fetching. */
 export const STALE_MS = 5000;
@@ -45,15 +46,30 @@ function request(path: string): Promise<unknown> {
 
 /** The shared store of the current cluster (created on first use). */
 export function storeFor(cluster: string) {
-  return getSharedStore(cluster, () => createClusterStore({ request }));
+  const settings = loadSettings();
+  return getSharedStore(`${cluster}|${settings.requestTimeoutMs}`, () =>
+    createClusterStore({ request, timeoutMs: settings.requestTimeoutMs })
+  );
 }
 
 const metricsSources: Record<string, ReturnType<typeof createMetricsSource>> = {};
 
-/** The shared Prometheus client of the current cluster (discovery cache lives here). */
+/**
+ * The shared Prometheus client of the current cluster (its discovery cache
+ * lives here). Keyed by the settings that shape it, so saving new settings
+ * takes effect on the next mount.
+ */
 export function metricsSourceFor(cluster: string) {
-  if (!metricsSources[cluster]) metricsSources[cluster] = createMetricsSource({ request });
-  return metricsSources[cluster];
+  const settings = loadSettings();
+  const key = `${cluster}|${JSON.stringify(settings.prometheus)}|${settings.requestTimeoutMs}`;
+  if (!metricsSources[key]) {
+    metricsSources[key] = createMetricsSource({
+      request,
+      services: prometheusCandidates(settings),
+      timeoutMs: settings.requestTimeoutMs,
+    });
+  }
+  return metricsSources[key];
 }
 
 export function AmdGpuDataProvider({ children }: { children: React.ReactNode }) {
@@ -74,6 +90,14 @@ export function AmdGpuDataProvider({ children }: { children: React.ReactNode }) 
   useEffect(() => {
     void store.revalidate(STALE_MS);
   }, [store]);
+
+  // Optional auto-refresh (settings; the reference only refreshes on click).
+  const refreshIntervalSec = loadSettings().refreshIntervalSec;
+  useEffect(() => {
+    const poller = createPoller(refreshIntervalSec);
+    poller.start(() => store.revalidate(STALE_MS));
+    return () => poller.stop();
+  }, [store, refreshIntervalSec]);
 
   const snapshot = useSyncExternalStore(store.subscribe, store.getSnapshot);
   const value = useMemo<AmdGpuContextValue>(
@@ -111,6 +135,7 @@ export const PROMETHEUS_UNREACHABLE =
  */
 export function useGpuMetrics(enabled = true): GpuMetricsState {
   const source = metricsSourceFor(clusterKey());
+  const settings = loadSettings();
   const [state, setState] = useState<Omit<GpuMetricsState, 'refresh'>>({
     metrics: null,
     series: null,
@@ -123,7 +148,7 @@ export function useGpuMetrics(enabled = true): GpuMetricsState {
     if (!enabled) return;
     let cancelled = false;
     setState(s => ({ ...s, fetching: true, fetchError: null }));
-    Promise.all([source.fetchGpuMetrics(), source.fetchSeries(1800, 30)])
+    Promise.all([source.fetchGpuMetrics(), source.fetchSeries(settings.seriesMinutes * 60, seriesStepSec(settings))])
       .then(([metrics, series]) => {
         if (cancelled) return;
         setState({ metrics, series, fetching: false, fetchError: metrics ? null : PROMETHEUS_UNREACHABLE });
@@ -135,7 +160,14 @@ export function useGpuMetrics(enabled = true): GpuMetricsState {
     return () => {
       cancelled = true;
     };
-  }, [enabled, seq, source]);
+  }, [enabled, seq, source, settings.seriesMinutes]);
+
+  useEffect(() => {
+    if (!enabled) return;
+    const poller = createPoller(settings.refreshIntervalSec);
+    poller.start(() => setSeq(s => s + 1));
+    return () => poller.stop();
+  }, [enabled, settings.refreshIntervalSec]);
 
   return useMemo(() => ({ ...state, refresh: () => setSeq(s => s + 1) }), [state]);
 }

@@ -1,0 +1,155 @@
+/**
+ * Plugin settings — validated, persisted, framework-free.
+ *
+ * The reference has no runtime configuration: its Prometheus namespace /
+ * service / port, request timeout and rate window are compile-time constants
+ * (SURVEY.md §5 "Config / flag system: absent"; reference
+ * src/api/metrics.ts:61-65, IntelGpuDataContext.tsx:72). Here they are user
+ * settings, stored in the browser (localStorage) and edited on Headlamp's
+ * plugin settings page (src/components/SettingsPage.tsx).
+ *
+ * Every value read back is re-validated: a corrupted or hand-edited entry
+ * falls back to the defaults field by field instead of breaking the plugin.
+ */
+
+import { PROMETHEUS_SERVICES } from './metrics.js';
+import { isObject } from './amdgpu.js';
+
+export const SETTINGS_KEY = 'headlamp-amd-gpu-plugin.settings';
+
+export const REFRESH_CHOICES = [0, 15, 30, 60, 300];
+
+export const DEFAULT_SETTINGS = Object.freeze({
+  /** Explicit Prometheus service, tried before the built-in candidates. */
+  prometheus: null,
+  /** Auto-refresh period in seconds (0 = manual refresh only, like the reference). */
+  refreshIntervalSec: 0,
+  /** Per-request timeout for the CRD / pod / discovery requests. */
+  requestTimeoutMs: 2000,
+  /** Time-series window on the Metrics page. */
+  seriesMinutes: 30,
+});
+
+const DNS_LABEL = /^[a-z0-9]([-a-z0-9]*[a-z0-9])?$/;
+
+function clampInt(v, lo, hi, dflt) {
+  const n = typeof v === 'number' ? v : parseInt(String(v), 10);
+  if (!isFinite(n)) return dflt;
+  return Math.min(hi, Math.max(lo, Math.round(n)));
+}
+
+/** Validate a {namespace, service, port} triple; null when incomplete or invalid. */
+export function parsePrometheus(v) {
+  if (!isObject(v)) return null;
+  const ns = String(v.namespace || '').trim();
+  const svc = String(v.service || '').trim();
+  const port = String(v.port || '').trim();
+  if (!DNS_LABEL.test(ns) || !DNS_LABEL.test(svc)) return null;
+  if (!/^([0-9]{1,5}|[a-z][-a-z0-9]{0,14})$/.test(port)) return null;
+  return { namespace: ns, service: svc, port: port };
+}
+
+/**
+ * Unknown → settings, field by field, with defaults for anything invalid.
+ * @returns {{prometheus: ({namespace: string, service: string, port: string}|null), refreshIntervalSec: number,
+ *            requestTimeoutMs: number, seriesMinutes: number}}
+ */
+export function parseSettings(raw) {
+  const o = isObject(raw) ? raw : {};
+  const refresh = clampInt(o.refreshIntervalSec, 0, 3600, DEFAULT_SETTINGS.refreshIntervalSec);
+  return {
+    prometheus: parsePrometheus(o.prometheus),
+    refreshIntervalSec: refresh > 0 && refresh < 5 ? 5 : refresh,
+    requestTimeoutMs: clampInt(o.requestTimeoutMs, 250, 30000, DEFAULT_SETTINGS.requestTimeoutMs),
+    seriesMinutes: clampInt(o.seriesMinutes, 5, 24 * 60, DEFAULT_SETTINGS.seriesMinutes),
+  };
+}
+
+/** Prometheus candidates in priority order: the configured service first, then the defaults. */
+export function prometheusCandidates(settings) {
+  const out = [];
+  const p = settings && settings.prometheus;
+  if (p) out.push(p);
+  for (let i = 0; i < PROMETHEUS_SERVICES.length; i++) {
+    const d = PROMETHEUS_SERVICES[i];
+    if (!p || d.namespace !== p.namespace || d.service !== p.service || d.port !== p.port) out.push(d);
+  }
+  return out;
+}
+
+/** Range-query step that keeps the series near 60 points. */
+export function seriesStepSec(settings) {
+  return Math.max(15, Math.round((settings.seriesMinutes * 60) / 60 / 15) * 15);
+}
+
+function defaultStorage() {
+  try {
+    if (typeof localStorage !== 'undefined' && localStorage && typeof localStorage.getItem === 'function') return localStorage;
+  } catch (e) {
+    // storage disabled (privacy mode): settings stay in memory
+  }
+  return null;
+}
+
+/** Read settings from storage (defaults when absent or unreadable). */
+export function loadSettings(storage) {
+  const st = storage === undefined ? defaultStorage() : storage;
+  if (!st) return parseSettings(null);
+  try {
+    const raw = st.getItem(SETTINGS_KEY);
+    return parseSettings(raw ? JSON.parse(raw) : null);
+  } catch (e) {
+    return parseSettings(null);
+  }
+}
+
+/** Validate and persist; returns what was stored. */
+export function saveSettings(value, storage) {
+  const clean = parseSettings(value);
+  const st = storage === undefined ? defaultStorage() : storage;
+  if (st) {
+    try {
+      st.setItem(SETTINGS_KEY, JSON.stringify(clean));
+    } catch (e) {
+      // quota / disabled storage: keep the in-memory value
+    }
+  }
+  return clean;
+}
+
+/**
+ * Interval poller with an injectable clock. `start(fn)` calls fn every
+ * `periodSec` seconds, skipping a tick while the previous call's promise is
+ * still pending (no overlapping refreshes). Period 0 → never.
+ */
+export function createPoller(periodSec, clock) {
+  const c = clock || { setInterval: setInterval, clearInterval: clearInterval };
+  let handle = null;
+  let busy = false;
+  let ticks = 0;
+  let skipped = 0;
+  return {
+    start: function (fn) {
+      if (handle !== null || !(periodSec > 0)) return;
+      handle = c.setInterval(function () {
+        if (busy) {
+          skipped++;
+          return;
+        }
+        busy = true;
+        ticks++;
+        Promise.resolve()
+          .then(fn)
+          .then(
+            function () { busy = false; },
+            function () { busy = false; }
+          );
+      }, periodSec * 1000);
+    },
+    stop: function () {
+      if (handle !== null) c.clearInterval(handle);
+      handle = null;
+    },
+    stats: function () { return { ticks: ticks, skipped: skipped, running: handle !== null }; },
+  };
+}

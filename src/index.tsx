@@ -14,6 +14,7 @@
  * revalidates in the background (reference quirk Q7).
  */
 
+import * as pluginLib from '@kinvolk/headlamp-plugin/lib';
 import {
   registerDetailsViewSection,
   registerResourceTableColumnsProcessor,
@@ -30,6 +31,7 @@ import NodesPage from './components/NodesPage';
 import OverviewPage from './components/OverviewPage';
 import PodDetailSection from './components/PodDetailSection';
 import PodsPage from './components/PodsPage';
+import SettingsPage from './components/SettingsPage';
 import { processColumns, ROUTES, SIDEBAR } from './routes.js';
 
 // ---------------------------------------------------------------------------
@@ -92,3 +94,17 @@ registerDetailsViewSection(({ resource }: { resource?: { kind?: string } }) => {
 registerResourceTableColumnsProcessor((args: { id: string; columns: unknown[] }) =>
   processColumns(args, buildNodeGpuColumns)
 );
+
+// ---------------------------------------------------------------------------
+// Plugin settings (Headlamp >= 0.22 exposes registerPluginSettings; older
+// hosts simply run with the defaults of src/api/settings.js)
+// ---------------------------------------------------------------------------
+
+const registerPluginSettings = (pluginLib as unknown as Record<string, unknown>)['registerPluginSettings'];
+if (typeof registerPluginSettings === 'function') {
+  (registerPluginSettings as (name: string, c: React.ComponentType<any>, save: boolean) => void)(
+    'amd-gpu',
+    SettingsPage,
+    false
+  );
+}

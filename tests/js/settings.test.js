@@ -1,0 +1,133 @@
+/**
+ * Settings subsystem (src/api/settings.js) — new: the reference has no
+ * runtime configuration (SURVEY.md §5).
+ */
+import {
+  DEFAULT_SETTINGS,
+  SETTINGS_KEY,
+  createPoller,
+  loadSettings,
+  parsePrometheus,
+  parseSettings,
+  prometheusCandidates,
+  saveSettings,
+  seriesStepSec,
+} from '../../src/api/settings.js';
+import { PROMETHEUS_SERVICES } from '../../src/api/metrics.js';
+
+function memStorage() {
+  const m = new Map();
+  return {
+    getItem: (k) => (m.has(k) ? m.get(k) : null),
+    setItem: (k, v) => m.set(k, String(v)),
+    raw: m,
+  };
+}
+
+describe('parseSettings', () => {
+  it('returns the defaults for garbage', () => {
+    expect(parseSettings(null)).toEqual(Object.assign({}, DEFAULT_SETTINGS));
+    expect(parseSettings('x')).toEqual(Object.assign({}, DEFAULT_SETTINGS));
+  });
+  it('clamps numbers field by field', () => {
+    const s = parseSettings({ refreshIntervalSec: 2, requestTimeoutMs: 10, seriesMinutes: 100000 });
+    expect(s.refreshIntervalSec).toBe(5);
+    expect(s.requestTimeoutMs).toBe(250);
+    expect(s.seriesMinutes).toBe(1440);
+  });
+  it('keeps valid values and parses numeric strings', () => {
+    const s = parseSettings({ refreshIntervalSec: '30', requestTimeoutMs: 5000, seriesMinutes: 60 });
+    expect(s).toEqual({ prometheus: null, refreshIntervalSec: 30, requestTimeoutMs: 5000, seriesMinutes: 60 });
+  });
+  it('zero refresh interval means manual', () => {
+    expect(parseSettings({ refreshIntervalSec: 0 }).refreshIntervalSec).toBe(0);
+  });
+});
+
+describe('parsePrometheus', () => {
+  it('accepts DNS-label names and numeric or named ports', () => {
+    expect(parsePrometheus({ namespace: 'obs', service: 'vmsingle', port: '8429' })).toEqual({ namespace: 'obs', service: 'vmsingle', port: '8429' });
+    expect(parsePrometheus({ namespace: 'obs', service: 'prom', port: 'web' })).not.toBeNull();
+  });
+  it('rejects path tricks and incomplete triples', () => {
+    expect(parsePrometheus({ namespace: '../x', service: 'p', port: '9090' })).toBeNull();
+    expect(parsePrometheus({ namespace: 'a', service: 'p/../q', port: '9090' })).toBeNull();
+    expect(parsePrometheus({ namespace: 'a', service: 'p' })).toBeNull();
+    expect(parsePrometheus(null)).toBeNull();
+  });
+});
+
+describe('prometheusCandidates', () => {
+  it('defaults to the built-in services', () => {
+    expect(prometheusCandidates(parseSettings(null))).toEqual(PROMETHEUS_SERVICES);
+  });
+  it('puts the configured service first without duplicating it', () => {
+    const own = { namespace: 'monitoring', service: 'prometheus-operated', port: '9090' };
+    const c = prometheusCandidates(parseSettings({ prometheus: own }));
+    expect(c[0]).toEqual(own);
+    expect(c).toHaveLength(PROMETHEUS_SERVICES.length);
+  });
+});
+
+describe('persistence', () => {
+  it('round-trips through storage with validation', () => {
+    const st = memStorage();
+    saveSettings({ refreshIntervalSec: 60, prometheus: { namespace: 'o', service: 's', port: '1' } }, st);
+    expect(JSON.parse(st.raw.get(SETTINGS_KEY)).refreshIntervalSec).toBe(60);
+    expect(loadSettings(st).prometheus).toEqual({ namespace: 'o', service: 's', port: '1' });
+  });
+  it('survives corrupted storage', () => {
+    const st = memStorage();
+    st.setItem(SETTINGS_KEY, '{not json');
+    expect(loadSettings(st)).toEqual(Object.assign({}, DEFAULT_SETTINGS));
+  });
+  it('works without storage', () => {
+    expect(loadSettings(null).requestTimeoutMs).toBe(2000);
+    expect(saveSettings({ seriesMinutes: 10 }, null).seriesMinutes).toBe(10);
+  });
+});
+
+describe('seriesStepSec', () => {
+  it('keeps about 60 points on a 15 s grid', () => {
+    expect(seriesStepSec(parseSettings({ seriesMinutes: 30 }))).toBe(30);
+    expect(seriesStepSec(parseSettings({ seriesMinutes: 5 }))).toBe(15);
+    expect(seriesStepSec(parseSettings({ seriesMinutes: 360 }))).toBe(360);
+  });
+});
+
+describe('createPoller', () => {
+  it('ticks every period and stops', async () => {
+    vi.useFakeTimers();
+    const fn = vi.fn(() => Promise.resolve());
+    const p = createPoller(30);
+    p.start(fn);
+    await vi.advanceTimersByTimeAsync(95000);
+    expect(fn).toHaveBeenCalledTimes(3);
+    p.stop();
+    await vi.advanceTimersByTimeAsync(60000);
+    expect(fn).toHaveBeenCalledTimes(3);
+    expect(p.stats().running).toBe(false);
+    vi.useRealTimers();
+  });
+  it('skips ticks while a refresh is still running', async () => {
+    vi.useFakeTimers();
+    let release;
+    const fn = vi.fn(() => new Promise((r) => { release = r; }));
+    const p = createPoller(10);
+    p.start(fn);
+    await vi.advanceTimersByTimeAsync(35000);
+    expect(fn).toHaveBeenCalledTimes(1);
+    expect(p.stats().skipped).toBe(2);
+    release();
+    await vi.advanceTimersByTimeAsync(10000);
+    expect(fn).toHaveBeenCalledTimes(2);
+    p.stop();
+    vi.useRealTimers();
+  });
+  it('period 0 never polls', () => {
+    const fn = vi.fn();
+    const p = createPoller(0);
+    p.start(fn);
+    expect(p.stats().running).toBe(false);
+  });
+});
