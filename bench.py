@@ -176,6 +176,7 @@ def main(argv=None) -> int:
                          "requests_per_refresh": result["ref"]["requestsPerStep"]},
             "p95_ms": round(amd_s["p95"], 3),
             "requests_per_refresh": result["amd"]["requestsPerStep"],
+            "request_trace_p50_ms": {k: round(v["p50_ms"], 2) for k, v in (result["amd"].get("trace") or {}).items()},
             "cold_open_p50_ms": {"amd": round(summarize(result["amd_cold"]["latencies"])["p50"], 3),
                                  "reference": round(summarize(result["ref_cold"]["latencies"])["p50"], 3)},
             "route_switch_p50_ms": {"amd": round(summarize(result["amd_switch"]["latencies"])["p50"], 3),

@@ -161,8 +161,13 @@ function renderAll(ctx, mstate) {
 // ---------------------------------------------------------------------------
 
 function amdSchedule(request) {
-  const store = createClusterStore({ request: request });
-  const metrics = createMetricsSource({ request: request });
+  // Request spans from the data layer's tracing hook (clusterStore/metrics onTrace).
+  const spans = [];
+  function onTrace(span) {
+    spans.push(span);
+  }
+  const store = createClusterStore({ request: request, onTrace: onTrace });
+  const metrics = createMetricsSource({ request: request, onTrace: onTrace });
   const mstate = { metrics: null, fetchError: null, fetching: false, series: null };
   function fetchMetrics() {
     return Promise.all([metrics.fetchGpuMetrics(), metrics.fetchSeries(1800, 30)]).then(function (r) {
@@ -185,7 +190,22 @@ function amdSchedule(request) {
     },
     ctx: function () { return store.getSnapshot(); },
     mstate: function () { return mstate; },
+    spans: spans,
   };
+}
+
+/** p50 latency per traced request kind, plus how many of each were issued. */
+function traceSummary(spans) {
+  const by = {};
+  for (let i = 0; i < spans.length; i++) {
+    const s = spans[i];
+    const k = s.name.replace(/-\d+$/, '');
+    if (!by[k]) by[k] = [];
+    by[k].push(s.end - s.start);
+  }
+  const out = {};
+  for (const k in by) out[k] = { n: by[k].length, p50_ms: stats(by[k]).p50 };
+  return out;
 }
 
 function referenceSchedule(request) {
@@ -312,6 +332,7 @@ async function serve(a) {
         const lat = [];
         const before = counter.n;
         const bytesBefore = counter.bytes;
+        const spanStart = L.s.spans ? L.s.spans.length : 0;
         let rows = null;
         for (let i = 0; i < n; i++) {
           const t0 = process.hrtime();
@@ -319,6 +340,7 @@ async function serve(a) {
           rows = renderAll(L.s.ctx(), L.s.mstate());
           lat.push(ms(process.hrtime(t0)));
         }
+        if (L.s.spans) out.trace = traceSummary(L.s.spans.slice(spanStart));
         out.latencies = lat;
         out.requestsPerStep = (counter.n - before) / n;
         out.bytesPerStep = (counter.bytes - bytesBefore) / n;
