@@ -1,19 +1,22 @@
-"""Build the native extensions in-tree with hipcc for gfx950.
+"""Build the native code in-tree with hipcc for gfx950.
 
-Extensions (output next to this file so they travel with the repo snapshot
-to the GPU box; ``*.so`` is git-ignored):
+Targets (outputs next to this file so they travel with the repo snapshot to
+the GPU box; ``*.so`` and ``bin/`` are git-ignored):
 
-* ``_amdgpu_probe``  — C++ against the HIP runtime + amdgpu sysfs
-  (csrc/amdgpu_probe.cpp);
-* ``_workload``      — HIP kernels for gfx950 that the synthetic GPU pods run
-  (kernels/workload.hip).
+* ``_amdgpu_probe``   CPython extension — C++ over the HIP runtime + amdgpu
+  sysfs (csrc/amdgpu_probe.cpp + csrc/probe_core.h);
+* ``_workload``       CPython extension — HIP kernels for gfx950 run by the
+  synthetic GPU pods (kernels/workload.hip);
+* ``amdgpu-exporter`` standalone Prometheus exporter daemon built from the
+  same probe core (csrc/amdgpu_exporter.cpp) → ``bin/amdgpu-exporter``.
 
-Rebuilds only when a source is newer than its ``.so``. Usage::
+Rebuilds only when a source (or header) is newer than its output. Usage::
 
     python -m headlamp_intel_gpu_plugin_amd.ops.build [--force]
 """
 from __future__ import annotations
 
+import glob
 import os
 import shutil
 import subprocess
@@ -25,21 +28,33 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = "gfx950"
 
-EXTENSIONS: Dict[str, Dict] = {
-    "_amdgpu_probe": {"sources": ["csrc/amdgpu_probe.cpp"], "hip": False},
-    "_workload": {"sources": ["kernels/workload.hip"], "hip": True},
+TARGETS: Dict[str, Dict] = {
+    "_amdgpu_probe": {"sources": ["csrc/amdgpu_probe.cpp"], "hip": False, "kind": "ext"},
+    "_workload": {"sources": ["kernels/workload.hip"], "hip": True, "kind": "ext"},
+    "amdgpu-exporter": {"sources": ["csrc/amdgpu_exporter.cpp"], "hip": False, "kind": "exe"},
 }
+# Backwards-compatible alias used by the import helper.
+EXTENSIONS = TARGETS
 
 
 def hipcc() -> str:
     for c in (os.path.join(ROCM, "bin", "hipcc"), shutil.which("hipcc")):
         if c and os.path.exists(c):
             return c
-    raise RuntimeError("hipcc not found (ROCm required to build the native extensions)")
+    raise RuntimeError("hipcc not found (ROCm required to build the native code)")
 
 
 def so_path(name: str) -> str:
+    """Output path of a target (``.so`` for extensions, ``bin/<name>`` for executables)."""
+    if TARGETS[name]["kind"] == "exe":
+        return os.path.join(HERE, "bin", name)
     return os.path.join(HERE, name + ".so")
+
+
+def _deps(name: str) -> List[str]:
+    srcs = [os.path.join(HERE, s) for s in TARGETS[name]["sources"]]
+    headers = glob.glob(os.path.join(HERE, "csrc", "*.h")) + glob.glob(os.path.join(HERE, "kernels", "*.h"))
+    return srcs + headers
 
 
 def _stale(name: str) -> bool:
@@ -47,16 +62,14 @@ def _stale(name: str) -> bool:
     if not os.path.exists(out):
         return True
     t = os.path.getmtime(out)
-    srcs = [os.path.join(HERE, s) for s in EXTENSIONS[name]["sources"]]
-    deps = srcs + [os.path.join(HERE, "kernels", f) for f in os.listdir(os.path.join(HERE, "kernels"))
-                   if f.endswith((".h", ".hpp"))] if os.path.isdir(os.path.join(HERE, "kernels")) else srcs
-    return any(os.path.exists(s) and os.path.getmtime(s) > t for s in deps)
+    return any(os.path.exists(s) and os.path.getmtime(s) > t for s in _deps(name))
 
 
 def command(name: str) -> List[str]:
-    spec = EXTENSIONS[name]
-    py_inc = sysconfig.get_paths()["include"]
-    cmd = [hipcc(), "-O3", "-std=c++17", "-fPIC", "-shared", f"-I{py_inc}", "-Wall", "-Wno-unused-function"]
+    spec = TARGETS[name]
+    cmd = [hipcc(), "-O3", "-std=c++17", "-Wall", "-Wno-unused-function", f"-I{os.path.join(HERE, 'csrc')}"]
+    if spec["kind"] == "ext":
+        cmd += ["-fPIC", "-shared", f"-I{sysconfig.get_paths()['include']}"]
     if spec["hip"]:
         cmd += [f"--offload-arch={ARCH}", "-x", "hip", "-munsafe-fp-atomics"]
     cmd += [os.path.join(HERE, s) for s in spec["sources"]]
@@ -65,13 +78,13 @@ def command(name: str) -> List[str]:
 
 
 def build(names=None, force: bool = False, verbose: bool = False) -> Dict[str, str]:
-    """Compile the given extensions (default: all). Returns name → .so path."""
+    """Compile the given targets (default: all). Returns name → output path."""
     out = {}
-    for name in names or EXTENSIONS:
-        src_ok = all(os.path.exists(os.path.join(HERE, s)) for s in EXTENSIONS[name]["sources"])
-        if not src_ok:
+    for name in names or TARGETS:
+        if not all(os.path.exists(os.path.join(HERE, s)) for s in TARGETS[name]["sources"]):
             continue
         if force or _stale(name):
+            os.makedirs(os.path.dirname(so_path(name)), exist_ok=True)
             cmd = command(name)
             if verbose:
                 print(" ".join(cmd), file=sys.stderr)

@@ -1,0 +1,271 @@
+// probe_core.h — MI355X telemetry probe core (HIP runtime + amdgpu sysfs).
+//
+// Shared by the CPython module (amdgpu_probe.cpp) and the standalone exporter
+// daemon (amdgpu_exporter.cpp). See amdgpu_probe.cpp for what is read and why.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <dirent.h>
+#include <unistd.h>
+
+#include <cctype>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <string>
+#include <vector>
+
+namespace amdprobe {
+
+
+inline constexpr uint32_t kLinkTypeXgmi = 4;  // HSA_AMD_LINK_INFO_TYPE_XGMI
+inline constexpr uint32_t kLinkTypePcie = 2;  // HSA_AMD_LINK_INFO_TYPE_PCIE
+
+struct DeviceInfo {
+  int index = -1;
+  std::string name;
+  std::string arch;
+  std::string bdf;  // "0000:05:00.0"
+  std::string uuid;
+  size_t hbm_bytes = 0;
+  int compute_units = 0;
+  int wavefront = 0;
+  size_t lds_per_cu = 0;
+  int l2_bytes = 0;
+  int clock_khz = 0;
+  int mem_clock_khz = 0;
+  int mem_bus_width = 0;
+  int pci_domain = 0, pci_bus = 0, pci_device = 0;
+};
+
+struct Sample {
+  double power_w = NAN;      // average (or instantaneous) board power
+  double power_cap_w = NAN;  // power1_cap
+  double temp_edge_c = NAN, temp_junction_c = NAN, temp_mem_c = NAN;
+  double sclk_mhz = NAN, mclk_mhz = NAN;
+  double gfx_busy_pct = NAN, mem_busy_pct = NAN;
+  double vram_used_b = NAN, vram_total_b = NAN;
+};
+
+inline bool g_hip_ok = false;
+inline int g_count = 0;
+inline std::string g_error;
+
+inline bool read_text(const std::string& path, std::string* out) {
+  std::ifstream f(path);
+  if (!f) return false;
+  std::stringstream ss;
+  ss << f.rdbuf();
+  *out = ss.str();
+  while (!out->empty() && (out->back() == '\n' || out->back() == ' ')) out->pop_back();
+  return true;
+}
+
+inline bool read_double(const std::string& path, double* v) {
+  std::string s;
+  if (!read_text(path, &s) || s.empty()) return false;
+  char* end = nullptr;
+  double d = std::strtod(s.c_str(), &end);
+  if (end == s.c_str()) return false;
+  *v = d;
+  return true;
+}
+
+inline std::string lower_bdf(const char* bus_id) {
+  std::string s(bus_id);
+  for (auto& c : s) c = static_cast<char>(std::tolower(static_cast<unsigned char>(c)));
+  return s;
+}
+
+inline std::vector<std::string> hwmon_dirs(const std::string& dev_dir) {
+  std::vector<std::string> out;
+  std::string base = dev_dir + "/hwmon";
+  DIR* d = opendir(base.c_str());
+  if (!d) return out;
+  while (dirent* e = readdir(d)) {
+    if (std::strncmp(e->d_name, "hwmon", 5) == 0) out.push_back(base + "/" + e->d_name);
+  }
+  closedir(d);
+  return out;
+}
+
+inline bool init_hip() {
+  if (g_hip_ok) return true;
+  hipError_t err = hipGetDeviceCount(&g_count);
+  if (err != hipSuccess) {
+    g_error = std::string("hipGetDeviceCount: ") + hipGetErrorString(err);
+    g_count = 0;
+    return false;
+  }
+  g_hip_ok = true;
+  return true;
+}
+
+inline bool device_info(int dev, DeviceInfo* out) {
+  hipDeviceProp_t p;
+  hipError_t err = hipGetDeviceProperties(&p, dev);
+  if (err != hipSuccess) {
+    g_error = std::string("hipGetDeviceProperties: ") + hipGetErrorString(err);
+    return false;
+  }
+  out->index = dev;
+  out->name = p.name;
+  out->arch = p.gcnArchName;
+  out->hbm_bytes = p.totalGlobalMem;
+  out->compute_units = p.multiProcessorCount;
+  out->wavefront = p.warpSize;
+  out->lds_per_cu = p.maxSharedMemoryPerMultiProcessor;
+  out->l2_bytes = p.l2CacheSize;
+  out->clock_khz = p.clockRate;
+  out->mem_clock_khz = p.memoryClockRate;
+  out->mem_bus_width = p.memoryBusWidth;
+  out->pci_domain = p.pciDomainID;
+  out->pci_bus = p.pciBusID;
+  out->pci_device = p.pciDeviceID;
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, sizeof(bus), dev) == hipSuccess) {
+    out->bdf = lower_bdf(bus);
+  } else {
+    char tmp[64];
+    std::snprintf(tmp, sizeof(tmp), "%04x:%02x:%02x.0", p.pciDomainID, p.pciBusID, p.pciDeviceID);
+    out->bdf = tmp;
+  }
+  char hex[40] = {0};
+  for (int i = 0; i < 16; ++i) std::snprintf(hex + 2 * i, 3, "%02x", static_cast<unsigned char>(p.uuid.bytes[i]));
+  out->uuid = hex;
+  return true;
+}
+
+inline Sample sample_sysfs(const std::string& bdf) {
+  Sample s;
+  const std::string dir = "/sys/bus/pci/devices/" + bdf;
+  double v;
+  if (read_double(dir + "/gpu_busy_percent", &v)) s.gfx_busy_pct = v;
+  if (read_double(dir + "/mem_busy_percent", &v)) s.mem_busy_pct = v;
+  if (read_double(dir + "/mem_info_vram_used", &v)) s.vram_used_b = v;
+  if (read_double(dir + "/mem_info_vram_total", &v)) s.vram_total_b = v;
+  for (const auto& h : hwmon_dirs(dir)) {
+    // power: µW
+    if (std::isnan(s.power_w) && read_double(h + "/power1_average", &v)) s.power_w = v / 1e6;
+    if (std::isnan(s.power_w) && read_double(h + "/power1_input", &v)) s.power_w = v / 1e6;
+    if (std::isnan(s.power_cap_w) && read_double(h + "/power1_cap", &v)) s.power_cap_w = v / 1e6;
+    // temperatures: m°C, labelled edge / junction / mem
+    for (int t = 1; t <= 4; ++t) {
+      const std::string in = h + "/temp" + std::to_string(t) + "_input";
+      if (!read_double(in, &v)) continue;
+      std::string label;
+      read_text(h + "/temp" + std::to_string(t) + "_label", &label);
+      const double c = v / 1000.0;
+      if (label == "edge") s.temp_edge_c = c;
+      else if (label == "junction" || label == "hotspot") s.temp_junction_c = c;
+      else if (label == "mem") s.temp_mem_c = c;
+      else if (t == 1 && std::isnan(s.temp_edge_c)) s.temp_edge_c = c;
+    }
+    // clocks: Hz, freq1 = sclk, freq2 = mclk
+    if (read_double(h + "/freq1_input", &v)) s.sclk_mhz = v / 1e6;
+    if (read_double(h + "/freq2_input", &v)) s.mclk_mhz = v / 1e6;
+  }
+  return s;
+}
+
+inline void append_metric(std::string* out, const char* name, const std::string& labels, double v) {
+  if (std::isnan(v)) return;
+  char num[64];
+  std::snprintf(num, sizeof(num), "%.6g", v);
+  out->append(name).append("{").append(labels).append("} ").append(num).append("\n");
+}
+
+inline std::string escape_label(const std::string& s) {
+  std::string o;
+  for (char c : s) {
+    if (c == '\\' || c == '"') o.push_back('\\');
+    if (c == '\n') {
+      o.append("\\n");
+      continue;
+    }
+    o.push_back(c);
+  }
+  return o;
+}
+
+struct RenderOptions {
+  std::string hostname = "localhost";
+  int only_device = -1;      // export just this HIP device (-1 = all)
+  std::string gpu_label;     // override the gpu_id label (with only_device)
+  bool topology = true;      // emit xGMI link metrics between exported devices
+};
+
+// Render devices in exporter format. Units follow the AMD Device Metrics
+// Exporter conventions the plugin reads: watts, percent, MiB, °C, MHz.
+inline std::string render(const RenderOptions& opt) {
+  std::string out;
+  out.reserve(4096);
+  static const char* kHelp[][2] = {
+      {"gpu_power_usage", "GPU board power (W)"},
+      {"gpu_gfx_activity", "GFX engine busy (%)"},
+      {"gpu_umc_activity", "HBM memory-controller busy (%)"},
+      {"gpu_used_vram", "HBM in use (MiB)"},
+      {"gpu_total_vram", "HBM capacity (MiB)"},
+      {"gpu_edge_temperature", "edge temperature (C)"},
+      {"gpu_junction_temperature", "junction temperature (C)"},
+      {"gpu_memory_temperature", "HBM temperature (C)"},
+      {"gpu_clock", "GFX clock (MHz)"},
+      {"gpu_memory_clock", "memory clock (MHz)"},
+      {"gpu_power_cap", "board power cap (W)"},
+      {"gpu_xgmi_link_hops", "hops between two GPUs over xGMI (absent when not xGMI-connected)"},
+  };
+  for (auto& h : kHelp) {
+    out.append("# HELP ").append(h[0]).append(" ").append(h[1]).append("\n");
+    out.append("# TYPE ").append(h[0]).append(" gauge\n");
+  }
+  const double mib = 1024.0 * 1024.0;
+  for (int d = 0; d < g_count; ++d) {
+    if (opt.only_device >= 0 && d != opt.only_device) continue;
+    DeviceInfo info;
+    if (!device_info(d, &info)) continue;
+    Sample s = sample_sysfs(info.bdf);
+    const std::string gid = (opt.only_device >= 0 && !opt.gpu_label.empty()) ? opt.gpu_label : std::to_string(d);
+    std::string labels = "hostname=\"" + escape_label(opt.hostname) + "\",gpu_id=\"" + escape_label(gid) +
+                         "\",card_model=\"" + escape_label(info.name) + "\",pci_bus=\"" + info.bdf +
+                         "\",serial_number=\"" + info.uuid + "\"";
+    append_metric(&out, "gpu_power_usage", labels, s.power_w);
+    append_metric(&out, "gpu_power_cap", labels, s.power_cap_w);
+    append_metric(&out, "gpu_gfx_activity", labels, s.gfx_busy_pct);
+    append_metric(&out, "gpu_umc_activity", labels, s.mem_busy_pct);
+    append_metric(&out, "gpu_used_vram", labels, std::isnan(s.vram_used_b) ? NAN : s.vram_used_b / mib);
+    append_metric(&out, "gpu_total_vram", labels,
+                  std::isnan(s.vram_total_b) ? static_cast<double>(info.hbm_bytes) / mib : s.vram_total_b / mib);
+    append_metric(&out, "gpu_edge_temperature", labels, s.temp_edge_c);
+    append_metric(&out, "gpu_junction_temperature", labels, s.temp_junction_c);
+    append_metric(&out, "gpu_memory_temperature", labels, s.temp_mem_c);
+    append_metric(&out, "gpu_clock", labels, s.sclk_mhz);
+    append_metric(&out, "gpu_memory_clock", labels, s.mclk_mhz);
+  }
+  if (opt.topology && opt.only_device < 0) {
+    for (int a = 0; a < g_count; ++a) {
+      for (int b = 0; b < g_count; ++b) {
+        if (a == b) continue;
+        uint32_t type = 0, hops = 0;
+        if (hipExtGetLinkTypeAndHopCount(a, b, &type, &hops) != hipSuccess || type != kLinkTypeXgmi) continue;
+        append_metric(&out, "gpu_xgmi_link_hops",
+                      "hostname=\"" + escape_label(opt.hostname) + "\",gpu_id=\"" + std::to_string(a) +
+                          "\",peer_gpu_id=\"" + std::to_string(b) + "\"",
+                      static_cast<double>(hops));
+      }
+    }
+  }
+  return out;
+}
+
+inline std::string render(const std::string& hostname) {
+  RenderOptions o;
+  o.hostname = hostname;
+  return render(o);
+}
+
+}  // namespace amdprobe

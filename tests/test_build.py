@@ -12,7 +12,7 @@ pytestmark = pytest.mark.skipif(not (shutil.which("hipcc") or os.path.exists("/o
 
 def test_extensions_build_and_import():
     built = native_build.build()
-    assert set(built) == {"_amdgpu_probe", "_workload"}
+    assert set(built) == {"_amdgpu_probe", "_workload", "amdgpu-exporter"}
     from headlamp_intel_gpu_plugin_amd.ops import probe, workload
 
     assert probe.native().device_count() >= 0
