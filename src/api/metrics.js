@@ -51,6 +51,7 @@ export const SERIES = {
     umc: 'gpu_umc_activity', // % — HBM controller busy
     temp: 'gpu_junction_temperature', // °C
     xgmiRe: 'xgmi_neighbor_[0-6]_tx_throughput', // bytes/s per neighbour
+    linkHops: 'gpu_xgmi_link_hops', // measured link topology (this repo's native amdgpu-exporter)
   },
   exporterVramUnitBytes: 1024 * 1024,
   nodeExporter: {
@@ -169,7 +170,20 @@ export function joinExporterResults(r) {
       if (v !== null) xgmi[node][src + '-' + dst] = v / 1e9;
     }
   }
-  return { gpus: gpus, xgmi: xgmi };
+  // Measured topology: gpu_xgmi_link_hops{gpu_id, peer_gpu_id} per xGMI-connected pair.
+  const links = {};
+  const lr = r[E.linkHops];
+  if (Array.isArray(lr)) {
+    for (let i = 0; i < lr.length; i++) {
+      const m = lr[i].metric || {};
+      const node = m.hostname || m.instance || '';
+      const v = num(lr[i].value[1]);
+      if (v === null || m.gpu_id === undefined || m.peer_gpu_id === undefined) continue;
+      if (!links[node]) links[node] = {};
+      links[node][m.gpu_id + '-' + m.peer_gpu_id] = { type: 'XGMI', hops: v };
+    }
+  }
+  return { gpus: gpus, xgmi: xgmi, links: links };
 }
 
 /**
@@ -220,7 +234,7 @@ export function joinNodeExporterResults(r) {
   each(r[N.vramUsed], cardKey, function (g, v) { g.vramUsedBytes = v; });
   each(r[N.vramTotal], cardKey, function (g, v) { g.vramTotalBytes = v; });
   gpus.sort(byNodeGpu);
-  return { gpus: gpus, xgmi: {} };
+  return { gpus: gpus, xgmi: {}, links: {} };
 }
 
 /**
@@ -231,7 +245,7 @@ export function joinNodeExporterResults(r) {
  */
 export function exporterQuery() {
   const E = SERIES.exporter;
-  return '{__name__=~"' + [E.power, E.vramUsed, E.vramTotal, E.gfx, E.umc, E.temp, E.xgmiRe].join('|') + '"}';
+  return '{__name__=~"' + [E.power, E.vramUsed, E.vramTotal, E.gfx, E.umc, E.temp, E.xgmiRe, E.linkHops].join('|') + '"}';
 }
 
 export function nodeExporterQuery() {
@@ -363,7 +377,7 @@ export function createMetricsSource(opts) {
           invalidate();
           return null;
         }
-        let joined = { gpus: [], xgmi: {} };
+        let joined = { gpus: [], xgmi: {}, links: {} };
         let src = null;
         if (exp) {
           const j = joinExporterResults(exp);
@@ -384,6 +398,7 @@ export function createMetricsSource(opts) {
           source: src,
           gpus: joined.gpus,
           xgmi: joined.xgmi,
+          links: joined.links || {},
           fetchedAt: new Date(clock.now()).toISOString(),
           prometheusPath: base,
         };

@@ -81,9 +81,12 @@ export function buildXgmiMatrix(gpuCount, measured, probed) {
       const key = i + '-' + j;
       let kind = 'xgmi';
       let hops = 1;
-      if (probed && probed[key]) {
-        kind = probed[key].type === 'XGMI' ? 'xgmi' : probed[key].type === 'PCIE' ? 'pcie' : 'none';
-        hops = probed[key].hops;
+      if (probed) {
+        // A measured topology is authoritative: a pair it does not list is not
+        // xGMI-connected.
+        const p = probed[key];
+        kind = !p ? 'none' : p.type === 'XGMI' ? 'xgmi' : p.type === 'PCIE' ? 'pcie' : 'none';
+        hops = p ? p.hops : 0;
       }
       const m = measured && typeof measured[key] === 'number' ? measured[key] : null;
       if (kind === 'xgmi') links++;

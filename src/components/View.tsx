@@ -127,7 +127,8 @@ function Matrix({ b }: { b: IR }) {
   return (
     <div style={{ marginTop: '12px', overflowX: 'auto' }}>
       <div style={{ fontSize: '13px', marginBottom: '6px', color: 'var(--mui-palette-text-secondary)' }}>
-        xGMI topology — {b.fullMesh ? `full mesh, ${m.linksPerGpu} links/GPU` : 'partial'} · {m.linksPerGpu}×
+        xGMI topology ({b.measuredTopology ? 'measured' : 'MI355X platform model'}) —{' '}
+        {b.fullMesh ? `full mesh, ${m.linksPerGpu} links/GPU` : 'partial'} · {m.linksPerGpu}×
         {m.size > 1 ? ` ${m.cells[0][1].peakGBs}` : ''} GB/s per GPU · ring collectives bound at {m.ringBusGBs} GB/s per link
       </div>
       <table style={{ borderCollapse: 'collapse', fontSize: '11px' }}>

@@ -428,10 +428,11 @@ export function slotsBlock(node, podsOnNode, owners) {
   return { t: 'slots', slots: s.slots, exact: s.exact };
 }
 
-/** xGMI neighbour matrix block. */
+/** xGMI neighbour matrix block; `measuredTopology` when link hops came from the exporter. */
 export function matrixBlock(gpuCount, measured, probed) {
-  const m = buildXgmiMatrix(gpuCount, measured, probed);
-  return { t: 'matrix', matrix: m, fullMesh: isFullMesh(m) };
+  const hasProbe = !!probed && Object.keys(probed).length > 0;
+  const m = buildXgmiMatrix(gpuCount, measured, hasProbe ? probed : undefined);
+  return { t: 'matrix', matrix: m, fullMesh: isFullMesh(m), measuredTopology: hasProbe };
 }
 
 function nodeCardRows(node, podsOnNode, stats, now) {
@@ -486,13 +487,14 @@ export function nodesView(ctx, opts) {
     const stats = idx.nodeStats[name];
     const own = owners[name];
     const xg = metrics && metrics.xgmi ? metrics.xgmi[name] : undefined;
+    const lk = metrics && metrics.links ? metrics.links[name] : undefined;
     items.push(
-      memo('node-card:' + name, [n, pods, stats, keyOf(own), keyOf(xg), age], function () {
+      memo('node-card:' + name, [n, pods, stats, keyOf(own), keyOf(xg), keyOf(lk), age], function () {
         const blocks = [kv(nodeCardRows(n, pods, stats, now))];
         const count = getNodeGpuCount(n);
         if (count > 0) {
           blocks.push(slotsBlock(n, pods, own));
-          blocks.push(matrixBlock(count, xg));
+          blocks.push(matrixBlock(count, xg, lk));
         }
         return section(name, blocks, n.metadata.uid || name);
       })
@@ -839,12 +841,13 @@ export function nodeDetailView(resource, ctx, opts) {
   const metrics = opts && opts.metrics ? opts.metrics : null;
   const own = ownersByNode(metrics)[name];
   const xg = metrics && metrics.xgmi ? metrics.xgmi[name] : undefined;
-  return memo('node-detail:' + name, [raw, podsOnNode, !!ctx.loading, keyOf(own), keyOf(xg)], function () {
-    return nodeDetailSection(raw, name, cap, alloc, podsOnNode, ctx.loading, own, xg);
+  const lk = metrics && metrics.links ? metrics.links[name] : undefined;
+  return memo('node-detail:' + name, [raw, podsOnNode, !!ctx.loading, keyOf(own), keyOf(xg), keyOf(lk)], function () {
+    return nodeDetailSection(raw, name, cap, alloc, podsOnNode, ctx.loading, own, xg, lk);
   });
 }
 
-function nodeDetailSection(raw, name, cap, alloc, podsOnNode, loading, own, xg) {
+function nodeDetailSection(raw, name, cap, alloc, podsOnNode, loading, own, xg, lk) {
   const allocatable = parseInt(alloc[AMD_GPU_RESOURCE] || '0', 10) || 0;
   let inUse = 0;
   for (let i = 0; i < podsOnNode.length; i++) {
@@ -868,7 +871,7 @@ function nodeDetailSection(raw, name, cap, alloc, podsOnNode, loading, own, xg) 
   const blocks = [kv(rows)];
   if (count > 0) {
     blocks.push(slotsBlock(raw, podsOnNode, own));
-    blocks.push(matrixBlock(count, xg));
+    blocks.push(matrixBlock(count, xg, lk));
   }
   return section('AMD GPU', blocks);
 }

@@ -170,6 +170,12 @@ describe('topology', () => {
     expect(isFullMesh(m)).toBe(false);
     expect(m.cells[0][1].kind).toBe('pcie');
   });
+  it('treats pairs missing from a measured topology as unconnected', () => {
+    const m = buildXgmiMatrix(3, null, { '0-1': { type: 'XGMI', hops: 1 }, '1-0': { type: 'XGMI', hops: 1 } });
+    expect(m.cells[0][2].kind).toBe('none');
+    expect(m.linksPerGpu).toBe(1);
+    expect(isFullMesh(m)).toBe(false);
+  });
   it('a single GPU is not a mesh', () => {
     expect(isFullMesh(buildXgmiMatrix(1))).toBe(false);
   });

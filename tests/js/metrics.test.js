@@ -166,6 +166,16 @@ describe('fetchGpuMetrics', () => {
     expect(m.xgmi.n0['0-1']).toBe(50);
     expect(m.xgmi.n0['3-0']).toBe(50);
   });
+  it('reads measured xGMI link hops from the native exporter', async () => {
+    const d = exporterData(['n0']);
+    d.gpu_xgmi_link_hops = [
+      vec({ __name__: 'gpu_xgmi_link_hops', hostname: 'n0', gpu_id: '0', peer_gpu_id: '1' }, 1),
+      vec({ __name__: 'gpu_xgmi_link_hops', hostname: 'n0', gpu_id: '1', peer_gpu_id: '0' }, 1),
+    ];
+    const src = createMetricsSource({ request: prom({ data: d }) });
+    const m = await src.fetchGpuMetrics();
+    expect(m.links.n0).toEqual({ '0-1': { type: 'XGMI', hops: 1 }, '1-0': { type: 'XGMI', hops: 1 } });
+  });
   it('remembers the answering source and skips the other', async () => {
     const request = prom();
     const src = createMetricsSource({ request });
