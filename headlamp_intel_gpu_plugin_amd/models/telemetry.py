@@ -5,7 +5,8 @@ Two sources fill the TSDB, mirroring the two exporters the plugin reads
 
 * ``amd-exporter`` — AMD Device Metrics Exporter style ``gpu_*`` gauges keyed
   by ``hostname`` + ``gpu_id``, with ``pod``/``namespace`` labels on GPUs a
-  workload holds, and ``xgmi_neighbor_N_tx_throughput`` per link;
+  workload holds, ``xgmi_neighbor_N_tx_throughput`` per link and the
+  native exporter's ``gpu_xgmi_link_hops`` per peer;
 * ``node-exporter`` — ``node_hwmon_*`` (chip = PCI address, chip_name
   ``amdgpu``) and ``node_drm_*`` (card) series plus ``node_uname_info``.
 
@@ -121,6 +122,10 @@ def populate(db: TSDB, cluster: SyntheticCluster, source: str = "amd-exporter", 
                         return (0.55 + 0.3 * math.sin(t / 23.0 + lph)) * XGMI_LINK_GBS * 1e9 if active else 0.0
 
                     db.add(Series(dict(base, __name__=f"xgmi_neighbor_{k}_tx_throughput"), fn=xgmi, interval=interval))
+                    # Link hop count as the framework's amdgpu-exporter reports it
+                    # (ops/csrc/probe_core.h): one hop to every peer on the mesh.
+                    db.add(Series(dict(base, __name__="gpu_xgmi_link_hops", peer_gpu_id=str(peer)),
+                                  fn=lambda t: 1.0, interval=interval))
             else:
                 chip = pci_address(i, g)
                 inst = f"{instance}:9100"
