@@ -27,7 +27,7 @@ import hashlib
 from typing import Dict, List, Optional
 
 GPUS_PER_NODE = 8
-HBM_BYTES = 288 * 2**30  # 288 GiB (device reports 309,220,868,096 B)
+HBM_BYTES = 294896 * 2**20  # 288 GiB less 16 MiB, as the device reports it (309,220,868,096 B)
 OPERATOR_NS = "kube-amd-gpu"
 NFD_LABEL = "feature.node.kubernetes.io/amd-gpu"
 EPOCH = _dt.datetime(2026, 10, 1, tzinfo=_dt.timezone.utc)

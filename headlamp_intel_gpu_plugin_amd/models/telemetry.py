@@ -99,7 +99,8 @@ def populate(db: TSDB, cluster: SyntheticCluster, source: str = "amd-exporter", 
                 base = {"hostname": node, "gpu_id": str(g), "instance": f"{instance}:5000", "job": "amd-metrics-exporter",
                         "card_model": "AMD Instinct MI355X", "serial_number": f"MI355X{i:03d}{g}"}
                 own = {"pod": owner[1], "namespace": owner[0]} if owner else {}
-                for name, fn, extra in (("gpu_power_usage", power, own), ("gpu_gfx_activity", gfx, {}),
+                for name, fn, extra in (("gpu_power_usage", power, own), ("gpu_power_cap", lambda t: BOARD_POWER_W, {}),
+                                        ("gpu_gfx_activity", gfx, {}),
                                         ("gpu_used_vram", vram_mib, {}),
                                         ("gpu_total_vram", lambda t: HBM_BYTES / MIB, {}),
                                         ("gpu_umc_activity", umc, {}), ("gpu_junction_temperature", temp, {})):

@@ -60,8 +60,9 @@ PyObject* py_device_info(PyObject*, PyObject* args) {
   DeviceInfo i;
   if (!device_info(dev, &i)) return raise_hip();
   return Py_BuildValue(
-      "{s:i,s:s,s:s,s:s,s:s,s:K,s:i,s:i,s:K,s:i,s:i,s:i,s:i}", "index", i.index, "name", i.name.c_str(), "arch",
-      i.arch.c_str(), "bdf", i.bdf.c_str(), "uuid", i.uuid.c_str(), "hbm_bytes",
+      "{s:i,s:s,s:s,s:s,s:s,s:s,s:s,s:K,s:i,s:i,s:K,s:i,s:i,s:i,s:i}", "index", i.index, "name", i.name.c_str(), "arch",
+      i.arch.c_str(), "bdf", i.bdf.c_str(), "uuid", i.uuid.c_str(), "serial", i.serial.c_str(), "device_id",
+      i.device_id.c_str(), "hbm_bytes",
       static_cast<unsigned long long>(i.hbm_bytes), "compute_units", i.compute_units, "wavefront", i.wavefront,
       "lds_per_cu", static_cast<unsigned long long>(i.lds_per_cu), "l2_bytes", i.l2_bytes, "clock_khz", i.clock_khz,
       "mem_clock_khz", i.mem_clock_khz, "mem_bus_width", i.mem_bus_width);
@@ -113,6 +114,13 @@ PyObject* py_sample(PyObject*, PyObject* args) {
   put("mem_busy_pct", s.mem_busy_pct);
   put("vram_used_b", s.vram_used_b);
   put("vram_total_b", s.vram_total_b);
+  auto put_str = [&](const char* k, const std::string& v) {
+    PyObject* o = v.empty() ? (Py_INCREF(Py_None), Py_None) : PyUnicode_FromString(v.c_str());
+    PyDict_SetItemString(d, k, o);
+    Py_DECREF(o);
+  };
+  put_str("compute_partition", s.compute_partition);
+  put_str("memory_partition", s.memory_partition);
   return d;
 }
 

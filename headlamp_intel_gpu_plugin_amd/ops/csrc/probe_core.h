@@ -31,7 +31,9 @@ struct DeviceInfo {
   std::string name;
   std::string arch;
   std::string bdf;  // "0000:05:00.0"
-  std::string uuid;
+  std::string uuid;    // 32 hex digits of the 16 raw uuid bytes
+  std::string serial;  // ASIC serial (amd-smi asic_serial without "0x")
+  std::string device_id;  // PCI device id, e.g. "0x75a3"
   size_t hbm_bytes = 0;
   int compute_units = 0;
   int wavefront = 0;
@@ -43,6 +45,12 @@ struct DeviceInfo {
   int pci_domain = 0, pci_bus = 0, pci_device = 0;
 };
 
+// PCI device ids confirmed on hardware (amd-smi static, tests/fixtures/mi355x).
+inline const char* product_for_device_id(const std::string& id) {
+  if (id == "0x75a3") return "AMD Instinct MI355X";
+  return nullptr;
+}
+
 struct Sample {
   double power_w = NAN;      // average (or instantaneous) board power
   double power_cap_w = NAN;  // power1_cap
@@ -50,6 +58,7 @@ struct Sample {
   double sclk_mhz = NAN, mclk_mhz = NAN;
   double gfx_busy_pct = NAN, mem_busy_pct = NAN;
   double vram_used_b = NAN, vram_total_b = NAN;
+  std::string compute_partition, memory_partition;  // "SPX"/"CPX", "NPS1"/"NPS4"
 };
 
 inline bool g_hip_ok = false;
@@ -138,6 +147,31 @@ inline bool device_info(int dev, DeviceInfo* out) {
   char hex[40] = {0};
   for (int i = 0; i < 16; ++i) std::snprintf(hex + 2 * i, 3, "%02x", static_cast<unsigned char>(p.uuid.bytes[i]));
   out->uuid = hex;
+  // ROCm fills the uuid with the ASIC serial as ASCII hex digits (an MI355X
+  // reads "cc63d7a5..." where amd-smi prints asic_serial 0xCC63D7A5...).
+  out->serial.clear();
+  for (int i = 0; i < 16; ++i) {
+    const char c = p.uuid.bytes[i];
+    if (c == 0) break;
+    if (!std::isxdigit(static_cast<unsigned char>(c))) {
+      out->serial.clear();
+      break;
+    }
+    out->serial.push_back(static_cast<char>(std::toupper(static_cast<unsigned char>(c))));
+  }
+  if (out->serial.empty()) out->serial = out->uuid;
+  const std::string dir = "/sys/bus/pci/devices/" + out->bdf;
+  std::string s;
+  if (read_text(dir + "/device", &s)) out->device_id = s;
+  // The HIP device name is empty or generic on some ROCm builds: prefer the
+  // board's product name, then the device-id table.
+  if (read_text(dir + "/product_name", &s) && !s.empty()) {
+    out->name = s;
+  } else if (const char* prod = product_for_device_id(out->device_id)) {
+    out->name = prod;
+  } else if (out->name.empty() || out->name == "AMD Radeon Graphics") {
+    out->name = "AMD Instinct (" + (out->device_id.empty() ? out->arch : out->device_id) + ")";
+  }
   return true;
 }
 
@@ -149,6 +183,8 @@ inline Sample sample_sysfs(const std::string& bdf) {
   if (read_double(dir + "/mem_busy_percent", &v)) s.mem_busy_pct = v;
   if (read_double(dir + "/mem_info_vram_used", &v)) s.vram_used_b = v;
   if (read_double(dir + "/mem_info_vram_total", &v)) s.vram_total_b = v;
+  read_text(dir + "/current_compute_partition", &s.compute_partition);
+  read_text(dir + "/current_memory_partition", &s.memory_partition);
   for (const auto& h : hwmon_dirs(dir)) {
     // power: µW
     if (std::isnan(s.power_w) && read_double(h + "/power1_average", &v)) s.power_w = v / 1e6;
@@ -218,6 +254,7 @@ inline std::string render(const RenderOptions& opt) {
       {"gpu_memory_clock", "memory clock (MHz)"},
       {"gpu_power_cap", "board power cap (W)"},
       {"gpu_xgmi_link_hops", "hops between two GPUs over xGMI (absent when not xGMI-connected)"},
+      {"gpu_partition_info", "compute/memory partition mode of the GPU (value is always 1)"},
   };
   for (auto& h : kHelp) {
     out.append("# HELP ").append(h[0]).append(" ").append(h[1]).append("\n");
@@ -232,7 +269,7 @@ inline std::string render(const RenderOptions& opt) {
     const std::string gid = (opt.only_device >= 0 && !opt.gpu_label.empty()) ? opt.gpu_label : std::to_string(d);
     std::string labels = "hostname=\"" + escape_label(opt.hostname) + "\",gpu_id=\"" + escape_label(gid) +
                          "\",card_model=\"" + escape_label(info.name) + "\",pci_bus=\"" + info.bdf +
-                         "\",serial_number=\"" + info.uuid + "\"";
+                         "\",serial_number=\"" + escape_label(info.serial) + "\"";
     append_metric(&out, "gpu_power_usage", labels, s.power_w);
     append_metric(&out, "gpu_power_cap", labels, s.power_cap_w);
     append_metric(&out, "gpu_gfx_activity", labels, s.gfx_busy_pct);
@@ -245,6 +282,12 @@ inline std::string render(const RenderOptions& opt) {
     append_metric(&out, "gpu_memory_temperature", labels, s.temp_mem_c);
     append_metric(&out, "gpu_clock", labels, s.sclk_mhz);
     append_metric(&out, "gpu_memory_clock", labels, s.mclk_mhz);
+    if (!s.compute_partition.empty() || !s.memory_partition.empty()) {
+      append_metric(&out, "gpu_partition_info",
+                    labels + ",compute_partition=\"" + escape_label(s.compute_partition) + "\",memory_partition=\"" +
+                        escape_label(s.memory_partition) + "\"",
+                    1.0);
+    }
   }
   if (opt.topology && opt.only_device < 0) {
     for (int a = 0; a < g_count; ++a) {

@@ -94,7 +94,7 @@ export const MI355X = Object.freeze({
   product: 'AMD Instinct MI355X',
   shortName: 'MI355X',
   arch: 'gfx950 (CDNA4)',
-  hbmBytes: 288 * 1024 * 1024 * 1024, // 288 GiB: the device reports 309,220,868,096 B usable
+  hbmBytes: 294896 * 1024 * 1024, // 288 GiB HBM3E less 16 MiB: what the device reports (amd-smi total_vram 294896 MB)
   hbmLabel: '288 GB HBM3E',
   hbmPeakTBs: 8.0,
   computeUnits: 256,
@@ -342,6 +342,23 @@ export function labellerValue(node, prop) {
 }
 
 /**
+ * PCI device ids → short product name. Only ids confirmed on hardware are
+ * listed: 0x75a3 is what amd-smi reports for an MI355X (market name
+ * "AMD Instinct MI355 OAM", IFWI "AMD MI355X"; tests/fixtures/mi355x).
+ */
+export const GPU_DEVICE_IDS = Object.freeze({ '75a3': 'MI355X' });
+
+/** Short product name from a device id ("0x75a3") or a product string ("AMD_Instinct_MI355X"). */
+export function shortProductName(deviceId, product) {
+  if (deviceId) {
+    const id = String(deviceId).toLowerCase().replace(/^0x/, '');
+    if (GPU_DEVICE_IDS[id]) return GPU_DEVICE_IDS[id];
+  }
+  const m = product ? /MI\d{3}[A-Z]*/i.exec(String(product)) : null;
+  return m ? m[0].toUpperCase() : MI355X.shortName;
+}
+
+/**
  * Product model of the node's GPUs. Replaces the reference's
  * discrete/integrated "GPU type" (k8s.ts:183-203): every GPU this plugin
  * targets is an MI355X, so the interesting fact is the product and its
@@ -355,9 +372,10 @@ export function getNodeGpuModel(node) {
   const mp = labels[LABEL_MEMORY_PARTITION] || labellerValue(node, 'memory-partitioning-mode');
   const vram = labellerValue(node, 'vram');
   const cu = labellerValue(node, 'cu-count');
+  const deviceId = labellerValue(node, 'device-id');
   return {
     product: productLabel ? String(productLabel).replace(/_/g, ' ') : MI355X.product,
-    shortName: MI355X.shortName,
+    shortName: shortProductName(deviceId, productLabel),
     fromLabels: !!productLabel,
     computePartition: cp ? String(cp).toUpperCase() : null,
     memoryPartition: mp ? String(mp).toUpperCase() : null,
@@ -762,8 +780,11 @@ export function formatBytes(b) {
     v /= 1024;
     u++;
   }
-  const digits = v >= 100 || u === 0 ? 0 : 1;
-  return v.toFixed(digits) + ' ' + units[u];
+  // Three significant digits, trailing zeros dropped: "288 GiB", "2.25 TiB", "4.5 TiB".
+  const digits = v >= 100 || u === 0 ? 0 : v >= 10 ? 1 : 2;
+  let t = v.toFixed(digits);
+  if (digits > 0) t = t.replace(/\.?0+$/, '');
+  return t + ' ' + units[u];
 }
 
 export function formatWatts(w) {

@@ -45,8 +45,9 @@ export function servicePath(svc) {
 export const SERIES = {
   exporter: {
     power: 'gpu_power_usage', // W
-    vramUsed: 'gpu_used_vram', // MiB (verify unit)
-    vramTotal: 'gpu_total_vram', // MiB
+    powerCap: 'gpu_power_cap', // W (board power cap; 1400 on MI355X)
+    vramUsed: 'gpu_used_vram', // MiB
+    vramTotal: 'gpu_total_vram', // MiB: an MI355X reads 294896 = 288 GiB (tests/fixtures/mi355x)
     gfx: 'gpu_gfx_activity', // %
     umc: 'gpu_umc_activity', // % — HBM controller busy
     temp: 'gpu_junction_temperature', // °C
@@ -139,6 +140,7 @@ export function joinExporterResults(r) {
       g.namespace = m.namespace || null;
     }
   });
+  each(r[E.powerCap], function (g, v) { if (v !== null && v > 0) g.powerCapWatts = v; });
   each(r[E.vramUsed], function (g, v) { g.vramUsedBytes = v === null ? null : v * SERIES.exporterVramUnitBytes; });
   each(r[E.vramTotal], function (g, v) { g.vramTotalBytes = v === null ? null : v * SERIES.exporterVramUnitBytes; });
   each(r[E.gfx], function (g, v) { g.gfxActivityPct = v; });
@@ -245,7 +247,8 @@ export function joinNodeExporterResults(r) {
  */
 export function exporterQuery() {
   const E = SERIES.exporter;
-  return '{__name__=~"' + [E.power, E.vramUsed, E.vramTotal, E.gfx, E.umc, E.temp, E.xgmiRe, E.linkHops].join('|') + '"}';
+  const names = [E.power, E.powerCap, E.vramUsed, E.vramTotal, E.gfx, E.umc, E.temp, E.xgmiRe, E.linkHops];
+  return '{__name__=~"' + names.join('|') + '"}';
 }
 
 export function nodeExporterQuery() {

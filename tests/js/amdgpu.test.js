@@ -19,6 +19,7 @@ import {
   formatAge,
   formatBytes,
   formatGpuModel,
+  shortProductName,
   formatGpuResourceName,
   formatPercent,
   formatPodGpuRequests,
@@ -62,7 +63,8 @@ describe('constants', () => {
     expect(AMD_GPU_RESOURCE).toBe('amd.com/gpu');
   });
   it('describes an MI355X with 288 GB HBM and an 8-GPU xGMI mesh', () => {
-    expect(MI355X.hbmBytes).toBe(288 * 1024 * 1024 * 1024);
+    expect(MI355X.hbmBytes).toBe(294896 * 1024 * 1024); // device-reported: tests/fixtures/mi355x
+    expect(formatBytes(MI355X.hbmBytes)).toBe('288 GiB');
     expect(MI355X.gpusPerNode).toBe(8);
     expect(MI355X.xgmiLinksPerGpu).toBe(MI355X.gpusPerNode - 1);
     expect(MI355X.computeUnits).toBe(256);
@@ -171,6 +173,21 @@ describe('GPU model', () => {
   });
   it('formats partitioned nodes with their modes', () => {
     expect(formatGpuModel(getNodeGpuModel(makeGpuNode('g', { partition: 'cpx/nps4' })))).toBe('MI355X (CPX/NPS4)');
+  });
+  it('names the product from the device id amd-smi reports for MI355X', () => {
+    // tests/fixtures/mi355x/amd_smi_static.json: device_id 0x75a3, market name "AMD Instinct MI355 OAM"
+    expect(shortProductName('0x75a3', 'AMD Instinct MI355 OAM')).toBe('MI355X');
+    expect(shortProductName('75A3', null)).toBe('MI355X');
+  });
+  it('falls back to the product string, then to MI355X', () => {
+    expect(shortProductName(null, 'AMD_Instinct_MI300X')).toBe('MI300X');
+    expect(shortProductName('74b5', 'AMD_Instinct_MI300X')).toBe('MI300X');
+    expect(shortProductName(null, null)).toBe('MI355X');
+  });
+  it('uses the labeller product for a non-MI355X node', () => {
+    const n = makeGpuNode('g');
+    n.metadata.labels['amd.com/gpu.product-name'] = 'AMD_Instinct_MI325X';
+    expect(formatGpuModel(getNodeGpuModel(n))).toBe('MI325X');
   });
 });
 
@@ -408,7 +425,7 @@ describe('formatters', () => {
   });
   it('formatBytes uses decimal units', () => {
     expect(formatBytes(288 * 1024 ** 3)).toBe('288 GiB');
-    expect(formatBytes(8 * 288 * 1024 ** 3)).toBe('2.3 TiB');
+    expect(formatBytes(8 * 288 * 1024 ** 3)).toBe('2.25 TiB');
     expect(formatBytes(512)).toBe('512 B');
     expect(formatBytes(null)).toBe('—');
   });

@@ -1,0 +1,65 @@
+/**
+ * Real MI355X captures (tests/fixtures/mi355x, taken on a GPU box with
+ * tools/capture_box.sh, serials scrubbed) run through the metrics client's
+ * join — the exporter schema the plugin assumes, checked against hardware
+ * rather than against our own synthetic telemetry.
+ */
+import fs from 'fs';
+import path from 'path';
+import { SERIES, joinExporterResults, splitByName } from '../../src/api/metrics.js';
+import { MI355X, formatBytes, shortProductName } from '../../src/api/amdgpu.js';
+
+const DIR = path.join(process.cwd(), 'tests', 'fixtures', 'mi355x');
+
+/** Prometheus text exposition → instant-vector rows, as /api/v1/query returns them. */
+function parseExposition(text) {
+  const rows = [];
+  text.split('\n').forEach((line) => {
+    if (!line || line[0] === '#') return;
+    const m = /^([a-zA-Z_:][a-zA-Z0-9_:]*)(\{(.*)\})?\s+(\S+)$/.exec(line);
+    if (!m) return;
+    const metric = { __name__: m[1] };
+    const re = /([a-zA-Z_][a-zA-Z0-9_]*)="((?:[^"\\]|\\.)*)"/g;
+    let l;
+    while ((l = re.exec(m[3] || '')) !== null) metric[l[1]] = l[2];
+    rows.push({ metric, value: [1760000000, m[4]] });
+  });
+  return rows;
+}
+
+function load(name) {
+  return fs.readFileSync(path.join(DIR, name), 'utf8');
+}
+
+describe('MI355X hardware fixtures', () => {
+  const rows = parseExposition(load('exporter_once.prom'));
+  const smiStatic = JSON.parse(load('amd_smi_static.json')).gpu_data[0];
+  const smiMetric = JSON.parse(load('amd_smi_metric.json')).gpu_data[0];
+
+  it('the real exporter scrape carries every per-GPU series the plugin reads', () => {
+    const names = rows.map((r) => r.metric.__name__);
+    const E = SERIES.exporter;
+    [E.power, E.powerCap, E.vramUsed, E.vramTotal, E.gfx, E.umc, E.temp].forEach((n) => expect(names).toContain(n));
+  });
+
+  it('joins into one GPU with the board facts amd-smi reports', () => {
+    const j = joinExporterResults(splitByName(rows));
+    expect(j.gpus).toHaveLength(1);
+    const g = j.gpus[0];
+    expect(g.nodeName).toBe('mi355x-node-0');
+    expect(g.vramTotalBytes).toBe(smiMetric.mem_usage.total_vram.value * 1024 * 1024);
+    expect(g.vramTotalBytes).toBe(MI355X.hbmBytes);
+    expect(formatBytes(g.vramTotalBytes)).toBe('288 GiB');
+    expect(g.powerCapWatts).toBe(smiStatic.limit.ppt0.max_power_limit.value);
+    expect(g.powerCapWatts).toBe(MI355X.tdpWatts);
+    expect(g.tempC).toBe(smiMetric.temperature.hotspot.value);
+    expect(Math.abs(g.powerWatts - smiMetric.power.socket_power.value)).toBeLessThan(30);
+  });
+
+  it('amd-smi identifies the board the way the node model expects', () => {
+    expect(smiStatic.asic.target_graphics_version).toBe('gfx950');
+    expect(smiStatic.asic.num_compute_units).toBe(MI355X.computeUnits);
+    expect(shortProductName(smiStatic.asic.device_id, smiStatic.asic.market_name)).toBe('MI355X');
+    expect(smiStatic.vram.type).toBe('HBM3E');
+  });
+});

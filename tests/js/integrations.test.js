@@ -31,7 +31,7 @@ describe('nodeDetailView', () => {
     expect(rowValue(s, 'GPU (capacity)')).toBe('8');
     expect(rowValue(s, 'GPU (allocatable)')).toBe('8');
     expect(rowValue(s, 'GPU Model')).toBe('AMD Instinct MI355X');
-    expect(rowValue(s, 'HBM')).toBe('2.3 TiB');
+    expect(rowValue(s, 'HBM')).toBe('2.25 TiB');
   });
   it('computes allocation from pods on this node with threshold status', () => {
     const s = nodeDetailView(node, ctx);
@@ -135,7 +135,7 @@ describe('nodeColumns', () => {
   it('counts devices and HBM from KubeObject wrappers', () => {
     const w = { jsonData: makeGpuNode('g', { gpus: 4 }) };
     expect(cols[1].getter(w)).toBe('4');
-    expect(cols[2].getter(w)).toBe('1.1 TiB');
+    expect(cols[2].getter(w)).toBe('1.12 TiB');
   });
   it('shows — devices for label-only nodes', () => {
     expect(cols[1].getter(makeGpuNode('g', { capacity: false }))).toBe('—');

@@ -216,7 +216,7 @@ describe('fetchGpuMetrics', () => {
     await src.fetchGpuMetrics();
     const qs = request.mock.calls.map((c) => decodeURIComponent(c[0])).filter((p) => p.indexOf('query=1') < 0);
     expect(qs).toHaveLength(2);
-    expect(qs[0]).toContain('gpu_power_usage|gpu_used_vram');
+    expect(qs[0]).toContain('gpu_power_usage|gpu_power_cap|gpu_used_vram');
     expect(qs[1]).toContain('node_hwmon_chip_names|node_hwmon_power_average_watt');
   });
   it('returns an empty GPU list when Prometheus has no AMD series', async () => {

@@ -211,7 +211,7 @@ describe('nodesView', () => {
     const ctx = makeContext({ nodes: [makeGpuNode('g0')], pods: [makeGpuPod('a', { node: 'g0', gpus: 2 })] });
     const s = findSection(nodesView(ctx, opts), 'g0');
     expect(rowValue(s, 'GPU Devices (amd.com/gpu)')).toBe('8');
-    expect(rowValue(s, 'HBM')).toBe('2.3 TiB (8 × 288G)');
+    expect(rowValue(s, 'HBM')).toBe('2.25 TiB (8 × 288G)');
     expect(rowValue(s, 'GPU Workload Pods')).toBe('a');
     expect(rowValue(s, 'GPU (capacity)')).toBe('8');
     expect(rowValue(s, 'Kubelet')).toBe('v1.31.2');

@@ -4,6 +4,7 @@ CPU tests run the binary with no GPU (it must still answer, with no GPU series);
 the GPU test checks real MI355X series and the single-device relabelling mode.
 """
 import os
+import re
 import shutil
 import signal
 import subprocess
@@ -79,6 +80,13 @@ def test_exporter_reports_mi355x(exe):
     assert {"gpu_total_vram", "gpu_power_usage"} <= names, names
     total = [v for n, l, v in rows if n == "gpu_total_vram" and l["gpu_id"] == "0"][0]
     assert 280e9 / 2**20 < total <= 288 * 1024
+    labels = [l for n, l, _ in rows if n == "gpu_power_usage" and l["gpu_id"] == "0"][0]
+    # HIP's device name is empty on this ROCm; the probe names the board from sysfs / device id.
+    assert labels["card_model"] == "AMD Instinct MI355X", labels
+    assert re.fullmatch(r"[0-9A-F]{16}", labels["serial_number"]), labels
+    part = [l for n, l, _ in rows if n == "gpu_partition_info"]
+    assert part and part[0]["compute_partition"] in {"SPX", "DPX", "QPX", "CPX"}, part
+    assert part[0]["memory_partition"] in {"NPS1", "NPS2", "NPS4", "NPS8"}, part
     one = subprocess.run([exe, "--once", "--hostname", "n0", "--device", "0", "--gpu-label", "7"],
                          capture_output=True, text=True, timeout=60)
     ids = {l["gpu_id"] for n, l, _ in parse_exposition(one.stdout)}

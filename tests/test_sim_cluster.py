@@ -91,7 +91,7 @@ def test_exporter_telemetry_series_counts():
     c = SyntheticCluster(spec_for_nodes(2))
     db = promql.TSDB()
     n = populate(db, c, source="amd-exporter")
-    assert n == 2 * 8 * (6 + 7 + 7)  # 6 gauges + 7 xGMI throughput + 7 link-hop series per GPU
+    assert n == 2 * 8 * (7 + 7 + 7)  # 7 gauges + 7 xGMI throughput + 7 link-hop series per GPU
 
 
 def test_busy_gpus_draw_more_power_and_carry_pod_labels():
