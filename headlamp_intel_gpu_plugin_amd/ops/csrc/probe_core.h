@@ -163,12 +163,13 @@ inline bool device_info(int dev, DeviceInfo* out) {
   const std::string dir = "/sys/bus/pci/devices/" + out->bdf;
   std::string s;
   if (read_text(dir + "/device", &s)) out->device_id = s;
-  // The HIP device name is empty or generic on some ROCm builds: prefer the
-  // board's product name, then the device-id table.
-  if (read_text(dir + "/product_name", &s) && !s.empty()) {
-    out->name = s;
-  } else if (const char* prod = product_for_device_id(out->device_id)) {
+  // The HIP device name is empty or generic on some ROCm builds. Prefer the
+  // product name of a known device id ("AMD Instinct MI355X"), then the
+  // board's FRU name (an MI355X reads "AMD Instinct MI355 OAM").
+  if (const char* prod = product_for_device_id(out->device_id)) {
     out->name = prod;
+  } else if (read_text(dir + "/product_name", &s) && !s.empty()) {
+    out->name = s;
   } else if (out->name.empty() || out->name == "AMD Radeon Graphics") {
     out->name = "AMD Instinct (" + (out->device_id.empty() ? out->arch : out->device_id) + ")";
   }

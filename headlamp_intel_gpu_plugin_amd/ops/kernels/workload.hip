@@ -6,24 +6,26 @@
 // HBM. Two kernels, written for CDNA4 directly:
 //
 //   gemm_bf16_nt  C[M,N] = A[M,K] · B[N,K]ᵀ, bf16 in, fp32 accumulate on
-//                 MFMA (v_mfma_f32_16x16x32_bf16), bf16 out (RNE).
-//                 Two instantiations of one template:
-//                   256×256×64 tile, 8 wave64s as 2×4, each wave a 128×64
-//                   sub-tile (8×4 MFMA tiles), 144 KiB of LDS → 1 block/CU —
-//                   used when M and N are multiples of 256;
-//                   128×128×64 tile, 4 wave64s as 2×2 (64×64 each), 72 KiB.
-//                 A/B staged global→LDS with 16-byte vector loads into a double
-//                 buffer (one barrier per K-step: tile k+1 is fetched into
-//                 registers while tile k is consumed, then written to the
-//                 other buffer); LDS rows padded to 144 B so the 16 lanes of a
-//                 ds_read_b128 group hit 16 distinct 4-bank slots; each MFMA
-//                 cluster runs at s_setprio 1 (keeps hipcc from moving MFMAs
-//                 into the load phase, guide T5); bijective XCD-aware block
-//                 remap + 8-row tile grouping so blocks sharing an XCD's L2
-//                 work on neighbouring tiles. Measured on MI355X (random
-//                 [-1,1) operands, tools/microbench/gemm_variants.hip):
-//                 256² tile 1177 TFLOP/s at 8192³, 1025 at 4096³; 128² tile
-//                 888–950 at 8192³.
+//                 MFMA (v_mfma_f32_16x16x32_bf16), bf16 out (RNE). Three
+//                 kernels, picked by shape (or forced with `variant`):
+//                   gemm_bf16_nt_8ph — 256×256×64 tile, 8 wave64s, operands
+//                   staged by LDS-DMA (global_load_lds_dwordx4) with a
+//                   source-side XOR swizzle, 8-phase ping-pong schedule with
+//                   three half-tiles in flight (design notes above the
+//                   kernel). Used when M,N % 256 == 0, K % 128 == 0 and the
+//                   grid has ≥ 128 blocks: 1483 TFLOP/s at 8192³ on random
+//                   operands (profiles/r1_gemm_ab.json);
+//                   gemm_bf16_nt<256,256,2,4> — same tile, register-staged
+//                   double buffer (1121 TFLOP/s), for K % 128 == 64;
+//                   gemm_bf16_nt<128,128,2,2> — 4 waves, 64×64 per wave,
+//                   for shapes the 256² tiles do not cover or fill.
+//                 The register-staged kernels fetch tile k+1 into registers
+//                 while tile k is consumed, write it to the other LDS buffer
+//                 (rows padded to 144 B: conflict-free ds_read_b128), one
+//                 barrier per K-step. All three run each MFMA cluster at
+//                 s_setprio 1 and use a bijective XCD-aware block remap with
+//                 8-row tile grouping so blocks sharing an XCD's L2 work on
+//                 neighbouring tiles.
 //   stream_triad  c = a + s·b over fp32, 16-byte accesses, one pass with 4
 //                 vectors per thread and non-temporal stores: 5.78 TB/s.
 //
@@ -190,6 +192,212 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_nt(const uint16_t* __r
       }
 }
 
+// ---------------------------------------------------------------------------
+// gemm_bf16_nt_8ph: 256×256×64 tile, LDS-DMA staging, 8-phase ping-pong.
+//
+// Same C = A·Bᵀ contract as gemm_bf16_nt, restructured around what gfx950
+// rewards at one 512-thread block per CU (cdna_hip_programming.md §5, "The
+// 256² 8-phase template"):
+//   * operands go global → LDS with global_load_lds_dwordx4 (no VGPR staging,
+//     no ds_write pass); the LDS image is lane-linear, so the bank swizzle is
+//     applied to the per-lane SOURCE address and undone on the ds_read:
+//     16-byte chunk c of row r lives at chunk c ^ (r & 7), which makes every
+//     ds_read_b128 lane group hit 16 distinct 16-byte slots (conflict-free);
+//   * LDS holds two K-tiles (128 KiB), each as four 16 KiB half-tiles:
+//     A0/A1 = the first/second 64-row subtile of both wave rows, B0/B1 = the
+//     first/second 32-column subtile of all four wave columns. A phase
+//     computes one 64×32 quadrant of each wave's 128×64 output (16 MFMAs)
+//     and issues one half-tile of prefetch, so 8 phases cover 2 K-tiles;
+//   * three half-tiles stay in flight across barriers: a counted
+//     `s_waitcnt vmcnt(6)` at phases 4 and 8 (never 0 in the loop) and raw
+//     s_barrier instead of __syncthreads (whose fence would drain vmcnt);
+//   * the two wave rows run one barrier apart (wave row 1 takes an extra
+//     barrier up front, row 0 one at the end), so on each SIMD one wave
+//     issues ds_reads while its partner runs MFMAs.
+// Staging order (half-tile written → phase), chosen so every buffer is
+// rewritten only after all its readers retired their ds_reads (B reads are
+// retired before the phase's first barrier by lgkmcnt(8)) and read only after
+// a vmcnt wait plus a barrier:
+//   even buffer (read phases 1-3): B0@2 A0@3 B1@4 A1@5 (next even K-tile)
+//   odd  buffer (read phases 5-7): B0@6 A0@7 B1@8 A1@1 (next odd K-tile)
+// Staging past the last K-tile reloads the last tile into a buffer that is
+// never read again, keeping every wave's vmcnt arithmetic identical.
+// ---------------------------------------------------------------------------
+
+constexpr int P8_THREADS = 512;
+constexpr int P8_HALF = 128 * 128;       // bytes per half-tile (128 rows × 64 bf16)
+constexpr int P8_BUF = 4 * P8_HALF;      // one K-tile: A0 A1 B0 B1
+constexpr int P8_LDS = 2 * P8_BUF;       // 128 KiB
+enum { kA0 = 0, kA1 = 1, kB0 = 2, kB1 = 3 };
+
+// Row of the 256-row operand tile held by LDS row `r` (0..127) of half-tile `kind`.
+__device__ __forceinline__ int p8_src_row(int kind, int r) {
+  return kind < 2 ? (r >> 6) * 128 + (kind & 1) * 64 + (r & 63)   // A: wave row r/64, subtile kind
+                  : (r >> 5) * 64 + (kind & 1) * 32 + (r & 31);   // B: wave col r/32, subtile kind-2
+}
+
+__global__ __launch_bounds__(P8_THREADS) void gemm_bf16_nt_8ph(const uint16_t* __restrict__ A,
+                                                              const uint16_t* __restrict__ B,
+                                                              uint16_t* __restrict__ C, int M, int N, int K) {
+  extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
+
+  const int tiles_m = M / 256;
+  const int tiles_n = N / 256;
+  const int wg = xcd_remap(static_cast<int>(blockIdx.x), tiles_m * tiles_n);
+  const int span = 8 * tiles_n;
+  const int first_m = (wg / span) * 8;
+  const int rows_in_group = min(8, tiles_m - first_m);
+  const int m0 = (first_m + (wg % span) % rows_in_group) * 256;
+  const int n0 = ((wg % span) / rows_in_group) * 256;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 2;  // 2 wave rows × 4 wave columns
+  const int wc = wave & 3;
+  const int nk = K / 64;
+
+  // Staging: this wave writes LDS rows [16·wave, 16·wave+16) of every
+  // half-tile with two 1 KiB glds; lane l covers row 16·wave + 8s + l/8,
+  // physical chunk l%8, loaded from logical chunk (l%8) ^ (row & 7).
+  uint32_t src_off[4][2];  // element offset of this lane's 16 B at k = 0
+#pragma unroll
+  for (int kind = 0; kind < 4; ++kind)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int r = wave * 16 + s * 8 + (lane >> 3);
+      const int chunk = (lane & 7) ^ (r & 7);
+      const int grow = (kind < 2 ? m0 : n0) + p8_src_row(kind, r);
+      src_off[kind][s] = static_cast<uint32_t>(grow) * static_cast<uint32_t>(K) + chunk * 8;
+    }
+
+#define P8_STAGE(kind, buf, ktile)                                                                         \
+  {                                                                                                        \
+    const int kt_ = min((ktile), nk - 1);                                                                  \
+    const uint16_t* base_ = (kind) < 2 ? A : B;                                                            \
+    _Pragma("unroll") for (int s = 0; s < 2; ++s) {                                                        \
+      __builtin_amdgcn_global_load_lds(                                                                    \
+          (__attribute__((address_space(1))) void*)(base_ + src_off[kind][s] + kt_ * 64),                  \
+          (__attribute__((address_space(3))) void*)(                                                       \
+              smem + (buf) * P8_BUF + (kind) * P8_HALF + (wave * 16 + s * 8) * 128),                        \
+          16, 0, 0);                                                                                       \
+    }                                                                                                      \
+  }
+
+  // Fragment reads: lane l takes row l&15 of a 16-row group, k-chunk
+  // (l>>4) + 4·ks, through the same XOR (row & 7 == frow & 7).
+  const int frow = lane & 15;
+  const int rd0 = (((lane >> 4)) ^ (frow & 7)) * 16;  // byte offset of ks = 0; ks = 1 is rd0 ^ 64
+  const int a_row = wr * 64 + frow;                    // LDS row within an A half-tile
+  const int b_row = wc * 32 + frow;                    // … within a B half-tile
+
+  bf16x8 af[8];     // A fragments of one 64-row subtile: [mt*2 + ks]
+  bf16x8 bq[2][4];  // B fragments of both 32-col subtiles: [nh][nt*2 + ks]
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#define P8_READ_A(buf, mh)                                                                                 \
+  {                                                                                                        \
+    const unsigned char* h_ = smem + (buf) * P8_BUF + (mh) * P8_HALF;                                       \
+    _Pragma("unroll") for (int mt = 0; mt < 4; ++mt) {                                                     \
+      const unsigned char* row_ = h_ + (a_row + mt * 16) * 128;                                            \
+      af[mt * 2 + 0] = *reinterpret_cast<const bf16x8*>(row_ + rd0);                                       \
+      af[mt * 2 + 1] = *reinterpret_cast<const bf16x8*>(row_ + (rd0 ^ 64));                                \
+    }                                                                                                      \
+  }
+#define P8_READ_B(buf, nh)                                                                                 \
+  {                                                                                                        \
+    const unsigned char* h_ = smem + (buf) * P8_BUF + (2 + (nh)) * P8_HALF;                                 \
+    _Pragma("unroll") for (int nt = 0; nt < 2; ++nt) {                                                     \
+      const unsigned char* row_ = h_ + (b_row + nt * 16) * 128;                                            \
+      bq[nh][nt * 2 + 0] = *reinterpret_cast<const bf16x8*>(row_ + rd0);                                   \
+      bq[nh][nt * 2 + 1] = *reinterpret_cast<const bf16x8*>(row_ + (rd0 ^ 64));                            \
+    }                                                                                                      \
+  }
+#define P8_MFMA(mh, nh)                                                                                    \
+  {                                                                                                        \
+    __builtin_amdgcn_s_setprio(1);                                                                         \
+    _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                                       \
+    _Pragma("unroll") for (int mt = 0; mt < 4; ++mt)                                                       \
+    _Pragma("unroll") for (int nt = 0; nt < 2; ++nt)                                                       \
+      acc[(mh) * 4 + mt][(nh) * 2 + nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(                         \
+          af[mt * 2 + ks], bq[nh][nt * 2 + ks], acc[(mh) * 4 + mt][(nh) * 2 + nt], 0, 0, 0);               \
+    __builtin_amdgcn_s_setprio(0);                                                                         \
+  }
+#define P8_SYNC_MFMA(mh, nh)                                                                               \
+  __builtin_amdgcn_s_barrier();                                                                            \
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                       \
+  __builtin_amdgcn_sched_barrier(0);                                                                       \
+  P8_MFMA(mh, nh)                                                                                          \
+  __builtin_amdgcn_s_barrier();
+
+  // Prologue: K-tile 0 → even buffer, then B0 A0 B1 of K-tile 1 → odd buffer;
+  // vmcnt(6) leaves those three half-tiles in flight and retires K-tile 0.
+  P8_STAGE(kB0, 0, 0) P8_STAGE(kA0, 0, 0) P8_STAGE(kB1, 0, 0) P8_STAGE(kA1, 0, 0)
+  P8_STAGE(kB0, 1, 1) P8_STAGE(kA0, 1, 1) P8_STAGE(kB1, 1, 1)
+  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger the wave rows by one barrier
+
+  for (int it = 0; it < nk / 2; ++it) {
+    const int kt = 2 * it;
+    // ---- even buffer: K-tile kt ----
+    P8_READ_B(0, 0)
+    __builtin_amdgcn_sched_barrier(0);
+    P8_READ_A(0, 0)
+    P8_STAGE(kA1, 1, kt + 1)
+    asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");  // retire the 4 B reads before the barrier
+    P8_SYNC_MFMA(0, 0)
+    P8_READ_B(0, 1)
+    P8_STAGE(kB0, 0, kt + 2)
+    P8_SYNC_MFMA(0, 1)
+    P8_READ_A(0, 1)
+    P8_STAGE(kA0, 0, kt + 2)
+    P8_SYNC_MFMA(1, 1)
+    P8_STAGE(kB1, 0, kt + 2)
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // odd buffer (K-tile kt+1) complete
+    P8_SYNC_MFMA(1, 0)
+    // ---- odd buffer: K-tile kt+1 ----
+    P8_READ_B(1, 0)
+    __builtin_amdgcn_sched_barrier(0);
+    P8_READ_A(1, 0)
+    P8_STAGE(kA1, 0, kt + 2)
+    asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+    P8_SYNC_MFMA(0, 0)
+    P8_READ_B(1, 1)
+    P8_STAGE(kB0, 1, kt + 3)
+    P8_SYNC_MFMA(0, 1)
+    P8_READ_A(1, 1)
+    P8_STAGE(kA0, 1, kt + 3)
+    P8_SYNC_MFMA(1, 1)
+    P8_STAGE(kB1, 1, kt + 3)
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // even buffer (K-tile kt+2) complete
+    P8_SYNC_MFMA(1, 0)
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the block
+  if (wr == 0) __builtin_amdgcn_s_barrier();        // balance the stagger barrier
+#undef P8_STAGE
+#undef P8_READ_A
+#undef P8_READ_B
+#undef P8_MFMA
+#undef P8_SYNC_MFMA
+
+  const int ccol = lane & 15;
+  const int crow = (lane >> 4) * 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wr * 128 + (i >> 2) * 64 + (i & 3) * 16 + crow + r;
+        const int col = n0 + wc * 64 + (j >> 1) * 32 + (j & 1) * 16 + ccol;
+        C[static_cast<size_t>(row) * N + col] = f32_to_bf16_rne(acc[i][j][r]);
+      }
+}
+
 // One pass, no grid-stride loop: each thread moves TRIAD_U 16-byte vectors,
 // all loads issued before any store (memory-level parallelism), and the
 // result is written non-temporally so it does not evict the operands from
@@ -221,6 +429,7 @@ using Big = GemmTile<256, 256, 2, 4>;
 using Small = GemmTile<128, 128, 2, 2>;
 bool g_big_attr = false;
 bool g_small_attr = false;
+bool g_8ph_attr = false;
 
 template <int BM, int BN, int WM, int WN>
 const char* launch_tile(const void* a, const void* b, void* c, int m, int n, int k, hipStream_t stream, bool* attr) {
@@ -239,12 +448,54 @@ const char* launch_tile(const void* a, const void* b, void* c, int m, int n, int
   return err == hipSuccess ? nullptr : hipGetErrorString(err);
 }
 
-const char* launch_gemm(const void* a, const void* b, void* c, int m, int n, int k, hipStream_t stream) {
+const char* launch_8ph(const void* a, const void* b, void* c, int m, int n, int k, hipStream_t stream) {
+  if (!g_8ph_attr) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_bf16_nt_8ph), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            P8_LDS) != hipSuccess)
+      return "gemm_bf16_nt_8ph: cannot reserve LDS";
+    g_8ph_attr = true;
+  }
+  hipLaunchKernelGGL(gemm_bf16_nt_8ph, dim3((m / 256) * (n / 256)), dim3(P8_THREADS), P8_LDS, stream,
+                     static_cast<const uint16_t*>(a), static_cast<const uint16_t*>(b), static_cast<uint16_t*>(c), m, n,
+                     k);
+  hipError_t err = hipGetLastError();
+  return err == hipSuccess ? nullptr : hipGetErrorString(err);
+}
+
+// Kernel variants: 0 = pick by shape, 1 = 128² register-staged, 2 = 256²
+// register-staged, 3 = 256² 8-phase LDS-DMA.
+enum { kAuto = 0, kTile128 = 1, kTile256 = 2, kTile256Dma = 3 };
+
+bool fits_8ph(int m, int n, int k) {
+  // 32-bit per-lane source offsets: every element index must fit in uint32.
+  return m % 256 == 0 && n % 256 == 0 && k % 128 == 0 &&
+         static_cast<uint64_t>(m) * k < (1ull << 32) && static_cast<uint64_t>(n) * k < (1ull << 32);
+}
+
+const char* launch_gemm(const void* a, const void* b, void* c, int m, int n, int k, hipStream_t stream,
+                        int variant = kAuto) {
   if (m <= 0 || n <= 0 || k <= 0 || m % 128 || n % 128 || k % BK) return "gemm_bf16_nt: M,N must be multiples of 128 and K of 64";
   if ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) return "gemm_bf16_nt: A and B must be 16-byte aligned";
-  // The 256² tile needs ≥ one block per CU to beat the 128² tile (256 CUs).
-  if (m % 256 == 0 && n % 256 == 0 && (m / 256) * (n / 256) >= 128)
+  const bool big = m % 256 == 0 && n % 256 == 0;
+  switch (variant) {
+    case kTile128:
+      return launch_tile<128, 128, 2, 2>(a, b, c, m, n, k, stream, &g_small_attr);
+    case kTile256:
+      if (!big) return "gemm_bf16_nt: the 256x256 tile needs M,N multiples of 256";
+      return launch_tile<256, 256, 2, 4>(a, b, c, m, n, k, stream, &g_big_attr);
+    case kTile256Dma:
+      if (!fits_8ph(m, n, k)) return "gemm_bf16_nt: the 8-phase tile needs M,N multiples of 256, K of 128, M*K and N*K < 2^32";
+      return launch_8ph(a, b, c, m, n, k, stream);
+    case kAuto:
+      break;
+    default:
+      return "gemm_bf16_nt: unknown variant";
+  }
+  // The 256² tiles need ≥ one block per CU to beat the 128² tile (256 CUs).
+  if (big && (m / 256) * (n / 256) >= 128) {
+    if (fits_8ph(m, n, k)) return launch_8ph(a, b, c, m, n, k, stream);
     return launch_tile<256, 256, 2, 4>(a, b, c, m, n, k, stream, &g_big_attr);
+  }
   return launch_tile<128, 128, 2, 2>(a, b, c, m, n, k, stream, &g_small_attr);
 }
 
@@ -268,10 +519,10 @@ const char* launch_triad(const void* a, const void* b, void* c, size_t n, float 
 
 PyObject* py_gemm(PyObject*, PyObject* args) {
   unsigned long long a, b, c, stream;
-  int m, n, k;
-  if (!PyArg_ParseTuple(args, "KKKiiiK", &a, &b, &c, &m, &n, &k, &stream)) return nullptr;
+  int m, n, k, variant = kAuto;
+  if (!PyArg_ParseTuple(args, "KKKiiiK|i", &a, &b, &c, &m, &n, &k, &stream, &variant)) return nullptr;
   const char* err = launch_gemm(reinterpret_cast<void*>(a), reinterpret_cast<void*>(b), reinterpret_cast<void*>(c), m,
-                                n, k, reinterpret_cast<hipStream_t>(stream));
+                                n, k, reinterpret_cast<hipStream_t>(stream), variant);
   if (err) {
     PyErr_SetString(PyExc_RuntimeError, err);
     return nullptr;
@@ -295,7 +546,9 @@ PyObject* py_triad(PyObject*, PyObject* args) {
 PyObject* py_tile(PyObject*, PyObject*) { return Py_BuildValue("(iii)", 128, 128, BK); }
 
 PyMethodDef kMethods[] = {
-    {"gemm_bf16_nt", py_gemm, METH_VARARGS, "gemm_bf16_nt(a, b, c, M, N, K, stream): C = A @ B^T (bf16, fp32 acc)."},
+    {"gemm_bf16_nt", py_gemm, METH_VARARGS,
+     "gemm_bf16_nt(a, b, c, M, N, K, stream, variant=0): C = A @ B^T (bf16, fp32 acc); variant 0 auto, "
+     "1 128x128, 2 256x256 register-staged, 3 256x256 8-phase LDS-DMA."},
     {"stream_triad", py_triad, METH_VARARGS, "stream_triad(a, b, c, n, s, stream): c = a + s*b (fp32)."},
     {"tile", py_tile, METH_NOARGS, "(BM, BN, BK) of the GEMM tiling."},
     {nullptr, nullptr, 0, nullptr}};

@@ -37,9 +37,20 @@ def _stream_handle(stream: Optional[torch.cuda.Stream], device) -> int:
     return int(s.cuda_stream)
 
 
+#: Kernel variants of gemm_bf16_nt (see kernels/workload.hip): picked by shape
+#: by default; forcing one is for tests and A/B timing.
+GEMM_VARIANTS = {"auto": 0, "tile128": 1, "tile256": 2, "tile256_dma": 3}
+
+
 def gemm_bf16_nt(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None,
-                 stream: Optional[torch.cuda.Stream] = None) -> torch.Tensor:
-    """C[M,N] = A[M,K] @ B[N,K]^T with M,N multiples of 128 and K of 64."""
+                 stream: Optional[torch.cuda.Stream] = None, variant: str = "auto") -> torch.Tensor:
+    """C[M,N] = A[M,K] @ B[N,K]^T with M,N multiples of 128 and K of 64.
+
+    ``variant`` forces one kernel: ``tile256`` needs M,N multiples of 256 and
+    ``tile256_dma`` (the 8-phase LDS-DMA kernel) additionally K a multiple of 128.
+    """
+    if variant not in GEMM_VARIANTS:
+        raise ValueError(f"unknown variant {variant!r}; one of {sorted(GEMM_VARIANTS)}")
     if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16:
         raise TypeError("gemm_bf16_nt expects bfloat16 inputs")
     if a.dim() != 2 or b.dim() != 2 or a.shape[1] != b.shape[1]:
@@ -57,7 +68,8 @@ def gemm_bf16_nt(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] =
         out = torch.empty((m, n), dtype=torch.bfloat16, device=a.device)
     elif out.shape != (m, n) or out.dtype != torch.bfloat16 or not out.is_contiguous() or out.device != a.device:
         raise ValueError("out must be a contiguous bfloat16 [M,N] tensor on A's device")
-    native().gemm_bf16_nt(a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k, _stream_handle(stream, a.device))
+    native().gemm_bf16_nt(a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k, _stream_handle(stream, a.device),
+                          GEMM_VARIANTS[variant])
     return out
 
 
@@ -139,20 +151,20 @@ def gemm_tflops(m: int, n: int, k: int, seconds: float) -> float:
     return 2.0 * m * n * k / seconds / 1e12
 
 
-def time_gemm(size: int = 8192, iters: int = 20, device: int = 0) -> float:
+def time_gemm(size: int = 8192, iters: int = 20, device: int = 0, variant: str = "auto") -> float:
     """Median TFLOP/s of gemm_bf16_nt at size³ (uniform random operands)."""
     dev = torch.device("cuda", device)
     a = (torch.rand(size, size, device=dev) * 2 - 1).to(torch.bfloat16)
     b = (torch.rand(size, size, device=dev) * 2 - 1).to(torch.bfloat16)
     c = torch.empty_like(a)
     for _ in range(3):
-        gemm_bf16_nt(a, b, out=c)
+        gemm_bf16_nt(a, b, out=c, variant=variant)
     torch.cuda.synchronize(dev)
     times = []
     for _ in range(iters):
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
-        gemm_bf16_nt(a, b, out=c)
+        gemm_bf16_nt(a, b, out=c, variant=variant)
         e.record()
         e.synchronize()
         times.append(s.elapsed_time(e) / 1e3)

@@ -1,7 +1,8 @@
 """Profiling target: the workload kernels at benchmark shapes (run under rocprofv3)."""
+import os
 import sys
 
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from headlamp_intel_gpu_plugin_amd.ops import workload  # noqa: E402
@@ -11,8 +12,9 @@ for size in (4096, 8192):
     a = (torch.rand(size, size, device=dev) * 2 - 1).to(torch.bfloat16)
     b = (torch.rand(size, size, device=dev) * 2 - 1).to(torch.bfloat16)
     c = torch.empty_like(a)
-    for _ in range(10):
-        workload.gemm_bf16_nt(a, b, out=c)
+    for variant in ("tile256", "tile256_dma"):
+        for _ in range(10):
+            workload.gemm_bf16_nt(a, b, out=c, variant=variant)
     ref = torch.empty_like(a)
     for _ in range(10):
         torch.matmul(a, b.T, out=ref)  # hipBLASLt reference point

@@ -132,6 +132,66 @@ def test_gemm_big_tile_identity_asymmetric(dev):
     assert torch.count_nonzero(c[k:]) == 0
 
 
+# Every kernel variant forced on shapes that exercise its edges: one block,
+# one loop iteration (K=128 for the 8-phase kernel), odd tile counts, M != N.
+VARIANT_SHAPES = {
+    "tile128": [(128, 128, 64), (384, 640, 192), (1024, 512, 1024)],
+    "tile256": [(256, 256, 64), (512, 768, 320), (2048, 1024, 1024)],
+    "tile256_dma": [(256, 256, 128), (256, 512, 384), (768, 512, 256), (2048, 1024, 1024), (1280, 2304, 640)],
+}
+
+
+@pytest.mark.parametrize("variant,m,n,k", [(v, *shape) for v, shapes in VARIANT_SHAPES.items() for shape in shapes])
+def test_gemm_variant_exact_integers(dev, variant, m, n, k):
+    a = (torch.arange(m * k, device=dev) % 5 - 2).reshape(m, k).to(torch.bfloat16)
+    b = ((torch.arange(n * k, device=dev) * 7 + 3) % 3 - 1).reshape(n, k).to(torch.bfloat16)
+    c = workload.gemm_bf16_nt(a, b, variant=variant)
+    assert torch.equal(c.float(), _ref(a, b)), (c.float() - _ref(a, b)).abs().max().item()
+
+
+@pytest.mark.parametrize("variant", ["tile256", "tile256_dma"])
+def test_gemm_variant_identity_asymmetric(dev, variant):
+    # A = I with an asymmetric B: a transposed store or a swapped half-tile shows up exactly.
+    m, n, k = 512, 768, 256
+    a = torch.zeros(m, k, device=dev, dtype=torch.bfloat16)
+    a[:k, :k] = torch.eye(k, device=dev, dtype=torch.bfloat16)
+    bvals = (torch.arange(n * k, device=dev, dtype=torch.float32).reshape(n, k) % 61) - 30
+    c = workload.gemm_bf16_nt(a, bvals.to(torch.bfloat16), variant=variant)
+    assert torch.equal(c[:k].float(), bvals.T[:k].contiguous())
+    assert torch.count_nonzero(c[k:]) == 0
+
+
+def test_gemm_dma_kernel_repeatable_random(dev):
+    # LDS-DMA ordering bugs show up as rare wrong tiles: compare 30 launches
+    # at two sizes against one fp32 reference each, bit for bit across runs.
+    for m, n, k in [(4096, 4096, 1024), (2048, 3072, 2048)]:
+        g = torch.Generator(device=dev).manual_seed(m + n + k)
+        a = torch.randn(m, k, device=dev, dtype=torch.bfloat16, generator=g)
+        b = torch.randn(n, k, device=dev, dtype=torch.bfloat16, generator=g)
+        ref = _ref(a, b)
+        first = workload.gemm_bf16_nt(a, b, variant="tile256_dma")
+        tol = ref.abs().clamp_min(1.0) * 2 ** -7
+        assert ((first.float() - ref).abs() <= tol).all()
+        for _ in range(29):
+            again = workload.gemm_bf16_nt(a, b, variant="tile256_dma")
+            assert torch.equal(again, first)
+
+
+def test_gemm_variant_rejects_unfit_shapes(dev):
+    a = torch.randn(256, 192, device=dev, dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError):
+        workload.gemm_bf16_nt(a, a, variant="tile256_dma")  # K % 128 != 0
+    with pytest.raises(ValueError):
+        workload.gemm_bf16_nt(a, a, variant="nope")
+
+
+def test_gemm_variants_throughput(dev):
+    # A/B in one process (guide §5.4 rule 24); the default path must be the fastest.
+    tf = {v: workload.time_gemm(size=8192, iters=10, variant=v) for v in ("tile128", "tile256", "tile256_dma", "auto")}
+    print("gemm 8192^3 TFLOP/s: " + ", ".join(f"{v} {t:.0f}" for v, t in tf.items()))
+    assert tf["auto"] >= 0.97 * max(tf.values()), tf
+
+
 def test_gemm_respects_stream(dev):
     a = torch.randn(512, 256, device=dev, dtype=torch.bfloat16)
     b = torch.randn(512, 256, device=dev, dtype=torch.bfloat16)
