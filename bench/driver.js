@@ -24,6 +24,7 @@
 
 import http from 'http';
 import fs from 'fs';
+import path from 'path';
 import { createClusterStore } from '../src/api/clusterStore.js';
 import { createMetricsSource } from '../src/api/metrics.js';
 import {
@@ -154,6 +155,46 @@ function renderAll(ctx, mstate) {
     columnCells: columnCells,
     htmlBytes: htmlBytes,
   };
+}
+
+const SNAPSHOT_CSS =
+  'body{font-family:system-ui,sans-serif;margin:24px;color:#222;max-width:1200px}' +
+  'h1{font-size:22px}h2{font-size:16px;border-bottom:1px solid #ddd;padding-bottom:4px;margin-top:28px}' +
+  'table{border-collapse:collapse;font-size:13px;margin:8px 0}td,th{border:1px solid #e0e0e0;padding:3px 8px;text-align:left}' +
+  'dl{display:grid;grid-template-columns:max-content auto;gap:2px 16px;font-size:13px}dt{font-weight:600}' +
+  '[data-status=success]{color:#2e7d32}[data-status=warning]{color:#ef6c00}[data-status=error]{color:#c62828}' +
+  'button{margin-left:12px}';
+
+/** Write one static HTML file per view (plus a node and a pod detail section). */
+function writeSnapshots(ctx, mstate, dir, now) {
+  fs.mkdirSync(dir, { recursive: true });
+  const opts = { metrics: mstate.metrics, now: now };
+  const views = [
+    ['01-overview', renderPage(overviewView(ctx, opts))],
+    ['02-device-plugins', renderPage(devicePluginsView(ctx, opts))],
+    ['03-gpu-nodes', renderPage(nodesView(ctx, opts))],
+    ['04-gpu-pods', renderPage(podsView(ctx, opts))],
+    ['05-metrics', renderPage(metricsView(ctx, Object.assign({}, mstate, { now: now })))],
+  ];
+  if (ctx.gpuNodes.length) {
+    const s = nodeDetailView(ctx.gpuNodes[0], ctx, opts);
+    if (s) views.push(['06-node-detail', renderSection(s)]);
+  }
+  if (ctx.gpuPods.length) {
+    const s = podDetailView(ctx.gpuPods[0], opts);
+    if (s) views.push(['07-pod-detail', renderSection(s)]);
+  }
+  const files = [];
+  for (let i = 0; i < views.length; i++) {
+    const f = path.join(dir, views[i][0] + '.html');
+    fs.writeFileSync(
+      f,
+      '<!doctype html><html><head><meta charset="utf-8"><title>amd-gpu — ' + views[i][0] + '</title><style>' +
+        SNAPSHOT_CSS + '</style></head><body>\n' + views[i][1] + '\n</body></html>\n'
+    );
+    files.push(f);
+  }
+  return files;
 }
 
 // ---------------------------------------------------------------------------
@@ -345,6 +386,14 @@ async function serve(a) {
         out.requestsPerStep = (counter.n - before) / n;
         out.bytesPerStep = (counter.bytes - bytesBefore) / n;
         out.rows = rows;
+      } else if (c.cmd === 'snapshot') {
+        // Static HTML of every view (docs/screenshots): same IR → HTML path as the benchmark.
+        const L = get(name);
+        if (!L.opened) {
+          await L.s.coldOpen();
+          L.opened = true;
+        }
+        out.files = writeSnapshots(L.s.ctx(), L.s.mstate(), c.dir, c.now);
       } else if (c.cmd === 'switch') {
         const L = get(name);
         if (!L.opened) {

@@ -25,9 +25,9 @@ class Driver:
                                      cwd=ROOT, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                                      text=True, bufsize=1)
 
-    def call(self, cmd: str, schedule: str = "amd", n: int = 1, timeout: Optional[float] = None) -> Dict:
+    def call(self, cmd: str, schedule: str = "amd", n: int = 1, timeout: Optional[float] = None, **extra) -> Dict:
         assert self.proc.stdin and self.proc.stdout
-        self.proc.stdin.write(json.dumps({"cmd": cmd, "schedule": schedule, "n": n}) + "\n")
+        self.proc.stdin.write(json.dumps(dict({"cmd": cmd, "schedule": schedule, "n": n}, **extra)) + "\n")
         self.proc.stdin.flush()
         line = self.proc.stdout.readline()
         if not line:

@@ -1,0 +1,21 @@
+"""tools/screenshots.py renders every view of a fake cluster through the shipped view-models."""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_screenshots_render_every_view(tmp_path):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "screenshots.py"), "--nodes", "2", "--out",
+                        str(tmp_path)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    names = sorted(os.listdir(tmp_path))
+    assert names == ["01-overview.html", "02-device-plugins.html", "03-gpu-nodes.html", "04-gpu-pods.html",
+                     "05-metrics.html", "06-node-detail.html", "07-pod-detail.html"]
+    html = {n: (tmp_path / n).read_text() for n in names}
+    assert "<h1>AMD GPU — Overview</h1>" in html["01-overview.html"]
+    assert "GPU Node Summary" in html["03-gpu-nodes.html"]
+    assert "mi355x-001" in html["03-gpu-nodes.html"]
+    assert "<h2>AMD GPU</h2>" in html["06-node-detail.html"]
+    assert "<h2>AMD GPU Resources</h2>" in html["07-pod-detail.html"]
