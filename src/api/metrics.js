@@ -245,9 +245,11 @@ export function joinNodeExporterResults(r) {
  * A browser allows 6 concurrent HTTP/1.1 connections per origin, so a
  * refresh that stays within 6 requests completes in one round-trip.
  */
-export function exporterQuery() {
+export function exporterQuery(withTopology) {
   const E = SERIES.exporter;
-  const names = [E.power, E.powerCap, E.vramUsed, E.vramTotal, E.gfx, E.umc, E.temp, E.xgmiRe, E.linkHops];
+  const names = [E.power, E.powerCap, E.vramUsed, E.vramTotal, E.gfx, E.umc, E.temp, E.xgmiRe];
+  // Link topology is static: callers include it only when their cached copy is stale.
+  if (withTopology !== false) names.push(E.linkHops);
   return '{__name__=~"' + names.join('|') + '"}';
 }
 
@@ -299,6 +301,8 @@ export function createMetricsSource(opts) {
   let cachedAt = 0;
   let discovering = null;
   let source = null; // which exporter answered last time
+  let links = null; // measured xGMI link topology per node (static), refreshed every `ttl`
+  let linksAt = 0;
 
   function get(name, path) {
     const start = clock.now();
@@ -341,6 +345,7 @@ export function createMetricsSource(opts) {
     cachedPath = null;
     source = null;
     seriesCache = null;
+    links = null;
   }
 
   function instant(base, q) {
@@ -368,8 +373,9 @@ export function createMetricsSource(opts) {
       if (!base) return null;
       const wantExp = source === null || source === 'amd-exporter';
       const wantNe = source === null || source === 'node-exporter';
+      const withTopology = links === null || clock.now() - linksAt >= ttl;
       const waves = [
-        wantExp ? combined(base, exporterQuery()) : Promise.resolve(null),
+        wantExp ? combined(base, exporterQuery(withTopology)) : Promise.resolve(null),
         wantNe ? combined(base, nodeExporterQuery()) : Promise.resolve(null),
       ];
       return Promise.all(waves).then(function (res) {
@@ -387,6 +393,12 @@ export function createMetricsSource(opts) {
           if (j.gpus.length) {
             joined = j;
             src = 'amd-exporter';
+            if (withTopology) {
+              links = j.links;
+              linksAt = clock.now();
+            } else {
+              joined.links = links;
+            }
           }
         }
         if (!src && ne) {

@@ -176,6 +176,24 @@ describe('fetchGpuMetrics', () => {
     const m = await src.fetchGpuMetrics();
     expect(m.links.n0).toEqual({ '0-1': { type: 'XGMI', hops: 1 }, '1-0': { type: 'XGMI', hops: 1 } });
   });
+  it('asks for the static link topology only when its cached copy is stale', async () => {
+    const d = exporterData(['n0']);
+    d.gpu_xgmi_link_hops = [vec({ __name__: 'gpu_xgmi_link_hops', hostname: 'n0', gpu_id: '0', peer_gpu_id: '1' }, 1)];
+    const request = prom({ data: d });
+    let now = 1000000;
+    const src = createMetricsSource({ request, clock: { setTimeout, clearTimeout, now: () => now } });
+    const asked = () =>
+      request.mock.calls.map((c) => decodeURIComponent(c[0])).filter((p) => p.indexOf('gpu_power_usage') >= 0);
+    await src.fetchGpuMetrics();
+    now += 1000;
+    const m = await src.fetchGpuMetrics();
+    expect(asked()[0]).toContain('gpu_xgmi_link_hops');
+    expect(asked()[1]).not.toContain('gpu_xgmi_link_hops');
+    expect(m.links.n0).toEqual({ '0-1': { type: 'XGMI', hops: 1 } }); // served from the cache
+    now += 10 * 60 * 1000;
+    await src.fetchGpuMetrics();
+    expect(asked()[asked().length - 1]).toContain('gpu_xgmi_link_hops');
+  });
   it('remembers the answering source and skips the other', async () => {
     const request = prom();
     const src = createMetricsSource({ request });
