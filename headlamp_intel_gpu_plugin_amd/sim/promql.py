@@ -101,13 +101,34 @@ class TSDB:
         self._index: Dict[tuple, Series] = {}
         self._select_cache: Dict[tuple, List[Series]] = {}
         self._by_labels_id: Dict[int, Series] = {}
+        # `by (...)` projections of stored label sets: (id(labels), by) → (key, projected, labels, json)
+        self._proj_cache: Dict[tuple, tuple] = {}
+        self._proj_json: Dict[int, tuple] = {}
 
     def label_json(self, labels: Labels) -> str:
-        """JSON for a label set; cached when it is a stored series' own dict."""
+        """JSON for a label set; cached when it is a stored series' own dict
+        or a cached ``by`` projection of one."""
         s = self._by_labels_id.get(id(labels))
         if s is not None and s.labels is labels:
             return s.metric_json()
+        p = self._proj_json.get(id(labels))
+        if p is not None and p[0] is labels:
+            return p[1]
         return json.dumps(labels, separators=(",", ":"))
+
+    def project(self, labels: Labels, by: tuple) -> tuple:
+        """(group key, projected labels) of ``labels`` onto ``by``, cached per
+        stored label set so a repeated aggregation query does no dict work."""
+        ck = (id(labels), by)
+        hit = self._proj_cache.get(ck)
+        if hit is not None and hit[2] is labels:
+            return hit[0], hit[1]
+        gl = {k: labels[k] for k in by if k in labels}
+        key = tuple(sorted(gl.items()))
+        if self._by_labels_id.get(id(labels)) is not None:
+            self._proj_cache[ck] = (key, gl, labels)
+            self._proj_json[id(gl)] = (gl, json.dumps(gl, separators=(",", ":")))
+        return key, gl
 
     def add(self, series: Series) -> Series:
         key = series._key
@@ -438,14 +459,14 @@ class Evaluator:
                 raise PromQLError("aggregation over scalar")
             groups: Dict[tuple, List] = {}
             glabels: Dict[tuple, Labels] = {}
+            byt = tuple(by) if by is not None else None
             for labels, v in vec:
-                if by is not None:
-                    gl = {k: labels[k] for k in by if k in labels}
-                elif without is not None:
-                    gl = {k: x for k, x in _drop_name(labels).items() if k not in without}
+                if byt is not None:
+                    k, gl = self.db.project(labels, byt)
                 else:
-                    gl = {}
-                k = tuple(sorted(gl.items()))
+                    gl = ({k: x for k, x in _drop_name(labels).items() if k not in without}
+                          if without is not None else {})
+                    k = tuple(sorted(gl.items()))
                 groups.setdefault(k, []).append(v)
                 glabels[k] = gl
             res = []

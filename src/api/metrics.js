@@ -245,12 +245,22 @@ export function joinNodeExporterResults(r) {
  * A browser allows 6 concurrent HTTP/1.1 connections per origin, so a
  * refresh that stays within 6 requests completes in one round-trip.
  */
+/**
+ * Labels the exporter join reads. The combined query projects every series
+ * onto them (`max by (...)`), so the response carries no per-series
+ * card/driver/serial/job labels: the Device Metrics Exporter attaches a
+ * dozen of those to every gauge, which would otherwise dominate the bytes
+ * moved through the Headlamp proxy on each refresh. `max` also folds
+ * duplicate scrapes of one GPU (two jobs scraping one exporter).
+ */
+export const EXPORTER_JOIN_LABELS = ['__name__', 'hostname', 'node', 'instance', 'gpu_id', 'peer_gpu_id', 'pod', 'namespace'];
+
 export function exporterQuery(withTopology) {
   const E = SERIES.exporter;
   const names = [E.power, E.powerCap, E.vramUsed, E.vramTotal, E.gfx, E.umc, E.temp, E.xgmiRe];
   // Link topology is static: callers include it only when their cached copy is stale.
   if (withTopology !== false) names.push(E.linkHops);
-  return '{__name__=~"' + names.join('|') + '"}';
+  return 'max by (' + EXPORTER_JOIN_LABELS.join(', ') + ') ({__name__=~"' + names.join('|') + '"})';
 }
 
 export function nodeExporterQuery() {

@@ -6,8 +6,10 @@
  */
 import {
   PROMETHEUS_SERVICES,
+  EXPORTER_JOIN_LABELS,
   SERIES,
   createMetricsSource,
+  exporterQuery,
   joinExporterResults,
   joinNodeExporterResults,
   servicePath,
@@ -69,7 +71,7 @@ function prom(opts) {
         data: { resultType: 'matrix', result: [{ metric: { hostname: 'n0' }, values: [[end - 30, '100'], [end, '200']] }] },
       });
     }
-    const m = /^\{__name__=~"(.*)"\}$/.exec(q);
+    const m = /^(?:max by \([^)]*\) \()?\{__name__=~"(.*)"\}\)?$/.exec(q);
     if (!m) return Promise.resolve(ok([]));
     const re = new RegExp('^(?:' + m[1] + ')$');
     return Promise.resolve(ok(rows.filter((r) => re.test(r.metric.__name__ || ''))));
@@ -175,6 +177,12 @@ describe('fetchGpuMetrics', () => {
     const src = createMetricsSource({ request: prom({ data: d }) });
     const m = await src.fetchGpuMetrics();
     expect(m.links.n0).toEqual({ '0-1': { type: 'XGMI', hops: 1 }, '1-0': { type: 'XGMI', hops: 1 } });
+  });
+  it('projects exporter series onto the labels the join reads', () => {
+    const q = exporterQuery();
+    expect(q.indexOf('max by (__name__, hostname,')).toBe(0);
+    EXPORTER_JOIN_LABELS.forEach((l) => expect(q).toContain(l));
+    expect(q).not.toContain('serial_number');
   });
   it('asks for the static link topology only when its cached copy is stale', async () => {
     const d = exporterData(['n0']);
