@@ -11,10 +11,11 @@ cluster of 8×MI355X nodes (weak scaling: per-node work is fixed as N grows).
 * rank 0 hosts the fake kube-apiserver + Prometheus (service proxy) with an
   injected per-request round-trip latency (``--rtt-ms``, default 20 ms),
   identical for both schedules measured;
-* every rank with a GPU runs a node agent that exports its MI355X's live
-  telemetry through the native probe, and (unless ``--no-burn``) a workload
-  "pod" running the MFMA GEMM + HBM triad kernels, so GPU 0 of every node
-  reports real power / HBM / activity; rank 0 scrapes the agents into the TSDB;
+* every rank with a GPU runs (unless ``--no-burn``) a workload "pod" running
+  the MFMA GEMM + HBM triad kernels on its own MI355X; rank 0 starts the
+  native ``amdgpu-exporter`` daemon (C++/HIP, one for the host) and scrapes
+  it every 2 s into the TSDB, HIP device r → GPU 0 of node r, so GPU 0 of
+  every node reports real power / HBM / activity;
 * rank 0 drives the SHIPPED plugin data layer (src/, Node.js) over real HTTP:
   the reference plugin's request schedule is replayed first as the measured
   baseline (untimed), then the flagship schedule runs W warm-up refreshes and
@@ -70,22 +71,24 @@ def main(argv=None) -> int:
     node_name = gpu_node_name(info.rank)
     gpu = info.device is not None
 
-    # --- per-rank node agent + workload pod ---------------------------------
-    agent = burner = None
+    # --- workload pod per rank; one native exporter for the host ----------
+    burner = exporter = None
     live_on = gpu and not args.no_live
-    if live_on:
-        from headlamp_intel_gpu_plugin_amd.ops import probe
-        from headlamp_intel_gpu_plugin_amd.parallel.agent import NodeAgent
-
-        if not probe.available():
-            raise RuntimeError("GPU present but the native probe sees no device: " + probe.native().last_error())
-        dev_index = info.device.index
-        agent = NodeAgent(node_name, lambda: probe.sample(dev_index)).start()
     if gpu and not args.no_burn:
         from headlamp_intel_gpu_plugin_amd.ops.workload import Burner
 
         burner = Burner(device=info.device.index, size=4096, gemms=4, triad_mb=512).start()
-    targets = D.all_gather_object(info, (node_name, agent.url if agent else None))
+    ranks = D.all_gather_object(info, (node_name, info.device.index if gpu else None))
+    if live_on and info.is_main:
+        from headlamp_intel_gpu_plugin_amd.parallel.agent import ExporterProcess
+
+        # The C++ amdgpu-exporter daemon exports every MI355X on the host
+        # (one process, whatever the rank count); HIP device d belongs to
+        # the rank that owns it, i.e. to that rank's synthetic node.
+        exporter = ExporterProcess(hostname=socket.gethostname()).start()
+        if "gpu_total_vram{" not in exporter.scrape():
+            exporter.stop()
+            raise RuntimeError("GPU present but amdgpu-exporter exports no device")
 
     result = None
     elapsed = 0.0
@@ -94,11 +97,14 @@ def main(argv=None) -> int:
         from headlamp_intel_gpu_plugin_amd.sim.apiserver import ServerThread, make_fake
         from headlamp_intel_gpu_plugin_amd.utils.nodebridge import Driver
 
-        live_targets = {n: u for n, u in targets if u}
-        live = live_series(list(live_targets)) if live_targets else None
+        from headlamp_intel_gpu_plugin_amd.parallel.agent import device_to_node
+
+        node_of_device = {str(d): n for n, d in ranks if d is not None} if exporter else {}
+        live = live_series(list(node_of_device.values())) if node_of_device else None
         fc = make_fake(n_nodes, source="both", latency_ms=args.rtt_ms, live=live, preset=args.preset)
         n_nodes = len(fc.cluster.gpu_nodes)
-        scraper = Scraper(live_targets, live, interval=2.0).start() if live_targets else None
+        scraper = (Scraper([(exporter.url, device_to_node(node_of_device))], live, interval=2.0).start()
+                   if node_of_device else None)
         server = ServerThread(fc).start()
         drv = Driver(server.url)
         try:
@@ -140,8 +146,8 @@ def main(argv=None) -> int:
     ms_per_step = D.max_float(info, elapsed * 1000.0 / max(1, args.steps))
     if burner:
         burner.stop()
-    if agent:
-        agent.stop()
+    if exporter:
+        exporter.stop()
 
     if info.is_main:
         amd_s = summarize(result["amd"]["latencies"])
@@ -185,6 +191,7 @@ def main(argv=None) -> int:
                          "gpus_monitored": rows["gpusMonitored"], "gpu_cells": rows["gpuCells"],
                          "pod_table_rows": rows["podTableRows"], "detail_sections": rows["detailSections"]},
             "live_telemetry": bool(result["scrapes"]) and n_nodes > 0,
+            "telemetry_source": "native amdgpu-exporter (C++/HIP) scraped every 2 s" if exporter else "synthetic",
             "host": socket.gethostname(),
         }
         print(json.dumps(line), flush=True)

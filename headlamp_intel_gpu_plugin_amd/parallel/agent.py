@@ -1,21 +1,26 @@
 """Per-node telemetry agents and the scraper that feeds the fake Prometheus.
 
-One process per GPU (torchrun): rank ``r`` plays synthetic node ``r``. Its
-:class:`NodeAgent` serves ``/metrics`` in AMD Device Metrics Exporter format,
-sampled live from its own MI355X through the native probe
-(``ops/csrc/amdgpu_probe.cpp``) — the DaemonSet-per-node exporter of a real
-cluster. Rank 0's :class:`Scraper` pulls every agent on a fixed interval, as
-Prometheus would, and pushes the samples into the TSDB series of
-(node r, GPU 0); the node's other seven GPUs stay synthetic because each rank
-owns exactly one physical device.
+One process per GPU (torchrun): rank ``r`` plays synthetic node ``r`` and owns
+HIP device ``r``. Live telemetry comes from the native ``amdgpu-exporter``
+daemon (:class:`ExporterProcess`, ops/csrc/amdgpu_exporter.cpp) — the
+DaemonSet-per-node exporter of a real cluster — started once on the host and
+exporting every visible MI355X; :class:`NodeAgent` is the in-process Python
+equivalent (one GPU, probe-backed) used by smoke tests. Rank 0's
+:class:`Scraper` pulls the targets on a fixed interval, as Prometheus would,
+and pushes each sample into the TSDB series of (node r, GPU 0) for device r;
+the node's other seven GPUs stay synthetic because each rank owns exactly one
+physical device.
 """
 from __future__ import annotations
 
 import http.server
+import os
+import signal
+import subprocess
 import threading
 import time
 import urllib.request
-from typing import Callable, Dict, List, Optional, Tuple
+from typing import Callable, Dict, List, Optional, Sequence, Tuple, Union
 
 from ..ops.probe import parse_exposition
 from ..sim.promql import Series
@@ -23,6 +28,7 @@ from ..sim.promql import Series
 #: exporter metric → (sample key, scale)
 LIVE_FIELDS = {
     "gpu_power_usage": ("power_w", 1.0),
+    "gpu_power_cap": ("power_cap_w", 1.0),
     "gpu_gfx_activity": ("gfx_busy_pct", 1.0),
     "gpu_umc_activity": ("mem_busy_pct", 1.0),
     "gpu_junction_temperature": ("temp_junction_c", 1.0),
@@ -84,6 +90,55 @@ class NodeAgent:
         self._srv.server_close()
 
 
+class ExporterProcess:
+    """The native ``amdgpu-exporter`` daemon as a child process on an ephemeral port."""
+
+    def __init__(self, hostname: str, device: Optional[int] = None, gpu_label: Optional[str] = None,
+                 topology: bool = True):
+        from ..ops import build as native_build
+
+        exe = native_build.so_path("amdgpu-exporter")
+        if not os.path.exists(exe):
+            raise RuntimeError(f"amdgpu-exporter not built ({exe}); run `python __graft_entry__.py build`")
+        self.cmd = [exe, "--port", "0", "--bind", "127.0.0.1", "--hostname", hostname]
+        if device is not None:
+            self.cmd += ["--device", str(device)]
+            if gpu_label is not None:
+                self.cmd += ["--gpu-label", gpu_label]
+        if not topology:
+            self.cmd.append("--no-topology")
+        self.proc: Optional[subprocess.Popen] = None
+        self.url = ""
+
+    def start(self, timeout: float = 60.0) -> "ExporterProcess":
+        self.proc = subprocess.Popen(self.cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+        deadline = time.monotonic() + timeout
+        line = ""
+        while time.monotonic() < deadline and "listening on" not in line:
+            line = self.proc.stdout.readline()
+            if not line and self.proc.poll() is not None:
+                raise RuntimeError("amdgpu-exporter exited: " + self.proc.stderr.read()[-2000:])
+        if "listening on" not in line:
+            self.stop()
+            raise RuntimeError("amdgpu-exporter did not start")
+        port = int(line.split("127.0.0.1:")[1].split()[0])
+        self.url = f"http://127.0.0.1:{port}/metrics"
+        return self
+
+    def scrape(self, timeout: float = 10.0) -> str:
+        with urllib.request.urlopen(self.url, timeout=timeout) as r:
+            return r.read().decode()
+
+    def stop(self) -> None:
+        if self.proc is not None and self.proc.poll() is None:
+            self.proc.send_signal(signal.SIGTERM)
+            try:
+                self.proc.wait(10)
+            except subprocess.TimeoutExpired:
+                self.proc.kill()
+                self.proc.wait(5)
+
+
 def live_series(nodes: List[str]) -> Dict[Tuple[str, int], Dict[str, Series]]:
     """Empty pushed series for GPU 0 of each node (``models.telemetry.populate(live=...)``)."""
     out = {}
@@ -92,12 +147,32 @@ def live_series(nodes: List[str]) -> Dict[Tuple[str, int], Dict[str, Series]]:
     return out
 
 
-class Scraper:
-    """Pulls every agent every ``interval`` s and appends to the live series."""
+#: maps a scraped series' labels to the (node, gpu) it belongs to, or None to drop it
+Relabel = Callable[[Dict[str, str]], Optional[Tuple[str, int]]]
 
-    def __init__(self, targets: Dict[str, str], live: Dict[Tuple[str, int], Dict[str, Series]], interval: float = 2.0,
+
+def _by_hostname(default_node: str) -> Relabel:
+    return lambda labels: (labels.get("hostname", default_node), int(labels.get("gpu_id", "0")))
+
+
+def device_to_node(node_of_device: Dict[str, str]) -> Relabel:
+    """Relabel a host-wide exporter: series of HIP device ``d`` → (node of rank d, GPU 0)."""
+    return lambda labels: (node_of_device[labels["gpu_id"]], 0) if labels.get("gpu_id") in node_of_device else None
+
+
+class Scraper:
+    """Pulls every target every ``interval`` s and appends to the live series.
+
+    ``targets`` is ``{node: url}`` (per-node agents, labels used as-is) or a
+    list of ``(url, relabel)`` pairs.
+    """
+
+    def __init__(self, targets: Union[Dict[str, str], Sequence[Tuple[str, Relabel]]],
+                 live: Dict[Tuple[str, int], Dict[str, Series]], interval: float = 2.0,
                  now: Callable[[], float] = time.time):
-        self.targets = targets
+        if isinstance(targets, dict):
+            targets = [(url, _by_hostname(node)) for node, url in targets.items()]
+        self.targets = list(targets)
         self.live = live
         self.interval = interval
         self.now = now
@@ -108,7 +183,7 @@ class Scraper:
 
     def scrape_once(self) -> None:
         t = self.now()
-        for node, url in self.targets.items():
+        for url, relabel in self.targets:
             try:
                 with urllib.request.urlopen(url, timeout=2) as r:
                     text = r.read().decode()
@@ -116,7 +191,8 @@ class Scraper:
                 self.errors += 1
                 continue
             for name, labels, value in parse_exposition(text):
-                series = self.live.get((labels.get("hostname", node), int(labels.get("gpu_id", "0"))), {}).get(name)
+                key = relabel(labels)
+                series = self.live.get(key, {}).get(name) if key is not None else None
                 if series is not None:
                     series.push(t, value)
             self.scrapes += 1

@@ -92,3 +92,27 @@ def test_exporter_reports_mi355x(exe):
     ids = {l["gpu_id"] for n, l, _ in parse_exposition(one.stdout)}
     assert ids == {"7"}
     time.sleep(0)
+
+
+def test_exporter_process_and_device_relabel(exe):
+    from headlamp_intel_gpu_plugin_amd.parallel.agent import (ExporterProcess, NodeAgent, Scraper, device_to_node,
+                                                              live_series)
+
+    p = ExporterProcess(hostname="host-a").start()
+    try:
+        assert "# TYPE gpu_power_usage gauge" in p.scrape()
+    finally:
+        p.stop()
+    assert p.proc.returncode == 0
+    # A host-wide exporter's device 0 belongs to rank 0's synthetic node.
+    agent = NodeAgent("host-a", lambda: {"power_w": 321.0, "vram_total_b": 2.0 ** 30}).start()
+    try:
+        live = live_series(["mi355x-003"])
+        s = Scraper([(agent.url, device_to_node({"0": "mi355x-003"}))], live, now=lambda: 100.0)
+        s.scrape_once()
+        assert s.scrapes == 1
+        assert live[("mi355x-003", 0)]["gpu_power_usage"].at(100.0)[1] == 321.0
+        assert live[("mi355x-003", 0)]["gpu_total_vram"].at(100.0)[1] == 1024.0
+        assert device_to_node({"0": "n"})({"gpu_id": "5"}) is None
+    finally:
+        agent.stop()
