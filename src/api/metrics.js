@@ -459,7 +459,7 @@ export function createMetricsSource(opts) {
    * Incremental: samples are aligned to `step`, and Prometheus never rewrites
    * a past step, so after the first call only the steps newer than the cache
    * are requested — and none at all until the next step boundary.
-   * @returns {Promise<{ power: Record<string, Array<[number, number]>>, vram: Record<string, Array<[number, number]>> } | null>}
+   * @returns {Promise<{ rangeSec: number, power: Record<string, Array<[number, number]>>, vram: Record<string, Array<[number, number]>> } | null>}
    */
   function fetchSeries(rangeSec, stepSec) {
     const range = rangeSec || 1800;
@@ -471,6 +471,7 @@ export function createMetricsSource(opts) {
         seriesCache.base !== base || end - seriesCache.end >= range;
       const start = fresh ? end - range : seriesCache.end + step;
       if (!fresh && start > end) return seriesCache.data;
+      // The window travels with the data so the page can title it.
       const E = SERIES.exporter;
       const qs = [
         ['power', 'sum by (hostname) (' + E.power + ')', 1],
@@ -479,7 +480,7 @@ export function createMetricsSource(opts) {
       return Promise.all(
         qs.map(function (q) { return rangeQuery(base, q[0], q[1], q[2], start, end, step); })
       ).then(function (rows) {
-        const data = {};
+        const data = { rangeSec: range };
         const cutoff = end - range;
         let allOk = true;
         for (let i = 0; i < rows.length; i++) {

@@ -81,6 +81,13 @@ function ageKey(now) {
   return Math.floor(now / 1000);
 }
 
+/** Seconds → "30 min" / "1 h" / "6 h" / "90 s" for section titles. */
+export function formatWindow(sec) {
+  if (sec >= 3600 && sec % 3600 === 0) return sec / 3600 + ' h';
+  if (sec >= 60 && sec % 60 === 0) return sec / 60 + ' min';
+  return sec + ' s';
+}
+
 /** Drop memoised sections (tests; cluster switch). */
 export function clearViewMemo() {
   memo.clear();
@@ -773,7 +780,11 @@ export function metricsView(ctx, mstate, opts) {
     );
 
     if (mstate.series && mstate.series.power) {
-      items.push(section('Power & HBM (last 30 min)', [{ t: 'series', power: mstate.series.power, vram: mstate.series.vram || {} }]));
+      items.push(
+        section('Power & HBM (last ' + formatWindow(mstate.series.rangeSec || 1800) + ')', [
+          { t: 'series', power: mstate.series.power, vram: mstate.series.vram || {} },
+        ])
+      );
     }
 
     const byNode = {};

@@ -10,6 +10,7 @@ import {
   nodesView,
   podsView,
   metricsView,
+  formatWindow,
   allocationBar,
   powerBar,
   hbmBar,
@@ -359,6 +360,13 @@ describe('metricsView', () => {
   it('adds the time-series section when range data exists', () => {
     const vm = metricsView(ctx, { metrics: metrics(['n0'], 1), fetchError: null, fetching: false, series: { power: { n0: [[1, 2]] }, vram: {} } }, opts);
     expect(sectionTitles(vm)).toContain('Power & HBM (last 30 min)');
+  });
+  it('titles the time-series section with the configured window', () => {
+    const series = { rangeSec: 6 * 3600, power: { n0: [[1, 2]] }, vram: {} };
+    const vm = metricsView(ctx, { metrics: metrics(['n0'], 1), fetchError: null, fetching: false, series }, opts);
+    expect(sectionTitles(vm)).toContain('Power & HBM (last 6 h)');
+    expect(formatWindow(90)).toBe('90 s');
+    expect(formatWindow(900)).toBe('15 min');
   });
   it('powerBar without a cap shows watts only', () => {
     expect(powerBar(512.25, null).text).toBe('512.3 W');
