@@ -119,7 +119,11 @@ export function AmdGpuDataProvider({ children }: { children: React.ReactNode }) 
 
 export interface GpuMetricsState {
   metrics: GpuMetrics | null;
-  series: { power: Record<string, Array<[number, number]>>; vram: Record<string, Array<[number, number]>> } | null;
+  series: {
+    rangeSec: number;
+    power: Record<string, Array<[number, number]>>;
+    vram: Record<string, Array<[number, number]>>;
+  } | null;
   fetchError: string | null;
   fetching: boolean;
   refresh: () => void;

@@ -88,6 +88,8 @@ export const DISCOVERY_TTL_MS = 5 * 60 * 1000;
  * @property {'amd-exporter'|'node-exporter'|null} source
  * @property {GpuTelemetry[]} gpus
  * @property {Record<string, Record<string, number>>} xgmi  node → "src-dst" → GB/s
+ * @property {Record<string, Record<string, {type: string, hops: number}>>} links  node → "src-dst" →
+ *           measured link (gpu_xgmi_link_hops); empty when the exporter does not report topology
  * @property {string} fetchedAt
  * @property {string} prometheusPath
  */
