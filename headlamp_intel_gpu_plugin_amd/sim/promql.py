@@ -33,6 +33,11 @@ Labels = Dict[str, str]
 # Storage
 # ---------------------------------------------------------------------------
 
+# Bumped on every sample push / series add: instant-query results cached by
+# :func:`query` are valid only while it is unchanged.
+_MUTATIONS = [0]
+
+
 class Series:
     """One time series: labels + samples.
 
@@ -60,6 +65,7 @@ class Series:
         return self._json
 
     def push(self, t: float, v: float) -> None:
+        _MUTATIONS[0] += 1
         if self.ts and t <= self.ts[-1]:
             if t == self.ts[-1]:
                 self.vs[-1] = v
@@ -104,6 +110,8 @@ class TSDB:
         # `by (...)` projections of stored label sets: (id(labels), by) → (key, projected, labels, json)
         self._proj_cache: Dict[tuple, tuple] = {}
         self._proj_json: Dict[int, tuple] = {}
+        self._fn_intervals: set = set()
+        self._query_cache: Dict[str, tuple] = {}
 
     def label_json(self, labels: Labels) -> str:
         """JSON for a label set; cached when it is a stored series' own dict
@@ -135,6 +143,9 @@ class TSDB:
         if key in self._index:
             return self._index[key]
         self._index[key] = series
+        _MUTATIONS[0] += 1
+        if series.fn is not None:
+            self._fn_intervals.add(series.interval)
         self.by_name.setdefault(series.labels.get("__name__", ""), []).append(series)
         self._by_labels_id[id(series.labels)] = series
         self._select_cache.clear()
@@ -565,15 +576,36 @@ class RawJSON(str):
 
 
 def query(db: TSDB, q: str, t: float):
-    """Prometheus ``/api/v1/query`` response body (dict on error/scalar, RawJSON for vectors)."""
+    """Prometheus ``/api/v1/query`` response body (dict on error/scalar, RawJSON for vectors).
+
+    Function-backed series only change at their sample interval and pushed
+    series only on push, so a vector result is reused for repeated queries
+    within one interval bucket while nothing was pushed — the evaluation
+    cost of a Python TSDB would otherwise dominate the fake's latency, where
+    a real Prometheus answers such a selector in well under a millisecond.
+    """
+    cacheable = len(db._fn_intervals) <= 1
+    if cacheable:
+        iv = next(iter(db._fn_intervals)) if db._fn_intervals else 1.0
+        stamp = (math.floor(t / iv), _MUTATIONS[0])
+        hit = db._query_cache.get(q)
+        if hit is not None and hit[0] == stamp:
+            return _vector_body(hit[1], t)
     try:
         typ, val = Evaluator(db).instant(parse(q), t)
     except PromQLError as e:
         return {"status": "error", "errorType": "bad_data", "error": str(e)}
     if typ == "scalar":
         return {"status": "success", "data": {"resultType": "scalar", "result": [t, _fmt(val)]}}
+    rows = [(db.label_json(l), _fmt(v)) for l, v in val]
+    if cacheable:
+        db._query_cache[q] = (stamp, rows)
+    return _vector_body(rows, t)
+
+
+def _vector_body(rows, t: float) -> "RawJSON":
     ts = repr(float(t))
-    parts = ['{"metric":' + db.label_json(l) + ',"value":[' + ts + ',"' + _fmt(v) + '"]}' for l, v in val]
+    parts = ['{"metric":' + lj + ',"value":[' + ts + ',"' + fv + '"]}' for lj, fv in rows]
     return RawJSON('{"status":"success","data":{"resultType":"vector","result":[' + ",".join(parts) + "]}}")
 
 

@@ -294,6 +294,64 @@ export function splitByName(result) {
   return out;
 }
 
+// ---------------------------------------------------------------------------
+// Structural sharing between consecutive snapshots
+// ---------------------------------------------------------------------------
+
+/** Deep equality for the plain JSON-like values a snapshot holds. */
+function sameValue(a, b) {
+  if (a === b) return true;
+  if (!a || !b || typeof a !== 'object' || typeof b !== 'object') return false;
+  const ka = Object.keys(a);
+  if (ka.length !== Object.keys(b).length) return false;
+  for (let i = 0; i < ka.length; i++) {
+    if (!sameValue(a[ka[i]], b[ka[i]])) return false;
+  }
+  return true;
+}
+
+/**
+ * Reuse objects of `prev` wherever `next` holds equal content, so that
+ * identity-keyed memos downstream (view sections, renderers) hit when a
+ * refresh returns what the last one did — the common case, since exporters
+ * are scraped every 15-30 s and a dashboard refreshes more often than that.
+ * GPU lists are matched by (node, gpu); maps by key. Returns `prev` itself
+ * when nothing changed.
+ */
+export function shareGpus(prev, next) {
+  if (!prev) return next;
+  const byKey = {};
+  for (let i = 0; i < prev.length; i++) byKey[prev[i].nodeName + '\u0000' + prev[i].gpu] = prev[i];
+  let all = prev.length === next.length;
+  const out = new Array(next.length);
+  for (let i = 0; i < next.length; i++) {
+    const p = byKey[next[i].nodeName + '\u0000' + next[i].gpu];
+    if (p && sameValue(p, next[i])) {
+      out[i] = p;
+      if (prev[i] !== p) all = false;
+    } else {
+      out[i] = next[i];
+      all = false;
+    }
+  }
+  return all ? prev : out;
+}
+
+export function shareMap(prev, next) {
+  if (!prev) return next;
+  const out = {};
+  let all = Object.keys(prev).length === Object.keys(next).length;
+  for (const k in next) {
+    if (prev[k] !== undefined && sameValue(prev[k], next[k])) {
+      out[k] = prev[k];
+    } else {
+      out[k] = next[k];
+      all = false;
+    }
+  }
+  return all ? prev : out;
+}
+
 /**
  * @param {{ request: (path: string) => Promise<any>, timeoutMs?: number,
  *           clock?: {setTimeout: Function, clearTimeout: Function, now: Function},
@@ -315,6 +373,7 @@ export function createMetricsSource(opts) {
   let source = null; // which exporter answered last time
   let links = null; // measured xGMI link topology per node (static), refreshed every `ttl`
   let linksAt = 0;
+  let last = null; // previous snapshot, for structural sharing
 
   function get(name, path) {
     const start = clock.now();
@@ -358,6 +417,7 @@ export function createMetricsSource(opts) {
     source = null;
     seriesCache = null;
     links = null;
+    last = null;
   }
 
   function instant(base, q) {
@@ -420,15 +480,17 @@ export function createMetricsSource(opts) {
             src = 'node-exporter';
           }
         }
+        const same = last && last.source === src;
         source = src;
-        return {
+        last = {
           source: src,
-          gpus: joined.gpus,
-          xgmi: joined.xgmi,
-          links: joined.links || {},
+          gpus: same ? shareGpus(last.gpus, joined.gpus) : joined.gpus,
+          xgmi: same ? shareMap(last.xgmi, joined.xgmi) : joined.xgmi,
+          links: same ? shareMap(last.links, joined.links || {}) : joined.links || {},
           fetchedAt: new Date(clock.now()).toISOString(),
           prometheusPath: base,
         };
+        return last;
       });
     });
   }

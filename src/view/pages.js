@@ -496,7 +496,9 @@ export function nodesView(ctx, opts) {
     const xg = metrics && metrics.xgmi ? metrics.xgmi[name] : undefined;
     const lk = metrics && metrics.links ? metrics.links[name] : undefined;
     items.push(
-      memo('node-card:' + name, [n, pods, stats, keyOf(own), keyOf(xg), keyOf(lk), age], function () {
+      // own / xg / lk keep their identity while their content is unchanged
+      // (ownersByNode + the metrics client's structural sharing).
+      memo('node-card:' + name, [n, pods, stats, own, xg, lk, age], function () {
         const blocks = [kv(nodeCardRows(n, pods, stats, now))];
         const count = getNodeGpuCount(n);
         if (count > 0) {
@@ -510,17 +512,25 @@ export function nodesView(ctx, opts) {
   return page(BRAND + ' — Nodes', refreshButton('Refresh node data', ctx.refreshing), items);
 }
 
-/** Stable string key of a small JSON value (undefined → ''). */
-function keyOf(v) {
-  return v === undefined || v === null ? '' : JSON.stringify(v);
+const ownersCache = typeof WeakMap === 'function' ? new WeakMap() : null;
+let lastOwners = {};
+
+function sameOwners(a, b) {
+  if (!a || !b || a.length !== b.length) return false;
+  for (let i = 0; i < a.length; i++) {
+    if (a[i].gpu !== b[i].gpu || a[i].pod !== b[i].pod || a[i].namespace !== b[i].namespace) return false;
+  }
+  return true;
 }
 
-const ownersCache = typeof WeakMap === 'function' ? new WeakMap() : null;
-
-/** node → [{gpu, pod, namespace}] from exporter pod labels, computed once per metrics object. */
+/**
+ * node → [{gpu, pod, namespace}] from exporter pod labels, computed once per
+ * GPU list; a node's array keeps its identity while its owners are unchanged
+ * (telemetry values change every scrape, GPU ownership rarely).
+ */
 function ownersByNode(metrics) {
   if (!metrics || !metrics.gpus) return {};
-  if (ownersCache && ownersCache.has(metrics)) return ownersCache.get(metrics);
+  if (ownersCache && ownersCache.has(metrics.gpus)) return ownersCache.get(metrics.gpus);
   const out = {};
   for (let i = 0; i < metrics.gpus.length; i++) {
     const g = metrics.gpus[i];
@@ -528,7 +538,11 @@ function ownersByNode(metrics) {
     if (!out[g.nodeName]) out[g.nodeName] = [];
     out[g.nodeName].push({ gpu: g.gpu, pod: g.pod, namespace: g.namespace });
   }
-  if (ownersCache) ownersCache.set(metrics, out);
+  for (const k in out) {
+    if (sameOwners(lastOwners[k], out[k])) out[k] = lastOwners[k];
+  }
+  lastOwners = out;
+  if (ownersCache) ownersCache.set(metrics.gpus, out);
   return out;
 }
 
@@ -799,30 +813,37 @@ export function metricsView(ctx, mstate, opts) {
     }
     for (let i = 0; i < order.length; i++) {
       const gs = byNode[order[i]];
-      items.push(
-        section(order[i] + ' — ' + gs.length + ' × ' + MI355X.shortName, [
-          table(
-            ['GPU', 'Power', 'HBM Used', 'GFX', 'HBM Activity', 'Temp', 'Pod'],
-            gs.map(function (g) {
-              return [
-                'GPU ' + g.gpu,
-                g.powerWatts !== null ? powerBar(g.powerWatts, g.powerCapWatts) : status('warning', 'No data'),
-                hbmBar(g.vramUsedBytes, g.vramTotalBytes),
-                pctText(g.gfxActivityPct),
-                pctText(g.memActivityPct),
-                g.tempC === null ? '—' : Math.round(g.tempC) + ' °C',
-                g.pod ? (g.namespace ? g.namespace + '/' : '') + g.pod : '—',
-              ];
-            }),
-            gs.map(function (g) { return g.nodeName + '-' + g.gpu; })
-          ),
-        ], order[i])
-      );
+      // Deps are the node's GPU objects, which the metrics client reuses while unchanged.
+      items.push(memo('metrics-node:' + order[i], gs, function () { return metricsNodeSection(order[i], gs); }));
     }
   }
 
   void now;
   return page(BRAND + ' — Metrics', refreshButton('Refresh metrics', mstate.fetching || ctx.loading), items);
+}
+
+function metricsNodeSection(name, gs) {
+  return section(
+    name + ' — ' + gs.length + ' × ' + MI355X.shortName,
+    [
+      table(
+        ['GPU', 'Power', 'HBM Used', 'GFX', 'HBM Activity', 'Temp', 'Pod'],
+        gs.map(function (g) {
+          return [
+            'GPU ' + g.gpu,
+            g.powerWatts !== null ? powerBar(g.powerWatts, g.powerCapWatts) : status('warning', 'No data'),
+            hbmBar(g.vramUsedBytes, g.vramTotalBytes),
+            pctText(g.gfxActivityPct),
+            pctText(g.memActivityPct),
+            g.tempC === null ? '—' : Math.round(g.tempC) + ' °C',
+            g.pod ? (g.namespace ? g.namespace + '/' : '') + g.pod : '—',
+          ];
+        }),
+        gs.map(function (g) { return g.nodeName + '-' + g.gpu; })
+      ),
+    ],
+    name
+  );
 }
 
 // ---------------------------------------------------------------------------
@@ -853,7 +874,7 @@ export function nodeDetailView(resource, ctx, opts) {
   const own = ownersByNode(metrics)[name];
   const xg = metrics && metrics.xgmi ? metrics.xgmi[name] : undefined;
   const lk = metrics && metrics.links ? metrics.links[name] : undefined;
-  return memo('node-detail:' + name, [raw, podsOnNode, !!ctx.loading, keyOf(own), keyOf(xg), keyOf(lk)], function () {
+  return memo('node-detail:' + name, [raw, podsOnNode, !!ctx.loading, own, xg, lk], function () {
     return nodeDetailSection(raw, name, cap, alloc, podsOnNode, ctx.loading, own, xg, lk);
   });
 }

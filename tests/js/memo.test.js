@@ -4,7 +4,7 @@
  * inputs → recomputed sections.
  */
 import { createMemo, sections } from '../../src/view/ir.js';
-import { clearViewMemo, nodesView, overviewView, podDetailView, podsView } from '../../src/view/pages.js';
+import { clearViewMemo, metricsView, nodesView, overviewView, podDetailView, podsView } from '../../src/view/pages.js';
 import { renderSection } from '../../src/view/html.js';
 import { createClusterStore, sameObjects } from '../../src/api/clusterStore.js';
 import { DEVICE_CONFIG_LIST_PATH, PLUGIN_POD_QUERIES } from '../../src/api/amdgpu.js';
@@ -69,6 +69,29 @@ describe('view memoisation', () => {
     const card = (ss, name) => ss.find((s) => s.title === name);
     expect(card(b, 'g0')).toBe(card(a, 'g0'));
     expect(card(b, 'g1')).not.toBe(card(a, 'g1'));
+  });
+
+  it('keeps node cards when only telemetry values change, not ownership', () => {
+    const n0 = makeGpuNode('g0');
+    const ctx = makeContext({ nodes: [n0] });
+    const gpu = (power) => ({ nodeName: 'g0', gpu: '0', pod: 'train', namespace: 'ml', powerWatts: power });
+    const a = sections(nodesView(ctx, { now: NOW, metrics: { gpus: [gpu(900)], xgmi: {}, links: {} } }));
+    const b = sections(nodesView(ctx, { now: NOW, metrics: { gpus: [gpu(1200)], xgmi: {}, links: {} } }));
+    expect(b.find((s) => s.title === 'g0')).toBe(a.find((s) => s.title === 'g0'));
+    const c = sections(nodesView(ctx, { now: NOW, metrics: { gpus: [Object.assign(gpu(1200), { pod: 'eval' })], xgmi: {}, links: {} } }));
+    expect(c.find((s) => s.title === 'g0')).not.toBe(a.find((s) => s.title === 'g0'));
+  });
+
+  it('metrics page reuses a node section while its GPU objects are reused', () => {
+    const ctx = makeContext({ nodes: [makeGpuNode('g0')] });
+    const g = { nodeName: 'g0', gpu: '0', pod: null, namespace: null, powerWatts: 900, powerCapWatts: 1400,
+      vramUsedBytes: 1, vramTotalBytes: 2, gfxActivityPct: 50, memActivityPct: 20, tempC: 60 };
+    const m1 = { source: 'amd-exporter', gpus: [g], xgmi: {}, links: {}, fetchedAt: new Date(NOW).toISOString() };
+    const m2 = Object.assign({}, m1, { fetchedAt: new Date(NOW + 5000).toISOString() });
+    const find = (vm) => sections(vm).find((s) => s.title.indexOf('g0 — ') === 0);
+    const a = find(metricsView(ctx, { metrics: m1, fetchError: null, fetching: false }, { now: NOW }));
+    const b = find(metricsView(ctx, { metrics: m2, fetchError: null, fetching: false }, { now: NOW }));
+    expect(b).toBe(a);
   });
 
   it('pod detail sections are cached per pod object', () => {

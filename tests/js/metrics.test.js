@@ -13,6 +13,8 @@ import {
   joinExporterResults,
   joinNodeExporterResults,
   servicePath,
+  shareGpus,
+  shareMap,
   summarizeMetrics,
 } from '../../src/api/metrics.js';
 
@@ -177,6 +179,31 @@ describe('fetchGpuMetrics', () => {
     const src = createMetricsSource({ request: prom({ data: d }) });
     const m = await src.fetchGpuMetrics();
     expect(m.links.n0).toEqual({ '0-1': { type: 'XGMI', hops: 1 }, '1-0': { type: 'XGMI', hops: 1 } });
+  });
+  it('reuses unchanged GPU objects and maps across refreshes (structural sharing)', async () => {
+    const d = exporterData(['n0', 'n1']);
+    const request = prom({ data: d });
+    const src = createMetricsSource({ request });
+    const a = await src.fetchGpuMetrics();
+    const b = await src.fetchGpuMetrics();
+    expect(b.gpus).toBe(a.gpus);
+    expect(b.xgmi).toBe(a.xgmi);
+    // One GPU's power changes: a new list, every other GPU object reused.
+    d[SERIES.exporter.power][0].value = [1760000001, '999'];
+    const c = await src.fetchGpuMetrics();
+    expect(c.gpus).not.toBe(b.gpus);
+    const changed = c.gpus.filter((g, i) => g !== b.gpus[i]);
+    expect(changed).toHaveLength(1);
+    expect(changed[0].powerWatts).toBe(999);
+  });
+  it('shareMap keeps equal entries and returns prev when nothing changed', () => {
+    const prev = { n0: { '0-1': 1 }, n1: { '0-1': 2 } };
+    expect(shareMap(prev, { n0: { '0-1': 1 }, n1: { '0-1': 2 } })).toBe(prev);
+    const next = shareMap(prev, { n0: { '0-1': 1 }, n1: { '0-1': 3 } });
+    expect(next).not.toBe(prev);
+    expect(next.n0).toBe(prev.n0);
+    expect(next.n1).toEqual({ '0-1': 3 });
+    expect(shareGpus(null, [1])).toEqual([1]);
   });
   it('projects exporter series onto the labels the join reads', () => {
     const q = exporterQuery();

@@ -169,3 +169,21 @@ def test_parse_ast_shapes():
     node = parse("x[5m]")
     assert node[0] == "sel" and node[2] == 300.0 and node[1][0].value == "x"
     assert parse("sum by (a) (x)")[0] == "agg"
+
+
+def test_instant_cache_sees_pushes_and_interval_changes():
+    db = promql.TSDB()
+    live = db.add(promql.Series({"__name__": "gpu_power_usage", "hostname": "n0"}))
+    db.add(promql.Series({"__name__": "gpu_power_usage", "hostname": "n1"}, fn=lambda t: t, interval=15))
+    live.push(100.0, 1.0)
+    q = "gpu_power_usage"
+
+    def values(t):
+        return {r["metric"]["hostname"]: float(r["value"][1]) for r in json.loads(promql.query(db, q, t))["data"]["result"]}
+
+    assert values(101.0) == {"n0": 1.0, "n1": 90.0}
+    live.push(102.0, 7.0)  # a push invalidates the cached result
+    assert values(103.0)["n0"] == 7.0
+    assert values(106.0)["n1"] == 105.0  # next 15 s bucket re-evaluates fn series
+    body = json.loads(promql.query(db, q, 107.5))
+    assert body["data"]["result"][0]["value"][0] == 107.5  # eval timestamp is current, not cached
