@@ -140,7 +140,10 @@ export function createClusterStore(opts) {
     podError: null,
     deviceConfigs: [],
     crdAvailable: false,
-    pluginPods: [],
+    pluginPods: [], // from the plugin-pod queries (used when the pod list is not available)
+    // Where the pod list stands: 'unknown' (never fed: harness/tests),
+    // 'pending' (a list/watch is in flight), 'ready', or 'error'.
+    podsState: 'unknown',
     asyncLoaded: false,
     refreshing: false,
     asyncError: null,
@@ -148,6 +151,7 @@ export function createClusterStore(opts) {
   };
   let seq = 0;
   let inflight = null;
+  let podsQueried = false; // the in-flight refresh includes the plugin-pod requests
   let version = 0;
   const listeners = [];
 
@@ -156,6 +160,8 @@ export function createClusterStore(opts) {
   let memoGpuNodes = [];
   let memoPodsIn = undefined;
   let memoGpuPods = [];
+  let memoPluginIn = undefined;
+  let memoPluginPods = [];
   let memoIndexKey = [null, null];
   let memoIndex = buildClusterIndex([], []);
   let snapshot = null;
@@ -174,6 +180,22 @@ export function createClusterStore(opts) {
     }
     return memoGpuPods;
   }
+  /**
+   * Operator pods. Once Headlamp's pod list (all namespaces) is in, they are
+   * derived from it: it already holds every pod the reference's three
+   * plugin-pod requests return, so a refresh needs only the CRD request.
+   * Without that list (forbidden cluster-wide, failed, or no watch at all)
+   * they come from the PLUGIN_POD_QUERIES requests.
+   */
+  function pluginPods() {
+    if (s.podsState !== 'ready' || !s.pods) return s.pluginPods;
+    if (s.pods !== memoPluginIn) {
+      memoPluginIn = s.pods;
+      const next = filterAmdGpuPluginPods(s.pods);
+      memoPluginPods = sameObjects(memoPluginPods, next) ? memoPluginPods : next;
+    }
+    return memoPluginPods;
+  }
   function index(n, p) {
     if (memoIndexKey[0] !== n || memoIndexKey[1] !== p) {
       memoIndexKey = [n, p];
@@ -189,13 +211,14 @@ export function createClusterStore(opts) {
     if (s.nodeError) errors.push(String(s.nodeError));
     if (s.podError) errors.push(String(s.podError));
     if (s.asyncError) errors.push(s.asyncError);
+    const pp = pluginPods();
     version++;
     return Object.freeze({
       deviceConfigs: s.deviceConfigs,
-      pluginInstalled: s.deviceConfigs.length > 0 || s.pluginPods.length > 0,
+      pluginInstalled: s.deviceConfigs.length > 0 || pp.length > 0,
       gpuNodes: n,
       gpuPods: p,
-      pluginPods: s.pluginPods,
+      pluginPods: pp,
       crdAvailable: s.crdAvailable,
       loading: !s.asyncLoaded || s.nodes === null || s.pods === null,
       refreshing: s.refreshing,
@@ -228,9 +251,29 @@ export function createClusterStore(opts) {
     );
   }
 
+  /** Run the plugin-pod requests; resolves to the deduplicated operator pods. */
+  function queryPluginPods() {
+    const pods = podQueries.map(function (path, i) {
+      return traced('plugin-pods-' + i, path).then(
+        function (list) { return isKubeList(list) ? filterAmdGpuPluginPods(list.items) : []; },
+        function () { return []; }
+      );
+    });
+    return Promise.all(pods).then(function (results) {
+      let found = [];
+      for (let i = 0; i < results.length; i++) found = found.concat(results[i]);
+      return dedupePods(found);
+    });
+  }
+
+  function commitQueriedPods(pods) {
+    s.pluginPods = sameObjects(s.pluginPods, pods) ? s.pluginPods : pods;
+  }
+
   /**
-   * Re-fetch the DeviceConfig CRD and operator pods. Resolves once the new
-   * data is committed (or dropped because a newer refresh superseded it).
+   * Re-fetch the DeviceConfig CRD (and, only while no pod list is available,
+   * the operator pods). Resolves once the new data is committed (or dropped
+   * because a newer refresh superseded it).
    * @returns {Promise<void>}
    */
   function refresh() {
@@ -246,24 +289,19 @@ export function createClusterStore(opts) {
         return { ok: false, items: [] };
       }
     );
-    const pods = podQueries.map(function (path, i) {
-      return traced('plugin-pods-' + i, path).then(
-        function (list) { return isKubeList(list) ? filterAmdGpuPluginPods(list.items) : []; },
-        function () { return []; }
-      );
-    });
-    const run = Promise.all([crd].concat(pods)).then(
+    const needPods = s.podsState === 'unknown' || s.podsState === 'error';
+    podsQueried = needPods;
+    const pods = needPods ? queryPluginPods() : Promise.resolve(null);
+    const run = Promise.all([crd, pods]).then(
       function (results) {
         if (my !== seq) return;
+        podsQueried = false;
         const c = results[0];
         s.crdAvailable = c.ok;
         // Structural sharing: an unchanged list keeps its identity, so every
         // memoised view (and React.memo'd section) downstream is reused.
         s.deviceConfigs = sameObjects(s.deviceConfigs, c.items) ? s.deviceConfigs : c.items;
-        let found = [];
-        for (let i = 1; i < results.length; i++) found = found.concat(results[i]);
-        const pods = dedupePods(found);
-        s.pluginPods = sameObjects(s.pluginPods, pods) ? s.pluginPods : pods;
+        if (results[1]) commitQueriedPods(results[1]);
         s.asyncError = null;
         s.asyncLoaded = true;
         s.refreshing = false;
@@ -272,6 +310,7 @@ export function createClusterStore(opts) {
       },
       function (err) {
         if (my !== seq) return;
+        podsQueried = false;
         s.asyncError = err instanceof Error ? err.message : String(err);
         s.asyncLoaded = true;
         s.refreshing = false;
@@ -295,10 +334,22 @@ export function createClusterStore(opts) {
   function setPods(items, error) {
     const next = items ? unwrapAll(items) : null;
     const err = error ? String(error) : null;
-    if (items === null && s.pods === null && err === s.podError) return;
+    const state = err ? 'error' : next ? 'ready' : 'pending';
+    if (items === null && s.pods === null && err === s.podError && state === s.podsState) return;
+    const wasError = s.podsState === 'error';
     s.pods = next;
     s.podError = err;
+    s.podsState = state;
     emit();
+    // The pod list failed (e.g. cluster-wide list forbidden): fall back to the
+    // plugin-pod requests so operator pods still show.
+    if (state === 'error' && !wasError && !(s.refreshing && podsQueried)) {
+      queryPluginPods().then(function (pods) {
+        if (s.podsState !== 'error') return;
+        commitQueriedPods(pods);
+        emit();
+      });
+    }
   }
 
   /**
@@ -307,6 +358,7 @@ export function createClusterStore(opts) {
    * `Promise.all([store.loadLists(), store.refresh()])`.
    */
   function loadLists() {
+    if (s.podsState === 'unknown') s.podsState = 'pending';
     const nodesP = traced('nodes', '/api/v1/nodes').then(
       function (l) { setNodes(isKubeList(l) ? l.items : [], null); },
       function (e) { setNodes([], e instanceof Error ? e.message : String(e)); }

@@ -271,6 +271,34 @@ export function nodeExporterQuery() {
   return '{__name__=~"' + names.join('|') + '"}';
 }
 
+/** Labels the node-exporter join reads (hwmon chip, DRM card, uname). */
+export const NODE_EXPORTER_JOIN_LABELS = ['__name__', 'instance', 'node', 'nodename', 'chip', 'chip_name', 'card'];
+
+/**
+ * First query of a session, while it is not yet known which exporter feeds
+ * this Prometheus: both exporters' series in ONE request, projected onto the
+ * union of the labels the two joins read. Later refreshes ask only the
+ * exporter that answered.
+ */
+export function mergedQuery(withTopology) {
+  const E = SERIES.exporter;
+  const N = SERIES.nodeExporter;
+  const names = [E.power, E.powerCap, E.vramUsed, E.vramTotal, E.gfx, E.umc, E.temp, E.xgmiRe];
+  if (withTopology !== false) names.push(E.linkHops);
+  names.push(N.chips.split('{')[0], N.power, N.powerCap, N.busy, N.vramUsed, N.vramTotal, N.uname);
+  const labels = EXPORTER_JOIN_LABELS.slice();
+  for (let i = 0; i < NODE_EXPORTER_JOIN_LABELS.length; i++) {
+    if (labels.indexOf(NODE_EXPORTER_JOIN_LABELS[i]) < 0) labels.push(NODE_EXPORTER_JOIN_LABELS[i]);
+  }
+  return 'max by (' + labels.join(', ') + ') ({__name__=~"' + names.join('|') + '"})';
+}
+
+/** Per-node power + HBM-used history in one range query (split by `__name__`). */
+export function seriesQuery() {
+  const E = SERIES.exporter;
+  return 'sum by (__name__, hostname) ({__name__=~"' + E.power + '|' + E.vramUsed + '"})';
+}
+
 /** Split a combined result into `name → rows` (xGMI rows under `__xgmi`). */
 export function splitByName(result) {
   const out = { __xgmi: [] };
@@ -420,6 +448,35 @@ export function createMetricsSource(opts) {
     last = null;
   }
 
+  /** Marker for "the request did not reach a Prometheus". */
+  const UNREACHABLE = {};
+
+  /**
+   * Run `fn(base)` against Prometheus. With no cached service the preferred
+   * candidate is queried directly — its answer doubles as discovery, so the
+   * first fetch costs one round trip instead of probe + query; only when it
+   * does not answer are all candidates probed in parallel. `fn` resolves to
+   * UNREACHABLE when its request failed.
+   */
+  function withPrometheus(fn, onCachedFailure) {
+    if (cachedPath && clock.now() - cachedAt < ttl) {
+      const base = cachedPath;
+      return fn(base).then(function (r) { return r === UNREACHABLE ? onCachedFailure() : r; });
+    }
+    const first = servicePath(services[0]);
+    return fn(first).then(function (r) {
+      if (r !== UNREACHABLE) {
+        cachedPath = first;
+        cachedAt = clock.now();
+        return r;
+      }
+      return discover().then(function (base) {
+        if (!base) return null;
+        return fn(base).then(function (r2) { return r2 === UNREACHABLE ? onCachedFailure() : r2; });
+      });
+    });
+  }
+
   function instant(base, q) {
     return get('query', base + '/api/v1/query?query=' + encodeURIComponent(q)).then(function (raw) {
       if (!raw || raw.status !== 'success' || !raw.data || !Array.isArray(raw.data.result)) return [];
@@ -441,64 +498,61 @@ export function createMetricsSource(opts) {
    * @returns {Promise<GpuMetrics|null>}
    */
   function fetchGpuMetrics() {
-    return discover().then(function (base) {
-      if (!base) return null;
-      const wantExp = source === null || source === 'amd-exporter';
-      const wantNe = source === null || source === 'node-exporter';
-      const withTopology = links === null || clock.now() - linksAt >= ttl;
-      const waves = [
-        wantExp ? combined(base, exporterQuery(withTopology)) : Promise.resolve(null),
-        wantNe ? combined(base, nodeExporterQuery()) : Promise.resolve(null),
-      ];
-      return Promise.all(waves).then(function (res) {
-        const exp = res[0] ? res[0].rows : null;
-        const ne = res[1] ? res[1].rows : null;
-        if ((!res[0] || !res[0].ok) && (!res[1] || !res[1].ok)) {
-          // Prometheus went away between discovery and query.
-          invalidate();
-          return null;
-        }
-        let joined = { gpus: [], xgmi: {}, links: {} };
-        let src = null;
-        if (exp) {
-          const j = joinExporterResults(exp);
-          if (j.gpus.length) {
-            joined = j;
-            src = 'amd-exporter';
-            if (withTopology) {
-              links = j.links;
-              linksAt = clock.now();
-            } else {
-              joined.links = links;
-            }
+    return withPrometheus(snapshotFrom, function () {
+      // Prometheus went away after discovery.
+      invalidate();
+      return null;
+    });
+  }
+
+  function snapshotFrom(base) {
+    const withTopology = links === null || clock.now() - linksAt >= ttl;
+    const q = source === 'amd-exporter' ? exporterQuery(withTopology)
+      : source === 'node-exporter' ? nodeExporterQuery() : mergedQuery(withTopology);
+    return combined(base, q).then(function (res) {
+      if (!res.ok) return UNREACHABLE;
+      const rows = res.rows;
+      let joined = { gpus: [], xgmi: {}, links: {} };
+      let src = null;
+      if (source !== 'node-exporter') {
+        const j = joinExporterResults(rows);
+        if (j.gpus.length) {
+          joined = j;
+          src = 'amd-exporter';
+          if (withTopology) {
+            links = j.links;
+            linksAt = clock.now();
+          } else {
+            joined.links = links;
           }
         }
-        if (!src && ne) {
-          const j = joinNodeExporterResults(ne);
-          if (j.gpus.length) {
-            joined = j;
-            src = 'node-exporter';
-          }
+      }
+      if (!src && source !== 'amd-exporter') {
+        const j = joinNodeExporterResults(rows);
+        if (j.gpus.length) {
+          joined = j;
+          src = 'node-exporter';
         }
-        const same = last && last.source === src;
-        source = src;
-        last = {
-          source: src,
-          gpus: same ? shareGpus(last.gpus, joined.gpus) : joined.gpus,
-          xgmi: same ? shareMap(last.xgmi, joined.xgmi) : joined.xgmi,
-          links: same ? shareMap(last.links, joined.links || {}) : joined.links || {},
-          fetchedAt: new Date(clock.now()).toISOString(),
-          prometheusPath: base,
-        };
-        return last;
-      });
+      }
+      const same = last && last.source === src;
+      source = src;
+      last = {
+        source: src,
+        gpus: same ? shareGpus(last.gpus, joined.gpus) : joined.gpus,
+        xgmi: same ? shareMap(last.xgmi, joined.xgmi) : joined.xgmi,
+        links: same ? shareMap(last.links, joined.links || {}) : joined.links || {},
+        fetchedAt: new Date(clock.now()).toISOString(),
+        prometheusPath: base,
+      };
+      return last;
     });
   }
 
   // Incremental range cache: step-aligned samples per series key.
   let seriesCache = null; // { range, step, end, data: { power: {node: [[t,v]]}, vram: {...} } }
 
-  function rangeQuery(base, key, q, scale, start, end, step) {
+  /** One range query; resolves {name → {node → [[t, v]]}} or UNREACHABLE. */
+  function rangeQuery(base, q, start, end, step) {
     const path = base + '/api/v1/query_range?query=' + encodeURIComponent(q) +
       '&start=' + start + '&end=' + end + '&step=' + step;
     return get('query_range', path).then(
@@ -506,19 +560,23 @@ export function createMetricsSource(opts) {
         const out = {};
         const res = raw && raw.status === 'success' && raw.data && Array.isArray(raw.data.result) ? raw.data.result : [];
         for (let i = 0; i < res.length; i++) {
-          const node = (res[i].metric && (res[i].metric.hostname || res[i].metric.instance)) || 'cluster';
+          const m = res[i].metric || {};
+          const name = m.__name__ || '';
+          const node = m.hostname || m.instance || 'cluster';
           const vals = Array.isArray(res[i].values) ? res[i].values : [];
-          out[node] = vals.map(function (v) { return [Number(v[0]), (num(v[1]) || 0) * scale]; });
+          if (!out[name]) out[name] = {};
+          out[name][node] = vals;
         }
-        return [key, out, true];
+        return out;
       },
-      function () { return [key, {}, false]; }
+      function () { return UNREACHABLE; }
     );
   }
 
   /**
    * Per-node power and HBM-used time series over the last `rangeSec`.
-   * Server-side `sum by (hostname)` keeps the payload O(nodes × points).
+   * Server-side `sum by (__name__, hostname)` keeps the payload
+   * O(nodes × points) and both series in one request.
    *
    * Incremental: samples are aligned to `step`, and Prometheus never rewrites
    * a past step, so after the first call only the steps newer than the cache
@@ -528,43 +586,38 @@ export function createMetricsSource(opts) {
   function fetchSeries(rangeSec, stepSec) {
     const range = rangeSec || 1800;
     const step = stepSec || 30;
-    return discover().then(function (base) {
-      if (!base) return null;
+    const E = SERIES.exporter;
+    const parts = [['power', E.power, 1], ['vram', E.vramUsed, SERIES.exporterVramUnitBytes]];
+    function from(base) {
       const end = Math.floor(clock.now() / 1000 / step) * step;
       const fresh = !seriesCache || seriesCache.range !== range || seriesCache.step !== step ||
         seriesCache.base !== base || end - seriesCache.end >= range;
       const start = fresh ? end - range : seriesCache.end + step;
-      if (!fresh && start > end) return seriesCache.data;
-      // The window travels with the data so the page can title it.
-      const E = SERIES.exporter;
-      const qs = [
-        ['power', 'sum by (hostname) (' + E.power + ')', 1],
-        ['vram', 'sum by (hostname) (' + E.vramUsed + ')', SERIES.exporterVramUnitBytes],
-      ];
-      return Promise.all(
-        qs.map(function (q) { return rangeQuery(base, q[0], q[1], q[2], start, end, step); })
-      ).then(function (rows) {
+      if (!fresh && start > end) return Promise.resolve(seriesCache.data);
+      return rangeQuery(base, seriesQuery(), start, end, step).then(function (got) {
+        if (got === UNREACHABLE) return UNREACHABLE;
         const data = { rangeSec: range };
         const cutoff = end - range;
-        let allOk = true;
-        for (let i = 0; i < rows.length; i++) {
-          const key = rows[i][0];
-          const got = rows[i][1];
-          if (!rows[i][2]) allOk = false;
+        for (let i = 0; i < parts.length; i++) {
+          const key = parts[i][0];
+          const scale = parts[i][2];
+          const rows = got[parts[i][1]] || {};
           const prev = fresh ? {} : seriesCache.data[key] || {};
           const merged = {};
-          const nodes = Object.keys(Object.assign({}, prev, got));
+          const nodes = Object.keys(Object.assign({}, prev, rows));
           for (let n = 0; n < nodes.length; n++) {
-            const pts = (prev[nodes[n]] || []).concat(got[nodes[n]] || []).filter(function (p) { return p[0] >= cutoff; });
+            const add = (rows[nodes[n]] || []).map(function (v) { return [Number(v[0]), (num(v[1]) || 0) * scale]; });
+            const pts = (prev[nodes[n]] || []).concat(add).filter(function (p) { return p[0] >= cutoff; });
             if (pts.length) merged[nodes[n]] = pts;
           }
           data[key] = merged;
         }
-        // Only advance the cache when every query answered; otherwise retry the window next time.
-        if (allOk) seriesCache = { range: range, step: step, end: end, base: base, data: data };
+        seriesCache = { range: range, step: step, end: end, base: base, data: data };
         return data;
       });
-    });
+    }
+    // A failed range request keeps the last window (retried next time).
+    return withPrometheus(from, function () { return seriesCache ? seriesCache.data : null; });
   }
 
   return {

@@ -93,6 +93,47 @@ describe('createClusterStore', () => {
     expect(store.getSnapshot().crdAvailable).toBe(true);
   });
 
+  it('derives operator pods from the pod list once it is in: a refresh is one request', async () => {
+    const request = router(baseRoutes());
+    const store = createClusterStore({ request });
+    store.setPods([makePluginPod('dp-0'), makePluginPod('dp-1'), makePlainPod('web')], null);
+    await store.refresh();
+    expect(request).toHaveBeenCalledTimes(1);
+    expect(request.mock.calls[0][0]).toBe(DEVICE_CONFIG_LIST_PATH);
+    const s = store.getSnapshot();
+    expect(s.pluginPods.map((p) => p.metadata.name).sort()).toEqual(['dp-0', 'dp-1']);
+    expect(s.pluginInstalled).toBe(true);
+  });
+
+  it('does not query operator pods while the pod list is pending', async () => {
+    const request = router(baseRoutes());
+    const store = createClusterStore({ request });
+    await Promise.all([store.loadLists(), store.refresh()]);
+    const paths = request.mock.calls.map((c) => c[0]).sort();
+    expect(paths).toEqual(['/api/v1/nodes', '/api/v1/pods', DEVICE_CONFIG_LIST_PATH].sort());
+    expect(store.getSnapshot().loading).toBe(false);
+  });
+
+  it('falls back to the plugin-pod requests when the pod list fails', async () => {
+    const request = router(baseRoutes());
+    const store = createClusterStore({ request });
+    store.setPods(null, 'pods is forbidden');
+    await store.refresh();
+    const s = store.getSnapshot();
+    expect(s.pluginPods.map((p) => p.metadata.name).sort()).toEqual(['dp-0', 'dp-1']);
+    expect(s.error).toContain('pods is forbidden');
+    expect(request.mock.calls.map((c) => c[0])).toContain(PLUGIN_POD_QUERIES[1]);
+  });
+
+  it('keeps the derived operator-pod list identity while it is unchanged', () => {
+    const store = createClusterStore({ request: router(baseRoutes()) });
+    const dp = makePluginPod('dp-0');
+    store.setPods([dp, makePlainPod('a')], null);
+    const a = store.getSnapshot().pluginPods;
+    store.setPods([dp, makePlainPod('b')], null);
+    expect(store.getSnapshot().pluginPods).toBe(a);
+  });
+
   it('sets crdAvailable and deviceConfigs from the CRD list', async () => {
     const store = createClusterStore({ request: router(baseRoutes()) });
     await store.refresh();

@@ -10,6 +10,7 @@ import {
   SERIES,
   createMetricsSource,
   exporterQuery,
+  mergedQuery,
   joinExporterResults,
   joinNodeExporterResults,
   servicePath,
@@ -68,9 +69,16 @@ function prom(opts) {
     if (q === '1') return Promise.resolve(ok([{ metric: {}, value: [0, '1'] }]));
     if (path.indexOf('/query_range') >= 0) {
       const end = Number(/end=(\d+)/.exec(path)[1]);
+      const values = [[end - 30, '100'], [end, '200']];
       return Promise.resolve({
         status: 'success',
-        data: { resultType: 'matrix', result: [{ metric: { hostname: 'n0' }, values: [[end - 30, '100'], [end, '200']] }] },
+        data: {
+          resultType: 'matrix',
+          result: [
+            { metric: { __name__: 'gpu_power_usage', hostname: 'n0' }, values },
+            { metric: { __name__: 'gpu_used_vram', hostname: 'n0' }, values },
+          ],
+        },
       });
     }
     const m = /^(?:max by \([^)]*\) \()?\{__name__=~"(.*)"\}\)?$/.exec(q);
@@ -263,14 +271,34 @@ describe('fetchGpuMetrics', () => {
     ]);
     expect(m.gpus[1].gfxActivityPct).toBe(88);
   });
-  it('issues one combined query per source on the first fetch', async () => {
+  it('first fetch: one merged query straight to the preferred service, no discovery probes', async () => {
     const request = prom();
     const src = createMetricsSource({ request });
+    const m = await src.fetchGpuMetrics();
+    const paths = request.mock.calls.map((c) => decodeURIComponent(c[0]));
+    expect(paths).toHaveLength(1);
+    expect(paths[0].indexOf(BASE0)).toBe(0);
+    expect(paths[0]).toContain('gpu_power_usage|gpu_power_cap|gpu_used_vram');
+    expect(paths[0]).toContain('node_hwmon_chip_names|node_hwmon_power_average_watt');
+    expect(m.source).toBe('amd-exporter');
     await src.fetchGpuMetrics();
-    const qs = request.mock.calls.map((c) => decodeURIComponent(c[0])).filter((p) => p.indexOf('query=1') < 0);
-    expect(qs).toHaveLength(2);
-    expect(qs[0]).toContain('gpu_power_usage|gpu_power_cap|gpu_used_vram');
-    expect(qs[1]).toContain('node_hwmon_chip_names|node_hwmon_power_average_watt');
+    const second = decodeURIComponent(request.mock.calls[1][0]);
+    expect(second).toContain('gpu_power_usage');
+    expect(second).not.toContain('node_hwmon'); // only the exporter that answered
+  });
+  it('falls back to parallel discovery when the preferred service does not answer', async () => {
+    const request = prom({ up: [BASE1] });
+    const src = createMetricsSource({ request });
+    const m = await src.fetchGpuMetrics();
+    expect(m.prometheusPath).toBe(BASE1);
+    const probes = request.mock.calls.filter((c) => c[0].indexOf('query=1') >= 0);
+    expect(probes).toHaveLength(PROMETHEUS_SERVICES.length);
+    expect(m.gpus.length).toBeGreaterThan(0);
+  });
+  it('the merged first query projects onto both joins\' labels', () => {
+    const q = mergedQuery();
+    ['hostname', 'gpu_id', 'pod', 'chip', 'card', 'nodename'].forEach((l) => expect(q).toContain(l));
+    expect(q.indexOf('max by (')).toBe(0);
   });
   it('returns an empty GPU list when Prometheus has no AMD series', async () => {
     const src = createMetricsSource({ request: prom({ data: null }) });
@@ -315,14 +343,14 @@ describe('fetchSeries', () => {
     const src = createMetricsSource({ request, clock: { setTimeout, clearTimeout, now: () => now } });
     await src.fetchSeries(600, 30);
     const ranges = () => request.mock.calls.map((c) => c[0]).filter((p) => p.indexOf('query_range') >= 0);
-    expect(ranges()).toHaveLength(2);
+    expect(ranges()).toHaveLength(1); // power and HBM in one query
     now += 10000; // same 30 s step: served from cache, no request
     await src.fetchSeries(600, 30);
-    expect(ranges()).toHaveLength(2);
+    expect(ranges()).toHaveLength(1);
     now += 50000; // two steps later: only the new window is requested
     await src.fetchSeries(600, 30);
-    expect(ranges()).toHaveLength(4);
-    const last = ranges()[3];
+    expect(ranges()).toHaveLength(2);
+    const last = ranges()[1];
     const startT = Number(/start=(\d+)/.exec(last)[1]);
     const endT = Number(/end=(\d+)/.exec(last)[1]);
     expect(endT - startT).toBe(30);
@@ -335,7 +363,10 @@ describe('fetchSeries', () => {
       const end = Number(/end=(\d+)/.exec(path)[1]);
       const values = [];
       for (let t = start; t <= end; t += 30) values.push([t, '1']);
-      return Promise.resolve({ status: 'success', data: { resultType: 'matrix', result: [{ metric: { hostname: 'n0' }, values }] } });
+      return Promise.resolve({
+        status: 'success',
+        data: { resultType: 'matrix', result: [{ metric: { __name__: 'gpu_power_usage', hostname: 'n0' }, values }] },
+      });
     });
     const src = createMetricsSource({ request, clock: { setTimeout, clearTimeout, now: () => now } });
     const a = await src.fetchSeries(300, 30);
