@@ -2,7 +2,7 @@ import { ApiProxy, K8s } from '@kinvolk/headlamp-plugin/lib';
 import { renderHook, waitFor } from '@testing-library/react';
 import React from 'react';
 import { beforeEach, describe, expect, it, vi } from 'vitest';
-import { makeDeviceConfig, makeGpuNode } from '../../tests/js/fixtures.js';
+import { makeDeviceConfig, makeGpuNode, makePluginPod } from '../../tests/js/fixtures.js';
 import { AmdGpuDataProvider, useAmdGpuContext } from './AmdGpuDataContext';
 import { resetSharedStores } from './clusterStore.js';
 
@@ -64,7 +64,19 @@ describe('AmdGpuDataProvider', () => {
     expect(result.current.error).toBeNull();
   });
 
-  it('refresh() re-issues the CRD and operator-pod requests', async () => {
+  it('derives operator pods from the watched pod list (no plugin-pod requests)', async () => {
+    vi.mocked(K8s.ResourceClasses.Node.useList).mockReturnValue([[], null] as any);
+    vi.mocked(K8s.ResourceClasses.Pod.useList).mockReturnValue([[{ jsonData: makePluginPod('dp-0') }], null] as any);
+    vi.mocked(ApiProxy.request).mockResolvedValue({ items: [] });
+    const { result } = renderHook(() => useAmdGpuContext(), { wrapper: Wrapper });
+    await waitFor(() => expect(result.current.loading).toBe(false));
+    expect(result.current.pluginPods.map((p: any) => p.metadata.name)).toEqual(['dp-0']);
+    expect(result.current.pluginInstalled).toBe(true);
+    const paths = vi.mocked(ApiProxy.request).mock.calls.map(c => String(c[0]));
+    expect(paths.every(p => p.indexOf('deviceconfigs') >= 0)).toBe(true);
+  });
+
+  it('refresh() re-issues the CRD request', async () => {
     vi.mocked(K8s.ResourceClasses.Node.useList).mockReturnValue([[], null] as any);
     vi.mocked(K8s.ResourceClasses.Pod.useList).mockReturnValue([[], null] as any);
     vi.mocked(ApiProxy.request).mockResolvedValue({ items: [] });
