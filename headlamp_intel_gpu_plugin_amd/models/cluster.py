@@ -27,6 +27,8 @@ import hashlib
 from typing import Dict, List, Optional
 
 GPUS_PER_NODE = 8
+#: devices per MI355X board in each compute-partition mode (src/api/amdgpu.js COMPUTE_PARTITIONS)
+COMPUTE_PARTITIONS = {"SPX": 1, "DPX": 2, "QPX": 4, "CPX": 8}
 HBM_BYTES = 294896 * 2**20  # 288 GiB less 16 MiB, as the device reports it (309,220,868,096 B)
 OPERATOR_NS = "kube-amd-gpu"
 NFD_LABEL = "feature.node.kubernetes.io/amd-gpu"
@@ -205,11 +207,14 @@ class SyntheticCluster:
                     "amd.com/gpu.simd-count": "1024",
                     "amd.com/gpu.driver-version": "6.12.12",
                 })
-            capacity = {"cpu": "256", "memory": "3Ti", "pods": "110", "amd.com/gpu": str(s.gpus_per_node)}
+            devices = s.gpus_per_node
             if s.partition:
                 cp, mp = s.partition.split("/")
                 labels["amd.com/compute-partitioning-mode"] = cp
                 labels["amd.com/memory-partitioning-mode"] = mp
+                # Each MI355X (8 XCDs) exposes one device per compute partition.
+                devices *= COMPUTE_PARTITIONS.get(cp.upper(), 1)
+            capacity = {"cpu": "256", "memory": "3Ti", "pods": "110", "amd.com/gpu": str(devices)}
             self.nodes.append(_node(name, labels, capacity, age_days=14))
         self._operator_objects()
         self._workloads()

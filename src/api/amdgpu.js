@@ -305,13 +305,50 @@ export function getGpuResources(resources) {
   return out;
 }
 
-/** Whole GPUs on the node (`amd.com/gpu` capacity). */
+/** True for resources that schedule GPU compute: `amd.com/gpu` and partition resources. */
+export function isDeviceResource(key) {
+  return key === AMD_GPU_RESOURCE || AMD_PARTITION_RESOURCE_RE.test(key);
+}
+
+function deviceSum(resources) {
+  if (!isObject(resources)) return 0;
+  let n = 0;
+  const keys = Object.keys(resources);
+  for (let i = 0; i < keys.length; i++) if (isDeviceResource(keys[i])) n += parseCount(resources[keys[i]]);
+  return n;
+}
+
+/**
+ * Schedulable GPU devices on the node: `amd.com/gpu` plus partition
+ * resources (`amd.com/cpx_nps4` … in the device plugin's mixed naming). On
+ * an SPX node this is the number of MI355X boards; on a partitioned node it
+ * is the number of partitions (see getNodePhysicalGpuCount).
+ */
 export function getNodeGpuCount(node) {
-  return parseCount(get(node, ['status', 'capacity', AMD_GPU_RESOURCE], 0));
+  return deviceSum(get(node, ['status', 'capacity'], null));
 }
 
 export function getNodeGpuAllocatable(node) {
-  return parseCount(get(node, ['status', 'allocatable', AMD_GPU_RESOURCE], 0));
+  return deviceSum(get(node, ['status', 'allocatable'], null));
+}
+
+/**
+ * Compute partitions per MI355X in each mode: the chip has 8 XCDs, so CPX
+ * exposes 8 devices per board, QPX 4, DPX 2, SPX 1.
+ */
+export const COMPUTE_PARTITIONS = Object.freeze({ SPX: 1, DPX: 2, QPX: 4, CPX: 8 });
+
+/** Devices per physical GPU on this node (1 unless the labeller reports a partition mode). */
+export function partitionsPerGpu(node) {
+  const labels = labelsOf(node);
+  const cp = labels[LABEL_COMPUTE_PARTITION] || labellerValue(node, 'compute-partitioning-mode');
+  return (cp && COMPUTE_PARTITIONS[String(cp).toUpperCase()]) || 1;
+}
+
+/** MI355X boards on the node: devices ÷ partitions per board. */
+export function getNodePhysicalGpuCount(node) {
+  const d = getNodeGpuCount(node);
+  return d > 0 ? Math.ceil(d / partitionsPerGpu(node)) : 0;
 }
 
 /** Partition resources (`amd.com/cpx_nps4` …) summed, for nodes in mixed naming mode. */
@@ -509,9 +546,12 @@ export function getPodGpuDemand(pod) {
 }
 
 /** Whole GPUs the pod holds (`amd.com/gpu`). */
+/** GPU devices the pod holds: `amd.com/gpu` plus partition resources. */
 export function getPodGpuCount(pod) {
   const d = getPodGpuDemand(pod);
-  return d[AMD_GPU_RESOURCE] || 0;
+  let n = 0;
+  for (const k in d) if (isDeviceResource(k)) n += d[k];
+  return n;
 }
 
 /** String map of the pod's effective AMD demand (API-compatible with the reference's requests map). */
@@ -667,6 +707,9 @@ export function buildClusterIndex(gpuNodes, gpuPods) {
   let inUse = 0;
   let readyNodes = 0;
   let partitions = 0;
+  let physicalGpus = 0;
+  let hbmBytes = 0;
+  let hbmAllocatedBytes = 0;
   const phases = { Running: 0, Pending: 0, Succeeded: 0, Failed: 0, Other: 0 };
   for (let i = 0; i < gpuNodes.length; i++) {
     const n = gpuNodes[i];
@@ -674,11 +717,18 @@ export function buildClusterIndex(gpuNodes, gpuPods) {
     const cap = getNodeGpuCount(n);
     const alloc = getNodeGpuAllocatable(n);
     const ready = isNodeReady(n);
+    const pp = partitionsPerGpu(n);
+    const phys = cap > 0 ? Math.ceil(cap / pp) : 0;
     capacity += cap;
     allocatable += alloc;
     partitions += getNodePartitionCount(n);
+    physicalGpus += phys;
+    hbmBytes += phys * MI355X.hbmBytes;
     if (ready) readyNodes++;
-    nodeStats[name] = { capacity: cap, allocatable: alloc, inUse: 0, pods: 0, ready: ready };
+    nodeStats[name] = {
+      capacity: cap, allocatable: alloc, inUse: 0, pods: 0, ready: ready,
+      physicalGpus: phys, partitionsPerGpu: pp,
+    };
     podsByNode[name] = [];
   }
   for (let i = 0; i < gpuPods.length; i++) {
@@ -699,6 +749,8 @@ export function buildClusterIndex(gpuNodes, gpuPods) {
       const g = getPodGpuCount(p);
       st.inUse += g;
       inUse += g;
+      // A partition holds its share of the board's HBM.
+      hbmAllocatedBytes += (g * MI355X.hbmBytes) / st.partitionsPerGpu;
     }
   }
   return {
@@ -712,6 +764,9 @@ export function buildClusterIndex(gpuNodes, gpuPods) {
       inUse: inUse,
       free: Math.max(0, allocatable - inUse),
       partitions: partitions,
+      physicalGpus: physicalGpus,
+      hbmBytes: hbmBytes,
+      hbmAllocatedBytes: hbmAllocatedBytes,
       utilizationPct: pct(inUse, allocatable),
     },
     phases: phases,

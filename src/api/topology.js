@@ -12,10 +12,14 @@
  * exact; otherwise they are filled in pod order and flagged `inferred`.
  */
 
-import { MI355X, getNodeGpuCount, getPodGpuCount, get } from './amdgpu.js';
+import { MI355X, getNodeGpuCount, getPodGpuCount, get, partitionsPerGpu } from './amdgpu.js';
 
 /**
- * @typedef {{ index: number, pod: string|null, namespace: string|null, inferred: boolean }} GpuSlot
+ * One schedulable device. On a partitioned node (DPX/QPX/CPX) device `index`
+ * is partition `partition` of board `board`; otherwise board === index and
+ * partition is null.
+ * @typedef {{ index: number, board: number, partition: number|null, pod: string|null, namespace: string|null,
+ *             inferred: boolean }} GpuSlot
  */
 
 /**
@@ -23,12 +27,17 @@ import { MI355X, getNodeGpuCount, getPodGpuCount, get } from './amdgpu.js';
  * @param {any[]} podsOnNode  GPU pods bound to the node
  * @param {Array<{gpu: string, pod?: string|null, namespace?: string|null}>} [perGpuOwners]
  *        exporter-derived owners keyed by gpu index (as string)
- * @returns {{ slots: GpuSlot[], exact: boolean }}
+ * @returns {{ slots: GpuSlot[], exact: boolean, partitionsPerGpu: number }}
  */
 export function buildGpuSlots(node, podsOnNode, perGpuOwners) {
   const n = getNodeGpuCount(node) || 0;
+  const pp = partitionsPerGpu(node);
   const slots = [];
-  for (let i = 0; i < n; i++) slots.push({ index: i, pod: null, namespace: null, inferred: false });
+  for (let i = 0; i < n; i++) {
+    slots.push({
+      index: i, board: Math.floor(i / pp), partition: pp > 1 ? i % pp : null, pod: null, namespace: null, inferred: false,
+    });
+  }
   if (perGpuOwners && perGpuOwners.length) {
     for (let i = 0; i < perGpuOwners.length; i++) {
       const o = perGpuOwners[i];
@@ -38,7 +47,7 @@ export function buildGpuSlots(node, podsOnNode, perGpuOwners) {
         slots[idx].namespace = o.namespace || null;
       }
     }
-    return { slots: slots, exact: true };
+    return { slots: slots, exact: true, partitionsPerGpu: pp };
   }
   let next = 0;
   for (let p = 0; p < podsOnNode.length; p++) {
@@ -52,7 +61,7 @@ export function buildGpuSlots(node, podsOnNode, perGpuOwners) {
       slots[next].inferred = true;
     }
   }
-  return { slots: slots, exact: false };
+  return { slots: slots, exact: false, partitionsPerGpu: pp };
 }
 
 /**

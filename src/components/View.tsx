@@ -94,7 +94,14 @@ function Slots({ b }: { b: IR }) {
       <div style={{ fontSize: '13px', marginBottom: '6px', color: 'var(--mui-palette-text-secondary)' }}>
         Per-GPU allocation{b.exact ? '' : ' (inferred from pod order — exporter pod labels unavailable)'}
       </div>
-      <div style={{ display: 'grid', gridTemplateColumns: 'repeat(8, minmax(0, 1fr))', gap: '4px' }}>
+      <div
+        style={{
+          display: 'grid',
+          // one row per board on partitioned nodes (up to 8 partitions each)
+          gridTemplateColumns: `repeat(${Math.min(8, b.partitionsPerGpu > 1 ? b.partitionsPerGpu : 8)}, minmax(0, 1fr))`,
+          gap: '4px',
+        }}
+      >
         {b.slots.map((s: IR) => (
           <div
             key={s.index}
@@ -112,7 +119,7 @@ function Slots({ b }: { b: IR }) {
               opacity: s.inferred ? 0.8 : 1,
             }}
           >
-            GPU {s.index}
+            {s.partition === null || s.partition === undefined ? `GPU ${s.index}` : `GPU ${s.board}·${s.partition}`}
             <br />
             {s.pod || 'free'}
           </div>

@@ -72,7 +72,7 @@ function renderBlock(b) {
         b.slots
           .map(function (s) {
             return '<li data-gpu="' + s.index + '"' + (s.pod ? ' data-pod="' + esc(s.pod) + '"' : '') + '>' +
-              'GPU ' + s.index + ': ' + (s.pod ? esc(s.pod) + (s.inferred ? ' (inferred)' : '') : 'free') + '</li>';
+              'GPU ' + (s.partition === null || s.partition === undefined ? s.index : s.board + '·' + s.partition) + ': ' + (s.pod ? esc(s.pod) + (s.inferred ? ' (inferred)' : '') : 'free') + '</li>';
           })
           .join('') +
         '</ol>'

@@ -43,7 +43,9 @@ import {
   getGpuResources,
   getNodeGpuCount,
   getNodeGpuModel,
+  getNodePhysicalGpuCount,
   getPodGpuCount,
+  getPodGpuDemand,
   getPodRestarts,
   gpuContainers,
   gpuInitContainers,
@@ -268,7 +270,8 @@ function overviewItems(ctx, now) {
   if (t.nodes > 0) nodeRows.push(row('GPU Model', MI355X.product + ' (' + MI355X.arch + ')'));
   if (t.capacity > 0) {
     nodeRows.push(row('Total GPU Devices', String(t.capacity)));
-    nodeRows.push(row('Total HBM', formatBytes(t.capacity * MI355X.hbmBytes) + ' (' + MI355X.hbmLabel + ' per GPU)'));
+    if (t.physicalGpus !== t.capacity) nodeRows.push(row('Physical GPUs', String(t.physicalGpus)));
+    nodeRows.push(row('Total HBM', formatBytes(t.hbmBytes) + ' (' + MI355X.hbmLabel + ' per GPU)'));
   }
   if (t.partitions > 0) nodeRows.push(row('GPU Partitions', String(t.partitions)));
   nodeBlocks.push(kv(nodeRows));
@@ -290,7 +293,7 @@ function overviewItems(ctx, now) {
           row('Allocatable', String(t.allocatable)),
           row('In Use', String(t.inUse)),
           row('Free', status(t.free > 0 ? 'success' : 'warning', t.free)),
-          row('HBM Allocated', formatBytes(t.inUse * MI355X.hbmBytes)),
+          row('HBM Allocated', formatBytes(t.hbmAllocatedBytes)),
         ]),
       ])
     );
@@ -432,7 +435,7 @@ function devicePluginsItems(ctx, now) {
 /** Per-GPU allocation strip block. */
 export function slotsBlock(node, podsOnNode, owners) {
   const s = buildGpuSlots(node, podsOnNode, owners);
-  return { t: 'slots', slots: s.slots, exact: s.exact };
+  return { t: 'slots', slots: s.slots, exact: s.exact, partitionsPerGpu: s.partitionsPerGpu };
 }
 
 /** xGMI neighbour matrix block; `measuredTopology` when link hops came from the exporter. */
@@ -453,8 +456,9 @@ function nodeCardRows(node, podsOnNode, stats, now) {
     row('GPU Model', model.product),
   ];
   if (count > 0) {
-    rows.push(row('GPU Devices (amd.com/gpu)', String(count)));
-    rows.push(row('HBM', formatBytes(count * MI355X.hbmBytes) + ' (' + count + ' × ' + model.vram + ')'));
+    const phys = getNodePhysicalGpuCount(node);
+    rows.push(row('GPU Devices (amd.com/gpu)', phys !== count ? count + ' (' + phys + ' × ' + model.shortName + ' in ' + model.computePartition + ')' : String(count)));
+    rows.push(row('HBM', formatBytes(phys * MI355X.hbmBytes) + ' (' + phys + ' × ' + model.vram + ')'));
   }
   for (const k in cap) rows.push(row(formatGpuResourceName(k) + ' (capacity)', cap[k]));
   for (const k in alloc) rows.push(row(formatGpuResourceName(k) + ' (allocatable)', alloc[k]));
@@ -503,7 +507,7 @@ export function nodesView(ctx, opts) {
         const count = getNodeGpuCount(n);
         if (count > 0) {
           blocks.push(slotsBlock(n, pods, own));
-          blocks.push(matrixBlock(count, xg, lk));
+          blocks.push(matrixBlock(getNodePhysicalGpuCount(n), xg, lk));
         }
         return section(name, blocks, n.metadata.uid || name);
       })
@@ -892,7 +896,8 @@ function nodeDetailSection(raw, name, cap, alloc, podsOnNode, loading, own, xg, 
   for (const k in cap) rows.push(row(formatGpuResourceName(k) + ' (capacity)', cap[k]));
   for (const k in alloc) rows.push(row(formatGpuResourceName(k) + ' (allocatable)', alloc[k]));
   const count = getNodeGpuCount(raw);
-  if (count > 0) rows.push(row('HBM', formatBytes(count * MI355X.hbmBytes)));
+  const phys = getNodePhysicalGpuCount(raw);
+  if (count > 0) rows.push(row('HBM', formatBytes(phys * MI355X.hbmBytes)));
   if (allocatable > 0) rows.push(row('GPU Allocation', status(pctToStatus(p), inUse + '/' + allocatable + ' (' + p + '%)')));
   rows.push(
     row(
@@ -903,7 +908,7 @@ function nodeDetailSection(raw, name, cap, alloc, podsOnNode, loading, own, xg, 
   const blocks = [kv(rows)];
   if (count > 0) {
     blocks.push(slotsBlock(raw, podsOnNode, own));
-    blocks.push(matrixBlock(count, xg, lk));
+    blocks.push(matrixBlock(phys, xg, lk));
   }
   return section('AMD GPU', blocks);
 }
@@ -948,13 +953,19 @@ function podDetailSection(raw) {
   const phase = get(raw, ['status', 'phase'], null);
   const phaseStatus = phase === 'Running' || phase === 'Succeeded' ? 'success' : phase === 'Pending' ? 'warning' : 'error';
   const gpus = getPodGpuCount(raw);
+  const whole = getPodGpuDemand(raw)[AMD_GPU_RESOURCE] === gpus;
   return section('AMD GPU Resources', [
     kv(
       [
         row('Phase', status(phaseStatus, phase || 'Unknown')),
         row('Scheduled Node', get(raw, ['spec', 'nodeName'], '—')),
         row('GPU Containers', String(all.length)),
-        row('GPUs (effective)', gpus > 0 ? gpus + ' × ' + MI355X.shortName + ' (' + formatBytes(gpus * MI355X.hbmBytes) + ' HBM)' : '—'),
+        row(
+          'GPUs (effective)',
+          gpus === 0 ? '—'
+            : whole ? gpus + ' × ' + MI355X.shortName + ' (' + formatBytes(gpus * MI355X.hbmBytes) + ' HBM)'
+              : gpus + ' GPU device' + (gpus === 1 ? '' : 's') + ' (partitions)'
+        ),
       ].concat(rows)
     ),
   ]);
@@ -976,7 +987,9 @@ export function nodeColumns() {
     const key = resource && typeof resource === 'object' ? resource : null;
     if (cache && key && cache.has(key)) return cache.get(key);
     const raw = unwrapKubeObject(resource);
-    const v = isAmdGpuNode(raw) ? { raw: raw, count: getNodeGpuCount(raw), model: getNodeGpuModel(raw) } : null;
+    const v = isAmdGpuNode(raw)
+      ? { raw: raw, count: getNodeGpuCount(raw), physical: getNodePhysicalGpuCount(raw), model: getNodeGpuModel(raw) }
+      : null;
     if (cache && key) cache.set(key, v);
     return v;
   }
@@ -999,7 +1012,7 @@ export function nodeColumns() {
       label: 'GPU HBM',
       getter: function (resource) {
         const i = info(resource);
-        return i && i.count > 0 ? formatBytes(i.count * MI355X.hbmBytes) : '—';
+        return i && i.count > 0 ? formatBytes(i.physical * MI355X.hbmBytes) : '—';
       },
     },
   ];

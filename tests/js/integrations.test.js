@@ -8,6 +8,14 @@ import { nodeColumns, nodeDetailView, podDetailView } from '../../src/view/pages
 import { findSection, firstBlock, rowNames, rowValue, text } from '../../src/view/ir.js';
 import { buildGpuSlots, buildXgmiMatrix, isFullMesh } from '../../src/api/topology.js';
 import { NOW, makeContext, makeGpuNode, makeGpuPod, makeNode, makePlainPod } from './fixtures.js';
+import {
+  MI355X,
+  buildClusterIndex,
+  getNodeGpuCount,
+  getNodePhysicalGpuCount,
+  getPodGpuCount,
+  partitionsPerGpu,
+} from '../../src/api/amdgpu.js';
 
 describe('nodeDetailView', () => {
   const node = makeGpuNode('g0');
@@ -193,9 +201,50 @@ describe('topology', () => {
   it('uses exporter owners when present', () => {
     const s = buildGpuSlots(makeGpuNode('g'), [], [{ gpu: '7', pod: 'x', namespace: 'ns' }, { gpu: '9', pod: 'bad' }]);
     expect(s.exact).toBe(true);
-    expect(s.slots[7]).toEqual({ index: 7, pod: 'x', namespace: 'ns', inferred: false });
+    expect(s.slots[7]).toEqual({ index: 7, board: 7, partition: null, pod: 'x', namespace: 'ns', inferred: false });
   });
 });
 
 void NOW;
 void findSection;
+
+describe('partitioned MI355X nodes (CPX: 8 devices per board)', () => {
+  function cpxNode(name) {
+    const n = makeGpuNode(name, { partition: 'cpx/nps2' });
+    n.status.capacity['amd.com/gpu'] = '64';
+    n.status.allocatable['amd.com/gpu'] = '64';
+    return n;
+  }
+  it('counts boards, not partitions, for HBM and the xGMI matrix', () => {
+    const n = cpxNode('c0');
+    expect(getNodeGpuCount(n)).toBe(64);
+    expect(partitionsPerGpu(n)).toBe(8);
+    expect(getNodePhysicalGpuCount(n)).toBe(8);
+    const s = nodeDetailView(n, makeContext({ nodes: [n] }));
+    expect(rowValue(s, 'HBM')).toBe('2.25 TiB');
+    const m = s.blocks.find((b) => b.t === 'matrix');
+    expect(m.matrix.size).toBe(8);
+  });
+  it('labels each partition slot with its board', () => {
+    const n = cpxNode('c1');
+    const slots = buildGpuSlots(n, [], []).slots;
+    expect(slots).toHaveLength(64);
+    expect(slots[9].board).toBe(1);
+    expect(slots[9].partition).toBe(1);
+  });
+  it('accounts HBM allocated per partition share', () => {
+    const n = cpxNode('c2');
+    const pod = makeGpuPod('p', { node: 'c2', gpus: 4 });
+    const idx = buildClusterIndex([n], [pod]);
+    expect(idx.totals.physicalGpus).toBe(8);
+    expect(idx.totals.hbmAllocatedBytes).toBe((4 * MI355X.hbmBytes) / 8);
+  });
+  it('counts mixed-strategy partition resources as devices', () => {
+    const n = makeGpuNode('m0', { partition: 'cpx/nps4' });
+    delete n.status.capacity['amd.com/gpu'];
+    n.status.capacity['amd.com/cpx_nps4'] = '16';
+    expect(getNodeGpuCount(n)).toBe(16);
+    expect(getNodePhysicalGpuCount(n)).toBe(2);
+    expect(getPodGpuCount(makeGpuPod('q', { resource: 'amd.com/cpx_nps4', gpus: 3 }))).toBe(3);
+  });
+});

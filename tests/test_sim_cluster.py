@@ -81,6 +81,7 @@ def test_partition_labels():
     c = SyntheticCluster(ClusterSpec(gpu_nodes=1, partition="cpx/nps4"))
     labels = c.gpu_nodes[0]["metadata"]["labels"]
     assert labels["amd.com/compute-partitioning-mode"] == "cpx"
+    assert c.gpu_nodes[0]["status"]["capacity"]["amd.com/gpu"] == "64"  # 8 boards x 8 CPX partitions
 
 
 # ---------------------------------------------------------------------------
