@@ -21,8 +21,8 @@
 //                   for shapes the 256² tiles do not cover or fill.
 //                 The register-staged kernels fetch tile k+1 into registers
 //                 while tile k is consumed, write it to the other LDS buffer
-//                 (rows padded to 144 B: conflict-free ds_read_b128), one
-//                 barrier per K-step. All three run each MFMA cluster at
+//                 (128-B rows, XOR-swizzled 16-B chunks: conflict-free
+//                 ds_read_b128), one barrier per K-step. All three run each MFMA cluster at
 //                 s_setprio 1 and use a bijective XCD-aware block remap with
 //                 8-row tile grouping so blocks sharing an XCD's L2 work on
 //                 neighbouring tiles.
@@ -50,7 +50,11 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BK = 64;
-constexpr int LDS_STRIDE = BK + 8;  // bf16 elements per LDS row (144 B)
+// LDS rows are 128 B (no padding). 16-byte chunk c of row r is stored at
+// chunk c ^ (r & 7): the 16 lanes of each ds_read_b128 lane group then hit
+// 16 distinct 16-byte slots (the 144-B padded layout measured 33-37 % of LDS
+// cycles in bank conflicts, profiles/r1_pmc_kernels.md).
+constexpr int LDS_STRIDE = BK;
 
 __device__ __forceinline__ uint16_t f32_to_bf16_rne(float f) {
   uint32_t u = __builtin_bit_cast(uint32_t, f);
@@ -108,6 +112,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_nt(const uint16_t* __r
   // Chunk p of this thread: row srow + p*kRowStep, 16-byte column scol.
   const int srow = tid >> 3;
   const int scol = (tid & 7) * 8;
+  const int sswz = ((tid & 7) ^ (srow & 7)) * 8;  // swizzled LDS column of this thread's chunk
   const uint16_t* ga = A + static_cast<size_t>(m0 + srow) * K + scol;
   const uint16_t* gb = B + static_cast<size_t>(n0 + srow) * K + scol;
   const size_t gstep = static_cast<size_t>(T::kRowStep) * K;
@@ -126,7 +131,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_nt(const uint16_t* __r
   }
 #define GEMM_STORE(buf)                                                                                 \
   {                                                                                                     \
-    uint16_t* la_ = lds + (buf) * (BM + BN) * LDS_STRIDE + srow * LDS_STRIDE + scol;                    \
+    uint16_t* la_ = lds + (buf) * (BM + BN) * LDS_STRIDE + srow * LDS_STRIDE + sswz;                    \
     uint16_t* lb_ = la_ + BM * LDS_STRIDE;                                                              \
     _Pragma("unroll") for (int p = 0; p < T::kCa; ++p)                                                  \
       *reinterpret_cast<u32x4*>(la_ + p * T::kRowStep * LDS_STRIDE) = ra[p];                            \
@@ -143,6 +148,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_nt(const uint16_t* __r
   // and B[k 8(l>>4)..+7][col l&15].
   const int frow = lane & 15;
   const int fk = (lane >> 4) * 8;
+  const int fswz = frow & 7;  // every fragment row ≡ frow (mod 16)
   const int arow = wr * (BM / WM) + frow;
   const int brow = wc * (BN / WN) + frow;
 
@@ -157,10 +163,10 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_nt(const uint16_t* __r
       bf16x8 af[T::kTm], bfr[T::kTn];
 #pragma unroll
       for (int i = 0; i < T::kTm; ++i)
-        af[i] = *reinterpret_cast<const bf16x8*>(la + (arow + i * 16) * LDS_STRIDE + kk + fk);
+        af[i] = *reinterpret_cast<const bf16x8*>(la + (arow + i * 16) * LDS_STRIDE + ((((kk + fk) >> 3) ^ fswz) << 3));
 #pragma unroll
       for (int j = 0; j < T::kTn; ++j)
-        bfr[j] = *reinterpret_cast<const bf16x8*>(lb + (brow + j * 16) * LDS_STRIDE + kk + fk);
+        bfr[j] = *reinterpret_cast<const bf16x8*>(lb + (brow + j * 16) * LDS_STRIDE + ((((kk + fk) >> 3) ^ fswz) << 3));
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < T::kTm; ++i)
