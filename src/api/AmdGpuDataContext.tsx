@@ -137,7 +137,7 @@ export const PROMETHEUS_UNREACHABLE =
  * wait for the cluster context to finish loading: the two are independent
  * and fetched in parallel. Stale responses are dropped on unmount / re-run.
  */
-export function useGpuMetrics(enabled = true): GpuMetricsState {
+export function useGpuMetrics(enabled = true, withSeries = true): GpuMetricsState {
   const source = metricsSourceFor(clusterKey());
   const settings = loadSettings();
   const [state, setState] = useState<Omit<GpuMetricsState, 'refresh'>>({
@@ -152,7 +152,10 @@ export function useGpuMetrics(enabled = true): GpuMetricsState {
     if (!enabled) return;
     let cancelled = false;
     setState(s => ({ ...s, fetching: true, fetchError: null }));
-    Promise.all([source.fetchGpuMetrics(), source.fetchSeries(settings.seriesMinutes * 60, seriesStepSec(settings))])
+    Promise.all([
+      source.fetchGpuMetrics(),
+      withSeries ? source.fetchSeries(settings.seriesMinutes * 60, seriesStepSec(settings)) : Promise.resolve(null),
+    ])
       .then(([metrics, series]) => {
         if (cancelled) return;
         setState({ metrics, series, fetching: false, fetchError: metrics ? null : PROMETHEUS_UNREACHABLE });
@@ -164,7 +167,7 @@ export function useGpuMetrics(enabled = true): GpuMetricsState {
     return () => {
       cancelled = true;
     };
-  }, [enabled, seq, source, settings.seriesMinutes]);
+  }, [enabled, withSeries, seq, source, settings.seriesMinutes]);
 
   useEffect(() => {
     if (!enabled) return;

@@ -550,6 +550,71 @@ function ownersByNode(metrics) {
   return out;
 }
 
+let lastAssign = {};
+
+function sameAssign(a, b) {
+  if (!a || !b || a.length !== b.length) return false;
+  for (let i = 0; i < a.length; i++) if (a[i] !== b[i]) return false;
+  return true;
+}
+
+/**
+ * "namespace/pod" → the GPUs the exporter attributes to that pod (its
+ * pod/namespace labels), as GPU objects of the metrics snapshot. Kubernetes
+ * itself does not say which device a pod got; this is the exporter's view.
+ * A pod's array keeps its identity while its GPUs are the same objects
+ * (see the metrics client's structural sharing), and the whole map keeps
+ * its identity while no pod's list changed.
+ */
+export function podGpuAssignments(metrics) {
+  if (!metrics || !metrics.gpus) return {};
+  if (assignCache && assignCache.has(metrics.gpus)) return assignCache.get(metrics.gpus);
+  const out = {};
+  for (let i = 0; i < metrics.gpus.length; i++) {
+    const g = metrics.gpus[i];
+    if (!g.pod) continue;
+    const k = (g.namespace || '') + '/' + g.pod;
+    if (!out[k]) out[k] = [];
+    out[k].push(g);
+  }
+  let same = Object.keys(out).length === Object.keys(lastAssign).length;
+  for (const k in out) {
+    if (sameAssign(lastAssign[k], out[k])) out[k] = lastAssign[k];
+    else same = false;
+  }
+  const res = same ? lastAssign : out;
+  lastAssign = res;
+  if (assignCache) assignCache.set(metrics.gpus, res);
+  return res;
+}
+const assignCache = typeof WeakMap === 'function' ? new WeakMap() : null;
+
+function assignedLines(gs) {
+  return lines(
+    gs.map(function (g) {
+      const parts = [];
+      if (g.powerWatts !== null && g.powerWatts !== undefined) parts.push(formatWatts(g.powerWatts));
+      if (g.gfxActivityPct !== null && g.gfxActivityPct !== undefined) parts.push(Math.round(g.gfxActivityPct) + '% GFX');
+      if (g.vramUsedBytes !== null && g.vramUsedBytes !== undefined) parts.push(formatBytes(g.vramUsedBytes) + ' HBM');
+      return { label: g.nodeName + ' GPU ' + g.gpu, text: parts.length ? parts.join(', ') : 'no telemetry' };
+    })
+  );
+}
+
+function assignedText(gs) {
+  if (!gs || gs.length === 0) return '—';
+  const byNode = {};
+  const order = [];
+  for (let i = 0; i < gs.length; i++) {
+    if (!byNode[gs[i].nodeName]) {
+      byNode[gs[i].nodeName] = [];
+      order.push(gs[i].nodeName);
+    }
+    byNode[gs[i].nodeName].push(gs[i].gpu);
+  }
+  return order.map(function (n) { return n + ': GPU ' + byNode[n].join(', '); }).join('; ');
+}
+
 function nodesHeadItems(ctx, now) {
   const items = [];
   if (ctx.error) items.push(errorSection(ctx.error));
@@ -626,13 +691,14 @@ export function gpuContainerLines(pod) {
 export function podsView(ctx, opts) {
   const now = nowOf(opts);
   if (ctx.loading && !ctx.lastUpdated) return page(null, null, [loader('Loading GPU pod data...')]);
-  const items = memo('pods', [ctx.gpuPods, ctx.index, ctx.error, ageKey(now)], function () {
-    return podsItems(ctx, now);
+  const assign = opts && opts.metrics ? podGpuAssignments(opts.metrics) : null;
+  const items = memo('pods', [ctx.gpuPods, ctx.index, ctx.error, assign, ageKey(now)], function () {
+    return podsItems(ctx, now, assign);
   });
   return page(BRAND + ' — Pods', refreshButton('Refresh pod data', ctx.refreshing), items);
 }
 
-function podsItems(ctx, now) {
+function podsItems(ctx, now, assign) {
   const items = [];
   if (ctx.error) items.push(errorSection(ctx.error));
   const pods = ctx.gpuPods;
@@ -663,16 +729,22 @@ function podsItems(ctx, now) {
     rows.push(row('GPUs Held', String(gpus)));
     items.push(section('Summary', [kv(rows)]));
 
+    // With exporter pod labels, show which physical GPUs each pod holds.
+    const exact = assign && Object.keys(assign).length > 0;
+    const cols = ['Name', 'Namespace', 'Node', 'Phase', 'GPU Resources', 'Restarts', 'Age'];
+    if (exact) cols.splice(5, 0, 'Assigned GPUs');
     items.push(
       section('All GPU Pods', [
         table(
-          ['Name', 'Namespace', 'Node', 'Phase', 'GPU Resources', 'Restarts', 'Age'],
+          cols,
           pods.map(function (p) {
             const phase = podPhase(p);
-            return [
+            const r = [
               podName(p), podNs(p), podNode(p), status(phaseToStatus(phase), phase), gpuContainerLines(p),
               restartsCell(p), formatAge(p.metadata.creationTimestamp, now),
             ];
+            if (exact) r.splice(5, 0, assignedText(assign[(p.metadata.namespace || '') + '/' + p.metadata.name]));
+            return r;
           }),
           pods.map(function (p) { return p.metadata.uid || (p.metadata.namespace + '/' + p.metadata.name); })
         ),
@@ -922,8 +994,18 @@ function nodeDetailSection(raw, name, cap, alloc, podsOnNode, loading, own, xg, 
  * an init-only GPU pod renders (reference quirk Q3), and the effective GPU
  * demand the scheduler uses is shown.
  */
-export function podDetailView(resource) {
+export function podDetailView(resource, opts) {
   const raw = unwrapKubeObject(resource);
+  const metrics = opts && opts.metrics ? opts.metrics : null;
+  if (metrics && raw && typeof raw === 'object' && raw.metadata) {
+    // Live telemetry of the GPUs this pod holds (exporter pod labels).
+    const gs = podGpuAssignments(metrics)[(raw.metadata.namespace || '') + '/' + raw.metadata.name];
+    if (gs) {
+      return memo('pod-detail:' + (raw.metadata.uid || raw.metadata.namespace + '/' + raw.metadata.name), [raw, gs], function () {
+        return podDetailSection(raw, gs);
+      });
+    }
+  }
   if (podDetailCache && raw && typeof raw === 'object') {
     if (podDetailCache.has(raw)) return podDetailCache.get(raw);
     const s = podDetailSection(raw);
@@ -933,7 +1015,7 @@ export function podDetailView(resource) {
   return podDetailSection(raw);
 }
 
-function podDetailSection(raw) {
+function podDetailSection(raw, assigned) {
   if (!isGpuRequestingPod(raw)) return null;
   const ics = gpuInitContainers(raw);
   const cs = gpuContainers(raw);
@@ -966,7 +1048,7 @@ function podDetailSection(raw) {
             : whole ? gpus + ' × ' + MI355X.shortName + ' (' + formatBytes(gpus * MI355X.hbmBytes) + ' HBM)'
               : gpus + ' GPU device' + (gpus === 1 ? '' : 's') + ' (partitions)'
         ),
-      ].concat(rows)
+      ].concat(assigned ? [row('Assigned GPUs', assignedLines(assigned))] : []).concat(rows)
     ),
   ]);
 }

@@ -9,6 +9,8 @@ import {
   devicePluginsView,
   nodesView,
   podsView,
+  podDetailView,
+  podGpuAssignments,
   metricsView,
   formatWindow,
   allocationBar,
@@ -297,6 +299,38 @@ describe('podsView', () => {
 });
 
 // ---------------------------------------------------------------------------
+describe('pod → GPU assignment (exporter pod labels)', () => {
+  const pods = [makeGpuPod('train', { node: 'g0', gpus: 2 }), makeGpuPod('idle', { node: 'g0', gpus: 1 })];
+  const ctx = makeContext({ nodes: [makeGpuNode('g0')], pods });
+  const gpu = (i, pod) => ({ nodeName: 'g0', gpu: String(i), pod, namespace: pod ? 'ml' : null, powerWatts: 1000 + i,
+    gfxActivityPct: 90, vramUsedBytes: 64 * 1024 ** 3 });
+  const metrics = { source: 'amd-exporter', gpus: [gpu(0, 'train'), gpu(1, 'train'), gpu(2, null)], xgmi: {}, links: {} };
+  it('adds an Assigned GPUs column when the exporter labels pods', () => {
+    const t = firstTable(findSection(podsView(ctx, { now: NOW, metrics }), 'All GPU Pods'));
+    expect(t.columns).toContain('Assigned GPUs');
+    const col = t.columns.indexOf('Assigned GPUs');
+    const trainRow = t.rows.find((r) => r[0] === 'train');
+    expect(trainRow[col]).toBe('g0: GPU 0, 1');
+    expect(t.rows.find((r) => r[0] === 'idle')[col]).toBe('—');
+  });
+  it('keeps the reference columns without exporter data', () => {
+    const t = firstTable(findSection(podsView(ctx, { now: NOW }), 'All GPU Pods'));
+    expect(t.columns).toEqual(['Name', 'Namespace', 'Node', 'Phase', 'GPU Resources', 'Restarts', 'Age']);
+  });
+  it('shows live telemetry of the held GPUs on the pod detail section', () => {
+    const s = podDetailView(pods[0], { metrics });
+    const v = rowValue(s, 'Assigned GPUs');
+    expect(v.t).toBe('lines');
+    expect(v.lines[0]).toEqual({ label: 'g0 GPU 0', text: '1000.0 W, 90% GFX, 64 GiB HBM' });
+    expect(rowValue(podDetailView(pods[1], { metrics }), 'Assigned GPUs')).toBeUndefined();
+  });
+  it('keeps assignment identity across snapshots with unchanged ownership', () => {
+    const a = podGpuAssignments(metrics);
+    const b = podGpuAssignments(Object.assign({}, metrics, { gpus: metrics.gpus.slice() }));
+    expect(b).toBe(a);
+  });
+});
+
 describe('metricsView', () => {
   const E = SERIES.exporter;
   function metrics(nodes, gpusPer) {
