@@ -111,7 +111,7 @@ function renderAll(ctx, mstate) {
     overview: overviewView(ctx),
     devicePlugins: devicePluginsView(ctx),
     nodes: nodesView(ctx, { metrics: mstate.metrics }),
-    pods: podsView(ctx),
+    pods: podsView(ctx, { metrics: mstate.metrics }),
     metrics: metricsView(ctx, mstate),
   };
   const rows = {};
@@ -129,7 +129,7 @@ function renderAll(ctx, mstate) {
     }
   }
   for (let i = 0; i < ctx.gpuPods.length; i++) {
-    const s = podDetailView(ctx.gpuPods[i]);
+    const s = podDetailView(ctx.gpuPods[i], { metrics: mstate.metrics });
     if (s) {
       detailSections++;
       htmlBytes += renderSection(s).length;
