@@ -166,17 +166,23 @@ export function createClusterStore(opts) {
   let memoIndex = buildClusterIndex([], []);
   let snapshot = null;
 
+  // The watch delivers a new list on every event anywhere in the cluster;
+  // the GPU subsets keep their identity unless a GPU node / pod actually
+  // changed (uid + resourceVersion), so churn of unrelated pods does not
+  // invalidate any memoised view downstream.
   function gpuNodes() {
     if (s.nodes !== memoNodesIn) {
       memoNodesIn = s.nodes;
-      memoGpuNodes = s.nodes ? filterAmdGpuNodes(s.nodes) : [];
+      const next = s.nodes ? filterAmdGpuNodes(s.nodes) : [];
+      memoGpuNodes = sameObjects(memoGpuNodes, next) ? memoGpuNodes : next;
     }
     return memoGpuNodes;
   }
   function gpuPods() {
     if (s.pods !== memoPodsIn) {
       memoPodsIn = s.pods;
-      memoGpuPods = s.pods ? filterGpuRequestingPods(s.pods) : [];
+      const next = s.pods ? filterGpuRequestingPods(s.pods) : [];
+      memoGpuPods = sameObjects(memoGpuPods, next) ? memoGpuPods : next;
     }
     return memoGpuPods;
   }

@@ -8,7 +8,7 @@ import { clearViewMemo, metricsView, nodesView, overviewView, podDetailView, pod
 import { renderSection } from '../../src/view/html.js';
 import { createClusterStore, sameObjects } from '../../src/api/clusterStore.js';
 import { DEVICE_CONFIG_LIST_PATH, PLUGIN_POD_QUERIES } from '../../src/api/amdgpu.js';
-import { NOW, makeContext, makeDeviceConfig, makeGpuNode, makeGpuPod, makePluginPod } from './fixtures.js';
+import { NOW, makeContext, makeDeviceConfig, makeGpuNode, makeGpuPod, makeNode, makePlainPod, makePluginPod } from './fixtures.js';
 
 describe('createMemo', () => {
   it('returns the cached value while deps are identical', () => {
@@ -107,6 +107,21 @@ describe('view memoisation', () => {
 });
 
 describe('structural sharing in the store', () => {
+  it('keeps the GPU pod / node lists when only unrelated pods change', () => {
+    const store = createClusterStore({ request: () => Promise.resolve({ items: [] }) });
+    const g = makeGpuPod('train', { node: 'g0' });
+    const n = makeGpuNode('g0');
+    store.setNodes([n], null);
+    store.setPods([g, makePlainPod('web-1')], null);
+    const a = store.getSnapshot();
+    store.setPods([g, makePlainPod('web-2'), makePlainPod('web-3')], null);
+    store.setNodes([n, makeNode('cpu-9')], null);
+    const b = store.getSnapshot();
+    expect(b.gpuPods).toBe(a.gpuPods);
+    expect(b.gpuNodes).toBe(a.gpuNodes);
+    expect(b.index).toBe(a.index);
+  });
+
   it('sameObjects compares uid + resourceVersion', () => {
     const a = [{ metadata: { uid: 'x', resourceVersion: '1' } }];
     expect(sameObjects(a, [{ metadata: { uid: 'x', resourceVersion: '1' } }])).toBe(true);
