@@ -361,6 +361,7 @@ async function serve(a) {
           renderAll(s.ctx(), s.mstate());
           lat.push(ms(process.hrtime(t0)));
           req = counter.n - before;
+          if (s.spans) out.trace = traceSummary(s.spans);
         }
         out.latencies = lat;
         out.requests = req;

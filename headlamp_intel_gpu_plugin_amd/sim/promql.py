@@ -45,7 +45,7 @@ class Series:
     or explicit samples appended with :meth:`push` (kept sorted, bounded).
     """
 
-    __slots__ = ("labels", "fn", "interval", "ts", "vs", "cap", "_key", "_json")
+    __slots__ = ("labels", "fn", "interval", "ts", "vs", "cap", "_key", "_json", "_memo")
 
     def __init__(self, labels: Labels, fn: Optional[Callable[[float], float]] = None,
                  interval: float = 15.0, cap: int = 4096):
@@ -57,6 +57,7 @@ class Series:
         self.cap = cap
         self._key = tuple(sorted(self.labels.items()))
         self._json = None
+        self._memo: Dict[float, float] = {}  # fn value per sample time (fn series are deterministic)
 
     def metric_json(self) -> str:
         """JSON of the label set (cached — series labels never change once stored)."""
@@ -77,13 +78,21 @@ class Series:
             del self.ts[:drop]
             del self.vs[:drop]
 
+    def _fn_at(self, ts: float) -> float:
+        v = self._memo.get(ts)
+        if v is None:
+            if len(self._memo) >= 4096:
+                self._memo.clear()
+            v = self._memo[ts] = self.fn(ts)
+        return v
+
     def samples(self, start: float, end: float) -> List[Tuple[float, float]]:
         """Samples with start < t <= end."""
         if self.fn is not None:
             iv = self.interval
             k0 = math.floor(start / iv) + 1
             k1 = math.floor(end / iv)
-            return [(k * iv, self.fn(k * iv)) for k in range(k0, k1 + 1)]
+            return [(k * iv, self._fn_at(k * iv)) for k in range(k0, k1 + 1)]
         lo = bisect.bisect_right(self.ts, start)
         hi = bisect.bisect_right(self.ts, end)
         return list(zip(self.ts[lo:hi], self.vs[lo:hi]))
@@ -92,7 +101,7 @@ class Series:
         """Latest sample within the lookback window ending at ``t``."""
         if self.fn is not None:
             k = math.floor(t / self.interval) * self.interval
-            return (k, self.fn(k))
+            return (k, self._fn_at(k))
         i = bisect.bisect_right(self.ts, t) - 1
         if i < 0 or t - self.ts[i] > LOOKBACK_S:
             return None
