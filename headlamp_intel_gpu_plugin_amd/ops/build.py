@@ -16,6 +16,7 @@ Rebuilds only when a source (or header) is newer than its output. Usage::
 """
 from __future__ import annotations
 
+import fcntl
 import glob
 import os
 import shutil
@@ -65,7 +66,7 @@ def _stale(name: str) -> bool:
     return any(os.path.exists(s) and os.path.getmtime(s) > t for s in _deps(name))
 
 
-def command(name: str) -> List[str]:
+def command(name: str, out: str = "") -> List[str]:
     spec = TARGETS[name]
     cmd = [hipcc(), "-O3", "-std=c++17", "-Wall", "-Wno-unused-function", f"-I{os.path.join(HERE, 'csrc')}"]
     if spec["kind"] == "ext":
@@ -73,25 +74,38 @@ def command(name: str) -> List[str]:
     if spec["hip"]:
         cmd += [f"--offload-arch={ARCH}", "-x", "hip", "-munsafe-fp-atomics"]
     cmd += [os.path.join(HERE, s) for s in spec["sources"]]
-    cmd += ["-o", so_path(name), f"-L{ROCM}/lib", "-lamdhip64", f"-Wl,-rpath,{ROCM}/lib"]
+    cmd += ["-o", out or so_path(name), f"-L{ROCM}/lib", "-lamdhip64", f"-Wl,-rpath,{ROCM}/lib"]
     return cmd
 
 
 def build(names=None, force: bool = False, verbose: bool = False) -> Dict[str, str]:
-    """Compile the given targets (default: all). Returns name → output path."""
+    """Compile the given targets (default: all). Returns name → output path.
+
+    Safe to call from several processes at once (one rank per GPU): each
+    target builds under an exclusive file lock into a temporary file that is
+    renamed into place, so no process ever loads a half-written library.
+    """
     out = {}
     for name in names or TARGETS:
         if not all(os.path.exists(os.path.join(HERE, s)) for s in TARGETS[name]["sources"]):
             continue
+        target = so_path(name)
         if force or _stale(name):
-            os.makedirs(os.path.dirname(so_path(name)), exist_ok=True)
-            cmd = command(name)
-            if verbose:
-                print(" ".join(cmd), file=sys.stderr)
-            r = subprocess.run(cmd, capture_output=True, text=True)
-            if r.returncode != 0:
-                raise RuntimeError(f"building {name} failed:\n{r.stderr[-4000:]}")
-        out[name] = so_path(name)
+            os.makedirs(os.path.dirname(target), exist_ok=True)
+            with open(target + ".lock", "w") as lock:
+                fcntl.flock(lock, fcntl.LOCK_EX)
+                if force or _stale(name):  # another process may have built it meanwhile
+                    tmp = f"{target}.tmp{os.getpid()}"
+                    cmd = command(name, tmp)
+                    if verbose:
+                        print(" ".join(cmd), file=sys.stderr)
+                    r = subprocess.run(cmd, capture_output=True, text=True)
+                    if r.returncode != 0:
+                        if os.path.exists(tmp):
+                            os.unlink(tmp)
+                        raise RuntimeError(f"building {name} failed:\n{r.stderr[-4000:]}")
+                    os.replace(tmp, target)
+        out[name] = target
     return out
 
 

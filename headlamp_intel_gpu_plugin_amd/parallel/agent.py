@@ -97,9 +97,11 @@ class ExporterProcess:
                  topology: bool = True):
         from ..ops import build as native_build
 
-        exe = native_build.so_path("amdgpu-exporter")
-        if not os.path.exists(exe):
-            raise RuntimeError(f"amdgpu-exporter not built ({exe}); run `python __graft_entry__.py build`")
+        # Builds (under the build lock) only when missing or stale, e.g. on a
+        # box that received the sources without the in-tree binaries.
+        exe = native_build.build(["amdgpu-exporter"]).get("amdgpu-exporter", "")
+        if not exe or not os.path.exists(exe):
+            raise RuntimeError("amdgpu-exporter could not be built (hipcc / ROCm missing?)")
         self.cmd = [exe, "--port", "0", "--bind", "127.0.0.1", "--hostname", hostname]
         if device is not None:
             self.cmd += ["--device", str(device)]

@@ -49,3 +49,27 @@ def test_workload_rejects_cpu_tensors():
         workload.gemm_bf16_nt(a, a)
     with pytest.raises(TypeError):
         workload.gemm_bf16_nt(a.float(), a.float())
+
+
+def test_concurrent_builds_do_not_clobber_each_other(tmp_path):
+    # One rank per GPU may all find an extension stale at start-up; the build
+    # lock + atomic rename must leave one complete, loadable library.
+    import subprocess
+    import sys
+
+    from headlamp_intel_gpu_plugin_amd.ops import build as b
+
+    so = b.so_path("_amdgpu_probe")
+    if os.path.exists(so):
+        os.utime(so, (0, 0))  # make it stale for every process below
+    code = ("from headlamp_intel_gpu_plugin_amd.ops import build as b; "
+            "b.build(['_amdgpu_probe']); "
+            "import importlib; m = importlib.import_module('headlamp_intel_gpu_plugin_amd.ops._amdgpu_probe'); "
+            "print('ok', m.device_count() >= 0)")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    procs = [subprocess.Popen([sys.executable, "-c", code], cwd=root, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                              text=True) for _ in range(3)]
+    outs = [p.communicate(timeout=600) for p in procs]
+    assert all(p.returncode == 0 for p in procs), [o[1][-500:] for o in outs]
+    assert all("ok True" in o[0] for o in outs)
+    assert not [f for f in os.listdir(os.path.dirname(so)) if ".tmp" in f]
