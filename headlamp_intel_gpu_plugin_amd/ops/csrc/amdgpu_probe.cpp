@@ -108,6 +108,9 @@ PyObject* py_sample(PyObject*, PyObject* args) {
   put("temp_edge_c", s.temp_edge_c);
   put("temp_junction_c", s.temp_junction_c);
   put("temp_mem_c", s.temp_mem_c);
+  put("temp_junction_slowdown_c", s.temp_junction_slowdown_c);
+  put("temp_junction_shutdown_c", s.temp_junction_shutdown_c);
+  put("temp_mem_slowdown_c", s.temp_mem_slowdown_c);
   put("sclk_mhz", s.sclk_mhz);
   put("mclk_mhz", s.mclk_mhz);
   put("gfx_busy_pct", s.gfx_busy_pct);

@@ -55,6 +55,9 @@ struct Sample {
   double power_w = NAN;      // average (or instantaneous) board power
   double power_cap_w = NAN;  // power1_cap
   double temp_edge_c = NAN, temp_junction_c = NAN, temp_mem_c = NAN;
+  // hwmon tempN_crit / tempN_emergency: the slowdown and shutdown thresholds
+  // (an MI355X reads 100 / 112 °C junction, 115 / 125 °C HBM: amd-smi static).
+  double temp_junction_slowdown_c = NAN, temp_junction_shutdown_c = NAN, temp_mem_slowdown_c = NAN;
   double sclk_mhz = NAN, mclk_mhz = NAN;
   double gfx_busy_pct = NAN, mem_busy_pct = NAN;
   double vram_used_b = NAN, vram_total_b = NAN;
@@ -198,10 +201,22 @@ inline Sample sample_sysfs(const std::string& bdf) {
       std::string label;
       read_text(h + "/temp" + std::to_string(t) + "_label", &label);
       const double c = v / 1000.0;
-      if (label == "edge") s.temp_edge_c = c;
-      else if (label == "junction" || label == "hotspot") s.temp_junction_c = c;
-      else if (label == "mem") s.temp_mem_c = c;
-      else if (t == 1 && std::isnan(s.temp_edge_c)) s.temp_edge_c = c;
+      const std::string base = h + "/temp" + std::to_string(t);
+      double crit = NAN, emerg = NAN;
+      if (read_double(base + "_crit", &v)) crit = v / 1000.0;
+      if (read_double(base + "_emergency", &v)) emerg = v / 1000.0;
+      if (label == "edge") {
+        s.temp_edge_c = c;
+      } else if (label == "junction" || label == "hotspot") {
+        s.temp_junction_c = c;
+        s.temp_junction_slowdown_c = crit;
+        s.temp_junction_shutdown_c = emerg;
+      } else if (label == "mem") {
+        s.temp_mem_c = c;
+        s.temp_mem_slowdown_c = crit;
+      } else if (t == 1 && std::isnan(s.temp_edge_c)) {
+        s.temp_edge_c = c;
+      }
     }
     // clocks: Hz, freq1 = sclk, freq2 = mclk
     if (read_double(h + "/freq1_input", &v)) s.sclk_mhz = v / 1e6;
@@ -251,6 +266,9 @@ inline std::string render(const RenderOptions& opt) {
       {"gpu_edge_temperature", "edge temperature (C)"},
       {"gpu_junction_temperature", "junction temperature (C)"},
       {"gpu_memory_temperature", "HBM temperature (C)"},
+      {"gpu_junction_temperature_slowdown", "junction temperature at which the GPU throttles (C)"},
+      {"gpu_junction_temperature_shutdown", "junction temperature at which the GPU shuts down (C)"},
+      {"gpu_memory_temperature_slowdown", "HBM temperature at which the GPU throttles (C)"},
       {"gpu_clock", "GFX clock (MHz)"},
       {"gpu_memory_clock", "memory clock (MHz)"},
       {"gpu_power_cap", "board power cap (W)"},
@@ -281,6 +299,9 @@ inline std::string render(const RenderOptions& opt) {
     append_metric(&out, "gpu_edge_temperature", labels, s.temp_edge_c);
     append_metric(&out, "gpu_junction_temperature", labels, s.temp_junction_c);
     append_metric(&out, "gpu_memory_temperature", labels, s.temp_mem_c);
+    append_metric(&out, "gpu_junction_temperature_slowdown", labels, s.temp_junction_slowdown_c);
+    append_metric(&out, "gpu_junction_temperature_shutdown", labels, s.temp_junction_shutdown_c);
+    append_metric(&out, "gpu_memory_temperature_slowdown", labels, s.temp_mem_slowdown_c);
     append_metric(&out, "gpu_clock", labels, s.sclk_mhz);
     append_metric(&out, "gpu_memory_clock", labels, s.mclk_mhz);
     if (!s.compute_partition.empty() || !s.memory_partition.empty()) {

@@ -103,6 +103,9 @@ export const MI355X = Object.freeze({
   xgmiLinksPerGpu: 7,
   xgmiLinkGBs: 153,
   tdpWatts: 1400,
+  // Junction (hotspot) throttle threshold: amd-smi slowdown_hotspot_temperature
+  // on an MI355X (tests/fixtures/mi355x/amd_smi_static.json).
+  junctionSlowdownC: 100,
 });
 
 /** Allocation / power colour thresholds (reference NodesPage.tsx:38, MetricsPage.tsx:52-53). */

@@ -51,6 +51,7 @@ export const SERIES = {
     gfx: 'gpu_gfx_activity', // %
     umc: 'gpu_umc_activity', // % — HBM controller busy
     temp: 'gpu_junction_temperature', // °C
+    tempSlowdown: 'gpu_junction_temperature_slowdown', // °C throttle threshold (this repo's amdgpu-exporter)
     xgmiRe: 'xgmi_neighbor_[0-6]_tx_throughput', // bytes/s per neighbour
     linkHops: 'gpu_xgmi_link_hops', // measured link topology (this repo's native amdgpu-exporter)
   },
@@ -81,6 +82,7 @@ export const DISCOVERY_TTL_MS = 5 * 60 * 1000;
  * @property {number|null} gfxActivityPct
  * @property {number|null} memActivityPct
  * @property {number|null} tempC
+ * @property {number|null} tempSlowdownC  junction throttle threshold (exporter), if reported
  * @property {string|null} pod
  * @property {string|null} namespace
  *
@@ -103,7 +105,7 @@ function emptyGpu(nodeName, gpu, instance) {
   return {
     nodeName: nodeName, gpu: gpu, instance: instance,
     powerWatts: null, powerCapWatts: null, vramUsedBytes: null, vramTotalBytes: null,
-    gfxActivityPct: null, memActivityPct: null, tempC: null, pod: null, namespace: null,
+    gfxActivityPct: null, memActivityPct: null, tempC: null, tempSlowdownC: null, pod: null, namespace: null,
   };
 }
 
@@ -148,6 +150,7 @@ export function joinExporterResults(r) {
   each(r[E.gfx], function (g, v) { g.gfxActivityPct = v; });
   each(r[E.umc], function (g, v) { g.memActivityPct = v; });
   each(r[E.temp], function (g, v) { g.tempC = v; });
+  each(r[E.tempSlowdown], function (g, v) { g.tempSlowdownC = v; });
   const gpus = [];
   for (const k in map) {
     const g = map[k];
@@ -259,7 +262,7 @@ export const EXPORTER_JOIN_LABELS = ['__name__', 'hostname', 'node', 'instance',
 
 export function exporterQuery(withTopology) {
   const E = SERIES.exporter;
-  const names = [E.power, E.powerCap, E.vramUsed, E.vramTotal, E.gfx, E.umc, E.temp, E.xgmiRe];
+  const names = [E.power, E.powerCap, E.vramUsed, E.vramTotal, E.gfx, E.umc, E.temp, E.tempSlowdown, E.xgmiRe];
   // Link topology is static: callers include it only when their cached copy is stale.
   if (withTopology !== false) names.push(E.linkHops);
   return 'max by (' + EXPORTER_JOIN_LABELS.join(', ') + ') ({__name__=~"' + names.join('|') + '"})';
@@ -283,7 +286,7 @@ export const NODE_EXPORTER_JOIN_LABELS = ['__name__', 'instance', 'node', 'noden
 export function mergedQuery(withTopology) {
   const E = SERIES.exporter;
   const N = SERIES.nodeExporter;
-  const names = [E.power, E.powerCap, E.vramUsed, E.vramTotal, E.gfx, E.umc, E.temp, E.xgmiRe];
+  const names = [E.power, E.powerCap, E.vramUsed, E.vramTotal, E.gfx, E.umc, E.temp, E.tempSlowdown, E.xgmiRe];
   if (withTopology !== false) names.push(E.linkHops);
   names.push(N.chips.split('{')[0], N.power, N.powerCap, N.busy, N.vramUsed, N.vramTotal, N.uname);
   const labels = EXPORTER_JOIN_LABELS.slice();

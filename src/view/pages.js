@@ -898,6 +898,20 @@ export function metricsView(ctx, mstate, opts) {
   return page(BRAND + ' — Metrics', refreshButton('Refresh metrics', mstate.fetching || ctx.loading), items);
 }
 
+/**
+ * Junction temperature, coloured against the GPU's throttle threshold
+ * (exporter-reported, else the MI355X's 100 °C): warning within 10 °C of
+ * it, error at or above it.
+ */
+export function tempCell(g) {
+  if (g.tempC === null || g.tempC === undefined) return '—';
+  const limit = g.tempSlowdownC > 0 ? g.tempSlowdownC : MI355X.junctionSlowdownC;
+  const text = Math.round(g.tempC) + ' °C';
+  if (g.tempC >= limit) return status('error', text + ' (throttling at ' + Math.round(limit) + ' °C)');
+  if (g.tempC >= limit - 10) return status('warning', text);
+  return text;
+}
+
 function metricsNodeSection(name, gs) {
   return section(
     name + ' — ' + gs.length + ' × ' + MI355X.shortName,
@@ -911,7 +925,7 @@ function metricsNodeSection(name, gs) {
             hbmBar(g.vramUsedBytes, g.vramTotalBytes),
             pctText(g.gfxActivityPct),
             pctText(g.memActivityPct),
-            g.tempC === null ? '—' : Math.round(g.tempC) + ' °C',
+            tempCell(g),
             g.pod ? (g.namespace ? g.namespace + '/' : '') + g.pod : '—',
           ];
         }),

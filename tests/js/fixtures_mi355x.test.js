@@ -61,5 +61,6 @@ describe('MI355X hardware fixtures', () => {
     expect(smiStatic.asic.num_compute_units).toBe(MI355X.computeUnits);
     expect(shortProductName(smiStatic.asic.device_id, smiStatic.asic.market_name)).toBe('MI355X');
     expect(smiStatic.vram.type).toBe('HBM3E');
+    expect(smiStatic.limit.slowdown_hotspot_temperature.value).toBe(MI355X.junctionSlowdownC);
   });
 });

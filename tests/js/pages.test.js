@@ -11,6 +11,7 @@ import {
   podsView,
   podDetailView,
   podGpuAssignments,
+  tempCell,
   metricsView,
   formatWindow,
   allocationBar,
@@ -23,6 +24,7 @@ import { countRows, findSection, firstBlock, firstTable, loaders, rowNames, rowV
 import { renderPage, textContent } from '../../src/view/html.js';
 import { joinExporterResults, SERIES } from '../../src/api/metrics.js';
 import { NOW, makeContext, makeDeviceConfig, makeGpuNode, makeGpuPod, makeNode, makePlainPod, makePluginPod } from './fixtures.js';
+import { MI355X } from '../../src/api/amdgpu.js';
 
 const opts = { now: NOW };
 
@@ -299,6 +301,19 @@ describe('podsView', () => {
 });
 
 // ---------------------------------------------------------------------------
+describe('temperature against the throttle threshold', () => {
+  it('is plain text when cool, warning within 10 °C, error at the threshold', () => {
+    expect(tempCell({ tempC: 60, tempSlowdownC: 100 })).toBe('60 °C');
+    expect(tempCell({ tempC: 93, tempSlowdownC: 100 })).toEqual({ t: 'status', status: 'warning', text: '93 °C' });
+    expect(tempCell({ tempC: 101, tempSlowdownC: 100 }).status).toBe('error');
+    expect(tempCell({ tempC: null })).toBe('—');
+  });
+  it('falls back to the MI355X threshold without exporter data', () => {
+    expect(MI355X.junctionSlowdownC).toBe(100);
+    expect(tempCell({ tempC: 95, tempSlowdownC: null }).status).toBe('warning');
+  });
+});
+
 describe('pod → GPU assignment (exporter pod labels)', () => {
   const pods = [makeGpuPod('train', { node: 'g0', gpus: 2 }), makeGpuPod('idle', { node: 'g0', gpus: 1 })];
   const ctx = makeContext({ nodes: [makeGpuNode('g0')], pods });

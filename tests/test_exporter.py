@@ -84,6 +84,8 @@ def test_exporter_reports_mi355x(exe):
     # HIP's device name is empty on this ROCm; the probe names the board from sysfs / device id.
     assert labels["card_model"] == "AMD Instinct MI355X", labels
     assert re.fullmatch(r"[0-9A-F]{16}", labels["serial_number"]), labels
+    slow = [v for n, l, v in rows if n == "gpu_junction_temperature_slowdown" and l["gpu_id"] == "0"]
+    assert slow and 90 <= slow[0] <= 120, slow  # amd-smi: slowdown_hotspot_temperature 100 C
     part = [l for n, l, _ in rows if n == "gpu_partition_info"]
     assert part and part[0]["compute_partition"] in {"SPX", "DPX", "QPX", "CPX"}, part
     assert part[0]["memory_partition"] in {"NPS1", "NPS2", "NPS4", "NPS8"}, part
