@@ -30,6 +30,7 @@ MIB = 1024 * 1024
 BOARD_POWER_W = 1400.0
 IDLE_POWER_W = 185.0
 XGMI_LINK_GBS = 153.0
+JUNCTION_SLOWDOWN_C = 100.0  # amd-smi slowdown_hotspot_temperature on an MI355X
 
 
 def _phase(*parts) -> float:
@@ -103,7 +104,8 @@ def populate(db: TSDB, cluster: SyntheticCluster, source: str = "amd-exporter", 
                                         ("gpu_gfx_activity", gfx, {}),
                                         ("gpu_used_vram", vram_mib, {}),
                                         ("gpu_total_vram", lambda t: HBM_BYTES / MIB, {}),
-                                        ("gpu_umc_activity", umc, {}), ("gpu_junction_temperature", temp, {})):
+                                        ("gpu_umc_activity", umc, {}), ("gpu_junction_temperature", temp, {}),
+                                        ("gpu_junction_temperature_slowdown", lambda t: JUNCTION_SLOWDOWN_C, {})):
                     labels = dict(base, __name__=name, **extra)
                     if name in lv:
                         s = lv[name]

@@ -32,6 +32,7 @@ LIVE_FIELDS = {
     "gpu_gfx_activity": ("gfx_busy_pct", 1.0),
     "gpu_umc_activity": ("mem_busy_pct", 1.0),
     "gpu_junction_temperature": ("temp_junction_c", 1.0),
+    "gpu_junction_temperature_slowdown": ("temp_junction_slowdown_c", 1.0),
     "gpu_used_vram": ("vram_used_b", 1.0 / (1024 * 1024)),
     "gpu_total_vram": ("vram_total_b", 1.0 / (1024 * 1024)),
 }
