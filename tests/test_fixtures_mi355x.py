@@ -52,3 +52,10 @@ def test_exporter_capture_units():
     assert rows["gpu_junction_temperature"] == smi["temperature"]["hotspot"]["value"]
     assert rows["gpu_memory_temperature"] == smi["temperature"]["mem"]["value"]
     assert rows["gpu_power_cap"] == BOARD_POWER_W
+    limits = _json("amd_smi_static.json")["limit"]
+    assert rows["gpu_junction_temperature_slowdown"] == limits["slowdown_hotspot_temperature"]["value"]
+    assert rows["gpu_junction_temperature_shutdown"] == limits["shutdown_hotspot_temperature"]["value"]
+    assert rows["gpu_memory_temperature_slowdown"] == limits["slowdown_vram_temperature"]["value"]
+    labels = [lb for n, lb, _ in parse_exposition(open(os.path.join(FIX, "exporter_once.prom")).read())
+              if n == "gpu_power_usage"][0]
+    assert labels["card_model"] == "AMD Instinct MI355X"
