@@ -1,0 +1,172 @@
+/**
+ * Randomised property checks (seeded, so failures reproduce): the domain
+ * model and the structural-sharing helpers against independent oracles
+ * over a few hundred generated nodes / pods / snapshots each.
+ */
+import { buildClusterIndex, formatBytes, getPodGpuDemand } from '../../src/api/amdgpu.js';
+import { shareGpus, shareMap } from '../../src/api/metrics.js';
+import { buildXgmiMatrix, isFullMesh } from '../../src/api/topology.js';
+import { makeGpuNode } from './fixtures.js';
+
+/** mulberry32: tiny deterministic PRNG. */
+function rng(seed) {
+  let a = seed >>> 0;
+  return function () {
+    a = (a + 0x6d2b79f5) >>> 0;
+    let t = a;
+    t = Math.imul(t ^ (t >>> 15), t | 1);
+    t ^= t + Math.imul(t ^ (t >>> 7), t | 61);
+    return ((t ^ (t >>> 14)) >>> 0) / 4294967296;
+  };
+}
+const int = (r, lo, hi) => lo + Math.floor(r() * (hi - lo + 1));
+const pick = (r, xs) => xs[Math.floor(r() * xs.length)];
+
+const RES = ['amd.com/gpu', 'amd.com/cpx_nps4'];
+
+function randContainer(r, name, sidecar) {
+  const requests = {};
+  const limits = {};
+  RES.forEach((k) => {
+    if (r() < 0.5) {
+      const v = int(r, 0, 4);
+      const mode = int(r, 0, 2); // requests only / limits only / both
+      if (mode !== 1) requests[k] = String(v);
+      if (mode !== 0) limits[k] = String(mode === 2 ? v : int(r, 0, 4));
+    }
+  });
+  const c = { name, resources: { requests, limits } };
+  if (sidecar) c.restartPolicy = 'Always';
+  return c;
+}
+
+function randPod(r, i, nodes) {
+  const containers = [];
+  const initContainers = [];
+  for (let j = 0, n = int(r, 1, 3); j < n; j++) containers.push(randContainer(r, 'c' + j, false));
+  for (let j = 0, n = int(r, 0, 3); j < n; j++) initContainers.push(randContainer(r, 'i' + j, r() < 0.4));
+  return {
+    metadata: { name: 'p' + i, namespace: 'ns', uid: 'u' + i, creationTimestamp: '2026-10-01T00:00:00Z' },
+    spec: { nodeName: r() < 0.9 ? pick(r, nodes) : undefined, containers, initContainers },
+    status: { phase: pick(r, ['Running', 'Running', 'Pending', 'Succeeded', 'Failed']) },
+  };
+}
+
+/** Kubernetes effective request, simulated as a timeline of container starts. */
+function oracleDemand(pod, key) {
+  const val = (c) => {
+    const q = c.resources.requests[key];
+    const l = c.resources.limits[key];
+    // extended resources: a limit alone implies an equal request
+    return q !== undefined ? parseInt(q, 10) : l !== undefined ? parseInt(l, 10) : 0;
+  };
+  let running = 0; // sidecars started so far
+  let peak = 0;
+  for (const c of pod.spec.initContainers) {
+    if (c.restartPolicy === 'Always') running += val(c);
+    else peak = Math.max(peak, running + val(c));
+  }
+  let steady = running;
+  for (const c of pod.spec.containers) steady += val(c);
+  return Math.max(peak, steady);
+}
+
+describe('properties', () => {
+  it('effective GPU demand matches a timeline simulation of container starts', () => {
+    const r = rng(42);
+    for (let i = 0; i < 400; i++) {
+      const p = randPod(r, i, ['n0']);
+      const d = getPodGpuDemand(p);
+      RES.forEach((k) => expect(d[k] || 0).toBe(oracleDemand(p, k)));
+    }
+  });
+
+  it('cluster index: per-node sums equal totals, free never negative, terminal pods hold nothing', () => {
+    const r = rng(7);
+    for (let trial = 0; trial < 40; trial++) {
+      const names = [];
+      const nodes = [];
+      for (let i = 0, n = int(r, 1, 6); i < n; i++) {
+        const name = 'n' + i;
+        names.push(name);
+        nodes.push(makeGpuNode(name, { gpus: int(r, 0, 8) }));
+      }
+      const pods = [];
+      for (let i = 0, n = int(r, 0, 30); i < n; i++) pods.push(randPod(r, i, names.concat(['elsewhere'])));
+      const idx = buildClusterIndex(nodes, pods);
+      let inUse = 0;
+      let cap = 0;
+      for (const n of names) {
+        inUse += idx.nodeStats[n].inUse;
+        cap += idx.nodeStats[n].capacity;
+      }
+      expect(idx.totals.inUse).toBe(inUse);
+      expect(idx.totals.capacity).toBe(cap);
+      expect(idx.totals.free).toBe(Math.max(0, idx.totals.allocatable - idx.totals.inUse));
+      expect(idx.totals.free).toBeGreaterThanOrEqual(0);
+      let expected = 0;
+      for (const p of pods) {
+        if (!p.spec.nodeName || names.indexOf(p.spec.nodeName) < 0) continue;
+        if (p.status.phase === 'Succeeded' || p.status.phase === 'Failed') continue;
+        expected += RES.reduce((s, k) => s + oracleDemand(p, k), 0);
+      }
+      expect(inUse).toBe(expected);
+    }
+  });
+
+  it('formatBytes is within 0.5 % of the value and never loses the unit', () => {
+    const r = rng(3);
+    const unit = { B: 1, KiB: 1024, MiB: 1024 ** 2, GiB: 1024 ** 3, TiB: 1024 ** 4, PiB: 1024 ** 5 };
+    for (let i = 0; i < 500; i++) {
+      const v = Math.floor(Math.pow(2, r() * 52));
+      const [num, u] = formatBytes(v).split(' ');
+      expect(unit[u]).toBeDefined();
+      const back = parseFloat(num) * unit[u];
+      expect(Math.abs(back - v)).toBeLessThanOrEqual(Math.max(0.5, v * 0.005));
+    }
+  });
+
+  it('structural sharing returns content-equal results and reuses every unchanged element', () => {
+    const r = rng(11);
+    const mk = () => {
+      const gpus = [];
+      for (let n = 0; n < 3; n++) {
+        for (let g = 0; g < 4; g++) {
+          gpus.push({ nodeName: 'n' + n, gpu: String(g), powerWatts: int(r, 0, 2) * 100, pod: r() < 0.5 ? 'p' : null });
+        }
+      }
+      return gpus;
+    };
+    let prev = mk();
+    for (let i = 0; i < 200; i++) {
+      const next = mk();
+      const out = shareGpus(prev, next);
+      expect(out).toEqual(next);
+      out.forEach((g, j) => {
+        const p = prev.find((x) => x.nodeName === g.nodeName && x.gpu === g.gpu);
+        if (JSON.stringify(p) === JSON.stringify(next[j])) expect(g).toBe(p);
+      });
+      const m1 = { a: { x: int(r, 0, 1) }, b: { y: int(r, 0, 1) } };
+      const m2 = { a: { x: int(r, 0, 1) }, b: { y: int(r, 0, 1) } };
+      const sm = shareMap(m1, m2);
+      expect(sm).toEqual(m2);
+      if (JSON.stringify(m1) === JSON.stringify(m2)) expect(sm).toBe(m1);
+      prev = out;
+    }
+  });
+
+  it('a symmetric measured topology gives a symmetric matrix; the default is a full mesh', () => {
+    const r = rng(5);
+    for (let n = 1; n <= 8; n++) {
+      const probed = {};
+      for (let i = 0; i < n; i++) {
+        for (let j = i + 1; j < n; j++) {
+          if (r() < 0.7) probed[i + '-' + j] = probed[j + '-' + i] = { type: 'XGMI', hops: 1 };
+        }
+      }
+      const m = buildXgmiMatrix(n, null, probed);
+      for (let i = 0; i < n; i++) for (let j = 0; j < n; j++) expect(m.cells[i][j].kind).toBe(m.cells[j][i].kind);
+      expect(isFullMesh(buildXgmiMatrix(n))).toBe(n > 1);
+    }
+  });
+});
