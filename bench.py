@@ -165,7 +165,10 @@ def main(argv=None) -> int:
             "higher_is_better": False,
             "scaling": "weak",
             "vs_baseline": round(value / ref_s["p50"], 4),
-            "dtype": "n/a (dashboard; GPU workload pods run bf16 MFMA)" if gpu else "n/a (dashboard)",
+            # The metric is a dashboard latency; the compute running on the GPUs
+            # while it is measured (the workload pods) is bf16 MFMA.
+            "dtype": "bf16" if gpu and burner else "n/a",
+            "dtype_note": "dashboard latency metric; dtype is the MFMA workload the GPU pods run during the measurement",
             "data": "synthetic cluster + synthetic/live telemetry (no real cluster or network)",
             "config": {
                 "model": "amd-gpu Headlamp plugin on a synthetic 8xMI355X-per-node cluster",
