@@ -383,6 +383,12 @@ async function serve(a) {
           lat.push(ms(process.hrtime(t0)));
         }
         if (L.s.spans) out.trace = traceSummary(L.s.spans.slice(spanStart));
+        const snap = L.s.ctx();
+        const ms_ = L.s.mstate();
+        out.state = {
+          error: snap.error, crdAvailable: snap.crdAvailable, deviceConfigs: snap.deviceConfigs.length,
+          pluginPods: snap.pluginPods.length, metrics: !!ms_.metrics, stale: !!(ms_.metrics && ms_.metrics.stale),
+        };
         out.latencies = lat;
         out.requestsPerStep = (counter.n - before) / n;
         out.bytesPerStep = (counter.bytes - bytesBefore) / n;

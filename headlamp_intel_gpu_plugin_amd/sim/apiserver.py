@@ -23,6 +23,7 @@ Runs on its own asyncio loop in a daemon thread (:class:`ServerThread`).
 from __future__ import annotations
 
 import asyncio
+import random
 import json
 import re
 import threading
@@ -114,8 +115,16 @@ class FakeCluster:
 
     def __init__(self, cluster: SyntheticCluster, db: Optional[promql.TSDB] = None, *, latency_ms: float = 20.0,
                  crd_installed: bool = True, prometheus_up: Iterable[Tuple[str, str, str]] = (DEFAULT_PROM_SERVICE,),
-                 per_kb_us: float = 0.0, now=time.time):
+                 per_kb_us: float = 0.0, now=time.time, fail_rate: float = 0.0, hang_rate: float = 0.0,
+                 seed: int = 0):
         self.cluster = cluster
+        # Fault injection: each request independently fails with a 503 Status
+        # (fail_rate) or never answers within the client's 2 s budget
+        # (hang_rate, held 3 s) — seeded, so a failing run reproduces.
+        self.fail_rate = fail_rate
+        self.hang_rate = hang_rate
+        self._rng = random.Random(seed)
+        self.faults = {"failed": 0, "hung": 0}
         self.db = db if db is not None else promql.TSDB()
         self.latency_ms = latency_ms
         self.per_kb_us = per_kb_us
@@ -194,6 +203,17 @@ def build_app(fc: FakeCluster) -> web.Application:
     @web.middleware
     async def latency(request: web.Request, handler):
         t0 = time.perf_counter()
+        if fc.fail_rate or fc.hang_rate:
+            x = fc._rng.random()
+            if x < fc.hang_rate:
+                fc.faults["hung"] += 1
+                await asyncio.sleep(3.0)
+            elif x < fc.hang_rate + fc.fail_rate:
+                fc.faults["failed"] += 1
+                await asyncio.sleep(fc.latency_ms / 1000.0)
+                return web.json_response({"kind": "Status", "apiVersion": "v1", "status": "Failure",
+                                          "message": "injected fault", "reason": "ServiceUnavailable", "code": 503},
+                                         status=503)
         resp = await handler(request)
         work = time.perf_counter() - t0
         delay = fc.latency_ms / 1000.0
@@ -326,7 +346,8 @@ class ServerThread:
 
 
 def make_fake(nodes: int, *, source: str = "amd-exporter", latency_ms: float = 20.0, crd_installed: bool = True,
-              prometheus_up=(DEFAULT_PROM_SERVICE,), live=None, preset: Optional[str] = None) -> FakeCluster:
+              prometheus_up=(DEFAULT_PROM_SERVICE,), live=None, preset: Optional[str] = None,
+              fail_rate: float = 0.0, hang_rate: float = 0.0, seed: int = 0) -> FakeCluster:
     """Convenience: synthetic cluster of ``nodes`` × 8 MI355X (or a BASELINE ``preset``) + telemetry + fake control plane."""
     import copy
 
@@ -338,7 +359,8 @@ def make_fake(nodes: int, *, source: str = "amd-exporter", latency_ms: float = 2
     # "both": a kube-prometheus-stack cluster scrapes node-exporter AND the AMD exporter.
     for src in (("amd-exporter", "node-exporter") if source == "both" else (source,)):
         populate(db, cluster, source=src, live=live)
-    return FakeCluster(cluster, db, latency_ms=latency_ms, crd_installed=crd_installed, prometheus_up=prometheus_up)
+    return FakeCluster(cluster, db, latency_ms=latency_ms, crd_installed=crd_installed, prometheus_up=prometheus_up,
+                       fail_rate=fail_rate, hang_rate=hang_rate, seed=seed)
 
 
 __all__ = ["FakeCluster", "ServerThread", "build_app", "make_fake", "parse_label_selector", "parse_field_selector",

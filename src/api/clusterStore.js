@@ -76,6 +76,16 @@ const defaultClock = {
  * @param {{setTimeout: Function, clearTimeout: Function}} [clock]
  * @returns {Promise<T>}
  */
+/**
+ * True when a failed request proves the resource is not there for this user
+ * (404 / 403 / 401), as opposed to a timeout or a server / network error.
+ * Headlamp's ApiProxy errors carry the HTTP status in `status`.
+ */
+export function isAbsent(err) {
+  const st = err && (err.status || (err.response && err.response.status));
+  return st === 404 || st === 403 || st === 401;
+}
+
 export function withTimeout(promise, ms, clock) {
   const c = clock || defaultClock;
   return new Promise(function (resolve, reject) {
@@ -290,9 +300,11 @@ export function createClusterStore(opts) {
       function (list) {
         return isKubeList(list) ? { ok: true, items: list.items.filter(isDeviceConfig) } : { ok: false, items: [] };
       },
-      function () {
-        // Missing / forbidden / timed-out CRD degrades silently (reference ADR 003).
-        return { ok: false, items: [] };
+      function (e) {
+        // A missing or forbidden CRD degrades silently (reference ADR 003).
+        // A timeout or server error says nothing about the CRD: keep the last
+        // known state instead of flapping to "CRD Not Available".
+        return { ok: isAbsent(e) ? false : null, items: [] };
       }
     );
     const needPods = s.podsState === 'unknown' || s.podsState === 'error';
@@ -303,10 +315,12 @@ export function createClusterStore(opts) {
         if (my !== seq) return;
         podsQueried = false;
         const c = results[0];
-        s.crdAvailable = c.ok;
-        // Structural sharing: an unchanged list keeps its identity, so every
-        // memoised view (and React.memo'd section) downstream is reused.
-        s.deviceConfigs = sameObjects(s.deviceConfigs, c.items) ? s.deviceConfigs : c.items;
+        if (c.ok !== null || !s.asyncLoaded) {
+          s.crdAvailable = c.ok === true;
+          // Structural sharing: an unchanged list keeps its identity, so every
+          // memoised view (and React.memo'd section) downstream is reused.
+          s.deviceConfigs = sameObjects(s.deviceConfigs, c.items) ? s.deviceConfigs : c.items;
+        }
         if (results[1]) commitQueriedPods(results[1]);
         s.asyncError = null;
         s.asyncLoaded = true;

@@ -69,6 +69,8 @@ export const SERIES = {
 
 /** Discovery cache lifetime. Prometheus services move rarely. */
 export const DISCOVERY_TTL_MS = 5 * 60 * 1000;
+/** Consecutive failed metrics fetches before the page switches to "Prometheus Unreachable". */
+export const STALE_FAILURES = 3;
 
 /**
  * @typedef {Object} GpuTelemetry
@@ -93,6 +95,7 @@ export const DISCOVERY_TTL_MS = 5 * 60 * 1000;
  * @property {Record<string, Record<string, {type: string, hops: number}>>} links  node → "src-dst" →
  *           measured link (gpu_xgmi_link_hops); empty when the exporter does not report topology
  * @property {string} fetchedAt
+ * @property {boolean} [stale]  the latest fetch failed; this is the previous snapshot
  * @property {string} prometheusPath
  */
 
@@ -405,6 +408,7 @@ export function createMetricsSource(opts) {
   let links = null; // measured xGMI link topology per node (static), refreshed every `ttl`
   let linksAt = 0;
   let last = null; // previous snapshot, for structural sharing
+  let failures = 0; // consecutive failed fetches against the cached service
 
   function get(name, path) {
     const start = clock.now();
@@ -502,7 +506,12 @@ export function createMetricsSource(opts) {
    */
   function fetchGpuMetrics() {
     return withPrometheus(snapshotFrom, function () {
-      // Prometheus went away after discovery.
+      // A transient failure (timeout, 5xx) serves the last snapshot marked
+      // stale; only repeated failures mean Prometheus went away.
+      failures++;
+      if (last && failures < STALE_FAILURES) {
+        return Object.assign({}, last, { stale: true });
+      }
       invalidate();
       return null;
     });
@@ -514,6 +523,7 @@ export function createMetricsSource(opts) {
       : source === 'node-exporter' ? nodeExporterQuery() : mergedQuery(withTopology);
     return combined(base, q).then(function (res) {
       if (!res.ok) return UNREACHABLE;
+      failures = 0;
       const rows = res.rows;
       let joined = { gpus: [], xgmi: {}, links: {} };
       let src = null;

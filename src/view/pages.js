@@ -864,7 +864,12 @@ export function metricsView(ctx, mstate, opts) {
           row('HBM In Use', hbmBar(sum.vramUsedBytes, sum.vramTotalBytes > 0 ? sum.vramTotalBytes : null)),
           row('Avg GFX Activity', pctText(sum.avgGfxActivityPct)),
           row('Source', m.source === 'amd-exporter' ? 'AMD Device Metrics Exporter' : 'node-exporter (amdgpu hwmon + DRM)'),
-          row('Last Fetched', new Date(m.fetchedAt).toISOString().slice(11, 19) + ' UTC'),
+          row(
+            'Last Fetched',
+            m.stale
+              ? status('warning', new Date(m.fetchedAt).toISOString().slice(11, 19) + ' UTC (stale: the latest refresh failed)')
+              : new Date(m.fetchedAt).toISOString().slice(11, 19) + ' UTC'
+          ),
         ]),
       ])
     );

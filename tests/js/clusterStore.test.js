@@ -134,6 +134,23 @@ describe('createClusterStore', () => {
     expect(store.getSnapshot().pluginPods).toBe(a);
   });
 
+  it('keeps the last DeviceConfigs through a transient CRD failure, clears them on 404', async () => {
+    const r = baseRoutes();
+    const request = router(r);
+    const store = createClusterStore({ request });
+    await store.refresh();
+    const before = store.getSnapshot().deviceConfigs;
+    const fail = (status) => () => Promise.reject(Object.assign(new Error('HTTP ' + status), { status }));
+    r[DEVICE_CONFIG_LIST_PATH] = fail(503);
+    await store.refresh();
+    expect(store.getSnapshot().crdAvailable).toBe(true);
+    expect(store.getSnapshot().deviceConfigs).toBe(before);
+    r[DEVICE_CONFIG_LIST_PATH] = fail(404);
+    await store.refresh();
+    expect(store.getSnapshot().crdAvailable).toBe(false);
+    expect(store.getSnapshot().deviceConfigs).toHaveLength(0);
+  });
+
   it('sets crdAvailable and deviceConfigs from the CRD list', async () => {
     const store = createClusterStore({ request: router(baseRoutes()) });
     await store.refresh();

@@ -188,6 +188,24 @@ describe('fetchGpuMetrics', () => {
     const m = await src.fetchGpuMetrics();
     expect(m.links.n0).toEqual({ '0-1': { type: 'XGMI', hops: 1 }, '1-0': { type: 'XGMI', hops: 1 } });
   });
+  it('serves the last snapshot marked stale through transient failures, then reports unreachable', async () => {
+    let up = true;
+    const ok = prom();
+    const request = vi.fn((path) => (up ? ok(path) : Promise.reject(Object.assign(new Error('503'), { status: 503 }))));
+    const src = createMetricsSource({ request });
+    const a = await src.fetchGpuMetrics();
+    up = false;
+    const b = await src.fetchGpuMetrics();
+    expect(b.stale).toBe(true);
+    expect(b.gpus).toBe(a.gpus);
+    const c = await src.fetchGpuMetrics();
+    expect(c.stale).toBe(true);
+    expect(await src.fetchGpuMetrics()).toBeNull(); // STALE_FAILURES in a row
+    up = true;
+    const d = await src.fetchGpuMetrics();
+    expect(d.stale).toBeUndefined();
+    expect(d.gpus.length).toBe(a.gpus.length);
+  });
   it('reuses unchanged GPU objects and maps across refreshes (structural sharing)', async () => {
     const d = exporterData(['n0', 'n1']);
     const request = prom({ data: d });
