@@ -193,6 +193,10 @@ def main(argv=None) -> int:
             "rendered": {"gpu_nodes": rows["gpuNodes"], "gpu_pods": rows["gpuPods"],
                          "gpus_monitored": rows["gpusMonitored"], "gpu_cells": rows["gpuCells"],
                          "pod_table_rows": rows["podTableRows"], "detail_sections": rows["detailSections"]},
+            # Both schedules must show the same cluster: same nodes, pods, GPUs, rows.
+            "rendered_parity_with_reference": all(
+                rows[k] == result["ref"]["rows"][k]
+                for k in ("gpuNodes", "gpuPods", "gpusMonitored", "podTableRows", "detailSections")),
             "live_telemetry": bool(result["scrapes"]) and n_nodes > 0,
             "telemetry_source": "native amdgpu-exporter (C++/HIP) scraped every 2 s" if exporter else "synthetic",
             "host": socket.gethostname(),

@@ -27,6 +27,7 @@ def _check(line, n):
     assert line["config"]["nodes"] == n
     assert line["rendered"]["gpu_nodes"] == n
     assert line["rendered"]["gpus_monitored"] == 8 * n
+    assert line["rendered_parity_with_reference"] is True
 
 
 def test_bench_single_rank():
