@@ -79,6 +79,16 @@ def main(argv=None) -> int:
 
         burner = Burner(device=info.device.index, size=4096, gemms=4, triad_mb=512).start()
     ranks = D.all_gather_object(info, (node_name, info.device.index if gpu else None))
+
+    def quiet_sync():
+        """torch.cuda.synchronize() with the workload pod briefly paused (it
+        replays HIP graphs back to back, leaving the device no idle point)."""
+        if burner:
+            burner.pause()
+        D.sync_device(info)
+        if burner:
+            burner.resume()
+
     if live_on and info.is_main:
         from headlamp_intel_gpu_plugin_amd.parallel.agent import ExporterProcess
 
@@ -118,10 +128,10 @@ def main(argv=None) -> int:
             amd_cold = drv.call("cold", "amd", n=3)
             drv.call("steps", "amd", n=max(1, args.warmup))
             D.barrier(info)
-            D.sync_device(info)
+            quiet_sync()
             t0 = time.perf_counter()
             amd = drv.call("steps", "amd", n=args.steps)
-            D.sync_device(info)
+            quiet_sync()
             D.barrier(info)
             elapsed = time.perf_counter() - t0
             amd_switch = drv.call("switch", "amd", n=5)
@@ -137,9 +147,9 @@ def main(argv=None) -> int:
     else:
         # Agents serve scrapes while rank 0 measures; join its timed region.
         D.barrier(info)
-        D.sync_device(info)
+        quiet_sync()
         t0 = time.perf_counter()
-        D.sync_device(info)
+        quiet_sync()
         D.barrier(info)
         elapsed = time.perf_counter() - t0
 

@@ -93,15 +93,24 @@ class Burner:
     """Keeps one GPU busy with a training-like mix until stopped.
 
     Each iteration runs ``gemms`` MFMA GEMMs of ``size``³ then one HBM triad
-    over ``triad_mb`` MB, on its own stream, from a background thread.
+    over ``triad_mb`` MB on its own stream. ``graph_iters`` iterations are
+    captured once into a HIP graph and replayed, so the host thread wakes up
+    once per replay instead of launching every kernel from Python: in the
+    benchmark this thread shares a process (and the GIL) with the fake
+    control plane, and an eager loop would launch ~10k kernels a second.
     """
 
-    def __init__(self, device: int = 0, size: int = 4096, gemms: int = 4, triad_mb: int = 1024):
+    def __init__(self, device: int = 0, size: int = 4096, gemms: int = 4, triad_mb: int = 1024,
+                 graph_iters: int = 4):
         self.device = torch.device("cuda", device)
         self.size = size
         self.gemms = gemms
         self.triad_n = (triad_mb * 1024 * 1024 // 4) // 4 * 4
+        self.graph_iters = graph_iters
+        self.mode = "pending"  # "graph" once capture succeeded, "eager" if graphs are disabled
         self._stop = threading.Event()
+        self._pause = threading.Event()
+        self._idle = threading.Event()
         self._thread: Optional[threading.Thread] = None
         self.iterations = 0
         self.error: Optional[BaseException] = None
@@ -117,15 +126,64 @@ class Burner:
             y = torch.rand(self.triad_n, device=self.device, generator=g)
             z = torch.empty_like(x)
             stream = torch.cuda.Stream(self.device)
-            while not self._stop.is_set():
-                with torch.cuda.stream(stream):
-                    for _ in range(self.gemms):
-                        gemm_bf16_nt(a, b, out=c, stream=stream)
-                    stream_triad(x, y, 0.5, out=z, stream=stream)
-                stream.synchronize()
-                self.iterations += 1
+
+            def one_iteration():
+                for _ in range(self.gemms):
+                    gemm_bf16_nt(a, b, out=c, stream=stream)
+                stream_triad(x, y, 0.5, out=z, stream=stream)
+
+            with torch.cuda.stream(stream):
+                one_iteration()  # warm-up outside capture (sets kernel attributes once)
+            stream.synchronize()
+            if self.graph_iters > 0:
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph, stream=stream):
+                    for _ in range(self.graph_iters):
+                        one_iteration()
+                self.mode = "graph"
+                while not self._stop.is_set():
+                    if self._pause.is_set():
+                        self._hold()
+                        continue
+                    graph.replay()
+                    stream.synchronize()
+                    self.iterations += self.graph_iters
+            else:
+                self.mode = "eager"
+                while not self._stop.is_set():
+                    if self._pause.is_set():
+                        self._hold()
+                        continue
+                    with torch.cuda.stream(stream):
+                        one_iteration()
+                    stream.synchronize()
+                    self.iterations += 1
         except BaseException as e:  # surfaced by stop()
             self.error = e
+        finally:
+            self._idle.set()
+
+    def _hold(self) -> None:
+        self._idle.set()
+        while self._pause.is_set() and not self._stop.is_set():
+            self._stop.wait(0.001)
+        self._idle.clear()
+
+    def pause(self, timeout: float = 10.0) -> None:
+        """Stop issuing work and wait until the in-flight replay finished.
+
+        A device-wide ``torch.cuda.synchronize()`` waits for the device to go
+        idle; with graph replays issued back to back it finds no idle point
+        for seconds (measured: ~2 s per call, tools/diag/sync_vs_burner.py),
+        so callers pause the burner around such a synchronize.
+        """
+        if self._thread is None or not self._thread.is_alive():
+            return
+        self._pause.set()
+        self._idle.wait(timeout)
+
+    def resume(self) -> None:
+        self._pause.clear()
 
     def start(self) -> "Burner":
         self._thread = threading.Thread(target=self._run, daemon=True, name="gpu-burner")

@@ -236,6 +236,43 @@ def test_burner_runs_and_loads_gpu(dev):
     with workload.Burner(device=0, size=2048, gemms=2, triad_mb=64) as b:
         time.sleep(1.5)
         busy = probe.sample(0)["gfx_busy_pct"]
-    assert b.iterations > 0
+        # Paused, the device drains within one replay and a device-wide
+        # synchronize returns at once (bench.py brackets its timed region so).
+        b.pause()
+        t = time.perf_counter()
+        torch.cuda.synchronize()
+        assert time.perf_counter() - t < 0.2
+        b.resume()
+        time.sleep(0.3)
+    assert b.mode == "graph"  # the kernel mix replays as one captured HIP graph
+    assert b.iterations >= b.graph_iters
     if busy is not None:
         assert busy >= 0
+    with workload.Burner(device=0, size=1024, gemms=1, triad_mb=16, graph_iters=0) as e:
+        time.sleep(0.5)
+    assert e.mode == "eager" and e.iterations > 0
+
+
+def test_native_kernels_replay_in_a_hip_graph(dev):
+    # The extension launches on the caller's stream, so it is capturable.
+    a = torch.randn(512, 256, device=dev, dtype=torch.bfloat16)
+    b = torch.randn(768, 256, device=dev, dtype=torch.bfloat16)
+    c = torch.empty(512, 768, device=dev, dtype=torch.bfloat16)
+    x = torch.rand(1 << 16, device=dev)
+    y = torch.rand(1 << 16, device=dev)
+    z = torch.empty_like(x)
+    s = torch.cuda.Stream(dev)
+    with torch.cuda.stream(s):
+        workload.gemm_bf16_nt(a, b, out=c, stream=s)
+        workload.stream_triad(x, y, 2.0, out=z, stream=s)
+    s.synchronize()
+    eager_c, eager_z = c.clone(), z.clone()
+    c.zero_()
+    z.zero_()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        workload.gemm_bf16_nt(a, b, out=c, stream=s)
+        workload.stream_triad(x, y, 2.0, out=z, stream=s)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(c, eager_c) and torch.equal(z, eager_z)
