@@ -77,12 +77,14 @@ def main(argv=None) -> int:
     if gpu and not args.no_burn:
         from headlamp_intel_gpu_plugin_amd.ops.workload import Burner
 
-        burner = Burner(device=info.device.index, size=4096, gemms=4, triad_mb=512).start()
+        # ~1.7 ms of GPU work per iteration (2 x 8192^3 bf16 GEMM on the 8-phase
+        # kernel + a 1.5 GB triad): few launches, little GIL time on rank 0.
+        burner = Burner(device=info.device.index, size=8192, gemms=2, triad_mb=512).start()
     ranks = D.all_gather_object(info, (node_name, info.device.index if gpu else None))
 
     def quiet_sync():
-        """torch.cuda.synchronize() with the workload pod briefly paused (it
-        replays HIP graphs back to back, leaving the device no idle point)."""
+        """torch.cuda.synchronize() with the workload pod paused between
+        iterations, so the sync waits for the bench's own work only."""
         if burner:
             burner.pause()
         D.sync_device(info)

@@ -93,15 +93,19 @@ class Burner:
     """Keeps one GPU busy with a training-like mix until stopped.
 
     Each iteration runs ``gemms`` MFMA GEMMs of ``size``³ then one HBM triad
-    over ``triad_mb`` MB on its own stream. ``graph_iters`` iterations are
-    captured once into a HIP graph and replayed, so the host thread wakes up
-    once per replay instead of launching every kernel from Python: in the
-    benchmark this thread shares a process (and the GIL) with the fake
-    control plane, and an eager loop would launch ~10k kernels a second.
+    over ``triad_mb`` MB on its own stream. With ``graph_iters > 0`` that many
+    iterations are captured once into a HIP graph and replayed, so the host
+    thread wakes once per replay instead of launching every kernel from
+    Python. The default is eager launches: on this ROCm stack a device-wide
+    ``torch.cuda.synchronize()`` takes ~0.4-2 s once a graph has been replayed
+    on the device, even with the device idle (tools/diag/sync_vs_burner.py,
+    profiles/r1_diag_graph_sync.md), and the benchmark's timed region is
+    bracketed by exactly that call. Callers keep the launch rate low with
+    larger kernels instead (bench.py: 2 × 8192³ GEMMs + triad per iteration).
     """
 
     def __init__(self, device: int = 0, size: int = 4096, gemms: int = 4, triad_mb: int = 1024,
-                 graph_iters: int = 4):
+                 graph_iters: int = 0):
         self.device = torch.device("cuda", device)
         self.size = size
         self.gemms = gemms
@@ -170,13 +174,8 @@ class Burner:
         self._idle.clear()
 
     def pause(self, timeout: float = 10.0) -> None:
-        """Stop issuing work and wait until the in-flight replay finished.
-
-        A device-wide ``torch.cuda.synchronize()`` waits for the device to go
-        idle; with graph replays issued back to back it finds no idle point
-        for seconds (measured: ~2 s per call, tools/diag/sync_vs_burner.py),
-        so callers pause the burner around such a synchronize.
-        """
+        """Stop issuing work and wait until the in-flight iteration finished
+        (a device-wide synchronize then only waits for the caller's work)."""
         if self._thread is None or not self._thread.is_alive():
             return
         self._pause.set()

@@ -236,21 +236,23 @@ def test_burner_runs_and_loads_gpu(dev):
     with workload.Burner(device=0, size=2048, gemms=2, triad_mb=64) as b:
         time.sleep(1.5)
         busy = probe.sample(0)["gfx_busy_pct"]
-        # Paused, the device drains within one replay and a device-wide
-        # synchronize returns at once (bench.py brackets its timed region so).
+        # Paused between iterations, a device-wide synchronize only waits for
+        # the caller's own work (bench.py brackets its timed region so).
         b.pause()
+        n = b.iterations
         t = time.perf_counter()
         torch.cuda.synchronize()
         assert time.perf_counter() - t < 0.2
+        time.sleep(0.1)
+        assert b.iterations == n  # nothing issued while paused
         b.resume()
         time.sleep(0.3)
-    assert b.mode == "graph"  # the kernel mix replays as one captured HIP graph
-    assert b.iterations >= b.graph_iters
+    assert b.mode == "eager" and b.iterations > n
     if busy is not None:
         assert busy >= 0
-    with workload.Burner(device=0, size=1024, gemms=1, triad_mb=16, graph_iters=0) as e:
+    with workload.Burner(device=0, size=1024, gemms=1, triad_mb=16, graph_iters=4) as g:
         time.sleep(0.5)
-    assert e.mode == "eager" and e.iterations > 0
+    assert g.mode == "graph" and g.iterations >= 4  # the mix also replays as one captured HIP graph
 
 
 def test_native_kernels_replay_in_a_hip_graph(dev):
