@@ -60,7 +60,6 @@ def parse_args(argv=None):
 
 def main(argv=None) -> int:
     args = parse_args(argv)
-    import torch
 
     from headlamp_intel_gpu_plugin_amd.models.cluster import gpu_node_name
     from headlamp_intel_gpu_plugin_amd.parallel import dist as D
