@@ -1,0 +1,169 @@
+#!/usr/bin/env node
+/**
+ * amd-gpu-dash — the plugin's dashboard in a terminal.
+ *
+ * Runs the plugin's own data layer (src/api: cluster store, metrics client)
+ * and view-models (src/view/pages.js) against a cluster reached through
+ * `kubectl proxy` (or any URL that speaks the Kubernetes API with the
+ * caller's credentials), and prints the pages with the text renderer. Same
+ * requests, same degradation rules, same numbers as the Headlamp pages.
+ *
+ *   kubectl proxy --port 8001 &
+ *   node bin/amd-gpu-dash.js --url http://127.0.0.1:8001 --page nodes
+ *   node bin/amd-gpu-dash.js --page all --watch 10 --color
+ *   node bin/amd-gpu-dash.js --prometheus monitoring/my-prom:9090 --page metrics
+ *   node bin/amd-gpu-dash.js --json --page pods          # the view-model IR
+ *
+ * Plain ES2019 modules: runs on the Node 12 of the development image.
+ */
+import http from 'http';
+import https from 'https';
+import { createClusterStore } from '../src/api/clusterStore.js';
+import { createMetricsSource } from '../src/api/metrics.js';
+import { parsePrometheus, prometheusCandidates } from '../src/api/settings.js';
+import { devicePluginsView, metricsView, nodesView, overviewView, podsView } from '../src/view/pages.js';
+import { renderText } from '../src/view/text.js';
+
+const PAGES = ['overview', 'device-plugins', 'nodes', 'pods', 'metrics'];
+
+function usage(msg) {
+  if (msg) process.stderr.write('amd-gpu-dash: ' + msg + '\n');
+  process.stderr.write(
+    'usage: amd-gpu-dash [--url http://127.0.0.1:8001] [--page ' + PAGES.join('|') + '|all] [--watch SECONDS]\n' +
+      '                    [--prometheus NAMESPACE/SERVICE:PORT] [--timeout MS] [--token TOKEN] [--insecure]\n' +
+      '                    [--color] [--json]\n'
+  );
+  process.exit(2);
+}
+
+export function parseArgs(argv) {
+  const a = { url: 'http://127.0.0.1:8001', page: 'overview', watch: 0, prometheus: null, timeout: 2000,
+    token: null, insecure: false, color: false, json: false };
+  for (let i = 0; i < argv.length; i++) {
+    const k = argv[i];
+    const v = argv[i + 1];
+    if (k === '--url') a.url = v;
+    else if (k === '--page') a.page = v;
+    else if (k === '--watch') a.watch = Number(v);
+    else if (k === '--timeout') a.timeout = Number(v);
+    else if (k === '--token') a.token = v;
+    else if (k === '--prometheus') {
+      const m = /^([^/]+)\/([^:]+):(.+)$/.exec(v || '');
+      a.prometheus = m ? parsePrometheus({ namespace: m[1], service: m[2], port: m[3] }) : null;
+      if (!a.prometheus) return { error: 'bad --prometheus ' + v + ' (want namespace/service:port)' };
+    } else if (k === '--insecure') {
+      a.insecure = true;
+      continue;
+    } else if (k === '--color') {
+      a.color = true;
+      continue;
+    } else if (k === '--json') {
+      a.json = true;
+      continue;
+    } else if (k === '--help' || k === '-h') return { error: '' };
+    else return { error: 'unknown argument ' + k };
+    if (v === undefined) return { error: 'missing value for ' + k };
+    i++;
+  }
+  if (a.page !== 'all' && PAGES.indexOf(a.page) < 0) return { error: 'unknown page ' + a.page };
+  if (!(a.watch >= 0) || !(a.timeout > 0)) return { error: 'bad --watch / --timeout' };
+  return a;
+}
+
+/** GET path → parsed JSON; rejects with `.status` set on HTTP errors (like Headlamp's ApiProxy). */
+function makeRequest(a) {
+  const base = new URL(a.url);
+  const mod = base.protocol === 'https:' ? https : http;
+  const agent = new mod.Agent({ keepAlive: true, maxSockets: 6, rejectUnauthorized: !a.insecure });
+  const prefix = base.pathname.replace(/\/$/, '');
+  return function request(path) {
+    return new Promise(function (resolve, reject) {
+      const headers = { Accept: 'application/json' };
+      if (a.token) headers.Authorization = 'Bearer ' + a.token;
+      const req = mod.get(
+        { protocol: base.protocol, hostname: base.hostname, port: base.port, path: prefix + path, agent: agent, headers: headers },
+        function (res) {
+          const chunks = [];
+          res.on('data', function (c) { chunks.push(c); });
+          res.on('end', function () {
+            let json = null;
+            try {
+              json = JSON.parse(Buffer.concat(chunks).toString('utf8'));
+            } catch (e) {
+              json = null;
+            }
+            if (res.statusCode >= 400) {
+              if (json && json.status === 'error') return resolve(json); // Prometheus error body
+              const err = new Error((json && json.message) || 'HTTP ' + res.statusCode);
+              err.status = res.statusCode;
+              return reject(err);
+            }
+            if (json === null) return reject(new Error('bad JSON from ' + path));
+            resolve(json);
+          });
+        }
+      );
+      req.on('error', reject);
+    });
+  };
+}
+
+export function views(ctx, mstate, page) {
+  const opts = { metrics: mstate.metrics };
+  const all = {
+    overview: function () { return overviewView(ctx, opts); },
+    'device-plugins': function () { return devicePluginsView(ctx, opts); },
+    nodes: function () { return nodesView(ctx, opts); },
+    pods: function () { return podsView(ctx, opts); },
+    metrics: function () { return metricsView(ctx, mstate, opts); },
+  };
+  return (page === 'all' ? PAGES : [page]).map(function (p) { return all[p](); });
+}
+
+async function main() {
+  const a = parseArgs(process.argv.slice(2));
+  if (a.error !== undefined) usage(a.error);
+  const request = makeRequest(a);
+  const store = createClusterStore({ request: request, timeoutMs: a.timeout });
+  const settings = { prometheus: a.prometheus };
+  const metrics = createMetricsSource({ request: request, timeoutMs: a.timeout, services: prometheusCandidates(settings) });
+  const mstate = { metrics: null, series: null, fetchError: null, fetching: false };
+
+  async function fetchAll(first) {
+    const jobs = [store.refresh(), metrics.fetchGpuMetrics(), metrics.fetchSeries(1800, 30)];
+    if (first) jobs.push(store.loadLists());
+    const r = await Promise.all(jobs);
+    mstate.metrics = r[1];
+    mstate.series = r[2];
+    mstate.fetchError = r[1] ? null : 'Could not reach Prometheus';
+  }
+
+  function print() {
+    const vms = views(store.getSnapshot(), mstate, a.page);
+    if (a.json) {
+      process.stdout.write(JSON.stringify(vms.length === 1 ? vms[0] : vms) + '\n');
+      return;
+    }
+    if (a.watch > 0) process.stdout.write('\u001b[2J\u001b[H');
+    process.stdout.write(vms.map(function (vm) { return renderText(vm, { color: a.color }); }).join('\n') + '\n');
+  }
+
+  await fetchAll(true);
+  print();
+  while (a.watch > 0) {
+    await new Promise(function (r) { setTimeout(r, a.watch * 1000); });
+    await store.loadLists(); // no watch here: re-list nodes and pods each cycle
+    await fetchAll(false);
+    print();
+  }
+}
+
+if (process.argv[1] && /amd-gpu-dash(\.js)?$/.test(process.argv[1])) {
+  main().then(
+    function () { process.exit(0); },
+    function (e) {
+      process.stderr.write('amd-gpu-dash: ' + (e && e.stack ? e.stack : e) + '\n');
+      process.exit(1);
+    }
+  );
+}

@@ -134,7 +134,8 @@ def populate(db: TSDB, cluster: SyntheticCluster, source: str = "amd-exporter", 
                 inst = f"{instance}:9100"
                 db.add(Series({"__name__": "node_hwmon_chip_names", "chip": chip, "chip_name": "amdgpu", "instance": inst},
                               fn=lambda t: 1.0, interval=interval))
-                db.add(Series({"__name__": "node_hwmon_power_average_watt", "chip": chip, "sensor": "power1",
+                # An MI355X exposes hwmon power1_input only (no power1_average).
+                db.add(Series({"__name__": "node_hwmon_power_input_watt", "chip": chip, "sensor": "power1",
                                "instance": inst}, fn=power, interval=interval))
                 db.add(Series({"__name__": "node_hwmon_power_cap_watt", "chip": chip, "sensor": "power1",
                                "instance": inst}, fn=lambda t: BOARD_POWER_W, interval=interval))

@@ -59,6 +59,10 @@ export const SERIES = {
   nodeExporter: {
     chips: 'node_hwmon_chip_names{chip_name="amdgpu"}',
     power: 'node_hwmon_power_average_watt',
+    // hwmon power1_input. An MI355X exposes power1_input and no power1_average
+    // (tests/fixtures/mi355x/sysfs_amdgpu_files.txt), so this is its only power
+    // series through node-exporter; the average wins where both exist.
+    powerInput: 'node_hwmon_power_input_watt',
     powerCap: 'node_hwmon_power_cap_watt',
     busy: 'node_drm_gpu_busy_percent',
     vramUsed: 'node_drm_memory_vram_used_bytes',
@@ -238,7 +242,8 @@ export function joinNodeExporterResults(r) {
   }
   function chipKey(m) { return 'chip:' + (m.chip || ''); }
   function cardKey(m) { return 'card:' + (m.card || ''); }
-  each(r[N.power], chipKey, function (g, v) { g.powerWatts = v; });
+  each(r[N.powerInput], chipKey, function (g, v) { g.powerWatts = v; });
+  each(r[N.power], chipKey, function (g, v) { if (v !== null) g.powerWatts = v; });
   each(r[N.powerCap], chipKey, function (g, v) { g.powerCapWatts = v; });
   each(r[N.busy], cardKey, function (g, v) { g.gfxActivityPct = v; });
   each(r[N.vramUsed], cardKey, function (g, v) { g.vramUsedBytes = v; });
@@ -273,7 +278,7 @@ export function exporterQuery(withTopology) {
 
 export function nodeExporterQuery() {
   const N = SERIES.nodeExporter;
-  const names = [N.chips.split('{')[0], N.power, N.powerCap, N.busy, N.vramUsed, N.vramTotal, N.uname];
+  const names = [N.chips.split('{')[0], N.power, N.powerInput, N.powerCap, N.busy, N.vramUsed, N.vramTotal, N.uname];
   return '{__name__=~"' + names.join('|') + '"}';
 }
 
@@ -291,7 +296,7 @@ export function mergedQuery(withTopology) {
   const N = SERIES.nodeExporter;
   const names = [E.power, E.powerCap, E.vramUsed, E.vramTotal, E.gfx, E.umc, E.temp, E.tempSlowdown, E.xgmiRe];
   if (withTopology !== false) names.push(E.linkHops);
-  names.push(N.chips.split('{')[0], N.power, N.powerCap, N.busy, N.vramUsed, N.vramTotal, N.uname);
+  names.push(N.chips.split('{')[0], N.power, N.powerInput, N.powerCap, N.busy, N.vramUsed, N.vramTotal, N.uname);
   const labels = EXPORTER_JOIN_LABELS.slice();
   for (let i = 0; i < NODE_EXPORTER_JOIN_LABELS.length; i++) {
     if (labels.indexOf(NODE_EXPORTER_JOIN_LABELS[i]) < 0) labels.push(NODE_EXPORTER_JOIN_LABELS[i]);

@@ -5,7 +5,7 @@
  * METRIC AVAILABILITY on AMD (the reference's i915 page lists most of these
  * as unavailable; amdgpu exposes all of them):
  *   Power (W)            gpu_power_usage (AMD Device Metrics Exporter) or
- *                        amdgpu hwmon power1_average via node-exporter
+ *                        amdgpu hwmon power (power1_input on MI355X) via node-exporter
  *   HBM used / total     gpu_used_vram / gpu_total_vram, or node-exporter
  *                        --collector.drm node_drm_memory_vram_{used,size}_bytes
  *   GFX activity (%)     gpu_gfx_activity, or node_drm_gpu_busy_percent

@@ -796,7 +796,7 @@ export function metricAvailabilitySection() {
   return section('Metric Availability', [
     kv([
       row('Power (W)', lines([
-        { label: '', text: 'Available — gpu_power_usage (AMD Device Metrics Exporter) or amdgpu hwmon power1_average via node-exporter' },
+        { label: '', text: 'Available — gpu_power_usage (AMD Device Metrics Exporter) or amdgpu hwmon power via node-exporter (power1_input on MI355X, which has no power1_average)' },
       ])),
       row('HBM used / total', lines([
         { label: '', text: 'Available — gpu_used_vram / gpu_total_vram, or node-exporter --collector.drm node_drm_memory_vram_* (288 GB HBM3E per MI355X)' },

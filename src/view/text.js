@@ -1,0 +1,127 @@
+/**
+ * View IR → plain text for terminals (bin/amd-gpu-dash.js).
+ *
+ * The third renderer of the same IR (after View.tsx and html.js): sections
+ * become underlined titles, name/value tables aligned "name  value" lines,
+ * tables fixed-width columns, bars "[#####.....] 6/8 (75%)", statuses a
+ * marker (✓ ! ✗) before the text, the per-GPU strip one line per board and
+ * the xGMI matrix a small grid. Optional ANSI colour for statuses.
+ */
+
+const MARK = { success: '✓', warning: '!', error: '✗' };
+const ANSI = { success: '\u001b[32m', warning: '\u001b[33m', error: '\u001b[31m', reset: '\u001b[0m' };
+
+/** Pad to `w` printable characters (ANSI colour escapes take no columns). */
+function pad(s, w) {
+  s = String(s);
+  const n = [...s.replace(/\u001b\[[0-9;]*m/g, '')].length;
+  return n >= w ? s : s + ' '.repeat(w - n);
+}
+
+function barText(p, width) {
+  if (p === null || p === undefined) return '';
+  const k = Math.max(0, Math.min(width, Math.round((p / 100) * width)));
+  return '[' + '#'.repeat(k) + '.'.repeat(width - k) + '] ';
+}
+
+/** One IR cell/value as a single line of text. */
+export function textValue(v, color) {
+  if (v === null || v === undefined) return '';
+  if (typeof v === 'string' || typeof v === 'number') return String(v);
+  switch (v.t) {
+    case 'status': {
+      const s = (MARK[v.status] || '·') + ' ' + v.text;
+      return color && ANSI[v.status] ? ANSI[v.status] + s + ANSI.reset : s;
+    }
+    case 'bar':
+      return barText(v.pct, 10) + v.text;
+    case 'lines':
+      return v.lines.map(function (l) { return (l.label ? l.label + ': ' : '') + l.text; }).join('; ');
+    default:
+      return '';
+  }
+}
+
+function blockLines(b, color) {
+  const out = [];
+  switch (b.t) {
+    case 'kv': {
+      let w = 0;
+      b.rows.forEach(function (r) { w = Math.max(w, [...r.name].length); });
+      b.rows.forEach(function (r) { out.push('  ' + pad(r.name, w) + '  ' + textValue(r.value, color)); });
+      break;
+    }
+    case 'table': {
+      const cells = b.rows.map(function (r) { return r.map(function (c) { return textValue(c, color); }); });
+      const widths = b.columns.map(function (c, i) {
+        let w = [...c].length;
+        cells.forEach(function (r) { w = Math.max(w, [...String(r[i]).replace(/\u001b\[[0-9;]*m/g, '')].length); });
+        return Math.min(w, 48);
+      });
+      out.push('  ' + b.columns.map(function (c, i) { return pad(c, widths[i]); }).join('  '));
+      out.push('  ' + widths.map(function (w) { return '-'.repeat(w); }).join('  '));
+      cells.forEach(function (r) { out.push('  ' + r.map(function (c, i) { return pad(c, widths[i]); }).join('  ')); });
+      break;
+    }
+    case 'pctbar': {
+      const parts = b.data.map(function (d) { return d.name + ' ' + d.value; }).join(', ');
+      out.push('  ' + b.label + ': ' + parts + (b.total ? ' (of ' + b.total + ')' : ''));
+      break;
+    }
+    case 'slots': {
+      const per = b.partitionsPerGpu > 1 ? b.partitionsPerGpu : 8;
+      out.push('  Per-GPU allocation' + (b.exact ? '' : ' (inferred)') + ':');
+      for (let i = 0; i < b.slots.length; i += per) {
+        out.push('    ' + b.slots.slice(i, i + per).map(function (s) {
+          const id = s.partition === null || s.partition === undefined ? String(s.index) : s.board + '.' + s.partition;
+          return id + ':' + (s.pod || '-');
+        }).join('  '));
+      }
+      break;
+    }
+    case 'matrix': {
+      const m = b.matrix;
+      out.push('  xGMI (' + (b.measuredTopology ? 'measured' : 'MI355X platform model') + '): ' +
+        (b.fullMesh ? 'full mesh, ' + m.linksPerGpu + ' links/GPU' : 'partial') + ', ring bus ' + m.ringBusGBs + ' GB/s per link');
+      m.cells.forEach(function (row, i) {
+        out.push('    ' + pad('GPU ' + i, 6) + row.map(function (c) {
+          const v = c.kind === 'self' ? '-' : c.measuredGBs !== null ? String(Math.round(c.measuredGBs))
+            : c.kind === 'xgmi' ? 'x' : '.';
+          return ' '.repeat(Math.max(1, 4 - v.length)) + v; // right-aligned, 4 columns per cell
+        }).join(''));
+      });
+      break;
+    }
+    case 'series': {
+      Object.keys(b.power || {}).forEach(function (n) {
+        const pts = b.power[n];
+        const last = pts.length ? pts[pts.length - 1][1] : null;
+        out.push('  ' + n + ': ' + pts.length + ' power samples' + (last === null ? '' : ', last ' + last.toFixed(0) + ' W'));
+      });
+      break;
+    }
+    default:
+      break;
+  }
+  return out;
+}
+
+/** A section as text lines (title underlined). */
+export function textSection(s, color) {
+  if (!s) return [];
+  const out = [s.title, '='.repeat([...s.title].length)];
+  s.blocks.forEach(function (b) { out.push.apply(out, blockLines(b, color)); });
+  return out;
+}
+
+/** A page view-model as one string. */
+export function renderText(vm, opts) {
+  const color = !!(opts && opts.color);
+  const out = [];
+  if (vm.title) out.push('# ' + vm.title, '');
+  vm.items.forEach(function (it) {
+    if (it.t === 'loader') out.push('… ' + it.title, '');
+    else out.push.apply(out, textSection(it, color).concat(['']));
+  });
+  return out.join('\n');
+}
