@@ -339,6 +339,16 @@ describe('joins (direct)', () => {
     expect(j.gpus).toHaveLength(1);
     expect(j.gpus[0].powerWatts).toBeNull();
   });
+  it('reads hwmon power1_input where power1_average does not exist (MI355X), preferring the average', () => {
+    const N = SERIES.nodeExporter;
+    const r = {};
+    r[N.chips] = [vec({ instance: 'i', chip: 'c0', chip_name: 'amdgpu' }, 1), vec({ instance: 'i', chip: 'c1', chip_name: 'amdgpu' }, 1)];
+    r[N.powerInput] = [vec({ instance: 'i', chip: 'c0' }, 700), vec({ instance: 'i', chip: 'c1' }, 800)];
+    r[N.power] = [vec({ instance: 'i', chip: 'c1' }, 810)];
+    const g = joinNodeExporterResults(r).gpus;
+    expect(g[0].powerWatts).toBe(700);
+    expect(g[1].powerWatts).toBe(810);
+  });
   it('joinNodeExporterResults maps instance to nodename', () => {
     const N = SERIES.nodeExporter;
     const r = {};
