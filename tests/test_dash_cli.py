@@ -1,0 +1,49 @@
+"""bin/amd-gpu-dash.js: the plugin's data layer + view-models in a terminal, against the fake cluster."""
+import json
+import os
+import subprocess
+
+import pytest
+
+from headlamp_intel_gpu_plugin_amd.sim.apiserver import ServerThread, make_fake
+from headlamp_intel_gpu_plugin_amd.utils.nodebridge import node_binary
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CLI = os.path.join(ROOT, "bin", "amd-gpu-dash.js")
+
+
+def run(*args, timeout=60):
+    return subprocess.run([node_binary(), CLI] + list(args), capture_output=True, text=True, timeout=timeout, cwd=ROOT)
+
+
+@pytest.fixture(scope="module")
+def url():
+    fc = make_fake(2, source="amd-exporter", latency_ms=1)
+    with ServerThread(fc) as srv:
+        yield srv.url
+
+
+def test_all_pages_render(url):
+    r = run("--url", url, "--page", "all")
+    assert r.returncode == 0, r.stderr
+    for title in ("AMD GPU — Overview", "AMD GPU — Device Plugins", "AMD GPU — Nodes", "AMD GPU — Pods",
+                  "AMD GPU — Metrics"):
+        assert "# " + title in r.stdout
+    assert "mi355x-001" in r.stdout and "xGMI (" in r.stdout and "Assigned GPUs" in r.stdout
+
+
+def test_json_is_the_view_model(url):
+    r = run("--url", url, "--page", "nodes", "--json")
+    assert r.returncode == 0, r.stderr
+    vm = json.loads(r.stdout)
+    assert vm["title"] == "AMD GPU — Nodes"
+    assert [s["title"] for s in vm["items"]][:3] == ["GPU Node Summary", "mi355x-000", "mi355x-001"]
+
+
+def test_unreachable_prometheus_and_bad_arguments(url):
+    r = run("--url", url, "--page", "metrics", "--prometheus", "monitoring/none:9090")
+    assert r.returncode == 0 and "GPU Power Summary" in r.stdout  # falls back to the built-in candidates
+    assert run("--page", "nope").returncode == 2
+    assert run("--prometheus", "not-a-service").returncode == 2
+    dead = run("--url", "http://127.0.0.1:9", "--page", "overview", "--timeout", "500")
+    assert dead.returncode == 0 and "Error" in dead.stdout  # the page's own error state, not a crash
