@@ -41,7 +41,10 @@ def init(timeout_s: int = 1800) -> DistInfo:
         torch.cuda.set_device(local % torch.cuda.device_count())
         device = torch.device("cuda", torch.cuda.current_device())
     info = DistInfo(rank=rank, world=world, local_rank=local, device=device)
-    if world > 1 and not dist.is_initialized():
+    # HEADLAMP_AMD_FORCE_PG=1 builds the process groups even for one rank, so
+    # the RCCL init / all-reduce path can be exercised on a single-GPU box.
+    force = os.environ.get("HEADLAMP_AMD_FORCE_PG") == "1" and "MASTER_PORT" in os.environ
+    if (world > 1 or force) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         backend = "nccl" if has_gpu else "gloo"
         kw = {"device_id": device} if has_gpu else {}
@@ -51,8 +54,12 @@ def init(timeout_s: int = 1800) -> DistInfo:
     return info
 
 
+def _active(info: DistInfo) -> bool:
+    return info.world > 1 or dist.is_initialized()
+
+
 def barrier(info: DistInfo) -> None:
-    if info.world > 1:
+    if _active(info):
         dist.barrier(group=info.cpu_group)
 
 
@@ -62,7 +69,7 @@ def sync_device(info: DistInfo) -> None:
 
 
 def all_gather_object(info: DistInfo, obj) -> List:
-    if info.world == 1:
+    if not _active(info):
         return [obj]
     out: List = [None] * info.world
     dist.all_gather_object(out, obj, group=info.cpu_group)
@@ -70,7 +77,7 @@ def all_gather_object(info: DistInfo, obj) -> List:
 
 
 def broadcast_object(info: DistInfo, obj, src: int = 0):
-    if info.world == 1:
+    if not _active(info):
         return obj
     box = [obj]
     dist.broadcast_object_list(box, src=src, group=info.cpu_group)
@@ -79,7 +86,7 @@ def broadcast_object(info: DistInfo, obj, src: int = 0):
 
 def max_float(info: DistInfo, x: float) -> float:
     """MAX over ranks, on the device collective backend (RCCL) when present."""
-    if info.world == 1:
+    if not _active(info):
         return x
     if info.device is not None:
         t = torch.tensor([x], dtype=torch.float64, device=info.device)
@@ -91,5 +98,5 @@ def max_float(info: DistInfo, x: float) -> float:
 
 
 def shutdown(info: DistInfo) -> None:
-    if info.world > 1 and dist.is_initialized():
+    if dist.is_initialized():
         dist.destroy_process_group()
