@@ -6,21 +6,28 @@
  * then runs four instant queries on i915 hwmon series and joins power by
  * PCI `chip` only (:127-138, quirk Q1).
  *
- * This client:
- *   * probes the candidate services IN PARALLEL with a timeout, keeps the
- *     highest-priority success, and caches it (TTL) so steady-state
- *     refreshes skip discovery entirely;
+ * This client (ADR 002, 003, 006):
+ *   * sends the first query straight to the preferred service (its answer
+ *     is the discovery); only if that fails are all candidates probed IN
+ *     PARALLEL with a timeout (reference: serial, no timeout,
+ *     src/api/metrics.ts:77-90). The winner is cached for 5 min;
  *   * reads AMD series — the AMD Device Metrics Exporter (`gpu_*`, per-GPU,
- *     optionally pod-labelled) and, as a fallback, node-exporter's amdgpu
- *     hwmon + DRM collectors — in ONE parallel wave, then remembers which
- *     source answered so later waves only query that one;
- *   * keys every GPU by (node, gpu index), never by PCI address alone;
+ *     optionally pod-labelled), this repo's amdgpu-exporter extensions
+ *     (power cap, link hops, throttle thresholds) and, as a fallback,
+ *     node-exporter's amdgpu hwmon + DRM collectors — with ONE merged first
+ *     query, then only the exporter that answered, projected onto the labels
+ *     the join reads (reference: four queries per fetch, :101-116);
+ *   * keys every GPU by (node, gpu index), never by PCI address alone
+ *     (reference quirk Q1, :127-138);
  *   * exposes power, HBM used/total, GFX and memory-controller activity,
- *     temperature, and `query_range` time series (power / HBM per node);
- *   * surfaces xGMI per-link throughput when the exporter publishes it.
+ *     temperature vs throttle threshold, xGMI per-link throughput and measured
+ *     link topology, and incremental `query_range` series (power / HBM per
+ *     node; the reference has instant queries only, :67-75);
+ *   * shares structure between snapshots and serves the last snapshot marked
+ *     `stale` through transient failures.
  *
- * Metric and label names marked (verify) must be checked against the
- * exporter release deployed on the cluster; they are all in `SERIES`.
+ * Metric and label names are all in `SERIES`; the device-level ones are
+ * pinned by captures from a real MI355X (tests/fixtures/mi355x).
  */
 
 import { MI355X, isObject } from './amdgpu.js';
