@@ -4,9 +4,13 @@
  * Replaces the reference's per-route React provider state
  * (src/api/IntelGpuDataContext.tsx:96-254, SURVEY.md C3) with a store that:
  *
- *   * fetches the DeviceConfig CRD and the operator pods IN PARALLEL
- *     (reference: 4 serial round-trips, :122-165) — refresh latency is
- *     max(RTT) instead of Σ RTT;
+ *   * refreshes with ONE request (the DeviceConfig list): operator pods are
+ *     derived from the watched pod list, and the plugin-pod requests run —
+ *     in parallel, each time-boxed — only when that list is unavailable
+ *     (reference: CRD + 3 selectors, serial, :122-165) — refresh latency is
+ *     one RTT instead of Σ RTT;
+ *   * keeps its last CRD state through transient failures and clears it on
+ *     404 / 403 (reference: any failure = absent, :133-138);
  *   * keeps the last good data visible while a refresh is in flight
  *     (stale-while-revalidate) instead of swapping the page for a Loader;
  *   * is shared across routes and detail views through `getSharedStore`, so
