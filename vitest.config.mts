@@ -1,14 +1,20 @@
 import { defineConfig } from 'vitest/config';
 
+// Two spec families share one runner:
+//  - src/**/*.test.tsx: React bindings and renderers (jsdom, CommonComponents mocked);
+//  - tests/js/*.test.js: the framework-free plugin logic, also run on bare Node
+//    by tools/minitest.js (`npm run test:node12`), so they use only vitest globals.
+const specs = ['src/**/*.test.{ts,tsx}', 'tests/js/**/*.test.js'];
+
 export default defineConfig({
   test: {
-    globals: true,
+    include: specs,
+    exclude: ['node_modules/**', 'dist/**', 'gpurun_out/**'],
     environment: 'jsdom',
+    globals: true,
     setupFiles: ['./vitest.setup.ts'],
-    // tests/js/*.test.js are the framework-free specs of the plugin logic; they
-    // also run on bare Node via tools/minitest.js (see package.json test:node12).
-    include: ['src/**/*.test.{ts,tsx}', 'tests/js/**/*.test.js'],
-    exclude: ['node_modules/**'],
+    testTimeout: 20000,
     env: { NODE_ENV: 'test' },
+    coverage: { provider: 'v8', include: ['src/**'], reporter: ['text', 'lcov'] },
   },
 });
