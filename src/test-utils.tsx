@@ -1,58 +1,46 @@
 /**
- * Shared vitest mocks: Headlamp CommonComponents rendered as semantic HTML,
- * the same stand-ins the reference's component tests use
- * (src/components/OverviewPage.test.tsx:8-61 there) and that src/view/html.js
- * emits for the Node-side specs.
+ * Shared vitest stand-ins for Headlamp CommonComponents.
+ *
+ * Each component renders the plain semantic element that src/view/html.js
+ * emits for the same IR node, so TSX tests and the Node-side specs assert on
+ * one markup (the reference's component tests mock CommonComponents with the
+ * same element mapping, SURVEY.md §4). Built with createElement from a small
+ * table rather than per-component JSX.
  */
 import React from 'react';
 
-export const commonComponentsMock = {
-  Loader: ({ title }: { title: string }) => <div data-testid="loader">{title}</div>,
-  SectionBox: ({ title, children }: { title: string; children?: React.ReactNode }) => (
-    <section>
-      <h2>{title}</h2>
-      {children}
-    </section>
+/* eslint-disable @typescript-eslint/no-explicit-any */
+type Props = Record<string, any>;
+const h = React.createElement;
+
+/** Component → [tag, attributes] for the stand-ins that only wrap children. */
+const WRAPPERS: Record<string, [string, Record<string, string>]> = {
+  PercentageBar: ['div', { 'data-testid': 'percentage-bar' }],
+};
+
+function cells(columns: Props[], item: unknown) {
+  return columns.map((c, j) => h('td', { key: j }, c.getter(item)));
+}
+
+export const commonComponentsMock: Record<string, (p: Props) => React.ReactElement> = {
+  Loader: p => h('div', { 'data-testid': 'loader' }, p.title),
+  SectionHeader: p => h('h1', null, p.title),
+  SectionBox: p => h('section', null, h('h2', null, p.title), p.children),
+  StatusLabel: p => h('span', { 'data-status': p.status }, p.children),
+  NameValueTable: p =>
+    h(
+      'dl',
+      null,
+      (p.rows as Props[]).map((r, i) => h('div', { key: i }, h('dt', null, r.name), h('dd', null, r.value)))
+    ),
+  SimpleTable: p =>
+    h(
+      'table',
+      null,
+      h('thead', null, h('tr', null, (p.columns as Props[]).map((c, j) => h('th', { key: j }, c.label)))),
+      h('tbody', null, (p.data as unknown[]).map((item, i) => h('tr', { key: i }, cells(p.columns, item))))
+    ),
+  ...Object.fromEntries(
+    Object.entries(WRAPPERS).map(([name, [tag, attrs]]) => [name, (p: Props) => h(tag, attrs, p.children)])
   ),
-  SectionHeader: ({ title }: { title: string }) => <h1>{title}</h1>,
-  NameValueTable: ({ rows }: { rows: Array<{ name: React.ReactNode; value: React.ReactNode }> }) => (
-    <dl>
-      {rows.map((r, i) => (
-        <div key={i}>
-          <dt>{r.name}</dt>
-          <dd>{r.value}</dd>
-        </div>
-      ))}
-    </dl>
-  ),
-  SimpleTable: ({
-    columns,
-    data,
-  }: {
-    columns: Array<{ label: string; getter: (item: unknown) => React.ReactNode }>;
-    data: unknown[];
-  }) => (
-    <table>
-      <thead>
-        <tr>
-          {columns.map(c => (
-            <th key={c.label}>{c.label}</th>
-          ))}
-        </tr>
-      </thead>
-      <tbody>
-        {data.map((item, i) => (
-          <tr key={i}>
-            {columns.map(c => (
-              <td key={c.label}>{c.getter(item)}</td>
-            ))}
-          </tr>
-        ))}
-      </tbody>
-    </table>
-  ),
-  StatusLabel: ({ status, children }: { status: string; children?: React.ReactNode }) => (
-    <span data-status={status}>{children}</span>
-  ),
-  PercentageBar: () => <div data-testid="percentage-bar" />,
 };
