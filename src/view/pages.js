@@ -76,7 +76,9 @@ export const BRAND = 'AMD GPU';
  * section reads plus the age clock (ages are shown with 1 s resolution), so a
  * refresh that returns unchanged Kubernetes objects reuses the section IR.
  */
-const memo = createMemo(512);
+// One slot per section: node cards, node details, metrics nodes and pod details
+// of a few hundred nodes / thousands of pods fit without LRU churn.
+const memo = createMemo(8192);
 const podDetailCache = typeof WeakMap === 'function' ? new WeakMap() : null;
 
 function ageKey(now) {
