@@ -51,6 +51,11 @@ class LiveGpu:
         self.series: Dict[str, Series] = {}
 
 
+def _ce(node_index: int, gpu: int) -> int:
+    """Corrected-error count of a synthetic GPU (non-zero on one GPU in 37)."""
+    return 3 if (node_index * 8 + gpu) % 37 == 5 else 0
+
+
 def populate(db: TSDB, cluster: SyntheticCluster, source: str = "amd-exporter", interval: float = 15.0,
              live: Optional[Dict[Tuple[str, int], Dict[str, Series]]] = None) -> int:
     """Register telemetry series for every GPU in ``cluster``. Returns the series count.
@@ -105,7 +110,11 @@ def populate(db: TSDB, cluster: SyntheticCluster, source: str = "amd-exporter", 
                                         ("gpu_used_vram", vram_mib, {}),
                                         ("gpu_total_vram", lambda t: HBM_BYTES / MIB, {}),
                                         ("gpu_umc_activity", umc, {}), ("gpu_junction_temperature", temp, {}),
-                                        ("gpu_junction_temperature_slowdown", lambda t: JUNCTION_SLOWDOWN_C, {})):
+                                        ("gpu_junction_temperature_slowdown", lambda t: JUNCTION_SLOWDOWN_C, {}),
+                                        # RAS counters: a healthy fleet reads 0; one GPU in 37
+                                        # carries a few corrected HBM errors.
+                                        ("gpu_ecc_correct_total", lambda t, c=float(_ce(i, g)): c, {}),
+                                        ("gpu_ecc_uncorrect_total", lambda t: 0.0, {})):
                     labels = dict(base, __name__=name, **extra)
                     if name in lv:
                         s = lv[name]

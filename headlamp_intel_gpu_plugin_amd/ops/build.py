@@ -73,6 +73,10 @@ def command(name: str, out: str = "") -> List[str]:
         cmd += ["-fPIC", "-shared", f"-I{sysconfig.get_paths()['include']}"]
     if spec["hip"]:
         cmd += [f"--offload-arch={ARCH}", "-x", "hip", "-munsafe-fp-atomics"]
+    else:
+        # Host-only sources (HIP runtime API, no kernels): hipcc still runs a
+        # device pass over them, which must target gfx950 like everything else.
+        cmd += [f"--offload-arch={ARCH}"]
     cmd += [os.path.join(HERE, s) for s in spec["sources"]]
     cmd += ["-o", out or so_path(name), f"-L{ROCM}/lib", "-lamdhip64", f"-Wl,-rpath,{ROCM}/lib"]
     return cmd

@@ -117,6 +117,10 @@ PyObject* py_sample(PyObject*, PyObject* args) {
   put("mem_busy_pct", s.mem_busy_pct);
   put("vram_used_b", s.vram_used_b);
   put("vram_total_b", s.vram_total_b);
+  put("ecc_correct", s.ecc_correct);
+  put("ecc_uncorrect", s.ecc_uncorrect);
+  put("ecc_deferred", s.ecc_deferred);
+  put("ecc_retired_pages", s.ecc_retired_pages);
   auto put_str = [&](const char* k, const std::string& v) {
     PyObject* o = v.empty() ? (Py_INCREF(Py_None), Py_None) : PyUnicode_FromString(v.c_str());
     PyDict_SetItemString(d, k, o);
@@ -146,12 +150,31 @@ PyObject* py_render(PyObject*, PyObject* args) {
 
 PyObject* py_last_error(PyObject*, PyObject*) { return PyUnicode_FromString(g_error.c_str()); }
 
+// RAS counters of a ras/ directory (no HIP needed: tests point it at a fixture tree).
+PyObject* py_read_ras(PyObject*, PyObject* args) {
+  const char* dir;
+  if (!PyArg_ParseTuple(args, "s", &dir)) return nullptr;
+  const RasCounts r = read_ras(dir);
+  PyObject* ce = py_float_or_none(r.ce);
+  PyObject* ue = py_float_or_none(r.ue);
+  PyObject* de = py_float_or_none(r.de);
+  PyObject* pages = py_float_or_none(r.retired_pages);
+  PyObject* d = Py_BuildValue("{s:O,s:O,s:O,s:O,s:i}", "ce", ce, "ue", ue, "de", de, "retired_pages", pages,
+                              "blocks", r.blocks);
+  Py_DECREF(ce);
+  Py_DECREF(ue);
+  Py_DECREF(de);
+  Py_DECREF(pages);
+  return d;
+}
+
 PyMethodDef kMethods[] = {
     {"device_count", py_device_count, METH_NOARGS, "Number of HIP devices (0 if HIP is unavailable)."},
     {"device_info", py_device_info, METH_VARARGS, "Static inventory of one device."},
     {"link", py_link, METH_VARARGS, "(type, hops, can_access_peer) between two devices."},
     {"sample", py_sample, METH_VARARGS, "Current amdgpu sysfs telemetry of one device."},
     {"render_metrics", py_render, METH_VARARGS, "Exporter-format text exposition for every device."},
+    {"read_ras", py_read_ras, METH_VARARGS, "Summed RAS error counters of one ras/ sysfs directory."},
     {"last_error", py_last_error, METH_NOARGS, "Last HIP error string."},
     {nullptr, nullptr, 0, nullptr}};
 

@@ -62,6 +62,9 @@ struct Sample {
   double gfx_busy_pct = NAN, mem_busy_pct = NAN;
   double vram_used_b = NAN, vram_total_b = NAN;
   std::string compute_partition, memory_partition;  // "SPX"/"CPX", "NPS1"/"NPS4"
+  // RAS error counters summed over the IP blocks (NaN when the driver has no
+  // ras/ directory): corrected, uncorrected, deferred; plus retired HBM pages.
+  double ecc_correct = NAN, ecc_uncorrect = NAN, ecc_deferred = NAN, ecc_retired_pages = NAN;
 };
 
 inline bool g_hip_ok = false;
@@ -86,6 +89,75 @@ inline bool read_double(const std::string& path, double* v) {
   if (end == s.c_str()) return false;
   *v = d;
   return true;
+}
+
+struct RasCounts {
+  double ce = NAN, ue = NAN, de = NAN, retired_pages = NAN;
+  int blocks = 0;  // IP blocks that reported counters
+};
+
+// One counter file: "ue: N\nce: N[\nde: N]" (ras/aca_<block> on MI300/MI355X,
+// ras/<block>_err_count on older parts). Missing keys stay NaN.
+inline void parse_ras_counter(const std::string& text, double* ue, double* ce, double* de) {
+  std::istringstream in(text);
+  std::string line;
+  while (std::getline(in, line)) {
+    const size_t colon = line.find(':');
+    if (colon == std::string::npos) continue;
+    std::string key = line.substr(0, colon);
+    while (!key.empty() && key.back() == ' ') key.pop_back();
+    char* end = nullptr;
+    const char* num = line.c_str() + colon + 1;
+    const double v = std::strtod(num, &end);
+    if (end == num) continue;
+    if (key == "ue") *ue = v;
+    else if (key == "ce") *ce = v;
+    else if (key == "de") *de = v;
+  }
+}
+
+inline void add_count(double* acc, double v) {
+  if (std::isnan(v)) return;
+  *acc = std::isnan(*acc) ? v : *acc + v;
+}
+
+// Sum a device's RAS counters. `ras_dir` is <pci device>/ras; the retired
+// page table (gpu_vram_bad_pages) has one line per retired page. Per-block
+// aca_* files are preferred; the legacy *_err_count files are read only when
+// no aca_* file exists, so nothing is counted twice.
+inline RasCounts read_ras(const std::string& ras_dir) {
+  RasCounts r;
+  DIR* d = opendir(ras_dir.c_str());
+  if (!d) return r;
+  std::vector<std::string> aca, legacy;
+  while (dirent* e = readdir(d)) {
+    const std::string n = e->d_name;
+    if (n.rfind("aca_", 0) == 0) aca.push_back(n);
+    else if (n.size() > 10 && n.compare(n.size() - 10, 10, "_err_count") == 0) legacy.push_back(n);
+  }
+  closedir(d);
+  for (const auto& n : aca.empty() ? legacy : aca) {
+    std::string text;
+    if (!read_text(ras_dir + "/" + n, &text)) continue;
+    double ue = NAN, ce = NAN, de = NAN;
+    parse_ras_counter(text, &ue, &ce, &de);
+    if (std::isnan(ue) && std::isnan(ce)) continue;
+    add_count(&r.ue, ue);
+    add_count(&r.ce, ce);
+    add_count(&r.de, de);
+    ++r.blocks;
+  }
+  std::string pages;
+  if (read_text(ras_dir + "/gpu_vram_bad_pages", &pages)) {
+    double n = 0;
+    std::istringstream in(pages);
+    std::string line;
+    while (std::getline(in, line)) {
+      if (line.find_first_not_of(" \t") != std::string::npos) n += 1;
+    }
+    r.retired_pages = n;
+  }
+  return r;
 }
 
 inline std::string lower_bdf(const char* bus_id) {
@@ -189,6 +261,11 @@ inline Sample sample_sysfs(const std::string& bdf) {
   if (read_double(dir + "/mem_info_vram_total", &v)) s.vram_total_b = v;
   read_text(dir + "/current_compute_partition", &s.compute_partition);
   read_text(dir + "/current_memory_partition", &s.memory_partition);
+  const RasCounts ras = read_ras(dir + "/ras");
+  s.ecc_correct = ras.ce;
+  s.ecc_uncorrect = ras.ue;
+  s.ecc_deferred = ras.de;
+  s.ecc_retired_pages = ras.retired_pages;
   for (const auto& h : hwmon_dirs(dir)) {
     // power: µW
     if (std::isnan(s.power_w) && read_double(h + "/power1_average", &v)) s.power_w = v / 1e6;
@@ -274,10 +351,16 @@ inline std::string render(const RenderOptions& opt) {
       {"gpu_power_cap", "board power cap (W)"},
       {"gpu_xgmi_link_hops", "hops between two GPUs over xGMI (absent when not xGMI-connected)"},
       {"gpu_partition_info", "compute/memory partition mode of the GPU (value is always 1)"},
+      {"gpu_ecc_correct_total", "corrected RAS errors since driver load, all IP blocks"},
+      {"gpu_ecc_uncorrect_total", "uncorrected RAS errors since driver load, all IP blocks"},
+      {"gpu_ecc_deferred_total", "deferred RAS errors since driver load, all IP blocks"},
+      {"gpu_ecc_retired_pages", "HBM pages retired by the driver"},
   };
   for (auto& h : kHelp) {
     out.append("# HELP ").append(h[0]).append(" ").append(h[1]).append("\n");
-    out.append("# TYPE ").append(h[0]).append(" gauge\n");
+    const std::string n = h[0];
+    const bool counter = n.size() > 6 && n.compare(n.size() - 6, 6, "_total") == 0;
+    out.append("# TYPE ").append(h[0]).append(counter ? " counter\n" : " gauge\n");
   }
   const double mib = 1024.0 * 1024.0;
   for (int d = 0; d < g_count; ++d) {
@@ -304,6 +387,10 @@ inline std::string render(const RenderOptions& opt) {
     append_metric(&out, "gpu_memory_temperature_slowdown", labels, s.temp_mem_slowdown_c);
     append_metric(&out, "gpu_clock", labels, s.sclk_mhz);
     append_metric(&out, "gpu_memory_clock", labels, s.mclk_mhz);
+    append_metric(&out, "gpu_ecc_correct_total", labels, s.ecc_correct);
+    append_metric(&out, "gpu_ecc_uncorrect_total", labels, s.ecc_uncorrect);
+    append_metric(&out, "gpu_ecc_deferred_total", labels, s.ecc_deferred);
+    append_metric(&out, "gpu_ecc_retired_pages", labels, s.ecc_retired_pages);
     if (!s.compute_partition.empty() || !s.memory_partition.empty()) {
       append_metric(&out, "gpu_partition_info",
                     labels + ",compute_partition=\"" + escape_label(s.compute_partition) + "\",memory_partition=\"" +

@@ -97,3 +97,10 @@ def parse_exposition(text: str) -> List[Tuple[str, Dict[str, str], float]]:
             i = j + 1
         out.append((name, labels, float(val)))
     return out
+
+
+def read_ras(ras_dir: str) -> Dict[str, Optional[float]]:
+    """Summed RAS counters of an amdgpu ``ras/`` sysfs directory: ``ce``/``ue``/``de``
+    (corrected / uncorrected / deferred), ``retired_pages`` and the number of IP
+    ``blocks`` that reported. Pure file parsing: works without a GPU."""
+    return native().read_ras(ras_dir)

@@ -59,6 +59,8 @@ export const SERIES = {
     umc: 'gpu_umc_activity', // % — HBM controller busy
     temp: 'gpu_junction_temperature', // °C
     tempSlowdown: 'gpu_junction_temperature_slowdown', // °C throttle threshold (this repo's amdgpu-exporter)
+    eccCorrect: 'gpu_ecc_correct_total', // corrected RAS errors, all IP blocks
+    eccUncorrect: 'gpu_ecc_uncorrect_total', // uncorrected RAS errors, all IP blocks
     xgmiRe: 'xgmi_neighbor_[0-6]_tx_throughput', // bytes/s per neighbour
     linkHops: 'gpu_xgmi_link_hops', // measured link topology (this repo's native amdgpu-exporter)
   },
@@ -96,6 +98,8 @@ export const STALE_FAILURES = 3;
  * @property {number|null} memActivityPct
  * @property {number|null} tempC
  * @property {number|null} tempSlowdownC  junction throttle threshold (exporter), if reported
+ * @property {number|null} eccCorrectable    corrected RAS errors since driver load (exporter only)
+ * @property {number|null} eccUncorrectable  uncorrected RAS errors since driver load (exporter only)
  * @property {string|null} pod
  * @property {string|null} namespace
  *
@@ -119,7 +123,8 @@ function emptyGpu(nodeName, gpu, instance) {
   return {
     nodeName: nodeName, gpu: gpu, instance: instance,
     powerWatts: null, powerCapWatts: null, vramUsedBytes: null, vramTotalBytes: null,
-    gfxActivityPct: null, memActivityPct: null, tempC: null, tempSlowdownC: null, pod: null, namespace: null,
+    gfxActivityPct: null, memActivityPct: null, tempC: null, tempSlowdownC: null,
+    eccCorrectable: null, eccUncorrectable: null, pod: null, namespace: null,
   };
 }
 
@@ -165,6 +170,8 @@ export function joinExporterResults(r) {
   each(r[E.umc], function (g, v) { g.memActivityPct = v; });
   each(r[E.temp], function (g, v) { g.tempC = v; });
   each(r[E.tempSlowdown], function (g, v) { g.tempSlowdownC = v; });
+  each(r[E.eccCorrect], function (g, v) { g.eccCorrectable = v; });
+  each(r[E.eccUncorrect], function (g, v) { g.eccUncorrectable = v; });
   const gpus = [];
   for (const k in map) {
     const g = map[k];
@@ -275,9 +282,16 @@ export function joinNodeExporterResults(r) {
  */
 export const EXPORTER_JOIN_LABELS = ['__name__', 'hostname', 'node', 'instance', 'gpu_id', 'peer_gpu_id', 'pod', 'namespace'];
 
+/** Per-GPU exporter gauges of every refresh (topology excluded). */
+function exporterNames() {
+  const E = SERIES.exporter;
+  return [E.power, E.powerCap, E.vramUsed, E.vramTotal, E.gfx, E.umc, E.temp, E.tempSlowdown, E.eccCorrect,
+    E.eccUncorrect, E.xgmiRe];
+}
+
 export function exporterQuery(withTopology) {
   const E = SERIES.exporter;
-  const names = [E.power, E.powerCap, E.vramUsed, E.vramTotal, E.gfx, E.umc, E.temp, E.tempSlowdown, E.xgmiRe];
+  const names = exporterNames();
   // Link topology is static: callers include it only when their cached copy is stale.
   if (withTopology !== false) names.push(E.linkHops);
   return 'max by (' + EXPORTER_JOIN_LABELS.join(', ') + ') ({__name__=~"' + names.join('|') + '"})';
@@ -301,7 +315,7 @@ export const NODE_EXPORTER_JOIN_LABELS = ['__name__', 'instance', 'node', 'noden
 export function mergedQuery(withTopology) {
   const E = SERIES.exporter;
   const N = SERIES.nodeExporter;
-  const names = [E.power, E.powerCap, E.vramUsed, E.vramTotal, E.gfx, E.umc, E.temp, E.tempSlowdown, E.xgmiRe];
+  const names = exporterNames();
   if (withTopology !== false) names.push(E.linkHops);
   names.push(N.chips.split('{')[0], N.power, N.powerInput, N.powerCap, N.busy, N.vramUsed, N.vramTotal, N.uname);
   const labels = EXPORTER_JOIN_LABELS.slice();
@@ -663,8 +677,16 @@ export function summarizeMetrics(m) {
   let gfx = 0;
   let gfxN = 0;
   let withPower = 0;
+  let eccGpus = 0;
+  let eccUncorrectable = 0;
+  let eccCorrectable = 0;
   for (let i = 0; i < m.gpus.length; i++) {
     const g = m.gpus[i];
+    if (g.eccUncorrectable !== null && g.eccUncorrectable !== undefined) {
+      eccGpus++;
+      eccUncorrectable += g.eccUncorrectable;
+      eccCorrectable += g.eccCorrectable || 0;
+    }
     if (g.powerWatts !== null) {
       power += g.powerWatts;
       withPower++;
@@ -685,5 +707,8 @@ export function summarizeMetrics(m) {
     vramUsedBytes: vramUsed,
     vramTotalBytes: vramTotal,
     avgGfxActivityPct: gfxN ? gfx / gfxN : null,
+    // RAS totals over the GPUs that report them (null: no GPU does, e.g. node-exporter)
+    eccCorrectable: eccGpus ? eccCorrectable : null,
+    eccUncorrectable: eccGpus ? eccUncorrectable : null,
   };
 }

@@ -865,6 +865,7 @@ export function metricsView(ctx, mstate, opts) {
           row('Total Power', powerBar(sum.powerWatts, sum.powerCapWatts > 0 ? sum.powerCapWatts : null)),
           row('HBM In Use', hbmBar(sum.vramUsedBytes, sum.vramTotalBytes > 0 ? sum.vramTotalBytes : null)),
           row('Avg GFX Activity', pctText(sum.avgGfxActivityPct)),
+        ].concat(sum.eccUncorrectable === null ? [] : [row('RAS Errors', eccCell(sum))], [
           row('Source', m.source === 'amd-exporter' ? 'AMD Device Metrics Exporter' : 'node-exporter (amdgpu hwmon + DRM)'),
           row(
             'Last Fetched',
@@ -872,7 +873,7 @@ export function metricsView(ctx, mstate, opts) {
               ? status('warning', new Date(m.fetchedAt).toISOString().slice(11, 19) + ' UTC (stale: the latest refresh failed)')
               : new Date(m.fetchedAt).toISOString().slice(11, 19) + ' UTC'
           ),
-        ]),
+        ])),
       ])
     );
 
@@ -919,12 +920,28 @@ export function tempCell(g) {
   return text;
 }
 
+/**
+ * RAS error counts of one GPU (or cluster totals): uncorrected errors are an
+ * error (the driver may already have retired HBM pages or poisoned data),
+ * corrected ones a warning, none "OK". '—' when the source reports no RAS
+ * counters (node-exporter).
+ */
+export function eccCell(g) {
+  if (g.eccUncorrectable === null || g.eccUncorrectable === undefined) return '—';
+  const ce = g.eccCorrectable || 0;
+  if (g.eccUncorrectable > 0) {
+    return status('error', g.eccUncorrectable + ' uncorrected' + (ce > 0 ? ', ' + ce + ' corrected' : ''));
+  }
+  if (ce > 0) return status('warning', ce + ' corrected');
+  return 'OK';
+}
+
 function metricsNodeSection(name, gs) {
   return section(
     name + ' — ' + gs.length + ' × ' + MI355X.shortName,
     [
       table(
-        ['GPU', 'Power', 'HBM Used', 'GFX', 'HBM Activity', 'Temp', 'Pod'],
+        ['GPU', 'Power', 'HBM Used', 'GFX', 'HBM Activity', 'Temp', 'ECC', 'Pod'],
         gs.map(function (g) {
           return [
             'GPU ' + g.gpu,
@@ -933,6 +950,7 @@ function metricsNodeSection(name, gs) {
             pctText(g.gfxActivityPct),
             pctText(g.memActivityPct),
             tempCell(g),
+            eccCell(g),
             g.pod ? (g.namespace ? g.namespace + '/' : '') + g.pod : '—',
           ];
         }),

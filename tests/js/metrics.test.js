@@ -421,4 +421,23 @@ describe('summarizeMetrics', () => {
     expect(s.powerCapWatts).toBe(8 * 1400);
     expect(s.avgGfxActivityPct).toBe(50);
   });
+  it('totals RAS counters only over GPUs that report them', () => {
+    const E = SERIES.exporter;
+    const r = exporterData(['n0']);
+    r[E.eccCorrect] = [vec({ hostname: 'n0', gpu_id: '0' }, 4), vec({ hostname: 'n0', gpu_id: '1' }, 0)];
+    r[E.eccUncorrect] = [vec({ hostname: 'n0', gpu_id: '0' }, 1), vec({ hostname: 'n0', gpu_id: '1' }, 0)];
+    const j = joinExporterResults(r);
+    expect([j.gpus[0].eccCorrectable, j.gpus[0].eccUncorrectable]).toEqual([4, 1]);
+    expect(j.gpus[2].eccUncorrectable).toBeNull();
+    const s = summarizeMetrics(j);
+    expect([s.eccCorrectable, s.eccUncorrectable]).toEqual([4, 1]);
+    expect(summarizeMetrics(joinExporterResults(exporterData(['n0']))).eccUncorrectable).toBeNull();
+  });
+  it('asks for the RAS counters in the refresh and merged queries', () => {
+    const E = SERIES.exporter;
+    [exporterQuery(false), mergedQuery(false)].forEach((q) => {
+      expect(q).toContain(E.eccCorrect);
+      expect(q).toContain(E.eccUncorrect);
+    });
+  });
 });

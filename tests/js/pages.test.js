@@ -12,6 +12,7 @@ import {
   podDetailView,
   podGpuAssignments,
   tempCell,
+  eccCell,
   metricsView,
   formatWindow,
   allocationBar,
@@ -311,6 +312,30 @@ describe('temperature against the throttle threshold', () => {
   it('falls back to the MI355X threshold without exporter data', () => {
     expect(MI355X.junctionSlowdownC).toBe(100);
     expect(tempCell({ tempC: 95, tempSlowdownC: null }).status).toBe('warning');
+  });
+});
+
+describe('RAS error cell', () => {
+  it('is OK when clean, a warning for corrected and an error for uncorrected errors', () => {
+    expect(eccCell({ eccCorrectable: 0, eccUncorrectable: 0 })).toBe('OK');
+    expect(eccCell({ eccCorrectable: 3, eccUncorrectable: 0 })).toEqual({ t: 'status', status: 'warning', text: '3 corrected' });
+    expect(eccCell({ eccCorrectable: 3, eccUncorrectable: 1 })).toEqual({
+      t: 'status', status: 'error', text: '1 uncorrected, 3 corrected' });
+    expect(eccCell({ eccCorrectable: null, eccUncorrectable: null })).toBe('—');
+  });
+  it('adds an ECC column per GPU and a cluster RAS row on the Metrics page', () => {
+    const E = SERIES.exporter;
+    const r = {};
+    r[E.power] = [0, 1].map((i) => ({ metric: { hostname: 'g0', gpu_id: String(i) }, value: [0, '900'] }));
+    r[E.eccCorrect] = [0, 1].map((i) => ({ metric: { hostname: 'g0', gpu_id: String(i) }, value: [0, String(i * 2)] }));
+    r[E.eccUncorrect] = [0, 1].map((i) => ({ metric: { hostname: 'g0', gpu_id: String(i) }, value: [0, '0'] }));
+    const m = Object.assign(joinExporterResults(r), { source: 'amd-exporter', fetchedAt: NOW, prometheusPath: '/p' });
+    const vm = metricsView(makeContext({ nodes: [makeGpuNode('g0')] }), { metrics: m, series: null, fetching: false }, {});
+    const t = firstTable(findSection(vm, 'g0 — 2 × ' + MI355X.shortName));
+    expect(t.columns).toContain('ECC');
+    const col = t.columns.indexOf('ECC');
+    expect(t.rows.map((row) => text(row[col]))).toEqual(['OK', '2 corrected']);
+    expect(text(rowValue(findSection(vm, 'GPU Power Summary'), 'RAS Errors'))).toBe('2 corrected');
   });
 });
 

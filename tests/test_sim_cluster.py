@@ -92,7 +92,7 @@ def test_exporter_telemetry_series_counts():
     c = SyntheticCluster(spec_for_nodes(2))
     db = promql.TSDB()
     n = populate(db, c, source="amd-exporter")
-    assert n == 2 * 8 * (8 + 7 + 7)  # 8 gauges + 7 xGMI throughput + 7 link-hop series per GPU
+    assert n == 2 * 8 * (10 + 7 + 7)  # 8 gauges + 2 RAS counters + 7 xGMI throughput + 7 link-hop series per GPU
 
 
 def test_busy_gpus_draw_more_power_and_carry_pod_labels():
