@@ -121,6 +121,7 @@ class TSDB:
         self._proj_json: Dict[int, tuple] = {}
         self._fn_intervals: set = set()
         self._query_cache: Dict[str, tuple] = {}
+        self._range_cache: Dict[str, tuple] = {}  # query → (mutation stamp, {t → rows})
 
     def label_json(self, labels: Labels) -> str:
         """JSON for a label set; cached when it is a stored series' own dict
@@ -624,6 +625,14 @@ def query_range(db: TSDB, q: str, start: float, end: float, step: float):
         return {"status": "error", "errorType": "bad_data", "error": "invalid range"}
     if (end - start) / step > 11000:
         return {"status": "error", "errorType": "bad_data", "error": "exceeded maximum resolution of 11,000 points"}
+    # Per-step results are memoised while no series was pushed (same rule as
+    # query()): a window that slides by one step re-evaluates one step. A real
+    # Prometheus evaluates the whole window in milliseconds; evaluating it
+    # point by point in Python would otherwise dominate the fake's latency.
+    memo = db._range_cache.get(q)
+    if memo is None or memo[0] != _MUTATIONS[0]:
+        memo = db._range_cache[q] = (_MUTATIONS[0], {})
+    steps = memo[1]
     try:
         node = parse(q)
         ev = Evaluator(db)
@@ -631,16 +640,22 @@ def query_range(db: TSDB, q: str, start: float, end: float, step: float):
         n = int(math.floor((end - start) / step))
         for i in range(n + 1):
             t = start + i * step
-            typ, val = ev.instant(node, t)
-            if typ == "scalar":
-                val = [({}, val)]
-            tsr = repr(float(t))
-            for labels, v in val:
-                k = tuple(sorted(labels.items()))
+            rows = steps.get(t)
+            if rows is None:
+                typ, val = ev.instant(node, t)
+                if typ == "scalar":
+                    val = [({}, val)]
+                tsr = repr(float(t))
+                rows = [(tuple(sorted(labels.items())), labels, "[" + tsr + ',"' + _fmt(v) + '"]') for labels, v in val]
+                steps[t] = rows
+            for k, labels, cell in rows:
                 ent = series.get(k)
                 if ent is None:
                     ent = series[k] = (labels, [])
-                ent[1].append("[" + tsr + ',"' + _fmt(v) + '"]')
+                ent[1].append(cell)
+        if len(steps) > 4 * (n + 1) + 64:  # keep the memo bounded to about the live window
+            for t in sorted(steps)[: len(steps) - 2 * (n + 1)]:
+                del steps[t]
     except PromQLError as e:
         return {"status": "error", "errorType": "bad_data", "error": str(e)}
     parts = ['{"metric":' + db.label_json(l) + ',"values":[' + ",".join(vs) + "]}" for l, vs in series.values()]
