@@ -282,18 +282,24 @@ export function joinNodeExporterResults(r) {
  */
 export const EXPORTER_JOIN_LABELS = ['__name__', 'hostname', 'node', 'instance', 'gpu_id', 'peer_gpu_id', 'pod', 'namespace'];
 
-/** Per-GPU exporter gauges of every refresh (topology excluded). */
-function exporterNames() {
+/**
+ * Per-GPU exporter gauges. The static ones (HBM capacity, power cap, throttle
+ * threshold, link topology) change only with a reconfiguration of the node,
+ * so callers ask for them once per DISCOVERY_TTL_MS and keep a copy; every
+ * refresh asks for the live ones.
+ */
+function exporterNames(withStatic) {
   const E = SERIES.exporter;
-  return [E.power, E.powerCap, E.vramUsed, E.vramTotal, E.gfx, E.umc, E.temp, E.tempSlowdown, E.eccCorrect,
-    E.eccUncorrect, E.xgmiRe];
+  const names = [E.power, E.vramUsed, E.gfx, E.umc, E.temp, E.eccCorrect, E.eccUncorrect, E.xgmiRe];
+  if (withStatic !== false) names.push(E.powerCap, E.vramTotal, E.tempSlowdown, E.linkHops);
+  return names;
 }
 
-export function exporterQuery(withTopology) {
-  const E = SERIES.exporter;
-  const names = exporterNames();
-  // Link topology is static: callers include it only when their cached copy is stale.
-  if (withTopology !== false) names.push(E.linkHops);
+/** Fields of GpuTelemetry that come from the static series (see exporterNames). */
+export const STATIC_GPU_FIELDS = ['powerCapWatts', 'vramTotalBytes', 'tempSlowdownC'];
+
+export function exporterQuery(withStatic) {
+  const names = exporterNames(withStatic);
   return 'max by (' + EXPORTER_JOIN_LABELS.join(', ') + ') ({__name__=~"' + names.join('|') + '"})';
 }
 
@@ -312,11 +318,9 @@ export const NODE_EXPORTER_JOIN_LABELS = ['__name__', 'instance', 'node', 'noden
  * union of the labels the two joins read. Later refreshes ask only the
  * exporter that answered.
  */
-export function mergedQuery(withTopology) {
-  const E = SERIES.exporter;
+export function mergedQuery(withStatic) {
   const N = SERIES.nodeExporter;
-  const names = exporterNames();
-  if (withTopology !== false) names.push(E.linkHops);
+  const names = exporterNames(withStatic);
   names.push(N.chips.split('{')[0], N.power, N.powerInput, N.powerCap, N.busy, N.vramUsed, N.vramTotal, N.uname);
   const labels = EXPORTER_JOIN_LABELS.slice();
   for (let i = 0; i < NODE_EXPORTER_JOIN_LABELS.length; i++) {
@@ -431,7 +435,8 @@ export function createMetricsSource(opts) {
   let cachedAt = 0;
   let discovering = null;
   let source = null; // which exporter answered last time
-  let links = null; // measured xGMI link topology per node (static), refreshed every `ttl`
+  let links = null; // measured xGMI link topology per node (static), refreshed every `ttl` with `statics`
+  let statics = null; // static per-GPU fields (STATIC_GPU_FIELDS), fetched with the topology
   let linksAt = 0;
   let last = null; // previous snapshot, for structural sharing
   let failures = 0; // consecutive failed fetches against the cached service
@@ -478,6 +483,7 @@ export function createMetricsSource(opts) {
     source = null;
     seriesCache = null;
     links = null;
+    statics = null;
     last = null;
   }
 
@@ -544,9 +550,9 @@ export function createMetricsSource(opts) {
   }
 
   function snapshotFrom(base) {
-    const withTopology = links === null || clock.now() - linksAt >= ttl;
-    const q = source === 'amd-exporter' ? exporterQuery(withTopology)
-      : source === 'node-exporter' ? nodeExporterQuery() : mergedQuery(withTopology);
+    const withStatic = links === null || clock.now() - linksAt >= ttl;
+    const q = source === 'amd-exporter' ? exporterQuery(withStatic)
+      : source === 'node-exporter' ? nodeExporterQuery() : mergedQuery(withStatic);
     return combined(base, q).then(function (res) {
       if (!res.ok) return UNREACHABLE;
       failures = 0;
@@ -558,11 +564,15 @@ export function createMetricsSource(opts) {
         if (j.gpus.length) {
           joined = j;
           src = 'amd-exporter';
-          if (withTopology) {
+          if (withStatic) {
             links = j.links;
+            statics = staticsOf(j.gpus);
             linksAt = clock.now();
           } else {
             joined.links = links;
+            // A GPU the static copy does not know yet (node added since):
+            // fetch the static series again on the next refresh.
+            if (!applyStatics(j.gpus, statics)) linksAt = -Infinity;
           }
         }
       }
@@ -666,6 +676,36 @@ export function createMetricsSource(opts) {
     fetchSeries: fetchSeries,
     source: function () { return source; },
   };
+}
+
+function gpuKey(g) {
+  return g.nodeName + '\u0000' + g.gpu;
+}
+
+/** The static fields of each GPU, keyed by (node, gpu). */
+export function staticsOf(gpus) {
+  const out = {};
+  for (let i = 0; i < gpus.length; i++) {
+    const g = gpus[i];
+    const v = {};
+    for (let f = 0; f < STATIC_GPU_FIELDS.length; f++) v[STATIC_GPU_FIELDS[f]] = g[STATIC_GPU_FIELDS[f]];
+    out[gpuKey(g)] = v;
+  }
+  return out;
+}
+
+/** Copy cached static fields onto freshly joined GPUs; false if some GPU has none cached. */
+export function applyStatics(gpus, statics) {
+  let complete = true;
+  for (let i = 0; i < gpus.length; i++) {
+    const c = statics && statics[gpuKey(gpus[i])];
+    if (!c) {
+      complete = false;
+      continue;
+    }
+    for (let f = 0; f < STATIC_GPU_FIELDS.length; f++) gpus[i][STATIC_GPU_FIELDS[f]] = c[STATIC_GPU_FIELDS[f]];
+  }
+  return complete;
 }
 
 /** Cluster totals for the summary box. */

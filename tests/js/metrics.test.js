@@ -17,6 +17,8 @@ import {
   shareGpus,
   shareMap,
   summarizeMetrics,
+  staticsOf,
+  applyStatics,
 } from '../../src/api/metrics.js';
 
 const BASE0 = servicePath(PROMETHEUS_SERVICES[0]);
@@ -255,6 +257,47 @@ describe('fetchGpuMetrics', () => {
     await src.fetchGpuMetrics();
     expect(asked()[asked().length - 1]).toContain('gpu_xgmi_link_hops');
   });
+  it('fetches static per-GPU series with the topology and serves them from the copy in between', async () => {
+    const E = SERIES.exporter;
+    const d = exporterData(['n0']);
+    d[E.powerCap] = [vec({ __name__: E.powerCap, hostname: 'n0', gpu_id: '0' }, 1200)];
+    const request = prom({ data: d });
+    let now = 1000000;
+    const src = createMetricsSource({ request, clock: { setTimeout, clearTimeout, now: () => now } });
+    const a = await src.fetchGpuMetrics();
+    now += 1000;
+    const b = await src.fetchGpuMetrics();
+    const second = decodeURIComponent(request.mock.calls[1][0]);
+    [E.powerCap, E.vramTotal, E.tempSlowdown].forEach((n) => expect(second).not.toContain(n));
+    expect(b.gpus[0].powerCapWatts).toBe(1200);
+    expect(b.gpus[0].vramTotalBytes).toBe(a.gpus[0].vramTotalBytes);
+    expect(b.gpus).toBe(a.gpus); // nothing changed: the same objects
+  });
+  it('refetches the static series when a GPU appears that the copy does not know', async () => {
+    const E = SERIES.exporter;
+    let inner = prom({ data: exporterData(['n0']) });
+    const request = vi.fn((p) => inner(p));
+    let now = 1000000;
+    const src = createMetricsSource({ request, clock: { setTimeout, clearTimeout, now: () => now } });
+    await src.fetchGpuMetrics();
+    // A node joins: its live series arrive on the next refresh, without statics.
+    inner = prom({ data: exporterData(['n0', 'n1']) });
+    now += 1000;
+    await src.fetchGpuMetrics();
+    now += 1000;
+    const c = await src.fetchGpuMetrics();
+    const asked = request.mock.calls.map((x) => decodeURIComponent(x[0]));
+    expect(asked[1]).not.toContain(E.vramTotal);
+    expect(asked[2]).toContain(E.vramTotal);
+    expect(c.gpus.find((g) => g.nodeName === 'n1').vramTotalBytes).toBeGreaterThan(0);
+  });
+  it('applyStatics reports GPUs missing from the copy', () => {
+    const g = [{ nodeName: 'n', gpu: '0', powerCapWatts: null }, { nodeName: 'n', gpu: '1', powerCapWatts: null }];
+    const st = staticsOf([{ nodeName: 'n', gpu: '0', powerCapWatts: 1400, vramTotalBytes: 1, tempSlowdownC: 100 }]);
+    expect(applyStatics(g, st)).toBe(false);
+    expect(g[0].powerCapWatts).toBe(1400);
+    expect(g[1].powerCapWatts).toBeNull();
+  });
   it('remembers the answering source and skips the other', async () => {
     const request = prom();
     const src = createMetricsSource({ request });
@@ -296,7 +339,8 @@ describe('fetchGpuMetrics', () => {
     const paths = request.mock.calls.map((c) => decodeURIComponent(c[0]));
     expect(paths).toHaveLength(1);
     expect(paths[0].indexOf(BASE0)).toBe(0);
-    expect(paths[0]).toContain('gpu_power_usage|gpu_power_cap|gpu_used_vram');
+    expect(paths[0]).toContain('gpu_power_usage|gpu_used_vram');
+    expect(paths[0]).toContain('gpu_power_cap|gpu_total_vram');
     expect(paths[0]).toContain('node_hwmon_chip_names|node_hwmon_power_average_watt');
     expect(m.source).toBe('amd-exporter');
     await src.fetchGpuMetrics();
