@@ -1,18 +1,13 @@
 import '@testing-library/jest-dom';
+import { cleanup } from '@testing-library/react';
+import { afterEach } from 'vitest';
+import { resetSharedStores } from './src/api/clusterStore.js';
 
-// Node 22+ ships a property-bag `localStorage` global that shadows jsdom's
-// Web Storage; install a spec-compliant one so code under test behaves.
-if (typeof localStorage !== 'undefined' && typeof localStorage.getItem !== 'function') {
-  const store = new Map<string, string>();
-  const storage: Storage = {
-    getItem: (k: string) => (store.has(k) ? (store.get(k) as string) : null),
-    setItem: (k: string, v: string) => void store.set(k, String(v)),
-    removeItem: (k: string) => void store.delete(k),
-    clear: () => store.clear(),
-    key: (i: number) => Array.from(store.keys())[i] ?? null,
-    get length() {
-      return store.size;
-    },
-  };
-  Object.defineProperty(globalThis, 'localStorage', { value: storage, configurable: true, writable: true });
-}
+// Provider instances share one module-level store per cluster (ADR 001), so a
+// snapshot cached by one spec would otherwise be served to the next one.
+// Settings need no storage shim: src/api/settings.js falls back to defaults
+// when `localStorage` is missing or is Node's method-less global.
+afterEach(() => {
+  cleanup();
+  resetSharedStores();
+});
