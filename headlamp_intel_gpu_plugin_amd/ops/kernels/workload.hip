@@ -12,9 +12,12 @@
 //                   staged by LDS-DMA (global_load_lds_dwordx4) with a
 //                   source-side XOR swizzle, 8-phase ping-pong schedule with
 //                   three half-tiles in flight (design notes above the
-//                   kernel). Used when M,N % 256 == 0, K % 128 == 0 and the
-//                   grid has ≥ 128 blocks: 1483 TFLOP/s at 8192³ on random
-//                   operands (profiles/r1_gemm_ab.json);
+//                   kernel), and a packed epilogue (operands swapped in
+//                   the MFMA so each lane holds a row segment, cvt_pk +
+//                   permlane16_swap → 16-byte stores). Used when
+//                   M,N % 256 == 0, K % 128 == 0 and the grid has ≥ 128
+//                   blocks: 1566 TFLOP/s at 8192³ on random operands
+//                   (profiles/r1_gemm_ab_latest.json);
 //                   gemm_bf16_nt<256,256,2,4> — same tile, register-staged
 //                   double buffer (1121 TFLOP/s), for K % 128 == 64;
 //                   gemm_bf16_nt<128,128,2,2> — 4 waves, 64×64 per wave,
@@ -61,6 +64,15 @@ __device__ __forceinline__ uint16_t f32_to_bf16_rne(float f) {
   if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fc0;  // NaN
   u += 0x7fffu + ((u >> 16) & 1u);
   return static_cast<uint16_t>(u >> 16);
+}
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+// Two floats → packed bf16 (lo in bits 0-15), round-to-nearest-even: one
+// v_cvt_pk_bf16_f32 on gfx950.
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){lo, hi}, bf16x2));
 }
 
 // Bijective remap: blocks b and b+8 run on the same XCD (round-robin dispatch),
@@ -322,6 +334,10 @@ __global__ __launch_bounds__(P8_THREADS) void gemm_bf16_nt_8ph(const uint16_t* _
       bq[nh][nt * 2 + 1] = *reinterpret_cast<const bf16x8*>(row_ + (rd0 ^ 64));                            \
     }                                                                                                      \
   }
+// Operands enter the MFMA as (B, A): the product is the 16×16 tile of Cᵀ,
+// whose C/D layout puts FOUR CONSECUTIVE COLUMNS of one C row in each lane
+// (row m = lane&15, columns 4(lane>>4)..+3) — what the packed epilogue
+// below stores. Same fragments, same products, same accumulation.
 #define P8_MFMA(mh, nh)                                                                                    \
   {                                                                                                        \
     __builtin_amdgcn_s_setprio(1);                                                                         \
@@ -329,7 +345,7 @@ __global__ __launch_bounds__(P8_THREADS) void gemm_bf16_nt_8ph(const uint16_t* _
     _Pragma("unroll") for (int mt = 0; mt < 4; ++mt)                                                       \
     _Pragma("unroll") for (int nt = 0; nt < 2; ++nt)                                                       \
       acc[(mh) * 4 + mt][(nh) * 2 + nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(                         \
-          af[mt * 2 + ks], bq[nh][nt * 2 + ks], acc[(mh) * 4 + mt][(nh) * 2 + nt], 0, 0, 0);               \
+          bq[nh][nt * 2 + ks], af[mt * 2 + ks], acc[(mh) * 4 + mt][(nh) * 2 + nt], 0, 0, 0);               \
     __builtin_amdgcn_s_setprio(0);                                                                         \
   }
 #define P8_SYNC_MFMA(mh, nh)                                                                               \
@@ -390,18 +406,30 @@ __global__ __launch_bounds__(P8_THREADS) void gemm_bf16_nt_8ph(const uint16_t* _
 #undef P8_MFMA
 #undef P8_SYNC_MFMA
 
-  const int ccol = lane & 15;
-  const int crow = (lane >> 4) * 4;
+  // Epilogue (guide T21): acc[i][j] holds C[row][4g..4g+3] of its 16×16 tile,
+  // g = lane>>4. Pack to bf16 pairs, then one v_permlane16_swap per dword
+  // between the two 16-column tiles of a 32-column subtile (j = 2p, 2p+1)
+  // leaves each lane 8 CONSECUTIVE columns: lane group g holds columns
+  // 16(g&1) + 8(g>>1) .. +7 — one 16-byte store where the plain layout
+  // needed sixteen 2-byte ones (the store tail is issue-bound).
+  const int g = lane >> 4;
+  const int col16 = (g & 1) * 16 + (g >> 1) * 8;
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < 8; ++i) {
+    const int row = m0 + wr * 128 + (i >> 2) * 64 + (i & 3) * 16 + (lane & 15);
+    uint16_t* crow = C + static_cast<size_t>(row) * N + n0 + wc * 64 + col16;
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wr * 128 + (i >> 2) * 64 + (i & 3) * 16 + crow + r;
-        const int col = n0 + wc * 64 + (j >> 1) * 32 + (j & 1) * 16 + ccol;
-        C[static_cast<size_t>(row) * N + col] = f32_to_bf16_rne(acc[i][j][r]);
-      }
+    for (int p = 0; p < 2; ++p) {
+      uint32_t a0 = pack_bf16x2(acc[i][2 * p][0], acc[i][2 * p][1]);
+      uint32_t a1 = pack_bf16x2(acc[i][2 * p][2], acc[i][2 * p][3]);
+      uint32_t b0 = pack_bf16x2(acc[i][2 * p + 1][0], acc[i][2 * p + 1][1]);
+      uint32_t b1 = pack_bf16x2(acc[i][2 * p + 1][2], acc[i][2 * p + 1][3]);
+      // Odd 16-lane rows of the first operand swap with even rows of the second.
+      const auto s0 = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
+      const auto s1 = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
+      *reinterpret_cast<u32x4*>(crow + p * 32) = u32x4{s0[0], s1[0], s0[1], s1[1]};
+    }
+  }
 }
 
 // One pass, no grid-stride loop: each thread moves TRIAD_U 16-byte vectors,
@@ -472,9 +500,10 @@ const char* launch_8ph(const void* a, const void* b, void* c, int m, int n, int 
 // register-staged, 3 = 256² 8-phase LDS-DMA.
 enum { kAuto = 0, kTile128 = 1, kTile256 = 2, kTile256Dma = 3 };
 
-bool fits_8ph(int m, int n, int k) {
-  // 32-bit per-lane source offsets: every element index must fit in uint32.
-  return m % 256 == 0 && n % 256 == 0 && k % 128 == 0 &&
+bool fits_8ph(const void* c, int m, int n, int k) {
+  // 32-bit per-lane source offsets: every element index must fit in uint32;
+  // the packed epilogue stores 16 bytes per lane, so C must be 16-B aligned.
+  return m % 256 == 0 && n % 256 == 0 && k % 128 == 0 && (reinterpret_cast<uintptr_t>(c) & 15) == 0 &&
          static_cast<uint64_t>(m) * k < (1ull << 32) && static_cast<uint64_t>(n) * k < (1ull << 32);
 }
 
@@ -490,7 +519,8 @@ const char* launch_gemm(const void* a, const void* b, void* c, int m, int n, int
       if (!big) return "gemm_bf16_nt: the 256x256 tile needs M,N multiples of 256";
       return launch_tile<256, 256, 2, 4>(a, b, c, m, n, k, stream, &g_big_attr);
     case kTile256Dma:
-      if (!fits_8ph(m, n, k)) return "gemm_bf16_nt: the 8-phase tile needs M,N multiples of 256, K of 128, M*K and N*K < 2^32";
+      if (!fits_8ph(c, m, n, k))
+        return "gemm_bf16_nt: the 8-phase tile needs M,N multiples of 256, K of 128, M*K and N*K < 2^32, C 16-byte aligned";
       return launch_8ph(a, b, c, m, n, k, stream);
     case kAuto:
       break;
@@ -499,7 +529,7 @@ const char* launch_gemm(const void* a, const void* b, void* c, int m, int n, int
   }
   // The 256² tiles need ≥ one block per CU to beat the 128² tile (256 CUs).
   if (big && (m / 256) * (n / 256) >= 128) {
-    if (fits_8ph(m, n, k)) return launch_8ph(a, b, c, m, n, k, stream);
+    if (fits_8ph(c, m, n, k)) return launch_8ph(a, b, c, m, n, k, stream);
     return launch_tile<256, 256, 2, 4>(a, b, c, m, n, k, stream, &g_big_attr);
   }
   return launch_tile<128, 128, 2, 2>(a, b, c, m, n, k, stream, &g_small_attr);

@@ -185,6 +185,21 @@ def test_gemm_variant_rejects_unfit_shapes(dev):
         workload.gemm_bf16_nt(a, a, variant="nope")
 
 
+def test_gemm_misaligned_output(dev):
+    # The 8-phase kernel's packed epilogue stores 16 B per lane: a C that is
+    # contiguous but not 16-B aligned is refused by that variant and routed
+    # to a 2-byte-store kernel by `auto`, with the same result.
+    g = torch.Generator(device=dev).manual_seed(7)
+    a = torch.randn(2048, 256, device=dev, dtype=torch.bfloat16, generator=g)
+    b = torch.randn(4096, 256, device=dev, dtype=torch.bfloat16, generator=g)
+    buf = torch.empty(2048 * 4096 + 1, device=dev, dtype=torch.bfloat16)
+    out = buf[1:].view(2048, 4096)  # 2-byte offset
+    with pytest.raises(RuntimeError):
+        workload.gemm_bf16_nt(a, b, out=out, variant="tile256_dma")
+    workload.gemm_bf16_nt(a, b, out=out)
+    assert torch.equal(out, workload.gemm_bf16_nt(a, b, variant="tile256"))
+
+
 def test_gemm_variants_throughput(dev):
     # A/B in one process (guide §5.4 rule 24): the kernel the default dispatch
     # picks at this shape (8-phase LDS-DMA) must beat the other two, and `auto`
