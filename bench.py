@@ -136,8 +136,9 @@ def main(argv=None) -> int:
             D.barrier(info)
             elapsed = time.perf_counter() - t0
             amd_switch = drv.call("switch", "amd", n=5)
+            detail = drv.call("detail", "amd", n=5)["detail"]
             result = {"ref": ref, "ref_cold": ref_cold, "ref_switch": ref_switch,
-                      "amd": amd, "amd_cold": amd_cold, "amd_switch": amd_switch,
+                      "amd": amd, "amd_cold": amd_cold, "amd_switch": amd_switch, "detail": detail,
                       "server_requests": fc.stats(),
                       "scrapes": scraper.scrapes if scraper else 0}
         finally:
@@ -201,6 +202,11 @@ def main(argv=None) -> int:
                                  "reference": round(summarize(result["ref_cold"]["latencies"])["p50"], 3)},
             "route_switch_p50_ms": {"amd": round(summarize(result["amd_switch"]["latencies"])["p50"], 3),
                                     "reference": round(summarize(result["ref_switch"]["latencies"])["p50"], 3)},
+            # Native Pod / Node detail page opened on a warm cluster: the node's
+            # telemetry by a hostname-scoped query vs the cluster-wide snapshot.
+            "detail_open": {k: {"p50_ms": round(summarize(v["latencies"])["p50"], 3) if v["latencies"] else None,
+                                "bytes": round(v["bytesPerOpen"]), "requests": v["requestsPerOpen"]}
+                            for k, v in result["detail"].items()},
             "rendered": {"gpu_nodes": rows["gpuNodes"], "gpu_pods": rows["gpuPods"],
                          "gpus_monitored": rows["gpusMonitored"], "gpu_cells": rows["gpuCells"],
                          "pod_table_rows": rows["podTableRows"], "detail_sections": rows["detailSections"]},

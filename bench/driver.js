@@ -401,6 +401,47 @@ async function serve(a) {
           L.opened = true;
         }
         out.files = writeSnapshots(L.s.ctx(), L.s.mstate(), c.dir, c.now);
+      } else if (c.cmd === 'detail') {
+        // Native detail pages opened on a warm cluster (a plugin page loaded
+        // before): Pod detail and Node detail each fetch their node's
+        // telemetry with a hostname-scoped query on a fresh metrics client,
+        // next to the cluster-wide snapshot the pod detail would otherwise need.
+        const L = get('amd');
+        if (!L.opened) {
+          await L.s.coldOpen();
+          L.opened = true;
+        }
+        const ctx = L.s.ctx();
+        const pods = ctx.gpuPods.filter(function (p) { return p.spec && p.spec.nodeName; });
+        const modes = { podScoped: [], podClusterWide: [], nodeScoped: [] };
+        const bytes = { podScoped: 0, podClusterWide: 0, nodeScoped: 0 };
+        const reqs = { podScoped: 0, podClusterWide: 0, nodeScoped: 0 };
+        for (let i = 0; i < n && pods.length; i++) {
+          const pod = pods[i % pods.length];
+          const node = ctx.gpuNodes.filter(function (x) { return x.metadata.name === pod.spec.nodeName; })[0];
+          const runs = [
+            ['podScoped', function (src) { return src.fetchNodeMetrics(pod.spec.nodeName).then(function (m) { return podDetailView(pod, { metrics: m }); }); }],
+            ['podClusterWide', function (src) { return src.fetchGpuMetrics().then(function (m) { return podDetailView(pod, { metrics: m }); }); }],
+            ['nodeScoped', function (src) {
+              return src.fetchNodeMetrics(pod.spec.nodeName).then(function (m) { return node ? nodeDetailView(node, ctx, { metrics: m }) : null; });
+            }],
+          ];
+          for (let r = 0; r < runs.length; r++) {
+            const src = createMetricsSource({ request: makeRequest(a.url, counter) });
+            const b0 = counter.bytes;
+            const n0 = counter.n;
+            const t0 = process.hrtime();
+            const s = await runs[r][1](src);
+            if (s) renderSection(s);
+            modes[runs[r][0]].push(ms(process.hrtime(t0)));
+            bytes[runs[r][0]] += counter.bytes - b0;
+            reqs[runs[r][0]] += counter.n - n0;
+          }
+        }
+        out.detail = {};
+        for (const k in modes) {
+          out.detail[k] = { latencies: modes[k], bytesPerOpen: bytes[k] / Math.max(1, modes[k].length), requestsPerOpen: reqs[k] / Math.max(1, modes[k].length) };
+        }
       } else if (c.cmd === 'switch') {
         const L = get(name);
         if (!L.opened) {

@@ -3,7 +3,7 @@ import { renderHook, waitFor } from '@testing-library/react';
 import React from 'react';
 import { beforeEach, describe, expect, it, vi } from 'vitest';
 import { makeDeviceConfig, makeGpuNode, makePluginPod } from '../../tests/js/fixtures.js';
-import { AmdGpuDataProvider, useAmdGpuContext } from './AmdGpuDataContext';
+import { AmdGpuDataProvider, useAmdGpuContext, useNodeGpuMetrics } from './AmdGpuDataContext';
 import { resetSharedStores } from './clusterStore.js';
 
 vi.mock('@kinvolk/headlamp-plugin/lib', () => ({
@@ -85,5 +85,27 @@ describe('AmdGpuDataProvider', () => {
     const before = vi.mocked(ApiProxy.request).mock.calls.length;
     result.current.refresh();
     await waitFor(() => expect(vi.mocked(ApiProxy.request).mock.calls.length).toBeGreaterThan(before));
+  });
+});
+
+describe('useNodeGpuMetrics', () => {
+  it('asks Prometheus for the one node only (hostname matcher)', async () => {
+    vi.mocked(ApiProxy.request).mockResolvedValue({
+      status: 'success',
+      data: {
+        resultType: 'vector',
+        result: [{ metric: { __name__: 'gpu_power_usage', hostname: 'g0', gpu_id: '0' }, value: [0, '700'] }],
+      },
+    });
+    const { result } = renderHook(() => useNodeGpuMetrics('g0'));
+    await waitFor(() => expect(result.current.metrics).not.toBeNull());
+    expect(result.current.metrics!.gpus.map(g => [g.nodeName, g.powerWatts])).toEqual([['g0', 700]]);
+    const paths = vi.mocked(ApiProxy.request).mock.calls.map(c => decodeURIComponent(String(c[0])));
+    expect(paths.every(p => p.indexOf('hostname="g0"') >= 0)).toBe(true);
+  });
+
+  it('fetches nothing without a node name', () => {
+    renderHook(() => useNodeGpuMetrics(null));
+    expect(vi.mocked(ApiProxy.request)).not.toHaveBeenCalled();
   });
 });

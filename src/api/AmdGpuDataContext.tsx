@@ -178,3 +178,51 @@ export function useGpuMetrics(enabled = true, withSeries = true): GpuMetricsStat
 
   return useMemo(() => ({ ...state, refresh: () => setSeq(s => s + 1) }), [state]);
 }
+
+/**
+ * Telemetry of one node's GPUs for the native Node / Pod detail pages: a
+ * `hostname`-scoped query through the shared client (metrics.js
+ * fetchNodeMetrics), so a detail page costs the same few KB on a 500-node
+ * cluster as on one node. `nodeName` null (or `enabled` false) fetches
+ * nothing.
+ */
+export function useNodeGpuMetrics(nodeName: string | null, enabled = true): GpuMetricsState {
+  const source = metricsSourceFor(clusterKey());
+  const refreshIntervalSec = loadSettings().refreshIntervalSec;
+  const active = enabled && !!nodeName;
+  const [state, setState] = useState<Omit<GpuMetricsState, 'refresh'>>({
+    metrics: null,
+    series: null,
+    fetchError: null,
+    fetching: false,
+  });
+  const [seq, setSeq] = useState(0);
+
+  useEffect(() => {
+    if (!active || !nodeName) return;
+    let cancelled = false;
+    setState(s => ({ ...s, fetching: true, fetchError: null }));
+    source
+      .fetchNodeMetrics(nodeName)
+      .then(metrics => {
+        if (cancelled) return;
+        setState({ metrics, series: null, fetching: false, fetchError: metrics ? null : PROMETHEUS_UNREACHABLE });
+      })
+      .catch((e: unknown) => {
+        if (cancelled) return;
+        setState(s => ({ ...s, fetching: false, fetchError: e instanceof Error ? e.message : String(e) }));
+      });
+    return () => {
+      cancelled = true;
+    };
+  }, [active, nodeName, seq, source]);
+
+  useEffect(() => {
+    if (!active) return;
+    const poller = createPoller(refreshIntervalSec);
+    poller.start(() => setSeq(s => s + 1));
+    return () => poller.stop();
+  }, [active, refreshIntervalSec]);
+
+  return useMemo(() => ({ ...state, refresh: () => setSeq(s => s + 1) }), [state]);
+}

@@ -303,6 +303,36 @@ export function exporterQuery(withStatic) {
   return 'max by (' + EXPORTER_JOIN_LABELS.join(', ') + ') ({__name__=~"' + names.join('|') + '"})';
 }
 
+/** A PromQL double-quoted string literal body. */
+export function promString(s) {
+  return String(s).replace(/\\/g, '\\\\').replace(/"/g, '\\"');
+}
+
+/**
+ * The exporter query scoped to ONE node (`hostname` label = Kubernetes node
+ * name, the same key the joins and views use): what the native Node / Pod
+ * detail pages ask for, O(GPUs per node) series whatever the cluster size.
+ */
+export function exporterNodeQuery(nodeName, withStatic) {
+  const names = exporterNames(withStatic);
+  return 'max by (' + EXPORTER_JOIN_LABELS.join(', ') + ') ({__name__=~"' + names.join('|') + '", hostname="' +
+    promString(nodeName) + '"})';
+}
+
+/** The part of a snapshot that belongs to one node (GPU objects shared, not copied). */
+export function nodeSlice(m, nodeName) {
+  if (!m) return m;
+  const out = {};
+  for (const k in m) out[k] = m[k];
+  out.gpus = m.gpus.filter(function (g) { return g.nodeName === nodeName; });
+  out.xgmi = {};
+  out.links = {};
+  if (m.xgmi && m.xgmi[nodeName]) out.xgmi[nodeName] = m.xgmi[nodeName];
+  if (m.links && m.links[nodeName]) out.links[nodeName] = m.links[nodeName];
+  out.scope = nodeName;
+  return out;
+}
+
 export function nodeExporterQuery() {
   const N = SERIES.nodeExporter;
   const names = [N.chips.split('{')[0], N.power, N.powerInput, N.powerCap, N.busy, N.vramUsed, N.vramTotal, N.uname];
@@ -485,6 +515,7 @@ export function createMetricsSource(opts) {
     links = null;
     statics = null;
     last = null;
+    for (const k in nodeStates) delete nodeStates[k];
   }
 
   /** Marker for "the request did not reach a Prometheus". */
@@ -597,6 +628,72 @@ export function createMetricsSource(opts) {
     });
   }
 
+  // Per-node snapshots for the detail pages: node → {last, links, statics, staticAt, failures}.
+  const nodeStates = {};
+  /** Marker: the scoped query found no exporter GPU on this node. */
+  const NOT_SCOPED = {};
+
+  /**
+   * Telemetry of ONE node's GPUs — what the native Node and Pod detail pages
+   * show. The exporter query carries a `hostname` matcher, so opening a
+   * detail page moves O(GPUs per node) bytes (a few KB) instead of the whole
+   * cluster's telemetry (O(GPUs in the cluster): MBs on a few hundred
+   * nodes). Static series (power cap, HBM size, throttle threshold, link
+   * topology) are re-read per node every discovery TTL, as in the
+   * cluster-wide path.
+   *
+   * Falls back to the cluster-wide snapshot, cut to the node, when the
+   * scoped query finds no GPU: node-exporter as the source (its series carry
+   * `instance`, not `hostname`) or an exporter whose hostname label is not
+   * the node name. Transient failures serve the node's last snapshot marked
+   * stale, like fetchGpuMetrics. Resolves to null when Prometheus is
+   * unreachable.
+   * @param {string} nodeName
+   * @returns {Promise<GpuMetrics|null>}
+   */
+  function fetchNodeMetrics(nodeName) {
+    const key = String(nodeName);
+    if (!nodeStates[key]) nodeStates[key] = { last: null, links: null, statics: null, staticAt: 0, failures: 0 };
+    const st = nodeStates[key];
+    function clusterWide() {
+      return fetchGpuMetrics().then(function (m) { return m ? nodeSlice(m, key) : null; });
+    }
+    if (source === 'node-exporter') return clusterWide();
+    return withPrometheus(function (base) {
+      const withStatic = st.links === null || clock.now() - st.staticAt >= ttl;
+      return combined(base, exporterNodeQuery(key, withStatic)).then(function (res) {
+        if (!res.ok) return UNREACHABLE;
+        st.failures = 0;
+        const j = joinExporterResults(res.rows);
+        if (!j.gpus.length) return NOT_SCOPED;
+        if (withStatic) {
+          st.links = j.links;
+          st.statics = staticsOf(j.gpus);
+          st.staticAt = clock.now();
+        } else {
+          j.links = st.links;
+          if (!applyStatics(j.gpus, st.statics)) st.staticAt = -Infinity;
+        }
+        const prev = st.last;
+        st.last = {
+          source: 'amd-exporter',
+          gpus: prev ? shareGpus(prev.gpus, j.gpus) : j.gpus,
+          xgmi: prev ? shareMap(prev.xgmi, j.xgmi) : j.xgmi,
+          links: prev ? shareMap(prev.links, j.links || {}) : j.links || {},
+          fetchedAt: new Date(clock.now()).toISOString(),
+          prometheusPath: base,
+          scope: key,
+        };
+        return st.last;
+      });
+    }, function () {
+      st.failures++;
+      if (st.last && st.failures < STALE_FAILURES) return Object.assign({}, st.last, { stale: true });
+      st.last = null;
+      return null;
+    }).then(function (r) { return r === NOT_SCOPED ? clusterWide() : r; });
+  }
+
   // Incremental range cache: step-aligned samples per series key.
   let seriesCache = null; // { range, step, end, data: { power: {node: [[t,v]]}, vram: {...} } }
 
@@ -673,6 +770,7 @@ export function createMetricsSource(opts) {
     discover: discover,
     invalidate: invalidate,
     fetchGpuMetrics: fetchGpuMetrics,
+    fetchNodeMetrics: fetchNodeMetrics,
     fetchSeries: fetchSeries,
     source: function () { return source; },
   };

@@ -19,6 +19,9 @@ import {
   summarizeMetrics,
   staticsOf,
   applyStatics,
+  exporterNodeQuery,
+  nodeSlice,
+  promString,
 } from '../../src/api/metrics.js';
 
 const BASE0 = servicePath(PROMETHEUS_SERVICES[0]);
@@ -83,10 +86,11 @@ function prom(opts) {
         },
       });
     }
-    const m = /^(?:max by \([^)]*\) \()?\{__name__=~"(.*)"\}\)?$/.exec(q);
+    const m = /^(?:max by \([^)]*\) \()?\{__name__=~"(.*?)"(?:, hostname="((?:[^"\\]|\\.)*)")?\}\)?$/.exec(q);
     if (!m) return Promise.resolve(ok([]));
     const re = new RegExp('^(?:' + m[1] + ')$');
-    return Promise.resolve(ok(rows.filter((r) => re.test(r.metric.__name__ || ''))));
+    const host = m[2] === undefined ? null : m[2].replace(/\\(.)/g, '$1');
+    return Promise.resolve(ok(rows.filter((r) => re.test(r.metric.__name__ || '') && (host === null || r.metric.hostname === host))));
   });
 }
 
@@ -372,6 +376,94 @@ describe('fetchGpuMetrics', () => {
     const src = createMetricsSource({ request: prom() });
     const m = await src.fetchGpuMetrics();
     expect(m.gpus[0].powerCapWatts).toBe(1400);
+  });
+});
+
+describe('fetchNodeMetrics (detail pages)', () => {
+  const paths = (request, from) => request.mock.calls.slice(from || 0).map((c) => decodeURIComponent(c[0]));
+
+  it('asks for one node only, with a hostname matcher, and returns that node\'s GPUs', async () => {
+    const request = prom({ data: exporterData(['n0', 'n1', 'n2']) });
+    const src = createMetricsSource({ request });
+    const m = await src.fetchNodeMetrics('n1');
+    expect(paths(request)).toHaveLength(1);
+    expect(paths(request)[0]).toContain('hostname="n1"');
+    expect(m.scope).toBe('n1');
+    expect(m.gpus).toHaveLength(8);
+    expect(m.gpus.every((g) => g.nodeName === 'n1')).toBe(true);
+    expect(m.gpus[0].pod).toBe('train-0');
+    expect(Object.keys(m.xgmi)).toEqual(['n1']);
+  });
+  it('escapes the node name inside the matcher', () => {
+    expect(exporterNodeQuery('a"b\\c', false)).toContain('hostname="a\\"b\\\\c"');
+    expect(promString('x"y')).toBe('x\\"y');
+  });
+  it('re-reads a node\'s static series only after the TTL', async () => {
+    let now = 0;
+    const request = prom({ data: exporterData(['n0']) });
+    const src = createMetricsSource({ request, discoveryTtlMs: 1000, clock: { setTimeout, clearTimeout, now: () => now } });
+    const a = await src.fetchNodeMetrics('n0');
+    await src.fetchNodeMetrics('n0');
+    now = 5000;
+    await src.fetchNodeMetrics('n0');
+    const qs = paths(request);
+    expect(qs.map((q) => q.indexOf(SERIES.exporter.vramTotal) >= 0)).toEqual([true, false, true]);
+    const b = await src.fetchNodeMetrics('n0');
+    expect(b.gpus[0].vramTotalBytes).toBe(a.gpus[0].vramTotalBytes); // from the node's static copy
+  });
+  it('shares unchanged GPU objects between fetches of the same node', async () => {
+    const src = createMetricsSource({ request: prom({ data: exporterData(['n0']) }) });
+    const a = await src.fetchNodeMetrics('n0');
+    const b = await src.fetchNodeMetrics('n0');
+    expect(b.gpus).toBe(a.gpus);
+  });
+  it('falls back to the cluster-wide snapshot, cut to the node, when the exporter has no such hostname', async () => {
+    const i = '10.0.0.1:9100';
+    const ne = {
+      chips: [vec({ __name__: 'node_hwmon_chip_names', instance: i, chip: '0000:05:00_0', chip_name: 'amdgpu' }, 1)],
+      power: [vec({ __name__: 'node_hwmon_power_average_watt', instance: i, chip: '0000:05:00_0' }, 650)],
+      uname: [vec({ __name__: 'node_uname_info', instance: i, nodename: 'mi355x-0' }, 1)],
+    };
+    const request = prom({ data: null, ne });
+    const src = createMetricsSource({ request });
+    const m = await src.fetchNodeMetrics('mi355x-0');
+    expect(m.source).toBe('node-exporter');
+    expect(m.gpus.map((g) => [g.nodeName, g.powerWatts])).toEqual([['mi355x-0', 650]]);
+    // node-exporter is now the known source: later detail fetches skip the scoped query.
+    const n = request.mock.calls.length;
+    await src.fetchNodeMetrics('mi355x-0');
+    expect(paths(request, n)).toHaveLength(1);
+    expect(paths(request, n)[0]).not.toContain('hostname=');
+  });
+  it('serves the node\'s last snapshot stale through a transient failure, then null', async () => {
+    let up = true;
+    const good = prom({ data: exporterData(['n0']) });
+    const request = vi.fn((p) => (up ? good(p) : Promise.reject(Object.assign(new Error('503'), { status: 503 }))));
+    const src = createMetricsSource({ request });
+    const a = await src.fetchNodeMetrics('n0');
+    up = false;
+    const b = await src.fetchNodeMetrics('n0');
+    expect(b.stale).toBe(true);
+    expect(b.gpus).toBe(a.gpus);
+    await src.fetchNodeMetrics('n0');
+    expect(await src.fetchNodeMetrics('n0')).toBeNull();
+  });
+  it('returns null when Prometheus is unreachable', async () => {
+    const src = createMetricsSource({ request: prom({ up: [] }) });
+    expect(await src.fetchNodeMetrics('n0')).toBeNull();
+  });
+  it('nodeSlice keeps the node\'s GPUs, xGMI and links and shares their objects', () => {
+    const m = {
+      source: 'amd-exporter', fetchedAt: 'x', prometheusPath: 'p',
+      gpus: [{ nodeName: 'a', gpu: '0' }, { nodeName: 'b', gpu: '0' }],
+      xgmi: { a: { '0-1': 1 }, b: { '0-1': 2 } }, links: { b: { '0-1': { type: 'XGMI', hops: 1 } } },
+    };
+    const s = nodeSlice(m, 'b');
+    expect(s.gpus).toEqual([m.gpus[1]]);
+    expect(s.gpus[0]).toBe(m.gpus[1]);
+    expect(s.xgmi).toEqual({ b: { '0-1': 2 } });
+    expect(s.links.b).toBe(m.links.b);
+    expect(s.source).toBe('amd-exporter');
   });
 });
 

@@ -58,3 +58,19 @@ def test_bench_node_override(n):
     assert r.returncode == 0, r.stderr[-3000:]
     line = _json_lines(r.stdout)[0]
     assert line["config"]["nodes"] == n and line["rendered"]["gpu_nodes"] == n
+
+
+def test_detail_pages_cost_one_node_of_telemetry_whatever_the_cluster_size():
+    # Native Pod / Node detail pages fetch their node's telemetry with a
+    # hostname-scoped query: one request, the same bytes on 1 and on 16
+    # nodes, where the cluster-wide snapshot grows with the GPU count.
+    out = {}
+    for n in (1, 16):
+        r = subprocess.run([sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--rtt-ms", "5",
+                            "--nodes", str(n)], cwd=ROOT, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-3000:]
+        out[n] = _json_lines(r.stdout)[0]["detail_open"]
+    for kind in ("podScoped", "nodeScoped"):
+        assert out[1][kind]["requests"] == 1 and out[16][kind]["requests"] == 1
+        assert abs(out[16][kind]["bytes"] - out[1][kind]["bytes"]) <= 0.05 * out[1][kind]["bytes"], out
+    assert out[16]["podClusterWide"]["bytes"] > 10 * out[16]["podScoped"]["bytes"], out
