@@ -405,7 +405,8 @@ async function serve(a) {
         // Native detail pages opened on a warm cluster (a plugin page loaded
         // before): Pod detail and Node detail each fetch their node's
         // telemetry with a hostname-scoped query on a fresh metrics client,
-        // next to the cluster-wide snapshot the pod detail would otherwise need.
+        // next to the cluster-wide snapshot the pod detail would otherwise
+        // need; and the GPU Pods page with its attribution-only query.
         const L = get('amd');
         if (!L.opened) {
           await L.s.coldOpen();
@@ -413,9 +414,9 @@ async function serve(a) {
         }
         const ctx = L.s.ctx();
         const pods = ctx.gpuPods.filter(function (p) { return p.spec && p.spec.nodeName; });
-        const modes = { podScoped: [], podClusterWide: [], nodeScoped: [] };
-        const bytes = { podScoped: 0, podClusterWide: 0, nodeScoped: 0 };
-        const reqs = { podScoped: 0, podClusterWide: 0, nodeScoped: 0 };
+        const modes = { podScoped: [], podClusterWide: [], nodeScoped: [], podsPageOwners: [] };
+        const bytes = { podScoped: 0, podClusterWide: 0, nodeScoped: 0, podsPageOwners: 0 };
+        const reqs = { podScoped: 0, podClusterWide: 0, nodeScoped: 0, podsPageOwners: 0 };
         for (let i = 0; i < n && pods.length; i++) {
           const pod = pods[i % pods.length];
           const node = ctx.gpuNodes.filter(function (x) { return x.metadata.name === pod.spec.nodeName; })[0];
@@ -424,6 +425,10 @@ async function serve(a) {
             ['podClusterWide', function (src) { return src.fetchGpuMetrics().then(function (m) { return podDetailView(pod, { metrics: m }); }); }],
             ['nodeScoped', function (src) {
               return src.fetchNodeMetrics(pod.spec.nodeName).then(function (m) { return node ? nodeDetailView(node, ctx, { metrics: m }) : null; });
+            }],
+            // GPU Pods page: pod → GPU attribution only.
+            ['podsPageOwners', function (src) {
+              return src.fetchGpuOwners().then(function (m) { renderPage(podsView(ctx, { metrics: m })); return null; });
             }],
           ];
           for (let r = 0; r < runs.length; r++) {

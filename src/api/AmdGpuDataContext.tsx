@@ -180,16 +180,12 @@ export function useGpuMetrics(enabled = true, withSeries = true): GpuMetricsStat
 }
 
 /**
- * Telemetry of one node's GPUs for the native Node / Pod detail pages: a
- * `hostname`-scoped query through the shared client (metrics.js
- * fetchNodeMetrics), so a detail page costs the same few KB on a 500-node
- * cluster as on one node. `nodeName` null (or `enabled` false) fetches
- * nothing.
+ * A metrics fetch narrower than the cluster-wide snapshot, re-run by the
+ * auto-refresh poller and by `refresh()`. `key` null fetches nothing; a new
+ * key drops the previous key's in-flight answer.
  */
-export function useNodeGpuMetrics(nodeName: string | null, enabled = true): GpuMetricsState {
-  const source = metricsSourceFor(clusterKey());
+function useScopedMetrics(key: string | null, fetch: () => Promise<GpuMetrics | null>): GpuMetricsState {
   const refreshIntervalSec = loadSettings().refreshIntervalSec;
-  const active = enabled && !!nodeName;
   const [state, setState] = useState<Omit<GpuMetricsState, 'refresh'>>({
     metrics: null,
     series: null,
@@ -199,11 +195,10 @@ export function useNodeGpuMetrics(nodeName: string | null, enabled = true): GpuM
   const [seq, setSeq] = useState(0);
 
   useEffect(() => {
-    if (!active || !nodeName) return;
+    if (key === null) return;
     let cancelled = false;
     setState(s => ({ ...s, fetching: true, fetchError: null }));
-    source
-      .fetchNodeMetrics(nodeName)
+    fetch()
       .then(metrics => {
         if (cancelled) return;
         setState({ metrics, series: null, fetching: false, fetchError: metrics ? null : PROMETHEUS_UNREACHABLE });
@@ -215,14 +210,40 @@ export function useNodeGpuMetrics(nodeName: string | null, enabled = true): GpuM
     return () => {
       cancelled = true;
     };
-  }, [active, nodeName, seq, source]);
+    // `fetch` is rebuilt every render; `key` names what it fetches.
+    // eslint-disable-next-line react-hooks/exhaustive-deps
+  }, [key, seq]);
 
   useEffect(() => {
-    if (!active) return;
+    if (key === null) return;
     const poller = createPoller(refreshIntervalSec);
     poller.start(() => setSeq(s => s + 1));
     return () => poller.stop();
-  }, [active, refreshIntervalSec]);
+  }, [key, refreshIntervalSec]);
 
   return useMemo(() => ({ ...state, refresh: () => setSeq(s => s + 1) }), [state]);
+}
+
+/**
+ * Telemetry of one node's GPUs for the native Node / Pod detail pages: a
+ * `hostname`-scoped query through the shared client (metrics.js
+ * fetchNodeMetrics), so a detail page costs the same few KB on a 500-node
+ * cluster as on one node. `nodeName` null (or `enabled` false) fetches
+ * nothing.
+ */
+export function useNodeGpuMetrics(nodeName: string | null, enabled = true): GpuMetricsState {
+  const source = metricsSourceFor(clusterKey());
+  const active = enabled && !!nodeName;
+  return useScopedMetrics(active ? `node|${clusterKey()}|${nodeName}` : null, () =>
+    source.fetchNodeMetrics(nodeName as string)
+  );
+}
+
+/**
+ * Pod → GPU attribution for the Pods page (metrics.js fetchGpuOwners): one
+ * series per allocated GPU instead of the whole cluster's telemetry.
+ */
+export function useGpuOwners(enabled = true): GpuMetricsState {
+  const source = metricsSourceFor(clusterKey());
+  return useScopedMetrics(enabled ? `owners|${clusterKey()}` : null, () => source.fetchGpuOwners());
 }

@@ -319,6 +319,15 @@ export function exporterNodeQuery(nodeName, withStatic) {
     promString(nodeName) + '"})';
 }
 
+/**
+ * Pod → GPU attribution only (the Pods page): the power gauge of GPUs whose
+ * `pod` label is set — one series per allocated GPU, instead of every live
+ * gauge and xGMI link of every GPU.
+ */
+export function ownersQuery() {
+  return 'max by (' + EXPORTER_JOIN_LABELS.join(', ') + ') ({__name__="' + SERIES.exporter.power + '", pod!=""})';
+}
+
 /** The part of a snapshot that belongs to one node (GPU objects shared, not copied). */
 export function nodeSlice(m, nodeName) {
   if (!m) return m;
@@ -694,6 +703,43 @@ export function createMetricsSource(opts) {
     }).then(function (r) { return r === NOT_SCOPED ? clusterWide() : r; });
   }
 
+  let ownersLast = null;
+  let ownersFailures = 0;
+
+  /**
+   * Which GPUs each pod holds (exporter `pod`/`namespace` labels) and their
+   * power — all the Pods page reads from Prometheus — in one query whose
+   * size follows the number of allocated GPUs, not every gauge of every GPU.
+   * `gpus` lists the attributed GPUs only; an empty list means no
+   * attribution (no pod on a GPU, or a source without pod labels, e.g.
+   * node-exporter). Stale / null handling as in fetchGpuMetrics.
+   * @returns {Promise<GpuMetrics|null>}
+   */
+  function fetchGpuOwners() {
+    return withPrometheus(function (base) {
+      return combined(base, ownersQuery()).then(function (res) {
+        if (!res.ok) return UNREACHABLE;
+        ownersFailures = 0;
+        const j = joinExporterResults(res.rows);
+        ownersLast = {
+          source: j.gpus.length ? 'amd-exporter' : source,
+          gpus: ownersLast ? shareGpus(ownersLast.gpus, j.gpus) : j.gpus,
+          xgmi: {},
+          links: {},
+          fetchedAt: new Date(clock.now()).toISOString(),
+          prometheusPath: base,
+          scope: 'owners',
+        };
+        return ownersLast;
+      });
+    }, function () {
+      ownersFailures++;
+      if (ownersLast && ownersFailures < STALE_FAILURES) return Object.assign({}, ownersLast, { stale: true });
+      ownersLast = null;
+      return null;
+    });
+  }
+
   // Incremental range cache: step-aligned samples per series key.
   let seriesCache = null; // { range, step, end, data: { power: {node: [[t,v]]}, vram: {...} } }
 
@@ -771,6 +817,7 @@ export function createMetricsSource(opts) {
     invalidate: invalidate,
     fetchGpuMetrics: fetchGpuMetrics,
     fetchNodeMetrics: fetchNodeMetrics,
+    fetchGpuOwners: fetchGpuOwners,
     fetchSeries: fetchSeries,
     source: function () { return source; },
   };

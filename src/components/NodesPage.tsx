@@ -11,7 +11,8 @@ import { Page } from './View';
 
 export default function NodesPage() {
   const ctx = useAmdGpuContext();
-  const m = useGpuMetrics(true);
+  // Telemetry only (owners, xGMI): this page draws no time series.
+  const m = useGpuMetrics(true, false);
   const refresh = () => {
     ctx.refresh();
     m.refresh();

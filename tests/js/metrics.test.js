@@ -21,6 +21,7 @@ import {
   applyStatics,
   exporterNodeQuery,
   nodeSlice,
+  ownersQuery,
   promString,
 } from '../../src/api/metrics.js';
 
@@ -86,6 +87,8 @@ function prom(opts) {
         },
       });
     }
+    const own = /^max by \([^)]*\) \(\{__name__="([a-z_]+)", pod!=""\}\)$/.exec(q);
+    if (own) return Promise.resolve(ok(rows.filter((r) => r.metric.__name__ === own[1] && r.metric.pod)));
     const m = /^(?:max by \([^)]*\) \()?\{__name__=~"(.*?)"(?:, hostname="((?:[^"\\]|\\.)*)")?\}\)?$/.exec(q);
     if (!m) return Promise.resolve(ok([]));
     const re = new RegExp('^(?:' + m[1] + ')$');
@@ -464,6 +467,43 @@ describe('fetchNodeMetrics (detail pages)', () => {
     expect(s.xgmi).toEqual({ b: { '0-1': 2 } });
     expect(s.links.b).toBe(m.links.b);
     expect(s.source).toBe('amd-exporter');
+  });
+});
+
+describe('fetchGpuOwners (Pods page)', () => {
+  it('asks for the power gauge of pod-attributed GPUs only', async () => {
+    const request = prom({ data: exporterData(['n0', 'n1']) });
+    const src = createMetricsSource({ request });
+    const m = await src.fetchGpuOwners();
+    const q = decodeURIComponent(request.mock.calls[0][0]);
+    expect(request.mock.calls).toHaveLength(1);
+    expect(q).toContain('pod!=""');
+    expect(q).not.toContain('xgmi');
+    expect(m.scope).toBe('owners');
+    expect(m.gpus.map((g) => [g.nodeName, g.gpu, g.pod])).toEqual([
+      ['n0', '0', 'train-0'], ['n0', '1', 'train-1'], ['n1', '0', 'train-0'], ['n1', '1', 'train-1'],
+    ]);
+    expect(m.gpus[0].powerWatts).toBe(700);
+  });
+  it('an empty answer means no attribution, not an unreachable Prometheus', async () => {
+    const src = createMetricsSource({ request: prom({ data: null }) });
+    const m = await src.fetchGpuOwners();
+    expect(m).not.toBeNull();
+    expect(m.gpus).toEqual([]);
+  });
+  it('serves the last attribution stale through a transient failure', async () => {
+    let up = true;
+    const good = prom();
+    const request = vi.fn((p) => (up ? good(p) : Promise.reject(Object.assign(new Error('503'), { status: 503 }))));
+    const src = createMetricsSource({ request });
+    const a = await src.fetchGpuOwners();
+    up = false;
+    const b = await src.fetchGpuOwners();
+    expect(b.stale).toBe(true);
+    expect(b.gpus).toBe(a.gpus);
+  });
+  it('projects onto the join labels', () => {
+    expect(ownersQuery()).toBe('max by (' + EXPORTER_JOIN_LABELS.join(', ') + ') ({__name__="gpu_power_usage", pod!=""})');
   });
 });
 
