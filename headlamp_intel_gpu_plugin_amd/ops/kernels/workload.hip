@@ -27,7 +27,8 @@
 //                 (128-B rows, XOR-swizzled 16-B chunks: conflict-free
 //                 ds_read_b128), one barrier per K-step. All three run each MFMA cluster at
 //                 s_setprio 1 and use a bijective XCD-aware block remap with
-//                 8-row tile grouping so blocks sharing an XCD's L2 work on
+//                 tile-row grouping (8 rows; 4 in the 8-phase kernel, where
+//                 the A/B measured it fastest) so blocks sharing an XCD's L2 work on
 //                 neighbouring tiles.
 //   stream_triad  c = a + s·b over fp32, 16-byte accesses, one pass with 4
 //                 vectors per thread and non-temporal stores: 5.78 TB/s.
@@ -243,6 +244,14 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_nt(const uint16_t* __r
 // ---------------------------------------------------------------------------
 
 constexpr int P8_THREADS = 512;
+// Tile-rows per L2 group of the block → tile map. Same-process A/B on one
+// MI355X (tools/build_variants.py + tools/ab_two_builds.py, 7 rounds, random
+// operands, TFLOP/s at 4096³ / 8192³ / 16384³): 1 → 1429 / 1421 / 1341,
+// 2 → 1430 / 1511 / 1340, 4 → 1452 / 1546 / 1513, 8 → 1439 / 1544 / 1490,
+// 16 → 1428 / 1486 / — (profiles/r1_gemm_group_ab.md).
+#ifndef P8_GROUP
+#define P8_GROUP 4
+#endif
 constexpr int P8_HALF = 128 * 128;       // bytes per half-tile (128 rows × 64 bf16)
 constexpr int P8_BUF = 4 * P8_HALF;      // one K-tile: A0 A1 B0 B1
 constexpr int P8_LDS = 2 * P8_BUF;       // 128 KiB
@@ -262,9 +271,9 @@ __global__ __launch_bounds__(P8_THREADS) void gemm_bf16_nt_8ph(const uint16_t* _
   const int tiles_m = M / 256;
   const int tiles_n = N / 256;
   const int wg = xcd_remap(static_cast<int>(blockIdx.x), tiles_m * tiles_n);
-  const int span = 8 * tiles_n;
-  const int first_m = (wg / span) * 8;
-  const int rows_in_group = min(8, tiles_m - first_m);
+  const int span = P8_GROUP * tiles_n;
+  const int first_m = (wg / span) * P8_GROUP;
+  const int rows_in_group = min(P8_GROUP, tiles_m - first_m);
   const int m0 = (first_m + (wg % span) % rows_in_group) * 256;
   const int n0 = ((wg % span) / rows_in_group) * 256;
 

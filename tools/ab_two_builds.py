@@ -1,10 +1,11 @@
-"""Same-process A/B of two builds of the `_workload` module (guide §5.4 rule 24).
+"""Same-process A/B of builds of the `_workload` module (guide §5.4 rule 24).
 
-    python tools/ab_two_builds.py OLD.so [NEW.so] [--sizes 4096 8192] [--iters 20] [--rounds 3]
+    python tools/ab_two_builds.py OTHER.so [OTHER2.so ...] [--sizes 4096 8192] [--iters 20] [--rounds 3]
 
-Loads both extension builds side by side, then times the 8-phase GEMM
-(variant tile256_dma) of each, interleaved round by round on the same
-uniform random [-1, 1) operands, and prints the medians (TFLOP/s).
+Loads the in-tree build ("new") and every given build (named after its
+directory) side by side, then times the 8-phase GEMM (variant tile256_dma)
+of each, interleaved round by round on the same uniform random [-1, 1)
+operands, and prints the medians (TFLOP/s) and whether all outputs agree.
 """
 import argparse
 import importlib.machinery
@@ -47,13 +48,15 @@ def time_one(mod, a, b, c, size, iters):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("old")
-    ap.add_argument("new", nargs="?", default=os.path.join(ROOT, "headlamp_intel_gpu_plugin_amd", "ops", "_workload.so"))
+    ap.add_argument("builds", nargs="+")
     ap.add_argument("--sizes", type=int, nargs="+", default=[4096, 8192])
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
     args = ap.parse_args()
-    mods = {"old": load(args.old), "new": load(args.new)}
+    mods = {"new": load(os.path.join(ROOT, "headlamp_intel_gpu_plugin_amd", "ops", "_workload.so"))}
+    for path in args.builds:
+        name = os.path.basename(os.path.dirname(os.path.abspath(path)))
+        mods["old" if name == "prev" else name] = load(path)
     for size in args.sizes:
         a = (torch.rand(size, size, device="cuda") * 2 - 1).to(torch.bfloat16)
         b = (torch.rand(size, size, device="cuda") * 2 - 1).to(torch.bfloat16)
@@ -62,7 +65,7 @@ def main():
         for _ in range(args.rounds):
             for k, m in mods.items():
                 tf[k].append(time_one(m, a, b, outs[k], size, args.iters))
-        same = torch.equal(outs["old"], outs["new"])
+        same = all(torch.equal(outs["new"], o) for o in outs.values())
         print(json.dumps({"size": size, **{k: round(statistics.median(v), 1) for k, v in tf.items()},
                           "rounds": {k: [round(x, 1) for x in v] for k, v in tf.items()}, "bitwise_equal": same}),
               flush=True)
