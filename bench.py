@@ -8,9 +8,10 @@ BASELINE.json metric: "p50 dashboard refresh (ms) + GPU nodes/pods rendered at
 1/2/4/8-node cluster". One rank per GPU; rank r plays node r of an N-node
 cluster of 8×MI355X nodes (weak scaling: per-node work is fixed as N grows).
 
-* rank 0 hosts the fake kube-apiserver + Prometheus (service proxy) with an
-  injected per-request round-trip latency (``--rtt-ms``, default 20 ms),
-  identical for both schedules measured;
+* rank 0 starts the fake kube-apiserver + Prometheus (service proxy) as a
+  child process (sim/serve.py: its own interpreter, like a control plane on
+  other hosts) with an injected per-request round-trip latency
+  (``--rtt-ms``, default 20 ms), identical for both schedules measured;
 * every rank with a GPU runs (unless ``--no-burn``) a workload "pod" running
   the MFMA GEMM + HBM triad kernels on its own MI355X; rank 0 starts the
   native ``amdgpu-exporter`` daemon (C++/HIP, one for the host) and scrapes
@@ -54,6 +55,8 @@ def parse_args(argv=None):
     p.add_argument("--ref-steps", type=int, default=None, help="reference-schedule refreshes (default: --steps)")
     p.add_argument("--no-burn", action="store_true", help="do not run the GPU workload pods")
     p.add_argument("--no-live", action="store_true", help="synthetic telemetry only (no native probe)")
+    p.add_argument("--control-plane", default="process", choices=["process", "thread"],
+                   help="run the fake apiserver/Prometheus in a child process (default) or a thread of rank 0")
     p.add_argument("--out", default=None, help="also write the full result JSON here")
     return p.parse_args(argv)
 
@@ -104,19 +107,29 @@ def main(argv=None) -> int:
     result = None
     elapsed = 0.0
     if info.is_main:
-        from headlamp_intel_gpu_plugin_amd.parallel.agent import Scraper, live_series
-        from headlamp_intel_gpu_plugin_amd.sim.apiserver import ServerThread, make_fake
         from headlamp_intel_gpu_plugin_amd.utils.nodebridge import Driver
 
-        from headlamp_intel_gpu_plugin_amd.parallel.agent import device_to_node
-
         node_of_device = {str(d): n for n, d in ranks if d is not None} if exporter else {}
-        live = live_series(list(node_of_device.values())) if node_of_device else None
-        fc = make_fake(n_nodes, source="both", latency_ms=args.rtt_ms, live=live, preset=args.preset)
-        n_nodes = len(fc.cluster.gpu_nodes)
-        scraper = (Scraper([(exporter.url, device_to_node(node_of_device))], live, interval=2.0).start()
-                   if node_of_device else None)
-        server = ServerThread(fc).start()
+        if args.control_plane == "process":
+            # Its own interpreter, like a real apiserver / Prometheus on other
+            # hosts: no request waits for this process's GIL (workload pod).
+            from headlamp_intel_gpu_plugin_amd.sim.serve import ControlPlaneProcess
+
+            server = ControlPlaneProcess(n_nodes, source="both", latency_ms=args.rtt_ms, preset=args.preset,
+                                         exporter_url=exporter.url if exporter else None,
+                                         node_of_device=node_of_device).start()
+            n_nodes, gpus_per_node = server.info["gpu_nodes"], server.info["gpus_per_node"]
+            scraper = None
+        else:
+            from headlamp_intel_gpu_plugin_amd.parallel.agent import Scraper, device_to_node, live_series
+            from headlamp_intel_gpu_plugin_amd.sim.apiserver import ServerThread, make_fake
+
+            live = live_series(list(node_of_device.values())) if node_of_device else None
+            fc = make_fake(n_nodes, source="both", latency_ms=args.rtt_ms, live=live, preset=args.preset)
+            n_nodes, gpus_per_node = len(fc.cluster.gpu_nodes), fc.cluster.spec.gpus_per_node
+            scraper = (Scraper([(exporter.url, device_to_node(node_of_device))], live, interval=2.0).start()
+                       if node_of_device else None)
+            server = ServerThread(fc).start()
         drv = Driver(server.url)
         try:
             ref_steps = args.ref_steps if args.ref_steps is not None else args.steps
@@ -137,10 +150,10 @@ def main(argv=None) -> int:
             elapsed = time.perf_counter() - t0
             amd_switch = drv.call("switch", "amd", n=5)
             detail = drv.call("detail", "amd", n=5)["detail"]
+            served = (server.stats() if args.control_plane == "process"
+                      else {"server_requests": fc.stats(), "scrapes": scraper.scrapes if scraper else 0})
             result = {"ref": ref, "ref_cold": ref_cold, "ref_switch": ref_switch,
-                      "amd": amd, "amd_cold": amd_cold, "amd_switch": amd_switch, "detail": detail,
-                      "server_requests": fc.stats(),
-                      "scrapes": scraper.scrapes if scraper else 0}
+                      "amd": amd, "amd_cold": amd_cold, "amd_switch": amd_switch, "detail": detail, **served}
         finally:
             drv.close()
             server.stop()
@@ -185,12 +198,13 @@ def main(argv=None) -> int:
             "config": {
                 "model": "amd-gpu Headlamp plugin on a synthetic 8xMI355X-per-node cluster",
                 "nodes": n_nodes,
-                "gpus_per_node": fc.cluster.spec.gpus_per_node,
+                "gpus_per_node": gpus_per_node,
                 "preset": args.preset,
                 "global_batch": None,
                 "seq_len": None,
                 "parallelism": f"rank-per-node x{info.world}",
                 "rtt_ms": args.rtt_ms,
+                "control_plane": args.control_plane,
             },
             "baseline": {"schedule": "reference plugin request schedule replayed on the same server",
                          "p50_ms": round(ref_s["p50"], 3), "p95_ms": round(ref_s["p95"], 3),
