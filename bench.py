@@ -149,11 +149,13 @@ def main(argv=None) -> int:
             D.barrier(info)
             elapsed = time.perf_counter() - t0
             amd_switch = drv.call("switch", "amd", n=5)
-            detail = drv.call("detail", "amd", n=5)["detail"]
+            detail_out = drv.call("detail", "amd", n=5)
+            detail = detail_out["detail"]
             served = (server.stats() if args.control_plane == "process"
                       else {"server_requests": fc.stats(), "scrapes": scraper.scrapes if scraper else 0})
             result = {"ref": ref, "ref_cold": ref_cold, "ref_switch": ref_switch,
-                      "amd": amd, "amd_cold": amd_cold, "amd_switch": amd_switch, "detail": detail, **served}
+                      "amd": amd, "amd_cold": amd_cold, "amd_switch": amd_switch, "detail": detail,
+                      "detail_slow": detail_out.get("detailSlow"), **served}
         finally:
             drv.close()
             server.stop()
@@ -212,6 +214,9 @@ def main(argv=None) -> int:
             "p95_ms": round(amd_s["p95"], 3),
             "requests_per_refresh": result["amd"]["requestsPerStep"],
             "request_trace_p50_ms": {k: round(v["p50_ms"], 2) for k, v in (result["amd"].get("trace") or {}).items()},
+            # Data committed → all views rebuilt and rendered (part of `value`).
+            "render_p50_ms": (round(summarize(result["amd"]["renderMs"])["p50"], 3)
+                              if result["amd"].get("renderMs") else None),
             "cold_open_p50_ms": {"amd": round(summarize(result["amd_cold"]["latencies"])["p50"], 3),
                                  "reference": round(summarize(result["ref_cold"]["latencies"])["p50"], 3)},
             "route_switch_p50_ms": {"amd": round(summarize(result["amd_switch"]["latencies"])["p50"], 3),

@@ -92,6 +92,16 @@ function ms(hr) {
   return hr[0] * 1e3 + hr[1] / 1e6;
 }
 
+// Epoch milliseconds with sub-millisecond resolution (Date.now() anchored,
+// hrtime deltas): request spans resolve to microseconds instead of 1 ms.
+const EPOCH0 = Date.now();
+const HR0 = process.hrtime();
+const hiResClock = {
+  setTimeout: function (fn, t) { return setTimeout(fn, t); },
+  clearTimeout: function (h) { clearTimeout(h); },
+  now: function () { return EPOCH0 + ms(process.hrtime(HR0)); },
+};
+
 function stats(xs) {
   const s = xs.slice().sort(function (a, b) { return a - b; });
   const q = function (p) {
@@ -207,8 +217,8 @@ function amdSchedule(request) {
   function onTrace(span) {
     spans.push(span);
   }
-  const store = createClusterStore({ request: request, onTrace: onTrace });
-  const metrics = createMetricsSource({ request: request, onTrace: onTrace });
+  const store = createClusterStore({ request: request, onTrace: onTrace, clock: hiResClock });
+  const metrics = createMetricsSource({ request: request, onTrace: onTrace, clock: hiResClock });
   const mstate = { metrics: null, fetchError: null, fetching: false, series: null };
   function fetchMetrics() {
     return Promise.all([metrics.fetchGpuMetrics(), metrics.fetchSeries(1800, 30)]).then(function (r) {
@@ -375,13 +385,18 @@ async function serve(a) {
         const before = counter.n;
         const bytesBefore = counter.bytes;
         const spanStart = L.s.spans ? L.s.spans.length : 0;
+        const render = [];
         let rows = null;
         for (let i = 0; i < n; i++) {
           const t0 = process.hrtime();
           await L.s.refresh();
+          const t1 = process.hrtime();
           rows = renderAll(L.s.ctx(), L.s.mstate());
+          render.push(ms(process.hrtime(t1)));
           lat.push(ms(process.hrtime(t0)));
         }
+        // Data committed → every view rebuilt and rendered, per step.
+        out.renderMs = render;
         if (L.s.spans) out.trace = traceSummary(L.s.spans.slice(spanStart));
         const snap = L.s.ctx();
         const ms_ = L.s.mstate();
@@ -417,6 +432,8 @@ async function serve(a) {
         const modes = { podScoped: [], podClusterWide: [], nodeScoped: [], podsPageOwners: [] };
         const bytes = { podScoped: 0, podClusterWide: 0, nodeScoped: 0, podsPageOwners: 0 };
         const reqs = { podScoped: 0, podClusterWide: 0, nodeScoped: 0, podsPageOwners: 0 };
+        const slow = [];
+        const detailRequest = makeRequest(a.url, counter);
         for (let i = 0; i < n && pods.length; i++) {
           const pod = pods[i % pods.length];
           const node = ctx.gpuNodes.filter(function (x) { return x.metadata.name === pod.spec.nodeName; })[0];
@@ -432,18 +449,33 @@ async function serve(a) {
             }],
           ];
           for (let r = 0; r < runs.length; r++) {
-            const src = createMetricsSource({ request: makeRequest(a.url, counter) });
+            const spans = [];
+            // A fresh metrics client (cold cache) per open, over the page's
+            // connection pool: a browser keeps its keep-alive sockets to the
+            // Headlamp origin across in-app navigations.
+            const src = createMetricsSource({
+              request: detailRequest, clock: hiResClock, onTrace: function (sp) { spans.push(sp); },
+            });
             const b0 = counter.bytes;
             const n0 = counter.n;
             const t0 = process.hrtime();
+            const start = hiResClock.now();
             const s = await runs[r][1](src);
             if (s) renderSection(s);
-            modes[runs[r][0]].push(ms(process.hrtime(t0)));
+            const took = ms(process.hrtime(t0));
+            modes[runs[r][0]].push(took);
+            // Opens far above the injected RTT: where the time went (request spans vs client work).
+            if (took > 80) {
+              slow.push({ mode: runs[r][0], i: i, ms: took, spans: spans.map(function (sp) {
+                return { name: sp.name, startMs: sp.start - start, durMs: sp.end - sp.start, ok: sp.ok };
+              }) });
+            }
             bytes[runs[r][0]] += counter.bytes - b0;
             reqs[runs[r][0]] += counter.n - n0;
           }
         }
         out.detail = {};
+        out.detailSlow = slow;
         for (const k in modes) {
           out.detail[k] = { latencies: modes[k], bytesPerOpen: bytes[k] / Math.max(1, modes[k].length), requestsPerOpen: reqs[k] / Math.max(1, modes[k].length) };
         }

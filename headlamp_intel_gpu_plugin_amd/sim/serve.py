@@ -52,7 +52,14 @@ def main(argv=None) -> int:
         for line in sys.stdin:
             cmd = line.strip()
             if cmd == "stats":
-                print(json.dumps({"server_requests": fc.stats(), "scrapes": scraper.scrapes if scraper else 0}),
+                with fc.lock:
+                    work = sorted(w for _, w in fc.requests)
+                    slowest = sorted(fc.requests, key=lambda r: -r[1])[:5]
+                print(json.dumps({"server_requests": fc.stats(), "scrapes": scraper.scrapes if scraper else 0,
+                                  # server-side work per request (ms), on top of the injected latency
+                                  "server_work_ms": {"p50": round(work[len(work) // 2] * 1e3, 3) if work else None,
+                                                     "max": round(work[-1] * 1e3, 3) if work else None,
+                                                     "slowest": [[p[:120], round(w * 1e3, 3)] for p, w in slowest]}}),
                       flush=True)
             elif cmd == "quit":
                 break
