@@ -283,6 +283,15 @@ export function joinNodeExporterResults(r) {
 export const EXPORTER_JOIN_LABELS = ['__name__', 'hostname', 'node', 'instance', 'gpu_id', 'peer_gpu_id', 'pod', 'namespace'];
 
 /**
+ * The projection of the per-refresh (live-only) query once the static query
+ * has shown that every exporter series carries `hostname` (the Device Metrics
+ * Exporter labels all its gauges with it): `node` / `instance` are then only
+ * fallback keys, and `instance` ("10.0.0.17:5000") is ~18 % of the response
+ * bytes. The GPU's `instance` is kept from the static query (STATIC_GPU_FIELDS).
+ */
+export const EXPORTER_LEAN_LABELS = ['__name__', 'hostname', 'gpu_id', 'peer_gpu_id', 'pod', 'namespace'];
+
+/**
  * Per-GPU exporter gauges. The static ones (HBM capacity, power cap, throttle
  * threshold, link topology) change only with a reconfiguration of the node,
  * so callers ask for them once per DISCOVERY_TTL_MS and keep a copy; every
@@ -295,12 +304,42 @@ function exporterNames(withStatic) {
   return names;
 }
 
-/** Fields of GpuTelemetry that come from the static series (see exporterNames). */
-export const STATIC_GPU_FIELDS = ['powerCapWatts', 'vramTotalBytes', 'tempSlowdownC'];
+function isExporterName(name) {
+  const E = SERIES.exporter;
+  for (const k in E) if (E[k] === name) return true;
+  return false;
+}
 
-export function exporterQuery(withStatic) {
+/** Fields of GpuTelemetry that come from the static series (see exporterNames). */
+export const STATIC_GPU_FIELDS = ['powerCapWatts', 'vramTotalBytes', 'tempSlowdownC', 'instance'];
+
+/**
+ * @param {boolean} [withStatic]  include the static series (default true)
+ * @param {boolean} [lean]        project onto EXPORTER_LEAN_LABELS (live-only queries of a hostname-keyed exporter)
+ */
+export function exporterQuery(withStatic, lean) {
   const names = exporterNames(withStatic);
-  return 'max by (' + EXPORTER_JOIN_LABELS.join(', ') + ') ({__name__=~"' + names.join('|') + '"})';
+  const labels = lean && withStatic === false ? EXPORTER_LEAN_LABELS : EXPORTER_JOIN_LABELS;
+  return 'max by (' + labels.join(', ') + ') ({__name__=~"' + names.join('|') + '"})';
+}
+
+/**
+ * True when every exporter row of a combined result (splitByName output)
+ * carries a `hostname` label; node-exporter rows in a merged result are not
+ * looked at.
+ */
+export function keyedByHostname(rows) {
+  let n = 0;
+  for (const k in rows) {
+    const list = rows[k];
+    if (!Array.isArray(list) || (k !== '__xgmi' && !isExporterName(k))) continue;
+    for (let i = 0; i < list.length; i++) {
+      const m = list[i] && list[i].metric;
+      if (!m || !m.hostname) return false;
+      n++;
+    }
+  }
+  return n > 0;
 }
 
 /** A PromQL double-quoted string literal body. */
@@ -315,7 +354,9 @@ export function promString(s) {
  */
 export function exporterNodeQuery(nodeName, withStatic) {
   const names = exporterNames(withStatic);
-  return 'max by (' + EXPORTER_JOIN_LABELS.join(', ') + ') ({__name__=~"' + names.join('|') + '", hostname="' +
+  // Every row matches the hostname matcher: the live-only query needs no fallback keys.
+  const labels = withStatic === false ? EXPORTER_LEAN_LABELS : EXPORTER_JOIN_LABELS;
+  return 'max by (' + labels.join(', ') + ') ({__name__=~"' + names.join('|') + '", hostname="' +
     promString(nodeName) + '"})';
 }
 
@@ -477,6 +518,7 @@ export function createMetricsSource(opts) {
   let links = null; // measured xGMI link topology per node (static), refreshed every `ttl` with `statics`
   let statics = null; // static per-GPU fields (STATIC_GPU_FIELDS), fetched with the topology
   let linksAt = 0;
+  let lean = false; // the last static query showed every exporter series keyed by hostname
   let last = null; // previous snapshot, for structural sharing
   let failures = 0; // consecutive failed fetches against the cached service
 
@@ -520,6 +562,7 @@ export function createMetricsSource(opts) {
   function invalidate() {
     cachedPath = null;
     source = null;
+    lean = false;
     seriesCache = null;
     links = null;
     statics = null;
@@ -591,7 +634,7 @@ export function createMetricsSource(opts) {
 
   function snapshotFrom(base) {
     const withStatic = links === null || clock.now() - linksAt >= ttl;
-    const q = source === 'amd-exporter' ? exporterQuery(withStatic)
+    const q = source === 'amd-exporter' ? exporterQuery(withStatic, lean)
       : source === 'node-exporter' ? nodeExporterQuery() : mergedQuery(withStatic);
     return combined(base, q).then(function (res) {
       if (!res.ok) return UNREACHABLE;
@@ -608,6 +651,7 @@ export function createMetricsSource(opts) {
             links = j.links;
             statics = staticsOf(j.gpus);
             linksAt = clock.now();
+            lean = keyedByHostname(rows);
           } else {
             joined.links = links;
             // A GPU the static copy does not know yet (node added since):

@@ -7,6 +7,8 @@
 import {
   PROMETHEUS_SERVICES,
   EXPORTER_JOIN_LABELS,
+  EXPORTER_LEAN_LABELS,
+  keyedByHostname,
   SERIES,
   createMetricsSource,
   exporterQuery,
@@ -279,6 +281,53 @@ describe('fetchGpuMetrics', () => {
     expect(b.gpus[0].powerCapWatts).toBe(1200);
     expect(b.gpus[0].vramTotalBytes).toBe(a.gpus[0].vramTotalBytes);
     expect(b.gpus).toBe(a.gpus); // nothing changed: the same objects
+  });
+  it('drops the fallback keys from live-only queries once every exporter series carries hostname', async () => {
+    const E = SERIES.exporter;
+    // The fake answers with the labels the `max by (...)` projection keeps, as Prometheus does.
+    const inner = prom({ data: exporterData(['n0', 'n1']), ne: { [SERIES.nodeExporter.power]: [vec({ __name__: SERIES.nodeExporter.power, instance: 'x:9100' }, 5)] } });
+    const request = vi.fn((p) => inner(p).then((r) => {
+      const q = decodeURIComponent((p.split('query=')[1] || '').split('&')[0]);
+      const by = /^max by \(([^)]*)\)/.exec(q);
+      if (!by || !r.data) return r;
+      const keep = by[1].split(', ');
+      const result = r.data.result.map((row) => {
+        const m = {};
+        keep.forEach((k) => { if (row.metric[k] !== undefined) m[k] = row.metric[k]; });
+        return { metric: m, value: row.value };
+      });
+      return ok(result);
+    }));
+    let now = 1000000;
+    const src = createMetricsSource({ request, clock: { setTimeout, clearTimeout, now: () => now } });
+    const a = await src.fetchGpuMetrics(); // merged discovery query: full projection, node-exporter rows ignored
+    now += 1000;
+    const b = await src.fetchGpuMetrics();
+    const asked = request.mock.calls.map((x) => decodeURIComponent(x[0]));
+    expect(asked[0]).toContain('instance');
+    expect(/max by \(([^)]*)\)/.exec(asked[1])[1]).toBe(EXPORTER_LEAN_LABELS.join(', '));
+    expect(b.gpus.map((g) => g.instance)).toEqual(a.gpus.map((g) => g.instance));
+    expect(b.gpus[9]).toMatchObject({ nodeName: 'n1', gpu: '1', instance: 'n1:5000', powerWatts: 701 });
+    expect(b.gpus).toBe(a.gpus); // same content: structural sharing still hits
+    expect(exporterQuery(true, true)).toBe(exporterQuery(true)); // static queries keep the fallback keys
+  });
+  it('keeps the fallback keys when an exporter series has no hostname', async () => {
+    const d = exporterData(['n0']);
+    d[SERIES.exporter.temp].push(vec({ __name__: SERIES.exporter.temp, instance: '10.0.0.9:5000', gpu_id: '0' }, 70));
+    expect(keyedByHostname(d)).toBe(false);
+    expect(keyedByHostname(exporterData(['n0']))).toBe(true);
+    expect(keyedByHostname({})).toBe(false);
+    const request = prom({ data: d });
+    let now = 1000000;
+    const src = createMetricsSource({ request, clock: { setTimeout, clearTimeout, now: () => now } });
+    await src.fetchGpuMetrics();
+    now += 1000;
+    await src.fetchGpuMetrics();
+    expect(/max by \(([^)]*)\)/.exec(decodeURIComponent(request.mock.calls[1][0]))[1]).toBe(EXPORTER_JOIN_LABELS.join(', '));
+  });
+  it('scopes live-only node queries with the lean projection', () => {
+    expect(exporterNodeQuery('n0', false)).toContain('max by (' + EXPORTER_LEAN_LABELS.join(', ') + ')');
+    expect(exporterNodeQuery('n0', true)).toContain('max by (' + EXPORTER_JOIN_LABELS.join(', ') + ')');
   });
   it('refetches the static series when a GPU appears that the copy does not know', async () => {
     const E = SERIES.exporter;
