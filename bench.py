@@ -219,6 +219,9 @@ def main(argv=None) -> int:
                               if result["amd"].get("renderMs") else None),
             "cold_open_p50_ms": {"amd": round(summarize(result["amd_cold"]["latencies"])["p50"], 3),
                                  "reference": round(summarize(result["ref_cold"]["latencies"])["p50"], 3)},
+            # Part of the cold open spent rebuilding every view from an empty memo.
+            "cold_render_p50_ms": (round(summarize(result["amd_cold"]["renderMs"])["p50"], 3)
+                                   if result["amd_cold"].get("renderMs") else None),
             "route_switch_p50_ms": {"amd": round(summarize(result["amd_switch"]["latencies"])["p50"], 3),
                                     "reference": round(summarize(result["ref_switch"]["latencies"])["p50"], 3)},
             # Native Pod / Node detail page opened on a warm cluster: the node's

@@ -362,18 +362,22 @@ async function serve(a) {
       const n = c.n || 1;
       if (c.cmd === 'cold') {
         const lat = [];
+        const renderMs = [];
         let req = 0;
         for (let i = 0; i < n; i++) {
           const s = (name === 'reference' ? referenceSchedule : amdSchedule)(makeRequest(a.url, counter));
           const before = counter.n;
           const t0 = process.hrtime();
           await s.coldOpen();
+          const t1 = process.hrtime();
           renderAll(s.ctx(), s.mstate());
           lat.push(ms(process.hrtime(t0)));
+          renderMs.push(ms(process.hrtime(t1)));
           req = counter.n - before;
           if (s.spans) out.trace = traceSummary(s.spans);
         }
         out.latencies = lat;
+        out.renderMs = renderMs;
         out.requests = req;
       } else if (c.cmd === 'steps') {
         const L = get(name);

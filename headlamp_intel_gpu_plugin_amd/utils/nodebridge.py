@@ -21,7 +21,10 @@ class Driver:
     """A long-lived ``bench/driver.js --serve`` process speaking JSON lines."""
 
     def __init__(self, url: str):
-        self.proc = subprocess.Popen([node_binary(), os.path.join(ROOT, "bench", "driver.js"), "--serve", "--url", url],
+        # HEADLAMP_AMD_NODE_FLAGS: extra node flags for diagnostics, e.g. "--cpu-prof --cpu-prof-dir=/tmp/p"
+        # (node 12 refuses --cpu-prof in NODE_OPTIONS).
+        flags = os.environ.get("HEADLAMP_AMD_NODE_FLAGS", "").split()
+        self.proc = subprocess.Popen([node_binary(), *flags, os.path.join(ROOT, "bench", "driver.js"), "--serve", "--url", url],
                                      cwd=ROOT, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                                      text=True, bufsize=1)
 

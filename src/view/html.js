@@ -12,7 +12,11 @@
  * (src/components/View.tsx).
  */
 
+const NEEDS_ESC = /[&<>"]/;
+
 function esc(s) {
+  // Most values (names, numbers, units) need no escaping: one test, no copies.
+  if (typeof s === 'number' || !NEEDS_ESC.test(s)) return String(s);
   return String(s)
     .replace(/&/g, '&amp;')
     .replace(/</g, '&lt;')

@@ -57,9 +57,9 @@ def main():
         with open(os.path.join(args.out, "sweep.json"), "w") as f:
             json.dump(rows, f, indent=1)
     md = ["| Config | GPU nodes | Ref-schedule p50 refresh (ms) | New p50 refresh (ms) | New p95 (ms) | Speed-up | "
-          "Requests/refresh (ref → new) | Cold open p50 ref → new (ms) | Route switch p50 ref → new (ms) | "
-          "GPU nodes rendered | GPU pods rendered | GPUs monitored | Live GPU telemetry |",
-          "|---|---:|---:|---:|---:|---:|---|---|---|---:|---:|---:|---|"]
+          "Requests/refresh (ref → new) | Cold open p50 ref → new (ms) | New cold-open render p50 (ms) | "
+          "Route switch p50 ref → new (ms) | GPU nodes rendered | GPU pods rendered | GPUs monitored | Live GPU telemetry |",
+          "|---|---:|---:|---:|---:|---:|---|---|---:|---|---:|---:|---:|---|"]
     for r in rows:
         l = r["line"]
         label = f"{r['point']}-node scaling point" if r["kind"] == "nodes" else PRESET_LABEL[r["point"]]
@@ -67,6 +67,7 @@ def main():
             f"| {label} | {l['config']['nodes']} | {l['baseline']['p50_ms']:.1f} | {l['value']:.1f} | {l['p95_ms']:.1f} | "
             f"{l['baseline']['p50_ms'] / l['value']:.1f}× | {l['baseline']['requests_per_refresh']:.0f} → "
             f"{l['requests_per_refresh']:.0f} | {l['cold_open_p50_ms']['reference']:.0f} → {l['cold_open_p50_ms']['amd']:.0f} | "
+            f"{l.get('cold_render_p50_ms') or float('nan'):.1f} | "
             f"{l['route_switch_p50_ms']['reference']:.0f} → {l['route_switch_p50_ms']['amd']:.1f} | "
             f"{l['rendered']['gpu_nodes']} | {l['rendered']['gpu_pods']} | {l['rendered']['gpus_monitored']} | "
             f"{'yes' if l.get('live_telemetry') else 'no'} |")
