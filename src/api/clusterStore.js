@@ -124,7 +124,10 @@ export function withTimeout(promise, ms, clock) {
  * @property {any[]} gpuPods
  * @property {any[]} pluginPods
  * @property {boolean} crdAvailable
- * @property {boolean} loading      true until nodes, pods and the first CRD/pod fetch are in
+ * @property {boolean} loading      true until the node and pod lists have settled (arrived or
+ *                                  failed) and the first CRD/pod fetch is in
+ * @property {'unknown'|'pending'|'ready'|'error'} nodesState
+ * @property {'unknown'|'pending'|'ready'|'error'} podsState
  * @property {boolean} refreshing   a refresh is in flight (data above is still valid)
  * @property {string|null} error
  * @property {ReturnType<typeof buildClusterIndex>} index
@@ -155,8 +158,13 @@ export function createClusterStore(opts) {
     deviceConfigs: [],
     crdAvailable: false,
     pluginPods: [], // from the plugin-pod queries (used when the pod list is not available)
-    // Where the pod list stands: 'unknown' (never fed: harness/tests),
-    // 'pending' (a list/watch is in flight), 'ready', or 'error'.
+    // Where each list stands: 'unknown' (never fed: harness/tests),
+    // 'pending' (a list/watch is in flight), 'ready', or 'error'. An errored
+    // list (e.g. pods forbidden cluster-wide) is settled: the page leaves its
+    // loading state and shows the error, instead of waiting forever for a
+    // list that will not come (reference quirk Q11 inferred loading from
+    // `items === null`, IntelGpuDataContext.tsx:214).
+    nodesState: 'unknown',
     podsState: 'unknown',
     asyncLoaded: false,
     refreshing: false,
@@ -240,13 +248,19 @@ export function createClusterStore(opts) {
       gpuPods: p,
       pluginPods: pp,
       crdAvailable: s.crdAvailable,
-      loading: !s.asyncLoaded || s.nodes === null || s.pods === null,
+      loading: !s.asyncLoaded || !settled(s.nodesState) || !settled(s.podsState),
+      nodesState: s.nodesState,
+      podsState: s.podsState,
       refreshing: s.refreshing,
       error: errors.length ? errors.join('; ') : null,
       index: index(n, p),
       lastUpdated: s.lastUpdated,
       version: version,
     });
+  }
+
+  function settled(state) {
+    return state === 'ready' || state === 'error';
   }
 
   function emit() {
@@ -349,9 +363,11 @@ export function createClusterStore(opts) {
   function setNodes(items, error) {
     const next = items ? unwrapAll(items) : null;
     const err = error ? String(error) : null;
-    if (items === null && s.nodes === null && err === s.nodeError) return;
+    const state = err ? 'error' : next ? 'ready' : 'pending';
+    if (items === null && s.nodes === null && err === s.nodeError && state === s.nodesState) return;
     s.nodes = next;
     s.nodeError = err;
+    s.nodesState = state;
     emit();
   }
 
@@ -383,6 +399,7 @@ export function createClusterStore(opts) {
    */
   function loadLists() {
     if (s.podsState === 'unknown') s.podsState = 'pending';
+    if (s.nodesState === 'unknown') s.nodesState = 'pending';
     const nodesP = traced('nodes', '/api/v1/nodes').then(
       function (l) { setNodes(isKubeList(l) ? l.items : [], null); },
       function (e) { setNodes([], e instanceof Error ? e.message : String(e)); }

@@ -989,12 +989,13 @@ export function nodeDetailView(resource, ctx, opts) {
   const own = ownersByNode(metrics)[name];
   const xg = metrics && metrics.xgmi ? metrics.xgmi[name] : undefined;
   const lk = metrics && metrics.links ? metrics.links[name] : undefined;
-  return memo('node-detail:' + name, [raw, podsOnNode, !!ctx.loading, own, xg, lk], function () {
-    return nodeDetailSection(raw, name, cap, alloc, podsOnNode, ctx.loading, own, xg, lk);
+  const podsUnreadable = ctx.podsState === 'error';
+  return memo('node-detail:' + name, [raw, podsOnNode, !!ctx.loading, podsUnreadable, own, xg, lk], function () {
+    return nodeDetailSection(raw, name, cap, alloc, podsOnNode, ctx.loading, own, xg, lk, podsUnreadable);
   });
 }
 
-function nodeDetailSection(raw, name, cap, alloc, podsOnNode, loading, own, xg, lk) {
+function nodeDetailSection(raw, name, cap, alloc, podsOnNode, loading, own, xg, lk, podsUnreadable) {
   const allocatable = parseInt(alloc[AMD_GPU_RESOURCE] || '0', 10) || 0;
   let inUse = 0;
   for (let i = 0; i < podsOnNode.length; i++) {
@@ -1009,11 +1010,19 @@ function nodeDetailSection(raw, name, cap, alloc, podsOnNode, loading, own, xg, 
   const count = getNodeGpuCount(raw);
   const phys = getNodePhysicalGpuCount(raw);
   if (count > 0) rows.push(row('HBM', formatBytes(phys * MI355X.hbmBytes)));
-  if (allocatable > 0) rows.push(row('GPU Allocation', status(pctToStatus(p), inUse + '/' + allocatable + ' (' + p + '%)')));
+  if (allocatable > 0 && !podsUnreadable) {
+    rows.push(row('GPU Allocation', status(pctToStatus(p), inUse + '/' + allocatable + ' (' + p + '%)')));
+  }
+  // With the pod list unreadable (RBAC) the node's pods are unknown, not
+  // absent: say so rather than "None" or an endless "Loading…".
   rows.push(
     row(
       'GPU Workload Pods',
-      podsOnNode.length > 0 ? podsOnNode.map(podName).join(', ') : loading ? 'Loading…' : 'None'
+      podsOnNode.length > 0
+        ? podsOnNode.map(podName).join(', ')
+        : podsUnreadable
+          ? status('warning', 'Unavailable — the pod list could not be read')
+          : loading ? 'Loading…' : 'None'
     )
   );
   const blocks = [kv(rows)];

@@ -5,7 +5,9 @@
  */
 import { createClusterStore, getSharedStore, resetSharedStores, withTimeout } from '../../src/api/clusterStore.js';
 import { DEVICE_CONFIG_LIST_PATH, PLUGIN_POD_QUERIES } from '../../src/api/amdgpu.js';
-import { makeDeviceConfig, makeGpuNode, makeGpuPod, makeNode, makePlainPod, makePluginPod } from './fixtures.js';
+import { makeDeviceConfig, makeGpuNode, makeGpuPod, makeNode, makePlainPod, makePluginPod, NOW } from './fixtures.js';
+import { metricsView, nodeDetailView } from '../../src/view/pages.js';
+import { rowValue, text } from '../../src/view/ir.js';
 
 function deferred() {
   let resolve;
@@ -320,6 +322,67 @@ describe('createClusterStore', () => {
     await store.refresh();
     expect(spans.map((s) => s.name).sort()).toEqual(['crd', 'plugin-pods-0', 'plugin-pods-1']);
     expect(spans.every((s) => s.end >= s.start && s.ok)).toBe(true);
+  });
+});
+
+describe('degraded RBAC: an errored list is settled, not loading', () => {
+  const idle = { metrics: null, fetchError: null, fetching: false };
+  const cases = [
+    ['pods forbidden', (st) => { st.setNodes([makeGpuNode('mi355x-0')], null); st.setPods(null, 'pods is forbidden'); }],
+    ['nodes forbidden', (st) => { st.setNodes(null, 'nodes is forbidden'); st.setPods([makeGpuPod('train-0')], null); }],
+    ['both forbidden', (st) => { st.setNodes(null, 'nodes is forbidden'); st.setPods(null, 'pods is forbidden'); }],
+  ];
+  it.each(cases)('%s: loading clears after refresh', async (_name, feed) => {
+    const store = createClusterStore({ request: router(baseRoutes()) });
+    feed(store);
+    await store.refresh();
+    const s = store.getSnapshot();
+    expect(s.loading).toBe(false);
+    expect(s.error).toContain('forbidden');
+  });
+  it.each(cases)('%s: the Metrics Refresh button is enabled', async (_name, feed) => {
+    const store = createClusterStore({ request: router(baseRoutes()) });
+    feed(store);
+    await store.refresh();
+    const vm = metricsView(store.getSnapshot(), idle, { now: NOW });
+    expect(vm.refresh.disabled).toBe(false);
+    expect(vm.refresh.label).toBe('Refresh');
+  });
+  it.each(cases)('%s: Node detail does not say Loading…', async (_name, feed) => {
+    const store = createClusterStore({ request: router(baseRoutes()) });
+    feed(store);
+    await store.refresh();
+    const snap = store.getSnapshot();
+    const sec = nodeDetailView(makeGpuNode('mi355x-0'), snap, {});
+    const pods = text(rowValue(sec, 'GPU Workload Pods'));
+    expect(pods).not.toBe('Loading…');
+    if (snap.podsState === 'error') {
+      expect(pods).toContain('Unavailable');
+      expect(rowValue(sec, 'GPU Allocation')).toBeUndefined();
+    } else {
+      expect(pods).toBe('train-0');
+    }
+  });
+  it('a list still in flight keeps the page loading', async () => {
+    const store = createClusterStore({ request: router(baseRoutes()) });
+    store.setNodes(null, null);
+    store.setPods([], null);
+    await store.refresh();
+    expect(store.getSnapshot().loading).toBe(true);
+    expect(store.getSnapshot().nodesState).toBe('pending');
+    store.setNodes([], null);
+    expect(store.getSnapshot().loading).toBe(false);
+  });
+  it('a list that recovers from an error clears the error', async () => {
+    const store = createClusterStore({ request: router(baseRoutes()) });
+    store.setNodes([], null);
+    store.setPods(null, 'pods is forbidden');
+    await store.refresh();
+    store.setPods([makeGpuPod('train-0')], null);
+    const s = store.getSnapshot();
+    expect(s.error).toBeNull();
+    expect(s.podsState).toBe('ready');
+    expect(s.gpuPods).toHaveLength(1);
   });
 });
 
