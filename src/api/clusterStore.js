@@ -365,6 +365,10 @@ export function createClusterStore(opts) {
     const err = error ? String(error) : null;
     const state = err ? 'error' : next ? 'ready' : 'pending';
     if (items === null && s.nodes === null && err === s.nodeError && state === s.nodesState) return;
+    // A view mounting a fresh list hook reports "no items yet" while its
+    // watch starts; the list already held stays valid (stale-while-
+    // revalidate) instead of blanking every page back to its loader.
+    if (state === 'pending' && s.nodesState === 'ready') return;
     s.nodes = next;
     s.nodeError = err;
     s.nodesState = state;
@@ -376,6 +380,7 @@ export function createClusterStore(opts) {
     const err = error ? String(error) : null;
     const state = err ? 'error' : next ? 'ready' : 'pending';
     if (items === null && s.pods === null && err === s.podError && state === s.podsState) return;
+    if (state === 'pending' && s.podsState === 'ready') return;
     const wasError = s.podsState === 'error';
     s.pods = next;
     s.podError = err;

@@ -1,0 +1,56 @@
+/** Types of the provider core (./providerCore.js). */
+import type { ComponentType, Context, ReactNode } from 'react';
+import type { AmdGpuContextValue, GpuMetrics, GpuMetricsState } from './types';
+
+export const STALE_MS: number;
+export const PROMETHEUS_UNREACHABLE: string;
+export const OUTSIDE_PROVIDER: string;
+
+export interface HeadlampLibLike {
+  K8s: {
+    ResourceClasses: {
+      Node: { useList: (opts?: { namespace?: string }) => [unknown[] | null, unknown, ...unknown[]] };
+      Pod: { useList: (opts?: { namespace?: string }) => [unknown[] | null, unknown, ...unknown[]] };
+    };
+  };
+  ApiProxy: { request: (path: string) => Promise<unknown> };
+}
+
+export interface ProviderDeps {
+  request?: (path: string) => Promise<unknown>;
+  clusterKey?: () => string;
+  loadSettings?: () => { prometheus: { namespace: string; service: string; port: string } | null; refreshIntervalSec: number; requestTimeoutMs: number; seriesMinutes: number };
+}
+
+/** The shared data store (./clusterStore.js createClusterStore). */
+export interface ClusterStore {
+  subscribe(fn: () => void): () => void;
+  getSnapshot(): Omit<AmdGpuContextValue, 'refresh'>;
+  setNodes(items: unknown[] | null, error: string | null): void;
+  setPods(items: unknown[] | null, error: string | null): void;
+  refresh(): Promise<void>;
+  revalidate(maxAgeMs?: number): Promise<void>;
+  loadLists(): Promise<void>;
+  settled(): Promise<void>;
+  hasLoaded(): boolean;
+}
+
+export interface MetricsSource {
+  fetchGpuMetrics(): Promise<GpuMetrics | null>;
+  fetchNodeMetrics(nodeName: string): Promise<GpuMetrics | null>;
+  fetchGpuOwners(): Promise<GpuMetrics | null>;
+  fetchSeries(rangeSec: number, stepSec: number): Promise<GpuMetricsState['series']>;
+}
+
+export interface ProviderCore {
+  Context: Context<AmdGpuContextValue | null>;
+  AmdGpuDataProvider: ComponentType<{ children?: ReactNode }>;
+  useAmdGpuContext(): AmdGpuContextValue;
+  useGpuMetrics(enabled?: boolean, withSeries?: boolean): GpuMetricsState;
+  useNodeGpuMetrics(nodeName: string | null, enabled?: boolean): GpuMetricsState;
+  useGpuOwners(enabled?: boolean): GpuMetricsState;
+  storeFor(cluster: string): ClusterStore;
+  metricsSourceFor(cluster: string): MetricsSource;
+}
+
+export function createProviderCore(React: unknown, lib: HeadlampLibLike, deps?: ProviderDeps): ProviderCore;

@@ -1,0 +1,258 @@
+/**
+ * Provider core — the React binding of the shared ClusterStore and of the
+ * Prometheus client, written against INJECTED React hooks and an injected
+ * Headlamp library, so the exact code Headlamp runs also runs under the
+ * Node-12 harness's React stand-in (tests/js/stubs/react.js).
+ *
+ * Reference analog: src/api/IntelGpuDataContext.tsx (SURVEY.md C3) and the
+ * MetricsPage state/effect (src/components/MetricsPage.tsx:191-231). Same
+ * public contract — `useAmdGpuContext()` returns {deviceConfigs,
+ * pluginInstalled, gpuNodes, gpuPods, pluginPods, crdAvailable, loading,
+ * error, refresh} and throws outside a provider (reference :60-66) — but
+ * the provider is a thin view onto one store per cluster
+ * (src/api/clusterStore.js):
+ *
+ *   * Headlamp's reactive `useList()` hooks feed nodes and pods into the
+ *     store (two-track design, reference ADR 002 / :98-99); an errored list
+ *     is fed as an error, which the store treats as settled;
+ *   * the imperative track (DeviceConfig CRD, operator pods only when the
+ *     pod list is unavailable) runs in parallel inside the store, with
+ *     timeouts and a sequence guard (reference: serial, :122-165);
+ *   * a mounting provider calls `revalidate(STALE_MS)`: if another view
+ *     fetched moments ago (route switch, Node detail section next to a page)
+ *     nothing is re-fetched and the cached snapshot renders at once
+ *     (reference quirk Q7: every route mounted a cold provider).
+ */
+
+import { createClusterStore, getSharedStore } from './clusterStore.js';
+import { createMetricsSource } from './metrics.js';
+import { clusterKey as defaultClusterKey } from './cluster.js';
+import { createPoller, loadSettings as defaultLoadSettings, prometheusCandidates, seriesStepSec } from './settings.js';
+
+/** Data younger than this is served from the shared store on mount without re-fetching. */
+export const STALE_MS = 5000;
+
+export const PROMETHEUS_UNREACHABLE =
+  'Could not reach Prometheus. Ensure kube-prometheus-stack is installed in the monitoring namespace.';
+
+export const OUTSIDE_PROVIDER = 'useAmdGpuContext must be used within an AmdGpuDataProvider';
+
+const HOOKS = ['createContext', 'createElement', 'useContext', 'useEffect', 'useMemo', 'useState', 'useSyncExternalStore'];
+
+function errorText(e) {
+  return e instanceof Error ? e.message : String(e);
+}
+
+/**
+ * @param {any} React  React 18 (or the harness stand-in)
+ * @param {{K8s: any, ApiProxy: any}} lib  '@kinvolk/headlamp-plugin/lib'
+ * @param {{request?: (path: string) => Promise<any>, clusterKey?: () => string,
+ *          loadSettings?: () => ReturnType<typeof defaultLoadSettings>}} [deps]
+ */
+export function createProviderCore(React, lib, deps) {
+  for (let i = 0; i < HOOKS.length; i++) {
+    if (!React || typeof React[HOOKS[i]] !== 'function') throw new Error('createProviderCore: React.' + HOOKS[i] + ' is required');
+  }
+  const d = deps || {};
+  const request = d.request || function (path) { return lib.ApiProxy.request(path); };
+  const clusterKey = d.clusterKey || defaultClusterKey;
+  const loadSettings = d.loadSettings || function () { return defaultLoadSettings(); };
+  const h = React.createElement;
+  const useEffect = React.useEffect;
+  const useMemo = React.useMemo;
+  const useState = React.useState;
+
+  const Context = React.createContext(null);
+
+  /** The shared store of a cluster (created on first use; keyed by the settings that shape it). */
+  function storeFor(cluster) {
+    const settings = loadSettings();
+    return getSharedStore(cluster + '|' + settings.requestTimeoutMs, function () {
+      return createClusterStore({ request: request, timeoutMs: settings.requestTimeoutMs });
+    });
+  }
+
+  const metricsSources = {};
+
+  function sourceKey(cluster, settings) {
+    return cluster + '|' + JSON.stringify(settings.prometheus) + '|' + settings.requestTimeoutMs;
+  }
+
+  /**
+   * The shared Prometheus client of a cluster (its discovery cache lives
+   * here). Keyed by the settings that shape it, so saving new settings takes
+   * effect on the next mount.
+   */
+  function metricsSourceFor(cluster) {
+    const settings = loadSettings();
+    const key = sourceKey(cluster, settings);
+    if (!metricsSources[key]) {
+      metricsSources[key] = createMetricsSource({
+        request: request,
+        services: prometheusCandidates(settings),
+        timeoutMs: settings.requestTimeoutMs,
+      });
+    }
+    return metricsSources[key];
+  }
+
+  function useAmdGpuContext() {
+    const ctx = React.useContext(Context);
+    if (!ctx) throw new Error(OUTSIDE_PROVIDER);
+    return ctx;
+  }
+
+  function useListOf(cls, opts) {
+    // Headlamp returns [items, error, ...]; items is null while the first
+    // list is in flight and stays null when the list failed.
+    const res = opts ? cls.useList(opts) : cls.useList();
+    return [res && res[0] !== undefined ? res[0] : null, res ? res[1] : null];
+  }
+
+  function AmdGpuDataProvider(props) {
+    const store = storeFor(clusterKey());
+
+    // Track 1 — reactive lists from Headlamp (all namespaces for pods).
+    const nodes = useListOf(lib.K8s.ResourceClasses.Node);
+    const pods = useListOf(lib.K8s.ResourceClasses.Pod, { namespace: '' });
+    const allNodes = nodes[0];
+    const nodeError = nodes[1];
+    const allPods = pods[0];
+    const podError = pods[1];
+
+    useEffect(function () {
+      store.setNodes(allNodes === undefined ? null : allNodes, nodeError ? errorText(nodeError) : null);
+    }, [store, allNodes, nodeError]);
+    useEffect(function () {
+      store.setPods(allPods === undefined ? null : allPods, podError ? errorText(podError) : null);
+    }, [store, allPods, podError]);
+
+    // Track 2 — imperative CRD / operator-pod fetch, shared and deduplicated.
+    useEffect(function () {
+      store.revalidate(STALE_MS);
+    }, [store]);
+
+    // Optional auto-refresh (settings; the reference only refreshes on click).
+    const refreshIntervalSec = loadSettings().refreshIntervalSec;
+    useEffect(function () {
+      const poller = createPoller(refreshIntervalSec);
+      poller.start(function () { return store.revalidate(STALE_MS); });
+      return function () { poller.stop(); };
+    }, [store, refreshIntervalSec]);
+
+    const snapshot = React.useSyncExternalStore(store.subscribe, store.getSnapshot);
+    const value = useMemo(function () {
+      return Object.assign({}, snapshot, { refresh: function () { store.refresh(); } });
+    }, [snapshot, store]);
+
+    return h(Context.Provider, { value: value }, props.children);
+  }
+
+  const IDLE = { metrics: null, series: null, fetchError: null, fetching: false };
+
+  /**
+   * One metrics fetch bound to component state, re-run by `refresh()` and by
+   * the auto-refresh poller. `key` null fetches nothing; a new key (or an
+   * unmount) drops the previous key's in-flight answer (the reference's
+   * `cancelled` flag, MetricsPage.tsx:206-230).
+   * @param {string|null} key
+   * @param {() => Promise<[any, any]>} fetchPair  resolves [metrics, series]
+   */
+  function useMetricsFetch(key, fetchPair) {
+    const refreshIntervalSec = loadSettings().refreshIntervalSec;
+    const st = useState(IDLE);
+    const state = st[0];
+    const setState = st[1];
+    const sq = useState(0);
+    const seq = sq[0];
+    const setSeq = sq[1];
+
+    useEffect(function () {
+      if (key === null) return undefined;
+      let cancelled = false;
+      setState(function (s) { return Object.assign({}, s, { fetching: true, fetchError: null }); });
+      fetchPair().then(
+        function (pair) {
+          if (cancelled) return;
+          const metrics = pair[0];
+          setState({ metrics: metrics, series: pair[1], fetching: false, fetchError: metrics ? null : PROMETHEUS_UNREACHABLE });
+        },
+        function (e) {
+          if (cancelled) return;
+          setState(function (s) { return Object.assign({}, s, { fetching: false, fetchError: errorText(e) }); });
+        }
+      );
+      return function () { cancelled = true; };
+      // `fetchPair` is rebuilt every render; `key` names what it fetches.
+    }, [key, seq]);
+
+    useEffect(function () {
+      if (key === null) return undefined;
+      const poller = createPoller(refreshIntervalSec);
+      poller.start(function () { setSeq(function (s) { return s + 1; }); });
+      return function () { poller.stop(); };
+    }, [key, refreshIntervalSec]);
+
+    return useMemo(function () {
+      return Object.assign({}, state, { refresh: function () { setSeq(function (s) { return s + 1; }); } });
+    }, [state]);
+  }
+
+  /**
+   * Cluster-wide GPU telemetry (+ power/HBM series when `withSeries`).
+   * Unlike the reference it does not wait for the cluster context to finish
+   * loading (MetricsPage.tsx:203-205): the two are independent and fetched in
+   * parallel.
+   */
+  function useGpuMetrics(enabled, withSeries) {
+    const on = enabled === undefined ? true : enabled;
+    const series = withSeries === undefined ? true : withSeries;
+    const cluster = clusterKey();
+    const source = metricsSourceFor(cluster);
+    const settings = loadSettings();
+    const key = 'gpus|' + sourceKey(cluster, settings) + '|' + series + '|' + settings.seriesMinutes;
+    return useMetricsFetch(on ? key : null, function () {
+      return Promise.all([
+        source.fetchGpuMetrics(),
+        series ? source.fetchSeries(settings.seriesMinutes * 60, seriesStepSec(settings)) : Promise.resolve(null),
+      ]);
+    });
+  }
+
+  /**
+   * Telemetry of one node's GPUs for the native Node / Pod detail pages: a
+   * `hostname`-scoped query through the shared client (metrics.js
+   * fetchNodeMetrics), so a detail page costs the same few KB on a 500-node
+   * cluster as on one node. `nodeName` null (or `enabled` false) fetches
+   * nothing.
+   */
+  function useNodeGpuMetrics(nodeName, enabled) {
+    const cluster = clusterKey();
+    const source = metricsSourceFor(cluster);
+    const active = (enabled === undefined ? true : enabled) && !!nodeName;
+    return useMetricsFetch(active ? 'node|' + sourceKey(cluster, loadSettings()) + '|' + nodeName : null, function () {
+      return source.fetchNodeMetrics(nodeName).then(function (m) { return [m, null]; });
+    });
+  }
+
+  /** Pod → GPU attribution for the Pods page (metrics.js fetchGpuOwners): one series per allocated GPU. */
+  function useGpuOwners(enabled) {
+    const cluster = clusterKey();
+    const source = metricsSourceFor(cluster);
+    const on = enabled === undefined ? true : enabled;
+    return useMetricsFetch(on ? 'owners|' + sourceKey(cluster, loadSettings()) : null, function () {
+      return source.fetchGpuOwners().then(function (m) { return [m, null]; });
+    });
+  }
+
+  return {
+    Context: Context,
+    AmdGpuDataProvider: AmdGpuDataProvider,
+    useAmdGpuContext: useAmdGpuContext,
+    useGpuMetrics: useGpuMetrics,
+    useNodeGpuMetrics: useNodeGpuMetrics,
+    useGpuOwners: useGpuOwners,
+    storeFor: storeFor,
+    metricsSourceFor: metricsSourceFor,
+  };
+}

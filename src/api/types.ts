@@ -185,6 +185,8 @@ export interface NodeStats {
   inUse: number;
   pods: number;
   ready: boolean;
+  physicalGpus: number;
+  partitionsPerGpu: number;
 }
 
 export interface ClusterIndex {
@@ -198,7 +200,91 @@ export interface ClusterIndex {
     inUse: number;
     free: number;
     partitions: number;
+    physicalGpus: number;
+    hbmBytes: number;
+    hbmAllocatedBytes: number;
     utilizationPct: number;
   };
   phases: { Running: number; Pending: number; Succeeded: number; Failed: number; Other: number };
+}
+
+// ---------------------------------------------------------------------------
+// Store snapshot (clusterStore.js getSnapshot()) — the context value minus `refresh`
+// ---------------------------------------------------------------------------
+
+export type ListState = 'unknown' | 'pending' | 'ready' | 'error';
+
+export interface ClusterSnapshot {
+  deviceConfigs: DeviceConfig[];
+  pluginInstalled: boolean;
+  gpuNodes: AmdGpuNode[];
+  gpuPods: AmdGpuPod[];
+  pluginPods: AmdGpuPod[];
+  crdAvailable: boolean;
+  /** true until the node and pod lists settled (arrived or failed) and the first CRD fetch is in */
+  loading: boolean;
+  nodesState: ListState;
+  podsState: ListState;
+  /** a refresh is in flight; the data above is still valid */
+  refreshing: boolean;
+  error: string | null;
+  index: ClusterIndex;
+  lastUpdated: number | null;
+  version: number;
+}
+
+/** The provider's context value (reference IntelGpuContextValue, IntelGpuDataContext.tsx:28-52). */
+export interface AmdGpuContextValue extends ClusterSnapshot {
+  refresh: () => void;
+}
+
+// ---------------------------------------------------------------------------
+// Telemetry (metrics.js)
+// ---------------------------------------------------------------------------
+
+export interface GpuTelemetry {
+  nodeName: string;
+  /** device index on the node ("0".."7") */
+  gpu: string;
+  instance: string;
+  powerWatts: number | null;
+  powerCapWatts: number | null;
+  vramUsedBytes: number | null;
+  vramTotalBytes: number | null;
+  gfxActivityPct: number | null;
+  memActivityPct: number | null;
+  tempC: number | null;
+  tempSlowdownC: number | null;
+  eccCorrectable: number | null;
+  eccUncorrectable: number | null;
+  pod: string | null;
+  namespace: string | null;
+}
+
+export interface GpuMetrics {
+  source: 'amd-exporter' | 'node-exporter' | null;
+  gpus: GpuTelemetry[];
+  /** node → "src-dst" → GB/s */
+  xgmi: Record<string, Record<string, number>>;
+  /** node → "src-dst" → link type / hops (measured topology) */
+  links: Record<string, Record<string, { type: string; hops: number }>>;
+  fetchedAt: string;
+  stale?: boolean;
+  prometheusPath: string;
+  /** PromQL of the main telemetry query (shown on the Metrics page) */
+  query?: string;
+}
+
+export interface GpuSeries {
+  rangeSec: number;
+  power: Record<string, Array<[number, number]>>;
+  vram: Record<string, Array<[number, number]>>;
+}
+
+export interface GpuMetricsState {
+  metrics: GpuMetrics | null;
+  series: GpuSeries | null;
+  fetchError: string | null;
+  fetching: boolean;
+  refresh: () => void;
 }

@@ -1,13 +1,7 @@
 /**
- * DevicePluginsPage — AMD GPU Operator DeviceConfigs and operand pods
- * (reference DevicePluginsPage.tsx, SURVEY.md C6).
+ * DevicePluginsPage — AMD GPU Operator DeviceConfigs and operand pods (reference DevicePluginsPage.tsx, C6).
+ * Implementation: src/plugin.js (`createPlugin`).
  */
-import React from 'react';
-import { useAmdGpuContext } from '../api/AmdGpuDataContext';
-import { devicePluginsView } from '../view/pages.js';
-import { Page } from './View';
+import { plugin } from '../headlamp';
 
-export default function DevicePluginsPage() {
-  const ctx = useAmdGpuContext();
-  return <Page vm={devicePluginsView(ctx)} onRefresh={ctx.refresh} />;
-}
+export default plugin.DevicePluginsPage;

@@ -1,21 +1,7 @@
 /**
- * NodesPage — MI355X nodes: summary table, per-node cards with per-GPU
- * allocation and the xGMI neighbour matrix (reference NodesPage.tsx, SURVEY.md C7).
- * Exporter telemetry, when reachable, upgrades the slots to exact pod→GPU
- * ownership and overlays measured xGMI throughput.
+ * NodesPage — MI355X nodes with per-GPU allocation and the xGMI matrix (reference NodesPage.tsx, C7).
+ * Implementation: src/plugin.js (`createPlugin`).
  */
-import React from 'react';
-import { useAmdGpuContext, useGpuMetrics } from '../api/AmdGpuDataContext';
-import { nodesView } from '../view/pages.js';
-import { Page } from './View';
+import { plugin } from '../headlamp';
 
-export default function NodesPage() {
-  const ctx = useAmdGpuContext();
-  // Telemetry only (owners, xGMI): this page draws no time series.
-  const m = useGpuMetrics(true, false);
-  const refresh = () => {
-    ctx.refresh();
-    m.refresh();
-  };
-  return <Page vm={nodesView(ctx, { metrics: m.metrics })} onRefresh={refresh} />;
-}
+export default plugin.NodesPage;

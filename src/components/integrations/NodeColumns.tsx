@@ -1,15 +1,9 @@
 /**
- * NodeColumns — GPU columns appended to Headlamp's native Nodes table
- * (reference integrations/NodeColumns.tsx, SURVEY.md C12): GPU Model,
- * GPU Devices and GPU HBM. Each row is classified once for all columns.
+ * NodeColumns — GPU Model / GPU Devices / GPU HBM columns appended to the
+ * native Nodes table (reference integrations/NodeColumns.tsx, SURVEY.md C12).
+ * Implementation: src/plugin.js (`buildNodeGpuColumns`) over
+ * src/view/pages.js (`nodeColumns`).
  */
-import React from 'react';
-import { nodeColumns } from '../../view/pages.js';
-import { Value } from '../View';
+import { plugin } from '../../headlamp';
 
-export function buildNodeGpuColumns() {
-  return nodeColumns().map((c: { label: string; getter: (r: unknown) => unknown }) => ({
-    label: c.label,
-    getter: (resource: unknown) => <Value v={c.getter(resource)} />,
-  }));
-}
+export const buildNodeGpuColumns = plugin.buildNodeGpuColumns;

@@ -1,0 +1,224 @@
+/**
+ * The plugin, assembled: every page, detail section, table column and the
+ * settings page, built from the pure view-models (./view/pages.js), the IR
+ * renderer (./view/react.js) and the provider core (./api/providerCore.js)
+ * against an INJECTED React + Headlamp library. `registerPlugin` performs the
+ * registration the reference does at module load (src/index.tsx:35-182,
+ * SURVEY.md C1): sidebar root + 5 children, 5 exact routes, the Node and Pod
+ * detail sections and the `headlamp-nodes` column processor, plus the plugin
+ * settings page when the host offers `registerPluginSettings`.
+ *
+ * src/index.tsx is a shim that calls these two functions with the real React
+ * and '@kinvolk/headlamp-plugin/lib'; the Node-12 harness calls them with
+ * its stand-ins (tests/js/stubs/), so what the tests execute is the shipped
+ * code, not a copy.
+ *
+ * Unlike the reference, routes do not each mount a cold provider: the
+ * provider is a view onto one shared per-cluster store, so switching pages
+ * or opening a Node detail view renders cached data at once and revalidates
+ * in the background (reference quirk Q7).
+ */
+
+import { createProviderCore } from './api/providerCore.js';
+import { get, isAmdGpuNode, isGpuRequestingPod, unwrapKubeObject } from './api/amdgpu.js';
+import {
+  devicePluginsView,
+  metricsView,
+  nodeColumns,
+  nodeDetailView,
+  nodesView,
+  overviewView,
+  podDetailView,
+  podsView,
+} from './view/pages.js';
+import { createRenderer } from './view/react.js';
+import { createSettingsPage } from './view/settingsPage.js';
+import { processColumns, ROUTES, SIDEBAR } from './routes.js';
+
+/** Plugin name used for `registerPluginSettings`. */
+export const PLUGIN_NAME = 'amd-gpu';
+
+/**
+ * @param {{React: any, lib: any, CommonComponents: Record<string, Function>,
+ *          deps?: Parameters<typeof createProviderCore>[2], settingsStorage?: {load: Function, save: Function}}} env
+ */
+export function createPlugin(env) {
+  if (!env || !env.React || !env.lib || !env.CommonComponents) throw new Error('createPlugin: React, lib and CommonComponents are required');
+  const React = env.React;
+  const h = React.createElement;
+  const core = createProviderCore(React, env.lib, env.deps);
+  const view = createRenderer(React, env.CommonComponents);
+  const Page = view.Page;
+  const Section = view.Section;
+  const Value = view.Value;
+
+  // -------------------------------------------------------------------------
+  // Pages (reference src/components/*Page.tsx, SURVEY.md C5–C9)
+  // -------------------------------------------------------------------------
+
+  /** Cluster-level MI355X dashboard (reference OverviewPage.tsx, C5). */
+  function OverviewPage() {
+    const ctx = core.useAmdGpuContext();
+    return h(Page, { vm: overviewView(ctx), onRefresh: ctx.refresh });
+  }
+
+  /** AMD GPU Operator DeviceConfigs and operand pods (reference DevicePluginsPage.tsx, C6). */
+  function DevicePluginsPage() {
+    const ctx = core.useAmdGpuContext();
+    return h(Page, { vm: devicePluginsView(ctx), onRefresh: ctx.refresh });
+  }
+
+  /**
+   * MI355X nodes: summary table, per-node cards with the per-GPU allocation
+   * strip and the xGMI matrix (reference NodesPage.tsx, C7). Exporter
+   * telemetry (no time series: this page draws none) upgrades the strip to
+   * exact pod→GPU ownership and overlays measured xGMI throughput.
+   */
+  function NodesPage() {
+    const ctx = core.useAmdGpuContext();
+    const m = core.useGpuMetrics(true, false);
+    function refresh() {
+      ctx.refresh();
+      m.refresh();
+    }
+    return h(Page, { vm: nodesView(ctx, { metrics: m.metrics }), onRefresh: refresh });
+  }
+
+  /**
+   * Pods requesting amd.com/* (reference PodsPage.tsx, C8). Exporter pod
+   * labels add the physical GPUs each pod holds — fetched as attribution only,
+   * one series per allocated GPU.
+   */
+  function PodsPage() {
+    const ctx = core.useAmdGpuContext();
+    const m = core.useGpuOwners();
+    function refresh() {
+      ctx.refresh();
+      m.refresh();
+    }
+    return h(Page, { vm: podsView(ctx, { metrics: m.metrics }), onRefresh: refresh });
+  }
+
+  /** Power, HBM, activity, temperature, RAS and xGMI telemetry from Prometheus (reference MetricsPage.tsx, C9). */
+  function MetricsPage() {
+    const ctx = core.useAmdGpuContext();
+    const m = core.useGpuMetrics(true, true);
+    return h(Page, { vm: metricsView(ctx, m), onRefresh: m.refresh });
+  }
+
+  // -------------------------------------------------------------------------
+  // Native-view integrations (reference C10–C12)
+  // -------------------------------------------------------------------------
+
+  /**
+   * Section on Headlamp's Node detail page (reference NodeDetailSection.tsx,
+   * C10). Nothing for non-AMD nodes. Reads the shared store, so it costs no
+   * fetch when a plugin page already loaded the cluster; the node's own
+   * telemetry comes from one `hostname`-scoped query.
+   */
+  function NodeDetailSection(props) {
+    const ctx = core.useAmdGpuContext();
+    const raw = unwrapKubeObject(props.resource);
+    const gpuNode = isAmdGpuNode(raw);
+    const m = core.useNodeGpuMetrics(gpuNode ? raw.metadata.name : null, gpuNode);
+    const section = nodeDetailView(props.resource, ctx, { metrics: m.metrics });
+    return section ? h(Section, { s: section }) : null;
+  }
+
+  /**
+   * Section on Headlamp's Pod detail page (reference PodDetailSection.tsx,
+   * C11). Needs no cluster data, so it mounts no provider; for a scheduled GPU
+   * pod it reads the telemetry of the pod's node only (live power / GFX / HBM
+   * of the GPUs the pod holds).
+   */
+  function PodDetailSection(props) {
+    const raw = unwrapKubeObject(props.resource);
+    const gpuPod = isGpuRequestingPod(raw);
+    const nodeName = gpuPod ? get(raw, ['spec', 'nodeName'], null) : null;
+    const m = core.useNodeGpuMetrics(nodeName, gpuPod);
+    const section = podDetailView(props.resource, { metrics: m.metrics });
+    return section ? h(Section, { s: section }) : null;
+  }
+
+  /** GPU Model / GPU Devices / GPU HBM columns for the native Nodes table (reference NodeColumns.tsx, C12). */
+  function buildNodeGpuColumns() {
+    return nodeColumns().map(function (c) {
+      return { label: c.label, getter: function (resource) { return h(Value, { v: c.getter(resource) }); } };
+    });
+  }
+
+  const pages = {
+    overview: OverviewPage,
+    'device-plugins': DevicePluginsPage,
+    nodes: NodesPage,
+    pods: PodsPage,
+    metrics: MetricsPage,
+  };
+
+  /** Route component: the page under the (shared-store) provider. */
+  function routeComponent(page) {
+    const P = pages[page];
+    if (!P) throw new Error('createPlugin: unknown page ' + page);
+    function Route() {
+      return h(core.AmdGpuDataProvider, null, h(P, null));
+    }
+    Route.displayName = 'AmdGpuRoute(' + page + ')';
+    return Route;
+  }
+
+  /** Detail-view section callback for Nodes (reference src/index.tsx:152-160). */
+  function nodeDetailSectionFor(args) {
+    const resource = args && args.resource;
+    if (!resource || resource.kind !== 'Node') return null;
+    return h(core.AmdGpuDataProvider, null, h(NodeDetailSection, { resource: resource }));
+  }
+
+  /** Detail-view section callback for Pods: no provider (reference src/index.tsx:167-170). */
+  function podDetailSectionFor(args) {
+    const resource = args && args.resource;
+    if (!resource || resource.kind !== 'Pod') return null;
+    return h(PodDetailSection, { resource: resource });
+  }
+
+  return {
+    core: core,
+    view: view,
+    AmdGpuDataProvider: core.AmdGpuDataProvider,
+    useAmdGpuContext: core.useAmdGpuContext,
+    OverviewPage: OverviewPage,
+    DevicePluginsPage: DevicePluginsPage,
+    NodesPage: NodesPage,
+    PodsPage: PodsPage,
+    MetricsPage: MetricsPage,
+    NodeDetailSection: NodeDetailSection,
+    PodDetailSection: PodDetailSection,
+    SettingsPage: createSettingsPage(React, env.CommonComponents, env.settingsStorage),
+    buildNodeGpuColumns: buildNodeGpuColumns,
+    pages: pages,
+    routeComponent: routeComponent,
+    nodeDetailSectionFor: nodeDetailSectionFor,
+    podDetailSectionFor: podDetailSectionFor,
+  };
+}
+
+/**
+ * Register every extension point with Headlamp (reference src/index.tsx:35-182).
+ * @param {any} lib  '@kinvolk/headlamp-plugin/lib'
+ * @param {ReturnType<typeof createPlugin>} plugin
+ * @returns {{sidebar: number, routes: number, detailSections: number, columnProcessors: number, settings: boolean}}
+ */
+export function registerPlugin(lib, plugin) {
+  for (let i = 0; i < SIDEBAR.length; i++) lib.registerSidebarEntry(SIDEBAR[i]);
+  for (let i = 0; i < ROUTES.length; i++) {
+    const r = ROUTES[i];
+    lib.registerRoute({ path: r.path, sidebar: r.sidebar, name: r.name, exact: true, component: plugin.routeComponent(r.page) });
+  }
+  lib.registerDetailsViewSection(plugin.nodeDetailSectionFor);
+  lib.registerDetailsViewSection(plugin.podDetailSectionFor);
+  lib.registerResourceTableColumnsProcessor(function (args) { return processColumns(args, plugin.buildNodeGpuColumns); });
+  // Headlamp >= 0.22 offers plugin settings; older hosts run with the
+  // defaults of src/api/settings.js.
+  const settings = typeof lib.registerPluginSettings === 'function';
+  if (settings) lib.registerPluginSettings(PLUGIN_NAME, plugin.SettingsPage, false);
+  return { sidebar: SIDEBAR.length, routes: ROUTES.length, detailSections: 2, columnProcessors: 1, settings: settings };
+}

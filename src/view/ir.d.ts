@@ -1,0 +1,174 @@
+/**
+ * Types of the view IR (./ir.js): what every view-model in ./pages.js
+ * returns and what ./react.js renders. Replaces the untyped `IR = any` of
+ * round 1; the reference's convention is "no `any`, unknown + guards"
+ * (reference CLAUDE.md:76).
+ */
+import type { Status } from '../api/types';
+
+export type { Status };
+
+/** A status label cell (StatusLabel). */
+export interface StatusCell {
+  t: 'status';
+  status: Status;
+  text: string;
+}
+
+/** Inline allocation / power bar cell; `pct` null draws the text only. */
+export interface BarCell {
+  t: 'bar';
+  used: number;
+  total: number | null;
+  pct: number | null;
+  color: string;
+  text: string;
+}
+
+/** Multi-line cell: "<strong>label</strong>: text" per line. */
+export interface LinesCell {
+  t: 'lines';
+  lines: Array<{ label: string; text: string }>;
+}
+
+export type Cell = string | number | null | StatusCell | BarCell | LinesCell;
+
+export interface KvRow {
+  name: string;
+  value: Cell;
+}
+
+export interface KvBlock {
+  t: 'kv';
+  rows: KvRow[];
+}
+
+export interface TableBlock {
+  t: 'table';
+  columns: string[];
+  rows: Cell[][];
+  /** Stable row keys (uids) when the rows are Kubernetes objects. */
+  keys: string[] | null;
+}
+
+export interface PctbarDatum {
+  name: string;
+  value: number;
+  fill: string;
+}
+
+export interface PctbarBlock {
+  t: 'pctbar';
+  label: string;
+  data: PctbarDatum[];
+  total: number;
+}
+
+/** One schedulable device of a node (src/api/topology.js buildGpuSlots). */
+export interface GpuSlot {
+  index: number;
+  board: number;
+  partition: number | null;
+  pod: string | null;
+  namespace: string | null;
+  inferred: boolean;
+}
+
+export interface SlotsBlock {
+  t: 'slots';
+  slots: GpuSlot[];
+  /** Owners came from exporter pod labels (else inferred from pod order). */
+  exact: boolean;
+  partitionsPerGpu: number;
+}
+
+export interface XgmiCell {
+  kind: 'self' | 'xgmi' | 'pcie' | 'none';
+  hops: number;
+  peakGBs: number;
+  measuredGBs: number | null;
+}
+
+export interface XgmiMatrix {
+  size: number;
+  cells: XgmiCell[][];
+  linksPerGpu: number;
+  perGpuPeakGBs: number;
+  ringBusGBs: number;
+}
+
+export interface MatrixBlock {
+  t: 'matrix';
+  matrix: XgmiMatrix;
+  fullMesh: boolean;
+  /** Link types / hops were measured (exporter link series) rather than assumed. */
+  measuredTopology: boolean;
+  /** Per-link throughput was measured (stock exporter xgmi_neighbor_* series). */
+  measuredThroughput: boolean;
+}
+
+/** [unix seconds, value] */
+export type SeriesPoint = [number, number];
+
+export interface SeriesBlock {
+  t: 'series';
+  power: Record<string, SeriesPoint[]>;
+  vram: Record<string, SeriesPoint[]>;
+}
+
+export type Block = KvBlock | TableBlock | PctbarBlock | SlotsBlock | MatrixBlock | SeriesBlock;
+
+export interface Section {
+  t: 'section';
+  title: string;
+  key: string;
+  blocks: Block[];
+}
+
+export interface LoaderItem {
+  t: 'loader';
+  title: string;
+}
+
+export interface RefreshButton {
+  label: string;
+  ariaLabel: string;
+  disabled: boolean;
+}
+
+export interface PageVM {
+  t: 'page';
+  /** null while the page is only a loader */
+  title: string | null;
+  refresh: RefreshButton | null;
+  items: Array<Section | LoaderItem>;
+}
+
+export function status(st: Status, text: string | number): StatusCell;
+export function bar(used: number, total: number | null, pctValue: number | null, color: string, text: string): BarCell;
+export function lines(items: Array<{ label: string; text: string }>): LinesCell;
+export function kv(rows: KvRow[]): KvBlock;
+export function row(name: string, value: Cell): KvRow;
+export function table(columns: string[], rows: Cell[][], keys?: string[]): TableBlock;
+export function pctbar(label: string, data: PctbarDatum[], total: number): PctbarBlock;
+export function section(title: string, blocks: Block[], key?: string): Section;
+export function loader(title: string): LoaderItem;
+export function page(title: string | null, refresh: RefreshButton | null, items: Array<Section | LoaderItem>): PageVM;
+
+export interface Memo {
+  <T>(key: string, deps: readonly unknown[], compute: () => T): T;
+  clear(): void;
+  size(): number;
+}
+export function createMemo(limit?: number): Memo;
+
+export function sections(vm: PageVM | Section | null): Section[];
+export function sectionTitles(vm: PageVM | Section | null): string[];
+export function findSection(vm: PageVM | Section | null, title: string): Section | null;
+export function loaders(vm: PageVM | null): string[];
+export function rowValue(scope: PageVM | Section | null, name: string): Cell | undefined;
+export function rowNames(sec: Section | null): string[];
+export function firstTable(sec: Section | null): TableBlock | null;
+export function firstBlock(sec: Section | null, t: Block['t']): Block | null;
+export function text(v: Cell | undefined): string;
+export function countRows(vm: PageVM | Section | null): { sections: number; tableRows: number; kvRows: number; gpuCells: number };

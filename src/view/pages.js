@@ -154,7 +154,7 @@ function restartsCell(p) {
  */
 export function overviewView(ctx, opts) {
   const now = nowOf(opts);
-  if (ctx.loading && !ctx.lastUpdated) return page(null, null, [loader('Loading ' + BRAND + ' data...')]);
+  if (ctx.loading) return page(null, null, [loader('Loading ' + BRAND + ' data...')]);
   const items = memo(
     'overview',
     [ctx.deviceConfigs, ctx.pluginPods, ctx.pluginInstalled, ctx.crdAvailable, ctx.gpuNodes, ctx.gpuPods, ctx.index, ctx.error, ageKey(now)],
@@ -339,7 +339,7 @@ function enabledCell(on, detail) {
  */
 export function devicePluginsView(ctx, opts) {
   const now = nowOf(opts);
-  if (ctx.loading && !ctx.lastUpdated) return page(null, null, [loader('Loading device plugin data...')]);
+  if (ctx.loading) return page(null, null, [loader('Loading device plugin data...')]);
   const items = memo(
     'device-plugins',
     [ctx.deviceConfigs, ctx.pluginPods, ctx.crdAvailable, ctx.error, ageKey(now)],
@@ -485,7 +485,7 @@ function nodeCardRows(node, podsOnNode, stats, now) {
 export function nodesView(ctx, opts) {
   const now = nowOf(opts);
   const metrics = opts && opts.metrics ? opts.metrics : null;
-  if (ctx.loading && !ctx.lastUpdated) return page(null, null, [loader('Loading GPU node data...')]);
+  if (ctx.loading) return page(null, null, [loader('Loading GPU node data...')]);
   const age = ageKey(now);
   const head = memo('nodes-head', [ctx.gpuNodes, ctx.index, ctx.error, age], function () {
     return nodesHeadItems(ctx, now);
@@ -692,7 +692,7 @@ export function gpuContainerLines(pod) {
 
 export function podsView(ctx, opts) {
   const now = nowOf(opts);
-  if (ctx.loading && !ctx.lastUpdated) return page(null, null, [loader('Loading GPU pod data...')]);
+  if (ctx.loading) return page(null, null, [loader('Loading GPU pod data...')]);
   const assign = opts && opts.metrics ? podGpuAssignments(opts.metrics) : null;
   const items = memo('pods', [ctx.gpuPods, ctx.index, ctx.error, assign, ageKey(now)], function () {
     return podsItems(ctx, now, assign);
@@ -822,7 +822,7 @@ export function metricAvailabilitySection() {
 export function metricsView(ctx, mstate, opts) {
   const now = nowOf(opts);
   const items = [];
-  if (ctx.loading && !ctx.lastUpdated) items.push(loader('Loading ' + BRAND + ' data...'));
+  if (ctx.loading) items.push(loader('Loading ' + BRAND + ' data...'));
   items.push(metricAvailabilitySection());
   const m = mstate.metrics;
   if (mstate.fetching && !m) items.push(loader('Querying Prometheus for GPU metrics...'));
@@ -982,7 +982,7 @@ export function nodeDetailView(resource, ctx, opts) {
   if (Object.keys(cap).length === 0 && Object.keys(alloc).length === 0) return null;
   const name = raw.metadata.name;
   let podsOnNode;
-  if (ctx.loading && !ctx.lastUpdated) podsOnNode = [];
+  if (ctx.loading) podsOnNode = [];
   else if (ctx.index && ctx.index.podsByNode && ctx.index.podsByNode[name]) podsOnNode = ctx.index.podsByNode[name];
   else podsOnNode = ctx.gpuPods.filter(function (p) { return get(p, ['spec', 'nodeName'], null) === name; });
   const metrics = opts && opts.metrics ? opts.metrics : null;

@@ -1,0 +1,46 @@
+/**
+ * Types of the IR renderer (./react.js). `ReactLike` is the slice of React
+ * the renderer needs, so the real React and the harness stand-in
+ * (tests/js/stubs/react.js) both satisfy it.
+ */
+import type { ComponentType, CSSProperties, ReactElement, ReactNode } from 'react';
+import type { Block as IRBlock, Cell, MatrixBlock, PageVM, Section as IRSection, SeriesPoint } from './ir';
+
+export interface ReactLike {
+  createElement: (...args: never[]) => ReactElement;
+  memo: <P>(c: ComponentType<P>) => ComponentType<P>;
+  Fragment: unknown;
+}
+
+/** The Headlamp CommonComponents the renderer draws with. */
+export interface CommonComponentsLike {
+  Loader: ComponentType<{ title: string }>;
+  NameValueTable: ComponentType<{ rows: Array<{ name: string; value: ReactNode }> }>;
+  PercentageBar: ComponentType<{ data: Array<{ name: string; value: number; fill: string }>; total: number }>;
+  SectionBox: ComponentType<{ title: string; children?: ReactNode }>;
+  SectionHeader: ComponentType<{ title: string }>;
+  SimpleTable: ComponentType<{ columns: Array<{ label: string; getter: (row: never) => ReactNode }>; data: unknown[] }>;
+  StatusLabel: ComponentType<{ status: 'success' | 'warning' | 'error'; children?: ReactNode }>;
+}
+
+export const REQUIRED_COMPONENTS: ReadonlyArray<keyof CommonComponentsLike>;
+
+export function buttonStyle(disabled: boolean): CSSProperties;
+export function sparklinePath(points: SeriesPoint[] | null | undefined, w: number, h: number): string | null;
+export function matrixCellColor(c: MatrixBlock['matrix']['cells'][number][number]): string;
+export function matrixCaption(b: MatrixBlock): string;
+
+export interface Renderer {
+  Value: ComponentType<{ v: Cell | undefined }>;
+  InlineBar: ComponentType<{ pct: number | null; color: string; text: string }>;
+  Slots: ComponentType<{ b: IRBlock }>;
+  Matrix: ComponentType<{ b: MatrixBlock }>;
+  Sparkline: ComponentType<{ points: SeriesPoint[]; color: string; label?: string }>;
+  Series: ComponentType<{ b: IRBlock }>;
+  Block: ComponentType<{ b: IRBlock }>;
+  Section: ComponentType<{ s: IRSection | null }>;
+  SectionImpl: ComponentType<{ s: IRSection | null }>;
+  Page: ComponentType<{ vm: PageVM; onRefresh?: () => void }>;
+}
+
+export function createRenderer(React: ReactLike, CC: CommonComponentsLike): Renderer;

@@ -373,6 +373,30 @@ describe('degraded RBAC: an errored list is settled, not loading', () => {
     store.setNodes([], null);
     expect(store.getSnapshot().loading).toBe(false);
   });
+  it('a fresh list hook reporting "no items yet" keeps the list already held', async () => {
+    const store = createClusterStore({ request: router(baseRoutes()) });
+    store.setNodes([makeGpuNode('mi355x-0')], null);
+    store.setPods([makeGpuPod('train-0')], null);
+    await store.refresh();
+    const before = store.getSnapshot();
+    store.setNodes(null, null);
+    store.setPods(null, null);
+    const s = store.getSnapshot();
+    expect(s).toBe(before);
+    expect(s.loading).toBe(false);
+    expect(s.gpuNodes).toHaveLength(1);
+    expect(s.gpuPods).toHaveLength(1);
+  });
+  it('a refresh after the first load never brings the loader back', async () => {
+    const store = createClusterStore({ request: router(baseRoutes()) });
+    store.setNodes([], null);
+    store.setPods([], null);
+    await store.refresh();
+    const p = store.refresh();
+    expect(store.getSnapshot().loading).toBe(false);
+    expect(store.getSnapshot().refreshing).toBe(true);
+    await p;
+  });
   it('a list that recovers from an error clears the error', async () => {
     const store = createClusterStore({ request: router(baseRoutes()) });
     store.setNodes([], null);

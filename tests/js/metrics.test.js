@@ -27,77 +27,7 @@ import {
   promString,
 } from '../../src/api/metrics.js';
 
-const BASE0 = servicePath(PROMETHEUS_SERVICES[0]);
-const BASE1 = servicePath(PROMETHEUS_SERVICES[1]);
-
-function vec(metric, v) {
-  return { metric, value: [1760000000, String(v)] };
-}
-function ok(result) {
-  return { status: 'success', data: { resultType: 'vector', result } };
-}
-
-/** Exporter series for `nodes` × 8 GPUs, as a name → rows map (rows carry __name__). */
-function exporterData(nodes) {
-  const d = {};
-  const E = SERIES.exporter;
-  [E.power, E.vramUsed, E.vramTotal, E.gfx, E.umc, E.temp].forEach((k) => (d[k] = []));
-  d.__xgmi = [];
-  const add = (name, m, v) => d[name].push(vec(Object.assign({ __name__: name }, m), v));
-  nodes.forEach((node) => {
-    for (let g = 0; g < 8; g++) {
-      const m = { hostname: node, gpu_id: String(g), instance: node + ':5000' };
-      add(E.power, Object.assign({}, m, g < 2 ? { pod: 'train-' + g, namespace: 'ml' } : {}), 700 + g);
-      add(E.vramUsed, m, 1024 * (g + 1));
-      add(E.vramTotal, m, 288 * 1000 * 1000 * 1000 / (1024 * 1024));
-      add(E.gfx, m, 50);
-      add(E.umc, m, 30);
-      add(E.temp, m, 60);
-      d.__xgmi.push(vec(Object.assign({ __name__: 'xgmi_neighbor_0_tx_throughput' }, m), 50e9));
-    }
-  });
-  return d;
-}
-
-function flatten(d) {
-  const out = [];
-  if (!d) return out;
-  Object.keys(d).forEach((k) => d[k].forEach((r) => out.push(r)));
-  return out;
-}
-
-/** A fake proxy: answers probes on `up` services and `{__name__=~"a|b"}` queries from `data` / `ne`. */
-function prom(opts) {
-  const o = Object.assign({ up: [BASE0], data: exporterData(['n0']), ne: null }, opts || {});
-  const rows = flatten(o.data).concat(flatten(o.ne));
-  return vi.fn((path) => {
-    const base = o.up.find((b) => path.indexOf(b) === 0);
-    if (!base) return Promise.reject(new Error('503'));
-    const q = decodeURIComponent((path.split('query=')[1] || '').split('&')[0]);
-    if (q === '1') return Promise.resolve(ok([{ metric: {}, value: [0, '1'] }]));
-    if (path.indexOf('/query_range') >= 0) {
-      const end = Number(/end=(\d+)/.exec(path)[1]);
-      const values = [[end - 30, '100'], [end, '200']];
-      return Promise.resolve({
-        status: 'success',
-        data: {
-          resultType: 'matrix',
-          result: [
-            { metric: { __name__: 'gpu_power_usage', hostname: 'n0' }, values },
-            { metric: { __name__: 'gpu_used_vram', hostname: 'n0' }, values },
-          ],
-        },
-      });
-    }
-    const own = /^max by \([^)]*\) \(\{__name__="([a-z_]+)", pod!=""\}\)$/.exec(q);
-    if (own) return Promise.resolve(ok(rows.filter((r) => r.metric.__name__ === own[1] && r.metric.pod)));
-    const m = /^(?:max by \([^)]*\) \()?\{__name__=~"(.*?)"(?:, hostname="((?:[^"\\]|\\.)*)")?\}\)?$/.exec(q);
-    if (!m) return Promise.resolve(ok([]));
-    const re = new RegExp('^(?:' + m[1] + ')$');
-    const host = m[2] === undefined ? null : m[2].replace(/\\(.)/g, '$1');
-    return Promise.resolve(ok(rows.filter((r) => re.test(r.metric.__name__ || '') && (host === null || r.metric.hostname === host))));
-  });
-}
+import { BASE0, BASE1, exporterData, ok, prom, vec } from './promFake.js';
 
 describe('discovery', () => {
   it('probes all candidate services in parallel', async () => {

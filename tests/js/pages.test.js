@@ -38,10 +38,16 @@ describe('overviewView', () => {
   });
 
   it('keeps content visible during a refresh (no loader swap)', () => {
-    const vm = overviewView(makeContext({ loading: true, refreshing: true, nodes: [makeGpuNode('g')] }), opts);
+    // The store keeps `loading` false once everything settled; a refresh only sets `refreshing`.
+    const vm = overviewView(makeContext({ loading: false, refreshing: true, nodes: [makeGpuNode('g')] }), opts);
     expect(loaders(vm)).toEqual([]);
     expect(vm.refresh.label).toBe('Refreshing…');
     expect(vm.refresh.disabled).toBe(true);
+  });
+
+  it('shows the loader while a list is still in flight even if the CRD answered', () => {
+    const vm = overviewView(makeContext({ loading: true, lastUpdated: 1, nodes: [makeGpuNode('g')] }), opts);
+    expect(loaders(vm)).toEqual(['Loading AMD GPU data...']);
   });
 
   it('has the page header and refresh aria-label', () => {

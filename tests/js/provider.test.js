@@ -1,0 +1,422 @@
+/**
+ * Provider core (src/api/providerCore.js) executed under the harness React
+ * (tests/js/stubs/react.js) and the Headlamp library stand-in
+ * (tests/js/stubs/headlamp-lib.js). Mirrors the reference's provider specs
+ * (src/api/IntelGpuDataContext.test.tsx:46-176: outside-provider throw,
+ * request issuing, CRD absent vs present) and adds what the shared store
+ * promises: request counts on mount, dedup across providers, stale-while-
+ * revalidate remounts, degraded RBAC and the metrics hooks.
+ */
+import React, { render } from './stubs/react.js';
+import * as lib from './stubs/headlamp-lib.js';
+import { OUTSIDE_PROVIDER, PROMETHEUS_UNREACHABLE, STALE_MS, createProviderCore } from '../../src/api/providerCore.js';
+import { resetSharedStores } from '../../src/api/clusterStore.js';
+import { DEVICE_CONFIG_LIST_PATH, PLUGIN_POD_QUERIES } from '../../src/api/amdgpu.js';
+import { DEFAULT_SETTINGS } from '../../src/api/settings.js';
+import { makeDeviceConfig, makeGpuNode, makeGpuPod, makeNode, makePlainPod, makePluginPod } from './fixtures.js';
+import { BASE0, exporterData, prom } from './promFake.js';
+
+const h = React.createElement;
+
+function kubeList(items) {
+  return { kind: 'List', apiVersion: 'v1', metadata: {}, items: items };
+}
+
+function notFound() {
+  return Promise.reject(Object.assign(new Error('404 page not found'), { status: 404 }));
+}
+
+/** API server fake: CRD → `dcs` (or `crd` handler), plugin-pod queries → `pluginPods`. */
+function apiServer(o) {
+  const opt = Object.assign({ dcs: [makeDeviceConfig()], pluginPods: [] }, o || {});
+  return vi.fn((path) => {
+    if (path === DEVICE_CONFIG_LIST_PATH) return opt.crd ? opt.crd() : Promise.resolve(kubeList(opt.dcs));
+    if (PLUGIN_POD_QUERIES.indexOf(path) >= 0) return Promise.resolve(kubeList(opt.pluginPods));
+    if (opt.prom) return opt.prom(path);
+    return notFound();
+  });
+}
+
+function crdCalls(request) {
+  return request.mock.calls.filter((c) => c[0] === DEVICE_CONFIG_LIST_PATH).length;
+}
+
+let settings;
+
+function core(request) {
+  return createProviderCore(React, lib, {
+    request: request,
+    clusterKey: () => 'test-cluster',
+    loadSettings: () => settings,
+  });
+}
+
+/** A consumer that records every context value it renders with. */
+function probe(c) {
+  const seen = [];
+  function Probe() {
+    const ctx = c.useAmdGpuContext();
+    seen.push(ctx);
+    return h('div', { 'data-testid': 'probe' }, ctx.loading ? 'loading' : 'nodes=' + ctx.gpuNodes.length + ' pods=' + ctx.gpuPods.length);
+  }
+  return { Probe, seen, last: () => seen[seen.length - 1] };
+}
+
+beforeEach(() => {
+  lib.resetHeadlamp();
+  resetSharedStores();
+  settings = Object.assign({}, DEFAULT_SETTINGS);
+});
+
+afterEach(() => {
+  vi.useRealTimers();
+});
+
+describe('createProviderCore', () => {
+  it('requires the React hooks it uses', () => {
+    expect(() => createProviderCore({ createElement: React.createElement }, lib)).toThrow('React.createContext is required');
+  });
+});
+
+describe('useAmdGpuContext', () => {
+  it('throws outside a provider', () => {
+    const c = core(apiServer());
+    const { Probe } = probe(c);
+    expect(() => render(h(Probe))).toThrow(OUTSIDE_PROVIDER);
+  });
+
+  it('exposes the reference context contract inside a provider', async () => {
+    const c = core(apiServer());
+    const p = probe(c);
+    const r = render(h(c.AmdGpuDataProvider, null, h(p.Probe)));
+    await r.settle();
+    const ctx = p.last();
+    ['deviceConfigs', 'pluginInstalled', 'gpuNodes', 'gpuPods', 'pluginPods', 'crdAvailable', 'loading', 'error'].forEach((k) =>
+      expect(ctx).toHaveProperty(k)
+    );
+    expect(typeof ctx.refresh).toBe('function');
+  });
+});
+
+describe('AmdGpuDataProvider — requests', () => {
+  it('issues exactly one CRD request on mount while the pod watch is in flight', async () => {
+    const request = apiServer();
+    const c = core(request);
+    const p = probe(c);
+    const r = render(h(c.AmdGpuDataProvider, null, h(p.Probe)));
+    await r.settle();
+    expect(request).toHaveBeenCalledTimes(1);
+    expect(request.mock.calls[0][0]).toBe(DEVICE_CONFIG_LIST_PATH);
+    expect(p.last().crdAvailable).toBe(true);
+    expect(p.last().deviceConfigs).toHaveLength(1);
+  });
+
+  it('asks Headlamp for nodes and for pods in all namespaces', () => {
+    const c = core(apiServer());
+    const p = probe(c);
+    render(h(c.AmdGpuDataProvider, null, h(p.Probe)));
+    expect(lib.lists.calls.Node[0]).toBeNull();
+    expect(lib.lists.calls.Pod[0]).toEqual({ namespace: '' });
+  });
+
+  it('a second provider mounted at the same time adds no request', async () => {
+    const request = apiServer();
+    const c = core(request);
+    const a = probe(c);
+    const b = probe(c);
+    const r = render(h('div', null, h(c.AmdGpuDataProvider, null, h(a.Probe)), h(c.AmdGpuDataProvider, null, h(b.Probe))));
+    await r.settle();
+    expect(crdCalls(request)).toBe(1);
+    expect(a.last().deviceConfigs).toBe(b.last().deviceConfigs);
+  });
+
+  it('a remount within STALE_MS renders the cached data at once with no request', async () => {
+    const request = apiServer();
+    lib.lists.Node = [[makeGpuNode('mi355x-0')], null];
+    lib.lists.Pod = [[makeGpuPod('train-a')], null];
+    const c = core(request);
+    const p1 = probe(c);
+    const r1 = render(h(c.AmdGpuDataProvider, null, h(p1.Probe)));
+    await r1.settle();
+    r1.unmount();
+    expect(crdCalls(request)).toBe(1);
+
+    const p2 = probe(c);
+    const r2 = render(h(c.AmdGpuDataProvider, null, h(p2.Probe)));
+    expect(p2.seen[0].loading).toBe(false);
+    expect(p2.seen[0].deviceConfigs).toHaveLength(1);
+    expect(r2.getByTestId('probe').children[0]).toBe('nodes=1 pods=1');
+    await r2.settle();
+    expect(crdCalls(request)).toBe(1);
+  });
+
+  it('a remount after STALE_MS revalidates once', async () => {
+    vi.useFakeTimers();
+    const request = apiServer();
+    const c = core(request);
+    const p1 = probe(c);
+    const r1 = render(h(c.AmdGpuDataProvider, null, h(p1.Probe)));
+    await r1.settle();
+    r1.unmount();
+    vi.setSystemTime(Date.now() + STALE_MS + 1);
+    const p2 = probe(c);
+    const r2 = render(h(c.AmdGpuDataProvider, null, h(p2.Probe)));
+    await r2.settle();
+    expect(crdCalls(request)).toBe(2);
+  });
+
+  it('refresh() re-fetches the CRD only (the pod list comes from the watch)', async () => {
+    const request = apiServer();
+    lib.lists.Pod = [[makePlainPod('web-0')], null];
+    const c = core(request);
+    const p = probe(c);
+    const r = render(h(c.AmdGpuDataProvider, null, h(p.Probe)));
+    await r.settle();
+    const before = request.mock.calls.length;
+    r.act(() => p.last().refresh());
+    await r.settle();
+    expect(request.mock.calls.length).toBe(before + 1);
+    expect(request.mock.calls[before][0]).toBe(DEVICE_CONFIG_LIST_PATH);
+  });
+
+  it('auto-refresh (settings) revalidates on the poller period', async () => {
+    vi.useFakeTimers();
+    settings.refreshIntervalSec = 15;
+    const request = apiServer();
+    const c = core(request);
+    const p = probe(c);
+    const r = render(h(c.AmdGpuDataProvider, null, h(p.Probe)));
+    await r.settle();
+    expect(crdCalls(request)).toBe(1);
+    await vi.advanceTimersByTimeAsync(15000);
+    await r.settle();
+    expect(crdCalls(request)).toBe(2);
+    r.unmount();
+    await vi.advanceTimersByTimeAsync(60000);
+    expect(crdCalls(request)).toBe(2);
+  });
+});
+
+describe('AmdGpuDataProvider — data', () => {
+  it('classifies the useList nodes and pods', async () => {
+    lib.lists.Node = [[makeGpuNode('mi355x-0'), makeGpuNode('mi355x-1'), makeNode('cpu-0')], null];
+    lib.lists.Pod = [[makeGpuPod('train-a'), makePlainPod('web-0'), makePluginPod('amdgpu-dp-1')], null];
+    const c = core(apiServer());
+    const p = probe(c);
+    const r = render(h(c.AmdGpuDataProvider, null, h(p.Probe)));
+    await r.settle();
+    expect(p.last().gpuNodes.map((n) => n.metadata.name)).toEqual(['mi355x-0', 'mi355x-1']);
+    expect(p.last().gpuPods.map((x) => x.metadata.name)).toEqual(['train-a']);
+    expect(p.last().pluginPods.map((x) => x.metadata.name)).toEqual(['amdgpu-dp-1']);
+    expect(r.getByTestId('probe').children[0]).toBe('nodes=2 pods=1');
+  });
+
+  it('unwraps Headlamp KubeObject wrappers (jsonData)', async () => {
+    lib.lists.Node = [[{ jsonData: makeGpuNode('mi355x-0') }], null];
+    lib.lists.Pod = [[{ jsonData: makeGpuPod('train-a') }], null];
+    const c = core(apiServer());
+    const p = probe(c);
+    const r = render(h(c.AmdGpuDataProvider, null, h(p.Probe)));
+    await r.settle();
+    expect(p.last().gpuNodes[0].metadata.name).toBe('mi355x-0');
+    expect(p.last().gpuPods[0].metadata.name).toBe('train-a');
+  });
+
+  it('stays loading while the lists are in flight, then settles', async () => {
+    const c = core(apiServer());
+    const p = probe(c);
+    const r = render(h(c.AmdGpuDataProvider, null, h(p.Probe)));
+    await r.settle();
+    expect(p.last().loading).toBe(true);
+    lib.lists.Node = [[makeGpuNode('mi355x-0')], null];
+    lib.lists.Pod = [[], null];
+    r.rerender(h(c.AmdGpuDataProvider, null, h(p.Probe)));
+    await r.settle();
+    expect(p.last().loading).toBe(false);
+  });
+
+  it('a watch event on an unrelated pod keeps the GPU pod list identity', async () => {
+    const gpu = makeGpuPod('train-a');
+    lib.lists.Node = [[makeGpuNode('mi355x-0')], null];
+    lib.lists.Pod = [[gpu, makePlainPod('web-0')], null];
+    const c = core(apiServer());
+    const p = probe(c);
+    const r = render(h(c.AmdGpuDataProvider, null, h(p.Probe)));
+    await r.settle();
+    const before = p.last().gpuPods;
+    lib.lists.Pod = [[gpu, makePlainPod('web-0'), makePlainPod('web-1')], null];
+    r.rerender(h(c.AmdGpuDataProvider, null, h(p.Probe)));
+    await r.settle();
+    expect(p.last().gpuPods).toBe(before);
+  });
+
+  it('CRD 404 → crdAvailable false, no error', async () => {
+    const c = core(apiServer({ crd: notFound }));
+    lib.lists.Node = [[], null];
+    lib.lists.Pod = [[], null];
+    const p = probe(c);
+    const r = render(h(c.AmdGpuDataProvider, null, h(p.Probe)));
+    await r.settle();
+    expect(p.last().crdAvailable).toBe(false);
+    expect(p.last().error).toBeNull();
+    expect(p.last().loading).toBe(false);
+  });
+
+  it('a transient CRD failure after a success keeps the last known DeviceConfigs', async () => {
+    let fail = false;
+    const crd = () => (fail ? Promise.reject(Object.assign(new Error('503'), { status: 503 })) : Promise.resolve(kubeList([makeDeviceConfig()])));
+    const c = core(apiServer({ crd }));
+    const p = probe(c);
+    const r = render(h(c.AmdGpuDataProvider, null, h(p.Probe)));
+    await r.settle();
+    fail = true;
+    r.act(() => p.last().refresh());
+    await r.settle();
+    expect(p.last().crdAvailable).toBe(true);
+    expect(p.last().deviceConfigs).toHaveLength(1);
+  });
+});
+
+describe('AmdGpuDataProvider — degraded RBAC', () => {
+  it('pods forbidden: leaves loading, reports the error, finds operator pods by query', async () => {
+    const request = apiServer({ pluginPods: [makePluginPod('amdgpu-dp-1')] });
+    lib.lists.Node = [[makeGpuNode('mi355x-0')], null];
+    lib.lists.Pod = [null, new Error('pods is forbidden')];
+    const c = core(request);
+    const p = probe(c);
+    const r = render(h(c.AmdGpuDataProvider, null, h(p.Probe)));
+    await r.settle();
+    expect(p.last().loading).toBe(false);
+    expect(p.last().error).toContain('pods is forbidden');
+    expect(p.last().pluginPods.map((x) => x.metadata.name)).toEqual(['amdgpu-dp-1']);
+    PLUGIN_POD_QUERIES.forEach((q) => expect(request.mock.calls.map((x) => x[0])).toContain(q));
+  });
+
+  it('nodes forbidden: leaves loading with no GPU nodes and the error', async () => {
+    lib.lists.Node = [null, new Error('nodes is forbidden')];
+    lib.lists.Pod = [[makeGpuPod('train-a')], null];
+    const c = core(apiServer());
+    const p = probe(c);
+    const r = render(h(c.AmdGpuDataProvider, null, h(p.Probe)));
+    await r.settle();
+    expect(p.last().loading).toBe(false);
+    expect(p.last().gpuNodes).toEqual([]);
+    expect(p.last().error).toContain('nodes is forbidden');
+  });
+
+  it('both forbidden: leaves loading and reports both errors', async () => {
+    lib.lists.Node = [null, 'nodes is forbidden'];
+    lib.lists.Pod = [null, 'pods is forbidden'];
+    const c = core(apiServer());
+    const p = probe(c);
+    const r = render(h(c.AmdGpuDataProvider, null, h(p.Probe)));
+    await r.settle();
+    expect(p.last().loading).toBe(false);
+    expect(p.last().error).toContain('nodes is forbidden');
+    expect(p.last().error).toContain('pods is forbidden');
+  });
+});
+
+describe('metrics hooks', () => {
+  function metricsProbe(useHook) {
+    const seen = [];
+    function M() {
+      const m = useHook();
+      seen.push(m);
+      return h('div', null, m.fetching ? 'fetching' : m.fetchError || (m.metrics ? 'gpus=' + m.metrics.gpus.length : 'idle'));
+    }
+    return { M, seen, last: () => seen[seen.length - 1] };
+  }
+
+  it('useGpuMetrics: Prometheus unreachable → the reference error text', async () => {
+    const request = apiServer({ prom: () => Promise.reject(new Error('503')) });
+    const c = core(request);
+    const mp = metricsProbe(() => c.useGpuMetrics(true, false));
+    const r = render(h(mp.M));
+    expect(mp.seen[mp.seen.length - 1].fetching).toBe(true);
+    await r.settle();
+    expect(mp.last().fetching).toBe(false);
+    expect(mp.last().fetchError).toBe(PROMETHEUS_UNREACHABLE);
+    expect(r.text()).toBe(PROMETHEUS_UNREACHABLE);
+  });
+
+  it('useGpuMetrics: exporter reachable → per-GPU metrics and series', async () => {
+    const request = apiServer({ prom: prom() });
+    const c = core(request);
+    const mp = metricsProbe(() => c.useGpuMetrics(true, true));
+    const r = render(h(mp.M));
+    await r.settle();
+    expect(mp.last().fetchError).toBeNull();
+    expect(mp.last().metrics.gpus).toHaveLength(8);
+    expect(mp.last().series.power.n0.length).toBeGreaterThan(1);
+    expect(request.mock.calls.every((x) => x[0].indexOf(BASE0) === 0)).toBe(true);
+  });
+
+  it('useGpuMetrics: refresh() fetches again; discovery is cached', async () => {
+    const request = apiServer({ prom: prom() });
+    const c = core(request);
+    const mp = metricsProbe(() => c.useGpuMetrics(true, false));
+    const r = render(h(mp.M));
+    await r.settle();
+    const n = request.mock.calls.length;
+    const probes = () => request.mock.calls.filter((x) => x[0].indexOf('query=1') >= 0).length;
+    const p0 = probes();
+    r.act(() => mp.last().refresh());
+    await r.settle();
+    expect(request.mock.calls.length).toBeGreaterThan(n);
+    expect(probes()).toBe(p0);
+  });
+
+  it('useNodeGpuMetrics(null) fetches nothing', async () => {
+    const request = apiServer({ prom: prom() });
+    const c = core(request);
+    const mp = metricsProbe(() => c.useNodeGpuMetrics(null, true));
+    const r = render(h(mp.M));
+    await r.settle();
+    expect(request).not.toHaveBeenCalled();
+    expect(r.text()).toBe('idle');
+  });
+
+  it('useNodeGpuMetrics(node) reads one node through a hostname-scoped query', async () => {
+    const request = apiServer({ prom: prom() });
+    const c = core(request);
+    const mp = metricsProbe(() => c.useNodeGpuMetrics('n0', true));
+    const r = render(h(mp.M));
+    await r.settle();
+    expect(mp.last().metrics.gpus).toHaveLength(8);
+    const scoped = request.mock.calls.filter((x) => decodeURIComponent(x[0]).indexOf('hostname="n0"') >= 0);
+    expect(scoped.length).toBeGreaterThan(0);
+  });
+
+  it('switching node while a fetch is in flight drops the old answer', async () => {
+    let release;
+    const gate = new Promise((res) => (release = res));
+    const inner = prom({ data: exporterData(['n0', 'n1']) });
+    const slow = (path) => decodeURIComponent(path).indexOf('hostname="n0"') >= 0;
+    const request = apiServer({ prom: (path) => (slow(path) ? gate.then(() => inner(path)) : inner(path)) });
+    const c = core(request);
+    let node = 'n0';
+    const mp = metricsProbe(() => c.useNodeGpuMetrics(node, true));
+    const r = render(h(mp.M));
+    await r.settle();
+    node = 'n1';
+    r.rerender(h(mp.M));
+    await r.settle();
+    expect(mp.last().metrics.gpus[0].nodeName).toBe('n1');
+    release();
+    await r.settle();
+    expect(mp.last().metrics.gpus.every((g) => g.nodeName === 'n1')).toBe(true);
+  });
+
+  it('useGpuOwners fetches pod attribution only', async () => {
+    const request = apiServer({ prom: prom() });
+    const c = core(request);
+    const mp = metricsProbe(() => c.useGpuOwners());
+    const r = render(h(mp.M));
+    await r.settle();
+    expect(mp.last().fetchError).toBeNull();
+    const qs = request.mock.calls.map((x) => decodeURIComponent(x[0])).filter((q) => q.indexOf('query=') >= 0 && q.indexOf('query=1') < 0);
+    expect(qs.length).toBeGreaterThan(0);
+    qs.forEach((q) => expect(q).toContain('pod!=""'));
+  });
+});

@@ -1,0 +1,261 @@
+/**
+ * IR → CommonComponents renderer (src/view/react.js), executed under the
+ * harness React (tests/js/stubs/react.js) with CommonComponents stand-ins
+ * that render the markup the reference's component tests mock them with
+ * (reference src/components/OverviewPage.test.tsx:8-61). Every spec checks
+ * what the renderer HANDS each CommonComponent (props), not only the text.
+ */
+import React, { render } from './stubs/react.js';
+import * as CC from './stubs/CommonComponents.js';
+import { createRenderer, REQUIRED_COMPONENTS, buttonStyle, matrixCaption, matrixCellColor, sparklinePath } from '../../src/view/react.js';
+import { bar, kv, lines, loader, page, pctbar, row, section, status, table } from '../../src/view/ir.js';
+import { clearViewMemo, matrixBlock, overviewView, slotsBlock } from '../../src/view/pages.js';
+import { makeContext, makeGpuNode, makeGpuPod } from './fixtures.js';
+
+const h = React.createElement;
+
+function setup() {
+  return createRenderer(React, CC);
+}
+
+function only(handle, type) {
+  const all = handle.instances(type);
+  expect(all).toHaveLength(1);
+  return all[0].props;
+}
+
+describe('createRenderer', () => {
+  it('requires React.createElement', () => {
+    expect(() => createRenderer({}, CC)).toThrow('React is required');
+  });
+  it('names every missing CommonComponent', () => {
+    REQUIRED_COMPONENTS.forEach((name) => {
+      const partial = Object.assign({}, CC);
+      delete partial[name];
+      expect(() => createRenderer(React, partial)).toThrow('CommonComponents.' + name + ' is missing');
+    });
+  });
+});
+
+describe('Page', () => {
+  it('renders the title through SectionHeader', () => {
+    const v = setup();
+    const r = render(h(v.Page, { vm: page('AMD GPU — Overview', null, []) }));
+    expect(only(r, CC.SectionHeader).title).toBe('AMD GPU — Overview');
+    expect(r.byTag('h1')).toHaveLength(1);
+  });
+
+  it('renders no header while the page is only a loader', () => {
+    const v = setup();
+    const r = render(h(v.Page, { vm: page(null, null, [loader('Loading AMD GPU data...')]) }));
+    expect(r.instances(CC.SectionHeader)).toHaveLength(0);
+    expect(only(r, CC.Loader).title).toBe('Loading AMD GPU data...');
+    expect(r.getByTestId('loader')).toBeTruthy();
+  });
+
+  it('refresh button carries the aria-label and calls onRefresh on click', () => {
+    const v = setup();
+    const onRefresh = vi.fn();
+    const vm = page('T', { label: 'Refresh', ariaLabel: 'Refresh AMD GPU data', disabled: false }, []);
+    const r = render(h(v.Page, { vm, onRefresh }));
+    const btn = r.getByLabelText('Refresh AMD GPU data');
+    expect(btn.tag).toBe('button');
+    expect(btn.props.disabled).toBe(false);
+    r.click(btn);
+    r.click(btn);
+    expect(onRefresh).toHaveBeenCalledTimes(2);
+  });
+
+  it('disabled refresh button does not fire and uses the not-allowed style', () => {
+    const v = setup();
+    const onRefresh = vi.fn();
+    const vm = page('T', { label: 'Refreshing...', ariaLabel: 'Refresh metrics', disabled: true }, []);
+    const r = render(h(v.Page, { vm, onRefresh }));
+    const btn = r.getByLabelText('Refresh metrics');
+    expect(btn.props.disabled).toBe(true);
+    expect(btn.props.style).toEqual(buttonStyle(true));
+    expect(btn.props.style.cursor).toBe('not-allowed');
+    r.click(btn);
+    expect(onRefresh).not.toHaveBeenCalled();
+  });
+
+  it('maps loader and section items in order', () => {
+    const v = setup();
+    const vm = page('T', null, [section('A', []), loader('wait'), section('B', [])]);
+    const r = render(h(v.Page, { vm }));
+    expect(r.instances(CC.SectionBox).map((i) => i.props.title)).toEqual(['A', 'B']);
+    expect(r.text()).toBe('TAwaitB');
+  });
+});
+
+describe('blocks', () => {
+  it('kv → NameValueTable rows (name + rendered value)', () => {
+    const v = setup();
+    const s = section('Cluster', [kv([row('GPU Nodes', '2'), row('State', status('success', 'Ready'))])]);
+    const r = render(h(v.Section, { s }));
+    expect(only(r, CC.SectionBox).title).toBe('Cluster');
+    const rows = only(r, CC.NameValueTable).rows;
+    expect(rows.map((x) => x.name)).toEqual(['GPU Nodes', 'State']);
+    expect(r.byTag('dt').map((n) => n.children[0])).toEqual(['GPU Nodes', 'State']);
+    expect(only(r, CC.StatusLabel).status).toBe('success');
+    expect(r.getByText('Ready').props['data-status']).toBe('success');
+  });
+
+  it('table → SimpleTable with one column per label and getters reading cell i', () => {
+    const v = setup();
+    const rows = [['n0', '8'], ['n1', status('warning', '4')]];
+    const r = render(h(v.Section, { s: section('Nodes', [table(['Node', 'GPUs'], rows)]) }));
+    const p = only(r, CC.SimpleTable);
+    expect(p.columns.map((c) => c.label)).toEqual(['Node', 'GPUs']);
+    expect(p.data).toBe(rows);
+    expect(p.columns[0].getter(rows[0]).props.v).toBe('n0');
+    expect(p.columns[1].getter(rows[1]).props.v).toEqual(status('warning', '4'));
+    expect(r.byTag('tr')).toHaveLength(3);
+    expect(r.byTag('th').map((n) => n.children[0])).toEqual(['Node', 'GPUs']);
+  });
+
+  it('pctbar → PercentageBar with data and total, under its label', () => {
+    const v = setup();
+    const data = [{ name: 'Allocated', value: 3, fill: '#f00' }, { name: 'Free', value: 5, fill: '#ccc' }];
+    const r = render(h(v.Section, { s: section('Alloc', [pctbar('GPU allocation', data, 8)]) }));
+    const p = only(r, CC.PercentageBar);
+    expect(p.data).toBe(data);
+    expect(p.total).toBe(8);
+    expect(r.getByText('GPU allocation')).toBeTruthy();
+    expect(r.getByTestId('percentage-bar').props['data-total']).toBe(8);
+  });
+
+  it('bar cell → inline track with its fill width and text', () => {
+    const v = setup();
+    const r = render(h(v.Value, { v: bar(3, 8, 38, '#4caf50', '3/8 (38%)') }));
+    const fill = r.queryAll((n) => n.props['data-pct'] !== undefined);
+    expect(fill).toHaveLength(1);
+    expect(fill[0].props.style.width).toBe('38%');
+    expect(fill[0].props.style.backgroundColor).toBe('#4caf50');
+    expect(r.text()).toBe('3/8 (38%)');
+  });
+
+  it('bar cell without a percentage draws only the text', () => {
+    const v = setup();
+    const r = render(h(v.Value, { v: bar(3, null, null, '#000', '3 GPUs') }));
+    expect(r.queryAll((n) => n.props['data-pct'] !== undefined)).toHaveLength(0);
+    expect(r.text()).toBe('3 GPUs');
+  });
+
+  it('lines cell → one div per line with a bold label', () => {
+    const v = setup();
+    const r = render(h(v.Value, { v: lines([{ label: 'trainer', text: '2 GPUs' }, { label: '', text: 'plain' }]) }));
+    expect(r.byTag('strong').map((n) => n.children[0])).toEqual(['trainer']);
+    expect(r.text()).toBe('trainer: 2 GPUsplain');
+  });
+
+  it('null, strings and numbers render as plain text; unknown cells as nothing', () => {
+    const v = setup();
+    expect(render(h(v.Value, { v: null })).text()).toBe('');
+    expect(render(h(v.Value, { v: 7 })).text()).toBe('7');
+    expect(render(h(v.Value, { v: 'x' })).text()).toBe('x');
+    expect(render(h(v.Value, { v: { t: 'nope' } })).text()).toBe('');
+  });
+
+  it('unknown block types render nothing', () => {
+    const v = setup();
+    const r = render(h(v.Section, { s: section('S', [{ t: 'mystery' }]) }));
+    expect(r.text()).toBe('S');
+  });
+
+  it('slots → one tile per GPU, pod owners and free slots labelled', () => {
+    const v = setup();
+    const node = makeGpuNode('mi355x-0');
+    const pods = [makeGpuPod('train-a', { gpus: 2 }), makeGpuPod('train-b', { gpus: 1 })];
+    const b = slotsBlock(node, pods, null);
+    const r = render(h(v.Block, { b }));
+    const tiles = r.queryAll((n) => n.props['data-slot'] !== undefined);
+    expect(tiles).toHaveLength(8);
+    expect(tiles.filter((t) => t.props.title === 'free')).toHaveLength(5);
+    expect(r.text()).toContain('inferred from pod order');
+    expect(tiles[0].props.title).toBe('ml/train-a');
+  });
+
+  it('matrix → 8×8 table, self cells dashed, caption says the topology is assumed', () => {
+    const v = setup();
+    const b = matrixBlock(8, null, null);
+    const r = render(h(v.Block, { b }));
+    expect(r.byTag('tbody')[0].children).toHaveLength(8);
+    const selfCells = r.byTag('td').filter((n) => n.children[0] === '—');
+    expect(selfCells).toHaveLength(8);
+    expect(r.text()).toContain('assumed MI355X full mesh');
+    expect(matrixCaption(b)).toContain('assumed');
+    expect(matrixCellColor({ kind: 'self' })).toBe('transparent');
+  });
+
+  it('series → SimpleTable of per-node sparklines', () => {
+    const v = setup();
+    const pts = [[0, 100], [30, 300], [60, 200]];
+    const b = { t: 'series', power: { n0: pts, n1: [] }, vram: { n0: pts } };
+    const r = render(h(v.Block, { b }));
+    const p = only(r, CC.SimpleTable);
+    expect(p.columns.map((c) => c.label)).toEqual(['Node', 'Power (W)', 'HBM in use']);
+    expect(p.data).toEqual(['n0', 'n1']);
+    const svgs = r.byTag('svg');
+    expect(svgs).toHaveLength(2); // n1 has no points for either series
+    expect(svgs[0].props['aria-label']).toBe('n0 power');
+    expect(r.byTag('path')[0].props.d).toBe(sparklinePath(pts, 240, 36));
+  });
+
+  it('sparklinePath needs two points and spans the box', () => {
+    expect(sparklinePath([[0, 1]], 10, 10)).toBeNull();
+    expect(sparklinePath([[0, 0], [10, 10]], 100, 50)).toBe('M0.0,50.0 L100.0,0.0');
+  });
+});
+
+describe('Section memo', () => {
+  it('skips re-rendering an unchanged section object', () => {
+    const v = setup();
+    const s = section('Stable', [kv([row('a', '1')])]);
+    const r = render(h(v.Section, { s }));
+    const inst = r.instances(v.Section)[0];
+    expect(inst.renders).toBe(1);
+    r.rerender(h(v.Section, { s }));
+    r.rerender(h(v.Section, { s }));
+    expect(inst.renders).toBe(1);
+    expect(inst.skips).toBe(2);
+    expect(only(r, CC.NameValueTable).rows[0].name).toBe('a');
+  });
+
+  it('re-renders when the section object changes', () => {
+    const v = setup();
+    const r = render(h(v.Section, { s: section('S', [kv([row('a', '1')])]) }));
+    r.rerender(h(v.Section, { s: section('S', [kv([row('a', '2')])]) }));
+    expect(r.instances(v.Section)[0].renders).toBe(2);
+    expect(r.text()).toBe('Sa2');
+  });
+
+  it('a page refresh with one changed section re-renders only that section', () => {
+    const v = setup();
+    const a = section('A', []);
+    const b1 = section('B', [kv([row('x', '1')])]);
+    const b2 = section('B', [kv([row('x', '2')])]);
+    const r = render(h(v.Page, { vm: page('T', null, [a, b1]) }));
+    r.rerender(h(v.Page, { vm: page('T', null, [a, b2]) }));
+    const counts = r.instances(v.Section).map((i) => [i.props.s.title, i.renders]);
+    expect(counts).toEqual([['A', 1], ['B', 2]]);
+  });
+});
+
+describe('a real view-model end to end', () => {
+  beforeEach(() => clearViewMemo());
+
+  it('Overview of a 2-node MI355X cluster renders every section through CommonComponents', () => {
+    const v = setup();
+    const nodes = [makeGpuNode('mi355x-0'), makeGpuNode('mi355x-1')];
+    const pods = [makeGpuPod('train-a', { gpus: 4 }), makeGpuPod('train-b', { gpus: 2, node: 'mi355x-1' })];
+    const vm = overviewView(makeContext({ nodes, pods }));
+    const r = render(h(v.Page, { vm, onRefresh: () => {} }));
+    const titles = r.instances(CC.SectionBox).map((i) => i.props.title);
+    expect(titles.length).toBeGreaterThan(2);
+    expect(titles).toEqual(vm.items.filter((it) => it.t === 'section').map((it) => it.title));
+    expect(r.instances(CC.PercentageBar).length).toBeGreaterThan(0);
+    expect(r.html()).toContain('mi355x-1');
+    expect(r.getByLabelText(vm.refresh.ariaLabel).tag).toBe('button');
+  });
+});

@@ -1,0 +1,671 @@
+/**
+ * A small React 18 stand-in for the Node-12 test harness (no npm registry
+ * here, so the real React cannot be installed). It implements the subset of
+ * React the plugin's shipped code uses — createElement, Fragment, memo,
+ * createContext, useState / useReducer / useEffect / useLayoutEffect /
+ * useMemo / useCallback / useRef / useContext / useSyncExternalStore — and a
+ * reconciling renderer:
+ *
+ *   * component instances keep their hook state across renders (matched by
+ *     key, else position, and type, like React);
+ *   * `memo` components skip rendering when their props are shallow-equal
+ *     and nothing below them is dirty (render counts are observable);
+ *   * effects run after the render pass, children before parents; cleanups
+ *     run before the next effect and on unmount;
+ *   * state updates outside `act` are batched on a microtask.
+ *
+ * The rendered host tree ({tag, props, children}) can be queried
+ * testing-library style (getByText, getByLabelText, getByTestId, …),
+ * clicked, and serialised to HTML. Only what the plugin needs is modelled:
+ * no refs to host nodes, no portals, no suspense, no concurrent mode.
+ */
+
+const ELEMENT = Symbol.for('stub.react.element');
+const MEMO = Symbol.for('stub.react.memo');
+const PROVIDER = Symbol.for('stub.react.provider');
+const LIST = Symbol.for('stub.react.list');
+
+export const Fragment = Symbol.for('stub.react.fragment');
+
+export function createElement(type, props) {
+  const p = {};
+  let key = null;
+  if (props) {
+    for (const k in props) {
+      if (k === 'key') key = props.key === undefined || props.key === null ? null : String(props.key);
+      else if (k !== 'ref') p[k] = props[k];
+    }
+  }
+  if (arguments.length === 3) p.children = arguments[2];
+  else if (arguments.length > 3) p.children = Array.prototype.slice.call(arguments, 2);
+  if (type === undefined || type === null) throw new Error('createElement: element type is ' + type);
+  return { $$typeof: ELEMENT, type: type, key: key, props: p };
+}
+
+export function isValidElement(v) {
+  return !!v && v.$$typeof === ELEMENT;
+}
+
+function shallowEqual(a, b) {
+  if (a === b) return true;
+  const ka = Object.keys(a);
+  const kb = Object.keys(b);
+  if (ka.length !== kb.length) return false;
+  for (let i = 0; i < ka.length; i++) if (!Object.is(a[ka[i]], b[ka[i]])) return false;
+  return true;
+}
+
+export function memo(type, compare) {
+  return { $$typeof: MEMO, type: type, compare: compare || shallowEqual, displayName: 'Memo(' + (type.displayName || type.name) + ')' };
+}
+
+export function createContext(defaultValue) {
+  const ctx = { _default: defaultValue };
+  ctx.Provider = { $$typeof: PROVIDER, context: ctx };
+  return ctx;
+}
+
+// ---------------------------------------------------------------------------
+// Hooks
+// ---------------------------------------------------------------------------
+
+let current = null; // instance being rendered
+let hookIndex = 0;
+let currentRoot = null;
+const ctxStack = [];
+
+function hookSlot(init) {
+  if (!current) throw new Error('Invalid hook call: hooks can only be called inside a function component');
+  const hooks = current.hooks;
+  if (hookIndex >= hooks.length) {
+    if (current.renders > 1) throw new Error('Rendered more hooks than during the previous render');
+    hooks.push(init());
+  }
+  return hooks[hookIndex++];
+}
+
+function depsChanged(prev, next) {
+  if (!prev || !next) return true;
+  if (prev.length !== next.length) return true;
+  for (let i = 0; i < prev.length; i++) if (!Object.is(prev[i], next[i])) return true;
+  return false;
+}
+
+export function useReducer(reducer, initialArg, init) {
+  const inst = current;
+  const slot = hookSlot(function () {
+    const s = { state: init ? init(initialArg) : initialArg, dispatch: null };
+    s.dispatch = function (action) {
+      if (inst.unmounted) return;
+      const next = s.reducer(s.state, action);
+      if (Object.is(next, s.state)) return;
+      s.state = next;
+      markDirty(inst);
+    };
+    return s;
+  });
+  slot.reducer = reducer;
+  return [slot.state, slot.dispatch];
+}
+
+function basicReducer(s, a) {
+  return typeof a === 'function' ? a(s) : a;
+}
+
+export function useState(init) {
+  return useReducer(basicReducer, init, typeof init === 'function' ? function (f) { return f(); } : undefined);
+}
+
+function effectHook(fn, deps, layout) {
+  const inst = current;
+  const slot = hookSlot(function () { return { deps: undefined, cleanup: null, first: true }; });
+  if (slot.first || deps === undefined || depsChanged(slot.deps, deps)) {
+    slot.first = false;
+    slot.deps = deps;
+    inst.root.pendingEffects.push({ inst: inst, slot: slot, fn: fn, depth: inst.depth, layout: layout });
+  }
+}
+
+export function useEffect(fn, deps) {
+  effectHook(fn, deps, false);
+}
+
+export function useLayoutEffect(fn, deps) {
+  effectHook(fn, deps, true);
+}
+
+export function useMemo(fn, deps) {
+  const slot = hookSlot(function () { return { deps: undefined, value: undefined, first: true }; });
+  if (slot.first || depsChanged(slot.deps, deps)) {
+    slot.first = false;
+    slot.deps = deps;
+    slot.value = fn();
+  }
+  return slot.value;
+}
+
+export function useCallback(fn, deps) {
+  return useMemo(function () { return fn; }, deps);
+}
+
+export function useRef(v) {
+  return hookSlot(function () { return { current: v }; });
+}
+
+function readContext(ctx) {
+  for (let i = ctxStack.length - 1; i >= 0; i--) if (ctxStack[i].context === ctx) return ctxStack[i].value;
+  return ctx._default;
+}
+
+export function useContext(ctx) {
+  if (!current) throw new Error('Invalid hook call: useContext outside a component');
+  const v = readContext(ctx);
+  current.ctxReads.set(ctx, v);
+  return v;
+}
+
+export function useSyncExternalStore(subscribe, getSnapshot) {
+  const inst = current;
+  const slot = hookSlot(function () { return { subscribe: null, unsubscribe: null, value: undefined }; });
+  const value = getSnapshot();
+  slot.value = value;
+  slot.getSnapshot = getSnapshot;
+  if (slot.subscribe !== subscribe) {
+    slot.subscribe = subscribe;
+    inst.root.pendingEffects.push({
+      inst: inst,
+      slot: slot,
+      depth: inst.depth,
+      layout: true,
+      fn: function () {
+        if (slot.unsubscribe) slot.unsubscribe();
+        const check = function () {
+          if (!Object.is(slot.getSnapshot(), slot.value)) markDirty(inst);
+        };
+        slot.unsubscribe = subscribe(check);
+        check(); // the store may have changed between render and subscribe
+        return function () {
+          if (slot.unsubscribe) slot.unsubscribe();
+          slot.unsubscribe = null;
+        };
+      },
+    });
+  }
+  return value;
+}
+
+const React = {
+  createElement: createElement,
+  isValidElement: isValidElement,
+  Fragment: Fragment,
+  memo: memo,
+  createContext: createContext,
+  useState: useState,
+  useReducer: useReducer,
+  useEffect: useEffect,
+  useLayoutEffect: useLayoutEffect,
+  useMemo: useMemo,
+  useCallback: useCallback,
+  useRef: useRef,
+  useContext: useContext,
+  useSyncExternalStore: useSyncExternalStore,
+  version: '18.3.1-stub',
+};
+export default React;
+
+// ---------------------------------------------------------------------------
+// Renderer
+// ---------------------------------------------------------------------------
+
+function typeName(t) {
+  if (typeof t === 'string') return t;
+  if (t === Fragment) return 'Fragment';
+  if (t === LIST) return 'List';
+  if (t && t.$$typeof === MEMO) return t.displayName;
+  if (t && t.$$typeof === PROVIDER) return 'Context.Provider';
+  return (t && (t.displayName || t.name)) || 'Anonymous';
+}
+
+function newInstance(root, parent, type, key) {
+  return {
+    root: root,
+    parent: parent,
+    depth: parent ? parent.depth + 1 : 0,
+    type: type,
+    key: key,
+    props: null,
+    hooks: [],
+    kids: [],
+    out: [],
+    dirty: true,
+    renders: 0,
+    skips: 0,
+    ctxReads: new Map(),
+    unmounted: false,
+    text: null,
+  };
+}
+
+function markDirty(inst) {
+  inst.dirty = true;
+  inst.root.schedule();
+}
+
+/**
+ * True when `inst` or anything below it has pending state, or (with
+ * `checkCtx`, used at memo boundaries) read a context value that has
+ * changed since. Providers inside the subtree push their current value so
+ * descendants compare against what they would read now.
+ */
+function subtreeNeedsRender(inst, checkCtx) {
+  if (inst.dirty) return true;
+  if (checkCtx) {
+    let changed = false;
+    inst.ctxReads.forEach(function (v, ctx) {
+      if (!Object.is(readContext(ctx), v)) changed = true;
+    });
+    if (changed) return true;
+  }
+  const provider = inst.type && inst.type.$$typeof === PROVIDER;
+  if (provider) ctxStack.push({ context: inst.type.context, value: inst.props.value });
+  try {
+    for (let i = 0; i < inst.kids.length; i++) if (subtreeNeedsRender(inst.kids[i], checkCtx)) return true;
+  } finally {
+    if (provider) ctxStack.pop();
+  }
+  return false;
+}
+
+function childList(children) {
+  if (children === undefined) return [];
+  return Array.isArray(children) ? children : [children];
+}
+
+function identity(item, index) {
+  if (isValidElement(item) && item.key !== null) return 'k:' + item.key;
+  return 'i:' + index;
+}
+
+function sameType(inst, item) {
+  if (typeof item === 'string' || typeof item === 'number') return inst.type === '#text';
+  if (Array.isArray(item)) return inst.type === LIST;
+  return inst.type === item.type;
+}
+
+function reconcileChildren(root, parent, children) {
+  const list = childList(children);
+  const old = new Map();
+  for (let i = 0; i < parent.kids.length; i++) old.set(parent.kids[i].ident, parent.kids[i]);
+  const kids = [];
+  const seen = {};
+  for (let i = 0; i < list.length; i++) {
+    const item = list[i];
+    if (item === null || item === undefined || item === false || item === true || item === '') continue;
+    const id = identity(item, i);
+    if (seen[id]) throw new Error('Duplicate key "' + id.slice(2) + '" among children of ' + typeName(parent.type));
+    seen[id] = true;
+    let inst = old.get(id);
+    if (inst && !sameType(inst, item)) inst = null;
+    if (inst) old.delete(id);
+    if (typeof item === 'string' || typeof item === 'number') {
+      inst = inst || newInstance(root, parent, '#text', null);
+      inst.text = String(item);
+      inst.out = [inst.text];
+      inst.dirty = false;
+    } else if (Array.isArray(item)) {
+      inst = inst || newInstance(root, parent, LIST, null);
+      inst.props = { children: item };
+      renderInstance(inst);
+    } else if (isValidElement(item)) {
+      const fresh = !inst;
+      inst = inst || newInstance(root, parent, item.type, item.key);
+      const prevProps = inst.props;
+      inst.props = item.props;
+      renderInstance(inst, fresh ? null : prevProps);
+    } else {
+      throw new Error('Objects are not valid as a React child (found: ' + Object.keys(item).join(', ') + ')');
+    }
+    inst.ident = id;
+    kids.push(inst);
+  }
+  old.forEach(function (inst) { unmount(inst); });
+  parent.kids = kids;
+  const out = [];
+  for (let i = 0; i < kids.length; i++) for (let j = 0; j < kids[i].out.length; j++) out.push(kids[i].out[j]);
+  return out;
+}
+
+function hostProps(props) {
+  const p = {};
+  for (const k in props) if (k !== 'children') p[k] = props[k];
+  return p;
+}
+
+function renderInstance(inst, prevProps) {
+  const t = inst.type;
+  const root = inst.root;
+  if (typeof t === 'string') {
+    inst.renders++;
+    const children = reconcileChildren(root, inst, inst.props.children);
+    inst.out = [{ tag: t, props: hostProps(inst.props), children: children, instance: inst }];
+  } else if (t === Fragment || t === LIST) {
+    inst.out = reconcileChildren(root, inst, inst.props.children);
+  } else if (t && t.$$typeof === PROVIDER) {
+    ctxStack.push({ context: t.context, value: inst.props.value });
+    try {
+      inst.out = reconcileChildren(root, inst, inst.props.children);
+    } finally {
+      ctxStack.pop();
+    }
+  } else if (t && t.$$typeof === MEMO) {
+    if (prevProps && !inst.dirty && t.compare(prevProps, inst.props) && !subtreeNeedsRender(inst, true)) {
+      inst.skips++;
+      return;
+    }
+    inst.renders++;
+    inst.out = reconcileChildren(root, inst, createElement(t.type, inst.props));
+  } else if (typeof t === 'function') {
+    const prev = current;
+    const prevIdx = hookIndex;
+    current = inst;
+    hookIndex = 0;
+    inst.renders++;
+    inst.ctxReads = new Map();
+    let result;
+    try {
+      result = t(inst.props);
+    } finally {
+      current = prev;
+      hookIndex = prevIdx;
+    }
+    if (result === undefined) throw new Error(typeName(t) + ' returned undefined (return null to render nothing)');
+    inst.out = reconcileChildren(root, inst, result);
+  } else {
+    throw new Error('Unsupported element type: ' + String(t));
+  }
+  inst.dirty = false;
+}
+
+function unmount(inst) {
+  if (inst.unmounted) return;
+  inst.unmounted = true;
+  for (let i = 0; i < inst.kids.length; i++) unmount(inst.kids[i]);
+  for (let i = 0; i < inst.hooks.length; i++) {
+    const hk = inst.hooks[i];
+    if (hk && typeof hk.cleanup === 'function') {
+      const c = hk.cleanup;
+      hk.cleanup = null;
+      c();
+    }
+  }
+  inst.root.unmounts++;
+}
+
+function textOf(node) {
+  if (typeof node === 'string') return node;
+  let s = '';
+  for (let i = 0; i < node.children.length; i++) s += textOf(node.children[i]);
+  return s;
+}
+
+const VOID = { br: true, input: true, hr: true, img: true };
+
+function esc(s) {
+  return String(s).replace(/&/g, '&amp;').replace(/</g, '&lt;').replace(/>/g, '&gt;').replace(/"/g, '&quot;');
+}
+
+function attrs(props) {
+  let s = '';
+  const keys = Object.keys(props).sort();
+  for (let i = 0; i < keys.length; i++) {
+    const k = keys[i];
+    const v = props[k];
+    if (v === null || v === undefined || v === false || typeof v === 'function' || k === 'style') continue;
+    s += ' ' + k + (v === true ? '' : '="' + esc(v) + '"');
+  }
+  return s;
+}
+
+function htmlOf(node) {
+  if (typeof node === 'string') return esc(node);
+  const inner = node.children.map(htmlOf).join('');
+  if (VOID[node.tag]) return '<' + node.tag + attrs(node.props) + '>';
+  return '<' + node.tag + attrs(node.props) + '>' + inner + '</' + node.tag + '>';
+}
+
+function walk(nodes, fn) {
+  for (let i = 0; i < nodes.length; i++) {
+    const n = nodes[i];
+    if (typeof n === 'string') continue;
+    fn(n);
+    walk(n.children, fn);
+  }
+}
+
+function walkInstances(inst, fn) {
+  fn(inst);
+  for (let i = 0; i < inst.kids.length; i++) walkInstances(inst.kids[i], fn);
+}
+
+function matches(text, m) {
+  const t = text.replace(/\s+/g, ' ').trim();
+  return m instanceof RegExp ? m.test(t) : t === m;
+}
+
+function flushMicrotasks() {
+  return new Promise(function (r) { setImmediate(r); });
+}
+
+/**
+ * Mount `element` and return a handle. All rendering is synchronous; state
+ * updates from promises are flushed on a microtask or by `settle()`.
+ */
+export function render(element) {
+  const root = {
+    element: element,
+    top: null,
+    pendingEffects: [],
+    scheduled: false,
+    batching: 0,
+    unmounts: 0,
+    commits: 0,
+    error: null,
+  };
+  root.top = newInstance(root, null, Fragment, null);
+
+  root.schedule = function () {
+    if (root.batching > 0 || root.scheduled || root.top.unmounted) return;
+    root.scheduled = true;
+    Promise.resolve().then(function () {
+      root.scheduled = false;
+      try {
+        flush();
+      } catch (e) {
+        root.error = e;
+      }
+    });
+  };
+
+  function runEffects() {
+    const list = root.pendingEffects;
+    root.pendingEffects = [];
+    // Children's effects run before their parents' (React commit order);
+    // layout effects (and store subscriptions) before passive ones.
+    list.sort(function (a, b) { return (b.layout - a.layout) || (b.depth - a.depth); });
+    for (let i = 0; i < list.length; i++) {
+      const e = list[i];
+      if (e.inst.unmounted) continue;
+      if (typeof e.slot.cleanup === 'function') e.slot.cleanup();
+      const r = e.fn();
+      e.slot.cleanup = typeof r === 'function' ? r : null;
+    }
+  }
+
+  function pass() {
+    const prev = currentRoot;
+    currentRoot = root;
+    try {
+      root.top.props = { children: root.element };
+      renderInstance(root.top);
+      root.commits++;
+      runEffects();
+    } finally {
+      currentRoot = prev;
+    }
+  }
+
+  function flush() {
+    if (root.top.unmounted) return;
+    for (let i = 0; i < 100; i++) {
+      if (!subtreeNeedsRender(root.top, false) && root.pendingEffects.length === 0) return;
+      pass();
+    }
+    throw new Error('Too many re-renders (update loop?)');
+  }
+
+  root.batching++;
+  try {
+    pass();
+  } finally {
+    root.batching--;
+  }
+  flush();
+
+  const handle = {
+    /** Synchronously apply pending state updates. */
+    flush: function () {
+      if (root.error) {
+        const e = root.error;
+        root.error = null;
+        throw e;
+      }
+      flush();
+      return handle;
+    },
+    /** Run `fn` with updates batched, then flush (awaits a returned promise). */
+    act: function (fn) {
+      root.batching++;
+      let r;
+      try {
+        r = fn();
+      } catch (e) {
+        root.batching--;
+        throw e;
+      }
+      if (r && typeof r.then === 'function') {
+        return r.then(
+          function (v) { root.batching--; flush(); return v; },
+          function (e) { root.batching--; throw e; }
+        );
+      }
+      root.batching--;
+      flush();
+      return r;
+    },
+    /** Let pending promises (requests, timers at 0) run and flush, until quiet. */
+    settle: async function (rounds) {
+      const n = rounds || 20;
+      for (let i = 0; i < n; i++) {
+        await flushMicrotasks();
+        handle.flush();
+      }
+      return handle;
+    },
+    rerender: function (el) {
+      root.element = el;
+      root.batching++;
+      try {
+        pass();
+      } finally {
+        root.batching--;
+      }
+      flush();
+      return handle;
+    },
+    unmount: function () {
+      unmount(root.top);
+    },
+    nodes: function () { return root.top.out; },
+    html: function () { return root.top.out.map(htmlOf).join(''); },
+    text: function () { return root.top.out.map(textOf).join(''); },
+    stats: function () { return { commits: root.commits, unmounts: root.unmounts }; },
+    /** Host nodes (deepest first match semantics like testing-library). */
+    queryAll: function (pred) {
+      const out = [];
+      walk(root.top.out, function (n) { if (pred(n)) out.push(n); });
+      return out;
+    },
+    getAllByText: function (m) {
+      const hits = handle.queryAll(function (n) {
+        if (!matches(textOf(n), m)) return false;
+        // deepest: no host child matches as well
+        for (let i = 0; i < n.children.length; i++) {
+          const c = n.children[i];
+          if (typeof c !== 'string' && matches(textOf(c), m)) return false;
+        }
+        return true;
+      });
+      if (hits.length === 0) throw new Error('Unable to find an element with the text: ' + String(m));
+      return hits;
+    },
+    getByText: function (m) {
+      const hits = handle.getAllByText(m);
+      if (hits.length > 1) throw new Error('Found multiple elements with the text: ' + String(m));
+      return hits[0];
+    },
+    queryByText: function (m) {
+      try {
+        return handle.getByText(m);
+      } catch (e) {
+        return null;
+      }
+    },
+    getByLabelText: function (label) {
+      const hits = handle.queryAll(function (n) { return n.props['aria-label'] !== undefined && matches(String(n.props['aria-label']), label); });
+      if (hits.length !== 1) throw new Error((hits.length ? 'Found multiple' : 'Unable to find') + ' elements labelled ' + String(label));
+      return hits[0];
+    },
+    getAllByTestId: function (id) {
+      const hits = handle.queryAll(function (n) { return n.props['data-testid'] === id; });
+      if (hits.length === 0) throw new Error('Unable to find data-testid=' + id);
+      return hits;
+    },
+    getByTestId: function (id) {
+      const hits = handle.getAllByTestId(id);
+      if (hits.length > 1) throw new Error('Found multiple data-testid=' + id);
+      return hits[0];
+    },
+    byTag: function (tag) {
+      return handle.queryAll(function (n) { return n.tag === tag; });
+    },
+    /** Component instances of `type` (function, memo or host tag). */
+    instances: function (type) {
+      const out = [];
+      walkInstances(root.top, function (i) { if (i.type === type && !i.unmounted) out.push(i); });
+      return out;
+    },
+    click: function (node) {
+      if (node.props.disabled) return handle;
+      handle.act(function () {
+        if (typeof node.props.onClick === 'function') node.props.onClick({ type: 'click', target: node, preventDefault: function () {} });
+      });
+      return handle;
+    },
+    change: function (node, value) {
+      handle.act(function () {
+        if (typeof node.props.onChange === 'function') node.props.onChange({ type: 'change', target: { value: value } });
+      });
+      return handle;
+    },
+    blur: function (node, value) {
+      handle.act(function () {
+        const v = value === undefined ? node.props.value !== undefined ? node.props.value : node.props.defaultValue : value;
+        if (typeof node.props.onBlur === 'function') node.props.onBlur({ type: 'blur', target: { value: v } });
+      });
+      return handle;
+    },
+  };
+  return handle;
+}
+
+export { textOf, htmlOf };

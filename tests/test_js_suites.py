@@ -19,10 +19,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 NODE = shutil.which("node") or shutil.which("nodejs")
 SPECS = sorted(os.path.relpath(p, ROOT) for p in glob.glob(os.path.join(ROOT, "tests", "js", "*.test.js")))
 RUNNER = os.path.join("tools", "minitest.js")
+# Resolves 'react' / '@kinvolk/headlamp-plugin/lib' to the harness stand-ins
+# and loads the TypeScript entry shims, so the specs import src/index.tsx and
+# src/components/*.tsx exactly as Headlamp bundles them.
+LOADER = ["--no-warnings", "--experimental-loader", "./tools/plugin-loader.js"]
 
 
 def _node(args, timeout=120):
-    return subprocess.run([NODE, RUNNER] + args, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
+    return subprocess.run([NODE] + LOADER + [RUNNER] + args, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
 
 
 def _list_ids():
@@ -61,6 +65,14 @@ def js_results():
 def test_node_runtime_present():
     assert NODE, "node is required to run the plugin's JS specs"
     assert len(IDS) >= 150, f"expected the full JS suite, collected {len(IDS)}"
+
+
+def test_react_layer_specs_collected():
+    """The executed React layer (renderer, provider, shipped entry) has its own specs."""
+    files = {i.split("::")[0] for i in IDS}
+    for f in ("tests/js/react.test.js", "tests/js/provider.test.js", "tests/js/plugin.test.js"):
+        assert f in files, f
+    assert sum(1 for i in IDS if i.split("::")[0] in files) >= 30
 
 
 @pytest.mark.parametrize("spec_id", IDS)

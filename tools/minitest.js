@@ -369,12 +369,13 @@ global.describe = describe;
 global.it = it;
 global.test = it;
 global.expect = expect;
-global.beforeEach = function (f) { if (suiteStack.length) beforeEach(f); else rootHooks.be.push(f); };
-global.afterEach = function (f) { if (suiteStack.length) afterEach(f); else rootHooks.ae.push(f); };
+global.beforeEach = beforeEach;
+global.afterEach = afterEach;
 global.vi = vi;
-const rootHooks = { be: [], ae: [] };
-suiteStack.push({ name: '', beforeEach: rootHooks.be, afterEach: rootHooks.ae });
-// The root suite's name must not appear in ids.
+// Each file gets its own unnamed root suite (main() swaps it in before the
+// file is imported), so file-level hooks apply to that file's tests only, as
+// in vitest. The root suite's name must not appear in ids.
+suiteStack.push({ name: '', beforeEach: [], afterEach: [] });
 const origIt = it;
 void origIt;
 
@@ -441,6 +442,7 @@ async function main() {
   for (let i = 0; i < files.length; i++) {
     const abs = path.resolve(files[i]);
     currentFile = path.relative(root, abs);
+    suiteStack[0] = { name: '', beforeEach: [], afterEach: [] };
     await import(pathToFileURL(abs).href);
   }
   let selected = tests;

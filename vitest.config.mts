@@ -1,16 +1,26 @@
+import path from 'path';
 import { defineConfig } from 'vitest/config';
 
-// Two spec families share one runner:
-//  - src/**/*.test.tsx: React bindings and renderers (jsdom, CommonComponents mocked);
-//  - tests/js/*.test.js: the framework-free plugin logic, also run on bare Node
-//    by tools/minitest.js (`npm run test:node12`), so they use only vitest globals.
-const specs = ['src/**/*.test.{ts,tsx}', 'tests/js/**/*.test.js'];
+// One spec family: tests/js/*.test.js, written against the vitest globals API
+// so that they also run on bare Node via tools/minitest.js
+// (`npm run test:node12`). The React layer is exercised against the same
+// stand-ins under both runners: 'react' and the Headlamp library resolve to
+// tests/js/stubs/ (tools/plugin-loader.js does the same under Node), so a
+// spec asserts the same markup and props whichever runner executes it.
+const stubs = path.resolve(__dirname, 'tests/js/stubs');
 
 export default defineConfig({
+  resolve: {
+    alias: [
+      { find: /^@kinvolk\/headlamp-plugin\/lib\/CommonComponents$/, replacement: path.join(stubs, 'CommonComponents.js') },
+      { find: /^@kinvolk\/headlamp-plugin\/lib$/, replacement: path.join(stubs, 'headlamp-lib.js') },
+      { find: /^react$/, replacement: path.join(stubs, 'react.js') },
+    ],
+  },
   test: {
-    include: specs,
+    include: ['tests/js/**/*.test.js'],
     exclude: ['node_modules/**', 'dist/**', 'gpurun_out/**'],
-    environment: 'jsdom',
+    environment: 'node',
     globals: true,
     setupFiles: ['./vitest.setup.ts'],
     testTimeout: 20000,

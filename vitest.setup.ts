@@ -1,5 +1,3 @@
-import '@testing-library/jest-dom';
-import { cleanup } from '@testing-library/react';
 import { afterEach } from 'vitest';
 import { resetSharedStores } from './src/api/clusterStore.js';
 
@@ -8,6 +6,5 @@ import { resetSharedStores } from './src/api/clusterStore.js';
 // Settings need no storage shim: src/api/settings.js falls back to defaults
 // when `localStorage` is missing or is Node's method-less global.
 afterEach(() => {
-  cleanup();
   resetSharedStores();
 });
