@@ -167,6 +167,21 @@ function renderAll(ctx, mstate) {
   };
 }
 
+/** The five routes, in sidebar order (src/routes.js). */
+export const PAGES = ['overview', 'devicePlugins', 'nodes', 'pods', 'metrics'];
+
+/** Build and render ONE page (the one whose Refresh was clicked); returns its row count. */
+function renderOne(page, ctx, mstate, pageMetrics) {
+  let vm;
+  if (page === 'overview') vm = overviewView(ctx);
+  else if (page === 'devicePlugins') vm = devicePluginsView(ctx);
+  else if (page === 'nodes') vm = nodesView(ctx, { metrics: pageMetrics });
+  else if (page === 'pods') vm = podsView(ctx, { metrics: pageMetrics });
+  else vm = metricsView(ctx, mstate);
+  renderPage(vm);
+  return countRows(vm).tableRows;
+}
+
 const SNAPSHOT_CSS =
   'body{font-family:system-ui,sans-serif;margin:24px;color:#222;max-width:1200px}' +
   'h1{font-size:22px}h2{font-size:16px;border-bottom:1px solid #ddd;padding-bottom:4px;margin-top:28px}' +
@@ -220,6 +235,9 @@ function amdSchedule(request) {
   const store = createClusterStore({ request: request, onTrace: onTrace, clock: hiResClock });
   const metrics = createMetricsSource({ request: request, onTrace: onTrace, clock: hiResClock });
   const mstate = { metrics: null, fetchError: null, fetching: false, series: null };
+  // Per-page metrics state, as each page's own hook holds it (plugin.js):
+  // GPU Nodes → telemetry without series, GPU Pods → pod→GPU attribution only.
+  const pageMetrics = { nodes: null, pods: null };
   function fetchMetrics() {
     return Promise.all([metrics.fetchGpuMetrics(), metrics.fetchSeries(1800, 30)]).then(function (r) {
       mstate.metrics = r[0];
@@ -234,6 +252,18 @@ function amdSchedule(request) {
     refresh: function () {
       return Promise.all([store.refresh(), fetchMetrics()]);
     },
+    /** One page's Refresh button, as src/plugin.js wires it. */
+    refreshPage: function (page) {
+      if (page === 'nodes') {
+        return Promise.all([store.refresh(), metrics.fetchGpuMetrics().then(function (m) { pageMetrics.nodes = m; })]);
+      }
+      if (page === 'pods') {
+        return Promise.all([store.refresh(), metrics.fetchGpuOwners().then(function (m) { pageMetrics.pods = m; })]);
+      }
+      if (page === 'metrics') return fetchMetrics();
+      return store.refresh();
+    },
+    pageMetrics: function (page) { return page in pageMetrics && pageMetrics[page] ? pageMetrics[page] : mstate.metrics; },
     /** Route switch: render from the shared store now, revalidate in the background. */
     switchRoute: function () {
       const bg = Promise.all([store.refresh(), fetchMetrics()]);
@@ -268,6 +298,8 @@ function referenceSchedule(request) {
       const p = r.coldOpen();
       return { rendered: p, background: p };
     },
+    refreshPage: r.refreshPage,
+    pageMetrics: function () { return r.metrics(); },
     ctx: r.snapshot,
     mstate: function () { return { metrics: r.metrics(), fetchError: r.metrics() ? null : 'unreachable', fetching: false }; },
   };
@@ -412,6 +444,37 @@ async function serve(a) {
         out.requestsPerStep = (counter.n - before) / n;
         out.bytesPerStep = (counter.bytes - bytesBefore) / n;
         out.rows = rows;
+      } else if (c.cmd === 'pages') {
+        // Per-page refresh: n rounds through the five routes; on each, the
+        // page's own Refresh button is clicked and the time to its data
+        // committed + that page rebuilt and rendered is recorded.
+        const L = get(name);
+        if (!L.opened) {
+          await L.s.coldOpen();
+          L.opened = true;
+        }
+        const lat = {};
+        const reqs = {};
+        const rows = {};
+        for (let p = 0; p < PAGES.length; p++) {
+          lat[PAGES[p]] = [];
+          reqs[PAGES[p]] = 0;
+        }
+        for (let i = 0; i < n; i++) {
+          for (let p = 0; p < PAGES.length; p++) {
+            const page = PAGES[p];
+            const before = counter.n;
+            const t0 = process.hrtime();
+            await L.s.refreshPage(page);
+            rows[page] = renderOne(page, L.s.ctx(), L.s.mstate(), L.s.pageMetrics(page));
+            lat[page].push(ms(process.hrtime(t0)));
+            reqs[page] += counter.n - before;
+          }
+        }
+        out.pages = {};
+        for (let p = 0; p < PAGES.length; p++) {
+          out.pages[PAGES[p]] = { latencies: lat[PAGES[p]], requestsPerClick: reqs[PAGES[p]] / n, tableRows: rows[PAGES[p]] };
+        }
       } else if (c.cmd === 'snapshot') {
         // Static HTML of every view (docs/screenshots): same IR → HTML path as the benchmark.
         const L = get(name);

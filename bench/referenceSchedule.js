@@ -147,10 +147,25 @@ export function createReferenceSchedule(request) {
     state.pods = r[1].items;
   }
 
-  /** Dashboard refresh: provider chain, then the Metrics page's re-fetch. */
+  /**
+   * Composite refresh: provider chain, then the Metrics page's re-fetch. No
+   * single reference button does this (kept as a secondary figure); a click
+   * runs ONE of the two, see refreshPage.
+   */
   async function refresh() {
     await providerRefresh();
     await fetchMetrics();
+  }
+
+  /**
+   * One page's Refresh button, as the reference wires it:
+   *   Overview / Device Plugins / GPU Nodes / GPU Pods → the provider's
+   *   `refresh` (OverviewPage.tsx:143-158, DevicePluginsPage.tsx:39,
+   *   NodesPage.tsx:203, PodsPage.tsx:118 → IntelGpuDataContext.tsx:122-165);
+   *   Metrics → `fetchGpuMetrics` only (MetricsPage.tsx:198-200,238-258).
+   */
+  function refreshPage(page) {
+    return page === 'metrics' ? fetchMetrics() : providerRefresh();
   }
 
   /** Cold route mount: lists alongside the chain, then metrics. */
@@ -178,5 +193,5 @@ export function createReferenceSchedule(request) {
     };
   }
 
-  return { refresh: refresh, coldOpen: coldOpen, snapshot: snapshot, metrics: function () { return state.metrics; } };
+  return { refresh: refresh, refreshPage: refreshPage, coldOpen: coldOpen, snapshot: snapshot, metrics: function () { return state.metrics; } };
 }

@@ -28,6 +28,20 @@ def _check(line, n):
     assert line["rendered"]["gpu_nodes"] == n
     assert line["rendered"]["gpus_monitored"] == 8 * n
     assert line["rendered_parity_with_reference"] is True
+    assert line["dtype"] == "n/a"
+    # The headline is per page, each page's click against the reference's
+    # wiring of that page's button (not the all-pages composite).
+    pp = line["per_page_refresh_p50_ms"]
+    assert set(pp) == {"overview", "devicePlugins", "nodes", "pods", "metrics"}
+    mean = sum(v["amd"] for v in pp.values()) / 5
+    assert abs(line["value"] - mean) < 1e-2
+    assert abs(line["baseline"]["value_ms"] - sum(v["reference"] for v in pp.values()) / 5) < 1e-2
+    for k in ("overview", "devicePlugins", "nodes", "pods"):
+        assert pp[k]["requests"]["reference"] == 4  # CRD, then 3 plugin-pod selectors, in series
+    assert pp["metrics"]["requests"]["reference"] == 5  # probe, then 4 queries
+    for v in pp.values():
+        assert v["amd"] < v["reference"], pp
+    assert line["all_pages_refresh"]["requests"]["reference"] == 9
 
 
 def test_bench_single_rank():

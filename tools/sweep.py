@@ -40,6 +40,34 @@ def run(kind, val, args):
     return json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
 
 
+PAGE_COLS = [("overview", "Overview"), ("devicePlugins", "Device Plugins"), ("nodes", "GPU Nodes"),
+             ("pods", "GPU Pods"), ("metrics", "Metrics")]
+
+
+def table(rows):
+    """Markdown table led by the per-page Refresh-click p50s (reference → new)."""
+    head = ["Config", "GPU nodes"] + [f"{t} ref → new (ms)" for _, t in PAGE_COLS] + [
+        "Mean per page ref → new (ms)", "Speed-up", "All-pages composite ref → new (ms)",
+        "Cold open ref → new (ms)", "Route switch ref → new (ms)", "GPU nodes rendered", "GPU pods rendered",
+        "GPUs monitored", "Live GPU telemetry"]
+    md = ["| " + " | ".join(head) + " |", "|---|---:|" + "---|" * (len(head) - 2)]
+    for r in rows:
+        l = r["line"]
+        pp = l["per_page_refresh_p50_ms"]
+        comp = l["all_pages_refresh"]
+        label = f"{r['point']}-node scaling point" if r["kind"] == "nodes" else PRESET_LABEL[r["point"]]
+        cells = [label, str(l["config"]["nodes"])]
+        cells += [f"{pp[k]['reference']:.1f} → {pp[k]['amd']:.1f}" for k, _ in PAGE_COLS]
+        cells += [f"{l['baseline']['value_ms']:.1f} → {l['value']:.1f}", f"{l['baseline']['value_ms'] / l['value']:.1f}×",
+                  f"{comp['reference_p50_ms']:.1f} → {comp['amd_p50_ms']:.1f}",
+                  f"{l['cold_open_p50_ms']['reference']:.0f} → {l['cold_open_p50_ms']['amd']:.0f}",
+                  f"{l['route_switch_p50_ms']['reference']:.0f} → {l['route_switch_p50_ms']['amd']:.1f}",
+                  str(l["rendered"]["gpu_nodes"]), str(l["rendered"]["gpu_pods"]), str(l["rendered"]["gpus_monitored"]),
+                  "yes" if l.get("live_telemetry") else "no"]
+        md.append("| " + " | ".join(cells) + " |")
+    return md
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--out", default="gpurun_out/sweep")
@@ -53,24 +81,10 @@ def main():
     for kind, val in POINTS:
         line = run(kind, val, args)
         rows.append({"kind": kind, "point": val, "line": line})
-        print(f"{kind}={val}: p50 {line['value']} ms vs ref {line['baseline']['p50_ms']} ms", flush=True)
+        print(f"{kind}={val}: per-page p50 {line['value']} ms vs ref {line['baseline']['value_ms']} ms", flush=True)
         with open(os.path.join(args.out, "sweep.json"), "w") as f:
             json.dump(rows, f, indent=1)
-    md = ["| Config | GPU nodes | Ref-schedule p50 refresh (ms) | New p50 refresh (ms) | New p95 (ms) | Speed-up | "
-          "Requests/refresh (ref → new) | Cold open p50 ref → new (ms) | New cold-open render p50 (ms) | "
-          "Route switch p50 ref → new (ms) | GPU nodes rendered | GPU pods rendered | GPUs monitored | Live GPU telemetry |",
-          "|---|---:|---:|---:|---:|---:|---|---|---:|---|---:|---:|---:|---|"]
-    for r in rows:
-        l = r["line"]
-        label = f"{r['point']}-node scaling point" if r["kind"] == "nodes" else PRESET_LABEL[r["point"]]
-        md.append(
-            f"| {label} | {l['config']['nodes']} | {l['baseline']['p50_ms']:.1f} | {l['value']:.1f} | {l['p95_ms']:.1f} | "
-            f"{l['baseline']['p50_ms'] / l['value']:.1f}× | {l['baseline']['requests_per_refresh']:.0f} → "
-            f"{l['requests_per_refresh']:.0f} | {l['cold_open_p50_ms']['reference']:.0f} → {l['cold_open_p50_ms']['amd']:.0f} | "
-            f"{l.get('cold_render_p50_ms') or float('nan'):.1f} | "
-            f"{l['route_switch_p50_ms']['reference']:.0f} → {l['route_switch_p50_ms']['amd']:.1f} | "
-            f"{l['rendered']['gpu_nodes']} | {l['rendered']['gpu_pods']} | {l['rendered']['gpus_monitored']} | "
-            f"{'yes' if l.get('live_telemetry') else 'no'} |")
+    md = table(rows)
     with open(os.path.join(args.out, "sweep.md"), "w") as f:
         f.write("\n".join(md) + "\n")
     print("\n".join(md))
