@@ -696,15 +696,80 @@ export function formatComponent(c) {
 // Cluster-level aggregation (computed once per data change, not per render)
 // ---------------------------------------------------------------------------
 
+// Per-object facts the index needs, cached on the (immutable) object: a
+// watch event that changes one pod re-derives that pod only.
+const nodeFactCache = new WeakMap();
+const podFactCache = new WeakMap();
+
+function nodeFacts(n) {
+  let f = nodeFactCache.get(n);
+  if (!f) {
+    const cap = getNodeGpuCount(n);
+    const pp = partitionsPerGpu(n);
+    f = {
+      capacity: cap,
+      allocatable: getNodeGpuAllocatable(n),
+      ready: isNodeReady(n),
+      partitionsPerGpu: pp,
+      physicalGpus: cap > 0 ? Math.ceil(cap / pp) : 0,
+      partitions: getNodePartitionCount(n),
+    };
+    nodeFactCache.set(n, f);
+  }
+  return f;
+}
+
 /**
- * Per-node GPU accounting and the pod index every page needs.
+ * {phase, nodeName, gpus} of a GPU pod, derived once per object; `gpus` is
+ * what the pod holds (0 once it terminated).
+ */
+export function podFacts(p) {
+  let f = podFactCache.get(p);
+  if (!f) {
+    const phase = podPhase(p);
+    f = {
+      phase: phase,
+      nodeName: get(p, ['spec', 'nodeName'], null),
+      // The kubelet allocates devices at admission and releases them when the
+      // pod terminates, so a bound non-terminal pod holds its GPUs.
+      gpus: phase !== 'Succeeded' && phase !== 'Failed' ? getPodGpuCount(p) : 0,
+    };
+    podFactCache.set(p, f);
+  }
+  return f;
+}
+
+function sameArray(a, b) {
+  if (a === b) return true;
+  if (!a || !b || a.length !== b.length) return false;
+  for (let i = 0; i < a.length; i++) if (a[i] !== b[i]) return false;
+  return true;
+}
+
+function sameFields(a, b) {
+  if (a === b) return true;
+  if (!a || !b) return false;
+  for (const k in a) if (a[k] !== b[k]) return false;
+  return true;
+}
+
+/**
+ * Per-node GPU accounting and the pod index every page needs:
+ * `podsByNode` and `nodeStats` are Maps keyed by node name.
  * Fixes reference quirks Q2 (pods vs GPUs), Q3 (init containers), Q10 (negative free).
+ *
+ * With `prev` (the index of the previous data), every per-node pod array and
+ * stats object whose content did not change is taken from `prev`, and `prev`
+ * itself is returned when nothing changed — so a memoised per-node view
+ * (node card, Node detail section) is rebuilt only for the nodes an event
+ * touched.
  * @param {any[]} gpuNodes
  * @param {any[]} gpuPods
+ * @param {ReturnType<typeof buildClusterIndex>} [prev]
  */
-export function buildClusterIndex(gpuNodes, gpuPods) {
-  const podsByNode = {};
-  const nodeStats = {};
+export function buildClusterIndex(gpuNodes, gpuPods, prev) {
+  const podsByNode = new Map();
+  const nodeStats = new Map();
   let capacity = 0;
   let allocatable = 0;
   let inUse = 0;
@@ -713,66 +778,198 @@ export function buildClusterIndex(gpuNodes, gpuPods) {
   let physicalGpus = 0;
   let hbmBytes = 0;
   let hbmAllocatedBytes = 0;
+  let heldGpus = 0;
   const phases = { Running: 0, Pending: 0, Succeeded: 0, Failed: 0, Other: 0 };
   for (let i = 0; i < gpuNodes.length; i++) {
     const n = gpuNodes[i];
     const name = n.metadata.name;
-    const cap = getNodeGpuCount(n);
-    const alloc = getNodeGpuAllocatable(n);
-    const ready = isNodeReady(n);
-    const pp = partitionsPerGpu(n);
-    const phys = cap > 0 ? Math.ceil(cap / pp) : 0;
-    capacity += cap;
-    allocatable += alloc;
-    partitions += getNodePartitionCount(n);
-    physicalGpus += phys;
-    hbmBytes += phys * MI355X.hbmBytes;
-    if (ready) readyNodes++;
-    nodeStats[name] = {
-      capacity: cap, allocatable: alloc, inUse: 0, pods: 0, ready: ready,
-      physicalGpus: phys, partitionsPerGpu: pp,
-    };
-    podsByNode[name] = [];
+    const f = nodeFacts(n);
+    capacity += f.capacity;
+    allocatable += f.allocatable;
+    partitions += f.partitions;
+    physicalGpus += f.physicalGpus;
+    hbmBytes += f.physicalGpus * MI355X.hbmBytes;
+    if (f.ready) readyNodes++;
+    nodeStats.set(name, {
+      capacity: f.capacity, allocatable: f.allocatable, inUse: 0, pods: 0, ready: f.ready,
+      physicalGpus: f.physicalGpus, partitionsPerGpu: f.partitionsPerGpu,
+    });
+    podsByNode.set(name, []);
   }
   for (let i = 0; i < gpuPods.length; i++) {
     const p = gpuPods[i];
-    const phase = podPhase(p);
-    if (phase in phases) phases[phase]++;
+    const f = podFacts(p);
+    if (f.phase in phases) phases[f.phase]++;
     else phases.Other++;
-    const nodeName = get(p, ['spec', 'nodeName'], null);
+    const nodeName = f.nodeName;
     if (!nodeName) continue;
-    if (!podsByNode[nodeName]) podsByNode[nodeName] = [];
-    podsByNode[nodeName].push(p);
-    const st = nodeStats[nodeName];
+    heldGpus += f.gpus;
+    let bucket = podsByNode.get(nodeName);
+    if (!bucket) podsByNode.set(nodeName, (bucket = []));
+    bucket.push(p);
+    const st = nodeStats.get(nodeName);
     if (!st) continue;
     st.pods++;
-    // The kubelet allocates devices at admission and releases them when the
-    // pod terminates, so a bound non-terminal pod holds its GPUs.
-    if (phase !== 'Succeeded' && phase !== 'Failed') {
-      const g = getPodGpuCount(p);
-      st.inUse += g;
-      inUse += g;
-      // A partition holds its share of the board's HBM.
-      hbmAllocatedBytes += (g * MI355X.hbmBytes) / st.partitionsPerGpu;
-    }
+    st.inUse += f.gpus;
+    inUse += f.gpus;
+    // A partition holds its share of the board's HBM.
+    hbmAllocatedBytes += (f.gpus * MI355X.hbmBytes) / st.partitionsPerGpu;
   }
+  const totals = {
+    nodes: gpuNodes.length,
+    readyNodes: readyNodes,
+    capacity: capacity,
+    allocatable: allocatable,
+    inUse: inUse,
+    free: Math.max(0, allocatable - inUse),
+    partitions: partitions,
+    physicalGpus: physicalGpus,
+    hbmBytes: hbmBytes,
+    hbmAllocatedBytes: hbmAllocatedBytes,
+    utilizationPct: pct(inUse, allocatable),
+    // GPUs held by bound, non-terminated pods, on any node (GPU Pods summary).
+    heldGpus: heldGpus,
+  };
+  if (!prev) return { podsByNode: podsByNode, nodeStats: nodeStats, totals: totals, phases: phases };
+
+  // Structural sharing with the previous index.
+  let same = podsByNode.size === prev.podsByNode.size && nodeStats.size === prev.nodeStats.size;
+  podsByNode.forEach(function (pods, name) {
+    const old = prev.podsByNode.get(name);
+    if (sameArray(old, pods)) podsByNode.set(name, old);
+    else same = false;
+  });
+  nodeStats.forEach(function (st, name) {
+    const old = prev.nodeStats.get(name);
+    if (sameFields(old, st)) nodeStats.set(name, old);
+    else same = false;
+  });
+  const sameTotals = sameFields(prev.totals, totals);
+  const samePhases = sameFields(prev.phases, phases);
+  if (same && sameTotals && samePhases) return prev;
   return {
     podsByNode: podsByNode,
     nodeStats: nodeStats,
-    totals: {
-      nodes: gpuNodes.length,
-      readyNodes: readyNodes,
-      capacity: capacity,
-      allocatable: allocatable,
-      inUse: inUse,
-      free: Math.max(0, allocatable - inUse),
-      partitions: partitions,
-      physicalGpus: physicalGpus,
-      hbmBytes: hbmBytes,
-      hbmAllocatedBytes: hbmAllocatedBytes,
-      utilizationPct: pct(inUse, allocatable),
-    },
-    phases: phases,
+    totals: sameTotals ? prev.totals : totals,
+    phases: samePhases ? prev.phases : phases,
+  };
+}
+
+function phaseBucket(phase) {
+  return phase === 'Running' || phase === 'Pending' || phase === 'Succeeded' || phase === 'Failed' ? phase : 'Other';
+}
+
+/**
+ * The index after a delta of the GPU pod list — pods replaced by new
+ * versions (status updates), removed and added — derived from `prev` in
+ * O(changed pods + nodes) instead of rebuilt from every GPU node and pod.
+ * Equal to `buildClusterIndex` of the new lists (tests/js/listCache.test.js
+ * pins it); null when it cannot tell (the caller rebuilds).
+ * @param {ReturnType<typeof buildClusterIndex>} prev
+ * @param {{replaced: Array<[any, any]>, removed: any[], added: any[]}} delta
+ * @param {(pod: any) => number} positionOf  list position (orders a node's pods)
+ */
+export function patchClusterIndex(prev, delta, positionOf) {
+  const phases = Object.assign({}, prev.phases);
+  const buckets = new Map();
+  const stats = new Map();
+  let inUse = prev.totals.inUse;
+  let hbmAllocatedBytes = prev.totals.hbmAllocatedBytes;
+  let heldGpus = prev.totals.heldGpus;
+
+  function bucketOf(node, create) {
+    let b = buckets.get(node);
+    if (b === undefined) {
+      const old = prev.podsByNode.get(node);
+      if (!old && !create) return null;
+      b = old ? old.slice() : [];
+      buckets.set(node, b);
+    }
+    return b;
+  }
+  function account(f, sign) {
+    phases[phaseBucket(f.phase)] += sign;
+    if (!f.nodeName) return;
+    heldGpus += sign * f.gpus;
+    const base = stats.get(f.nodeName) || prev.nodeStats.get(f.nodeName);
+    if (!base) return;
+    const st = stats.get(f.nodeName) || Object.assign({}, base);
+    stats.set(f.nodeName, st);
+    st.pods += sign;
+    st.inUse += sign * f.gpus;
+    inUse += sign * f.gpus;
+    hbmAllocatedBytes += (sign * f.gpus * MI355X.hbmBytes) / st.partitionsPerGpu;
+  }
+  function remove(p) {
+    const f = podFacts(p);
+    account(f, -1);
+    if (!f.nodeName) return true;
+    const b = bucketOf(f.nodeName, false);
+    const idx = b ? b.indexOf(p) : -1;
+    if (idx < 0) return false;
+    b.splice(idx, 1);
+    return true;
+  }
+  function add(p) {
+    const f = podFacts(p);
+    account(f, +1);
+    if (!f.nodeName) return;
+    const b = bucketOf(f.nodeName, true);
+    const pos = positionOf(p);
+    let at = b.length;
+    while (at > 0 && positionOf(b[at - 1]) > pos) at--;
+    b.splice(at, 0, p);
+  }
+
+  for (let k = 0; k < delta.replaced.length; k++) {
+    const o = delta.replaced[k][0];
+    const n = delta.replaced[k][1];
+    const fo = podFacts(o);
+    const fn = podFacts(n);
+    if (fo.nodeName === fn.nodeName && fn.nodeName) {
+      // Same place in its node's list.
+      const b = bucketOf(fn.nodeName, false);
+      const idx = b ? b.indexOf(o) : -1;
+      if (idx < 0) return null;
+      b[idx] = n;
+      account(fo, -1);
+      account(fn, +1);
+    } else {
+      if (!remove(o)) return null;
+      add(n);
+    }
+  }
+  for (let k = 0; k < delta.removed.length; k++) if (!remove(delta.removed[k])) return null;
+  for (let k = 0; k < delta.added.length; k++) add(delta.added[k]);
+
+  let podsByNode = prev.podsByNode;
+  if (buckets.size > 0) {
+    podsByNode = new Map(prev.podsByNode);
+    buckets.forEach(function (b, node) {
+      // Only GPU nodes keep an empty list (as buildClusterIndex does).
+      if (b.length === 0 && !prev.nodeStats.has(node)) podsByNode.delete(node);
+      else podsByNode.set(node, b);
+    });
+  }
+  let nodeStats = prev.nodeStats;
+  const changedStats = [];
+  stats.forEach(function (st, node) { if (!sameFields(prev.nodeStats.get(node), st)) changedStats.push([node, st]); });
+  if (changedStats.length > 0) {
+    nodeStats = new Map(prev.nodeStats);
+    for (let k = 0; k < changedStats.length; k++) nodeStats.set(changedStats[k][0], changedStats[k][1]);
+  }
+  const totals = Object.assign({}, prev.totals, {
+    inUse: inUse,
+    free: Math.max(0, prev.totals.allocatable - inUse),
+    hbmAllocatedBytes: hbmAllocatedBytes,
+    utilizationPct: pct(inUse, prev.totals.allocatable),
+    heldGpus: heldGpus,
+  });
+  return {
+    podsByNode: podsByNode,
+    nodeStats: nodeStats,
+    totals: sameFields(prev.totals, totals) ? prev.totals : totals,
+    phases: sameFields(prev.phases, phases) ? prev.phases : phases,
   };
 }
 
@@ -803,9 +1000,41 @@ export function pctToColor(p) {
 // ---------------------------------------------------------------------------
 
 /** Age as Ns / Nm / Nh / Nd (reference k8s.ts:337-348 semantics). `now` is injectable for tests. */
+const timeCache = new Map();
+
+/** Epoch ms of an RFC 3339 timestamp (NaN when unparseable); parsed once per string. */
+export function parseTime(timestamp) {
+  let t = timeCache.get(timestamp);
+  if (t === undefined) {
+    t = new Date(timestamp).getTime();
+    if (timeCache.size > 65536) timeCache.clear();
+    timeCache.set(timestamp, t);
+  }
+  return t;
+}
+
+/**
+ * The instant (epoch ms) at which `formatAge(timestamp, now)` next shows a
+ * different label: the next whole second, minute, hour or day of age
+ * (Infinity when the label never changes).
+ */
+export function nextAgeChange(timestamp, now) {
+  if (!timestamp) return Infinity;
+  const t = parseTime(timestamp);
+  if (!isFinite(t)) return Infinity;
+  const n = now === undefined ? Date.now() : now;
+  const secs = Math.max(0, Math.floor((n - t) / 1000));
+  if (secs < 60) return t + (secs + 1) * 1000;
+  const mins = Math.floor(secs / 60);
+  if (mins < 60) return t + (mins + 1) * 60000;
+  const hours = Math.floor(mins / 60);
+  if (hours < 24) return t + (hours + 1) * 3600000;
+  return t + (Math.floor(hours / 24) + 1) * 86400000;
+}
+
 export function formatAge(timestamp, now) {
   if (!timestamp) return 'unknown';
-  const t = new Date(timestamp).getTime();
+  const t = parseTime(timestamp);
   if (!isFinite(t)) return 'unknown';
   const diffMs = (now === undefined ? Date.now() : now) - t;
   const secs = Math.max(0, Math.floor(diffMs / 1000));

@@ -19,8 +19,10 @@
  *   * clears its timeout timers (reference Q6) and drops responses from a
  *     superseded refresh via a sequence number (the analog of the
  *     reference's `cancelled` flag, :114/:187);
- *   * computes GPU node/pod filters and the cluster index once per data
- *     change (memoised on input identity), not once per render.
+ *   * classifies only the objects a watch event changed (./listCache.js) and
+ *     rebuilds the cluster index only when a GPU node / pod changed, with
+ *     structural sharing per node (reference: every pod re-filtered per
+ *     event, every aggregate recomputed per render).
  *
  * Nodes and pods arrive from Headlamp's `useList` watch through
  * `setNodes` / `setPods` (same two-track design as reference ADR 002);
@@ -35,13 +37,15 @@ import {
   PLUGIN_POD_QUERIES,
   buildClusterIndex,
   dedupePods,
-  filterAmdGpuNodes,
   filterAmdGpuPluginPods,
-  filterGpuRequestingPods,
+  isAmdGpuNode,
+  isAmdGpuPluginPod,
   isDeviceConfig,
+  isGpuRequestingPod,
   isKubeList,
-  unwrapAll,
+  patchClusterIndex,
 } from './amdgpu.js';
+import { createListTracker } from './listCache.js';
 
 export const DEFAULT_REQUEST_TIMEOUT_MS = 2000;
 
@@ -177,35 +181,54 @@ export function createClusterStore(opts) {
   let version = 0;
   const listeners = [];
 
-  // Memoised derivations keyed on input identity.
-  let memoNodesIn = undefined;
+  // GPU nodes, GPU pods and operator pods are kept incrementally
+  // (./listCache.js): the watch delivers a new list on every event anywhere
+  // in the cluster, but only objects that changed are classified again, and
+  // each subset keeps its identity unless one of its members was added,
+  // changed or removed — churn of unrelated pods costs one pass of identity
+  // compares and invalidates no memoised view downstream.
+  const nodeTracker = createListTracker([isAmdGpuNode]);
+  const podTracker = createListTracker([isGpuRequestingPod, isAmdGpuPluginPod]);
   let memoGpuNodes = [];
-  let memoPodsIn = undefined;
   let memoGpuPods = [];
-  let memoPluginIn = undefined;
   let memoPluginPods = [];
+  const counters = { indexBuilds: 0, indexPatches: 0 };
   let memoIndexKey = [null, null];
   let memoIndex = buildClusterIndex([], []);
   let snapshot = null;
 
-  // The watch delivers a new list on every event anywhere in the cluster;
-  // the GPU subsets keep their identity unless a GPU node / pod actually
-  // changed (uid + resourceVersion), so churn of unrelated pods does not
-  // invalidate any memoised view downstream.
-  function gpuNodes() {
-    if (s.nodes !== memoNodesIn) {
-      memoNodesIn = s.nodes;
-      const next = s.nodes ? filterAmdGpuNodes(s.nodes) : [];
-      memoGpuNodes = sameObjects(memoGpuNodes, next) ? memoGpuNodes : next;
+  function trackNodes(items) {
+    const r = nodeTracker.update(items || []);
+    if (r.changed[0] && !sameObjects(memoGpuNodes, r.subsets[0])) memoGpuNodes = r.subsets[0];
+    if (!items) memoGpuNodes = [];
+  }
+  function trackPods(items) {
+    const r = podTracker.update(items || []);
+    if (r.changed[0] && !sameObjects(memoGpuPods, r.subsets[0])) {
+      // A delta of the GPU pods (status updates, pods added / removed):
+      // patch the index of the current nodes + previous pods instead of
+      // rebuilding it from every GPU node and pod.
+      const delta = r.deltas[0];
+      if (delta && memoIndexKey[0] === memoGpuNodes && memoIndexKey[1] === memoGpuPods) {
+        const patched = patchClusterIndex(memoIndex, delta, podTracker.positionOf);
+        if (patched) {
+          counters.indexPatches++;
+          memoIndex = patched;
+          memoIndexKey = [memoGpuNodes, r.subsets[0]];
+        }
+      }
+      memoGpuPods = r.subsets[0];
     }
+    if (r.changed[1] && !sameObjects(memoPluginPods, r.subsets[1])) memoPluginPods = r.subsets[1];
+    if (!items) {
+      memoGpuPods = [];
+      memoPluginPods = [];
+    }
+  }
+  function gpuNodes() {
     return memoGpuNodes;
   }
   function gpuPods() {
-    if (s.pods !== memoPodsIn) {
-      memoPodsIn = s.pods;
-      const next = s.pods ? filterGpuRequestingPods(s.pods) : [];
-      memoGpuPods = sameObjects(memoGpuPods, next) ? memoGpuPods : next;
-    }
     return memoGpuPods;
   }
   /**
@@ -217,17 +240,13 @@ export function createClusterStore(opts) {
    */
   function pluginPods() {
     if (s.podsState !== 'ready' || !s.pods) return s.pluginPods;
-    if (s.pods !== memoPluginIn) {
-      memoPluginIn = s.pods;
-      const next = filterAmdGpuPluginPods(s.pods);
-      memoPluginPods = sameObjects(memoPluginPods, next) ? memoPluginPods : next;
-    }
     return memoPluginPods;
   }
   function index(n, p) {
     if (memoIndexKey[0] !== n || memoIndexKey[1] !== p) {
       memoIndexKey = [n, p];
-      memoIndex = buildClusterIndex(n, p);
+      memoIndex = buildClusterIndex(n, p, memoIndex);
+      counters.indexBuilds++;
     }
     return memoIndex;
   }
@@ -361,7 +380,7 @@ export function createClusterStore(opts) {
 
   /** Feed the Headlamp `useList()` result for nodes (wrappers are unwrapped here). */
   function setNodes(items, error) {
-    const next = items ? unwrapAll(items) : null;
+    const next = items ? (Array.isArray(items) ? items : []) : null;
     const err = error ? String(error) : null;
     const state = err ? 'error' : next ? 'ready' : 'pending';
     if (items === null && s.nodes === null && err === s.nodeError && state === s.nodesState) return;
@@ -372,11 +391,12 @@ export function createClusterStore(opts) {
     s.nodes = next;
     s.nodeError = err;
     s.nodesState = state;
+    trackNodes(next);
     emit();
   }
 
   function setPods(items, error) {
-    const next = items ? unwrapAll(items) : null;
+    const next = items ? (Array.isArray(items) ? items : []) : null;
     const err = error ? String(error) : null;
     const state = err ? 'error' : next ? 'ready' : 'pending';
     if (items === null && s.pods === null && err === s.podError && state === s.podsState) return;
@@ -385,6 +405,7 @@ export function createClusterStore(opts) {
     s.pods = next;
     s.podError = err;
     s.podsState = state;
+    trackPods(next);
     emit();
     // The pod list failed (e.g. cluster-wide list forbidden): fall back to the
     // plugin-pod requests so operator pods still show.
@@ -453,6 +474,13 @@ export function createClusterStore(opts) {
     settled: function () { return inflight || Promise.resolve(); },
     /** True once a CRD/pod fetch has committed at least once. */
     hasLoaded: function () { return s.asyncLoaded; },
+    /**
+     * Work counters: cluster-index rebuilds vs delta patches, and the list
+     * trackers' classification counts (objects classified / reused / skipped).
+     */
+    counters: function () {
+      return Object.assign({}, counters, { pods: podTracker.stats(), nodes: nodeTracker.stats() });
+    },
   };
 }
 

@@ -190,8 +190,8 @@ export interface NodeStats {
 }
 
 export interface ClusterIndex {
-  podsByNode: Record<string, AmdGpuPod[]>;
-  nodeStats: Record<string, NodeStats>;
+  podsByNode: Map<string, AmdGpuPod[]>;
+  nodeStats: Map<string, NodeStats>;
   totals: {
     nodes: number;
     readyNodes: number;

@@ -67,37 +67,93 @@ export function page(title, refresh, items) {
 // Memoisation
 // ---------------------------------------------------------------------------
 
+// Time-dependent output (ages: "42s", "7m", "3h", "12d") stays valid until
+// the first label it shows changes. While a section or row is built, the
+// earliest such instant is collected here (noteExpiry), so a cached value can
+// be reused until then instead of being rebuilt on every clock tick.
+let horizon = null;
+
+/** Record that the value being built changes at epoch-ms `t`. */
+export function noteExpiry(t) {
+  if (horizon !== null && t < horizon.until) horizon.until = t;
+}
+
+function computeWithHorizon(compute) {
+  const saved = horizon;
+  const h = { until: Infinity };
+  horizon = h;
+  let value;
+  try {
+    value = compute();
+  } finally {
+    horizon = saved;
+  }
+  noteExpiry(h.until); // a nested value bounds the enclosing one
+  return { value: value, until: h.until };
+}
+
+function sameDeps(a, b) {
+  if (a.length !== b.length) return false;
+  for (let i = 0; i < a.length; i++) if (a[i] !== b[i]) return false;
+  return true;
+}
+
+function fresh(e, deps, now) {
+  if (!e || !sameDeps(e.deps, deps)) return false;
+  if (now === undefined) return true;
+  return now >= e.from && now < e.until;
+}
+
 /**
  * Identity-keyed memo with a bounded number of slots. `memo(key, deps, fn)`
  * returns the previous value for `key` when every dep is `===` to last time.
  * The store keeps unchanged lists by identity (structural sharing), so
  * sections whose inputs did not change are returned as the SAME IR objects —
- * which `React.memo` (View.tsx) and `renderSection`'s cache then skip.
+ * which `React.memo` (react.js Section) and `renderSection`'s cache then skip.
+ *
+ * `memo(key, deps, fn, now)` also holds the value only until the first age
+ * label inside it changes (see noteExpiry), instead of keying on the clock.
  */
 export function createMemo(limit) {
   const max = limit || 256;
   const slots = new Map();
-  function memo(key, deps, compute) {
+  function memo(key, deps, compute, now) {
     const e = slots.get(key);
-    if (e && e.deps.length === deps.length) {
-      let same = true;
-      for (let i = 0; i < deps.length; i++) {
-        if (e.deps[i] !== deps[i]) {
-          same = false;
-          break;
-        }
-      }
-      if (same) return e.value;
+    if (fresh(e, deps, now)) {
+      noteExpiry(e.until);
+      return e.value;
     }
-    const value = compute();
+    const r = computeWithHorizon(compute);
     slots.delete(key);
-    slots.set(key, { deps: deps, value: value });
+    slots.set(key, { deps: deps, value: r.value, until: r.until, from: now === undefined ? -Infinity : now });
     if (slots.size > max) slots.delete(slots.keys().next().value);
-    return value;
+    return r.value;
   }
   memo.clear = function () { slots.clear(); };
   memo.size = function () { return slots.size; };
   return memo;
+}
+
+/**
+ * Per-object cache of derived values (table rows of a pod, a node), keyed on
+ * the Kubernetes object itself: a watch event that changes one pod rebuilds
+ * that pod's row only. Same contract as `memo` (deps + age expiry); entries
+ * go away with their objects.
+ */
+export function createObjectCache() {
+  let cache = new WeakMap();
+  function cached(obj, deps, compute, now) {
+    const e = cache.get(obj);
+    if (fresh(e, deps, now)) {
+      noteExpiry(e.until);
+      return e.value;
+    }
+    const r = computeWithHorizon(compute);
+    cache.set(obj, { deps: deps, value: r.value, until: r.until, from: now === undefined ? -Infinity : now });
+    return r.value;
+  }
+  cached.clear = function () { cache = new WeakMap(); };
+  return cached;
 }
 
 // ---------------------------------------------------------------------------

@@ -31,6 +31,8 @@ import {
   deviceConfigStatus,
   deviceConfigStatusText,
   formatAge,
+  nextAgeChange,
+  podFacts,
   formatBytes,
   formatComponent,
   formatGpuModel,
@@ -67,7 +69,7 @@ import {
 } from '../api/amdgpu.js';
 import { buildGpuSlots, buildXgmiMatrix, isFullMesh } from '../api/topology.js';
 import { PROMETHEUS_SERVICES, summarizeMetrics } from '../api/metrics.js';
-import { bar, createMemo, kv, lines, loader, page, pctbar, row, section, status, table } from './ir.js';
+import { bar, createMemo, createObjectCache, kv, lines, loader, noteExpiry, page, pctbar, row, section, status, table } from './ir.js';
 
 export const BRAND = 'AMD GPU';
 
@@ -79,10 +81,58 @@ export const BRAND = 'AMD GPU';
 // One slot per section: node cards, node details, metrics nodes and pod details
 // of a few hundred nodes / thousands of pods fit without LRU churn.
 const memo = createMemo(8192);
+// Table rows per Kubernetes object, one cache per table (pods, nodes): an
+// event rebuilds the changed object's row only.
+const ovPluginRows = createObjectCache();
+const dpPluginRows = createObjectCache();
+const nodeSummaryRows = createObjectCache();
+const podRows = createObjectCache();
+const pendingRows = createObjectCache();
+const ROW_CACHES = [ovPluginRows, dpPluginRows, nodeSummaryRows, podRows, pendingRows];
 const podDetailCache = typeof WeakMap === 'function' ? new WeakMap() : null;
 
-function ageKey(now) {
-  return Math.floor(now / 1000);
+/** Rows per memo slot in the large tables (see chunkedRows). */
+const ROW_CHUNK = 64;
+
+/**
+ * `objs.map(build)` for a large table, memoised in chunks of ROW_CHUNK
+ * objects keyed on their identities: after a watch event that replaced one
+ * pod in a 5000-row table, 78 chunks are identity-compared and one is
+ * rebuilt (its other rows come from `rowCacheOf`'s per-object cache).
+ */
+function chunkedRows(name, objs, deps, build, now, depsOf) {
+  const out = [];
+  for (let c = 0; c < objs.length; c += ROW_CHUNK) {
+    const part = objs.slice(c, c + ROW_CHUNK);
+    const key = part.concat(deps);
+    // Per-object inputs besides the object itself (its stats, its pods).
+    if (depsOf) {
+      for (let i = 0; i < part.length; i++) {
+        const d = depsOf(part[i]);
+        for (let k = 0; k < d.length; k++) key.push(d[k]);
+      }
+    }
+    const rows = memo(name + ':' + c / ROW_CHUNK, key, function () { return part.map(build); }, now);
+    for (let i = 0; i < rows.length; i++) out.push(rows[i]);
+  }
+  return out;
+}
+
+/** `objs.filter(pred)` memoised in chunks the same way (pred depends on the object only). */
+function chunkedFilter(name, objs, pred) {
+  const out = [];
+  for (let c = 0; c < objs.length; c += ROW_CHUNK) {
+    const part = objs.slice(c, c + ROW_CHUNK);
+    const kept = memo(name + ':' + c / ROW_CHUNK, part, function () { return part.filter(pred); });
+    for (let i = 0; i < kept.length; i++) out.push(kept[i]);
+  }
+  return out;
+}
+
+/** formatAge, noting when the label changes (the enclosing memo holds until then). */
+function ageText(timestamp, now) {
+  noteExpiry(nextAgeChange(timestamp, now));
+  return formatAge(timestamp, now);
 }
 
 /** Seconds → "30 min" / "1 h" / "6 h" / "90 s" for section titles. */
@@ -95,6 +145,7 @@ export function formatWindow(sec) {
 /** Drop memoised sections (tests; cluster switch). */
 export function clearViewMemo() {
   memo.clear();
+  for (let i = 0; i < ROW_CACHES.length; i++) ROW_CACHES[i].clear();
 }
 export const ACTIVE_PODS_LIMIT = 10;
 
@@ -157,8 +208,9 @@ export function overviewView(ctx, opts) {
   if (ctx.loading) return page(null, null, [loader('Loading ' + BRAND + ' data...')]);
   const items = memo(
     'overview',
-    [ctx.deviceConfigs, ctx.pluginPods, ctx.pluginInstalled, ctx.crdAvailable, ctx.gpuNodes, ctx.gpuPods, ctx.index, ctx.error, ageKey(now)],
-    function () { return overviewItems(ctx, now); }
+    [ctx.deviceConfigs, ctx.pluginPods, ctx.pluginInstalled, ctx.crdAvailable, ctx.gpuNodes, ctx.gpuPods, ctx.index, ctx.error],
+    function () { return overviewItems(ctx, now); },
+    now
   );
   return page(BRAND + ' — Overview', refreshButton('Refresh AMD GPU data', ctx.refreshing), items);
 }
@@ -214,40 +266,56 @@ function overviewItems(ctx, now) {
   }
 
   if (ctx.crdAvailable && ctx.deviceConfigs.length > 0) {
-    items.push(
-      section('Device Config Status', [
-        table(
-          ['Name', 'Namespace', 'Status', 'Metrics Exporter', 'Node Labeller', 'Selector', 'Age'],
-          ctx.deviceConfigs.map(function (dc) {
-            return [
-              dc.metadata.name,
-              dc.metadata.namespace || '—',
-              status(deviceConfigStatus(dc), deviceConfigStatusText(dc)),
-              operandEnabled(dc, 'metricsExporter') ? status('success', 'Enabled') : status('warning', 'Disabled'),
-              operandEnabled(dc, 'nodeLabeller') ? status('success', 'Enabled') : status('warning', 'Disabled'),
-              formatSelector(get(dc, ['spec', 'selector'], null)),
-              formatAge(dc.metadata.creationTimestamp, now),
-            ];
-          }),
-          ctx.deviceConfigs.map(function (dc) { return dc.metadata.uid || dc.metadata.name; })
-        ),
-      ])
-    );
+    items.push(memo('overview-dc', [ctx.deviceConfigs], function () { return overviewDeviceConfigs(ctx.deviceConfigs, now); }, now));
   }
 
   if (ctx.pluginPods.length > 0) {
-    items.push(
-      section('Plugin Daemon Pods', [
-        table(
-          ['Name', 'Namespace', 'Component', 'Node', 'Status', 'Age'],
-          ctx.pluginPods.map(function (p) {
-            return [podName(p), podNs(p), formatComponent(pluginPodComponent(p)), podNode(p), readyLabel(p), formatAge(p.metadata.creationTimestamp, now)];
-          })
-        ),
-      ])
-    );
+    items.push(memo('overview-plugin-pods', [ctx.pluginPods], function () { return overviewPluginPods(ctx.pluginPods, now); }, now));
   }
 
+  items.push(memo('overview-nodes', [ctx.gpuNodes, t], function () { return overviewNodes(ctx.gpuNodes, t); }));
+  if (t.capacity > 0) items.push(memo('overview-alloc', [t], function () { return overviewAllocation(t); }));
+  const ph = ctx.index.phases;
+  items.push(memo('overview-workloads', [ph, ctx.gpuPods.length], function () { return overviewWorkloads(ph, ctx.gpuPods.length); }));
+  const active = memo('overview-active', [ctx.gpuPods], function () { return overviewActivePods(ctx.gpuPods, now); }, now);
+  if (active) items.push(active);
+  return items;
+}
+
+function overviewDeviceConfigs(dcs, now) {
+  return section('Device Config Status', [
+    table(
+      ['Name', 'Namespace', 'Status', 'Metrics Exporter', 'Node Labeller', 'Selector', 'Age'],
+      dcs.map(function (dc) {
+        return [
+          dc.metadata.name,
+          dc.metadata.namespace || '—',
+          status(deviceConfigStatus(dc), deviceConfigStatusText(dc)),
+          operandEnabled(dc, 'metricsExporter') ? status('success', 'Enabled') : status('warning', 'Disabled'),
+          operandEnabled(dc, 'nodeLabeller') ? status('success', 'Enabled') : status('warning', 'Disabled'),
+          formatSelector(get(dc, ['spec', 'selector'], null)),
+          ageText(dc.metadata.creationTimestamp, now),
+        ];
+      }),
+      dcs.map(function (dc) { return dc.metadata.uid || dc.metadata.name; })
+    ),
+  ]);
+}
+
+function overviewPluginPods(pods, now) {
+  return section('Plugin Daemon Pods', [
+    table(
+      ['Name', 'Namespace', 'Component', 'Node', 'Status', 'Age'],
+      chunkedRows('ov-plugin-rows', pods, [], function (p) {
+        return ovPluginRows(p, [], function () {
+          return [podName(p), podNs(p), formatComponent(pluginPodComponent(p)), podNode(p), readyLabel(p), ageText(p.metadata.creationTimestamp, now)];
+        }, now);
+      }, now)
+    ),
+  ]);
+}
+
+function overviewNodes(gpuNodes, t) {
   const nodeBlocks = [];
   if (t.nodes > 0) {
     nodeBlocks.push(
@@ -262,7 +330,8 @@ function overviewItems(ctx, now) {
     );
     // Analog of the reference's GPU-type distribution (OverviewPage.tsx:37-48):
     // every GPU is an MI355X, so what varies between nodes is the partition mode.
-    const modes = partitionModeDistribution(ctx.gpuNodes);
+    // Node labels only: holds across pod events.
+    const modes = memo('overview-modes', [gpuNodes], function () { return partitionModeDistribution(gpuNodes); });
     if (modes.length > 0) nodeBlocks.push(pctbar('GPU Partition Modes', modes, t.nodes));
   }
   const nodeRows = [
@@ -277,52 +346,52 @@ function overviewItems(ctx, now) {
   }
   if (t.partitions > 0) nodeRows.push(row('GPU Partitions', String(t.partitions)));
   nodeBlocks.push(kv(nodeRows));
-  items.push(section('GPU Nodes', nodeBlocks));
+  return section('GPU Nodes', nodeBlocks);
+}
 
-  if (t.capacity > 0) {
-    items.push(
-      section('GPU Allocation', [
-        pctbar(
-          'GPU Allocation (' + t.utilizationPct + '%)',
-          [
-            { name: 'In Use', value: t.inUse, fill: BAR_COLORS.ok },
-            { name: 'Available', value: t.free, fill: BAR_COLORS.track },
-          ],
-          t.allocatable
-        ),
-        kv([
-          row('Total Capacity (GPU devices)', String(t.capacity)),
-          row('Allocatable', String(t.allocatable)),
-          row('In Use', String(t.inUse)),
-          row('Free', status(t.free > 0 ? 'success' : 'warning', t.free)),
-          row('HBM Allocated', formatBytes(t.hbmAllocatedBytes)),
-        ]),
-      ])
-    );
-  }
+function overviewAllocation(t) {
+  return section('GPU Allocation', [
+    pctbar(
+      'GPU Allocation (' + t.utilizationPct + '%)',
+      [
+        { name: 'In Use', value: t.inUse, fill: BAR_COLORS.ok },
+        { name: 'Available', value: t.free, fill: BAR_COLORS.track },
+      ],
+      t.allocatable
+    ),
+    kv([
+      row('Total Capacity (GPU devices)', String(t.capacity)),
+      row('Allocatable', String(t.allocatable)),
+      row('In Use', String(t.inUse)),
+      row('Free', status(t.free > 0 ? 'success' : 'warning', t.free)),
+      row('HBM Allocated', formatBytes(t.hbmAllocatedBytes)),
+    ]),
+  ]);
+}
 
-  const ph = ctx.index.phases;
-  const wl = [row('Total GPU Pods', String(ctx.gpuPods.length))];
+function overviewWorkloads(ph, total) {
+  const wl = [row('Total GPU Pods', String(total))];
   if (ph.Running > 0) wl.push(row('Running', status('success', ph.Running)));
   if (ph.Pending > 0) wl.push(row('Pending', status('warning', ph.Pending)));
   if (ph.Failed > 0) wl.push(row('Failed', status('error', ph.Failed)));
-  items.push(section('GPU Workloads', [kv(wl)]));
+  return section('GPU Workloads', [kv(wl)]);
+}
 
-  const running = ctx.gpuPods.filter(function (p) { return podPhase(p) === 'Running'; });
-  if (running.length > 0) {
-    items.push(
-      section('Active GPU Pods', [
-        table(
-          ['Name', 'Namespace', 'Node', 'GPU Request', 'Age'],
-          running.slice(0, ACTIVE_PODS_LIMIT).map(function (p) {
-            return [podName(p), podNs(p), podNode(p), formatPodGpuRequests(p), formatAge(p.metadata.creationTimestamp, now)];
-          })
-        ),
-      ])
-    );
+/** The first ACTIVE_PODS_LIMIT running GPU pods (reference OverviewPage.tsx:414), or null. */
+function overviewActivePods(gpuPods, now) {
+  const running = [];
+  for (let i = 0; i < gpuPods.length && running.length < ACTIVE_PODS_LIMIT; i++) {
+    if (podFacts(gpuPods[i]).phase === 'Running') running.push(gpuPods[i]);
   }
-
-  return items;
+  if (running.length === 0) return null;
+  return section('Active GPU Pods', [
+    table(
+      ['Name', 'Namespace', 'Node', 'GPU Request', 'Age'],
+      running.map(function (p) {
+        return [podName(p), podNs(p), podNode(p), formatPodGpuRequests(p), ageText(p.metadata.creationTimestamp, now)];
+      })
+    ),
+  ]);
 }
 
 // ---------------------------------------------------------------------------
@@ -342,8 +411,9 @@ export function devicePluginsView(ctx, opts) {
   if (ctx.loading) return page(null, null, [loader('Loading device plugin data...')]);
   const items = memo(
     'device-plugins',
-    [ctx.deviceConfigs, ctx.pluginPods, ctx.crdAvailable, ctx.error, ageKey(now)],
-    function () { return devicePluginsItems(ctx, now); }
+    [ctx.deviceConfigs, ctx.pluginPods, ctx.crdAvailable, ctx.error],
+    function () { return devicePluginsItems(ctx, now); },
+    now
   );
   return page(BRAND + ' — Device Plugins', refreshButton('Refresh device plugin data', ctx.refreshing), items);
 }
@@ -407,7 +477,7 @@ function devicePluginsItems(ctx, now) {
       rows.push(row(op.label + ' Pods', status(countsToStatus(st.desired, st.available), countsToText(st.desired, st.available))));
     }
     rows.push(row('Node Selector', formatSelector(get(dc, ['spec', 'selector'], null))));
-    rows.push(row('Age', formatAge(dc.metadata.creationTimestamp, now)));
+    rows.push(row('Age', ageText(dc.metadata.creationTimestamp, now)));
     items.push(section('DeviceConfig: ' + dc.metadata.name, [kv(rows)], dc.metadata.uid || dc.metadata.name));
   }
 
@@ -416,12 +486,14 @@ function devicePluginsItems(ctx, now) {
       section('Plugin Daemon Pods', [
         table(
           ['Name', 'Namespace', 'Component', 'Node', 'Ready', 'Restarts', 'Age'],
-          ctx.pluginPods.map(function (p) {
-            return [
-              podName(p), podNs(p), formatComponent(pluginPodComponent(p)), podNode(p), readyLabel(p),
-              restartsCell(p), formatAge(p.metadata.creationTimestamp, now),
-            ];
-          })
+          chunkedRows('dp-plugin-rows', ctx.pluginPods, [], function (p) {
+            return dpPluginRows(p, [], function () {
+              return [
+                podName(p), podNs(p), formatComponent(pluginPodComponent(p)), podNode(p), readyLabel(p),
+                restartsCell(p), ageText(p.metadata.creationTimestamp, now),
+              ];
+            }, now);
+          }, now)
         ),
       ])
     );
@@ -472,7 +544,7 @@ function nodeCardRows(node, podsOnNode, stats, now) {
   rows.push(row('OS Image', get(node, ['status', 'nodeInfo', 'osImage'], '—')));
   rows.push(row('Kernel', get(node, ['status', 'nodeInfo', 'kernelVersion'], '—')));
   rows.push(row('Kubelet', get(node, ['status', 'nodeInfo', 'kubeletVersion'], '—')));
-  rows.push(row('Age', formatAge(node.metadata.creationTimestamp, now)));
+  rows.push(row('Age', ageText(node.metadata.creationTimestamp, now)));
   return rows;
 }
 
@@ -486,25 +558,32 @@ export function nodesView(ctx, opts) {
   const now = nowOf(opts);
   const metrics = opts && opts.metrics ? opts.metrics : null;
   if (ctx.loading) return page(null, null, [loader('Loading GPU node data...')]);
-  const age = ageKey(now);
-  const head = memo('nodes-head', [ctx.gpuNodes, ctx.index, ctx.error, age], function () {
+  const head = memo('nodes-head', [ctx.gpuNodes, ctx.index, ctx.error], function () {
     return nodesHeadItems(ctx, now);
-  });
-  const items = head.slice();
-  const idx = ctx.index;
+  }, now);
   const owners = ownersByNode(metrics);
-  for (let i = 0; i < ctx.gpuNodes.length; i++) {
-    const n = ctx.gpuNodes[i];
-    const name = n.metadata.name;
-    const pods = idx.podsByNode[name] || [];
-    const stats = idx.nodeStats[name];
-    const own = owners[name];
-    const xg = metrics && metrics.xgmi ? metrics.xgmi[name] : undefined;
-    const lk = metrics && metrics.links ? metrics.links[name] : undefined;
-    items.push(
+  const xgmi = metrics ? metrics.xgmi : undefined;
+  const links = metrics ? metrics.links : undefined;
+  // The card list as a whole holds while no input changed (most watch events
+  // touch no GPU node or pod); otherwise only changed cards are rebuilt.
+  const items = memo('nodes-cards', [head, ctx.gpuNodes, ctx.index, owners, xgmi, links], function () {
+    const idx = ctx.index;
+    function inputs(n) {
+      const name = n.metadata.name;
+      return [idx.podsByNode.get(name) || NO_PODS, idx.nodeStats.get(name), owners[name],
+        xgmi ? xgmi[name] : undefined, links ? links[name] : undefined];
+    }
+    const cards = chunkedRows('node-cards', ctx.gpuNodes, [], function (n) {
+      const name = n.metadata.name;
+      const d = inputs(n);
+      const pods = d[0];
+      const stats = d[1];
+      const own = d[2];
+      const xg = d[3];
+      const lk = d[4];
       // own / xg / lk keep their identity while their content is unchanged
       // (ownersByNode + the metrics client's structural sharing).
-      memo('node-card:' + name, [n, pods, stats, own, xg, lk, age], function () {
+      return memo('node-card:' + name, [n, pods, stats, own, xg, lk], function () {
         const blocks = [kv(nodeCardRows(n, pods, stats, now))];
         const count = getNodeGpuCount(n);
         if (count > 0) {
@@ -512,9 +591,10 @@ export function nodesView(ctx, opts) {
           blocks.push(matrixBlock(getNodePhysicalGpuCount(n), xg, lk));
         }
         return section(name, blocks, n.metadata.uid || name);
-      })
-    );
-  }
+      }, now);
+    }, now, inputs);
+    return head.concat(cards);
+  }, now);
   return page(BRAND + ' — Nodes', refreshButton('Refresh node data', ctx.refreshing), items);
 }
 
@@ -534,8 +614,11 @@ function sameOwners(a, b) {
  * GPU list; a node's array keeps its identity while its owners are unchanged
  * (telemetry values change every scrape, GPU ownership rarely).
  */
+const NO_OWNERS = Object.freeze({});
+const NO_PODS = Object.freeze([]);
+
 function ownersByNode(metrics) {
-  if (!metrics || !metrics.gpus) return {};
+  if (!metrics || !metrics.gpus) return NO_OWNERS;
   if (ownersCache && ownersCache.has(metrics.gpus)) return ownersCache.get(metrics.gpus);
   const out = {};
   for (let i = 0; i < metrics.gpus.length; i++) {
@@ -642,20 +725,23 @@ function nodesHeadItems(ctx, now) {
       section('GPU Node Summary', [
         table(
           ['Node', 'Ready', 'GPU Model', 'GPU Devices', 'Allocation', 'GPU Pods', 'Age'],
-          ctx.gpuNodes.map(function (n) {
-            const st = idx.nodeStats[n.metadata.name];
-            const count = getNodeGpuCount(n);
-            const ready = isNodeReady(n);
-            return [
-              n.metadata.name,
-              status(ready ? 'success' : 'error', ready ? 'Ready' : 'Not Ready'),
-              formatGpuModel(getNodeGpuModel(n)),
-              count > 0 ? String(count) : '—',
-              allocationBar(st ? st.inUse : 0, (st && st.allocatable) || count),
-              String(st ? st.pods : 0),
-              formatAge(n.metadata.creationTimestamp, now),
-            ];
-          }),
+          chunkedRows('node-summary-rows', ctx.gpuNodes, [], function (n) {
+            const st = idx.nodeStats.get(n.metadata.name);
+            // Per-node stats keep their identity while unchanged (buildClusterIndex).
+            return nodeSummaryRows(n, [st], function () {
+              const count = getNodeGpuCount(n);
+              const ready = isNodeReady(n);
+              return [
+                n.metadata.name,
+                status(ready ? 'success' : 'error', ready ? 'Ready' : 'Not Ready'),
+                formatGpuModel(getNodeGpuModel(n)),
+                count > 0 ? String(count) : '—',
+                allocationBar(st ? st.inUse : 0, (st && st.allocatable) || count),
+                String(st ? st.pods : 0),
+                ageText(n.metadata.creationTimestamp, now),
+              ];
+            }, now);
+          }, now, function (n) { return [idx.nodeStats.get(n.metadata.name)]; }),
           ctx.gpuNodes.map(function (n) { return n.metadata.uid || n.metadata.name; })
         ),
       ])
@@ -694,9 +780,9 @@ export function podsView(ctx, opts) {
   const now = nowOf(opts);
   if (ctx.loading) return page(null, null, [loader('Loading GPU pod data...')]);
   const assign = opts && opts.metrics ? podGpuAssignments(opts.metrics) : null;
-  const items = memo('pods', [ctx.gpuPods, ctx.index, ctx.error, assign, ageKey(now)], function () {
+  const items = memo('pods', [ctx.gpuPods, ctx.index, ctx.error, assign], function () {
     return podsItems(ctx, now, assign);
-  });
+  }, now);
   return page(BRAND + ' — Pods', refreshButton('Refresh pod data', ctx.refreshing), items);
 }
 
@@ -717,18 +803,13 @@ function podsItems(ctx, now, assign) {
   }
 
   const ph = ctx.index.phases;
-  const pending = pods.filter(function (p) { return podPhase(p) === 'Pending'; });
+  const pending = ph.Pending > 0 ? chunkedFilter('pending-pods', pods, function (p) { return podFacts(p).phase === 'Pending'; }) : [];
   if (pods.length > 0) {
     const rows = [row('Total GPU Pods', String(pods.length))];
     if (ph.Running > 0) rows.push(row('Running', status('success', ph.Running)));
     if (ph.Pending > 0) rows.push(row('Pending', status('warning', ph.Pending)));
     if (ph.Failed > 0) rows.push(row('Failed', status('error', ph.Failed)));
-    let gpus = 0;
-    for (let i = 0; i < pods.length; i++) {
-      const phase = podPhase(pods[i]);
-      if (phase !== 'Succeeded' && phase !== 'Failed' && get(pods[i], ['spec', 'nodeName'], null)) gpus += getPodGpuCount(pods[i]);
-    }
-    rows.push(row('GPUs Held', String(gpus)));
+    rows.push(row('GPUs Held', String(ctx.index.totals.heldGpus)));
     items.push(section('Summary', [kv(rows)]));
 
     // With exporter pod labels, show which physical GPUs each pod holds.
@@ -739,15 +820,19 @@ function podsItems(ctx, now, assign) {
       section('All GPU Pods', [
         table(
           cols,
-          pods.map(function (p) {
-            const phase = podPhase(p);
-            const r = [
-              podName(p), podNs(p), podNode(p), status(phaseToStatus(phase), phase), gpuContainerLines(p),
-              restartsCell(p), formatAge(p.metadata.creationTimestamp, now),
-            ];
-            if (exact) r.splice(5, 0, assignedText(assign[(p.metadata.namespace || '') + '/' + p.metadata.name]));
-            return r;
-          }),
+          chunkedRows('pod-rows', pods, [exact, assign], function (p) {
+            // A pod's assignment keeps its identity while its GPUs are unchanged (podGpuAssignments).
+            const gs = exact ? assign[(p.metadata.namespace || '') + '/' + p.metadata.name] : undefined;
+            return podRows(p, [exact, gs], function () {
+              const phase = podPhase(p);
+              const r = [
+                podName(p), podNs(p), podNode(p), status(phaseToStatus(phase), phase), gpuContainerLines(p),
+                restartsCell(p), ageText(p.metadata.creationTimestamp, now),
+              ];
+              if (exact) r.splice(5, 0, assignedText(gs));
+              return r;
+            }, now);
+          }, now),
           pods.map(function (p) { return p.metadata.uid || (p.metadata.namespace + '/' + p.metadata.name); })
         ),
       ])
@@ -760,7 +845,9 @@ function podsItems(ctx, now, assign) {
         table(
           ['Name', 'Namespace', 'GPU Resources', 'Waiting Reason', 'Age'],
           pending.map(function (p) {
-            return [podName(p), podNs(p), formatPodGpuRequests(p), podWaitingReason(p) || '—', formatAge(p.metadata.creationTimestamp, now)];
+            return pendingRows(p, [], function () {
+              return [podName(p), podNs(p), formatPodGpuRequests(p), podWaitingReason(p) || '—', ageText(p.metadata.creationTimestamp, now)];
+            }, now);
           })
         ),
       ])
@@ -983,7 +1070,7 @@ export function nodeDetailView(resource, ctx, opts) {
   const name = raw.metadata.name;
   let podsOnNode;
   if (ctx.loading) podsOnNode = [];
-  else if (ctx.index && ctx.index.podsByNode && ctx.index.podsByNode[name]) podsOnNode = ctx.index.podsByNode[name];
+  else if (ctx.index && ctx.index.podsByNode && ctx.index.podsByNode.get(name)) podsOnNode = ctx.index.podsByNode.get(name);
   else podsOnNode = ctx.gpuPods.filter(function (p) { return get(p, ['spec', 'nodeName'], null) === name; });
   const metrics = opts && opts.metrics ? opts.metrics : null;
   const own = ownersByNode(metrics)[name];

@@ -383,13 +383,13 @@ describe('buildClusterIndex', () => {
     expect(idx.totals.allocatable).toBe(15);
   });
   it('counts GPUs held by bound non-terminal pods', () => {
-    expect(idx.nodeStats.n0.inUse).toBe(6);
-    expect(idx.nodeStats.n1.inUse).toBe(0);
+    expect(idx.nodeStats.get('n0').inUse).toBe(6);
+    expect(idx.nodeStats.get('n1').inUse).toBe(0);
     expect(idx.totals.inUse).toBe(6);
   });
   it('indexes pods by node', () => {
-    expect(idx.podsByNode.n0.map((p) => p.metadata.name)).toEqual(['a', 'b']);
-    expect(idx.nodeStats.n1.pods).toBe(1);
+    expect(idx.podsByNode.get('n0').map((p) => p.metadata.name)).toEqual(['a', 'b']);
+    expect(idx.nodeStats.get('n1').pods).toBe(1);
   });
   it('counts phases including unbound pods', () => {
     expect(idx.phases).toEqual({ Running: 1, Pending: 2, Succeeded: 1, Failed: 0, Other: 0 });

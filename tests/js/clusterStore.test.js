@@ -77,7 +77,7 @@ describe('createClusterStore', () => {
     const s = store.getSnapshot();
     expect(s.gpuNodes.map((n) => n.metadata.name)).toEqual(['g0']);
     expect(s.gpuPods.map((p) => p.metadata.name)).toEqual(['p0']);
-    expect(s.index.nodeStats.g0.inUse).toBe(1);
+    expect(s.index.nodeStats.get('g0').inUse).toBe(1);
   });
 
   it('issues the CRD and every plugin-pod query concurrently', async () => {

@@ -46,10 +46,36 @@ describe('view memoisation', () => {
     expect(b.refresh.label).toBe('Refreshing…');
   });
 
-  it('recomputes when the age clock ticks a second', () => {
-    const ctx = makeContext({ nodes: [makeGpuNode('g0')] });
+  it('recomputes when an age label it shows changes, not on every clock tick', () => {
+    // A running pod started 10 s ago: "10s" turns "11s" one second later.
+    const young = makeGpuPod('a', { node: 'g0' });
+    young.metadata.creationTimestamp = new Date(NOW - 10000).toISOString();
+    const ctx = makeContext({ nodes: [makeGpuNode('g0')], pods: [young] });
     const a = overviewView(ctx, { now: NOW });
-    expect(overviewView(ctx, { now: NOW + 1000 }).items).not.toBe(a.items);
+    expect(overviewView(ctx, { now: NOW + 500 }).items).toBe(a.items);
+    const b = overviewView(ctx, { now: NOW + 1000 });
+    expect(b.items).not.toBe(a.items);
+    expect(JSON.stringify(b)).toContain('"11s"');
+  });
+
+  it('holds a section whose ages only show hours until the next hour of age', () => {
+    // Node and pods an hour old or more: no label changes for a while.
+    const old = makeGpuPod('a', { node: 'g0' });
+    old.metadata.creationTimestamp = new Date(NOW - 3600 * 1000).toISOString();
+    const ctx = makeContext({ nodes: [makeGpuNode('g0')], pods: [old] });
+    const a = podsView(ctx, { now: NOW });
+    expect(podsView(ctx, { now: NOW + 59 * 60 * 1000 }).items).toBe(a.items);
+    const b = podsView(ctx, { now: NOW + 3600 * 1000 });
+    expect(b.items).not.toBe(a.items);
+    expect(JSON.stringify(b)).toContain('"2h"');
+  });
+
+  it('does not reuse a section for an earlier clock', () => {
+    const young = makeGpuPod('a', { node: 'g0' });
+    young.metadata.creationTimestamp = new Date(NOW - 10000).toISOString();
+    const ctx = makeContext({ nodes: [makeGpuNode('g0')], pods: [young] });
+    const a = podsView(ctx, { now: NOW });
+    expect(podsView(ctx, { now: NOW - 2000 }).items).not.toBe(a.items);
   });
 
   it('recomputes when the pod list changes', () => {

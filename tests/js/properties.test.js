@@ -97,8 +97,8 @@ describe('properties', () => {
       let inUse = 0;
       let cap = 0;
       for (const n of names) {
-        inUse += idx.nodeStats[n].inUse;
-        cap += idx.nodeStats[n].capacity;
+        inUse += idx.nodeStats.get(n).inUse;
+        cap += idx.nodeStats.get(n).capacity;
       }
       expect(idx.totals.inUse).toBe(inUse);
       expect(idx.totals.capacity).toBe(cap);

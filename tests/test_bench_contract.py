@@ -91,3 +91,26 @@ def test_detail_pages_cost_one_node_of_telemetry_whatever_the_cluster_size():
     # The GPU Pods page asks for pod attribution only: one series per allocated GPU.
     assert out[16]["podsPageOwners"]["requests"] == 1
     assert out[16]["podsPageOwners"]["bytes"] < 0.1 * out[16]["podClusterWide"]["bytes"], out
+
+
+def test_watch_churn_stress_is_incremental():
+    # bench/stress.js: the store + all five view-models per pod watch event
+    # against a replay of the reference's full recompute. Both agree on the
+    # cluster; most GPU-pod events patch the index instead of rebuilding it;
+    # per-event cost grows far slower than the pod count.
+    out = os.path.join(ROOT, "gpurun_out", "test_stress.json")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    r = subprocess.run(["node", "--expose-gc", "bench/stress.js", "--nodes", "16,128", "--events", "300",
+                        "--out", out], cwd=ROOT, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    pts = json.load(open(out))["points"]
+    for p in pts:
+        assert p["consistent"], p
+        assert p["amd"]["p50"] < p["reference"]["p50"], p
+        c = p["storeCounters"]
+        assert c["indexPatches"] > 5 * c["indexBuilds"], c
+        # Only changed pods are classified: initial list + about one per event.
+        assert c["pods"]["classified"] < p["pods"] + 2 * p["events"], c
+    small, big = pts
+    assert big["pods"] > 7 * small["pods"]
+    assert big["amd"]["p50"] < 4 * small["amd"]["p50"] + 0.05, (small["amd"], big["amd"])

@@ -2,6 +2,14 @@
 """Scaling curve + BASELINE configs: run bench.py per point and tabulate.
 
     python tools/sweep.py --out gpurun_out/sweep [--steps 30] [--rtt-ms 20]
+    python tools/sweep.py --stress --out gpurun_out/stress [--stress-nodes 16,64,256,1000] [--events 1000]
+
+``--stress``: the cluster-size axis under watch churn (bench/stress.js) —
+16/64/256/1000 GPU nodes × 8, 30 plain pods per node, 50 pod watch events/s —
+per delivery mode (identity / rewrapped / reparsed): CPU ms per event for the
+shipped store + all five page view-models vs a replay of the reference's
+per-event recompute, per event kind, heap growth and list bytes. Writes
+``stress.json`` and ``stress.md``.
 
 Points: synthetic clusters of 1, 2, 4 and 8 nodes × 8 MI355X (one process,
 ``--nodes N``) and the five BASELINE.json presets. Writes ``sweep.json`` and
@@ -68,6 +76,48 @@ def table(rows):
     return md
 
 
+MODES = ["identity", "rewrapped", "reparsed"]
+KINDS = ["modified", "gpu-modified", "added", "gpu-added", "deleted", "gpu-deleted"]
+
+
+def stress(args):
+    os.makedirs(args.out, exist_ok=True)
+    res = {}
+    for mode in MODES:
+        out = os.path.join(args.out, f"stress_{mode}.json")
+        cmd = ["node", "--expose-gc", os.path.join(ROOT, "bench", "stress.js"), "--nodes", args.stress_nodes,
+               "--events", str(args.events), "--rate", "50", "--mode", mode, "--out", out]
+        r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=1800)
+        if r.returncode != 0:
+            raise RuntimeError(f"{' '.join(cmd)} failed:\n{r.stderr[-3000:]}")
+        print(r.stderr.strip(), flush=True)
+        res[mode] = json.load(open(out))
+    with open(os.path.join(args.out, "stress.json"), "w") as f:
+        json.dump(res, f, indent=1)
+    md = ["| Delivery | GPU nodes | Pods | Events | New p50 / p95 / mean (ms) | Reference replay p50 / p95 (ms) | "
+          "p50 speed-up | Index rebuilds / patches | Heap growth (MB) | Pod list (MB) |",
+          "|---|---:|---:|---:|---|---|---:|---|---:|---:|"]
+    for mode in MODES:
+        for p in res[mode]["points"]:
+            a, ref = p["amd"], p["reference"]
+            c = p["storeCounters"]
+            md.append(f"| {mode} | {p['nodes']} | {p['pods']} | {p['events']} | {a['p50']:.3f} / {a['p95']:.3f} / "
+                      f"{a['mean']:.3f} | {ref['p50']:.2f} / {ref['p95']:.2f} | {ref['p50'] / a['p50']:.0f}× | "
+                      f"{c['indexBuilds']} / {c['indexPatches']} | {p['heapGrowthBytes'] / 1e6:.1f} | "
+                      f"{p['podListBytes'] / 1e6:.1f} |")
+    md += ["", "Per event kind, identity delivery (new p50 / p95 ms):", "",
+           "| GPU nodes | " + " | ".join(KINDS) + " |", "|---:|" + "---|" * len(KINDS)]
+    for p in res["identity"]["points"]:
+        cells = []
+        for k in KINDS:
+            v = p["amdByKind"].get(k)
+            cells.append(f"{v['p50']:.3f} / {v['p95']:.3f} (n={v['n']})" if v else "—")
+        md.append(f"| {p['nodes']} | " + " | ".join(cells) + " |")
+    with open(os.path.join(args.out, "stress.md"), "w") as f:
+        f.write("\n".join(md) + "\n")
+    print("\n".join(md))
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--out", default="gpurun_out/sweep")
@@ -75,7 +125,12 @@ def main():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--rtt-ms", type=float, default=20.0)
     p.add_argument("--extra", default="")
+    p.add_argument("--stress", action="store_true", help="watch-churn stress of the cluster-size axis instead")
+    p.add_argument("--stress-nodes", default="16,64,256,1000")
+    p.add_argument("--events", type=int, default=1000)
     args = p.parse_args()
+    if args.stress:
+        return stress(args)
     os.makedirs(args.out, exist_ok=True)
     rows = []
     for kind, val in POINTS:
