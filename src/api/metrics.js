@@ -676,6 +676,8 @@ export function createMetricsSource(opts) {
         links: same ? shareMap(last.links, joined.links || {}) : joined.links || {},
         fetchedAt: new Date(clock.now()).toISOString(),
         prometheusPath: base,
+        // The PromQL this snapshot came from (Metrics page "Query" row).
+        query: q,
       };
       return last;
     });

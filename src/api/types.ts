@@ -271,6 +271,8 @@ export interface GpuMetrics {
   fetchedAt: string;
   stale?: boolean;
   prometheusPath: string;
+  /** PromQL the snapshot came from (Metrics page "Query" row). */
+  query?: string;
   /** PromQL of the main telemetry query (shown on the Metrics page) */
   query?: string;
 }

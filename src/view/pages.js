@@ -954,13 +954,14 @@ export function metricsView(ctx, mstate, opts) {
           row('Avg GFX Activity', pctText(sum.avgGfxActivityPct)),
         ].concat(sum.eccUncorrectable === null ? [] : [row('RAS Errors', eccCell(sum))], [
           row('Source', m.source === 'amd-exporter' ? 'AMD Device Metrics Exporter' : 'node-exporter (amdgpu hwmon + DRM)'),
+          // Browser-local time, as the reference shows it (MetricsPage.tsx:336-338).
           row(
             'Last Fetched',
             m.stale
-              ? status('warning', new Date(m.fetchedAt).toISOString().slice(11, 19) + ' UTC (stale: the latest refresh failed)')
-              : new Date(m.fetchedAt).toISOString().slice(11, 19) + ' UTC'
+              ? status('warning', new Date(m.fetchedAt).toLocaleTimeString() + ' (stale: the latest refresh failed)')
+              : new Date(m.fetchedAt).toLocaleTimeString()
           ),
-        ])),
+        ], m.query ? [row('Query', m.query)] : [])),
       ])
     );
 

@@ -106,6 +106,14 @@ describe('fetchGpuMetrics', () => {
     expect(m.gpus.find((x) => x.nodeName === 'a' && x.gpu === '5').powerWatts).toBe(705);
     expect(m.gpus.find((x) => x.nodeName === 'b' && x.gpu === '5').powerWatts).toBe(111);
   });
+  it('records the PromQL it sent with the snapshot (Metrics page "Query" row)', async () => {
+    const request = prom({ data: exporterData(['n0']) });
+    const src = createMetricsSource({ request });
+    const m = await src.fetchGpuMetrics();
+    const sent = request.mock.calls.map((c) => c[0]).filter((u) => u.indexOf('/api/v1/query?query=') >= 0 && !/query=1$/.test(u));
+    expect(sent.map((u) => decodeURIComponent(u.split('query=')[1]))).toContain(m.query);
+    expect(m.query).toContain('gpu_power_usage');
+  });
   it('captures pod ownership labels', async () => {
     const src = createMetricsSource({ request: prom() });
     const m = await src.fetchGpuMetrics();

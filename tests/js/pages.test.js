@@ -431,6 +431,14 @@ describe('metricsView', () => {
     expect(rowValue(s, 'Total Power').color).toBe('#d32f2f');
     expect(rowValue(s, 'Source')).toBe('AMD Device Metrics Exporter');
   });
+  it('shows Last Fetched in browser-local time and the PromQL it ran (reference MetricsPage.tsx:336-343)', () => {
+    const m = Object.assign(metrics(['n0'], 1), { query: 'max by (hostname, gpu_id) ({__name__=~"gpu_power_usage"})' });
+    const s = findSection(metricsView(ctx, { metrics: m, fetchError: null, fetching: false }, opts), 'GPU Power Summary');
+    expect(rowValue(s, 'Last Fetched')).toBe(new Date(NOW).toLocaleTimeString());
+    expect(rowValue(s, 'Query')).toBe(m.query);
+    const stale = findSection(metricsView(ctx, { metrics: Object.assign({}, m, { stale: true }), fetchError: null, fetching: false }, opts), 'GPU Power Summary');
+    expect(rowValue(stale, 'Last Fetched').text).toBe(new Date(NOW).toLocaleTimeString() + ' (stale: the latest refresh failed)');
+  });
   it('renders one card per node with a per-GPU table', () => {
     const vm = metricsView(ctx, { metrics: metrics(['n0', 'n1'], 8), fetchError: null, fetching: false }, opts);
     const s = findSection(vm, 'n1 — 8 × MI355X');
