@@ -125,6 +125,8 @@ function emptyGpu(nodeName, gpu, instance) {
     powerWatts: null, powerCapWatts: null, vramUsedBytes: null, vramTotalBytes: null,
     gfxActivityPct: null, memActivityPct: null, tempC: null, tempSlowdownC: null,
     eccCorrectable: null, eccUncorrectable: null, pod: null, namespace: null,
+    // The cap is the MI355X board limit because the source reported none.
+    powerCapAssumed: false,
   };
 }
 
@@ -175,7 +177,12 @@ export function joinExporterResults(r) {
   const gpus = [];
   for (const k in map) {
     const g = map[k];
-    if (g.powerCapWatts === null) g.powerCapWatts = MI355X.tdpWatts;
+    if (g.powerCapWatts === null) {
+      // The stock Device Metrics Exporter has no cap series: every GPU is an
+      // MI355X, so bars use its board limit, flagged as assumed.
+      g.powerCapWatts = MI355X.tdpWatts;
+      g.powerCapAssumed = true;
+    }
     gpus.push(g);
   }
   gpus.sort(byNodeGpu);
@@ -311,7 +318,7 @@ function isExporterName(name) {
 }
 
 /** Fields of GpuTelemetry that come from the static series (see exporterNames). */
-export const STATIC_GPU_FIELDS = ['powerCapWatts', 'vramTotalBytes', 'tempSlowdownC', 'instance'];
+export const STATIC_GPU_FIELDS = ['powerCapWatts', 'powerCapAssumed', 'vramTotalBytes', 'tempSlowdownC', 'instance'];
 
 /**
  * @param {boolean} [withStatic]  include the static series (default true)
@@ -911,8 +918,12 @@ export function summarizeMetrics(m) {
   let eccGpus = 0;
   let eccUncorrectable = 0;
   let eccCorrectable = 0;
+  let capAssumed = 0;
+  let tempLimitAssumed = 0;
   for (let i = 0; i < m.gpus.length; i++) {
     const g = m.gpus[i];
+    if (g.powerCapAssumed) capAssumed++;
+    if (g.tempC !== null && g.tempC !== undefined && !(g.tempSlowdownC > 0)) tempLimitAssumed++;
     if (g.eccUncorrectable !== null && g.eccUncorrectable !== undefined) {
       eccGpus++;
       eccUncorrectable += g.eccUncorrectable;
@@ -941,5 +952,9 @@ export function summarizeMetrics(m) {
     // RAS totals over the GPUs that report them (null: no GPU does, e.g. node-exporter)
     eccCorrectable: eccGpus ? eccCorrectable : null,
     eccUncorrectable: eccGpus ? eccUncorrectable : null,
+    // GPUs whose power cap / throttle threshold is the MI355X platform value
+    // because the source reports none (stock exporter, node-exporter).
+    powerCapAssumed: capAssumed,
+    tempLimitAssumed: tempLimitAssumed,
   };
 }

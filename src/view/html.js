@@ -12,6 +12,8 @@
  * (src/components/View.tsx).
  */
 
+import { matrixCaption } from './ir.js';
+
 const NEEDS_ESC = /[&<>"]/;
 
 function esc(s) {
@@ -83,7 +85,9 @@ function renderBlock(b) {
       );
     case 'matrix': {
       const m = b.matrix;
-      let h = '<table data-testid="xgmi-matrix" data-full-mesh="' + (b.fullMesh ? 'true' : 'false') + '"><thead><tr><th></th>';
+      let h = '<table data-testid="xgmi-matrix" data-full-mesh="' + (b.fullMesh ? 'true' : 'false') + '" data-topology="' +
+        (b.measuredTopology ? 'measured' : 'assumed') + '" data-throughput="' + (b.measuredThroughput ? 'measured' : 'none') +
+        '"><caption>' + esc(matrixCaption(b)) + '</caption><thead><tr><th></th>';
       for (let j = 0; j < m.size; j++) h += '<th>GPU ' + j + '</th>';
       h += '</tr></thead><tbody>';
       for (let i = 0; i < m.size; i++) {

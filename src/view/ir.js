@@ -157,6 +157,26 @@ export function createObjectCache() {
 }
 
 // ---------------------------------------------------------------------------
+// Shared captions (React, HTML and text renderers)
+// ---------------------------------------------------------------------------
+
+/** Caption of the xGMI matrix: says whether the link topology was measured or is the platform model. */
+export function matrixCaption(b) {
+  const m = b.matrix;
+  const peak = m.size > 1 ? ' ' + m.cells[0][1].peakGBs : '';
+  const kind = b.measuredTopology
+    ? 'measured'
+    : b.measuredThroughput
+      ? 'assumed MI355X full mesh; link throughput measured'
+      : 'assumed MI355X full mesh';
+  return (
+    'xGMI topology (' + kind + ') — ' +
+    (b.fullMesh ? 'full mesh, ' + m.linksPerGpu + ' links/GPU' : 'partial') +
+    ' · ' + m.linksPerGpu + '×' + peak + ' GB/s per GPU · ring collectives bound at ' + m.ringBusGBs + ' GB/s per link'
+  );
+}
+
+// ---------------------------------------------------------------------------
 // Query helpers (tests, benchmark row counting)
 // ---------------------------------------------------------------------------
 

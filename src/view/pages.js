@@ -516,7 +516,17 @@ export function slotsBlock(node, podsOnNode, owners) {
 export function matrixBlock(gpuCount, measured, probed) {
   const hasProbe = !!probed && Object.keys(probed).length > 0;
   const m = buildXgmiMatrix(gpuCount, measured, hasProbe ? probed : undefined);
-  return { t: 'matrix', matrix: m, fullMesh: isFullMesh(m), measuredTopology: hasProbe };
+  return {
+    t: 'matrix',
+    matrix: m,
+    fullMesh: isFullMesh(m),
+    // Link types / hops come from the exporter's gpu_xgmi_link_hops (this
+    // repo's amdgpu-exporter); without them the matrix is the MI355X
+    // platform model, and only per-link throughput (stock exporter
+    // xgmi_neighbor_*_tx_throughput) is measured.
+    measuredTopology: hasProbe,
+    measuredThroughput: !!measured && Object.keys(measured).length > 0,
+  };
 }
 
 function nodeCardRows(node, podsOnNode, stats, now) {
@@ -954,6 +964,7 @@ export function metricsView(ctx, mstate, opts) {
           row('Avg GFX Activity', pctText(sum.avgGfxActivityPct)),
         ].concat(sum.eccUncorrectable === null ? [] : [row('RAS Errors', eccCell(sum))], [
           row('Source', m.source === 'amd-exporter' ? 'AMD Device Metrics Exporter' : 'node-exporter (amdgpu hwmon + DRM)'),
+        ], limitsRows(sum), [
           // Browser-local time, as the reference shows it (MetricsPage.tsx:336-338).
           row(
             'Last Fetched',
@@ -999,6 +1010,20 @@ export function metricsView(ctx, mstate, opts) {
  * (exporter-reported, else the MI355X's 100 °C): warning within 10 °C of
  * it, error at or above it.
  */
+/** Says which limits are MI355X platform values because the source reports none. */
+function limitsRows(sum) {
+  const parts = [];
+  if (sum.powerCapAssumed > 0) {
+    parts.push('power cap ' + formatWatts(MI355X.tdpWatts) + ' (MI355X board limit; no gpu_power_cap series for ' +
+      sum.powerCapAssumed + ' of ' + sum.gpus + ' GPUs)');
+  }
+  if (sum.tempLimitAssumed > 0) {
+    parts.push('throttle threshold ' + MI355X.junctionSlowdownC + ' °C (MI355X; no gpu_junction_temperature_slowdown series for ' +
+      sum.tempLimitAssumed + ' of ' + sum.gpus + ' GPUs)');
+  }
+  return parts.length ? [row('Assumed Limits', status('warning', parts.join('; ')))] : [];
+}
+
 export function tempCell(g) {
   if (g.tempC === null || g.tempC === undefined) return '—';
   const limit = g.tempSlowdownC > 0 ? g.tempSlowdownC : MI355X.junctionSlowdownC;

@@ -25,6 +25,7 @@
  */
 
 import { BAR_COLORS } from '../api/amdgpu.js';
+import { matrixCaption } from './ir.js';
 
 /** CommonComponents the renderer needs (reference src/components/OverviewPage.tsx:8-16). */
 export const REQUIRED_COMPONENTS = [
@@ -84,21 +85,7 @@ export function matrixCellColor(c) {
   return c.kind === 'xgmi' ? 'rgba(237, 28, 36, 0.08)' : BAR_COLORS.track;
 }
 
-/** Caption of the xGMI matrix: says whether the link topology was measured or is the platform model. */
-export function matrixCaption(b) {
-  const m = b.matrix;
-  const peak = m.size > 1 ? ' ' + m.cells[0][1].peakGBs : '';
-  const kind = b.measuredTopology
-    ? 'measured'
-    : b.measuredThroughput
-      ? 'assumed MI355X full mesh; link throughput measured'
-      : 'assumed MI355X full mesh';
-  return (
-    'xGMI topology (' + kind + ') — ' +
-    (b.fullMesh ? 'full mesh, ' + m.linksPerGpu + ' links/GPU' : 'partial') +
-    ' · ' + m.linksPerGpu + '×' + peak + ' GB/s per GPU · ring collectives bound at ' + m.ringBusGBs + ' GB/s per link'
-  );
-}
+export { matrixCaption };
 
 /**
  * @param {{createElement: Function, memo: Function, Fragment: any}} React

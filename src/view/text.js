@@ -8,6 +8,8 @@
  * the xGMI matrix a small grid. Optional ANSI colour for statuses.
  */
 
+import { matrixCaption } from './ir.js';
+
 const MARK = { success: '✓', warning: '!', error: '✗' };
 const ANSI = { success: '\u001b[32m', warning: '\u001b[33m', error: '\u001b[31m', reset: '\u001b[0m' };
 
@@ -81,8 +83,7 @@ function blockLines(b, color) {
     }
     case 'matrix': {
       const m = b.matrix;
-      out.push('  xGMI (' + (b.measuredTopology ? 'measured' : 'MI355X platform model') + '): ' +
-        (b.fullMesh ? 'full mesh, ' + m.linksPerGpu + ' links/GPU' : 'partial') + ', ring bus ' + m.ringBusGBs + ' GB/s per link');
+      out.push('  ' + matrixCaption(b));
       m.cells.forEach(function (row, i) {
         out.push('    ' + pad('GPU ' + i, 6) + row.map(function (c) {
           const v = c.kind === 'self' ? '-' : c.measuredGBs !== null ? String(Math.round(c.measuredGBs))

@@ -8,24 +8,9 @@ import fs from 'fs';
 import path from 'path';
 import { SERIES, joinExporterResults, splitByName } from '../../src/api/metrics.js';
 import { MI355X, formatBytes, shortProductName } from '../../src/api/amdgpu.js';
+import { parseExposition } from './promFake.js';
 
 const DIR = path.join(process.cwd(), 'tests', 'fixtures', 'mi355x');
-
-/** Prometheus text exposition → instant-vector rows, as /api/v1/query returns them. */
-function parseExposition(text) {
-  const rows = [];
-  text.split('\n').forEach((line) => {
-    if (!line || line[0] === '#') return;
-    const m = /^([a-zA-Z_:][a-zA-Z0-9_:]*)(\{(.*)\})?\s+(\S+)$/.exec(line);
-    if (!m) return;
-    const metric = { __name__: m[1] };
-    const re = /([a-zA-Z_][a-zA-Z0-9_]*)="((?:[^"\\]|\\.)*)"/g;
-    let l;
-    while ((l = re.exec(m[3] || '')) !== null) metric[l[1]] = l[2];
-    rows.push({ metric, value: [1760000000, m[4]] });
-  });
-  return rows;
-}
 
 function load(name) {
   return fs.readFileSync(path.join(DIR, name), 'utf8');

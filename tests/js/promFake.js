@@ -10,6 +10,22 @@ import { PROMETHEUS_SERVICES, SERIES, servicePath } from '../../src/api/metrics.
 export const BASE0 = servicePath(PROMETHEUS_SERVICES[0]);
 export const BASE1 = servicePath(PROMETHEUS_SERVICES[1]);
 
+/** Prometheus text exposition → instant-vector rows, as /api/v1/query returns them. */
+export function parseExposition(text) {
+  const rows = [];
+  text.split('\n').forEach((line) => {
+    if (!line || line[0] === '#') return;
+    const m = /^([a-zA-Z_:][a-zA-Z0-9_:]*)(\{(.*)\})?\s+(\S+)$/.exec(line);
+    if (!m) return;
+    const metric = { __name__: m[1] };
+    const re = /([a-zA-Z_][a-zA-Z0-9_]*)="((?:[^"\\]|\\.)*)"/g;
+    let l;
+    while ((l = re.exec(m[3] || '')) !== null) metric[l[1]] = l[2];
+    rows.push({ metric, value: [1760000000, m[4]] });
+  });
+  return rows;
+}
+
 export function vec(metric, v) {
   return { metric, value: [1760000000, String(v)] };
 }

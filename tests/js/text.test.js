@@ -33,7 +33,7 @@ describe('text renderer', () => {
     expect(t.indexOf('# AMD GPU — Nodes')).toBe(0);
     expect(t).toContain('GPU Node Summary');
     expect(t).toContain('0:p  1:p  2:-');
-    expect(t).toContain('xGMI (MI355X platform model): full mesh, 7 links/GPU');
+    expect(t).toContain('xGMI topology (assumed MI355X full mesh) — full mesh, 7 links/GPU');
     expect(t).toContain('    GPU 0    -   x   x');
   });
   it('renders detail sections', () => {
