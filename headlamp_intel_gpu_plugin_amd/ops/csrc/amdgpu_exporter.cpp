@@ -7,32 +7,51 @@
 // it uses for the AMD Device Metrics Exporter (src/api/metrics.js SERIES).
 //
 //   amdgpu-exporter [--port 9400] [--bind 0.0.0.0] [--hostname NAME]
-//                   [--device N [--gpu-label L]] [--no-topology] [--once]
+//                   [--device N [--gpu-label L]] [--no-topology] [--sysfs-only] [--once]
 //
 // --hostname defaults to $NODE_NAME (set from the downward API in a
 // DaemonSet), then gethostname(). --once prints one scrape and exits (used by
 // tests and for debugging). Endpoints: GET /metrics, GET /healthz.
 //
-// Single-threaded accept loop: a scrape every few seconds from one Prometheus
-// needs nothing more, and sampling sysfs is cheap (~100 µs per GPU). Every
-// request is answered or dropped within a bounded read timeout, SIGINT /
-// SIGTERM stop the loop cleanly.
+// --sysfs-only never starts the HIP runtime: devices come from the DRM cards
+// in sysfs and xGMI links from the KFD topology where it is readable
+// (probe_core.h), so the exporter needs no device node and runs unprivileged
+// with /sys mounted read-only (deploy/exporter/daemonset.yaml).
+//
+// Serving: the accept loop hands connections to a few worker threads through
+// a bounded queue (full → the connection is closed at once). Each connection
+// has ONE deadline for the whole request (kRequestDeadlineMs, enforced with
+// poll() on every read) and a send timeout, so a client that trickles bytes
+// or stops reading holds one worker for at most a few seconds and never the
+// /healthz probe or the Prometheus scrape behind it. SIGINT / SIGTERM stop
+// the loop and the workers cleanly.
 
 #include <arpa/inet.h>
 #include <netinet/in.h>
+#include <poll.h>
 #include <signal.h>
 #include <sys/socket.h>
 #include <sys/time.h>
 
 #include <atomic>
 #include <cerrno>
+#include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "probe_core.h"
 
 namespace {
 
 std::atomic<bool> g_stop{false};
+
+constexpr int kRequestDeadlineMs = 3000;  // whole request: headers in, response out
+constexpr int kWorkers = 4;
+constexpr size_t kMaxQueued = 64;
 
 void on_signal(int) { g_stop.store(true); }
 
@@ -82,11 +101,13 @@ bool parse_args(int argc, char** argv, Args* a) {
       a->render.gpu_label = v;
     } else if (k == "--no-topology") {
       a->render.topology = false;
+    } else if (k == "--sysfs-only") {
+      a->render.sysfs_only = true;
     } else if (k == "--once") {
       a->once = true;
     } else if (k == "--help" || k == "-h") {
       std::printf("usage: amdgpu-exporter [--port 9400] [--bind ADDR] [--hostname NAME] [--device N [--gpu-label L]] "
-                  "[--no-topology] [--once]\n");
+                  "[--no-topology] [--sysfs-only] [--once]\n");
       std::exit(0);
     } else {
       std::fprintf(stderr, "unknown argument %s\n", k.c_str());
@@ -115,12 +136,25 @@ void respond(int fd, int code, const char* reason, const std::string& type, cons
   send_all(fd, h + body);
 }
 
+using Clock = std::chrono::steady_clock;
+
+int remaining_ms(Clock::time_point deadline) {
+  const auto left = std::chrono::duration_cast<std::chrono::milliseconds>(deadline - Clock::now()).count();
+  return left > 0 ? static_cast<int>(left) : 0;
+}
+
 void handle(int fd, const Args& a) {
-  timeval tv{2, 0};
-  setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+  const Clock::time_point deadline = Clock::now() + std::chrono::milliseconds(kRequestDeadlineMs);
+  // A peer that stops reading cannot hold the worker past the deadline either.
+  timeval stv{kRequestDeadlineMs / 1000, 0};
+  setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &stv, sizeof(stv));
   std::string req;
   char buf[2048];
   while (req.find("\r\n\r\n") == std::string::npos && req.size() < 16384) {
+    // One deadline for the whole header, however slowly the bytes arrive.
+    pollfd p{fd, POLLIN, 0};
+    const int wait = remaining_ms(deadline);
+    if (wait <= 0 || poll(&p, 1, wait) <= 0) return;
     ssize_t n = recv(fd, buf, sizeof(buf), 0);
     if (n <= 0) return;
     req.append(buf, static_cast<size_t>(n));
@@ -138,7 +172,15 @@ void handle(int fd, const Args& a) {
   if (method != "GET") {
     respond(fd, 405, "Method Not Allowed", "text/plain", "GET only\n");
   } else if (path == "/metrics") {
-    respond(fd, 200, "OK", "text/plain; version=0.0.4", amdprobe::render(a.render));
+    std::string body;
+    {
+      // The probe keeps process-wide state (error text, HIP handles): one
+      // scrape renders at a time; /healthz never waits for it.
+      static std::mutex render_mu;
+      std::lock_guard<std::mutex> lk(render_mu);
+      body = amdprobe::render(a.render);
+    }
+    respond(fd, 200, "OK", "text/plain; version=0.0.4", body);
   } else if (path == "/healthz") {
     respond(fd, 200, "OK", "text/plain", "ok\n");
   } else {
@@ -146,12 +188,51 @@ void handle(int fd, const Args& a) {
   }
 }
 
+// Accepted connections waiting for a worker.
+class ConnQueue {
+ public:
+  bool push(int fd) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (q_.size() >= kMaxQueued) return false;
+    q_.push_back(fd);
+    cv_.notify_one();
+    return true;
+  }
+  // Next connection, or -1 once stopped.
+  int pop() {
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait(lk, [&] { return stopped_ || !q_.empty(); });
+    if (q_.empty()) return -1;
+    const int fd = q_.front();
+    q_.pop_front();
+    return fd;
+  }
+  void stop() {
+    std::lock_guard<std::mutex> lk(mu_);
+    stopped_ = true;
+    cv_.notify_all();
+  }
+  void drain() {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (int fd : q_) close(fd);
+    q_.clear();
+  }
+
+ private:
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<int> q_;
+  bool stopped_ = false;
+};
+
 }  // namespace
 
 int main(int argc, char** argv) {
   Args a;
   if (!parse_args(argc, argv, &a)) return 2;
-  if (!amdprobe::init_hip()) {
+  if (a.render.sysfs_only) {
+    std::fprintf(stderr, "amdgpu-exporter: sysfs-only (no HIP runtime)\n");
+  } else if (!amdprobe::init_hip()) {
     // No device is not fatal: the exporter still answers (with no GPU series),
     // which is what the plugin's "No AMD GPU Metrics" state expects.
     std::fprintf(stderr, "amdgpu-exporter: %s\n", amdprobe::g_error.c_str());
@@ -182,9 +263,20 @@ int main(int argc, char** argv) {
   }
   socklen_t len = sizeof(addr);
   getsockname(srv, reinterpret_cast<sockaddr*>(&addr), &len);
-  std::printf("amdgpu-exporter listening on %s:%d (%d GPU%s, hostname %s)\n", a.bind.c_str(), ntohs(addr.sin_port),
-              amdprobe::g_count, amdprobe::g_count == 1 ? "" : "s", a.render.hostname.c_str());
+  const int gpus = a.render.sysfs_only ? static_cast<int>(amdprobe::sysfs_gpu_bdfs().size()) : amdprobe::g_count;
+  std::printf("amdgpu-exporter listening on %s:%d (%d GPU%s, hostname %s%s)\n", a.bind.c_str(), ntohs(addr.sin_port),
+              gpus, gpus == 1 ? "" : "s", a.render.hostname.c_str(), a.render.sysfs_only ? ", sysfs-only" : "");
   std::fflush(stdout);
+  ConnQueue queue;
+  std::vector<std::thread> workers;
+  for (int i = 0; i < kWorkers; ++i) {
+    workers.emplace_back([&] {
+      for (int fd = queue.pop(); fd >= 0; fd = queue.pop()) {
+        handle(fd, a);
+        close(fd);
+      }
+    });
+  }
   // Wake accept() periodically so a signal ends the loop promptly.
   timeval tv{1, 0};
   setsockopt(srv, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
@@ -195,9 +287,11 @@ int main(int argc, char** argv) {
       std::perror("accept");
       break;
     }
-    handle(fd, a);
-    close(fd);
+    if (!queue.push(fd)) close(fd);  // overloaded: shed the connection
   }
+  queue.stop();
+  for (auto& w : workers) w.join();
+  queue.drain();
   close(srv);
   return 0;
 }

@@ -9,6 +9,7 @@
 #include <dirent.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cctype>
 #include <cmath>
 #include <cstdint>
@@ -70,6 +71,15 @@ struct Sample {
 inline bool g_hip_ok = false;
 inline int g_count = 0;
 inline std::string g_error;
+
+// Root of the sysfs tree (tests point it at a captured copy:
+// AMDGPU_EXPORTER_SYSFS_ROOT=/tmp/tree reads /tmp/tree/sys/...).
+inline std::string sysfs_root() {
+  const char* r = std::getenv("AMDGPU_EXPORTER_SYSFS_ROOT");
+  return r ? std::string(r) : std::string();
+}
+
+inline std::string pci_dir(const std::string& bdf) { return sysfs_root() + "/sys/bus/pci/devices/" + bdf; }
 
 inline bool read_text(const std::string& path, std::string* out) {
   std::ifstream f(path);
@@ -235,7 +245,7 @@ inline bool device_info(int dev, DeviceInfo* out) {
     out->serial.push_back(static_cast<char>(std::toupper(static_cast<unsigned char>(c))));
   }
   if (out->serial.empty()) out->serial = out->uuid;
-  const std::string dir = "/sys/bus/pci/devices/" + out->bdf;
+  const std::string dir = pci_dir(out->bdf);
   std::string s;
   if (read_text(dir + "/device", &s)) out->device_id = s;
   // The HIP device name is empty or generic on some ROCm builds. Prefer the
@@ -253,7 +263,7 @@ inline bool device_info(int dev, DeviceInfo* out) {
 
 inline Sample sample_sysfs(const std::string& bdf) {
   Sample s;
-  const std::string dir = "/sys/bus/pci/devices/" + bdf;
+  const std::string dir = pci_dir(bdf);
   double v;
   if (read_double(dir + "/gpu_busy_percent", &v)) s.gfx_busy_pct = v;
   if (read_double(dir + "/mem_busy_percent", &v)) s.mem_busy_pct = v;
@@ -302,6 +312,150 @@ inline Sample sample_sysfs(const std::string& bdf) {
   return s;
 }
 
+// ---------------------------------------------------------------------------
+// Device source without the HIP runtime (--sysfs-only): it needs no device
+// node, so the exporter runs unprivileged with only /sys mounted read-only.
+//   * GPUs are the DRM cards of vendor 0x1002 (/sys/class/drm/cardN/device),
+//     in card order — the order the driver probed them, which is also the
+//     KFD node order and so the HIP device order (no *_VISIBLE_DEVICES mask);
+//   * telemetry comes from the same amdgpu sysfs / hwmon files as with HIP;
+//   * xGMI links come from the KFD topology (/sys/class/kfd/kfd/topology):
+//     io_links of type 11 (CRAT_IOLINK_TYPE_XGMI) between GPU nodes, 1 hop.
+//     KFD shows a GPU node's properties only to a process whose device cgroup
+//     admits that GPU's render node ("Operation not permitted" otherwise:
+//     tests/fixtures/mi355x/kfd_topology.txt, captured in a 1-GPU container on
+//     an 8 x MI355X host). A link is exported only when both ends are
+//     readable; an unprivileged pod therefore exports no link series, and the
+//     plugin says its xGMI matrix is the assumed MI355X mesh.
+// ---------------------------------------------------------------------------
+
+inline constexpr int kKfdIoLinkXgmi = 11;
+
+// "key value" lines of a KFD properties file.
+inline bool kfd_props(const std::string& path, std::vector<std::pair<std::string, double>>* out) {
+  std::string text;
+  if (!read_text(path, &text)) return false;
+  std::istringstream in(text);
+  std::string k;
+  double v;
+  while (in >> k >> v) out->emplace_back(k, v);
+  return !out->empty();
+}
+
+inline double kfd_get(const std::vector<std::pair<std::string, double>>& p, const char* key, double dflt) {
+  for (const auto& kv : p)
+    if (kv.first == key) return kv.second;
+  return dflt;
+}
+
+// Numeric suffixes of the entries of `dir` that start with `prefix` ("card3" → 3).
+inline std::vector<int> numbered_entries(const std::string& dir, const char* prefix) {
+  std::vector<int> out;
+  DIR* d = opendir(dir.c_str());
+  if (!d) return out;
+  const size_t pl = std::strlen(prefix);
+  while (dirent* e = readdir(d)) {
+    if (std::strncmp(e->d_name, prefix, pl) != 0) continue;
+    const char* num = e->d_name + pl;
+    char* end = nullptr;
+    const long n = std::strtol(num, &end, 10);
+    if (end != num && *end == '\0') out.push_back(static_cast<int>(n));
+  }
+  closedir(d);
+  std::sort(out.begin(), out.end());
+  return out;
+}
+
+inline std::string lower_hex(std::string s) {
+  for (auto& c : s) c = static_cast<char>(std::tolower(static_cast<unsigned char>(c)));
+  return s;
+}
+
+// PCI addresses of the AMD GPUs, in DRM card order.
+inline std::vector<std::string> sysfs_gpu_bdfs() {
+  std::vector<std::string> out;
+  const std::string drm = sysfs_root() + "/sys/class/drm";
+  for (int n : numbered_entries(drm, "card")) {
+    const std::string dev = drm + "/card" + std::to_string(n) + "/device";
+    std::string vendor;
+    if (!read_text(dev + "/vendor", &vendor) || lower_hex(vendor) != "0x1002") continue;
+    char buf[4096];
+    const ssize_t len = readlink(dev.c_str(), buf, sizeof(buf) - 1);
+    if (len <= 0) continue;
+    buf[len] = 0;
+    std::string bdf = buf;
+    const size_t slash = bdf.rfind('/');
+    if (slash != std::string::npos) bdf = bdf.substr(slash + 1);
+    bdf = lower_hex(bdf);
+    if (std::find(out.begin(), out.end(), bdf) == out.end()) out.push_back(bdf);
+  }
+  return out;
+}
+
+inline std::string kfd_bdf(long long domain, long long location_id) {
+  char b[32];
+  std::snprintf(b, sizeof(b), "%04llx:%02llx:%02llx.%llx", domain, (location_id >> 8) & 0xff,
+                (location_id >> 3) & 0x1f, location_id & 0x7);
+  return b;
+}
+
+// Direct xGMI links between GPU ordinals (indices into `bdfs`), one pair per
+// direction, from the KFD nodes this process may read.
+inline std::vector<std::pair<int, int>> kfd_xgmi_links(const std::vector<std::string>& bdfs) {
+  const std::string base = sysfs_root() + "/sys/class/kfd/kfd/topology/nodes";
+  std::vector<int> ordinal_of_node;  // KFD node → GPU ordinal (-1: CPU or unreadable)
+  std::vector<std::vector<std::pair<int, int>>> links;  // per node: (type, node_to)
+  for (int n : numbered_entries(base, "")) {
+    if (n >= static_cast<int>(ordinal_of_node.size())) {
+      ordinal_of_node.resize(n + 1, -1);
+      links.resize(n + 1);
+    }
+    const std::string nd = base + "/" + std::to_string(n);
+    std::vector<std::pair<std::string, double>> p;
+    if (!kfd_props(nd + "/properties", &p) || kfd_get(p, "simd_count", 0) <= 0) continue;
+    const std::string bdf = kfd_bdf(static_cast<long long>(kfd_get(p, "domain", 0)),
+                                    static_cast<long long>(kfd_get(p, "location_id", 0)));
+    const auto it = std::find(bdfs.begin(), bdfs.end(), bdf);
+    if (it == bdfs.end()) continue;
+    ordinal_of_node[n] = static_cast<int>(it - bdfs.begin());
+    for (int l : numbered_entries(nd + "/io_links", "")) {
+      std::vector<std::pair<std::string, double>> lp;
+      if (!kfd_props(nd + "/io_links/" + std::to_string(l) + "/properties", &lp)) continue;
+      links[n].emplace_back(static_cast<int>(kfd_get(lp, "type", 0)), static_cast<int>(kfd_get(lp, "node_to", -1)));
+    }
+  }
+  std::vector<std::pair<int, int>> out;
+  for (size_t n = 0; n < links.size(); ++n) {
+    if (ordinal_of_node[n] < 0) continue;
+    for (const auto& tl : links[n]) {
+      if (tl.first != kKfdIoLinkXgmi || tl.second < 0 || tl.second >= static_cast<int>(ordinal_of_node.size())) continue;
+      const int peer = ordinal_of_node[tl.second];
+      if (peer >= 0 && peer != ordinal_of_node[n]) out.emplace_back(ordinal_of_node[n], peer);
+    }
+  }
+  return out;
+}
+
+// DeviceInfo from sysfs alone (no HIP): what the labels and HBM total need.
+inline DeviceInfo sysfs_device_info(const std::string& bdf, int ordinal) {
+  DeviceInfo d;
+  d.index = ordinal;
+  d.bdf = bdf;
+  const std::string dir = pci_dir(bdf);
+  std::string s;
+  if (read_text(dir + "/device", &s)) d.device_id = lower_hex(s);
+  if (read_text(dir + "/unique_id", &s) && !s.empty()) {
+    d.serial = s;
+    for (auto& c : d.serial) c = static_cast<char>(std::toupper(static_cast<unsigned char>(c)));
+  }
+  double v;
+  if (read_double(dir + "/mem_info_vram_total", &v)) d.hbm_bytes = static_cast<size_t>(v);
+  if (const char* prod = product_for_device_id(d.device_id)) d.name = prod;
+  else if (read_text(dir + "/product_name", &s) && !s.empty()) d.name = s;
+  else d.name = "AMD Instinct (" + (d.device_id.empty() ? std::string("unknown") : d.device_id) + ")";
+  return d;
+}
+
 inline void append_metric(std::string* out, const char* name, const std::string& labels, double v) {
   if (std::isnan(v)) return;
   char num[64];
@@ -327,6 +481,7 @@ struct RenderOptions {
   int only_device = -1;      // export just this HIP device (-1 = all)
   std::string gpu_label;     // override the gpu_id label (with only_device)
   bool topology = true;      // emit xGMI link metrics between exported devices
+  bool sysfs_only = false;   // enumerate devices from sysfs, links from the KFD topology (no HIP)
 };
 
 // Render devices in exporter format. Units follow the AMD Device Metrics
@@ -363,10 +518,15 @@ inline std::string render(const RenderOptions& opt) {
     out.append("# TYPE ").append(h[0]).append(counter ? " counter\n" : " gauge\n");
   }
   const double mib = 1024.0 * 1024.0;
-  for (int d = 0; d < g_count; ++d) {
+  // Devices from HIP, or from sysfs alone (--sysfs-only).
+  const bool from_sysfs = opt.sysfs_only;
+  const std::vector<std::string> bdfs = from_sysfs ? sysfs_gpu_bdfs() : std::vector<std::string>();
+  const int count = from_sysfs ? static_cast<int>(bdfs.size()) : g_count;
+  for (int d = 0; d < count; ++d) {
     if (opt.only_device >= 0 && d != opt.only_device) continue;
     DeviceInfo info;
-    if (!device_info(d, &info)) continue;
+    if (from_sysfs) info = sysfs_device_info(bdfs[d], d);
+    else if (!device_info(d, &info)) continue;
     Sample s = sample_sysfs(info.bdf);
     const std::string gid = (opt.only_device >= 0 && !opt.gpu_label.empty()) ? opt.gpu_label : std::to_string(d);
     std::string labels = "hostname=\"" + escape_label(opt.hostname) + "\",gpu_id=\"" + escape_label(gid) +
@@ -399,15 +559,22 @@ inline std::string render(const RenderOptions& opt) {
     }
   }
   if (opt.topology && opt.only_device < 0) {
-    for (int a = 0; a < g_count; ++a) {
-      for (int b = 0; b < g_count; ++b) {
-        if (a == b) continue;
-        uint32_t type = 0, hops = 0;
-        if (hipExtGetLinkTypeAndHopCount(a, b, &type, &hops) != hipSuccess || type != kLinkTypeXgmi) continue;
-        append_metric(&out, "gpu_xgmi_link_hops",
-                      "hostname=\"" + escape_label(opt.hostname) + "\",gpu_id=\"" + std::to_string(a) +
-                          "\",peer_gpu_id=\"" + std::to_string(b) + "\"",
-                      static_cast<double>(hops));
+    auto link = [&](int a, int b, double hops) {
+      append_metric(&out, "gpu_xgmi_link_hops",
+                    "hostname=\"" + escape_label(opt.hostname) + "\",gpu_id=\"" + std::to_string(a) +
+                        "\",peer_gpu_id=\"" + std::to_string(b) + "\"",
+                    hops);
+    };
+    if (from_sysfs) {
+      for (const auto& ab : kfd_xgmi_links(bdfs)) link(ab.first, ab.second, 1.0);
+    } else {
+      for (int a = 0; a < g_count; ++a) {
+        for (int b = 0; b < g_count; ++b) {
+          if (a == b) continue;
+          uint32_t type = 0, hops = 0;
+          if (hipExtGetLinkTypeAndHopCount(a, b, &type, &hops) != hipSuccess || type != kLinkTypeXgmi) continue;
+          link(a, b, static_cast<double>(hops));
+        }
       }
     }
   }

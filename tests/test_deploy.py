@@ -44,6 +44,30 @@ def test_exporter_manifests_are_consistent():
     assert "metrics-exporter" in dset["metadata"]["name"]  # classified as the metrics-exporter operand
 
 
+def test_exporter_daemonset_is_least_privilege():
+    ds = docs("exporter/daemonset.yaml")
+    pod = by_kind(ds, "DaemonSet")[0]["spec"]["template"]["spec"]
+    c = pod["containers"][0]
+    sc = c["securityContext"]
+    assert sc.get("privileged") is not True and sc["allowPrivilegeEscalation"] is False
+    assert sc["readOnlyRootFilesystem"] is True and sc["capabilities"]["drop"] == ["ALL"]
+    assert pod["securityContext"]["runAsNonRoot"] is True and pod["securityContext"]["runAsUser"] != 0
+    # No device nodes and no host /dev: the exporter runs without the HIP runtime.
+    assert "--sysfs-only" in c["args"]
+    host_paths = [v["hostPath"]["path"] for v in pod["volumes"] if "hostPath" in v]
+    assert host_paths == ["/sys"]
+    assert all(m.get("readOnly") for m in c["volumeMounts"])
+    # A pinned image, and ingress only from Prometheus on the metrics port.
+    assert not c["image"].endswith(":latest") and (":" in c["image"].split("/")[-1] or "@sha256:" in c["image"])
+    np = by_kind(ds, "NetworkPolicy")[0]
+    assert np["spec"]["podSelector"]["matchLabels"].items() <= pod_labels_of(ds).items()
+    assert [p["port"] for r in np["spec"]["ingress"] for p in r["ports"]] == ["metrics"]
+
+
+def pod_labels_of(ds):
+    return by_kind(ds, "DaemonSet")[0]["spec"]["template"]["metadata"]["labels"]
+
+
 def test_exporter_daemonset_args_are_accepted_by_the_binary():
     from headlamp_intel_gpu_plugin_amd.ops import build as native_build
 

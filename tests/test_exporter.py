@@ -118,3 +118,186 @@ def test_exporter_process_and_device_relabel(exe):
         assert device_to_node({"0": "n"})({"gpu_id": "5"}) is None
     finally:
         agent.stop()
+
+
+# ---------------------------------------------------------------------------
+# --sysfs-only: devices and xGMI links from the KFD topology, no HIP runtime
+# ---------------------------------------------------------------------------
+
+FIX = os.path.join(os.path.dirname(__file__), "fixtures", "mi355x")
+
+
+def _kfd_nodes(path):
+    """tests/fixtures/mi355x/kfd_topology.txt → [(node, props text, {link: props text})]."""
+    nodes, cur, link = [], None, None
+    for line in open(path):
+        line = line.rstrip("\n")
+        if line.startswith("== node "):
+            cur = [int(line.split()[2]), [], {}]
+            nodes.append(cur)
+            link = None
+        elif line.startswith("-- "):
+            link = line[3:]
+            cur[2][link] = []
+        elif cur is not None and line and not line.startswith("#") and not line.startswith(("gpu_id ", "name ")):
+            (cur[2][link] if link else cur[1]).append(line)
+    return nodes
+
+
+def _drm_cards():
+    """tests/fixtures/mi355x/drm_cards.txt → [(card number, bdf)] in card order."""
+    out = []
+    for line in open(os.path.join(FIX, "drm_cards.txt")):
+        if line.startswith("#") or not line.strip():
+            continue
+        f = line.split()
+        out.append((int(f[0][4:]), f[3]))
+    return sorted(out)
+
+
+def _sysfs_tree(root, kfd_nodes):
+    """DRM cards + PCI device dirs of the captured host, and the given KFD nodes."""
+    for i, (card, bdf) in enumerate(_drm_cards()):
+        d = root / "sys/bus/pci/devices" / bdf
+        (d / "hwmon/hwmon0").mkdir(parents=True)
+        (d / "vendor").write_text("0x1002\n")
+        (d / "device").write_text("0x75a3\n")
+        (d / "mem_info_vram_total").write_text(str(294896 * 1024 * 1024) + "\n")
+        (d / "mem_info_vram_used").write_text(str((1000 + i) * 1024 * 1024) + "\n")
+        (d / "gpu_busy_percent").write_text(f"{10 * i}\n")
+        (d / "hwmon/hwmon0/power1_input").write_text(f"{(200 + i) * 1000000}\n")
+        c = root / "sys/class/drm" / f"card{card}"
+        c.mkdir(parents=True)
+        os.symlink(d, c / "device")
+    base = root / "sys/class/kfd/kfd/topology/nodes"
+    for node, props, links in kfd_nodes:
+        nd = base / str(node)
+        nd.mkdir(parents=True)
+        if props:  # an unreadable node (another container's GPU) has no properties for us
+            (nd / "properties").write_text("\n".join(props) + "\n")
+        for name, lp in links.items():
+            (nd / name).mkdir(parents=True, exist_ok=True)
+            if lp:
+                (nd / name / "properties").write_text("\n".join(lp) + "\n")
+    return root
+
+
+def _scrape_sysfs_only(exe, root):
+    env = dict(os.environ, AMDGPU_EXPORTER_SYSFS_ROOT=str(root))
+    r = subprocess.run([exe, "--once", "--sysfs-only", "--hostname", "n0"], capture_output=True, text=True,
+                       timeout=60, env=env)
+    assert r.returncode == 0, r.stderr
+    assert "sysfs-only" in r.stderr
+    return parse_exposition(r.stdout)
+
+
+def test_sysfs_only_enumerates_gpus_from_drm_cards(exe, tmp_path):
+    # The KFD tree as captured in a 1-GPU container: only this container's GPU
+    # node (2) is readable, so no link has two readable ends.
+    rows = _scrape_sysfs_only(exe, _sysfs_tree(tmp_path, _kfd_nodes(os.path.join(FIX, "kfd_topology.txt"))))
+    power = [(l["gpu_id"], l["pci_bus"], l["card_model"], v) for n, l, v in rows if n == "gpu_power_usage"]
+    cards = _drm_cards()
+    assert [p[0] for p in power] == [str(i) for i in range(8)]
+    assert [p[1] for p in power] == [b for _, b in cards]  # card order: card0, card8, card16, ...
+    assert all(p[2] == "AMD Instinct MI355X" for p in power)
+    assert [p[3] for p in power] == [200.0 + i for i in range(8)]
+    assert {v for n, l, v in rows if n == "gpu_total_vram"} == {294896.0}
+    assert [v for n, l, v in rows if n == "gpu_gfx_activity"] == [10.0 * i for i in range(8)]
+    assert not [1 for n, _, _ in rows if n == "gpu_xgmi_link_hops"]
+
+
+def test_sysfs_only_reads_xgmi_links_from_a_readable_kfd_topology(exe, tmp_path):
+    # Every GPU node readable (a pod whose device cgroup admits the render
+    # nodes): node 2's captured properties as the template, each node at its
+    # card's PCI address, every GPU linked to the 7 others (io_link type 11).
+    # SYNTHETIC beyond node 2: the capture could read only its own GPU.
+    captured = {n: (p, l) for n, p, l in _kfd_nodes(os.path.join(FIX, "kfd_topology.txt"))}
+    template = [l for l in captured[2][0] if not l.startswith(("location_id ", "domain "))]
+    xgmi_tmpl = next(lp for name, lp in captured[2][1].items() if lp and "type 11" in lp)
+    nodes = [(0, captured[0][0], {}), (1, captured[1][0], {})]
+    cards = _drm_cards()
+    for k, (_, bdf) in enumerate(cards):
+        bus, dev, fn = int(bdf[5:7], 16), int(bdf[8:10], 16), int(bdf[11], 16)
+        props = template + [f"location_id {bus << 8 | dev << 3 | fn}", "domain 0"]
+        links = {}
+        for j in range(len(cards)):
+            if j != k:
+                links[f"io_links/{len(links)}"] = [l if not l.startswith("node_to ") else f"node_to {j + 2}"
+                                                   for l in xgmi_tmpl]
+        nodes.append((k + 2, props, links))
+    rows = _scrape_sysfs_only(exe, _sysfs_tree(tmp_path, nodes))
+    hops = {(l["gpu_id"], l["peer_gpu_id"]): v for n, l, v in rows if n == "gpu_xgmi_link_hops"}
+    assert len(hops) == 56 and set(hops.values()) == {1.0}
+    assert all((str(a), str(b)) in hops for a in range(8) for b in range(8) if a != b)
+
+
+def test_captured_kfd_topology_links_this_gpu_to_seven_peers_over_xgmi():
+    # What the capture itself shows about an MI355X: its GPU node has 7 xGMI
+    # io_links (type 11, weight 15, 76 GB/s) and one PCIe link to its CPU node.
+    nodes = {n: (p, l) for n, p, l in _kfd_nodes(os.path.join(FIX, "kfd_topology.txt"))}
+    props = dict(l.split(" ", 1) for l in nodes[2][0])
+    assert props["simd_count"] == "1024" and props["gfx_target_version"] == "90500"
+    assert int(props["device_id"]) == 0x75A3 and props["lds_size_in_kb"] == "160" and props["num_xcc"] == "8"
+    links = [dict(x.split(" ", 1) for x in lp) for name, lp in nodes[2][1].items() if name.startswith("io_links") and lp]
+    xgmi = [l for l in links if l["type"] == "11"]
+    assert len(xgmi) == 7 and {l["weight"] for l in xgmi} == {"15"} and {l["max_bandwidth"] for l in xgmi} == {"76000"}
+    assert sorted(int(l["node_to"]) for l in xgmi) == list(range(3, 10))
+
+
+def test_slow_client_does_not_block_scrapes(exe):
+    """A client trickling header bytes holds one worker until the request
+    deadline; /healthz and /metrics keep answering meanwhile."""
+    import socket
+
+    p = subprocess.Popen([exe, "--port", "0", "--bind", "127.0.0.1", "--hostname", "slow", "--sysfs-only"],
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        line = p.stdout.readline()
+        port = int(line.split("127.0.0.1:")[1].split()[0])
+        slow = [socket.create_connection(("127.0.0.1", port)) for _ in range(6)]
+        t0 = time.time()
+        for s in slow:
+            s.sendall(b"G")
+        for _ in range(3):
+            t = time.time()
+            with urllib.request.urlopen(f"http://127.0.0.1:{port}/healthz", timeout=5) as r:
+                assert r.read() == b"ok\n"
+            assert time.time() - t < 4.5
+            for s in slow:
+                try:
+                    s.sendall(b"E")
+                except OSError:
+                    pass
+            time.sleep(0.5)
+        # The trickling connections are dropped at the deadline (~3 s), not held.
+        slow[0].settimeout(10)
+        try:
+            data = slow[0].recv(100)
+        except ConnectionResetError:
+            data = b""
+        assert data == b"" and time.time() - t0 < 8
+        for s in slow:
+            s.close()
+    finally:
+        p.send_signal(signal.SIGTERM)
+        assert p.wait(15) == 0
+
+
+@pytest.mark.gpu
+def test_sysfs_only_on_the_box_matches_the_hip_scrape(exe):
+    """--sysfs-only (no HIP, what the unprivileged DaemonSet runs) sees every
+    MI355X card of the host in sysfs; for the GPU HIP sees, the series agree."""
+    hip = parse_exposition(subprocess.run([exe, "--once", "--hostname", "n0"], capture_output=True, text=True,
+                                          timeout=60).stdout)
+    r = subprocess.run([exe, "--once", "--sysfs-only", "--hostname", "n0"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    sysfs = parse_exposition(r.stdout)
+    models = {l["pci_bus"]: l["card_model"] for n, l, _ in sysfs if n == "gpu_total_vram"}
+    assert len(models) >= 1 and set(models.values()) == {"AMD Instinct MI355X"}, models
+    hip_bus = [l["pci_bus"] for n, l, _ in hip if n == "gpu_total_vram"][0]
+    assert hip_bus in models
+    total = lambda rows, bus: [v for n, l, v in rows if n == "gpu_total_vram" and l["pci_bus"] == bus][0]
+    assert total(sysfs, hip_bus) == total(hip, hip_bus)
+    # Power / temperature of the visible GPU come from the same hwmon files.
+    assert [v for n, l, v in sysfs if n == "gpu_junction_temperature" and l["pci_bus"] == hip_bus]
+    print("sysfs-only GPUs:", len(models), "link series:", sum(1 for n, _, _ in sysfs if n == "gpu_xgmi_link_hops"))
