@@ -29,7 +29,7 @@ def test_all_pages_render(url):
     for title in ("AMD GPU — Overview", "AMD GPU — Device Plugins", "AMD GPU — Nodes", "AMD GPU — Pods",
                   "AMD GPU — Metrics"):
         assert "# " + title in r.stdout
-    assert "mi355x-001" in r.stdout and "xGMI (" in r.stdout and "Assigned GPUs" in r.stdout
+    assert "mi355x-001" in r.stdout and "xGMI topology (measured)" in r.stdout and "Assigned GPUs" in r.stdout
 
 
 def test_json_is_the_view_model(url):
