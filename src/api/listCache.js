@@ -48,6 +48,18 @@ function versionOf(raw) {
   return m && m.resourceVersion ? m.resourceVersion : null;
 }
 
+/**
+ * `raw` is the object of record `rec`, at the same version: same uid and
+ * resourceVersion. Used for the object alongside in the old list, so a
+ * re-parsed list whose order did not change costs two string compares per
+ * object instead of a hash lookup.
+ */
+function samePositional(rec, raw) {
+  if (rec.version === null || rec.key === null) return false;
+  const m = raw && raw.metadata;
+  return !!m && m.resourceVersion === rec.version && m.uid === rec.key;
+}
+
 /** Beyond this many changed members a subset is rebuilt instead of patched. */
 const MAX_PATCH = 64;
 
@@ -160,8 +172,10 @@ export function createListTracker(predicates) {
     for (let i = lo; i < hiNew; i++) {
       const raw = unwrapKubeObject(list[i]);
       let rec;
-      if (j < hiOld && prevRec[j].raw === raw && prevRec[j].gen !== gen) {
-        rec = prevRec[j];
+      const pj = j < hiOld ? prevRec[j] : null;
+      if (pj !== null && pj.gen !== gen && (pj.raw === raw || samePositional(pj, raw))) {
+        rec = pj;
+        if (rec.raw !== raw) stats.reused++;
         rec.gen = gen;
         j++;
         w.replaced = null;
