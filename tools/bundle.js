@@ -1,0 +1,232 @@
+#!/usr/bin/env node
+/**
+ * Offline plugin bundler: src/index.tsx and everything it imports → one
+ * self-contained script (default `dist-offline/main.js`; `headlamp-plugin build`
+ * writes `dist/main.js`), the file Headlamp loads for a plugin.
+ *
+ *   node tools/bundle.js [--entry src/index.tsx] [--out dist-offline/main.js]
+ *
+ * The reference builds its bundle with `headlamp-plugin build` (vite;
+ * /root/reference/package.json:16-18, CI /root/reference/.github/workflows/ci.yaml:169-170).
+ * That CLI is an npm package and this build environment has no registry, so
+ * this file does the part of that job the plugin needs, with no dependency:
+ *
+ *   * module graph from the entry, relative specifiers resolved like
+ *     tools/plugin-loader.js (./x → x.tsx | x.ts | x.js | x/index.*);
+ *   * TypeScript: the .ts/.tsx shims are written in the JavaScript subset of
+ *     TypeScript (types live in .d.ts files), so the only TypeScript syntax
+ *     is `import type`, which is dropped;
+ *   * ES modules → functions in a module table (import bindings resolved
+ *     through getters, so exports are live), executed once, in import order;
+ *   * host modules are not bundled: they resolve to the globals Headlamp
+ *     hands every plugin (`pluginLib`) — the externals `headlamp-plugin
+ *     build` declares for the same imports (EXTERNALS below).
+ *
+ * Anything else (an `import`/`export` form this does not understand, a bare
+ * specifier that is not a host module) is an error, not a silent pass-through.
+ * CI still runs the real `npm run build`; this bundle is what the offline
+ * checks load (tests/js/bundle.test.js evaluates it against the harness
+ * stand-ins and mounts every registered component).
+ */
+import fs from 'fs';
+import path from 'path';
+import { fileURLToPath } from 'url';
+
+const ROOT = path.resolve(path.dirname(fileURLToPath(import.meta.url)), '..');
+
+/** Host modules → expression over the `pluginLib` object Headlamp provides. */
+export const EXTERNALS = {
+  '@kinvolk/headlamp-plugin/lib': 'pluginLib',
+  '@kinvolk/headlamp-plugin/lib/CommonComponents': 'pluginLib.CommonComponents',
+  react: 'pluginLib.React',
+};
+
+const TRY = ['', '.tsx', '.ts', '.js', '/index.tsx', '/index.ts', '/index.js'];
+const IDENT = /^[A-Za-z_$][\w$]*$/;
+
+function resolveFile(fromFile, spec) {
+  const base = path.resolve(path.dirname(fromFile), spec);
+  for (let i = 0; i < TRY.length; i++) {
+    const f = base + TRY[i];
+    if (fs.existsSync(f) && fs.statSync(f).isFile()) return f;
+  }
+  throw new Error('bundle: cannot resolve ' + JSON.stringify(spec) + ' from ' + path.relative(ROOT, fromFile));
+}
+
+/** `a, b as c` → [[local, exported]] (import: [imported, local]). */
+function specList(body, where) {
+  return body
+    .split(',')
+    .map(function (s) { return s.trim(); })
+    .filter(function (s) { return s.length > 0; })
+    .map(function (s) {
+      const m = /^([A-Za-z_$][\w$]*)(?:\s+as\s+([A-Za-z_$][\w$]*))?$/.exec(s);
+      if (!m) throw new Error('bundle: unsupported specifier ' + JSON.stringify(s) + ' in ' + where);
+      return [m[1], m[2] || m[1]];
+    });
+}
+
+/** Names bound by `{ a, b: c, ...rest }` / `[a, b]` / `name`. */
+function boundNames(target, where) {
+  const t = target.trim();
+  if (IDENT.test(t)) return [t];
+  const inner = t.slice(1, -1);
+  return inner
+    .split(',')
+    .map(function (s) { return s.trim(); })
+    .filter(function (s) { return s.length > 0; })
+    .map(function (s) {
+      const rest = /^\.\.\.([A-Za-z_$][\w$]*)$/.exec(s);
+      if (rest) return rest[1];
+      const m = /^(?:[A-Za-z_$][\w$]*\s*:\s*)?([A-Za-z_$][\w$]*)(?:\s*=.*)?$/.exec(s);
+      if (!m) throw new Error('bundle: unsupported destructuring ' + JSON.stringify(s) + ' in ' + where);
+      return m[1];
+    });
+}
+
+/**
+ * One module's source → { code, deps } where code is the body of
+ * `function (__exports, __req) { … }`.
+ */
+export function transformModule(source, file, resolveDep) {
+  const where = path.relative(ROOT, file);
+  const getters = []; // [exported, expression]
+  const deps = [];
+  let nextTmp = 0;
+  function req(spec) {
+    if (Object.prototype.hasOwnProperty.call(EXTERNALS, spec)) return '__ext(' + JSON.stringify(spec) + ')';
+    if (!(spec.startsWith('./') || spec.startsWith('../'))) {
+      throw new Error('bundle: bare import ' + JSON.stringify(spec) + ' in ' + where + ' is not a host module');
+    }
+    const id = resolveDep(file, spec);
+    deps.push(id);
+    return '__req(' + JSON.stringify(id) + ')';
+  }
+  let s = String(source).replace(/^import type [^;]*;[ \t]*$/gm, '');
+  s = s.replace(/^import\s+([\s\S]*?)\s+from\s+'([^']+)';?/gm, function (m, clause, spec) {
+    const src = req(spec);
+    const out = [];
+    let c = clause.trim();
+    const ns = /^\*\s+as\s+([A-Za-z_$][\w$]*)$/.exec(c);
+    if (ns) return 'const ' + ns[1] + ' = ' + src + ';';
+    let def = null;
+    const d = /^([A-Za-z_$][\w$]*)\s*(?:,\s*([\s\S]*))?$/.exec(c);
+    if (d) {
+      def = d[1];
+      c = (d[2] || '').trim();
+    }
+    const tmp = '__m' + nextTmp++;
+    out.push('const ' + tmp + ' = ' + src + ';');
+    if (def) out.push('const ' + def + ' = __default(' + tmp + ');');
+    if (c) {
+      if (c[0] !== '{' || c[c.length - 1] !== '}') throw new Error('bundle: unsupported import ' + JSON.stringify(m) + ' in ' + where);
+      specList(c.slice(1, -1), where).forEach(function (p) {
+        out.push('const ' + p[1] + ' = ' + tmp + '.' + p[0] + ';');
+        out.push('if (!(' + JSON.stringify(p[0]) + ' in ' + tmp + ')) __missing(' + JSON.stringify(p[0]) + ', ' + JSON.stringify(spec) + ', ' + JSON.stringify(where) + ');');
+      });
+    }
+    return out.join(' ');
+  });
+  s = s.replace(/^import\s+'([^']+)';?/gm, function (m, spec) { return req(spec) + ';'; });
+  s = s.replace(/^export\s+\{([^}]*)\}\s+from\s+'([^']+)';?/gm, function (m, body, spec) {
+    const tmp = '__re' + getters.length;
+    specList(body, where).forEach(function (p) { getters.push([p[1], tmp + '.' + p[0]]); });
+    return 'const ' + tmp + ' = ' + req(spec) + ';';
+  });
+  s = s.replace(/^export\s+\{([^}]*)\};?/gm, function (m, body) {
+    specList(body, where).forEach(function (p) { getters.push([p[1], p[0]]); });
+    return '';
+  });
+  s = s.replace(/^export\s+default\s+/gm, '__exports.default = ');
+  s = s.replace(/^export\s+(const|let|var)\s+(\{[^}]*\}|\[[^\]]*\]|[A-Za-z_$][\w$]*)/gm, function (m, kw, target) {
+    boundNames(target, where).forEach(function (n) { getters.push([n, n]); });
+    return kw + ' ' + target;
+  });
+  s = s.replace(/^export\s+((?:async\s+)?function\*?|class)\s+([A-Za-z_$][\w$]*)/gm, function (m, kw, name) {
+    getters.push([name, name]);
+    return kw + ' ' + name;
+  });
+  const left = /^(import|export)\b.*$/m.exec(s);
+  if (left) throw new Error('bundle: unsupported statement in ' + where + ': ' + left[0]);
+  if (/\bimport\s*\(|\bimport\.meta\b/.test(s)) throw new Error('bundle: dynamic import / import.meta in ' + where);
+  const head = getters
+    .map(function (g) { return '__export(__exports, ' + JSON.stringify(g[0]) + ', function () { return ' + g[1] + '; });'; })
+    .join('\n');
+  return { code: "'use strict';\n" + head + '\n' + s, deps: deps };
+}
+
+/**
+ * Bundle the graph rooted at `entry` (absolute path) → script text.
+ * @returns {{code: string, modules: string[]}}
+ */
+export function bundle(entry) {
+  const order = [];
+  const mods = {};
+  function id(file) { return path.relative(ROOT, file).split(path.sep).join('/'); }
+  function resolveDep(fromFile, spec) { return id(resolveFile(fromFile, spec)); }
+  function visit(file) {
+    const key = id(file);
+    if (mods[key]) return;
+    mods[key] = transformModule(fs.readFileSync(file, 'utf8'), file, resolveDep);
+    mods[key].deps.forEach(function (d) { visit(path.join(ROOT, d)); });
+    order.push(key);
+  }
+  visit(entry);
+  const pkg = JSON.parse(fs.readFileSync(path.join(ROOT, 'package.json'), 'utf8'));
+  const parts = [];
+  parts.push('/* ' + pkg.name + ' ' + pkg.version + ' — Headlamp plugin bundle built by tools/bundle.js from ' + id(entry) + ' (' + order.length + ' modules). */');
+  parts.push('(function (pluginLib) {');
+  parts.push("  'use strict';");
+  parts.push('  if (!pluginLib) throw new Error(' + JSON.stringify(pkg.name + ': Headlamp plugin library (pluginLib) not found') + ');');
+  parts.push('  var __defs = Object.create(null);');
+  parts.push('  var __cache = Object.create(null);');
+  parts.push('  var __externals = {');
+  Object.keys(EXTERNALS).forEach(function (k) {
+    parts.push('    ' + JSON.stringify(k) + ': function () { return ' + EXTERNALS[k] + '; },');
+  });
+  parts.push('  };');
+  parts.push('  function __export(o, k, get) { Object.defineProperty(o, k, { enumerable: true, get: get }); }');
+  parts.push('  function __default(m) { return m && m.__esModule !== true && m.default !== undefined ? m.default : m; }');
+  parts.push('  function __missing(name, spec, from) { throw new Error("bundle: \'" + name + "\' is not exported by " + spec + " (imported by " + from + ")"); }');
+  parts.push('  function __ext(spec) { var v = __externals[spec](); if (v === undefined || v === null) throw new Error("host module " + spec + " missing from pluginLib"); return v; }');
+  parts.push('  function __req(id) {');
+  parts.push('    var m = __cache[id];');
+  parts.push('    if (m) return m;');
+  parts.push('    m = __cache[id] = {};');
+  parts.push('    __defs[id](m, __req, __ext);');
+  parts.push('    return m;');
+  parts.push('  }');
+  order.forEach(function (key) {
+    parts.push('  // ---- ' + key);
+    parts.push('  __defs[' + JSON.stringify(key) + '] = function (__exports, __req, __ext) {');
+    parts.push(mods[key].code);
+    parts.push('  };');
+  });
+  parts.push('  return __req(' + JSON.stringify(id(entry)) + ');');
+  parts.push("})(typeof pluginLib !== 'undefined' ? pluginLib : (typeof globalThis !== 'undefined' ? globalThis.pluginLib : undefined));");
+  return { code: parts.join('\n') + '\n', modules: order };
+}
+
+function main(argv) {
+  let entry = path.join(ROOT, 'src', 'index.tsx');
+  let out = path.join(ROOT, 'dist-offline', 'main.js');
+  for (let i = 0; i < argv.length; i++) {
+    if (argv[i] === '--entry') entry = path.resolve(argv[++i]);
+    else if (argv[i] === '--out') out = path.resolve(argv[++i]);
+    else {
+      process.stderr.write('usage: node tools/bundle.js [--entry src/index.tsx] [--out dist-offline/main.js]\n');
+      return 2;
+    }
+  }
+  const b = bundle(entry);
+  fs.mkdirSync(path.dirname(out), { recursive: true });
+  const tmp = out + '.tmp' + process.pid;
+  fs.writeFileSync(tmp, b.code);
+  fs.renameSync(tmp, out);
+  process.stdout.write(path.relative(process.cwd(), out) + ': ' + b.modules.length + ' modules, ' + b.code.length + ' bytes\n');
+  return 0;
+}
+
+if (process.argv[1] && path.resolve(process.argv[1]) === fileURLToPath(import.meta.url)) {
+  process.exitCode = main(process.argv.slice(2));
+}
