@@ -236,10 +236,13 @@ function amdSchedule(request) {
   const metrics = createMetricsSource({ request: request, onTrace: onTrace, clock: hiResClock });
   const mstate = { metrics: null, fetchError: null, fetching: false, series: null };
   // Per-page metrics state, as each page's own hook holds it (plugin.js):
-  // GPU Nodes → telemetry without series, GPU Pods → pod→GPU attribution only.
+  // GPU Nodes → owners + xGMI links ('topology'), GPU Pods → pod→GPU
+  // attribution only, Metrics → per-GPU gauges + series ('gauges'). Cold
+  // open / route switch / the all-pages composite fetch every live series
+  // in one query ('all').
   const pageMetrics = { nodes: null, pods: null };
-  function fetchMetrics() {
-    return Promise.all([metrics.fetchGpuMetrics(), metrics.fetchSeries(1800, 30)]).then(function (r) {
+  function fetchMetrics(view) {
+    return Promise.all([metrics.fetchGpuMetrics(view), metrics.fetchSeries(1800, 30)]).then(function (r) {
       mstate.metrics = r[0];
       mstate.series = r[1];
       mstate.fetchError = r[0] ? null : 'Could not reach Prometheus';
@@ -255,12 +258,12 @@ function amdSchedule(request) {
     /** One page's Refresh button, as src/plugin.js wires it. */
     refreshPage: function (page) {
       if (page === 'nodes') {
-        return Promise.all([store.refresh(), metrics.fetchGpuMetrics().then(function (m) { pageMetrics.nodes = m; })]);
+        return Promise.all([store.refresh(), metrics.fetchGpuMetrics('topology').then(function (m) { pageMetrics.nodes = m; })]);
       }
       if (page === 'pods') {
         return Promise.all([store.refresh(), metrics.fetchGpuOwners().then(function (m) { pageMetrics.pods = m; })]);
       }
-      if (page === 'metrics') return fetchMetrics();
+      if (page === 'metrics') return fetchMetrics('gauges');
       return store.refresh();
     },
     pageMetrics: function (page) { return page in pageMetrics && pageMetrics[page] ? pageMetrics[page] : mstate.metrics; },

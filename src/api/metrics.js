@@ -299,14 +299,26 @@ export const EXPORTER_JOIN_LABELS = ['__name__', 'hostname', 'node', 'instance',
 export const EXPORTER_LEAN_LABELS = ['__name__', 'hostname', 'gpu_id', 'peer_gpu_id', 'pod', 'namespace'];
 
 /**
+ * What a cluster-wide fetch is for — each page asks only for the live series
+ * it draws (the same idea as the Pods page's ownersQuery):
+ *   all       every live gauge and every xGMI link (terminal client, detail fallback);
+ *   gauges    the Metrics page: per-GPU power / HBM / activity / temperature /
+ *             RAS, no xGMI links (7 of the 14 live series of a GPU);
+ *   topology  the GPU Nodes page: per-GPU pod owners (from the power gauge)
+ *             and the per-link xGMI throughput of the neighbour matrix.
+ */
+export const METRIC_VIEWS = ['all', 'gauges', 'topology'];
+
+/**
  * Per-GPU exporter gauges. The static ones (HBM capacity, power cap, throttle
  * threshold, link topology) change only with a reconfiguration of the node,
  * so callers ask for them once per DISCOVERY_TTL_MS and keep a copy; every
- * refresh asks for the live ones.
+ * refresh asks for the live ones (those of `view`, METRIC_VIEWS).
  */
-function exporterNames(withStatic) {
+function exporterNames(withStatic, view) {
   const E = SERIES.exporter;
-  const names = [E.power, E.vramUsed, E.gfx, E.umc, E.temp, E.eccCorrect, E.eccUncorrect, E.xgmiRe];
+  const gauges = [E.power, E.vramUsed, E.gfx, E.umc, E.temp, E.eccCorrect, E.eccUncorrect];
+  const names = view === 'gauges' ? gauges : view === 'topology' ? [E.power, E.xgmiRe] : gauges.concat([E.xgmiRe]);
   if (withStatic !== false) names.push(E.powerCap, E.vramTotal, E.tempSlowdown, E.linkHops);
   return names;
 }
@@ -323,9 +335,10 @@ export const STATIC_GPU_FIELDS = ['powerCapWatts', 'powerCapAssumed', 'vramTotal
 /**
  * @param {boolean} [withStatic]  include the static series (default true)
  * @param {boolean} [lean]        project onto EXPORTER_LEAN_LABELS (live-only queries of a hostname-keyed exporter)
+ * @param {string} [view]         METRIC_VIEWS entry (default 'all')
  */
-export function exporterQuery(withStatic, lean) {
-  const names = exporterNames(withStatic);
+export function exporterQuery(withStatic, lean, view) {
+  const names = exporterNames(withStatic, view);
   const labels = lean && withStatic === false ? EXPORTER_LEAN_LABELS : EXPORTER_JOIN_LABELS;
   return 'max by (' + labels.join(', ') + ') ({__name__=~"' + names.join('|') + '"})';
 }
@@ -405,9 +418,9 @@ export const NODE_EXPORTER_JOIN_LABELS = ['__name__', 'instance', 'node', 'noden
  * union of the labels the two joins read. Later refreshes ask only the
  * exporter that answered.
  */
-export function mergedQuery(withStatic) {
+export function mergedQuery(withStatic, view) {
   const N = SERIES.nodeExporter;
-  const names = exporterNames(withStatic);
+  const names = exporterNames(withStatic, view);
   names.push(N.chips.split('{')[0], N.power, N.powerInput, N.powerCap, N.busy, N.vramUsed, N.vramTotal, N.uname);
   const labels = EXPORTER_JOIN_LABELS.slice();
   for (let i = 0; i < NODE_EXPORTER_JOIN_LABELS.length; i++) {
@@ -526,8 +539,8 @@ export function createMetricsSource(opts) {
   let statics = null; // static per-GPU fields (STATIC_GPU_FIELDS), fetched with the topology
   let linksAt = 0;
   let lean = false; // the last static query showed every exporter series keyed by hostname
-  let last = null; // previous snapshot, for structural sharing
-  let failures = 0; // consecutive failed fetches against the cached service
+  let lastBy = {}; // view → previous snapshot, for structural sharing and stale fallbacks
+  const failuresBy = {}; // view → consecutive failed fetches against the cached service
 
   function get(name, path) {
     const start = clock.now();
@@ -573,7 +586,7 @@ export function createMetricsSource(opts) {
     seriesCache = null;
     links = null;
     statics = null;
-    last = null;
+    lastBy = {};
     for (const k in nodeStates) delete nodeStates[k];
   }
 
@@ -622,16 +635,21 @@ export function createMetricsSource(opts) {
   }
 
   /**
-   * One metrics snapshot. Resolves to null when no Prometheus is reachable
-   * (the page's "Prometheus Unreachable" state).
+   * One metrics snapshot of the series `view` needs (METRIC_VIEWS; default
+   * 'all'). Resolves to null when no Prometheus is reachable (the page's
+   * "Prometheus Unreachable" state).
+   * @param {string} [view]
    * @returns {Promise<GpuMetrics|null>}
    */
-  function fetchGpuMetrics() {
-    return withPrometheus(snapshotFrom, function () {
+  function fetchGpuMetrics(view) {
+    const v = view === undefined ? 'all' : view;
+    if (METRIC_VIEWS.indexOf(v) < 0) return Promise.reject(new Error('fetchGpuMetrics: unknown view ' + JSON.stringify(view)));
+    return withPrometheus(function (base) { return snapshotFrom(base, v); }, function () {
       // A transient failure (timeout, 5xx) serves the last snapshot marked
       // stale; only repeated failures mean Prometheus went away.
-      failures++;
-      if (last && failures < STALE_FAILURES) {
+      failuresBy[v] = (failuresBy[v] || 0) + 1;
+      const last = lastBy[v];
+      if (last && failuresBy[v] < STALE_FAILURES) {
         return Object.assign({}, last, { stale: true });
       }
       invalidate();
@@ -639,13 +657,13 @@ export function createMetricsSource(opts) {
     });
   }
 
-  function snapshotFrom(base) {
+  function snapshotFrom(base, view) {
     const withStatic = links === null || clock.now() - linksAt >= ttl;
-    const q = source === 'amd-exporter' ? exporterQuery(withStatic, lean)
-      : source === 'node-exporter' ? nodeExporterQuery() : mergedQuery(withStatic);
+    const q = source === 'amd-exporter' ? exporterQuery(withStatic, lean, view)
+      : source === 'node-exporter' ? nodeExporterQuery() : mergedQuery(withStatic, view);
     return combined(base, q).then(function (res) {
       if (!res.ok) return UNREACHABLE;
-      failures = 0;
+      failuresBy[view] = 0;
       const rows = res.rows;
       let joined = { gpus: [], xgmi: {}, links: {} };
       let src = null;
@@ -674,10 +692,12 @@ export function createMetricsSource(opts) {
           src = 'node-exporter';
         }
       }
+      const last = lastBy[view];
       const same = last && last.source === src;
       source = src;
-      last = {
+      lastBy[view] = {
         source: src,
+        view: view,
         gpus: same ? shareGpus(last.gpus, joined.gpus) : joined.gpus,
         xgmi: same ? shareMap(last.xgmi, joined.xgmi) : joined.xgmi,
         links: same ? shareMap(last.links, joined.links || {}) : joined.links || {},
@@ -686,7 +706,7 @@ export function createMetricsSource(opts) {
         // The PromQL this snapshot came from (Metrics page "Query" row).
         query: q,
       };
-      return last;
+      return lastBy[view];
     });
   }
 

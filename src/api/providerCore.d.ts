@@ -36,7 +36,7 @@ export interface ClusterStore {
 }
 
 export interface MetricsSource {
-  fetchGpuMetrics(): Promise<GpuMetrics | null>;
+  fetchGpuMetrics(view?: 'all' | 'gauges' | 'topology'): Promise<GpuMetrics | null>;
   fetchNodeMetrics(nodeName: string): Promise<GpuMetrics | null>;
   fetchGpuOwners(): Promise<GpuMetrics | null>;
   fetchSeries(rangeSec: number, stepSec: number): Promise<GpuMetricsState['series']>;
@@ -46,7 +46,7 @@ export interface ProviderCore {
   Context: Context<AmdGpuContextValue | null>;
   AmdGpuDataProvider: ComponentType<{ children?: ReactNode }>;
   useAmdGpuContext(): AmdGpuContextValue;
-  useGpuMetrics(enabled?: boolean, withSeries?: boolean): GpuMetricsState;
+  useGpuMetrics(enabled?: boolean, withSeries?: boolean, view?: 'all' | 'gauges' | 'topology'): GpuMetricsState;
   useNodeGpuMetrics(nodeName: string | null, enabled?: boolean): GpuMetricsState;
   useGpuOwners(enabled?: boolean): GpuMetricsState;
   storeFor(cluster: string): ClusterStore;

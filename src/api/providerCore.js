@@ -199,21 +199,24 @@ export function createProviderCore(React, lib, deps) {
   }
 
   /**
-   * Cluster-wide GPU telemetry (+ power/HBM series when `withSeries`).
+   * Cluster-wide GPU telemetry (+ power/HBM series when `withSeries`) of the
+   * series `view` draws (metrics.js METRIC_VIEWS: 'gauges' for the Metrics
+   * page, 'topology' for GPU Nodes, default 'all').
    * Unlike the reference it does not wait for the cluster context to finish
    * loading (MetricsPage.tsx:203-205): the two are independent and fetched in
    * parallel.
    */
-  function useGpuMetrics(enabled, withSeries) {
+  function useGpuMetrics(enabled, withSeries, view) {
     const on = enabled === undefined ? true : enabled;
     const series = withSeries === undefined ? true : withSeries;
+    const v = view || 'all';
     const cluster = clusterKey();
     const source = metricsSourceFor(cluster);
     const settings = loadSettings();
-    const key = 'gpus|' + sourceKey(cluster, settings) + '|' + series + '|' + settings.seriesMinutes;
+    const key = 'gpus|' + sourceKey(cluster, settings) + '|' + v + '|' + series + '|' + settings.seriesMinutes;
     return useMetricsFetch(on ? key : null, function () {
       return Promise.all([
-        source.fetchGpuMetrics(),
+        source.fetchGpuMetrics(v),
         series ? source.fetchSeries(settings.seriesMinutes * 60, seriesStepSec(settings)) : Promise.resolve(null),
       ]);
     });

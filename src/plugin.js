@@ -76,7 +76,7 @@ export function createPlugin(env) {
    */
   function NodesPage() {
     const ctx = core.useAmdGpuContext();
-    const m = core.useGpuMetrics(true, false);
+    const m = core.useGpuMetrics(true, false, 'topology');
     function refresh() {
       ctx.refresh();
       m.refresh();
@@ -102,7 +102,7 @@ export function createPlugin(env) {
   /** Power, HBM, activity, temperature, RAS and xGMI telemetry from Prometheus (reference MetricsPage.tsx, C9). */
   function MetricsPage() {
     const ctx = core.useAmdGpuContext();
-    const m = core.useGpuMetrics(true, true);
+    const m = core.useGpuMetrics(true, true, 'gauges');
     return h(Page, { vm: metricsView(ctx, m), onRefresh: m.refresh });
   }
 

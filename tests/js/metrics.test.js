@@ -25,6 +25,7 @@ import {
   nodeSlice,
   ownersQuery,
   promString,
+  METRIC_VIEWS,
 } from '../../src/api/metrics.js';
 
 import { BASE0, BASE1, exporterData, ok, prom, vec } from './promFake.js';
@@ -366,6 +367,87 @@ describe('fetchGpuMetrics', () => {
     const src = createMetricsSource({ request: prom() });
     const m = await src.fetchGpuMetrics();
     expect(m.gpus[0].powerCapWatts).toBe(1400);
+  });
+});
+
+describe('page views (each page asks only for what it draws)', () => {
+  const E = SERIES.exporter;
+  const queried = (request) => request.mock.calls.map((c) => decodeURIComponent(c[0])).filter((p) => p.indexOf('max by') >= 0);
+
+  it('lists the views', () => {
+    expect(METRIC_VIEWS).toEqual(['all', 'gauges', 'topology']);
+  });
+
+  it("'gauges' (Metrics page) asks for every per-GPU gauge and no xGMI link", () => {
+    const q = exporterQuery(false, true, 'gauges');
+    [E.power, E.vramUsed, E.gfx, E.umc, E.temp, E.eccCorrect, E.eccUncorrect].forEach((n) => expect(q).toContain(n));
+    expect(q).not.toContain('xgmi');
+    expect(mergedQuery(true, 'gauges')).not.toContain(E.xgmiRe);
+  });
+
+  it("'topology' (GPU Nodes page) asks for the owner-bearing power gauge and the xGMI links only", () => {
+    const q = exporterQuery(false, true, 'topology');
+    expect(q).toContain(E.power);
+    expect(q).toContain(E.xgmiRe);
+    [E.vramUsed, E.gfx, E.umc, E.temp, E.eccCorrect].forEach((n) => expect(q).not.toContain(n));
+    // static series (link hops, caps) still ride along when the cached copy is stale
+    expect(exporterQuery(true, false, 'topology')).toContain(E.linkHops);
+  });
+
+  it("'all' is the union and the default", () => {
+    expect(exporterQuery(false, true)).toBe(exporterQuery(false, true, 'all'));
+    const all = exporterQuery(false, true, 'all');
+    expect(all).toContain(E.xgmiRe);
+    expect(all).toContain(E.gfx);
+  });
+
+  it('a gauges snapshot has the GPU gauges and no links; a topology snapshot has owners and links', async () => {
+    const request = prom({ data: exporterData(['n0', 'n1']) });
+    const src = createMetricsSource({ request });
+    const g = await src.fetchGpuMetrics('gauges');
+    expect(g.view).toBe('gauges');
+    expect(g.gpus).toHaveLength(16);
+    expect(g.gpus[3].gfxActivityPct).toBe(50);
+    expect(Object.keys(g.xgmi)).toHaveLength(0);
+    const t = await src.fetchGpuMetrics('topology');
+    expect(t.view).toBe('topology');
+    expect(Object.keys(t.xgmi).sort()).toEqual(['n0', 'n1']);
+    expect(t.gpus.filter((x) => x.pod).map((x) => x.nodeName + '/' + x.pod)).toEqual(['n0/train-0', 'n0/train-1', 'n1/train-0', 'n1/train-1']);
+    expect(t.gpus[0].gfxActivityPct).toBe(null);
+    // the static copy fetched by the first query serves the second
+    expect(t.gpus[0].vramTotalBytes).toBe(g.gpus[0].vramTotalBytes);
+    const qs = queried(request);
+    expect(qs.filter((q) => q.indexOf(E.xgmiRe) >= 0)).toHaveLength(1);
+  });
+
+  it('each view keeps its own previous snapshot for sharing and stale fallbacks', async () => {
+    const src = createMetricsSource({ request: prom({ data: exporterData(['n0']) }) });
+    const g1 = await src.fetchGpuMetrics('gauges');
+    await src.fetchGpuMetrics('topology');
+    const g2 = await src.fetchGpuMetrics('gauges');
+    expect(g2.gpus).toBe(g1.gpus);
+  });
+
+  it('rejects an unknown view', async () => {
+    const src = createMetricsSource({ request: prom() });
+    let err = null;
+    await src.fetchGpuMetrics('everything').catch((e) => { err = e; });
+    expect(String(err)).toContain('unknown view');
+  });
+
+  it('a gauges refresh moves about half the bytes of the all-series refresh', async () => {
+    const sizes = {};
+    for (const v of ['all', 'gauges', 'topology']) {
+      const request = prom({ data: exporterData(['n0', 'n1', 'n2', 'n3']) });
+      const src = createMetricsSource({ request });
+      await src.fetchGpuMetrics(v); // static copy
+      const before = request.mock.calls.length;
+      await src.fetchGpuMetrics(v);
+      const res = await request.mock.results[before].value;
+      sizes[v] = JSON.stringify(res).length;
+    }
+    expect(sizes.gauges).toBeLessThan(sizes.all);
+    expect(sizes.topology).toBeLessThan(sizes.all);
   });
 });
 

@@ -24,6 +24,8 @@ import { resetSharedStores } from '../../src/api/clusterStore.js';
 import { clearViewMemo } from '../../src/view/pages.js';
 import { DEVICE_CONFIG_LIST_PATH } from '../../src/api/amdgpu.js';
 import { makeDeviceConfig, makeGpuNode, makeGpuPod, makeNode, makePlainPod, makePluginPod } from './fixtures.js';
+import { exporterData, prom } from './promFake.js';
+import { SERIES } from '../../src/api/metrics.js';
 
 const h = React.createElement;
 
@@ -332,5 +334,43 @@ describe('settings page', () => {
     r.change(r.getByLabelText('Prometheus port'), '9090');
     r.blur(r.getByLabelText('Prometheus port'));
     expect(storage.saved[2].prometheus).toEqual({ namespace: 'monitoring', service: 'prom', port: '9090' });
+  });
+});
+
+describe('page-scoped telemetry', () => {
+  function withPrometheus() {
+    cluster();
+    const fake = prom({ data: exporterData(['mi355x-0', 'mi355x-1']) });
+    const crd = lib.api.handler;
+    lib.api.handler = (p) => (p.indexOf('/proxy/api/v1/') >= 0 ? fake(p) : crd(p));
+    return fake;
+  }
+  const liveQueries = (fake) => fake.mock.calls.map((c) => decodeURIComponent(c[0])).filter((p) => p.indexOf('/query?query=max by') >= 0);
+
+  it('Metrics page: per-GPU gauges, no xGMI links', async () => {
+    const fake = withPrometheus();
+    const r = render(h(route('/amd-gpu/metrics')));
+    await r.settle();
+    const qs = liveQueries(fake);
+    expect(qs.length).toBeGreaterThan(0);
+    qs.forEach((q) => {
+      expect(q).toContain(SERIES.exporter.gfx);
+      expect(q).not.toContain(SERIES.exporter.xgmiRe);
+    });
+    expect(r.html()).toContain('GPU Power Summary');
+    r.unmount();
+  });
+
+  it('GPU Nodes page: owners and xGMI links, none of the Metrics gauges', async () => {
+    const fake = withPrometheus();
+    const r = render(h(route('/amd-gpu/nodes')));
+    await r.settle();
+    const qs = liveQueries(fake);
+    expect(qs.length).toBeGreaterThan(0);
+    qs.forEach((q) => {
+      expect(q).toContain(SERIES.exporter.xgmiRe);
+      expect(q).not.toContain(SERIES.exporter.gfx);
+    });
+    r.unmount();
   });
 });
