@@ -259,3 +259,33 @@ describe('a real view-model end to end', () => {
     expect(r.getByLabelText(vm.refresh.ariaLabel).tag).toBe('button');
   });
 });
+
+describe('harness React enforces the rules real React enforces', () => {
+  it('a getSnapshot that returns a new object every call is rejected (infinite re-render in React)', () => {
+    function Bad() {
+      const v = React.useSyncExternalStore(() => () => {}, () => ({}));
+      return h('div', null, String(!!v));
+    }
+    expect(() => render(h(Bad))).toThrow('getSnapshot should be cached');
+  });
+
+  it('a hook skipped on re-render is rejected', async () => {
+    let setFlag = null;
+    function Cond() {
+      const s = React.useState(false);
+      setFlag = s[1];
+      if (s[0]) return h('div', null, 'early');
+      React.useMemo(() => 1, []);
+      return h('div', null, 'late');
+    }
+    const r = render(h(Cond));
+    let err = null;
+    try {
+      setFlag(true);
+      await r.settle();
+    } catch (e) {
+      err = e;
+    }
+    expect(String(err)).toContain('Rendered fewer hooks than expected');
+  });
+});

@@ -168,6 +168,9 @@ export function useSyncExternalStore(subscribe, getSnapshot) {
   const inst = current;
   const slot = hookSlot(function () { return { subscribe: null, unsubscribe: null, value: undefined }; });
   const value = getSnapshot();
+  // React (dev) reads the snapshot twice: a store whose getSnapshot builds a
+  // new object each call would re-render forever.
+  if (!Object.is(getSnapshot(), value)) throw new Error('The result of getSnapshot should be cached to avoid an infinite loop');
   slot.value = value;
   slot.getSnapshot = getSnapshot;
   if (slot.subscribe !== subscribe) {
@@ -372,12 +375,16 @@ function renderInstance(inst, prevProps) {
     inst.renders++;
     inst.ctxReads = new Map();
     let result;
+    let used = 0;
     try {
       result = t(inst.props);
+      used = hookIndex;
     } finally {
       current = prev;
       hookIndex = prevIdx;
     }
+    // React: "Rendered fewer hooks than expected" (a hook behind a condition or an early return).
+    if (used < inst.hooks.length) throw new Error('Rendered fewer hooks than expected in ' + typeName(t));
     if (result === undefined) throw new Error(typeName(t) + ' returned undefined (return null to render nothing)');
     inst.out = reconcileChildren(root, inst, result);
   } else {
