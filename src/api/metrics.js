@@ -593,6 +593,20 @@ export function createMetricsSource(opts) {
   /** Marker for "the request did not reach a Prometheus". */
   const UNREACHABLE = {};
 
+  // Fetches in flight, by what they fetch: a second caller while one is
+  // pending (two views on one page, React StrictMode re-running a mount
+  // effect, a poller tick during a click) shares its answer instead of
+  // sending the same query again.
+  const inflight = {};
+  function shared(key, make) {
+    if (inflight[key]) return inflight[key];
+    const p = make();
+    inflight[key] = p;
+    const done = function () { if (inflight[key] === p) delete inflight[key]; };
+    p.then(done, done);
+    return p;
+  }
+
   /**
    * Run `fn(base)` against Prometheus. With no cached service the preferred
    * candidate is queried directly — its answer doubles as discovery, so the
@@ -644,6 +658,10 @@ export function createMetricsSource(opts) {
   function fetchGpuMetrics(view) {
     const v = view === undefined ? 'all' : view;
     if (METRIC_VIEWS.indexOf(v) < 0) return Promise.reject(new Error('fetchGpuMetrics: unknown view ' + JSON.stringify(view)));
+    return shared('gpus|' + v, function () { return gpuSnapshot(v); });
+  }
+
+  function gpuSnapshot(v) {
     return withPrometheus(function (base) { return snapshotFrom(base, v); }, function () {
       // A transient failure (timeout, 5xx) serves the last snapshot marked
       // stale; only repeated failures mean Prometheus went away.
@@ -734,7 +752,10 @@ export function createMetricsSource(opts) {
    * @returns {Promise<GpuMetrics|null>}
    */
   function fetchNodeMetrics(nodeName) {
-    const key = String(nodeName);
+    return shared('node|' + String(nodeName), function () { return nodeSnapshot(String(nodeName)); });
+  }
+
+  function nodeSnapshot(key) {
     if (!nodeStates[key]) nodeStates[key] = { last: null, links: null, statics: null, staticAt: 0, failures: 0 };
     const st = nodeStates[key];
     function clusterWide() {
@@ -789,6 +810,10 @@ export function createMetricsSource(opts) {
    * @returns {Promise<GpuMetrics|null>}
    */
   function fetchGpuOwners() {
+    return shared('owners', ownersSnapshot);
+  }
+
+  function ownersSnapshot() {
     return withPrometheus(function (base) {
       return combined(base, ownersQuery()).then(function (res) {
         if (!res.ok) return UNREACHABLE;

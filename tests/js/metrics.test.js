@@ -451,6 +451,35 @@ describe('page views (each page asks only for what it draws)', () => {
   });
 });
 
+describe('in-flight sharing', () => {
+  const live = (request) => request.mock.calls.filter((c) => decodeURIComponent(c[0]).indexOf('max by') >= 0).length;
+
+  it('concurrent fetches of one view share one request and one answer', async () => {
+    const request = prom({ data: exporterData(['n0']) });
+    const src = createMetricsSource({ request });
+    const [a, b] = await Promise.all([src.fetchGpuMetrics('gauges'), src.fetchGpuMetrics('gauges')]);
+    expect(a).toBe(b);
+    expect(live(request)).toBe(1);
+  });
+
+  it('different views, owners and nodes are separate requests', async () => {
+    const request = prom({ data: exporterData(['n0']) });
+    const src = createMetricsSource({ request });
+    await src.fetchGpuMetrics('gauges');
+    const n = live(request);
+    await Promise.all([src.fetchGpuMetrics('gauges'), src.fetchGpuMetrics('topology'), src.fetchGpuOwners(), src.fetchNodeMetrics('n0'), src.fetchNodeMetrics('n0')]);
+    expect(live(request) - n).toBe(4);
+  });
+
+  it('a fetch after the previous one settled asks again', async () => {
+    const request = prom({ data: exporterData(['n0']) });
+    const src = createMetricsSource({ request });
+    await src.fetchGpuMetrics();
+    await src.fetchGpuMetrics();
+    expect(live(request)).toBe(2);
+  });
+});
+
 describe('fetchNodeMetrics (detail pages)', () => {
   const paths = (request, from) => request.mock.calls.slice(from || 0).map((c) => decodeURIComponent(c[0]));
 

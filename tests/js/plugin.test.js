@@ -374,3 +374,42 @@ describe('page-scoped telemetry', () => {
     r.unmount();
   });
 });
+
+describe('React StrictMode (effects mounted, cleaned up and mounted again)', () => {
+  function withPrometheus() {
+    cluster();
+    const fake = prom({ data: exporterData(['mi355x-0', 'mi355x-1']) });
+    const crd = lib.api.handler;
+    lib.api.handler = (p) => (p.indexOf('/proxy/api/v1/') >= 0 ? fake(p) : crd(p));
+    return fake;
+  }
+  const liveQueries = (fake) => fake.mock.calls.filter((c) => decodeURIComponent(c[0]).indexOf('/query?query=max by') >= 0).length;
+
+  it('Overview mounts with one CRD request', async () => {
+    cluster();
+    const r = render(h(route('/amd-gpu')), { strict: true });
+    await r.settle();
+    expect(lib.api.calls.filter((p) => p === DEVICE_CONFIG_LIST_PATH)).toHaveLength(1);
+    expect(r.instances(CC.SectionHeader)[0].props.title).toBe('AMD GPU — Overview');
+    r.unmount();
+  });
+
+  it('Metrics page mounts with one live query and renders its data', async () => {
+    const fake = withPrometheus();
+    const r = render(h(route('/amd-gpu/metrics')), { strict: true });
+    await r.settle();
+    expect(liveQueries(fake)).toBe(1);
+    expect(r.html()).toContain('GPU Power Summary');
+    r.unmount();
+  });
+
+  it('Node detail section mounts with one node-scoped query', async () => {
+    const fake = withPrometheus();
+    const Detail = reg.details[0];
+    const r = render(h(() => Detail({ resource: { kind: 'Node', jsonData: makeGpuNode('mi355x-0') } })), { strict: true });
+    await r.settle();
+    const scoped = fake.mock.calls.filter((c) => decodeURIComponent(c[0]).indexOf('hostname="mi355x-0"') >= 0);
+    expect(scoped).toHaveLength(1);
+    r.unmount();
+  });
+});

@@ -467,9 +467,10 @@ function flushMicrotasks() {
  * Mount `element` and return a handle. All rendering is synchronous; state
  * updates from promises are flushed on a microtask or by `settle()`.
  */
-export function render(element) {
+export function render(element, options) {
   const root = {
     element: element,
+    strict: !!(options && options.strict),
     top: null,
     pendingEffects: [],
     scheduled: false,
@@ -505,6 +506,14 @@ export function render(element) {
       if (typeof e.slot.cleanup === 'function') e.slot.cleanup();
       const r = e.fn();
       e.slot.cleanup = typeof r === 'function' ? r : null;
+      // <StrictMode> (React 18, development): a newly mounted effect is run,
+      // cleaned up and run again, so effects must be idempotent.
+      if (root.strict && !e.slot.strictRemounted) {
+        e.slot.strictRemounted = true;
+        if (typeof e.slot.cleanup === 'function') e.slot.cleanup();
+        const r2 = e.fn();
+        e.slot.cleanup = typeof r2 === 'function' ? r2 : null;
+      }
     }
   }
 
