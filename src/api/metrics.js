@@ -907,7 +907,9 @@ export function createMetricsSource(opts) {
       });
     }
     // A failed range request keeps the last window (retried next time).
-    return withPrometheus(from, function () { return seriesCache ? seriesCache.data : null; });
+    return shared('series|' + range + '|' + step, function () {
+      return withPrometheus(from, function () { return seriesCache ? seriesCache.data : null; });
+    });
   }
 
   return {

@@ -471,6 +471,14 @@ describe('in-flight sharing', () => {
     expect(live(request) - n).toBe(4);
   });
 
+  it('concurrent range fetches of one window share one query_range', async () => {
+    const request = prom({ data: exporterData(['n0']) });
+    const src = createMetricsSource({ request });
+    const [a, b] = await Promise.all([src.fetchSeries(1800, 30), src.fetchSeries(1800, 30)]);
+    expect(a).toBe(b);
+    expect(request.mock.calls.filter((c) => c[0].indexOf('/query_range') >= 0)).toHaveLength(1);
+  });
+
   it('a fetch after the previous one settled asks again', async () => {
     const request = prom({ data: exporterData(['n0']) });
     const src = createMetricsSource({ request });

@@ -399,6 +399,8 @@ describe('React StrictMode (effects mounted, cleaned up and mounted again)', () 
     const r = render(h(route('/amd-gpu/metrics')), { strict: true });
     await r.settle();
     expect(liveQueries(fake)).toBe(1);
+    // at most one range query (none when the shared source's window is current)
+    expect(fake.mock.calls.filter((c) => c[0].indexOf('/query_range') >= 0).length).toBeLessThanOrEqual(1);
     expect(r.html()).toContain('GPU Power Summary');
     r.unmount();
   });
