@@ -156,11 +156,25 @@ export function loader(title: string): LoaderItem;
 export function page(title: string | null, refresh: RefreshButton | null, items: Array<Section | LoaderItem>): PageVM;
 
 export interface Memo {
-  <T>(key: string, deps: readonly unknown[], compute: () => T): T;
+  /** `now` (epoch ms): also hold the value only until the first age label inside it changes. */
+  <T>(key: string, deps: readonly unknown[], compute: () => T, now?: number): T;
   clear(): void;
   size(): number;
 }
 export function createMemo(limit?: number): Memo;
+
+/** Per-object cache (WeakMap keyed on the Kubernetes object); same contract as Memo. */
+export interface ObjectCache {
+  <T>(obj: object, deps: readonly unknown[], compute: () => T, now?: number): T;
+  clear(): void;
+}
+export function createObjectCache(): ObjectCache;
+
+/** Record that the value being built changes at epoch-ms `t` (age labels). */
+export function noteExpiry(t: number | null | undefined): void;
+
+/** Caption of the xGMI matrix: measured topology, or the platform model with measured throughput. */
+export function matrixCaption(b: MatrixBlock): string;
 
 export function sections(vm: PageVM | Section | null): Section[];
 export function sectionTitles(vm: PageVM | Section | null): string[];
