@@ -266,6 +266,18 @@ function amdSchedule(request) {
       if (page === 'metrics') return fetchMetrics('gauges');
       return store.refresh();
     },
+    /**
+     * One page opened on an empty cache, as src/plugin.js mounts it: the
+     * provider's lists + DeviceConfig request, plus that page's own metrics
+     * hook (none on Overview / Device Plugins), all in one wave.
+     */
+    coldOpenPage: function (page) {
+      const base = [store.loadLists(), store.refresh()];
+      if (page === 'nodes') base.push(metrics.fetchGpuMetrics('topology').then(function (m) { pageMetrics.nodes = m; }));
+      else if (page === 'pods') base.push(metrics.fetchGpuOwners().then(function (m) { pageMetrics.pods = m; }));
+      else if (page === 'metrics') base.push(fetchMetrics('gauges'));
+      return Promise.all(base);
+    },
     pageMetrics: function (page) { return page in pageMetrics && pageMetrics[page] ? pageMetrics[page] : mstate.metrics; },
     /** Route switch: render from the shared store now, revalidate in the background. */
     switchRoute: function () {
@@ -302,6 +314,7 @@ function referenceSchedule(request) {
       return { rendered: p, background: p };
     },
     refreshPage: r.refreshPage,
+    coldOpenPage: r.coldOpenPage,
     pageMetrics: function () { return r.metrics(); },
     ctx: r.snapshot,
     mstate: function () { return { metrics: r.metrics(), fetchError: r.metrics() ? null : 'unreachable', fetching: false }; },
@@ -414,6 +427,25 @@ async function serve(a) {
         out.latencies = lat;
         out.renderMs = renderMs;
         out.requests = req;
+      } else if (c.cmd === 'coldPages') {
+        // Per-page cold open: a fresh schedule (empty caches, new client)
+        // per open; time to that page's data committed + the page rendered.
+        out.pages = {};
+        for (let p = 0; p < PAGES.length; p++) {
+          const page = PAGES[p];
+          const lat = [];
+          let req = 0;
+          for (let i = 0; i < n; i++) {
+            const s = (name === 'reference' ? referenceSchedule : amdSchedule)(makeRequest(a.url, counter));
+            const before = counter.n;
+            const t0 = process.hrtime();
+            await s.coldOpenPage(page);
+            renderOne(page, s.ctx(), s.mstate(), s.pageMetrics(page));
+            lat.push(ms(process.hrtime(t0)));
+            req = counter.n - before;
+          }
+          out.pages[page] = { latencies: lat, requests: req };
+        }
       } else if (c.cmd === 'steps') {
         const L = get(name);
         if (!L.opened) {

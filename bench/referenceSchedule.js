@@ -174,6 +174,17 @@ export function createReferenceSchedule(request) {
     await fetchMetrics();
   }
 
+  /**
+   * One page mounted cold, as the reference wires it: every route mounts a
+   * fresh provider (lists alongside the serial CRD + selector chain,
+   * src/index.tsx:87-145); the Metrics page then waits for the provider to
+   * finish loading before it fetches (MetricsPage.tsx:203-205).
+   */
+  async function coldOpenPage(page) {
+    await Promise.all([loadLists(), providerRefresh()]);
+    if (page === 'metrics') await fetchMetrics();
+  }
+
   /** Snapshot in the shape the view-models take. */
   function snapshot() {
     const gpuNodes = filterAmdGpuNodes(state.nodes || []);
@@ -193,5 +204,5 @@ export function createReferenceSchedule(request) {
     };
   }
 
-  return { refresh: refresh, refreshPage: refreshPage, coldOpen: coldOpen, snapshot: snapshot, metrics: function () { return state.metrics; } };
+  return { refresh: refresh, refreshPage: refreshPage, coldOpen: coldOpen, coldOpenPage: coldOpenPage, snapshot: snapshot, metrics: function () { return state.metrics; } };
 }

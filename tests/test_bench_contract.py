@@ -42,6 +42,16 @@ def _check(line, n):
     for v in pp.values():
         assert v["amd"] < v["reference"], pp
     assert line["all_pages_refresh"]["requests"]["reference"] == 9
+    # Cold open per page: the reference mounts a fresh provider (2 lists + CRD + 3 selectors), and its Metrics
+    # page then runs discovery + 4 queries; the new plugin sends one wave (lists, CRD, the page's own query).
+    cold = line["cold_open_per_page_p50_ms"]
+    assert set(cold) == set(pp)
+    for k in ("overview", "devicePlugins", "nodes", "pods"):
+        assert cold[k]["requests"]["reference"] == 6
+    assert cold["metrics"]["requests"]["reference"] == 6 + 5
+    assert cold["overview"]["requests"]["amd"] == 3 and cold["nodes"]["requests"]["amd"] == 4
+    for v in cold.values():
+        assert v["amd"] < v["reference"], cold
 
 
 def test_bench_single_rank():

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Scaling curve + BASELINE configs: run bench.py per point and tabulate.
 
-    python tools/sweep.py --out gpurun_out/sweep [--steps 30] [--rtt-ms 20]
+    python tools/sweep.py --out gpurun_out/sweep [--steps 30] [--rtt-ms 20] [--beyond 16,32,64]
     python tools/sweep.py --stress --out gpurun_out/stress [--stress-nodes 16,64,256,1000] [--events 1000]
 
 ``--stress``: the cluster-size axis under watch churn (bench/stress.js) —
@@ -52,11 +52,21 @@ PAGE_COLS = [("overview", "Overview"), ("devicePlugins", "Device Plugins"), ("no
              ("pods", "GPU Pods"), ("metrics", "Metrics")]
 
 
+def cold_mean(line):
+    cp = line.get("cold_open_per_page_p50_ms")
+    if not cp:
+        return "—"
+    ref = sum(v["reference"] for v in cp.values()) / len(cp)
+    amd = sum(v["amd"] for v in cp.values()) / len(cp)
+    return f"{ref:.0f} → {amd:.0f}"
+
+
 def table(rows):
     """Markdown table led by the per-page Refresh-click p50s (reference → new)."""
     head = ["Config", "GPU nodes"] + [f"{t} ref → new (ms)" for _, t in PAGE_COLS] + [
         "Mean per page ref → new (ms)", "Speed-up", "All-pages composite ref → new (ms)",
-        "Cold open ref → new (ms)", "Route switch ref → new (ms)", "GPU nodes rendered", "GPU pods rendered",
+        "Cold open, mean per page ref → new (ms)", "Cold open, all pages ref → new (ms)", "Route switch ref → new (ms)",
+        "GPU nodes rendered", "GPU pods rendered",
         "GPUs monitored", "Live GPU telemetry"]
     md = ["| " + " | ".join(head) + " |", "|---|---:|" + "---|" * (len(head) - 2)]
     for r in rows:
@@ -68,6 +78,7 @@ def table(rows):
         cells += [f"{pp[k]['reference']:.1f} → {pp[k]['amd']:.1f}" for k, _ in PAGE_COLS]
         cells += [f"{l['baseline']['value_ms']:.1f} → {l['value']:.1f}", f"{l['baseline']['value_ms'] / l['value']:.1f}×",
                   f"{comp['reference_p50_ms']:.1f} → {comp['amd_p50_ms']:.1f}",
+                  cold_mean(l),
                   f"{l['cold_open_p50_ms']['reference']:.0f} → {l['cold_open_p50_ms']['amd']:.0f}",
                   f"{l['route_switch_p50_ms']['reference']:.0f} → {l['route_switch_p50_ms']['amd']:.1f}",
                   str(l["rendered"]["gpu_nodes"]), str(l["rendered"]["gpu_pods"]), str(l["rendered"]["gpus_monitored"]),
@@ -128,12 +139,14 @@ def main():
     p.add_argument("--stress", action="store_true", help="watch-churn stress of the cluster-size axis instead")
     p.add_argument("--stress-nodes", default="16,64,256,1000")
     p.add_argument("--events", type=int, default=1000)
+    p.add_argument("--beyond", default="", help="extra node counts past the BASELINE configs, e.g. 16,32,64")
     args = p.parse_args()
     if args.stress:
         return stress(args)
     os.makedirs(args.out, exist_ok=True)
     rows = []
-    for kind, val in POINTS:
+    points = POINTS + [("nodes", v.strip()) for v in args.beyond.split(",") if v.strip()]
+    for kind, val in points:
         line = run(kind, val, args)
         rows.append({"kind": kind, "point": val, "line": line})
         print(f"{kind}={val}: per-page p50 {line['value']} ms vs ref {line['baseline']['value_ms']} ms", flush=True)
