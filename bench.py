@@ -144,14 +144,14 @@ def main(argv=None) -> int:
             ref_steps = args.ref_steps if args.ref_steps is not None else args.steps
             # Measured baseline: the reference plugin's schedule (untimed region).
             ref_cold = drv.call("cold", "reference", n=3)
-            ref_cold_pages = drv.call("coldPages", "reference", n=3)
+            ref_cold_pages = drv.call("coldPages", "reference", n=5)
             drv.call("pages", "reference", n=max(1, args.warmup))
             ref_pages = drv.call("pages", "reference", n=ref_steps)
             ref = drv.call("steps", "reference", n=max(3, ref_steps // 2))
             ref_switch = drv.call("switch", "reference", n=3)
             # Flagship schedule.
             amd_cold = drv.call("cold", "amd", n=3)
-            amd_cold_pages = drv.call("coldPages", "amd", n=3)
+            amd_cold_pages = drv.call("coldPages", "amd", n=5)
             drv.call("pages", "amd", n=max(1, args.warmup))
             D.barrier(info)
             quiet_sync()

@@ -34,6 +34,26 @@ import {
 import { countRows } from '../src/view/ir.js';
 import { renderPage, renderSection } from '../src/view/html.js';
 import { createReferenceSchedule } from './referenceSchedule.js';
+import { PerformanceObserver, performance } from 'perf_hooks';
+
+// Garbage-collection pauses (start, duration in ms, performance.now() clock),
+// so a timed sample can say how much of it was the collector.
+const gcPauses = [];
+try {
+  new PerformanceObserver(function (list) {
+    list.getEntries().forEach(function (e) { gcPauses.push([e.startTime, e.duration]); });
+    if (gcPauses.length > 4096) gcPauses.splice(0, gcPauses.length - 4096);
+  }).observe({ entryTypes: ['gc'] });
+} catch (e) {
+  // no GC entries on this runtime
+}
+
+/** GC pause time (ms) that started inside [from, to] (performance.now() clock). */
+function gcBetween(from, to) {
+  let t = 0;
+  for (let i = 0; i < gcPauses.length; i++) if (gcPauses[i][0] >= from && gcPauses[i][0] <= to) t += gcPauses[i][1];
+  return t;
+}
 
 function parseArgs(argv) {
   const a = { url: null, steps: 20, warmup: 3, cold: 5, out: null, schedule: 'both' };
@@ -412,8 +432,11 @@ async function serve(a) {
         const lat = [];
         const renderMs = [];
         let req = 0;
+        // Cold caches, warm connections: a browser keeps its keep-alive
+        // sockets to the Headlamp origin across in-app navigations.
+        const pool = makeRequest(a.url, counter);
         for (let i = 0; i < n; i++) {
-          const s = (name === 'reference' ? referenceSchedule : amdSchedule)(makeRequest(a.url, counter));
+          const s = (name === 'reference' ? referenceSchedule : amdSchedule)(pool);
           const before = counter.n;
           const t0 = process.hrtime();
           await s.coldOpen();
@@ -431,20 +454,31 @@ async function serve(a) {
         // Per-page cold open: a fresh schedule (empty caches, new client)
         // per open; time to that page's data committed + the page rendered.
         out.pages = {};
+        const pool = makeRequest(a.url, counter); // warm connections, as for 'cold'
         for (let p = 0; p < PAGES.length; p++) {
           const page = PAGES[p];
           const lat = [];
+          const renderMs = [];
+          const gcMs = [];
           let req = 0;
+          let trace = null;
           for (let i = 0; i < n; i++) {
-            const s = (name === 'reference' ? referenceSchedule : amdSchedule)(makeRequest(a.url, counter));
+            const s = (name === 'reference' ? referenceSchedule : amdSchedule)(pool);
             const before = counter.n;
+            const p0 = performance.now();
             const t0 = process.hrtime();
             await s.coldOpenPage(page);
+            const t1 = process.hrtime();
             renderOne(page, s.ctx(), s.mstate(), s.pageMetrics(page));
+            renderMs.push(ms(process.hrtime(t1)));
             lat.push(ms(process.hrtime(t0)));
+            // observer entries are delivered asynchronously
+            await new Promise(function (r) { setImmediate(r); });
+            gcMs.push(gcBetween(p0, performance.now()));
             req = counter.n - before;
+            if (s.spans) trace = traceSummary(s.spans);
           }
-          out.pages[page] = { latencies: lat, requests: req };
+          out.pages[page] = { latencies: lat, renderMs: renderMs, gcMs: gcMs, requests: req, trace: trace };
         }
       } else if (c.cmd === 'steps') {
         const L = get(name);

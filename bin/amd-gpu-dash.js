@@ -129,13 +129,22 @@ async function main() {
   const metrics = createMetricsSource({ request: request, timeoutMs: a.timeout, services: prometheusCandidates(settings) });
   const mstate = { metrics: null, series: null, fetchError: null, fetching: false };
 
+  // Telemetry per page, as the plugin's pages ask for it (ADR 008): none for
+  // Overview / Device Plugins, the page's view for Nodes / Metrics, every
+  // series for `all`; range series only where the Metrics page draws them.
+  const VIEW = { all: 'all', nodes: 'topology', pods: 'owners', metrics: 'gauges' };
+  const view = VIEW[a.page] || null;
   async function fetchAll(first) {
-    const jobs = [store.refresh(), metrics.fetchGpuMetrics(), metrics.fetchSeries(1800, 30)];
+    const jobs = [
+      store.refresh(),
+      view === 'owners' ? metrics.fetchGpuOwners() : view ? metrics.fetchGpuMetrics(view) : Promise.resolve(null),
+      view === 'all' || view === 'gauges' ? metrics.fetchSeries(1800, 30) : Promise.resolve(null),
+    ];
     if (first) jobs.push(store.loadLists());
     const r = await Promise.all(jobs);
     mstate.metrics = r[1];
     mstate.series = r[2];
-    mstate.fetchError = r[1] ? null : 'Could not reach Prometheus';
+    mstate.fetchError = r[1] || !view ? null : 'Could not reach Prometheus';
   }
 
   function print() {

@@ -47,3 +47,18 @@ def test_unreachable_prometheus_and_bad_arguments(url):
     assert run("--prometheus", "not-a-service").returncode == 2
     dead = run("--url", "http://127.0.0.1:9", "--page", "overview", "--timeout", "500")
     assert dead.returncode == 0 and "Error" in dead.stdout  # the page's own error state, not a crash
+
+
+def test_single_pages_ask_only_for_their_telemetry(url):
+    pods = run("--url", url, "--page", "pods")
+    assert pods.returncode == 0 and "Assigned GPUs" in pods.stdout and "mi355x-000: GPU 0" in pods.stdout
+    nodes = run("--url", url, "--page", "nodes")
+    assert nodes.returncode == 0 and "xGMI topology (measured)" in nodes.stdout
+
+
+def test_overview_sends_no_prometheus_request():
+    fc = make_fake(1, source="amd-exporter", latency_ms=1)
+    with ServerThread(fc) as srv:
+        r = run("--url", srv.url, "--page", "overview")
+        assert r.returncode == 0 and "Error" not in r.stdout
+        assert fc.stats().get("prometheus", 0) == 0 and fc.stats()["apiserver"] >= 3
