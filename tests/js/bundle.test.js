@@ -30,6 +30,11 @@ function load(libObj) {
   return new Function('pluginLib', 'return (' + built.code.trim().replace(/;$/, '') + '\n);')(libObj);
 }
 
+function load2(code) {
+  // eslint-disable-next-line no-new-func
+  return new Function('pluginLib', 'return (' + code.trim().replace(/;$/, '') + '\n);')(pluginLib());
+}
+
 function cluster() {
   lib.lists.Node = [[makeGpuNode('mi355x-0'), makeGpuNode('mi355x-1'), makeNode('cpu-0')], null];
   lib.lists.Pod = [[makeGpuPod('train-a', { gpus: 4 }), makeGpuPod('train-b', { gpus: 2, node: 'mi355x-1' }), makePlainPod('web-0'), makePluginPod('amdgpu-dp-0')], null];
@@ -129,6 +134,33 @@ describe('transformModule', () => {
     expect(exportsObj.f()).toBe(6);
     expect(exportsObj.default).toBe(exportsObj.f);
     expect(exportsObj.m).toBe(1);
+  });
+
+  it('exports every name a destructuring declaration binds (src/components/View.tsx)', () => {
+    const t = transformModule("import { plugin } from './y.js';\nexport const { Page, Section: S, ...rest } = plugin.view;\n", file, dep);
+    const exportsObj = {};
+    // eslint-disable-next-line no-new-func
+    new Function('__exports', '__req', '__ext', '__export', '__default', '__missing', t.code)(
+      exportsObj,
+      () => ({ plugin: { view: { Page: 1, Section: 2, Value: 3 } } }),
+      null,
+      (o, k, g) => Object.defineProperty(o, k, { enumerable: true, get: g }),
+      (m) => m,
+      (name) => { throw new Error('missing ' + name); },
+    );
+    expect(Object.keys(exportsObj).sort()).toEqual(['Page', 'S', 'rest']);
+    expect(exportsObj.S).toBe(2);
+    expect(exportsObj.rest).toEqual({ Value: 3 });
+  });
+
+  it('bundles every TypeScript shim under src/ (not only those the entry reaches)', () => {
+    const shims = ['src/components/View.tsx', 'src/api/AmdGpuDataContext.tsx', 'src/components/integrations/NodeColumns.tsx', 'src/components/OverviewPage.tsx'];
+    shims.forEach((f) => {
+      const b = bundle(path.join(ROOT, f));
+      expect(b.modules[b.modules.length - 1]).toBe(f);
+      const mod = load2(b.code);
+      expect(Object.keys(mod).length).toBeGreaterThan(0);
+    });
   });
 
   it('rejects what it does not understand instead of passing it through', () => {
