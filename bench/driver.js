@@ -246,14 +246,15 @@ function writeSnapshots(ctx, mstate, dir, now) {
 // Schedules
 // ---------------------------------------------------------------------------
 
-function amdSchedule(request) {
+function amdSchedule(request, clock) {
   // Request spans from the data layer's tracing hook (clusterStore/metrics onTrace).
   const spans = [];
   function onTrace(span) {
     spans.push(span);
   }
-  const store = createClusterStore({ request: request, onTrace: onTrace, clock: hiResClock });
-  const metrics = createMetricsSource({ request: request, onTrace: onTrace, clock: hiResClock });
+  const clk = clock || hiResClock;
+  const store = createClusterStore({ request: request, onTrace: onTrace, clock: clk });
+  const metrics = createMetricsSource({ request: request, onTrace: onTrace, clock: clk });
   const mstate = { metrics: null, fetchError: null, fetching: false, series: null };
   // Per-page metrics state, as each page's own hook holds it (plugin.js):
   // GPU Nodes → owners + xGMI links ('topology'), GPU Pods → pod→GPU
@@ -545,13 +546,23 @@ async function serve(a) {
           out.pages[PAGES[p]] = { latencies: lat[PAGES[p]], requestsPerClick: reqs[PAGES[p]] / n, tableRows: rows[PAGES[p]] };
         }
       } else if (c.cmd === 'snapshot') {
-        // Static HTML of every view (docs/screenshots): same IR → HTML path as the benchmark.
-        const L = get(name);
-        if (!L.opened) {
-          await L.s.coldOpen();
-          L.opened = true;
+        // Static HTML of every view (docs/screenshots): same IR → HTML path as
+        // the benchmark. With `now` the data layer runs on that fixed clock
+        // (fetch times, range windows), so the files are reproducible.
+        let snap;
+        if (c.now) {
+          const fixed = { setTimeout: setTimeout, clearTimeout: clearTimeout, now: function () { return c.now; } };
+          snap = amdSchedule(makeRequest(a.url, counter), fixed);
+          await snap.coldOpen();
+        } else {
+          const L = get(name);
+          if (!L.opened) {
+            await L.s.coldOpen();
+            L.opened = true;
+          }
+          snap = L.s;
         }
-        out.files = writeSnapshots(L.s.ctx(), L.s.mstate(), c.dir, c.now);
+        out.files = writeSnapshots(snap.ctx(), snap.mstate(), c.dir, c.now);
       } else if (c.cmd === 'detail') {
         // Native detail pages opened on a warm cluster (a plugin page loaded
         // before): Pod detail and Node detail each fetch their node's

@@ -27,7 +27,11 @@ def main():
     ap.add_argument("--nodes", type=int, default=2)
     ap.add_argument("--out", default=os.path.join(ROOT, "docs", "screenshots"))
     a = ap.parse_args()
+    # Reproducible files: Prometheus evaluates at the same instant the data layer's clock reads, and "Last
+    # Fetched" (browser-local time) is rendered in UTC.
+    os.environ["TZ"] = "UTC"
     fc = make_fake(a.nodes, source="amd-exporter", latency_ms=0)
+    fc.now = lambda: NOW_MS / 1000.0
     with ServerThread(fc) as srv, Driver(srv.url) as d:
         files = d.call("snapshot", dir=os.path.abspath(a.out), now=NOW_MS)["files"]
     for f in files:
