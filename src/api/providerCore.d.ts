@@ -54,3 +54,6 @@ export interface ProviderCore {
 }
 
 export function createProviderCore(React: unknown, lib: HeadlampLibLike, deps?: ProviderDeps): ProviderCore;
+
+/** [items, error] from a Headlamp list hook: the `[items, error]` tuple or a `{items, error | errors, isLoading}` object. */
+export function listResult(res: unknown): [unknown[] | null, unknown];

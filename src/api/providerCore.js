@@ -44,6 +44,21 @@ function errorText(e) {
 }
 
 /**
+ * [items, error] from either shape of a Headlamp list-hook result (see
+ * useListOf). `items` null means "not listed yet" (or failed).
+ * @param {any} res
+ * @returns {[any[]|null, any]}
+ */
+export function listResult(res) {
+  if (!res) return [null, null];
+  if (Array.isArray(res)) return [res[0] !== undefined ? res[0] : null, res[1] !== undefined ? res[1] : null];
+  let err = res.error !== undefined ? res.error : null;
+  if (!err && res.errors) err = Array.isArray(res.errors) ? (res.errors.length ? res.errors[0] : null) : res.errors;
+  const items = res.isLoading || res.items === undefined ? null : res.items;
+  return [items, err || null];
+}
+
+/**
  * @param {any} React  React 18 (or the harness stand-in)
  * @param {{K8s: any, ApiProxy: any}} lib  '@kinvolk/headlamp-plugin/lib'
  * @param {{request?: (path: string) => Promise<any>, clusterKey?: () => string,
@@ -102,11 +117,16 @@ export function createProviderCore(React, lib, deps) {
     return ctx;
   }
 
+  /**
+   * [items, error] of a Headlamp list hook. Headlamp's `useList()` returns
+   * `[items, error, ...]` (the reference destructures it, :98-99; items null
+   * while the first list is in flight and when it failed); later Headlamp
+   * releases return a result object `{items, error | errors, isLoading}`.
+   * Both shapes are read, so a host upgrade does not leave pages loading.
+   */
   function useListOf(cls, opts) {
-    // Headlamp returns [items, error, ...]; items is null while the first
-    // list is in flight and stays null when the list failed.
     const res = opts ? cls.useList(opts) : cls.useList();
-    return [res && res[0] !== undefined ? res[0] : null, res ? res[1] : null];
+    return listResult(res);
   }
 
   function AmdGpuDataProvider(props) {

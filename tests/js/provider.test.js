@@ -9,7 +9,7 @@
  */
 import React, { render } from './stubs/react.js';
 import * as lib from './stubs/headlamp-lib.js';
-import { OUTSIDE_PROVIDER, PROMETHEUS_UNREACHABLE, STALE_MS, createProviderCore } from '../../src/api/providerCore.js';
+import { OUTSIDE_PROVIDER, PROMETHEUS_UNREACHABLE, STALE_MS, createProviderCore, listResult } from '../../src/api/providerCore.js';
 import { resetSharedStores } from '../../src/api/clusterStore.js';
 import { DEVICE_CONFIG_LIST_PATH, PLUGIN_POD_QUERIES } from '../../src/api/amdgpu.js';
 import { DEFAULT_SETTINGS } from '../../src/api/settings.js';
@@ -209,6 +209,27 @@ describe('AmdGpuDataProvider — data', () => {
     expect(p.last().gpuPods.map((x) => x.metadata.name)).toEqual(['train-a']);
     expect(p.last().pluginPods.map((x) => x.metadata.name)).toEqual(['amdgpu-dp-1']);
     expect(r.getByTestId('probe').children[0]).toBe('nodes=2 pods=1');
+  });
+
+  it('reads the object form of a list result ({items, errors, isLoading}) as well as the tuple', async () => {
+    lib.lists.Node = { items: [makeGpuNode('mi355x-0'), makeNode('cpu-0')], errors: null, isLoading: false };
+    lib.lists.Pod = { items: [makeGpuPod('train-a')], error: null, isLoading: false };
+    const c = core(apiServer());
+    const p = probe(c);
+    const r = render(h(c.AmdGpuDataProvider, null, h(p.Probe)));
+    await r.settle();
+    expect(p.last().loading).toBe(false);
+    expect(p.last().gpuNodes.map((n) => n.metadata.name)).toEqual(['mi355x-0']);
+    expect(p.last().gpuPods.map((x) => x.metadata.name)).toEqual(['train-a']);
+  });
+
+  it('listResult: loading, errors array, tuple', () => {
+    expect(listResult(undefined)).toEqual([null, null]);
+    expect(listResult([null, null])).toEqual([null, null]);
+    expect(listResult([[1], 'e'])).toEqual([[1], 'e']);
+    expect(listResult({ items: [], isLoading: true })).toEqual([null, null]);
+    expect(listResult({ items: null, errors: ['pods is forbidden'] })).toEqual([null, 'pods is forbidden']);
+    expect(listResult({ items: [1], errors: [] })).toEqual([[1], null]);
   });
 
   it('unwraps Headlamp KubeObject wrappers (jsonData)', async () => {
