@@ -269,6 +269,11 @@ describe('harness React enforces the rules real React enforces', () => {
     expect(() => render(h(Bad))).toThrow('getSnapshot should be cached');
   });
 
+  it('a keyless element in an array child is rejected; variadic children need no key', () => {
+    expect(() => render(h('ul', null, [h('li', null, 'a'), h('li', null, 'b')]))).toThrow('unique "key"');
+    expect(() => render(h('ul', null, h('li', null, 'a'), h('li', null, 'b')))).not.toThrow();
+  });
+
   it('a hook skipped on re-render is rejected', async () => {
     let setFlag = null;
     function Cond() {

@@ -304,6 +304,10 @@ function reconcileChildren(root, parent, children) {
   for (let i = 0; i < list.length; i++) {
     const item = list[i];
     if (item === null || item === undefined || item === false || item === true || item === '') continue;
+    // React warns for every keyless element of an array child.
+    if (parent.type === LIST && isValidElement(item) && (item.key === null || item.key === undefined)) {
+      throw new Error('Each child in a list should have a unique "key" prop (' + typeName(item.type) + ')');
+    }
     const id = identity(item, i);
     if (seen[id]) throw new Error('Duplicate key "' + id.slice(2) + '" among children of ' + typeName(parent.type));
     seen[id] = true;
