@@ -27,6 +27,11 @@ const LIST = Symbol.for('stub.react.list');
 
 export const Fragment = Symbol.for('stub.react.fragment');
 
+// Children arrays built by createElement from its arguments; any OTHER array
+// rendered as children (a .map() result, an array returned by a component)
+// is a list whose elements need keys.
+const VARIADIC = new WeakSet();
+
 export function createElement(type, props) {
   const p = {};
   let key = null;
@@ -37,7 +42,10 @@ export function createElement(type, props) {
     }
   }
   if (arguments.length === 3) p.children = arguments[2];
-  else if (arguments.length > 3) p.children = Array.prototype.slice.call(arguments, 2);
+  else if (arguments.length > 3) {
+    p.children = Array.prototype.slice.call(arguments, 2);
+    VARIADIC.add(p.children);
+  }
   if (type === undefined || type === null) throw new Error('createElement: element type is ' + type);
   return { $$typeof: ELEMENT, type: type, key: key, props: p };
 }
@@ -297,6 +305,7 @@ function sameType(inst, item) {
 
 function reconcileChildren(root, parent, children) {
   const list = childList(children);
+  const keyed = parent.type === LIST || (Array.isArray(children) && !VARIADIC.has(children));
   const old = new Map();
   for (let i = 0; i < parent.kids.length; i++) old.set(parent.kids[i].ident, parent.kids[i]);
   const kids = [];
@@ -305,7 +314,7 @@ function reconcileChildren(root, parent, children) {
     const item = list[i];
     if (item === null || item === undefined || item === false || item === true || item === '') continue;
     // React warns for every keyless element of an array child.
-    if (parent.type === LIST && isValidElement(item) && (item.key === null || item.key === undefined)) {
+    if (keyed && isValidElement(item) && (item.key === null || item.key === undefined)) {
       throw new Error('Each child in a list should have a unique "key" prop (' + typeName(item.type) + ')');
     }
     const id = identity(item, i);
