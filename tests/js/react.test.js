@@ -274,6 +274,31 @@ describe('harness React enforces the rules real React enforces', () => {
     expect(() => render(h('ul', null, h('li', null, 'a'), h('li', null, 'b')))).not.toThrow();
   });
 
+  it('hooks called in a different order on re-render are rejected', async () => {
+    let flip = null;
+    function Swap() {
+      const s = React.useState(false);
+      flip = s[1];
+      if (s[0]) {
+        React.useMemo(() => 1, []);
+        React.useRef(0);
+      } else {
+        React.useRef(0);
+        React.useMemo(() => 1, []);
+      }
+      return h('div', null, 'x');
+    }
+    const r = render(h(Swap));
+    let err = null;
+    try {
+      flip(true);
+      await r.settle();
+    } catch (e) {
+      err = e;
+    }
+    expect(String(err)).toContain('order of Hooks');
+  });
+
   it('a hook skipped on re-render is rejected', async () => {
     let setFlag = null;
     function Cond() {

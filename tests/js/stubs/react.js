@@ -82,13 +82,17 @@ let hookIndex = 0;
 let currentRoot = null;
 const ctxStack = [];
 
-function hookSlot(init) {
+function hookSlot(init, kind) {
   if (!current) throw new Error('Invalid hook call: hooks can only be called inside a function component');
   const hooks = current.hooks;
+  const kinds = current.hookKinds || (current.hookKinds = []);
   if (hookIndex >= hooks.length) {
     if (current.renders > 1) throw new Error('Rendered more hooks than during the previous render');
     hooks.push(init());
+    kinds.push(kind);
   }
+  // React: "React has detected a change in the order of Hooks".
+  if (kinds[hookIndex] !== kind) throw new Error('Change in the order of Hooks: ' + kinds[hookIndex] + ' then ' + kind + ' at hook ' + hookIndex);
   return hooks[hookIndex++];
 }
 
@@ -111,7 +115,7 @@ export function useReducer(reducer, initialArg, init) {
       markDirty(inst);
     };
     return s;
-  });
+  }, 'useReducer');
   slot.reducer = reducer;
   return [slot.state, slot.dispatch];
 }
@@ -126,7 +130,7 @@ export function useState(init) {
 
 function effectHook(fn, deps, layout) {
   const inst = current;
-  const slot = hookSlot(function () { return { deps: undefined, cleanup: null, first: true }; });
+  const slot = hookSlot(function () { return { deps: undefined, cleanup: null, first: true }; }, layout ? 'useLayoutEffect' : 'useEffect');
   if (slot.first || deps === undefined || depsChanged(slot.deps, deps)) {
     slot.first = false;
     slot.deps = deps;
@@ -143,7 +147,7 @@ export function useLayoutEffect(fn, deps) {
 }
 
 export function useMemo(fn, deps) {
-  const slot = hookSlot(function () { return { deps: undefined, value: undefined, first: true }; });
+  const slot = hookSlot(function () { return { deps: undefined, value: undefined, first: true }; }, 'useMemo');
   if (slot.first || depsChanged(slot.deps, deps)) {
     slot.first = false;
     slot.deps = deps;
@@ -157,7 +161,7 @@ export function useCallback(fn, deps) {
 }
 
 export function useRef(v) {
-  return hookSlot(function () { return { current: v }; });
+  return hookSlot(function () { return { current: v }; }, 'useRef');
 }
 
 function readContext(ctx) {
@@ -174,7 +178,7 @@ export function useContext(ctx) {
 
 export function useSyncExternalStore(subscribe, getSnapshot) {
   const inst = current;
-  const slot = hookSlot(function () { return { subscribe: null, unsubscribe: null, value: undefined }; });
+  const slot = hookSlot(function () { return { subscribe: null, unsubscribe: null, value: undefined }; }, 'useSyncExternalStore');
   const value = getSnapshot();
   // React (dev) reads the snapshot twice: a store whose getSnapshot builds a
   // new object each call would re-render forever.
