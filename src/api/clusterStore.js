@@ -77,14 +77,6 @@ const defaultClock = {
 };
 
 /**
- * Race `promise` against a timer; the timer is always cleared.
- * @template T
- * @param {Promise<T>} promise
- * @param {number} ms
- * @param {{setTimeout: Function, clearTimeout: Function}} [clock]
- * @returns {Promise<T>}
- */
-/**
  * True when a failed request proves the resource is not there for this user
  * (404 / 403 / 401), as opposed to a timeout or a server / network error.
  * Headlamp's ApiProxy errors carry the HTTP status in `status`.
@@ -94,6 +86,14 @@ export function isAbsent(err) {
   return st === 404 || st === 403 || st === 401;
 }
 
+/**
+ * Race `promise` against a timer; the timer is always cleared.
+ * @template T
+ * @param {Promise<T>} promise
+ * @param {number} ms
+ * @param {{setTimeout: Function, clearTimeout: Function}} [clock]
+ * @returns {Promise<T>}
+ */
 export function withTimeout(promise, ms, clock) {
   const c = clock || defaultClock;
   return new Promise(function (resolve, reject) {
