@@ -953,6 +953,42 @@ export function applyStatics(gpus, statics) {
   return complete;
 }
 
+/**
+ * Cluster power over a series window: the per-step sum over nodes
+ * (fetchSeries aligns every node's samples to the same steps), then its peak
+ * and mean — the "peak / average" figures the reference's Metrics mock-up
+ * advertises but its code never computed (reference docs/screenshots/03-metrics.svg,
+ * SURVEY.md Q12). Null when the window holds no sample.
+ * @param {Record<string, Array<[number, number]>>} powerByNode
+ * @returns {{peakWatts: number, peakAt: number, avgWatts: number, steps: number} | null}
+ */
+export function clusterPowerStats(powerByNode) {
+  const total = {};
+  for (const node in powerByNode || {}) {
+    const pts = powerByNode[node] || [];
+    for (let i = 0; i < pts.length; i++) {
+      const t = pts[i][0];
+      const v = pts[i][1];
+      if (typeof v !== 'number' || !isFinite(v)) continue;
+      total[t] = (total[t] || 0) + v;
+    }
+  }
+  const ts = Object.keys(total);
+  if (!ts.length) return null;
+  let peak = -Infinity;
+  let peakAt = 0;
+  let sum = 0;
+  for (let i = 0; i < ts.length; i++) {
+    const v = total[ts[i]];
+    sum += v;
+    if (v > peak) {
+      peak = v;
+      peakAt = Number(ts[i]);
+    }
+  }
+  return { peakWatts: peak, peakAt: peakAt, avgWatts: sum / ts.length, steps: ts.length };
+}
+
 /** Cluster totals for the summary box. */
 export function summarizeMetrics(m) {
   let power = 0;

@@ -68,7 +68,7 @@ import {
   unwrapKubeObject,
 } from '../api/amdgpu.js';
 import { buildGpuSlots, buildXgmiMatrix, isFullMesh } from '../api/topology.js';
-import { PROMETHEUS_SERVICES, summarizeMetrics } from '../api/metrics.js';
+import { PROMETHEUS_SERVICES, clusterPowerStats, summarizeMetrics } from '../api/metrics.js';
 import { bar, createMemo, createObjectCache, kv, lines, loader, noteExpiry, page, pctbar, row, section, status, table } from './ir.js';
 
 export const BRAND = 'AMD GPU';
@@ -977,10 +977,19 @@ export function metricsView(ctx, mstate, opts) {
     );
 
     if (mstate.series && mstate.series.power) {
+      const win = formatWindow(mstate.series.rangeSec || 1800);
+      const ps = clusterPowerStats(mstate.series.power);
+      const cap = sum.powerCapWatts > 0 ? sum.powerCapWatts : null;
+      const statRows = ps
+        ? [kv([
+          row('Peak Power (' + win + ')', powerBar(ps.peakWatts, cap)),
+          row('Average Power (' + win + ')', powerBar(ps.avgWatts, cap)),
+        ])]
+        : [];
       items.push(
-        section('Power & HBM (last ' + formatWindow(mstate.series.rangeSec || 1800) + ')', [
+        section('Power & HBM (last ' + win + ')', statRows.concat([
           { t: 'series', power: mstate.series.power, vram: mstate.series.vram || {} },
-        ])
+        ]))
       );
     }
 

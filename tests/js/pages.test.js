@@ -23,7 +23,7 @@ import {
 } from '../../src/view/pages.js';
 import { countRows, findSection, firstBlock, firstTable, loaders, rowNames, rowValue, sectionTitles, text } from '../../src/view/ir.js';
 import { renderPage, textContent } from '../../src/view/html.js';
-import { joinExporterResults, SERIES } from '../../src/api/metrics.js';
+import { clusterPowerStats, joinExporterResults, SERIES } from '../../src/api/metrics.js';
 import { NOW, makeContext, makeDeviceConfig, makeGpuNode, makeGpuPod, makeNode, makePlainPod, makePluginPod } from './fixtures.js';
 import { MI355X } from '../../src/api/amdgpu.js';
 
@@ -448,6 +448,20 @@ describe('metricsView', () => {
   it('adds the time-series section when range data exists', () => {
     const vm = metricsView(ctx, { metrics: metrics(['n0'], 1), fetchError: null, fetching: false, series: { power: { n0: [[1, 2]] }, vram: {} } }, opts);
     expect(sectionTitles(vm)).toContain('Power & HBM (last 30 min)');
+  });
+  it('shows cluster peak and average power over the window (per-step sums over nodes)', () => {
+    const series = { power: { n0: [[30, 100], [60, 300], [90, 200]], n1: [[30, 50], [60, 50], [90, 400]] }, vram: {} };
+    const vm = metricsView(ctx, { metrics: metrics(['n0', 'n1'], 1), fetchError: null, fetching: false, series }, opts);
+    const s = findSection(vm, 'Power & HBM (last 30 min)');
+    expect(rowValue(s, 'Peak Power (30 min)').text).toContain('600.0 W');
+    expect(rowValue(s, 'Average Power (30 min)').text).toContain('366.7 W');
+    // no samples in the window: no stat rows, the series block alone
+    const empty = findSection(metricsView(ctx, { metrics: metrics(['n0'], 1), fetchError: null, fetching: false, series: { power: {}, vram: {} } }, opts), 'Power & HBM (last 30 min)');
+    expect(rowValue(empty, 'Peak Power (30 min)')).toBeUndefined();
+  });
+  it('clusterPowerStats ignores non-numbers and reports the peak instant', () => {
+    expect(clusterPowerStats({})).toBeNull();
+    expect(clusterPowerStats({ a: [[10, 5], [20, NaN]], b: [[10, 1], [20, 7]] })).toEqual({ peakWatts: 7, peakAt: 20, avgWatts: 6.5, steps: 2 });
   });
   it('titles the time-series section with the configured window', () => {
     const series = { rangeSec: 6 * 3600, power: { n0: [[1, 2]] }, vram: {} };
