@@ -105,7 +105,10 @@ function renderBlock(b) {
     case 'series': {
       const nodes = Object.keys(b.power || {});
       return '<div data-testid="series" data-nodes="' + nodes.length + '">' +
-        nodes.map(function (n) { return '<div data-node="' + esc(n) + '" data-points="' + b.power[n].length + '"></div>'; }).join('') +
+        nodes.map(function (n) {
+          const avg = b.avgPower && b.avgPower[n] !== undefined ? ' data-avg-w="' + b.avgPower[n].toFixed(1) + '"' : '';
+          return '<div data-node="' + esc(n) + '" data-points="' + b.power[n].length + '"' + avg + '></div>';
+        }).join('') +
         '</div>';
     }
     default:

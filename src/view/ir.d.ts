@@ -114,6 +114,8 @@ export interface SeriesBlock {
   t: 'series';
   power: Record<string, SeriesPoint[]>;
   vram: Record<string, SeriesPoint[]>;
+  /** Mean power per node over the window (W); nodes without samples are absent. */
+  avgPower?: Record<string, number>;
 }
 
 export type Block = KvBlock | TableBlock | PctbarBlock | SlotsBlock | MatrixBlock | SeriesBlock;

@@ -872,6 +872,42 @@ function podsItems(ctx, now, assign) {
 // ---------------------------------------------------------------------------
 
 /** Power bar: "X W / Y W (Z%)" with 70/90 colouring (reference PowerBar, MetricsPage.tsx:50-89). */
+/** Mean value per node of a series map (node → [[t, v]]); nodes without samples are left out. */
+export function seriesMeans(byNode) {
+  const out = {};
+  for (const n in byNode || {}) {
+    const pts = byNode[n] || [];
+    let sum = 0;
+    let k = 0;
+    for (let i = 0; i < pts.length; i++) {
+      if (typeof pts[i][1] === 'number' && isFinite(pts[i][1])) {
+        sum += pts[i][1];
+        k++;
+      }
+    }
+    if (k) out[n] = sum / k;
+  }
+  return out;
+}
+
+/** "k / n GPU nodes": nodes with telemetry out of the cluster's GPU nodes (reference mock-up "Nodes Reporting"). */
+export function nodesReporting(m, ctx) {
+  const seen = {};
+  let k = 0;
+  for (let i = 0; i < m.gpus.length; i++) {
+    if (!seen[m.gpus[i].nodeName]) {
+      seen[m.gpus[i].nodeName] = true;
+      k++;
+    }
+  }
+  const n = ctx && ctx.gpuNodes ? ctx.gpuNodes.length : 0;
+  if (!n) return String(k);
+  let missing = 0;
+  for (let i = 0; i < ctx.gpuNodes.length; i++) if (!seen[ctx.gpuNodes[i].metadata.name]) missing++;
+  const text = k + ' / ' + n + ' GPU nodes';
+  return missing > 0 ? status('warning', text + ' (' + missing + ' without telemetry)') : text;
+}
+
 export function powerBar(watts, capWatts) {
   const hasCap = capWatts !== null && capWatts > 0;
   const p = hasCap ? Math.min(100, pct(watts, capWatts)) : null;
@@ -959,6 +995,7 @@ export function metricsView(ctx, mstate, opts) {
       section('GPU Power Summary', [
         kv([
           row('GPUs Monitored', String(sum.gpus)),
+          row('Nodes Reporting', nodesReporting(m, ctx)),
           row('Total Power', powerBar(sum.powerWatts, sum.powerCapWatts > 0 ? sum.powerCapWatts : null)),
           row('HBM In Use', hbmBar(sum.vramUsedBytes, sum.vramTotalBytes > 0 ? sum.vramTotalBytes : null)),
           row('Avg GFX Activity', pctText(sum.avgGfxActivityPct)),
@@ -988,7 +1025,7 @@ export function metricsView(ctx, mstate, opts) {
         : [];
       items.push(
         section('Power & HBM (last ' + win + ')', statRows.concat([
-          { t: 'series', power: mstate.series.power, vram: mstate.series.vram || {} },
+          { t: 'series', power: mstate.series.power, vram: mstate.series.vram || {}, avgPower: seriesMeans(mstate.series.power) },
         ]))
       );
     }

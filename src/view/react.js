@@ -24,7 +24,7 @@
  * for the inline bar idiom).
  */
 
-import { BAR_COLORS } from '../api/amdgpu.js';
+import { BAR_COLORS, formatWatts } from '../api/amdgpu.js';
 import { matrixCaption } from './ir.js';
 
 /** CommonComponents the renderer needs (reference src/components/OverviewPage.tsx:8-16). */
@@ -240,6 +240,10 @@ export function createRenderer(React, CC) {
     return h(CC.SimpleTable, {
       columns: [
         { label: 'Node', getter: function (n) { return n; } },
+        {
+          label: 'Avg Power',
+          getter: function (n) { return b.avgPower && b.avgPower[n] !== undefined ? formatWatts(b.avgPower[n]) : '—'; },
+        },
         {
           label: 'Power (W)',
           getter: function (n) { return h(Sparkline, { points: b.power[n] || [], color: BAR_COLORS.ok, label: n + ' power' }); },

@@ -97,7 +97,8 @@ function blockLines(b, color) {
       Object.keys(b.power || {}).forEach(function (n) {
         const pts = b.power[n];
         const last = pts.length ? pts[pts.length - 1][1] : null;
-        out.push('  ' + n + ': ' + pts.length + ' power samples' + (last === null ? '' : ', last ' + last.toFixed(0) + ' W'));
+        const avg = b.avgPower && b.avgPower[n] !== undefined ? ', avg ' + b.avgPower[n].toFixed(0) + ' W' : '';
+        out.push('  ' + n + ': ' + pts.length + ' power samples' + (last === null ? '' : ', last ' + last.toFixed(0) + ' W') + avg);
       });
       break;
     }

@@ -459,6 +459,18 @@ describe('metricsView', () => {
     const empty = findSection(metricsView(ctx, { metrics: metrics(['n0'], 1), fetchError: null, fetching: false, series: { power: {}, vram: {} } }, opts), 'Power & HBM (last 30 min)');
     expect(rowValue(empty, 'Peak Power (30 min)')).toBeUndefined();
   });
+  it('series block carries the per-node mean; summary counts the nodes reporting', () => {
+    const series = { power: { n0: [[30, 100], [60, 300]], n1: [] }, vram: {} };
+    const vm = metricsView(ctx, { metrics: metrics(['n0'], 1), fetchError: null, fetching: false, series }, opts);
+    const blk = findSection(vm, 'Power & HBM (last 30 min)').blocks.filter((b) => b.t === 'series')[0];
+    expect(blk.avgPower).toEqual({ n0: 200 });
+    expect(rowValue(findSection(vm, 'GPU Power Summary'), 'Nodes Reporting')).toBe('1 / 1 GPU nodes');
+    const two = makeContext({ nodes: [makeGpuNode('n0'), makeGpuNode('n9')] });
+    const vm2 = metricsView(two, { metrics: metrics(['n0'], 1), fetchError: null, fetching: false }, opts);
+    const rep = rowValue(findSection(vm2, 'GPU Power Summary'), 'Nodes Reporting');
+    expect(rep.status).toBe('warning');
+    expect(rep.text).toBe('1 / 2 GPU nodes (1 without telemetry)');
+  });
   it('clusterPowerStats ignores non-numbers and reports the peak instant', () => {
     expect(clusterPowerStats({})).toBeNull();
     expect(clusterPowerStats({ a: [[10, 5], [20, NaN]], b: [[10, 1], [20, 7]] })).toEqual({ peakWatts: 7, peakAt: 20, avgWatts: 6.5, steps: 2 });

@@ -191,11 +191,13 @@ describe('blocks', () => {
   it('series → SimpleTable of per-node sparklines', () => {
     const v = setup();
     const pts = [[0, 100], [30, 300], [60, 200]];
-    const b = { t: 'series', power: { n0: pts, n1: [] }, vram: { n0: pts } };
+    const b = { t: 'series', power: { n0: pts, n1: [] }, vram: { n0: pts }, avgPower: { n0: 200 } };
     const r = render(h(v.Block, { b }));
     const p = only(r, CC.SimpleTable);
-    expect(p.columns.map((c) => c.label)).toEqual(['Node', 'Power (W)', 'HBM in use']);
+    expect(p.columns.map((c) => c.label)).toEqual(['Node', 'Avg Power', 'Power (W)', 'HBM in use']);
     expect(p.data).toEqual(['n0', 'n1']);
+    expect(p.columns[1].getter('n0')).toBe('200.0 W');
+    expect(p.columns[1].getter('n1')).toBe('—');
     const svgs = r.byTag('svg');
     expect(svgs).toHaveLength(2); // n1 has no points for either series
     expect(svgs[0].props['aria-label']).toBe('n0 power');
