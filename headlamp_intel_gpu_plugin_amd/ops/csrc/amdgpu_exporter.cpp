@@ -18,13 +18,14 @@
 // (probe_core.h), so the exporter needs no device node and runs unprivileged
 // with /sys mounted read-only (deploy/exporter/daemonset.yaml).
 //
-// Serving: the accept loop hands connections to a few worker threads through
-// a bounded queue (full → the connection is closed at once). Each connection
-// has ONE deadline for the whole request (kRequestDeadlineMs, enforced with
-// poll() on every read) and a send timeout, so a client that trickles bytes
-// or stops reading holds one worker for at most a few seconds and never the
-// /healthz probe or the Prometheus scrape behind it. SIGINT / SIGTERM stop
-// the loop and the workers cleanly.
+// Serving: one thread multiplexes the listening socket and every connection
+// with poll() over non-blocking sockets. Each connection has ONE deadline for
+// the whole request (kRequestDeadlineMs: headers in, response out); a peer
+// that trickles bytes or stops reading only holds its own socket until then,
+// never a thread, so no number of slow peers below kMaxConns delays /healthz
+// or a Prometheus scrape. At kMaxConns the oldest connection still sending its
+// request is dropped for the new one. A /metrics render is shared by requests
+// arriving within kRenderCacheMs. SIGINT / SIGTERM end the loop.
 
 #include <arpa/inet.h>
 #include <netinet/in.h>
@@ -33,14 +34,11 @@
 #include <sys/socket.h>
 #include <sys/time.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cerrno>
 #include <chrono>
-#include <condition_variable>
-#include <deque>
-#include <mutex>
 #include <string>
-#include <thread>
 #include <vector>
 
 #include "probe_core.h"
@@ -50,8 +48,9 @@ namespace {
 std::atomic<bool> g_stop{false};
 
 constexpr int kRequestDeadlineMs = 3000;  // whole request: headers in, response out
-constexpr int kWorkers = 4;
-constexpr size_t kMaxQueued = 64;
+constexpr size_t kMaxConns = 512;         // open connections (each is a socket, not a thread)
+constexpr size_t kMaxHeader = 16384;
+constexpr int kRenderCacheMs = 250;       // /metrics requests this close together share one render
 
 void on_signal(int) { g_stop.store(true); }
 
@@ -121,109 +120,106 @@ bool parse_args(int argc, char** argv, Args* a) {
   return true;
 }
 
-void send_all(int fd, const std::string& s) {
-  size_t off = 0;
-  while (off < s.size()) {
-    ssize_t n = send(fd, s.data() + off, s.size() - off, MSG_NOSIGNAL);
-    if (n <= 0) return;
-    off += static_cast<size_t>(n);
-  }
-}
-
-void respond(int fd, int code, const char* reason, const std::string& type, const std::string& body) {
-  std::string h = "HTTP/1.1 " + std::to_string(code) + " " + reason + "\r\nContent-Type: " + type +
-                  "\r\nContent-Length: " + std::to_string(body.size()) + "\r\nConnection: close\r\n\r\n";
-  send_all(fd, h + body);
-}
-
 using Clock = std::chrono::steady_clock;
 
-int remaining_ms(Clock::time_point deadline) {
-  const auto left = std::chrono::duration_cast<std::chrono::milliseconds>(deadline - Clock::now()).count();
+int remaining_ms(Clock::time_point deadline, Clock::time_point now) {
+  const auto left = std::chrono::duration_cast<std::chrono::milliseconds>(deadline - now).count();
   return left > 0 ? static_cast<int>(left) : 0;
 }
 
-void handle(int fd, const Args& a) {
-  const Clock::time_point deadline = Clock::now() + std::chrono::milliseconds(kRequestDeadlineMs);
-  // A peer that stops reading cannot hold the worker past the deadline either.
-  timeval stv{kRequestDeadlineMs / 1000, 0};
-  setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &stv, sizeof(stv));
-  std::string req;
-  char buf[2048];
-  while (req.find("\r\n\r\n") == std::string::npos && req.size() < 16384) {
-    // One deadline for the whole header, however slowly the bytes arrive.
-    pollfd p{fd, POLLIN, 0};
-    const int wait = remaining_ms(deadline);
-    if (wait <= 0 || poll(&p, 1, wait) <= 0) return;
-    ssize_t n = recv(fd, buf, sizeof(buf), 0);
-    if (n <= 0) return;
-    req.append(buf, static_cast<size_t>(n));
+std::string response(int code, const char* reason, const std::string& type, const std::string& body) {
+  return "HTTP/1.1 " + std::to_string(code) + " " + reason + "\r\nContent-Type: " + type +
+         "\r\nContent-Length: " + std::to_string(body.size()) + "\r\nConnection: close\r\n\r\n" + body;
+}
+
+// /metrics body, re-rendered at most every kRenderCacheMs.
+const std::string& metrics_body(const Args& a, Clock::time_point now) {
+  static std::string body;
+  static Clock::time_point at;
+  static bool have = false;
+  if (!have || now - at >= std::chrono::milliseconds(kRenderCacheMs)) {
+    body = amdprobe::render(a.render);
+    at = Clock::now();
+    have = true;
   }
+  return body;
+}
+
+// The response to a complete request header.
+std::string answer(const std::string& req, const Args& a, Clock::time_point now) {
   const size_t sp1 = req.find(' ');
   const size_t sp2 = sp1 == std::string::npos ? std::string::npos : req.find(' ', sp1 + 1);
-  if (sp2 == std::string::npos) {
-    respond(fd, 400, "Bad Request", "text/plain", "bad request\n");
-    return;
-  }
+  if (sp2 == std::string::npos) return response(400, "Bad Request", "text/plain", "bad request\n");
   const std::string method = req.substr(0, sp1);
   std::string path = req.substr(sp1 + 1, sp2 - sp1 - 1);
   const size_t q = path.find('?');
   if (q != std::string::npos) path.resize(q);
-  if (method != "GET") {
-    respond(fd, 405, "Method Not Allowed", "text/plain", "GET only\n");
-  } else if (path == "/metrics") {
-    std::string body;
-    {
-      // The probe keeps process-wide state (error text, HIP handles): one
-      // scrape renders at a time; /healthz never waits for it.
-      static std::mutex render_mu;
-      std::lock_guard<std::mutex> lk(render_mu);
-      body = amdprobe::render(a.render);
+  if (method != "GET") return response(405, "Method Not Allowed", "text/plain", "GET only\n");
+  if (path == "/metrics") return response(200, "OK", "text/plain; version=0.0.4", metrics_body(a, now));
+  if (path == "/healthz") return response(200, "OK", "text/plain", "ok\n");
+  return response(404, "Not Found", "text/plain", "not found\n");
+}
+
+struct Conn {
+  int fd;
+  Clock::time_point accepted;
+  Clock::time_point deadline;
+  std::string in;
+  std::string out;
+  size_t off = 0;
+  bool writing = false;
+};
+
+// Read what is there; false when the peer closed or failed.
+bool read_some(Conn& c) {
+  char buf[4096];
+  for (;;) {
+    const ssize_t n = recv(c.fd, buf, sizeof(buf), 0);
+    if (n > 0) {
+      c.in.append(buf, static_cast<size_t>(n));
+      if (c.in.size() >= kMaxHeader) return true;
+      continue;
     }
-    respond(fd, 200, "OK", "text/plain; version=0.0.4", body);
-  } else if (path == "/healthz") {
-    respond(fd, 200, "OK", "text/plain", "ok\n");
-  } else {
-    respond(fd, 404, "Not Found", "text/plain", "not found\n");
+    if (n == 0) return false;
+    return errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR;
   }
 }
 
-// Accepted connections waiting for a worker.
-class ConnQueue {
- public:
-  bool push(int fd) {
-    std::lock_guard<std::mutex> lk(mu_);
-    if (q_.size() >= kMaxQueued) return false;
-    q_.push_back(fd);
-    cv_.notify_one();
-    return true;
+// Send what the socket takes; true when the whole response is out.
+bool write_some(Conn& c, bool* failed) {
+  while (c.off < c.out.size()) {
+    const ssize_t n = send(c.fd, c.out.data() + c.off, c.out.size() - c.off, MSG_NOSIGNAL);
+    if (n > 0) {
+      c.off += static_cast<size_t>(n);
+      continue;
+    }
+    if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR)) return false;
+    *failed = true;
+    return false;
   }
-  // Next connection, or -1 once stopped.
-  int pop() {
-    std::unique_lock<std::mutex> lk(mu_);
-    cv_.wait(lk, [&] { return stopped_ || !q_.empty(); });
-    if (q_.empty()) return -1;
-    const int fd = q_.front();
-    q_.pop_front();
-    return fd;
-  }
-  void stop() {
-    std::lock_guard<std::mutex> lk(mu_);
-    stopped_ = true;
-    cv_.notify_all();
-  }
-  void drain() {
-    std::lock_guard<std::mutex> lk(mu_);
-    for (int fd : q_) close(fd);
-    q_.clear();
-  }
+  return true;
+}
 
- private:
-  std::mutex mu_;
-  std::condition_variable cv_;
-  std::deque<int> q_;
-  bool stopped_ = false;
-};
+// Advance one connection; false when it is finished (to be closed).
+bool step(Conn& c, short revents, const Args& a, Clock::time_point now) {
+  if (!c.writing) {
+    if (revents & (POLLIN | POLLHUP | POLLERR)) {
+      if (!read_some(c)) return false;
+    }
+    const bool complete = c.in.find("\r\n\r\n") != std::string::npos;
+    if (complete || c.in.size() >= kMaxHeader) {
+      c.out = complete ? answer(c.in, a, now) : response(431, "Request Header Fields Too Large", "text/plain", "header too large\n");
+      c.writing = true;
+    }
+  } else if (revents & (POLLERR | POLLHUP | POLLNVAL)) {
+    return false;
+  }
+  if (c.writing) {
+    bool failed = false;
+    if (write_some(c, &failed) || failed) return false;  // all sent (Connection: close) or peer gone
+  }
+  return now < c.deadline;
+}
 
 }  // namespace
 
@@ -243,7 +239,7 @@ int main(int argc, char** argv) {
   }
   signal(SIGINT, on_signal);
   signal(SIGTERM, on_signal);
-  int srv = socket(AF_INET, SOCK_STREAM, 0);
+  int srv = socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
   if (srv < 0) {
     std::perror("socket");
     return 1;
@@ -257,7 +253,7 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "bad bind address %s\n", a.bind.c_str());
     return 2;
   }
-  if (bind(srv, reinterpret_cast<sockaddr*>(&addr), sizeof(addr)) < 0 || listen(srv, 16) < 0) {
+  if (bind(srv, reinterpret_cast<sockaddr*>(&addr), sizeof(addr)) < 0 || listen(srv, 128) < 0) {
     std::perror("bind/listen");
     return 1;
   }
@@ -267,31 +263,63 @@ int main(int argc, char** argv) {
   std::printf("amdgpu-exporter listening on %s:%d (%d GPU%s, hostname %s%s)\n", a.bind.c_str(), ntohs(addr.sin_port),
               gpus, gpus == 1 ? "" : "s", a.render.hostname.c_str(), a.render.sysfs_only ? ", sysfs-only" : "");
   std::fflush(stdout);
-  ConnQueue queue;
-  std::vector<std::thread> workers;
-  for (int i = 0; i < kWorkers; ++i) {
-    workers.emplace_back([&] {
-      for (int fd = queue.pop(); fd >= 0; fd = queue.pop()) {
-        handle(fd, a);
-        close(fd);
-      }
-    });
-  }
-  // Wake accept() periodically so a signal ends the loop promptly.
-  timeval tv{1, 0};
-  setsockopt(srv, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+  std::vector<Conn> conns;
+  std::vector<pollfd> pfds;
   while (!g_stop.load()) {
-    int fd = accept(srv, nullptr, nullptr);
-    if (fd < 0) {
-      if (errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR) continue;
-      std::perror("accept");
+    Clock::time_point now = Clock::now();
+    pfds.clear();
+    pfds.push_back(pollfd{srv, POLLIN, 0});
+    int wait = 1000;  // wake at least once a second so a signal ends the loop promptly
+    for (const Conn& c : conns) {
+      pfds.push_back(pollfd{c.fd, static_cast<short>(c.writing ? POLLOUT : POLLIN), 0});
+      wait = std::min(wait, remaining_ms(c.deadline, now));
+    }
+    const int r = poll(pfds.data(), pfds.size(), wait);
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      std::perror("poll");
       break;
     }
-    if (!queue.push(fd)) close(fd);  // overloaded: shed the connection
+    now = Clock::now();
+    for (size_t i = 0; i < conns.size(); ++i) {
+      if (!step(conns[i], pfds[i + 1].revents, a, now)) {
+        close(conns[i].fd);
+        conns[i].fd = -1;
+      }
+    }
+    conns.erase(std::remove_if(conns.begin(), conns.end(), [](const Conn& c) { return c.fd < 0; }), conns.end());
+    if (pfds[0].revents & POLLIN) {
+      for (;;) {
+        const int fd = accept4(srv, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
+        if (fd < 0) break;  // EAGAIN: nothing more to accept (or a transient error)
+        if (conns.size() >= kMaxConns) {
+          // Full: drop the oldest connection still sending its request (a
+          // slow peer, most likely) rather than the new one.
+          auto victim = conns.end();
+          for (auto it = conns.begin(); it != conns.end(); ++it) {
+            if (!it->writing && (victim == conns.end() || it->accepted < victim->accepted)) victim = it;
+          }
+          if (victim == conns.end()) {
+            close(fd);
+            continue;
+          }
+          close(victim->fd);
+          conns.erase(victim);
+        }
+        Conn c;
+        c.fd = fd;
+        c.accepted = now;
+        c.deadline = now + std::chrono::milliseconds(kRequestDeadlineMs);
+        conns.push_back(std::move(c));
+        // Most requests arrive with the connection: answer them in this pass.
+        if (!step(conns.back(), POLLIN, a, now)) {
+          close(conns.back().fd);
+          conns.pop_back();
+        }
+      }
+    }
   }
-  queue.stop();
-  for (auto& w : workers) w.join();
-  queue.drain();
+  for (const Conn& c : conns) close(c.fd);
   close(srv);
   return 0;
 }

@@ -95,7 +95,7 @@ class ExporterProcess:
     """The native ``amdgpu-exporter`` daemon as a child process on an ephemeral port."""
 
     def __init__(self, hostname: str, device: Optional[int] = None, gpu_label: Optional[str] = None,
-                 topology: bool = True):
+                 topology: bool = True, sysfs_only: bool = False):
         from ..ops import build as native_build
 
         # Builds (under the build lock) only when missing or stale, e.g. on a
@@ -110,6 +110,8 @@ class ExporterProcess:
                 self.cmd += ["--gpu-label", gpu_label]
         if not topology:
             self.cmd.append("--no-topology")
+        if sysfs_only:
+            self.cmd.append("--sysfs-only")
         self.proc: Optional[subprocess.Popen] = None
         self.url = ""
 

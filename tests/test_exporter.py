@@ -244,25 +244,37 @@ def test_captured_kfd_topology_links_this_gpu_to_seven_peers_over_xgmi():
     assert sorted(int(l["node_to"]) for l in xgmi) == list(range(3, 10))
 
 
+def _start(exe, name):
+    p = subprocess.Popen([exe, "--port", "0", "--bind", "127.0.0.1", "--hostname", name, "--sysfs-only"],
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    line = p.stdout.readline()
+    return p, int(line.split("127.0.0.1:")[1].split()[0])
+
+
 def test_slow_client_does_not_block_scrapes(exe):
-    """A client trickling header bytes holds one worker until the request
-    deadline; /healthz and /metrics keep answering meanwhile."""
+    """Peers trickling header bytes and peers that never read hold only their own sockets (one poll() loop, no
+    worker threads): /healthz and /metrics answer at once next to them, and the trickling connections are dropped
+    at the request deadline."""
     import socket
 
-    p = subprocess.Popen([exe, "--port", "0", "--bind", "127.0.0.1", "--hostname", "slow", "--sysfs-only"],
-                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    p, port = _start(exe, "slow")
     try:
-        line = p.stdout.readline()
-        port = int(line.split("127.0.0.1:")[1].split()[0])
-        slow = [socket.create_connection(("127.0.0.1", port)) for _ in range(6)]
+        slow = [socket.create_connection(("127.0.0.1", port)) for _ in range(64)]
+        stalled = []
+        for _ in range(8):
+            s = socket.create_connection(("127.0.0.1", port))
+            s.sendall(b"GET /metrics HTTP/1.1\r\nHost: x\r\n\r\n")  # never read
+            stalled.append(s)
         t0 = time.time()
         for s in slow:
             s.sendall(b"G")
         for _ in range(3):
-            t = time.time()
-            with urllib.request.urlopen(f"http://127.0.0.1:{port}/healthz", timeout=5) as r:
-                assert r.read() == b"ok\n"
-            assert time.time() - t < 4.5
+            for path in ("/healthz", "/metrics"):
+                t = time.time()
+                with urllib.request.urlopen(f"http://127.0.0.1:{port}{path}", timeout=5) as r:
+                    body = r.read()
+                assert time.time() - t < 0.5, path
+                assert body == b"ok\n" if path == "/healthz" else b"# HELP" in body or body == b""
             for s in slow:
                 try:
                     s.sendall(b"E")
@@ -276,9 +288,41 @@ def test_slow_client_does_not_block_scrapes(exe):
         except ConnectionResetError:
             data = b""
         assert data == b"" and time.time() - t0 < 8
-        for s in slow:
+        for s in slow + stalled:
             s.close()
     finally:
+        p.send_signal(signal.SIGTERM)
+        assert p.wait(15) == 0
+
+
+def test_full_connection_table_drops_the_oldest_request_in_progress(exe):
+    """At the connection limit (512) a new peer evicts the oldest connection still sending its request, so a
+    scrape gets through however many idle sockets an attacker opens."""
+    import resource
+    import socket
+
+    soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
+    if min(soft, hard) < 1200:
+        pytest.skip(f"needs ~600 client sockets (RLIMIT_NOFILE {soft})")
+    p, port = _start(exe, "full")
+    idle = []
+    try:
+        for _ in range(530):
+            idle.append(socket.create_connection(("127.0.0.1", port)))
+        time.sleep(0.2)
+        t = time.time()
+        with urllib.request.urlopen(f"http://127.0.0.1:{port}/healthz", timeout=5) as r:
+            assert r.read() == b"ok\n"
+        assert time.time() - t < 1.0
+        # the oldest idle peers were the ones dropped
+        idle[0].settimeout(2)
+        try:
+            assert idle[0].recv(10) == b""
+        except ConnectionResetError:
+            pass
+    finally:
+        for s in idle:
+            s.close()
         p.send_signal(signal.SIGTERM)
         assert p.wait(15) == 0
 
