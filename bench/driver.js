@@ -576,9 +576,9 @@ async function serve(a) {
         }
         const ctx = L.s.ctx();
         const pods = ctx.gpuPods.filter(function (p) { return p.spec && p.spec.nodeName; });
-        const modes = { podScoped: [], podClusterWide: [], nodeScoped: [], podsPageOwners: [] };
-        const bytes = { podScoped: 0, podClusterWide: 0, nodeScoped: 0, podsPageOwners: 0 };
-        const reqs = { podScoped: 0, podClusterWide: 0, nodeScoped: 0, podsPageOwners: 0 };
+        const modes = { podScoped: [], podDetail: [], podClusterWide: [], nodeScoped: [], podsPageOwners: [] };
+        const bytes = { podScoped: 0, podDetail: 0, podClusterWide: 0, nodeScoped: 0, podsPageOwners: 0 };
+        const reqs = { podScoped: 0, podDetail: 0, podClusterWide: 0, nodeScoped: 0, podsPageOwners: 0 };
         const slow = [];
         const detailRequest = makeRequest(a.url, counter);
         for (let i = 0; i < n && pods.length; i++) {
@@ -586,6 +586,14 @@ async function serve(a) {
           const node = ctx.gpuNodes.filter(function (x) { return x.metadata.name === pod.spec.nodeName; })[0];
           const runs = [
             ['podScoped', function (src) { return src.fetchNodeMetrics(pod.spec.nodeName).then(function (m) { return podDetailView(pod, { metrics: m }); }); }],
+            // As src/plugin.js wires the Pod detail page: the node's telemetry
+            // and the pod's power history, in one wave.
+            ['podDetail', function (src) {
+              return Promise.all([
+                src.fetchNodeMetrics(pod.spec.nodeName),
+                src.fetchPodSeries(pod.metadata.namespace || '', pod.metadata.name, 1800, 30),
+              ]).then(function (r) { return podDetailView(pod, { metrics: r[0], series: r[1] }); });
+            }],
             ['podClusterWide', function (src) { return src.fetchGpuMetrics().then(function (m) { return podDetailView(pod, { metrics: m }); }); }],
             ['nodeScoped', function (src) {
               return src.fetchNodeMetrics(pod.spec.nodeName).then(function (m) { return node ? nodeDetailView(node, ctx, { metrics: m }) : null; });

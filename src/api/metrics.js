@@ -429,6 +429,16 @@ export function mergedQuery(withStatic, view) {
   return 'max by (' + labels.join(', ') + ') ({__name__=~"' + names.join('|') + '"})';
 }
 
+/**
+ * One pod's total GPU power over time (Pod detail history): the power gauge
+ * of the GPUs the exporter attributes to the pod (`pod` / `namespace`
+ * labels), summed per step. O(points), whatever the cluster size.
+ */
+export function podPowerQuery(namespace, pod) {
+  return 'sum by (__name__) ({__name__="' + SERIES.exporter.power + '", namespace="' + promString(namespace) +
+    '", pod="' + promString(pod) + '"})';
+}
+
 /** Per-node power + HBM-used history in one range query (split by `__name__`). */
 export function seriesQuery() {
   const E = SERIES.exporter;
@@ -912,10 +922,45 @@ export function createMetricsSource(opts) {
     });
   }
 
+  /**
+   * A pod's GPU power over the last `rangeSec` (podPowerQuery), step-aligned
+   * like fetchSeries: `{rangeSec, power: [[t, W]]}`; `power` is empty when
+   * the exporter attributes no GPU to the pod (no pod association, or the pod
+   * holds none). Resolves to null when Prometheus is unreachable.
+   * @returns {Promise<{rangeSec: number, power: Array<[number, number]>} | null>}
+   */
+  function fetchPodSeries(namespace, pod, rangeSec, stepSec) {
+    const range = rangeSec || 1800;
+    const step = stepSec || 30;
+    const key = 'pod|' + namespace + '/' + pod + '|' + range + '|' + step;
+    return shared(key, function () {
+      return withPrometheus(function (base) {
+        const end = Math.floor(clock.now() / 1000 / step) * step;
+        return rangeQuery(base, podPowerQuery(namespace, pod), end - range, end, step).then(function (got) {
+          if (got === UNREACHABLE) return UNREACHABLE;
+          // Sum whatever rows came back per step (one row after `sum by (__name__)`).
+          const total = {};
+          const rows = got[SERIES.exporter.power] || {};
+          for (const k in rows) {
+            for (let i = 0; i < rows[k].length; i++) {
+              const t = Number(rows[k][i][0]);
+              const v = num(rows[k][i][1]);
+              if (v !== null) total[t] = (total[t] || 0) + v;
+            }
+          }
+          const power = Object.keys(total).map(Number).sort(function (a, b) { return a - b; })
+            .map(function (t) { return [t, total[t]]; });
+          return { rangeSec: range, power: power };
+        });
+      }, function () { return null; });
+    });
+  }
+
   return {
     discover: discover,
     invalidate: invalidate,
     fetchGpuMetrics: fetchGpuMetrics,
+    fetchPodSeries: fetchPodSeries,
     fetchNodeMetrics: fetchNodeMetrics,
     fetchGpuOwners: fetchGpuOwners,
     fetchSeries: fetchSeries,

@@ -39,6 +39,7 @@ export interface MetricsSource {
   fetchGpuMetrics(view?: 'all' | 'gauges' | 'topology'): Promise<GpuMetrics | null>;
   fetchNodeMetrics(nodeName: string): Promise<GpuMetrics | null>;
   fetchGpuOwners(): Promise<GpuMetrics | null>;
+  fetchPodSeries(namespace: string, pod: string, rangeSec: number, stepSec: number): Promise<{ rangeSec: number; power: Array<[number, number]> } | null>;
   fetchSeries(rangeSec: number, stepSec: number): Promise<GpuMetricsState['series']>;
 }
 
@@ -49,6 +50,7 @@ export interface ProviderCore {
   useGpuMetrics(enabled?: boolean, withSeries?: boolean, view?: 'all' | 'gauges' | 'topology'): GpuMetricsState;
   useNodeGpuMetrics(nodeName: string | null, enabled?: boolean): GpuMetricsState;
   useGpuOwners(enabled?: boolean): GpuMetricsState;
+  usePodGpuSeries(namespace: string | null, pod: string | null, enabled?: boolean): GpuMetricsState;
   storeFor(cluster: string): ClusterStore;
   metricsSourceFor(cluster: string): MetricsSource;
 }

@@ -177,8 +177,9 @@ export function createProviderCore(React, lib, deps) {
    * `cancelled` flag, MetricsPage.tsx:206-230).
    * @param {string|null} key
    * @param {() => Promise<[any, any]>} fetchPair  resolves [metrics, series]
+   * @param {boolean} [seriesOnly]  the fetch returns series only: unreachable = no series
    */
-  function useMetricsFetch(key, fetchPair) {
+  function useMetricsFetch(key, fetchPair, seriesOnly) {
     const refreshIntervalSec = loadSettings().refreshIntervalSec;
     const st = useState(IDLE);
     const state = st[0];
@@ -195,7 +196,8 @@ export function createProviderCore(React, lib, deps) {
         function (pair) {
           if (cancelled) return;
           const metrics = pair[0];
-          setState({ metrics: metrics, series: pair[1], fetching: false, fetchError: metrics ? null : PROMETHEUS_UNREACHABLE });
+          const reached = seriesOnly ? !!pair[1] : !!metrics;
+          setState({ metrics: metrics, series: pair[1], fetching: false, fetchError: reached ? null : PROMETHEUS_UNREACHABLE });
         },
         function (e) {
           if (cancelled) return;
@@ -258,6 +260,23 @@ export function createProviderCore(React, lib, deps) {
     });
   }
 
+  /**
+   * One pod's GPU power history for the native Pod detail page
+   * (metrics.js fetchPodSeries): one pod-scoped range query, next to the
+   * node-scoped telemetry query.
+   */
+  function usePodGpuSeries(namespace, pod, enabled) {
+    const cluster = clusterKey();
+    const source = metricsSourceFor(cluster);
+    const settings = loadSettings();
+    const active = (enabled === undefined ? true : enabled) && !!namespace && !!pod;
+    const key = 'podseries|' + sourceKey(cluster, settings) + '|' + namespace + '/' + pod + '|' + settings.seriesMinutes;
+    return useMetricsFetch(active ? key : null, function () {
+      return source.fetchPodSeries(namespace, pod, settings.seriesMinutes * 60, seriesStepSec(settings))
+        .then(function (sr) { return [null, sr]; });
+    }, true);
+  }
+
   /** Pod → GPU attribution for the Pods page (metrics.js fetchGpuOwners): one series per allocated GPU. */
   function useGpuOwners(enabled) {
     const cluster = clusterKey();
@@ -275,6 +294,7 @@ export function createProviderCore(React, lib, deps) {
     useGpuMetrics: useGpuMetrics,
     useNodeGpuMetrics: useNodeGpuMetrics,
     useGpuOwners: useGpuOwners,
+    usePodGpuSeries: usePodGpuSeries,
     storeFor: storeFor,
     metricsSourceFor: metricsSourceFor,
   };

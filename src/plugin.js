@@ -136,7 +136,10 @@ export function createPlugin(env) {
     const gpuPod = isGpuRequestingPod(raw);
     const nodeName = gpuPod ? get(raw, ['spec', 'nodeName'], null) : null;
     const m = core.useNodeGpuMetrics(nodeName, gpuPod);
-    const section = podDetailView(props.resource, { metrics: m.metrics });
+    // Power history of the pod's GPUs, fetched next to (not after) the node's telemetry.
+    const md = gpuPod && raw.metadata ? raw.metadata : null;
+    const ps = core.usePodGpuSeries(md ? md.namespace || '' : null, md ? md.name : null, !!nodeName);
+    const section = podDetailView(props.resource, { metrics: m.metrics, series: ps.series });
     return section ? h(Section, { s: section }) : null;
   }
 

@@ -114,6 +114,8 @@ export interface SeriesBlock {
   t: 'series';
   power: Record<string, SeriesPoint[]>;
   vram: Record<string, SeriesPoint[]>;
+  /** Header of the first column (default "Node"; "Pod" on the Pod detail page). */
+  label?: string;
   /** Mean power per node over the window (W); nodes without samples are absent. */
   avgPower?: Record<string, number>;
 }

@@ -1204,12 +1204,14 @@ function nodeDetailSection(raw, name, cap, alloc, podsOnNode, loading, own, xg, 
 export function podDetailView(resource, opts) {
   const raw = unwrapKubeObject(resource);
   const metrics = opts && opts.metrics ? opts.metrics : null;
-  if (metrics && raw && typeof raw === 'object' && raw.metadata) {
-    // Live telemetry of the GPUs this pod holds (exporter pod labels).
-    const gs = podGpuAssignments(metrics)[(raw.metadata.namespace || '') + '/' + raw.metadata.name];
-    if (gs) {
-      return memo('pod-detail:' + (raw.metadata.uid || raw.metadata.namespace + '/' + raw.metadata.name), [raw, gs], function () {
-        return podDetailSection(raw, gs);
+  const series = opts && opts.series && opts.series.power && opts.series.power.length ? opts.series : null;
+  if ((metrics || series) && raw && typeof raw === 'object' && raw.metadata) {
+    // Live telemetry of the GPUs this pod holds (exporter pod labels), and
+    // their power over the series window.
+    const gs = metrics ? podGpuAssignments(metrics)[(raw.metadata.namespace || '') + '/' + raw.metadata.name] : undefined;
+    if (gs || series) {
+      return memo('pod-detail:' + (raw.metadata.uid || raw.metadata.namespace + '/' + raw.metadata.name), [raw, gs, series], function () {
+        return podDetailSection(raw, gs, series);
       });
     }
   }
@@ -1222,7 +1224,39 @@ export function podDetailView(resource, opts) {
   return podDetailSection(raw);
 }
 
-function podDetailSection(raw, assigned) {
+/** Blocks of a pod's power history: peak / average over the window and the sparkline. */
+function podPowerBlocks(raw, series) {
+  const win = formatWindow(series.rangeSec || 1800);
+  const byPod = {};
+  byPod[raw.metadata.name] = series.power;
+  const st = clusterPowerStats(byPod);
+  return [
+    kv([
+      row('Peak GPU Power (' + win + ')', formatWatts(st.peakWatts)),
+      row('Average GPU Power (' + win + ')', formatWatts(st.avgWatts)),
+      // Σ samples × step: the energy the pod's GPUs drew over the window.
+      row('GPU Energy (' + win + ')', formatEnergy(seriesEnergyJoules(series.power))),
+    ]),
+    { t: 'series', label: 'Pod', power: byPod, vram: {}, avgPower: seriesMeans(byPod) },
+  ];
+}
+
+/** Energy (J) of a step-aligned power series [[t s, W]]: each sample holds for one step. */
+export function seriesEnergyJoules(pts) {
+  if (!pts || pts.length < 2) return 0;
+  const step = (pts[pts.length - 1][0] - pts[0][0]) / (pts.length - 1);
+  let sum = 0;
+  for (let i = 0; i < pts.length; i++) sum += pts[i][1];
+  return sum * step;
+}
+
+/** Joules → "x Wh" / "x kWh". */
+export function formatEnergy(joules) {
+  const wh = joules / 3600;
+  return wh >= 1000 ? (wh / 1000).toFixed(2) + ' kWh' : wh.toFixed(1) + ' Wh';
+}
+
+function podDetailSection(raw, assigned, series) {
   if (!isGpuRequestingPod(raw)) return null;
   const ics = gpuInitContainers(raw);
   const cs = gpuContainers(raw);
@@ -1257,7 +1291,7 @@ function podDetailSection(raw, assigned) {
         ),
       ].concat(assigned ? [row('Assigned GPUs', assignedLines(assigned))] : []).concat(rows)
     ),
-  ]);
+  ].concat(series ? podPowerBlocks(raw, series) : []));
 }
 
 // ---------------------------------------------------------------------------

@@ -237,9 +237,10 @@ export function createRenderer(React, CC) {
   function Series(props) {
     const b = props.b;
     const nodes = Object.keys(b.power || {});
+    const hbm = Object.keys(b.vram || {}).length > 0;
     return h(CC.SimpleTable, {
       columns: [
-        { label: 'Node', getter: function (n) { return n; } },
+        { label: b.label || 'Node', getter: function (n) { return n; } },
         {
           label: 'Avg Power',
           getter: function (n) { return b.avgPower && b.avgPower[n] !== undefined ? formatWatts(b.avgPower[n]) : '—'; },
@@ -248,11 +249,10 @@ export function createRenderer(React, CC) {
           label: 'Power (W)',
           getter: function (n) { return h(Sparkline, { points: b.power[n] || [], color: BAR_COLORS.ok, label: n + ' power' }); },
         },
-        {
-          label: 'HBM in use',
-          getter: function (n) { return h(Sparkline, { points: (b.vram && b.vram[n]) || [], color: '#6a1b9a', label: n + ' HBM' }); },
-        },
-      ],
+      ].concat(hbm ? [{
+        label: 'HBM in use',
+        getter: function (n) { return h(Sparkline, { points: b.vram[n] || [], color: '#6a1b9a', label: n + ' HBM' }); },
+      }] : []),
       data: nodes,
     });
   }

@@ -4,7 +4,7 @@
  * (PodDetailSection.test.tsx, 10 cases), the Nodes-table columns (untested in
  * the reference) and the topology model (new).
  */
-import { nodeColumns, nodeDetailView, podDetailView } from '../../src/view/pages.js';
+import { formatEnergy, nodeColumns, nodeDetailView, podDetailView, seriesEnergyJoules } from '../../src/view/pages.js';
 import { findSection, firstBlock, rowNames, rowValue, text } from '../../src/view/ir.js';
 import { buildGpuSlots, buildXgmiMatrix, isFullMesh } from '../../src/api/topology.js';
 import { NOW, makeContext, makeGpuNode, makeGpuPod, makeNode, makePlainPod } from './fixtures.js';
@@ -71,6 +71,32 @@ describe('nodeDetailView', () => {
     const s = nodeDetailView(node, ctx);
     expect(firstBlock(s, 'slots').slots).toHaveLength(8);
     expect(firstBlock(s, 'matrix').fullMesh).toBe(true);
+  });
+});
+
+describe('podDetailView: GPU power history', () => {
+  const series = { rangeSec: 1800, power: [[0, 1000], [30, 1200], [60, 1400]] };
+  it('adds peak / average / energy over the window and a sparkline row for the pod', () => {
+    const s = podDetailView(makeGpuPod('train-p', { gpus: 2 }), { series });
+    expect(rowValue(s, 'Peak GPU Power (30 min)')).toBe('1400.0 W');
+    expect(rowValue(s, 'Average GPU Power (30 min)')).toBe('1200.0 W');
+    // 3 samples × 30 s steps: (1000 + 1200 + 1400) W × 30 s = 108 kJ = 30 Wh
+    expect(rowValue(s, 'GPU Energy (30 min)')).toBe('30.0 Wh');
+    const blk = s.blocks.filter((b) => b.t === 'series')[0];
+    expect(blk.label).toBe('Pod');
+    expect(Object.keys(blk.power)).toEqual(['train-p']);
+    expect(blk.avgPower['train-p']).toBe(1200);
+  });
+  it('no history (empty or absent) leaves the section as it was', () => {
+    const plain = podDetailView(makeGpuPod('train-q'));
+    expect(podDetailView(makeGpuPod('train-q'), { series: { rangeSec: 1800, power: [] } }).blocks).toHaveLength(plain.blocks.length);
+    expect(rowValue(plain, 'Peak GPU Power (30 min)')).toBeUndefined();
+  });
+  it('energy helpers', () => {
+    expect(seriesEnergyJoules([[0, 100]])).toBe(0);
+    expect(seriesEnergyJoules([[0, 100], [60, 100]])).toBe(12000);
+    expect(formatEnergy(3600 * 1500)).toBe('1.50 kWh');
+    expect(formatEnergy(3600 * 2)).toBe('2.0 Wh');
   });
 });
 

@@ -26,6 +26,7 @@ import {
   ownersQuery,
   promString,
   METRIC_VIEWS,
+  podPowerQuery,
 } from '../../src/api/metrics.js';
 
 import { BASE0, BASE1, exporterData, ok, prom, vec } from './promFake.js';
@@ -485,6 +486,36 @@ describe('in-flight sharing', () => {
     await src.fetchGpuMetrics();
     await src.fetchGpuMetrics();
     expect(live(request)).toBe(2);
+  });
+});
+
+describe('fetchPodSeries (Pod detail power history)', () => {
+  it('asks for one pod\'s power, summed per step, with escaped matchers', () => {
+    expect(podPowerQuery('ml', 'train-0')).toBe('sum by (__name__) ({__name__="gpu_power_usage", namespace="ml", pod="train-0"})');
+    expect(podPowerQuery('a"b', 'c\\d')).toContain('namespace="a\\"b", pod="c\\\\d"');
+  });
+
+  it('returns the step-aligned total over the window (rows summed per step)', async () => {
+    const request = prom({ data: exporterData(['n0']) });
+    const src = createMetricsSource({ request, clock: { setTimeout, clearTimeout, now: () => 1800 * 1000 * 1000 } });
+    const sr = await src.fetchPodSeries('ml', 'train-0', 1800, 30);
+    const q = decodeURIComponent(request.mock.calls.map((c) => c[0]).find((p) => p.indexOf('/query_range') >= 0));
+    expect(q).toContain('pod="train-0"');
+    expect(q).toContain('step=30');
+    expect(sr.rangeSec).toBe(1800);
+    // the fake answers two power points for one node
+    expect(sr.power.map((p) => p[1])).toEqual([100, 200]);
+    expect(sr.power[0][0]).toBeLessThan(sr.power[1][0]);
+  });
+
+  it('concurrent fetches of one pod share a request; unreachable Prometheus gives null', async () => {
+    const request = prom({ data: exporterData(['n0']) });
+    const src = createMetricsSource({ request });
+    const [a, b] = await Promise.all([src.fetchPodSeries('ml', 'p', 1800, 30), src.fetchPodSeries('ml', 'p', 1800, 30)]);
+    expect(a).toBe(b);
+    expect(request.mock.calls.filter((c) => c[0].indexOf('/query_range') >= 0)).toHaveLength(1);
+    const down = createMetricsSource({ request: prom({ up: [] }) });
+    expect(await down.fetchPodSeries('ml', 'p', 1800, 30)).toBeNull();
   });
 });
 

@@ -415,3 +415,21 @@ describe('React StrictMode (effects mounted, cleaned up and mounted again)', () 
     r.unmount();
   });
 });
+
+describe('Pod detail: power history next to the node telemetry', () => {
+  it('sends the node-scoped query and the pod-scoped range query in one wave and shows the history', async () => {
+    cluster();
+    const fake = prom({ data: exporterData(['mi355x-0', 'mi355x-1']) });
+    const crd = lib.api.handler;
+    lib.api.handler = (p) => (p.indexOf('/proxy/api/v1/') >= 0 ? fake(p) : crd(p));
+    const pod = makeGpuPod('train-a', { gpus: 4 });
+    const Detail = reg.details[1];
+    const r = render(h(() => Detail({ resource: { kind: 'Pod', jsonData: pod } })));
+    await r.settle();
+    const paths = fake.mock.calls.map((c) => decodeURIComponent(c[0]));
+    expect(paths.filter((p) => p.indexOf('hostname="mi355x-0"') >= 0)).toHaveLength(1);
+    expect(paths.filter((p) => p.indexOf('/query_range') >= 0 && p.indexOf('pod="train-a"') >= 0)).toHaveLength(1);
+    expect(r.html()).toContain('Peak GPU Power');
+    r.unmount();
+  });
+});

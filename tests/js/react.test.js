@@ -204,6 +204,14 @@ describe('blocks', () => {
     expect(r.byTag('path')[0].props.d).toBe(sparklinePath(pts, 240, 36));
   });
 
+  it('series with a row label and no HBM data: "Pod" column, no HBM column', () => {
+    const v = setup();
+    const b = { t: 'series', label: 'Pod', power: { 'train-p': [[0, 1], [30, 2]] }, vram: {}, avgPower: { 'train-p': 1.5 } };
+    const r = render(h(v.Block, { b }));
+    const p = only(r, CC.SimpleTable);
+    expect(p.columns.map((c) => c.label)).toEqual(['Pod', 'Avg Power', 'Power (W)']);
+  });
+
   it('sparklinePath needs two points and spans the box', () => {
     expect(sparklinePath([[0, 1]], 10, 10)).toBeNull();
     expect(sparklinePath([[0, 0], [10, 10]], 100, 50)).toBe('M0.0,50.0 L100.0,0.0');
