@@ -576,9 +576,9 @@ async function serve(a) {
         }
         const ctx = L.s.ctx();
         const pods = ctx.gpuPods.filter(function (p) { return p.spec && p.spec.nodeName; });
-        const modes = { podScoped: [], podDetail: [], podClusterWide: [], nodeScoped: [], podsPageOwners: [] };
-        const bytes = { podScoped: 0, podDetail: 0, podClusterWide: 0, nodeScoped: 0, podsPageOwners: 0 };
-        const reqs = { podScoped: 0, podDetail: 0, podClusterWide: 0, nodeScoped: 0, podsPageOwners: 0 };
+        const modes = { podScoped: [], podDetail: [], podClusterWide: [], nodeScoped: [], nodeDetail: [], podsPageOwners: [] };
+        const bytes = { podScoped: 0, podDetail: 0, podClusterWide: 0, nodeScoped: 0, nodeDetail: 0, podsPageOwners: 0 };
+        const reqs = { podScoped: 0, podDetail: 0, podClusterWide: 0, nodeScoped: 0, nodeDetail: 0, podsPageOwners: 0 };
         const slow = [];
         const detailRequest = makeRequest(a.url, counter);
         for (let i = 0; i < n && pods.length; i++) {
@@ -597,6 +597,11 @@ async function serve(a) {
             ['podClusterWide', function (src) { return src.fetchGpuMetrics().then(function (m) { return podDetailView(pod, { metrics: m }); }); }],
             ['nodeScoped', function (src) {
               return src.fetchNodeMetrics(pod.spec.nodeName).then(function (m) { return node ? nodeDetailView(node, ctx, { metrics: m }) : null; });
+            }],
+            // As src/plugin.js wires the Node detail page: telemetry + power history in one wave.
+            ['nodeDetail', function (src) {
+              return Promise.all([src.fetchNodeMetrics(pod.spec.nodeName), src.fetchNodeSeries(pod.spec.nodeName, 1800, 30)])
+                .then(function (r) { return node ? nodeDetailView(node, ctx, { metrics: r[0], series: r[1] }) : null; });
             }],
             // GPU Pods page: pod → GPU attribution only.
             ['podsPageOwners', function (src) {

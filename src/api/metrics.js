@@ -439,6 +439,11 @@ export function podPowerQuery(namespace, pod) {
     '", pod="' + promString(pod) + '"})';
 }
 
+/** One node's total GPU power over time (Node detail history), summed per step. */
+export function nodePowerQuery(nodeName) {
+  return 'sum by (__name__) ({__name__="' + SERIES.exporter.power + '", hostname="' + promString(nodeName) + '"})';
+}
+
 /** Per-node power + HBM-used history in one range query (split by `__name__`). */
 export function seriesQuery() {
   const E = SERIES.exporter;
@@ -930,13 +935,22 @@ export function createMetricsSource(opts) {
    * @returns {Promise<{rangeSec: number, power: Array<[number, number]>} | null>}
    */
   function fetchPodSeries(namespace, pod, rangeSec, stepSec) {
+    return powerSeries('pod|' + namespace + '/' + pod, podPowerQuery(namespace, pod), rangeSec, stepSec);
+  }
+
+  /** A node's GPU power over the last `rangeSec` (nodePowerQuery); shape and nulls as fetchPodSeries. */
+  function fetchNodeSeries(nodeName, rangeSec, stepSec) {
+    return powerSeries('node|' + nodeName, nodePowerQuery(nodeName), rangeSec, stepSec);
+  }
+
+  function powerSeries(scope, q, rangeSec, stepSec) {
     const range = rangeSec || 1800;
     const step = stepSec || 30;
-    const key = 'pod|' + namespace + '/' + pod + '|' + range + '|' + step;
+    const key = 'power|' + scope + '|' + range + '|' + step;
     return shared(key, function () {
       return withPrometheus(function (base) {
         const end = Math.floor(clock.now() / 1000 / step) * step;
-        return rangeQuery(base, podPowerQuery(namespace, pod), end - range, end, step).then(function (got) {
+        return rangeQuery(base, q, end - range, end, step).then(function (got) {
           if (got === UNREACHABLE) return UNREACHABLE;
           // Sum whatever rows came back per step (one row after `sum by (__name__)`).
           const total = {};
@@ -961,6 +975,7 @@ export function createMetricsSource(opts) {
     invalidate: invalidate,
     fetchGpuMetrics: fetchGpuMetrics,
     fetchPodSeries: fetchPodSeries,
+    fetchNodeSeries: fetchNodeSeries,
     fetchNodeMetrics: fetchNodeMetrics,
     fetchGpuOwners: fetchGpuOwners,
     fetchSeries: fetchSeries,

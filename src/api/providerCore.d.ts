@@ -40,6 +40,7 @@ export interface MetricsSource {
   fetchNodeMetrics(nodeName: string): Promise<GpuMetrics | null>;
   fetchGpuOwners(): Promise<GpuMetrics | null>;
   fetchPodSeries(namespace: string, pod: string, rangeSec: number, stepSec: number): Promise<{ rangeSec: number; power: Array<[number, number]> } | null>;
+  fetchNodeSeries(nodeName: string, rangeSec: number, stepSec: number): Promise<{ rangeSec: number; power: Array<[number, number]> } | null>;
   fetchSeries(rangeSec: number, stepSec: number): Promise<GpuMetricsState['series']>;
 }
 
@@ -51,6 +52,7 @@ export interface ProviderCore {
   useNodeGpuMetrics(nodeName: string | null, enabled?: boolean): GpuMetricsState;
   useGpuOwners(enabled?: boolean): GpuMetricsState;
   usePodGpuSeries(namespace: string | null, pod: string | null, enabled?: boolean): GpuMetricsState;
+  useNodeGpuSeries(nodeName: string | null, enabled?: boolean): GpuMetricsState;
   storeFor(cluster: string): ClusterStore;
   metricsSourceFor(cluster: string): MetricsSource;
 }

@@ -277,6 +277,19 @@ export function createProviderCore(React, lib, deps) {
     }, true);
   }
 
+  /** One node's GPU power history for the native Node detail page (metrics.js fetchNodeSeries). */
+  function useNodeGpuSeries(nodeName, enabled) {
+    const cluster = clusterKey();
+    const source = metricsSourceFor(cluster);
+    const settings = loadSettings();
+    const active = (enabled === undefined ? true : enabled) && !!nodeName;
+    const key = 'nodeseries|' + sourceKey(cluster, settings) + '|' + nodeName + '|' + settings.seriesMinutes;
+    return useMetricsFetch(active ? key : null, function () {
+      return source.fetchNodeSeries(nodeName, settings.seriesMinutes * 60, seriesStepSec(settings))
+        .then(function (sr) { return [null, sr]; });
+    }, true);
+  }
+
   /** Pod → GPU attribution for the Pods page (metrics.js fetchGpuOwners): one series per allocated GPU. */
   function useGpuOwners(enabled) {
     const cluster = clusterKey();
@@ -295,6 +308,7 @@ export function createProviderCore(React, lib, deps) {
     useNodeGpuMetrics: useNodeGpuMetrics,
     useGpuOwners: useGpuOwners,
     usePodGpuSeries: usePodGpuSeries,
+    useNodeGpuSeries: useNodeGpuSeries,
     storeFor: storeFor,
     metricsSourceFor: metricsSourceFor,
   };

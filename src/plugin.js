@@ -121,7 +121,8 @@ export function createPlugin(env) {
     const raw = unwrapKubeObject(props.resource);
     const gpuNode = isAmdGpuNode(raw);
     const m = core.useNodeGpuMetrics(gpuNode ? raw.metadata.name : null, gpuNode);
-    const section = nodeDetailView(props.resource, ctx, { metrics: m.metrics });
+    const ps = core.useNodeGpuSeries(gpuNode ? raw.metadata.name : null, gpuNode);
+    const section = nodeDetailView(props.resource, ctx, { metrics: m.metrics, series: ps.series });
     return section ? h(Section, { s: section }) : null;
   }
 

@@ -1149,12 +1149,13 @@ export function nodeDetailView(resource, ctx, opts) {
   const xg = metrics && metrics.xgmi ? metrics.xgmi[name] : undefined;
   const lk = metrics && metrics.links ? metrics.links[name] : undefined;
   const podsUnreadable = ctx.podsState === 'error';
-  return memo('node-detail:' + name, [raw, podsOnNode, !!ctx.loading, podsUnreadable, own, xg, lk], function () {
-    return nodeDetailSection(raw, name, cap, alloc, podsOnNode, ctx.loading, own, xg, lk, podsUnreadable);
+  const series = opts && opts.series && opts.series.power && opts.series.power.length ? opts.series : null;
+  return memo('node-detail:' + name, [raw, podsOnNode, !!ctx.loading, podsUnreadable, own, xg, lk, series], function () {
+    return nodeDetailSection(raw, name, cap, alloc, podsOnNode, ctx.loading, own, xg, lk, podsUnreadable, series);
   });
 }
 
-function nodeDetailSection(raw, name, cap, alloc, podsOnNode, loading, own, xg, lk, podsUnreadable) {
+function nodeDetailSection(raw, name, cap, alloc, podsOnNode, loading, own, xg, lk, podsUnreadable, series) {
   const allocatable = parseInt(alloc[AMD_GPU_RESOURCE] || '0', 10) || 0;
   let inUse = 0;
   for (let i = 0; i < podsOnNode.length; i++) {
@@ -1184,11 +1185,12 @@ function nodeDetailSection(raw, name, cap, alloc, podsOnNode, loading, own, xg, 
           : loading ? 'Loading…' : 'None'
     )
   );
-  const blocks = [kv(rows)];
+  let blocks = [kv(rows)];
   if (count > 0) {
     blocks.push(slotsBlock(raw, podsOnNode, own));
     blocks.push(matrixBlock(phys, xg, lk));
   }
+  if (series) blocks = blocks.concat(powerHistoryBlocks(name, 'Node', series));
   return section('AMD GPU', blocks);
 }
 
@@ -1224,11 +1226,14 @@ export function podDetailView(resource, opts) {
   return podDetailSection(raw);
 }
 
-/** Blocks of a pod's power history: peak / average over the window and the sparkline. */
-function podPowerBlocks(raw, series) {
+/**
+ * Blocks of a node's or pod's GPU power history: peak / average / energy over
+ * the window and the sparkline row (`label` heads its first column).
+ */
+function powerHistoryBlocks(name, label, series) {
   const win = formatWindow(series.rangeSec || 1800);
   const byPod = {};
-  byPod[raw.metadata.name] = series.power;
+  byPod[name] = series.power;
   const st = clusterPowerStats(byPod);
   return [
     kv([
@@ -1237,7 +1242,7 @@ function podPowerBlocks(raw, series) {
       // Σ samples × step: the energy the pod's GPUs drew over the window.
       row('GPU Energy (' + win + ')', formatEnergy(seriesEnergyJoules(series.power))),
     ]),
-    { t: 'series', label: 'Pod', power: byPod, vram: {}, avgPower: seriesMeans(byPod) },
+    { t: 'series', label: label, power: byPod, vram: {}, avgPower: seriesMeans(byPod) },
   ];
 }
 
@@ -1291,7 +1296,7 @@ function podDetailSection(raw, assigned, series) {
         ),
       ].concat(assigned ? [row('Assigned GPUs', assignedLines(assigned))] : []).concat(rows)
     ),
-  ].concat(series ? podPowerBlocks(raw, series) : []));
+  ].concat(series ? powerHistoryBlocks(raw.metadata.name, 'Pod', series) : []));
 }
 
 // ---------------------------------------------------------------------------

@@ -100,6 +100,20 @@ describe('podDetailView: GPU power history', () => {
   });
 });
 
+describe('nodeDetailView: GPU power history', () => {
+  it('adds the node\'s peak / average / energy and a Node sparkline row after the matrix', () => {
+    const ctx = makeContext({ nodes: [makeGpuNode('mi355x-7')] });
+    const series = { rangeSec: 1800, power: [[0, 8000], [30, 9000]] };
+    const s = nodeDetailView(makeGpuNode('mi355x-7'), ctx, { series });
+    expect(rowValue(s, 'Peak GPU Power (30 min)')).toBe('9000.0 W');
+    const kinds = s.blocks.map((b) => b.t);
+    expect(kinds.slice(-2)).toEqual(['kv', 'series']);
+    expect(kinds.indexOf('matrix')).toBeLessThan(kinds.indexOf('series'));
+    expect(s.blocks[s.blocks.length - 1].label).toBe('Node');
+    expect(nodeDetailView(makeGpuNode('mi355x-7'), ctx, {}).blocks.filter((b) => b.t === 'series')).toHaveLength(0);
+  });
+});
+
 describe('podDetailView', () => {
   it('returns null for CPU pods', () => {
     expect(podDetailView(makePlainPod('x'))).toBeNull();

@@ -26,6 +26,7 @@ import {
   ownersQuery,
   promString,
   METRIC_VIEWS,
+  nodePowerQuery,
   podPowerQuery,
 } from '../../src/api/metrics.js';
 
@@ -506,6 +507,16 @@ describe('fetchPodSeries (Pod detail power history)', () => {
     // the fake answers two power points for one node
     expect(sr.power.map((p) => p[1])).toEqual([100, 200]);
     expect(sr.power[0][0]).toBeLessThan(sr.power[1][0]);
+  });
+
+  it('node history: hostname-scoped query; node and pod histories are separate requests', async () => {
+    expect(nodePowerQuery('mi355x-0')).toBe('sum by (__name__) ({__name__="gpu_power_usage", hostname="mi355x-0"})');
+    const request = prom({ data: exporterData(['n0']) });
+    const src = createMetricsSource({ request });
+    const [n, p] = await Promise.all([src.fetchNodeSeries('n0', 1800, 30), src.fetchPodSeries('ml', 'n0', 1800, 30)]);
+    expect(n.power.length).toBeGreaterThan(0);
+    expect(n).not.toBe(p);
+    expect(request.mock.calls.filter((c) => c[0].indexOf('/query_range') >= 0)).toHaveLength(2);
   });
 
   it('concurrent fetches of one pod share a request; unreachable Prometheus gives null', async () => {

@@ -410,8 +410,10 @@ describe('React StrictMode (effects mounted, cleaned up and mounted again)', () 
     const Detail = reg.details[0];
     const r = render(h(() => Detail({ resource: { kind: 'Node', jsonData: makeGpuNode('mi355x-0') } })), { strict: true });
     await r.settle();
-    const scoped = fake.mock.calls.filter((c) => decodeURIComponent(c[0]).indexOf('hostname="mi355x-0"') >= 0);
-    expect(scoped).toHaveLength(1);
+    const scoped = fake.mock.calls.map((c) => decodeURIComponent(c[0])).filter((p) => p.indexOf('hostname="mi355x-0"') >= 0);
+    // one node-scoped instant query (live telemetry) and one node-scoped range query (power history)
+    expect(scoped.filter((p) => p.indexOf('/query?') >= 0)).toHaveLength(1);
+    expect(scoped.filter((p) => p.indexOf('/query_range?') >= 0)).toHaveLength(1);
     r.unmount();
   });
 });

@@ -100,10 +100,11 @@ def test_detail_pages_cost_one_node_of_telemetry_whatever_the_cluster_size():
     assert out[16]["podClusterWide"]["bytes"] > 10 * out[16]["podScoped"]["bytes"], out
     # The Pod detail page as wired: node telemetry + the pod's power history, two requests in one wave, bytes
     # independent of the cluster size, latency one round trip (RTT 5 ms here).
-    pd = out[16]["podDetail"]
-    assert pd["requests"] == 2 and out[1]["podDetail"]["requests"] == 2
-    assert abs(pd["bytes"] - out[1]["podDetail"]["bytes"]) <= 0.05 * out[1]["podDetail"]["bytes"], out
-    assert pd["p50_ms"] < 2 * out[16]["podScoped"]["p50_ms"] + 5, out
+    for kind, one in (("podDetail", "podScoped"), ("nodeDetail", "nodeScoped")):
+        pd = out[16][kind]
+        assert pd["requests"] == 2 and out[1][kind]["requests"] == 2, out
+        assert abs(pd["bytes"] - out[1][kind]["bytes"]) <= 0.05 * out[1][kind]["bytes"], out
+        assert pd["p50_ms"] < 2 * out[16][one]["p50_ms"] + 5, out
     # The GPU Pods page asks for pod attribution only: one series per allocated GPU.
     assert out[16]["podsPageOwners"]["requests"] == 1
     assert out[16]["podsPageOwners"]["bytes"] < 0.1 * out[16]["podClusterWide"]["bytes"], out
