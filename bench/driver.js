@@ -211,7 +211,8 @@ const SNAPSHOT_CSS =
   'button{margin-left:12px}';
 
 /** Write one static HTML file per view (plus a node and a pod detail section). */
-function writeSnapshots(ctx, mstate, dir, now) {
+function writeSnapshots(ctx, mstate, dir, now, history) {
+  const hist = history || {};
   fs.mkdirSync(dir, { recursive: true });
   const opts = { metrics: mstate.metrics, now: now };
   const views = [
@@ -222,11 +223,11 @@ function writeSnapshots(ctx, mstate, dir, now) {
     ['05-metrics', renderPage(metricsView(ctx, Object.assign({}, mstate, { now: now })))],
   ];
   if (ctx.gpuNodes.length) {
-    const s = nodeDetailView(ctx.gpuNodes[0], ctx, opts);
+    const s = nodeDetailView(ctx.gpuNodes[0], ctx, Object.assign({}, opts, { series: hist.node }));
     if (s) views.push(['06-node-detail', renderSection(s)]);
   }
   if (ctx.gpuPods.length) {
-    const s = podDetailView(ctx.gpuPods[0], opts);
+    const s = podDetailView(ctx.gpuPods[0], Object.assign({}, opts, { series: hist.pod }));
     if (s) views.push(['07-pod-detail', renderSection(s)]);
   }
   const files = [];
@@ -307,6 +308,7 @@ function amdSchedule(request, clock) {
     },
     ctx: function () { return store.getSnapshot(); },
     mstate: function () { return mstate; },
+    source: metrics,
     spans: spans,
   };
 }
@@ -550,10 +552,19 @@ async function serve(a) {
         // the benchmark. With `now` the data layer runs on that fixed clock
         // (fetch times, range windows), so the files are reproducible.
         let snap;
+        let history = null;
         if (c.now) {
           const fixed = { setTimeout: setTimeout, clearTimeout: clearTimeout, now: function () { return c.now; } };
           snap = amdSchedule(makeRequest(a.url, counter), fixed);
           await snap.coldOpen();
+          // The detail pages' power history, as src/plugin.js fetches it.
+          const c0 = snap.ctx();
+          const n0 = c0.gpuNodes[0];
+          const p0 = c0.gpuPods[0];
+          history = {
+            node: n0 ? await snap.source.fetchNodeSeries(n0.metadata.name, 1800, 30) : null,
+            pod: p0 ? await snap.source.fetchPodSeries(p0.metadata.namespace || '', p0.metadata.name, 1800, 30) : null,
+          };
         } else {
           const L = get(name);
           if (!L.opened) {
@@ -562,7 +573,7 @@ async function serve(a) {
           }
           snap = L.s;
         }
-        out.files = writeSnapshots(snap.ctx(), snap.mstate(), c.dir, c.now);
+        out.files = writeSnapshots(snap.ctx(), snap.mstate(), c.dir, c.now, history);
       } else if (c.cmd === 'detail') {
         // Native detail pages opened on a warm cluster (a plugin page loaded
         // before): Pod detail and Node detail each fetch their node's
