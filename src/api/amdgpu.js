@@ -548,7 +548,6 @@ export function getPodGpuDemand(pod) {
   return out;
 }
 
-/** Whole GPUs the pod holds (`amd.com/gpu`). */
 /** GPU devices the pod holds: `amd.com/gpu` plus partition resources. */
 export function getPodGpuCount(pod) {
   const d = getPodGpuDemand(pod);
