@@ -27,3 +27,31 @@ def test_ci_prefers_npm_ci_when_locked():
     install = next(s for s in steps if s.get("name") == "Install")["run"]
     assert "package-lock.json" in install and "npm ci" in install
     assert any(s.get("uses", "").startswith("actions/upload-artifact") for s in steps)
+
+
+def test_offline_plugin_archive_is_installable_and_reproducible(tmp_path):
+    """`node tools/bundle.js --package`: `<name>/main.js` + `<name>/package.json` (the layout Headlamp loads from its
+    plugins directory), byte-identical across runs so the ArtifactHub checksum is stable."""
+    import hashlib
+    import subprocess
+    import tarfile
+
+    from headlamp_intel_gpu_plugin_amd.utils.nodebridge import node_binary
+
+    pkg = json.load(open(os.path.join(ROOT, "package.json")))
+    shas = []
+    for run in ("a", "b"):
+        out = tmp_path / run / "main.js"
+        r = subprocess.run([node_binary(), os.path.join(ROOT, "tools", "bundle.js"), "--out", str(out), "--package"],
+                           cwd=ROOT, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+        arc = tmp_path / run / f"{pkg['name']}-{pkg['version']}.tar.gz"
+        sha = hashlib.sha256(arc.read_bytes()).hexdigest()
+        assert f"sha256:{sha}" in r.stdout
+        shas.append(sha)
+        with tarfile.open(arc) as t:
+            assert t.getnames() == [f"{pkg['name']}/main.js", f"{pkg['name']}/package.json"]
+            assert t.extractfile(f"{pkg['name']}/main.js").read() == out.read_bytes()
+            meta = json.load(t.extractfile(f"{pkg['name']}/package.json"))
+    assert shas[0] == shas[1]
+    assert meta["name"] == pkg["name"] and meta["version"] == pkg["version"] and meta["main"] == "main.js"

@@ -4,7 +4,7 @@
  * self-contained script (default `dist-offline/main.js`; `headlamp-plugin build`
  * writes `dist/main.js`), the file Headlamp loads for a plugin.
  *
- *   node tools/bundle.js [--entry src/index.tsx] [--out dist-offline/main.js]
+ *   node tools/bundle.js [--entry src/index.tsx] [--out dist-offline/main.js] [--package]
  *
  * The reference builds its bundle with `headlamp-plugin build` (vite;
  * /root/reference/package.json:16-18, CI /root/reference/.github/workflows/ci.yaml:169-170).
@@ -28,9 +28,11 @@
  * checks load (tests/js/bundle.test.js evaluates it against the harness
  * stand-ins and mounts every registered component).
  */
+import crypto from 'crypto';
 import fs from 'fs';
 import path from 'path';
 import { fileURLToPath } from 'url';
+import zlib from 'zlib';
 
 const ROOT = path.resolve(path.dirname(fileURLToPath(import.meta.url)), '..');
 
@@ -207,14 +209,62 @@ export function bundle(entry) {
   return { code: parts.join('\n') + '\n', modules: order };
 }
 
+/** One ustar header + body (padded to 512-byte blocks). */
+function tarEntry(name, body, mtime) {
+  const h = Buffer.alloc(512, 0);
+  function put(off, len, str) { h.write(str, off, len, 'ascii'); }
+  function oct(off, len, n) { put(off, len, n.toString(8).padStart(len - 1, '0') + '\0'); }
+  if (Buffer.byteLength(name) > 100) throw new Error('bundle: tar name too long: ' + name);
+  put(0, 100, name);
+  oct(100, 8, 0o644);
+  oct(108, 8, 0);
+  oct(116, 8, 0);
+  oct(124, 12, body.length);
+  oct(136, 12, mtime);
+  put(148, 8, '        '); // checksum placeholder (spaces) while summing
+  put(156, 1, '0');
+  put(257, 6, 'ustar\0');
+  put(263, 2, '00');
+  let sum = 0;
+  for (let i = 0; i < 512; i++) sum += h[i];
+  put(148, 8, sum.toString(8).padStart(6, '0') + '\0 ');
+  const pad = Buffer.alloc((512 - (body.length % 512)) % 512, 0);
+  return Buffer.concat([h, body, pad]);
+}
+
+/**
+ * The installable plugin archive: `<name>/main.js` + `<name>/package.json`,
+ * the layout Headlamp loads from its plugins directory and `headlamp-plugin
+ * package` produces; gzip-compressed, deterministic (fixed mtime). Returns
+ * {file, sha256} — the checksum artifacthub-pkg.yml's archive-checksum takes.
+ */
+export function packageArchive(code, outDir) {
+  const pkg = JSON.parse(fs.readFileSync(path.join(ROOT, 'package.json'), 'utf8'));
+  const meta = { name: pkg.name, version: pkg.version, description: pkg.description, license: pkg.license, main: 'main.js' };
+  const mtime = 0;
+  const tar = Buffer.concat([
+    tarEntry(pkg.name + '/main.js', Buffer.from(code, 'utf8'), mtime),
+    tarEntry(pkg.name + '/package.json', Buffer.from(JSON.stringify(meta, null, 2) + '\n', 'utf8'), mtime),
+    Buffer.alloc(1024, 0),
+  ]);
+  const gz = zlib.gzipSync(tar, { level: 9 });
+  // gzip header bytes 4-7 hold an mtime; zlib writes 0, so the archive is reproducible.
+  const file = path.join(outDir, pkg.name + '-' + pkg.version + '.tar.gz');
+  fs.mkdirSync(outDir, { recursive: true });
+  fs.writeFileSync(file, gz);
+  return { file: file, sha256: crypto.createHash('sha256').update(gz).digest('hex') };
+}
+
 function main(argv) {
   let entry = path.join(ROOT, 'src', 'index.tsx');
   let out = path.join(ROOT, 'dist-offline', 'main.js');
+  let pack = false;
   for (let i = 0; i < argv.length; i++) {
     if (argv[i] === '--entry') entry = path.resolve(argv[++i]);
     else if (argv[i] === '--out') out = path.resolve(argv[++i]);
+    else if (argv[i] === '--package') pack = true;
     else {
-      process.stderr.write('usage: node tools/bundle.js [--entry src/index.tsx] [--out dist-offline/main.js]\n');
+      process.stderr.write('usage: node tools/bundle.js [--entry src/index.tsx] [--out dist-offline/main.js] [--package]\n');
       return 2;
     }
   }
@@ -224,6 +274,10 @@ function main(argv) {
   fs.writeFileSync(tmp, b.code);
   fs.renameSync(tmp, out);
   process.stdout.write(path.relative(process.cwd(), out) + ': ' + b.modules.length + ' modules, ' + b.code.length + ' bytes\n');
+  if (pack) {
+    const a = packageArchive(b.code, path.dirname(out));
+    process.stdout.write(path.relative(process.cwd(), a.file) + ': sha256:' + a.sha256 + '\n');
+  }
   return 0;
 }
 
