@@ -128,7 +128,7 @@ def _node(name: str, labels: Dict[str, str], capacity: Dict[str, str], age_days:
 
 def _pod(name: str, ns: str, node: Optional[str], containers: List[dict], phase: str = "Running",
          labels: Optional[dict] = None, init: Optional[List[dict]] = None, waiting: Optional[str] = None,
-         restarts: int = 0, age_hours: float = 2.0) -> dict:
+         restarts: int = 0, age_hours: float = 2.0, sched_msg: Optional[str] = None) -> dict:
     ready = phase == "Running"
     statuses = []
     for c in containers:
@@ -138,7 +138,10 @@ def _pod(name: str, ns: str, node: Optional[str], containers: List[dict], phase:
         statuses.append({"name": c["name"], "ready": ready, "restartCount": restarts, "image": c.get("image", ""), "state": st})
     conds = [{"type": "Ready", "status": "True" if ready else "False"}]
     if node is None:
-        conds.append({"type": "PodScheduled", "status": "False", "reason": "Unschedulable"})
+        c = {"type": "PodScheduled", "status": "False", "reason": "Unschedulable"}
+        if sched_msg:
+            c["message"] = sched_msg
+        conds.append(c)
     pod = {
         "apiVersion": "v1",
         "kind": "Pod",
@@ -287,8 +290,12 @@ class SyntheticCluster:
                     self.gpu_owner[(node, slot + k)] = ("ml", name)
                 slot += g
             for j in range(s.pending_per_node):
+                # kube-scheduler's fit-error wording: no GPU node has 8 free GPUs
+                n_all = s.gpu_nodes + s.cpu_nodes
+                msg = (f"0/{n_all} nodes are available: {s.gpu_nodes} Insufficient amd.com/gpu"
+                       + (f", {s.cpu_nodes} node(s) didn't match Pod's node affinity/selector" if s.cpu_nodes else "") + ".")
                 self.pods.append(_pod(f"queued-{i:03d}-{j}", "ml", None, [_gpu_container("trainer", 8)],
-                                      phase="Pending", age_hours=0.2))
+                                      phase="Pending", age_hours=0.2, sched_msg=msg))
         # one finished job on the first node
         if s.gpu_nodes > 0 and s.pods_per_node:
             self.pods.append(_pod("eval-000-done", "ml", gpu_node_name(0), [_gpu_container("eval", 1)],

@@ -611,6 +611,28 @@ export function podWaitingReason(pod) {
   return null;
 }
 
+/**
+ * The message behind podWaitingReason: the scheduler's explanation of an
+ * unschedulable pod ("0/8 nodes are available: 8 Insufficient amd.com/gpu.")
+ * or the kubelet's for a waiting container (image pull errors, …). Null when
+ * there is none.
+ */
+export function podWaitingMessage(pod) {
+  const lists = [get(pod, ['status', 'initContainerStatuses'], []), get(pod, ['status', 'containerStatuses'], [])];
+  for (let j = 0; j < lists.length; j++) {
+    for (let i = 0; i < lists[j].length; i++) {
+      if (get(lists[j][i], ['state', 'waiting', 'reason'], null)) return get(lists[j][i], ['state', 'waiting', 'message'], null);
+    }
+  }
+  const conds = get(pod, ['status', 'conditions'], []);
+  for (let i = 0; i < conds.length; i++) {
+    if (conds[i] && conds[i].type === 'PodScheduled' && conds[i].status === 'False' && conds[i].reason) {
+      return conds[i].message || null;
+    }
+  }
+  return null;
+}
+
 /** Running/Succeeded → success, Pending/unknown → warning, Failed → error (reference PodsPage.tsx:30-43). */
 export function phaseToStatus(phase) {
   switch (phase) {

@@ -64,6 +64,7 @@ import {
   phaseToStatus,
   pluginPodComponent,
   podPhase,
+  podWaitingMessage,
   podWaitingReason,
   unwrapKubeObject,
 } from '../api/amdgpu.js';
@@ -853,10 +854,12 @@ function podsItems(ctx, now, assign) {
     items.push(
       section('Attention: Pending GPU Pods', [
         table(
-          ['Name', 'Namespace', 'GPU Resources', 'Waiting Reason', 'Age'],
+          // "Message" (beyond the reference): why the scheduler cannot place the pod.
+          ['Name', 'Namespace', 'GPU Resources', 'Waiting Reason', 'Message', 'Age'],
           pending.map(function (p) {
             return pendingRows(p, [], function () {
-              return [podName(p), podNs(p), formatPodGpuRequests(p), podWaitingReason(p) || '—', ageText(p.metadata.creationTimestamp, now)];
+              return [podName(p), podNs(p), formatPodGpuRequests(p), podWaitingReason(p) || '—', podWaitingMessage(p) || '—',
+                ageText(p.metadata.creationTimestamp, now)];
             }, now);
           })
         ),
@@ -871,7 +874,6 @@ function podsItems(ctx, now, assign) {
 // Metrics (reference MetricsPage.tsx:191-355)
 // ---------------------------------------------------------------------------
 
-/** Power bar: "X W / Y W (Z%)" with 70/90 colouring (reference PowerBar, MetricsPage.tsx:50-89). */
 /** Mean value per node of a series map (node → [[t, v]]); nodes without samples are left out. */
 export function seriesMeans(byNode) {
   const out = {};
@@ -908,6 +910,7 @@ export function nodesReporting(m, ctx) {
   return missing > 0 ? status('warning', text + ' (' + missing + ' without telemetry)') : text;
 }
 
+/** Power bar: "X W / Y W (Z%)" with 70/90 colouring (reference PowerBar, MetricsPage.tsx:50-89). */
 export function powerBar(watts, capWatts) {
   const hasCap = capWatts !== null && capWatts > 0;
   const p = hasCap ? Math.min(100, pct(watts, capWatts)) : null;

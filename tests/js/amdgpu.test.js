@@ -49,6 +49,7 @@ import {
   pctToStatus,
   phaseToStatus,
   pluginPodComponent,
+  podWaitingMessage,
   podWaitingReason,
   unwrapAll,
   unwrapKubeObject,
@@ -268,6 +269,16 @@ describe('pod status helpers', () => {
     p.status.containerStatuses = [];
     p.status.conditions = [{ type: 'PodScheduled', status: 'False', reason: 'Unschedulable' }];
     expect(podWaitingReason(p)).toBe('Unschedulable');
+  });
+  it('podWaitingMessage: the scheduler\'s explanation, or the waiting container\'s message', () => {
+    const p = makeGpuPod('p', { phase: 'Pending', node: null });
+    p.status.containerStatuses = [];
+    p.status.conditions = [{ type: 'PodScheduled', status: 'False', reason: 'Unschedulable', message: '0/8 nodes are available: 8 Insufficient amd.com/gpu.' }];
+    expect(podWaitingMessage(p)).toBe('0/8 nodes are available: 8 Insufficient amd.com/gpu.');
+    const q = makeGpuPod('q', { phase: 'Pending', waiting: 'ImagePullBackOff' });
+    q.status.containerStatuses[0].state.waiting.message = 'Back-off pulling image "rocm/pytorch:bad"';
+    expect(podWaitingMessage(q)).toBe('Back-off pulling image "rocm/pytorch:bad"');
+    expect(podWaitingMessage(makeGpuPod('r'))).toBeNull();
   });
   it('phaseToStatus maps phases', () => {
     expect(phaseToStatus('Running')).toBe('success');

@@ -293,6 +293,8 @@ describe('podsView', () => {
     expect(t.rows).toHaveLength(1);
     expect(t.rows[0][2]).toBe('GPU: 4');
     expect(t.rows[0][3]).toBe('ImagePullBackOff');
+    expect(t.columns).toEqual(['Name', 'Namespace', 'GPU Resources', 'Waiting Reason', 'Message', 'Age']);
+    expect(t.rows[0][4]).toBe('—'); // no message on this fixture
   });
   it('omits the pending table when nothing is pending', () => {
     expect(sectionTitles(podsView(makeContext({ pods: [makeGpuPod('a')] }), opts))).not.toContain('Attention: Pending GPU Pods');
