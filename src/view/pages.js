@@ -530,16 +530,36 @@ export function matrixBlock(gpuCount, measured, probed) {
   };
 }
 
+/**
+ * Readiness as `kubectl get nodes` words it: "Ready", "Not Ready", and
+ * ", SchedulingDisabled" on a cordoned node (spec.unschedulable) — whose free
+ * GPUs new pods cannot use, hence a warning.
+ */
+export function nodeReadyCell(node) {
+  const ready = isNodeReady(node);
+  const cordoned = get(node, ['spec', 'unschedulable'], false) === true;
+  const text = (ready ? 'Ready' : 'Not Ready') + (cordoned ? ', SchedulingDisabled' : '');
+  return status(!ready ? 'error' : cordoned ? 'warning' : 'success', text);
+}
+
+/** "key=value:Effect" per taint (the reference models NodeSpec.taints, k8s.ts:92-122, but never shows them). */
+export function formatTaints(node) {
+  const ts = get(node, ['spec', 'taints'], []);
+  if (!Array.isArray(ts) || ts.length === 0) return null;
+  return ts.map(function (t) { return (t.key || '') + (t.value ? '=' + t.value : '') + ':' + (t.effect || ''); }).join(', ');
+}
+
 function nodeCardRows(node, podsOnNode, stats, now) {
   const model = getNodeGpuModel(node);
-  const ready = isNodeReady(node);
   const count = getNodeGpuCount(node);
   const cap = getGpuResources(get(node, ['status', 'capacity'], null));
   const alloc = getGpuResources(get(node, ['status', 'allocatable'], null));
   const rows = [
-    row('Status', status(ready ? 'success' : 'error', ready ? 'Ready' : 'Not Ready')),
+    row('Status', nodeReadyCell(node)),
     row('GPU Model', model.product),
   ];
+  const taints = formatTaints(node);
+  if (taints) rows.push(row('Taints', taints));
   if (count > 0) {
     const phys = getNodePhysicalGpuCount(node);
     rows.push(row('GPU Devices (amd.com/gpu)', phys !== count ? count + ' (' + phys + ' × ' + model.shortName + ' in ' + model.computePartition + ')' : String(count)));
@@ -741,10 +761,9 @@ function nodesHeadItems(ctx, now) {
             // Per-node stats keep their identity while unchanged (buildClusterIndex).
             return nodeSummaryRows(n, [st], function () {
               const count = getNodeGpuCount(n);
-              const ready = isNodeReady(n);
               return [
                 n.metadata.name,
-                status(ready ? 'success' : 'error', ready ? 'Ready' : 'Not Ready'),
+                nodeReadyCell(n),
                 formatGpuModel(getNodeGpuModel(n)),
                 count > 0 ? String(count) : '—',
                 allocationBar(st ? st.inUse : 0, (st && st.allocatable) || count),

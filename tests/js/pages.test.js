@@ -20,6 +20,8 @@ import {
   hbmBar,
   gpuContainerLines,
   ACTIVE_PODS_LIMIT,
+  formatTaints,
+  nodeReadyCell,
 } from '../../src/view/pages.js';
 import { countRows, findSection, firstBlock, firstTable, loaders, rowNames, rowValue, sectionTitles, text } from '../../src/view/ir.js';
 import { renderPage, textContent } from '../../src/view/html.js';
@@ -199,6 +201,21 @@ describe('devicePluginsView', () => {
 
 // ---------------------------------------------------------------------------
 describe('nodesView', () => {
+  it('a cordoned GPU node reads "Ready, SchedulingDisabled" (warning) and its card lists the taints', () => {
+    const n = makeGpuNode('g0');
+    n.spec = { unschedulable: true, taints: [{ key: 'amd.com/gpu', value: 'present', effect: 'NoSchedule' }, { key: 'node.kubernetes.io/unschedulable', effect: 'NoSchedule' }] };
+    const vm = nodesView(makeContext({ nodes: [n] }), opts);
+    const t = firstTable(findSection(vm, 'GPU Node Summary'));
+    expect(t.rows[0][1]).toEqual({ t: 'status', status: 'warning', text: 'Ready, SchedulingDisabled' });
+    const card = findSection(vm, 'g0');
+    expect(rowValue(card, 'Taints')).toBe('amd.com/gpu=present:NoSchedule, node.kubernetes.io/unschedulable:NoSchedule');
+    expect(rowValue(card, 'Status').text).toBe('Ready, SchedulingDisabled');
+    // an untainted, schedulable node: plain "Ready", no Taints row
+    const plain = nodesView(makeContext({ nodes: [makeGpuNode('g1')] }), opts);
+    expect(rowValue(findSection(plain, 'g1'), 'Taints')).toBeUndefined();
+    expect(nodeReadyCell(makeGpuNode('g1'))).toEqual({ t: 'status', status: 'success', text: 'Ready' });
+    expect(formatTaints({ spec: {} })).toBeNull();
+  });
   it('shows the loader on first load', () => {
     expect(loaders(nodesView(makeContext({ loading: true, lastUpdated: null }), opts))).toEqual(['Loading GPU node data...']);
   });
