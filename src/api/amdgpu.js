@@ -731,6 +731,7 @@ function nodeFacts(n) {
       capacity: cap,
       allocatable: getNodeGpuAllocatable(n),
       ready: isNodeReady(n),
+      cordoned: get(n, ['spec', 'unschedulable'], false) === true,
       partitionsPerGpu: pp,
       physicalGpus: cap > 0 ? Math.ceil(cap / pp) : 0,
       partitions: getNodePartitionCount(n),
@@ -795,6 +796,7 @@ export function buildClusterIndex(gpuNodes, gpuPods, prev) {
   let allocatable = 0;
   let inUse = 0;
   let readyNodes = 0;
+  let cordonedNodes = 0;
   let partitions = 0;
   let physicalGpus = 0;
   let hbmBytes = 0;
@@ -811,8 +813,11 @@ export function buildClusterIndex(gpuNodes, gpuPods, prev) {
     physicalGpus += f.physicalGpus;
     hbmBytes += f.physicalGpus * MI355X.hbmBytes;
     if (f.ready) readyNodes++;
+    if (f.cordoned) cordonedNodes++;
     nodeStats.set(name, {
       capacity: f.capacity, allocatable: f.allocatable, inUse: 0, pods: 0, ready: f.ready,
+      // New pods can land here: Ready and not cordoned.
+      schedulable: f.ready && !f.cordoned,
       physicalGpus: f.physicalGpus, partitionsPerGpu: f.partitionsPerGpu,
     });
     podsByNode.set(name, []);
@@ -836,9 +841,14 @@ export function buildClusterIndex(gpuNodes, gpuPods, prev) {
     // A partition holds its share of the board's HBM.
     hbmAllocatedBytes += (f.gpus * MI355X.hbmBytes) / st.partitionsPerGpu;
   }
+  let schedulableFree = 0;
+  nodeStats.forEach(function (st) { schedulableFree += schedulableFreeOf(st); });
   const totals = {
     nodes: gpuNodes.length,
     readyNodes: readyNodes,
+    cordonedNodes: cordonedNodes,
+    // Free GPUs a new pod can get: on Ready, uncordoned nodes only.
+    schedulableFree: schedulableFree,
     capacity: capacity,
     allocatable: allocatable,
     inUse: inUse,
@@ -878,6 +888,11 @@ export function buildClusterIndex(gpuNodes, gpuPods, prev) {
 
 function phaseBucket(phase) {
   return phase === 'Running' || phase === 'Pending' || phase === 'Succeeded' || phase === 'Failed' ? phase : 'Other';
+}
+
+/** Free GPUs of one node that a new pod could be scheduled onto (0 on a cordoned or not-Ready node). */
+function schedulableFreeOf(st) {
+  return st && st.schedulable ? Math.max(0, st.allocatable - st.inUse) : 0;
 }
 
 /**
@@ -974,7 +989,12 @@ export function patchClusterIndex(prev, delta, positionOf) {
   }
   let nodeStats = prev.nodeStats;
   const changedStats = [];
-  stats.forEach(function (st, node) { if (!sameFields(prev.nodeStats.get(node), st)) changedStats.push([node, st]); });
+  let schedulableFree = prev.totals.schedulableFree;
+  stats.forEach(function (st, node) {
+    const old = prev.nodeStats.get(node);
+    schedulableFree += schedulableFreeOf(st) - schedulableFreeOf(old);
+    if (!sameFields(old, st)) changedStats.push([node, st]);
+  });
   if (changedStats.length > 0) {
     nodeStats = new Map(prev.nodeStats);
     for (let k = 0; k < changedStats.length; k++) nodeStats.set(changedStats[k][0], changedStats[k][1]);
@@ -985,6 +1005,7 @@ export function patchClusterIndex(prev, delta, positionOf) {
     hbmAllocatedBytes: hbmAllocatedBytes,
     utilizationPct: pct(inUse, prev.totals.allocatable),
     heldGpus: heldGpus,
+    schedulableFree: schedulableFree,
   });
   return {
     podsByNode: podsByNode,

@@ -339,6 +339,7 @@ function overviewNodes(gpuNodes, t) {
     row('Total GPU Nodes', status(t.nodes > 0 ? 'success' : 'warning', t.nodes)),
     row('Ready Nodes', String(t.readyNodes)),
   ];
+  if (t.cordonedNodes > 0) nodeRows.push(row('Cordoned Nodes', status('warning', t.cordonedNodes + ' (SchedulingDisabled)')));
   if (t.nodes > 0) nodeRows.push(row('GPU Model', MI355X.product + ' (' + MI355X.arch + ')'));
   if (t.capacity > 0) {
     nodeRows.push(row('Total GPU Devices', String(t.capacity)));
@@ -365,8 +366,12 @@ function overviewAllocation(t) {
       row('Allocatable', String(t.allocatable)),
       row('In Use', String(t.inUse)),
       row('Free', status(t.free > 0 ? 'success' : 'warning', t.free)),
+    ].concat(t.cordonedNodes > 0 || t.readyNodes < t.nodes ? [
+      // Free GPUs on cordoned / not-Ready nodes take no new pods.
+      row('Free on Schedulable Nodes', status(t.schedulableFree > 0 ? 'success' : 'warning', t.schedulableFree)),
+    ] : [], [
       row('HBM Allocated', formatBytes(t.hbmAllocatedBytes)),
-    ]),
+    ])),
   ]);
 }
 

@@ -183,6 +183,8 @@ describe('store: incremental index', () => {
     for (let seed = 11; seed <= 16; seed++) {
       const r = rng(seed);
       const nodes = NODES.map((n, i) => versioned(makeGpuNode(n, { gpus: 8, partition: i === 3 ? 'CPX/NPS4' : undefined })));
+      // g1 cordoned: its free GPUs must stay out of the schedulable total through every patch
+      nodes[1].spec = Object.assign({}, nodes[1].spec, { unschedulable: true });
       nodes.push(versioned(makeNode('cpu-0')));
       let pods = initialPods(r);
       const store = createClusterStore({ request: () => Promise.resolve({ kind: 'List', items: [] }) });

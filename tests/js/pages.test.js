@@ -200,6 +200,24 @@ describe('devicePluginsView', () => {
 });
 
 // ---------------------------------------------------------------------------
+describe('overview: cordoned nodes', () => {
+  it('counts cordoned nodes and the free GPUs new pods can still get', () => {
+    const a = makeGpuNode('g0');
+    const b = makeGpuNode('g1');
+    b.spec = { unschedulable: true };
+    const ctx = makeContext({ nodes: [a, b], pods: [makeGpuPod('x', { node: 'g0', gpus: 6 })] });
+    const vm = overviewView(ctx, opts);
+    expect(rowValue(findSection(vm, 'GPU Nodes'), 'Cordoned Nodes').text).toBe('1 (SchedulingDisabled)');
+    const alloc = findSection(vm, 'GPU Allocation');
+    expect(rowValue(alloc, 'Free').text).toBe('10');
+    expect(rowValue(alloc, 'Free on Schedulable Nodes').text).toBe('2');
+    // no cordon: no extra rows
+    const plain = overviewView(makeContext({ nodes: [makeGpuNode('g0')] }), opts);
+    expect(rowValue(findSection(plain, 'GPU Allocation'), 'Free on Schedulable Nodes')).toBeUndefined();
+    expect(rowValue(findSection(plain, 'GPU Nodes'), 'Cordoned Nodes')).toBeUndefined();
+  });
+});
+
 describe('nodesView', () => {
   it('a cordoned GPU node reads "Ready, SchedulingDisabled" (warning) and its card lists the taints', () => {
     const n = makeGpuNode('g0');
