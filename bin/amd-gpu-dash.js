@@ -21,15 +21,16 @@ import https from 'https';
 import { createClusterStore } from '../src/api/clusterStore.js';
 import { createMetricsSource } from '../src/api/metrics.js';
 import { parsePrometheus, prometheusCandidates } from '../src/api/settings.js';
-import { devicePluginsView, metricsView, nodesView, overviewView, podsView } from '../src/view/pages.js';
-import { renderText } from '../src/view/text.js';
+import { devicePluginsView, metricsView, nodeDetailView, nodesView, overviewView, podDetailView, podsView } from '../src/view/pages.js';
+import { renderText, textSection } from '../src/view/text.js';
 
 const PAGES = ['overview', 'device-plugins', 'nodes', 'pods', 'metrics'];
 
 function usage(msg) {
   if (msg) process.stderr.write('amd-gpu-dash: ' + msg + '\n');
   process.stderr.write(
-    'usage: amd-gpu-dash [--url http://127.0.0.1:8001] [--page ' + PAGES.join('|') + '|all] [--watch SECONDS]\n' +
+    'usage: amd-gpu-dash [--url http://127.0.0.1:8001] [--page ' + PAGES.join('|') + '|all|node:NAME|pod:NS/NAME]\n' +
+      '                    [--watch SECONDS]\n' +
       '                    [--prometheus NAMESPACE/SERVICE:PORT] [--timeout MS] [--token TOKEN] [--insecure]\n' +
       '                    [--color] [--json]\n'
   );
@@ -65,7 +66,12 @@ export function parseArgs(argv) {
     if (v === undefined) return { error: 'missing value for ' + k };
     i++;
   }
-  if (a.page !== 'all' && PAGES.indexOf(a.page) < 0) return { error: 'unknown page ' + a.page };
+  // node:NAME / pod:NAMESPACE/NAME — the sections the plugin adds to Headlamp's native detail pages.
+  const node = /^node:(.+)$/.exec(a.page);
+  const pod = /^pod:([^/]+)\/(.+)$/.exec(a.page);
+  if (node) a.detail = { kind: 'node', name: node[1] };
+  else if (pod) a.detail = { kind: 'pod', namespace: pod[1], name: pod[2] };
+  else if (a.page !== 'all' && PAGES.indexOf(a.page) < 0) return { error: 'unknown page ' + a.page };
   if (!(a.watch >= 0) || !(a.timeout > 0)) return { error: 'bad --watch / --timeout' };
   return a;
 }
@@ -134,6 +140,49 @@ async function main() {
   // series for `all`; range series only where the Metrics page draws them.
   const VIEW = { all: 'all', nodes: 'topology', pods: 'owners', metrics: 'gauges' };
   const view = VIEW[a.page] || null;
+
+  // Detail sections: the node's (or the pod's node's) telemetry + the power
+  // history, one wave, as src/plugin.js wires the native detail pages.
+  async function showDetail(first) {
+    await Promise.all(first ? [store.refresh(), store.loadLists()] : [store.refresh()]);
+    const ctx = store.getSnapshot();
+    const d = a.detail;
+    let section = null;
+    let what = d.kind + ' ' + (d.namespace ? d.namespace + '/' : '') + d.name;
+    if (d.kind === 'node') {
+      const n = ctx.gpuNodes.filter(function (x) { return x.metadata.name === d.name; })[0];
+      if (n) {
+        const r = await Promise.all([metrics.fetchNodeMetrics(d.name), metrics.fetchNodeSeries(d.name, 1800, 30)]);
+        section = nodeDetailView(n, ctx, { metrics: r[0], series: r[1] });
+      } else what += ' (not an AMD GPU node, or not found)';
+    } else {
+      const p = ctx.gpuPods.filter(function (x) { return x.metadata.name === d.name && (x.metadata.namespace || '') === d.namespace; })[0];
+      if (p) {
+        const node = p.spec && p.spec.nodeName;
+        const r = await Promise.all([
+          node ? metrics.fetchNodeMetrics(node) : Promise.resolve(null),
+          metrics.fetchPodSeries(d.namespace, d.name, 1800, 30),
+        ]);
+        section = podDetailView(p, { metrics: r[0], series: r[1] });
+      } else what += ' (not a GPU pod, or not found)';
+    }
+    if (a.json) {
+      process.stdout.write(JSON.stringify(section) + '\n');
+      return;
+    }
+    if (a.watch > 0) process.stdout.write('\u001b[2J\u001b[H');
+    process.stdout.write(section ? textSection(section, a.color).join('\n') + '\n' : 'No AMD GPU section for ' + what + '\n');
+  }
+  if (a.detail) {
+    await showDetail(true);
+    while (a.watch > 0) {
+      await new Promise(function (r) { setTimeout(r, a.watch * 1000); });
+      await store.loadLists();
+      await showDetail(false);
+    }
+    return;
+  }
+
   async function fetchAll(first) {
     const jobs = [
       store.refresh(),

@@ -62,3 +62,17 @@ def test_overview_sends_no_prometheus_request():
         r = run("--url", srv.url, "--page", "overview")
         assert r.returncode == 0 and "Error" not in r.stdout
         assert fc.stats().get("prometheus", 0) == 0 and fc.stats()["apiserver"] >= 3
+
+
+def test_detail_sections_with_power_history(url):
+    node = run("--url", url, "--page", "node:mi355x-001")
+    assert node.returncode == 0, node.stderr
+    assert node.stdout.startswith("AMD GPU\n") and "Peak GPU Power (30 min)" in node.stdout and "xGMI topology" in node.stdout
+    pod = run("--url", url, "--page", "pod:ml/train-000-2")
+    assert pod.returncode == 0, pod.stderr
+    assert "AMD GPU Resources" in pod.stdout and "GPU Energy (30 min)" in pod.stdout and "Assigned GPUs" in pod.stdout
+    missing = run("--url", url, "--page", "node:cpu-0")
+    assert missing.returncode == 0 and "No AMD GPU section for node cpu-0" in missing.stdout
+    js = run("--url", url, "--page", "pod:ml/train-000-2", "--json")
+    assert json.loads(js.stdout)["title"] == "AMD GPU Resources"
+    assert run("--page", "pod:no-slash").returncode == 2
