@@ -1262,6 +1262,7 @@ function powerHistoryBlocks(name, label, series) {
   const byPod = {};
   byPod[name] = series.power;
   const st = clusterPowerStats(byPod);
+  if (!st) return []; // no numeric sample in the window
   return [
     kv([
       row('Peak GPU Power (' + win + ')', formatWatts(st.peakWatts)),

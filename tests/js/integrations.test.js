@@ -92,6 +92,11 @@ describe('podDetailView: GPU power history', () => {
     expect(podDetailView(makeGpuPod('train-q'), { series: { rangeSec: 1800, power: [] } }).blocks).toHaveLength(plain.blocks.length);
     expect(rowValue(plain, 'Peak GPU Power (30 min)')).toBeUndefined();
   });
+  it('a window of non-numeric samples adds nothing (and does not throw)', () => {
+    const plain = podDetailView(makeGpuPod('train-z'));
+    const s = podDetailView(makeGpuPod('train-z'), { series: { rangeSec: 1800, power: [[0, NaN], [30, null]] } });
+    expect(s.blocks).toHaveLength(plain.blocks.length);
+  });
   it('energy helpers', () => {
     expect(seriesEnergyJoules([[0, 100]])).toBe(0);
     expect(seriesEnergyJoules([[0, 100], [60, 100]])).toBe(12000);
