@@ -119,6 +119,11 @@ function num(v) {
   return isFinite(f) ? f : null;
 }
 
+/** A well-formed instant-vector row: `{metric: {...}, value: [ts, "v"]}`. */
+function isRow(row) {
+  return !!row && isObject(row.metric) && Array.isArray(row.value);
+}
+
 function emptyGpu(nodeName, gpu, instance) {
   return {
     nodeName: nodeName, gpu: gpu, instance: instance,
@@ -154,7 +159,7 @@ export function joinExporterResults(r) {
     if (!Array.isArray(list)) return;
     for (let i = 0; i < list.length; i++) {
       const row = list[i];
-      if (!row || !isObject(row.metric) || !Array.isArray(row.value)) continue;
+      if (!isRow(row)) continue;
       fn(slot(row.metric), num(row.value[1]), row.metric);
     }
   }
@@ -192,11 +197,13 @@ export function joinExporterResults(r) {
   const xr = r.__xgmi;
   if (Array.isArray(xr)) {
     for (let i = 0; i < xr.length; i++) {
-      const m = xr[i].metric || {};
-      const name = m.__name__ || '';
+      if (!isRow(xr[i])) continue;
+      const m = xr[i].metric;
+      const name = typeof m.__name__ === 'string' ? m.__name__ : '';
       const mm = /^xgmi_neighbor_(\d)_tx_throughput$/.exec(name);
       if (!mm) continue;
       const src = parseInt(m.gpu_id, 10);
+      if (!isFinite(src)) continue;
       const k = parseInt(mm[1], 10);
       const dst = k < src ? k : k + 1;
       const node = m.hostname || m.instance || '';
@@ -210,7 +217,8 @@ export function joinExporterResults(r) {
   const lr = r[E.linkHops];
   if (Array.isArray(lr)) {
     for (let i = 0; i < lr.length; i++) {
-      const m = lr[i].metric || {};
+      if (!isRow(lr[i])) continue;
+      const m = lr[i].metric;
       const node = m.hostname || m.instance || '';
       const v = num(lr[i].value[1]);
       if (v === null || m.gpu_id === undefined || m.peer_gpu_id === undefined) continue;
@@ -229,15 +237,17 @@ export function joinExporterResults(r) {
 export function joinNodeExporterResults(r) {
   const N = SERIES.nodeExporter;
   const instToNode = {};
-  const un = r[N.uname] || [];
+  const un = Array.isArray(r[N.uname]) ? r[N.uname] : [];
   for (let i = 0; i < un.length; i++) {
-    const m = un[i].metric || {};
+    if (!isRow(un[i])) continue;
+    const m = un[i].metric;
     if (m.instance) instToNode[m.instance] = m.nodename || m.node || m.instance;
   }
   const chipsByInst = {};
-  const chips = r[N.chips] || [];
+  const chips = Array.isArray(r[N.chips]) ? r[N.chips] : [];
   for (let i = 0; i < chips.length; i++) {
-    const m = chips[i].metric || {};
+    if (!isRow(chips[i])) continue;
+    const m = chips[i].metric;
     if (!m.instance || !m.chip) continue;
     if (!chipsByInst[m.instance]) chipsByInst[m.instance] = [];
     if (chipsByInst[m.instance].indexOf(m.chip) < 0) chipsByInst[m.instance].push(m.chip);
@@ -256,7 +266,8 @@ export function joinNodeExporterResults(r) {
   function each(list, keyFn, fn) {
     if (!Array.isArray(list)) return;
     for (let i = 0; i < list.length; i++) {
-      const m = list[i].metric || {};
+      if (!isRow(list[i])) continue;
+      const m = list[i].metric;
       const g = map[(m.instance || '') + '\u0000' + keyFn(m)];
       if (g) fn(g, num(list[i].value[1]));
     }
@@ -452,14 +463,16 @@ export function seriesQuery() {
 
 /** Split a combined result into `name → rows` (xGMI rows under `__xgmi`). */
 export function splitByName(result) {
-  const out = { __xgmi: [] };
+  // No prototype: a series named e.g. "__proto__" is a plain key here.
+  const out = Object.create(null);
+  out.__xgmi = [];
   const N = SERIES.nodeExporter;
   const xre = new RegExp('^' + SERIES.exporter.xgmiRe + '$');
   for (let i = 0; i < result.length; i++) {
     const row = result[i];
     const m = row && row.metric;
     if (!isObject(m)) continue;
-    const name = m.__name__ || '';
+    const name = typeof m.__name__ === 'string' ? m.__name__ : '';
     if (xre.test(name)) {
       out.__xgmi.push(row);
       continue;
@@ -862,14 +875,16 @@ export function createMetricsSource(opts) {
       '&start=' + start + '&end=' + end + '&step=' + step;
     return get('query_range', path).then(
       function (raw) {
-        const out = {};
+        const out = Object.create(null);
         const res = raw && raw.status === 'success' && raw.data && Array.isArray(raw.data.result) ? raw.data.result : [];
         for (let i = 0; i < res.length; i++) {
-          const m = res[i].metric || {};
-          const name = m.__name__ || '';
-          const node = m.hostname || m.instance || 'cluster';
-          const vals = Array.isArray(res[i].values) ? res[i].values : [];
-          if (!out[name]) out[name] = {};
+          if (!res[i] || !isObject(res[i].metric) || !Array.isArray(res[i].values)) continue;
+          const m = res[i].metric;
+          const name = typeof m.__name__ === 'string' ? m.__name__ : '';
+          const node = typeof m.hostname === 'string' && m.hostname ? m.hostname : typeof m.instance === 'string' && m.instance ? m.instance : 'cluster';
+          // Only [t, v] pairs; a malformed point is dropped, not propagated.
+          const vals = res[i].values.filter(function (p) { return Array.isArray(p) && p.length >= 2; });
+          if (!out[name]) out[name] = Object.create(null);
           out[name][node] = vals;
         }
         return out;

@@ -28,6 +28,7 @@ import {
   METRIC_VIEWS,
   nodePowerQuery,
   podPowerQuery,
+  splitByName,
 } from '../../src/api/metrics.js';
 
 import { BASE0, BASE1, exporterData, ok, prom, vec } from './promFake.js';
@@ -487,6 +488,39 @@ describe('in-flight sharing', () => {
     await src.fetchGpuMetrics();
     await src.fetchGpuMetrics();
     expect(live(request)).toBe(2);
+  });
+});
+
+describe('hostile / malformed answers', () => {
+  it('a series named "__proto__" is a plain key, not a prototype write', () => {
+    const out = splitByName([{ metric: { __name__: '__proto__', hostname: 'n0' }, value: [0, '1'] }, null, { metric: 'x' }]);
+    expect(Array.isArray(out.__proto__)).toBe(true);
+    expect(Object.getPrototypeOf(out)).toBeNull();
+    expect({}.push).toBeUndefined();
+  });
+
+  it('range answers with malformed rows and points are filtered, not thrown on', async () => {
+    const request = vi.fn((path) => {
+      if (path.indexOf('query=1') >= 0) return Promise.resolve(ok([{ metric: {}, value: [0, '1'] }]));
+      return Promise.resolve({
+        status: 'success',
+        data: {
+          resultType: 'matrix',
+          result: [
+            null,
+            { metric: null, values: [] },
+            { metric: { __name__: 'gpu_power_usage', hostname: 'n0' }, values: [[3000, '5'], 'bad', [3030]] },
+            { metric: { __name__: 'gpu_power_usage', hostname: 'n1' }, values: 'nope' },
+          ],
+        },
+      });
+    });
+    const src = createMetricsSource({ request, clock: { setTimeout, clearTimeout, now: () => 3600 * 1000 } });
+    const sr = await src.fetchSeries(1800, 30);
+    expect(Object.keys(sr.power)).toEqual(['n0']);
+    expect(sr.power.n0).toEqual([[3000, 5]]);
+    const ps = await src.fetchPodSeries('ml', 'p', 1800, 30);
+    expect(ps.power).toEqual([[3000, 5]]);
   });
 });
 

@@ -170,3 +170,90 @@ describe('properties', () => {
     }
   });
 });
+
+describe('malformed cluster objects (what a real apiserver, an old CRD version or a half-written object can hand over)', () => {
+  // Replace a random leaf or subtree of `o` with a value of the wrong shape.
+  const WRONG = [null, undefined, 0, 7, -1, '', 'x', 'NaN', true, [], {}, [null], { a: 1 }];
+  function mutate(r, o, depth) {
+    if (o === null || typeof o !== 'object' || depth > 6) return pick(r, WRONG);
+    const keys = Object.keys(o);
+    if (!keys.length) return pick(r, WRONG);
+    const out = Array.isArray(o) ? o.slice() : Object.assign({}, o);
+    const k = pick(r, keys);
+    if (r() < 0.35) {
+      if (Array.isArray(out)) out.splice(Number(k), 1);
+      else delete out[k];
+    } else out[k] = r() < 0.5 ? pick(r, WRONG) : mutate(r, o[k], depth + 1);
+    return out;
+  }
+
+  it('no page, detail section, column or index throws on them', async () => {
+    const pages = await import('../../src/view/pages.js');
+    const { createClusterStore } = await import('../../src/api/clusterStore.js');
+    const { makeGpuPod, makePlainPod, makePluginPod, makeNode, makeDeviceConfig } = await import('./fixtures.js');
+    const r = rng(4242);
+    const ROUNDS = Number(process.env.FUZZ_ROUNDS || 120);
+    const now = Date.parse('2026-10-16T00:00:00Z');
+    for (let round = 0; round < ROUNDS; round++) {
+      const nodes = [makeGpuNode('g0'), makeGpuNode('g1', { partition: 'CPX/NPS4' }), makeNode('c0')].map((n) => (r() < 0.5 ? mutate(r, n, 0) : n));
+      const pods = [makeGpuPod('a', { node: 'g0', gpus: 2 }), makeGpuPod('b', { node: 'g1' }), makePlainPod('w', 'c0'), makePluginPod('dp')]
+        .map((p) => (r() < 0.5 ? mutate(r, p, 0) : p));
+      const dcs = [makeDeviceConfig()].map((d) => (r() < 0.5 ? mutate(r, d, 0) : d));
+      const store = createClusterStore({
+        request: (path) => Promise.resolve({ kind: 'List', items: path.indexOf('deviceconfigs') >= 0 ? dcs : [] }),
+      });
+      store.setNodes(nodes, null);
+      store.setPods(pods, null);
+      await store.refresh();
+      const ctx = store.getSnapshot();
+      const opts = { now };
+      pages.overviewView(ctx, opts);
+      pages.devicePluginsView(ctx, opts);
+      pages.nodesView(ctx, opts);
+      pages.podsView(ctx, opts);
+      pages.metricsView(ctx, { metrics: null, fetchError: null, fetching: false }, opts);
+      nodes.forEach((n) => pages.nodeDetailView(n, ctx, opts));
+      pods.forEach((p) => pages.podDetailView(p, opts));
+      const cols = pages.nodeColumns();
+      nodes.forEach((n) => cols.forEach((c) => c.getter(n)));
+      pages.clearViewMemo();
+    }
+  });
+});
+
+describe('malformed Prometheus answers', () => {
+  it('joins and telemetry views never throw on wrong-shaped rows', async () => {
+    const pages = await import('../../src/view/pages.js');
+    const { joinExporterResults, joinNodeExporterResults, splitByName, summarizeMetrics, clusterPowerStats } = await import('../../src/api/metrics.js');
+    const { exporterData, flatten } = await import('./promFake.js');
+    const { makeContext, makeGpuNode, makeGpuPod } = await import('./fixtures.js');
+    const r = rng(77);
+    const WRONG = [null, undefined, 0, '', 'NaN', '+Inf', '-1', [], {}, [1], { x: 1 }, 'abc'];
+    const ctx = makeContext({ nodes: [makeGpuNode('n0'), makeGpuNode('n1')], pods: [makeGpuPod('train-0', { node: 'n0' })] });
+    for (let round = 0; round < 200; round++) {
+      const rows = flatten(exporterData(['n0', 'n1'])).map((row) => {
+        if (r() > 0.15) return row;
+        const k = pick(r, ['metric', 'value', 'metric.gpu_id', 'metric.hostname', 'value.1', 'metric.__name__']);
+        const out = JSON.parse(JSON.stringify(row));
+        const path = k.split('.');
+        let o = out;
+        for (let i = 0; i < path.length - 1; i++) o = o[path[i]];
+        o[path[path.length - 1]] = pick(r, WRONG);
+        return out;
+      });
+      if (r() < 0.1) rows.push(pick(r, WRONG));
+      const split = splitByName(rows.filter((x) => x && typeof x === 'object'));
+      const m = Object.assign({ source: 'amd-exporter', fetchedAt: new Date(0).toISOString(), prometheusPath: '/p' }, joinExporterResults(split));
+      joinNodeExporterResults(split);
+      summarizeMetrics(m);
+      const power = { n0: [[0, pick(r, [1, NaN, null])], [30, 2]] };
+      clusterPowerStats(power);
+      pages.metricsView(ctx, { metrics: m, series: { power, vram: {} }, fetchError: null, fetching: false }, { now: 0 });
+      pages.nodesView(ctx, { metrics: m, now: 0 });
+      pages.podsView(ctx, { metrics: m, now: 0 });
+      pages.nodeDetailView(ctx.gpuNodes[0], ctx, { metrics: m, series: { power: power.n0 } });
+      pages.podDetailView(ctx.gpuPods[0], { metrics: m, series: { power: power.n0 } });
+      pages.clearViewMemo();
+    }
+  });
+});
