@@ -345,3 +345,44 @@ def test_sysfs_only_on_the_box_matches_the_hip_scrape(exe):
     # Power / temperature of the visible GPU come from the same hwmon files.
     assert [v for n, l, v in sysfs if n == "gpu_junction_temperature" and l["pci_bus"] == hip_bus]
     print("sysfs-only GPUs:", len(models), "link series:", sum(1 for n, _, _ in sysfs if n == "gpu_xgmi_link_hops"))
+
+
+def test_garbage_requests_do_not_break_the_daemon(exe):
+    """Random bytes, truncated request lines, huge headers, pipelined junk: each gets a 4xx or a close, and the
+    daemon keeps serving."""
+    import random
+    import socket
+
+    p, port = _start(exe, "fuzz")
+    rnd = random.Random(7)
+    payloads = [b"", b"\r\n\r\n", b"GET\r\n\r\n", b"GET / HTTP/1.1", b"POST /metrics HTTP/1.1\r\n\r\n",
+                b"GET /" + b"a" * 20000 + b" HTTP/1.1\r\n\r\n", b"\x00\xff" * 100 + b"\r\n\r\n",
+                b"GET /healthz HTTP/1.1\r\n\r\nGET /metrics HTTP/1.1\r\n\r\n"]
+    payloads += [bytes(rnd.getrandbits(8) for _ in range(rnd.randint(1, 3000))) for _ in range(40)]
+    try:
+        for data in payloads:
+            with socket.create_connection(("127.0.0.1", port), timeout=5) as s:
+                try:
+                    s.sendall(data)
+                    s.shutdown(socket.SHUT_WR)
+                    s.recv(65536)
+                except OSError:
+                    pass
+        with urllib.request.urlopen(f"http://127.0.0.1:{port}/healthz", timeout=5) as r:
+            assert r.read() == b"ok\n"
+        assert p.poll() is None
+    finally:
+        p.send_signal(signal.SIGTERM)
+        assert p.wait(15) == 0
+
+
+def test_http_serving_is_clean_under_asan_and_ubsan(tmp_path):
+    """Host-code AddressSanitizer + UBSan build of the daemon (tools/asan_exporter.py): fuzzed requests, slow
+    peers, scrapes and shutdown produce no report and no leak."""
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import asan_exporter
+
+    ok, rc, err = asan_exporter.drive(asan_exporter.build(str(tmp_path)))
+    assert ok, (rc, err[-3000:])
