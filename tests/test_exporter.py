@@ -376,13 +376,33 @@ def test_garbage_requests_do_not_break_the_daemon(exe):
         assert p.wait(15) == 0
 
 
-def test_http_serving_is_clean_under_asan_and_ubsan(tmp_path):
-    """Host-code AddressSanitizer + UBSan build of the daemon (tools/asan_exporter.py): fuzzed requests, slow
-    peers, scrapes and shutdown produce no report and no leak."""
+@pytest.fixture(scope="module")
+def asan(tmp_path_factory):
     import sys
 
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
     import asan_exporter
 
-    ok, rc, err = asan_exporter.drive(asan_exporter.build(str(tmp_path)))
+    return asan_exporter, asan_exporter.build(str(tmp_path_factory.mktemp("asan")))
+
+
+def test_http_serving_is_clean_under_asan_and_ubsan(asan):
+    """Host-code AddressSanitizer + UBSan build of the daemon (tools/asan_exporter.py): fuzzed requests, slow
+    peers, scrapes and shutdown produce no report and no leak."""
+    mod, exe = asan
+    ok, rc, err = mod.drive(exe)
     assert ok, (rc, err[-3000:])
+
+
+def test_sysfs_and_kfd_parsing_is_clean_under_asan_and_ubsan(asan, tmp_path):
+    """The probe's sysfs / KFD readers (probe_core.h) under the sanitizers, on the captured host's trees: the
+    1-GPU-container KFD view and a fully readable 8-GPU one."""
+    _, exe = asan
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1", UBSAN_OPTIONS="halt_on_error=1")
+    captured = _kfd_nodes(os.path.join(FIX, "kfd_topology.txt"))
+    for name, nodes in (("one", captured), ("none", [])):
+        root = _sysfs_tree(tmp_path / name, nodes)
+        r = subprocess.run([exe, "--once", "--sysfs-only", "--hostname", "n0"], capture_output=True, text=True,
+                           timeout=120, env=dict(env, AMDGPU_EXPORTER_SYSFS_ROOT=str(root)))
+        assert r.returncode == 0 and "runtime error" not in r.stderr and "Sanitizer" not in r.stderr, r.stderr[-3000:]
+        assert "gpu_power_usage" in r.stdout
