@@ -7,4 +7,4 @@ import { plugin } from '../headlamp';
 
 export const { AmdGpuDataProvider, useAmdGpuContext } = plugin;
 export const { useGpuMetrics, useNodeGpuMetrics, useGpuOwners, storeFor, metricsSourceFor } = plugin.core;
-export { STALE_MS, PROMETHEUS_UNREACHABLE } from './providerCore.js';
+export { STALE_MS, PROMETHEUS_UNREACHABLE, PROMETHEUS_FORBIDDEN } from './providerCore.js';

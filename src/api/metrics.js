@@ -570,9 +570,20 @@ export function createMetricsSource(opts) {
   let lastBy = {}; // view → previous snapshot, for structural sharing and stale fallbacks
   const failuresBy = {}; // view → consecutive failed fetches against the cached service
 
+  // HTTP status of the most recent failed request (401 / 403: the user may not
+  // proxy to the Prometheus service — RBAC, not an outage); 0 after a success.
+  let lastFailureStatus = 0;
+
   function get(name, path) {
     const start = clock.now();
-    const p = withTimeout(request(path), timeoutMs, clock);
+    const p = withTimeout(request(path), timeoutMs, clock).then(
+      function (v) { lastFailureStatus = 0; return v; },
+      function (e) {
+        const st = e && (e.status || (e.response && e.response.status));
+        lastFailureStatus = typeof st === 'number' ? st : -1;
+        throw e;
+      }
+    );
     if (!onTrace) return p;
     return p.then(
       function (v) { onTrace({ name: name, path: path, start: start, end: clock.now(), ok: true }); return v; },
@@ -988,6 +999,12 @@ export function createMetricsSource(opts) {
   return {
     discover: discover,
     invalidate: invalidate,
+    /**
+     * Why the last fetch found no Prometheus: 'forbidden' when the proxy
+     * answered 401 / 403 (the user lacks `services/proxy` get on the
+     * Prometheus service), else 'unreachable'.
+     */
+    failureReason: function () { return lastFailureStatus === 401 || lastFailureStatus === 403 ? 'forbidden' : 'unreachable'; },
     fetchGpuMetrics: fetchGpuMetrics,
     fetchPodSeries: fetchPodSeries,
     fetchNodeSeries: fetchNodeSeries,

@@ -4,6 +4,7 @@ import type { AmdGpuContextValue, GpuMetrics, GpuMetricsState } from './types';
 
 export const STALE_MS: number;
 export const PROMETHEUS_UNREACHABLE: string;
+export const PROMETHEUS_FORBIDDEN: string;
 export const OUTSIDE_PROVIDER: string;
 
 export interface HeadlampLibLike {
@@ -39,6 +40,7 @@ export interface MetricsSource {
   fetchGpuMetrics(view?: 'all' | 'gauges' | 'topology'): Promise<GpuMetrics | null>;
   fetchNodeMetrics(nodeName: string): Promise<GpuMetrics | null>;
   fetchGpuOwners(): Promise<GpuMetrics | null>;
+  failureReason(): 'forbidden' | 'unreachable';
   fetchPodSeries(namespace: string, pod: string, rangeSec: number, stepSec: number): Promise<{ rangeSec: number; power: Array<[number, number]> } | null>;
   fetchNodeSeries(nodeName: string, rangeSec: number, stepSec: number): Promise<{ rangeSec: number; power: Array<[number, number]> } | null>;
   fetchSeries(rangeSec: number, stepSec: number): Promise<GpuMetricsState['series']>;

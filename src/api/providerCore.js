@@ -35,6 +35,9 @@ export const STALE_MS = 5000;
 export const PROMETHEUS_UNREACHABLE =
   'Could not reach Prometheus. Ensure kube-prometheus-stack is installed in the monitoring namespace.';
 
+export const PROMETHEUS_FORBIDDEN =
+  'Access to Prometheus was denied (HTTP 403): your user needs "get" on services/proxy for the Prometheus service in the monitoring namespace (deploy/rbac/headlamp-amd-gpu-viewer.yaml).';
+
 export const OUTSIDE_PROVIDER = 'useAmdGpuContext must be used within an AmdGpuDataProvider';
 
 const HOOKS = ['createContext', 'createElement', 'useContext', 'useEffect', 'useMemo', 'useState', 'useSyncExternalStore'];
@@ -178,8 +181,9 @@ export function createProviderCore(React, lib, deps) {
    * @param {string|null} key
    * @param {() => Promise<[any, any]>} fetchPair  resolves [metrics, series]
    * @param {boolean} [seriesOnly]  the fetch returns series only: unreachable = no series
+   * @param {{failureReason?: () => string}} [source]  says whether a failure was RBAC (403) or an outage
    */
-  function useMetricsFetch(key, fetchPair, seriesOnly) {
+  function useMetricsFetch(key, fetchPair, seriesOnly, source) {
     const refreshIntervalSec = loadSettings().refreshIntervalSec;
     const st = useState(IDLE);
     const state = st[0];
@@ -197,7 +201,11 @@ export function createProviderCore(React, lib, deps) {
           if (cancelled) return;
           const metrics = pair[0];
           const reached = seriesOnly ? !!pair[1] : !!metrics;
-          setState({ metrics: metrics, series: pair[1], fetching: false, fetchError: reached ? null : PROMETHEUS_UNREACHABLE });
+          const why = !reached && source && source.failureReason ? source.failureReason() : 'unreachable';
+          setState({
+            metrics: metrics, series: pair[1], fetching: false,
+            fetchError: reached ? null : why === 'forbidden' ? PROMETHEUS_FORBIDDEN : PROMETHEUS_UNREACHABLE,
+          });
         },
         function (e) {
           if (cancelled) return;
@@ -241,7 +249,7 @@ export function createProviderCore(React, lib, deps) {
         source.fetchGpuMetrics(v),
         series ? source.fetchSeries(settings.seriesMinutes * 60, seriesStepSec(settings)) : Promise.resolve(null),
       ]);
-    });
+    }, false, source);
   }
 
   /**
@@ -257,7 +265,7 @@ export function createProviderCore(React, lib, deps) {
     const active = (enabled === undefined ? true : enabled) && !!nodeName;
     return useMetricsFetch(active ? 'node|' + sourceKey(cluster, loadSettings()) + '|' + nodeName : null, function () {
       return source.fetchNodeMetrics(nodeName).then(function (m) { return [m, null]; });
-    });
+    }, false, source);
   }
 
   /**
@@ -297,7 +305,7 @@ export function createProviderCore(React, lib, deps) {
     const on = enabled === undefined ? true : enabled;
     return useMetricsFetch(on ? 'owners|' + sourceKey(cluster, loadSettings()) : null, function () {
       return source.fetchGpuOwners().then(function (m) { return [m, null]; });
-    });
+    }, false, source);
   }
 
   return {

@@ -988,8 +988,10 @@ export function metricsView(ctx, mstate, opts) {
   if (mstate.fetching && !m) items.push(loader('Querying Prometheus for GPU metrics...'));
 
   if (mstate.fetchError) {
+    // RBAC (HTTP 403 from the service proxy) is not an outage: say which permission is missing.
+    const denied = /denied \(HTTP 403\)/.test(String(mstate.fetchError));
     items.push(
-      section('Prometheus Unreachable', [
+      section(denied ? 'Prometheus Access Denied' : 'Prometheus Unreachable', [
         kv([
           row('Error', status('error', mstate.fetchError)),
           row(

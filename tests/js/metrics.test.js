@@ -524,6 +524,24 @@ describe('hostile / malformed answers', () => {
   });
 });
 
+describe('failureReason (RBAC vs outage)', () => {
+  it('"forbidden" when the service proxy answers 403, "unreachable" on 503, cleared by a success', async () => {
+    let mode = 403;
+    const request = vi.fn(() => (mode === 200
+      ? Promise.resolve(ok([{ metric: {}, value: [0, '1'] }]))
+      : Promise.reject(Object.assign(new Error('HTTP ' + mode), { status: mode }))));
+    const src = createMetricsSource({ request });
+    expect(await src.fetchGpuMetrics('gauges')).toBeNull();
+    expect(src.failureReason()).toBe('forbidden');
+    mode = 503;
+    expect(await src.fetchGpuMetrics('gauges')).toBeNull();
+    expect(src.failureReason()).toBe('unreachable');
+    mode = 200;
+    await src.discover();
+    expect(src.failureReason()).toBe('unreachable'); // no failure pending: the default wording
+  });
+});
+
 describe('fetchPodSeries (Pod detail power history)', () => {
   it('asks for one pod\'s power, summed per step, with escaped matchers', () => {
     expect(podPowerQuery('ml', 'train-0')).toBe('sum by (__name__) ({__name__="gpu_power_usage", namespace="ml", pod="train-0"})');

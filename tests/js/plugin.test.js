@@ -435,3 +435,22 @@ describe('Pod detail: power history next to the node telemetry', () => {
     r.unmount();
   });
 });
+
+describe('Metrics page without RBAC for the Prometheus proxy', () => {
+  it('says access was denied and which permission is missing, not "unreachable"', async () => {
+    cluster();
+    const crd = lib.api.handler;
+    lib.api.handler = (p) => (p.indexOf('/proxy/api/v1/') >= 0
+      ? Promise.reject(Object.assign(new Error('services "kube-prometheus-stack-prometheus" is forbidden'), { status: 403 }))
+      : crd(p));
+    // A fresh plugin: the shared one's metrics client still holds earlier specs' snapshots (served stale on failure).
+    const fresh = createPlugin({ React, lib, CommonComponents: CC });
+    const r = render(h(fresh.AmdGpuDataProvider, null, h(fresh.MetricsPage)));
+    await r.settle();
+    const titles = r.instances(CC.SectionBox).map((i) => i.props.title);
+    expect(titles).toContain('Prometheus Access Denied');
+    expect(titles).not.toContain('Prometheus Unreachable');
+    expect(r.html()).toContain('services/proxy');
+    r.unmount();
+  });
+});
