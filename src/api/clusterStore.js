@@ -128,6 +128,7 @@ export function withTimeout(promise, ms, clock) {
  * @property {any[]} gpuPods
  * @property {any[]} pluginPods
  * @property {boolean} crdAvailable
+ * @property {boolean} crdForbidden  the DeviceConfig list was refused (401 / 403) rather than absent (404)
  * @property {boolean} loading      true until the node and pod lists have settled (arrived or
  *                                  failed) and the first CRD/pod fetch is in
  * @property {'unknown'|'pending'|'ready'|'error'} nodesState
@@ -161,6 +162,7 @@ export function createClusterStore(opts) {
     podError: null,
     deviceConfigs: [],
     crdAvailable: false,
+    crdForbidden: false, // the CRD list answered 401 / 403: RBAC, not a missing operator
     pluginPods: [], // from the plugin-pod queries (used when the pod list is not available)
     // Where each list stands: 'unknown' (never fed: harness/tests),
     // 'pending' (a list/watch is in flight), 'ready', or 'error'. An errored
@@ -267,6 +269,7 @@ export function createClusterStore(opts) {
       gpuPods: p,
       pluginPods: pp,
       crdAvailable: s.crdAvailable,
+      crdForbidden: s.crdForbidden,
       loading: !s.asyncLoaded || !settled(s.nodesState) || !settled(s.podsState),
       nodesState: s.nodesState,
       podsState: s.podsState,
@@ -341,7 +344,8 @@ export function createClusterStore(opts) {
         // A missing or forbidden CRD degrades silently (reference ADR 003).
         // A timeout or server error says nothing about the CRD: keep the last
         // known state instead of flapping to "CRD Not Available".
-        return { ok: isAbsent(e) ? false : null, items: [] };
+        const st = e && (e.status || (e.response && e.response.status));
+        return { ok: isAbsent(e) ? false : null, items: [], forbidden: st === 403 || st === 401 };
       }
     );
     const needPods = s.podsState === 'unknown' || s.podsState === 'error';
@@ -354,6 +358,7 @@ export function createClusterStore(opts) {
         const c = results[0];
         if (c.ok !== null || !s.asyncLoaded) {
           s.crdAvailable = c.ok === true;
+          s.crdForbidden = !!c.forbidden;
           // Structural sharing: an unchanged list keeps its identity, so every
           // memoised view (and React.memo'd section) downstream is reused.
           s.deviceConfigs = sameObjects(s.deviceConfigs, c.items) ? s.deviceConfigs : c.items;

@@ -221,6 +221,8 @@ export interface ClusterSnapshot {
   gpuPods: AmdGpuPod[];
   pluginPods: AmdGpuPod[];
   crdAvailable: boolean;
+  /** The DeviceConfig list was refused (401 / 403) rather than absent (404). */
+  crdForbidden: boolean;
   /** true until the node and pod lists settled (arrived or failed) and the first CRD fetch is in */
   loading: boolean;
   nodesState: ListState;

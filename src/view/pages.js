@@ -256,7 +256,9 @@ function overviewItems(ctx, now) {
     items.push(
       section('Notice', [
         kv([
-          row('CRD Status', status('warning', 'DeviceConfig CRD not found — limited visibility available')),
+          row('CRD Status', status('warning', ctx.crdForbidden
+            ? 'DeviceConfig list forbidden for this user (HTTP 403) — limited visibility available'
+            : 'DeviceConfig CRD not found — limited visibility available')),
           row(
             'Note',
             'Device plugin pods detected via DaemonSet labels. Install the AMD GPU Operator for DeviceConfig-based management.'
@@ -431,13 +433,19 @@ function devicePluginsItems(ctx, now) {
   if (!ctx.crdAvailable) {
     items.push(
       section('CRD Not Available', [
-        kv([
-          row('Status', status('warning', 'DeviceConfig CRD (amd.com/v1alpha1) is not installed')),
-          row(
-            'Note',
-            'Install the AMD GPU Operator to manage DeviceConfig resources. Device plugin daemon pods are shown below if detected.'
-          ),
-        ]),
+        kv(ctx.crdForbidden
+          ? [
+            // 403: the operator may well be installed; this user cannot list its CRs.
+            row('Status', status('warning', 'DeviceConfig list forbidden for this user (HTTP 403)')),
+            row('Note', 'Grant list on deviceconfigs.amd.com (deploy/rbac/headlamp-amd-gpu-viewer.yaml). Device plugin daemon pods are shown below if detected.'),
+          ]
+          : [
+            row('Status', status('warning', 'DeviceConfig CRD (amd.com/v1alpha1) is not installed')),
+            row(
+              'Note',
+              'Install the AMD GPU Operator to manage DeviceConfig resources. Device plugin daemon pods are shown below if detected.'
+            ),
+          ]),
       ])
     );
   }

@@ -448,3 +448,20 @@ describe('getSharedStore', () => {
     resetSharedStores();
   });
 });
+
+describe('CRD refused vs absent', () => {
+  it('a 403 on the DeviceConfig list sets crdForbidden; a 404 does not', async () => {
+    for (const [st, forbidden] of [[403, true], [404, false]]) {
+      const store = createClusterStore({
+        request: () => Promise.reject(Object.assign(new Error('HTTP ' + st), { status: st })),
+      });
+      store.setNodes([], null);
+      store.setPods([], null);
+      await store.refresh();
+      const snap = store.getSnapshot();
+      expect(snap.crdAvailable).toBe(false);
+      expect(snap.crdForbidden).toBe(forbidden);
+      expect(snap.error).toBeNull();
+    }
+  });
+});

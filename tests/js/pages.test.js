@@ -155,6 +155,14 @@ describe('overviewView', () => {
 
 // ---------------------------------------------------------------------------
 describe('devicePluginsView', () => {
+  it('a forbidden DeviceConfig list says which permission is missing, not "not installed"', () => {
+    const vm = devicePluginsView(makeContext({ crdAvailable: false, crdForbidden: true }), opts);
+    const s = findSection(vm, 'CRD Not Available');
+    expect(rowValue(s, 'Status').text).toBe('DeviceConfig list forbidden for this user (HTTP 403)');
+    expect(rowValue(s, 'Note')).toContain('deviceconfigs.amd.com');
+    const absent = findSection(devicePluginsView(makeContext({ crdAvailable: false }), opts), 'CRD Not Available');
+    expect(rowValue(absent, 'Status').text).toContain('not installed');
+  });
   it('shows the loader on first load', () => {
     expect(loaders(devicePluginsView(makeContext({ loading: true, lastUpdated: null }), opts))).toEqual(['Loading device plugin data...']);
   });
