@@ -858,7 +858,7 @@ function podsItems(ctx, now, assign) {
     // With exporter pod labels, show which physical GPUs each pod holds.
     const exact = assign && Object.keys(assign).length > 0;
     const cols = ['Name', 'Namespace', 'Node', 'Phase', 'GPU Resources', 'Restarts', 'Age'];
-    if (exact) cols.splice(5, 0, 'Assigned GPUs');
+    if (exact) cols.splice(5, 0, 'Assigned GPUs', 'GPU Power');
     items.push(
       section('All GPU Pods', [
         table(
@@ -872,7 +872,7 @@ function podsItems(ctx, now, assign) {
                 podName(p), podNs(p), podNode(p), status(phaseToStatus(phase), phase), gpuContainerLines(p),
                 restartsCell(p), ageText(p.metadata.creationTimestamp, now),
               ];
-              if (exact) r.splice(5, 0, assignedText(gs));
+              if (exact) r.splice(5, 0, assignedText(gs), podPowerText(gs));
               return r;
             }, now);
           }, now),
@@ -905,6 +905,20 @@ function podsItems(ctx, now, assign) {
 // ---------------------------------------------------------------------------
 // Metrics (reference MetricsPage.tsx:191-355)
 // ---------------------------------------------------------------------------
+
+/** Live power of the GPUs a pod holds (exporter pod labels), summed; "—" without a reading. */
+export function podPowerText(gs) {
+  if (!gs || !gs.length) return '—';
+  let w = 0;
+  let any = false;
+  for (let i = 0; i < gs.length; i++) {
+    if (typeof gs[i].powerWatts === 'number' && isFinite(gs[i].powerWatts)) {
+      w += gs[i].powerWatts;
+      any = true;
+    }
+  }
+  return any ? formatWatts(w) : '—';
+}
 
 /** Mean value per node of a series map (node → [[t, v]]); nodes without samples are left out. */
 export function seriesMeans(byNode) {

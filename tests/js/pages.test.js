@@ -403,6 +403,11 @@ describe('pod → GPU assignment (exporter pod labels)', () => {
     const trainRow = t.rows.find((r) => r[0] === 'train');
     expect(trainRow[col]).toBe('g0: GPU 0, 1');
     expect(t.rows.find((r) => r[0] === 'idle')[col]).toBe('—');
+    // GPU Power: the held GPUs' live power, summed (1000 W + 1001 W)
+    const pw = t.columns.indexOf('GPU Power');
+    expect(pw).toBe(col + 1);
+    expect(trainRow[pw]).toBe('2001.0 W');
+    expect(t.rows.find((r) => r[0] === 'idle')[pw]).toBe('—');
   });
   it('keeps the reference columns without exporter data', () => {
     const t = firstTable(findSection(podsView(ctx, { now: NOW }), 'All GPU Pods'));
