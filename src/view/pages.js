@@ -602,8 +602,12 @@ export function nodesView(ctx, opts) {
   const now = nowOf(opts);
   const metrics = opts && opts.metrics ? opts.metrics : null;
   if (ctx.loading) return page(null, null, [loader('Loading GPU node data...')]);
-  const head = memo('nodes-head', [ctx.gpuNodes, ctx.index, ctx.error], function () {
-    return nodesHeadItems(ctx, now);
+  // Live node power (the GPU Nodes query carries the power gauge for pod
+  // attribution anyway): "watts|cap" per node, whole watts, so the head and
+  // its rows rebuild only when a shown value changes.
+  const power = nodePowerKeys(metrics);
+  const head = memo('nodes-head', [ctx.gpuNodes, ctx.index, ctx.error, power.sig], function () {
+    return nodesHeadItems(ctx, now, power.byNode);
   }, now);
   const owners = ownersByNode(metrics);
   const xgmi = metrics ? metrics.xgmi : undefined;
@@ -744,7 +748,33 @@ function assignedText(gs) {
   return order.map(function (n) { return n + ': GPU ' + byNode[n].join(', '); }).join('; ');
 }
 
-function nodesHeadItems(ctx, now) {
+/** Per-node GPU power from a telemetry snapshot: {byNode: {node: "watts|cap"}, sig} (whole watts). */
+export function nodePowerKeys(metrics) {
+  const sum = {};
+  const gs = metrics && Array.isArray(metrics.gpus) ? metrics.gpus : [];
+  for (let i = 0; i < gs.length; i++) {
+    const g = gs[i];
+    if (typeof g.powerWatts !== 'number' || !isFinite(g.powerWatts)) continue;
+    const e = sum[g.nodeName] || (sum[g.nodeName] = [0, 0]);
+    e[0] += g.powerWatts;
+    e[1] += typeof g.powerCapWatts === 'number' && isFinite(g.powerCapWatts) ? g.powerCapWatts : 0;
+  }
+  const byNode = {};
+  const names = Object.keys(sum).sort();
+  for (let i = 0; i < names.length; i++) byNode[names[i]] = Math.round(sum[names[i]][0]) + '|' + Math.round(sum[names[i]][1]);
+  return { byNode: byNode, sig: names.map(function (n) { return n + '=' + byNode[n]; }).join(',') };
+}
+
+function nodePowerCell(key) {
+  if (!key) return '—';
+  const parts = key.split('|');
+  const cap = Number(parts[1]);
+  return powerBar(Number(parts[0]), cap > 0 ? cap : null);
+}
+
+function nodesHeadItems(ctx, now, powerByNode) {
+  const pw = powerByNode || {};
+  const withPower = Object.keys(pw).length > 0;
   const items = [];
   if (ctx.error) items.push(errorSection(ctx.error));
 
@@ -768,11 +798,13 @@ function nodesHeadItems(ctx, now) {
     items.push(
       section('GPU Node Summary', [
         table(
-          ['Node', 'Ready', 'GPU Model', 'GPU Devices', 'Allocation', 'GPU Pods', 'Age'],
-          chunkedRows('node-summary-rows', ctx.gpuNodes, [], function (n) {
+          // "Power" (beyond the reference): the node's GPUs' live power against their summed cap.
+          ['Node', 'Ready', 'GPU Model', 'GPU Devices', 'Allocation', 'GPU Pods'].concat(withPower ? ['Power'] : [], ['Age']),
+          chunkedRows('node-summary-rows', ctx.gpuNodes, [withPower], function (n) {
             const st = idx.nodeStats.get(n.metadata.name);
+            const pk = pw[n.metadata.name];
             // Per-node stats keep their identity while unchanged (buildClusterIndex).
-            return nodeSummaryRows(n, [st], function () {
+            return nodeSummaryRows(n, [st, withPower, pk], function () {
               const count = getNodeGpuCount(n);
               return [
                 n.metadata.name,
@@ -781,10 +813,9 @@ function nodesHeadItems(ctx, now) {
                 count > 0 ? String(count) : '—',
                 allocationBar(st ? st.inUse : 0, (st && st.allocatable) || count),
                 String(st ? st.pods : 0),
-                ageText(n.metadata.creationTimestamp, now),
-              ];
+              ].concat(withPower ? [nodePowerCell(pk)] : [], [ageText(n.metadata.creationTimestamp, now)]);
             }, now);
-          }, now, function (n) { return [idx.nodeStats.get(n.metadata.name)]; }),
+          }, now, function (n) { return [idx.nodeStats.get(n.metadata.name), withPower, pw[n.metadata.name]]; }),
           ctx.gpuNodes.map(function (n) { return n.metadata.uid || n.metadata.name; })
         ),
       ])

@@ -22,6 +22,7 @@ import {
   ACTIVE_PODS_LIMIT,
   formatTaints,
   nodeReadyCell,
+  nodePowerKeys,
 } from '../../src/view/pages.js';
 import { countRows, findSection, firstBlock, firstTable, loaders, rowNames, rowValue, sectionTitles, text } from '../../src/view/ir.js';
 import { renderPage, textContent } from '../../src/view/html.js';
@@ -223,6 +224,22 @@ describe('overview: cordoned nodes', () => {
     const plain = overviewView(makeContext({ nodes: [makeGpuNode('g0')] }), opts);
     expect(rowValue(findSection(plain, 'GPU Allocation'), 'Free on Schedulable Nodes')).toBeUndefined();
     expect(rowValue(findSection(plain, 'GPU Nodes'), 'Cordoned Nodes')).toBeUndefined();
+  });
+});
+
+describe('nodesView: live node power', () => {
+  it('adds a Power column (GPUs summed against their caps) when telemetry is there, whole watts', () => {
+    const ctx = makeContext({ nodes: [makeGpuNode('g0'), makeGpuNode('g1')] });
+    const g = (node, i, w) => ({ nodeName: node, gpu: String(i), powerWatts: w, powerCapWatts: 1400 });
+    const metrics = { source: 'amd-exporter', gpus: [g('g0', 0, 700.4), g('g0', 1, 699.8), g('g1', 0, NaN)], xgmi: {}, links: {} };
+    const t = firstTable(findSection(nodesView(ctx, { now: NOW, metrics }), 'GPU Node Summary'));
+    const col = t.columns.indexOf('Power');
+    expect(col).toBe(t.columns.length - 2); // before Age
+    expect(t.rows[0][col].text).toBe('1400.0 W / 2800.0 W (50%)');
+    expect(t.rows[1][col]).toBe('—');
+    expect(nodePowerKeys(metrics).byNode).toEqual({ g0: '1400|2800' });
+    const plain = firstTable(findSection(nodesView(ctx, { now: NOW }), 'GPU Node Summary'));
+    expect(plain.columns).not.toContain('Power');
   });
 });
 
