@@ -309,6 +309,20 @@ describe('harness React enforces the rules real React enforces', () => {
     expect(String(err)).toContain('order of Hooks');
   });
 
+  it('a state update of one component during another\'s render is rejected', () => {
+    let setA = null;
+    function A() {
+      const s = React.useState(0);
+      setA = s[1];
+      return h('i', null, String(s[0]));
+    }
+    function B() {
+      setA(1); // side effect in render
+      return h('b', null, 'x');
+    }
+    expect(() => render(h('div', null, h(A), h(B)))).toThrow('while rendering');
+  });
+
   it('a hook skipped on re-render is rejected', async () => {
     let setFlag = null;
     function Cond() {

@@ -109,6 +109,10 @@ export function useReducer(reducer, initialArg, init) {
     const s = { state: init ? init(initialArg) : initialArg, dispatch: null };
     s.dispatch = function (action) {
       if (inst.unmounted) return;
+      // React: "Cannot update a component while rendering a different component".
+      if (current && current !== inst) {
+        throw new Error('Cannot update ' + typeName(inst.type) + ' while rendering ' + typeName(current.type));
+      }
       const next = s.reducer(s.state, action);
       if (Object.is(next, s.state)) return;
       s.state = next;
