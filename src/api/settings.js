@@ -120,20 +120,28 @@ export function saveSettings(value, storage) {
 /**
  * Interval poller with an injectable clock. `start(fn)` calls fn every
  * `periodSec` seconds, skipping a tick while the previous call's promise is
- * still pending (no overlapping refreshes). Period 0 → never.
+ * still pending (no overlapping refreshes), and while the browser tab is
+ * hidden (an auto-refreshing dashboard left in a background tab would keep
+ * querying the apiserver and Prometheus for nobody). Period 0 → never.
  */
 export function createPoller(periodSec, clock) {
   const c = clock || { setInterval: setInterval, clearInterval: clearInterval };
+  const hidden = typeof c.hidden === 'function' ? c.hidden : documentHidden;
   let handle = null;
   let busy = false;
   let ticks = 0;
   let skipped = 0;
+  let hiddenSkips = 0;
   return {
     start: function (fn) {
       if (handle !== null || !(periodSec > 0)) return;
       handle = c.setInterval(function () {
         if (busy) {
           skipped++;
+          return;
+        }
+        if (hidden()) {
+          hiddenSkips++;
           return;
         }
         busy = true;
@@ -150,6 +158,13 @@ export function createPoller(periodSec, clock) {
       if (handle !== null) c.clearInterval(handle);
       handle = null;
     },
-    stats: function () { return { ticks: ticks, skipped: skipped, running: handle !== null }; },
+    stats: function () {
+      return { ticks: ticks, skipped: skipped, hiddenSkips: hiddenSkips, running: handle !== null };
+    },
   };
+}
+
+/** True in a browser tab that is not visible; false outside a browser (the terminal dashboard). */
+function documentHidden() {
+  return typeof document !== 'undefined' && !!document && document.visibilityState === 'hidden';
 }

@@ -124,6 +124,45 @@ describe('createPoller', () => {
     p.stop();
     vi.useRealTimers();
   });
+  it('skips ticks while the tab is hidden and resumes when it is shown', async () => {
+    vi.useFakeTimers();
+    let hidden = false;
+    const fn = vi.fn(() => Promise.resolve());
+    const p = createPoller(10, { setInterval, clearInterval, hidden: () => hidden });
+    p.start(fn);
+    await vi.advanceTimersByTimeAsync(10000);
+    expect(fn).toHaveBeenCalledTimes(1);
+    hidden = true;
+    await vi.advanceTimersByTimeAsync(30000);
+    expect(fn).toHaveBeenCalledTimes(1);
+    expect(p.stats().hiddenSkips).toBe(3);
+    hidden = false;
+    await vi.advanceTimersByTimeAsync(10000);
+    expect(fn).toHaveBeenCalledTimes(2);
+    p.stop();
+    vi.useRealTimers();
+  });
+  it('reads document.visibilityState by default', async () => {
+    vi.useFakeTimers();
+    const had = Object.prototype.hasOwnProperty.call(globalThis, 'document');
+    const prev = globalThis.document;
+    globalThis.document = { visibilityState: 'hidden' };
+    try {
+      const fn = vi.fn(() => Promise.resolve());
+      const p = createPoller(5);
+      p.start(fn);
+      await vi.advanceTimersByTimeAsync(15000);
+      expect(fn).not.toHaveBeenCalled();
+      globalThis.document.visibilityState = 'visible';
+      await vi.advanceTimersByTimeAsync(5000);
+      expect(fn).toHaveBeenCalledTimes(1);
+      p.stop();
+    } finally {
+      if (had) globalThis.document = prev;
+      else delete globalThis.document;
+      vi.useRealTimers();
+    }
+  });
   it('period 0 never polls', () => {
     const fn = vi.fn();
     const p = createPoller(0);
