@@ -23,14 +23,15 @@
 // the whole request (kRequestDeadlineMs: headers in, response out); a peer
 // that trickles bytes or stops reading only holds its own socket until then,
 // never a thread, so no number of slow peers below kMaxConns delays /healthz
-// or a Prometheus scrape. At kMaxConns the oldest connection still sending its
-// request is dropped for the new one. A /metrics render is shared by requests
+// or a Prometheus scrape. At kMaxConns (or near the descriptor limit) the
+// oldest connection still sending its request is dropped for the new one. A /metrics render is shared by requests
 // arriving within kRenderCacheMs. SIGINT / SIGTERM end the loop.
 
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <poll.h>
 #include <signal.h>
+#include <sys/resource.h>
 #include <sys/socket.h>
 #include <sys/time.h>
 
@@ -263,6 +264,14 @@ int main(int argc, char** argv) {
   std::printf("amdgpu-exporter listening on %s:%d (%d GPU%s, hostname %s%s)\n", a.bind.c_str(), ntohs(addr.sin_port),
               gpus, gpus == 1 ? "" : "s", a.render.hostname.c_str(), a.render.sysfs_only ? ", sysfs-only" : "");
   std::fflush(stdout);
+  // Stay below the descriptor limit: an accept() failing with EMFILE would
+  // leave the listen socket readable and spin poll() until a peer closes.
+  size_t max_conns = kMaxConns;
+  rlimit nofile{};
+  if (getrlimit(RLIMIT_NOFILE, &nofile) == 0 && nofile.rlim_cur != RLIM_INFINITY) {
+    const rlim_t spare = 16;  // stdio, the listen socket, sysfs files opened while rendering
+    max_conns = nofile.rlim_cur > spare + 1 ? std::min<size_t>(kMaxConns, nofile.rlim_cur - spare) : 1;
+  }
   std::vector<Conn> conns;
   std::vector<pollfd> pfds;
   while (!g_stop.load()) {
@@ -292,7 +301,7 @@ int main(int argc, char** argv) {
       for (;;) {
         const int fd = accept4(srv, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
         if (fd < 0) break;  // EAGAIN: nothing more to accept (or a transient error)
-        if (conns.size() >= kMaxConns) {
+        if (conns.size() >= max_conns) {
           // Full: drop the oldest connection still sending its request (a
           // slow peer, most likely) rather than the new one.
           auto victim = conns.end();

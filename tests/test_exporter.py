@@ -327,6 +327,44 @@ def test_full_connection_table_drops_the_oldest_request_in_progress(exe):
         assert p.wait(15) == 0
 
 
+def test_descriptor_limit_caps_the_connection_table(exe):
+    """With a small RLIMIT_NOFILE the table is capped below it: idle peers past the cap evict older ones instead of
+    making accept() fail with EMFILE (which would leave the listen socket readable and spin poll()), so scrapes
+    still answer and the daemon stays idle on the CPU."""
+    import resource
+    import socket
+
+    def small_limit():
+        resource.setrlimit(resource.RLIMIT_NOFILE, (64, resource.getrlimit(resource.RLIMIT_NOFILE)[1]))
+
+    p = subprocess.Popen([exe, "--port", "0", "--bind", "127.0.0.1", "--hostname", "fd", "--sysfs-only"],
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, preexec_fn=small_limit)
+    port = int(p.stdout.readline().split("127.0.0.1:")[1].split()[0])
+    idle = []
+    try:
+        for _ in range(100):
+            idle.append(socket.create_connection(("127.0.0.1", port)))
+        time.sleep(0.3)
+
+        def cpu_ticks():
+            f = open(f"/proc/{p.pid}/stat").read().rsplit(")", 1)[1].split()
+            return int(f[11]) + int(f[12])  # utime + stime
+
+        before = cpu_ticks()
+        time.sleep(1.0)
+        assert cpu_ticks() - before < 30  # < 0.3 s of CPU in 1 s: no EMFILE spin
+        for path in ("/healthz", "/metrics"):
+            t = time.time()
+            with urllib.request.urlopen(f"http://127.0.0.1:{port}{path}", timeout=5) as r:
+                assert r.status == 200
+            assert time.time() - t < 1.0, path
+    finally:
+        for s in idle:
+            s.close()
+        p.send_signal(signal.SIGTERM)
+        assert p.wait(15) == 0
+
+
 @pytest.mark.gpu
 def test_sysfs_only_on_the_box_matches_the_hip_scrape(exe):
     """--sysfs-only (no HIP, what the unprivileged DaemonSet runs) sees every
