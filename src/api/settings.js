@@ -122,41 +122,54 @@ export function saveSettings(value, storage) {
  * `periodSec` seconds, skipping a tick while the previous call's promise is
  * still pending (no overlapping refreshes), and while the browser tab is
  * hidden (an auto-refreshing dashboard left in a background tab would keep
- * querying the apiserver and Prometheus for nobody). Period 0 → never.
+ * querying the apiserver and Prometheus for nobody). When the tab is shown
+ * again after a skipped tick, the refresh runs at once instead of up to one
+ * period later. Period 0 → never.
  */
 export function createPoller(periodSec, clock) {
   const c = clock || { setInterval: setInterval, clearInterval: clearInterval };
   const hidden = typeof c.hidden === 'function' ? c.hidden : documentHidden;
+  const onVisible = typeof c.onVisible === 'function' ? c.onVisible : documentOnVisible;
   let handle = null;
+  let unsubscribe = null;
   let busy = false;
+  let missed = false;
   let ticks = 0;
   let skipped = 0;
   let hiddenSkips = 0;
+  function tick(fn) {
+    if (busy) {
+      skipped++;
+      return;
+    }
+    if (hidden()) {
+      hiddenSkips++;
+      missed = true;
+      return;
+    }
+    missed = false;
+    busy = true;
+    ticks++;
+    Promise.resolve()
+      .then(fn)
+      .then(
+        function () { busy = false; },
+        function () { busy = false; }
+      );
+  }
   return {
     start: function (fn) {
       if (handle !== null || !(periodSec > 0)) return;
-      handle = c.setInterval(function () {
-        if (busy) {
-          skipped++;
-          return;
-        }
-        if (hidden()) {
-          hiddenSkips++;
-          return;
-        }
-        busy = true;
-        ticks++;
-        Promise.resolve()
-          .then(fn)
-          .then(
-            function () { busy = false; },
-            function () { busy = false; }
-          );
-      }, periodSec * 1000);
+      handle = c.setInterval(function () { tick(fn); }, periodSec * 1000);
+      unsubscribe = onVisible(function () {
+        if (handle !== null && missed) tick(fn);
+      });
     },
     stop: function () {
       if (handle !== null) c.clearInterval(handle);
       handle = null;
+      if (unsubscribe) unsubscribe();
+      unsubscribe = null;
     },
     stats: function () {
       return { ticks: ticks, skipped: skipped, hiddenSkips: hiddenSkips, running: handle !== null };
@@ -167,4 +180,16 @@ export function createPoller(periodSec, clock) {
 /** True in a browser tab that is not visible; false outside a browser (the terminal dashboard). */
 function documentHidden() {
   return typeof document !== 'undefined' && !!document && document.visibilityState === 'hidden';
+}
+
+/** Calls `cb` when the tab becomes visible; returns the unsubscribe. A no-op outside a browser. */
+function documentOnVisible(cb) {
+  if (typeof document === 'undefined' || !document || typeof document.addEventListener !== 'function') {
+    return function () {};
+  }
+  const listener = function () {
+    if (document.visibilityState !== 'hidden') cb();
+  };
+  document.addEventListener('visibilitychange', listener);
+  return function () { document.removeEventListener('visibilitychange', listener); };
 }

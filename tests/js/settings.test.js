@@ -142,21 +142,62 @@ describe('createPoller', () => {
     p.stop();
     vi.useRealTimers();
   });
+  it('refreshes at once when the tab is shown after a skipped tick, and unsubscribes on stop', async () => {
+    vi.useFakeTimers();
+    let hidden = true;
+    const listeners = new Set();
+    const clock = {
+      setInterval,
+      clearInterval,
+      hidden: () => hidden,
+      onVisible: (cb) => {
+        listeners.add(cb);
+        return () => listeners.delete(cb);
+      },
+    };
+    const fn = vi.fn(() => Promise.resolve());
+    const p = createPoller(60, clock);
+    p.start(fn);
+    hidden = false;
+    listeners.forEach((cb) => cb());
+    expect(fn).not.toHaveBeenCalled(); // shown before any tick was missed: nothing is stale
+    hidden = true;
+    await vi.advanceTimersByTimeAsync(60000);
+    expect(fn).not.toHaveBeenCalled();
+    hidden = false;
+    listeners.forEach((cb) => cb());
+    await vi.advanceTimersByTimeAsync(0);
+    expect(fn).toHaveBeenCalledTimes(1);
+    listeners.forEach((cb) => cb()); // a second show without a missed tick does nothing
+    await vi.advanceTimersByTimeAsync(0);
+    expect(fn).toHaveBeenCalledTimes(1);
+    p.stop();
+    expect(listeners.size).toBe(0);
+    vi.useRealTimers();
+  });
   it('reads document.visibilityState by default', async () => {
     vi.useFakeTimers();
     const had = Object.prototype.hasOwnProperty.call(globalThis, 'document');
     const prev = globalThis.document;
-    globalThis.document = { visibilityState: 'hidden' };
+    const listeners = new Set();
+    globalThis.document = {
+      visibilityState: 'hidden',
+      addEventListener: (type, l) => type === 'visibilitychange' && listeners.add(l),
+      removeEventListener: (type, l) => listeners.delete(l),
+    };
     try {
       const fn = vi.fn(() => Promise.resolve());
       const p = createPoller(5);
       p.start(fn);
+      expect(listeners.size).toBe(1);
       await vi.advanceTimersByTimeAsync(15000);
       expect(fn).not.toHaveBeenCalled();
       globalThis.document.visibilityState = 'visible';
-      await vi.advanceTimersByTimeAsync(5000);
+      listeners.forEach((l) => l());
+      await vi.advanceTimersByTimeAsync(0);
       expect(fn).toHaveBeenCalledTimes(1);
       p.stop();
+      expect(listeners.size).toBe(0);
     } finally {
       if (had) globalThis.document = prev;
       else delete globalThis.document;
