@@ -208,6 +208,47 @@ describe('store: incremental index', () => {
     }
   });
 
+  it('stays equal to buildClusterIndex when node events (cordon, uncordon, resize, leave, join) interleave with pod events', () => {
+    for (let seed = 21; seed <= 24; seed++) {
+      const r = rng(seed);
+      let nodes = NODES.map((n) => versioned(makeGpuNode(n, { gpus: 8 })));
+      nodes.push(versioned(makeNode('cpu-0')));
+      let pods = initialPods(r);
+      const store = createClusterStore({ request: () => Promise.resolve({ kind: 'List', items: [] }) });
+      store.setNodes(nodes, null);
+      store.setPods(pods, null);
+      let cordonedSeen = 0;
+      for (let e = 0; e < 120; e++) {
+        if (r() < 0.3) {
+          nodes = nodes.slice();
+          const i = Math.floor(r() * nodes.length);
+          const y = r();
+          if (y < 0.5) {
+            nodes[i] = bump(nodes[i], function (c) { c.spec = Object.assign({}, c.spec, { unschedulable: !(c.spec && c.spec.unschedulable) }); });
+          } else if (y < 0.75) {
+            const n = 2 + Math.floor(r() * 7);
+            nodes[i] = bump(nodes[i], function (c) {
+              if (c.status && c.status.allocatable && c.status.allocatable['amd.com/gpu'] !== undefined) c.status.allocatable['amd.com/gpu'] = String(n);
+            });
+          } else if (y < 0.87 && nodes.length > 2) {
+            nodes.splice(i, 1);
+          } else {
+            const name = NODES[Math.floor(r() * NODES.length)];
+            if (!nodes.some((x) => x.metadata.name === name)) nodes.push(versioned(makeGpuNode(name, { gpus: 8 })));
+          }
+          store.setNodes(r() < 0.7 ? nodes : nodes.map((x) => ({ jsonData: x })), null);
+        } else {
+          pods = step(r, pods);
+          store.setPods(pods, null);
+        }
+        const snap = store.getSnapshot();
+        expect(plainIndex(snap.index)).toEqual(plainIndex(buildClusterIndex(filterAmdGpuNodes(nodes), snap.gpuPods)));
+        cordonedSeen += snap.index.totals.cordonedNodes > 0 ? 1 : 0;
+      }
+      expect(cordonedSeen).toBeGreaterThan(0);
+    }
+  });
+
   it('patches only the nodes an event touched (others keep their identity)', () => {
     const nodes = NODES.map((n) => versioned(makeGpuNode(n)));
     const pods = NODES.map((n, i) => versioned(makeGpuPod('t' + i, { node: n })));
