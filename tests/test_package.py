@@ -55,3 +55,32 @@ def test_offline_plugin_archive_is_installable_and_reproducible(tmp_path):
             meta = json.load(t.extractfile(f"{pkg['name']}/package.json"))
     assert shas[0] == shas[1]
     assert meta["name"] == pkg["name"] and meta["version"] == pkg["version"] and meta["main"] == "main.js"
+
+
+def test_artifacthub_metadata_is_valid_and_matches_the_manifest(tmp_path):
+    """CI's ArtifactHub gate (reference .github/workflows/ci.yaml:25-72) accepts the shipped metadata, whose version is
+    package.json's, and rejects the mistakes it exists to catch."""
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    try:
+        from validate_artifacthub import validate
+    finally:
+        sys.path.pop(0)
+    shipped = os.path.join(ROOT, "artifacthub-pkg.yml")
+    assert validate(shipped) == []
+    meta = yaml.safe_load(open(shipped))
+    assert str(meta["version"]) == json.load(open(os.path.join(ROOT, "package.json")))["version"]
+
+    def broken(mutate):
+        m = yaml.safe_load(open(shipped))
+        mutate(m)
+        p = tmp_path / "pkg.yml"
+        p.write_text(yaml.safe_dump(m))
+        return validate(str(p))
+
+    assert any("SemVer" in e for e in broken(lambda m: m.update(version="1.2")))
+    assert any("checksum" in e for e in broken(lambda m: m["annotations"].update({"headlamp/plugin/archive-checksum": "sha256:xyz"})))
+    assert any("v9.9.9" in e for e in broken(lambda m: m.update(version="9.9.9")))
+    assert any("license" in e for e in broken(lambda m: m.pop("license")))
+    assert validate(str(tmp_path / "missing.yml")) == [f"{tmp_path / 'missing.yml'} not found"]
