@@ -17,6 +17,7 @@ import {
   filterAmdGpuPluginPods,
   filterGpuRequestingPods,
   formatAge,
+  nextAgeChange,
   formatBytes,
   formatGpuModel,
   shortProductName,
@@ -453,5 +454,29 @@ describe('formatters', () => {
     expect(pctToStatus(90)).toBe('error');
     expect(pctToColor(95)).toBe('#d32f2f');
     expect(pctToColor(75)).toBe('#f57c00');
+  });
+});
+
+describe('nextAgeChange', () => {
+  it('is the first instant at which formatAge shows a different label', () => {
+    let a = 7;
+    const r = () => {
+      a = (a * 1103515245 + 12345) % 2147483648;
+      return a / 2147483648;
+    };
+    const t0 = Date.UTC(2026, 0, 1);
+    for (let i = 0; i < 2000; i++) {
+      const ts = new Date(t0 + Math.floor(r() * 1e9)).toISOString();
+      // ages from "in the future" (clock skew) to ~40 days
+      const now = t0 + Math.floor(r() * 1e9) + Math.floor((r() - 0.05) * 40 * 86400000);
+      const next = nextAgeChange(ts, now);
+      expect(next).toBeGreaterThan(now);
+      expect(formatAge(ts, next - 1)).toBe(formatAge(ts, now));
+      expect(formatAge(ts, next)).not.toBe(formatAge(ts, now));
+    }
+  });
+  it('never changes for a missing or unparseable timestamp', () => {
+    expect(nextAgeChange(undefined, 0)).toBe(Infinity);
+    expect(nextAgeChange('not a time', 0)).toBe(Infinity);
   });
 });
