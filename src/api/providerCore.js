@@ -27,7 +27,7 @@
 import { createClusterStore, getSharedStore } from './clusterStore.js';
 import { createMetricsSource } from './metrics.js';
 import { clusterKey as defaultClusterKey } from './cluster.js';
-import { createPoller, loadSettings as defaultLoadSettings, prometheusCandidates, seriesStepSec } from './settings.js';
+import { POLL_MISS, createPoller, loadSettings as defaultLoadSettings, prometheusCandidates, seriesStepSec } from './settings.js';
 
 /** Data younger than this is served from the shared store on mount without re-fetching. */
 export const STALE_MS = 5000;
@@ -216,10 +216,20 @@ export function createProviderCore(React, lib, deps) {
       // `fetchPair` is rebuilt every render; `key` names what it fetches.
     }, [key, seq]);
 
+    // The poller backs off while Prometheus does not answer (each tick would
+    // otherwise re-run discovery: a query plus one probe per candidate).
+    const unreachable = React.useRef(false);
+    useEffect(function () {
+      unreachable.current = state.fetchError === PROMETHEUS_UNREACHABLE;
+    }, [state.fetchError]);
     useEffect(function () {
       if (key === null) return undefined;
       const poller = createPoller(refreshIntervalSec);
-      poller.start(function () { setSeq(function (s) { return s + 1; }); });
+      poller.start(function () {
+        const miss = unreachable.current;
+        setSeq(function (s) { return s + 1; });
+        return miss ? POLL_MISS : undefined;
+      });
       return function () { poller.stop(); };
     }, [key, refreshIntervalSec]);
 

@@ -124,8 +124,13 @@ export function saveSettings(value, storage) {
  * hidden (an auto-refreshing dashboard left in a background tab would keep
  * querying the apiserver and Prometheus for nobody). When the tab is shown
  * again after a skipped tick, the refresh runs at once instead of up to one
- * period later. Period 0 → never.
+ * period later. When `fn` resolves to POLL_MISS (its target did not answer)
+ * the poller backs off: it skips the next 1, 2, 4, then at most
+ * MAX_MISS_SKIPS ticks, until a call succeeds again. Period 0 → never.
  */
+export const POLL_MISS = 'miss';
+export const MAX_MISS_SKIPS = 8;
+
 export function createPoller(periodSec, clock) {
   const c = clock || { setInterval: setInterval, clearInterval: clearInterval };
   const hidden = typeof c.hidden === 'function' ? c.hidden : documentHidden;
@@ -137,9 +142,17 @@ export function createPoller(periodSec, clock) {
   let ticks = 0;
   let skipped = 0;
   let hiddenSkips = 0;
+  let backoff = 0; // ticks to skip after each consecutive miss
+  let skipLeft = 0;
+  let missSkips = 0;
   function tick(fn) {
     if (busy) {
       skipped++;
+      return;
+    }
+    if (skipLeft > 0) {
+      skipLeft--;
+      missSkips++;
       return;
     }
     if (hidden()) {
@@ -153,7 +166,16 @@ export function createPoller(periodSec, clock) {
     Promise.resolve()
       .then(fn)
       .then(
-        function () { busy = false; },
+        function (r) {
+          busy = false;
+          if (r === POLL_MISS) {
+            backoff = backoff ? Math.min(backoff * 2, MAX_MISS_SKIPS) : 1;
+            skipLeft = backoff;
+          } else {
+            backoff = 0;
+            skipLeft = 0;
+          }
+        },
         function () { busy = false; }
       );
   }
@@ -172,7 +194,7 @@ export function createPoller(periodSec, clock) {
       unsubscribe = null;
     },
     stats: function () {
-      return { ticks: ticks, skipped: skipped, hiddenSkips: hiddenSkips, running: handle !== null };
+      return { ticks: ticks, skipped: skipped, hiddenSkips: hiddenSkips, missSkips: missSkips, running: handle !== null };
     },
   };
 }

@@ -361,6 +361,27 @@ describe('metrics hooks', () => {
     expect(r.text()).toBe(PROMETHEUS_UNREACHABLE);
   });
 
+  it('useGpuMetrics auto-refresh backs off while Prometheus is unreachable', async () => {
+    vi.useFakeTimers();
+    settings.refreshIntervalSec = 10;
+    const request = apiServer({ prom: () => Promise.reject(new Error('503')) });
+    const c = core(request);
+    const mp = metricsProbe(() => c.useGpuMetrics(true, false));
+    const r = render(h(mp.M));
+    await r.settle();
+    const fetches = () => mp.seen.filter((m, i) => m.fetching && (i === 0 || !mp.seen[i - 1].fetching)).length;
+    expect(fetches()).toBe(1);
+    for (let i = 0; i < 30; i++) {
+      await vi.advanceTimersByTimeAsync(10000);
+      await r.settle();
+    }
+    // 30 ticks of 10 s: without back-off 30 more fetches; with it one per 1 + 2 + 4 + 8 + 8 ... ticks
+    expect(fetches()).toBeGreaterThan(2);
+    expect(fetches()).toBeLessThanOrEqual(7);
+    expect(mp.last().fetchError).toBe(PROMETHEUS_UNREACHABLE);
+    r.unmount();
+  });
+
   it('useGpuMetrics: exporter reachable → per-GPU metrics and series', async () => {
     const request = apiServer({ prom: prom() });
     const c = core(request);

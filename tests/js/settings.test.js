@@ -5,6 +5,8 @@
 import {
   DEFAULT_SETTINGS,
   SETTINGS_KEY,
+  MAX_MISS_SKIPS,
+  POLL_MISS,
   createPoller,
   loadSettings,
   parsePrometheus,
@@ -203,6 +205,24 @@ describe('createPoller', () => {
       else delete globalThis.document;
       vi.useRealTimers();
     }
+  });
+  it('backs off 1, 2, 4, 8, 8 ticks while calls miss and resets on the first success', async () => {
+    vi.useFakeTimers();
+    const at = [];
+    let n = 0;
+    const fn = vi.fn(() => {
+      at.push(Date.now());
+      n++;
+      return Promise.resolve(n <= 5 ? POLL_MISS : undefined);
+    });
+    const t0 = Date.now();
+    const p = createPoller(10, { setInterval, clearInterval, hidden: () => false, onVisible: () => () => {} });
+    p.start(fn);
+    await vi.advanceTimersByTimeAsync(300000);
+    expect(at.map((t) => (t - t0) / 1000)).toEqual([10, 30, 60, 110, 200, 290, 300]);
+    expect(p.stats().missSkips).toBe(1 + 2 + 4 + MAX_MISS_SKIPS + MAX_MISS_SKIPS);
+    p.stop();
+    vi.useRealTimers();
   });
   it('period 0 never polls', () => {
     const fn = vi.fn();
