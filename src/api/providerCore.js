@@ -216,11 +216,12 @@ export function createProviderCore(React, lib, deps) {
       // `fetchPair` is rebuilt every render; `key` names what it fetches.
     }, [key, seq]);
 
-    // The poller backs off while Prometheus does not answer (each tick would
-    // otherwise re-run discovery: a query plus one probe per candidate).
+    // The poller backs off while Prometheus does not answer or refuses the
+    // proxy (each tick would otherwise re-run discovery: a query plus one
+    // probe per candidate); a manual refresh is never delayed.
     const unreachable = React.useRef(false);
     useEffect(function () {
-      unreachable.current = state.fetchError === PROMETHEUS_UNREACHABLE;
+      unreachable.current = state.fetchError === PROMETHEUS_UNREACHABLE || state.fetchError === PROMETHEUS_FORBIDDEN;
     }, [state.fetchError]);
     useEffect(function () {
       if (key === null) return undefined;

@@ -9,7 +9,7 @@
  */
 import React, { render } from './stubs/react.js';
 import * as lib from './stubs/headlamp-lib.js';
-import { OUTSIDE_PROVIDER, PROMETHEUS_UNREACHABLE, STALE_MS, createProviderCore, listResult } from '../../src/api/providerCore.js';
+import { OUTSIDE_PROVIDER, PROMETHEUS_FORBIDDEN, PROMETHEUS_UNREACHABLE, STALE_MS, createProviderCore, listResult } from '../../src/api/providerCore.js';
 import { resetSharedStores } from '../../src/api/clusterStore.js';
 import { DEVICE_CONFIG_LIST_PATH, PLUGIN_POD_QUERIES } from '../../src/api/amdgpu.js';
 import { DEFAULT_SETTINGS } from '../../src/api/settings.js';
@@ -361,10 +361,14 @@ describe('metrics hooks', () => {
     expect(r.text()).toBe(PROMETHEUS_UNREACHABLE);
   });
 
-  it('useGpuMetrics auto-refresh backs off while Prometheus is unreachable', async () => {
+  for (const [why, fail, text] of [
+    ['unreachable', () => Promise.reject(new Error('503')), PROMETHEUS_UNREACHABLE],
+    ['refused (403)', () => Promise.reject(Object.assign(new Error('forbidden'), { status: 403 })), PROMETHEUS_FORBIDDEN],
+  ]) {
+  it('useGpuMetrics auto-refresh backs off while Prometheus is ' + why, async () => {
     vi.useFakeTimers();
     settings.refreshIntervalSec = 10;
-    const request = apiServer({ prom: () => Promise.reject(new Error('503')) });
+    const request = apiServer({ prom: fail });
     const c = core(request);
     const mp = metricsProbe(() => c.useGpuMetrics(true, false));
     const r = render(h(mp.M));
@@ -378,9 +382,10 @@ describe('metrics hooks', () => {
     // 30 ticks of 10 s: without back-off 30 more fetches; with it one per 1 + 2 + 4 + 8 + 8 ... ticks
     expect(fetches()).toBeGreaterThan(2);
     expect(fetches()).toBeLessThanOrEqual(7);
-    expect(mp.last().fetchError).toBe(PROMETHEUS_UNREACHABLE);
+    expect(mp.last().fetchError).toBe(text);
     r.unmount();
   });
+  }
 
   it('useGpuMetrics: exporter reachable → per-GPU metrics and series', async () => {
     const request = apiServer({ prom: prom() });
