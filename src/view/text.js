@@ -5,7 +5,8 @@
  * become underlined titles, name/value tables aligned "name  value" lines,
  * tables fixed-width columns, bars "[#####.....] 6/8 (75%)", statuses a
  * marker (✓ ! ✗) before the text, the per-GPU strip one line per board and
- * the xGMI matrix a small grid. Optional ANSI colour for statuses.
+ * the xGMI matrix a small grid, power history a sparkline. Optional ANSI
+ * colour for statuses.
  */
 
 import { matrixCaption } from './ir.js';
@@ -24,6 +25,33 @@ function barText(p, width) {
   if (p === null || p === undefined) return '';
   const k = Math.max(0, Math.min(width, Math.round((p / 100) * width)));
   return '[' + '#'.repeat(k) + '.'.repeat(width - k) + '] ';
+}
+
+const SPARK = '▁▂▃▄▅▆▇█';
+
+/**
+ * Values as a sparkline of at most `width` characters: consecutive samples
+ * are averaged into buckets, each bucket drawn by its height between the
+ * window's min and max (a flat series is drawn mid-height). Non-numbers skip.
+ */
+export function sparkline(values, width) {
+  const v = (values || []).filter(function (x) { return typeof x === 'number' && isFinite(x); });
+  if (!v.length) return '';
+  const w = Math.max(1, Math.min(width || 32, v.length));
+  const buckets = [];
+  for (let i = 0; i < w; i++) {
+    const a = Math.floor((i * v.length) / w);
+    const b = Math.max(a + 1, Math.floor(((i + 1) * v.length) / w));
+    let sum = 0;
+    for (let k = a; k < b; k++) sum += v[k];
+    buckets.push(sum / (b - a));
+  }
+  const lo = Math.min.apply(null, buckets);
+  const hi = Math.max.apply(null, buckets);
+  return buckets.map(function (x) {
+    const k = hi > lo ? Math.round(((x - lo) / (hi - lo)) * (SPARK.length - 1)) : 3;
+    return SPARK[k];
+  }).join('');
 }
 
 /** One IR cell/value as a single line of text. */
@@ -98,7 +126,9 @@ function blockLines(b, color) {
         const pts = b.power[n];
         const last = pts.length ? pts[pts.length - 1][1] : null;
         const avg = b.avgPower && b.avgPower[n] !== undefined ? ', avg ' + b.avgPower[n].toFixed(0) + ' W' : '';
-        out.push('  ' + n + ': ' + pts.length + ' power samples' + (last === null ? '' : ', last ' + last.toFixed(0) + ' W') + avg);
+        const spark = sparkline(pts.map(function (p) { return p[1]; }), 32);
+        out.push('  ' + n + ': ' + pts.length + ' power samples' + (last === null ? '' : ', last ' + last.toFixed(0) + ' W') + avg +
+          (spark ? '  ' + spark : ''));
       });
       break;
     }

@@ -1,7 +1,7 @@
 /**
  * Terminal renderer (src/view/text.js) — the third renderer of the view IR.
  */
-import { renderText, textSection, textValue } from '../../src/view/text.js';
+import { renderText, sparkline, textSection, textValue } from '../../src/view/text.js';
 import { nodesView, podDetailView } from '../../src/view/pages.js';
 import { bar, kv, lines, row, section, status, table } from '../../src/view/ir.js';
 import { NOW, makeContext, makeGpuNode, makeGpuPod } from './fixtures.js';
@@ -38,5 +38,19 @@ describe('text renderer', () => {
   });
   it('renders detail sections', () => {
     expect(textSection(podDetailView(makeGpuPod('q')))[0]).toBe('AMD GPU Resources');
+  });
+  it('draws power history as a sparkline scaled to the window', () => {
+    expect(sparkline([0, 1, 2, 3, 4, 5, 6, 7], 8)).toBe('▁▂▃▄▅▆▇█');
+    expect(sparkline([5, 5, 5], 8)).toBe('▄▄▄'); // flat: mid-height, one cell per sample
+    expect(sparkline([], 8)).toBe('');
+    expect(sparkline([1, null, 'x', 3], 8)).toBe('▁█'); // non-numbers skipped
+    const long = [];
+    for (let i = 0; i < 120; i++) long.push(i < 60 ? 100 : 1400);
+    const s = sparkline(long, 32);
+    expect([...s]).toHaveLength(32);
+    expect(s[0]).toBe('▁');
+    expect(s[s.length - 1]).toBe('█');
+    const lines = textSection(section('h', [{ t: 'series', power: { n0: [[0, 600], [30, 1200], [60, 900]] }, avgPower: { n0: 900 } }]));
+    expect(lines[2]).toBe('  n0: 3 power samples, last 900 W, avg 900 W  ▁█▅');
   });
 });
