@@ -323,6 +323,24 @@ describe('harness React enforces the rules real React enforces', () => {
     expect(() => render(h('div', null, h(A), h(B)))).toThrow('while rendering');
   });
 
+  it('a ref written while rendering is rejected; written in an effect it is fine', async () => {
+    function Bad() {
+      const r = React.useRef(0);
+      r.current = r.current + 1; // side effect in render
+      return h('i', null, 'x');
+    }
+    expect(() => render(h(Bad))).toThrow('ref.current written while rendering Bad');
+    let seen = null;
+    function Good(props) {
+      const r = React.useRef(null);
+      React.useEffect(function () { r.current = props.v; seen = r; }, [props.v]);
+      return h('i', null, String(r.current)); // reading is allowed
+    }
+    const g = render(h(Good, { v: 7 }));
+    await g.settle();
+    expect(seen.current).toBe(7);
+  });
+
   it('a hook skipped on re-render is rejected', async () => {
     let setFlag = null;
     function Cond() {

@@ -165,7 +165,20 @@ export function useCallback(fn, deps) {
 }
 
 export function useRef(v) {
-  return hookSlot(function () { return { current: v }; }, 'useRef');
+  return hookSlot(function () {
+    let value = v;
+    return Object.defineProperty({}, 'current', {
+      enumerable: true,
+      get: function () { return value; },
+      set: function (x) {
+        // React: a ref holds what rendering does not depend on; writing one
+        // while rendering breaks StrictMode's double render and concurrent
+        // rendering. Write it in an effect or an event handler.
+        if (current) throw new Error('ref.current written while rendering ' + typeName(current.type));
+        value = x;
+      },
+    });
+  }, 'useRef');
 }
 
 function readContext(ctx) {
