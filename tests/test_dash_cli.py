@@ -68,6 +68,8 @@ def test_detail_sections_with_power_history(url):
     node = run("--url", url, "--page", "node:mi355x-001")
     assert node.returncode == 0, node.stderr
     assert node.stdout.startswith("AMD GPU\n") and "Peak GPU Power (30 min)" in node.stdout and "xGMI topology" in node.stdout
+    history = [l for l in node.stdout.splitlines() if "power samples" in l]
+    assert history and any(c in history[0] for c in "▁▂▃▄▅▆▇█")  # the sparkline of the window
     pod = run("--url", url, "--page", "pod:ml/train-000-2")
     assert pod.returncode == 0, pod.stderr
     assert "AMD GPU Resources" in pod.stdout and "GPU Energy (30 min)" in pod.stdout and "Assigned GPUs" in pod.stdout
