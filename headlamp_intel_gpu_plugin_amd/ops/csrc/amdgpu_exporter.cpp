@@ -169,9 +169,12 @@ struct Conn {
   std::string out;
   size_t off = 0;
   bool writing = false;
+  bool eof = false;  // the peer shut its write side (recv returned 0)
 };
 
-// Read what is there; false when the peer closed or failed.
+// Read what is there; false when the read failed. A peer that sends its
+// request and then half-closes (`nc -N`, some HTTP/1.0 probes) sets `eof`:
+// what was read so far is still answered if it is a complete request.
 bool read_some(Conn& c) {
   char buf[4096];
   for (;;) {
@@ -181,7 +184,10 @@ bool read_some(Conn& c) {
       if (c.in.size() >= kMaxHeader) return true;
       continue;
     }
-    if (n == 0) return false;
+    if (n == 0) {
+      c.eof = true;
+      return true;
+    }
     return errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR;
   }
 }
@@ -211,6 +217,8 @@ bool step(Conn& c, short revents, const Args& a, Clock::time_point now) {
     if (complete || c.in.size() >= kMaxHeader) {
       c.out = complete ? answer(c.in, a, now) : response(431, "Request Header Fields Too Large", "text/plain", "header too large\n");
       c.writing = true;
+    } else if (c.eof) {
+      return false;  // closed before a whole request arrived: nothing to answer
     }
   } else if (revents & (POLLERR | POLLHUP | POLLNVAL)) {
     return false;

@@ -927,7 +927,7 @@ export function createMetricsSource(opts) {
       if (!fresh && start > end) return Promise.resolve(seriesCache.data);
       return rangeQuery(base, seriesQuery(), start, end, step).then(function (got) {
         if (got === UNREACHABLE) return UNREACHABLE;
-        const data = { rangeSec: range };
+        const data = { rangeSec: range, stepSec: step };
         const cutoff = end - range;
         for (let i = 0; i < parts.length; i++) {
           const key = parts[i][0];
@@ -990,7 +990,7 @@ export function createMetricsSource(opts) {
           }
           const power = Object.keys(total).map(Number).sort(function (a, b) { return a - b; })
             .map(function (t) { return [t, total[t]]; });
-          return { rangeSec: range, power: power };
+          return { rangeSec: range, stepSec: step, power: power };
         });
       }, function () { return null; });
     });

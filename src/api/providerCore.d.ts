@@ -41,8 +41,8 @@ export interface MetricsSource {
   fetchNodeMetrics(nodeName: string): Promise<GpuMetrics | null>;
   fetchGpuOwners(): Promise<GpuMetrics | null>;
   failureReason(): 'forbidden' | 'unreachable';
-  fetchPodSeries(namespace: string, pod: string, rangeSec: number, stepSec: number): Promise<{ rangeSec: number; power: Array<[number, number]> } | null>;
-  fetchNodeSeries(nodeName: string, rangeSec: number, stepSec: number): Promise<{ rangeSec: number; power: Array<[number, number]> } | null>;
+  fetchPodSeries(namespace: string, pod: string, rangeSec: number, stepSec: number): Promise<{ rangeSec: number; stepSec: number; power: Array<[number, number]> } | null>;
+  fetchNodeSeries(nodeName: string, rangeSec: number, stepSec: number): Promise<{ rangeSec: number; stepSec: number; power: Array<[number, number]> } | null>;
   fetchSeries(rangeSec: number, stepSec: number): Promise<GpuMetricsState['series']>;
 }
 

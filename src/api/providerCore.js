@@ -40,7 +40,7 @@ export const PROMETHEUS_FORBIDDEN =
 
 export const OUTSIDE_PROVIDER = 'useAmdGpuContext must be used within an AmdGpuDataProvider';
 
-const HOOKS = ['createContext', 'createElement', 'useContext', 'useEffect', 'useMemo', 'useState', 'useSyncExternalStore'];
+const HOOKS = ['createContext', 'createElement', 'useContext', 'useEffect', 'useMemo', 'useRef', 'useState', 'useSyncExternalStore'];
 
 function errorText(e) {
   return e instanceof Error ? e.message : String(e);

@@ -91,9 +91,7 @@ function defaultStorage() {
   return null;
 }
 
-/** Read settings from storage (defaults when absent or unreadable). */
-export function loadSettings(storage) {
-  const st = storage === undefined ? defaultStorage() : storage;
+function readSettings(st) {
   if (!st) return parseSettings(null);
   try {
     const raw = st.getItem(SETTINGS_KEY);
@@ -101,6 +99,52 @@ export function loadSettings(storage) {
   } catch (e) {
     return parseSettings(null);
   }
+}
+
+// Memo of the browser-storage read. Every hook of every render asks for the
+// settings (providerCore.js); parsing localStorage JSON each time is wasted
+// work, so the parsed value is kept until `saveSettings` writes a new one or
+// another tab changes the key (the `storage` event).
+let settingsVersion = 0;
+let memo = null; // {version, value}
+let storageListener = false;
+
+/** `storage` event handler: another tab wrote the settings key (or cleared storage, key null). */
+export function onStorageEvent(e) {
+  if (!e || e.key === null || e.key === undefined || e.key === SETTINGS_KEY) invalidateSettings();
+}
+
+function listenForStorage() {
+  if (storageListener) return;
+  if (typeof window === 'undefined' || !window || typeof window.addEventListener !== 'function') return;
+  storageListener = true;
+  window.addEventListener('storage', onStorageEvent);
+}
+
+/** Drop the memoised settings; the next `loadSettings()` reads storage again. */
+export function invalidateSettings() {
+  settingsVersion++;
+  memo = null;
+}
+
+/** Memo generation (tests): bumped by `saveSettings` and by `storage` events. */
+export function settingsGeneration() {
+  return settingsVersion;
+}
+
+/**
+ * Read settings from storage (defaults when absent or unreadable). With the
+ * default storage the parsed value is memoised (a frozen object, the same one
+ * until invalidated); an explicit `storage` argument always reads it.
+ */
+export function loadSettings(storage) {
+  if (storage !== undefined) return readSettings(storage);
+  listenForStorage();
+  if (memo && memo.version === settingsVersion) return memo.value;
+  const value = Object.freeze(readSettings(defaultStorage()));
+  if (value.prometheus) Object.freeze(value.prometheus);
+  memo = { version: settingsVersion, value: value };
+  return value;
 }
 
 /** Validate and persist; returns what was stored. */
@@ -113,6 +157,12 @@ export function saveSettings(value, storage) {
     } catch (e) {
       // quota / disabled storage: keep the in-memory value
     }
+  }
+  if (storage === undefined) {
+    invalidateSettings();
+    // Storage refused the write (disabled / quota): the memo still serves the
+    // value just saved, as the comment above promises.
+    if (!st) memo = { version: settingsVersion, value: Object.freeze(Object.assign({}, clean)) };
   }
   return clean;
 }

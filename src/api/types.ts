@@ -281,6 +281,8 @@ export interface GpuMetrics {
 
 export interface GpuSeries {
   rangeSec: number;
+  /** step of the range query (s): each sample stands for one step */
+  stepSec?: number;
   power: Record<string, Array<[number, number]>>;
   vram: Record<string, Array<[number, number]>>;
 }

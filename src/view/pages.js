@@ -1322,24 +1322,34 @@ function powerHistoryBlocks(name, label, series) {
     kv([
       row('Peak GPU Power (' + win + ')', formatWatts(st.peakWatts)),
       row('Average GPU Power (' + win + ')', formatWatts(st.avgWatts)),
-      // Σ samples × step: the energy the pod's GPUs drew over the window.
-      row('GPU Energy (' + win + ')', formatEnergy(seriesEnergyJoules(series.power))),
+      // Σ samples × query step: the energy the GPUs drew while observed.
+      row('GPU Energy (' + win + ')', formatEnergy(seriesEnergyJoules(series.power, series.stepSec))),
     ]),
     { t: 'series', label: label, power: byPod, vram: {}, avgPower: seriesMeans(byPod) },
   ];
 }
 
-/** Energy (J) of a step-aligned power series [[t s, W]]: each sample holds for one step. */
-export function seriesEnergyJoules(pts) {
-  if (!pts || pts.length < 2) return 0;
-  const step = (pts[pts.length - 1][0] - pts[0][0]) / (pts.length - 1);
+/**
+ * Energy (J) of a power series [[t s, W]]; null with fewer than 2 samples.
+ * With the range query's `stepSec` each sample holds for one step, so a gap
+ * Prometheus left (an exporter restart) adds nothing instead of stretching
+ * the step guessed from the first and last timestamps. Without it the
+ * trapezoid rule runs over the real timestamps.
+ */
+export function seriesEnergyJoules(pts, stepSec) {
+  if (!pts || pts.length < 2) return null;
   let sum = 0;
-  for (let i = 0; i < pts.length; i++) sum += pts[i][1];
-  return sum * step;
+  if (stepSec > 0) {
+    for (let i = 0; i < pts.length; i++) sum += pts[i][1];
+    return sum * stepSec;
+  }
+  for (let i = 1; i < pts.length; i++) sum += ((pts[i][1] + pts[i - 1][1]) / 2) * (pts[i][0] - pts[i - 1][0]);
+  return sum;
 }
 
-/** Joules → "x Wh" / "x kWh". */
+/** Joules → "x Wh" / "x kWh"; "—" when unknown. */
 export function formatEnergy(joules) {
+  if (joules === null || joules === undefined || !isFinite(joules)) return '—';
   const wh = joules / 3600;
   return wh >= 1000 ? (wh / 1000).toFixed(2) + ' kWh' : wh.toFixed(1) + ' Wh';
 }

@@ -75,7 +75,7 @@ describe('nodeDetailView', () => {
 });
 
 describe('podDetailView: GPU power history', () => {
-  const series = { rangeSec: 1800, power: [[0, 1000], [30, 1200], [60, 1400]] };
+  const series = { rangeSec: 1800, stepSec: 30, power: [[0, 1000], [30, 1200], [60, 1400]] };
   it('adds peak / average / energy over the window and a sparkline row for the pod', () => {
     const s = podDetailView(makeGpuPod('train-p', { gpus: 2 }), { series });
     expect(rowValue(s, 'Peak GPU Power (30 min)')).toBe('1400.0 W');
@@ -98,8 +98,15 @@ describe('podDetailView: GPU power history', () => {
     expect(s.blocks).toHaveLength(plain.blocks.length);
   });
   it('energy helpers', () => {
-    expect(seriesEnergyJoules([[0, 100]])).toBe(0);
-    expect(seriesEnergyJoules([[0, 100], [60, 100]])).toBe(12000);
+    // fewer than 2 samples: unknown, shown as a dash (not "0.0 Wh" next to a non-zero peak)
+    expect(seriesEnergyJoules([[0, 100]])).toBe(null);
+    expect(formatEnergy(seriesEnergyJoules([[0, 100]]))).toBe('—');
+    // with the query step each sample holds one step
+    expect(seriesEnergyJoules([[0, 100], [60, 100]], 60)).toBe(12000);
+    // a gap Prometheus left adds nothing (the old first-to-last guess stretched the step to 150 s: 45 kJ)
+    expect(seriesEnergyJoules([[0, 100], [30, 100], [300, 100]], 30)).toBe(9000);
+    // no step: trapezoid over the real timestamps
+    expect(seriesEnergyJoules([[0, 100], [60, 200]])).toBe(9000);
     expect(formatEnergy(3600 * 1500)).toBe('1.50 kWh');
     expect(formatEnergy(3600 * 2)).toBe('2.0 Wh');
   });

@@ -76,6 +76,11 @@ describe('createProviderCore', () => {
   it('requires the React hooks it uses', () => {
     expect(() => createProviderCore({ createElement: React.createElement }, lib)).toThrow('React.createContext is required');
   });
+  it('checks useRef up front (the metrics hooks keep their back-off flag in a ref)', () => {
+    const noRef = Object.assign({}, React);
+    delete noRef.useRef;
+    expect(() => createProviderCore(noRef, lib)).toThrow('React.useRef is required');
+  });
 });
 
 describe('useAmdGpuContext', () => {

@@ -8,7 +8,10 @@ import {
   MAX_MISS_SKIPS,
   POLL_MISS,
   createPoller,
+  invalidateSettings,
   loadSettings,
+  onStorageEvent,
+  settingsGeneration,
   parsePrometheus,
   parseSettings,
   prometheusCandidates,
@@ -86,6 +89,78 @@ describe('persistence', () => {
   it('works without storage', () => {
     expect(loadSettings(null).requestTimeoutMs).toBe(2000);
     expect(saveSettings({ seriesMinutes: 10 }, null).seriesMinutes).toBe(10);
+  });
+});
+
+describe('loadSettings memo (browser storage)', () => {
+  let saved;
+  let reads;
+  let listeners;
+  beforeEach(() => {
+    saved = { ls: global.localStorage, win: global.window };
+    const st = memStorage();
+    reads = 0;
+    const get = st.getItem;
+    st.getItem = (k) => {
+      reads++;
+      return get(k);
+    };
+    listeners = [];
+    global.localStorage = st;
+    if (!saved.win) global.window = { addEventListener: (type, fn) => listeners.push({ type: type, fn: fn }) };
+    invalidateSettings();
+  });
+  afterEach(() => {
+    if (saved.ls === undefined) delete global.localStorage;
+    else global.localStorage = saved.ls;
+    if (saved.win === undefined) delete global.window;
+    invalidateSettings();
+  });
+
+  it('parses storage once and hands every caller the same frozen object', () => {
+    const a = loadSettings();
+    const b = loadSettings();
+    expect(reads).toBe(1);
+    expect(a).toBe(b);
+    expect(Object.isFrozen(a)).toBe(true);
+  });
+  it('saveSettings invalidates the memo', () => {
+    const before = loadSettings();
+    const g = settingsGeneration();
+    saveSettings({ refreshIntervalSec: 30 });
+    expect(settingsGeneration()).toBeGreaterThan(g);
+    const after = loadSettings();
+    expect(after).not.toBe(before);
+    expect(after.refreshIntervalSec).toBe(30);
+    expect(reads).toBe(2);
+  });
+  it('a storage event for the settings key (or a clear) invalidates it; other keys do not', () => {
+    loadSettings();
+    onStorageEvent({ key: 'some-other-plugin' });
+    loadSettings();
+    expect(reads).toBe(1);
+    global.localStorage.setItem(SETTINGS_KEY, JSON.stringify({ seriesMinutes: 60 }));
+    onStorageEvent({ key: SETTINGS_KEY });
+    expect(loadSettings().seriesMinutes).toBe(60);
+    onStorageEvent({ key: null });
+    loadSettings();
+    expect(reads).toBe(3);
+  });
+  it('registers the storage listener on the window when one exists', () => {
+    loadSettings();
+    if (saved.win) return; // a real DOM window: registration happened on its own object
+    // the module attaches once per process; a runner sharing modules across files may have attached earlier
+    if (listeners.length) {
+      expect(listeners[0].type).toBe('storage');
+      expect(listeners[0].fn).toBe(onStorageEvent);
+    }
+  });
+  it('explicit storage bypasses the memo', () => {
+    const st = memStorage();
+    st.setItem(SETTINGS_KEY, JSON.stringify({ requestTimeoutMs: 900 }));
+    loadSettings();
+    expect(loadSettings(st).requestTimeoutMs).toBe(900);
+    expect(loadSettings().requestTimeoutMs).toBe(2000);
   });
 });
 

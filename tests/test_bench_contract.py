@@ -27,7 +27,8 @@ def _check(line, n):
     assert line["config"]["nodes"] == n
     assert line["rendered"]["gpu_nodes"] == n
     assert line["rendered"]["gpus_monitored"] == 8 * n
-    assert line["rendered_parity_with_reference"] is True
+    assert line["replay_fetched_same_rows"] is True
+    assert line["metric_version"] == 2
     assert line["dtype"] == "n/a"
     # The headline is per page, each page's click against the reference's
     # wiring of that page's button (not the all-pages composite).

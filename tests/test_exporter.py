@@ -414,6 +414,35 @@ def test_garbage_requests_do_not_break_the_daemon(exe):
         assert p.wait(15) == 0
 
 
+def test_half_closed_client_still_gets_its_answer(exe):
+    """A peer that sends a whole request and then shuts its write side (`nc -N`, HTTP/1.0 probes) is answered; one
+    that half-closes mid-request is dropped without an answer."""
+    import socket
+
+    p, port = _start(exe, "halfclose")
+    try:
+        for path, expect in ((b"/healthz", b"ok\n"), (b"/metrics", b"")):
+            with socket.create_connection(("127.0.0.1", port), timeout=5) as s:
+                s.sendall(b"GET " + path + b" HTTP/1.0\r\n\r\n")
+                s.shutdown(socket.SHUT_WR)
+                data = b""
+                while True:
+                    chunk = s.recv(65536)
+                    if not chunk:
+                        break
+                    data += chunk
+            assert data.startswith(b"HTTP/1.1 200"), data[:80]
+            assert data.endswith(expect)
+        with socket.create_connection(("127.0.0.1", port), timeout=5) as s:
+            s.sendall(b"GET /healthz HTTP/1.0\r\n")  # no blank line: incomplete
+            s.shutdown(socket.SHUT_WR)
+            assert s.recv(100) == b""
+        assert p.poll() is None
+    finally:
+        p.send_signal(signal.SIGTERM)
+        assert p.wait(15) == 0
+
+
 @pytest.fixture(scope="module")
 def asan(tmp_path_factory):
     import sys
