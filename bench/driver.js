@@ -495,7 +495,9 @@ async function serve(a) {
         const spanStart = L.s.spans ? L.s.spans.length : 0;
         const render = [];
         let rows = null;
+        const stepStarts = [];
         for (let i = 0; i < n; i++) {
+          stepStarts.push(hiResClock.now());
           const t0 = process.hrtime();
           await L.s.refresh();
           const t1 = process.hrtime();
@@ -506,6 +508,13 @@ async function serve(a) {
         // Data committed → every view rebuilt and rendered, per step.
         out.renderMs = render;
         if (L.s.spans) out.trace = traceSummary(L.s.spans.slice(spanStart));
+        // Every request of these steps, epoch ms (diagnostics: attribute one slow step).
+        if (c.rawSpans && L.s.spans) {
+          out.spans = L.s.spans.slice(spanStart).map(function (sp) {
+            return { name: sp.name, start: sp.start, end: sp.end, ok: sp.ok };
+          });
+          out.stepStarts = stepStarts;
+        }
         const snap = L.s.ctx();
         const ms_ = L.s.mstate();
         out.state = {

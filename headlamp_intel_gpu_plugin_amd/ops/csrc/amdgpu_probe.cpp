@@ -24,6 +24,8 @@
 
 #include <Python.h>
 
+#include <mutex>
+
 #include "probe_core.h"
 
 namespace {
@@ -86,6 +88,29 @@ PyObject* py_link(PyObject*, PyObject* args) {
   return Py_BuildValue("(sii)", name, static_cast<int>(hops), peer);
 }
 
+// PCI address per device, resolved once. sample() used to call
+// hipGetDeviceProperties on every call only to learn the BDF; the inventory
+// never changes while the process lives.
+std::mutex g_bdf_mu;
+std::vector<std::string> g_bdf;
+
+bool cached_bdf(int dev, std::string* bdf) {
+  {
+    std::lock_guard<std::mutex> lk(g_bdf_mu);
+    if (dev < static_cast<int>(g_bdf.size()) && !g_bdf[dev].empty()) {
+      *bdf = g_bdf[dev];
+      return true;
+    }
+  }
+  DeviceInfo i;
+  if (!device_info(dev, &i)) return false;
+  std::lock_guard<std::mutex> lk(g_bdf_mu);
+  if (static_cast<int>(g_bdf.size()) <= dev) g_bdf.resize(dev + 1);
+  g_bdf[dev] = i.bdf;
+  *bdf = i.bdf;
+  return true;
+}
+
 PyObject* py_sample(PyObject*, PyObject* args) {
   int dev;
   if (!PyArg_ParseTuple(args, "i", &dev)) return nullptr;
@@ -94,9 +119,17 @@ PyObject* py_sample(PyObject*, PyObject* args) {
     PyErr_Format(PyExc_IndexError, "device %d out of range (count %d)", dev, g_count);
     return nullptr;
   }
-  DeviceInfo i;
-  if (!device_info(dev, &i)) return raise_hip();
-  Sample s = sample_sysfs(i.bdf);
+  // The sysfs pass reads firmware-backed files (hwmon power, RAS aca_*) that
+  // can block for hundreds of milliseconds; holding the GIL across it froze
+  // every other Python thread in the process (the smoke's fake apiserver).
+  std::string bdf;
+  bool ok;
+  Sample s;
+  Py_BEGIN_ALLOW_THREADS
+  ok = cached_bdf(dev, &bdf);
+  if (ok) s = sample_sysfs(bdf);
+  Py_END_ALLOW_THREADS
+  if (!ok) return raise_hip();
   PyObject* d = PyDict_New();
   auto put = [&](const char* k, double v) {
     PyObject* o = py_float_or_none(v);
