@@ -160,6 +160,9 @@ def main(argv=None) -> int:
             quiet_sync()
             D.barrier(info)
             elapsed = time.perf_counter() - t0
+            # Untimed: every page mounted in the harness React and re-rendered
+            # after a refresh (element count, mount / re-render ms).
+            amd_react = drv.call("pages", "amd", n=1, react=True).get("react") or {}
             # Secondary: the all-pages composite refresh.
             drv.call("steps", "amd", n=1)
             amd = drv.call("steps", "amd", n=max(3, args.steps // 2))
@@ -174,7 +177,7 @@ def main(argv=None) -> int:
             result = {"ref": ref, "ref_pages": ref_pages["pages"], "amd_pages": amd_pages["pages"], "ref_cold": ref_cold, "ref_switch": ref_switch,
                       "amd": amd, "amd_cold": amd_cold, "amd_switch": amd_switch, "detail": detail,
                       "ref_cold_pages": ref_cold_pages["pages"], "amd_cold_pages": amd_cold_pages["pages"],
-                      "detail_slow": detail_out.get("detailSlow"), **served}
+                      "detail_slow": detail_out.get("detailSlow"), "react": amd_react, **served}
         finally:
             drv.close()
             server.stop()
@@ -268,6 +271,14 @@ def main(argv=None) -> int:
                      "requests": {"amd": result["amd_cold_pages"][pg]["requests"],
                                   "reference": result["ref_cold_pages"][pg]["requests"]}}
                 for pg in pages},
+            # Per page, untimed: the page's view-model mounted in the harness
+            # React through the shipped renderer (src/view/react.js), then
+            # re-rendered after one refresh; elements = host nodes mounted,
+            # html_elements = tags of the IR → HTML render. Bounded by the
+            # pager on GPU Nodes / Metrics, whatever the node count.
+            "render_per_page": {pg: {"mount_ms": round(v["mountMs"], 3), "rerender_ms": round(v["rerenderMs"], 3),
+                                     "elements": v["elements"], "html_elements": v["htmlElements"]}
+                                for pg, v in result["react"].items()},
             # Secondary: every page's data (all telemetry + series) in one cold open.
             "cold_open_p50_ms": {"amd": round(summarize(result["amd_cold"]["latencies"])["p50"], 3),
                                  "reference": round(summarize(result["ref_cold"]["latencies"])["p50"], 3)},

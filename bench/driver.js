@@ -29,11 +29,18 @@ import { createClusterStore } from '../src/api/clusterStore.js';
 import { createMetricsSource } from '../src/api/metrics.js';
 import {
   overviewView, devicePluginsView, nodesView, podsView, metricsView,
-  nodeDetailView, podDetailView, nodeColumns,
+  nodeDetailView, podDetailView, nodeColumns, telemetryScope,
 } from '../src/view/pages.js';
 import { countRows } from '../src/view/ir.js';
 import { renderPage, renderSection } from '../src/view/html.js';
 import { createReferenceSchedule } from './referenceSchedule.js';
+// The harness React (the Node-12 stand-in the spec suite renders the plugin
+// with) and its CommonComponents: the pages are also mounted through the
+// shipped renderer (src/view/react.js) to count elements and time a
+// mount / re-render, next to the IR → HTML figure.
+import * as HarnessReact from '../tests/js/stubs/react.js';
+import * as HarnessCC from '../tests/js/stubs/CommonComponents.js';
+import { createRenderer } from '../src/view/react.js';
 import { PerformanceObserver, performance } from 'perf_hooks';
 
 // Garbage-collection pauses (start, duration in ms, performance.now() clock),
@@ -190,16 +197,49 @@ function renderAll(ctx, mstate) {
 /** The five routes, in sidebar order (src/routes.js). */
 export const PAGES = ['overview', 'devicePlugins', 'nodes', 'pods', 'metrics'];
 
-/** Build and render ONE page (the one whose Refresh was clicked); returns its row count. */
+/** Build ONE page's view-model (the one whose Refresh was clicked), first page of the pager. */
+function pageVm(page, ctx, mstate, pageMetrics) {
+  if (page === 'overview') return overviewView(ctx);
+  if (page === 'devicePlugins') return devicePluginsView(ctx);
+  if (page === 'nodes') return nodesView(ctx, { metrics: pageMetrics, pager: PAGER });
+  if (page === 'pods') return podsView(ctx, { metrics: pageMetrics });
+  return metricsView(ctx, mstate, { pager: PAGER });
+}
+
+/** Build and render ONE page; returns its row count. */
 function renderOne(page, ctx, mstate, pageMetrics) {
-  let vm;
-  if (page === 'overview') vm = overviewView(ctx);
-  else if (page === 'devicePlugins') vm = devicePluginsView(ctx);
-  else if (page === 'nodes') vm = nodesView(ctx, { metrics: pageMetrics });
-  else if (page === 'pods') vm = podsView(ctx, { metrics: pageMetrics });
-  else vm = metricsView(ctx, mstate);
+  const vm = pageVm(page, ctx, mstate, pageMetrics);
   renderPage(vm);
   return countRows(vm).tableRows;
+}
+
+/** The pager state a page opens with (plugin.js usePager). */
+const PAGER = { page: 0, filter: '' };
+
+const harnessView = createRenderer(HarnessReact, HarnessCC);
+
+/** Elements in an HTML string (opening tags). */
+function htmlElements(html) {
+  const m = html.match(/<[a-z]/g);
+  return m ? m.length : 0;
+}
+
+/**
+ * Mount `vm` as the page component renders it (harness React + shipped
+ * renderer), then re-render with `vm2` (the page after a refresh).
+ * @returns {{mountMs: number, rerenderMs: number, elements: number, htmlElements: number}}
+ */
+function reactMeasure(vm, vm2) {
+  const h = HarnessReact.createElement;
+  const t0 = process.hrtime();
+  const r = HarnessReact.render(h(harnessView.Page, { vm: vm }));
+  const mountMs = ms(process.hrtime(t0));
+  const t1 = process.hrtime();
+  r.rerender(h(harnessView.Page, { vm: vm2 }));
+  const rerenderMs = ms(process.hrtime(t1));
+  const elements = r.queryAll(function () { return true; }).length;
+  r.unmount();
+  return { mountMs: mountMs, rerenderMs: rerenderMs, elements: elements, htmlElements: htmlElements(renderPage(vm2)) };
 }
 
 const SNAPSHOT_CSS =
@@ -258,16 +298,34 @@ function amdSchedule(request, clock) {
   const metrics = createMetricsSource({ request: request, onTrace: onTrace, clock: clk });
   const mstate = { metrics: null, fetchError: null, fetching: false, series: null };
   // Per-page metrics state, as each page's own hook holds it (plugin.js):
-  // GPU Nodes → owners + xGMI links ('topology'), GPU Pods → pod→GPU
-  // attribution only, Metrics → per-GPU gauges + series ('gauges'). Cold
-  // open / route switch / the all-pages composite fetch every live series
-  // in one query ('all').
+  // GPU Nodes → owners + xGMI links of the nodes on its first page
+  // ('topology', scoped), GPU Pods → pod→GPU attribution only, Metrics →
+  // cluster totals + per-GPU gauges + series of the nodes on its first page
+  // ('gauges', scoped). Cold open / route switch / the all-pages composite
+  // fetch every live series in one query ('all').
   const pageMetrics = { nodes: null, pods: null };
+  const metricsPage = { metrics: null, fetchError: null, fetching: false, series: null };
   function fetchMetrics(view) {
     return Promise.all([metrics.fetchGpuMetrics(view), metrics.fetchSeries(1800, 30)]).then(function (r) {
       mstate.metrics = r[0];
       mstate.series = r[1];
       mstate.fetchError = r[0] ? null : 'Could not reach Prometheus';
+    });
+  }
+  /** What the page's hook asks for once the node list is there (pages.js telemetryScope). */
+  function scoped(summary) {
+    const t = telemetryScope(store.getSnapshot(), PAGER);
+    return t.scope === undefined ? { opts: undefined, scope: undefined } : { opts: { scope: t.scope, summary: summary }, scope: t.scope };
+  }
+  function fetchNodesPage() {
+    return metrics.fetchGpuMetrics('topology', scoped(false).opts).then(function (m) { pageMetrics.nodes = m; });
+  }
+  function fetchMetricsPage() {
+    const sc = scoped(true);
+    return Promise.all([metrics.fetchGpuMetrics('gauges', sc.opts), metrics.fetchSeries(1800, 30, sc.scope)]).then(function (r) {
+      metricsPage.metrics = r[0];
+      metricsPage.series = r[1];
+      metricsPage.fetchError = r[0] ? null : 'Could not reach Prometheus';
     });
   }
   return {
@@ -279,28 +337,31 @@ function amdSchedule(request, clock) {
     },
     /** One page's Refresh button, as src/plugin.js wires it. */
     refreshPage: function (page) {
-      if (page === 'nodes') {
-        return Promise.all([store.refresh(), metrics.fetchGpuMetrics('topology').then(function (m) { pageMetrics.nodes = m; })]);
-      }
+      if (page === 'nodes') return Promise.all([store.refresh(), fetchNodesPage()]);
       if (page === 'pods') {
         return Promise.all([store.refresh(), metrics.fetchGpuOwners().then(function (m) { pageMetrics.pods = m; })]);
       }
-      if (page === 'metrics') return fetchMetrics('gauges');
+      if (page === 'metrics') return fetchMetricsPage();
       return store.refresh();
     },
     /**
      * One page opened on an empty cache, as src/plugin.js mounts it: the
-     * provider's lists + DeviceConfig request, plus that page's own metrics
-     * hook (none on Overview / Device Plugins), all in one wave.
+     * provider's lists + DeviceConfig request in one wave; GPU Pods adds its
+     * owners query to it; GPU Nodes and Metrics ask for the telemetry of
+     * their first page of nodes once the node list is there (a second wave).
      */
     coldOpenPage: function (page) {
+      // The page's metrics hook is enabled once the provider stops loading
+      // (lists and DeviceConfig answered): pages.js telemetryScope.
+      if (page === 'nodes') return Promise.all([store.loadLists(), store.refresh()]).then(fetchNodesPage);
+      if (page === 'metrics') return Promise.all([store.loadLists(), store.refresh()]).then(fetchMetricsPage);
       const base = [store.loadLists(), store.refresh()];
-      if (page === 'nodes') base.push(metrics.fetchGpuMetrics('topology').then(function (m) { pageMetrics.nodes = m; }));
-      else if (page === 'pods') base.push(metrics.fetchGpuOwners().then(function (m) { pageMetrics.pods = m; }));
-      else if (page === 'metrics') base.push(fetchMetrics('gauges'));
+      if (page === 'pods') base.push(metrics.fetchGpuOwners().then(function (m) { pageMetrics.pods = m; }));
       return Promise.all(base);
     },
     pageMetrics: function (page) { return page in pageMetrics && pageMetrics[page] ? pageMetrics[page] : mstate.metrics; },
+    /** The Metrics page's own state (its hook), for rendering that page. */
+    pageMstate: function () { return metricsPage; },
     /** Route switch: render from the shared store now, revalidate in the background. */
     switchRoute: function () {
       const bg = Promise.all([store.refresh(), fetchMetrics()]);
@@ -339,6 +400,7 @@ function referenceSchedule(request) {
     refreshPage: r.refreshPage,
     coldOpenPage: r.coldOpenPage,
     pageMetrics: function () { return r.metrics(); },
+    pageMstate: function () { return { metrics: r.metrics(), fetchError: r.metrics() ? null : 'unreachable', fetching: false }; },
     ctx: r.snapshot,
     mstate: function () { return { metrics: r.metrics(), fetchError: r.metrics() ? null : 'unreachable', fetching: false }; },
   };
@@ -472,7 +534,7 @@ async function serve(a) {
             const t0 = process.hrtime();
             await s.coldOpenPage(page);
             const t1 = process.hrtime();
-            renderOne(page, s.ctx(), s.mstate(), s.pageMetrics(page));
+            renderOne(page, s.ctx(), page === 'metrics' ? s.pageMstate() : s.mstate(), s.pageMetrics(page));
             renderMs.push(ms(process.hrtime(t1)));
             lat.push(ms(process.hrtime(t0)));
             // observer entries are delivered asynchronously
@@ -537,8 +599,10 @@ async function serve(a) {
         const lat = {};
         const reqs = {};
         const rows = {};
+        const rend = {};
         for (let p = 0; p < PAGES.length; p++) {
           lat[PAGES[p]] = [];
+          rend[PAGES[p]] = [];
           reqs[PAGES[p]] = 0;
         }
         for (let i = 0; i < n; i++) {
@@ -547,14 +611,30 @@ async function serve(a) {
             const before = counter.n;
             const t0 = process.hrtime();
             await L.s.refreshPage(page);
-            rows[page] = renderOne(page, L.s.ctx(), L.s.mstate(), L.s.pageMetrics(page));
+            const t1 = process.hrtime();
+            rows[page] = renderOne(page, L.s.ctx(), page === 'metrics' ? L.s.pageMstate() : L.s.mstate(), L.s.pageMetrics(page));
             lat[page].push(ms(process.hrtime(t0)));
+            rend[page].push(ms(process.hrtime(t1)));
             reqs[page] += counter.n - before;
           }
         }
         out.pages = {};
         for (let p = 0; p < PAGES.length; p++) {
-          out.pages[PAGES[p]] = { latencies: lat[PAGES[p]], requestsPerClick: reqs[PAGES[p]] / n, tableRows: rows[PAGES[p]] };
+          out.pages[PAGES[p]] = {
+            latencies: lat[PAGES[p]], renderMs: rend[PAGES[p]], requestsPerClick: reqs[PAGES[p]] / n, tableRows: rows[PAGES[p]],
+          };
+        }
+        if (c.react) {
+          // Untimed: each page mounted in the harness React, refreshed, re-rendered.
+          out.react = {};
+          for (let p = 0; p < PAGES.length; p++) {
+            const page = PAGES[p];
+            const ms0 = function () { return page === 'metrics' ? L.s.pageMstate() : L.s.mstate(); };
+            const vm = pageVm(page, L.s.ctx(), ms0(), L.s.pageMetrics(page));
+            await L.s.refreshPage(page);
+            const vm2 = pageVm(page, L.s.ctx(), ms0(), L.s.pageMetrics(page));
+            out.react[page] = reactMeasure(vm, vm2);
+          }
         }
       } else if (c.cmd === 'snapshot') {
         // Static HTML of every view (docs/screenshots): same IR → HTML path as

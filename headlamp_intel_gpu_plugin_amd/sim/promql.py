@@ -10,6 +10,9 @@ to serve every query the plugin and the reference-schedule replay issue:
   in either position;
 * binary arithmetic/comparison between scalars and vectors, with
   ``on(...)`` / ``ignoring(...)`` and ``group_left(...)`` / ``group_right(...)``;
+* the set operators ``or and unless`` between vectors (matching on every
+  label but ``__name__``, or on ``on(...)`` / ``ignoring(...)``);
+* ``label_replace(v, "dst", "replacement", "src", "regex")``;
 * number literals (the reference's discovery probe is ``query=1``).
 
 Series are stored either as a deterministic function of time sampled on a
@@ -213,7 +216,10 @@ _DUR = {"s": 1, "m": 60, "h": 3600, "d": 86400, "w": 604800}
 AGGREGATIONS = {"sum", "avg", "max", "min", "count"}
 RANGE_FUNCS = {"rate", "irate", "increase", "avg_over_time", "max_over_time", "min_over_time",
                "sum_over_time", "count_over_time", "last_over_time"}
-BIN_PREC = {"+": 1, "-": 1, "*": 2, "/": 2, "%": 2, "==": 0, "!=": 0, ">": 0, "<": 0, ">=": 0, "<=": 0}
+BIN_PREC = {"+": 1, "-": 1, "*": 2, "/": 2, "%": 2, "==": 0, "!=": 0, ">": 0, "<": 0, ">=": 0, "<=": 0,
+            "and": -1, "unless": -1, "or": -2}
+SET_OPS = {"and", "unless", "or"}
+MIN_PREC = min(BIN_PREC.values())
 
 
 def _tokenize(q: str) -> List[Tuple[str, str]]:
@@ -267,7 +273,7 @@ class _Parser:
         return t
 
     def parse(self):
-        e = self.expr(0)
+        e = self.expr(MIN_PREC)
         self.take("eof")
         return e
 
@@ -275,7 +281,8 @@ class _Parser:
         lhs = self.unary()
         while True:
             k, v = self.peek()
-            if k != "op" or v not in BIN_PREC or BIN_PREC[v] < min_prec:
+            is_op = (k == "op" and v in BIN_PREC) or (k == "ident" and v in SET_OPS)
+            if not is_op or BIN_PREC[v] < min_prec:
                 return lhs
             self.i += 1
             matching = self.vector_matching()
@@ -320,7 +327,7 @@ class _Parser:
             return ("num", float(v))
         if k == "op" and v == "(":
             self.i += 1
-            e = self.expr(0)
+            e = self.expr(MIN_PREC)
             self.take("op", ")")
             return e
         if k == "op" and v == "{":
@@ -328,9 +335,19 @@ class _Parser:
         if k == "ident":
             if v in AGGREGATIONS and self.peek(1)[1] in ("(", "by", "without"):
                 return self.aggregation()
+            if v == "label_replace" and self.peek(1)[1] == "(":
+                self.i += 2
+                arg = self.expr(MIN_PREC)
+                strs = []
+                for _ in range(4):
+                    self.take("op", ",")
+                    raw = self.take("str")[1]
+                    strs.append(bytes(raw[1:-1], "utf-8").decode("unicode_escape"))
+                self.take("op", ")")
+                return ("label_replace", arg, *strs)
             if v in RANGE_FUNCS and self.peek(1)[1] == "(":
                 self.i += 2
-                arg = self.expr(0)
+                arg = self.expr(MIN_PREC)
                 self.take("op", ")")
                 if arg[0] != "sel" or arg[2] is None:
                     raise PromQLError(f"{v}() expects a range vector")
@@ -347,7 +364,7 @@ class _Parser:
             lst = self.label_list()
             by, without = (lst, None) if kw == "by" else (None, lst)
         self.take("op", "(")
-        e = self.expr(0)
+        e = self.expr(MIN_PREC)
         self.take("op", ")")
         if self.peek()[1] in ("by", "without"):
             kw = self.take("ident")[1]
@@ -506,12 +523,57 @@ class Evaluator:
             return ("vector", res)
         if kind == "bin":
             return self._binary(node, t)
+        if kind == "label_replace":
+            return self._label_replace(node, t)
         raise PromQLError(f"cannot evaluate {kind}")
+
+    def _label_replace(self, node, t):
+        _, arg, dst, repl, src, regex = node
+        typ, vec = self.instant(arg, t)
+        if typ != "vector":
+            raise PromQLError("label_replace expects a vector")
+        try:
+            rx = re.compile("^(?:" + regex + ")$")
+        except re.error as e:
+            raise PromQLError(f"bad regex {regex!r}: {e}") from None
+        # Prometheus' $1 / ${1} / ${name} → Python's \g<...>
+        template = re.sub(r"\$\{(\w+)\}|\$(\w+)", lambda m: "\\g<" + (m.group(1) or m.group(2)) + ">", repl)
+        out = []
+        for labels, v in vec:
+            m = rx.match(labels.get(src, ""))
+            if not m:
+                out.append((labels, v))
+                continue
+            value = m.expand(template)
+            nl = dict(labels)
+            if value:
+                nl[dst] = value
+            else:
+                nl.pop(dst, None)
+            out.append((nl, v))
+        return ("vector", out)
+
+    def _set_op(self, op, lv, rv, matching):
+        on = ignoring = None
+        if matching:
+            mode, labels, _ = matching
+            on, ignoring = (labels, None) if mode == "on" else (None, labels)
+        rkeys = {_key(l, on, ignoring) for l, _ in rv}
+        if op == "and":
+            return ("vector", [(l, v) for l, v in lv if _key(l, on, ignoring) in rkeys])
+        if op == "unless":
+            return ("vector", [(l, v) for l, v in lv if _key(l, on, ignoring) not in rkeys])
+        lkeys = {_key(l, on, ignoring) for l, _ in lv}
+        return ("vector", list(lv) + [(l, v) for l, v in rv if _key(l, on, ignoring) not in lkeys])
 
     def _binary(self, node, t):
         _, op, lhs, rhs, matching = node
         lt, lv = self.instant(lhs, t)
         rt, rv = self.instant(rhs, t)
+        if op in SET_OPS:
+            if lt != "vector" or rt != "vector":
+                raise PromQLError(f"set operator {op} needs vectors on both sides")
+            return self._set_op(op, lv, rv, matching)
         is_cmp = op in ("==", "!=", ">", "<", ">=", "<=")
         if lt == "scalar" and rt == "scalar":
             r = _apply(op, lv, rv)

@@ -119,6 +119,11 @@ function num(v) {
   return isFinite(f) ? f : null;
 }
 
+/** A label value, or '' when it is missing or not a string. */
+function labelStr(v) {
+  return typeof v === 'string' ? v : '';
+}
+
 /** A well-formed instant-vector row: `{metric: {...}, value: [ts, "v"]}`. */
 function isRow(row) {
   return !!row && isObject(row.metric) && Array.isArray(row.value);
@@ -149,7 +154,8 @@ export function joinExporterResults(r) {
   const E = SERIES.exporter;
   const map = {};
   function slot(m) {
-    const node = m.hostname || m.node || m.instance || '';
+    // Label values are strings; anything else in a malformed answer is ignored.
+    const node = labelStr(m.hostname) || labelStr(m.node) || labelStr(m.instance);
     const gpu = m.gpu_id !== undefined ? String(m.gpu_id) : '0';
     const k = node + '\u0000' + gpu;
     if (!map[k]) map[k] = emptyGpu(node, gpu, m.instance || '');
@@ -206,7 +212,7 @@ export function joinExporterResults(r) {
       if (!isFinite(src)) continue;
       const k = parseInt(mm[1], 10);
       const dst = k < src ? k : k + 1;
-      const node = m.hostname || m.instance || '';
+      const node = labelStr(m.hostname) || labelStr(m.instance);
       if (!xgmi[node]) xgmi[node] = {};
       const v = num(xr[i].value[1]);
       if (v !== null) xgmi[node][src + '-' + dst] = v / 1e9;
@@ -219,7 +225,7 @@ export function joinExporterResults(r) {
     for (let i = 0; i < lr.length; i++) {
       if (!isRow(lr[i])) continue;
       const m = lr[i].metric;
-      const node = m.hostname || m.instance || '';
+      const node = labelStr(m.hostname) || labelStr(m.instance);
       const v = num(lr[i].value[1]);
       if (v === null || m.gpu_id === undefined || m.peer_gpu_id === undefined) continue;
       if (!links[node]) links[node] = {};
@@ -348,10 +354,97 @@ export const STATIC_GPU_FIELDS = ['powerCapWatts', 'powerCapAssumed', 'vramTotal
  * @param {boolean} [lean]        project onto EXPORTER_LEAN_LABELS (live-only queries of a hostname-keyed exporter)
  * @param {string} [view]         METRIC_VIEWS entry (default 'all')
  */
-export function exporterQuery(withStatic, lean, view) {
+export function exporterQuery(withStatic, lean, view, scope) {
   const names = exporterNames(withStatic, view);
+  if (scope) {
+    // Every row matches the hostname matcher: the live-only query needs no fallback keys.
+    const scopedLabels = withStatic === false ? EXPORTER_LEAN_LABELS : EXPORTER_JOIN_LABELS;
+    return 'max by (' + scopedLabels.join(', ') + ') ({__name__=~"' + names.join('|') + '", ' + hostnameMatcher(scope) + '})';
+  }
   const labels = lean && withStatic === false ? EXPORTER_LEAN_LABELS : EXPORTER_JOIN_LABELS;
   return 'max by (' + labels.join(', ') + ') ({__name__=~"' + names.join('|') + '"})';
+}
+
+/** A regex matching exactly `s` (RE2 metacharacters escaped). */
+export function regexLiteral(s) {
+  return String(s).replace(/[\\.+*?()|[\]{}^$]/g, '\\$&');
+}
+
+/**
+ * `hostname=~"a|b|…"` for the nodes a paged view shows — the label the joins
+ * key GPUs by (Kubernetes node name). An empty scope matches nothing.
+ */
+export function hostnameMatcher(names) {
+  // "." is no valid node name: an empty scope matches nothing (callers skip it anyway).
+  if (!names.length) return 'hostname="."';
+  return 'hostname=~"' + promString(names.map(regexLiteral).join('|')) + '"';
+}
+
+/** Exporter series the cluster totals of the Metrics page summary sum or count. */
+function summaryNames() {
+  const E = SERIES.exporter;
+  return {
+    sum: [E.power, E.powerCap, E.vramUsed, E.vramTotal, E.gfx, E.eccCorrect, E.eccUncorrect],
+    count: [E.power, E.powerCap, E.vramUsed, E.gfx, E.temp, E.tempSlowdown, E.eccUncorrect],
+  };
+}
+
+/**
+ * Cluster totals for the Metrics page summary as server-side aggregates: a
+ * handful of rows whatever the cluster size, instead of every gauge of every
+ * GPU. Each aggregation is tagged with an `agg` label (sum / count / nodes)
+ * so the rows survive `or` next to each other and next to a per-GPU query.
+ */
+export function summaryQuery() {
+  const s = summaryNames();
+  const E = SERIES.exporter;
+  return 'label_replace(sum by (__name__) ({__name__=~"' + s.sum.join('|') + '"}), "agg", "sum", "", "")' +
+    ' or label_replace(count by (__name__) ({__name__=~"' + s.count.join('|') + '"}), "agg", "count", "", "")' +
+    ' or label_replace(count by (__name__) (count by (__name__, hostname) ({__name__="' + E.power + '"})), "agg", "nodes", "", "")';
+}
+
+/**
+ * Rows of a summaryQuery answer (those with an `agg` label) → the shape of
+ * summarizeMetrics plus `nodes` (nodes reporting); null when there are none.
+ */
+export function totalsFromRows(rows) {
+  const E = SERIES.exporter;
+  const sum = {};
+  const cnt = {};
+  let nodes = 0;
+  let any = false;
+  for (let i = 0; i < rows.length; i++) {
+    const row = rows[i];
+    if (!isRow(row) || typeof row.metric.agg !== 'string') continue;
+    const v = num(row.value[1]);
+    if (v === null) continue;
+    const name = row.metric.__name__;
+    any = true;
+    if (row.metric.agg === 'sum') sum[name] = v;
+    else if (row.metric.agg === 'count') cnt[name] = v;
+    else if (row.metric.agg === 'nodes' && name === E.power) nodes = v;
+  }
+  if (!any) return null;
+  const c = function (n) { return cnt[n] || 0; };
+  const s = function (n) { return sum[n] || 0; };
+  const gpus = c(E.power);
+  const capAssumed = Math.max(0, gpus - c(E.powerCap));
+  const eccGpus = c(E.eccUncorrect);
+  return {
+    gpus: gpus,
+    withPower: gpus,
+    nodes: nodes,
+    powerWatts: s(E.power),
+    // GPUs without a cap series get the MI355X board limit, as in the per-GPU join.
+    powerCapWatts: s(E.powerCap) + capAssumed * MI355X.tdpWatts,
+    vramUsedBytes: s(E.vramUsed) * SERIES.exporterVramUnitBytes,
+    vramTotalBytes: s(E.vramTotal) * SERIES.exporterVramUnitBytes,
+    avgGfxActivityPct: c(E.gfx) ? s(E.gfx) / c(E.gfx) : null,
+    eccCorrectable: eccGpus ? s(E.eccCorrect) : null,
+    eccUncorrectable: eccGpus ? s(E.eccUncorrect) : null,
+    powerCapAssumed: capAssumed,
+    tempLimitAssumed: Math.max(0, c(E.temp) - c(E.tempSlowdown)),
+  };
 }
 
 /**
@@ -461,17 +554,39 @@ export function seriesQuery() {
   return 'sum by (__name__, hostname) ({__name__=~"' + E.power + '|' + E.vramUsed + '"})';
 }
 
+/**
+ * Power + HBM-used history of the nodes a paged view shows (`hostname=~`)
+ * plus the cluster-wide total (tagged `scope="cluster"`): O(visible nodes ×
+ * points) whatever the cluster size.
+ */
+export function scopedSeriesQuery(scope) {
+  const E = SERIES.exporter;
+  const names = '__name__=~"' + E.power + '|' + E.vramUsed + '"';
+  return 'sum by (__name__, hostname) ({' + names + ', ' + hostnameMatcher(scope) + '})' +
+    ' or label_replace(sum by (__name__) ({' + names + '}), "scope", "cluster", "", "")';
+}
+
+/** Key of the cluster-wide line in a scoped series answer (no node name can be this). */
+export const TOTAL_SERIES = '\u0000cluster';
+
 /** Split a combined result into `name → rows` (xGMI rows under `__xgmi`). */
 export function splitByName(result) {
   // No prototype: a series named e.g. "__proto__" is a plain key here.
   const out = Object.create(null);
   out.__xgmi = [];
+  // Cluster aggregates (summaryQuery) carry an `agg` label and share metric
+  // names with the per-GPU rows: kept apart so no join mistakes one for a GPU.
+  out.__agg = [];
   const N = SERIES.nodeExporter;
   const xre = new RegExp('^' + SERIES.exporter.xgmiRe + '$');
   for (let i = 0; i < result.length; i++) {
     const row = result[i];
     const m = row && row.metric;
     if (!isObject(m)) continue;
+    if (typeof m.agg === 'string') {
+      out.__agg.push(row);
+      continue;
+    }
     const name = typeof m.__name__ === 'string' ? m.__name__ : '';
     if (xre.test(name)) {
       out.__xgmi.push(row);
@@ -626,6 +741,8 @@ export function createMetricsSource(opts) {
     links = null;
     statics = null;
     lastBy = {};
+    scopeStatic = {};
+    scopedState = new Map();
     for (const k in nodeStates) delete nodeStates[k];
   }
 
@@ -694,10 +811,168 @@ export function createMetricsSource(opts) {
    * @param {string} [view]
    * @returns {Promise<GpuMetrics|null>}
    */
-  function fetchGpuMetrics(view) {
+  function fetchGpuMetrics(view, opts) {
     const v = view === undefined ? 'all' : view;
     if (METRIC_VIEWS.indexOf(v) < 0) return Promise.reject(new Error('fetchGpuMetrics: unknown view ' + JSON.stringify(view)));
-    return shared('gpus|' + v, function () { return gpuSnapshot(v); });
+    const scope = opts && Array.isArray(opts.scope) ? opts.scope.map(String) : null;
+    if (!scope) return shared('gpus|' + v, function () { return gpuSnapshot(v); });
+    const summary = !!opts.summary;
+    const key = v + '|' + (summary ? 'sum' : '') + '|' + scope.join(',');
+    return shared('scoped|' + key, function () { return scopedSnapshot(v, scope, summary, key); });
+  }
+
+  // ---- Scoped snapshots (paged views: the GPU nodes on screen) -------------
+
+  // node → {at, statics: gpuKey → static fields, links}: static series of the
+  // nodes a paged view has shown, re-read per node every `ttl`.
+  let scopeStatic = {};
+  // scoped key → {last, failures}; the most recent SCOPED_KEYS kept.
+  let scopedState = new Map();
+  const SCOPED_KEYS = 16;
+
+  function scopedEntry(key) {
+    let e = scopedState.get(key);
+    if (e) {
+      scopedState.delete(key); // most recently used last
+    } else {
+      e = { last: null, failures: 0 };
+    }
+    scopedState.set(key, e);
+    if (scopedState.size > SCOPED_KEYS) scopedState.delete(scopedState.keys().next().value);
+    return e;
+  }
+
+  function scopeNeedsStatic(scope) {
+    const now = clock.now();
+    for (let i = 0; i < scope.length; i++) {
+      const e = scopeStatic[scope[i]];
+      if (!e || now - e.at >= ttl) return true;
+    }
+    return false;
+  }
+
+  /**
+   * Telemetry of the GPU nodes a paged view shows (`scope`: Kubernetes node
+   * names = exporter `hostname`), plus the cluster totals when `summary`: one
+   * request whose size follows the page, not the cluster — `hostname=~` on
+   * the per-GPU series, server-side aggregates for the totals (summaryQuery),
+   * joined with `or`. A node-exporter source (no `hostname` label) or a
+   * first query that finds no exporter series falls back to the cluster-wide
+   * snapshot cut to the scope. Stale / null handling as in the cluster-wide
+   * path, per scope.
+   */
+  function scopedSnapshot(v, scope, summary, key) {
+    const st = scopedEntry(key);
+    if (source === 'node-exporter') return clusterCut(v, scope, summary, key);
+    return withPrometheus(function (base) {
+      const withStatic = scope.length > 0 && scopeNeedsStatic(scope);
+      const parts = [];
+      if (scope.length) parts.push(exporterQuery(withStatic, true, v, scope));
+      if (summary) parts.push(summaryQuery());
+      if (!parts.length) return Promise.resolve(scopedResult(st, base, null, { gpus: [], xgmi: {}, links: {} }, scope, undefined, v));
+      const q = parts.join(' or ');
+      return combined(base, q).then(function (res) {
+        if (!res.ok) return UNREACHABLE;
+        st.failures = 0;
+        const rows = res.rows;
+        const j = joinExporterResults(rows);
+        const totals = summary ? totalsFromRows(rows.__agg) : undefined;
+        const found = j.gpus.length > 0 || (!!totals && totals.gpus > 0);
+        // Nothing from the exporter yet: maybe node-exporter feeds this
+        // Prometheus (no hostname label) — ask cluster-wide once to find out.
+        if (!found && source !== 'amd-exporter') return NOT_SCOPED;
+        if (found) source = 'amd-exporter';
+        const now = clock.now();
+        if (withStatic) {
+          const per = {};
+          for (let i = 0; i < scope.length; i++) per[scope[i]] = {};
+          const sts = staticsOf(j.gpus);
+          for (let i = 0; i < j.gpus.length; i++) {
+            const g = j.gpus[i];
+            if (!per[g.nodeName]) per[g.nodeName] = {};
+            per[g.nodeName][gpuKey(g)] = sts[gpuKey(g)];
+          }
+          for (const n in per) scopeStatic[n] = { at: now, statics: per[n], links: (j.links && j.links[n]) || {} };
+        } else {
+          const merged = {};
+          const links = {};
+          for (let i = 0; i < scope.length; i++) {
+            const e = scopeStatic[scope[i]];
+            if (!e) continue;
+            for (const k in e.statics) merged[k] = e.statics[k];
+            if (Object.keys(e.links).length) links[scope[i]] = e.links;
+          }
+          for (let i = 0; i < j.gpus.length; i++) {
+            // A GPU the static copy does not know yet: re-read its node's statics next time.
+            if (!merged[gpuKey(j.gpus[i])] && scopeStatic[j.gpus[i].nodeName]) scopeStatic[j.gpus[i].nodeName].at = -Infinity;
+          }
+          applyStatics(j.gpus, merged);
+          j.links = links;
+        }
+        return scopedResult(st, base, q, j, scope, totals, v);
+      });
+    }, function () {
+      st.failures++;
+      if (st.last && st.failures < STALE_FAILURES) return Object.assign({}, st.last, { stale: true });
+      st.last = null;
+      return null;
+    }).then(function (r) { return r === NOT_SCOPED ? clusterCut(v, scope, summary, key) : r; });
+  }
+
+  function scopedResult(st, base, q, j, scope, totals, v) {
+    const prev = st.last;
+    st.last = {
+      source: source,
+      view: v,
+      gpus: prev ? shareGpus(prev.gpus, j.gpus) : j.gpus,
+      xgmi: prev ? shareMap(prev.xgmi, j.xgmi) : j.xgmi,
+      links: prev ? shareMap(prev.links, j.links || {}) : j.links || {},
+      fetchedAt: new Date(clock.now()).toISOString(),
+      prometheusPath: base,
+      query: q,
+      scope: scope,
+      totals: totals && prev && prev.totals && sameValue(prev.totals, totals) ? prev.totals : totals,
+    };
+    return st.last;
+  }
+
+  /** The cluster-wide snapshot cut to `scope` (node-exporter source; exporter not found by a scoped query). */
+  function clusterCut(v, scope, summary, key) {
+    return fetchGpuMetrics(v).then(function (m) {
+      if (!m) return null;
+      const st = scopedEntry(key);
+      if (st.cutOf === m && st.last) return st.last;
+      const inScope = {};
+      for (let i = 0; i < scope.length; i++) inScope[scope[i]] = true;
+      const xgmi = {};
+      const links = {};
+      for (let i = 0; i < scope.length; i++) {
+        if (m.xgmi && m.xgmi[scope[i]]) xgmi[scope[i]] = m.xgmi[scope[i]];
+        if (m.links && m.links[scope[i]]) links[scope[i]] = m.links[scope[i]];
+      }
+      let totals;
+      if (summary) {
+        const seen = {};
+        let nodes = 0;
+        for (let i = 0; i < m.gpus.length; i++) {
+          if (!seen[m.gpus[i].nodeName]) {
+            seen[m.gpus[i].nodeName] = true;
+            nodes++;
+          }
+        }
+        totals = Object.assign(summarizeMetrics(m), { nodes: nodes });
+      }
+      const out = Object.assign({}, m, {
+        gpus: m.gpus.filter(function (g) { return inScope[g.nodeName] === true; }),
+        xgmi: xgmi,
+        links: links,
+        scope: scope,
+        totals: totals,
+      });
+      st.cutOf = m;
+      st.last = out;
+      return out;
+    });
   }
 
   function gpuSnapshot(v) {
@@ -892,7 +1167,8 @@ export function createMetricsSource(opts) {
           if (!res[i] || !isObject(res[i].metric) || !Array.isArray(res[i].values)) continue;
           const m = res[i].metric;
           const name = typeof m.__name__ === 'string' ? m.__name__ : '';
-          const node = typeof m.hostname === 'string' && m.hostname ? m.hostname : typeof m.instance === 'string' && m.instance ? m.instance : 'cluster';
+          const node = m.scope === 'cluster' ? TOTAL_SERIES
+            : typeof m.hostname === 'string' && m.hostname ? m.hostname : typeof m.instance === 'string' && m.instance ? m.instance : 'cluster';
           // Only [t, v] pairs; a malformed point is dropped, not propagated.
           const vals = res[i].values.filter(function (p) { return Array.isArray(p) && p.length >= 2; });
           if (!out[name]) out[name] = Object.create(null);
@@ -914,20 +1190,27 @@ export function createMetricsSource(opts) {
    * are requested — and none at all until the next step boundary.
    * @returns {Promise<{ rangeSec: number, power: Record<string, Array<[number, number]>>, vram: Record<string, Array<[number, number]>> } | null>}
    */
-  function fetchSeries(rangeSec, stepSec) {
+  function fetchSeries(rangeSec, stepSec, scope) {
     const range = rangeSec || 1800;
     const step = stepSec || 30;
     const E = SERIES.exporter;
     const parts = [['power', E.power, 1], ['vram', E.vramUsed, SERIES.exporterVramUnitBytes]];
+    const scoped = Array.isArray(scope);
+    const sk = scoped ? scope.map(String).join(',') : null;
+    const q = scoped ? scopedSeriesQuery(scope.map(String)) : seriesQuery();
     function from(base) {
       const end = Math.floor(clock.now() / 1000 / step) * step;
       const fresh = !seriesCache || seriesCache.range !== range || seriesCache.step !== step ||
-        seriesCache.base !== base || end - seriesCache.end >= range;
+        seriesCache.base !== base || seriesCache.scope !== sk || end - seriesCache.end >= range;
       const start = fresh ? end - range : seriesCache.end + step;
       if (!fresh && start > end) return Promise.resolve(seriesCache.data);
-      return rangeQuery(base, seriesQuery(), start, end, step).then(function (got) {
+      return rangeQuery(base, q, start, end, step).then(function (got) {
         if (got === UNREACHABLE) return UNREACHABLE;
         const data = { rangeSec: range, stepSec: step };
+        if (scoped) {
+          data.scope = scope.map(String);
+          data.total = {};
+        }
         const cutoff = end - range;
         for (let i = 0; i < parts.length; i++) {
           const key = parts[i][0];
@@ -937,19 +1220,26 @@ export function createMetricsSource(opts) {
           const merged = {};
           const nodes = Object.keys(Object.assign({}, prev, rows));
           for (let n = 0; n < nodes.length; n++) {
+            if (nodes[n] === TOTAL_SERIES) continue;
             const add = (rows[nodes[n]] || []).map(function (v) { return [Number(v[0]), (num(v[1]) || 0) * scale]; });
             const pts = (prev[nodes[n]] || []).concat(add).filter(function (p) { return p[0] >= cutoff; });
             if (pts.length) merged[nodes[n]] = pts;
           }
           data[key] = merged;
+          if (scoped) {
+            // The cluster-wide line (peak / average over the whole cluster).
+            const add = (rows[TOTAL_SERIES] || []).map(function (v) { return [Number(v[0]), (num(v[1]) || 0) * scale]; });
+            const prevTotal = fresh ? [] : (seriesCache.data.total && seriesCache.data.total[key]) || [];
+            data.total[key] = prevTotal.concat(add).filter(function (p) { return p[0] >= cutoff; });
+          }
         }
-        seriesCache = { range: range, step: step, end: end, base: base, data: data };
+        seriesCache = { range: range, step: step, end: end, base: base, scope: sk, data: data };
         return data;
       });
     }
-    // A failed range request keeps the last window (retried next time).
-    return shared('series|' + range + '|' + step, function () {
-      return withPrometheus(from, function () { return seriesCache ? seriesCache.data : null; });
+    // A failed range request keeps the last window of the same scope (retried next time).
+    return shared('series|' + range + '|' + step + '|' + sk, function () {
+      return withPrometheus(from, function () { return seriesCache && seriesCache.scope === sk ? seriesCache.data : null; });
     });
   }
 

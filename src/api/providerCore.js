@@ -240,25 +240,37 @@ export function createProviderCore(React, lib, deps) {
   }
 
   /**
-   * Cluster-wide GPU telemetry (+ power/HBM series when `withSeries`) of the
-   * series `view` draws (metrics.js METRIC_VIEWS: 'gauges' for the Metrics
-   * page, 'topology' for GPU Nodes, default 'all').
+   * GPU telemetry (+ power/HBM series when `withSeries`) of the series `view`
+   * draws (metrics.js METRIC_VIEWS: 'gauges' for the Metrics page, 'topology'
+   * for GPU Nodes, default 'all').
+   *
+   * `scope` (optional) is the list of GPU node names the page shows (a paged
+   * view, pages.js nodePage): telemetry and series are then fetched for those
+   * nodes only, and on the 'gauges' view with the cluster totals as
+   * server-side aggregates — O(page) bytes on any cluster. Without `scope`
+   * the whole cluster is fetched (terminal client, small clusters).
+   *
    * Unlike the reference it does not wait for the cluster context to finish
    * loading (MetricsPage.tsx:203-205): the two are independent and fetched in
-   * parallel.
+   * parallel (with a scope, the page's node names come from the node list;
+   * an empty scope still fetches the totals).
    */
-  function useGpuMetrics(enabled, withSeries, view) {
+  function useGpuMetrics(enabled, withSeries, view, scope) {
     const on = enabled === undefined ? true : enabled;
     const series = withSeries === undefined ? true : withSeries;
     const v = view || 'all';
     const cluster = clusterKey();
     const source = metricsSourceFor(cluster);
     const settings = loadSettings();
-    const key = 'gpus|' + sourceKey(cluster, settings) + '|' + v + '|' + series + '|' + settings.seriesMinutes;
+    const scoped = Array.isArray(scope);
+    const names = scoped ? scope.slice() : null;
+    const key = 'gpus|' + sourceKey(cluster, settings) + '|' + v + '|' + series + '|' + settings.seriesMinutes +
+      (scoped ? '|scope:' + names.join(',') : '');
     return useMetricsFetch(on ? key : null, function () {
+      const opts = scoped ? { scope: names, summary: v === 'gauges' } : undefined;
       return Promise.all([
-        source.fetchGpuMetrics(v),
-        series ? source.fetchSeries(settings.seriesMinutes * 60, seriesStepSec(settings)) : Promise.resolve(null),
+        source.fetchGpuMetrics(v, opts),
+        series ? source.fetchSeries(settings.seriesMinutes * 60, seriesStepSec(settings), names || undefined) : Promise.resolve(null),
       ]);
     }, false, source);
   }

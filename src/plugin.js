@@ -30,6 +30,7 @@ import {
   overviewView,
   podDetailView,
   podsView,
+  telemetryScope,
 } from './view/pages.js';
 import { createRenderer } from './view/react.js';
 import { createSettingsPage } from './view/settingsPage.js';
@@ -69,19 +70,40 @@ export function createPlugin(env) {
   }
 
   /**
+   * Pager state of a paged page (GPU Nodes, Metrics): {page, filter}. A new
+   * filter starts again at the first page.
+   */
+  function usePager() {
+    const st = React.useState({ page: 0, filter: '' });
+    const pg = st[0];
+    const setPg = st[1];
+    return {
+      state: pg,
+      onPage: function (p) { setPg(function (s) { return { page: p, filter: s.filter }; }); },
+      onFilter: function (f) { setPg({ page: 0, filter: f }); },
+    };
+  }
+
+  /**
    * MI355X nodes: summary table, per-node cards with the per-GPU allocation
-   * strip and the xGMI matrix (reference NodesPage.tsx, C7). Exporter
-   * telemetry (no time series: this page draws none) upgrades the strip to
-   * exact pod→GPU ownership and overlays measured xGMI throughput.
+   * strip and the xGMI matrix (reference NodesPage.tsx, C7), one page of
+   * nodes at a time. Exporter telemetry of the nodes on the page (no time
+   * series: this page draws none) upgrades the strip to exact pod→GPU
+   * ownership and overlays measured xGMI throughput.
    */
   function NodesPage() {
     const ctx = core.useAmdGpuContext();
-    const m = core.useGpuMetrics(true, false, 'topology');
+    const pager = usePager();
+    const t = telemetryScope(ctx, pager.state);
+    const m = core.useGpuMetrics(t.enabled, false, 'topology', t.scope);
     function refresh() {
       ctx.refresh();
       m.refresh();
     }
-    return h(Page, { vm: nodesView(ctx, { metrics: m.metrics }), onRefresh: refresh });
+    return h(Page, {
+      vm: nodesView(ctx, { metrics: m.metrics, pager: pager.state }), onRefresh: refresh,
+      onPage: pager.onPage, onFilter: pager.onFilter,
+    });
   }
 
   /**
@@ -99,11 +121,20 @@ export function createPlugin(env) {
     return h(Page, { vm: podsView(ctx, { metrics: m.metrics }), onRefresh: refresh });
   }
 
-  /** Power, HBM, activity, temperature, RAS and xGMI telemetry from Prometheus (reference MetricsPage.tsx, C9). */
+  /**
+   * Power, HBM, activity, temperature, RAS and xGMI telemetry from Prometheus
+   * (reference MetricsPage.tsx, C9): cluster totals as server-side
+   * aggregates, per-node cards and series for one page of GPU nodes.
+   */
   function MetricsPage() {
     const ctx = core.useAmdGpuContext();
-    const m = core.useGpuMetrics(true, true, 'gauges');
-    return h(Page, { vm: metricsView(ctx, m), onRefresh: m.refresh });
+    const pager = usePager();
+    const t = telemetryScope(ctx, pager.state);
+    const m = core.useGpuMetrics(t.enabled, true, 'gauges', t.scope);
+    return h(Page, {
+      vm: metricsView(ctx, m, { pager: pager.state }), onRefresh: m.refresh,
+      onPage: pager.onPage, onFilter: pager.onFilter,
+    });
   }
 
   // -------------------------------------------------------------------------

@@ -12,7 +12,7 @@
  * (src/components/View.tsx).
  */
 
-import { matrixCaption } from './ir.js';
+import { matrixCaption, pagerText } from './ir.js';
 
 const NEEDS_ESC = /[&<>"]/;
 
@@ -134,6 +134,15 @@ export function renderSection(s) {
   return h;
 }
 
+/** Pager → <nav>: the range shown, the name filter and previous / next buttons. */
+export function renderPager(p) {
+  return '<nav data-testid="pager" data-page="' + p.page + '" data-pages="' + p.pages + '" data-total="' + p.total + '">' +
+    '<input aria-label="Filter ' + esc(p.noun) + ' by name" value="' + esc(p.filter) + '">' +
+    '<span>' + esc(pagerText(p)) + '</span>' +
+    '<button aria-label="Previous page"' + (p.page > 0 ? '' : ' disabled') + '>‹</button>' +
+    '<button aria-label="Next page"' + (p.page + 1 < p.pages ? '' : ' disabled') + '>›</button></nav>';
+}
+
 export function renderPage(vm) {
   let h = '';
   if (vm.title) {
@@ -147,6 +156,7 @@ export function renderPage(vm) {
   for (let i = 0; i < vm.items.length; i++) {
     const it = vm.items[i];
     if (it.t === 'loader') h += '<div data-testid="loader">' + esc(it.title) + '</div>';
+    else if (it.t === 'pager') h += renderPager(it);
     else h += renderSection(it);
   }
   return h;

@@ -134,6 +134,24 @@ export interface LoaderItem {
   title: string;
 }
 
+/** Page-level pager over a long list (GPU nodes): the slice shown and the name filter. */
+export interface PagerItem {
+  t: 'pager';
+  key: 'pager';
+  /** what is counted, e.g. "GPU nodes" */
+  noun: string;
+  /** 0-based */
+  page: number;
+  pages: number;
+  /** slice [from, to) of the matching list */
+  from: number;
+  to: number;
+  total: number;
+  matched: number;
+  filter: string;
+  perPage: number;
+}
+
 export interface RefreshButton {
   label: string;
   ariaLabel: string;
@@ -145,7 +163,7 @@ export interface PageVM {
   /** null while the page is only a loader */
   title: string | null;
   refresh: RefreshButton | null;
-  items: Array<Section | LoaderItem>;
+  items: Array<Section | LoaderItem | PagerItem>;
 }
 
 export function status(st: Status, text: string | number): StatusCell;
@@ -157,7 +175,14 @@ export function table(columns: string[], rows: Cell[][], keys?: string[]): Table
 export function pctbar(label: string, data: PctbarDatum[], total: number): PctbarBlock;
 export function section(title: string, blocks: Block[], key?: string): Section;
 export function loader(title: string): LoaderItem;
-export function page(title: string | null, refresh: RefreshButton | null, items: Array<Section | LoaderItem>): PageVM;
+export function page(title: string | null, refresh: RefreshButton | null, items: Array<Section | LoaderItem | PagerItem>): PageVM;
+export function pager(
+  p: { page: number; pages: number; from: number; to: number; total: number; matched: number; filter: string; perPage: number },
+  noun: string
+): PagerItem;
+/** "Showing 17–24 of 1000 GPU nodes · page 3 of 125" */
+export function pagerText(p: PagerItem): string;
+export function pagerOf(vm: PageVM | null): PagerItem | null;
 
 export interface Memo {
   /** `now` (epoch ms): also hold the value only until the first age label inside it changes. */

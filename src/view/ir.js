@@ -55,6 +55,29 @@ export function loader(title) {
 }
 
 /**
+ * Page-level pager over a long list (GPU nodes): which slice is shown, and
+ * the name filter that selected it. A page item, not a section block, so the
+ * renderer can wire its buttons to the page's own state.
+ * @param {{page: number, pages: number, from: number, to: number, total: number, matched: number,
+ *          filter: string, perPage: number}} p
+ * @param {string} noun  what is counted ("GPU nodes")
+ */
+export function pager(p, noun) {
+  return {
+    t: 'pager', key: 'pager', noun: noun, page: p.page, pages: p.pages, from: p.from, to: p.to,
+    total: p.total, matched: p.matched, filter: p.filter, perPage: p.perPage,
+  };
+}
+
+/** "Showing 17–32 of 1000 GPU nodes" (with the filter's match count when one is set). */
+export function pagerText(p) {
+  const f = p.filter ? p.filter.trim() : '';
+  const of = f ? p.matched + ' matching "' + f + '" (' + p.total + ' ' + p.noun + ')' : p.total + ' ' + p.noun;
+  if (p.matched === 0) return 'No ' + p.noun + (f ? ' match "' + f + '"' : '');
+  return 'Showing ' + (p.from + 1) + '–' + p.to + ' of ' + of + (p.pages > 1 ? ' · page ' + (p.page + 1) + ' of ' + p.pages : '');
+}
+
+/**
  * @param {string|null} title  page header (null while the page is only a loader)
  * @param {{label: string, ariaLabel: string, disabled: boolean}|null} refresh
  * @param {any[]} items
@@ -195,6 +218,13 @@ export function sectionTitles(vm) {
 export function findSection(vm, title) {
   const ss = sections(vm);
   for (let i = 0; i < ss.length; i++) if (ss[i].title === title) return ss[i];
+  return null;
+}
+
+/** The page's pager item, or null. */
+export function pagerOf(vm) {
+  if (!vm || !vm.items) return null;
+  for (let i = 0; i < vm.items.length; i++) if (vm.items[i].t === 'pager') return vm.items[i];
   return null;
 }
 

@@ -70,7 +70,7 @@ import {
 } from '../api/amdgpu.js';
 import { buildGpuSlots, buildXgmiMatrix, isFullMesh } from '../api/topology.js';
 import { PROMETHEUS_SERVICES, clusterPowerStats, summarizeMetrics } from '../api/metrics.js';
-import { bar, createMemo, createObjectCache, kv, lines, loader, noteExpiry, page, pctbar, row, section, status, table } from './ir.js';
+import { bar, createMemo, createObjectCache, kv, lines, loader, noteExpiry, page, pager, pctbar, row, section, status, table } from './ir.js';
 
 export const BRAND = 'AMD GPU';
 
@@ -520,6 +520,70 @@ function devicePluginsItems(ctx, now) {
 // Nodes (reference NodesPage.tsx:145-293)
 // ---------------------------------------------------------------------------
 
+/** GPU nodes per page on the GPU Nodes and Metrics pages. */
+export const NODES_PER_PAGE = 8;
+
+function nodeNameOf(n) {
+  return typeof n === 'string' ? n : n.metadata.name;
+}
+
+/**
+ * The slice of GPU nodes a paged view shows: `state` = {page, filter,
+ * perPage} (page 0-based, clamped; filter a case-insensitive substring of the
+ * node name). Memoised on the node list's identity, so the same state over
+ * the same list returns the same object (and the same `nodes` array) — the
+ * page's memos and the metrics hook's scope key stay put between refreshes.
+ *
+ * The reference renders one card per GPU node with no cap (NodesPage.tsx:
+ * 285-291; its Metrics page one card per chip, MetricsPage.tsx:348-350): at
+ * 1,000 nodes that is thousands of cards and every node's telemetry per
+ * refresh. Here a page holds NODES_PER_PAGE nodes and fetches their
+ * telemetry only.
+ * @returns {{nodes: any[], names: string[], page: number, pages: number, from: number, to: number,
+ *            total: number, matched: number, filter: string, perPage: number}}
+ */
+export function nodePage(gpuNodes, state) {
+  const st = state || {};
+  const per = st.perPage > 0 ? Math.min(Math.floor(st.perPage), 200) : NODES_PER_PAGE;
+  // The raw text is kept for the input box; matching ignores surrounding spaces.
+  const filter = typeof st.filter === 'string' ? st.filter : '';
+  const all = gpuNodes || NO_PODS;
+  const want = Math.max(0, Math.floor(st.page) || 0);
+  return memo('node-page:' + per + '|' + want + '|' + filter, [all], function () {
+    const f = filter.trim().toLowerCase();
+    const list = f ? all.filter(function (n) { return nodeNameOf(n).toLowerCase().indexOf(f) >= 0; }) : all;
+    const pages = Math.max(1, Math.ceil(list.length / per));
+    const pg = Math.min(want, pages - 1);
+    const from = pg * per;
+    const to = Math.min(list.length, from + per);
+    const nodes = list.slice(from, to);
+    return {
+      nodes: nodes, names: nodes.map(nodeNameOf), page: pg, pages: pages, from: from, to: to,
+      total: all.length, matched: list.length, filter: filter, perPage: per,
+    };
+  });
+}
+
+/** Names of the GPU nodes a paged view shows ([] while the node list is loading). */
+export function visibleNodeNames(ctx, state) {
+  if (!ctx || ctx.loading || !ctx.gpuNodes) return [];
+  return nodePage(ctx.gpuNodes, state).names;
+}
+
+/**
+ * What a paged page asks Prometheus for: `{enabled: false}` while the node
+ * list is loading (the page's node names are not known yet — one wave after
+ * the lists instead of a cluster-wide one before them); the names on the page
+ * once it is listed; cluster-wide (`scope` undefined) when the node list
+ * failed (e.g. RBAC denies listing nodes), so telemetry still shows.
+ * @returns {{enabled: boolean, scope: (string[]|undefined)}}
+ */
+export function telemetryScope(ctx, state) {
+  if (!ctx || ctx.loading) return { enabled: false, scope: [] };
+  if (ctx.error && (!ctx.gpuNodes || ctx.gpuNodes.length === 0)) return { enabled: true, scope: undefined };
+  return { enabled: true, scope: nodePage(ctx.gpuNodes, state).names };
+}
+
 /** Per-GPU allocation strip block. */
 export function slotsBlock(node, podsOnNode, owners) {
   const s = buildGpuSlots(node, podsOnNode, owners);
@@ -602,26 +666,29 @@ export function nodesView(ctx, opts) {
   const now = nowOf(opts);
   const metrics = opts && opts.metrics ? opts.metrics : null;
   if (ctx.loading) return page(null, null, [loader('Loading GPU node data...')]);
+  // One page of nodes (NODES_PER_PAGE, name filter): the summary rows, the
+  // cards and the telemetry the page asks for are all O(page), not O(cluster).
+  const pg = nodePage(ctx.gpuNodes, opts && opts.pager);
   // Live node power (the GPU Nodes query carries the power gauge for pod
   // attribution anyway): "watts|cap" per node, whole watts, so the head and
   // its rows rebuild only when a shown value changes.
   const power = nodePowerKeys(metrics);
-  const head = memo('nodes-head', [ctx.gpuNodes, ctx.index, ctx.error, power.sig], function () {
-    return nodesHeadItems(ctx, now, power.byNode);
+  const head = memo('nodes-head', [pg, ctx.index, ctx.error, power.sig], function () {
+    return nodesHeadItems(ctx, now, power.byNode, pg);
   }, now);
   const owners = ownersByNode(metrics);
   const xgmi = metrics ? metrics.xgmi : undefined;
   const links = metrics ? metrics.links : undefined;
   // The card list as a whole holds while no input changed (most watch events
   // touch no GPU node or pod); otherwise only changed cards are rebuilt.
-  const items = memo('nodes-cards', [head, ctx.gpuNodes, ctx.index, owners, xgmi, links], function () {
+  const items = memo('nodes-cards', [head, pg, ctx.index, owners, xgmi, links], function () {
     const idx = ctx.index;
     function inputs(n) {
       const name = n.metadata.name;
       return [idx.podsByNode.get(name) || NO_PODS, idx.nodeStats.get(name), owners[name],
         xgmi ? xgmi[name] : undefined, links ? links[name] : undefined];
     }
-    const cards = chunkedRows('node-cards', ctx.gpuNodes, [], function (n) {
+    const cards = chunkedRows('node-cards', pg.nodes, [], function (n) {
       const name = n.metadata.name;
       const d = inputs(n);
       const pods = d[0];
@@ -772,7 +839,7 @@ function nodePowerCell(key) {
   return powerBar(Number(parts[0]), cap > 0 ? cap : null);
 }
 
-function nodesHeadItems(ctx, now, powerByNode) {
+function nodesHeadItems(ctx, now, powerByNode, pg) {
   const pw = powerByNode || {};
   const withPower = Object.keys(pw).length > 0;
   const items = [];
@@ -791,16 +858,18 @@ function nodesHeadItems(ctx, now, powerByNode) {
         ]),
       ])
     );
+    return items;
   }
 
+  items.push(pager(pg, 'GPU nodes'));
   const idx = ctx.index;
-  if (ctx.gpuNodes.length > 0) {
+  if (pg.nodes.length > 0) {
     items.push(
       section('GPU Node Summary', [
         table(
           // "Power" (beyond the reference): the node's GPUs' live power against their summed cap.
           ['Node', 'Ready', 'GPU Model', 'GPU Devices', 'Allocation', 'GPU Pods'].concat(withPower ? ['Power'] : [], ['Age']),
-          chunkedRows('node-summary-rows', ctx.gpuNodes, [withPower], function (n) {
+          chunkedRows('node-summary-rows', pg.nodes, [withPower], function (n) {
             const st = idx.nodeStats.get(n.metadata.name);
             const pk = pw[n.metadata.name];
             // Per-node stats keep their identity while unchanged (buildClusterIndex).
@@ -816,7 +885,7 @@ function nodesHeadItems(ctx, now, powerByNode) {
               ].concat(withPower ? [nodePowerCell(pk)] : [], [ageText(n.metadata.creationTimestamp, now)]);
             }, now);
           }, now, function (n) { return [idx.nodeStats.get(n.metadata.name), withPower, pw[n.metadata.name]]; }),
-          ctx.gpuNodes.map(function (n) { return n.metadata.uid || n.metadata.name; })
+          pg.nodes.map(function (n) { return n.metadata.uid || n.metadata.name; })
         ),
       ])
     );
@@ -987,6 +1056,37 @@ export function nodesReporting(m, ctx) {
   return missing > 0 ? status('warning', text + ' (' + missing + ' without telemetry)') : text;
 }
 
+/** "k / n GPU nodes" from an aggregate count of nodes reporting (paged snapshot totals). */
+export function nodesReportingCount(k, ctx) {
+  const n = ctx && ctx.gpuNodes ? ctx.gpuNodes.length : 0;
+  if (!n) return String(k);
+  const text = k + ' / ' + n + ' GPU nodes';
+  return k < n ? status('warning', text + ' (' + (n - k) + ' without telemetry)') : text;
+}
+
+/** The "GPU Nodes" row of the empty state: names, capped (a 1,000-node list is no help in one cell). */
+function gpuNodeNamesText(ctx) {
+  const ns = ctx.gpuNodes || [];
+  if (!ns.length) return 'None detected';
+  const shown = ns.slice(0, 20).map(function (n) { return n.metadata.name; }).join(', ');
+  return ns.length > 20 ? shown + ' … (' + ns.length + ' GPU nodes)' : shown;
+}
+
+/** Label of the cluster-wide line in the series table. */
+export const ALL_NODES_SERIES = 'All GPU nodes';
+
+function withTotal(pts) {
+  const o = {};
+  if (pts && pts.length) o[ALL_NODES_SERIES] = pts;
+  return o;
+}
+
+function noTelemetrySection(name) {
+  return section(name + ' — no telemetry', [
+    kv([row('Status', status('warning', 'No exporter series for this node (exporter not scheduled here, or not scraped yet)'))]),
+  ], name);
+}
+
 /** Power bar: "X W / Y W (Z%)" with 70/90 colouring (reference PowerBar, MetricsPage.tsx:50-89). */
 export function powerBar(watts, capWatts) {
   const hasCap = capWatts !== null && capWatts > 0;
@@ -1056,12 +1156,13 @@ export function metricsView(ctx, mstate, opts) {
     );
   }
 
-  if (m && m.gpus.length === 0) {
+  const tot = m && m.totals ? m.totals : null;
+  if (m && m.gpus.length === 0 && !(tot && tot.gpus > 0) && !(m.scope && !tot)) {
     items.push(
       section('No AMD GPU Metrics in Prometheus', [
         kv([
           row('Status', status('warning', 'Prometheus reachable — no gpu_power_usage or amdgpu hwmon series found')),
-          row('GPU Nodes', ctx.gpuNodes.length > 0 ? ctx.gpuNodes.map(function (n) { return n.metadata.name; }).join(', ') : 'None detected'),
+          row('GPU Nodes', gpuNodeNamesText(ctx)),
           row(
             'Likely cause',
             'The AMD Device Metrics Exporter is not deployed (DeviceConfig spec.metricsExporter.enable) or not scraped, and node-exporter is not running on the GPU nodes.'
@@ -1071,18 +1172,20 @@ export function metricsView(ctx, mstate, opts) {
     );
   }
 
-  if (m && m.gpus.length > 0) {
-    const sum = summarizeMetrics(m);
+  if (m && (m.gpus.length > 0 || (tot && tot.gpus > 0))) {
+    // Cluster totals: server-side aggregates on a paged (scoped) snapshot,
+    // else summed here from every GPU of the snapshot.
+    const sum = tot || summarizeMetrics(m);
     items.push(
       section('GPU Power Summary', [
         kv([
           row('GPUs Monitored', String(sum.gpus)),
-          row('Nodes Reporting', nodesReporting(m, ctx)),
+          row('Nodes Reporting', tot ? nodesReportingCount(tot.nodes, ctx) : nodesReporting(m, ctx)),
           row('Total Power', powerBar(sum.powerWatts, sum.powerCapWatts > 0 ? sum.powerCapWatts : null)),
           row('HBM In Use', hbmBar(sum.vramUsedBytes, sum.vramTotalBytes > 0 ? sum.vramTotalBytes : null)),
           row('Avg GFX Activity', pctText(sum.avgGfxActivityPct)),
         ].concat(sum.eccUncorrectable === null ? [] : [row('RAS Errors', eccCell(sum))], [
-          row('Source', m.source === 'amd-exporter' ? 'AMD Device Metrics Exporter' : 'node-exporter (amdgpu hwmon + DRM)'),
+          row('Source', m.source === 'node-exporter' ? 'node-exporter (amdgpu hwmon + DRM)' : 'AMD Device Metrics Exporter'),
         ], limitsRows(sum), [
           // Browser-local time, as the reference shows it (MetricsPage.tsx:336-338).
           row(
@@ -1095,9 +1198,13 @@ export function metricsView(ctx, mstate, opts) {
       ])
     );
 
-    if (mstate.series && mstate.series.power) {
-      const win = formatWindow(mstate.series.rangeSec || 1800);
-      const ps = clusterPowerStats(mstate.series.power);
+    const sr = mstate.series;
+    if (sr && sr.power) {
+      const win = formatWindow(sr.rangeSec || 1800);
+      // A paged snapshot's series carry the cluster line apart (series.total);
+      // peak / average are the cluster's either way.
+      const clusterPower = sr.total ? { cluster: sr.total.power || [] } : sr.power;
+      const ps = clusterPowerStats(clusterPower);
       const cap = sum.powerCapWatts > 0 ? sum.powerCapWatts : null;
       const statRows = ps
         ? [kv([
@@ -1105,9 +1212,11 @@ export function metricsView(ctx, mstate, opts) {
           row('Average Power (' + win + ')', powerBar(ps.avgWatts, cap)),
         ])]
         : [];
+      const power = sr.total ? Object.assign({}, withTotal(sr.total.power), sr.power) : sr.power;
+      const vram = sr.total ? Object.assign({}, withTotal(sr.total.vram), sr.vram || {}) : sr.vram || {};
       items.push(
         section('Power & HBM (last ' + win + ')', statRows.concat([
-          { t: 'series', power: mstate.series.power, vram: mstate.series.vram || {}, avgPower: seriesMeans(mstate.series.power) },
+          { t: 'series', power: power, vram: vram, avgPower: seriesMeans(power) },
         ]))
       );
     }
@@ -1122,10 +1231,35 @@ export function metricsView(ctx, mstate, opts) {
       }
       byNode[g.nodeName].push(g);
     }
-    for (let i = 0; i < order.length; i++) {
-      const gs = byNode[order[i]];
-      // Deps are the node's GPU objects, which the metrics client reuses while unchanged.
-      items.push(memo('metrics-node:' + order[i], gs, function () { return metricsNodeSection(order[i], gs); }));
+    // One page of per-node cards. A paged snapshot covers the GPU nodes of
+    // the page (m.scope); a cluster-wide one is paged over the nodes reporting.
+    const scoped = Array.isArray(m.scope);
+    const k8s = scoped && !ctx.loading && ctx.gpuNodes && ctx.gpuNodes.length > 0;
+    const pg = k8s ? nodePage(ctx.gpuNodes, opts && opts.pager) : nodePage(scoped ? m.scope : order, opts && opts.pager);
+    items.push(pager(pg, k8s || scoped ? 'GPU nodes' : 'GPU nodes reporting'));
+    const covered = {};
+    if (scoped) for (let i = 0; i < m.scope.length; i++) covered[m.scope[i]] = true;
+    let matched = 0;
+    for (let i = 0; i < pg.names.length; i++) {
+      const name = pg.names[i];
+      const gs = byNode[name];
+      if (gs) {
+        matched++;
+        // Deps are the node's GPU objects, which the metrics client reuses while unchanged.
+        items.push(memo('metrics-node:' + name, gs, function () { return metricsNodeSection(name, gs); }));
+      } else if (!scoped || covered[name]) {
+        items.push(memo('metrics-none:' + name, [], function () { return noTelemetrySection(name); }));
+      } else {
+        items.push(section(name + ' — fetching telemetry…', [], name));
+      }
+    }
+    if (scoped && tot && tot.gpus > 0 && matched === 0 && pg.names.length > 0 && pg.names.every(function (n) { return covered[n]; })) {
+      items.push(section('Telemetry Not Matched To Nodes', [
+        kv([
+          row('Status', status('warning', 'Prometheus reports ' + tot.gpus + ' GPUs on ' + tot.nodes + ' nodes, none under the names of the nodes on this page')),
+          row('Likely cause', 'The exporter\'s hostname label is not the Kubernetes node name (Device Metrics Exporter: set the node name as hostname).'),
+        ]),
+      ]));
     }
   }
 

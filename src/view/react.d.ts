@@ -4,7 +4,7 @@
  * (tests/js/stubs/react.js) both satisfy it.
  */
 import type { ComponentType, CSSProperties, ReactElement, ReactNode } from 'react';
-import type { Block as IRBlock, Cell, MatrixBlock, PageVM, Section as IRSection, SeriesPoint } from './ir';
+import type { Block as IRBlock, Cell, MatrixBlock, PageVM, PagerItem, Section as IRSection, SeriesPoint } from './ir';
 
 export interface ReactLike {
   createElement: (...args: never[]) => ReactElement;
@@ -40,7 +40,9 @@ export interface Renderer {
   Block: ComponentType<{ b: IRBlock }>;
   Section: ComponentType<{ s: IRSection | null }>;
   SectionImpl: ComponentType<{ s: IRSection | null }>;
-  Page: ComponentType<{ vm: PageVM; onRefresh?: () => void }>;
+  /** name filter + range shown + previous / next; the page owns the state */
+  Pager: ComponentType<{ p: PagerItem; onPage?: (page: number) => void; onFilter?: (filter: string) => void }>;
+  Page: ComponentType<{ vm: PageVM; onRefresh?: () => void; onPage?: (page: number) => void; onFilter?: (filter: string) => void }>;
 }
 
 export function createRenderer(React: ReactLike, CC: CommonComponentsLike): Renderer;

@@ -18,6 +18,7 @@
  *   slots    → per-GPU allocation strip (MI355X, new)
  *   matrix   → xGMI neighbour matrix (MI355X, new)
  *   series   → inline SVG sparklines of per-node power / HBM (new)
+ *   pager    → name filter + "Showing 1–16 of N" + previous / next (page item)
  *
  * Only CommonComponents plus inline-styled elements are used, like the
  * reference (reference CLAUDE.md conventions; src/components/NodesPage.tsx:35-63
@@ -25,7 +26,7 @@
  */
 
 import { BAR_COLORS, formatWatts } from '../api/amdgpu.js';
-import { matrixCaption } from './ir.js';
+import { matrixCaption, pagerText } from './ir.js';
 
 /** CommonComponents the renderer needs (reference src/components/OverviewPage.tsx:8-16). */
 export const REQUIRED_COMPONENTS = [
@@ -305,6 +306,37 @@ export function createRenderer(React, CC) {
   // Section skips re-rendering the unchanged parts of a page on refresh.
   const Section = React.memo(SectionImpl);
 
+  /**
+   * Pager of a long list (GPU nodes): name filter, the range shown and
+   * previous / next. The page component owns the state (props.onPage /
+   * props.onFilter); without handlers the controls are inert.
+   */
+  function Pager(props) {
+    const p = props.p;
+    const prev = p.page > 0;
+    const next = p.page + 1 < p.pages;
+    return h(
+      'div',
+      { 'data-pager': p.noun, style: { display: 'flex', alignItems: 'center', gap: '8px', flexWrap: 'wrap', margin: '0 0 16px' } },
+      h('input', {
+        'aria-label': 'Filter ' + p.noun + ' by name',
+        placeholder: 'Filter by name',
+        value: p.filter,
+        style: { padding: '4px 6px', fontSize: '13px', minWidth: '180px' },
+        onChange: function (e) { if (props.onFilter) props.onFilter(e.target.value); },
+      }),
+      h('span', { style: { fontSize: '13px', color: 'var(--mui-palette-text-secondary)' } }, pagerText(p)),
+      h('button', {
+        'aria-label': 'Previous page', disabled: !prev, style: buttonStyle(!prev),
+        onClick: function () { if (prev && props.onPage) props.onPage(p.page - 1); },
+      }, '‹ Prev'),
+      h('button', {
+        'aria-label': 'Next page', disabled: !next, style: buttonStyle(!next),
+        onClick: function () { if (next && props.onPage) props.onPage(p.page + 1); },
+      }, 'Next ›')
+    );
+  }
+
   function Page(props) {
     const vm = props.vm;
     const onRefresh = props.onRefresh;
@@ -332,7 +364,9 @@ export function createRenderer(React, CC) {
       null,
       header,
       vm.items.map(function (it, i) {
-        return it.t === 'loader' ? h(CC.Loader, { key: 'loader-' + i, title: it.title }) : h(Section, { key: it.key || i, s: it });
+        if (it.t === 'loader') return h(CC.Loader, { key: 'loader-' + i, title: it.title });
+        if (it.t === 'pager') return h(Pager, { key: 'pager', p: it, onPage: props.onPage, onFilter: props.onFilter });
+        return h(Section, { key: it.key || i, s: it });
       })
     );
   }
@@ -347,6 +381,7 @@ export function createRenderer(React, CC) {
     Block: Block,
     Section: Section,
     SectionImpl: SectionImpl,
+    Pager: Pager,
     Page: Page,
   };
 }

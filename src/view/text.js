@@ -9,7 +9,7 @@
  * colour for statuses.
  */
 
-import { matrixCaption } from './ir.js';
+import { matrixCaption, pagerText } from './ir.js';
 
 const MARK = { success: '✓', warning: '!', error: '✗' };
 const ANSI = { success: '\u001b[32m', warning: '\u001b[33m', error: '\u001b[31m', reset: '\u001b[0m' };
@@ -153,6 +153,7 @@ export function renderText(vm, opts) {
   if (vm.title) out.push('# ' + vm.title, '');
   vm.items.forEach(function (it) {
     if (it.t === 'loader') out.push('… ' + it.title, '');
+    else if (it.t === 'pager') out.push('[' + pagerText(it) + ']', '');
     else out.push.apply(out, textSection(it, color).concat(['']));
   });
   return out.join('\n');

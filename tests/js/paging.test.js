@@ -1,0 +1,287 @@
+/**
+ * O(visible) GPU Nodes and Metrics pages: the pager (pages.js nodePage), the
+ * scoped telemetry queries (metrics.js exporterQuery / summaryQuery /
+ * scopedSeriesQuery with `hostname=~`), and the pages built from them.
+ *
+ * The reference renders one card per GPU node (NodesPage.tsx:285-291) and
+ * one per chip on its Metrics page (MetricsPage.tsx:348-350), with every
+ * node's telemetry per fetch; here what a page renders and fetches is bounded
+ * by NODES_PER_PAGE, whatever the cluster size.
+ */
+import React, { render } from './stubs/react.js';
+import * as lib from './stubs/headlamp-lib.js';
+import * as CC from './stubs/CommonComponents.js';
+import { createPlugin } from '../../src/plugin.js';
+import { resetSharedStores } from '../../src/api/clusterStore.js';
+import { DEVICE_CONFIG_LIST_PATH } from '../../src/api/amdgpu.js';
+import {
+  ALL_NODES_SERIES, NODES_PER_PAGE, clearViewMemo, metricsView, nodePage, nodesView, telemetryScope,
+} from '../../src/view/pages.js';
+import { countRows, findSection, pagerOf, pagerText, rowValue, sectionTitles } from '../../src/view/ir.js';
+import { renderPage } from '../../src/view/html.js';
+import {
+  SERIES, TOTAL_SERIES, createMetricsSource, hostnameMatcher, regexLiteral, scopedSeriesQuery, summarizeMetrics,
+  summaryQuery, totalsFromRows, joinExporterResults, splitByName,
+} from '../../src/api/metrics.js';
+import { makeContext, makeDeviceConfig, makeGpuNode, makeGpuPod } from './fixtures.js';
+import { BASE0, exporterData, flatten, prom } from './promFake.js';
+
+const h = React.createElement;
+const names = (n) => Array.from({ length: n }, (_, i) => 'mi355x-' + String(i).padStart(3, '0'));
+const ctxOf = (n) => makeContext({ nodes: names(n).map((x) => makeGpuNode(x)), pods: [makeGpuPod('train-0', { node: 'mi355x-000' })] });
+const cards = (vm) => sectionTitles(vm).filter((t) => /^mi355x-/.test(t));
+const decoded = (fake) => fake.mock.calls.map((c) => decodeURIComponent(c[0]));
+
+beforeEach(() => {
+  clearViewMemo();
+  resetSharedStores();
+});
+
+describe('nodePage', () => {
+  const nodes = names(20).map((x) => makeGpuNode(x));
+  it('slices NODES_PER_PAGE nodes and counts the pages', () => {
+    const p = nodePage(nodes, { page: 0 });
+    expect(NODES_PER_PAGE).toBe(8);
+    expect(p.names).toEqual(names(8));
+    expect([p.page, p.pages, p.from, p.to, p.total, p.matched]).toEqual([0, 3, 0, 8, 20, 20]);
+    expect(nodePage(nodes, { page: 2 }).names).toEqual(names(20).slice(16));
+  });
+  it('clamps the page into range', () => {
+    expect(nodePage(nodes, { page: 99 }).page).toBe(2);
+    expect(nodePage(nodes, { page: -3 }).page).toBe(0);
+    expect(nodePage([], { page: 4 })).toEqual(Object.assign({}, nodePage([], {}), {}));
+    expect(nodePage([], {}).pages).toBe(1);
+  });
+  it('filters by a case-insensitive name substring (surrounding spaces ignored) and keeps the raw text', () => {
+    const p = nodePage(nodes, { filter: ' X-01 ' });
+    expect(p.names).toEqual(['mi355x-010', 'mi355x-011', 'mi355x-012', 'mi355x-013', 'mi355x-014', 'mi355x-015', 'mi355x-016', 'mi355x-017']);
+    expect([p.matched, p.pages, p.filter]).toEqual([10, 2, ' X-01 ']);
+    expect(nodePage(nodes, { filter: 'nope' }).matched).toBe(0);
+  });
+  it('returns the same object for the same list and state (memo)', () => {
+    expect(nodePage(nodes, { page: 1 })).toBe(nodePage(nodes, { page: 1 }));
+    expect(nodePage(nodes, { page: 1 })).not.toBe(nodePage(nodes.slice(), { page: 1 }));
+  });
+  it('pager text', () => {
+    expect(pagerText(Object.assign({ noun: 'GPU nodes' }, nodePage(nodes, { page: 1 })))).toBe('Showing 9–16 of 20 GPU nodes · page 2 of 3');
+    expect(pagerText(Object.assign({ noun: 'GPU nodes' }, nodePage(nodes, { filter: 'x-01' })))).toBe(
+      'Showing 1–8 of 10 matching "x-01" (20 GPU nodes) · page 1 of 2'
+    );
+    expect(pagerText(Object.assign({ noun: 'GPU nodes' }, nodePage(nodes, { filter: 'zz' })))).toBe('No GPU nodes match "zz"');
+  });
+});
+
+describe('telemetryScope', () => {
+  it('waits for the node list, then scopes to the page; cluster-wide when the node list failed', () => {
+    expect(telemetryScope(makeContext({ loading: true }), {}).enabled).toBe(false);
+    expect(telemetryScope(ctxOf(12), { page: 1 })).toEqual({ enabled: true, scope: names(12).slice(8) });
+    const denied = Object.assign(makeContext({ nodes: [] }), { error: 'nodes is forbidden' });
+    expect(telemetryScope(denied, {})).toEqual({ enabled: true, scope: undefined });
+  });
+});
+
+describe('nodesView: one page of nodes', () => {
+  it('renders at most NODES_PER_PAGE rows and cards, with a pager, whatever the node count', () => {
+    const small = nodesView(ctxOf(8), {});
+    const big = nodesView(ctxOf(200), {});
+    const last = nodesView(ctxOf(200), { pager: { page: 24 } });
+    expect(cards(big)).toEqual(names(8));
+    expect(cards(last)).toEqual(names(200).slice(192));
+    expect(countRows(big)).toEqual(countRows(small));
+    const p = pagerOf(big);
+    expect([p.total, p.pages, p.noun]).toEqual([200, 25, 'GPU nodes']);
+    expect(findSection(big, 'GPU Node Summary').blocks[0].rows).toHaveLength(8);
+    expect(renderPage(big)).toContain('data-testid="pager"');
+  });
+  it('a filter narrows rows and cards; no match leaves the pager saying so', () => {
+    const vm = nodesView(ctxOf(30), { pager: { filter: '02' } });
+    expect(cards(vm)).toEqual(['mi355x-002', 'mi355x-020', 'mi355x-021', 'mi355x-022', 'mi355x-023', 'mi355x-024', 'mi355x-025', 'mi355x-026']);
+    const none = nodesView(ctxOf(30), { pager: { filter: 'gpu-z' } });
+    expect(findSection(none, 'GPU Node Summary')).toBe(null);
+    expect(pagerText(pagerOf(none))).toBe('No GPU nodes match "gpu-z"');
+  });
+  it('no pager without GPU nodes (the empty state stands alone)', () => {
+    const vm = nodesView(makeContext({ nodes: [] }), {});
+    expect(pagerOf(vm)).toBe(null);
+    expect(sectionTitles(vm)).toContain('No GPU Nodes Found');
+  });
+});
+
+describe('scoped queries', () => {
+  it('hostname matcher escapes regex metacharacters; an empty scope matches no node', () => {
+    expect(regexLiteral('a.b+c')).toBe('a\\.b\\+c');
+    expect(hostnameMatcher(['n.0', 'n1'])).toBe('hostname=~"n\\\\.0|n1"');
+    expect(hostnameMatcher([])).toBe('hostname="."');
+  });
+  it('the summary query tags each aggregate so `or` keeps them apart', () => {
+    const q = summaryQuery();
+    expect(q.split(' or ')).toHaveLength(3);
+    ['"agg", "sum"', '"agg", "count"', '"agg", "nodes"'].forEach((t) => expect(q).toContain(t));
+  });
+  it('totals from aggregates equal the totals summed over every GPU', () => {
+    const data = exporterData(['n0', 'n1', 'n2']);
+    data[SERIES.exporter.powerCap] = [];
+    const fake = prom({ data: data });
+    return fake(BASE0 + '/api/v1/query?query=' + encodeURIComponent(summaryQuery())).then((r) => {
+      const t = totalsFromRows(r.data.result);
+      const m = joinExporterResults(splitByName(flatten(data)));
+      const s = summarizeMetrics(m);
+      ['gpus', 'powerWatts', 'powerCapWatts', 'vramUsedBytes', 'vramTotalBytes', 'avgGfxActivityPct', 'powerCapAssumed'].forEach((k) => {
+        expect(t[k]).toBe(s[k]);
+      });
+      expect(t.nodes).toBe(3);
+    });
+  });
+  it('aggregate rows never join as GPUs', () => {
+    const rows = splitByName([{ metric: { __name__: SERIES.exporter.power, agg: 'sum' }, value: [0, '9'] }]);
+    expect(rows.__agg).toHaveLength(1);
+    expect(joinExporterResults(rows).gpus).toHaveLength(0);
+  });
+  it('scoped series ask for the page nodes and the cluster line', () => {
+    const q = scopedSeriesQuery(['n0']);
+    expect(q).toContain('hostname=~"n0"');
+    expect(q).toContain('"scope", "cluster"');
+  });
+});
+
+describe('metrics client: scoped snapshots', () => {
+  function source(fake) {
+    return createMetricsSource({ request: fake });
+  }
+  it('fetches only the GPUs of the scope, plus cluster totals on request, in one query', async () => {
+    const fake = prom({ data: exporterData(names(12)) });
+    const s = source(fake);
+    const m = await s.fetchGpuMetrics('gauges', { scope: ['mi355x-003', 'mi355x-007'], summary: true });
+    expect(fake.mock.calls).toHaveLength(1);
+    expect(decoded(fake)[0]).toContain('hostname=~"mi355x-003|mi355x-007"');
+    expect(Array.from(new Set(m.gpus.map((g) => g.nodeName)))).toEqual(['mi355x-003', 'mi355x-007']);
+    expect(m.scope).toEqual(['mi355x-003', 'mi355x-007']);
+    expect([m.totals.gpus, m.totals.nodes]).toEqual([96, 12]);
+    expect(m.source).toBe('amd-exporter');
+  });
+  it('later fetches of the same scope are live-only (statics cached per node) and share unchanged GPUs', async () => {
+    const fake = prom({ data: exporterData(names(3)) });
+    const s = source(fake);
+    const a = await s.fetchGpuMetrics('topology', { scope: ['mi355x-001'] });
+    const b = await s.fetchGpuMetrics('topology', { scope: ['mi355x-001'] });
+    const qs = decoded(fake);
+    expect(qs[0]).toContain(SERIES.exporter.vramTotal);
+    expect(qs[1]).not.toContain(SERIES.exporter.vramTotal);
+    expect(b.gpus).toBe(a.gpus);
+    // a new page of nodes needs their statics: asked for again
+    await s.fetchGpuMetrics('topology', { scope: ['mi355x-002'] });
+    expect(decoded(fake)[2]).toContain(SERIES.exporter.vramTotal);
+  });
+  it('falls back to the cluster-wide snapshot cut to the scope for a node-exporter source', async () => {
+    const ne = { node_uname_info: [{ metric: { __name__: 'node_uname_info', instance: 'i0', nodename: 'mi355x-000' }, value: [0, '1'] }] };
+    ne[SERIES.nodeExporter.chips] = [{ metric: { __name__: 'node_hwmon_chip_names', chip_name: 'amdgpu', instance: 'i0', chip: '0000:05:00_0' }, value: [0, '1'] }];
+    const fake = prom({ data: {}, ne: ne });
+    const s = source(fake);
+    const m = await s.fetchGpuMetrics('gauges', { scope: ['mi355x-000'], summary: true });
+    expect(m.source).toBe('node-exporter');
+    expect(m.gpus.map((g) => g.nodeName)).toEqual(['mi355x-000']);
+    expect(m.totals.gpus).toBe(1);
+  });
+  it('an empty scope with a summary asks for the totals only', async () => {
+    const fake = prom({ data: exporterData(names(2)) });
+    const m = await source(fake).fetchGpuMetrics('gauges', { scope: [], summary: true });
+    expect(decoded(fake)[0]).not.toContain('hostname=');
+    expect(m.gpus).toHaveLength(0);
+    expect(m.totals.gpus).toBe(16);
+  });
+  it('scoped series keep the cluster line apart', async () => {
+    const fake = prom({ data: exporterData(names(2)) });
+    const sr = await source(fake).fetchSeries(1800, 30, ['n0']);
+    expect(Object.keys(sr.power)).toEqual(['n0']);
+    expect(sr.total.power.length).toBe(2);
+    expect(sr.power[TOTAL_SERIES]).toBe(undefined);
+  });
+});
+
+describe('metricsView: one page of per-node cards', () => {
+  async function state(n, scope) {
+    const fake = prom({ data: exporterData(names(n).filter((x) => x !== 'mi355x-001')) });
+    const s = createMetricsSource({ request: fake });
+    const m = await s.fetchGpuMetrics('gauges', { scope: scope, summary: true });
+    const series = await s.fetchSeries(1800, 30, scope);
+    return { metrics: m, series: series, fetchError: null, fetching: false };
+  }
+  it('summary from the cluster totals; cards for the page; a node without series gets a no-telemetry card', async () => {
+    const ctx = ctxOf(20);
+    const st = await state(20, names(20).slice(0, 8));
+    const vm = metricsView(ctx, st, {});
+    expect(rowValue(vm, 'GPUs Monitored')).toBe('152');
+    expect(rowValue(vm, 'Nodes Reporting').text).toBe('19 / 20 GPU nodes (1 without telemetry)');
+    expect(cards(vm)).toEqual(['mi355x-000 — 8 × MI355X', 'mi355x-001 — no telemetry'].concat(names(8).slice(2).map((x) => x + ' — 8 × MI355X')));
+    const series = findSection(vm, 'Power & HBM (last 30 min)').blocks.filter((b) => b.t === 'series')[0];
+    expect(Object.keys(series.power)[0]).toBe(ALL_NODES_SERIES);
+    expect(pagerOf(vm).total).toBe(20);
+  });
+  it('cards of nodes not yet covered by the snapshot say telemetry is on its way', async () => {
+    const st = await state(20, names(8));
+    const vm = metricsView(ctxOf(20), st, { pager: { page: 1 } });
+    expect(cards(vm)[0]).toBe('mi355x-008 — fetching telemetry…');
+  });
+  it('warns when the exporter hostnames match no node on the page', async () => {
+    const fake = prom({ data: exporterData(['10.0.0.1', '10.0.0.2']) });
+    const s = createMetricsSource({ request: fake });
+    const m = await s.fetchGpuMetrics('gauges', { scope: names(2), summary: true });
+    const vm = metricsView(ctxOf(2), { metrics: m, series: null, fetchError: null, fetching: false }, {});
+    expect(sectionTitles(vm)).toContain('Telemetry Not Matched To Nodes');
+  });
+  it('a cluster-wide snapshot (terminal client) is paged over the nodes reporting', async () => {
+    const fake = prom({ data: exporterData(names(12)) });
+    const m = await createMetricsSource({ request: fake }).fetchGpuMetrics('gauges');
+    const vm = metricsView(ctxOf(12), { metrics: m, series: null, fetchError: null, fetching: false }, { pager: { page: 1 } });
+    expect(cards(vm)).toEqual(names(12).slice(8).map((x) => x + ' — 8 × MI355X'));
+    expect(pagerOf(vm).noun).toBe('GPU nodes reporting');
+  });
+});
+
+describe('plugin pages: pager state drives the scoped queries', () => {
+  function setup(n) {
+    lib.resetHeadlamp();
+    const nodes = names(n).map((x) => makeGpuNode(x));
+    lib.lists.Node = [nodes, null];
+    lib.lists.Pod = [[makeGpuPod('train-a', { node: 'mi355x-000' })], null];
+    const fake = prom({ data: exporterData(names(n)) });
+    lib.api.handler = (p) => {
+      if (p === DEVICE_CONFIG_LIST_PATH) return Promise.resolve({ kind: 'List', metadata: {}, items: [makeDeviceConfig()] });
+      if (p.indexOf('/proxy/api/v1/') >= 0) return fake(p);
+      return Promise.reject(Object.assign(new Error('503'), { status: 503 }));
+    };
+    const plugin = createPlugin({ React: React, lib: lib, CommonComponents: CC });
+    return { fake: fake, plugin: plugin };
+  }
+  const scoped = (fake) => decoded(fake).filter((p) => p.indexOf('/query?') >= 0 && p.indexOf('hostname=~') >= 0);
+
+  it('GPU Nodes: the first query covers page 1; Next page asks for page 2; the filter narrows it', async () => {
+    const { fake, plugin } = setup(20);
+    const r = render(h(plugin.routeComponent('nodes')));
+    await r.settle();
+    expect(scoped(fake)).toHaveLength(1);
+    expect(scoped(fake)[0]).toContain('hostname=~"' + names(8).join('|') + '"');
+    expect(r.text()).toContain('Showing 1–8 of 20 GPU nodes');
+    r.click(r.getByLabelText('Next page'));
+    await r.settle();
+    expect(scoped(fake)[1]).toContain('hostname=~"' + names(16).slice(8).join('|') + '"');
+    expect(r.text()).toContain('mi355x-015');
+    expect(r.text()).not.toContain('mi355x-007');
+    r.change(r.getByLabelText('Filter GPU nodes by name'), 'x-019');
+    await r.settle();
+    expect(scoped(fake).pop()).toContain('hostname=~"mi355x-019"');
+    expect(r.getByLabelText('Next page').props.disabled).toBe(true);
+    r.unmount();
+  });
+  it('Metrics: cluster totals and the page scope in one live query', async () => {
+    const { fake, plugin } = setup(12);
+    const r = render(h(plugin.routeComponent('metrics')));
+    await r.settle();
+    const live = scoped(fake);
+    expect(live).toHaveLength(1);
+    expect(live[0]).toContain('"agg", "sum"');
+    expect(r.text()).toContain('12 / 12 GPU nodes');
+    expect(r.byTag('section').length).toBeLessThan(8 + 6);
+    r.unmount();
+  });
+});

@@ -62,7 +62,49 @@ export function flatten(d) {
   return out;
 }
 
-/** A fake proxy: answers probes on `up` services and `{__name__=~"a|b"}` queries from `data` / `ne`. */
+/**
+ * One instant-query term against `rows`: the selector / projection shapes the
+ * client sends (optionally `hostname="…"` or `hostname=~"a|b"` scoped), the
+ * pod-owner query, and the summary aggregates (label_replace(sum|count by
+ * (__name__) …, "agg", …)). Unknown shapes answer no rows.
+ */
+function term(q, rows) {
+  const own = /^max by \([^)]*\) \(\{__name__="([a-z_]+)", pod!=""\}\)$/.exec(q);
+  if (own) return rows.filter((r) => r.metric.__name__ === own[1] && r.metric.pod);
+  const agg = /^label_replace\((sum|count) by \(__name__\) \(\{__name__=~"(.*?)"\}\), "agg", "(\w+)", "", ""\)$/.exec(q);
+  if (agg) {
+    const re = new RegExp('^(?:' + agg[2] + ')$');
+    const by = {};
+    rows.filter((r) => re.test(r.metric.__name__ || '')).forEach((r) => {
+      const k = r.metric.__name__;
+      const v = parseFloat(r.value[1]);
+      by[k] = (by[k] || 0) + (agg[1] === 'sum' ? v : 1);
+    });
+    return Object.keys(by).map((k) => vec({ __name__: k, agg: agg[3] }, by[k]));
+  }
+  const nodes = /^label_replace\(count by \(__name__\) \(count by \(__name__, hostname\) \(\{__name__="([a-z_]+)"\}\)\), "agg", "nodes", "", ""\)$/.exec(q);
+  if (nodes) {
+    const hs = {};
+    rows.filter((r) => r.metric.__name__ === nodes[1]).forEach((r) => (hs[r.metric.hostname] = true));
+    const n = Object.keys(hs).length;
+    return n ? [vec({ __name__: nodes[1], agg: 'nodes' }, n)] : [];
+  }
+  const m = /^(?:max by \([^)]*\) \()?\{__name__=~"(.*?)"(?:, hostname(=~?)"((?:[^"\\]|\\.)*)")?\}\)?$/.exec(q);
+  if (!m) return [];
+  const re = new RegExp('^(?:' + m[1] + ')$');
+  let hostOk = () => true;
+  if (m[3] !== undefined) {
+    const v = m[3].replace(/\\(.)/g, '$1');
+    if (m[2] === '=') hostOk = (h) => h === v;
+    else {
+      const hre = new RegExp('^(?:' + v + ')$');
+      hostOk = (h) => hre.test(h || '');
+    }
+  }
+  return rows.filter((r) => re.test(r.metric.__name__ || '') && hostOk(r.metric.hostname));
+}
+
+/** A fake proxy: answers probes on `up` services and the client's queries from `data` / `ne`. */
 export function prom(opts) {
   const o = Object.assign({ up: [BASE0], data: exporterData(['n0']), ne: null }, opts || {});
   const rows = flatten(o.data).concat(flatten(o.ne));
@@ -74,23 +116,20 @@ export function prom(opts) {
     if (path.indexOf('/query_range') >= 0) {
       const end = Number(/end=(\d+)/.exec(path)[1]);
       const values = [[end - 30, '100'], [end, '200']];
-      return Promise.resolve({
-        status: 'success',
-        data: {
-          resultType: 'matrix',
-          result: [
-            { metric: { __name__: 'gpu_power_usage', hostname: 'n0' }, values },
-            { metric: { __name__: 'gpu_used_vram', hostname: 'n0' }, values },
-          ],
-        },
-      });
+      const result = [
+        { metric: { __name__: 'gpu_power_usage', hostname: 'n0' }, values },
+        { metric: { __name__: 'gpu_used_vram', hostname: 'n0' }, values },
+      ];
+      // the scoped series query also asks for the cluster-wide line
+      if (q.indexOf('"scope", "cluster"') >= 0) {
+        result.push({ metric: { __name__: 'gpu_power_usage', scope: 'cluster' }, values });
+        result.push({ metric: { __name__: 'gpu_used_vram', scope: 'cluster' }, values });
+      }
+      return Promise.resolve({ status: 'success', data: { resultType: 'matrix', result } });
     }
-    const own = /^max by \([^)]*\) \(\{__name__="([a-z_]+)", pod!=""\}\)$/.exec(q);
-    if (own) return Promise.resolve(ok(rows.filter((r) => r.metric.__name__ === own[1] && r.metric.pod)));
-    const m = /^(?:max by \([^)]*\) \()?\{__name__=~"(.*?)"(?:, hostname="((?:[^"\\]|\\.)*)")?\}\)?$/.exec(q);
-    if (!m) return Promise.resolve(ok([]));
-    const re = new RegExp('^(?:' + m[1] + ')$');
-    const host = m[2] === undefined ? null : m[2].replace(/\\(.)/g, '$1');
-    return Promise.resolve(ok(rows.filter((r) => re.test(r.metric.__name__ || '') && (host === null || r.metric.hostname === host))));
+    // `a or b`: every term's rows (the client keeps their label sets apart).
+    const out = [];
+    q.split(' or ').forEach((t) => term(t, rows).forEach((r) => out.push(r)));
+    return Promise.resolve(ok(out));
   });
 }

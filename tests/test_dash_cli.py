@@ -37,7 +37,9 @@ def test_json_is_the_view_model(url):
     assert r.returncode == 0, r.stderr
     vm = json.loads(r.stdout)
     assert vm["title"] == "AMD GPU — Nodes"
-    assert [s["title"] for s in vm["items"]][:3] == ["GPU Node Summary", "mi355x-000", "mi355x-001"]
+    assert [s["title"] for s in vm["items"] if s["t"] == "section"][:3] == ["GPU Node Summary", "mi355x-000", "mi355x-001"]
+    pager = [s for s in vm["items"] if s["t"] == "pager"][0]
+    assert pager["noun"] == "GPU nodes" and pager["page"] == 0 and pager["from"] == 0
 
 
 def test_unreachable_prometheus_and_bad_arguments(url):

@@ -187,3 +187,71 @@ def test_instant_cache_sees_pushes_and_interval_changes():
     assert values(106.0)["n1"] == 105.0  # next 15 s bucket re-evaluates fn series
     body = json.loads(promql.query(db, q, 107.5))
     assert body["data"]["result"][0]["value"][0] == 107.5  # eval timestamp is current, not cached
+
+
+# ---- set operators and label_replace (the paged views' scoped + summary queries) ----
+
+def test_or_keeps_lhs_and_adds_unmatched_rhs_ignoring_the_name(db):
+    # Prometheus matches `or` on every label but __name__: gfx rows carry the same
+    # hostname/gpu_id sets as the power rows, so none of them is added.
+    rows = _vec(query(db, "gpu_power_usage or gpu_gfx_activity", 1000.0))
+    assert len(rows) == 4 and {r["metric"]["__name__"] for r in rows} == {"gpu_power_usage"}
+    rows = _vec(query(db, 'gpu_power_usage{hostname="n0"} or gpu_gfx_activity{hostname="n1"}', 1000.0))
+    assert sorted((r["metric"]["__name__"], r["metric"]["hostname"]) for r in rows) == [
+        ("gpu_gfx_activity", "n1"), ("gpu_gfx_activity", "n1"), ("gpu_power_usage", "n0"), ("gpu_power_usage", "n0")]
+
+
+def test_or_on_name_keeps_both_metrics(db):
+    rows = _vec(query(db, "gpu_power_usage or on(__name__, hostname, gpu_id) gpu_gfx_activity", 1000.0))
+    assert len(rows) == 8
+
+
+def test_and_unless(db):
+    assert len(_vec(query(db, 'gpu_power_usage and on(hostname) gpu_gfx_activity{hostname="n1"}', 1000.0))) == 2
+    rows = _vec(query(db, 'gpu_power_usage unless on(hostname) gpu_gfx_activity{hostname="n1"}', 1000.0))
+    assert {r["metric"]["hostname"] for r in rows} == {"n0"}
+
+
+def test_or_binds_weaker_than_arithmetic(db):
+    # (sum * 2) or (count): tagged so both survive
+    q = ('label_replace(sum(gpu_power_usage) * 2, "agg", "double", "", "") or '
+         'label_replace(count(gpu_power_usage), "agg", "n", "", "")')
+    rows = {r["metric"]["agg"]: float(r["value"][1]) for r in _vec(query(db, q, 1000.0))}
+    assert rows == {"double": 2 * (100 + 101 + 200 + 201), "n": 4.0}
+
+
+def test_label_replace_sets_copies_and_removes():
+    d = TSDB()
+    d.add(Series({"__name__": "up", "instance": "10.0.0.7:9100", "job": "ne"}, fn=lambda t: 1.0))
+    q = 'label_replace(up, "host", "$1", "instance", "(.*):.*")'
+    (r,) = _vec(query(d, q, 100.0))
+    assert r["metric"]["host"] == "10.0.0.7" and r["metric"]["__name__"] == "up"
+    (r,) = _vec(query(d, 'label_replace(up, "job", "", "", "")', 100.0))
+    assert "job" not in r["metric"]
+    (r,) = _vec(query(d, 'label_replace(up, "host", "x", "instance", "nomatch")', 100.0))
+    assert "host" not in r["metric"]  # no match: the series is unchanged
+    (r,) = _vec(query(d, 'label_replace(up, "host", "${1}-${2}", "instance", "([0-9.]+):([0-9]+)")', 100.0))
+    assert r["metric"]["host"] == "10.0.0.7-9100"
+
+
+def test_summary_query_of_the_metrics_page():
+    """metrics.js summaryQuery over an exporter-shaped TSDB: sums, counts and nodes reporting, one tagged row each."""
+    import subprocess
+
+    from headlamp_intel_gpu_plugin_amd.utils.nodebridge import ROOT, node_binary
+
+    q = subprocess.run([node_binary(), "-e", "import('./src/api/metrics.js').then(m => process.stdout.write(m.summaryQuery()))"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=60).stdout
+    d = TSDB()
+    for node in ("a", "b", "c"):
+        for g in range(8):
+            lab = {"hostname": node, "gpu_id": str(g)}
+            d.add(Series({"__name__": "gpu_power_usage", **lab}, fn=lambda t: 500.0))
+            d.add(Series({"__name__": "gpu_total_vram", **lab}, fn=lambda t: 294896.0))
+            if node != "c":
+                d.add(Series({"__name__": "gpu_power_cap", **lab}, fn=lambda t: 1400.0))
+    got = {(r["metric"]["agg"], r["metric"]["__name__"]): float(r["value"][1]) for r in _vec(query(d, q, 100.0))}
+    assert got[("sum", "gpu_power_usage")] == 24 * 500.0
+    assert got[("count", "gpu_power_usage")] == 24 and got[("count", "gpu_power_cap")] == 16
+    assert got[("nodes", "gpu_power_usage")] == 3
+    assert got[("sum", "gpu_total_vram")] == 24 * 294896.0
