@@ -25,11 +25,12 @@
 import http from 'http';
 import fs from 'fs';
 import path from 'path';
-import { createClusterStore } from '../src/api/clusterStore.js';
+import { createClusterStore, fetchNodePods } from '../src/api/clusterStore.js';
 import { createMetricsSource } from '../src/api/metrics.js';
+import { filterGpuRequestingPods } from '../src/api/amdgpu.js';
 import {
   overviewView, devicePluginsView, nodesView, podsView, metricsView,
-  nodeDetailView, podDetailView, nodeColumns, telemetryScope,
+  nodeDetailView, podDetailView, nodeColumns, ownersScope, telemetryScope,
 } from '../src/view/pages.js';
 import { countRows } from '../src/view/ir.js';
 import { renderPage, renderSection } from '../src/view/html.js';
@@ -200,9 +201,9 @@ export const PAGES = ['overview', 'devicePlugins', 'nodes', 'pods', 'metrics'];
 /** Build ONE page's view-model (the one whose Refresh was clicked), first page of the pager. */
 function pageVm(page, ctx, mstate, pageMetrics) {
   if (page === 'overview') return overviewView(ctx);
-  if (page === 'devicePlugins') return devicePluginsView(ctx);
+  if (page === 'devicePlugins') return devicePluginsView(ctx, { pager: PAGER });
   if (page === 'nodes') return nodesView(ctx, { metrics: pageMetrics, pager: PAGER });
-  if (page === 'pods') return podsView(ctx, { metrics: pageMetrics });
+  if (page === 'pods') return podsView(ctx, { metrics: pageMetrics, pager: PAGER });
   return metricsView(ctx, mstate, { pager: PAGER });
 }
 
@@ -317,6 +318,29 @@ function amdSchedule(request, clock) {
     const t = telemetryScope(store.getSnapshot(), PAGER);
     return t.scope === undefined ? { opts: undefined, scope: undefined } : { opts: { scope: t.scope, summary: summary }, scope: t.scope };
   }
+  /** Resolves when the store's snapshot has the node list (or its error). */
+  function nodesListed() {
+    return listed('nodesState');
+  }
+  function listed(which) {
+    return new Promise(function (resolve) {
+      function done() {
+        const st = store.getSnapshot()[which];
+        return st === 'ready' || st === 'error';
+      }
+      if (done()) return resolve();
+      const off = store.subscribe(function () {
+        if (done()) {
+          off();
+          resolve();
+        }
+      });
+    });
+  }
+  function fetchPodsPage() {
+    const o = ownersScope(store.getSnapshot(), PAGER);
+    return metrics.fetchGpuOwners(o.pods === undefined ? undefined : { pods: o.pods }).then(function (m) { pageMetrics.pods = m; });
+  }
   function fetchNodesPage() {
     return metrics.fetchGpuMetrics('topology', scoped(false).opts).then(function (m) { pageMetrics.nodes = m; });
   }
@@ -338,26 +362,24 @@ function amdSchedule(request, clock) {
     /** One page's Refresh button, as src/plugin.js wires it. */
     refreshPage: function (page) {
       if (page === 'nodes') return Promise.all([store.refresh(), fetchNodesPage()]);
-      if (page === 'pods') {
-        return Promise.all([store.refresh(), metrics.fetchGpuOwners().then(function (m) { pageMetrics.pods = m; })]);
-      }
+      if (page === 'pods') return Promise.all([store.refresh(), fetchPodsPage()]);
       if (page === 'metrics') return fetchMetricsPage();
       return store.refresh();
     },
     /**
      * One page opened on an empty cache, as src/plugin.js mounts it: the
-     * provider's lists + DeviceConfig request in one wave; GPU Pods adds its
-     * owners query to it; GPU Nodes and Metrics ask for the telemetry of
-     * their first page of nodes once the node list is there (a second wave).
+     * provider's lists + DeviceConfig request in one wave; GPU Nodes and
+     * Metrics ask for the telemetry of their first page of nodes once the
+     * node list is there, GPU Pods for the owners of its first page of pods
+     * once the pod list is there (a second wave).
      */
     coldOpenPage: function (page) {
-      // The page's metrics hook is enabled once the provider stops loading
-      // (lists and DeviceConfig answered): pages.js telemetryScope.
-      if (page === 'nodes') return Promise.all([store.loadLists(), store.refresh()]).then(fetchNodesPage);
-      if (page === 'metrics') return Promise.all([store.loadLists(), store.refresh()]).then(fetchMetricsPage);
-      const base = [store.loadLists(), store.refresh()];
-      if (page === 'pods') base.push(metrics.fetchGpuOwners().then(function (m) { pageMetrics.pods = m; }));
-      return Promise.all(base);
+      // The page's metrics hook is enabled once the node list is in
+      // (pages.js telemetryScope): it re-runs on the snapshot that carries it.
+      if (page === 'nodes') return Promise.all([store.loadLists(), store.refresh(), nodesListed().then(fetchNodesPage)]);
+      if (page === 'metrics') return Promise.all([store.loadLists(), store.refresh(), nodesListed().then(fetchMetricsPage)]);
+      if (page === 'pods') return Promise.all([store.loadLists(), store.refresh(), listed('podsState').then(fetchPodsPage)]);
+      return Promise.all([store.loadLists(), store.refresh()]);
     },
     pageMetrics: function (page) { return page in pageMetrics && pageMetrics[page] ? pageMetrics[page] : mstate.metrics; },
     /** The Metrics page's own state (its hook), for rendering that page. */
@@ -676,9 +698,12 @@ async function serve(a) {
         }
         const ctx = L.s.ctx();
         const pods = ctx.gpuPods.filter(function (p) { return p.spec && p.spec.nodeName; });
-        const modes = { podScoped: [], podDetail: [], podClusterWide: [], nodeScoped: [], nodeDetail: [], podsPageOwners: [] };
-        const bytes = { podScoped: 0, podDetail: 0, podClusterWide: 0, nodeScoped: 0, nodeDetail: 0, podsPageOwners: 0 };
-        const reqs = { podScoped: 0, podDetail: 0, podClusterWide: 0, nodeScoped: 0, nodeDetail: 0, podsPageOwners: 0 };
+        const MODES = ['podScoped', 'podDetail', 'podClusterWide', 'nodeScoped', 'nodeDetail', 'nodeDetailCold',
+          'nodeDetailColdReference', 'podsPageOwners'];
+        const modes = {};
+        const bytes = {};
+        const reqs = {};
+        MODES.forEach(function (k) { modes[k] = []; bytes[k] = 0; reqs[k] = 0; });
         const slow = [];
         const detailRequest = makeRequest(a.url, counter);
         for (let i = 0; i < n && pods.length; i++) {
@@ -703,9 +728,31 @@ async function serve(a) {
               return Promise.all([src.fetchNodeMetrics(pod.spec.nodeName), src.fetchNodeSeries(pod.spec.nodeName, 1800, 30)])
                 .then(function (r) { return node ? nodeDetailView(node, ctx, { metrics: r[0], series: r[1] }) : null; });
             }],
-            // GPU Pods page: pod → GPU attribution only.
+            // Node detail on a COLD store (no plugin page visited), as
+            // src/plugin.js NodeDetailCold wires it: the node's pods by one
+            // field-selected request, its telemetry and history, one wave.
+            ['nodeDetailCold', function (src) {
+              const nm = pod.spec.nodeName;
+              return Promise.all([fetchNodePods(detailRequest, nm), src.fetchNodeMetrics(nm), src.fetchNodeSeries(nm, 1800, 30)])
+                .then(function (r) {
+                  const cold = { loading: false, gpuPods: filterGpuRequestingPods(r[0]), podsState: 'ready', error: null };
+                  return node ? nodeDetailView(node, cold, { metrics: r[1], series: r[2] }) : null;
+                });
+            }],
+            // The reference on the same open: a full provider (both
+            // cluster-wide lists alongside CRD + 3 serial selector requests,
+            // src/index.tsx:152-160), then its section from that context.
+            ['nodeDetailColdReference', function () {
+              const ref = createReferenceSchedule(detailRequest);
+              return ref.coldOpenPage('nodes').then(function () { return node ? nodeDetailView(node, ref.snapshot()) : null; });
+            }],
+            // GPU Pods page: pod → GPU attribution of its first page of pods only.
             ['podsPageOwners', function (src) {
-              return src.fetchGpuOwners().then(function (m) { renderPage(podsView(ctx, { metrics: m })); return null; });
+              const o = ownersScope(ctx, PAGER);
+              return src.fetchGpuOwners(o.pods === undefined ? undefined : { pods: o.pods }).then(function (m) {
+                renderPage(podsView(ctx, { metrics: m, pager: PAGER }));
+                return null;
+              });
             }],
           ];
           for (let r = 0; r < runs.length; r++) {

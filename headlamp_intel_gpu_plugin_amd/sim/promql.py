@@ -48,7 +48,7 @@ class Series:
     or explicit samples appended with :meth:`push` (kept sorted, bounded).
     """
 
-    __slots__ = ("labels", "fn", "interval", "ts", "vs", "cap", "_key", "_json", "_memo")
+    __slots__ = ("labels", "fn", "interval", "ts", "vs", "cap", "_key", "_json", "_memo", "seq")
 
     def __init__(self, labels: Labels, fn: Optional[Callable[[float], float]] = None,
                  interval: float = 15.0, cap: int = 4096):
@@ -59,6 +59,7 @@ class Series:
         self.vs: List[float] = []
         self.cap = cap
         self._key = tuple(sorted(self.labels.items()))
+        self.seq = 0  # insertion order in its TSDB
         self._json = None
         self._memo: Dict[float, float] = {}  # fn value per sample time (fn series are deterministic)
 
@@ -125,6 +126,14 @@ class TSDB:
         self._fn_intervals: set = set()
         self._query_cache: Dict[str, tuple] = {}
         self._range_cache: Dict[str, tuple] = {}  # query → (mutation stamp, {t → rows})
+        # Inverted index (label, value) → series, as a real TSDB's postings:
+        # a `hostname=~"a|b|…"` page scope or `hostname="x"` detail query
+        # reads the matching series only, not every series of its names.
+        self._by_label: Dict[tuple, List[Series]] = {}
+        self._name_rank: Dict[str, int] = {}
+        # Aggregations over a plain selector: the function-backed series' part
+        # per (query part, sample-grid bucket); pushed series are added each time.
+        self._agg_cache: Dict[tuple, dict] = {}
 
     def label_json(self, labels: Labels) -> str:
         """JSON for a label set; cached when it is a stored series' own dict
@@ -157,11 +166,18 @@ class TSDB:
             return self._index[key]
         self._index[key] = series
         _MUTATIONS[0] += 1
+        series.seq = len(self._index)
         if series.fn is not None:
             self._fn_intervals.add(series.interval)
-        self.by_name.setdefault(series.labels.get("__name__", ""), []).append(series)
+        name = series.labels.get("__name__", "")
+        if name not in self.by_name:
+            self._name_rank[name] = len(self._name_rank)
+        self.by_name.setdefault(name, []).append(series)
+        for kv in series.labels.items():
+            self._by_label.setdefault(kv, []).append(series)
         self._by_labels_id[id(series.labels)] = series
         self._select_cache.clear()
+        self._agg_cache.clear()
         return series
 
     def get_or_create(self, labels: Labels) -> Series:
@@ -178,6 +194,25 @@ class TSDB:
         hit = self._select_cache.get(sig)
         if hit is not None:
             return hit
+        # The most selective indexable matcher (= or a =~ of literal
+        # alternatives) picks the candidates; every matcher then filters.
+        best = None
+        for m in matchers:
+            vals = m.literals()
+            if vals is None:
+                continue
+            lists = [self._by_label.get((m.label, v), []) for v in vals]
+            n = sum(len(x) for x in lists)
+            if best is None or n < best[0]:
+                best = (n, lists)
+        if best is not None:
+            cands = best[1][0] if len(best[1]) == 1 else [x for lst in best[1] for x in lst]
+            out = [x for x in cands if all(m.matches(x.labels.get(m.label, "")) for m in matchers)]
+            # the order a scan by name would give: names in insertion order, then series
+            rank = self._name_rank
+            out.sort(key=lambda x: (rank.get(x.labels.get("__name__", ""), 0), x.seq))
+            self._select_cache[sig] = out
+            return out
         names = [m for m in matchers if m.label == "__name__" and m.op == "="]
         if names:
             cands = self.by_name.get(names[0].value, [])
@@ -244,6 +279,21 @@ class Matcher:
     def __init__(self, label: str, op: str, value: str):
         self.label, self.op, self.value = label, op, value
         self._re = re.compile("^(?:" + value + ")$") if op in ("=~", "!~") else None
+
+    def literals(self) -> Optional[List[str]]:
+        """The exact values this matcher accepts, when it is `=` / a `=~` of
+        literal alternatives and none is empty (an empty value also matches
+        series without the label); else None."""
+        if self.op == "=":
+            return [self.value] if self.value else None
+        if self.op != "=~":
+            return None
+        out = []
+        for part in re.split(r"(?<!\\)\|", self.value):
+            if not part or re.search(r"(?<!\\)[.^$*+?()\[\]{}|]", part):
+                return None
+            out.append(re.sub(r"\\(.)", r"\1", part))
+        return out
 
     def matches(self, v: str) -> bool:
         if self.op == "=":
@@ -492,6 +542,8 @@ class Evaluator:
             return ("vector", out)
         if kind == "agg":
             _, op, by, without, e = node
+            if e[0] == "sel" and e[2] is None and len(self.db._fn_intervals) <= 1:
+                return self._agg_selector(node, t)
             typ, vec = self.instant(e, t)
             if typ != "vector":
                 raise PromQLError("aggregation over scalar")
@@ -526,6 +578,74 @@ class Evaluator:
         if kind == "label_replace":
             return self._label_replace(node, t)
         raise PromQLError(f"cannot evaluate {kind}")
+
+    def _group(self, labels, byt, without):
+        if byt is not None:
+            return self.db.project(labels, byt)
+        gl = ({k: x for k, x in _drop_name(labels).items() if k not in without} if without is not None else {})
+        return tuple(sorted(gl.items())), gl
+
+    def _agg_selector(self, node, t):
+        """`op by (…) (selector)`: the function-backed series change only on
+        their sample grid, so their per-group partial (sum, count, max, min)
+        is kept per grid bucket; pushed (live) series are folded in on every
+        evaluation. Same result as aggregating the selected vector."""
+        _, op, by, without, e = node
+        byt = tuple(by) if by is not None else None
+        wt = tuple(without) if without is not None else None
+        db = self.db
+        iv = next(iter(db._fn_intervals)) if db._fn_intervals else 1.0
+        sig = tuple((m.label, m.op, m.value) for m in e[1])
+        key = (sig, byt, wt, math.floor(t / iv))
+        hit = db._agg_cache.get(key)
+        if hit is None:
+            parts: Dict[tuple, list] = {}
+            pushed = []
+            counting = op == "count"  # a function-backed series always has a sample: no value needed
+            for s in db.select(e[1]):
+                if s.fn is None:
+                    pushed.append(s)
+                    continue
+                v = 1.0 if counting else s.at(t)[1]
+                k, gl = self._group(s.labels, byt, wt)
+                a = parts.get(k)
+                if a is None:
+                    parts[k] = [gl, v, 1, v, v]
+                else:
+                    a[1] += v
+                    a[2] += 1
+                    if v > a[3]:
+                        a[3] = v
+                    if v < a[4]:
+                        a[4] = v
+            if len(db._agg_cache) > 512:
+                db._agg_cache.clear()
+            hit = db._agg_cache[key] = (parts, pushed)
+        parts, pushed = hit
+        groups = parts
+        if pushed:
+            groups = {k: list(a) for k, a in parts.items()}
+            for s in pushed:
+                smp = s.at(t)
+                if smp is None:
+                    continue
+                v = smp[1]
+                k, gl = self._group(s.labels, byt, wt)
+                a = groups.get(k)
+                if a is None:
+                    groups[k] = [gl, v, 1, v, v]
+                else:
+                    a[1] += v
+                    a[2] += 1
+                    if v > a[3]:
+                        a[3] = v
+                    if v < a[4]:
+                        a[4] = v
+        res = []
+        for gl, total, n, hi, lo in groups.values():
+            r = {"sum": total, "avg": total / n, "max": hi, "min": lo}.get(op, float(n))
+            res.append((gl, r))
+        return ("vector", res)
 
     def _label_replace(self, node, t):
         _, arg, dst, repl, src, regex = node

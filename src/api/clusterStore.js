@@ -48,6 +48,8 @@ import {
 import { createListTracker } from './listCache.js';
 
 export const DEFAULT_REQUEST_TIMEOUT_MS = 2000;
+/** Time limit of a whole-cluster node / pod list (loadLists). */
+export const LIST_TIMEOUT_MS = 60000;
 
 /**
  * True when two lists hold the same Kubernetes objects at the same versions
@@ -291,9 +293,9 @@ export function createClusterStore(opts) {
     for (let i = 0; i < ls.length; i++) ls[i]();
   }
 
-  function traced(name, path) {
+  function traced(name, path, ms) {
     const start = clock.now();
-    const p = withTimeout(request(path), timeoutMs, clock);
+    const p = withTimeout(request(path), ms || timeoutMs, clock);
     if (!onTrace) return p;
     return p.then(
       function (v) {
@@ -431,11 +433,14 @@ export function createClusterStore(opts) {
   function loadLists() {
     if (s.podsState === 'unknown') s.podsState = 'pending';
     if (s.nodesState === 'unknown') s.nodesState = 'pending';
-    const nodesP = traced('nodes', '/api/v1/nodes').then(
+    // Whole-cluster lists (what Headlamp's useList() delivers in the plugin;
+    // loaded here by the terminal client and the harness) take far longer
+    // than a CRD request on a large cluster: tens of MB at 1,000 nodes.
+    const nodesP = traced('nodes', '/api/v1/nodes', LIST_TIMEOUT_MS).then(
       function (l) { setNodes(isKubeList(l) ? l.items : [], null); },
       function (e) { setNodes([], e instanceof Error ? e.message : String(e)); }
     );
-    const podsP = traced('pods', '/api/v1/pods').then(
+    const podsP = traced('pods', '/api/v1/pods', LIST_TIMEOUT_MS).then(
       function (l) { setPods(isKubeList(l) ? l.items : [], null); },
       function (e) { setPods([], e instanceof Error ? e.message : String(e)); }
     );
@@ -507,4 +512,33 @@ export function getSharedStore(key, factory) {
 
 export function resetSharedStores() {
   for (const k in shared) delete shared[k];
+}
+
+/** Path of one node's pods (a field selector: the apiserver filters, O(pods on the node)). */
+export function nodePodsPath(nodeName) {
+  return '/api/v1/pods?fieldSelector=' + encodeURIComponent('spec.nodeName=' + nodeName);
+}
+
+/**
+ * The pods of ONE node, for a Node detail page opened on a cold store: one
+ * field-selected list instead of the cluster-wide node + pod lists and the
+ * CRD / operator-pod requests the reference's provider mounts there
+ * (reference src/index.tsx:152-160, IntelGpuDataContext.tsx:98-165).
+ * Resolves to the node's pods; rejects with the request's error.
+ * @param {(path: string) => Promise<any>} request
+ * @param {string} nodeName
+ * @param {number} [timeoutMs]
+ * @param {{setTimeout: Function, clearTimeout: Function}} [clock]
+ * @returns {Promise<any[]>}
+ */
+export function fetchNodePods(request, nodeName, timeoutMs, clock) {
+  return withTimeout(request(nodePodsPath(nodeName)), timeoutMs || DEFAULT_REQUEST_TIMEOUT_MS, clock || defaultClock).then(function (l) {
+    return isKubeList(l) ? l.items : [];
+  });
+}
+
+/** True when the store has both cluster lists (a plugin page fed it): detail views can read it. */
+export function storeIsWarm(store) {
+  const s = store && store.getSnapshot();
+  return !!s && s.nodesState === 'ready' && s.podsState === 'ready';
 }

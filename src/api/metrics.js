@@ -489,8 +489,20 @@ export function exporterNodeQuery(nodeName, withStatic) {
  * `pod` label is set — one series per allocated GPU, instead of every live
  * gauge and xGMI link of every GPU.
  */
-export function ownersQuery() {
-  return 'max by (' + EXPORTER_JOIN_LABELS.join(', ') + ') ({__name__="' + SERIES.exporter.power + '", pod!=""})';
+export function ownersQuery(pods) {
+  const sel = '{__name__="' + SERIES.exporter.power + '", ';
+  if (!pods) return 'max by (' + EXPORTER_JOIN_LABELS.join(', ') + ') (' + sel + 'pod!=""})';
+  // The pods of one page of the Pods table ("namespace/name" keys): O(page).
+  const names = {};
+  const nss = {};
+  for (let i = 0; i < pods.length; i++) {
+    const k = String(pods[i]);
+    const slash = k.indexOf('/');
+    nss[k.slice(0, slash)] = true;
+    names[k.slice(slash + 1)] = true;
+  }
+  const alt = function (o) { return promString(Object.keys(o).map(regexLiteral).join('|')); };
+  return 'max by (' + EXPORTER_JOIN_LABELS.join(', ') + ') (' + sel + 'pod=~"' + alt(names) + '", namespace=~"' + alt(nss) + '"})';
 }
 
 /** The part of a snapshot that belongs to one node (GPU objects shared, not copied). */
@@ -1123,13 +1135,18 @@ export function createMetricsSource(opts) {
    * node-exporter). Stale / null handling as in fetchGpuMetrics.
    * @returns {Promise<GpuMetrics|null>}
    */
-  function fetchGpuOwners() {
-    return shared('owners', ownersSnapshot);
+  function fetchGpuOwners(opts) {
+    const pods = opts && Array.isArray(opts.pods) ? opts.pods.map(String) : null;
+    if (pods && pods.length === 0) {
+      return Promise.resolve({ source: source, gpus: [], xgmi: {}, links: {}, fetchedAt: new Date(clock.now()).toISOString(),
+        prometheusPath: cachedPath, scope: 'owners' });
+    }
+    return shared('owners|' + (pods ? pods.join(',') : '*'), function () { return ownersSnapshot(pods); });
   }
 
-  function ownersSnapshot() {
+  function ownersSnapshot(pods) {
     return withPrometheus(function (base) {
-      return combined(base, ownersQuery()).then(function (res) {
+      return combined(base, ownersQuery(pods)).then(function (res) {
         if (!res.ok) return UNREACHABLE;
         ownersFailures = 0;
         const j = joinExporterResults(res.rows);

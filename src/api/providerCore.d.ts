@@ -37,22 +37,24 @@ export interface ClusterStore {
 }
 
 export interface MetricsSource {
-  fetchGpuMetrics(view?: 'all' | 'gauges' | 'topology'): Promise<GpuMetrics | null>;
+  /** `scope`: node names of a paged view (hostname=~); `summary`: also the cluster totals (GpuMetrics.totals) */
+  fetchGpuMetrics(view?: 'all' | 'gauges' | 'topology', opts?: { scope: string[]; summary?: boolean }): Promise<GpuMetrics | null>;
   fetchNodeMetrics(nodeName: string): Promise<GpuMetrics | null>;
-  fetchGpuOwners(): Promise<GpuMetrics | null>;
+  /** `pods`: "namespace/name" keys of one page of the Pods table */
+  fetchGpuOwners(opts?: { pods: string[] }): Promise<GpuMetrics | null>;
   failureReason(): 'forbidden' | 'unreachable';
   fetchPodSeries(namespace: string, pod: string, rangeSec: number, stepSec: number): Promise<{ rangeSec: number; stepSec: number; power: Array<[number, number]> } | null>;
   fetchNodeSeries(nodeName: string, rangeSec: number, stepSec: number): Promise<{ rangeSec: number; stepSec: number; power: Array<[number, number]> } | null>;
-  fetchSeries(rangeSec: number, stepSec: number): Promise<GpuMetricsState['series']>;
+  fetchSeries(rangeSec: number, stepSec: number, scope?: string[]): Promise<GpuMetricsState['series']>;
 }
 
 export interface ProviderCore {
   Context: Context<AmdGpuContextValue | null>;
   AmdGpuDataProvider: ComponentType<{ children?: ReactNode }>;
   useAmdGpuContext(): AmdGpuContextValue;
-  useGpuMetrics(enabled?: boolean, withSeries?: boolean, view?: 'all' | 'gauges' | 'topology'): GpuMetricsState;
+  useGpuMetrics(enabled?: boolean, withSeries?: boolean, view?: 'all' | 'gauges' | 'topology', scope?: string[]): GpuMetricsState;
   useNodeGpuMetrics(nodeName: string | null, enabled?: boolean): GpuMetricsState;
-  useGpuOwners(enabled?: boolean): GpuMetricsState;
+  useGpuOwners(enabled?: boolean, pods?: string[]): GpuMetricsState;
   usePodGpuSeries(namespace: string | null, pod: string | null, enabled?: boolean): GpuMetricsState;
   useNodeGpuSeries(nodeName: string | null, enabled?: boolean): GpuMetricsState;
   storeFor(cluster: string): ClusterStore;

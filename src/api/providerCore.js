@@ -24,7 +24,8 @@
  *     (reference quirk Q7: every route mounted a cold provider).
  */
 
-import { createClusterStore, getSharedStore } from './clusterStore.js';
+import { createClusterStore, fetchNodePods, getSharedStore, storeIsWarm } from './clusterStore.js';
+import { filterGpuRequestingPods } from './amdgpu.js';
 import { createMetricsSource } from './metrics.js';
 import { clusterKey as defaultClusterKey } from './cluster.js';
 import { POLL_MISS, createPoller, loadSettings as defaultLoadSettings, prometheusCandidates, seriesStepSec } from './settings.js';
@@ -308,6 +309,49 @@ export function createProviderCore(React, lib, deps) {
     }, true);
   }
 
+  /**
+   * True when the cluster's shared store already holds the node and pod lists
+   * (a plugin page fed it): a Node detail section then reads it; otherwise it
+   * reads its own node's pods (useNodePods) instead of mounting the
+   * cluster-wide watches.
+   */
+  function storeWarm() {
+    return storeIsWarm(storeFor(clusterKey()));
+  }
+
+  /**
+   * The pods of one node for a Node detail section on a cold store: ONE
+   * field-selected request (clusterStore.js fetchNodePods), fetched in the
+   * same wave as the node's telemetry and history — O(pods on the node)
+   * instead of the reference's full provider on every Node detail page
+   * (src/index.tsx:152-160: both cluster-wide lists + 4 serial requests).
+   * Returns the slice of the context nodeDetailView reads.
+   */
+  function useNodePods(nodeName, enabled) {
+    const active = (enabled === undefined ? true : enabled) && !!nodeName;
+    const st = useState({ node: null, pods: null, error: null });
+    const state = st[0];
+    const setState = st[1];
+    useEffect(function () {
+      if (!active) return undefined;
+      let cancelled = false;
+      fetchNodePods(request, nodeName, loadSettings().requestTimeoutMs).then(
+        function (items) { if (!cancelled) setState({ node: nodeName, pods: items, error: null }); },
+        function (e) { if (!cancelled) setState({ node: nodeName, pods: [], error: errorText(e) }); }
+      );
+      return function () { cancelled = true; };
+    }, [nodeName, active]);
+    return useMemo(function () {
+      const mine = state.node === nodeName;
+      return {
+        loading: active && (!mine || state.pods === null),
+        gpuPods: mine && state.pods ? filterGpuRequestingPods(state.pods) : [],
+        podsState: mine && state.error ? 'error' : mine && state.pods ? 'ready' : 'pending',
+        error: mine ? state.error : null,
+      };
+    }, [state, nodeName, active]);
+  }
+
   /** One node's GPU power history for the native Node detail page (metrics.js fetchNodeSeries). */
   function useNodeGpuSeries(nodeName, enabled) {
     const cluster = clusterKey();
@@ -321,13 +365,20 @@ export function createProviderCore(React, lib, deps) {
     }, true);
   }
 
-  /** Pod → GPU attribution for the Pods page (metrics.js fetchGpuOwners): one series per allocated GPU. */
-  function useGpuOwners(enabled) {
+  /**
+   * Pod → GPU attribution for the Pods page (metrics.js fetchGpuOwners): one
+   * series per allocated GPU — of the pods on the page when `pods` (their
+   * "namespace/name" keys) is given, else of every pod.
+   */
+  function useGpuOwners(enabled, pods) {
     const cluster = clusterKey();
     const source = metricsSourceFor(cluster);
     const on = enabled === undefined ? true : enabled;
-    return useMetricsFetch(on ? 'owners|' + sourceKey(cluster, loadSettings()) : null, function () {
-      return source.fetchGpuOwners().then(function (m) { return [m, null]; });
+    const scoped = Array.isArray(pods);
+    const keys = scoped ? pods.slice() : null;
+    const key = 'owners|' + sourceKey(cluster, loadSettings()) + (scoped ? '|pods:' + keys.join(',') : '');
+    return useMetricsFetch(on ? key : null, function () {
+      return source.fetchGpuOwners(scoped ? { pods: keys } : undefined).then(function (m) { return [m, null]; });
     }, false, source);
   }
 
@@ -340,6 +391,8 @@ export function createProviderCore(React, lib, deps) {
     useGpuOwners: useGpuOwners,
     usePodGpuSeries: usePodGpuSeries,
     useNodeGpuSeries: useNodeGpuSeries,
+    useNodePods: useNodePods,
+    storeWarm: storeWarm,
     storeFor: storeFor,
     metricsSourceFor: metricsSourceFor,
   };

@@ -275,8 +275,26 @@ export interface GpuMetrics {
   prometheusPath: string;
   /** PromQL the snapshot came from (Metrics page "Query" row). */
   query?: string;
-  /** PromQL of the main telemetry query (shown on the Metrics page) */
-  query?: string;
+  /** node names a paged snapshot covers (gpus holds only theirs) */
+  scope?: string[];
+  /** cluster totals of a paged snapshot, from server-side aggregates */
+  totals?: GpuTotals;
+}
+
+/** Cluster totals (metrics.js totalsFromRows / summarizeMetrics + nodes reporting). */
+export interface GpuTotals {
+  gpus: number;
+  withPower: number;
+  nodes?: number;
+  powerWatts: number;
+  powerCapWatts: number;
+  vramUsedBytes: number;
+  vramTotalBytes: number;
+  avgGfxActivityPct: number | null;
+  eccCorrectable: number | null;
+  eccUncorrectable: number | null;
+  powerCapAssumed: number;
+  tempLimitAssumed: number;
 }
 
 export interface GpuSeries {
@@ -285,6 +303,10 @@ export interface GpuSeries {
   stepSec?: number;
   power: Record<string, Array<[number, number]>>;
   vram: Record<string, Array<[number, number]>>;
+  /** node names of a paged window (power / vram hold only theirs) */
+  scope?: string[];
+  /** the cluster-wide line of a paged window */
+  total?: { power: Array<[number, number]>; vram: Array<[number, number]> };
 }
 
 export interface GpuMetricsState {

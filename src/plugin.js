@@ -30,6 +30,7 @@ import {
   overviewView,
   podDetailView,
   podsView,
+  ownersScope,
   telemetryScope,
 } from './view/pages.js';
 import { createRenderer } from './view/react.js';
@@ -66,7 +67,11 @@ export function createPlugin(env) {
   /** AMD GPU Operator DeviceConfigs and operand pods (reference DevicePluginsPage.tsx, C6). */
   function DevicePluginsPage() {
     const ctx = core.useAmdGpuContext();
-    return h(Page, { vm: devicePluginsView(ctx), onRefresh: ctx.refresh });
+    const pager = usePager();
+    return h(Page, {
+      vm: devicePluginsView(ctx, { pager: pager.state }), onRefresh: ctx.refresh,
+      onPage: pager.onPage, onFilter: pager.onFilter,
+    });
   }
 
   /**
@@ -107,18 +112,24 @@ export function createPlugin(env) {
   }
 
   /**
-   * Pods requesting amd.com/* (reference PodsPage.tsx, C8). Exporter pod
-   * labels add the physical GPUs each pod holds — fetched as attribution only,
-   * one series per allocated GPU.
+   * Pods requesting amd.com/* (reference PodsPage.tsx, C8), one page of the
+   * table at a time. Exporter pod labels add the physical GPUs each pod on
+   * the page holds — fetched as attribution only, one series per allocated
+   * GPU of those pods.
    */
   function PodsPage() {
     const ctx = core.useAmdGpuContext();
-    const m = core.useGpuOwners();
+    const pager = usePager();
+    const o = ownersScope(ctx, pager.state);
+    const m = core.useGpuOwners(o.enabled, o.pods);
     function refresh() {
       ctx.refresh();
       m.refresh();
     }
-    return h(Page, { vm: podsView(ctx, { metrics: m.metrics }), onRefresh: refresh });
+    return h(Page, {
+      vm: podsView(ctx, { metrics: m.metrics, pager: pager.state }), onRefresh: refresh,
+      onPage: pager.onPage, onFilter: pager.onFilter,
+    });
   }
 
   /**
@@ -155,6 +166,31 @@ export function createPlugin(env) {
     const ps = core.useNodeGpuSeries(gpuNode ? raw.metadata.name : null, gpuNode);
     const section = nodeDetailView(props.resource, ctx, { metrics: m.metrics, series: ps.series });
     return section ? h(Section, { s: section }) : null;
+  }
+
+  /**
+   * The Node detail section on a cold store (no plugin page visited yet): the
+   * node's own pods by one field-selected request, with its telemetry and
+   * power history in the same wave — no cluster-wide watch is mounted.
+   */
+  function NodeDetailCold(props) {
+    const raw = unwrapKubeObject(props.resource);
+    const gpuNode = isAmdGpuNode(raw);
+    const name = gpuNode ? raw.metadata.name : null;
+    const ctx = core.useNodePods(name, gpuNode);
+    const m = core.useNodeGpuMetrics(name, gpuNode);
+    const ps = core.useNodeGpuSeries(name, gpuNode);
+    const section = nodeDetailView(props.resource, ctx, { metrics: m.metrics, series: ps.series });
+    return section ? h(Section, { s: section }) : null;
+  }
+
+  /**
+   * Warm store (a plugin page loaded the cluster): the section reads it under
+   * the shared provider. Cold: NodeDetailCold, O(one node).
+   */
+  function NodeDetailHost(props) {
+    if (core.storeWarm()) return h(core.AmdGpuDataProvider, null, h(NodeDetailSection, props));
+    return h(NodeDetailCold, props);
   }
 
   /**
@@ -201,11 +237,15 @@ export function createPlugin(env) {
     return Route;
   }
 
-  /** Detail-view section callback for Nodes (reference src/index.tsx:152-160). */
+  /**
+   * Detail-view section callback for Nodes (reference src/index.tsx:152-160,
+   * which mounts a full provider — both cluster-wide lists and the CRD /
+   * operator-pod requests — on every Node detail page).
+   */
   function nodeDetailSectionFor(args) {
     const resource = args && args.resource;
     if (!resource || resource.kind !== 'Node') return null;
-    return h(core.AmdGpuDataProvider, null, h(NodeDetailSection, { resource: resource }));
+    return h(NodeDetailHost, { resource: resource });
   }
 
   /** Detail-view section callback for Pods: no provider (reference src/index.tsx:167-170). */
@@ -226,6 +266,7 @@ export function createPlugin(env) {
     PodsPage: PodsPage,
     MetricsPage: MetricsPage,
     NodeDetailSection: NodeDetailSection,
+    NodeDetailCold: NodeDetailCold,
     PodDetailSection: PodDetailSection,
     SettingsPage: createSettingsPage(React, env.CommonComponents, env.settingsStorage),
     buildNodeGpuColumns: buildNodeGpuColumns,

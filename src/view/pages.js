@@ -305,17 +305,42 @@ function overviewDeviceConfigs(dcs, now) {
   ]);
 }
 
+/** Operator pods listed on the Overview (the Device Plugins page pages through all of them). */
+export const OVERVIEW_PLUGIN_PODS = 10;
+
+/**
+ * Operator pods on the Overview: the not-ready ones first, at most
+ * OVERVIEW_PLUGIN_PODS rows, with a count of the rest. The reference lists
+ * every daemon pod here (OverviewPage.tsx:252-272): three per GPU node, so
+ * thousands of rows on a large cluster.
+ */
 function overviewPluginPods(pods, now) {
-  return section('Plugin Daemon Pods', [
+  const notReady = chunkedFilter('ov-plugin-not-ready', pods, function (p) { return !isPodReady(p); });
+  let shown = pods;
+  if (pods.length > OVERVIEW_PLUGIN_PODS) {
+    shown = notReady.slice(0, OVERVIEW_PLUGIN_PODS);
+    for (let i = 0; i < pods.length && shown.length < OVERVIEW_PLUGIN_PODS; i++) {
+      if (isPodReady(pods[i])) shown.push(pods[i]);
+    }
+  }
+  const blocks = [
     table(
       ['Name', 'Namespace', 'Component', 'Node', 'Status', 'Age'],
-      chunkedRows('ov-plugin-rows', pods, [], function (p) {
+      chunkedRows('ov-plugin-rows', shown, [], function (p) {
         return ovPluginRows(p, [], function () {
           return [podName(p), podNs(p), formatComponent(pluginPodComponent(p)), podNode(p), readyLabel(p), ageText(p.metadata.creationTimestamp, now)];
         }, now);
       }, now)
     ),
-  ]);
+  ];
+  if (shown.length < pods.length) {
+    const nr = notReady.length > 0 ? status('warning', notReady.length + ' not ready') : status('success', 'all ready');
+    blocks.push(kv([
+      row('Shown', shown.length + ' of ' + pods.length + ' operator pods (not-ready first; all of them on the Device Plugins page)'),
+      row('Readiness', nr),
+    ]));
+  }
+  return section('Plugin Daemon Pods', blocks);
 }
 
 function overviewNodes(gpuNodes, t) {
@@ -417,16 +442,19 @@ function enabledCell(on, detail) {
 export function devicePluginsView(ctx, opts) {
   const now = nowOf(opts);
   if (ctx.loading) return page(null, null, [loader('Loading device plugin data...')]);
+  // One page of the operator pod table (PODS_PER_PAGE; filter on
+  // namespace/name and node): three per GPU node on a real cluster.
+  const pg = podPage(ctx.pluginPods, opts && opts.pager, 'plugin-pod');
   const items = memo(
     'device-plugins',
-    [ctx.deviceConfigs, ctx.pluginPods, ctx.crdAvailable, ctx.error],
-    function () { return devicePluginsItems(ctx, now); },
+    [ctx.deviceConfigs, pg, ctx.crdAvailable, ctx.error],
+    function () { return devicePluginsItems(ctx, now, pg); },
     now
   );
   return page(BRAND + ' — Device Plugins', refreshButton('Refresh device plugin data', ctx.refreshing), items);
 }
 
-function devicePluginsItems(ctx, now) {
+function devicePluginsItems(ctx, now, pg) {
   const items = [];
   if (ctx.error) items.push(errorSection(ctx.error));
 
@@ -496,11 +524,12 @@ function devicePluginsItems(ctx, now) {
   }
 
   if (ctx.pluginPods.length > 0) {
+    items.push(pager(pg, 'operator pods'));
     items.push(
       section('Plugin Daemon Pods', [
         table(
           ['Name', 'Namespace', 'Component', 'Node', 'Ready', 'Restarts', 'Age'],
-          chunkedRows('dp-plugin-rows', ctx.pluginPods, [], function (p) {
+          chunkedRows('dp-plugin-rows', pg.nodes, [], function (p) {
             return dpPluginRows(p, [], function () {
               return [
                 podName(p), podNs(p), formatComponent(pluginPodComponent(p)), podNode(p), readyLabel(p),
@@ -543,22 +572,51 @@ function nodeNameOf(n) {
  *            total: number, matched: number, filter: string, perPage: number}}
  */
 export function nodePage(gpuNodes, state) {
+  const p = listPage('node', gpuNodes, state, nodeNameOf, nodeNameOf, NODES_PER_PAGE);
+  return p;
+}
+
+/** GPU pods per page on the GPU Pods page (and operator pods on Device Plugins). */
+export const PODS_PER_PAGE = 25;
+
+function podKeyOf(p) {
+  return (p.metadata.namespace || '') + '/' + p.metadata.name;
+}
+
+function podSearchText(p) {
+  return podKeyOf(p) + ' ' + get(p, ['spec', 'nodeName'], '');
+}
+
+/**
+ * The slice of pods a paged table shows (nodePage for pods): the filter is
+ * a case-insensitive substring of "namespace/name node". `names` are
+ * "namespace/name" keys; `nodes` holds the pod objects.
+ */
+export function podPage(pods, state, kind) {
+  return listPage(kind || 'pod', pods, state, podKeyOf, podSearchText, PODS_PER_PAGE);
+}
+
+/**
+ * Slice `all` for a pager `state` ({page, filter, perPage}); memoised per
+ * kind + state on the list's identity.
+ */
+function listPage(kind, all0, state, keyOf, textOf, perDefault) {
   const st = state || {};
-  const per = st.perPage > 0 ? Math.min(Math.floor(st.perPage), 200) : NODES_PER_PAGE;
+  const per = st.perPage > 0 ? Math.min(Math.floor(st.perPage), 200) : perDefault;
   // The raw text is kept for the input box; matching ignores surrounding spaces.
   const filter = typeof st.filter === 'string' ? st.filter : '';
-  const all = gpuNodes || NO_PODS;
+  const all = all0 || NO_PODS;
   const want = Math.max(0, Math.floor(st.page) || 0);
-  return memo('node-page:' + per + '|' + want + '|' + filter, [all], function () {
+  return memo(kind + '-page:' + per + '|' + want + '|' + filter, [all], function () {
     const f = filter.trim().toLowerCase();
-    const list = f ? all.filter(function (n) { return nodeNameOf(n).toLowerCase().indexOf(f) >= 0; }) : all;
+    const list = f ? all.filter(function (n) { return textOf(n).toLowerCase().indexOf(f) >= 0; }) : all;
     const pages = Math.max(1, Math.ceil(list.length / per));
     const pg = Math.min(want, pages - 1);
     const from = pg * per;
     const to = Math.min(list.length, from + per);
-    const nodes = list.slice(from, to);
+    const items = list.slice(from, to);
     return {
-      nodes: nodes, names: nodes.map(nodeNameOf), page: pg, pages: pages, from: from, to: to,
+      nodes: items, names: items.map(keyOf), page: pg, pages: pages, from: from, to: to,
       total: all.length, matched: list.length, filter: filter, perPage: per,
     };
   });
@@ -579,7 +637,12 @@ export function visibleNodeNames(ctx, state) {
  * @returns {{enabled: boolean, scope: (string[]|undefined)}}
  */
 export function telemetryScope(ctx, state) {
-  if (!ctx || ctx.loading) return { enabled: false, scope: [] };
+  if (!ctx) return { enabled: false, scope: [] };
+  // The node list alone decides the page (the pod list of a large cluster
+  // arrives later: tens of MB against the node list's few).
+  const nodes = ctx.nodesState;
+  if (nodes === 'error') return { enabled: true, scope: undefined };
+  if (nodes !== 'ready' && ctx.loading) return { enabled: false, scope: [] };
   if (ctx.error && (!ctx.gpuNodes || ctx.gpuNodes.length === 0)) return { enabled: true, scope: undefined };
   return { enabled: true, scope: nodePage(ctx.gpuNodes, state).names };
 }
@@ -894,6 +957,19 @@ function nodesHeadItems(ctx, now, powerByNode, pg) {
   return items;
 }
 
+/**
+ * The Pods page's owner query: the pods of its page (namespace/name keys)
+ * once the pod list is in; cluster-wide when the pod list failed.
+ * @returns {{enabled: boolean, pods: (string[]|undefined)}}
+ */
+export function ownersScope(ctx, state) {
+  if (!ctx) return { enabled: false, pods: [] };
+  if (ctx.podsState === 'error') return { enabled: true, pods: undefined };
+  if (ctx.podsState !== 'ready' && ctx.loading) return { enabled: false, pods: [] };
+  if (ctx.error && (!ctx.gpuPods || ctx.gpuPods.length === 0)) return { enabled: true, pods: undefined };
+  return { enabled: true, pods: podPage(ctx.gpuPods, state).names };
+}
+
 // ---------------------------------------------------------------------------
 // Pods (reference PodsPage.tsx:94-270)
 // ---------------------------------------------------------------------------
@@ -923,13 +999,16 @@ export function podsView(ctx, opts) {
   const now = nowOf(opts);
   if (ctx.loading) return page(null, null, [loader('Loading GPU pod data...')]);
   const assign = opts && opts.metrics ? podGpuAssignments(opts.metrics) : null;
-  const items = memo('pods', [ctx.gpuPods, ctx.index, ctx.error, assign], function () {
-    return podsItems(ctx, now, assign);
+  // One page of the GPU pod table (PODS_PER_PAGE, filter on namespace/name
+  // and node): the reference lists every GPU pod (PodsPage.tsx:201-236).
+  const pg = podPage(ctx.gpuPods, opts && opts.pager);
+  const items = memo('pods', [pg, ctx.index, ctx.error, assign], function () {
+    return podsItems(ctx, now, assign, pg);
   }, now);
   return page(BRAND + ' — Pods', refreshButton('Refresh pod data', ctx.refreshing), items);
 }
 
-function podsItems(ctx, now, assign) {
+function podsItems(ctx, now, assign, pg) {
   const items = [];
   if (ctx.error) items.push(errorSection(ctx.error));
   const pods = ctx.gpuPods;
@@ -959,11 +1038,12 @@ function podsItems(ctx, now, assign) {
     const exact = assign && Object.keys(assign).length > 0;
     const cols = ['Name', 'Namespace', 'Node', 'Phase', 'GPU Resources', 'Restarts', 'Age'];
     if (exact) cols.splice(5, 0, 'Assigned GPUs', 'GPU Power');
+    items.push(pager(pg, 'GPU pods'));
     items.push(
       section('All GPU Pods', [
         table(
           cols,
-          chunkedRows('pod-rows', pods, [exact, assign], function (p) {
+          chunkedRows('pod-rows', pg.nodes, [exact, assign], function (p) {
             // A pod's assignment keeps its identity while its GPUs are unchanged (podGpuAssignments).
             const gs = exact ? assign[(p.metadata.namespace || '') + '/' + p.metadata.name] : undefined;
             return podRows(p, [exact, gs], function () {
@@ -976,27 +1056,32 @@ function podsItems(ctx, now, assign) {
               return r;
             }, now);
           }, now),
-          pods.map(function (p) { return p.metadata.uid || (p.metadata.namespace + '/' + p.metadata.name); })
+          pg.nodes.map(function (p) { return p.metadata.uid || (p.metadata.namespace + '/' + p.metadata.name); })
         ),
       ])
     );
   }
 
   if (pending.length > 0) {
-    items.push(
-      section('Attention: Pending GPU Pods', [
-        table(
-          // "Message" (beyond the reference): why the scheduler cannot place the pod.
-          ['Name', 'Namespace', 'GPU Resources', 'Waiting Reason', 'Message', 'Age'],
-          pending.map(function (p) {
-            return pendingRows(p, [], function () {
-              return [podName(p), podNs(p), formatPodGpuRequests(p), podWaitingReason(p) || '—', podWaitingMessage(p) || '—',
-                ageText(p.metadata.creationTimestamp, now)];
-            }, now);
-          })
-        ),
-      ])
-    );
+    // The oldest PODS_PER_PAGE pending pods (a scheduler backlog can be
+    // thousands deep); the rest are counted, and found with the filter.
+    const shown = pending.length > PODS_PER_PAGE ? pending.slice(0, PODS_PER_PAGE) : pending;
+    const blocks = [
+      table(
+        // "Message" (beyond the reference): why the scheduler cannot place the pod.
+        ['Name', 'Namespace', 'GPU Resources', 'Waiting Reason', 'Message', 'Age'],
+        shown.map(function (p) {
+          return pendingRows(p, [], function () {
+            return [podName(p), podNs(p), formatPodGpuRequests(p), podWaitingReason(p) || '—', podWaitingMessage(p) || '—',
+              ageText(p.metadata.creationTimestamp, now)];
+          }, now);
+        })
+      ),
+    ];
+    if (shown.length < pending.length) {
+      blocks.push(kv([row('Not shown', (pending.length - shown.length) + ' more pending GPU pods (filter the table above by name)')]));
+    }
+    items.push(section('Attention: Pending GPU Pods', blocks));
   }
 
   return items;
@@ -1079,6 +1164,30 @@ function withTotal(pts) {
   const o = {};
   if (pts && pts.length) o[ALL_NODES_SERIES] = pts;
   return o;
+}
+
+/** The entries of `byNode` for `names`, in that order. */
+function pick(byNode, names) {
+  const out = {};
+  for (let i = 0; i < names.length; i++) if (byNode[names[i]]) out[names[i]] = byNode[names[i]];
+  return out;
+}
+
+/** Per-step sum over every node of a cluster-wide series window (memoised per window). */
+function seriesTotal(sr) {
+  return memo('series-total', [sr], function () {
+    function sum(byNode) {
+      const total = {};
+      for (const n in byNode || {}) {
+        const pts = byNode[n] || [];
+        for (let i = 0; i < pts.length; i++) {
+          if (typeof pts[i][1] === 'number' && isFinite(pts[i][1])) total[pts[i][0]] = (total[pts[i][0]] || 0) + pts[i][1];
+        }
+      }
+      return Object.keys(total).map(Number).sort(function (a, b) { return a - b; }).map(function (t) { return [t, total[t]]; });
+    }
+    return { power: sum(sr.power), vram: sum(sr.vram) };
+  });
 }
 
 function noTelemetrySection(name) {
@@ -1198,29 +1307,6 @@ export function metricsView(ctx, mstate, opts) {
       ])
     );
 
-    const sr = mstate.series;
-    if (sr && sr.power) {
-      const win = formatWindow(sr.rangeSec || 1800);
-      // A paged snapshot's series carry the cluster line apart (series.total);
-      // peak / average are the cluster's either way.
-      const clusterPower = sr.total ? { cluster: sr.total.power || [] } : sr.power;
-      const ps = clusterPowerStats(clusterPower);
-      const cap = sum.powerCapWatts > 0 ? sum.powerCapWatts : null;
-      const statRows = ps
-        ? [kv([
-          row('Peak Power (' + win + ')', powerBar(ps.peakWatts, cap)),
-          row('Average Power (' + win + ')', powerBar(ps.avgWatts, cap)),
-        ])]
-        : [];
-      const power = sr.total ? Object.assign({}, withTotal(sr.total.power), sr.power) : sr.power;
-      const vram = sr.total ? Object.assign({}, withTotal(sr.total.vram), sr.vram || {}) : sr.vram || {};
-      items.push(
-        section('Power & HBM (last ' + win + ')', statRows.concat([
-          { t: 'series', power: power, vram: vram, avgPower: seriesMeans(power) },
-        ]))
-      );
-    }
-
     const byNode = {};
     const order = [];
     for (let i = 0; i < m.gpus.length; i++) {
@@ -1236,6 +1322,31 @@ export function metricsView(ctx, mstate, opts) {
     const scoped = Array.isArray(m.scope);
     const k8s = scoped && !ctx.loading && ctx.gpuNodes && ctx.gpuNodes.length > 0;
     const pg = k8s ? nodePage(ctx.gpuNodes, opts && opts.pager) : nodePage(scoped ? m.scope : order, opts && opts.pager);
+
+    const sr = mstate.series;
+    if (sr && sr.power) {
+      const win = formatWindow(sr.rangeSec || 1800);
+      // A paged snapshot's series carry the cluster line apart (series.total);
+      // a cluster-wide one is summed here. Peak / average are the cluster's;
+      // the table shows the cluster line and the nodes of the page.
+      const total = sr.total || seriesTotal(sr);
+      const ps = clusterPowerStats({ cluster: total.power || [] });
+      const cap = sum.powerCapWatts > 0 ? sum.powerCapWatts : null;
+      const statRows = ps
+        ? [kv([
+          row('Peak Power (' + win + ')', powerBar(ps.peakWatts, cap)),
+          row('Average Power (' + win + ')', powerBar(ps.avgWatts, cap)),
+        ])]
+        : [];
+      const power = Object.assign(withTotal(total.power), pick(sr.power, pg.names));
+      const vram = Object.assign(withTotal(total.vram), pick(sr.vram || {}, pg.names));
+      items.push(
+        section('Power & HBM (last ' + win + ')', statRows.concat([
+          { t: 'series', power: power, vram: vram, avgPower: seriesMeans(power) },
+        ]))
+      );
+    }
+
     items.push(pager(pg, k8s || scoped ? 'GPU nodes' : 'GPU nodes reporting'));
     const covered = {};
     if (scoped) for (let i = 0; i < m.scope.length; i++) covered[m.scope[i]] = true;

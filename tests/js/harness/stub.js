@@ -1,0 +1,31 @@
+/**
+ * Render adapter of the shared specs (tests/js/shared/) on the harness React
+ * (tests/js/stubs/react.js): what `npm run test:node12`, `npm test` and the
+ * pytest bridge run. tests/js/harness/dom.js is the same API on real React 18
+ * + react-dom under jsdom (vitest.react.config.mts, networked CI only).
+ *
+ * A shared spec imports this API from 'amd-test-harness' and never a stub
+ * internal: no component instances, no render counters.
+ */
+import React, { render as stubRender, textOf } from '../stubs/react.js';
+
+export { React };
+export const tier = 'harness';
+
+export function render(element, options) {
+  const r = stubRender(element, options);
+  const handle = {
+    settle: function (rounds) { return r.settle(rounds).then(function () { return handle; }); },
+    text: function () { return r.text(); },
+    html: function () { return r.html(); },
+    /** The one element whose aria-label is exactly `label`. */
+    byLabel: function (label) { return r.getByLabelText(label); },
+    byTag: function (tag) { return r.byTag(tag); },
+    click: function (node) { r.click(node); return handle; },
+    change: function (node, value) { r.change(node, value); return handle; },
+    isDisabled: function (node) { return !!node.props.disabled; },
+    textOf: function (node) { return textOf(node); },
+    unmount: function () { r.unmount(); },
+  };
+  return handle;
+}

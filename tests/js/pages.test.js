@@ -530,7 +530,9 @@ describe('metricsView', () => {
     const series = { power: { n0: [[30, 100], [60, 300]], n1: [] }, vram: {} };
     const vm = metricsView(ctx, { metrics: metrics(['n0'], 1), fetchError: null, fetching: false, series }, opts);
     const blk = findSection(vm, 'Power & HBM (last 30 min)').blocks.filter((b) => b.t === 'series')[0];
-    expect(blk.avgPower).toEqual({ n0: 200 });
+    // the cluster line (summed over the nodes) first, then the nodes of the page
+    expect(blk.avgPower).toEqual({ 'All GPU nodes': 200, n0: 200 });
+    expect(Object.keys(blk.power)).toEqual(['All GPU nodes', 'n0']);
     expect(rowValue(findSection(vm, 'GPU Power Summary'), 'Nodes Reporting')).toBe('1 / 1 GPU nodes');
     const two = makeContext({ nodes: [makeGpuNode('n0'), makeGpuNode('n9')] });
     const vm2 = metricsView(two, { metrics: metrics(['n0'], 1), fetchError: null, fetching: false }, opts);

@@ -15,7 +15,8 @@ import { createPlugin } from '../../src/plugin.js';
 import { resetSharedStores } from '../../src/api/clusterStore.js';
 import { DEVICE_CONFIG_LIST_PATH } from '../../src/api/amdgpu.js';
 import {
-  ALL_NODES_SERIES, NODES_PER_PAGE, clearViewMemo, metricsView, nodePage, nodesView, telemetryScope,
+  ALL_NODES_SERIES, NODES_PER_PAGE, OVERVIEW_PLUGIN_PODS, PODS_PER_PAGE, clearViewMemo, devicePluginsView, metricsView,
+  nodePage, nodesView, overviewView, ownersScope, podsView, telemetryScope,
 } from '../../src/view/pages.js';
 import { countRows, findSection, pagerOf, pagerText, rowValue, sectionTitles } from '../../src/view/ir.js';
 import { renderPage } from '../../src/view/html.js';
@@ -23,7 +24,7 @@ import {
   SERIES, TOTAL_SERIES, createMetricsSource, hostnameMatcher, regexLiteral, scopedSeriesQuery, summarizeMetrics,
   summaryQuery, totalsFromRows, joinExporterResults, splitByName,
 } from '../../src/api/metrics.js';
-import { makeContext, makeDeviceConfig, makeGpuNode, makeGpuPod } from './fixtures.js';
+import { makeContext, makeDeviceConfig, makeGpuNode, makeGpuPod, makePluginPod } from './fixtures.js';
 import { BASE0, exporterData, flatten, prom } from './promFake.js';
 
 const h = React.createElement;
@@ -283,5 +284,46 @@ describe('plugin pages: pager state drives the scoped queries', () => {
     expect(r.text()).toContain('12 / 12 GPU nodes');
     expect(r.byTag('section').length).toBeLessThan(8 + 6);
     r.unmount();
+  });
+});
+
+describe('GPU Pods / Device Plugins / Overview tables are bounded too', () => {
+  const pods = (n) => Array.from({ length: n }, (_, i) => makeGpuPod('train-' + String(i).padStart(4, '0'), { node: 'mi355x-' + String(i % 50).padStart(3, '0') }));
+  const withPods = (list) => makeContext({ nodes: names(50).map((x) => makeGpuNode(x)), pods: list });
+  it('GPU Pods: PODS_PER_PAGE rows per page, filter on namespace/name and node', () => {
+    const vm = podsView(withPods(pods(120)), {});
+    expect(PODS_PER_PAGE).toBe(25);
+    expect(findSection(vm, 'All GPU Pods').blocks[0].rows).toHaveLength(25);
+    expect(pagerText(pagerOf(vm))).toBe('Showing 1–25 of 120 GPU pods · page 1 of 5');
+    const byNode = podsView(withPods(pods(120)), { pager: { filter: 'mi355x-007' } });
+    expect(findSection(byNode, 'All GPU Pods').blocks[0].rows.map((r) => r[0])).toEqual(['train-0007', 'train-0057', 'train-0107']);
+    expect(rowValue(vm, 'Total GPU Pods')).toBe('120'); // the summary still counts every pod
+  });
+  it('pending pods: the oldest PODS_PER_PAGE, the rest counted', () => {
+    const list = Array.from({ length: 40 }, (_, i) => makeGpuPod('wait-' + i, { phase: 'Pending', node: null, waiting: 'Unschedulable' }));
+    const sec = findSection(podsView(withPods(list), {}), 'Attention: Pending GPU Pods');
+    expect(sec.blocks[0].rows).toHaveLength(25);
+    expect(rowValue(sec, 'Not shown')).toBe('15 more pending GPU pods (filter the table above by name)');
+  });
+  it('owners are asked for the pods of the page only', async () => {
+    const fake = prom({ data: exporterData(['n0']) });
+    const s = createMetricsSource({ request: fake });
+    await s.fetchGpuOwners({ pods: ['ml/train-0', 'ml/train-1'] });
+    expect(decoded(fake)[0]).toContain('pod=~"train-0|train-1", namespace=~"ml"');
+    const none = await s.fetchGpuOwners({ pods: [] });
+    expect(none.gpus).toHaveLength(0);
+    expect(fake.mock.calls).toHaveLength(1);
+    expect(ownersScope(withPods(pods(30)), { page: 1 }).pods).toEqual(pods(30).slice(25).map((p) => 'ml/' + p.metadata.name));
+  });
+  it('Overview lists at most OVERVIEW_PLUGIN_PODS operator pods, not-ready first; Device Plugins pages through them', () => {
+    const ops = Array.from({ length: 30 }, (_, i) => makePluginPod('amd-dp-' + i, { ready: i !== 17 }));
+    const ctx = makeContext({ nodes: [makeGpuNode('mi355x-000')], pluginPods: ops });
+    const ov = findSection(overviewView(ctx), 'Plugin Daemon Pods');
+    expect(ov.blocks[0].rows).toHaveLength(OVERVIEW_PLUGIN_PODS);
+    expect(ov.blocks[0].rows[0][0]).toBe('amd-dp-17');
+    expect(rowValue(ov, 'Readiness').text).toBe('1 not ready');
+    const dp = devicePluginsView(ctx, { pager: { page: 1 } });
+    expect(findSection(dp, 'Plugin Daemon Pods').blocks[0].rows.map((r) => r[0])).toEqual(ops.slice(25).map((p) => p.metadata.name));
+    expect(pagerOf(dp).noun).toBe('operator pods');
   });
 });

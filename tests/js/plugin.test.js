@@ -50,6 +50,14 @@ function cluster(o) {
     : opt.pods;
   lib.api.handler = (path) => {
     if (path === DEVICE_CONFIG_LIST_PATH) return Promise.resolve(kubeList([makeDeviceConfig()]));
+    // One node's pods (the cold Node detail section's field-selected list).
+    const fs = /^\/api\/v1\/pods\?fieldSelector=(.*)$/.exec(path);
+    if (fs) {
+      const node = decodeURIComponent(fs[1]).replace(/^spec\.nodeName=/, '');
+      const list = lib.lists.Pod;
+      if (!list || !list[0]) return Promise.reject(Object.assign(new Error(list && list[1] ? list[1] : 'pods is forbidden'), { status: 403 }));
+      return Promise.resolve(kubeList(list[0].filter((p) => p.spec && p.spec.nodeName === node)));
+    }
     return Promise.reject(Object.assign(new Error('503 Service Unavailable'), { status: 503 }));
   };
 }
@@ -250,6 +258,33 @@ describe('detail sections', () => {
     await r.settle();
     expect(r.text()).not.toContain('Loading…');
     expect(r.text()).toContain('Unavailable — the pod list could not be read');
+  });
+
+  it('cold Node detail (no plugin page yet) reads its own pods: one field-selected request, no cluster-wide watch', async () => {
+    cluster();
+    const r = render(nodeSection(makeGpuNode('mi355x-1')));
+    await r.settle();
+    expect(lib.lists.calls.Node).toHaveLength(0);
+    expect(lib.lists.calls.Pod).toHaveLength(0);
+    expect(lib.api.calls.filter((p) => p === DEVICE_CONFIG_LIST_PATH)).toHaveLength(0);
+    const own = lib.api.calls.filter((p) => p.indexOf('/api/v1/pods?') === 0);
+    expect(own).toEqual(['/api/v1/pods?fieldSelector=' + encodeURIComponent('spec.nodeName=mi355x-1')]);
+    expect(r.html()).toContain('train-b');
+    expect(r.html()).not.toContain('train-a'); // mi355x-0's pod
+    r.unmount();
+  });
+
+  it('warm Node detail (a plugin page fed the store) reads the store and sends no pod request', async () => {
+    cluster();
+    const page = render(h(route('/amd-gpu/nodes')));
+    await page.settle();
+    const before = lib.api.calls.length;
+    const r = render(nodeSection(makeGpuNode('mi355x-0')));
+    await r.settle();
+    expect(lib.api.calls.slice(before).filter((p) => p.indexOf('/api/v1/pods') === 0)).toHaveLength(0);
+    expect(r.html()).toContain('train-a');
+    r.unmount();
+    page.unmount();
   });
 
   it('Node detail opened next to a page adds no CRD request', async () => {

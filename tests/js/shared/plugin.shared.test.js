@@ -1,0 +1,194 @@
+/**
+ * Runner-agnostic specs of the shipped React layer: every page route, both
+ * detail sections, loading → data, the Refresh path, StrictMode and the
+ * pager, asserted on rendered text, aria-labels and the requests sent.
+ *
+ * They import their render API from 'amd-test-harness' and nothing from the
+ * harness React, so the same file runs
+ *   * on the harness React (tests/js/harness/stub.js): `npm run test:node12`,
+ *     `npm test` and the pytest bridge, offline;
+ *   * on real React 18 + react-dom in jsdom with @testing-library/react
+ *     (tests/js/harness/dom.js): `npm run test:react`
+ *     (vitest.react.config.mts), networked CI only.
+ * Only '@kinvolk/headlamp-plugin/lib[/CommonComponents]' is mocked, as the
+ * reference's component tests do (reference src/components/OverviewPage.test.tsx:8-61).
+ * Assertions on harness internals (component instances, render counters)
+ * live in the harness-only files (tests/js/plugin.test.js, react.test.js,
+ * provider.test.js).
+ */
+import { React, render, tier } from 'amd-test-harness';
+import * as lib from '@kinvolk/headlamp-plugin/lib';
+import '../../../src/index.tsx';
+import { resetSharedStores } from '../../../src/api/clusterStore.js';
+import { clearViewMemo } from '../../../src/view/pages.js';
+import { invalidateSettings } from '../../../src/api/settings.js';
+import { DEVICE_CONFIG_LIST_PATH } from '../../../src/api/amdgpu.js';
+import { makeDeviceConfig, makeGpuNode, makeGpuPod, makeNode, makePlainPod, makePluginPod } from '../fixtures.js';
+import { exporterData, prom } from '../promFake.js';
+
+const h = React.createElement;
+
+// Registration ran at import (src/index.tsx); keep it before any reset.
+const reg = { routes: lib.registry.routes.slice(), details: lib.registry.details.slice() };
+
+const nodeNames = (n) => Array.from({ length: n }, (_, i) => 'mi355x-' + String(i).padStart(3, '0'));
+
+function route(path) {
+  const r = reg.routes.find((x) => x.path === path);
+  expect(r).toBeTruthy();
+  return r.component;
+}
+
+/** A cluster: GPU + CPU nodes, GPU / plain / operator pods, one DeviceConfig, a Prometheus with exporter series. */
+function cluster(o) {
+  const opt = Object.assign({ gpuNodes: ['mi355x-000', 'mi355x-001'], loading: false }, o || {});
+  const nodes = opt.gpuNodes.map((n) => makeGpuNode(n)).concat([makeNode('cpu-0')]);
+  const pods = [
+    makeGpuPod('train-a', { gpus: 4, node: opt.gpuNodes[0] }),
+    makeGpuPod('train-b', { gpus: 2, node: opt.gpuNodes[1] || opt.gpuNodes[0] }),
+    makePlainPod('web-0'),
+    makePluginPod('amdgpu-dp-0'),
+  ];
+  lib.lists.Node = opt.loading ? [null, null] : [nodes, null];
+  lib.lists.Pod = opt.loading ? [null, null] : [pods, null];
+  const fake = prom({ data: exporterData(opt.gpuNodes) });
+  lib.api.handler = (path) => {
+    if (path === DEVICE_CONFIG_LIST_PATH) return Promise.resolve({ kind: 'List', metadata: {}, items: [makeDeviceConfig()] });
+    if (path.indexOf('/proxy/api/v1/') >= 0) return fake(path);
+    const fs = /^\/api\/v1\/pods\?fieldSelector=(.*)$/.exec(path);
+    if (fs) {
+      const node = decodeURIComponent(fs[1]).replace(/^spec\.nodeName=/, '');
+      return Promise.resolve({ kind: 'List', metadata: {}, items: pods.filter((p) => p.spec.nodeName === node) });
+    }
+    return Promise.reject(Object.assign(new Error('503 Service Unavailable'), { status: 503 }));
+  };
+  return fake;
+}
+
+const crdCalls = () => lib.api.calls.filter((p) => p === DEVICE_CONFIG_LIST_PATH).length;
+const promQueries = (fake) => fake.mock.calls.map((c) => decodeURIComponent(c[0])).filter((p) => p.indexOf('/query?query=max by') >= 0);
+
+beforeEach(() => {
+  lib.resetHeadlamp();
+  resetSharedStores();
+  clearViewMemo();
+  invalidateSettings();
+});
+
+describe('shared: every route mounts and renders its page (' + tier + ')', () => {
+  const pages = [
+    ['/amd-gpu', 'AMD GPU — Overview', 'GPU Nodes'],
+    ['/amd-gpu/device-plugins', 'AMD GPU — Device Plugins', 'DeviceConfig: gpu-operator'],
+    ['/amd-gpu/nodes', 'AMD GPU — Nodes', 'GPU Node Summary'],
+    ['/amd-gpu/pods', 'AMD GPU — Pods', 'All GPU Pods'],
+    ['/amd-gpu/metrics', 'AMD GPU — Metrics', 'GPU Power Summary'],
+  ];
+  pages.forEach(([path, title, section]) => {
+    it(path + ' → "' + title + '" with "' + section + '"', async () => {
+      cluster();
+      const r = render(h(route(path)));
+      await r.settle();
+      expect(r.text()).toContain(title);
+      expect(r.text()).toContain(section);
+      r.unmount();
+    });
+  });
+
+  it('shows the loader while the lists are loading, then no page header', async () => {
+    cluster({ loading: true });
+    const r = render(h(route('/amd-gpu')));
+    await r.settle();
+    expect(r.text()).toContain('Loading AMD GPU data...');
+    expect(r.text()).not.toContain('AMD GPU — Overview');
+    r.unmount();
+  });
+});
+
+describe('shared: refresh and StrictMode (' + tier + ')', () => {
+  it('the Overview Refresh button re-fetches the DeviceConfig list', async () => {
+    cluster();
+    const r = render(h(route('/amd-gpu')));
+    await r.settle();
+    const before = crdCalls();
+    r.click(r.byLabel('Refresh AMD GPU data'));
+    await r.settle();
+    expect(crdCalls()).toBe(before + 1);
+    r.unmount();
+  });
+
+  it('the Metrics Refresh button sends one more live query', async () => {
+    const fake = cluster();
+    const r = render(h(route('/amd-gpu/metrics')));
+    await r.settle();
+    const before = promQueries(fake).length;
+    expect(before).toBe(1);
+    r.click(r.byLabel('Refresh metrics'));
+    await r.settle();
+    expect(promQueries(fake).length).toBe(before + 1);
+    r.unmount();
+  });
+
+  it('under StrictMode a route mounts with one CRD request and one live query', async () => {
+    const fake = cluster();
+    const r = render(h(route('/amd-gpu/metrics')), { strict: true });
+    await r.settle();
+    expect(crdCalls()).toBe(1);
+    expect(promQueries(fake)).toHaveLength(1);
+    expect(r.text()).toContain('GPU Power Summary');
+    r.unmount();
+  });
+});
+
+describe('shared: the pager drives what is rendered and fetched (' + tier + ')', () => {
+  it('GPU Nodes: Next page shows and queries the next 8 nodes; the filter narrows them', async () => {
+    const fake = cluster({ gpuNodes: nodeNames(20) });
+    const r = render(h(route('/amd-gpu/nodes')));
+    await r.settle();
+    expect(r.text()).toContain('Showing 1–8 of 20 GPU nodes');
+    expect(r.text()).not.toContain('mi355x-008');
+    r.click(r.byLabel('Next page'));
+    await r.settle();
+    expect(r.text()).toContain('mi355x-008');
+    expect(r.text()).not.toContain('mi355x-007');
+    expect(promQueries(fake).pop()).toContain('hostname=~"' + nodeNames(16).slice(8).join('|') + '"');
+    r.change(r.byLabel('Filter GPU nodes by name'), '019');
+    await r.settle();
+    expect(r.text()).toContain('Showing 1–1 of 1 matching "019" (20 GPU nodes)');
+    expect(r.isDisabled(r.byLabel('Next page'))).toBe(true);
+    r.unmount();
+  });
+});
+
+describe('shared: native-view sections (' + tier + ')', () => {
+  it('Node detail on a cold store: the node\'s own pods, no cluster-wide list', async () => {
+    cluster();
+    const r = render(reg.details[0]({ resource: { kind: 'Node', jsonData: makeGpuNode('mi355x-001') } }));
+    await r.settle();
+    expect(r.text()).toContain('AMD GPU');
+    expect(r.text()).toContain('train-b');
+    expect(lib.lists.calls.Pod).toHaveLength(0);
+    expect(lib.api.calls.filter((p) => p.indexOf('/api/v1/pods?fieldSelector=') === 0)).toHaveLength(1);
+    r.unmount();
+  });
+
+  it('Pod detail: a GPU pod renders its resources without a cluster request', async () => {
+    cluster();
+    const r = render(reg.details[1]({ resource: { kind: 'Pod', jsonData: makeGpuPod('train-a', { gpus: 4, node: null }) } }));
+    await r.settle();
+    expect(r.text()).toContain('AMD GPU Resources');
+    expect(crdCalls()).toBe(0);
+    r.unmount();
+  });
+
+  it('nothing for CPU nodes and non-GPU pods', async () => {
+    cluster();
+    const a = render(h('div', null, reg.details[0]({ resource: { kind: 'Node', jsonData: makeNode('cpu-0') } })));
+    const b = render(h('div', null, reg.details[1]({ resource: { kind: 'Pod', jsonData: makePlainPod('web-0') } })));
+    await a.settle();
+    await b.settle();
+    expect(a.byTag('section')).toHaveLength(0);
+    expect(b.byTag('section')).toHaveLength(0);
+    a.unmount();
+    b.unmount();
+  });
+});

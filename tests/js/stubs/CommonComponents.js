@@ -13,50 +13,14 @@
  * handed each component (SimpleTable columns / getters / data, …).
  */
 import { createElement as h } from './react.js';
+import { makeCommonComponents } from '../harness/commonComponents.js';
 
-export function SectionBox(p) {
-  return h('section', null, h('h2', null, p.title), p.children);
-}
+const CC = makeCommonComponents(h);
 
-export function SectionHeader(p) {
-  return h('h1', null, p.title);
-}
-
-export function NameValueTable(p) {
-  return h(
-    'dl',
-    null,
-    p.rows.map(function (r, i) { return h('div', { key: i }, h('dt', null, r.name), h('dd', null, r.value)); })
-  );
-}
-
-export function SimpleTable(p) {
-  return h(
-    'table',
-    null,
-    h('thead', null, h('tr', null, p.columns.map(function (c, j) { return h('th', { key: j }, c.label); }))),
-    h(
-      'tbody',
-      null,
-      p.data.map(function (item, i) {
-        return h('tr', { key: i }, p.columns.map(function (c, j) { return h('td', { key: j }, c.getter(item)); }));
-      })
-    )
-  );
-}
-
-export function StatusLabel(p) {
-  return h('span', { 'data-status': p.status }, p.children);
-}
-
-export function Loader(p) {
-  return h('div', { 'data-testid': 'loader' }, p.title);
-}
-
-export function PercentageBar(p) {
-  return h(
-    'div',
-    { 'data-testid': 'percentage-bar', 'data-total': p.total },
-    p.data.map(function (d, i) { return h('span', { key: i, 'data-name': d.name, 'data-value': d.value, 'data-fill': d.fill }, d.name + ': ' + d.value); })
-  );
-}
+export const SectionBox = CC.SectionBox;
+export const SectionHeader = CC.SectionHeader;
+export const NameValueTable = CC.NameValueTable;
+export const SimpleTable = CC.SimpleTable;
+export const StatusLabel = CC.StatusLabel;
+export const Loader = CC.Loader;
+export const PercentageBar = CC.PercentageBar;

@@ -17,7 +17,8 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 NODE = shutil.which("node") or shutil.which("nodejs")
-SPECS = sorted(os.path.relpath(p, ROOT) for p in glob.glob(os.path.join(ROOT, "tests", "js", "*.test.js")))
+SPECS = sorted(os.path.relpath(p, ROOT) for p in glob.glob(os.path.join(ROOT, "tests", "js", "*.test.js"))
+               + glob.glob(os.path.join(ROOT, "tests", "js", "shared", "*.test.js")))
 RUNNER = os.path.join("tools", "minitest.js")
 # Resolves 'react' / '@kinvolk/headlamp-plugin/lib' to the harness stand-ins
 # and loads the TypeScript entry shims, so the specs import src/index.tsx and

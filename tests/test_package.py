@@ -1,8 +1,9 @@
-"""npm manifest: direct dependencies pinned, CI installs from the lock when one exists.
+"""npm manifest and lock: direct dependencies pinned, the lock derived from the reference's resolved tree, CI on `npm ci`.
 
 The reference ships package-lock.json and CI runs `npm ci` (reference .github/workflows/ci.yaml:147-167). A lock
-cannot be generated offline here, so the pins in package.json are the reproducibility floor until CI's first
-networked run produces one (uploaded as an artifact by .github/workflows/ci.yaml).
+cannot be resolved offline here; tools/derive_lock.py derives it from the reference's lock (lockfileVersion 3), which
+resolves exactly the versions package.json pins, rewriting only the root entry and dropping what our root no longer
+reaches.
 """
 import json
 import os
@@ -21,12 +22,60 @@ def test_dev_dependencies_are_exact_versions():
     assert pkg["peerDependencies"]["react"].startswith("^18")
 
 
-def test_ci_prefers_npm_ci_when_locked():
+def test_ci_installs_with_npm_ci():
     ci = yaml.safe_load(open(os.path.join(ROOT, ".github", "workflows", "ci.yaml")))
     steps = ci["jobs"]["plugin"]["steps"]
     install = next(s for s in steps if s.get("name") == "Install")["run"]
-    assert "package-lock.json" in install and "npm ci" in install
-    assert any(s.get("uses", "").startswith("actions/upload-artifact") for s in steps)
+    assert "npm ci" in install and "npm install" not in install
+
+
+def _lock():
+    return json.load(open(os.path.join(ROOT, "package-lock.json")))
+
+
+def test_lock_root_matches_the_manifest():
+    pkg = json.load(open(os.path.join(ROOT, "package.json")))
+    lock = _lock()
+    root = lock["packages"][""]
+    assert lock["lockfileVersion"] == 3 and lock["name"] == pkg["name"] == root["name"]
+    assert lock["version"] == pkg["version"] == root["version"]
+    for field in ("devDependencies", "peerDependencies", "bin", "engines"):
+        assert root.get(field) == pkg.get(field), field
+
+
+def test_lock_pins_the_declared_versions_with_integrity():
+    pkg = json.load(open(os.path.join(ROOT, "package.json")))
+    pkgs = _lock()["packages"]
+    for name, ver in pkg["devDependencies"].items():
+        assert pkgs["node_modules/" + name]["version"] == ver, name
+    for path, ent in pkgs.items():
+        if not path or ent.get("link"):
+            continue
+        assert ent.get("integrity", "").startswith("sha"), path
+        assert ent.get("resolved", "").startswith("https://registry.npmjs.org/"), path
+
+
+def test_lock_is_the_derivation_of_the_reference_tree():
+    import subprocess
+    import sys
+
+    ref = "/root/reference/package-lock.json"
+    if not os.path.exists(ref):
+        import pytest
+
+        pytest.skip("reference tree not mounted")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "derive_lock.py"), "--check"], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    lock = _lock()["packages"]
+    # our root reaches no Playwright (the reference's root lists it; this plugin has no e2e suite)
+    assert not [p for p in lock if "playwright" in p]
+    # every kept package is reachable from our root: nothing extraneous
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import derive_lock
+
+    keep = derive_lock.reachable(lock, list(lock[""]["devDependencies"]) + list(lock[""]["peerDependencies"]))
+    assert keep == {p for p in lock if p}
 
 
 def test_offline_plugin_archive_is_installable_and_reproducible(tmp_path):
@@ -84,3 +133,28 @@ def test_artifacthub_metadata_is_valid_and_matches_the_manifest(tmp_path):
     assert any("v9.9.9" in e for e in broken(lambda m: m.update(version="9.9.9")))
     assert any("license" in e for e in broken(lambda m: m.pop("license")))
     assert validate(str(tmp_path / "missing.yml")) == [f"{tmp_path / 'missing.yml'} not found"]
+
+
+def test_real_react_tier_is_configured_and_the_shared_specs_are_runner_agnostic():
+    """vitest.react.config.mts renders tests/js/shared/ with the real React in jsdom (no 'react' alias, only the
+    Headlamp library mocked); those specs import no harness internals; CI runs the tier."""
+    import glob
+
+    cfg = open(os.path.join(ROOT, "vitest.react.config.mts")).read()
+    assert "environment: 'jsdom'" in cfg and "tests/js/shared/**/*.test.js" in cfg
+    assert "find: /^react$/" not in cfg and "stubs', 'react.js'" not in cfg
+    assert "harness', 'dom.js'" in cfg and "@testing-library/react" in open(os.path.join(ROOT, "tests", "js", "harness", "dom.js")).read()
+    shared = glob.glob(os.path.join(ROOT, "tests", "js", "shared", "*.test.js"))
+    assert shared
+    for f in shared:
+        src = open(f).read()
+        imports = re.findall(r"^import .* from '([^']+)';", src, re.M)
+        assert "amd-test-harness" in imports, f
+        assert not [i for i in imports if "stubs/" in i or i == "react"], (f, imports)
+    pkg = json.load(open(os.path.join(ROOT, "package.json")))
+    assert pkg["scripts"]["test:react"] == "vitest run --config vitest.react.config.mts"
+    for dep in ("jsdom", "@testing-library/react", "react-dom"):
+        assert dep in pkg["devDependencies"], dep
+    ci = yaml.safe_load(open(os.path.join(ROOT, ".github", "workflows", "ci.yaml")))
+    runs = [s.get("run", "") for s in ci["jobs"]["plugin"]["steps"]]
+    assert "npm run test:react" in runs

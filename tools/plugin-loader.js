@@ -7,6 +7,7 @@
  *   react                                   → tests/js/stubs/react.js
  *   @kinvolk/headlamp-plugin/lib            → tests/js/stubs/headlamp-lib.js
  *   @kinvolk/headlamp-plugin/lib/CommonComponents → tests/js/stubs/CommonComponents.js
+ *   amd-test-harness                        → tests/js/harness/stub.js (shared specs' render API)
  *   './x' (no extension)                    → ./x.tsx | ./x.ts | ./x.js | ./x/index.tsx
  *   *.ts / *.tsx                            → ES module; `import type` lines removed
  *
@@ -30,6 +31,7 @@ const ALIASES = {
   react: path.join(STUBS, 'react.js'),
   '@kinvolk/headlamp-plugin/lib': path.join(STUBS, 'headlamp-lib.js'),
   '@kinvolk/headlamp-plugin/lib/CommonComponents': path.join(STUBS, 'CommonComponents.js'),
+  'amd-test-harness': path.join(ROOT, 'tests', 'js', 'harness', 'stub.js'),
 };
 
 const TRY = ['.tsx', '.ts', '.js', '/index.tsx', '/index.ts', '/index.js'];

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Scaling curve + BASELINE configs: run bench.py per point and tabulate.
 
-    python tools/sweep.py --out gpurun_out/sweep [--steps 30] [--rtt-ms 20] [--beyond 16,32,64]
+    python tools/sweep.py --out gpurun_out/sweep [--steps 30] [--rtt-ms 20] [--beyond 16,32,64,256,1000]
     python tools/sweep.py --stress --out gpurun_out/stress [--stress-nodes 16,64,256,1000] [--events 1000]
 
 ``--stress``: the cluster-size axis under watch churn (bench/stress.js) —
@@ -42,7 +42,7 @@ def run(kind, val, args):
            "--rtt-ms", str(args.rtt_ms), f"--{kind}", val]
     if args.extra:
         cmd += args.extra.split()
-    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600)
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=1800)
     if r.returncode != 0:
         raise RuntimeError(f"{' '.join(cmd)} failed:\n{r.stderr[-3000:]}")
     return json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
@@ -83,6 +83,26 @@ def table(rows):
                   f"{l['route_switch_p50_ms']['reference']:.0f} → {l['route_switch_p50_ms']['amd']:.1f}",
                   str(l["rendered"]["gpu_nodes"]), str(l["rendered"]["gpu_pods"]), str(l["rendered"]["gpus_monitored"]),
                   "yes" if l.get("live_telemetry") else "no"]
+        md.append("| " + " | ".join(cells) + " |")
+    return md
+
+
+def render_table(rows):
+    """Per page at each point: harness-React elements and mount / re-render ms, plus the cold Node detail open."""
+    head = ["GPU nodes"] + [f"{t}: elements, mount / re-render ms" for _, t in PAGE_COLS] + [
+        "Cold Node detail ref → new: ms, KB, requests"]
+    md = ["| " + " | ".join(head) + " |", "|---:|" + "---|" * (len(head) - 1)]
+    for r in rows:
+        l = r["line"]
+        rp = l.get("render_per_page") or {}
+        cells = [str(l["config"]["nodes"])]
+        for k, _ in PAGE_COLS:
+            v = rp.get(k)
+            cells.append(f"{v['elements']}, {v['mount_ms']:.1f} / {v['rerender_ms']:.1f}" if v else "—")
+        d = l.get("detail_open") or {}
+        a, ref = d.get("nodeDetailCold"), d.get("nodeDetailColdReference")
+        cells.append(f"{ref['p50_ms']:.0f} → {a['p50_ms']:.0f}; {ref['bytes'] / 1e3:.0f} → {a['bytes'] / 1e3:.0f}; "
+                     f"{ref['requests']:.0f} → {a['requests']:.0f}" if a and ref and a["p50_ms"] is not None else "—")
         md.append("| " + " | ".join(cells) + " |")
     return md
 
@@ -139,20 +159,21 @@ def main():
     p.add_argument("--stress", action="store_true", help="watch-churn stress of the cluster-size axis instead")
     p.add_argument("--stress-nodes", default="16,64,256,1000")
     p.add_argument("--events", type=int, default=1000)
-    p.add_argument("--beyond", default="", help="extra node counts past the BASELINE configs, e.g. 16,32,64")
+    p.add_argument("--beyond", default="", help="extra node counts past the BASELINE configs, e.g. 16,32,64,256,1000")
+    p.add_argument("--only-beyond", action="store_true", help="skip the BASELINE points (run --beyond only)")
     args = p.parse_args()
     if args.stress:
         return stress(args)
     os.makedirs(args.out, exist_ok=True)
     rows = []
-    points = POINTS + [("nodes", v.strip()) for v in args.beyond.split(",") if v.strip()]
+    points = ([] if args.only_beyond else POINTS) + [("nodes", v.strip()) for v in args.beyond.split(",") if v.strip()]
     for kind, val in points:
         line = run(kind, val, args)
         rows.append({"kind": kind, "point": val, "line": line})
         print(f"{kind}={val}: per-page p50 {line['value']} ms vs ref {line['baseline']['value_ms']} ms", flush=True)
         with open(os.path.join(args.out, "sweep.json"), "w") as f:
             json.dump(rows, f, indent=1)
-    md = table(rows)
+    md = table(rows) + ["", "Render (harness React, first page of each view) and the cold Node detail open:", ""] + render_table(rows)
     with open(os.path.join(args.out, "sweep.md"), "w") as f:
         f.write("\n".join(md) + "\n")
     print("\n".join(md))

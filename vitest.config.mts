@@ -1,7 +1,8 @@
 import path from 'path';
 import { defineConfig } from 'vitest/config';
 
-// One spec family: tests/js/*.test.js, written against the vitest globals API
+// The harness tier: tests/js/*.test.js and tests/js/shared/*.test.js, written
+// against the vitest globals API
 // so that they also run on bare Node via tools/minitest.js
 // (`npm run test:node12`). The React layer is exercised against the same
 // stand-ins under both runners: 'react' and the Headlamp library resolve to
@@ -15,6 +16,7 @@ export default defineConfig({
       { find: /^@kinvolk\/headlamp-plugin\/lib\/CommonComponents$/, replacement: path.join(stubs, 'CommonComponents.js') },
       { find: /^@kinvolk\/headlamp-plugin\/lib$/, replacement: path.join(stubs, 'headlamp-lib.js') },
       { find: /^react$/, replacement: path.join(stubs, 'react.js') },
+      { find: /^amd-test-harness$/, replacement: path.resolve(__dirname, 'tests/js/harness/stub.js') },
     ],
   },
   test: {
