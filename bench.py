@@ -140,19 +140,27 @@ def main(argv=None) -> int:
                        if node_of_device else None)
             server = ServerThread(fc).start()
         drv = Driver(server.url)
+
+        def call(*a, **k):
+            """drv.call + a progress line on stderr (a long 1,000-node run stays visibly alive)."""
+            t = time.perf_counter()
+            r = drv.call(*a, **k)
+            print(f"[bench] {a[0]} {a[1] if len(a) > 1 else ''} {time.perf_counter() - t:.1f} s", file=sys.stderr, flush=True)
+            return r
+
         try:
             ref_steps = args.ref_steps if args.ref_steps is not None else args.steps
             # Measured baseline: the reference plugin's schedule (untimed region).
-            ref_cold = drv.call("cold", "reference", n=3)
-            ref_cold_pages = drv.call("coldPages", "reference", n=5)
-            drv.call("pages", "reference", n=max(1, args.warmup))
-            ref_pages = drv.call("pages", "reference", n=ref_steps)
-            ref = drv.call("steps", "reference", n=max(3, ref_steps // 2))
-            ref_switch = drv.call("switch", "reference", n=3)
+            ref_cold = call("cold", "reference", n=3)
+            ref_cold_pages = call("coldPages", "reference", n=5)
+            call("pages", "reference", n=max(1, args.warmup))
+            ref_pages = call("pages", "reference", n=ref_steps)
+            ref = call("steps", "reference", n=max(3, ref_steps // 2))
+            ref_switch = call("switch", "reference", n=3)
             # Flagship schedule.
-            amd_cold = drv.call("cold", "amd", n=3)
-            amd_cold_pages = drv.call("coldPages", "amd", n=5)
-            drv.call("pages", "amd", n=max(1, args.warmup))
+            amd_cold = call("cold", "amd", n=3)
+            amd_cold_pages = call("coldPages", "amd", n=5)
+            call("pages", "amd", n=max(1, args.warmup))
             D.barrier(info)
             quiet_sync()
             t0 = time.perf_counter()
@@ -162,12 +170,12 @@ def main(argv=None) -> int:
             elapsed = time.perf_counter() - t0
             # Untimed: every page mounted in the harness React and re-rendered
             # after a refresh (element count, mount / re-render ms).
-            amd_react = drv.call("pages", "amd", n=1, react=True).get("react") or {}
+            amd_react = call("pages", "amd", n=1, react=True).get("react") or {}
             # Secondary: the all-pages composite refresh.
             drv.call("steps", "amd", n=1)
-            amd = drv.call("steps", "amd", n=max(3, args.steps // 2))
-            amd_switch = drv.call("switch", "amd", n=5)
-            detail_out = drv.call("detail", "amd", n=5)
+            amd = call("steps", "amd", n=max(3, args.steps // 2))
+            amd_switch = call("switch", "amd", n=5)
+            detail_out = call("detail", "amd", n=5)
             detail = detail_out["detail"]
             served = (server.stats() if args.control_plane == "process"
                       else {"server_requests": fc.stats(), "scrapes": scraper.scrapes if scraper else 0})

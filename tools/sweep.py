@@ -42,9 +42,10 @@ def run(kind, val, args):
            "--rtt-ms", str(args.rtt_ms), f"--{kind}", val]
     if args.extra:
         cmd += args.extra.split()
-    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=1800)
+    # bench progress lines (stderr) pass through: a long point stays visibly alive
+    r = subprocess.run(cmd, cwd=ROOT, stdout=subprocess.PIPE, text=True, timeout=1800)
     if r.returncode != 0:
-        raise RuntimeError(f"{' '.join(cmd)} failed:\n{r.stderr[-3000:]}")
+        raise RuntimeError(f"{' '.join(cmd)} failed (rc {r.returncode}); see its stderr above")
     return json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
 
 
