@@ -494,6 +494,16 @@ async function measure(name, factory, base, a) {
  *   {"cmd":"quit"}
  */
 async function serve(a) {
+  // The views format "Last Fetched" with Date#toLocaleTimeString. Its first
+  // call in a process builds an Intl formatter: V8 loads the ICU data the
+  // Node binary carries, paged in from disk on a fresh host. A browser
+  // (Headlamp) has ICU resident; a fresh Node process does not, and on the
+  // GPU box that cost landed in the first timed refresh (~1 s,
+  // profiles/r3b_smoke.log). It is paid here, once, before any command, and
+  // reported by 'hello'.
+  const icu0 = process.hrtime();
+  new Date(0).toLocaleTimeString();
+  const startup = { icuMs: ms(process.hrtime(icu0)), node: process.version };
   const counter = { n: 0, bytes: 0 };
   const live = {};
   function get(name) {
@@ -509,6 +519,11 @@ async function serve(a) {
     const c = JSON.parse(line);
     const out = { cmd: c.cmd };
     try {
+      if (c.cmd === 'hello') {
+        out.startup = startup;
+        process.stdout.write(JSON.stringify(out) + '\n');
+        continue;
+      }
       if (c.cmd === 'quit') {
         process.stdout.write(JSON.stringify(out) + '\n');
         break;
