@@ -586,6 +586,9 @@ async function serve(a) {
         const L = get(name);
         if (!L.opened) {
           await L.s.coldOpen();
+          // The page rendered when it mounted: a Refresh click always comes
+          // after a first render (untimed here, as in the browser).
+          renderAll(L.s.ctx(), L.s.mstate());
           L.opened = true;
         }
         const lat = [];
@@ -595,17 +598,24 @@ async function serve(a) {
         const render = [];
         let rows = null;
         const stepStarts = [];
+        const renderCpu = [];
         for (let i = 0; i < n; i++) {
           stepStarts.push(hiResClock.now());
           const t0 = process.hrtime();
           await L.s.refresh();
           const t1 = process.hrtime();
+          const c0 = process.cpuUsage();
           rows = renderAll(L.s.ctx(), L.s.mstate());
+          const cu = process.cpuUsage(c0);
           render.push(ms(process.hrtime(t1)));
+          // CPU this process spent rendering: far below the wall time means
+          // it was not running (descheduled / throttled), not slow code.
+          renderCpu.push((cu.user + cu.system) / 1000);
           lat.push(ms(process.hrtime(t0)));
         }
         // Data committed → every view rebuilt and rendered, per step.
         out.renderMs = render;
+        out.renderCpuMs = renderCpu;
         if (L.s.spans) out.trace = traceSummary(L.s.spans.slice(spanStart));
         // Every request of these steps, epoch ms (diagnostics: attribute one slow step).
         if (c.rawSpans && L.s.spans) {
@@ -631,6 +641,7 @@ async function serve(a) {
         const L = get(name);
         if (!L.opened) {
           await L.s.coldOpen();
+          renderAll(L.s.ctx(), L.s.mstate()); // mounted pages rendered once (untimed)
           L.opened = true;
         }
         const lat = {};
