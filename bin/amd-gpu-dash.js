@@ -30,7 +30,7 @@ function usage(msg) {
   if (msg) process.stderr.write('amd-gpu-dash: ' + msg + '\n');
   process.stderr.write(
     'usage: amd-gpu-dash [--url http://127.0.0.1:8001] [--page ' + PAGES.join('|') + '|all|node:NAME|pod:NS/NAME]\n' +
-      '                    [--watch SECONDS]\n' +
+      '                    [--watch SECONDS] [--filter TEXT] [--page-number N] [--per-page N]\n' +
       '                    [--prometheus NAMESPACE/SERVICE:PORT] [--timeout MS] [--token TOKEN] [--insecure]\n' +
       '                    [--color] [--json]\n'
   );
@@ -39,7 +39,7 @@ function usage(msg) {
 
 export function parseArgs(argv) {
   const a = { url: 'http://127.0.0.1:8001', page: 'overview', watch: 0, prometheus: null, timeout: 2000,
-    token: null, insecure: false, color: false, json: false };
+    token: null, insecure: false, color: false, json: false, pager: { page: 0, filter: '' } };
   for (let i = 0; i < argv.length; i++) {
     const k = argv[i];
     const v = argv[i + 1];
@@ -47,6 +47,10 @@ export function parseArgs(argv) {
     else if (k === '--page') a.page = v;
     else if (k === '--watch') a.watch = Number(v);
     else if (k === '--timeout') a.timeout = Number(v);
+    // The paged lists (GPU nodes, GPU / operator pods): which page, and a name filter (pages.js nodePage / podPage).
+    else if (k === '--filter') a.pager.filter = v;
+    else if (k === '--page-number') a.pager.page = Number(v) - 1;
+    else if (k === '--per-page') a.pager.perPage = Number(v);
     else if (k === '--token') a.token = v;
     else if (k === '--prometheus') {
       const m = /^([^/]+)\/([^:]+):(.+)$/.exec(v || '');
@@ -73,6 +77,7 @@ export function parseArgs(argv) {
   else if (pod) a.detail = { kind: 'pod', namespace: pod[1], name: pod[2] };
   else if (a.page !== 'all' && PAGES.indexOf(a.page) < 0) return { error: 'unknown page ' + a.page };
   if (!(a.watch >= 0) || !(a.timeout > 0)) return { error: 'bad --watch / --timeout' };
+  if (!(a.pager.page >= 0) || (a.pager.perPage !== undefined && !(a.pager.perPage > 0))) return { error: 'bad --page-number / --per-page' };
   return a;
 }
 
@@ -114,8 +119,8 @@ function makeRequest(a) {
   };
 }
 
-export function views(ctx, mstate, page) {
-  const opts = { metrics: mstate.metrics };
+export function views(ctx, mstate, page, pager) {
+  const opts = { metrics: mstate.metrics, pager: pager };
   const all = {
     overview: function () { return overviewView(ctx, opts); },
     'device-plugins': function () { return devicePluginsView(ctx, opts); },
@@ -197,7 +202,7 @@ async function main() {
   }
 
   function print() {
-    const vms = views(store.getSnapshot(), mstate, a.page);
+    const vms = views(store.getSnapshot(), mstate, a.page, a.pager);
     if (a.json) {
       process.stdout.write(JSON.stringify(vms.length === 1 ? vms[0] : vms) + '\n');
       return;

@@ -80,3 +80,15 @@ def test_detail_sections_with_power_history(url):
     js = run("--url", url, "--page", "pod:ml/train-000-2", "--json")
     assert json.loads(js.stdout)["title"] == "AMD GPU Resources"
     assert run("--page", "pod:no-slash").returncode == 2
+
+
+def test_pager_flags_select_the_page_and_filter(url):
+    r = run("--url", url, "--page", "nodes", "--json", "--filter", "001")
+    assert r.returncode == 0, r.stderr
+    vm = json.loads(r.stdout)
+    assert [s["title"] for s in vm["items"] if s["t"] == "section"][1:] == ["mi355x-001"]
+    pager = [s for s in vm["items"] if s["t"] == "pager"][0]
+    assert pager["matched"] == 1 and pager["filter"] == "001"
+    two = json.loads(run("--url", url, "--page", "nodes", "--json", "--per-page", "1", "--page-number", "2").stdout)
+    assert [s["title"] for s in two["items"] if s["t"] == "section"][1:] == ["mi355x-001"]
+    assert run("--url", url, "--page-number", "0").returncode == 2
