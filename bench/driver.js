@@ -30,7 +30,7 @@ import { createMetricsSource } from '../src/api/metrics.js';
 import { filterGpuRequestingPods } from '../src/api/amdgpu.js';
 import {
   overviewView, devicePluginsView, nodesView, podsView, metricsView,
-  nodeDetailView, podDetailView, nodeColumns, ownersScope, telemetryScope,
+  nodeDetailView, podDetailView, nodeColumns, nodePage, ownersScope, podPage, telemetryScope,
 } from '../src/view/pages.js';
 import { countRows } from '../src/view/ir.js';
 import { renderPage, renderSection } from '../src/view/html.js';
@@ -143,15 +143,19 @@ function stats(xs) {
   return { n: s.length, p50: q(0.5), p95: q(0.95), min: s[0], max: s[s.length - 1], mean: mean };
 }
 
-/** Build and render every dashboard view; returns the row counts. */
-function renderAll(ctx, mstate) {
-  const pages = {
-    overview: overviewView(ctx),
-    devicePlugins: devicePluginsView(ctx),
-    nodes: nodesView(ctx, { metrics: mstate.metrics }),
-    pods: podsView(ctx, { metrics: mstate.metrics }),
-    metrics: metricsView(ctx, mstate),
-  };
+/**
+ * Build and render every dashboard view of schedule `s` as each page holds
+ * its data (the first page of each pager, that page's own metrics), plus the
+ * native detail sections of the nodes and pods those first pages show and
+ * the Nodes-table columns of every node; returns the row counts.
+ */
+function renderAll(s) {
+  const ctx = s.ctx();
+  const pages = {};
+  for (let p = 0; p < PAGES.length; p++) {
+    const page = PAGES[p];
+    pages[page] = pageVm(page, ctx, page === 'metrics' ? s.pageMstate() : s.mstate(), s.pageMetrics(page));
+  }
   const rows = {};
   let htmlBytes = 0;
   for (const k in pages) {
@@ -159,18 +163,21 @@ function renderAll(ctx, mstate) {
     htmlBytes += renderPage(pages[k]).length;
   }
   let detailSections = 0;
-  for (let i = 0; i < ctx.gpuNodes.length; i++) {
-    const s = nodeDetailView(ctx.gpuNodes[i], ctx, { metrics: mstate.metrics });
-    if (s) {
+  const nodeMetrics = s.pageMetrics('nodes');
+  const shownNodes = nodePage(ctx.gpuNodes, PAGER).nodes;
+  for (let i = 0; i < shownNodes.length; i++) {
+    const sec = nodeDetailView(shownNodes[i], ctx, { metrics: nodeMetrics });
+    if (sec) {
       detailSections++;
-      htmlBytes += renderSection(s).length;
+      htmlBytes += renderSection(sec).length;
     }
   }
-  for (let i = 0; i < ctx.gpuPods.length; i++) {
-    const s = podDetailView(ctx.gpuPods[i], { metrics: mstate.metrics });
-    if (s) {
+  const shownPods = podPage(ctx.gpuPods, PAGER).nodes;
+  for (let i = 0; i < shownPods.length; i++) {
+    const sec = podDetailView(shownPods[i], { metrics: s.pageMetrics('pods') });
+    if (sec) {
       detailSections++;
-      htmlBytes += renderSection(s).length;
+      htmlBytes += renderSection(sec).length;
     }
   }
   const cols = nodeColumns();
@@ -181,10 +188,12 @@ function renderAll(ctx, mstate) {
       columnCells++;
     }
   }
+  const m = s.pageMstate().metrics;
   return {
     gpuNodes: ctx.gpuNodes.length,
     gpuPods: ctx.gpuPods.length,
-    gpusMonitored: mstate.metrics ? mstate.metrics.gpus.length : 0,
+    // every GPU reporting (the Metrics page's cluster totals), not only the page's
+    gpusMonitored: m ? (m.totals ? m.totals.gpus : m.gpus.length) : 0,
     nodeSummaryRows: rows.nodes.tableRows,
     podTableRows: rows.pods.tableRows,
     gpuCells: rows.nodes.gpuCells,
@@ -353,11 +362,24 @@ function amdSchedule(request, clock) {
     });
   }
   return {
+    /**
+     * Every page's data at once, as each page fetches it: the lists and the
+     * DeviceConfig in one wave; GPU Nodes / Metrics / GPU Pods telemetry of
+     * their first pages once the node (pod) list is in.
+     */
     coldOpen: function () {
-      return Promise.all([store.loadLists(), store.refresh(), fetchMetrics()]);
+      return Promise.all([
+        store.loadLists(), store.refresh(), nodesListed().then(fetchNodesPage), nodesListed().then(fetchMetricsPage),
+        listed('podsState').then(fetchPodsPage),
+      ]);
     },
+    /** Composite refresh: every page's Refresh in one wave (5 requests, within the 6 browser sockets). */
     refresh: function () {
-      return Promise.all([store.refresh(), fetchMetrics()]);
+      return Promise.all([store.refresh(), fetchNodesPage(), fetchPodsPage(), fetchMetricsPage()]);
+    },
+    /** Every live series of every GPU (the terminal client's and the screenshots' snapshot). */
+    fetchAll: function () {
+      return fetchMetrics();
     },
     /** One page's Refresh button, as src/plugin.js wires it. */
     refreshPage: function (page) {
@@ -392,7 +414,7 @@ function amdSchedule(request, clock) {
     pageMstate: function () { return metricsPage; },
     /** Route switch: render from the shared store now, revalidate in the background. */
     switchRoute: function () {
-      const bg = Promise.all([store.refresh(), fetchMetrics()]);
+      const bg = Promise.all([store.refresh(), fetchNodesPage(), fetchPodsPage(), fetchMetricsPage()]);
       return { rendered: Promise.resolve(), background: bg };
     },
     ctx: function () { return store.getSnapshot(); },
@@ -447,7 +469,7 @@ async function measure(name, factory, base, a) {
     const before = counter.n;
     const t0 = process.hrtime();
     await s.coldOpen();
-    renderAll(s.ctx(), s.mstate());
+    renderAll(s);
     cold.push(ms(process.hrtime(t0)));
     coldRequests = counter.n - before;
   }
@@ -459,7 +481,7 @@ async function measure(name, factory, base, a) {
   await s.coldOpen();
   for (let i = 0; i < a.warmup; i++) {
     await s.refresh();
-    renderAll(s.ctx(), s.mstate());
+    renderAll(s);
   }
   const lat = [];
   const reqBefore = counter.n;
@@ -468,7 +490,7 @@ async function measure(name, factory, base, a) {
   for (let i = 0; i < a.steps; i++) {
     const t0 = process.hrtime();
     await s.refresh();
-    rows = renderAll(s.ctx(), s.mstate());
+    rows = renderAll(s);
     lat.push(ms(process.hrtime(t0)));
   }
   out.refresh = stats(lat);
@@ -483,7 +505,7 @@ async function measure(name, factory, base, a) {
     const t0 = process.hrtime();
     const r = s.switchRoute();
     await r.rendered;
-    renderAll(s.ctx(), s.mstate());
+    renderAll(s);
     sw.push(ms(process.hrtime(t0)));
     await r.background;
   }
@@ -549,7 +571,7 @@ async function serve(a) {
           const t0 = process.hrtime();
           await s.coldOpen();
           const t1 = process.hrtime();
-          renderAll(s.ctx(), s.mstate());
+          renderAll(s);
           lat.push(ms(process.hrtime(t0)));
           renderMs.push(ms(process.hrtime(t1)));
           req = counter.n - before;
@@ -599,7 +621,7 @@ async function serve(a) {
           await L.s.coldOpen();
           // The page rendered when it mounted: a Refresh click always comes
           // after a first render (untimed here, as in the browser).
-          renderAll(L.s.ctx(), L.s.mstate());
+          renderAll(L.s);
           L.opened = true;
         }
         const lat = [];
@@ -616,7 +638,7 @@ async function serve(a) {
           await L.s.refresh();
           const t1 = process.hrtime();
           const c0 = process.cpuUsage();
-          rows = renderAll(L.s.ctx(), L.s.mstate());
+          rows = renderAll(L.s);
           const cu = process.cpuUsage(c0);
           render.push(ms(process.hrtime(t1)));
           // CPU this process spent rendering: far below the wall time means
@@ -636,7 +658,7 @@ async function serve(a) {
           out.stepStarts = stepStarts;
         }
         const snap = L.s.ctx();
-        const ms_ = L.s.mstate();
+        const ms_ = L.s.pageMstate ? L.s.pageMstate() : L.s.mstate();
         out.state = {
           error: snap.error, crdAvailable: snap.crdAvailable, deviceConfigs: snap.deviceConfigs.length,
           pluginPods: snap.pluginPods.length, metrics: !!ms_.metrics, stale: !!(ms_.metrics && ms_.metrics.stale),
@@ -652,7 +674,7 @@ async function serve(a) {
         const L = get(name);
         if (!L.opened) {
           await L.s.coldOpen();
-          renderAll(L.s.ctx(), L.s.mstate()); // mounted pages rendered once (untimed)
+          renderAll(L.s); // mounted pages rendered once (untimed)
           L.opened = true;
         }
         const lat = {};
@@ -705,6 +727,7 @@ async function serve(a) {
           const fixed = { setTimeout: setTimeout, clearTimeout: clearTimeout, now: function () { return c.now; } };
           snap = amdSchedule(makeRequest(a.url, counter), fixed);
           await snap.coldOpen();
+          await snap.fetchAll();
           // The detail pages' power history, as src/plugin.js fetches it.
           const c0 = snap.ctx();
           const n0 = c0.gpuNodes[0];
@@ -719,6 +742,7 @@ async function serve(a) {
             await L.s.coldOpen();
             L.opened = true;
           }
+          if (L.s.fetchAll) await L.s.fetchAll();
           snap = L.s;
         }
         out.files = writeSnapshots(snap.ctx(), snap.mstate(), c.dir, c.now, history);
@@ -834,7 +858,7 @@ async function serve(a) {
           const t0 = process.hrtime();
           const r = L.s.switchRoute();
           await r.rendered;
-          renderAll(L.s.ctx(), L.s.mstate());
+          renderAll(L.s);
           lat.push(ms(process.hrtime(t0)));
           await r.background;
         }

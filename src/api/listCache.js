@@ -78,6 +78,10 @@ export function createListTracker(predicates) {
   let prevItems = []; // the array handed to the previous update
   let prevRec = []; // its records, by position
   let gen = 0;
+  // The first list, classified but without records yet ({raws, bits}): a
+  // cold open pays the classification only, like a plain filter; the records
+  // (and the uid map) are built when a second list arrives.
+  let pending = null;
   let subsets = [];
   for (let b = 0; b < nSub; b++) subsets.push([]);
   const stats = { updates: 0, classified: 0, reused: 0, compared: 0, subsetPatches: 0, subsetRebuilds: 0 };
@@ -109,7 +113,24 @@ export function createListTracker(predicates) {
     return rec;
   }
 
+  function materialize() {
+    if (!pending) return;
+    const raws = pending.raws;
+    const bits = pending.bits;
+    const recs = new Array(raws.length);
+    for (let i = 0; i < raws.length; i++) {
+      const raw = raws[i];
+      const key = keyOf(raw);
+      const rec = { raw: raw, key: key, version: versionOf(raw), bits: bits[i], gen: pending.gen, pos: i };
+      if (key !== null) byKey.set(key, rec);
+      recs[i] = rec;
+    }
+    prevRec = recs;
+    pending = null;
+  }
+
   function positionOf(raw) {
+    materialize();
     const r = byKey.get(keyOf(raw));
     return r ? r.pos : -1;
   }
@@ -146,6 +167,8 @@ export function createListTracker(predicates) {
       deltas.push(null);
     }
     if (list === prevItems) return { subsets: subsets, changed: changed, deltas: deltas };
+    if (pn === 0 && !pending && byKey.size === 0 && n > 0) return firstLoad(list, changed, deltas);
+    materialize();
     gen++;
     // Common prefix and suffix: untouched.
     let lo = 0;
@@ -279,7 +302,34 @@ export function createListTracker(predicates) {
     return { subsets: subsets, changed: changed, deltas: deltas };
   }
 
+  /** The first non-empty list: classify each object, build the subsets, defer the records. */
+  function firstLoad(list, changed, deltas) {
+    gen++;
+    const n = list.length;
+    const raws = new Array(n);
+    const bits = new Uint32Array(n);
+    for (let i = 0; i < n; i++) {
+      const raw = unwrapKubeObject(list[i]);
+      raws[i] = raw;
+      bits[i] = keyOf(raw) === null ? 0 : classify(raw);
+    }
+    pending = { raws: raws, bits: bits, gen: gen };
+    prevItems = list;
+    prevRec = [];
+    for (let b = 0; b < nSub; b++) {
+      const bit = 1 << b;
+      const out = [];
+      for (let i = 0; i < n; i++) if (bits[i] & bit) out.push(raws[i]);
+      stats.subsetRebuilds++;
+      if (out.length === 0 && subsets[b].length === 0) continue;
+      subsets[b] = out;
+      changed[b] = true;
+    }
+    return { subsets: subsets, changed: changed, deltas: deltas };
+  }
+
   function reset() {
+    pending = null;
     byKey = new Map();
     prevItems = [];
     prevRec = [];

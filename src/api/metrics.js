@@ -755,6 +755,7 @@ export function createMetricsSource(opts) {
     lastBy = {};
     scopeStatic = {};
     scopedState = new Map();
+    noGpusUntil = 0;
     for (const k in nodeStates) delete nodeStates[k];
   }
 
@@ -891,8 +892,11 @@ export function createMetricsSource(opts) {
         const totals = summary ? totalsFromRows(rows.__agg) : undefined;
         const found = j.gpus.length > 0 || (!!totals && totals.gpus > 0);
         // Nothing from the exporter yet: maybe node-exporter feeds this
-        // Prometheus (no hostname label) — ask cluster-wide once to find out.
-        if (!found && source !== 'amd-exporter') return NOT_SCOPED;
+        // Prometheus (no hostname label) — ask cluster-wide to find out, at
+        // most once per discovery TTL when that finds no GPU either (a
+        // cluster without GPU telemetry would otherwise pay two round trips
+        // on every refresh).
+        if (!found && source !== 'amd-exporter' && clock.now() >= noGpusUntil) return NOT_SCOPED;
         if (found) source = 'amd-exporter';
         const now = clock.now();
         if (withStatic) {
@@ -948,10 +952,15 @@ export function createMetricsSource(opts) {
     return st.last;
   }
 
+  // Until then a scoped fetch that finds nothing does not ask cluster-wide
+  // again: the last cluster-wide look found no GPU telemetry at all.
+  let noGpusUntil = 0;
+
   /** The cluster-wide snapshot cut to `scope` (node-exporter source; exporter not found by a scoped query). */
   function clusterCut(v, scope, summary, key) {
     return fetchGpuMetrics(v).then(function (m) {
       if (!m) return null;
+      if (m.gpus.length === 0) noGpusUntil = clock.now() + ttl;
       const st = scopedEntry(key);
       if (st.cutOf === m && st.last) return st.last;
       const inScope = {};

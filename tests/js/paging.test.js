@@ -327,3 +327,20 @@ describe('GPU Pods / Device Plugins / Overview tables are bounded too', () => {
     expect(pagerOf(dp).noun).toBe('operator pods');
   });
 });
+
+describe('scoped fetches on a cluster without GPU telemetry', () => {
+  it('ask cluster-wide once per discovery TTL, not on every refresh', async () => {
+    const fake = prom({ data: {} });
+    let now = 1000;
+    const clock = { setTimeout: setTimeout, clearTimeout: clearTimeout, now: () => now };
+    const s = createMetricsSource({ request: fake, clock: clock });
+    await s.fetchGpuMetrics('gauges', { scope: [], summary: true });
+    const first = fake.mock.calls.length;
+    expect(first).toBe(2); // the scoped summary, then the cluster-wide look
+    await s.fetchGpuMetrics('gauges', { scope: [], summary: true });
+    expect(fake.mock.calls.length).toBe(first + 1); // scoped only
+    now += 6 * 60 * 1000; // past the discovery TTL
+    await s.fetchGpuMetrics('gauges', { scope: [], summary: true });
+    expect(fake.mock.calls.length).toBeGreaterThan(first + 2);
+  });
+});
