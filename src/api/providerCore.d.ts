@@ -57,6 +57,13 @@ export interface ProviderCore {
   useGpuOwners(enabled?: boolean, pods?: string[]): GpuMetricsState;
   usePodGpuSeries(namespace: string | null, pod: string | null, enabled?: boolean): GpuMetricsState;
   useNodeGpuSeries(nodeName: string | null, enabled?: boolean): GpuMetricsState;
+  /** One node's pods for a Node detail section on a cold store (one field-selected request) */
+  useNodePods(
+    nodeName: string | null,
+    enabled?: boolean
+  ): { loading: boolean; gpuPods: unknown[]; podsState: 'pending' | 'ready' | 'error'; error: string | null };
+  /** The shared store already holds the node and pod lists (a plugin page fed it) */
+  storeWarm(): boolean;
   storeFor(cluster: string): ClusterStore;
   metricsSourceFor(cluster: string): MetricsSource;
 }

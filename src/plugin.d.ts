@@ -30,6 +30,8 @@ export interface Plugin {
   PodsPage: ComponentType;
   MetricsPage: ComponentType;
   NodeDetailSection: ComponentType<{ resource: unknown }>;
+  /** Node detail on a cold store: the node's own pods by one field-selected request */
+  NodeDetailCold: ComponentType<{ resource: unknown }>;
   PodDetailSection: ComponentType<{ resource: unknown }>;
   SettingsPage: ComponentType<{ data?: Record<string, unknown>; onDataChange?: (data: Record<string, unknown>) => void }>;
   buildNodeGpuColumns(): NodeColumn[];
