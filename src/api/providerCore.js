@@ -329,18 +329,34 @@ export function createProviderCore(React, lib, deps) {
    */
   function useNodePods(nodeName, enabled) {
     const active = (enabled === undefined ? true : enabled) && !!nodeName;
+    const refreshIntervalSec = loadSettings().refreshIntervalSec;
     const st = useState({ node: null, pods: null, error: null });
     const state = st[0];
     const setState = st[1];
+    const sq = useState(0);
+    const seq = sq[0];
+    const setSeq = sq[1];
     useEffect(function () {
       if (!active) return undefined;
       let cancelled = false;
       fetchNodePods(request, nodeName, loadSettings().requestTimeoutMs).then(
         function (items) { if (!cancelled) setState({ node: nodeName, pods: items, error: null }); },
-        function (e) { if (!cancelled) setState({ node: nodeName, pods: [], error: errorText(e) }); }
+        function (e) {
+          if (cancelled) return;
+          // A failed re-fetch keeps the pods already shown; only a first failure says so.
+          setState(function (s) { return s.node === nodeName && s.pods && !s.error ? s : { node: nodeName, pods: [], error: errorText(e) }; });
+        }
       );
       return function () { cancelled = true; };
-    }, [nodeName, active]);
+    }, [nodeName, active, seq]);
+    // No watch on this path: with auto-refresh on (settings) the list is re-read
+    // each period, like the pages' imperative track.
+    useEffect(function () {
+      if (!active) return undefined;
+      const poller = createPoller(refreshIntervalSec);
+      poller.start(function () { setSeq(function (x) { return x + 1; }); });
+      return function () { poller.stop(); };
+    }, [nodeName, active, refreshIntervalSec]);
     return useMemo(function () {
       const mine = state.node === nodeName;
       return {

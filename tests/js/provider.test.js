@@ -472,3 +472,60 @@ describe('metrics hooks', () => {
     qs.forEach((q) => expect(q).toContain('pod!=""'));
   });
 });
+
+describe('useNodePods (cold Node detail)', () => {
+  function nodePodsServer(pods) {
+    return vi.fn((path) => {
+      const m = /^\/api\/v1\/pods\?fieldSelector=(.*)$/.exec(path);
+      if (!m) return notFound();
+      const node = decodeURIComponent(m[1]).replace(/^spec\.nodeName=/, '');
+      return Promise.resolve(kubeList(pods().filter((p) => p.spec.nodeName === node)));
+    });
+  }
+  function Section(c, node) {
+    return function S() {
+      const r = c.useNodePods(node, true);
+      return h('div', null, r.loading ? 'loading' : r.podsState + ':' + r.gpuPods.map((p) => p.metadata.name).join(','));
+    };
+  }
+
+  it('one field-selected request for the node, GPU pods only', async () => {
+    const request = nodePodsServer(() => [makeGpuPod('a', { node: 'n1' }), makeGpuPod('b', { node: 'n2' }), makePlainPod('web')]);
+    const r = render(h(Section(core(request), 'n1')));
+    expect(r.text()).toBe('loading');
+    await r.settle();
+    expect(r.text()).toBe('ready:a');
+    expect(request.mock.calls.map((c) => c[0])).toEqual(['/api/v1/pods?fieldSelector=' + encodeURIComponent('spec.nodeName=n1')]);
+    r.unmount();
+  });
+
+  it('re-reads the node\'s pods each auto-refresh period and keeps them through a failed re-read', async () => {
+    vi.useFakeTimers();
+    settings.refreshIntervalSec = 15;
+    let pods = [makeGpuPod('a', { node: 'n1' })];
+    let fail = false;
+    const ok = nodePodsServer(() => pods);
+    const request = vi.fn((p) => (fail ? Promise.reject(Object.assign(new Error('503'), { status: 503 })) : ok(p)));
+    const r = render(h(Section(core(request), 'n1')));
+    await r.settle();
+    expect(r.text()).toBe('ready:a');
+    pods = [makeGpuPod('a', { node: 'n1' }), makeGpuPod('c', { node: 'n1' })];
+    await vi.advanceTimersByTimeAsync(15000);
+    await r.settle();
+    expect(r.text()).toBe('ready:a,c');
+    fail = true;
+    await vi.advanceTimersByTimeAsync(15000);
+    await r.settle();
+    expect(r.text()).toBe('ready:a,c');
+    expect(request.mock.calls.length).toBe(3);
+    r.unmount();
+  });
+
+  it('a first failure says the pods are unreadable', async () => {
+    const request = vi.fn(() => Promise.reject(Object.assign(new Error('pods is forbidden'), { status: 403 })));
+    const r = render(h(Section(core(request), 'n1')));
+    await r.settle();
+    expect(r.text()).toBe('error:');
+    r.unmount();
+  });
+});
