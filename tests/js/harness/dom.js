@@ -17,7 +17,8 @@ export const tier = 'react-dom';
 
 export function render(element, options) {
   const strict = !!(options && options.strict);
-  const r = rtlRender(strict ? React.createElement(React.StrictMode, null, element) : element);
+  const wrap = function (el) { return strict ? React.createElement(React.StrictMode, null, el) : el; };
+  const r = rtlRender(wrap(element));
   const c = r.container;
   const handle = {
     /** Let pending requests resolve and React commit, `rounds` macrotask turns. */
@@ -44,6 +45,10 @@ export function render(element, options) {
     change: function (node, value) { fireEvent.change(node, { target: { value: value } }); return handle; },
     isDisabled: function (node) { return !!node.disabled; },
     textOf: function (node) { return node.textContent; },
+    rerender: function (element2) {
+      r.rerender(wrap(element2));
+      return handle;
+    },
     unmount: function () { r.unmount(); },
   };
   return handle;

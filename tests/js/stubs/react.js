@@ -10,9 +10,17 @@
  *     key, else position, and type, like React);
  *   * `memo` components skip rendering when their props are shallow-equal
  *     and nothing below them is dirty (render counts are observable);
- *   * effects run after the render pass, children before parents; cleanups
- *     run before the next effect and on unmount;
+ *   * effects run after the render pass in React's commit order: layout
+ *     before passive, children before parents, every cleanup of a phase
+ *     before its new effects; a deleted subtree cleans up parent first;
+ *   * <StrictMode> calls each component body twice and replays new effects
+ *     (mount, cleanup, mount), as React 18's development build does;
  *   * state updates outside `act` are batched on a microtask.
+ *
+ * tests/js/shared/react-semantics.shared.test.js pins these rules; it runs
+ * here and, in networked CI, on real React 18 + react-dom
+ * (vitest.react.config.mts), so a divergence of this file from React fails
+ * there.
  *
  * The rendered host tree ({tag, props, children}) can be queried
  * testing-library style (getByText, getByLabelText, getByTestId, …),
@@ -79,6 +87,7 @@ export function createContext(defaultValue) {
 
 let current = null; // instance being rendered
 let hookIndex = 0;
+let replaying = false; // StrictMode's discarded first call of a component body
 let currentRoot = null;
 const ctxStack = [];
 
@@ -135,6 +144,7 @@ export function useState(init) {
 function effectHook(fn, deps, layout) {
   const inst = current;
   const slot = hookSlot(function () { return { deps: undefined, cleanup: null, first: true }; }, layout ? 'useLayoutEffect' : 'useEffect');
+  if (replaying) return;
   if (slot.first || deps === undefined || depsChanged(slot.deps, deps)) {
     slot.first = false;
     slot.deps = deps;
@@ -200,15 +210,17 @@ export function useSyncExternalStore(subscribe, getSnapshot) {
   // React (dev) reads the snapshot twice: a store whose getSnapshot builds a
   // new object each call would re-render forever.
   if (!Object.is(getSnapshot(), value)) throw new Error('The result of getSnapshot should be cached to avoid an infinite loop');
+  if (replaying) return value;
   slot.value = value;
   slot.getSnapshot = getSnapshot;
   if (slot.subscribe !== subscribe) {
     slot.subscribe = subscribe;
+    // React 18 subscribes in a passive effect and re-checks the snapshot there.
     inst.root.pendingEffects.push({
       inst: inst,
       slot: slot,
       depth: inst.depth,
-      layout: true,
+      layout: false,
       fn: function () {
         if (slot.unsubscribe) slot.unsubscribe();
         const check = function () {
@@ -404,18 +416,27 @@ function renderInstance(inst, prevProps) {
   } else if (typeof t === 'function') {
     const prev = current;
     const prevIdx = hookIndex;
+    const prevReplay = replaying;
     current = inst;
-    hookIndex = 0;
     inst.renders++;
-    inst.ctxReads = new Map();
     let result;
     let used = 0;
     try {
-      result = t(inst.props);
-      used = hookIndex;
+      // <StrictMode> (React 18, development) calls every component body
+      // twice per render and keeps the second result, so a render with side
+      // effects shows up. The first call here queues no effects.
+      const calls = root.strict ? 2 : 1;
+      for (let c = 0; c < calls; c++) {
+        replaying = c < calls - 1;
+        hookIndex = 0;
+        inst.ctxReads = new Map();
+        result = t(inst.props);
+        used = hookIndex;
+      }
     } finally {
       current = prev;
       hookIndex = prevIdx;
+      replaying = prevReplay;
     }
     // React: "Rendered fewer hooks than expected" (a hook behind a condition or an early return).
     if (used < inst.hooks.length) throw new Error('Rendered fewer hooks than expected in ' + typeName(t));
@@ -427,19 +448,30 @@ function renderInstance(inst, prevProps) {
   inst.dirty = false;
 }
 
+// React 18 runs a deleted subtree's effect cleanups parent before child
+// (react-reconciler's "Deletion effects fire in parent -> child order"),
+// layout cleanups during the commit, passive ones after it.
 function unmount(inst) {
   if (inst.unmounted) return;
-  inst.unmounted = true;
-  for (let i = 0; i < inst.kids.length; i++) unmount(inst.kids[i]);
-  for (let i = 0; i < inst.hooks.length; i++) {
-    const hk = inst.hooks[i];
-    if (hk && typeof hk.cleanup === 'function') {
-      const c = hk.cleanup;
-      hk.cleanup = null;
-      c();
-    }
-  }
-  inst.root.unmounts++;
+  const removed = [];
+  walkInstances(inst, function (i) {
+    if (!i.unmounted) removed.push(i);
+  });
+  removed.forEach(function (i) { i.unmounted = true; });
+  [true, false].forEach(function (layout) {
+    removed.forEach(function (i) {
+      const kinds = i.hookKinds || [];
+      for (let h = 0; h < i.hooks.length; h++) {
+        const hk = i.hooks[h];
+        const isLayout = kinds[h] === 'useLayoutEffect';
+        if (isLayout !== layout || !hk || typeof hk.cleanup !== 'function') continue;
+        const c = hk.cleanup;
+        hk.cleanup = null;
+        c();
+      }
+    });
+  });
+  removed.forEach(function (i) { i.root.unmounts++; });
 }
 
 function textOf(node) {
@@ -528,26 +560,44 @@ export function render(element, options) {
     });
   };
 
+  function cleanupOf(e) {
+    if (e.inst.unmounted || typeof e.slot.cleanup !== 'function') return;
+    const c = e.slot.cleanup;
+    e.slot.cleanup = null;
+    c();
+  }
+
+  function mountOf(e) {
+    if (e.inst.unmounted) return;
+    const r = e.fn();
+    e.slot.cleanup = typeof r === 'function' ? r : null;
+  }
+
   function runEffects() {
     const list = root.pendingEffects;
     root.pendingEffects = [];
-    // Children's effects run before their parents' (React commit order);
-    // layout effects (and store subscriptions) before passive ones.
-    list.sort(function (a, b) { return (b.layout - a.layout) || (b.depth - a.depth); });
-    for (let i = 0; i < list.length; i++) {
-      const e = list[i];
-      if (e.inst.unmounted) continue;
-      if (typeof e.slot.cleanup === 'function') e.slot.cleanup();
-      const r = e.fn();
-      e.slot.cleanup = typeof r === 'function' ? r : null;
-      // <StrictMode> (React 18, development): a newly mounted effect is run,
-      // cleaned up and run again, so effects must be idempotent.
-      if (root.strict && !e.slot.strictRemounted) {
-        e.slot.strictRemounted = true;
-        if (typeof e.slot.cleanup === 'function') e.slot.cleanup();
-        const r2 = e.fn();
-        e.slot.cleanup = typeof r2 === 'function' ? r2 : null;
-      }
+    // React commit order: children's effects before their parents'; every
+    // cleanup of a phase before any of its new effects; the layout phase
+    // (inside the commit) before the passive one.
+    list.sort(function (a, b) { return b.depth - a.depth; });
+    const layout = list.filter(function (e) { return e.layout; });
+    const passive = list.filter(function (e) { return !e.layout; });
+    layout.forEach(cleanupOf);
+    layout.forEach(mountOf);
+    passive.forEach(cleanupOf);
+    passive.forEach(mountOf);
+    // <StrictMode> (React 18, development): newly mounted effects are torn
+    // down and run again — layout cleanups, passive cleanups, layout effects,
+    // passive effects — so effects must be idempotent.
+    if (root.strict) {
+      const fresh = list.filter(function (e) { return !e.slot.strictRemounted && !e.inst.unmounted; });
+      fresh.forEach(function (e) { e.slot.strictRemounted = true; });
+      const fl = fresh.filter(function (e) { return e.layout; });
+      const fp = fresh.filter(function (e) { return !e.layout; });
+      fl.forEach(cleanupOf);
+      fp.forEach(cleanupOf);
+      fl.forEach(mountOf);
+      fp.forEach(mountOf);
     }
   }
 
