@@ -45,6 +45,10 @@ export function render(element, options) {
     change: function (node, value) { fireEvent.change(node, { target: { value: value } }); return handle; },
     isDisabled: function (node) { return !!node.disabled; },
     textOf: function (node) { return node.textContent; },
+    act: function (fn) {
+      act(function () { fn(); });
+      return handle;
+    },
     rerender: function (element2) {
       r.rerender(wrap(element2));
       return handle;

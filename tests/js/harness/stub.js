@@ -25,6 +25,11 @@ export function render(element, options) {
     change: function (node, value) { r.change(node, value); return handle; },
     isDisabled: function (node) { return !!node.props.disabled; },
     textOf: function (node) { return textOf(node); },
+    /** Run `fn` (an event-like update) and commit what it scheduled. */
+    act: function (fn) {
+      r.act(function () { fn(); });
+      return handle;
+    },
     /** Render a new element at the same root (props change, key change). */
     rerender: function (element2) {
       r.rerender(element2);

@@ -1,20 +1,19 @@
 /**
- * Provider core (src/api/providerCore.js) executed under the harness React
- * (tests/js/stubs/react.js) and the Headlamp library stand-in
- * (tests/js/stubs/headlamp-lib.js). Mirrors the reference's provider specs
- * (src/api/IntelGpuDataContext.test.tsx:46-176: outside-provider throw,
- * request issuing, CRD absent vs present) and adds what the shared store
- * promises: request counts on mount, dedup across providers, stale-while-
- * revalidate remounts, degraded RBAC and the metrics hooks.
+ * Provider core (src/api/providerCore.js) specs that need the harness React
+ * (tests/js/stubs/react.js) or fake timers: STALE_MS revalidation, the
+ * auto-refresh poller, the metrics back-off and the cold Node detail's
+ * periodic re-read, plus the pure list-result reader. Everything that only
+ * renders and reads text, requests and context values is runner-agnostic
+ * and lives in tests/js/shared/provider.shared.test.js, which also runs on
+ * real React 18 in CI.
  */
 import React, { render } from './stubs/react.js';
 import * as lib from './stubs/headlamp-lib.js';
-import { OUTSIDE_PROVIDER, PROMETHEUS_FORBIDDEN, PROMETHEUS_UNREACHABLE, STALE_MS, createProviderCore, listResult } from '../../src/api/providerCore.js';
+import { PROMETHEUS_FORBIDDEN, PROMETHEUS_UNREACHABLE, STALE_MS, createProviderCore, listResult } from '../../src/api/providerCore.js';
 import { resetSharedStores } from '../../src/api/clusterStore.js';
 import { DEVICE_CONFIG_LIST_PATH, PLUGIN_POD_QUERIES } from '../../src/api/amdgpu.js';
 import { DEFAULT_SETTINGS } from '../../src/api/settings.js';
-import { makeDeviceConfig, makeGpuNode, makeGpuPod, makeNode, makePlainPod, makePluginPod } from './fixtures.js';
-import { BASE0, exporterData, prom } from './promFake.js';
+import { makeDeviceConfig, makeGpuPod } from './fixtures.js';
 
 const h = React.createElement;
 
@@ -26,11 +25,10 @@ function notFound() {
   return Promise.reject(Object.assign(new Error('404 page not found'), { status: 404 }));
 }
 
-/** API server fake: CRD → `dcs` (or `crd` handler), plugin-pod queries → `pluginPods`. */
 function apiServer(o) {
   const opt = Object.assign({ dcs: [makeDeviceConfig()], pluginPods: [] }, o || {});
   return vi.fn((path) => {
-    if (path === DEVICE_CONFIG_LIST_PATH) return opt.crd ? opt.crd() : Promise.resolve(kubeList(opt.dcs));
+    if (path === DEVICE_CONFIG_LIST_PATH) return Promise.resolve(kubeList(opt.dcs));
     if (PLUGIN_POD_QUERIES.indexOf(path) >= 0) return Promise.resolve(kubeList(opt.pluginPods));
     if (opt.prom) return opt.prom(path);
     return notFound();
@@ -51,15 +49,12 @@ function core(request) {
   });
 }
 
-/** A consumer that records every context value it renders with. */
 function probe(c) {
-  const seen = [];
   function Probe() {
     const ctx = c.useAmdGpuContext();
-    seen.push(ctx);
-    return h('div', { 'data-testid': 'probe' }, ctx.loading ? 'loading' : 'nodes=' + ctx.gpuNodes.length + ' pods=' + ctx.gpuPods.length);
+    return h('div', null, ctx.loading ? 'loading' : 'nodes=' + ctx.gpuNodes.length);
   }
-  return { Probe, seen, last: () => seen[seen.length - 1] };
+  return { Probe };
 }
 
 beforeEach(() => {
@@ -72,89 +67,18 @@ afterEach(() => {
   vi.useRealTimers();
 });
 
-describe('createProviderCore', () => {
-  it('requires the React hooks it uses', () => {
-    expect(() => createProviderCore({ createElement: React.createElement }, lib)).toThrow('React.createContext is required');
-  });
-  it('checks useRef up front (the metrics hooks keep their back-off flag in a ref)', () => {
-    const noRef = Object.assign({}, React);
-    delete noRef.useRef;
-    expect(() => createProviderCore(noRef, lib)).toThrow('React.useRef is required');
-  });
-});
-
-describe('useAmdGpuContext', () => {
-  it('throws outside a provider', () => {
-    const c = core(apiServer());
-    const { Probe } = probe(c);
-    expect(() => render(h(Probe))).toThrow(OUTSIDE_PROVIDER);
-  });
-
-  it('exposes the reference context contract inside a provider', async () => {
-    const c = core(apiServer());
-    const p = probe(c);
-    const r = render(h(c.AmdGpuDataProvider, null, h(p.Probe)));
-    await r.settle();
-    const ctx = p.last();
-    ['deviceConfigs', 'pluginInstalled', 'gpuNodes', 'gpuPods', 'pluginPods', 'crdAvailable', 'loading', 'error'].forEach((k) =>
-      expect(ctx).toHaveProperty(k)
-    );
-    expect(typeof ctx.refresh).toBe('function');
+describe('listResult', () => {
+  it('loading, errors array, tuple', () => {
+    expect(listResult(undefined)).toEqual([null, null]);
+    expect(listResult([null, null])).toEqual([null, null]);
+    expect(listResult([[1], 'e'])).toEqual([[1], 'e']);
+    expect(listResult({ items: [], isLoading: true })).toEqual([null, null]);
+    expect(listResult({ items: null, errors: ['pods is forbidden'] })).toEqual([null, 'pods is forbidden']);
+    expect(listResult({ items: [1], errors: [] })).toEqual([[1], null]);
   });
 });
 
-describe('AmdGpuDataProvider — requests', () => {
-  it('issues exactly one CRD request on mount while the pod watch is in flight', async () => {
-    const request = apiServer();
-    const c = core(request);
-    const p = probe(c);
-    const r = render(h(c.AmdGpuDataProvider, null, h(p.Probe)));
-    await r.settle();
-    expect(request).toHaveBeenCalledTimes(1);
-    expect(request.mock.calls[0][0]).toBe(DEVICE_CONFIG_LIST_PATH);
-    expect(p.last().crdAvailable).toBe(true);
-    expect(p.last().deviceConfigs).toHaveLength(1);
-  });
-
-  it('asks Headlamp for nodes and for pods in all namespaces', () => {
-    const c = core(apiServer());
-    const p = probe(c);
-    render(h(c.AmdGpuDataProvider, null, h(p.Probe)));
-    expect(lib.lists.calls.Node[0]).toBeNull();
-    expect(lib.lists.calls.Pod[0]).toEqual({ namespace: '' });
-  });
-
-  it('a second provider mounted at the same time adds no request', async () => {
-    const request = apiServer();
-    const c = core(request);
-    const a = probe(c);
-    const b = probe(c);
-    const r = render(h('div', null, h(c.AmdGpuDataProvider, null, h(a.Probe)), h(c.AmdGpuDataProvider, null, h(b.Probe))));
-    await r.settle();
-    expect(crdCalls(request)).toBe(1);
-    expect(a.last().deviceConfigs).toBe(b.last().deviceConfigs);
-  });
-
-  it('a remount within STALE_MS renders the cached data at once with no request', async () => {
-    const request = apiServer();
-    lib.lists.Node = [[makeGpuNode('mi355x-0')], null];
-    lib.lists.Pod = [[makeGpuPod('train-a')], null];
-    const c = core(request);
-    const p1 = probe(c);
-    const r1 = render(h(c.AmdGpuDataProvider, null, h(p1.Probe)));
-    await r1.settle();
-    r1.unmount();
-    expect(crdCalls(request)).toBe(1);
-
-    const p2 = probe(c);
-    const r2 = render(h(c.AmdGpuDataProvider, null, h(p2.Probe)));
-    expect(p2.seen[0].loading).toBe(false);
-    expect(p2.seen[0].deviceConfigs).toHaveLength(1);
-    expect(r2.getByTestId('probe').children[0]).toBe('nodes=1 pods=1');
-    await r2.settle();
-    expect(crdCalls(request)).toBe(1);
-  });
-
+describe('AmdGpuDataProvider — timers', () => {
   it('a remount after STALE_MS revalidates once', async () => {
     vi.useFakeTimers();
     const request = apiServer();
@@ -168,20 +92,6 @@ describe('AmdGpuDataProvider — requests', () => {
     const r2 = render(h(c.AmdGpuDataProvider, null, h(p2.Probe)));
     await r2.settle();
     expect(crdCalls(request)).toBe(2);
-  });
-
-  it('refresh() re-fetches the CRD only (the pod list comes from the watch)', async () => {
-    const request = apiServer();
-    lib.lists.Pod = [[makePlainPod('web-0')], null];
-    const c = core(request);
-    const p = probe(c);
-    const r = render(h(c.AmdGpuDataProvider, null, h(p.Probe)));
-    await r.settle();
-    const before = request.mock.calls.length;
-    r.act(() => p.last().refresh());
-    await r.settle();
-    expect(request.mock.calls.length).toBe(before + 1);
-    expect(request.mock.calls[before][0]).toBe(DEVICE_CONFIG_LIST_PATH);
   });
 
   it('auto-refresh (settings) revalidates on the poller period', async () => {
@@ -202,169 +112,16 @@ describe('AmdGpuDataProvider — requests', () => {
   });
 });
 
-describe('AmdGpuDataProvider — data', () => {
-  it('classifies the useList nodes and pods', async () => {
-    lib.lists.Node = [[makeGpuNode('mi355x-0'), makeGpuNode('mi355x-1'), makeNode('cpu-0')], null];
-    lib.lists.Pod = [[makeGpuPod('train-a'), makePlainPod('web-0'), makePluginPod('amdgpu-dp-1')], null];
-    const c = core(apiServer());
-    const p = probe(c);
-    const r = render(h(c.AmdGpuDataProvider, null, h(p.Probe)));
-    await r.settle();
-    expect(p.last().gpuNodes.map((n) => n.metadata.name)).toEqual(['mi355x-0', 'mi355x-1']);
-    expect(p.last().gpuPods.map((x) => x.metadata.name)).toEqual(['train-a']);
-    expect(p.last().pluginPods.map((x) => x.metadata.name)).toEqual(['amdgpu-dp-1']);
-    expect(r.getByTestId('probe').children[0]).toBe('nodes=2 pods=1');
-  });
-
-  it('reads the object form of a list result ({items, errors, isLoading}) as well as the tuple', async () => {
-    lib.lists.Node = { items: [makeGpuNode('mi355x-0'), makeNode('cpu-0')], errors: null, isLoading: false };
-    lib.lists.Pod = { items: [makeGpuPod('train-a')], error: null, isLoading: false };
-    const c = core(apiServer());
-    const p = probe(c);
-    const r = render(h(c.AmdGpuDataProvider, null, h(p.Probe)));
-    await r.settle();
-    expect(p.last().loading).toBe(false);
-    expect(p.last().gpuNodes.map((n) => n.metadata.name)).toEqual(['mi355x-0']);
-    expect(p.last().gpuPods.map((x) => x.metadata.name)).toEqual(['train-a']);
-  });
-
-  it('listResult: loading, errors array, tuple', () => {
-    expect(listResult(undefined)).toEqual([null, null]);
-    expect(listResult([null, null])).toEqual([null, null]);
-    expect(listResult([[1], 'e'])).toEqual([[1], 'e']);
-    expect(listResult({ items: [], isLoading: true })).toEqual([null, null]);
-    expect(listResult({ items: null, errors: ['pods is forbidden'] })).toEqual([null, 'pods is forbidden']);
-    expect(listResult({ items: [1], errors: [] })).toEqual([[1], null]);
-  });
-
-  it('unwraps Headlamp KubeObject wrappers (jsonData)', async () => {
-    lib.lists.Node = [[{ jsonData: makeGpuNode('mi355x-0') }], null];
-    lib.lists.Pod = [[{ jsonData: makeGpuPod('train-a') }], null];
-    const c = core(apiServer());
-    const p = probe(c);
-    const r = render(h(c.AmdGpuDataProvider, null, h(p.Probe)));
-    await r.settle();
-    expect(p.last().gpuNodes[0].metadata.name).toBe('mi355x-0');
-    expect(p.last().gpuPods[0].metadata.name).toBe('train-a');
-  });
-
-  it('stays loading while the lists are in flight, then settles', async () => {
-    const c = core(apiServer());
-    const p = probe(c);
-    const r = render(h(c.AmdGpuDataProvider, null, h(p.Probe)));
-    await r.settle();
-    expect(p.last().loading).toBe(true);
-    lib.lists.Node = [[makeGpuNode('mi355x-0')], null];
-    lib.lists.Pod = [[], null];
-    r.rerender(h(c.AmdGpuDataProvider, null, h(p.Probe)));
-    await r.settle();
-    expect(p.last().loading).toBe(false);
-  });
-
-  it('a watch event on an unrelated pod keeps the GPU pod list identity', async () => {
-    const gpu = makeGpuPod('train-a');
-    lib.lists.Node = [[makeGpuNode('mi355x-0')], null];
-    lib.lists.Pod = [[gpu, makePlainPod('web-0')], null];
-    const c = core(apiServer());
-    const p = probe(c);
-    const r = render(h(c.AmdGpuDataProvider, null, h(p.Probe)));
-    await r.settle();
-    const before = p.last().gpuPods;
-    lib.lists.Pod = [[gpu, makePlainPod('web-0'), makePlainPod('web-1')], null];
-    r.rerender(h(c.AmdGpuDataProvider, null, h(p.Probe)));
-    await r.settle();
-    expect(p.last().gpuPods).toBe(before);
-  });
-
-  it('CRD 404 → crdAvailable false, no error', async () => {
-    const c = core(apiServer({ crd: notFound }));
-    lib.lists.Node = [[], null];
-    lib.lists.Pod = [[], null];
-    const p = probe(c);
-    const r = render(h(c.AmdGpuDataProvider, null, h(p.Probe)));
-    await r.settle();
-    expect(p.last().crdAvailable).toBe(false);
-    expect(p.last().error).toBeNull();
-    expect(p.last().loading).toBe(false);
-  });
-
-  it('a transient CRD failure after a success keeps the last known DeviceConfigs', async () => {
-    let fail = false;
-    const crd = () => (fail ? Promise.reject(Object.assign(new Error('503'), { status: 503 })) : Promise.resolve(kubeList([makeDeviceConfig()])));
-    const c = core(apiServer({ crd }));
-    const p = probe(c);
-    const r = render(h(c.AmdGpuDataProvider, null, h(p.Probe)));
-    await r.settle();
-    fail = true;
-    r.act(() => p.last().refresh());
-    await r.settle();
-    expect(p.last().crdAvailable).toBe(true);
-    expect(p.last().deviceConfigs).toHaveLength(1);
-  });
-});
-
-describe('AmdGpuDataProvider — degraded RBAC', () => {
-  it('pods forbidden: leaves loading, reports the error, finds operator pods by query', async () => {
-    const request = apiServer({ pluginPods: [makePluginPod('amdgpu-dp-1')] });
-    lib.lists.Node = [[makeGpuNode('mi355x-0')], null];
-    lib.lists.Pod = [null, new Error('pods is forbidden')];
-    const c = core(request);
-    const p = probe(c);
-    const r = render(h(c.AmdGpuDataProvider, null, h(p.Probe)));
-    await r.settle();
-    expect(p.last().loading).toBe(false);
-    expect(p.last().error).toContain('pods is forbidden');
-    expect(p.last().pluginPods.map((x) => x.metadata.name)).toEqual(['amdgpu-dp-1']);
-    PLUGIN_POD_QUERIES.forEach((q) => expect(request.mock.calls.map((x) => x[0])).toContain(q));
-  });
-
-  it('nodes forbidden: leaves loading with no GPU nodes and the error', async () => {
-    lib.lists.Node = [null, new Error('nodes is forbidden')];
-    lib.lists.Pod = [[makeGpuPod('train-a')], null];
-    const c = core(apiServer());
-    const p = probe(c);
-    const r = render(h(c.AmdGpuDataProvider, null, h(p.Probe)));
-    await r.settle();
-    expect(p.last().loading).toBe(false);
-    expect(p.last().gpuNodes).toEqual([]);
-    expect(p.last().error).toContain('nodes is forbidden');
-  });
-
-  it('both forbidden: leaves loading and reports both errors', async () => {
-    lib.lists.Node = [null, 'nodes is forbidden'];
-    lib.lists.Pod = [null, 'pods is forbidden'];
-    const c = core(apiServer());
-    const p = probe(c);
-    const r = render(h(c.AmdGpuDataProvider, null, h(p.Probe)));
-    await r.settle();
-    expect(p.last().loading).toBe(false);
-    expect(p.last().error).toContain('nodes is forbidden');
-    expect(p.last().error).toContain('pods is forbidden');
-  });
-});
-
-describe('metrics hooks', () => {
+describe('metrics hooks — auto-refresh back-off', () => {
   function metricsProbe(useHook) {
     const seen = [];
     function M() {
       const m = useHook();
       seen.push(m);
-      return h('div', null, m.fetching ? 'fetching' : m.fetchError || (m.metrics ? 'gpus=' + m.metrics.gpus.length : 'idle'));
+      return h('div', null, m.fetching ? 'fetching' : m.fetchError || 'idle');
     }
     return { M, seen, last: () => seen[seen.length - 1] };
   }
-
-  it('useGpuMetrics: Prometheus unreachable → the reference error text', async () => {
-    const request = apiServer({ prom: () => Promise.reject(new Error('503')) });
-    const c = core(request);
-    const mp = metricsProbe(() => c.useGpuMetrics(true, false));
-    const r = render(h(mp.M));
-    expect(mp.seen[mp.seen.length - 1].fetching).toBe(true);
-    await r.settle();
-    expect(mp.last().fetching).toBe(false);
-    expect(mp.last().fetchError).toBe(PROMETHEUS_UNREACHABLE);
-    expect(r.text()).toBe(PROMETHEUS_UNREACHABLE);
-  });
 
   for (const [why, fail, text] of [
     ['unreachable', () => Promise.reject(new Error('503')), PROMETHEUS_UNREACHABLE],
@@ -391,122 +148,27 @@ describe('metrics hooks', () => {
     r.unmount();
   });
   }
-
-  it('useGpuMetrics: exporter reachable → per-GPU metrics and series', async () => {
-    const request = apiServer({ prom: prom() });
-    const c = core(request);
-    const mp = metricsProbe(() => c.useGpuMetrics(true, true));
-    const r = render(h(mp.M));
-    await r.settle();
-    expect(mp.last().fetchError).toBeNull();
-    expect(mp.last().metrics.gpus).toHaveLength(8);
-    expect(mp.last().series.power.n0.length).toBeGreaterThan(1);
-    expect(request.mock.calls.every((x) => x[0].indexOf(BASE0) === 0)).toBe(true);
-  });
-
-  it('useGpuMetrics: refresh() fetches again; discovery is cached', async () => {
-    const request = apiServer({ prom: prom() });
-    const c = core(request);
-    const mp = metricsProbe(() => c.useGpuMetrics(true, false));
-    const r = render(h(mp.M));
-    await r.settle();
-    const n = request.mock.calls.length;
-    const probes = () => request.mock.calls.filter((x) => x[0].indexOf('query=1') >= 0).length;
-    const p0 = probes();
-    r.act(() => mp.last().refresh());
-    await r.settle();
-    expect(request.mock.calls.length).toBeGreaterThan(n);
-    expect(probes()).toBe(p0);
-  });
-
-  it('useNodeGpuMetrics(null) fetches nothing', async () => {
-    const request = apiServer({ prom: prom() });
-    const c = core(request);
-    const mp = metricsProbe(() => c.useNodeGpuMetrics(null, true));
-    const r = render(h(mp.M));
-    await r.settle();
-    expect(request).not.toHaveBeenCalled();
-    expect(r.text()).toBe('idle');
-  });
-
-  it('useNodeGpuMetrics(node) reads one node through a hostname-scoped query', async () => {
-    const request = apiServer({ prom: prom() });
-    const c = core(request);
-    const mp = metricsProbe(() => c.useNodeGpuMetrics('n0', true));
-    const r = render(h(mp.M));
-    await r.settle();
-    expect(mp.last().metrics.gpus).toHaveLength(8);
-    const scoped = request.mock.calls.filter((x) => decodeURIComponent(x[0]).indexOf('hostname="n0"') >= 0);
-    expect(scoped.length).toBeGreaterThan(0);
-  });
-
-  it('switching node while a fetch is in flight drops the old answer', async () => {
-    let release;
-    const gate = new Promise((res) => (release = res));
-    const inner = prom({ data: exporterData(['n0', 'n1']) });
-    const slow = (path) => decodeURIComponent(path).indexOf('hostname="n0"') >= 0;
-    const request = apiServer({ prom: (path) => (slow(path) ? gate.then(() => inner(path)) : inner(path)) });
-    const c = core(request);
-    let node = 'n0';
-    const mp = metricsProbe(() => c.useNodeGpuMetrics(node, true));
-    const r = render(h(mp.M));
-    await r.settle();
-    node = 'n1';
-    r.rerender(h(mp.M));
-    await r.settle();
-    expect(mp.last().metrics.gpus[0].nodeName).toBe('n1');
-    release();
-    await r.settle();
-    expect(mp.last().metrics.gpus.every((g) => g.nodeName === 'n1')).toBe(true);
-  });
-
-  it('useGpuOwners fetches pod attribution only', async () => {
-    const request = apiServer({ prom: prom() });
-    const c = core(request);
-    const mp = metricsProbe(() => c.useGpuOwners());
-    const r = render(h(mp.M));
-    await r.settle();
-    expect(mp.last().fetchError).toBeNull();
-    const qs = request.mock.calls.map((x) => decodeURIComponent(x[0])).filter((q) => q.indexOf('query=') >= 0 && q.indexOf('query=1') < 0);
-    expect(qs.length).toBeGreaterThan(0);
-    qs.forEach((q) => expect(q).toContain('pod!=""'));
-  });
 });
 
-describe('useNodePods (cold Node detail)', () => {
-  function nodePodsServer(pods) {
-    return vi.fn((path) => {
-      const m = /^\/api\/v1\/pods\?fieldSelector=(.*)$/.exec(path);
-      if (!m) return notFound();
-      const node = decodeURIComponent(m[1]).replace(/^spec\.nodeName=/, '');
-      return Promise.resolve(kubeList(pods().filter((p) => p.spec.nodeName === node)));
-    });
-  }
-  function Section(c, node) {
-    return function S() {
-      const r = c.useNodePods(node, true);
-      return h('div', null, r.loading ? 'loading' : r.podsState + ':' + r.gpuPods.map((p) => p.metadata.name).join(','));
-    };
-  }
-
-  it('one field-selected request for the node, GPU pods only', async () => {
-    const request = nodePodsServer(() => [makeGpuPod('a', { node: 'n1' }), makeGpuPod('b', { node: 'n2' }), makePlainPod('web')]);
-    const r = render(h(Section(core(request), 'n1')));
-    expect(r.text()).toBe('loading');
-    await r.settle();
-    expect(r.text()).toBe('ready:a');
-    expect(request.mock.calls.map((c) => c[0])).toEqual(['/api/v1/pods?fieldSelector=' + encodeURIComponent('spec.nodeName=n1')]);
-    r.unmount();
-  });
-
+describe('useNodePods (cold Node detail) — auto-refresh', () => {
   it('re-reads the node\'s pods each auto-refresh period and keeps them through a failed re-read', async () => {
     vi.useFakeTimers();
     settings.refreshIntervalSec = 15;
     let pods = [makeGpuPod('a', { node: 'n1' })];
     let fail = false;
-    const ok = nodePodsServer(() => pods);
-    const request = vi.fn((p) => (fail ? Promise.reject(Object.assign(new Error('503'), { status: 503 })) : ok(p)));
-    const r = render(h(Section(core(request), 'n1')));
+    const request = vi.fn((path) => {
+      if (fail) return Promise.reject(Object.assign(new Error('503'), { status: 503 }));
+      const m = /^\/api\/v1\/pods\?fieldSelector=(.*)$/.exec(path);
+      if (!m) return notFound();
+      const node = decodeURIComponent(m[1]).replace(/^spec\.nodeName=/, '');
+      return Promise.resolve(kubeList(pods.filter((p) => p.spec.nodeName === node)));
+    });
+    const c = core(request);
+    function S() {
+      const res = c.useNodePods('n1', true);
+      return h('div', null, res.loading ? 'loading' : res.podsState + ':' + res.gpuPods.map((p) => p.metadata.name).join(','));
+    }
+    const r = render(h(S));
     await r.settle();
     expect(r.text()).toBe('ready:a');
     pods = [makeGpuPod('a', { node: 'n1' }), makeGpuPod('c', { node: 'n1' })];
@@ -518,14 +180,6 @@ describe('useNodePods (cold Node detail)', () => {
     await r.settle();
     expect(r.text()).toBe('ready:a,c');
     expect(request.mock.calls.length).toBe(3);
-    r.unmount();
-  });
-
-  it('a first failure says the pods are unreadable', async () => {
-    const request = vi.fn(() => Promise.reject(Object.assign(new Error('pods is forbidden'), { status: 403 })));
-    const r = render(h(Section(core(request), 'n1')));
-    await r.settle();
-    expect(r.text()).toBe('error:');
     r.unmount();
   });
 });
