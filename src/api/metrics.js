@@ -931,6 +931,7 @@ export function createMetricsSource(opts) {
       st.failures++;
       if (st.last && st.failures < STALE_FAILURES) return Object.assign({}, st.last, { stale: true });
       st.last = null;
+      invalidate(); // as the cluster-wide path: Prometheus is re-discovered next time
       return null;
     }).then(function (r) { return r === NOT_SCOPED ? clusterCut(v, scope, summary, key) : r; });
   }
@@ -1128,6 +1129,7 @@ export function createMetricsSource(opts) {
       st.failures++;
       if (st.last && st.failures < STALE_FAILURES) return Object.assign({}, st.last, { stale: true });
       st.last = null;
+      invalidate(); // as the cluster-wide path: Prometheus is re-discovered next time
       return null;
     }).then(function (r) { return r === NOT_SCOPED ? clusterWide() : r; });
   }
@@ -1174,6 +1176,7 @@ export function createMetricsSource(opts) {
       ownersFailures++;
       if (ownersLast && ownersFailures < STALE_FAILURES) return Object.assign({}, ownersLast, { stale: true });
       ownersLast = null;
+      invalidate();
       return null;
     });
   }

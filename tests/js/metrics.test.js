@@ -29,6 +29,7 @@ import {
   nodePowerQuery,
   podPowerQuery,
   splitByName,
+  STALE_FAILURES,
 } from '../../src/api/metrics.js';
 
 import { BASE0, BASE1, exporterData, ok, prom, vec } from './promFake.js';
@@ -158,6 +159,27 @@ describe('fetchGpuMetrics', () => {
     const d = await src.fetchGpuMetrics();
     expect(d.stale).toBeUndefined();
     expect(d.gpus.length).toBe(a.gpus.length);
+  });
+  it('paged, node and owner fetches re-discover a Prometheus that moved, once they report it unreachable', async () => {
+    const fetches = {
+      paged: (src) => src.fetchGpuMetrics('gauges', { scope: ['n0'], summary: true }),
+      node: (src) => src.fetchNodeMetrics('n0'),
+      owners: (src) => src.fetchGpuOwners({ pods: ['ml/train-0'] }),
+    };
+    for (const name of Object.keys(fetches)) {
+      const fetch = fetches[name];
+      let at = BASE0;
+      const inner = prom({ up: [BASE0, BASE1], data: exporterData(['n0']) });
+      const request = vi.fn((path) => (path.indexOf(at) === 0 ? inner(path) : Promise.reject(Object.assign(new Error('503'), { status: 503 }))));
+      const src = createMetricsSource({ request });
+      expect((await fetch(src)).prometheusPath).toBe(BASE0);
+      at = BASE1; // the service moved
+      let r;
+      for (let i = 0; i < STALE_FAILURES; i++) r = await fetch(src);
+      expect(r).toBeNull();
+      r = await fetch(src);
+      expect(r === null ? name + ': still unreachable' : r.prometheusPath).toBe(BASE1);
+    }
   });
   it('reuses unchanged GPU objects and maps across refreshes (structural sharing)', async () => {
     const d = exporterData(['n0', 'n1']);
