@@ -10,6 +10,9 @@ Round 2's GPU tests checked ranges (10 < W < 2000, > 280 GB). These compare valu
 * RAS: ``gpu_ecc_{correct,uncorrect,deferred}_total`` equal the sums over ``ras/aca_*`` (legacy ``*_err_count``
   when there is no ``aca_*`` file) read before and after — counters only grow, so the scrape lies between them;
 * HBM in use: ``gpu_used_vram`` lies between two direct ``mem_info_vram_used`` reads bracketing the scrape (±1 MiB);
+* temperatures: junction / memory within 3 °C of the hwmon sensors of that label read around the scrape, and the
+  slowdown / shutdown limits equal their ``temp*_crit`` / ``temp*_emergency`` files;
+* clocks: ``gpu_clock`` / ``gpu_memory_clock`` equal hwmon ``freq1_input`` / ``freq2_input`` when the level held;
 * ``probe.sample()`` (the in-process path) answers in well under a millisecond-scale budget.
 """
 import glob
@@ -146,6 +149,74 @@ def test_hbm_in_use_between_two_direct_reads(exe, dev):
     got = _value(rows, "gpu_used_vram", info["bdf"]) * MIB
     # %.6g keeps 6 significant digits of the MiB count: < 1 MiB below 1 TiB
     assert min(before, after) - MIB <= got <= max(before, after) + MIB, (before, got, after)
+
+
+def _temps(d):
+    """hwmon temperatures by label (m°C → °C): {label: (input, crit, emergency)}."""
+    out = {}
+    for h in sorted(glob.glob(f"{d}/hwmon/hwmon*")):
+        for t in range(1, 5):
+            base = f"{h}/temp{t}"
+            if not os.path.exists(base + "_input"):
+                continue
+            label = _read(base + "_label") if os.path.exists(base + "_label") else f"temp{t}"
+            vals = []
+            for suffix in ("_input", "_crit", "_emergency"):
+                try:
+                    vals.append(float(_read(base + suffix)) / 1000.0)
+                except (OSError, ValueError):
+                    vals.append(None)
+            out.setdefault(label, tuple(vals))
+    return out
+
+
+def test_temperatures_and_thermal_limits_match_hwmon(exe, dev):
+    info, d = dev
+    before = _temps(d)
+    rows = _scrape(exe)
+    after = _temps(d)
+    junction = before.get("junction") or before.get("hotspot")
+    if junction is None or "mem" not in before:
+        pytest.skip(f"hwmon exposes {sorted(before)}, no junction / mem sensors")
+    checked = 0
+    for label, name, slow, shut in (("junction", "gpu_junction_temperature", "gpu_junction_temperature_slowdown",
+                                     "gpu_junction_temperature_shutdown"),
+                                    ("mem", "gpu_memory_temperature", "gpu_memory_temperature_slowdown", None)):
+        key = label if label in before else "hotspot"
+        lo = min(before[key][0], after[key][0]) - 3.0
+        hi = max(before[key][0], after[key][0]) + 3.0
+        got = _value(rows, name, info["bdf"])
+        assert lo <= got <= hi, (name, before[key], got, after[key])
+        if before[key][1] is not None:
+            assert _value(rows, slow, info["bdf"]) == pytest.approx(before[key][1])
+            checked += 1
+        if shut and before[key][2] is not None:
+            assert _value(rows, shut, info["bdf"]) == pytest.approx(before[key][2])
+            checked += 1
+        checked += 1
+    print(f"temperatures: hwmon {before}, {checked} exporter values equal")
+
+
+def test_clocks_match_hwmon(exe, dev):
+    info, d = dev
+    f1 = [_hwmon(d, "freq1_input")]
+    f2 = [_hwmon(d, "freq2_input")]
+    if f1[0] is None and f2[0] is None:
+        pytest.skip("no hwmon clock files")
+    rows = _scrape(exe)
+    f1.append(_hwmon(d, "freq1_input"))
+    f2.append(_hwmon(d, "freq2_input"))
+    for name, pair in (("gpu_clock", f1), ("gpu_memory_clock", f2)):
+        if pair[0] is None:
+            continue
+        got = _value(rows, name, info["bdf"])
+        if pair[0] == pair[1]:
+            # Hz → MHz, exact while the clock holds its DPM level across the scrape (the memory clock does)
+            assert got == pytest.approx(pair[0] / 1e6, rel=1e-5), (name, pair, got)
+        else:
+            # the shader clock hops between DPM levels; the scrape saw one of them
+            assert 0 < got <= 1.5 * max(pair) / 1e6, (name, pair, got)
+    print(f"clocks: sclk hwmon {f1} Hz, mclk hwmon {f2} Hz")
 
 
 def test_probe_sample_matches_sysfs_and_is_fast(dev):
