@@ -322,14 +322,37 @@ function amdSchedule(request, clock) {
       mstate.fetchError = r[0] ? null : 'Could not reach Prometheus';
     });
   }
-  /** What the page's hook asks for once the node list is there (pages.js telemetryScope). */
+  /**
+   * What the page's hook asks for now (pages.js telemetryScope): its query
+   * key (null = disabled) and fetch options. While the node list loads, and
+   * while every GPU node fits on one page, that is the size-guarded
+   * small-cluster query under one key.
+   */
   function scoped(summary) {
     const t = telemetryScope(store.getSnapshot(), PAGER);
-    return t.scope === undefined ? { opts: undefined, scope: undefined } : { opts: { scope: t.scope, summary: summary }, scope: t.scope };
+    const key = !t.enabled ? null : t.scope === undefined ? 'all' : t.small ? 'small' : 'scope:' + t.scope.join(',');
+    return t.scope === undefined ? { key: key, opts: undefined, scope: undefined, small: false }
+      : { key: key, opts: { scope: t.scope, summary: summary, small: !!t.small }, scope: t.scope, small: !!t.small };
   }
-  /** Resolves when the store's snapshot has the node list (or its error). */
-  function nodesListed() {
-    return listed('nodesState');
+  function ownersKey() {
+    const o = ownersScope(store.getSnapshot(), PAGER);
+    return !o.enabled ? null : o.pods === undefined ? 'all' : o.small ? 'small' : 'pods:' + o.pods.join(',');
+  }
+  /**
+   * A page's metrics hook from mount to the lists: it fetches under the key
+   * of its first render and again only if the lists change that key (a
+   * larger cluster's first page), as useMetricsFetch does.
+   */
+  function pageOpen(page) {
+    const keyOf = page === 'pods' ? ownersKey : function () { return scoped(false).key; };
+    const fetch = page === 'pods' ? fetchPodsPage : page === 'nodes' ? fetchNodesPage : fetchMetricsPage;
+    const k0 = keyOf();
+    const first = k0 === null ? Promise.resolve() : fetch();
+    const second = listed(page === 'pods' ? 'podsState' : 'nodesState').then(function () {
+      const k1 = keyOf();
+      return k1 !== null && k1 !== k0 ? fetch() : first;
+    });
+    return Promise.all([first, second]);
   }
   function listed(which) {
     return new Promise(function (resolve) {
@@ -348,14 +371,14 @@ function amdSchedule(request, clock) {
   }
   function fetchPodsPage() {
     const o = ownersScope(store.getSnapshot(), PAGER);
-    return metrics.fetchGpuOwners(o.pods === undefined ? undefined : { pods: o.pods }).then(function (m) { pageMetrics.pods = m; });
+    return metrics.fetchGpuOwners(o.pods === undefined ? undefined : { pods: o.pods, small: !!o.small }).then(function (m) { pageMetrics.pods = m; });
   }
   function fetchNodesPage() {
     return metrics.fetchGpuMetrics('topology', scoped(false).opts).then(function (m) { pageMetrics.nodes = m; });
   }
   function fetchMetricsPage() {
     const sc = scoped(true);
-    return Promise.all([metrics.fetchGpuMetrics('gauges', sc.opts), metrics.fetchSeries(1800, 30, sc.scope)]).then(function (r) {
+    return Promise.all([metrics.fetchGpuMetrics('gauges', sc.opts), metrics.fetchSeries(1800, 30, sc.scope, sc.small)]).then(function (r) {
       metricsPage.metrics = r[0];
       metricsPage.series = r[1];
       metricsPage.fetchError = r[0] ? null : 'Could not reach Prometheus';
@@ -363,15 +386,13 @@ function amdSchedule(request, clock) {
   }
   return {
     /**
-     * Every page's data at once, as each page fetches it: the lists and the
-     * DeviceConfig in one wave; GPU Nodes / Metrics / GPU Pods telemetry of
-     * their first pages once the node (pod) list is in.
+     * Every page's data at once, as each page fetches it: the lists, the
+     * DeviceConfig and the pages' size-guarded telemetry in one wave; on a
+     * cluster larger than one page, GPU Nodes / Metrics / GPU Pods telemetry
+     * of their first pages once the node (pod) list is in.
      */
     coldOpen: function () {
-      return Promise.all([
-        store.loadLists(), store.refresh(), nodesListed().then(fetchNodesPage), nodesListed().then(fetchMetricsPage),
-        listed('podsState').then(fetchPodsPage),
-      ]);
+      return Promise.all([store.loadLists(), store.refresh(), pageOpen('nodes'), pageOpen('metrics'), pageOpen('pods')]);
     },
     /** Composite refresh: every page's Refresh in one wave (5 requests, within the 6 browser sockets). */
     refresh: function () {
@@ -390,23 +411,21 @@ function amdSchedule(request, clock) {
     },
     /**
      * One page opened on an empty cache, as src/plugin.js mounts it: the
-     * provider's lists + DeviceConfig request in one wave; GPU Nodes and
-     * Metrics ask for the telemetry of their first page of nodes once the
-     * node list is there, GPU Pods for the owners of its first page of pods
-     * once the pod list is there (a second wave).
+     * provider's lists + DeviceConfig request and the page's size-guarded
+     * telemetry in one wave — all of it on a cluster of one page; a larger
+     * cluster's GPU Nodes / Metrics (GPU Pods) ask for their first page of
+     * nodes (pods) once the node (pod) list is there (a second wave).
      */
     coldOpenPage: function (page, onContent) {
       // The provider's data (lists + DeviceConfig): the page renders
       // everything the reference's page shows once it is in.
-      // (Not on Metrics: there the content IS the telemetry, second wave.)
+      // (Not on Metrics: there the content IS the telemetry.)
       const content = Promise.all([store.loadLists(), store.refresh()]).then(function () {
         if (onContent && page !== 'metrics') onContent();
       });
-      // The page's metrics hook is enabled once the node list is in
-      // (pages.js telemetryScope): it re-runs on the snapshot that carries it.
-      if (page === 'nodes') return Promise.all([content, nodesListed().then(fetchNodesPage)]);
-      if (page === 'metrics') return Promise.all([content, nodesListed().then(fetchMetricsPage)]);
-      if (page === 'pods') return Promise.all([content, listed('podsState').then(fetchPodsPage)]);
+      // The page's metrics hook runs from the first render (pages.js
+      // telemetryScope) and once more if the node list changes its key.
+      if (page === 'nodes' || page === 'metrics' || page === 'pods') return Promise.all([content, pageOpen(page)]);
       return content;
     },
     pageMetrics: function (page) { return page in pageMetrics && pageMetrics[page] ? pageMetrics[page] : mstate.metrics; },

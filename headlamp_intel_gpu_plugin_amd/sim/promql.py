@@ -688,6 +688,19 @@ class Evaluator:
 
     def _binary(self, node, t):
         _, op, lhs, rhs, matching = node
+        if op == "and":
+            # `x and <empty>` is empty whatever x is: answered without evaluating x.
+            # Prometheus evaluates both sides, on its own cores and in parallel
+            # with other queries; this server's one event loop would instead
+            # hold every other request behind a cluster-wide evaluation (the
+            # client's size-guarded queries, metrics.js sizeGuard).
+            rt, rv = self.instant(rhs, t)
+            if rt == "vector" and not rv:
+                return ("vector", [])
+            lt, lv = self.instant(lhs, t)
+            if lt != "vector" or rt != "vector":
+                raise PromQLError(f"set operator {op} needs vectors on both sides")
+            return self._set_op(op, lv, rv, matching)
         lt, lv = self.instant(lhs, t)
         rt, rv = self.instant(rhs, t)
         if op in SET_OPS:

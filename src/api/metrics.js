@@ -84,6 +84,14 @@ export const SERIES = {
 export const DISCOVERY_TTL_MS = 5 * 60 * 1000;
 /** Consecutive failed metrics fetches before the page switches to "Prometheus Unreachable". */
 export const STALE_FAILURES = 3;
+/**
+ * GPUs (power gauges) up to which a paged view asks for the whole cluster
+ * instead of its page: one page of MI355X nodes (8 × 8). The guard is
+ * evaluated by Prometheus inside the same request (smallClusterQuery), so a
+ * page opened while the node list is still loading needs no second wave on
+ * a small cluster, and a large one gets nothing it did not ask for.
+ */
+export const SMALL_CLUSTER_GPUS = 64;
 
 /**
  * @typedef {Object} GpuTelemetry
@@ -380,6 +388,37 @@ export function hostnameMatcher(names) {
   return 'hostname=~"' + promString(names.map(regexLiteral).join('|')) + '"';
 }
 
+/**
+ * `q` when the cluster has at most SMALL_CLUSTER_GPUS power gauges (`small`),
+ * or when it has more (`!small`): `and on()` against a one-sample count keeps
+ * all of `q` or none of it, decided by Prometheus in the same evaluation.
+ */
+export function sizeGuard(q, small) {
+  return '(' + q + ') and on() (count({__name__="' + SERIES.exporter.power + '"}) ' + (small ? '<=' : '>') + ' ' +
+    SMALL_CLUSTER_GPUS + ')';
+}
+
+/**
+ * A paged view's telemetry while its page may be the whole cluster (the node
+ * list is loading, or every GPU node fits on one page): every GPU when the
+ * cluster is small, else the nodes of `scope` — one request either way, and
+ * none waits for the node list on a small cluster.
+ */
+export function smallClusterQuery(withStatic, view, scope) {
+  const all = sizeGuard(exporterQuery(withStatic, false, view), true);
+  // The GPU count itself: tells a large cluster (nothing asked for yet) from one without exporter series.
+  const count = 'label_replace(count({__name__="' + SERIES.exporter.power + '"}), "agg", "gpus", "", "")';
+  return (scope.length ? all + ' or ' + sizeGuard(exporterQuery(withStatic, true, view, scope), false) : all) + ' or ' + count;
+}
+
+/** The `agg="gpus"` row of a smallClusterQuery answer: power gauges in the cluster (0 when absent). */
+export function gpuCountFromRows(rows) {
+  for (let i = 0; i < rows.length; i++) {
+    if (isRow(rows[i]) && rows[i].metric.agg === 'gpus') return num(rows[i].value[1]) || 0;
+  }
+  return 0;
+}
+
 /** Exporter series the cluster totals of the Metrics page summary sum or count. */
 function summaryNames() {
   const E = SERIES.exporter;
@@ -489,8 +528,13 @@ export function exporterNodeQuery(nodeName, withStatic) {
  * `pod` label is set — one series per allocated GPU, instead of every live
  * gauge and xGMI link of every GPU.
  */
-export function ownersQuery(pods) {
+export function ownersQuery(pods, small) {
   const sel = '{__name__="' + SERIES.exporter.power + '", ';
+  if (small) {
+    // Every allocated GPU of a small cluster, else the page's pods (smallClusterQuery).
+    const all = sizeGuard(ownersQuery(null), true);
+    return pods && pods.length ? all + ' or ' + sizeGuard(ownersQuery(pods), false) : all;
+  }
   if (!pods) return 'max by (' + EXPORTER_JOIN_LABELS.join(', ') + ') (' + sel + 'pod!=""})';
   // The pods of one page of the Pods table ("namespace/name" keys): O(page).
   const names = {};
@@ -571,11 +615,17 @@ export function seriesQuery() {
  * plus the cluster-wide total (tagged `scope="cluster"`): O(visible nodes ×
  * points) whatever the cluster size.
  */
-export function scopedSeriesQuery(scope) {
+export function scopedSeriesQuery(scope, small) {
   const E = SERIES.exporter;
   const names = '__name__=~"' + E.power + '|' + E.vramUsed + '"';
-  return 'sum by (__name__, hostname) ({' + names + ', ' + hostnameMatcher(scope) + '})' +
-    ' or label_replace(sum by (__name__) ({' + names + '}), "scope", "cluster", "", "")';
+  const page = 'sum by (__name__, hostname) ({' + names + ', ' + hostnameMatcher(scope) + '})';
+  const total = 'label_replace(sum by (__name__) ({' + names + '}), "scope", "cluster", "", "")';
+  if (small) {
+    // Every node's line on a small cluster, else the page's (smallClusterQuery).
+    const all = sizeGuard(seriesQuery(), true);
+    return (scope.length ? all + ' or ' + sizeGuard(page, false) : all) + ' or ' + total;
+  }
+  return page + ' or ' + total;
 }
 
 /** Key of the cluster-wide line in a scoped series answer (no node name can be this). */
@@ -830,8 +880,9 @@ export function createMetricsSource(opts) {
     const scope = opts && Array.isArray(opts.scope) ? opts.scope.map(String) : null;
     if (!scope) return shared('gpus|' + v, function () { return gpuSnapshot(v); });
     const summary = !!opts.summary;
-    const key = v + '|' + (summary ? 'sum' : '') + '|' + scope.join(',');
-    return shared('scoped|' + key, function () { return scopedSnapshot(v, scope, summary, key); });
+    const small = !!opts.small;
+    const key = v + '|' + (summary ? 'sum' : '') + '|' + (small ? 'small|' : '') + scope.join(',');
+    return shared('scoped|' + key, function () { return scopedSnapshot(v, scope, summary, key, small); });
   }
 
   // ---- Scoped snapshots (paged views: the GPU nodes on screen) -------------
@@ -873,14 +924,19 @@ export function createMetricsSource(opts) {
    * first query that finds no exporter series falls back to the cluster-wide
    * snapshot cut to the scope. Stale / null handling as in the cluster-wide
    * path, per scope.
+   *
+   * `small`: the page may be the whole cluster (smallClusterQuery) — every
+   * GPU when the cluster has at most SMALL_CLUSTER_GPUS, else `scope`'s.
    */
-  function scopedSnapshot(v, scope, summary, key) {
+  function scopedSnapshot(v, scope, summary, key, small) {
     const st = scopedEntry(key);
     if (source === 'node-exporter') return clusterCut(v, scope, summary, key);
     return withPrometheus(function (base) {
-      const withStatic = scope.length > 0 && scopeNeedsStatic(scope);
+      // Nothing cached yet for a small-cluster fetch before the node list: statics too.
+      const withStatic = small && scope.length === 0 ? true : scope.length > 0 && scopeNeedsStatic(scope);
       const parts = [];
-      if (scope.length) parts.push(exporterQuery(withStatic, true, v, scope));
+      if (small) parts.push(smallClusterQuery(withStatic, v, scope));
+      else if (scope.length) parts.push(exporterQuery(withStatic, true, v, scope));
       if (summary) parts.push(summaryQuery());
       if (!parts.length) return Promise.resolve(scopedResult(st, base, null, { gpus: [], xgmi: {}, links: {} }, scope, undefined, v));
       const q = parts.join(' or ');
@@ -889,8 +945,8 @@ export function createMetricsSource(opts) {
         st.failures = 0;
         const rows = res.rows;
         const j = joinExporterResults(rows);
-        const totals = summary ? totalsFromRows(rows.__agg) : undefined;
-        const found = j.gpus.length > 0 || (!!totals && totals.gpus > 0);
+        const totals = summary ? totalsFromRows(rows.__agg.filter(function (r) { return r.metric.agg !== 'gpus'; })) : undefined;
+        const found = j.gpus.length > 0 || (!!totals && totals.gpus > 0) || (small && gpuCountFromRows(rows.__agg) > 0);
         // Nothing from the exporter yet: maybe node-exporter feeds this
         // Prometheus (no hostname label) — ask cluster-wide to find out, at
         // most once per discovery TTL when that finds no GPU either (a
@@ -1148,6 +1204,8 @@ export function createMetricsSource(opts) {
    */
   function fetchGpuOwners(opts) {
     const pods = opts && Array.isArray(opts.pods) ? opts.pods.map(String) : null;
+    const small = !!(opts && opts.small);
+    if (small) return shared('owners|small|' + (pods || []).join(','), function () { return ownersSnapshot(pods || [], true); });
     if (pods && pods.length === 0) {
       return Promise.resolve({ source: source, gpus: [], xgmi: {}, links: {}, fetchedAt: new Date(clock.now()).toISOString(),
         prometheusPath: cachedPath, scope: 'owners' });
@@ -1155,9 +1213,9 @@ export function createMetricsSource(opts) {
     return shared('owners|' + (pods ? pods.join(',') : '*'), function () { return ownersSnapshot(pods); });
   }
 
-  function ownersSnapshot(pods) {
+  function ownersSnapshot(pods, small) {
     return withPrometheus(function (base) {
-      return combined(base, ownersQuery(pods)).then(function (res) {
+      return combined(base, ownersQuery(pods, small)).then(function (res) {
         if (!res.ok) return UNREACHABLE;
         ownersFailures = 0;
         const j = joinExporterResults(res.rows);
@@ -1219,14 +1277,14 @@ export function createMetricsSource(opts) {
    * are requested — and none at all until the next step boundary.
    * @returns {Promise<{ rangeSec: number, power: Record<string, Array<[number, number]>>, vram: Record<string, Array<[number, number]>> } | null>}
    */
-  function fetchSeries(rangeSec, stepSec, scope) {
+  function fetchSeries(rangeSec, stepSec, scope, small) {
     const range = rangeSec || 1800;
     const step = stepSec || 30;
     const E = SERIES.exporter;
     const parts = [['power', E.power, 1], ['vram', E.vramUsed, SERIES.exporterVramUnitBytes]];
     const scoped = Array.isArray(scope);
-    const sk = scoped ? scope.map(String).join(',') : null;
-    const q = scoped ? scopedSeriesQuery(scope.map(String)) : seriesQuery();
+    const sk = scoped ? (small ? 'small:' : '') + scope.map(String).join(',') : null;
+    const q = scoped ? scopedSeriesQuery(scope.map(String), !!small) : seriesQuery();
     function from(base) {
       const end = Math.floor(clock.now() / 1000 / step) * step;
       const fresh = !seriesCache || seriesCache.range !== range || seriesCache.step !== step ||

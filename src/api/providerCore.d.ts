@@ -37,24 +37,33 @@ export interface ClusterStore {
 }
 
 export interface MetricsSource {
-  /** `scope`: node names of a paged view (hostname=~); `summary`: also the cluster totals (GpuMetrics.totals) */
-  fetchGpuMetrics(view?: 'all' | 'gauges' | 'topology', opts?: { scope: string[]; summary?: boolean }): Promise<GpuMetrics | null>;
+  /**
+   * `scope`: node names of a paged view (hostname=~); `summary`: also the cluster totals (GpuMetrics.totals);
+   * `small`: every GPU when the cluster has at most SMALL_CLUSTER_GPUS, else `scope`'s (one request)
+   */
+  fetchGpuMetrics(view?: 'all' | 'gauges' | 'topology', opts?: { scope: string[]; summary?: boolean; small?: boolean }): Promise<GpuMetrics | null>;
   fetchNodeMetrics(nodeName: string): Promise<GpuMetrics | null>;
-  /** `pods`: "namespace/name" keys of one page of the Pods table */
-  fetchGpuOwners(opts?: { pods: string[] }): Promise<GpuMetrics | null>;
+  /** `pods`: "namespace/name" keys of one page of the Pods table; `small` as in fetchGpuMetrics */
+  fetchGpuOwners(opts?: { pods: string[]; small?: boolean }): Promise<GpuMetrics | null>;
   failureReason(): 'forbidden' | 'unreachable';
   fetchPodSeries(namespace: string, pod: string, rangeSec: number, stepSec: number): Promise<{ rangeSec: number; stepSec: number; power: Array<[number, number]> } | null>;
   fetchNodeSeries(nodeName: string, rangeSec: number, stepSec: number): Promise<{ rangeSec: number; stepSec: number; power: Array<[number, number]> } | null>;
-  fetchSeries(rangeSec: number, stepSec: number, scope?: string[]): Promise<GpuMetricsState['series']>;
+  fetchSeries(rangeSec: number, stepSec: number, scope?: string[], small?: boolean): Promise<GpuMetricsState['series']>;
 }
 
 export interface ProviderCore {
   Context: Context<AmdGpuContextValue | null>;
   AmdGpuDataProvider: ComponentType<{ children?: ReactNode }>;
   useAmdGpuContext(): AmdGpuContextValue;
-  useGpuMetrics(enabled?: boolean, withSeries?: boolean, view?: 'all' | 'gauges' | 'topology', scope?: string[]): GpuMetricsState;
+  useGpuMetrics(
+    enabled?: boolean,
+    withSeries?: boolean,
+    view?: 'all' | 'gauges' | 'topology',
+    scope?: string[],
+    small?: boolean
+  ): GpuMetricsState;
   useNodeGpuMetrics(nodeName: string | null, enabled?: boolean): GpuMetricsState;
-  useGpuOwners(enabled?: boolean, pods?: string[]): GpuMetricsState;
+  useGpuOwners(enabled?: boolean, pods?: string[], small?: boolean): GpuMetricsState;
   usePodGpuSeries(namespace: string | null, pod: string | null, enabled?: boolean): GpuMetricsState;
   useNodeGpuSeries(nodeName: string | null, enabled?: boolean): GpuMetricsState;
   /** One node's pods for a Node detail section on a cold store (one field-selected request) */

@@ -251,12 +251,17 @@ export function createProviderCore(React, lib, deps) {
    * server-side aggregates — O(page) bytes on any cluster. Without `scope`
    * the whole cluster is fetched (terminal client, small clusters).
    *
+   * `small` (pages.js telemetryScope): the page may be the whole cluster —
+   * every GPU when the cluster is small, else `scope`'s nodes, decided by
+   * Prometheus (metrics.js smallClusterQuery). The query key then leaves out
+   * the names, so the node list arriving does not refetch; a refresh asks
+   * with the names of that render.
+   *
    * Unlike the reference it does not wait for the cluster context to finish
    * loading (MetricsPage.tsx:203-205): the two are independent and fetched in
-   * parallel (with a scope, the page's node names come from the node list;
-   * an empty scope still fetches the totals).
+   * parallel.
    */
-  function useGpuMetrics(enabled, withSeries, view, scope) {
+  function useGpuMetrics(enabled, withSeries, view, scope, small) {
     const on = enabled === undefined ? true : enabled;
     const series = withSeries === undefined ? true : withSeries;
     const v = view || 'all';
@@ -265,13 +270,14 @@ export function createProviderCore(React, lib, deps) {
     const settings = loadSettings();
     const scoped = Array.isArray(scope);
     const names = scoped ? scope.slice() : null;
+    const sm = scoped && !!small;
     const key = 'gpus|' + sourceKey(cluster, settings) + '|' + v + '|' + series + '|' + settings.seriesMinutes +
-      (scoped ? '|scope:' + names.join(',') : '');
+      (sm ? '|small' : scoped ? '|scope:' + names.join(',') : '');
     return useMetricsFetch(on ? key : null, function () {
-      const opts = scoped ? { scope: names, summary: v === 'gauges' } : undefined;
+      const opts = scoped ? { scope: names, summary: v === 'gauges', small: sm } : undefined;
       return Promise.all([
         source.fetchGpuMetrics(v, opts),
-        series ? source.fetchSeries(settings.seriesMinutes * 60, seriesStepSec(settings), names || undefined) : Promise.resolve(null),
+        series ? source.fetchSeries(settings.seriesMinutes * 60, seriesStepSec(settings), names || undefined, sm) : Promise.resolve(null),
       ]);
     }, false, source);
   }
@@ -384,17 +390,19 @@ export function createProviderCore(React, lib, deps) {
   /**
    * Pod → GPU attribution for the Pods page (metrics.js fetchGpuOwners): one
    * series per allocated GPU — of the pods on the page when `pods` (their
-   * "namespace/name" keys) is given, else of every pod.
+   * "namespace/name" keys) is given, else of every pod; `small` as in
+   * useGpuMetrics (pages.js ownersScope).
    */
-  function useGpuOwners(enabled, pods) {
+  function useGpuOwners(enabled, pods, small) {
     const cluster = clusterKey();
     const source = metricsSourceFor(cluster);
     const on = enabled === undefined ? true : enabled;
     const scoped = Array.isArray(pods);
     const keys = scoped ? pods.slice() : null;
-    const key = 'owners|' + sourceKey(cluster, loadSettings()) + (scoped ? '|pods:' + keys.join(',') : '');
+    const sm = scoped && !!small;
+    const key = 'owners|' + sourceKey(cluster, loadSettings()) + (sm ? '|small' : scoped ? '|pods:' + keys.join(',') : '');
     return useMetricsFetch(on ? key : null, function () {
-      return source.fetchGpuOwners(scoped ? { pods: keys } : undefined).then(function (m) { return [m, null]; });
+      return source.fetchGpuOwners(scoped ? { pods: keys, small: sm } : undefined).then(function (m) { return [m, null]; });
     }, false, source);
   }
 

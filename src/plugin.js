@@ -100,7 +100,7 @@ export function createPlugin(env) {
     const ctx = core.useAmdGpuContext();
     const pager = usePager();
     const t = telemetryScope(ctx, pager.state);
-    const m = core.useGpuMetrics(t.enabled, false, 'topology', t.scope);
+    const m = core.useGpuMetrics(t.enabled, false, 'topology', t.scope, t.small);
     function refresh() {
       ctx.refresh();
       m.refresh();
@@ -121,7 +121,7 @@ export function createPlugin(env) {
     const ctx = core.useAmdGpuContext();
     const pager = usePager();
     const o = ownersScope(ctx, pager.state);
-    const m = core.useGpuOwners(o.enabled, o.pods);
+    const m = core.useGpuOwners(o.enabled, o.pods, o.small);
     function refresh() {
       ctx.refresh();
       m.refresh();
@@ -141,7 +141,7 @@ export function createPlugin(env) {
     const ctx = core.useAmdGpuContext();
     const pager = usePager();
     const t = telemetryScope(ctx, pager.state);
-    const m = core.useGpuMetrics(t.enabled, true, 'gauges', t.scope);
+    const m = core.useGpuMetrics(t.enabled, true, 'gauges', t.scope, t.small);
     return h(Page, {
       vm: metricsView(ctx, m, { pager: pager.state }), onRefresh: m.refresh,
       onPage: pager.onPage, onFilter: pager.onFilter,

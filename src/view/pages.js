@@ -629,12 +629,17 @@ export function visibleNodeNames(ctx, state) {
 }
 
 /**
- * What a paged page asks Prometheus for: `{enabled: false}` while the node
- * list is loading (the page's node names are not known yet — one wave after
- * the lists instead of a cluster-wide one before them); the names on the page
- * once it is listed; cluster-wide (`scope` undefined) when the node list
- * failed (e.g. RBAC denies listing nodes), so telemetry still shows.
- * @returns {{enabled: boolean, scope: (string[]|undefined)}}
+ * What a paged page asks Prometheus for:
+ *   * while the node list is loading, and while every GPU node fits on one
+ *     page: `small` — the whole cluster if it has at most SMALL_CLUSTER_GPUS
+ *     GPUs, else the page's nodes, decided by Prometheus in the same request
+ *     (metrics.js smallClusterQuery). A small cluster's page thus needs no
+ *     second wave after the node list, and keeps one query key (no refetch)
+ *     when the list arrives;
+ *   * the names on the page once a larger cluster is listed;
+ *   * cluster-wide (`scope` undefined) when the node list failed (e.g. RBAC
+ *     denies listing nodes), so telemetry still shows.
+ * @returns {{enabled: boolean, scope: (string[]|undefined), small?: boolean}}
  */
 export function telemetryScope(ctx, state) {
   if (!ctx) return { enabled: false, scope: [] };
@@ -642,9 +647,10 @@ export function telemetryScope(ctx, state) {
   // arrives later: tens of MB against the node list's few).
   const nodes = ctx.nodesState;
   if (nodes === 'error') return { enabled: true, scope: undefined };
-  if (nodes !== 'ready' && ctx.loading) return { enabled: false, scope: [] };
+  if (nodes !== 'ready' && ctx.loading) return { enabled: true, scope: [], small: true };
   if (ctx.error && (!ctx.gpuNodes || ctx.gpuNodes.length === 0)) return { enabled: true, scope: undefined };
-  return { enabled: true, scope: nodePage(ctx.gpuNodes, state).names };
+  const names = nodePage(ctx.gpuNodes, state).names;
+  return ctx.gpuNodes.length <= NODES_PER_PAGE ? { enabled: true, scope: names, small: true } : { enabled: true, scope: names };
 }
 
 /** Per-GPU allocation strip block. */
@@ -958,16 +964,20 @@ function nodesHeadItems(ctx, now, powerByNode, pg) {
 }
 
 /**
- * The Pods page's owner query: the pods of its page (namespace/name keys)
- * once the pod list is in; cluster-wide when the pod list failed.
- * @returns {{enabled: boolean, pods: (string[]|undefined)}}
+ * The Pods page's owner query: `small` (every owner of a cluster with at most
+ * SMALL_CLUSTER_GPUS GPUs, else the page's pods) while the pod list loads or
+ * fits on one page; the pods of its page (namespace/name keys) once a longer
+ * list is in; cluster-wide when the pod list failed.
+ * @returns {{enabled: boolean, pods: (string[]|undefined), small?: boolean}}
  */
 export function ownersScope(ctx, state) {
   if (!ctx) return { enabled: false, pods: [] };
   if (ctx.podsState === 'error') return { enabled: true, pods: undefined };
-  if (ctx.podsState !== 'ready' && ctx.loading) return { enabled: false, pods: [] };
+  // As telemetryScope: every owner of a small cluster in the first wave.
+  if (ctx.podsState !== 'ready' && ctx.loading) return { enabled: true, pods: [], small: true };
   if (ctx.error && (!ctx.gpuPods || ctx.gpuPods.length === 0)) return { enabled: true, pods: undefined };
-  return { enabled: true, pods: podPage(ctx.gpuPods, state).names };
+  const pods = podPage(ctx.gpuPods, state).names;
+  return ctx.gpuPods.length <= PODS_PER_PAGE ? { enabled: true, pods: pods, small: true } : { enabled: true, pods: pods };
 }
 
 // ---------------------------------------------------------------------------

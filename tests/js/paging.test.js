@@ -21,7 +21,7 @@ import {
 import { countRows, findSection, pagerOf, pagerText, rowValue, sectionTitles } from '../../src/view/ir.js';
 import { renderPage } from '../../src/view/html.js';
 import {
-  SERIES, TOTAL_SERIES, createMetricsSource, hostnameMatcher, regexLiteral, scopedSeriesQuery, summarizeMetrics,
+  SERIES, SMALL_CLUSTER_GPUS, TOTAL_SERIES, createMetricsSource, hostnameMatcher, regexLiteral, scopedSeriesQuery, summarizeMetrics,
   summaryQuery, totalsFromRows, joinExporterResults, splitByName,
 } from '../../src/api/metrics.js';
 import { makeContext, makeDeviceConfig, makeGpuNode, makeGpuPod, makePluginPod } from './fixtures.js';
@@ -73,8 +73,10 @@ describe('nodePage', () => {
 });
 
 describe('telemetryScope', () => {
-  it('waits for the node list, then scopes to the page; cluster-wide when the node list failed', () => {
-    expect(telemetryScope(makeContext({ loading: true }), {}).enabled).toBe(false);
+  it('small-cluster mode while the node list loads and while it fits one page; then the page; cluster-wide when the node list failed', () => {
+    expect(telemetryScope(makeContext({ loading: true }), {})).toEqual({ enabled: true, scope: [], small: true });
+    expect(telemetryScope(ctxOf(8), {})).toEqual({ enabled: true, scope: names(8), small: true });
+    expect(telemetryScope(ctxOf(8), { filter: '003' })).toEqual({ enabled: true, scope: ['mi355x-003'], small: true });
     expect(telemetryScope(ctxOf(12), { page: 1 })).toEqual({ enabled: true, scope: names(12).slice(8) });
     const denied = Object.assign(makeContext({ nodes: [] }), { error: 'nodes is forbidden' });
     expect(telemetryScope(denied, {})).toEqual({ enabled: true, scope: undefined });
@@ -325,6 +327,72 @@ describe('GPU Pods / Device Plugins / Overview tables are bounded too', () => {
     const dp = devicePluginsView(ctx, { pager: { page: 1 } });
     expect(findSection(dp, 'Plugin Daemon Pods').blocks[0].rows.map((r) => r[0])).toEqual(ops.slice(25).map((p) => p.metadata.name));
     expect(pagerOf(dp).noun).toBe('operator pods');
+  });
+});
+
+describe('small-cluster mode: the first wave needs no node list on a cluster of one page', () => {
+  it('a small cluster answers with every GPU (statics included) in one request, before any node name is known', async () => {
+    const fake = prom({ data: exporterData(names(2)) });
+    const s = createMetricsSource({ request: fake });
+    const m = await s.fetchGpuMetrics('topology', { scope: [], small: true });
+    expect(fake.mock.calls).toHaveLength(1);
+    expect(decoded(fake)[0]).toContain('and on() (count({__name__="gpu_power_usage"}) <= ' + SMALL_CLUSTER_GPUS + ')');
+    expect(m.gpus).toHaveLength(16);
+    expect(m.gpus[0].vramTotalBytes).toBeGreaterThan(0);
+    expect(m.source).toBe('amd-exporter');
+  });
+  it('a larger cluster answers with nothing before the node list, then with the scope only; never cluster-wide', async () => {
+    const fake = prom({ data: exporterData(names(9)) });
+    const s = createMetricsSource({ request: fake });
+    const early = await s.fetchGpuMetrics('topology', { scope: [], small: true });
+    expect(early.gpus).toHaveLength(0);
+    expect(fake.mock.calls).toHaveLength(1); // the GPU count says "exporter present": no cluster-wide fallback
+    const later = await s.fetchGpuMetrics('topology', { scope: ['mi355x-004'], small: true });
+    expect(Array.from(new Set(later.gpus.map((g) => g.nodeName)))).toEqual(['mi355x-004']);
+    expect(fake.mock.calls).toHaveLength(2);
+  });
+  it('the Metrics summary rides along; the GPU count row is no total', async () => {
+    const fake = prom({ data: exporterData(names(3)) });
+    const m = await createMetricsSource({ request: fake }).fetchGpuMetrics('gauges', { scope: names(3), summary: true, small: true });
+    expect([m.totals.gpus, m.totals.nodes]).toEqual([24, 3]);
+    expect(m.gpus).toHaveLength(24);
+  });
+  it('owners and series have the same guarded form', async () => {
+    const fake = prom({ data: exporterData(['n0']) });
+    const s = createMetricsSource({ request: fake });
+    const o = await s.fetchGpuOwners({ pods: [], small: true });
+    expect(o.gpus.map((g) => g.pod)).toEqual(['train-0', 'train-1']);
+    expect(decoded(fake)[0]).toContain('pod!=""})) and on() (count(');
+    const sr = await s.fetchSeries(1800, 30, [], true);
+    expect(decoded(fake)[1]).toContain('and on() (count(');
+    expect(sr.total.power.length).toBe(2);
+  });
+  it('plugin: a cold GPU Nodes page on a small cluster asks once, before the node list, and keeps that answer', async () => {
+    lib.resetHeadlamp();
+    lib.lists.Node = [null, null];
+    lib.lists.Pod = [null, null];
+    const fake = prom({ data: exporterData(names(2)) });
+    lib.api.handler = (p) => {
+      if (p === DEVICE_CONFIG_LIST_PATH) return Promise.resolve({ kind: 'List', metadata: {}, items: [makeDeviceConfig()] });
+      if (p.indexOf('/proxy/api/v1/') >= 0) return fake(p);
+      return Promise.reject(Object.assign(new Error('503'), { status: 503 }));
+    };
+    const plugin = createPlugin({ React: React, lib: lib, CommonComponents: CC });
+    const Page = plugin.routeComponent('nodes');
+    const r = render(h(Page));
+    await r.settle();
+    const live = () => decoded(fake).filter((q) => /\/query\?query=(?!1$)/.test(q));
+    expect(live()).toHaveLength(1); // sent while the lists load
+    lib.lists.Node = [names(2).map((x) => makeGpuNode(x)), null];
+    lib.lists.Pod = [[makeGpuPod('train-0', { node: 'mi355x-000' })], null];
+    r.rerender(h(Page));
+    await r.settle();
+    expect(live()).toHaveLength(1); // the node list arriving sends nothing more
+    expect(r.text()).toContain('mi355x-001');
+    r.click(r.getByLabelText('Refresh node data'));
+    await r.settle();
+    expect(live()).toHaveLength(2);
+    r.unmount();
   });
 });
 

@@ -69,6 +69,19 @@ export function flatten(d) {
  * (__name__) …, "agg", …)). Unknown shapes answer no rows.
  */
 function term(q, rows) {
+  // sizeGuard: `(Q) and on() (count({__name__="P"}) <= N)` keeps Q's rows when the count passes.
+  const guard = /^\((.*)\) and on\(\) \(count\(\{__name__="([a-z_]+)"\}\) (<=|>) (\d+)\)$/.exec(q);
+  if (guard) {
+    const n = rows.filter((r) => r.metric.__name__ === guard[2]).length;
+    if (n === 0) return [];
+    const pass = guard[3] === '<=' ? n <= Number(guard[4]) : n > Number(guard[4]);
+    return pass ? term(guard[1], rows) : [];
+  }
+  const count = /^label_replace\(count\(\{__name__="([a-z_]+)"\}\), "agg", "gpus", "", ""\)$/.exec(q);
+  if (count) {
+    const n = rows.filter((r) => r.metric.__name__ === count[1]).length;
+    return n ? [vec({ agg: 'gpus' }, n)] : [];
+  }
   const own = /^max by \([^)]*\) \(\{__name__="([a-z_]+)", pod!=""\}\)$/.exec(q);
   if (own) return rows.filter((r) => r.metric.__name__ === own[1] && r.metric.pod);
   const agg = /^label_replace\((sum|count) by \(__name__\) \(\{__name__=~"(.*?)"\}\), "agg", "(\w+)", "", ""\)$/.exec(q);
@@ -104,6 +117,25 @@ function term(q, rows) {
   return rows.filter((r) => re.test(r.metric.__name__ || '') && hostOk(r.metric.hostname));
 }
 
+/** `q` split at its top-level ` or ` (not inside parentheses). */
+export function splitOr(q) {
+  const out = [];
+  let depth = 0;
+  let start = 0;
+  for (let i = 0; i < q.length; i++) {
+    const c = q[i];
+    if (c === '(') depth++;
+    else if (c === ')') depth--;
+    else if (depth === 0 && q.substr(i, 4) === ' or ') {
+      out.push(q.slice(start, i));
+      start = i + 4;
+      i += 3;
+    }
+  }
+  out.push(q.slice(start));
+  return out;
+}
+
 /** A fake proxy: answers probes on `up` services and the client's queries from `data` / `ne`. */
 export function prom(opts) {
   const o = Object.assign({ up: [BASE0], data: exporterData(['n0']), ne: null }, opts || {});
@@ -129,7 +161,7 @@ export function prom(opts) {
     }
     // `a or b`: every term's rows (the client keeps their label sets apart).
     const out = [];
-    q.split(' or ').forEach((t) => term(t, rows).forEach((r) => out.push(r)));
+    splitOr(q).forEach((t) => term(t, rows).forEach((r) => out.push(r)));
     return Promise.resolve(ok(out));
   });
 }

@@ -255,3 +255,37 @@ def test_summary_query_of_the_metrics_page():
     assert got[("count", "gpu_power_usage")] == 24 and got[("count", "gpu_power_cap")] == 16
     assert got[("nodes", "gpu_power_usage")] == 3
     assert got[("sum", "gpu_total_vram")] == 24 * 294896.0
+
+
+def test_size_guarded_small_cluster_query():
+    """metrics.js smallClusterQuery: every GPU of a cluster with at most SMALL_CLUSTER_GPUS, else the scope's, plus
+    the GPU count row; `x and <empty>` is answered without evaluating x."""
+    import subprocess
+
+    from headlamp_intel_gpu_plugin_amd.utils.nodebridge import ROOT, node_binary
+
+    js = ("import('./src/api/metrics.js').then(m => process.stdout.write(JSON.stringify("
+          "[m.smallClusterQuery(true, 'topology', ['b']), m.SMALL_CLUSTER_GPUS])))")
+    q, limit = json.loads(subprocess.run([node_binary(), "-e", js], cwd=ROOT, capture_output=True, text=True,
+                                         timeout=60).stdout)
+
+    def cluster(nodes):
+        d = TSDB()
+        for node in nodes:
+            for g in range(8):
+                d.add(Series({"__name__": "gpu_power_usage", "hostname": node, "gpu_id": str(g)}, fn=lambda t: 500.0))
+        return d
+
+    small = _vec(query(cluster("abc"), q, 100.0))
+    assert {r["metric"].get("hostname") for r in small if "agg" not in r["metric"]} == {"a", "b", "c"}
+    (count,) = [r for r in small if r["metric"].get("agg") == "gpus"]
+    assert float(count["value"][1]) == 24
+    many = [chr(ord("a") + i) for i in range(limit // 8 + 1)]
+    large = _vec(query(cluster(many), q, 100.0))
+    assert {r["metric"].get("hostname") for r in large if "agg" not in r["metric"]} == {"b"}
+
+    # The left side is not evaluated when the right is empty (a scalar there would be an error otherwise).
+    d = cluster("a")
+    assert _vec(query(d, "1 and on() (count(gpu_power_usage) > 1000)", 100.0)) == []
+    with pytest.raises(promql.PromQLError):
+        promql.Evaluator(d).instant(parse("1 and on() (count(gpu_power_usage) > 1)"), 100.0)
