@@ -41,6 +41,9 @@ export function render(element, options) {
       return hits[0];
     },
     byTag: function (tag) { return Array.prototype.slice.call(c.querySelectorAll(tag)); },
+    byAttr: function (name) { return Array.prototype.slice.call(c.querySelectorAll('[' + name + ']')); },
+    attr: function (node, name) { return node.getAttribute(name); },
+    style: function (node) { return node.style; },
     click: function (node) { fireEvent.click(node); return handle; },
     change: function (node, value) { fireEvent.change(node, { target: { value: value } }); return handle; },
     isDisabled: function (node) { return !!node.disabled; },

@@ -21,6 +21,14 @@ export function render(element, options) {
     /** The one element whose aria-label is exactly `label`. */
     byLabel: function (label) { return r.getByLabelText(label); },
     byTag: function (tag) { return r.byTag(tag); },
+    /** Host elements carrying attribute `name`. */
+    byAttr: function (name) { return r.queryAll(function (n) { return n.props[name] !== undefined; }); },
+    /** An attribute as the DOM reports it (a string), or null. */
+    attr: function (node, name) {
+      const v = node.props[name];
+      return v === undefined || v === null || v === false ? null : String(v);
+    },
+    style: function (node) { return node.props.style || {}; },
     click: function (node) { r.click(node); return handle; },
     change: function (node, value) { r.change(node, value); return handle; },
     isDisabled: function (node) { return !!node.props.disabled; },

@@ -3,7 +3,9 @@
  * harness React (tests/js/stubs/react.js) with CommonComponents stand-ins
  * that render the markup the reference's component tests mock them with
  * (reference src/components/OverviewPage.test.tsx:8-61). Every spec checks
- * what the renderer HANDS each CommonComponent (props), not only the text.
+ * what the renderer HANDS each CommonComponent (props), not only the text;
+ * what a user sees of the same blocks is also pinned runner-agnostically in
+ * tests/js/shared/renderer.shared.test.js (both React tiers).
  */
 import React, { render } from './stubs/react.js';
 import * as CC from './stubs/CommonComponents.js';

@@ -189,6 +189,12 @@ function makeMatchers(actual, negate, label) {
       check(actual.mock.calls.some(function (c) { return deepEqual(c, args); }),
         'expected a call with ' + fmt(args) + ', calls: ' + fmt(actual.mock.calls));
     },
+    toHaveBeenLastCalledWith: function () {
+      const args = Array.prototype.slice.call(arguments);
+      const calls = actual.mock.calls;
+      check(calls.length > 0 && deepEqual(calls[calls.length - 1], args),
+        'expected the last call with ' + fmt(args) + ', calls: ' + fmt(calls));
+    },
   };
   return m;
 }
