@@ -85,13 +85,16 @@ export const DISCOVERY_TTL_MS = 5 * 60 * 1000;
 /** Consecutive failed metrics fetches before the page switches to "Prometheus Unreachable". */
 export const STALE_FAILURES = 3;
 /**
- * GPUs (power gauges) up to which a paged view asks for the whole cluster
- * instead of its page: one page of MI355X nodes (8 × 8). The guard is
- * evaluated by Prometheus inside the same request (smallClusterQuery), so a
- * page opened while the node list is still loading needs no second wave on
- * a small cluster, and a large one gets nothing it did not ask for.
+ * GPU nodes (exporter hostnames) up to which a paged view asks for the whole
+ * cluster instead of its page: one page of nodes (pages.js NODES_PER_PAGE).
+ * Prometheus evaluates the guard inside the same request
+ * (smallClusterQuery), so a page opened while the node list is still loading
+ * needs no second wave on a small cluster, and a large one gets nothing it
+ * did not ask for.
  */
-export const SMALL_CLUSTER_GPUS = 64;
+export const SMALL_CLUSTER_NODES = 8;
+/** GPU pods (exporter `pod` labels) up to which the Pods page asks for every owner: one page (PODS_PER_PAGE). */
+export const SMALL_CLUSTER_PODS = 25;
 
 /**
  * @typedef {Object} GpuTelemetry
@@ -388,14 +391,28 @@ export function hostnameMatcher(names) {
   return 'hostname=~"' + promString(names.map(regexLiteral).join('|')) + '"';
 }
 
+/** Exporter hostnames reporting a power gauge: the GPU nodes Prometheus sees. */
+export function gpuNodeCount() {
+  return 'count(count by (hostname) ({__name__="' + SERIES.exporter.power + '"}))';
+}
+
+/** Pods the exporter attributes a GPU to. */
+export function gpuPodCount() {
+  return 'count(count by (namespace, pod) ({__name__="' + SERIES.exporter.power + '", pod!=""}))';
+}
+
 /**
- * `q` when the cluster has at most SMALL_CLUSTER_GPUS power gauges (`small`),
- * or when it has more (`!small`): `and on()` against a one-sample count keeps
- * all of `q` or none of it, decided by Prometheus in the same evaluation.
+ * `q` when `count` (a one-sample count, gpuNodeCount / gpuPodCount) is at
+ * most `limit` (`small`), or above it (`!small`): `and on()` keeps all of `q`
+ * or none of it, decided by Prometheus in the same evaluation.
  */
-export function sizeGuard(q, small) {
-  return '(' + q + ') and on() (count({__name__="' + SERIES.exporter.power + '"}) ' + (small ? '<=' : '>') + ' ' +
-    SMALL_CLUSTER_GPUS + ')';
+export function sizeGuard(q, small, count, limit) {
+  return '(' + q + ') and on() (' + count + ' ' + (small ? '<=' : '>') + ' ' + limit + ')';
+}
+
+/** The count itself as a row tagged `agg="<tag>"` (sizeFromRows reads it back). */
+function sizeRow(count, tag) {
+  return 'label_replace(' + count + ', "agg", "' + tag + '", "", "")';
 }
 
 /**
@@ -405,16 +422,18 @@ export function sizeGuard(q, small) {
  * none waits for the node list on a small cluster.
  */
 export function smallClusterQuery(withStatic, view, scope) {
-  const all = sizeGuard(exporterQuery(withStatic, false, view), true);
-  // The GPU count itself: tells a large cluster (nothing asked for yet) from one without exporter series.
-  const count = 'label_replace(count({__name__="' + SERIES.exporter.power + '"}), "agg", "gpus", "", "")';
-  return (scope.length ? all + ' or ' + sizeGuard(exporterQuery(withStatic, true, view, scope), false) : all) + ' or ' + count;
+  const n = gpuNodeCount();
+  const all = sizeGuard(exporterQuery(withStatic, false, view), true, n, SMALL_CLUSTER_NODES);
+  const page = scope.length ? ' or ' + sizeGuard(exporterQuery(withStatic, true, view, scope), false, n, SMALL_CLUSTER_NODES) : '';
+  // The count itself: which branch answered, and a large cluster (nothing
+  // asked for yet) told apart from one without exporter series.
+  return all + page + ' or ' + sizeRow(n, 'gpu_nodes');
 }
 
-/** The `agg="gpus"` row of a smallClusterQuery answer: power gauges in the cluster (0 when absent). */
-export function gpuCountFromRows(rows) {
+/** The `agg="<tag>"` count row of a size-guarded answer (0 when absent: nothing reports). */
+export function sizeFromRows(rows, tag) {
   for (let i = 0; i < rows.length; i++) {
-    if (isRow(rows[i]) && rows[i].metric.agg === 'gpus') return num(rows[i].value[1]) || 0;
+    if (isRow(rows[i]) && rows[i].metric.agg === tag) return num(rows[i].value[1]) || 0;
   }
   return 0;
 }
@@ -531,9 +550,11 @@ export function exporterNodeQuery(nodeName, withStatic) {
 export function ownersQuery(pods, small) {
   const sel = '{__name__="' + SERIES.exporter.power + '", ';
   if (small) {
-    // Every allocated GPU of a small cluster, else the page's pods (smallClusterQuery).
-    const all = sizeGuard(ownersQuery(null), true);
-    return pods && pods.length ? all + ' or ' + sizeGuard(ownersQuery(pods), false) : all;
+    // Every owner when they fit on one page of the Pods table, else the page's pods (smallClusterQuery).
+    const n = gpuPodCount();
+    const all = sizeGuard(ownersQuery(null), true, n, SMALL_CLUSTER_PODS);
+    const page = pods && pods.length ? ' or ' + sizeGuard(ownersQuery(pods), false, n, SMALL_CLUSTER_PODS) : '';
+    return all + page + ' or ' + sizeRow(n, 'gpu_pods');
   }
   if (!pods) return 'max by (' + EXPORTER_JOIN_LABELS.join(', ') + ') (' + sel + 'pod!=""})';
   // The pods of one page of the Pods table ("namespace/name" keys): O(page).
@@ -621,9 +642,10 @@ export function scopedSeriesQuery(scope, small) {
   const page = 'sum by (__name__, hostname) ({' + names + ', ' + hostnameMatcher(scope) + '})';
   const total = 'label_replace(sum by (__name__) ({' + names + '}), "scope", "cluster", "", "")';
   if (small) {
-    // Every node's line on a small cluster, else the page's (smallClusterQuery).
-    const all = sizeGuard(seriesQuery(), true);
-    return (scope.length ? all + ' or ' + sizeGuard(page, false) : all) + ' or ' + total;
+    // Every node's line on a cluster of one page, else the page's (smallClusterQuery).
+    const n = gpuNodeCount();
+    const all = sizeGuard(seriesQuery(), true, n, SMALL_CLUSTER_NODES);
+    return (scope.length ? all + ' or ' + sizeGuard(page, false, n, SMALL_CLUSTER_NODES) : all) + ' or ' + total;
   }
   return page + ' or ' + total;
 }
@@ -926,7 +948,8 @@ export function createMetricsSource(opts) {
    * path, per scope.
    *
    * `small`: the page may be the whole cluster (smallClusterQuery) — every
-   * GPU when the cluster has at most SMALL_CLUSTER_GPUS, else `scope`'s.
+   * GPU when at most SMALL_CLUSTER_NODES nodes report, else `scope`'s. The
+   * answer says which (`small.exceeded`).
    */
   function scopedSnapshot(v, scope, summary, key, small) {
     const st = scopedEntry(key);
@@ -945,8 +968,9 @@ export function createMetricsSource(opts) {
         st.failures = 0;
         const rows = res.rows;
         const j = joinExporterResults(rows);
-        const totals = summary ? totalsFromRows(rows.__agg.filter(function (r) { return r.metric.agg !== 'gpus'; })) : undefined;
-        const found = j.gpus.length > 0 || (!!totals && totals.gpus > 0) || (small && gpuCountFromRows(rows.__agg) > 0);
+        const totals = summary ? totalsFromRows(rows.__agg.filter(function (r) { return r.metric.agg !== 'gpu_nodes'; })) : undefined;
+        const reporting = small ? sizeFromRows(rows.__agg, 'gpu_nodes') : 0;
+        const found = j.gpus.length > 0 || (!!totals && totals.gpus > 0) || reporting > 0;
         // Nothing from the exporter yet: maybe node-exporter feeds this
         // Prometheus (no hostname label) — ask cluster-wide to find out, at
         // most once per discovery TTL when that finds no GPU either (a
@@ -981,7 +1005,8 @@ export function createMetricsSource(opts) {
           applyStatics(j.gpus, merged);
           j.links = links;
         }
-        return scopedResult(st, base, q, j, scope, totals, v);
+        const sized = small ? { count: reporting, limit: SMALL_CLUSTER_NODES, exceeded: reporting > SMALL_CLUSTER_NODES } : undefined;
+        return scopedResult(st, base, q, j, scope, totals, v, sized);
       });
     }, function () {
       st.failures++;
@@ -992,7 +1017,7 @@ export function createMetricsSource(opts) {
     }).then(function (r) { return r === NOT_SCOPED ? clusterCut(v, scope, summary, key) : r; });
   }
 
-  function scopedResult(st, base, q, j, scope, totals, v) {
+  function scopedResult(st, base, q, j, scope, totals, v, sized) {
     const prev = st.last;
     st.last = {
       source: source,
@@ -1005,6 +1030,8 @@ export function createMetricsSource(opts) {
       query: q,
       scope: scope,
       totals: totals && prev && prev.totals && sameValue(prev.totals, totals) ? prev.totals : totals,
+      // A small-cluster query: how many GPU nodes report, and whether that was more than one page.
+      small: sized,
     };
     return st.last;
   }
@@ -1219,7 +1246,9 @@ export function createMetricsSource(opts) {
         if (!res.ok) return UNREACHABLE;
         ownersFailures = 0;
         const j = joinExporterResults(res.rows);
+        const owning = small ? sizeFromRows(res.rows.__agg, 'gpu_pods') : 0;
         ownersLast = {
+          small: small ? { count: owning, limit: SMALL_CLUSTER_PODS, exceeded: owning > SMALL_CLUSTER_PODS } : undefined,
           source: j.gpus.length ? 'amd-exporter' : source,
           gpus: ownersLast ? shareGpus(ownersLast.gpus, j.gpus) : j.gpus,
           xgmi: {},

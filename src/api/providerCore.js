@@ -271,15 +271,39 @@ export function createProviderCore(React, lib, deps) {
     const scoped = Array.isArray(scope);
     const names = scoped ? scope.slice() : null;
     const sm = scoped && !!small;
+    const ex = useState(false);
     const key = 'gpus|' + sourceKey(cluster, settings) + '|' + v + '|' + series + '|' + settings.seriesMinutes +
-      (sm ? '|small' : scoped ? '|scope:' + names.join(',') : '');
-    return useMetricsFetch(on ? key : null, function () {
+      (sm ? smallKey(ex[0], names) : scoped ? '|scope:' + names.join(',') : '');
+    const res = useMetricsFetch(on ? key : null, function () {
       const opts = scoped ? { scope: names, summary: v === 'gauges', small: sm } : undefined;
       return Promise.all([
         source.fetchGpuMetrics(v, opts),
         series ? source.fetchSeries(settings.seriesMinutes * 60, seriesStepSec(settings), names || undefined, sm) : Promise.resolve(null),
       ]);
     }, false, source);
+    useExceeded(sm, res, ex);
+    return res;
+  }
+
+  /**
+   * Key suffix of a small-cluster fetch: one key while the answer held the
+   * whole cluster, so the node list arriving refetches nothing. An answer
+   * that found more than one page (stale series of a removed node, exporter
+   * hostnames the node list lacks) held only the names known when it was
+   * asked: then the key follows the names, and new names are fetched.
+   */
+  function smallKey(exceeded, names) {
+    return '|small' + (exceeded && names.length ? ':' + names.join(',') : '');
+  }
+
+  /** Track `res.metrics.small.exceeded` in the state pair `ex` (see smallKey). */
+  function useExceeded(sm, res, ex) {
+    const now = !!(sm && res.metrics && res.metrics.small && res.metrics.small.exceeded);
+    const was = ex[0];
+    const set = ex[1];
+    useEffect(function () {
+      if (now !== was) set(now);
+    }, [now, was]);
   }
 
   /**
@@ -400,10 +424,13 @@ export function createProviderCore(React, lib, deps) {
     const scoped = Array.isArray(pods);
     const keys = scoped ? pods.slice() : null;
     const sm = scoped && !!small;
-    const key = 'owners|' + sourceKey(cluster, loadSettings()) + (sm ? '|small' : scoped ? '|pods:' + keys.join(',') : '');
-    return useMetricsFetch(on ? key : null, function () {
+    const ex = useState(false);
+    const key = 'owners|' + sourceKey(cluster, loadSettings()) + (sm ? smallKey(ex[0], keys) : scoped ? '|pods:' + keys.join(',') : '');
+    const res = useMetricsFetch(on ? key : null, function () {
       return source.fetchGpuOwners(scoped ? { pods: keys, small: sm } : undefined).then(function (m) { return [m, null]; });
     }, false, source);
+    useExceeded(sm, res, ex);
+    return res;
   }
 
   return {

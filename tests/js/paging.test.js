@@ -21,7 +21,7 @@ import {
 import { countRows, findSection, pagerOf, pagerText, rowValue, sectionTitles } from '../../src/view/ir.js';
 import { renderPage } from '../../src/view/html.js';
 import {
-  SERIES, SMALL_CLUSTER_GPUS, TOTAL_SERIES, createMetricsSource, hostnameMatcher, regexLiteral, scopedSeriesQuery, summarizeMetrics,
+  SERIES, SMALL_CLUSTER_NODES, SMALL_CLUSTER_PODS, TOTAL_SERIES, createMetricsSource, hostnameMatcher, regexLiteral, scopedSeriesQuery, summarizeMetrics,
   summaryQuery, totalsFromRows, joinExporterResults, splitByName,
 } from '../../src/api/metrics.js';
 import { makeContext, makeDeviceConfig, makeGpuNode, makeGpuPod, makePluginPod } from './fixtures.js';
@@ -336,7 +336,8 @@ describe('small-cluster mode: the first wave needs no node list on a cluster of 
     const s = createMetricsSource({ request: fake });
     const m = await s.fetchGpuMetrics('topology', { scope: [], small: true });
     expect(fake.mock.calls).toHaveLength(1);
-    expect(decoded(fake)[0]).toContain('and on() (count({__name__="gpu_power_usage"}) <= ' + SMALL_CLUSTER_GPUS + ')');
+    expect(decoded(fake)[0]).toContain('and on() (count(count by (hostname) ({__name__="gpu_power_usage"})) <= ' + SMALL_CLUSTER_NODES + ')');
+    expect(m.small).toEqual({ count: 2, limit: SMALL_CLUSTER_NODES, exceeded: false });
     expect(m.gpus).toHaveLength(16);
     expect(m.gpus[0].vramTotalBytes).toBeGreaterThan(0);
     expect(m.source).toBe('amd-exporter');
@@ -346,12 +347,13 @@ describe('small-cluster mode: the first wave needs no node list on a cluster of 
     const s = createMetricsSource({ request: fake });
     const early = await s.fetchGpuMetrics('topology', { scope: [], small: true });
     expect(early.gpus).toHaveLength(0);
+    expect(early.small.exceeded).toBe(true);
     expect(fake.mock.calls).toHaveLength(1); // the GPU count says "exporter present": no cluster-wide fallback
     const later = await s.fetchGpuMetrics('topology', { scope: ['mi355x-004'], small: true });
     expect(Array.from(new Set(later.gpus.map((g) => g.nodeName)))).toEqual(['mi355x-004']);
     expect(fake.mock.calls).toHaveLength(2);
   });
-  it('the Metrics summary rides along; the GPU count row is no total', async () => {
+  it('the Metrics summary rides along; the node count row is no total', async () => {
     const fake = prom({ data: exporterData(names(3)) });
     const m = await createMetricsSource({ request: fake }).fetchGpuMetrics('gauges', { scope: names(3), summary: true, small: true });
     expect([m.totals.gpus, m.totals.nodes]).toEqual([24, 3]);
@@ -362,7 +364,8 @@ describe('small-cluster mode: the first wave needs no node list on a cluster of 
     const s = createMetricsSource({ request: fake });
     const o = await s.fetchGpuOwners({ pods: [], small: true });
     expect(o.gpus.map((g) => g.pod)).toEqual(['train-0', 'train-1']);
-    expect(decoded(fake)[0]).toContain('pod!=""})) and on() (count(');
+    expect(decoded(fake)[0]).toContain('pod!=""})) and on() (count(count by (namespace, pod)');
+    expect(o.small).toEqual({ count: 2, limit: 25, exceeded: false });
     const sr = await s.fetchSeries(1800, 30, [], true);
     expect(decoded(fake)[1]).toContain('and on() (count(');
     expect(sr.total.power.length).toBe(2);
@@ -392,6 +395,41 @@ describe('small-cluster mode: the first wave needs no node list on a cluster of 
     r.click(r.getByLabelText('Refresh node data'));
     await r.settle();
     expect(live()).toHaveLength(2);
+    r.unmount();
+  });
+});
+
+describe('small-cluster mode: guards and pages agree', () => {
+  it('the guards are one page of the views', () => {
+    expect(SMALL_CLUSTER_NODES).toBe(NODES_PER_PAGE);
+    expect(SMALL_CLUSTER_PODS).toBe(PODS_PER_PAGE);
+  });
+  it('an answer that found more than one page of nodes is asked again with the names, once the list has them', async () => {
+    lib.resetHeadlamp();
+    lib.lists.Node = [null, null];
+    lib.lists.Pod = [null, null];
+    // Two GPU nodes listed; the exporter still reports eight removed ones (stale series).
+    const fake = prom({ data: exporterData(names(10)) });
+    lib.api.handler = (p) => {
+      if (p === DEVICE_CONFIG_LIST_PATH) return Promise.resolve({ kind: 'List', metadata: {}, items: [] });
+      if (p.indexOf('/proxy/api/v1/') >= 0) return fake(p);
+      return Promise.reject(Object.assign(new Error('503'), { status: 503 }));
+    };
+    const plugin = createPlugin({ React: React, lib: lib, CommonComponents: CC });
+    const Page = plugin.routeComponent('nodes');
+    const r = render(h(Page));
+    await r.settle();
+    const live = () => decoded(fake).filter((q) => /\/query\?query=(?!1$)/.test(q));
+    expect(live()).toHaveLength(1);
+    lib.lists.Node = [names(2).map((x) => makeGpuNode(x)), null];
+    lib.lists.Pod = [[], null];
+    r.rerender(h(Page));
+    await r.settle();
+    expect(live()).toHaveLength(2);
+    expect(live()[1]).toContain('hostname=~"mi355x-000|mi355x-001"');
+    r.rerender(h(Page));
+    await r.settle();
+    expect(live()).toHaveLength(2); // settled: no refetch loop
     r.unmount();
   });
 });

@@ -69,18 +69,18 @@ export function flatten(d) {
  * (__name__) …, "agg", …)). Unknown shapes answer no rows.
  */
 function term(q, rows) {
-  // sizeGuard: `(Q) and on() (count({__name__="P"}) <= N)` keeps Q's rows when the count passes.
-  const guard = /^\((.*)\) and on\(\) \(count\(\{__name__="([a-z_]+)"\}\) (<=|>) (\d+)\)$/.exec(q);
+  // sizeGuard: `(Q) and on() (<count> <= N)` keeps Q's rows when the count passes.
+  const guard = /^\((.*)\) and on\(\) \((count\(count by .*\)) (<=|>) (\d+)\)$/.exec(q);
   if (guard) {
-    const n = rows.filter((r) => r.metric.__name__ === guard[2]).length;
-    if (n === 0) return [];
+    const n = countOf(guard[2], rows);
+    if (n === null || n === 0) return [];
     const pass = guard[3] === '<=' ? n <= Number(guard[4]) : n > Number(guard[4]);
     return pass ? term(guard[1], rows) : [];
   }
-  const count = /^label_replace\(count\(\{__name__="([a-z_]+)"\}\), "agg", "gpus", "", ""\)$/.exec(q);
-  if (count) {
-    const n = rows.filter((r) => r.metric.__name__ === count[1]).length;
-    return n ? [vec({ agg: 'gpus' }, n)] : [];
+  const sized = /^label_replace\((count\(count by .*\)), "agg", "(\w+)", "", ""\)$/.exec(q);
+  if (sized) {
+    const n = countOf(sized[1], rows);
+    return n ? [vec({ agg: sized[2] }, n)] : [];
   }
   const own = /^max by \([^)]*\) \(\{__name__="([a-z_]+)", pod!=""\}\)$/.exec(q);
   if (own) return rows.filter((r) => r.metric.__name__ === own[1] && r.metric.pod);
@@ -115,6 +115,18 @@ function term(q, rows) {
     }
   }
   return rows.filter((r) => re.test(r.metric.__name__ || '') && hostOk(r.metric.hostname));
+}
+
+/** metrics.js gpuNodeCount / gpuPodCount over `rows` (null for another shape). */
+function countOf(expr, rows) {
+  const m = /^count\(count by \((hostname|namespace, pod)\) \(\{__name__="([a-z_]+)"(, pod!="")?\}\)\)$/.exec(expr);
+  if (!m) return null;
+  const seen = {};
+  rows.forEach((r) => {
+    if (r.metric.__name__ !== m[2] || (m[3] && !r.metric.pod)) return;
+    seen[m[1] === 'hostname' ? r.metric.hostname : r.metric.namespace + '/' + r.metric.pod] = true;
+  });
+  return Object.keys(seen).length;
 }
 
 /** `q` split at its top-level ` or ` (not inside parentheses). */

@@ -258,14 +258,14 @@ def test_summary_query_of_the_metrics_page():
 
 
 def test_size_guarded_small_cluster_query():
-    """metrics.js smallClusterQuery: every GPU of a cluster with at most SMALL_CLUSTER_GPUS, else the scope's, plus
-    the GPU count row; `x and <empty>` is answered without evaluating x."""
+    """metrics.js smallClusterQuery: every GPU of a cluster of at most SMALL_CLUSTER_NODES GPU nodes, else the
+    scope's, plus the node count row; `x and <empty>` is answered without evaluating x."""
     import subprocess
 
     from headlamp_intel_gpu_plugin_amd.utils.nodebridge import ROOT, node_binary
 
     js = ("import('./src/api/metrics.js').then(m => process.stdout.write(JSON.stringify("
-          "[m.smallClusterQuery(true, 'topology', ['b']), m.SMALL_CLUSTER_GPUS])))")
+          "[m.smallClusterQuery(true, 'topology', ['b']), m.SMALL_CLUSTER_NODES])))")
     q, limit = json.loads(subprocess.run([node_binary(), "-e", js], cwd=ROOT, capture_output=True, text=True,
                                          timeout=60).stdout)
 
@@ -278,9 +278,9 @@ def test_size_guarded_small_cluster_query():
 
     small = _vec(query(cluster("abc"), q, 100.0))
     assert {r["metric"].get("hostname") for r in small if "agg" not in r["metric"]} == {"a", "b", "c"}
-    (count,) = [r for r in small if r["metric"].get("agg") == "gpus"]
-    assert float(count["value"][1]) == 24
-    many = [chr(ord("a") + i) for i in range(limit // 8 + 1)]
+    (count,) = [r for r in small if r["metric"].get("agg") == "gpu_nodes"]
+    assert float(count["value"][1]) == 3
+    many = [chr(ord("a") + i) for i in range(limit + 1)]
     large = _vec(query(cluster(many), q, 100.0))
     assert {r["metric"].get("hostname") for r in large if "agg" not in r["metric"]} == {"b"}
 
