@@ -93,8 +93,13 @@ export const STALE_FAILURES = 3;
  * did not ask for.
  */
 export const SMALL_CLUSTER_NODES = 8;
-/** GPU pods (exporter `pod` labels) up to which the Pods page asks for every owner: one page (PODS_PER_PAGE). */
-export const SMALL_CLUSTER_PODS = 25;
+/**
+ * GPU pods (exporter `pod` labels) up to which the Pods page asks for every
+ * owner: as many as a cluster of one page of nodes can run (8 × 8 GPUs, one
+ * each). Their owner series are at most a few KB; the table still shows one
+ * page of PODS_PER_PAGE, and paging through it needs no request.
+ */
+export const SMALL_CLUSTER_PODS = 64;
 
 /**
  * @typedef {Object} GpuTelemetry

@@ -69,7 +69,7 @@ import {
   unwrapKubeObject,
 } from '../api/amdgpu.js';
 import { buildGpuSlots, buildXgmiMatrix, isFullMesh } from '../api/topology.js';
-import { PROMETHEUS_SERVICES, clusterPowerStats, summarizeMetrics } from '../api/metrics.js';
+import { PROMETHEUS_SERVICES, SMALL_CLUSTER_NODES, SMALL_CLUSTER_PODS, clusterPowerStats, summarizeMetrics } from '../api/metrics.js';
 import { bar, createMemo, createObjectCache, kv, lines, loader, noteExpiry, page, pager, pctbar, row, section, status, table } from './ir.js';
 
 export const BRAND = 'AMD GPU';
@@ -650,7 +650,7 @@ export function telemetryScope(ctx, state) {
   if (nodes !== 'ready' && ctx.loading) return { enabled: true, scope: [], small: true };
   if (ctx.error && (!ctx.gpuNodes || ctx.gpuNodes.length === 0)) return { enabled: true, scope: undefined };
   const names = nodePage(ctx.gpuNodes, state).names;
-  return ctx.gpuNodes.length <= NODES_PER_PAGE ? { enabled: true, scope: names, small: true } : { enabled: true, scope: names };
+  return ctx.gpuNodes.length <= SMALL_CLUSTER_NODES ? { enabled: true, scope: names, small: true } : { enabled: true, scope: names };
 }
 
 /** Per-GPU allocation strip block. */
@@ -964,10 +964,10 @@ function nodesHeadItems(ctx, now, powerByNode, pg) {
 }
 
 /**
- * The Pods page's owner query: `small` (every owner of a cluster with at most
- * SMALL_CLUSTER_GPUS GPUs, else the page's pods) while the pod list loads or
- * fits on one page; the pods of its page (namespace/name keys) once a longer
- * list is in; cluster-wide when the pod list failed.
+ * The Pods page's owner query: `small` (every owner when at most
+ * SMALL_CLUSTER_PODS pods hold a GPU, else the page's pods) while the pod
+ * list loads or is that short; the pods of its page (namespace/name keys)
+ * once a longer list is in; cluster-wide when the pod list failed.
  * @returns {{enabled: boolean, pods: (string[]|undefined), small?: boolean}}
  */
 export function ownersScope(ctx, state) {
@@ -977,7 +977,7 @@ export function ownersScope(ctx, state) {
   if (ctx.podsState !== 'ready' && ctx.loading) return { enabled: true, pods: [], small: true };
   if (ctx.error && (!ctx.gpuPods || ctx.gpuPods.length === 0)) return { enabled: true, pods: undefined };
   const pods = podPage(ctx.gpuPods, state).names;
-  return ctx.gpuPods.length <= PODS_PER_PAGE ? { enabled: true, pods: pods, small: true } : { enabled: true, pods: pods };
+  return ctx.gpuPods.length <= SMALL_CLUSTER_PODS ? { enabled: true, pods: pods, small: true } : { enabled: true, pods: pods };
 }
 
 // ---------------------------------------------------------------------------

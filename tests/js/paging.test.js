@@ -365,7 +365,7 @@ describe('small-cluster mode: the first wave needs no node list on a cluster of 
     const o = await s.fetchGpuOwners({ pods: [], small: true });
     expect(o.gpus.map((g) => g.pod)).toEqual(['train-0', 'train-1']);
     expect(decoded(fake)[0]).toContain('pod!=""})) and on() (count(count by (namespace, pod)');
-    expect(o.small).toEqual({ count: 2, limit: 25, exceeded: false });
+    expect(o.small).toEqual({ count: 2, limit: SMALL_CLUSTER_PODS, exceeded: false });
     const sr = await s.fetchSeries(1800, 30, [], true);
     expect(decoded(fake)[1]).toContain('and on() (count(');
     expect(sr.total.power.length).toBe(2);
@@ -400,9 +400,13 @@ describe('small-cluster mode: the first wave needs no node list on a cluster of 
 });
 
 describe('small-cluster mode: guards and pages agree', () => {
-  it('the guards are one page of the views', () => {
+  it('the node guard is one page of nodes; the pod guard what such a cluster can run, one GPU each', () => {
     expect(SMALL_CLUSTER_NODES).toBe(NODES_PER_PAGE);
-    expect(SMALL_CLUSTER_PODS).toBe(PODS_PER_PAGE);
+    expect(SMALL_CLUSTER_PODS).toBe(NODES_PER_PAGE * 8);
+    expect(SMALL_CLUSTER_PODS).toBeGreaterThanOrEqual(PODS_PER_PAGE);
+    const pods = (n) => Array.from({ length: n }, (_, i) => makeGpuPod('p' + i, { node: 'mi355x-000' }));
+    expect(ownersScope(makeContext({ nodes: [makeGpuNode('mi355x-000')], pods: pods(64) }), {}).small).toBe(true);
+    expect(ownersScope(makeContext({ nodes: [makeGpuNode('mi355x-000')], pods: pods(65) }), {}).small).toBe(undefined);
   });
   it('an answer that found more than one page of nodes is asked again with the names, once the list has them', async () => {
     lib.resetHeadlamp();
