@@ -106,6 +106,15 @@ def test_detail_pages_cost_one_node_of_telemetry_whatever_the_cluster_size():
         assert pd["requests"] == 2 and out[1][kind]["requests"] == 2, out
         assert abs(pd["bytes"] - out[1][kind]["bytes"]) <= 0.05 * out[1][kind]["bytes"], out
         assert pd["p50_ms"] < 2 * out[16][one]["p50_ms"] + 5, out
+    # A Node detail opened on a cold store (no plugin page visited): its node's pods by field selector, its
+    # telemetry and its power history — three requests in ONE wave, the same bytes on 1 and 16 nodes. The
+    # reference mounts its full provider there: both cluster-wide lists + CRD + 3 serial requests, growing bytes.
+    cold, ref = out[16]["nodeDetailCold"], out[16]["nodeDetailColdReference"]
+    assert cold["requests"] == 3 and out[1]["nodeDetailCold"]["requests"] == 3, out
+    assert abs(cold["bytes"] - out[1]["nodeDetailCold"]["bytes"]) <= 0.05 * out[1]["nodeDetailCold"]["bytes"], out
+    assert cold["p50_ms"] < 2 * out[16]["nodeScoped"]["p50_ms"] + 5, out
+    assert ref["requests"] == 6 and ref["bytes"] > 3 * out[1]["nodeDetailColdReference"]["bytes"], out
+    assert ref["p50_ms"] > 3 * cold["p50_ms"], out
     # The GPU Pods page asks for pod attribution only: one series per allocated GPU.
     assert out[16]["podsPageOwners"]["requests"] == 1
     assert out[16]["podsPageOwners"]["bytes"] < 0.1 * out[16]["podClusterWide"]["bytes"], out
