@@ -404,8 +404,9 @@ function amdSchedule(request, clock) {
     },
     /** One page's Refresh button, as src/plugin.js wires it. */
     refreshPage: function (page) {
-      if (page === 'nodes') return Promise.all([store.refresh(), fetchNodesPage()]);
-      if (page === 'pods') return Promise.all([store.refresh(), fetchPodsPage()]);
+      // GPU Nodes / GPU Pods renew their telemetry only (plugin.js: the lists are watches).
+      if (page === 'nodes') return fetchNodesPage();
+      if (page === 'pods') return fetchPodsPage();
       if (page === 'metrics') return fetchMetricsPage();
       return store.refresh();
     },

@@ -101,12 +101,10 @@ export function createPlugin(env) {
     const pager = usePager();
     const t = telemetryScope(ctx, pager.state);
     const m = core.useGpuMetrics(t.enabled, false, 'topology', t.scope, t.small);
-    function refresh() {
-      ctx.refresh();
-      m.refresh();
-    }
+    // The node and pod lists are live watches; what Refresh can renew here is
+    // the telemetry (the DeviceConfigs are not on this page).
     return h(Page, {
-      vm: nodesView(ctx, { metrics: m.metrics, pager: pager.state }), onRefresh: refresh,
+      vm: nodesView(ctx, { metrics: m.metrics, pager: pager.state, fetching: m.fetching }), onRefresh: m.refresh,
       onPage: pager.onPage, onFilter: pager.onFilter,
     });
   }
@@ -122,12 +120,9 @@ export function createPlugin(env) {
     const pager = usePager();
     const o = ownersScope(ctx, pager.state);
     const m = core.useGpuOwners(o.enabled, o.pods, o.small);
-    function refresh() {
-      ctx.refresh();
-      m.refresh();
-    }
+    // As on GPU Nodes: the lists are watches; Refresh renews the attribution.
     return h(Page, {
-      vm: podsView(ctx, { metrics: m.metrics, pager: pager.state }), onRefresh: refresh,
+      vm: podsView(ctx, { metrics: m.metrics, pager: pager.state, fetching: m.fetching }), onRefresh: m.refresh,
       onPage: pager.onPage, onFilter: pager.onFilter,
     });
   }

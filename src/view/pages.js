@@ -779,7 +779,7 @@ export function nodesView(ctx, opts) {
     }, now, inputs);
     return head.concat(cards);
   }, now);
-  return page(BRAND + ' — Nodes', refreshButton('Refresh node data', ctx.refreshing), items);
+  return page(BRAND + ' — Nodes', refreshButton('Refresh node data', !!(opts && opts.fetching)), items);
 }
 
 const ownersCache = typeof WeakMap === 'function' ? new WeakMap() : null;
@@ -1015,7 +1015,7 @@ export function podsView(ctx, opts) {
   const items = memo('pods', [pg, ctx.index, ctx.error, assign], function () {
     return podsItems(ctx, now, assign, pg);
   }, now);
-  return page(BRAND + ' — Pods', refreshButton('Refresh pod data', ctx.refreshing), items);
+  return page(BRAND + ' — Pods', refreshButton('Refresh pod data', !!(opts && opts.fetching)), items);
 }
 
 function podsItems(ctx, now, assign, pg) {

@@ -128,6 +128,23 @@ describe('shared: refresh and StrictMode (' + tier + ')', () => {
     r.unmount();
   });
 
+  it('the GPU Nodes and GPU Pods Refresh buttons renew the telemetry only (the lists are watches)', async () => {
+    for (const [path, label] of [['/amd-gpu/nodes', 'Refresh node data'], ['/amd-gpu/pods', 'Refresh pod data']]) {
+      lib.resetHeadlamp();
+      resetSharedStores();
+      const fake = cluster();
+      const r = render(h(route(path)));
+      await r.settle();
+      const crd = crdCalls();
+      const live = fake.mock.calls.length;
+      r.click(r.byLabel(label));
+      await r.settle();
+      expect(crdCalls()).toBe(crd);
+      expect(fake.mock.calls.length).toBe(live + 1);
+      r.unmount();
+    }
+  });
+
   it('under StrictMode a route mounts with one CRD request and one live query', async () => {
     const fake = cluster();
     const r = render(h(route('/amd-gpu/metrics')), { strict: true });
