@@ -21,7 +21,9 @@ import https from 'https';
 import { createClusterStore } from '../src/api/clusterStore.js';
 import { createMetricsSource } from '../src/api/metrics.js';
 import { parsePrometheus, prometheusCandidates } from '../src/api/settings.js';
-import { devicePluginsView, metricsView, nodeDetailView, nodesView, overviewView, podDetailView, podsView } from '../src/view/pages.js';
+import {
+  NODE_SORTS, devicePluginsView, metricsView, nodeDetailView, nodesView, overviewView, podDetailView, podsView,
+} from '../src/view/pages.js';
 import { renderText, textSection } from '../src/view/text.js';
 
 const PAGES = ['overview', 'device-plugins', 'nodes', 'pods', 'metrics'];
@@ -31,6 +33,7 @@ function usage(msg) {
   process.stderr.write(
     'usage: amd-gpu-dash [--url http://127.0.0.1:8001] [--page ' + PAGES.join('|') + '|all|node:NAME|pod:NS/NAME]\n' +
       '                    [--watch SECONDS] [--filter TEXT] [--page-number N] [--per-page N]\n' +
+      '                    [--sort name|in-use|free|attention]\n' +
       '                    [--prometheus NAMESPACE/SERVICE:PORT] [--timeout MS] [--token TOKEN] [--insecure]\n' +
       '                    [--color] [--json]\n'
   );
@@ -51,6 +54,8 @@ export function parseArgs(argv) {
     else if (k === '--filter') a.pager.filter = v;
     else if (k === '--page-number') a.pager.page = Number(v) - 1;
     else if (k === '--per-page') a.pager.perPage = Number(v);
+    // The GPU node order (pages.js NODE_SORTS): name, most GPUs in use / free, not ready first.
+    else if (k === '--sort') a.pager.sort = v;
     else if (k === '--token') a.token = v;
     else if (k === '--prometheus') {
       const m = /^([^/]+)\/([^:]+):(.+)$/.exec(v || '');
@@ -78,6 +83,9 @@ export function parseArgs(argv) {
   else if (a.page !== 'all' && PAGES.indexOf(a.page) < 0) return { error: 'unknown page ' + a.page };
   if (!(a.watch >= 0) || !(a.timeout > 0)) return { error: 'bad --watch / --timeout' };
   if (!(a.pager.page >= 0) || (a.pager.perPage !== undefined && !(a.pager.perPage > 0))) return { error: 'bad --page-number / --per-page' };
+  if (a.pager.sort !== undefined && NODE_SORTS.map(function (o) { return o.value; }).indexOf(a.pager.sort) < 0) {
+    return { error: 'bad --sort (one of ' + NODE_SORTS.map(function (o) { return o.value; }).join(', ') + ')' };
+  }
   return a;
 }
 

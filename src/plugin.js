@@ -70,22 +70,23 @@ export function createPlugin(env) {
     const pager = usePager();
     return h(Page, {
       vm: devicePluginsView(ctx, { pager: pager.state }), onRefresh: ctx.refresh,
-      onPage: pager.onPage, onFilter: pager.onFilter,
+      onPage: pager.onPage, onFilter: pager.onFilter, onSort: pager.onSort,
     });
   }
 
   /**
-   * Pager state of a paged page (GPU Nodes, Metrics): {page, filter}. A new
-   * filter starts again at the first page.
+   * Pager state of a paged page: {page, filter, sort}. A new filter or order
+   * starts again at the first page.
    */
   function usePager() {
-    const st = React.useState({ page: 0, filter: '' });
+    const st = React.useState({ page: 0, filter: '', sort: 'name' });
     const pg = st[0];
     const setPg = st[1];
     return {
       state: pg,
-      onPage: function (p) { setPg(function (s) { return { page: p, filter: s.filter }; }); },
-      onFilter: function (f) { setPg({ page: 0, filter: f }); },
+      onPage: function (p) { setPg(function (s) { return { page: p, filter: s.filter, sort: s.sort }; }); },
+      onFilter: function (f) { setPg(function (s) { return { page: 0, filter: f, sort: s.sort }; }); },
+      onSort: function (o) { setPg(function (s) { return { page: 0, filter: s.filter, sort: o }; }); },
     };
   }
 
@@ -105,7 +106,7 @@ export function createPlugin(env) {
     // the telemetry (the DeviceConfigs are not on this page).
     return h(Page, {
       vm: nodesView(ctx, { metrics: m.metrics, pager: pager.state, fetching: m.fetching }), onRefresh: m.refresh,
-      onPage: pager.onPage, onFilter: pager.onFilter,
+      onPage: pager.onPage, onFilter: pager.onFilter, onSort: pager.onSort,
     });
   }
 
@@ -123,7 +124,7 @@ export function createPlugin(env) {
     // As on GPU Nodes: the lists are watches; Refresh renews the attribution.
     return h(Page, {
       vm: podsView(ctx, { metrics: m.metrics, pager: pager.state, fetching: m.fetching }), onRefresh: m.refresh,
-      onPage: pager.onPage, onFilter: pager.onFilter,
+      onPage: pager.onPage, onFilter: pager.onFilter, onSort: pager.onSort,
     });
   }
 
@@ -139,7 +140,7 @@ export function createPlugin(env) {
     const m = core.useGpuMetrics(t.enabled, true, 'gauges', t.scope, t.small);
     return h(Page, {
       vm: metricsView(ctx, m, { pager: pager.state }), onRefresh: m.refresh,
-      onPage: pager.onPage, onFilter: pager.onFilter,
+      onPage: pager.onPage, onFilter: pager.onFilter, onSort: pager.onSort,
     });
   }
 

@@ -138,6 +138,11 @@ export function renderSection(s) {
 export function renderPager(p) {
   return '<nav data-testid="pager" data-page="' + p.page + '" data-pages="' + p.pages + '" data-total="' + p.total + '">' +
     '<input aria-label="Filter ' + esc(p.noun) + ' by name" value="' + esc(p.filter) + '">' +
+    (p.sorts
+      ? '<select aria-label="Sort ' + esc(p.noun) + '">' + p.sorts.map(function (o) {
+        return '<option value="' + esc(o.value) + '"' + (o.value === p.sort ? ' selected' : '') + '>' + esc(o.label) + '</option>';
+      }).join('') + '</select>'
+      : '') +
     '<span>' + esc(pagerText(p)) + '</span>' +
     '<button aria-label="Previous page"' + (p.page > 0 ? '' : ' disabled') + '>‹</button>' +
     '<button aria-label="Next page"' + (p.page + 1 < p.pages ? '' : ' disabled') + '>›</button></nav>';

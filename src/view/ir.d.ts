@@ -150,6 +150,9 @@ export interface PagerItem {
   matched: number;
   filter: string;
   perPage: number;
+  /** the current order, when the list offers several (`sorts`) */
+  sort?: string;
+  sorts?: ReadonlyArray<{ value: string; label: string }>;
 }
 
 export interface RefreshButton {
@@ -178,7 +181,8 @@ export function loader(title: string): LoaderItem;
 export function page(title: string | null, refresh: RefreshButton | null, items: Array<Section | LoaderItem | PagerItem>): PageVM;
 export function pager(
   p: { page: number; pages: number; from: number; to: number; total: number; matched: number; filter: string; perPage: number },
-  noun: string
+  noun: string,
+  sorting?: { sort: string; sorts: ReadonlyArray<{ value: string; label: string }> }
 ): PagerItem;
 /** "Showing 17–24 of 1000 GPU nodes · page 3 of 125" */
 export function pagerText(p: PagerItem): string;

@@ -62,11 +62,17 @@ export function loader(title) {
  *          filter: string, perPage: number}} p
  * @param {string} noun  what is counted ("GPU nodes")
  */
-export function pager(p, noun) {
-  return {
+export function pager(p, noun, sorting) {
+  const item = {
     t: 'pager', key: 'pager', noun: noun, page: p.page, pages: p.pages, from: p.from, to: p.to,
     total: p.total, matched: p.matched, filter: p.filter, perPage: p.perPage,
   };
+  // Offered orders ({value, label}[]) and the current one, when the list can be ranked.
+  if (sorting && sorting.sorts) {
+    item.sort = sorting.sort;
+    item.sorts = sorting.sorts;
+  }
+  return item;
 }
 
 /** "Showing 17–32 of 1000 GPU nodes" (with the filter's match count when one is set). */

@@ -571,9 +571,62 @@ function nodeNameOf(n) {
  * @returns {{nodes: any[], names: string[], page: number, pages: number, from: number, to: number,
  *            total: number, matched: number, filter: string, perPage: number}}
  */
-export function nodePage(gpuNodes, state) {
-  const p = listPage('node', gpuNodes, state, nodeNameOf, nodeNameOf, NODES_PER_PAGE);
-  return p;
+export function nodePage(gpuNodes, state, index) {
+  const sort = nodeSortOf(state);
+  if (sort === 'name' || !gpuNodes) return listPage('node', gpuNodes, state, nodeNameOf, nodeNameOf, NODES_PER_PAGE);
+  // Another order: the list sorted once per node list and cluster index
+  // (allocations move with pod churn), then paged like the name order.
+  const sorted = memo('node-sort:' + sort, [gpuNodes, index], function () {
+    return gpuNodes.slice().sort(nodeComparator(sort, index));
+  });
+  return listPage('node-' + sort, sorted, state, nodeNameOf, nodeNameOf, NODES_PER_PAGE);
+}
+
+/**
+ * Orders a paged node view offers (pager `sort`): at 1,000 nodes a page of
+ * eight in name order does not show where the free GPUs or the broken nodes
+ * are, so the list can be ranked by the allocation the cluster index already
+ * holds (no request). Ties keep name order.
+ */
+export const NODE_SORTS = Object.freeze([
+  Object.freeze({ value: 'name', label: 'Name' }),
+  Object.freeze({ value: 'in-use', label: 'Most GPUs in use' }),
+  Object.freeze({ value: 'free', label: 'Most GPUs free' }),
+  Object.freeze({ value: 'attention', label: 'Not ready first' }),
+]);
+
+/** The pager state's sort if it is one of NODE_SORTS, else 'name'. */
+export function nodeSortOf(state) {
+  const want = state && state.sort;
+  for (let i = 0; i < NODE_SORTS.length; i++) if (NODE_SORTS[i].value === want) return want;
+  return 'name';
+}
+
+function nodeComparator(sort, index) {
+  function stats(n) {
+    return index && index.nodeStats ? index.nodeStats.get(nodeNameOf(n)) : undefined;
+  }
+  function inUse(n) {
+    const st = stats(n);
+    return st ? st.inUse || 0 : 0;
+  }
+  function free(n) {
+    const st = stats(n);
+    return st ? Math.max(0, (st.allocatable || 0) - (st.inUse || 0)) : 0;
+  }
+  function attention(n) {
+    if (typeof n === 'string') return 0;
+    if (!isNodeReady(n)) return 2;
+    return get(n, ['spec', 'unschedulable'], false) ? 1 : 0;
+  }
+  const rank = sort === 'in-use' ? inUse : sort === 'free' ? free : attention;
+  return function (a, b) {
+    const d = rank(b) - rank(a);
+    if (d) return d;
+    const x = nodeNameOf(a);
+    const y = nodeNameOf(b);
+    return x < y ? -1 : x > y ? 1 : 0;
+  };
 }
 
 /** GPU pods per page on the GPU Pods page (and operator pods on Device Plugins). */
@@ -625,7 +678,7 @@ function listPage(kind, all0, state, keyOf, textOf, perDefault) {
 /** Names of the GPU nodes a paged view shows ([] while the node list is loading). */
 export function visibleNodeNames(ctx, state) {
   if (!ctx || ctx.loading || !ctx.gpuNodes) return [];
-  return nodePage(ctx.gpuNodes, state).names;
+  return nodePage(ctx.gpuNodes, state, ctx.index).names;
 }
 
 /**
@@ -649,7 +702,7 @@ export function telemetryScope(ctx, state) {
   if (nodes === 'error') return { enabled: true, scope: undefined };
   if (nodes !== 'ready' && ctx.loading) return { enabled: true, scope: [], small: true };
   if (ctx.error && (!ctx.gpuNodes || ctx.gpuNodes.length === 0)) return { enabled: true, scope: undefined };
-  const names = nodePage(ctx.gpuNodes, state).names;
+  const names = nodePage(ctx.gpuNodes, state, ctx.index).names;
   return ctx.gpuNodes.length <= SMALL_CLUSTER_NODES ? { enabled: true, scope: names, small: true } : { enabled: true, scope: names };
 }
 
@@ -737,13 +790,13 @@ export function nodesView(ctx, opts) {
   if (ctx.loading) return page(null, null, [loader('Loading GPU node data...')]);
   // One page of nodes (NODES_PER_PAGE, name filter): the summary rows, the
   // cards and the telemetry the page asks for are all O(page), not O(cluster).
-  const pg = nodePage(ctx.gpuNodes, opts && opts.pager);
+  const pg = nodePage(ctx.gpuNodes, opts && opts.pager, ctx.index);
   // Live node power (the GPU Nodes query carries the power gauge for pod
   // attribution anyway): "watts|cap" per node, whole watts, so the head and
   // its rows rebuild only when a shown value changes.
   const power = nodePowerKeys(metrics);
   const head = memo('nodes-head', [pg, ctx.index, ctx.error, power.sig], function () {
-    return nodesHeadItems(ctx, now, power.byNode, pg);
+    return nodesHeadItems(ctx, now, power.byNode, pg, nodeSortOf(opts && opts.pager));
   }, now);
   const owners = ownersByNode(metrics);
   const xgmi = metrics ? metrics.xgmi : undefined;
@@ -908,7 +961,7 @@ function nodePowerCell(key) {
   return powerBar(Number(parts[0]), cap > 0 ? cap : null);
 }
 
-function nodesHeadItems(ctx, now, powerByNode, pg) {
+function nodesHeadItems(ctx, now, powerByNode, pg, sort) {
   const pw = powerByNode || {};
   const withPower = Object.keys(pw).length > 0;
   const items = [];
@@ -930,7 +983,7 @@ function nodesHeadItems(ctx, now, powerByNode, pg) {
     return items;
   }
 
-  items.push(pager(pg, 'GPU nodes'));
+  items.push(pager(pg, 'GPU nodes', { sort: sort, sorts: NODE_SORTS }));
   const idx = ctx.index;
   if (pg.nodes.length > 0) {
     items.push(
@@ -1331,7 +1384,7 @@ export function metricsView(ctx, mstate, opts) {
     // the page (m.scope); a cluster-wide one is paged over the nodes reporting.
     const scoped = Array.isArray(m.scope);
     const k8s = scoped && !ctx.loading && ctx.gpuNodes && ctx.gpuNodes.length > 0;
-    const pg = k8s ? nodePage(ctx.gpuNodes, opts && opts.pager) : nodePage(scoped ? m.scope : order, opts && opts.pager);
+    const pg = k8s ? nodePage(ctx.gpuNodes, opts && opts.pager, ctx.index) : nodePage(scoped ? m.scope : order, opts && opts.pager);
 
     const sr = mstate.series;
     if (sr && sr.power) {
@@ -1357,7 +1410,8 @@ export function metricsView(ctx, mstate, opts) {
       );
     }
 
-    items.push(pager(pg, k8s || scoped ? 'GPU nodes' : 'GPU nodes reporting'));
+    items.push(k8s ? pager(pg, 'GPU nodes', { sort: nodeSortOf(opts && opts.pager), sorts: NODE_SORTS })
+      : pager(pg, scoped ? 'GPU nodes' : 'GPU nodes reporting'));
     const covered = {};
     if (scoped) for (let i = 0; i < m.scope.length; i++) covered[m.scope[i]] = true;
     let matched = 0;

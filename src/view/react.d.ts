@@ -41,8 +41,19 @@ export interface Renderer {
   Section: ComponentType<{ s: IRSection | null }>;
   SectionImpl: ComponentType<{ s: IRSection | null }>;
   /** name filter + range shown + previous / next; the page owns the state */
-  Pager: ComponentType<{ p: PagerItem; onPage?: (page: number) => void; onFilter?: (filter: string) => void }>;
-  Page: ComponentType<{ vm: PageVM; onRefresh?: () => void; onPage?: (page: number) => void; onFilter?: (filter: string) => void }>;
+  Pager: ComponentType<{
+    p: PagerItem;
+    onPage?: (page: number) => void;
+    onFilter?: (filter: string) => void;
+    onSort?: (sort: string) => void;
+  }>;
+  Page: ComponentType<{
+    vm: PageVM;
+    onRefresh?: () => void;
+    onPage?: (page: number) => void;
+    onFilter?: (filter: string) => void;
+    onSort?: (sort: string) => void;
+  }>;
 }
 
 export function createRenderer(React: ReactLike, CC: CommonComponentsLike): Renderer;

@@ -308,8 +308,9 @@ export function createRenderer(React, CC) {
 
   /**
    * Pager of a long list (GPU nodes): name filter, the range shown and
-   * previous / next. The page component owns the state (props.onPage /
-   * props.onFilter); without handlers the controls are inert.
+   * previous / next, and the order when the list offers several (p.sorts).
+   * The page component owns the state (props.onPage / onFilter / onSort);
+   * without handlers the controls are inert.
    */
   function Pager(props) {
     const p = props.p;
@@ -325,6 +326,18 @@ export function createRenderer(React, CC) {
         style: { padding: '4px 6px', fontSize: '13px', minWidth: '180px' },
         onChange: function (e) { if (props.onFilter) props.onFilter(e.target.value); },
       }),
+      p.sorts
+        ? h(
+          'select',
+          {
+            'aria-label': 'Sort ' + p.noun,
+            value: p.sort,
+            style: { padding: '4px 6px', fontSize: '13px' },
+            onChange: function (e) { if (props.onSort) props.onSort(e.target.value); },
+          },
+          p.sorts.map(function (o) { return h('option', { key: o.value, value: o.value }, o.label); })
+        )
+        : null,
       h('span', { style: { fontSize: '13px', color: 'var(--mui-palette-text-secondary)' } }, pagerText(p)),
       h('button', {
         'aria-label': 'Previous page', disabled: !prev, style: buttonStyle(!prev),
@@ -365,7 +378,7 @@ export function createRenderer(React, CC) {
       header,
       vm.items.map(function (it, i) {
         if (it.t === 'loader') return h(CC.Loader, { key: 'loader-' + i, title: it.title });
-        if (it.t === 'pager') return h(Pager, { key: 'pager', p: it, onPage: props.onPage, onFilter: props.onFilter });
+        if (it.t === 'pager') return h(Pager, { key: 'pager', p: it, onPage: props.onPage, onFilter: props.onFilter, onSort: props.onSort });
         return h(Section, { key: it.key || i, s: it });
       })
     );

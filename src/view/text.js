@@ -11,6 +11,13 @@
 
 import { matrixCaption, pagerText } from './ir.js';
 
+/** " · sorted by <label>" for a pager ranked other than by name. */
+function sortText(p) {
+  if (!p.sorts || !p.sort || p.sort === p.sorts[0].value) return '';
+  for (let i = 0; i < p.sorts.length; i++) if (p.sorts[i].value === p.sort) return ' · sorted: ' + p.sorts[i].label;
+  return '';
+}
+
 const MARK = { success: '✓', warning: '!', error: '✗' };
 const ANSI = { success: '\u001b[32m', warning: '\u001b[33m', error: '\u001b[31m', reset: '\u001b[0m' };
 
@@ -153,7 +160,7 @@ export function renderText(vm, opts) {
   if (vm.title) out.push('# ' + vm.title, '');
   vm.items.forEach(function (it) {
     if (it.t === 'loader') out.push('… ' + it.title, '');
-    else if (it.t === 'pager') out.push('[' + pagerText(it) + ']', '');
+    else if (it.t === 'pager') out.push('[' + pagerText(it) + sortText(it) + ']', '');
     else out.push.apply(out, textSection(it, color).concat(['']));
   });
   return out.join('\n');

@@ -15,9 +15,10 @@ import { createPlugin } from '../../src/plugin.js';
 import { resetSharedStores } from '../../src/api/clusterStore.js';
 import { DEVICE_CONFIG_LIST_PATH } from '../../src/api/amdgpu.js';
 import {
-  ALL_NODES_SERIES, NODES_PER_PAGE, OVERVIEW_PLUGIN_PODS, PODS_PER_PAGE, clearViewMemo, devicePluginsView, metricsView,
-  nodePage, nodesView, overviewView, ownersScope, podsView, telemetryScope,
+  ALL_NODES_SERIES, NODE_SORTS, NODES_PER_PAGE, OVERVIEW_PLUGIN_PODS, PODS_PER_PAGE, clearViewMemo, devicePluginsView,
+  metricsView, nodePage, nodeSortOf, nodesView, overviewView, ownersScope, podsView, telemetryScope,
 } from '../../src/view/pages.js';
+import { renderText } from '../../src/view/text.js';
 import { countRows, findSection, pagerOf, pagerText, rowValue, sectionTitles } from '../../src/view/ir.js';
 import { renderPage } from '../../src/view/html.js';
 import {
@@ -69,6 +70,55 @@ describe('nodePage', () => {
       'Showing 1–8 of 10 matching "x-01" (20 GPU nodes) · page 1 of 2'
     );
     expect(pagerText(Object.assign({ noun: 'GPU nodes' }, nodePage(nodes, { filter: 'zz' })))).toBe('No GPU nodes match "zz"');
+  });
+});
+
+describe('node order', () => {
+  // 12 GPU nodes; mi355x-005 holds 6 GPUs, mi355x-009 holds 2, mi355x-003 is not ready.
+  function ctxSorted() {
+    const nodes = names(12).map((x) => makeGpuNode(x, { ready: x !== 'mi355x-003' }));
+    const pods = [makeGpuPod('big', { gpus: 6, node: 'mi355x-005' }), makeGpuPod('small', { gpus: 2, node: 'mi355x-009' })];
+    return makeContext({ nodes, pods });
+  }
+  it('name order by default and for an unknown sort', () => {
+    const ctx = ctxSorted();
+    expect(nodePage(ctx.gpuNodes, {}, ctx.index).names).toEqual(names(8));
+    expect(nodeSortOf({ sort: 'bogus' })).toBe('name');
+    expect(nodePage(ctx.gpuNodes, { sort: 'bogus' }, ctx.index).names).toEqual(names(8));
+  });
+  it('most GPUs in use / most free / not ready first, ties in name order', () => {
+    const ctx = ctxSorted();
+    expect(nodePage(ctx.gpuNodes, { sort: 'in-use' }, ctx.index).names.slice(0, 3)).toEqual(['mi355x-005', 'mi355x-009', 'mi355x-000']);
+    const free = nodePage(ctx.gpuNodes, { sort: 'free', page: 1 }, ctx.index).names;
+    expect(free.slice(-2)).toEqual(['mi355x-009', 'mi355x-005']);
+    expect(nodePage(ctx.gpuNodes, { sort: 'attention' }, ctx.index).names[0]).toBe('mi355x-003');
+  });
+  it('the sorted page is memoised on the list and the index; the filter applies after sorting', () => {
+    const ctx = ctxSorted();
+    expect(nodePage(ctx.gpuNodes, { sort: 'in-use' }, ctx.index)).toBe(nodePage(ctx.gpuNodes, { sort: 'in-use' }, ctx.index));
+    expect(nodePage(ctx.gpuNodes, { sort: 'in-use', filter: 'x-01' }, ctx.index).names).toEqual(['mi355x-010', 'mi355x-011']);
+    expect(nodePage(ctx.gpuNodes, { sort: 'in-use', filter: '00' }, ctx.index).names.slice(0, 3)).toEqual(['mi355x-005', 'mi355x-009', 'mi355x-000']);
+  });
+  it('the pager offers the orders; telemetry follows the sorted page', () => {
+    const ctx = ctxSorted();
+    const vm = nodesView(ctx, { pager: { sort: 'in-use' } });
+    const p = pagerOf(vm);
+    expect(p.sorts.map((o) => o.value)).toEqual(NODE_SORTS.map((o) => o.value));
+    expect(p.sort).toBe('in-use');
+    expect(cards(vm)[0]).toBe('mi355x-005');
+    expect(renderPage(vm)).toContain('<option value="in-use" selected>Most GPUs in use</option>');
+    expect(renderText(vm)).toContain('sorted: Most GPUs in use');
+    expect(telemetryScope(ctx, { sort: 'in-use' }).scope[0]).toBe('mi355x-005');
+  });
+  it('Metrics offers the same orders over the node list', async () => {
+    const ctx = ctxSorted();
+    const fake = prom({ data: exporterData(names(12)) });
+    const s = createMetricsSource({ request: fake });
+    const scope = telemetryScope(ctx, { sort: 'in-use' }).scope;
+    const m = await s.fetchGpuMetrics('gauges', { scope: scope, summary: true });
+    const vm = metricsView(ctx, { metrics: m, series: null, fetchError: null, fetching: false }, { pager: { sort: 'in-use' } });
+    expect(cards(vm)[0]).toBe('mi355x-005 — 8 × MI355X');
+    expect(pagerOf(vm).sort).toBe('in-use');
   });
 });
 

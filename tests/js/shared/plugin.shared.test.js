@@ -176,6 +176,21 @@ describe('shared: the pager drives what is rendered and fetched (' + tier + ')',
   });
 });
 
+describe('shared: the node order drives the page and its query (' + tier + ')', () => {
+  it('GPU Nodes: "Most GPUs in use" puts the busiest node first and scopes the query to that page', async () => {
+    const fake = cluster({ gpuNodes: nodeNames(12) }); // train-a (4 GPUs) on mi355x-000, train-b (2) on mi355x-001
+    lib.lists.Pod = [[makeGpuPod('hog', { gpus: 8, node: 'mi355x-010' })].concat(lib.lists.Pod[0]), null];
+    const r = render(h(route('/amd-gpu/nodes')));
+    await r.settle();
+    r.change(r.byLabel('Sort GPU nodes'), 'in-use');
+    await r.settle();
+    const titles = r.byTag('h2').map((n) => r.textOf(n)).filter((t) => /^mi355x-/.test(t));
+    expect(titles.slice(0, 3)).toEqual(['mi355x-010', 'mi355x-000', 'mi355x-001']);
+    expect(promQueries(fake).pop()).toContain('hostname=~"mi355x-010|mi355x-000|mi355x-001|');
+    r.unmount();
+  });
+});
+
 describe('shared: native-view sections (' + tier + ')', () => {
   it('Node detail on a cold store: the node\'s own pods, no cluster-wide list', async () => {
     cluster();

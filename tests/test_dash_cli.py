@@ -92,3 +92,14 @@ def test_pager_flags_select_the_page_and_filter(url):
     two = json.loads(run("--url", url, "--page", "nodes", "--json", "--per-page", "1", "--page-number", "2").stdout)
     assert [s["title"] for s in two["items"] if s["t"] == "section"][1:] == ["mi355x-001"]
     assert run("--url", url, "--page-number", "0").returncode == 2
+
+
+def test_sort_flag_orders_the_nodes(url):
+    r = run("--url", url, "--page", "nodes", "--json", "--sort", "attention")
+    assert r.returncode == 0, r.stderr
+    pager = [i for i in json.loads(r.stdout)["items"] if i["t"] == "pager"][0]
+    assert pager["sort"] == "attention" and [o["value"] for o in pager["sorts"]][0] == "name"
+    text = run("--url", url, "--page", "nodes", "--sort", "in-use")
+    assert text.returncode == 0 and "sorted: Most GPUs in use" in text.stdout
+    bad = run("--url", url, "--sort", "hottest")
+    assert bad.returncode == 2 and "bad --sort" in bad.stderr
