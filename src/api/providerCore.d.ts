@@ -75,6 +75,8 @@ export interface ProviderCore {
   storeWarm(): boolean;
   storeFor(cluster: string): ClusterStore;
   metricsSourceFor(cluster: string): MetricsSource;
+  /** The current cluster's key (per-cluster state: stores, view state). */
+  clusterKey(): string;
 }
 
 export function createProviderCore(React: unknown, lib: HeadlampLibLike, deps?: ProviderDeps): ProviderCore;

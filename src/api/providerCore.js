@@ -446,5 +446,7 @@ export function createProviderCore(React, lib, deps) {
     storeWarm: storeWarm,
     storeFor: storeFor,
     metricsSourceFor: metricsSourceFor,
+    /** The current cluster's key (per-cluster state: stores, view state). */
+    clusterKey: clusterKey,
   };
 }

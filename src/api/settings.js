@@ -167,6 +167,51 @@ export function saveSettings(value, storage) {
   return clean;
 }
 
+/** Key prefix of a page's view state (pager page / filter / order), per browser tab. */
+export const VIEW_STATE_KEY = 'headlamp-amd-gpu-plugin.view.';
+
+function defaultSessionStorage() {
+  try {
+    if (typeof sessionStorage !== 'undefined' && sessionStorage && typeof sessionStorage.getItem === 'function') return sessionStorage;
+  } catch (e) {
+    // storage disabled: the view state lives as long as the page
+  }
+  return null;
+}
+
+/**
+ * A paged page's view state saved in this tab's session ({page, filter,
+ * sort}), so leaving a page and coming back (Headlamp unmounts it) keeps the
+ * reader's place; null when nothing (valid) is stored. `storage` defaults to
+ * sessionStorage.
+ */
+export function loadViewState(key, storage) {
+  const st = storage === undefined ? defaultSessionStorage() : storage;
+  if (!st) return null;
+  try {
+    const v = JSON.parse(st.getItem(VIEW_STATE_KEY + key) || 'null');
+    if (!v || typeof v !== 'object') return null;
+    return {
+      page: typeof v.page === 'number' && v.page >= 0 && Math.floor(v.page) === v.page ? v.page : 0,
+      filter: typeof v.filter === 'string' ? v.filter.slice(0, 200) : '',
+      sort: typeof v.sort === 'string' ? v.sort.slice(0, 40) : 'name',
+    };
+  } catch (e) {
+    return null;
+  }
+}
+
+/** Persist a page's view state for this tab (see loadViewState); write errors are ignored. */
+export function saveViewState(key, value, storage) {
+  const st = storage === undefined ? defaultSessionStorage() : storage;
+  if (!st) return;
+  try {
+    st.setItem(VIEW_STATE_KEY + key, JSON.stringify({ page: value.page, filter: value.filter, sort: value.sort }));
+  } catch (e) {
+    // quota / disabled storage
+  }
+}
+
 /**
  * Interval poller with an injectable clock. `start(fn)` calls fn every
  * `periodSec` seconds, skipping a tick while the previous call's promise is

@@ -12,6 +12,8 @@ export interface PluginEnv {
   CommonComponents: unknown;
   deps?: ProviderDeps;
   settingsStorage?: { load: () => unknown; save: (v: unknown) => unknown };
+  /** Where the pages keep their pager state (default: sessionStorage). */
+  viewStorage?: { getItem: (k: string) => string | null; setItem: (k: string, v: string) => void } | null;
 }
 
 export interface NodeColumn {

@@ -35,6 +35,7 @@ import {
 } from './view/pages.js';
 import { createRenderer } from './view/react.js';
 import { createSettingsPage } from './view/settingsPage.js';
+import { loadViewState, saveViewState } from './api/settings.js';
 import { processColumns, ROUTES, SIDEBAR } from './routes.js';
 
 /** Plugin name used for `registerPluginSettings`. */
@@ -42,7 +43,8 @@ export const PLUGIN_NAME = 'amd-gpu';
 
 /**
  * @param {{React: any, lib: any, CommonComponents: Record<string, Function>,
- *          deps?: Parameters<typeof createProviderCore>[2], settingsStorage?: {load: Function, save: Function}}} env
+ *          deps?: Parameters<typeof createProviderCore>[2], settingsStorage?: {load: Function, save: Function},
+ *          viewStorage?: {getItem: Function, setItem: Function} | null}} env
  */
 export function createPlugin(env) {
   if (!env || !env.React || !env.lib || !env.CommonComponents) throw new Error('createPlugin: React, lib and CommonComponents are required');
@@ -67,7 +69,7 @@ export function createPlugin(env) {
   /** AMD GPU Operator DeviceConfigs and operand pods (reference DevicePluginsPage.tsx, C6). */
   function DevicePluginsPage() {
     const ctx = core.useAmdGpuContext();
-    const pager = usePager();
+    const pager = usePager('device-plugins');
     return h(Page, {
       vm: devicePluginsView(ctx, { pager: pager.state }), onRefresh: ctx.refresh,
       onPage: pager.onPage, onFilter: pager.onFilter, onSort: pager.onSort,
@@ -76,12 +78,20 @@ export function createPlugin(env) {
 
   /**
    * Pager state of a paged page: {page, filter, sort}. A new filter or order
-   * starts again at the first page.
+   * starts again at the first page. It is kept per cluster and page for this
+   * browser tab (settings.js loadViewState), so leaving the page and coming
+   * back — Headlamp unmounts it — returns to the same place.
    */
-  function usePager() {
-    const st = React.useState({ page: 0, filter: '', sort: 'name' });
+  function usePager(name) {
+    const key = core.clusterKey() + '|' + name;
+    const st = React.useState(function () {
+      return loadViewState(key, env.viewStorage) || { page: 0, filter: '', sort: 'name' };
+    });
     const pg = st[0];
     const setPg = st[1];
+    React.useEffect(function () {
+      saveViewState(key, pg, env.viewStorage);
+    }, [key, pg]);
     return {
       state: pg,
       onPage: function (p) { setPg(function (s) { return { page: p, filter: s.filter, sort: s.sort }; }); },
@@ -99,7 +109,7 @@ export function createPlugin(env) {
    */
   function NodesPage() {
     const ctx = core.useAmdGpuContext();
-    const pager = usePager();
+    const pager = usePager('nodes');
     const t = telemetryScope(ctx, pager.state);
     const m = core.useGpuMetrics(t.enabled, false, 'topology', t.scope, t.small);
     // The node and pod lists are live watches; what Refresh can renew here is
@@ -118,7 +128,7 @@ export function createPlugin(env) {
    */
   function PodsPage() {
     const ctx = core.useAmdGpuContext();
-    const pager = usePager();
+    const pager = usePager('pods');
     const o = ownersScope(ctx, pager.state);
     const m = core.useGpuOwners(o.enabled, o.pods, o.small);
     // As on GPU Nodes: the lists are watches; Refresh renews the attribution.
@@ -135,7 +145,7 @@ export function createPlugin(env) {
    */
   function MetricsPage() {
     const ctx = core.useAmdGpuContext();
-    const pager = usePager();
+    const pager = usePager('metrics');
     const t = telemetryScope(ctx, pager.state);
     const m = core.useGpuMetrics(t.enabled, true, 'gauges', t.scope, t.small);
     return h(Page, {

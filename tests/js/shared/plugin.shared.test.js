@@ -73,6 +73,8 @@ beforeEach(() => {
   resetSharedStores();
   clearViewMemo();
   invalidateSettings();
+  // jsdom has a sessionStorage: the pages keep their pager state there (plugin.js usePager).
+  if (typeof sessionStorage !== 'undefined' && sessionStorage) sessionStorage.clear();
 });
 
 describe('shared: every route mounts and renders its page (' + tier + ')', () => {
