@@ -23,6 +23,7 @@ Runs on its own asyncio loop in a daemon thread (:class:`ServerThread`).
 from __future__ import annotations
 
 import asyncio
+import concurrent.futures
 import random
 import json
 import re
@@ -256,22 +257,37 @@ def build_app(fc: FakeCluster) -> web.Application:
         if q is None:
             return web.json_response({"status": "error", "errorType": "bad_data", "error": "missing query"}, status=400)
         now = fc.now()
+        loop = asyncio.get_running_loop()
+        # Prometheus is its own server: its evaluation runs on its own thread,
+        # so a slow (Python) evaluation does not hold the apiserver's list
+        # responses on this event loop.
         if sub == "api/v1/query":
             t = float(req.query.get("time", now))
-            body = promql.query(fc.db, q, t)
+            body = await loop.run_in_executor(prom_pool, promql.query, fc.db, q, t)
         elif sub == "api/v1/query_range":
             try:
-                body = promql.query_range(fc.db, q, float(req.query["start"]), float(req.query["end"]),
-                                          float(req.query["step"]))
+                rng = float(req.query["start"]), float(req.query["end"]), float(req.query["step"])
             except (KeyError, ValueError):
+                rng = None
+            if rng is None:
                 body = {"status": "error", "errorType": "bad_data", "error": "bad range parameters"}
+            else:
+                body = await loop.run_in_executor(prom_pool, promql.query_range, fc.db, q, *rng)
         else:
             return _status(404, "NotFound", sub)
         if isinstance(body, promql.RawJSON):
             return web.Response(text=body, content_type="application/json")
         return web.json_response(body, status=200 if body["status"] == "success" else 400)
 
+    # One evaluation thread: the TSDB's lazily built indexes and caches are not
+    # shared between concurrent evaluations.
+    prom_pool = concurrent.futures.ThreadPoolExecutor(max_workers=1, thread_name_prefix="fake-prometheus")
+
+    async def stop_pool(_app):
+        prom_pool.shutdown(wait=False)
+
     app = web.Application(middlewares=[latency])
+    app.on_cleanup.append(stop_pool)
     app.router.add_get("/api/v1/nodes", nodes)
     app.router.add_get("/api/v1/pods", pods)
     app.router.add_get("/api/v1/namespaces/{ns}/pods", pods)
