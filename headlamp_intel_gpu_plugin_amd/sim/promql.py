@@ -249,6 +249,7 @@ _TOKEN_RE = re.compile(r"""
 
 _DUR = {"s": 1, "m": 60, "h": 3600, "d": 86400, "w": 604800}
 AGGREGATIONS = {"sum", "avg", "max", "min", "count"}
+RANK_AGGREGATIONS = {"topk", "bottomk"}
 RANGE_FUNCS = {"rate", "irate", "increase", "avg_over_time", "max_over_time", "min_over_time",
                "sum_over_time", "count_over_time", "last_over_time"}
 BIN_PREC = {"+": 1, "-": 1, "*": 2, "/": 2, "%": 2, "==": 0, "!=": 0, ">": 0, "<": 0, ">=": 0, "<=": 0,
@@ -385,6 +386,8 @@ class _Parser:
         if k == "ident":
             if v in AGGREGATIONS and self.peek(1)[1] in ("(", "by", "without"):
                 return self.aggregation()
+            if v in RANK_AGGREGATIONS and self.peek(1)[1] in ("(", "by", "without"):
+                return self.rank_aggregation()
             if v == "label_replace" and self.peek(1)[1] == "(":
                 self.i += 2
                 arg = self.expr(MIN_PREC)
@@ -421,6 +424,25 @@ class _Parser:
             lst = self.label_list()
             by, without = (lst, None) if kw == "by" else (None, lst)
         return ("agg", op, by, without, e)
+
+    def rank_aggregation(self):
+        """`topk(k, expr)` / `bottomk(k, expr)`, optionally `by (…)` / `without (…)`."""
+        op = self.take("ident")[1]
+        by = without = None
+        if self.peek()[1] in ("by", "without"):
+            kw = self.take("ident")[1]
+            lst = self.label_list()
+            by, without = (lst, None) if kw == "by" else (None, lst)
+        self.take("op", "(")
+        k = self.expr(MIN_PREC)
+        self.take("op", ",")
+        e = self.expr(MIN_PREC)
+        self.take("op", ")")
+        if self.peek()[1] in ("by", "without"):
+            kw = self.take("ident")[1]
+            lst = self.label_list()
+            by, without = (lst, None) if kw == "by" else (None, lst)
+        return ("rank", op, k, by, without, e)
 
     def selector(self, name: Optional[str]):
         matchers = []
@@ -573,11 +595,35 @@ class Evaluator:
                     r = float(len(vs))
                 res.append((glabels[k], r))
             return ("vector", res)
+        if kind == "rank":
+            return self._rank(node, t)
         if kind == "bin":
             return self._binary(node, t)
         if kind == "label_replace":
             return self._label_replace(node, t)
         raise PromQLError(f"cannot evaluate {kind}")
+
+    def _rank(self, node, t):
+        """topk / bottomk: the k largest (smallest) samples of each group, labels kept; NaN ranks last."""
+        _, op, k_node, by, without, e = node
+        kt, k = self.instant(k_node, t)
+        if kt != "scalar":
+            raise PromQLError(f"{op}: k must be a scalar")
+        typ, vec = self.instant(e, t)
+        if typ != "vector":
+            raise PromQLError(f"{op} over a scalar")
+        n = int(k)
+        groups: Dict[tuple, List] = {}
+        byt = tuple(by) if by is not None else None
+        for labels, v in vec:
+            key = self._group(labels, byt, without)[0] if (byt is not None or without is not None) else ()
+            groups.setdefault(key, []).append((labels, v))
+        out = []
+        sign = -1.0 if op == "topk" else 1.0
+        for members in groups.values():
+            members.sort(key=lambda lv: (math.isnan(lv[1]), sign * lv[1] if not math.isnan(lv[1]) else 0.0))
+            out.extend(members[:max(0, n)])
+        return ("vector", out)
 
     def _group(self, labels, byt, without):
         if byt is not None:

@@ -443,6 +443,42 @@ export function sizeFromRows(rows, tag) {
   return 0;
 }
 
+/** Node names are lowercase (RFC 1123): a name filter becomes a lowercase substring regex. */
+function hostnameFilter(filter) {
+  const f = String(filter || '').trim().toLowerCase();
+  return f ? ', hostname=~".*' + promString(regexLiteral(f)) + '.*"' : '';
+}
+
+/** Each GPU node's total GPU power (the ranking key), names matching `filter`. */
+export function nodePowerSum(filter) {
+  return 'sum by (hostname) ({__name__="' + SERIES.exporter.power + '"' + hostnameFilter(filter) + '})';
+}
+
+/**
+ * The GPU nodes of page `page` (0-based, `per` a page) ranked by total GPU
+ * power, highest first: `topk` of the pages so far minus `topk` of the pages
+ * before — Prometheus ranks, so the answer is one page whatever the cluster.
+ */
+export function powerRankQuery(page, per, filter) {
+  const r = nodePowerSum(filter);
+  const top = function (n) { return 'topk(' + n + ', ' + r + ')'; };
+  return page > 0 ? top(per * (page + 1)) + ' unless on(hostname) ' + top(per * page) : top(per);
+}
+
+/**
+ * A page of GPU nodes in power order, in ONE request: the view's series of
+ * the nodes the ranking picks (`and on(hostname)`), the ranking itself as
+ * `agg="rank"` rows (their order) and how many nodes are ranked
+ * (`agg="ranked"`, the pager's count).
+ */
+export function rankedClusterQuery(view, rank, withStatic) {
+  const s = powerRankQuery(rank.page, rank.per, rank.filter);
+  const st = withStatic !== false;
+  return '(' + exporterQuery(st, !st, view) + ') and on(hostname) (' + s + ')' +
+    ' or ' + sizeRow(s, 'rank') +
+    ' or ' + sizeRow('count(' + nodePowerSum(rank.filter) + ')', 'ranked');
+}
+
 /** Exporter series the cluster totals of the Metrics page summary sum or count. */
 function summaryNames() {
   const E = SERIES.exporter;
@@ -904,6 +940,17 @@ export function createMetricsSource(opts) {
   function fetchGpuMetrics(view, opts) {
     const v = view === undefined ? 'all' : view;
     if (METRIC_VIEWS.indexOf(v) < 0) return Promise.reject(new Error('fetchGpuMetrics: unknown view ' + JSON.stringify(view)));
+    if (opts && opts.rank) {
+      // A page of GPU nodes in power order (rankedClusterQuery).
+      const rank = {
+        by: 'power',
+        page: Math.max(0, Math.floor(opts.rank.page) || 0),
+        per: opts.rank.per > 0 ? Math.min(200, Math.floor(opts.rank.per)) : 8,
+        filter: String(opts.rank.filter || '').trim().toLowerCase(),
+      };
+      const rkey = 'rank|' + v + '|' + rank.page + '|' + rank.per + '|' + rank.filter + (opts.summary ? '|sum' : '');
+      return shared(rkey, function () { return rankedSnapshot(v, rank, !!opts.summary, rkey); });
+    }
     const scope = opts && Array.isArray(opts.scope) ? opts.scope.map(String) : null;
     if (!scope) return shared('gpus|' + v, function () { return gpuSnapshot(v); });
     const summary = !!opts.summary;
@@ -931,6 +978,44 @@ export function createMetricsSource(opts) {
     scopedState.set(key, e);
     if (scopedState.size > SCOPED_KEYS) scopedState.delete(scopedState.keys().next().value);
     return e;
+  }
+
+  /**
+   * Static series of a scoped answer: kept per node when the answer carried
+   * them (`withStatic`), else filled in from that per-node copy. A GPU the
+   * copy does not know yet marks its node to be re-read next time.
+   */
+  function scopeStatics(j, scope, withStatic) {
+    const now = clock.now();
+    if (withStatic) {
+      const per = {};
+      for (let i = 0; i < scope.length; i++) per[scope[i]] = {};
+      const sts = staticsOf(j.gpus);
+      for (let i = 0; i < j.gpus.length; i++) {
+        const g = j.gpus[i];
+        if (!per[g.nodeName]) per[g.nodeName] = {};
+        per[g.nodeName][gpuKey(g)] = sts[gpuKey(g)];
+      }
+      for (const n in per) scopeStatic[n] = { at: now, statics: per[n], links: (j.links && j.links[n]) || {} };
+      return;
+    }
+    const merged = {};
+    const links = {};
+    for (let i = 0; i < scope.length; i++) {
+      const e = scopeStatic[scope[i]];
+      if (!e) continue;
+      for (const k in e.statics) merged[k] = e.statics[k];
+      if (Object.keys(e.links).length) links[scope[i]] = e.links;
+    }
+    for (let i = 0; i < j.gpus.length; i++) {
+      const g = j.gpus[i];
+      if (merged[gpuKey(g)]) continue;
+      // Not known yet: re-read this node's statics next time.
+      if (scopeStatic[g.nodeName]) scopeStatic[g.nodeName].at = -Infinity;
+      else scopeStatic[g.nodeName] = { at: -Infinity, statics: {}, links: {} };
+    }
+    applyStatics(j.gpus, merged);
+    j.links = links;
   }
 
   function scopeNeedsStatic(scope) {
@@ -983,33 +1068,7 @@ export function createMetricsSource(opts) {
         // on every refresh).
         if (!found && source !== 'amd-exporter' && clock.now() >= noGpusUntil) return NOT_SCOPED;
         if (found) source = 'amd-exporter';
-        const now = clock.now();
-        if (withStatic) {
-          const per = {};
-          for (let i = 0; i < scope.length; i++) per[scope[i]] = {};
-          const sts = staticsOf(j.gpus);
-          for (let i = 0; i < j.gpus.length; i++) {
-            const g = j.gpus[i];
-            if (!per[g.nodeName]) per[g.nodeName] = {};
-            per[g.nodeName][gpuKey(g)] = sts[gpuKey(g)];
-          }
-          for (const n in per) scopeStatic[n] = { at: now, statics: per[n], links: (j.links && j.links[n]) || {} };
-        } else {
-          const merged = {};
-          const links = {};
-          for (let i = 0; i < scope.length; i++) {
-            const e = scopeStatic[scope[i]];
-            if (!e) continue;
-            for (const k in e.statics) merged[k] = e.statics[k];
-            if (Object.keys(e.links).length) links[scope[i]] = e.links;
-          }
-          for (let i = 0; i < j.gpus.length; i++) {
-            // A GPU the static copy does not know yet: re-read its node's statics next time.
-            if (!merged[gpuKey(j.gpus[i])] && scopeStatic[j.gpus[i].nodeName]) scopeStatic[j.gpus[i].nodeName].at = -Infinity;
-          }
-          applyStatics(j.gpus, merged);
-          j.links = links;
-        }
+        scopeStatics(j, scope, withStatic);
         const sized = small ? { count: reporting, limit: SMALL_CLUSTER_NODES, exceeded: reporting > SMALL_CLUSTER_NODES } : undefined;
         return scopedResult(st, base, q, j, scope, totals, v, sized);
       });
@@ -1039,6 +1098,55 @@ export function createMetricsSource(opts) {
       small: sized,
     };
     return st.last;
+  }
+
+  /**
+   * One page of GPU nodes ranked by total GPU power (rankedClusterQuery):
+   * `scope` is the page's nodes in rank order, `rank` the page, the ranked
+   * count and each node's watts. Static series ride along (the page's names
+   * are not known before the answer). Stale / null handling as scoped.
+   */
+  function rankedSnapshot(v, rank, summary, key) {
+    const st = scopedEntry(key);
+    return withPrometheus(function (base) {
+      // The page's names come with the answer: ask for the static series
+      // while the nodes last shown (most likely shown again) lack a copy.
+      const prev = st.last && st.last.scope;
+      const withStatic = !prev || prev.length === 0 || scopeNeedsStatic(prev);
+      const q = rankedClusterQuery(v, rank, withStatic) + (summary ? ' or ' + summaryQuery() : '');
+      return combined(base, q).then(function (res) {
+        if (!res.ok) return UNREACHABLE;
+        st.failures = 0;
+        const rows = res.rows;
+        const j = joinExporterResults(rows);
+        const ranked = [];
+        const watts = {};
+        for (let i = 0; i < rows.__agg.length; i++) {
+          const r = rows.__agg[i];
+          if (!isRow(r) || r.metric.agg !== 'rank' || typeof r.metric.hostname !== 'string') continue;
+          const w = num(r.value[1]);
+          ranked.push([r.metric.hostname, w === null ? -Infinity : w]);
+          watts[r.metric.hostname] = w;
+        }
+        ranked.sort(function (a, b) { return b[1] - a[1] || (a[0] < b[0] ? -1 : a[0] > b[0] ? 1 : 0); });
+        const names = ranked.map(function (x) { return x[0]; });
+        scopeStatics(j, names, withStatic);
+        const count = sizeFromRows(rows.__agg, 'ranked');
+        const totals = summary
+          ? totalsFromRows(rows.__agg.filter(function (r) { return r.metric.agg !== 'rank' && r.metric.agg !== 'ranked'; }))
+          : undefined;
+        if (j.gpus.length > 0 || count > 0) source = 'amd-exporter';
+        const out = scopedResult(st, base, q, j, names, totals, v, undefined);
+        out.rank = { by: rank.by, page: rank.page, per: rank.per, filter: rank.filter, count: count, watts: watts };
+        return out;
+      });
+    }, function () {
+      st.failures++;
+      if (st.last && st.failures < STALE_FAILURES) return Object.assign({}, st.last, { stale: true });
+      st.last = null;
+      invalidate();
+      return null;
+    });
   }
 
   // Until then a scoped fetch that finds nothing does not ask cluster-wide

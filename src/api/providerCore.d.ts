@@ -41,7 +41,10 @@ export interface MetricsSource {
    * `scope`: node names of a paged view (hostname=~); `summary`: also the cluster totals (GpuMetrics.totals);
    * `small`: every GPU when the cluster has at most SMALL_CLUSTER_GPUS, else `scope`'s (one request)
    */
-  fetchGpuMetrics(view?: 'all' | 'gauges' | 'topology', opts?: { scope: string[]; summary?: boolean; small?: boolean }): Promise<GpuMetrics | null>;
+  fetchGpuMetrics(
+    view?: 'all' | 'gauges' | 'topology',
+    opts?: { scope?: string[]; summary?: boolean; small?: boolean; rank?: { by: 'power'; page: number; per: number; filter: string } }
+  ): Promise<GpuMetrics | null>;
   fetchNodeMetrics(nodeName: string): Promise<GpuMetrics | null>;
   /** `pods`: "namespace/name" keys of one page of the Pods table; `small` as in fetchGpuMetrics */
   fetchGpuOwners(opts?: { pods: string[]; small?: boolean }): Promise<GpuMetrics | null>;
@@ -60,7 +63,8 @@ export interface ProviderCore {
     withSeries?: boolean,
     view?: 'all' | 'gauges' | 'topology',
     scope?: string[],
-    small?: boolean
+    small?: boolean,
+    rank?: { by: 'power'; page: number; per: number; filter: string }
   ): GpuMetricsState;
   useNodeGpuMetrics(nodeName: string | null, enabled?: boolean): GpuMetricsState;
   useGpuOwners(enabled?: boolean, pods?: string[], small?: boolean): GpuMetricsState;

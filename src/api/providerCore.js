@@ -251,6 +251,10 @@ export function createProviderCore(React, lib, deps) {
    * server-side aggregates — O(page) bytes on any cluster. Without `scope`
    * the whole cluster is fetched (terminal client, small clusters).
    *
+   * `rank` (pages.js telemetryScope, Metrics in power order): Prometheus
+   * picks the page (metrics.js rankedClusterQuery); the page's series are
+   * asked for once its names are in, a second round trip.
+   *
    * `small` (pages.js telemetryScope): the page may be the whole cluster —
    * every GPU when the cluster is small, else `scope`'s nodes, decided by
    * Prometheus (metrics.js smallClusterQuery). The query key then leaves out
@@ -261,7 +265,7 @@ export function createProviderCore(React, lib, deps) {
    * loading (MetricsPage.tsx:203-205): the two are independent and fetched in
    * parallel.
    */
-  function useGpuMetrics(enabled, withSeries, view, scope, small) {
+  function useGpuMetrics(enabled, withSeries, view, scope, small, rank) {
     const on = enabled === undefined ? true : enabled;
     const series = withSeries === undefined ? true : withSeries;
     const v = view || 'all';
@@ -272,9 +276,18 @@ export function createProviderCore(React, lib, deps) {
     const names = scoped ? scope.slice() : null;
     const sm = scoped && !!small;
     const ex = useState(false);
+    const rk = rank ? rank.by + ':' + rank.page + ':' + rank.per + ':' + rank.filter : null;
     const key = 'gpus|' + sourceKey(cluster, settings) + '|' + v + '|' + series + '|' + settings.seriesMinutes +
-      (sm ? smallKey(ex[0], names) : scoped ? '|scope:' + names.join(',') : '');
+      (rk ? '|rank:' + rk : sm ? smallKey(ex[0], names) : scoped ? '|scope:' + names.join(',') : '');
     const res = useMetricsFetch(on ? key : null, function () {
+      if (rk) {
+        // The ranked page's names come with the answer: its series follow it.
+        return source.fetchGpuMetrics(v, { rank: rank, summary: v === 'gauges' }).then(function (m) {
+          if (!series || !m) return [m, null];
+          return source.fetchSeries(settings.seriesMinutes * 60, seriesStepSec(settings), m.scope || [])
+            .then(function (sr) { return [m, sr]; });
+        });
+      }
       const opts = scoped ? { scope: names, summary: v === 'gauges', small: sm } : undefined;
       return Promise.all([
         source.fetchGpuMetrics(v, opts),

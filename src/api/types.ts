@@ -279,6 +279,10 @@ export interface GpuMetrics {
   scope?: string[];
   /** cluster totals of a paged snapshot, from server-side aggregates */
   totals?: GpuTotals;
+  /** a size-guarded (small-cluster) snapshot: GPU nodes (pods) reporting, and whether that was more than a page */
+  small?: { count: number; limit: number; exceeded: boolean };
+  /** a power-ranked page (metrics.js rankedSnapshot): `scope` is in rank order */
+  rank?: { by: 'power'; page: number; per: number; filter: string; count: number; watts: Record<string, number | null> };
 }
 
 /** Cluster totals (metrics.js totalsFromRows / summarizeMetrics + nodes reporting). */

@@ -146,8 +146,8 @@ export function createPlugin(env) {
   function MetricsPage() {
     const ctx = core.useAmdGpuContext();
     const pager = usePager('metrics');
-    const t = telemetryScope(ctx, pager.state);
-    const m = core.useGpuMetrics(t.enabled, true, 'gauges', t.scope, t.small);
+    const t = telemetryScope(ctx, pager.state, true);
+    const m = core.useGpuMetrics(t.enabled, true, 'gauges', t.scope, t.small, t.rank);
     return h(Page, {
       vm: metricsView(ctx, m, { pager: pager.state }), onRefresh: m.refresh,
       onPage: pager.onPage, onFilter: pager.onFilter, onSort: pager.onSort,

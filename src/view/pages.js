@@ -595,10 +595,19 @@ export const NODE_SORTS = Object.freeze([
   Object.freeze({ value: 'attention', label: 'Not ready first' }),
 ]);
 
-/** The pager state's sort if it is one of NODE_SORTS, else 'name'. */
-export function nodeSortOf(state) {
+/**
+ * The Metrics page adds an order only Prometheus knows: total GPU power,
+ * highest first. Prometheus ranks and returns that page's nodes in one
+ * request (metrics.js rankedClusterQuery); nodes without telemetry are not
+ * ranked.
+ */
+export const METRICS_SORTS = Object.freeze(NODE_SORTS.concat([Object.freeze({ value: 'power', label: 'Highest GPU power' })]));
+
+/** The pager state's sort if it is one of `sorts` (default NODE_SORTS), else 'name'. */
+export function nodeSortOf(state, sorts) {
   const want = state && state.sort;
-  for (let i = 0; i < NODE_SORTS.length; i++) if (NODE_SORTS[i].value === want) return want;
+  const list = sorts || NODE_SORTS;
+  for (let i = 0; i < list.length; i++) if (list[i].value === want) return want;
   return 'name';
 }
 
@@ -691,11 +700,22 @@ export function visibleNodeNames(ctx, state) {
  *     when the list arrives;
  *   * the names on the page once a larger cluster is listed;
  *   * cluster-wide (`scope` undefined) when the node list failed (e.g. RBAC
- *     denies listing nodes), so telemetry still shows.
- * @returns {{enabled: boolean, scope: (string[]|undefined), small?: boolean}}
+ *     denies listing nodes), so telemetry still shows;
+ *   * with `ranked` (Metrics) and the power order: `rank`, the page Prometheus
+ *     is to pick (metrics.js rankedClusterQuery).
+ * @returns {{enabled: boolean, scope?: (string[]|undefined), small?: boolean,
+ *            rank?: {by: string, page: number, per: number, filter: string}}}
  */
-export function telemetryScope(ctx, state) {
+export function telemetryScope(ctx, state, ranked) {
   if (!ctx) return { enabled: false, scope: [] };
+  // Power order (Metrics): Prometheus picks the page — no node list needed.
+  if (ranked && nodeSortOf(state, METRICS_SORTS) === 'power') {
+    const st = state || {};
+    return {
+      enabled: true,
+      rank: { by: 'power', page: Math.max(0, Math.floor(st.page) || 0), per: NODES_PER_PAGE, filter: (st.filter || '').trim().toLowerCase() },
+    };
+  }
   // The node list alone decides the page (the pod list of a large cluster
   // arrives later: tens of MB against the node list's few).
   const nodes = ctx.nodesState;
@@ -1384,7 +1404,11 @@ export function metricsView(ctx, mstate, opts) {
     // the page (m.scope); a cluster-wide one is paged over the nodes reporting.
     const scoped = Array.isArray(m.scope);
     const k8s = scoped && !ctx.loading && ctx.gpuNodes && ctx.gpuNodes.length > 0;
-    const pg = k8s ? nodePage(ctx.gpuNodes, opts && opts.pager, ctx.index) : nodePage(scoped ? m.scope : order, opts && opts.pager);
+    // Power order: Prometheus picked and ranked the page (metrics.js rankedSnapshot).
+    const pagerState = opts && opts.pager;
+    const rankedView = !!m.rank && nodeSortOf(pagerState, METRICS_SORTS) === 'power';
+    const pg = rankedView ? rankedPage(m, pagerState)
+      : k8s ? nodePage(ctx.gpuNodes, pagerState, ctx.index) : nodePage(scoped ? m.scope : order, pagerState);
 
     const sr = mstate.series;
     if (sr && sr.power) {
@@ -1410,8 +1434,9 @@ export function metricsView(ctx, mstate, opts) {
       );
     }
 
-    items.push(k8s ? pager(pg, 'GPU nodes', { sort: nodeSortOf(opts && opts.pager), sorts: NODE_SORTS })
-      : pager(pg, scoped ? 'GPU nodes' : 'GPU nodes reporting'));
+    items.push(rankedView ? pager(pg, 'GPU nodes reporting', { sort: 'power', sorts: METRICS_SORTS })
+      : k8s ? pager(pg, 'GPU nodes', { sort: nodeSortOf(pagerState, METRICS_SORTS), sorts: METRICS_SORTS })
+        : pager(pg, scoped ? 'GPU nodes' : 'GPU nodes reporting'));
     const covered = {};
     if (scoped) for (let i = 0; i < m.scope.length; i++) covered[m.scope[i]] = true;
     let matched = 0;
@@ -1440,6 +1465,19 @@ export function metricsView(ctx, mstate, opts) {
 
   void now;
   return page(BRAND + ' — Metrics', refreshButton('Refresh metrics', mstate.fetching || ctx.loading), items);
+}
+
+/** The pager page of a power-ranked answer: its nodes, in rank order, out of the nodes ranked. */
+function rankedPage(m, state) {
+  return memo('metrics-ranked-page', [m], function () {
+    const r = m.rank;
+    const count = Math.max(r.count, r.page * r.per + m.scope.length);
+    const from = Math.min(r.page * r.per, count);
+    return {
+      nodes: m.scope, names: m.scope, page: r.page, pages: Math.max(1, Math.ceil(count / r.per)), from: from,
+      to: from + m.scope.length, total: count, matched: count, filter: (state && state.filter) || '', perPage: r.per,
+    };
+  });
 }
 
 /**

@@ -8,21 +8,21 @@
  * node's telemetry per fetch; here what a page renders and fetches is bounded
  * by NODES_PER_PAGE, whatever the cluster size.
  */
-import React, { render } from './stubs/react.js';
+import React, { render, textOf as textOfNode } from './stubs/react.js';
 import * as lib from './stubs/headlamp-lib.js';
 import * as CC from './stubs/CommonComponents.js';
 import { createPlugin } from '../../src/plugin.js';
 import { resetSharedStores } from '../../src/api/clusterStore.js';
 import { DEVICE_CONFIG_LIST_PATH } from '../../src/api/amdgpu.js';
 import {
-  ALL_NODES_SERIES, NODE_SORTS, NODES_PER_PAGE, OVERVIEW_PLUGIN_PODS, PODS_PER_PAGE, clearViewMemo, devicePluginsView,
+  ALL_NODES_SERIES, METRICS_SORTS, NODE_SORTS, NODES_PER_PAGE, OVERVIEW_PLUGIN_PODS, PODS_PER_PAGE, clearViewMemo, devicePluginsView,
   metricsView, nodePage, nodeSortOf, nodesView, overviewView, ownersScope, podsView, telemetryScope,
 } from '../../src/view/pages.js';
 import { renderText } from '../../src/view/text.js';
 import { countRows, findSection, pagerOf, pagerText, rowValue, sectionTitles } from '../../src/view/ir.js';
 import { renderPage } from '../../src/view/html.js';
 import {
-  SERIES, SMALL_CLUSTER_NODES, SMALL_CLUSTER_PODS, TOTAL_SERIES, createMetricsSource, hostnameMatcher, regexLiteral, scopedSeriesQuery, summarizeMetrics,
+  SERIES, SMALL_CLUSTER_NODES, SMALL_CLUSTER_PODS, TOTAL_SERIES, createMetricsSource, powerRankQuery, hostnameMatcher, regexLiteral, scopedSeriesQuery, summarizeMetrics,
   summaryQuery, totalsFromRows, joinExporterResults, splitByName,
 } from '../../src/api/metrics.js';
 import { makeContext, makeDeviceConfig, makeGpuNode, makeGpuPod, makePluginPod } from './fixtures.js';
@@ -119,6 +119,85 @@ describe('node order', () => {
     const vm = metricsView(ctx, { metrics: m, series: null, fetchError: null, fetching: false }, { pager: { sort: 'in-use' } });
     expect(cards(vm)[0]).toBe('mi355x-005 — 8 × MI355X');
     expect(pagerOf(vm).sort).toBe('in-use');
+  });
+});
+
+describe('Metrics in power order: Prometheus ranks the page', () => {
+  // 12 reporting nodes; node i draws 700 + g + 10 * (i % 5) W per GPU, so the ranking is not the name order.
+  function hot(n) {
+    const d = exporterData(names(n));
+    d[SERIES.exporter.power].forEach((r) => {
+      const i = Number(r.metric.hostname.slice(-3));
+      r.value = [r.value[0], String(parseFloat(r.value[1]) + 10 * (i % 5))];
+    });
+    return d;
+  }
+  const rank = (page, filter) => ({ by: 'power', page: page, per: 8, filter: filter || '' });
+  it('the rank query pages with topk and `unless`; a name filter is a lowercase substring', () => {
+    expect(powerRankQuery(0, 8, '')).toBe('topk(8, sum by (hostname) ({__name__="gpu_power_usage"}))');
+    expect(powerRankQuery(2, 8, 'Rack-1')).toContain('topk(24, sum by (hostname) ({__name__="gpu_power_usage", hostname=~".*rack-1.*"})) unless on(hostname) topk(16,');
+    expect(powerRankQuery(0, 8, 'a.b')).toContain('hostname=~".*a\\\\.b.*"');
+  });
+  it('one request answers the page in power order, the ranked count and the totals', async () => {
+    const fake = prom({ data: hot(12) });
+    const s = createMetricsSource({ request: fake });
+    const m = await s.fetchGpuMetrics('gauges', { rank: rank(0), summary: true });
+    expect(fake.mock.calls).toHaveLength(1);
+    expect(m.scope.slice(0, 3)).toEqual(['mi355x-004', 'mi355x-009', 'mi355x-003']);
+    expect(m.rank.count).toBe(12);
+    expect(new Set(m.gpus.map((g) => g.nodeName)).size).toBe(8);
+    expect(m.totals.gpus).toBe(96);
+    const p1 = await s.fetchGpuMetrics('gauges', { rank: rank(1), summary: true });
+    expect(p1.scope).toHaveLength(4);
+    expect(p1.scope.filter((x) => m.scope.indexOf(x) >= 0)).toEqual([]);
+    // The same page again: its nodes' static series are cached, the query is live-only, the GPUs keep their caps.
+    const again = await s.fetchGpuMetrics('gauges', { rank: rank(0), summary: true });
+    const qs = decoded(fake);
+    const pagePart = (q) => q.split(') and on(hostname)')[0];
+    expect(pagePart(qs[0])).toContain(SERIES.exporter.vramTotal);
+    expect(pagePart(qs[2])).not.toContain(SERIES.exporter.vramTotal);
+    expect(again.gpus[0].vramTotalBytes).toBeGreaterThan(0);
+  });
+  it('telemetryScope asks for the ranked page on Metrics only', () => {
+    const ctx = ctxOf(12);
+    expect(telemetryScope(ctx, { sort: 'power', page: 1, filter: ' X-0 ' }, true)).toEqual({ enabled: true, rank: { by: 'power', page: 1, per: 8, filter: 'x-0' } });
+    expect(telemetryScope(ctx, { sort: 'power' }).rank).toBe(undefined); // GPU Nodes: no power order
+    expect(METRICS_SORTS.map((o) => o.value)).toEqual(NODE_SORTS.map((o) => o.value).concat(['power']));
+  });
+  it('metricsView shows the ranked page: cards in power order, pager over the nodes ranked', async () => {
+    const s = createMetricsSource({ request: prom({ data: hot(12) }) });
+    const m = await s.fetchGpuMetrics('gauges', { rank: rank(0), summary: true });
+    const vm = metricsView(ctxOf(12), { metrics: m, series: null, fetchError: null, fetching: false }, { pager: { sort: 'power' } });
+    expect(cards(vm).slice(0, 2)).toEqual(['mi355x-004 — 8 × MI355X', 'mi355x-009 — 8 × MI355X']);
+    const p = pagerOf(vm);
+    expect([p.sort, p.noun, p.pages, p.total]).toEqual(['power', 'GPU nodes reporting', 2, 12]);
+    expect(pagerText(p)).toBe('Showing 1–8 of 12 GPU nodes reporting · page 1 of 2');
+  });
+  it('plugin: choosing "Highest GPU power" on Metrics sends one ranked query, then the page\'s series', async () => {
+    lib.resetHeadlamp();
+    lib.lists.Node = [names(12).map((x) => makeGpuNode(x)), null];
+    lib.lists.Pod = [[], null];
+    const fake = prom({ data: hot(12) });
+    lib.api.handler = (p) => {
+      if (p === DEVICE_CONFIG_LIST_PATH) return Promise.resolve({ kind: 'List', metadata: {}, items: [] });
+      if (p.indexOf('/proxy/api/v1/') >= 0) return fake(p);
+      return Promise.reject(Object.assign(new Error('503'), { status: 503 }));
+    };
+    const plugin = createPlugin({ React: React, lib: lib, CommonComponents: CC });
+    const r = render(h(plugin.routeComponent('metrics')));
+    await r.settle();
+    const before = fake.mock.calls.length;
+    r.change(r.getByLabelText('Sort GPU nodes'), 'power');
+    await r.settle();
+    const sent = decoded(fake).slice(before);
+    expect(sent.filter((q) => q.indexOf('topk(8,') >= 0)).toHaveLength(1);
+    const range = sent.filter((q) => q.indexOf('/query_range') >= 0);
+    expect(range).toHaveLength(1);
+    expect(range[0]).toContain('hostname=~"mi355x-004|mi355x-009|');
+    expect(r.text()).toContain('Showing 1–8 of 12 GPU nodes reporting');
+    const titles = r.byTag('h2').map((n) => textOfNode(n)).filter((t) => /^mi355x-/.test(t));
+    expect(titles[0]).toBe('mi355x-004 — 8 × MI355X');
+    r.unmount();
   });
 });
 

@@ -77,6 +77,21 @@ function term(q, rows) {
     const pass = guard[3] === '<=' ? n <= Number(guard[4]) : n > Number(guard[4]);
     return pass ? term(guard[1], rows) : [];
   }
+  // rankedClusterQuery: the page's rows, the ranking, the ranked count.
+  const onRank = /^\((.*)\) and on\(hostname\) \((topk\(.*)\)$/.exec(q);
+  if (onRank) {
+    const ranked = rankOf(onRank[2], rows) || [];
+    const keep = {};
+    ranked.forEach((x) => (keep[x[0]] = true));
+    return term(onRank[1], rows).filter((r) => keep[r.metric.hostname]);
+  }
+  const rankRow = /^label_replace\((topk\(.*\)), "agg", "rank", "", ""\)$/.exec(q);
+  if (rankRow) return (rankOf(rankRow[1], rows) || []).map((x) => vec({ hostname: x[0], agg: 'rank' }, x[1]));
+  const rankedCount = /^label_replace\(count\((sum by \(hostname\) .*)\), "agg", "ranked", "", ""\)$/.exec(q);
+  if (rankedCount) {
+    const n = (powerSums(rankedCount[1], rows) || []).length;
+    return n ? [vec({ agg: 'ranked' }, n)] : [];
+  }
   const sized = /^label_replace\((count\(count by .*\)), "agg", "(\w+)", "", ""\)$/.exec(q);
   if (sized) {
     const n = countOf(sized[1], rows);
@@ -115,6 +130,29 @@ function term(q, rows) {
     }
   }
   return rows.filter((r) => re.test(r.metric.__name__ || '') && hostOk(r.metric.hostname));
+}
+
+/** metrics.js nodePowerSum over `rows`: [[hostname, watts], …] (null for another shape). */
+function powerSums(expr, rows) {
+  const m = /^sum by \(hostname\) \(\{__name__="([a-z_]+)"(?:, hostname=~"(.*)")?\}\)$/.exec(expr);
+  if (!m) return null;
+  const re = m[2] !== undefined ? new RegExp('^(?:' + m[2].replace(/\\\\/g, '\\') + ')$') : null;
+  const by = {};
+  rows.forEach((r) => {
+    if (r.metric.__name__ !== m[1] || (re && !re.test(r.metric.hostname || ''))) return;
+    by[r.metric.hostname] = (by[r.metric.hostname] || 0) + parseFloat(r.value[1]);
+  });
+  return Object.keys(by).map((h) => [h, by[h]]);
+}
+
+/** metrics.js powerRankQuery: the ranked page, [[hostname, watts], …] (null for another shape). */
+function rankOf(expr, rows) {
+  const m = /^topk\((\d+), (.*?)\)(?: unless on\(hostname\) topk\((\d+), (.*)\))?$/.exec(expr);
+  if (!m) return null;
+  const all = powerSums(m[2], rows);
+  if (!all) return null;
+  all.sort((a, b) => b[1] - a[1] || (a[0] < b[0] ? -1 : 1));
+  return all.slice(m[3] ? Number(m[3]) : 0, Number(m[1]));
 }
 
 /** metrics.js gpuNodeCount / gpuPodCount over `rows` (null for another shape). */

@@ -193,6 +193,19 @@ describe('shared: the node order drives the page and its query (' + tier + ')', 
   });
 });
 
+describe('shared: Metrics in power order (' + tier + ')', () => {
+  it('"Highest GPU power" asks Prometheus for the ranked page and shows the hottest node first', async () => {
+    const fake = cluster({ gpuNodes: nodeNames(12) });
+    const r = render(h(route('/amd-gpu/metrics')));
+    await r.settle();
+    r.change(r.byLabel('Sort GPU nodes'), 'power');
+    await r.settle();
+    expect(promQueries(fake).filter((q) => q.indexOf('topk(8,') >= 0).length).toBeGreaterThan(0);
+    expect(r.text()).toContain('Showing 1–8 of 12 GPU nodes reporting');
+    r.unmount();
+  });
+});
+
 describe('shared: native-view sections (' + tier + ')', () => {
   it('Node detail on a cold store: the node\'s own pods, no cluster-wide list', async () => {
     cluster();

@@ -289,3 +289,33 @@ def test_size_guarded_small_cluster_query():
     assert _vec(query(d, "1 and on() (count(gpu_power_usage) > 1000)", 100.0)) == []
     with pytest.raises(promql.PromQLError):
         promql.Evaluator(d).instant(parse("1 and on() (count(gpu_power_usage) > 1)"), 100.0)
+
+
+def test_topk_bottomk_and_the_power_ranked_page():
+    """topk / bottomk (optionally by), and metrics.js rankedClusterQuery: the page's rows, the rank rows, the count."""
+    import subprocess
+
+    from headlamp_intel_gpu_plugin_amd.utils.nodebridge import ROOT, node_binary
+
+    d = TSDB()
+    watts = {"a": 100.0, "b": 300.0, "c": 200.0, "d": 50.0, "e": 250.0}
+    for node, w in watts.items():
+        for g in range(2):
+            d.add(Series({"__name__": "gpu_power_usage", "hostname": node, "gpu_id": str(g)}, fn=lambda t, w=w: w))
+            d.add(Series({"__name__": "gpu_gfx_activity", "hostname": node, "gpu_id": str(g)}, fn=lambda t: 10.0))
+    top2 = _vec(query(d, "topk(2, sum by (hostname) (gpu_power_usage))", 100.0))
+    assert [(r["metric"]["hostname"], float(r["value"][1])) for r in top2] == [("b", 600.0), ("e", 500.0)]
+    page2 = _vec(query(d, "topk(4, sum by (hostname) (gpu_power_usage)) unless on(hostname) "
+                          "topk(2, sum by (hostname) (gpu_power_usage))", 100.0))
+    assert {r["metric"]["hostname"] for r in page2} == {"c", "a"}
+    low = _vec(query(d, "bottomk by (hostname) (1, gpu_power_usage)", 100.0))
+    assert len(low) == 5 and all(r["metric"]["__name__"] == "gpu_power_usage" for r in low)
+
+    js = ("import('./src/api/metrics.js').then(m => process.stdout.write("
+          "m.rankedClusterQuery('gauges', {page: 1, per: 2, filter: ''})))")
+    q = subprocess.run([node_binary(), "-e", js], cwd=ROOT, capture_output=True, text=True, timeout=60).stdout
+    rows = _vec(query(d, q, 100.0))
+    data = {r["metric"]["hostname"] for r in rows if "agg" not in r["metric"]}
+    ranks = {r["metric"]["hostname"]: float(r["value"][1]) for r in rows if r["metric"].get("agg") == "rank"}
+    (count,) = [float(r["value"][1]) for r in rows if r["metric"].get("agg") == "ranked"]
+    assert data == {"c", "a"} and ranks == {"c": 400.0, "a": 200.0} and count == 5
