@@ -22,7 +22,7 @@ import { createClusterStore } from '../src/api/clusterStore.js';
 import { createMetricsSource } from '../src/api/metrics.js';
 import { parsePrometheus, prometheusCandidates } from '../src/api/settings.js';
 import {
-  NODE_SORTS, devicePluginsView, metricsView, nodeDetailView, nodesView, overviewView, podDetailView, podsView,
+  NODE_SORTS, POD_SORTS, devicePluginsView, metricsView, nodeDetailView, nodesView, overviewView, podDetailView, podsView,
 } from '../src/view/pages.js';
 import { renderText, textSection } from '../src/view/text.js';
 
@@ -33,7 +33,7 @@ function usage(msg) {
   process.stderr.write(
     'usage: amd-gpu-dash [--url http://127.0.0.1:8001] [--page ' + PAGES.join('|') + '|all|node:NAME|pod:NS/NAME]\n' +
       '                    [--watch SECONDS] [--filter TEXT] [--page-number N] [--per-page N]\n' +
-      '                    [--sort name|in-use|free|attention]\n' +
+      '                    [--sort name|in-use|free|attention (nodes) | gpus|newest|attention (pods)]\n' +
       '                    [--prometheus NAMESPACE/SERVICE:PORT] [--timeout MS] [--token TOKEN] [--insecure]\n' +
       '                    [--color] [--json]\n'
   );
@@ -83,9 +83,10 @@ export function parseArgs(argv) {
   else if (a.page !== 'all' && PAGES.indexOf(a.page) < 0) return { error: 'unknown page ' + a.page };
   if (!(a.watch >= 0) || !(a.timeout > 0)) return { error: 'bad --watch / --timeout' };
   if (!(a.pager.page >= 0) || (a.pager.perPage !== undefined && !(a.pager.perPage > 0))) return { error: 'bad --page-number / --per-page' };
-  if (a.pager.sort !== undefined && NODE_SORTS.map(function (o) { return o.value; }).indexOf(a.pager.sort) < 0) {
-    return { error: 'bad --sort (one of ' + NODE_SORTS.map(function (o) { return o.value; }).join(', ') + ')' };
-  }
+  // Node orders apply to the GPU node pages, pod orders to GPU Pods ('name' to both).
+  const sorts = NODE_SORTS.concat(POD_SORTS).map(function (o) { return o.value; })
+    .filter(function (v, i, all) { return all.indexOf(v) === i; });
+  if (a.pager.sort !== undefined && sorts.indexOf(a.pager.sort) < 0) return { error: 'bad --sort (one of ' + sorts.join(', ') + ')' };
   return a;
 }
 

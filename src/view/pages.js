@@ -655,7 +655,50 @@ function podSearchText(p) {
  * "namespace/name" keys; `nodes` holds the pod objects.
  */
 export function podPage(pods, state, kind) {
-  return listPage(kind || 'pod', pods, state, podKeyOf, podSearchText, PODS_PER_PAGE);
+  const k = kind || 'pod';
+  const sort = k === 'pod' ? podSortOf(state) : 'name';
+  if (sort === 'name' || !pods) return listPage(k, pods, state, podKeyOf, podSearchText, PODS_PER_PAGE);
+  const sorted = memo('pod-sort:' + sort, [pods], function () { return pods.slice().sort(podComparator(sort)); });
+  return listPage(k + '-' + sort, sorted, state, podKeyOf, podSearchText, PODS_PER_PAGE);
+}
+
+/**
+ * Orders of the GPU Pods table (pager `sort`), from the pod objects alone:
+ * namespace / name (the list order), most GPUs held first, newest first,
+ * and not running first (pending / failed before running). Ties keep
+ * namespace / name order.
+ */
+export const POD_SORTS = Object.freeze([
+  Object.freeze({ value: 'name', label: 'Namespace / name' }),
+  Object.freeze({ value: 'gpus', label: 'Most GPUs held' }),
+  Object.freeze({ value: 'newest', label: 'Newest first' }),
+  Object.freeze({ value: 'attention', label: 'Not running first' }),
+]);
+
+/** The pager state's sort if it is one of POD_SORTS, else 'name'. */
+export function podSortOf(state) {
+  const want = state && state.sort;
+  for (let i = 0; i < POD_SORTS.length; i++) if (POD_SORTS[i].value === want) return want;
+  return 'name';
+}
+
+function podComparator(sort) {
+  function created(p) {
+    const t = Date.parse(get(p, ['metadata', 'creationTimestamp'], ''));
+    return isNaN(t) ? 0 : t;
+  }
+  function notRunning(p) {
+    const ph = podFacts(p).phase;
+    return ph === 'Running' || ph === 'Succeeded' ? 0 : 1;
+  }
+  const rank = sort === 'gpus' ? function (p) { return podFacts(p).gpus; } : sort === 'newest' ? created : notRunning;
+  return function (a, b) {
+    const d = rank(b) - rank(a);
+    if (d) return d;
+    const x = podKeyOf(a);
+    const y = podKeyOf(b);
+    return x < y ? -1 : x > y ? 1 : 0;
+  };
 }
 
 /**
@@ -1085,13 +1128,14 @@ export function podsView(ctx, opts) {
   // One page of the GPU pod table (PODS_PER_PAGE, filter on namespace/name
   // and node): the reference lists every GPU pod (PodsPage.tsx:201-236).
   const pg = podPage(ctx.gpuPods, opts && opts.pager);
-  const items = memo('pods', [pg, ctx.index, ctx.error, assign], function () {
-    return podsItems(ctx, now, assign, pg);
+  const sort = podSortOf(opts && opts.pager);
+  const items = memo('pods', [pg, ctx.index, ctx.error, assign, sort], function () {
+    return podsItems(ctx, now, assign, pg, sort);
   }, now);
   return page(BRAND + ' — Pods', refreshButton('Refresh pod data', !!(opts && opts.fetching)), items);
 }
 
-function podsItems(ctx, now, assign, pg) {
+function podsItems(ctx, now, assign, pg, sort) {
   const items = [];
   if (ctx.error) items.push(errorSection(ctx.error));
   const pods = ctx.gpuPods;
@@ -1121,7 +1165,7 @@ function podsItems(ctx, now, assign, pg) {
     const exact = assign && Object.keys(assign).length > 0;
     const cols = ['Name', 'Namespace', 'Node', 'Phase', 'GPU Resources', 'Restarts', 'Age'];
     if (exact) cols.splice(5, 0, 'Assigned GPUs', 'GPU Power');
-    items.push(pager(pg, 'GPU pods'));
+    items.push(pager(pg, 'GPU pods', { sort: sort, sorts: POD_SORTS }));
     items.push(
       section('All GPU Pods', [
         table(

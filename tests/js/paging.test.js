@@ -16,7 +16,8 @@ import { resetSharedStores } from '../../src/api/clusterStore.js';
 import { DEVICE_CONFIG_LIST_PATH } from '../../src/api/amdgpu.js';
 import {
   ALL_NODES_SERIES, METRICS_SORTS, NODE_SORTS, NODES_PER_PAGE, OVERVIEW_PLUGIN_PODS, PODS_PER_PAGE, clearViewMemo, devicePluginsView,
-  metricsView, nodePage, nodeSortOf, nodesView, overviewView, ownersScope, podsView, telemetryScope,
+  metricsView, nodePage, nodeSortOf, nodesView, overviewView, ownersScope, podPage, podSortOf, podsView, POD_SORTS,
+  telemetryScope,
 } from '../../src/view/pages.js';
 import { renderText } from '../../src/view/text.js';
 import { countRows, findSection, pagerOf, pagerText, rowValue, sectionTitles } from '../../src/view/ir.js';
@@ -119,6 +120,38 @@ describe('node order', () => {
     const vm = metricsView(ctx, { metrics: m, series: null, fetchError: null, fetching: false }, { pager: { sort: 'in-use' } });
     expect(cards(vm)[0]).toBe('mi355x-005 — 8 × MI355X');
     expect(pagerOf(vm).sort).toBe('in-use');
+  });
+});
+
+describe('GPU Pods order', () => {
+  function podsCtx() {
+    const nodes = [makeGpuNode('mi355x-000')];
+    const pods = [
+      makeGpuPod('a-small', { gpus: 1, node: 'mi355x-000' }),
+      makeGpuPod('b-big', { gpus: 8, node: 'mi355x-000' }),
+      makeGpuPod('c-wait', { gpus: 2, phase: 'Pending', node: null, waiting: 'Unschedulable' }),
+      makeGpuPod('d-mid', { gpus: 4, node: 'mi355x-000' }),
+    ];
+    pods[3].metadata.creationTimestamp = '2030-01-01T00:00:00Z';
+    return makeContext({ nodes, pods });
+  }
+  const order = (ctx, sort) => podPage(ctx.gpuPods, { sort }).names.map((k) => k.split('/')[1]);
+  it('namespace / name by default; most GPUs held, newest, not running first on request', () => {
+    const ctx = podsCtx();
+    expect(order(ctx, undefined)).toEqual(['a-small', 'b-big', 'c-wait', 'd-mid']);
+    expect(order(ctx, 'gpus')).toEqual(['b-big', 'd-mid', 'c-wait', 'a-small']);
+    expect(order(ctx, 'newest')[0]).toBe('d-mid');
+    expect(order(ctx, 'attention')[0]).toBe('c-wait');
+    expect(podSortOf({ sort: 'power' })).toBe('name');
+  });
+  it('the table and the owner query follow the order; operator pods keep theirs', () => {
+    const ctx = podsCtx();
+    const vm = podsView(ctx, { pager: { sort: 'gpus' } });
+    expect(findSection(vm, 'All GPU Pods').blocks[0].rows[0][0]).toBe('b-big');
+    const p = pagerOf(vm);
+    expect([p.sort, p.sorts.map((o) => o.value)]).toEqual(['gpus', POD_SORTS.map((o) => o.value)]);
+    expect(ownersScope(ctx, { sort: 'gpus' }).pods[0]).toBe('ml/b-big');
+    expect(podPage(ctx.gpuPods, { sort: 'gpus' }, 'plugin-pod').names[0]).toBe('ml/a-small');
   });
 });
 

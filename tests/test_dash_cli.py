@@ -103,3 +103,5 @@ def test_sort_flag_orders_the_nodes(url):
     assert text.returncode == 0 and "sorted: Most GPUs in use" in text.stdout
     bad = run("--url", url, "--sort", "hottest")
     assert bad.returncode == 2 and "bad --sort" in bad.stderr
+    pods = run("--url", url, "--page", "pods", "--sort", "gpus")
+    assert pods.returncode == 0 and "sorted: Most GPUs held" in pods.stdout
