@@ -114,7 +114,7 @@ def test_detail_pages_cost_one_node_of_telemetry_whatever_the_cluster_size():
     assert abs(cold["bytes"] - out[1]["nodeDetailCold"]["bytes"]) <= 0.05 * out[1]["nodeDetailCold"]["bytes"], out
     assert cold["p50_ms"] < 2 * out[16]["nodeScoped"]["p50_ms"] + 5, out
     assert ref["requests"] == 6 and ref["bytes"] > 3 * out[1]["nodeDetailColdReference"]["bytes"], out
-    assert ref["p50_ms"] > 3 * cold["p50_ms"], out
+    assert ref["p50_ms"] > 2 * cold["p50_ms"], out  # 4 serial round trips after the lists against one wave
     # The GPU Pods page asks for pod attribution only: one series per allocated GPU.
     assert out[16]["podsPageOwners"]["requests"] == 1
     assert out[16]["podsPageOwners"]["bytes"] < 0.1 * out[16]["podClusterWide"]["bytes"], out
