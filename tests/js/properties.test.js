@@ -256,4 +256,37 @@ describe('malformed Prometheus answers', () => {
       pages.clearViewMemo();
     }
   });
+
+  it('ranked and size-guarded answers with hostile rows never throw, in the client or the Metrics view', async () => {
+    const pages = await import('../../src/view/pages.js');
+    const { createMetricsSource } = await import('../../src/api/metrics.js');
+    const { exporterData, flatten, ok } = await import('./promFake.js');
+    const { makeContext, makeGpuNode } = await import('./fixtures.js');
+    const r = rng(91);
+    const WRONG = [null, undefined, 0, '', 'NaN', '+Inf', '-1', [], {}, [1], { x: 1 }, 'abc'];
+    const ctx = makeContext({ nodes: [makeGpuNode('n0'), makeGpuNode('n1')] });
+    for (let round = 0; round < 120; round++) {
+      const rows = flatten(exporterData(['n0', 'n1'])).filter(() => r() < 0.7);
+      for (let i = 0, n = Math.floor(r() * 6); i < n; i++) {
+        const agg = pick(r, ['rank', 'ranked', 'gpu_nodes', 'gpu_pods', 'sum', 'count', 'nodes', pick(r, WRONG)]);
+        const metric = { agg: agg };
+        if (r() < 0.7) metric.hostname = pick(r, ['n0', 'n1', 'ghost', pick(r, WRONG)]);
+        if (r() < 0.5) metric.__name__ = pick(r, ['gpu_power_usage', 'gpu_total_vram', pick(r, WRONG)]);
+        rows.push({ metric: metric, value: [0, pick(r, ['12', '0', '9e99'].concat(WRONG))] });
+      }
+      if (r() < 0.1) rows.push(pick(r, WRONG));
+      const request = (path) => Promise.resolve(/query=1$/.test(path) ? ok([{ metric: {}, value: [0, '1'] }]) : ok(rows));
+      const src = createMetricsSource({ request: request });
+      const ranked = await src.fetchGpuMetrics('gauges', { rank: { by: 'power', page: Math.floor(r() * 3), per: 8, filter: '' }, summary: true });
+      const small = await src.fetchGpuMetrics('topology', { scope: r() < 0.5 ? [] : ['n0'], small: true });
+      const owners = await src.fetchGpuOwners({ pods: [], small: true });
+      for (const m of [ranked, small, owners]) {
+        const st = { metrics: m, series: null, fetchError: null, fetching: false };
+        pages.metricsView(ctx, st, { now: 0, pager: { sort: pick(r, ['power', 'name', 'in-use']) } });
+        pages.nodesView(ctx, { metrics: m, now: 0 });
+        pages.podsView(ctx, { metrics: m, now: 0 });
+      }
+      pages.clearViewMemo();
+    }
+  });
 });
