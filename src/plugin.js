@@ -110,8 +110,8 @@ export function createPlugin(env) {
   function NodesPage() {
     const ctx = core.useAmdGpuContext();
     const pager = usePager('nodes');
-    const t = telemetryScope(ctx, pager.state);
-    const m = core.useGpuMetrics(t.enabled, false, 'topology', t.scope, t.small);
+    const t = telemetryScope(ctx, pager.state, true);
+    const m = core.useGpuMetrics(t.enabled, false, 'topology', t.scope, t.small, t.rank);
     // The node and pod lists are live watches; what Refresh can renew here is
     // the telemetry (the DeviceConfigs are not on this page).
     return h(Page, {

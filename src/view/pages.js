@@ -596,12 +596,12 @@ export const NODE_SORTS = Object.freeze([
 ]);
 
 /**
- * The Metrics page adds an order only Prometheus knows: total GPU power,
+ * GPU Nodes and Metrics add an order only Prometheus knows: total GPU power,
  * highest first. Prometheus ranks and returns that page's nodes in one
  * request (metrics.js rankedClusterQuery); nodes without telemetry are not
  * ranked.
  */
-export const METRICS_SORTS = Object.freeze(NODE_SORTS.concat([Object.freeze({ value: 'power', label: 'Highest GPU power' })]));
+export const RANKED_NODE_SORTS = Object.freeze(NODE_SORTS.concat([Object.freeze({ value: 'power', label: 'Highest GPU power' })]));
 
 /** The pager state's sort if it is one of `sorts` (default NODE_SORTS), else 'name'. */
 export function nodeSortOf(state, sorts) {
@@ -752,7 +752,7 @@ export function visibleNodeNames(ctx, state) {
 export function telemetryScope(ctx, state, ranked) {
   if (!ctx) return { enabled: false, scope: [] };
   // Power order (Metrics): Prometheus picks the page — no node list needed.
-  if (ranked && nodeSortOf(state, METRICS_SORTS) === 'power') {
+  if (ranked && nodeSortOf(state, RANKED_NODE_SORTS) === 'power') {
     const st = state || {};
     return {
       enabled: true,
@@ -853,13 +853,17 @@ export function nodesView(ctx, opts) {
   if (ctx.loading) return page(null, null, [loader('Loading GPU node data...')]);
   // One page of nodes (NODES_PER_PAGE, name filter): the summary rows, the
   // cards and the telemetry the page asks for are all O(page), not O(cluster).
-  const pg = nodePage(ctx.gpuNodes, opts && opts.pager, ctx.index);
+  // In power order Prometheus picked the page (metrics.js rankedSnapshot).
+  const pagerState = opts && opts.pager;
+  const sort = nodeSortOf(pagerState, RANKED_NODE_SORTS);
+  const pg = metrics && metrics.rank && sort === 'power' ? rankedNodePage(ctx, metrics, pagerState)
+    : nodePage(ctx.gpuNodes, pagerState, ctx.index);
   // Live node power (the GPU Nodes query carries the power gauge for pod
   // attribution anyway): "watts|cap" per node, whole watts, so the head and
   // its rows rebuild only when a shown value changes.
   const power = nodePowerKeys(metrics);
   const head = memo('nodes-head', [pg, ctx.index, ctx.error, power.sig], function () {
-    return nodesHeadItems(ctx, now, power.byNode, pg, nodeSortOf(opts && opts.pager));
+    return nodesHeadItems(ctx, now, power.byNode, pg, sort);
   }, now);
   const owners = ownersByNode(metrics);
   const xgmi = metrics ? metrics.xgmi : undefined;
@@ -1046,7 +1050,7 @@ function nodesHeadItems(ctx, now, powerByNode, pg, sort) {
     return items;
   }
 
-  items.push(pager(pg, 'GPU nodes', { sort: sort, sorts: NODE_SORTS }));
+  items.push(pager(pg, pg.ranked ? 'GPU nodes reporting' : 'GPU nodes', { sort: sort, sorts: RANKED_NODE_SORTS }));
   const idx = ctx.index;
   if (pg.nodes.length > 0) {
     items.push(
@@ -1450,7 +1454,7 @@ export function metricsView(ctx, mstate, opts) {
     const k8s = scoped && !ctx.loading && ctx.gpuNodes && ctx.gpuNodes.length > 0;
     // Power order: Prometheus picked and ranked the page (metrics.js rankedSnapshot).
     const pagerState = opts && opts.pager;
-    const rankedView = !!m.rank && nodeSortOf(pagerState, METRICS_SORTS) === 'power';
+    const rankedView = !!m.rank && nodeSortOf(pagerState, RANKED_NODE_SORTS) === 'power';
     const pg = rankedView ? rankedPage(m, pagerState)
       : k8s ? nodePage(ctx.gpuNodes, pagerState, ctx.index) : nodePage(scoped ? m.scope : order, pagerState);
 
@@ -1478,8 +1482,8 @@ export function metricsView(ctx, mstate, opts) {
       );
     }
 
-    items.push(rankedView ? pager(pg, 'GPU nodes reporting', { sort: 'power', sorts: METRICS_SORTS })
-      : k8s ? pager(pg, 'GPU nodes', { sort: nodeSortOf(pagerState, METRICS_SORTS), sorts: METRICS_SORTS })
+    items.push(rankedView ? pager(pg, 'GPU nodes reporting', { sort: 'power', sorts: RANKED_NODE_SORTS })
+      : k8s ? pager(pg, 'GPU nodes', { sort: nodeSortOf(pagerState, RANKED_NODE_SORTS), sorts: RANKED_NODE_SORTS })
         : pager(pg, scoped ? 'GPU nodes' : 'GPU nodes reporting'));
     const covered = {};
     if (scoped) for (let i = 0; i < m.scope.length; i++) covered[m.scope[i]] = true;
@@ -1509,6 +1513,24 @@ export function metricsView(ctx, mstate, opts) {
 
   void now;
   return page(BRAND + ' — Metrics', refreshButton('Refresh metrics', mstate.fetching || ctx.loading), items);
+}
+
+/**
+ * GPU Nodes in power order: the ranked page's names (metrics.rank) as the
+ * listed node objects; a ranked hostname that is no listed node is left out.
+ */
+function rankedNodePage(ctx, m, state) {
+  const byName = memo('nodes-by-name', [ctx.gpuNodes], function () {
+    const out = new Map();
+    for (let i = 0; i < ctx.gpuNodes.length; i++) out.set(ctx.gpuNodes[i].metadata.name, ctx.gpuNodes[i]);
+    return out;
+  });
+  return memo('nodes-ranked-page', [m, byName], function () {
+    const base = rankedPage(m, state);
+    const nodes = [];
+    for (let i = 0; i < base.names.length; i++) if (byName.has(base.names[i])) nodes.push(byName.get(base.names[i]));
+    return Object.assign({}, base, { nodes: nodes, names: nodes.map(nodeNameOf), ranked: true });
+  });
 }
 
 /** The pager page of a power-ranked answer: its nodes, in rank order, out of the nodes ranked. */

@@ -15,7 +15,7 @@ import { createPlugin } from '../../src/plugin.js';
 import { resetSharedStores } from '../../src/api/clusterStore.js';
 import { DEVICE_CONFIG_LIST_PATH } from '../../src/api/amdgpu.js';
 import {
-  ALL_NODES_SERIES, METRICS_SORTS, NODE_SORTS, NODES_PER_PAGE, OVERVIEW_PLUGIN_PODS, PODS_PER_PAGE, clearViewMemo, devicePluginsView,
+  ALL_NODES_SERIES, RANKED_NODE_SORTS, NODE_SORTS, NODES_PER_PAGE, OVERVIEW_PLUGIN_PODS, PODS_PER_PAGE, clearViewMemo, devicePluginsView,
   metricsView, nodePage, nodeSortOf, nodesView, overviewView, ownersScope, podPage, podSortOf, podsView, POD_SORTS,
   telemetryScope,
 } from '../../src/view/pages.js';
@@ -104,7 +104,7 @@ describe('node order', () => {
     const ctx = ctxSorted();
     const vm = nodesView(ctx, { pager: { sort: 'in-use' } });
     const p = pagerOf(vm);
-    expect(p.sorts.map((o) => o.value)).toEqual(NODE_SORTS.map((o) => o.value));
+    expect(p.sorts.map((o) => o.value)).toEqual(NODE_SORTS.map((o) => o.value).concat(['power']));
     expect(p.sort).toBe('in-use');
     expect(cards(vm)[0]).toBe('mi355x-005');
     expect(renderPage(vm)).toContain('<option value="in-use" selected>Most GPUs in use</option>');
@@ -191,11 +191,11 @@ describe('Metrics in power order: Prometheus ranks the page', () => {
     expect(pagePart(qs[2])).not.toContain(SERIES.exporter.vramTotal);
     expect(again.gpus[0].vramTotalBytes).toBeGreaterThan(0);
   });
-  it('telemetryScope asks for the ranked page on Metrics only', () => {
+  it('telemetryScope asks for the ranked page when the page can rank (GPU Nodes, Metrics)', () => {
     const ctx = ctxOf(12);
     expect(telemetryScope(ctx, { sort: 'power', page: 1, filter: ' X-0 ' }, true)).toEqual({ enabled: true, rank: { by: 'power', page: 1, per: 8, filter: 'x-0' } });
-    expect(telemetryScope(ctx, { sort: 'power' }).rank).toBe(undefined); // GPU Nodes: no power order
-    expect(METRICS_SORTS.map((o) => o.value)).toEqual(NODE_SORTS.map((o) => o.value).concat(['power']));
+    expect(telemetryScope(ctx, { sort: 'power' }).rank).toBe(undefined); // no `ranked`: name order
+    expect(RANKED_NODE_SORTS.map((o) => o.value)).toEqual(NODE_SORTS.map((o) => o.value).concat(['power']));
   });
   it('metricsView shows the ranked page: cards in power order, pager over the nodes ranked', async () => {
     const s = createMetricsSource({ request: prom({ data: hot(12) }) });
@@ -205,6 +205,31 @@ describe('Metrics in power order: Prometheus ranks the page', () => {
     const p = pagerOf(vm);
     expect([p.sort, p.noun, p.pages, p.total]).toEqual(['power', 'GPU nodes reporting', 2, 12]);
     expect(pagerText(p)).toBe('Showing 1–8 of 12 GPU nodes reporting · page 1 of 2');
+  });
+  it('GPU Nodes in power order: the ranked page as node cards, topology view, no series', async () => {
+    lib.resetHeadlamp();
+    lib.lists.Node = [names(12).map((x) => makeGpuNode(x)), null];
+    lib.lists.Pod = [[], null];
+    const fake = prom({ data: hot(12) });
+    lib.api.handler = (p) => {
+      if (p === DEVICE_CONFIG_LIST_PATH) return Promise.resolve({ kind: 'List', metadata: {}, items: [] });
+      if (p.indexOf('/proxy/api/v1/') >= 0) return fake(p);
+      return Promise.reject(Object.assign(new Error('503'), { status: 503 }));
+    };
+    const plugin = createPlugin({ React: React, lib: lib, CommonComponents: CC });
+    const r = render(h(plugin.routeComponent('nodes')));
+    await r.settle();
+    const before = fake.mock.calls.length;
+    r.change(r.getByLabelText('Sort GPU nodes'), 'power');
+    await r.settle();
+    const sent = decoded(fake).slice(before);
+    expect(sent).toHaveLength(1);
+    expect(sent[0]).toContain('topk(8,');
+    expect(sent[0]).toContain('xgmi');
+    const titles = r.byTag('h2').map((n) => textOfNode(n)).filter((t) => /^mi355x-/.test(t));
+    expect(titles.slice(0, 2)).toEqual(['mi355x-004', 'mi355x-009']);
+    expect(r.text()).toContain('Showing 1–8 of 12 GPU nodes reporting');
+    r.unmount();
   });
   it('plugin: choosing "Highest GPU power" on Metrics sends one ranked query, then the page\'s series', async () => {
     lib.resetHeadlamp();
