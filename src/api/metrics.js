@@ -1136,6 +1136,10 @@ export function createMetricsSource(opts) {
           ? totalsFromRows(rows.__agg.filter(function (r) { return r.metric.agg !== 'rank' && r.metric.agg !== 'ranked'; }))
           : undefined;
         if (j.gpus.length > 0 || count > 0) source = 'amd-exporter';
+        // Nothing ranked and no exporter seen: maybe node-exporter feeds this
+        // Prometheus (no hostname label to rank by) — the cluster-wide
+        // snapshot instead, in name order.
+        else if (source !== 'amd-exporter') return NOT_SCOPED;
         const out = scopedResult(st, base, q, j, names, totals, v, undefined);
         out.rank = { by: rank.by, page: rank.page, per: rank.per, filter: rank.filter, count: count, watts: watts };
         return out;
@@ -1146,7 +1150,7 @@ export function createMetricsSource(opts) {
       st.last = null;
       invalidate();
       return null;
-    });
+    }).then(function (r) { return r === NOT_SCOPED ? fetchGpuMetrics(v) : r; });
   }
 
   // Until then a scoped fetch that finds nothing does not ask cluster-wide

@@ -191,6 +191,18 @@ describe('Metrics in power order: Prometheus ranks the page', () => {
     expect(pagePart(qs[2])).not.toContain(SERIES.exporter.vramTotal);
     expect(again.gpus[0].vramTotalBytes).toBeGreaterThan(0);
   });
+  it('a node-exporter Prometheus (nothing to rank by) answers with the cluster-wide snapshot in name order', async () => {
+    const ne = { node_uname_info: [{ metric: { __name__: 'node_uname_info', instance: 'i0', nodename: 'mi355x-000' }, value: [0, '1'] }] };
+    ne[SERIES.nodeExporter.chips] = [{ metric: { __name__: 'node_hwmon_chip_names', chip_name: 'amdgpu', instance: 'i0', chip: '0000:05:00_0' }, value: [0, '1'] }];
+    const s = createMetricsSource({ request: prom({ data: {}, ne: ne }) });
+    const m = await s.fetchGpuMetrics('gauges', { rank: rank(0), summary: true });
+    expect(m.source).toBe('node-exporter');
+    expect(m.rank).toBe(undefined);
+    expect(m.gpus.map((g) => g.nodeName)).toEqual(['mi355x-000']);
+    const vm = metricsView(ctxOf(1), { metrics: m, series: null, fetchError: null, fetching: false }, { pager: { sort: 'power' } });
+    expect(sectionTitles(vm)).not.toContain('No AMD GPU Metrics in Prometheus');
+    expect(cards(vm)).toEqual(['mi355x-000 — 1 × MI355X']);
+  });
   it('telemetryScope asks for the ranked page when the page can rank (GPU Nodes, Metrics)', () => {
     const ctx = ctxOf(12);
     expect(telemetryScope(ctx, { sort: 'power', page: 1, filter: ' X-0 ' }, true)).toEqual({ enabled: true, rank: { by: 'power', page: 1, per: 8, filter: 'x-0' } });
