@@ -7,6 +7,8 @@
  * harness React, so the same file runs
  *   * on the harness React (tests/js/harness/stub.js): `npm run test:node12`,
  *     `npm test` and the pytest bridge, offline;
+ *   * on real React 18.3.1 + react-dom, offline: the UMD builds over a
+ *     minimal DOM (tests/js/harness/umd.js; tests/test_js_real_react.py);
  *   * on real React 18 + react-dom in jsdom with @testing-library/react
  *     (tests/js/harness/dom.js): `npm run test:react`
  *     (vitest.react.config.mts), networked CI only.

@@ -1,9 +1,10 @@
 /**
  * React 18 semantics the plugin relies on, as runner-agnostic specs: the
- * same file checks the harness React offline (tests/js/harness/stub.js) and
- * real React 18.3 + react-dom under jsdom in networked CI
- * (tests/js/harness/dom.js, `npm run test:react`). A spec that passes on
- * react-dom and fails on the harness is a fidelity bug of the harness.
+ * same file checks the harness React (tests/js/harness/stub.js) and real
+ * React 18.3.1 + react-dom — offline through the UMD builds
+ * (tests/js/harness/umd.js, tests/test_js_real_react.py) and under jsdom in
+ * networked CI (tests/js/harness/dom.js). A spec that passes on react-dom and
+ * fails on the harness is a fidelity bug of the harness.
  *
  * Covered: commit order of layout / passive effects and their cleanups
  * (mount, update, deletion), StrictMode's double render and effect replay,
@@ -393,10 +394,12 @@ describe('React semantics: useSyncExternalStore (' + tier + ')', () => {
     await r.settle();
     expect(store.subs.size).toBe(1);
     const before = bodies;
-    store.poke();
+    // Store changes inside act(), as React expects in a test (outside it, React
+    // 18.3 warns and may render an external-store update twice).
+    r.act(() => store.poke());
     await r.settle();
     expect(bodies).toBe(before);
-    store.set({ n: 2 });
+    r.act(() => store.set({ n: 2 }));
     await r.settle();
     expect(r.text()).toBe('2');
     expect(bodies).toBe(before + 1);

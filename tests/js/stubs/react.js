@@ -18,9 +18,9 @@
  *   * state updates outside `act` are batched on a microtask.
  *
  * tests/js/shared/react-semantics.shared.test.js pins these rules; it runs
- * here and, in networked CI, on real React 18 + react-dom
- * (vitest.react.config.mts), so a divergence of this file from React fails
- * there.
+ * here and on real React 18.3.1 + react-dom — offline through the UMD builds
+ * (tests/test_js_real_react.py), and in networked CI under jsdom
+ * (vitest.react.config.mts) — so a divergence of this file from React fails.
  *
  * The rendered host tree ({tag, props, children}) can be queried
  * testing-library style (getByText, getByLabelText, getByTestId, …),

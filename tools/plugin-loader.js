@@ -8,6 +8,8 @@
  *   @kinvolk/headlamp-plugin/lib            → tests/js/stubs/headlamp-lib.js
  *   @kinvolk/headlamp-plugin/lib/CommonComponents → tests/js/stubs/CommonComponents.js
  *   amd-test-harness                        → tests/js/harness/stub.js (shared specs' render API)
+ *   (with AMD_TEST_TIER=react-umd: react → tests/js/harness/umd-react.js, the REAL React 18.3.1 UMD
+ *    builds over a minimal DOM; CommonComponents → harness/cc-dom.js; amd-test-harness → harness/umd.js)
  *   './x' (no extension)                    → ./x.tsx | ./x.ts | ./x.js | ./x/index.tsx
  *   *.ts / *.tsx                            → ES module; `import type` lines removed
  *
@@ -27,11 +29,18 @@ import { fileURLToPath, pathToFileURL } from 'url';
 const ROOT = path.resolve(path.dirname(fileURLToPath(import.meta.url)), '..');
 const STUBS = path.join(ROOT, 'tests', 'js', 'stubs');
 
+const HARNESS = path.join(ROOT, 'tests', 'js', 'harness');
+
+// AMD_TEST_TIER=react-umd: the REAL React 18.3.1 + react-dom (UMD builds,
+// AMD_REACT_UMD_DIR) over a minimal DOM — the offline real-React tier
+// (tests/test_js_real_react.py); otherwise the harness React.
+const REAL = process.env.AMD_TEST_TIER === 'react-umd';
+
 const ALIASES = {
-  react: path.join(STUBS, 'react.js'),
+  react: REAL ? path.join(HARNESS, 'umd-react.js') : path.join(STUBS, 'react.js'),
   '@kinvolk/headlamp-plugin/lib': path.join(STUBS, 'headlamp-lib.js'),
-  '@kinvolk/headlamp-plugin/lib/CommonComponents': path.join(STUBS, 'CommonComponents.js'),
-  'amd-test-harness': path.join(ROOT, 'tests', 'js', 'harness', 'stub.js'),
+  '@kinvolk/headlamp-plugin/lib/CommonComponents': REAL ? path.join(HARNESS, 'cc-dom.js') : path.join(STUBS, 'CommonComponents.js'),
+  'amd-test-harness': REAL ? path.join(HARNESS, 'umd.js') : path.join(HARNESS, 'stub.js'),
 };
 
 const TRY = ['.tsx', '.ts', '.js', '/index.tsx', '/index.ts', '/index.js'];
