@@ -34,8 +34,11 @@ probe + 4 queries on the last — and each is replayed as wired.
 
 The "all pages" composite (every page's data + all views rebuilt in one go,
 which no single reference button does) is reported as a secondary figure.
-Render = view-model → HTML string (the IR renderer's output), not React
-reconciliation. Data is synthetic (no cluster, no network); say so in the JSON.
+Render in the timed click = view-model → HTML string (the IR renderer's
+output). Untimed, every page is also mounted and re-rendered through the
+shipped React renderer, on the harness React and on real React 18.3.1
+production builds (``render_per_page`` / ``render_per_page_react_dom``).
+Data is synthetic (no cluster, no network); say so in the JSON.
 """
 from __future__ import annotations
 
@@ -175,8 +178,12 @@ def main(argv=None) -> int:
             D.barrier(info)
             elapsed = time.perf_counter() - t0
             # Untimed: every page mounted in the harness React and re-rendered
-            # after a refresh (element count, mount / re-render ms).
-            amd_react = call("pages", "amd", n=1, react=True).get("react") or {}
+            # after a refresh (element count, mount / re-render ms); and on real
+            # React 18.3.1 (production builds) when this image vendors them.
+            from headlamp_intel_gpu_plugin_amd.utils.reactumd import PROD_BUILDS, umd_dir
+            react_out = call("pages", "amd", n=1, react=True, reactUmdDir=umd_dir(PROD_BUILDS))
+            amd_react = react_out.get("react") or {}
+            amd_react_dom = react_out.get("reactDom") or {}
             # Secondary: the all-pages composite refresh.
             drv.call("steps", "amd", n=1)
             amd = call("steps", "amd", n=max(3, args.steps // 2))
@@ -191,7 +198,8 @@ def main(argv=None) -> int:
             result = {"ref": ref, "ref_pages": ref_pages["pages"], "amd_pages": amd_pages["pages"], "ref_cold": ref_cold, "ref_switch": ref_switch,
                       "amd": amd, "amd_cold": amd_cold, "amd_switch": amd_switch, "detail": detail,
                       "ref_cold_pages": ref_cold_pages["pages"], "amd_cold_pages": amd_cold_pages["pages"],
-                      "detail_slow": detail_out.get("detailSlow"), "react": amd_react, **served}
+                      "detail_slow": detail_out.get("detailSlow"), "react": amd_react, "react_dom": amd_react_dom,
+                      **served}
         finally:
             drv.close()
             server.stop()
@@ -274,7 +282,8 @@ def main(argv=None) -> int:
                                                "reference": result["ref"]["requestsPerStep"]}},
             "request_trace_p50_ms": {k: round(v["p50_ms"], 2) for k, v in (result["amd"].get("trace") or {}).items()},
             # Data committed → all views rebuilt and rendered (composite refresh).
-            "render_note": "render = view-model IR -> HTML string, not React reconciliation",
+            "render_note": ("render in the timed click = view-model IR -> HTML string; React mount / re-render: "
+                            "render_per_page (harness React), render_per_page_react_dom (real React 18.3.1)"),
             "render_p50_ms": (round(summarize(result["amd"]["renderMs"])["p50"], 3)
                               if result["amd"].get("renderMs") else None),
             # Each page opened on an empty cache, as each is wired (reference: a
@@ -298,6 +307,13 @@ def main(argv=None) -> int:
             "render_per_page": {pg: {"mount_ms": round(v["mountMs"], 3), "rerender_ms": round(v["rerenderMs"], 3),
                                      "elements": v["elements"], "html_elements": v["htmlElements"]}
                                 for pg, v in result["react"].items()},
+            # The same page on REAL React: react@18.3.1 + react-dom@18.3.1
+            # production UMD builds, committed with flushSync into a minimal
+            # JS DOM (tests/js/harness/minidom.js; a browser DOM is native).
+            # Median of 9 mount / re-render cycles; null when not vendored.
+            "render_per_page_react_dom": ({pg: {"mount_ms": round(v["mountMs"], 3), "rerender_ms": round(v["rerenderMs"], 3),
+                                                "elements": v["elements"]}
+                                           for pg, v in result["react_dom"].items()} or None),
             # Secondary: every page's data (all telemetry + series) in one cold open.
             "cold_open_p50_ms": {"amd": round(summarize(result["amd_cold"]["latencies"])["p50"], 3),
                                  "reference": round(summarize(result["ref_cold"]["latencies"])["p50"], 3)},

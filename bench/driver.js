@@ -252,6 +252,49 @@ function reactMeasure(vm, vm2) {
   return { mountMs: mountMs, rerenderMs: rerenderMs, elements: elements, htmlElements: htmlElements(renderPage(vm2)) };
 }
 
+/** Real React 18.3.1 production builds + the shipped renderer, loaded on first use (umdDir: see reactDomMeasure). */
+let realDom = null;
+async function realReact(umdDir) {
+  if (!realDom) {
+    const umd = await import('../tests/js/harness/umd-load.js');
+    const cc = await import('../tests/js/harness/commonComponents.js');
+    const loaded = umd.loadUmdReact(umdDir, 'production');
+    realDom = { React: loaded.React, ReactDOM: loaded.ReactDOM,
+      view: createRenderer(loaded.React, cc.makeCommonComponents(loaded.React.createElement)) };
+  }
+  return realDom;
+}
+
+/**
+ * The same mount / re-render on REAL React: react@18.3.1 + react-dom@18.3.1
+ * production UMD builds (what Headlamp serves users) committing with
+ * ReactDOM.flushSync into the minimal DOM (tests/js/harness/minidom.js).
+ * Median of `reps` mount + re-render + unmount cycles (the first warms the
+ * JIT); elements = host elements in the container after the re-render.
+ */
+async function reactDomMeasure(umdDir, vm, vm2, reps) {
+  const R = await realReact(umdDir);
+  const h = R.React.createElement;
+  const mounts = [];
+  const rerenders = [];
+  let elements = 0;
+  for (let i = 0; i < reps; i++) {
+    const c = document.createElement('div');
+    document.body.appendChild(c);
+    const root = R.ReactDOM.createRoot(c);
+    const t0 = process.hrtime();
+    R.ReactDOM.flushSync(function () { root.render(h(R.view.Page, { vm: vm })); });
+    mounts.push(ms(process.hrtime(t0)));
+    const t1 = process.hrtime();
+    R.ReactDOM.flushSync(function () { root.render(h(R.view.Page, { vm: vm2 })); });
+    rerenders.push(ms(process.hrtime(t1)));
+    elements = c.querySelectorAll('*').length;
+    R.ReactDOM.flushSync(function () { root.unmount(); });
+    document.body.removeChild(c);
+  }
+  return { mountMs: stats(mounts).p50, rerenderMs: stats(rerenders).p50, elements: elements, reps: reps };
+}
+
 const SNAPSHOT_CSS =
   'body{font-family:system-ui,sans-serif;margin:24px;color:#222;max-width:1200px}' +
   'h1{font-size:22px}h2{font-size:16px;border-bottom:1px solid #ddd;padding-bottom:4px;margin-top:28px}' +
@@ -735,6 +778,10 @@ async function serve(a) {
             await L.s.refreshPage(page);
             const vm2 = pageVm(page, L.s.ctx(), ms0(), L.s.pageMetrics(page));
             out.react[page] = reactMeasure(vm, vm2);
+            if (c.reactUmdDir) {
+              out.reactDom = out.reactDom || {};
+              out.reactDom[page] = await reactDomMeasure(c.reactUmdDir, vm, vm2, c.reactReps || 9);
+            }
           }
         }
       } else if (c.cmd === 'snapshot') {

@@ -149,7 +149,7 @@ export class Node extends Target {
       for (let i = 0; i < n.childNodes.length; i++) {
         const c = n.childNodes[i];
         if (c.nodeType !== ELEMENT_NODE) continue;
-        if (attr ? c.hasAttribute(attr[1]) : c.localName === want) out.push(c);
+        if (attr ? c.hasAttribute(attr[1]) : want === '*' || c.localName === want) out.push(c);
         walk(c);
       }
     })(this);
@@ -175,12 +175,15 @@ export class Comment extends Node {
   get data() { return this.nodeValue; }
 }
 
+/** element.style: declarations as own properties, the CSSStyleDeclaration methods on the prototype. */
+class Style {
+  setProperty(k, v) { this[k] = String(v); }
+  removeProperty(k) { delete this[k]; }
+  getPropertyValue(k) { return Object.prototype.hasOwnProperty.call(this, k) ? this[k] : ''; }
+}
+
 function makeStyle() {
-  const style = {};
-  Object.defineProperty(style, 'setProperty', { value: function (k, v) { style[k] = String(v); } });
-  Object.defineProperty(style, 'removeProperty', { value: function (k) { delete style[k]; } });
-  Object.defineProperty(style, 'getPropertyValue', { value: function (k) { return k in style ? style[k] : ''; } });
-  return style;
+  return new Style();
 }
 
 export class Element extends Node {

@@ -6,6 +6,8 @@ import sys
 
 import pytest
 
+from headlamp_intel_gpu_plugin_amd.utils.reactumd import PROD_BUILDS, umd_dir
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REQUIRED = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
             "vs_baseline", "dtype", "data", "config"}
@@ -53,6 +55,16 @@ def _check(line, n):
     assert cold["overview"]["requests"]["amd"] == 3 and cold["nodes"]["requests"]["amd"] == 4
     for v in cold.values():
         assert v["amd"] < v["reference"], cold
+    # Every page mounted through the shipped renderer on the harness React and,
+    # where this image vendors them, on real React 18.3.1 production builds:
+    # the same IR mounts the same host elements on both.
+    harness, real = line["render_per_page"], line["render_per_page_react_dom"]
+    assert set(harness) == set(pp)
+    if umd_dir(PROD_BUILDS):
+        assert set(real) == set(pp)
+        for k in pp:
+            assert real[k]["elements"] == harness[k]["elements"] > 0, (k, real[k], harness[k])
+            assert real[k]["mount_ms"] > 0 and real[k]["rerender_ms"] > 0
 
 
 def test_bench_single_rank():

@@ -21,25 +21,15 @@ import tempfile
 
 import pytest
 
+from headlamp_intel_gpu_plugin_amd.utils.reactumd import umd_dir
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 NODE = shutil.which("node") or shutil.which("nodejs")
 SHARED = sorted(os.path.relpath(p, ROOT) for p in glob.glob(os.path.join(ROOT, "tests", "js", "shared", "*.test.js")))
 RUNNER = os.path.join("tools", "minitest.js")
 LOADER = ["--no-warnings", "--experimental-loader", "./tools/plugin-loader.js"]
-BUILDS = ("react@18.3.1.js", "react-dom@18.3.1.js")
 
-
-def _umd_dir():
-    """A directory of this image holding the React 18.3.1 UMD development builds, or None."""
-    try:
-        import dash  # noqa: PLC0415 — vendors React's UMD builds under dash/deps
-    except Exception:  # noqa: BLE001
-        return None
-    d = os.path.join(os.path.dirname(dash.__file__), "deps")
-    return d if all(os.path.exists(os.path.join(d, b)) for b in BUILDS) else None
-
-
-UMD = _umd_dir()
+UMD = umd_dir()
 ENV = dict(os.environ, AMD_TEST_TIER="react-umd", AMD_REACT_UMD_DIR=UMD or "")
 pytestmark = pytest.mark.skipif(not (NODE and UMD), reason="node or the React 18.3.1 UMD builds are not available")
 

@@ -108,6 +108,23 @@ def render_table(rows):
     return md
 
 
+def react_dom_table(rows):
+    """Per page at each point: real React 18.3.1 (production) elements and mount / re-render ms."""
+    if not any(r["line"].get("render_per_page_react_dom") for r in rows):
+        return []
+    head = ["GPU nodes"] + [f"{t}: elements, mount / re-render ms" for _, t in PAGE_COLS]
+    md = ["", "Render on real React 18.3.1 + react-dom (production UMD builds, minimal JS DOM, median of 9):", "",
+          "| " + " | ".join(head) + " |", "|---:|" + "---|" * (len(head) - 1)]
+    for r in rows:
+        rp = r["line"].get("render_per_page_react_dom") or {}
+        cells = [str(r["line"]["config"]["nodes"])]
+        for k, _ in PAGE_COLS:
+            v = rp.get(k)
+            cells.append(f"{v['elements']}, {v['mount_ms']:.1f} / {v['rerender_ms']:.1f}" if v else "—")
+        md.append("| " + " | ".join(cells) + " |")
+    return md
+
+
 MODES = ["identity", "rewrapped", "reparsed"]
 KINDS = ["modified", "gpu-modified", "added", "gpu-added", "deleted", "gpu-deleted"]
 
@@ -174,7 +191,8 @@ def main():
         print(f"{kind}={val}: per-page p50 {line['value']} ms vs ref {line['baseline']['value_ms']} ms", flush=True)
         with open(os.path.join(args.out, "sweep.json"), "w") as f:
             json.dump(rows, f, indent=1)
-    md = table(rows) + ["", "Render (harness React, first page of each view) and the cold Node detail open:", ""] + render_table(rows)
+    md = (table(rows) + ["", "Render (harness React, first page of each view) and the cold Node detail open:", ""]
+          + render_table(rows) + react_dom_table(rows))
     with open(os.path.join(args.out, "sweep.md"), "w") as f:
         f.write("\n".join(md) + "\n")
     print("\n".join(md))
