@@ -66,7 +66,9 @@ def react_results():
         if not os.path.exists(out) or os.path.getsize(out) == 0:
             pytest.fail("JS runner crashed on real React:\n" + r.stdout + r.stderr)
         with open(out) as fh:
-            return {x["id"]: x for x in json.load(fh)}
+            res = {x["id"]: x for x in json.load(fh)}
+        res["__console__"] = r.stdout + r.stderr
+        return res
     finally:
         if os.path.exists(out):
             os.unlink(out)
@@ -78,6 +80,16 @@ def test_real_react_loads_and_every_shared_file_runs(react_results):
     assert len(IDS) >= 80
     # the tier label in the spec names says which React rendered them
     assert all("react-dom-umd" in i for i in IDS), [i for i in IDS if "react-dom-umd" not in i][:3]
+
+
+def test_real_react_warns_about_nothing(react_results):
+    # React's development build reports misuse on console.error as "Warning: …":
+    # missing or duplicate keys, invalid DOM nesting or props, updates on
+    # unmounted components, setState in render, hook order changes. The shipped
+    # renderer, provider and pages must trigger none of them on any spec.
+    out = react_results["__console__"]
+    warnings = [l for l in out.splitlines() if "Warning:" in l]
+    assert not warnings, warnings[:5]
 
 
 @pytest.mark.parametrize("spec_id", IDS)
