@@ -532,9 +532,31 @@ export function nodePodsPath(nodeName) {
  * @returns {Promise<any[]>}
  */
 export function fetchNodePods(request, nodeName, timeoutMs, clock) {
-  return withTimeout(request(nodePodsPath(nodeName)), timeoutMs || DEFAULT_REQUEST_TIMEOUT_MS, clock || defaultClock).then(function (l) {
+  return withTimeout(sharedRequest(request, nodePodsPath(nodeName)), timeoutMs || DEFAULT_REQUEST_TIMEOUT_MS,
+    clock || defaultClock).then(function (l) {
     return isKubeList(l) ? l.items : [];
   });
+}
+
+// In-flight requests per request function and path: callers asking for the
+// same path while it is in flight share one request (two sections of the same
+// node, or React 18 StrictMode mounting an effect twice in development).
+const inFlight = typeof WeakMap === 'function' ? new WeakMap() : null;
+
+function sharedRequest(request, path) {
+  if (!inFlight) return request(path);
+  let paths = inFlight.get(request);
+  if (!paths) {
+    paths = new Map();
+    inFlight.set(request, paths);
+  }
+  const pending = paths.get(path);
+  if (pending) return pending;
+  const p = Promise.resolve(request(path));
+  const done = function () { if (paths.get(path) === p) paths.delete(path); };
+  paths.set(path, p);
+  p.then(done, done);
+  return p;
 }
 
 /** True when the store has both cluster lists (a plugin page fed it): detail views can read it. */

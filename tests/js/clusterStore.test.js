@@ -3,7 +3,7 @@
  * 8 cases) plus the parallel-fetch, SWR, race and shared-cache behaviour the
  * reference lacks.
  */
-import { createClusterStore, getSharedStore, resetSharedStores, withTimeout } from '../../src/api/clusterStore.js';
+import { createClusterStore, fetchNodePods, getSharedStore, nodePodsPath, resetSharedStores, withTimeout } from '../../src/api/clusterStore.js';
 import { DEVICE_CONFIG_LIST_PATH, PLUGIN_POD_QUERIES } from '../../src/api/amdgpu.js';
 import { makeDeviceConfig, makeGpuNode, makeGpuPod, makeNode, makePlainPod, makePluginPod, NOW } from './fixtures.js';
 import { metricsView, nodeDetailView } from '../../src/view/pages.js';
@@ -463,5 +463,56 @@ describe('CRD refused vs absent', () => {
       expect(snap.crdForbidden).toBe(forbidden);
       expect(snap.error).toBeNull();
     }
+  });
+});
+
+describe('fetchNodePods', () => {
+  function deferredRequest() {
+    const calls = [];
+    const pending = [];
+    const request = (p) => {
+      calls.push(p);
+      return new Promise((resolve, reject) => pending.push({ resolve, reject }));
+    };
+    return { request, calls, pending };
+  }
+
+  it('callers asking for the same node while it is in flight share one request', async () => {
+    const d = deferredRequest();
+    const a = fetchNodePods(d.request, 'n1');
+    const b = fetchNodePods(d.request, 'n1');
+    const c = fetchNodePods(d.request, 'n2');
+    expect(d.calls).toEqual([nodePodsPath('n1'), nodePodsPath('n2')]);
+    d.pending[0].resolve({ kind: 'PodList', items: [makeGpuPod('p', { node: 'n1' })] });
+    d.pending[1].resolve({ kind: 'PodList', items: [] });
+    const [ra, rb, rc] = await Promise.all([a, b, c]);
+    expect(ra).toHaveLength(1);
+    expect(rb).toBe(ra);
+    expect(rc).toEqual([]);
+    // settled: the next read is a new request
+    fetchNodePods(d.request, 'n1');
+    expect(d.calls).toHaveLength(3);
+  });
+
+  it('a failure reaches every sharer and is not cached', async () => {
+    const d = deferredRequest();
+    const a = fetchNodePods(d.request, 'n1');
+    const b = fetchNodePods(d.request, 'n1');
+    d.pending[0].reject(Object.assign(new Error('403 Forbidden'), { status: 403 }));
+    let errs = 0;
+    await a.catch(() => { errs++; });
+    await b.catch(() => { errs++; });
+    expect(errs).toBe(2);
+    fetchNodePods(d.request, 'n1');
+    expect(d.calls).toHaveLength(2);
+  });
+
+  it('different request functions (clusters) do not share', () => {
+    const d1 = deferredRequest();
+    const d2 = deferredRequest();
+    fetchNodePods(d1.request, 'n1');
+    fetchNodePods(d2.request, 'n1');
+    expect(d1.calls).toHaveLength(1);
+    expect(d2.calls).toHaveLength(1);
   });
 });

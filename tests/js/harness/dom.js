@@ -15,8 +15,11 @@ const React = ReactNS.default || ReactNS;
 export { React };
 export const tier = 'react-dom';
 
+// AMD_TEST_STRICT=1: every render under <StrictMode> (double render, effect replay).
+const STRICT_ALL = typeof process !== 'undefined' && process.env.AMD_TEST_STRICT === '1';
+
 export function render(element, options) {
-  const strict = !!(options && options.strict);
+  const strict = STRICT_ALL || !!(options && options.strict);
   const wrap = function (el) { return strict ? React.createElement(React.StrictMode, null, el) : el; };
   const r = rtlRender(wrap(element));
   const c = r.container;

@@ -12,8 +12,11 @@ import React, { render as stubRender, textOf } from '../stubs/react.js';
 export { React };
 export const tier = 'harness';
 
+// AMD_TEST_STRICT=1: every render under <StrictMode> (double render, effect replay).
+const STRICT_ALL = typeof process !== 'undefined' && process.env.AMD_TEST_STRICT === '1';
+
 export function render(element, options) {
-  const r = stubRender(element, options);
+  const r = stubRender(element, STRICT_ALL ? Object.assign({}, options, { strict: true }) : options);
   const handle = {
     settle: function (rounds) { return r.settle(rounds).then(function () { return handle; }); },
     text: function () { return r.text(); },

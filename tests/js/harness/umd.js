@@ -13,6 +13,8 @@ export { React };
 export const tier = 'react-dom-umd';
 
 const act = React.act;
+// AMD_TEST_STRICT=1: every render under <StrictMode> (double render, effect replay).
+const STRICT_ALL = process.env.AMD_TEST_STRICT === '1';
 
 /** The DOM's own value setter, so React's value tracker sees a user's edit (as testing-library does). */
 function setNativeValue(node, value) {
@@ -22,7 +24,7 @@ function setNativeValue(node, value) {
 }
 
 export function render(element, options) {
-  const strict = !!(options && options.strict);
+  const strict = STRICT_ALL || !!(options && options.strict);
   const wrap = function (el) { return strict ? React.createElement(React.StrictMode, null, el) : el; };
   const c = document.createElement('div');
   document.body.appendChild(c);
