@@ -486,10 +486,11 @@ export function createClusterStore(opts) {
     hasLoaded: function () { return s.asyncLoaded; },
     /**
      * Work counters: cluster-index rebuilds vs delta patches, and the list
-     * trackers' classification counts (objects classified / reused / skipped).
+     * trackers' classification counts (objects classified / reused / skipped),
+     * and the views subscribed right now.
      */
     counters: function () {
-      return Object.assign({}, counters, { pods: podTracker.stats(), nodes: nodeTracker.stats() });
+      return Object.assign({}, counters, { pods: podTracker.stats(), nodes: nodeTracker.stats(), subscribers: listeners.length });
     },
   };
 }
@@ -508,6 +509,11 @@ export function getSharedStore(key, factory) {
   const k = key || '__default__';
   if (!shared[k]) shared[k] = factory();
   return shared[k];
+}
+
+/** Every shared store alive (diagnostics and lifecycle specs). */
+export function sharedStores() {
+  return Object.keys(shared).map(function (k) { return shared[k]; });
 }
 
 export function resetSharedStores() {
