@@ -121,6 +121,21 @@ export function isObject(v) {
   return v !== null && typeof v === 'object' && !Array.isArray(v);
 }
 
+const optString = function (v) { return v === undefined || v === null || typeof v === 'string'; };
+
+/**
+ * A Kubernetes object the views can name: metadata with a non-empty string
+ * name, and a namespace / uid that are strings when present. What fails this
+ * (a half-written object, a wrong-shaped watch event) is never classified as
+ * a GPU node, GPU pod, operator pod or DeviceConfig, so no page renders its
+ * name — a view never hands React an object where it expects text.
+ */
+export function isNamedObject(v) {
+  if (!isObject(v) || !isObject(v.metadata)) return false;
+  const m = v.metadata;
+  return typeof m.name === 'string' && m.name !== '' && optString(m.namespace) && optString(m.uid);
+}
+
 /** Safe nested getter: get(obj, ['a','b']) without optional chaining. */
 export function get(obj, path, dflt) {
   let cur = obj;
@@ -178,7 +193,7 @@ export function isKubeList(value) {
  */
 
 export function isDeviceConfig(value) {
-  return isObject(value) && value.kind === DEVICE_CONFIG_KIND && isObject(value.metadata);
+  return isNamedObject(value) && value.kind === DEVICE_CONFIG_KIND;
 }
 
 /** Operand components the operator manages, in display order. */
@@ -282,7 +297,7 @@ function hasAmdResource(res) {
 
 /** A node is an AMD GPU node if NFD/labeller labels say so or it advertises `amd.com/*`. */
 export function isAmdGpuNode(node) {
-  if (!isObject(node) || !isObject(node.metadata)) return false;
+  if (!isNamedObject(node)) return false;
   if (hasAmdLabel(labelsOf(node))) return true;
   return hasAmdResource(get(node, ['status', 'capacity'], null));
 }
@@ -456,7 +471,7 @@ function containerAmdKeys(c) {
 
 /** True if any container, init or regular, requests or limits an `amd.com/*` resource. */
 export function isGpuRequestingPod(pod) {
-  if (!isObject(pod) || !isObject(pod.metadata)) return false;
+  if (!isNamedObject(pod)) return false;
   const cs = get(pod, ['spec', 'containers'], []);
   const ics = get(pod, ['spec', 'initContainers'], []);
   for (let i = 0; i < cs.length; i++) if (containerAmdKeys(cs[i]).length > 0) return true;
@@ -657,7 +672,7 @@ export function phaseToStatus(phase) {
  * @returns {'device-plugin'|'node-labeller'|'metrics-exporter'|'driver'|'operator'|null}
  */
 export function pluginPodComponent(pod) {
-  if (!isObject(pod) || !isObject(pod.metadata)) return null;
+  if (!isNamedObject(pod)) return null;
   const labels = labelsOf(pod);
   if (labels.name === AMD_DEVICE_PLUGIN_POD_LABEL) return 'device-plugin';
   if (labels.name === AMD_NODE_LABELLER_POD_LABEL) return 'node-labeller';

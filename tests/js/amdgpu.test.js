@@ -39,6 +39,7 @@ import {
   isAmdGpuPluginPod,
   isDeviceConfig,
   isGpuRequestingPod,
+  isNamedObject,
   isKubeList,
   isNodeReady,
   isPodReady,
@@ -478,5 +479,32 @@ describe('nextAgeChange', () => {
   it('never changes for a missing or unparseable timestamp', () => {
     expect(nextAgeChange(undefined, 0)).toBe(Infinity);
     expect(nextAgeChange('not a time', 0)).toBe(Infinity);
+  });
+});
+
+describe('isNamedObject: what the views can name', () => {
+  it('needs a non-empty string name; namespace and uid are strings when present', () => {
+    expect(isNamedObject(makeGpuNode('g0'))).toBe(true);
+    expect(isNamedObject(makeGpuPod('p'))).toBe(true);
+    expect(isNamedObject({ metadata: { name: 'x', namespace: null, uid: undefined } })).toBe(true);
+    for (const name of [undefined, null, '', 7, {}, { a: 1 }, [], ['x'], true]) {
+      expect(isNamedObject({ metadata: { name } })).toBe(false);
+    }
+    expect(isNamedObject({ metadata: { name: 'x', namespace: { a: 1 } } })).toBe(false);
+    expect(isNamedObject({ metadata: { name: 'x', uid: 3 } })).toBe(false);
+    expect(isNamedObject(null)).toBe(false);
+    expect(isNamedObject({ metadata: [] })).toBe(false);
+  });
+
+  it('an AMD node, GPU pod, operator pod or DeviceConfig without a usable name is not classified as one', () => {
+    const node = makeGpuNode('g0');
+    const pod = makeGpuPod('p');
+    const dp = makePluginPod('dp');
+    const dc = makeDeviceConfig();
+    const unnamed = (o) => Object.assign({}, o, { metadata: Object.assign({}, o.metadata, { name: { a: 1 } }) });
+    expect(isAmdGpuNode(node) && !isAmdGpuNode(unnamed(node))).toBe(true);
+    expect(isGpuRequestingPod(pod) && !isGpuRequestingPod(unnamed(pod))).toBe(true);
+    expect(isAmdGpuPluginPod(dp) && !isAmdGpuPluginPod(unnamed(dp))).toBe(true);
+    expect(isDeviceConfig(dc) && !isDeviceConfig(unnamed(dc))).toBe(true);
   });
 });

@@ -7,20 +7,7 @@ import { buildClusterIndex, formatBytes, getPodGpuDemand } from '../../src/api/a
 import { shareGpus, shareMap } from '../../src/api/metrics.js';
 import { buildXgmiMatrix, isFullMesh } from '../../src/api/topology.js';
 import { makeGpuNode } from './fixtures.js';
-
-/** mulberry32: tiny deterministic PRNG. */
-function rng(seed) {
-  let a = seed >>> 0;
-  return function () {
-    a = (a + 0x6d2b79f5) >>> 0;
-    let t = a;
-    t = Math.imul(t ^ (t >>> 15), t | 1);
-    t ^= t + Math.imul(t ^ (t >>> 7), t | 61);
-    return ((t ^ (t >>> 14)) >>> 0) / 4294967296;
-  };
-}
-const int = (r, lo, hi) => lo + Math.floor(r() * (hi - lo + 1));
-const pick = (r, xs) => xs[Math.floor(r() * xs.length)];
+import { int, mutate, pick, rng } from './fuzzlib.js';
 
 const RES = ['amd.com/gpu', 'amd.com/cpx_nps4'];
 
@@ -172,21 +159,6 @@ describe('properties', () => {
 });
 
 describe('malformed cluster objects (what a real apiserver, an old CRD version or a half-written object can hand over)', () => {
-  // Replace a random leaf or subtree of `o` with a value of the wrong shape.
-  const WRONG = [null, undefined, 0, 7, -1, '', 'x', 'NaN', true, [], {}, [null], { a: 1 }];
-  function mutate(r, o, depth) {
-    if (o === null || typeof o !== 'object' || depth > 6) return pick(r, WRONG);
-    const keys = Object.keys(o);
-    if (!keys.length) return pick(r, WRONG);
-    const out = Array.isArray(o) ? o.slice() : Object.assign({}, o);
-    const k = pick(r, keys);
-    if (r() < 0.35) {
-      if (Array.isArray(out)) out.splice(Number(k), 1);
-      else delete out[k];
-    } else out[k] = r() < 0.5 ? pick(r, WRONG) : mutate(r, o[k], depth + 1);
-    return out;
-  }
-
   it('no page, detail section, column or index throws on them', async () => {
     const pages = await import('../../src/view/pages.js');
     const { createClusterStore } = await import('../../src/api/clusterStore.js');
