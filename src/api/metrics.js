@@ -694,6 +694,25 @@ export function scopedSeriesQuery(scope, small) {
 /** Key of the cluster-wide line in a scoped series answer (no node name can be this). */
 export const TOTAL_SERIES = '\u0000cluster';
 
+/**
+ * A result row whose label values are all strings, as Prometheus promises: a
+ * label of any other type (a broken proxy, a hand-written exporter) is
+ * dropped, so no join, total or view ever takes an object or a number for a
+ * node, pod or card name. The row itself is returned when it is clean.
+ */
+export function stringLabels(row) {
+  const m = row && row.metric;
+  if (!isObject(m)) return row;
+  for (const k in m) {
+    if (typeof m[k] !== 'string') {
+      const clean = {};
+      for (const k2 in m) if (typeof m[k2] === 'string') clean[k2] = m[k2];
+      return { metric: clean, value: row.value };
+    }
+  }
+  return row;
+}
+
 /** Split a combined result into `name → rows` (xGMI rows under `__xgmi`). */
 export function splitByName(result) {
   // No prototype: a series named e.g. "__proto__" is a plain key here.
@@ -918,7 +937,7 @@ export function createMetricsSource(opts) {
   function instant(base, q) {
     return get('query', base + '/api/v1/query?query=' + encodeURIComponent(q)).then(function (raw) {
       if (!raw || raw.status !== 'success' || !raw.data || !Array.isArray(raw.data.result)) return [];
-      return raw.data.result;
+      return raw.data.result.map(stringLabels);
     });
   }
 

@@ -6,6 +6,7 @@
  */
 import {
   PROMETHEUS_SERVICES,
+  stringLabels,
   EXPORTER_JOIN_LABELS,
   EXPORTER_LEAN_LABELS,
   keyedByHostname,
@@ -32,7 +33,7 @@ import {
   STALE_FAILURES,
 } from '../../src/api/metrics.js';
 
-import { BASE0, BASE1, exporterData, ok, prom, vec } from './promFake.js';
+import { BASE0, BASE1, exporterData, flatten, ok, prom, vec } from './promFake.js';
 
 describe('discovery', () => {
   it('probes all candidate services in parallel', async () => {
@@ -837,5 +838,28 @@ describe('summarizeMetrics', () => {
       expect(q).toContain(E.eccCorrect);
       expect(q).toContain(E.eccUncorrect);
     });
+  });
+});
+
+describe('stringLabels: label values are strings or absent', () => {
+  it('returns a clean row as is and drops labels of any other type', () => {
+    const clean = { metric: { __name__: 'gpu_power_usage', hostname: 'n0', gpu_id: '0' }, value: [0, '1'] };
+    expect(stringLabels(clean)).toBe(clean);
+    const dirty = { metric: { __name__: 'gpu_power_usage', hostname: { a: 1 }, gpu_id: 0, card_model: ['x'], pod: null }, value: [0, '2'] };
+    expect(stringLabels(dirty)).toEqual({ metric: { __name__: 'gpu_power_usage' }, value: [0, '2'] });
+    expect(dirty.metric.hostname).toEqual({ a: 1 }); // the answer itself is not modified
+    expect(stringLabels(null)).toBe(null);
+    expect(stringLabels({ metric: 'x' })).toEqual({ metric: 'x' });
+  });
+
+  it('a node whose hostname label is not a string gets no telemetry, and the others keep theirs', async () => {
+    const bad = JSON.parse(JSON.stringify(flatten(exporterData(['n0', 'n1']))));
+    bad.forEach((r) => { if (r.metric.hostname === 'n1') r.metric.hostname = { name: 'n1' }; });
+    const src = createMetricsSource({ request: (p) => Promise.resolve(/query=1$/.test(p) ? ok([{ metric: {}, value: [0, '1'] }]) : ok(bad)) });
+    const m = await src.fetchGpuMetrics('gauges');
+    const hosts = new Set(m.gpus.map((g) => g.nodeName));
+    expect(hosts.has('n0')).toBe(true);
+    expect(m.gpus.filter((g) => g.nodeName === 'n0')).toHaveLength(8);
+    expect([...hosts].every((x) => typeof x === 'string')).toBe(true);
   });
 });

@@ -13,16 +13,49 @@ import * as CC from '@kinvolk/headlamp-plugin/lib/CommonComponents';
 import { createRenderer } from '../../../src/view/react.js';
 import * as pages from '../../../src/view/pages.js';
 import { createClusterStore } from '../../../src/api/clusterStore.js';
-import { makeDeviceConfig, makeGpuNode, makeGpuPod, makeNode, makePlainPod, makePluginPod } from '../fixtures.js';
-import { mutate, rng } from '../fuzzlib.js';
+import { createMetricsSource } from '../../../src/api/metrics.js';
+import { makeContext, makeDeviceConfig, makeGpuNode, makeGpuPod, makeNode, makePlainPod, makePluginPod } from '../fixtures.js';
+import { exporterData, flatten, ok } from '../promFake.js';
+import { mutate, pick, rng } from '../fuzzlib.js';
 
 const h = React.createElement;
-const ROUNDS = Number((typeof process !== 'undefined' && process.env.FUZZ_RENDER_ROUNDS) || 40);
+const env = (k) => (typeof process !== 'undefined' && process.env[k]) || null;
+const ROUNDS = Number(env('FUZZ_RENDER_ROUNDS') || 40);
+const SEED = Number(env('FUZZ_SEED') || 9001);
+
+/** Mount every view-model and section; a failure names the round and the view. */
+function mountAll(view, round, vms, sections) {
+  let mounted = 0;
+  const fail = (what, e) => {
+    e.message = 'round ' + round + ', ' + what + ': ' + e.message;
+    throw e;
+  };
+  vms.forEach((vm, i) => {
+    try {
+      const m = render(h(view.Page, { vm, onRefresh: () => {} }));
+      expect(typeof m.text()).toBe('string');
+      m.unmount();
+    } catch (e) {
+      fail('page ' + i + ' ' + JSON.stringify(vm.title), e);
+    }
+    mounted++;
+  });
+  sections.forEach((s, i) => {
+    if (!s) return;
+    try {
+      render(h(view.Section, { s })).unmount();
+    } catch (e) {
+      fail('section ' + i + ' ' + JSON.stringify(s.title), e);
+    }
+    mounted++;
+  });
+  return mounted;
+}
 
 describe('shared: malformed clusters render (' + tier + ')', () => {
   it('every page, detail section and Nodes-table cell of a mutated cluster mounts and unmounts', async () => {
     const view = createRenderer(React, CC);
-    const r = rng(Number((typeof process !== 'undefined' && process.env.FUZZ_SEED) || 9001));
+    const r = rng(SEED);
     const now = Date.parse('2026-10-16T00:00:00Z');
     let mounted = 0;
     for (let round = 0; round < ROUNDS; round++) {
@@ -41,30 +74,8 @@ describe('shared: malformed clusters render (' + tier + ')', () => {
       const opts = { now };
       const vms = [pages.overviewView(ctx, opts), pages.devicePluginsView(ctx, opts), pages.nodesView(ctx, opts),
         pages.podsView(ctx, opts), pages.metricsView(ctx, { metrics: null, fetchError: null, fetching: false }, opts)];
-      const where = (what) => (e) => {
-        e.message = 'round ' + round + ', ' + what + ': ' + e.message;
-        throw e;
-      };
-      vms.forEach((vm, i) => {
-        try {
-          const m = render(h(view.Page, { vm, onRefresh: () => {} }));
-          expect(typeof m.text()).toBe('string');
-          m.unmount();
-        } catch (e) {
-          where('page ' + i + ' ' + JSON.stringify(vm.title))(e);
-        }
-        mounted++;
-      });
       const sections = nodes.map((n) => pages.nodeDetailView(n, ctx, opts)).concat(pods.map((p) => pages.podDetailView(p, opts)));
-      sections.forEach((s, i) => {
-        if (!s) return;
-        try {
-          render(h(view.Section, { s })).unmount();
-        } catch (e) {
-          where('section ' + i + ' ' + JSON.stringify(s.title))(e);
-        }
-        mounted++;
-      });
+      mounted += mountAll(view, round, vms, sections);
       // Nodes-table cells, as the column processor hands them to Headlamp's table (plugin.js).
       const cols = pages.nodeColumns();
       const cells = [];
@@ -75,5 +86,43 @@ describe('shared: malformed clusters render (' + tier + ')', () => {
       pages.clearViewMemo();
     }
     expect(mounted).toBeGreaterThan(ROUNDS * 5);
+  });
+
+  it('telemetry from wrong-shaped Prometheus rows renders on every page that shows it', async () => {
+    const view = createRenderer(React, CC);
+    const r = rng(SEED + 1);
+    const WRONG = [null, undefined, 0, '', 'NaN', '+Inf', '-1', [], {}, [1], { x: 1 }, 'abc'];
+    const ctx = makeContext({ nodes: [makeGpuNode('n0'), makeGpuNode('n1')], pods: [makeGpuPod('train-0', { node: 'n0' })] });
+    let mounted = 0;
+    for (let round = 0; round < ROUNDS; round++) {
+      const rows = flatten(exporterData(['n0', 'n1'])).map((row) => {
+        if (r() > 0.2) return row;
+        const k = pick(r, ['metric', 'value', 'metric.gpu_id', 'metric.hostname', 'value.1', 'metric.__name__', 'metric.pod',
+          'metric.namespace', 'metric.card_model', 'metric.serial_number']);
+        const out = JSON.parse(JSON.stringify(row));
+        const path = k.split('.');
+        let o = out;
+        for (let i = 0; i < path.length - 1; i++) o = o[path[i]];
+        o[path[path.length - 1]] = pick(r, WRONG);
+        return out;
+      });
+      for (let i = 0, n = Math.floor(r() * 4); i < n; i++) {
+        const metric = { agg: pick(r, ['rank', 'ranked', 'gpu_nodes', 'sum', 'count', pick(r, WRONG)]) };
+        if (r() < 0.7) metric.hostname = pick(r, ['n0', 'n1', 'ghost', pick(r, WRONG)]);
+        rows.push({ metric: metric, value: [0, pick(r, ['12', '0', '9e99'].concat(WRONG))] });
+      }
+      const request = (path) => Promise.resolve(/query=1$/.test(path) ? ok([{ metric: {}, value: [0, '1'] }]) : ok(rows));
+      const src = createMetricsSource({ request: request });
+      const m = await src.fetchGpuMetrics(pick(r, ['gauges', 'topology']), { summary: r() < 0.5, small: r() < 0.5 });
+      const power = { n0: [[0, pick(r, [1, NaN, null, '3', { x: 1 }])], [30, 2]] };
+      const st = { metrics: m, series: { power, vram: {} }, fetchError: null, fetching: false };
+      const vms = [pages.metricsView(ctx, st, { now: 0 }), pages.nodesView(ctx, { metrics: m, now: 0 }),
+        pages.podsView(ctx, { metrics: m, now: 0 })];
+      const sections = [pages.nodeDetailView(ctx.gpuNodes[0], ctx, { metrics: m, series: { power: power.n0 } }),
+        pages.podDetailView(ctx.gpuPods[0], { metrics: m, series: { power: power.n0 } })];
+      mounted += mountAll(view, round, vms, sections);
+      pages.clearViewMemo();
+    }
+    expect(mounted).toBeGreaterThan(ROUNDS * 4);
   });
 });
