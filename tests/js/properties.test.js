@@ -161,6 +161,8 @@ describe('properties', () => {
 describe('malformed cluster objects (what a real apiserver, an old CRD version or a half-written object can hand over)', () => {
   it('no page, detail section, column or index throws on them', async () => {
     const pages = await import('../../src/view/pages.js');
+    const html = await import('../../src/view/html.js');
+    const text = await import('../../src/view/text.js');
     const { createClusterStore } = await import('../../src/api/clusterStore.js');
     const { makeGpuPod, makePlainPod, makePluginPod, makeNode, makeDeviceConfig } = await import('./fixtures.js');
     const r = rng(4242);
@@ -179,13 +181,19 @@ describe('malformed cluster objects (what a real apiserver, an old CRD version o
       await store.refresh();
       const ctx = store.getSnapshot();
       const opts = { now };
-      pages.overviewView(ctx, opts);
-      pages.devicePluginsView(ctx, opts);
-      pages.nodesView(ctx, opts);
-      pages.podsView(ctx, opts);
-      pages.metricsView(ctx, { metrics: null, fetchError: null, fetching: false }, opts);
-      nodes.forEach((n) => pages.nodeDetailView(n, ctx, opts));
-      pods.forEach((p) => pages.podDetailView(p, opts));
+      const vms = [pages.overviewView(ctx, opts), pages.devicePluginsView(ctx, opts), pages.nodesView(ctx, opts),
+        pages.podsView(ctx, opts), pages.metricsView(ctx, { metrics: null, fetchError: null, fetching: false }, opts)];
+      const sections = nodes.map((n) => pages.nodeDetailView(n, ctx, opts)).concat(pods.map((p) => pages.podDetailView(p, opts)));
+      // The HTML (bench, snapshots) and terminal (bin/amd-gpu-dash.js) renderers take them too.
+      vms.forEach((vm) => {
+        expect(typeof html.renderPage(vm)).toBe('string');
+        expect(typeof text.renderText(vm, { color: false })).toBe('string');
+      });
+      sections.forEach((sec) => {
+        if (!sec) return;
+        expect(typeof html.renderSection(sec)).toBe('string');
+        expect(text.textSection(sec, false).every((l) => typeof l === 'string')).toBe(true);
+      });
       const cols = pages.nodeColumns();
       nodes.forEach((n) => cols.forEach((c) => c.getter(n)));
       pages.clearViewMemo();
