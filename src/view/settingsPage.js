@@ -46,11 +46,20 @@ export function createSettingsPage(React, CC, storage) {
     });
     const prom = pr[0];
     const setProm = pr[1];
+    // What the number fields show while being edited; on leaving a field the
+    // validated (maybe clamped) value replaces the draft, so the screen never
+    // shows a number that was not saved.
+    const dr = React.useState(function () {
+      return { requestTimeoutMs: String(s.requestTimeoutMs), seriesMinutes: String(s.seriesMinutes) };
+    });
+    const drafts = dr[0];
+    const setDrafts = dr[1];
 
     function commit(next) {
       const saved = save(next);
       setS(saved);
       if (props && props.onDataChange) props.onDataChange(saved);
+      return saved;
     }
 
     function commitProm(p) {
@@ -58,16 +67,24 @@ export function createSettingsPage(React, CC, storage) {
       commit(parseSettings(Object.assign({}, s, { prometheus: any ? p : null })));
     }
 
-    function numberField(label, value, key) {
+    function numberField(label, key) {
       return h('input', {
         'aria-label': label,
         type: 'number',
         style: INPUT,
-        defaultValue: value,
+        value: drafts[key],
+        onChange: function (e) {
+          const next = Object.assign({}, drafts);
+          next[key] = e.target.value;
+          setDrafts(next);
+        },
         onBlur: function (e) {
           const patch = {};
           patch[key] = Number(e.target.value);
-          commit(parseSettings(Object.assign({}, s, patch)));
+          const saved = commit(parseSettings(Object.assign({}, s, patch)));
+          const next = Object.assign({}, drafts);
+          next[key] = String(saved[key]);
+          setDrafts(next);
         },
       });
     }
@@ -114,8 +131,8 @@ export function createSettingsPage(React, CC, storage) {
               REFRESH_CHOICES.map(function (v) { return h('option', { key: v, value: v }, refreshChoiceLabel(v)); })
             ),
           },
-          { name: 'Request timeout (ms)', value: numberField('Request timeout', s.requestTimeoutMs, 'requestTimeoutMs') },
-          { name: 'Metrics time-series window (min)', value: numberField('Series window', s.seriesMinutes, 'seriesMinutes') },
+          { name: 'Request timeout (ms)', value: numberField('Request timeout', 'requestTimeoutMs') },
+          { name: 'Metrics time-series window (min)', value: numberField('Series window', 'seriesMinutes') },
         ],
       })
     );

@@ -49,6 +49,12 @@ export function render(element, options) {
     style: function (node) { return node.style; },
     click: function (node) { fireEvent.click(node); return handle; },
     change: function (node, value) { fireEvent.change(node, { target: { value: value } }); return handle; },
+    blur: function (node, value) {
+      if (value !== undefined) fireEvent.change(node, { target: { value: value } });
+      fireEvent.blur(node);
+      return handle;
+    },
+    value: function (node) { return node.value; },
     isDisabled: function (node) { return !!node.disabled; },
     textOf: function (node) { return node.textContent; },
     act: function (fn) {

@@ -249,6 +249,9 @@ export class Element extends Node {
     }
     this._value = s;
   }
+  // The value attribute: an uncontrolled field's initial value (React sets defaultValue).
+  get defaultValue() { return this.hasAttribute('value') ? this.getAttribute('value') : ''; }
+  set defaultValue(v) { this.setAttribute('value', v); }
   get options() { return this.localName === 'select' ? this.querySelectorAll('option') : undefined; }
   get selectedIndex() {
     const opts = this.options || [];

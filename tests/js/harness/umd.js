@@ -63,6 +63,19 @@ export function render(element, options) {
       });
       return handle;
     },
+    /** Leave a field (onBlur: React listens to focusout), after typing `value` into it when given. */
+    blur: function (node, value) {
+      act(function () {
+        if (value !== undefined) {
+          setNativeValue(node, value);
+          node.dispatchEvent(new Event('input', { bubbles: true }));
+        }
+        node.dispatchEvent(new Event('focusout', { bubbles: true }));
+      });
+      return handle;
+    },
+    /** What a form field shows. */
+    value: function (node) { return node.value; },
     isDisabled: function (node) { return !!node.disabled; },
     textOf: function (node) { return node.textContent; },
     act: function (fn) {
