@@ -37,11 +37,7 @@ export function render(element, options) {
     /** Leave a field (onBlur), with `value` typed into it when given. */
     blur: function (node, value) { r.blur(node, value); return handle; },
     /** What a form field shows: its controlled value, else its initial (uncontrolled) value. */
-    value: function (node) {
-      const p = node.props;
-      const v = p.value !== undefined ? p.value : p.defaultValue;
-      return v === undefined || v === null ? '' : String(v);
-    },
+    value: function (node) { return r.fieldValue(node); },
     isDisabled: function (node) { return !!node.props.disabled; },
     textOf: function (node) { return textOf(node); },
     /** Run `fn` (an event-like update) and commit what it scheduled. */

@@ -422,3 +422,37 @@ describe('React semantics: useSyncExternalStore (' + tier + ')', () => {
     r.unmount();
   });
 });
+
+describe('React semantics: form fields (' + tier + ')', () => {
+  it('an uncontrolled field keeps what the user typed; a later defaultValue does not reach the screen', () => {
+    const r = render(h('input', { 'aria-label': 'f', defaultValue: 'a' }));
+    expect(r.value(r.byLabel('f'))).toBe('a');
+    r.change(r.byLabel('f'), 'typed');
+    r.rerender(h('input', { 'aria-label': 'f', defaultValue: 'b' }));
+    expect(r.value(r.byLabel('f'))).toBe('typed');
+    r.unmount();
+  });
+
+  it('a controlled field shows its value: what the handler stores, or its old value when the handler ignores the edit', () => {
+    function Field(props) {
+      const st = React.useState('x');
+      return h('input', { 'aria-label': 'f', value: st[0], onChange: (e) => { if (props.accept) st[1](e.target.value.toUpperCase()); } });
+    }
+    const a = render(h(Field, { accept: true }));
+    a.change(a.byLabel('f'), 'abc');
+    expect(a.value(a.byLabel('f'))).toBe('ABC');
+    a.unmount();
+    const b = render(h(Field, { accept: false }));
+    b.change(b.byLabel('f'), 'abc');
+    expect(b.value(b.byLabel('f'))).toBe('x');
+    b.unmount();
+  });
+
+  it('a remount (new key) starts from the new defaultValue', () => {
+    const r = render(h('input', { key: 1, 'aria-label': 'f', defaultValue: 'a' }));
+    r.change(r.byLabel('f'), 'typed');
+    r.rerender(h('input', { key: 2, 'aria-label': 'f', defaultValue: 'b' }));
+    expect(r.value(r.byLabel('f'))).toBe('b');
+    r.unmount();
+  });
+});

@@ -384,6 +384,12 @@ function reconcileChildren(root, parent, children) {
   return out;
 }
 
+/** After an event, a controlled field shows its current `value` prop, whether or not the handler changed it (React restores it). */
+function restoreControlled(node) {
+  const inst = node.instance;
+  if (inst && !inst.unmounted && inst.props.value !== undefined) inst.field = inst.props.value;
+}
+
 function hostProps(props) {
   const p = {};
   for (const k in props) if (k !== 'children') p[k] = props[k];
@@ -395,6 +401,11 @@ function renderInstance(inst, prevProps) {
   const root = inst.root;
   if (typeof t === 'string') {
     inst.renders++;
+    // A form field's displayed value, as the DOM keeps it: set from value /
+    // defaultValue at mount, then only by a controlled `value` or by the user
+    // (change / blur below); a later defaultValue does not reach the screen.
+    if (!('field' in inst)) inst.field = inst.props.value !== undefined ? inst.props.value : inst.props.defaultValue;
+    else if (inst.props.value !== undefined) inst.field = inst.props.value;
     const children = reconcileChildren(root, inst, inst.props.children);
     inst.out = [{ tag: t, props: hostProps(inst.props), children: children, instance: inst }];
   } else if (t === Fragment || t === LIST) {
@@ -753,16 +764,25 @@ export function render(element, options) {
     },
     change: function (node, value) {
       handle.act(function () {
+        node.instance.field = value;
         if (typeof node.props.onChange === 'function') node.props.onChange({ type: 'change', target: { value: value } });
       });
+      restoreControlled(node);
       return handle;
     },
     blur: function (node, value) {
       handle.act(function () {
-        const v = value === undefined ? node.props.value !== undefined ? node.props.value : node.props.defaultValue : value;
+        if (value !== undefined) node.instance.field = value;
+        const v = node.instance.field === undefined ? '' : node.instance.field;
         if (typeof node.props.onBlur === 'function') node.props.onBlur({ type: 'blur', target: { value: v } });
       });
+      restoreControlled(node);
       return handle;
+    },
+    /** What a form field shows (a string, like the DOM's `value`). */
+    fieldValue: function (node) {
+      const v = node.instance.field;
+      return v === undefined || v === null ? '' : String(v);
     },
   };
   return handle;
