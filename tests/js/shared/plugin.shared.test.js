@@ -175,6 +175,7 @@ describe('shared: the pager drives what is rendered and fetched (' + tier + ')',
     r.change(r.byLabel('Filter GPU nodes by name'), '019');
     await r.settle();
     expect(r.text()).toContain('Showing 1–1 of 1 matching "019" (20 GPU nodes)');
+    expect(r.value(r.byLabel('Filter GPU nodes by name'))).toBe('019');
     expect(r.isDisabled(r.byLabel('Next page'))).toBe(true);
     r.unmount();
   });
@@ -186,8 +187,10 @@ describe('shared: the node order drives the page and its query (' + tier + ')', 
     lib.lists.Pod = [[makeGpuPod('hog', { gpus: 8, node: 'mi355x-010' })].concat(lib.lists.Pod[0]), null];
     const r = render(h(route('/amd-gpu/nodes')));
     await r.settle();
+    expect(r.value(r.byLabel('Sort GPU nodes'))).toBe('name');
     r.change(r.byLabel('Sort GPU nodes'), 'in-use');
     await r.settle();
+    expect(r.value(r.byLabel('Sort GPU nodes'))).toBe('in-use');
     const titles = r.byTag('h2').map((n) => r.textOf(n)).filter((t) => /^mi355x-/.test(t));
     expect(titles.slice(0, 3)).toEqual(['mi355x-010', 'mi355x-000', 'mi355x-001']);
     expect(promQueries(fake).pop()).toContain('hostname=~"mi355x-010|mi355x-000|mi355x-001|');
