@@ -611,6 +611,36 @@ export function ownersQuery(pods, small) {
   return 'max by (' + EXPORTER_JOIN_LABELS.join(', ') + ') (' + sel + 'pod=~"' + alt(names) + '", namespace=~"' + alt(nss) + '"})';
 }
 
+/** Total GPU power per pod from the exporter's pod labels; `filter` is a substring of the pod name. */
+export function podPowerSum(filter) {
+  const f = typeof filter === 'string' ? filter.trim().toLowerCase() : '';
+  return 'sum by (namespace, pod) ({__name__="' + SERIES.exporter.power + '", pod!=""' +
+    (f ? ', pod=~".*' + promString(regexLiteral(f)) + '.*"' : '') + '})';
+}
+
+/**
+ * The GPU pods of page `page` (0-based, `per` a page) ranked by the power
+ * of the GPUs they hold, highest first — as powerRankQuery for nodes:
+ * Prometheus ranks, the answer is one page whatever the cluster.
+ */
+export function podPowerRankQuery(page, per, filter) {
+  const r = podPowerSum(filter);
+  const top = function (n) { return 'topk(' + n + ', ' + r + ')'; };
+  return page > 0 ? top(per * (page + 1)) + ' unless on(namespace, pod) ' + top(per * page) : top(per);
+}
+
+/**
+ * A page of GPU pods in power order, in ONE request: the owner series of the
+ * pods the ranking picks, the ranking as `agg="rank"` rows and how many pods
+ * draw GPU power (`agg="ranked"`, the pager's count).
+ */
+export function rankedOwnersQuery(rank) {
+  const s = podPowerRankQuery(rank.page, rank.per, rank.filter);
+  return '(' + ownersQuery(null) + ') and on(namespace, pod) (' + s + ')' +
+    ' or ' + sizeRow(s, 'rank') +
+    ' or ' + sizeRow('count(' + podPowerSum(rank.filter) + ')', 'ranked');
+}
+
 /** The part of a snapshot that belongs to one node (GPU objects shared, not copied). */
 export function nodeSlice(m, nodeName) {
   if (!m) return m;
@@ -1366,6 +1396,10 @@ export function createMetricsSource(opts) {
    * @returns {Promise<GpuMetrics|null>}
    */
   function fetchGpuOwners(opts) {
+    const rank = opts && opts.rank;
+    if (rank) {
+      return shared('owners|rank|' + rank.page + '|' + rank.per + '|' + rank.filter, function () { return ownersRanked(rank); });
+    }
     const pods = opts && Array.isArray(opts.pods) ? opts.pods.map(String) : null;
     const small = !!(opts && opts.small);
     if (small) return shared('owners|small|' + (pods || []).join(','), function () { return ownersSnapshot(pods || [], true); });
@@ -1392,6 +1426,51 @@ export function createMetricsSource(opts) {
           fetchedAt: new Date(clock.now()).toISOString(),
           prometheusPath: base,
           scope: 'owners',
+        };
+        return ownersLast;
+      });
+    }, function () {
+      ownersFailures++;
+      if (ownersLast && ownersFailures < STALE_FAILURES) return Object.assign({}, ownersLast, { stale: true });
+      ownersLast = null;
+      invalidate();
+      return null;
+    });
+  }
+
+  /**
+   * GPU pods in power order (rankedOwnersQuery): the page's owners plus
+   * `rank` = {by, page, per, filter, count, order: "namespace/pod" keys
+   * highest first, watts per key}.
+   */
+  function ownersRanked(rank) {
+    return withPrometheus(function (base) {
+      return combined(base, rankedOwnersQuery(rank)).then(function (res) {
+        if (!res.ok) return UNREACHABLE;
+        ownersFailures = 0;
+        const rows = res.rows;
+        const j = joinExporterResults(rows);
+        const ranked = [];
+        const watts = {};
+        for (let i = 0; i < rows.__agg.length; i++) {
+          const r = rows.__agg[i];
+          if (!isRow(r) || r.metric.agg !== 'rank' || typeof r.metric.pod !== 'string') continue;
+          const key = (typeof r.metric.namespace === 'string' ? r.metric.namespace : '') + '/' + r.metric.pod;
+          const w = num(r.value[1]);
+          ranked.push([key, w === null ? -Infinity : w]);
+          watts[key] = w;
+        }
+        ranked.sort(function (a, b) { return b[1] - a[1] || (a[0] < b[0] ? -1 : a[0] > b[0] ? 1 : 0); });
+        ownersLast = {
+          source: j.gpus.length ? 'amd-exporter' : source,
+          gpus: ownersLast ? shareGpus(ownersLast.gpus, j.gpus) : j.gpus,
+          xgmi: {},
+          links: {},
+          fetchedAt: new Date(clock.now()).toISOString(),
+          prometheusPath: base,
+          scope: 'owners',
+          rank: { by: rank.by, page: rank.page, per: rank.per, filter: rank.filter, count: sizeFromRows(rows.__agg, 'ranked'),
+            order: ranked.map(function (x) { return x[0]; }), watts: watts },
         };
         return ownersLast;
       });

@@ -47,7 +47,9 @@ export interface MetricsSource {
   ): Promise<GpuMetrics | null>;
   fetchNodeMetrics(nodeName: string): Promise<GpuMetrics | null>;
   /** `pods`: "namespace/name" keys of one page of the Pods table; `small` as in fetchGpuMetrics */
-  fetchGpuOwners(opts?: { pods: string[]; small?: boolean }): Promise<GpuMetrics | null>;
+  fetchGpuOwners(
+    opts?: { pods?: string[]; small?: boolean; rank?: { by: 'power'; page: number; per: number; filter: string } }
+  ): Promise<GpuMetrics | null>;
   failureReason(): 'forbidden' | 'unreachable';
   fetchPodSeries(namespace: string, pod: string, rangeSec: number, stepSec: number): Promise<{ rangeSec: number; stepSec: number; power: Array<[number, number]> } | null>;
   fetchNodeSeries(nodeName: string, rangeSec: number, stepSec: number): Promise<{ rangeSec: number; stepSec: number; power: Array<[number, number]> } | null>;
@@ -67,7 +69,12 @@ export interface ProviderCore {
     rank?: { by: 'power'; page: number; per: number; filter: string }
   ): GpuMetricsState;
   useNodeGpuMetrics(nodeName: string | null, enabled?: boolean): GpuMetricsState;
-  useGpuOwners(enabled?: boolean, pods?: string[], small?: boolean): GpuMetricsState;
+  useGpuOwners(
+    enabled?: boolean,
+    pods?: string[],
+    small?: boolean,
+    rank?: { by: 'power'; page: number; per: number; filter: string }
+  ): GpuMetricsState;
   usePodGpuSeries(namespace: string | null, pod: string | null, enabled?: boolean): GpuMetricsState;
   useNodeGpuSeries(nodeName: string | null, enabled?: boolean): GpuMetricsState;
   /** One node's pods for a Node detail section on a cold store (one field-selected request) */

@@ -430,17 +430,21 @@ export function createProviderCore(React, lib, deps) {
    * "namespace/name" keys) is given, else of every pod; `small` as in
    * useGpuMetrics (pages.js ownersScope).
    */
-  function useGpuOwners(enabled, pods, small) {
+  function useGpuOwners(enabled, pods, small, rank) {
     const cluster = clusterKey();
     const source = metricsSourceFor(cluster);
     const on = enabled === undefined ? true : enabled;
-    const scoped = Array.isArray(pods);
+    const scoped = !rank && Array.isArray(pods);
     const keys = scoped ? pods.slice() : null;
     const sm = scoped && !!small;
     const ex = useState(false);
-    const key = 'owners|' + sourceKey(cluster, loadSettings()) + (sm ? smallKey(ex[0], keys) : scoped ? '|pods:' + keys.join(',') : '');
+    // Power order (ownersScope rank): Prometheus picks the page's pods.
+    const rk = rank ? rank.by + ':' + rank.page + ':' + rank.per + ':' + rank.filter : null;
+    const key = 'owners|' + sourceKey(cluster, loadSettings()) +
+      (rk ? '|rank:' + rk : sm ? smallKey(ex[0], keys) : scoped ? '|pods:' + keys.join(',') : '');
     const res = useMetricsFetch(on ? key : null, function () {
-      return source.fetchGpuOwners(scoped ? { pods: keys, small: sm } : undefined).then(function (m) { return [m, null]; });
+      const opts = rank ? { rank: rank } : scoped ? { pods: keys, small: sm } : undefined;
+      return source.fetchGpuOwners(opts).then(function (m) { return [m, null]; });
     }, false, source);
     useExceeded(sm, res, ex);
     return res;

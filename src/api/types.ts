@@ -282,7 +282,16 @@ export interface GpuMetrics {
   /** a size-guarded (small-cluster) snapshot: GPU nodes (pods) reporting, and whether that was more than a page */
   small?: { count: number; limit: number; exceeded: boolean };
   /** a power-ranked page (metrics.js rankedSnapshot): `scope` is in rank order */
-  rank?: { by: 'power'; page: number; per: number; filter: string; count: number; watts: Record<string, number | null> };
+  /** power order: the page Prometheus ranked; `order` ("namespace/pod" keys, highest first) on an owners answer */
+  rank?: {
+    by: 'power';
+    page: number;
+    per: number;
+    filter: string;
+    count: number;
+    watts: Record<string, number | null>;
+    order?: string[];
+  };
 }
 
 /** Cluster totals (metrics.js totalsFromRows / summarizeMetrics + nodes reporting). */

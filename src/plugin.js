@@ -130,7 +130,7 @@ export function createPlugin(env) {
     const ctx = core.useAmdGpuContext();
     const pager = usePager('pods');
     const o = ownersScope(ctx, pager.state);
-    const m = core.useGpuOwners(o.enabled, o.pods, o.small);
+    const m = core.useGpuOwners(o.enabled, o.pods, o.small, o.rank);
     // As on GPU Nodes: the lists are watches; Refresh renews the attribution.
     return h(Page, {
       vm: podsView(ctx, { metrics: m.metrics, pager: pager.state, fetching: m.fetching }), onRefresh: m.refresh,

@@ -675,11 +675,39 @@ export const POD_SORTS = Object.freeze([
   Object.freeze({ value: 'attention', label: 'Not running first' }),
 ]);
 
-/** The pager state's sort if it is one of POD_SORTS, else 'name'. */
-export function podSortOf(state) {
+/**
+ * The GPU Pods table's orders: POD_SORTS plus the power of the GPUs each pod
+ * holds, ranked by Prometheus (metrics.js rankedOwnersQuery) from the
+ * exporter's pod labels, so one page is asked for whatever the cluster.
+ */
+export const RANKED_POD_SORTS = Object.freeze(POD_SORTS.concat([Object.freeze({ value: 'power', label: 'Highest GPU power' })]));
+
+/** The pager state's sort if it is one of `sorts` (default POD_SORTS), else 'name'. */
+export function podSortOf(state, sorts) {
   const want = state && state.sort;
-  for (let i = 0; i < POD_SORTS.length; i++) if (POD_SORTS[i].value === want) return want;
+  const list = sorts || POD_SORTS;
+  for (let i = 0; i < list.length; i++) if (list[i].value === want) return want;
   return 'name';
+}
+
+/** The rank of a power-ordered owners answer as a pager page: its pods, in rank order, out of the pods ranked. */
+function rankedPodPage(ctx, m, state) {
+  const byKey = memo('pods-by-key', [ctx.gpuPods], function () {
+    const out = new Map();
+    for (let i = 0; i < ctx.gpuPods.length; i++) out.set(podKeyOf(ctx.gpuPods[i]), ctx.gpuPods[i]);
+    return out;
+  });
+  return memo('pods-ranked-page', [m, byKey], function () {
+    const r = m.rank;
+    const pods = [];
+    for (let i = 0; i < r.order.length; i++) if (byKey.has(r.order[i])) pods.push(byKey.get(r.order[i]));
+    const count = Math.max(r.count, r.page * r.per + pods.length);
+    const from = Math.min(r.page * r.per, count);
+    return {
+      nodes: pods, names: pods.map(podKeyOf), page: r.page, pages: Math.max(1, Math.ceil(count / r.per)), from: from,
+      to: from + pods.length, total: count, matched: count, filter: (state && state.filter) || '', perPage: r.per, ranked: true,
+    };
+  });
 }
 
 function podComparator(sort) {
@@ -1092,6 +1120,14 @@ function nodesHeadItems(ctx, now, powerByNode, pg, sort) {
  */
 export function ownersScope(ctx, state) {
   if (!ctx) return { enabled: false, pods: [] };
+  // Power order: Prometheus picks the page — no pod list needed.
+  if (podSortOf(state, RANKED_POD_SORTS) === 'power') {
+    const st = state || {};
+    return {
+      enabled: true,
+      rank: { by: 'power', page: Math.max(0, Math.floor(st.page) || 0), per: PODS_PER_PAGE, filter: (st.filter || '').trim().toLowerCase() },
+    };
+  }
   if (ctx.podsState === 'error') return { enabled: true, pods: undefined };
   // As telemetryScope: every owner of a small cluster in the first wave.
   if (ctx.podsState !== 'ready' && ctx.loading) return { enabled: true, pods: [], small: true };
@@ -1131,8 +1167,9 @@ export function podsView(ctx, opts) {
   const assign = opts && opts.metrics ? podGpuAssignments(opts.metrics) : null;
   // One page of the GPU pod table (PODS_PER_PAGE, filter on namespace/name
   // and node): the reference lists every GPU pod (PodsPage.tsx:201-236).
-  const pg = podPage(ctx.gpuPods, opts && opts.pager);
-  const sort = podSortOf(opts && opts.pager);
+  const sort = podSortOf(opts && opts.pager, RANKED_POD_SORTS);
+  const m = opts && opts.metrics;
+  const pg = sort === 'power' && m && m.rank ? rankedPodPage(ctx, m, opts.pager) : podPage(ctx.gpuPods, opts && opts.pager);
   const items = memo('pods', [pg, ctx.index, ctx.error, assign, sort], function () {
     return podsItems(ctx, now, assign, pg, sort);
   }, now);
@@ -1169,7 +1206,7 @@ function podsItems(ctx, now, assign, pg, sort) {
     const exact = assign && Object.keys(assign).length > 0;
     const cols = ['Name', 'Namespace', 'Node', 'Phase', 'GPU Resources', 'Restarts', 'Age'];
     if (exact) cols.splice(5, 0, 'Assigned GPUs', 'GPU Power');
-    items.push(pager(pg, 'GPU pods', { sort: sort, sorts: POD_SORTS }));
+    items.push(pager(pg, pg.ranked ? 'GPU pods drawing power' : 'GPU pods', { sort: sort, sorts: RANKED_POD_SORTS }));
     items.push(
       section('All GPU Pods', [
         table(

@@ -17,7 +17,7 @@ import { DEVICE_CONFIG_LIST_PATH } from '../../src/api/amdgpu.js';
 import {
   ALL_NODES_SERIES, RANKED_NODE_SORTS, NODE_SORTS, NODES_PER_PAGE, OVERVIEW_PLUGIN_PODS, PODS_PER_PAGE, clearViewMemo, devicePluginsView,
   metricsView, nodePage, nodeSortOf, nodesView, overviewView, ownersScope, podPage, podSortOf, podsView, POD_SORTS,
-  telemetryScope,
+  RANKED_POD_SORTS, telemetryScope,
 } from '../../src/view/pages.js';
 import { renderText } from '../../src/view/text.js';
 import { countRows, findSection, pagerOf, pagerText, rowValue, sectionTitles } from '../../src/view/ir.js';
@@ -149,9 +149,69 @@ describe('GPU Pods order', () => {
     const vm = podsView(ctx, { pager: { sort: 'gpus' } });
     expect(findSection(vm, 'All GPU Pods').blocks[0].rows[0][0]).toBe('b-big');
     const p = pagerOf(vm);
-    expect([p.sort, p.sorts.map((o) => o.value)]).toEqual(['gpus', POD_SORTS.map((o) => o.value)]);
+    expect([p.sort, p.sorts.map((o) => o.value)]).toEqual(['gpus', RANKED_POD_SORTS.map((o) => o.value)]);
+    expect(RANKED_POD_SORTS.map((o) => o.value)).toEqual(POD_SORTS.map((o) => o.value).concat(['power']));
     expect(ownersScope(ctx, { sort: 'gpus' }).pods[0]).toBe('ml/b-big');
     expect(podPage(ctx.gpuPods, { sort: 'gpus' }, 'plugin-pod').names[0]).toBe('ml/a-small');
+  });
+});
+
+describe('GPU Pods in power order: Prometheus ranks the pods by the power of the GPUs they hold', () => {
+  // 30 GPU pods on one node; pod i holds GPU i % 8 and draws 100 + 10 * ((i * 7) % 30) W, so power order is not name order.
+  function cluster() {
+    const nodes = [makeGpuNode('mi355x-000')];
+    const pods = [];
+    const d = exporterData(['mi355x-000']);
+    const E = SERIES.exporter;
+    d[E.power] = [];
+    for (let i = 0; i < 30; i++) {
+      const name = 'job-' + String(i).padStart(2, '0');
+      pods.push(makeGpuPod(name, { gpus: 1, node: 'mi355x-000' }));
+      d[E.power].push({ metric: { __name__: E.power, hostname: 'mi355x-000', gpu_id: String(i % 8), instance: 'x', pod: name, namespace: 'ml' },
+        value: [0, String(100 + 10 * ((i * 7) % 30))] });
+    }
+    d[E.power].push({ metric: { __name__: E.power, hostname: 'mi355x-000', gpu_id: '7', instance: 'x' }, value: [0, '999'] }); // no owner
+    return { ctx: makeContext({ nodes, pods }), fake: prom({ data: d }) };
+  }
+  const watts = (i) => 100 + 10 * ((i * 7) % 30);
+  const byPower = Array.from({ length: 30 }, (_, i) => i).sort((a, b) => watts(b) - watts(a)).map((i) => 'job-' + String(i).padStart(2, '0'));
+
+  it('the owner query asks Prometheus for one ranked page; the table shows it in power order with its GPUs', async () => {
+    const { ctx, fake } = cluster();
+    const state = { sort: 'power', page: 0 };
+    const o = ownersScope(ctx, state);
+    expect(o.rank).toEqual({ by: 'power', page: 0, per: PODS_PER_PAGE, filter: '' });
+    const s = createMetricsSource({ request: fake });
+    const m = await s.fetchGpuOwners({ rank: o.rank });
+    expect(m.rank.count).toBe(30);
+    expect(m.rank.order).toEqual(byPower.slice(0, PODS_PER_PAGE).map((n) => 'ml/' + n));
+    expect(decoded(fake).filter((q) => q.indexOf('topk(' + PODS_PER_PAGE + ', sum by (namespace, pod)') >= 0).length).toBe(1);
+    const vm = podsView(ctx, { metrics: m, pager: state });
+    const rows = findSection(vm, 'All GPU Pods').blocks[0].rows;
+    expect(rows.map((r) => r[0])).toEqual(byPower.slice(0, PODS_PER_PAGE));
+    expect(findSection(vm, 'All GPU Pods').blocks[0].columns).toContain('GPU Power');
+    expect(pagerText(pagerOf(vm))).toBe('Showing 1–25 of 30 GPU pods drawing power · page 1 of 2');
+  });
+
+  it('page 2 and a name filter are ranked by Prometheus too', async () => {
+    const { ctx, fake } = cluster();
+    const s = createMetricsSource({ request: fake });
+    const p2 = await s.fetchGpuOwners({ rank: ownersScope(ctx, { sort: 'power', page: 1 }).rank });
+    expect(p2.rank.order).toEqual(byPower.slice(PODS_PER_PAGE).map((n) => 'ml/' + n));
+    const f = await s.fetchGpuOwners({ rank: ownersScope(ctx, { sort: 'power', filter: ' JOB-1' }).rank });
+    expect(f.rank.count).toBe(10);
+    expect(f.rank.order.every((k) => /^ml\/job-1\d$/.test(k))).toBe(true);
+    const vm = podsView(ctx, { metrics: f, pager: { sort: 'power', filter: ' JOB-1' } });
+    expect(findSection(vm, 'All GPU Pods').blocks[0].rows).toHaveLength(10);
+  });
+
+  it('before the ranked answer the page shows the name order; the client orders never ask Prometheus to rank', () => {
+    const { ctx } = cluster();
+    const vm = podsView(ctx, { pager: { sort: 'power' } });
+    expect(findSection(vm, 'All GPU Pods').blocks[0].rows[0][0]).toBe('job-00');
+    expect(pagerOf(vm).sort).toBe('power');
+    expect(ownersScope(ctx, { sort: 'gpus' }).rank).toBeUndefined();
+    expect(podSortOf({ sort: 'power' }, RANKED_POD_SORTS)).toBe('power');
   });
 });
 

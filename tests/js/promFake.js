@@ -78,16 +78,18 @@ function term(q, rows) {
     return pass ? term(guard[1], rows) : [];
   }
   // rankedClusterQuery: the page's rows, the ranking, the ranked count.
-  const onRank = /^\((.*)\) and on\(hostname\) \((topk\(.*)\)$/.exec(q);
+  // (rankedOwnersQuery: the same on (namespace, pod).)
+  const onRank = /^\((.*)\) and on\((hostname|namespace, pod)\) \((topk\(.*)\)$/.exec(q);
   if (onRank) {
-    const ranked = rankOf(onRank[2], rows) || [];
+    const ranked = rankOf(onRank[3], rows) || [];
     const keep = {};
     ranked.forEach((x) => (keep[x[0]] = true));
-    return term(onRank[1], rows).filter((r) => keep[r.metric.hostname]);
+    const keyOf = onRank[2] === 'hostname' ? (r) => r.metric.hostname : (r) => r.metric.namespace + '/' + r.metric.pod;
+    return term(onRank[1], rows).filter((r) => keep[keyOf(r)]);
   }
   const rankRow = /^label_replace\((topk\(.*\)), "agg", "rank", "", ""\)$/.exec(q);
-  if (rankRow) return (rankOf(rankRow[1], rows) || []).map((x) => vec({ hostname: x[0], agg: 'rank' }, x[1]));
-  const rankedCount = /^label_replace\(count\((sum by \(hostname\) .*)\), "agg", "ranked", "", ""\)$/.exec(q);
+  if (rankRow) return (rankOf(rankRow[1], rows) || []).map((x) => vec(Object.assign({ agg: 'rank' }, x[2]), x[1]));
+  const rankedCount = /^label_replace\(count\((sum by \((?:hostname|namespace, pod)\) .*)\), "agg", "ranked", "", ""\)$/.exec(q);
   if (rankedCount) {
     const n = (powerSums(rankedCount[1], rows) || []).length;
     return n ? [vec({ agg: 'ranked' }, n)] : [];
@@ -132,22 +134,33 @@ function term(q, rows) {
   return rows.filter((r) => re.test(r.metric.__name__ || '') && hostOk(r.metric.hostname));
 }
 
-/** metrics.js nodePowerSum over `rows`: [[hostname, watts], …] (null for another shape). */
+/**
+ * metrics.js nodePowerSum / podPowerSum over `rows`: [[key, watts, labels], …]
+ * (key = hostname, or "namespace/pod"; null for another shape).
+ */
 function powerSums(expr, rows) {
+  const unesc = (v) => new RegExp('^(?:' + v.replace(/\\\\/g, '\\') + ')$');
   const m = /^sum by \(hostname\) \(\{__name__="([a-z_]+)"(?:, hostname=~"(.*)")?\}\)$/.exec(expr);
-  if (!m) return null;
-  const re = m[2] !== undefined ? new RegExp('^(?:' + m[2].replace(/\\\\/g, '\\') + ')$') : null;
+  const p = m ? null : /^sum by \(namespace, pod\) \(\{__name__="([a-z_]+)", pod!=""(?:, pod=~"(.*)")?\}\)$/.exec(expr);
+  const x = m || p;
+  if (!x) return null;
+  const re = x[2] !== undefined ? unesc(x[2]) : null;
   const by = {};
+  const labels = {};
   rows.forEach((r) => {
-    if (r.metric.__name__ !== m[1] || (re && !re.test(r.metric.hostname || ''))) return;
-    by[r.metric.hostname] = (by[r.metric.hostname] || 0) + parseFloat(r.value[1]);
+    if (r.metric.__name__ !== x[1]) return;
+    if (p && !r.metric.pod) return;
+    const k = m ? r.metric.hostname : r.metric.namespace + '/' + r.metric.pod;
+    if (re && !re.test((m ? r.metric.hostname : r.metric.pod) || '')) return;
+    by[k] = (by[k] || 0) + parseFloat(r.value[1]);
+    labels[k] = m ? { hostname: r.metric.hostname } : { namespace: r.metric.namespace, pod: r.metric.pod };
   });
-  return Object.keys(by).map((h) => [h, by[h]]);
+  return Object.keys(by).map((k) => [k, by[k], labels[k]]);
 }
 
 /** metrics.js powerRankQuery: the ranked page, [[hostname, watts], …] (null for another shape). */
 function rankOf(expr, rows) {
-  const m = /^topk\((\d+), (.*?)\)(?: unless on\(hostname\) topk\((\d+), (.*)\))?$/.exec(expr);
+  const m = /^topk\((\d+), (.*?)\)(?: unless on\((?:hostname|namespace, pod)\) topk\((\d+), (.*)\))?$/.exec(expr);
   if (!m) return null;
   const all = powerSums(m[2], rows);
   if (!all) return null;

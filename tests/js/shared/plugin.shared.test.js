@@ -211,6 +211,24 @@ describe('shared: Metrics in power order (' + tier + ')', () => {
   });
 });
 
+describe('shared: GPU Pods in power order (' + tier + ')', () => {
+  it('"Highest GPU power" asks Prometheus for the ranked page of pods and lists the hungriest first', async () => {
+    const fake = cluster();
+    // the exporter fixture labels GPU 0 / 1 of each node with pods ml/train-0 (700 W) and ml/train-1 (701 W)
+    lib.lists.Pod = [[makeGpuPod('train-0', { gpus: 1, node: 'mi355x-000' }), makeGpuPod('train-1', { gpus: 1, node: 'mi355x-001' })], null];
+    const r = render(h(route('/amd-gpu/pods')));
+    await r.settle();
+    r.change(r.byLabel('Sort GPU pods'), 'power');
+    await r.settle();
+    expect(promQueries(fake).filter((q) => q.indexOf('sum by (namespace, pod)') >= 0).length).toBeGreaterThan(0);
+    expect(r.text()).toContain('Showing 1–2 of 2 GPU pods drawing power');
+    const text = r.text();
+    expect(text.indexOf('train-1')).toBeLessThan(text.indexOf('train-0'));
+    expect(r.value(r.byLabel('Sort GPU pods drawing power'))).toBe('power');
+    r.unmount();
+  });
+});
+
 describe('shared: native-view sections (' + tier + ')', () => {
   it('Node detail on a cold store: the node\'s own pods, no cluster-wide list', async () => {
     cluster();

@@ -319,3 +319,41 @@ def test_topk_bottomk_and_the_power_ranked_page():
     ranks = {r["metric"]["hostname"]: float(r["value"][1]) for r in rows if r["metric"].get("agg") == "rank"}
     (count,) = [float(r["value"][1]) for r in rows if r["metric"].get("agg") == "ranked"]
     assert data == {"c", "a"} and ranks == {"c": 400.0, "a": 200.0} and count == 5
+
+
+def test_the_pod_power_ranked_page():
+    """metrics.js rankedOwnersQuery: the owner series of the page's pods, their rank rows, the count; name filter."""
+    import subprocess
+
+    from headlamp_intel_gpu_plugin_amd.utils.nodebridge import ROOT, node_binary
+
+    d = TSDB()
+    # pod -> (namespace, node, GPUs, watts per GPU)
+    pods = {"train-a": ("ml", "n0", 4, 300.0), "train-b": ("ml", "n0", 2, 500.0), "infer-c": ("web", "n1", 1, 200.0),
+            "train-d": ("ml", "n1", 2, 50.0)}
+    gid = {"n0": 0, "n1": 0}
+    for pod, (ns, node, n, w) in pods.items():
+        for _ in range(n):
+            d.add(Series({"__name__": "gpu_power_usage", "hostname": node, "gpu_id": str(gid[node]), "pod": pod,
+                          "namespace": ns}, fn=lambda t, w=w: w))
+            gid[node] += 1
+    d.add(Series({"__name__": "gpu_power_usage", "hostname": "n1", "gpu_id": "7"}, fn=lambda t: 90.0))  # idle GPU
+
+    def ranked(page, per, flt):
+        js = ("import('./src/api/metrics.js').then(m => process.stdout.write(m.rankedOwnersQuery("
+              "{by: 'power', page: %d, per: %d, filter: %s})))" % (page, per, json.dumps(flt)))
+        q = subprocess.run([node_binary(), "-e", js], cwd=ROOT, capture_output=True, text=True, timeout=60).stdout
+        rows = _vec(query(d, q, 100.0))
+        owners = {(r["metric"]["namespace"], r["metric"]["pod"]) for r in rows if "agg" not in r["metric"]}
+        ranks = {r["metric"]["pod"]: float(r["value"][1]) for r in rows if r["metric"].get("agg") == "rank"}
+        (count,) = [float(r["value"][1]) for r in rows if r["metric"].get("agg") == "ranked"]
+        return owners, ranks, count
+
+    # totals: train-a 1200, train-b 1000, infer-c 200, train-d 100 W
+    owners, ranks, count = ranked(0, 2, "")
+    assert ranks == {"train-a": 1200.0, "train-b": 1000.0} and count == 4
+    assert owners == {("ml", "train-a"), ("ml", "train-b")}
+    owners, ranks, count = ranked(1, 2, "")
+    assert ranks == {"infer-c": 200.0, "train-d": 100.0} and owners == {("web", "infer-c"), ("ml", "train-d")}
+    owners, ranks, count = ranked(0, 2, "TRAIN-")
+    assert ranks == {"train-a": 1200.0, "train-b": 1000.0} and count == 3
