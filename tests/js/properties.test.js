@@ -251,6 +251,8 @@ describe('malformed Prometheus answers', () => {
         const agg = pick(r, ['rank', 'ranked', 'gpu_nodes', 'gpu_pods', 'sum', 'count', 'nodes', pick(r, WRONG)]);
         const metric = { agg: agg };
         if (r() < 0.7) metric.hostname = pick(r, ['n0', 'n1', 'ghost', pick(r, WRONG)]);
+        if (r() < 0.4) metric.pod = pick(r, ['train-0', 'ghost', pick(r, WRONG)]);
+        if (r() < 0.4) metric.namespace = pick(r, ['ml', pick(r, WRONG)]);
         if (r() < 0.5) metric.__name__ = pick(r, ['gpu_power_usage', 'gpu_total_vram', pick(r, WRONG)]);
         rows.push({ metric: metric, value: [0, pick(r, ['12', '0', '9e99'].concat(WRONG))] });
       }
@@ -260,6 +262,8 @@ describe('malformed Prometheus answers', () => {
       const ranked = await src.fetchGpuMetrics('gauges', { rank: { by: 'power', page: Math.floor(r() * 3), per: 8, filter: '' }, summary: true });
       const small = await src.fetchGpuMetrics('topology', { scope: r() < 0.5 ? [] : ['n0'], small: true });
       const owners = await src.fetchGpuOwners({ pods: [], small: true });
+      const rankedOwners = await src.fetchGpuOwners({ rank: { by: 'power', page: Math.floor(r() * 3), per: 25, filter: '' } });
+      if (rankedOwners) pages.podsView(ctx, { metrics: rankedOwners, now: 0, pager: { sort: 'power' } });
       for (const m of [ranked, small, owners]) {
         const st = { metrics: m, series: null, fetchError: null, fetching: false };
         pages.metricsView(ctx, st, { now: 0, pager: { sort: pick(r, ['power', 'name', 'in-use']) } });

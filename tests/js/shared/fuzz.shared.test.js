@@ -116,8 +116,9 @@ describe('shared: malformed clusters render (' + tier + ')', () => {
       const m = await src.fetchGpuMetrics(pick(r, ['gauges', 'topology']), { summary: r() < 0.5, small: r() < 0.5 });
       const power = { n0: [[0, pick(r, [1, NaN, null, '3', { x: 1 }])], [30, 2]] };
       const st = { metrics: m, series: { power, vram: {} }, fetchError: null, fetching: false };
+      const ro = await src.fetchGpuOwners({ rank: { by: 'power', page: 0, per: 25, filter: '' } });
       const vms = [pages.metricsView(ctx, st, { now: 0 }), pages.nodesView(ctx, { metrics: m, now: 0 }),
-        pages.podsView(ctx, { metrics: m, now: 0 })];
+        pages.podsView(ctx, { metrics: m, now: 0 }), pages.podsView(ctx, { metrics: ro, now: 0, pager: { sort: 'power' } })];
       const sections = [pages.nodeDetailView(ctx.gpuNodes[0], ctx, { metrics: m, series: { power: power.n0 } }),
         pages.podDetailView(ctx.gpuPods[0], { metrics: m, series: { power: power.n0 } })];
       mounted += mountAll(view, round, vms, sections);
