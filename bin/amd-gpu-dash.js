@@ -22,7 +22,8 @@ import { createClusterStore } from '../src/api/clusterStore.js';
 import { createMetricsSource } from '../src/api/metrics.js';
 import { parsePrometheus, prometheusCandidates } from '../src/api/settings.js';
 import {
-  NODE_SORTS, POD_SORTS, devicePluginsView, metricsView, nodeDetailView, nodesView, overviewView, podDetailView, podsView,
+  NODES_PER_PAGE, NODE_SORTS, PODS_PER_PAGE, POD_SORTS, RANKED_NODE_SORTS, RANKED_POD_SORTS, devicePluginsView, metricsView,
+  nodeDetailView, nodesView, overviewView, podDetailView, podsView,
 } from '../src/view/pages.js';
 import { renderText, textSection } from '../src/view/text.js';
 
@@ -33,7 +34,7 @@ function usage(msg) {
   process.stderr.write(
     'usage: amd-gpu-dash [--url http://127.0.0.1:8001] [--page ' + PAGES.join('|') + '|all|node:NAME|pod:NS/NAME]\n' +
       '                    [--watch SECONDS] [--filter TEXT] [--page-number N] [--per-page N]\n' +
-      '                    [--sort name|in-use|free|attention (nodes) | gpus|newest|attention (pods)]\n' +
+      '                    [--sort name|in-use|free|attention (nodes) | gpus|newest|attention (pods) | power (nodes, metrics, pods)]\n' +
       '                    [--prometheus NAMESPACE/SERVICE:PORT] [--timeout MS] [--token TOKEN] [--insecure]\n' +
       '                    [--color] [--json]\n'
   );
@@ -84,7 +85,7 @@ export function parseArgs(argv) {
   if (!(a.watch >= 0) || !(a.timeout > 0)) return { error: 'bad --watch / --timeout' };
   if (!(a.pager.page >= 0) || (a.pager.perPage !== undefined && !(a.pager.perPage > 0))) return { error: 'bad --page-number / --per-page' };
   // Node orders apply to the GPU node pages, pod orders to GPU Pods ('name' to both).
-  const sorts = NODE_SORTS.concat(POD_SORTS).map(function (o) { return o.value; })
+  const sorts = NODE_SORTS.concat(POD_SORTS, RANKED_NODE_SORTS, RANKED_POD_SORTS).map(function (o) { return o.value; })
     .filter(function (v, i, all) { return all.indexOf(v) === i; });
   if (a.pager.sort !== undefined && sorts.indexOf(a.pager.sort) < 0) return { error: 'bad --sort (one of ' + sorts.join(', ') + ')' };
   return a;
@@ -197,10 +198,17 @@ async function main() {
     return;
   }
 
+  // --sort power on one page: Prometheus ranks and returns that page (metrics.js rankedClusterQuery / rankedOwnersQuery).
+  const rank = a.pager.sort === 'power' && (view === 'topology' || view === 'gauges' || view === 'owners')
+    ? { by: 'power', page: a.pager.page, per: a.pager.perPage || (view === 'owners' ? PODS_PER_PAGE : NODES_PER_PAGE),
+      filter: (a.pager.filter || '').trim().toLowerCase() }
+    : null;
+
   async function fetchAll(first) {
     const jobs = [
       store.refresh(),
-      view === 'owners' ? metrics.fetchGpuOwners() : view ? metrics.fetchGpuMetrics(view) : Promise.resolve(null),
+      view === 'owners' ? metrics.fetchGpuOwners(rank ? { rank: rank } : undefined)
+        : view ? metrics.fetchGpuMetrics(view, rank ? { rank: rank, summary: view === 'gauges' } : undefined) : Promise.resolve(null),
       view === 'all' || view === 'gauges' ? metrics.fetchSeries(1800, 30) : Promise.resolve(null),
     ];
     if (first) jobs.push(store.loadLists());

@@ -105,3 +105,14 @@ def test_sort_flag_orders_the_nodes(url):
     assert bad.returncode == 2 and "bad --sort" in bad.stderr
     pods = run("--url", url, "--page", "pods", "--sort", "gpus")
     assert pods.returncode == 0 and "sorted: Most GPUs held" in pods.stdout
+
+
+def test_sort_power_lets_prometheus_rank_the_page(url):
+    for page, noun in (("nodes", "GPU nodes reporting"), ("metrics", "GPU nodes reporting"), ("pods", "GPU pods drawing power")):
+        r = run("--url", url, "--page", page, "--json", "--sort", "power")
+        assert r.returncode == 0, r.stderr
+        pager = [i for i in json.loads(r.stdout)["items"] if i["t"] == "pager"][0]
+        assert pager["sort"] == "power" and pager["noun"] == noun, (page, pager)
+        assert pager["total"] > 0, (page, pager)
+    text = run("--url", url, "--page", "pods", "--sort", "power")
+    assert text.returncode == 0 and "sorted: Highest GPU power" in text.stdout, text.stdout[-800:]
