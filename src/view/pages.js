@@ -1169,7 +1169,8 @@ export function podsView(ctx, opts) {
   // and node): the reference lists every GPU pod (PodsPage.tsx:201-236).
   const sort = podSortOf(opts && opts.pager, RANKED_POD_SORTS);
   const m = opts && opts.metrics;
-  const pg = sort === 'power' && m && m.rank ? rankedPodPage(ctx, m, opts.pager) : podPage(ctx.gpuPods, opts && opts.pager);
+  const ranked = sort === 'power' && m && m.rank && Array.isArray(m.rank.order);
+  const pg = ranked ? rankedPodPage(ctx, m, opts.pager) : podPage(ctx.gpuPods, opts && opts.pager);
   const items = memo('pods', [pg, ctx.index, ctx.error, assign, sort], function () {
     return podsItems(ctx, now, assign, pg, sort);
   }, now);
