@@ -22,6 +22,13 @@ const h = React.createElement;
 const env = (k) => (typeof process !== 'undefined' && process.env[k]) || null;
 const ROUNDS = Number(env('FUZZ_RENDER_ROUNDS') || 40);
 const SEED = Number(env('FUZZ_SEED') || 9001);
+// Mutations applied to each mutated object (FUZZ_MUTATIONS widens the search).
+const PASSES = Number(env('FUZZ_MUTATIONS') || 1);
+const mutateN = (r, o) => {
+  let x = o;
+  for (let i = 0; i < PASSES; i++) x = mutate(r, x, 0);
+  return x;
+};
 
 /** Mount every view-model and section; a failure names the round and the view. */
 function mountAll(view, round, vms, sections) {
@@ -60,10 +67,10 @@ describe('shared: malformed clusters render (' + tier + ')', () => {
     let mounted = 0;
     for (let round = 0; round < ROUNDS; round++) {
       const nodes = [makeGpuNode('g0'), makeGpuNode('g1', { partition: 'CPX/NPS4' }), makeNode('c0')]
-        .map((n) => (r() < 0.6 ? mutate(r, n, 0) : n));
+        .map((n) => (r() < 0.6 ? mutateN(r, n) : n));
       const pods = [makeGpuPod('a', { node: 'g0', gpus: 2 }), makeGpuPod('b', { node: 'g1' }), makePlainPod('w', 'c0'), makePluginPod('dp')]
-        .map((p) => (r() < 0.6 ? mutate(r, p, 0) : p));
-      const dcs = [makeDeviceConfig()].map((d) => (r() < 0.6 ? mutate(r, d, 0) : d));
+        .map((p) => (r() < 0.6 ? mutateN(r, p) : p));
+      const dcs = [makeDeviceConfig()].map((d) => (r() < 0.6 ? mutateN(r, d) : d));
       const store = createClusterStore({
         request: (path) => Promise.resolve({ kind: 'List', items: path.indexOf('deviceconfigs') >= 0 ? dcs : [] }),
       });
