@@ -495,37 +495,7 @@ describe('pager state survives leaving and reopening a page (this tab)', () => {
     const m = {};
     return { getItem: (k) => (k in m ? m[k] : null), setItem: (k, v) => { m[k] = String(v); }, m };
   }
-  it('GPU Nodes comes back on the same filter, order and page; other pages and clusters keep their own', async () => {
-    lib.resetHeadlamp();
-    resetSharedStores();
-    const names = Array.from({ length: 20 }, (_, i) => 'mi355x-' + String(i).padStart(3, '0'));
-    lib.lists.Node = [names.map((n) => makeGpuNode(n)), null];
-    lib.lists.Pod = [[], null];
-    lib.api.handler = () => Promise.reject(Object.assign(new Error('503'), { status: 503 }));
-    const storage = memStorage();
-    const plugin = createPlugin({ React, lib, CommonComponents: CC, viewStorage: storage });
-    const a = render(h(plugin.routeComponent('nodes')));
-    await a.settle();
-    a.change(a.getByLabelText('Sort GPU nodes'), 'attention');
-    a.change(a.getByLabelText('Filter GPU nodes by name'), 'x-01');
-    await a.settle();
-    a.click(a.getByLabelText('Next page'));
-    await a.settle();
-    expect(a.text()).toContain('Showing 9–10 of 10 matching "x-01" (20 GPU nodes)');
-    a.unmount();
-    const b = render(h(plugin.routeComponent('nodes')));
-    await b.settle();
-    expect(b.text()).toContain('Showing 9–10 of 10 matching "x-01" (20 GPU nodes)');
-    expect(b.getByLabelText('Sort GPU nodes').props.value).toBe('attention');
-    b.unmount();
-    const m = render(h(plugin.routeComponent('metrics')));
-    await m.settle();
-    m.unmount();
-    const keys = Object.keys(storage.m);
-    expect(keys.every((k) => k.indexOf('headlamp-amd-gpu-plugin.view.') === 0)).toBe(true);
-    const metricsKey = keys.filter((k) => /\|metrics$/.test(k))[0];
-    expect(JSON.parse(storage.m[metricsKey])).toEqual({ page: 0, filter: '', sort: 'name' });
-  });
+  // Leaving and reopening GPU Nodes through the controls: tests/js/shared/viewstate.shared.test.js (both React tiers).
   it('unreadable or hostile stored state falls back to the first page', async () => {
     const { loadViewState } = await import('../../src/api/settings.js');
     const st = memStorage();
