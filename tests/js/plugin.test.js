@@ -453,42 +453,7 @@ describe('React StrictMode (effects mounted, cleaned up and mounted again)', () 
   });
 });
 
-describe('Pod detail: power history next to the node telemetry', () => {
-  it('sends the node-scoped query and the pod-scoped range query in one wave and shows the history', async () => {
-    cluster();
-    const fake = prom({ data: exporterData(['mi355x-0', 'mi355x-1']) });
-    const crd = lib.api.handler;
-    lib.api.handler = (p) => (p.indexOf('/proxy/api/v1/') >= 0 ? fake(p) : crd(p));
-    const pod = makeGpuPod('train-a', { gpus: 4 });
-    const Detail = reg.details[1];
-    const r = render(h(() => Detail({ resource: { kind: 'Pod', jsonData: pod } })));
-    await r.settle();
-    const paths = fake.mock.calls.map((c) => decodeURIComponent(c[0]));
-    expect(paths.filter((p) => p.indexOf('hostname="mi355x-0"') >= 0)).toHaveLength(1);
-    expect(paths.filter((p) => p.indexOf('/query_range') >= 0 && p.indexOf('pod="train-a"') >= 0)).toHaveLength(1);
-    expect(r.html()).toContain('Peak GPU Power');
-    r.unmount();
-  });
-});
-
-describe('Metrics page without RBAC for the Prometheus proxy', () => {
-  it('says access was denied and which permission is missing, not "unreachable"', async () => {
-    cluster();
-    const crd = lib.api.handler;
-    lib.api.handler = (p) => (p.indexOf('/proxy/api/v1/') >= 0
-      ? Promise.reject(Object.assign(new Error('services "kube-prometheus-stack-prometheus" is forbidden'), { status: 403 }))
-      : crd(p));
-    // A fresh plugin: the shared one's metrics client still holds earlier specs' snapshots (served stale on failure).
-    const fresh = createPlugin({ React, lib, CommonComponents: CC });
-    const r = render(h(fresh.AmdGpuDataProvider, null, h(fresh.MetricsPage)));
-    await r.settle();
-    const titles = r.instances(CC.SectionBox).map((i) => i.props.title);
-    expect(titles).toContain('Prometheus Access Denied');
-    expect(titles).not.toContain('Prometheus Unreachable');
-    expect(r.html()).toContain('services/proxy');
-    r.unmount();
-  });
-});
+// Pod detail power history and Metrics without Prometheus RBAC: tests/js/shared/telemetry.shared.test.js (both React tiers).
 
 describe('pager state survives leaving and reopening a page (this tab)', () => {
   function memStorage() {
