@@ -137,9 +137,9 @@ export function renderSection(s) {
 /** Pager → <nav>: the range shown, the name filter and previous / next buttons. */
 export function renderPager(p) {
   return '<nav data-testid="pager" data-page="' + p.page + '" data-pages="' + p.pages + '" data-total="' + p.total + '">' +
-    '<input aria-label="Filter ' + esc(p.noun) + ' by name" value="' + esc(p.filter) + '">' +
+    '<input aria-label="Filter ' + esc(p.label || p.noun) + ' by name" value="' + esc(p.filter) + '">' +
     (p.sorts
-      ? '<select aria-label="Sort ' + esc(p.noun) + '">' + p.sorts.map(function (o) {
+      ? '<select aria-label="Sort ' + esc(p.label || p.noun) + '">' + p.sorts.map(function (o) {
         return '<option value="' + esc(o.value) + '"' + (o.value === p.sort ? ' selected' : '') + '>' + esc(o.label) + '</option>';
       }).join('') + '</select>'
       : '') +

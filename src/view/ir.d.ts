@@ -140,6 +140,8 @@ export interface PagerItem {
   key: 'pager';
   /** what is counted, e.g. "GPU nodes" */
   noun: string;
+  /** what the controls are named after ("Filter <label> by name", "Sort <label>"): stable across orders */
+  label: string;
   /** 0-based */
   page: number;
   pages: number;
@@ -182,7 +184,7 @@ export function page(title: string | null, refresh: RefreshButton | null, items:
 export function pager(
   p: { page: number; pages: number; from: number; to: number; total: number; matched: number; filter: string; perPage: number },
   noun: string,
-  sorting?: { sort: string; sorts: ReadonlyArray<{ value: string; label: string }> }
+  sorting?: { sort?: string; sorts?: ReadonlyArray<{ value: string; label: string }>; label?: string }
 ): PagerItem;
 /** "Showing 17–24 of 1000 GPU nodes · page 3 of 125" */
 export function pagerText(p: PagerItem): string;

@@ -64,7 +64,9 @@ export function loader(title) {
  */
 export function pager(p, noun, sorting) {
   const item = {
-    t: 'pager', key: 'pager', noun: noun, page: p.page, pages: p.pages, from: p.from, to: p.to,
+    // `label` names the controls and stays the same when the noun counts
+    // something narrower (a power-ranked page counts "GPU nodes reporting").
+    t: 'pager', key: 'pager', noun: noun, label: (sorting && sorting.label) || noun, page: p.page, pages: p.pages, from: p.from, to: p.to,
     total: p.total, matched: p.matched, filter: p.filter, perPage: p.perPage,
   };
   // Offered orders ({value, label}[]) and the current one, when the list can be ranked.

@@ -1078,7 +1078,7 @@ function nodesHeadItems(ctx, now, powerByNode, pg, sort) {
     return items;
   }
 
-  items.push(pager(pg, pg.ranked ? 'GPU nodes reporting' : 'GPU nodes', { sort: sort, sorts: RANKED_NODE_SORTS }));
+  items.push(pager(pg, pg.ranked ? 'GPU nodes reporting' : 'GPU nodes', { sort: sort, sorts: RANKED_NODE_SORTS, label: 'GPU nodes' }));
   const idx = ctx.index;
   if (pg.nodes.length > 0) {
     items.push(
@@ -1207,7 +1207,7 @@ function podsItems(ctx, now, assign, pg, sort) {
     const exact = assign && Object.keys(assign).length > 0;
     const cols = ['Name', 'Namespace', 'Node', 'Phase', 'GPU Resources', 'Restarts', 'Age'];
     if (exact) cols.splice(5, 0, 'Assigned GPUs', 'GPU Power');
-    items.push(pager(pg, pg.ranked ? 'GPU pods drawing power' : 'GPU pods', { sort: sort, sorts: RANKED_POD_SORTS }));
+    items.push(pager(pg, pg.ranked ? 'GPU pods drawing power' : 'GPU pods', { sort: sort, sorts: RANKED_POD_SORTS, label: 'GPU pods' }));
     items.push(
       section('All GPU Pods', [
         table(
@@ -1520,9 +1520,9 @@ export function metricsView(ctx, mstate, opts) {
       );
     }
 
-    items.push(rankedView ? pager(pg, 'GPU nodes reporting', { sort: 'power', sorts: RANKED_NODE_SORTS })
+    items.push(rankedView ? pager(pg, 'GPU nodes reporting', { sort: 'power', sorts: RANKED_NODE_SORTS, label: 'GPU nodes' })
       : k8s ? pager(pg, 'GPU nodes', { sort: nodeSortOf(pagerState, RANKED_NODE_SORTS), sorts: RANKED_NODE_SORTS })
-        : pager(pg, scoped ? 'GPU nodes' : 'GPU nodes reporting'));
+        : pager(pg, scoped ? 'GPU nodes' : 'GPU nodes reporting', { label: 'GPU nodes' }));
     const covered = {};
     if (scoped) for (let i = 0; i < m.scope.length; i++) covered[m.scope[i]] = true;
     let matched = 0;

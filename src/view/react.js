@@ -318,9 +318,9 @@ export function createRenderer(React, CC) {
     const next = p.page + 1 < p.pages;
     return h(
       'div',
-      { 'data-pager': p.noun, style: { display: 'flex', alignItems: 'center', gap: '8px', flexWrap: 'wrap', margin: '0 0 16px' } },
+      { 'data-pager': p.label || p.noun, style: { display: 'flex', alignItems: 'center', gap: '8px', flexWrap: 'wrap', margin: '0 0 16px' } },
       h('input', {
-        'aria-label': 'Filter ' + p.noun + ' by name',
+        'aria-label': 'Filter ' + (p.label || p.noun) + ' by name',
         placeholder: 'Filter by name',
         value: p.filter,
         style: { padding: '4px 6px', fontSize: '13px', minWidth: '180px' },
@@ -330,7 +330,7 @@ export function createRenderer(React, CC) {
         ? h(
           'select',
           {
-            'aria-label': 'Sort ' + p.noun,
+            'aria-label': 'Sort ' + (p.label || p.noun),
             value: p.sort,
             style: { padding: '4px 6px', fontSize: '13px' },
             onChange: function (e) { if (props.onSort) props.onSort(e.target.value); },

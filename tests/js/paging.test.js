@@ -191,6 +191,8 @@ describe('GPU Pods in power order: Prometheus ranks the pods by the power of the
     expect(rows.map((r) => r[0])).toEqual(byPower.slice(0, PODS_PER_PAGE));
     expect(findSection(vm, 'All GPU Pods').blocks[0].columns).toContain('GPU Power');
     expect(pagerText(pagerOf(vm))).toBe('Showing 1–25 of 30 GPU pods drawing power · page 1 of 2');
+    // the count narrows to the pods drawing power; the controls keep their names
+    expect([pagerOf(vm).noun, pagerOf(vm).label]).toEqual(['GPU pods drawing power', 'GPU pods']);
   });
 
   it('page 2 and a name filter are ranked by Prometheus too', async () => {
