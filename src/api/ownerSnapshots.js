@@ -1,0 +1,123 @@
+/**
+ * Pod → GPU attribution for the GPU Pods page: the exporter's power gauge of
+ * GPUs whose `pod` / `namespace` labels are set — one series per allocated
+ * GPU, of the pods on the page (or every owner on a small cluster, or a page
+ * Prometheus ranks by power). Nothing else of the GPU is fetched.
+ *
+ * Kubernetes does not say which device a pod holds (SURVEY §7.3); the
+ * reference shows requests only (src/components/PodsPage.tsx:49-88).
+ */
+
+import { SMALL_CLUSTER_PODS, STALE_FAILURES } from './series.js';
+import { ownersQuery, rankedOwnersQuery } from './promql.js';
+import { isRow, joinExporterResults, num, shareGpus, sizeFromRows } from './telemetry.js';
+import { UNREACHABLE, staleOrNull } from './promClient.js';
+
+/** Owner answers kept per request key (stale fallbacks, structural sharing). */
+const OWNER_KEYS = 16;
+
+/**
+ * @param {PromClient} client
+ * @param {{source: ('amd-exporter'|'node-exporter'|null)}} state
+ */
+export function createOwnerSnapshots(client, state) {
+  // request key → {last, failures}: a failed refresh of one page's owners
+  // serves THAT page's last answer, never another page's.
+  let byKey = new Map();
+  client.onInvalidate(function () { byKey = new Map(); });
+
+  function entry(key) {
+    let e = byKey.get(key);
+    if (e) byKey.delete(key);
+    else e = { last: null, failures: 0 };
+    byKey.set(key, e);
+    if (byKey.size > OWNER_KEYS) byKey.delete(byKey.keys().next().value);
+    return e;
+  }
+
+  /**
+   * @param {{pods?: string[], small?: boolean, rank?: {by: string, page: number, per: number, filter: string}}} [opts]
+   *   `pods`: "namespace/name" keys of the page; `small`: every owner when at
+   *   most SMALL_CLUSTER_PODS pods own a GPU, else the page's; `rank`: the
+   *   page of pods ranked by the power of the GPUs they hold.
+   */
+  function owners(opts) {
+    const rank = opts && opts.rank;
+    if (rank) {
+      const rk = 'owners|rank|' + rank.page + '|' + rank.per + '|' + rank.filter;
+      return client.shared(rk, function () { return rankedOwners(rank, rk); });
+    }
+    const pods = opts && Array.isArray(opts.pods) ? opts.pods.map(String) : null;
+    const small = !!(opts && opts.small);
+    if (small) {
+      const sk = 'owners|small|' + (pods || []).join(',');
+      return client.shared(sk, function () { return ownersOf(pods || [], true, sk); });
+    }
+    if (pods && pods.length === 0) {
+      return Promise.resolve({ source: state.source, gpus: [], xgmi: {}, links: {}, fetchedAt: client.fetchedAt(),
+        prometheusPath: client.cachedPath(), scope: 'owners' });
+    }
+    const k = 'owners|' + (pods ? pods.join(',') : '*');
+    return client.shared(k, function () { return ownersOf(pods, false, k); });
+  }
+
+  function answer(st, base, j, extra) {
+    st.failures = 0;
+    const prev = st.last;
+    st.last = Object.assign({
+      source: j.gpus.length ? 'amd-exporter' : state.source,
+      gpus: prev ? shareGpus(prev.gpus, j.gpus) : j.gpus,
+      xgmi: {},
+      links: {},
+      fetchedAt: client.fetchedAt(),
+      prometheusPath: base,
+      scope: 'owners',
+    }, extra);
+    return st.last;
+  }
+
+  function ownersOf(pods, small, key) {
+    const st = entry(key);
+    return client.withPrometheus(function (base) {
+      return client.combined(base, ownersQuery(pods, small)).then(function (res) {
+        if (!res.ok) return UNREACHABLE;
+        const owning = small ? sizeFromRows(res.rows.__agg, 'gpu_pods') : 0;
+        return answer(st, base, joinExporterResults(res.rows), {
+          small: small ? { count: owning, limit: SMALL_CLUSTER_PODS, exceeded: owning > SMALL_CLUSTER_PODS } : undefined,
+        });
+      });
+    }, function () { return staleOrNull(st, STALE_FAILURES, client.invalidate); });
+  }
+
+  /**
+   * GPU pods in power order (promql.js rankedOwnersQuery): the page's owners
+   * plus `rank` = {by, page, per, filter, count, order: "namespace/pod" keys
+   * highest first, watts per key}.
+   */
+  function rankedOwners(rank, key) {
+    const st = entry(key);
+    return client.withPrometheus(function (base) {
+      return client.combined(base, rankedOwnersQuery(rank)).then(function (res) {
+        if (!res.ok) return UNREACHABLE;
+        const rows = res.rows;
+        const ranked = [];
+        const watts = {};
+        for (let i = 0; i < rows.__agg.length; i++) {
+          const r = rows.__agg[i];
+          if (!isRow(r) || r.metric.agg !== 'rank' || typeof r.metric.pod !== 'string') continue;
+          const k = (typeof r.metric.namespace === 'string' ? r.metric.namespace : '') + '/' + r.metric.pod;
+          const w = num(r.value[1]);
+          ranked.push([k, w === null ? -Infinity : w]);
+          watts[k] = w;
+        }
+        ranked.sort(function (a, b) { return b[1] - a[1] || (a[0] < b[0] ? -1 : a[0] > b[0] ? 1 : 0); });
+        return answer(st, base, joinExporterResults(rows), {
+          rank: { by: rank.by, page: rank.page, per: rank.per, filter: rank.filter, count: sizeFromRows(rows.__agg, 'ranked'),
+            order: ranked.map(function (x) { return x[0]; }), watts: watts },
+        });
+      });
+    }, function () { return staleOrNull(st, STALE_FAILURES, client.invalidate); });
+  }
+
+  return { owners: owners };
+}

@@ -1,0 +1,119 @@
+/**
+ * Power / HBM time series (`query_range`) for the Metrics page and the
+ * detail pages' power history. The reference has instant queries only
+ * (src/api/metrics.ts:67-75); its mock-up's 30-minute chart was never built
+ * (SURVEY Q12).
+ *
+ *   * `series(range, step, scope, small)`: per-node power + HBM-used, one
+ *     request for both, `sum by (__name__, hostname)` server-side, scoped to
+ *     the page's nodes with the cluster line alongside. Incremental: samples
+ *     are step-aligned and Prometheus never rewrites a past step, so after the
+ *     first call only the steps newer than the cache are asked for — and none
+ *     at all until the next step boundary.
+ *   * `powerSeries(key, q, range, step)`: one pod's or node's total GPU power.
+ */
+
+import { SERIES, TOTAL_SERIES } from './series.js';
+import { scopedSeriesQuery, seriesQuery } from './promql.js';
+import { num } from './telemetry.js';
+import { UNREACHABLE } from './promClient.js';
+
+/**
+ * @param {PromClient} client
+ */
+export function createSeriesFetch(client) {
+  let cache = null; // { range, step, end, base, scope, data }
+  client.onInvalidate(function () { cache = null; });
+
+  /**
+   * @returns {Promise<{rangeSec: number, stepSec: number, power: Record<string, Array<[number, number]>>,
+   *   vram: Record<string, Array<[number, number]>>, scope?: string[], total?: any} | null>}
+   */
+  function series(rangeSec, stepSec, scope, small) {
+    const range = rangeSec || 1800;
+    const step = stepSec || 30;
+    const E = SERIES.exporter;
+    const parts = [['power', E.power, 1], ['vram', E.vramUsed, SERIES.exporterVramUnitBytes]];
+    const scoped = Array.isArray(scope);
+    const sk = scoped ? (small ? 'small:' : '') + scope.map(String).join(',') : null;
+    const q = scoped ? scopedSeriesQuery(scope.map(String), !!small) : seriesQuery();
+    function from(base) {
+      const end = Math.floor(client.now() / 1000 / step) * step;
+      const fresh = !cache || cache.range !== range || cache.step !== step ||
+        cache.base !== base || cache.scope !== sk || end - cache.end >= range;
+      const start = fresh ? end - range : cache.end + step;
+      if (!fresh && start > end) return Promise.resolve(cache.data);
+      return client.range(base, q, start, end, step, TOTAL_SERIES).then(function (got) {
+        if (got === UNREACHABLE) return UNREACHABLE;
+        const data = { rangeSec: range, stepSec: step };
+        if (scoped) {
+          data.scope = scope.map(String);
+          data.total = {};
+        }
+        const cutoff = end - range;
+        for (let i = 0; i < parts.length; i++) {
+          const key = parts[i][0];
+          const scale = parts[i][2];
+          const rows = got[parts[i][1]] || {};
+          const prev = fresh ? {} : cache.data[key] || {};
+          const merged = {};
+          const nodes = Object.keys(Object.assign({}, prev, rows));
+          for (let n = 0; n < nodes.length; n++) {
+            if (nodes[n] === TOTAL_SERIES) continue;
+            const add = (rows[nodes[n]] || []).map(function (v) { return [Number(v[0]), (num(v[1]) || 0) * scale]; });
+            const pts = (prev[nodes[n]] || []).concat(add).filter(function (p) { return p[0] >= cutoff; });
+            if (pts.length) merged[nodes[n]] = pts;
+          }
+          data[key] = merged;
+          if (scoped) {
+            // The cluster-wide line (peak / average over the whole cluster).
+            const add = (rows[TOTAL_SERIES] || []).map(function (v) { return [Number(v[0]), (num(v[1]) || 0) * scale]; });
+            const prevTotal = fresh ? [] : (cache.data.total && cache.data.total[key]) || [];
+            data.total[key] = prevTotal.concat(add).filter(function (p) { return p[0] >= cutoff; });
+          }
+        }
+        cache = { range: range, step: step, end: end, base: base, scope: sk, data: data };
+        return data;
+      });
+    }
+    // A failed range request keeps the last window of the same scope (retried next time).
+    return client.shared('series|' + range + '|' + step + '|' + sk, function () {
+      return client.withPrometheus(from, function () { return cache && cache.scope === sk ? cache.data : null; });
+    });
+  }
+
+  /**
+   * Total GPU power over the last `rangeSec` of what `q` selects (a pod's or
+   * a node's GPUs), step-aligned like series(): `{rangeSec, stepSec, power:
+   * [[t, W]]}`; `power` is empty when nothing matches. Null when Prometheus is
+   * unreachable.
+   */
+  function powerSeries(scope, q, rangeSec, stepSec) {
+    const range = rangeSec || 1800;
+    const step = stepSec || 30;
+    const key = 'power|' + scope + '|' + range + '|' + step;
+    return client.shared(key, function () {
+      return client.withPrometheus(function (base) {
+        const end = Math.floor(client.now() / 1000 / step) * step;
+        return client.range(base, q, end - range, end, step, TOTAL_SERIES).then(function (got) {
+          if (got === UNREACHABLE) return UNREACHABLE;
+          // Sum whatever rows came back per step (one row after `sum by (__name__)`).
+          const total = {};
+          const rows = got[SERIES.exporter.power] || {};
+          for (const k in rows) {
+            for (let i = 0; i < rows[k].length; i++) {
+              const t = Number(rows[k][i][0]);
+              const v = num(rows[k][i][1]);
+              if (v !== null) total[t] = (total[t] || 0) + v;
+            }
+          }
+          const power = Object.keys(total).map(Number).sort(function (a, b) { return a - b; })
+            .map(function (t) { return [t, total[t]]; });
+          return { rangeSec: range, stepSec: step, power: power };
+        });
+      }, function () { return null; });
+    });
+  }
+
+  return { series: series, powerSeries: powerSeries };
+}

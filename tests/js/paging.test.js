@@ -699,19 +699,68 @@ describe('small-cluster mode: guards and pages agree', () => {
   });
 });
 
-describe('scoped fetches on a cluster without GPU telemetry', () => {
-  it('ask cluster-wide once per discovery TTL, not on every refresh', async () => {
+describe('scoped fetches: the first answer decides the telemetry source (one wave)', () => {
+  const neOf = (nodes, chipsPerNode) => {
+    const ne = { node_uname_info: [], node_hwmon_power_input_watt: [] };
+    ne[SERIES.nodeExporter.chips] = [];
+    nodes.forEach((n, i) => {
+      const inst = '10.0.0.' + i + ':9100';
+      ne.node_uname_info.push({ metric: { __name__: 'node_uname_info', instance: inst, nodename: n }, value: [0, '1'] });
+      for (let c = 0; c < chipsPerNode; c++) {
+        const chip = '0000:' + String(5 + c).padStart(2, '0') + ':00_0';
+        ne[SERIES.nodeExporter.chips].push({ metric: { __name__: 'node_hwmon_chip_names', chip_name: 'amdgpu', instance: inst, chip: chip }, value: [0, '1'] });
+        ne.node_hwmon_power_input_watt.push({ metric: { __name__: 'node_hwmon_power_input_watt', instance: inst, chip: chip }, value: [0, '500'] });
+      }
+    });
+    return ne;
+  };
+
+  it('a cluster without GPU telemetry: one request per fetch, never a cluster-wide look; the view keeps the warning', async () => {
     const fake = prom({ data: {} });
-    let now = 1000;
-    const clock = { setTimeout: setTimeout, clearTimeout: clearTimeout, now: () => now };
-    const s = createMetricsSource({ request: fake, clock: clock });
-    await s.fetchGpuMetrics('gauges', { scope: [], summary: true });
-    const first = fake.mock.calls.length;
-    expect(first).toBe(2); // the scoped summary, then the cluster-wide look
-    await s.fetchGpuMetrics('gauges', { scope: [], summary: true });
-    expect(fake.mock.calls.length).toBe(first + 1); // scoped only
-    now += 6 * 60 * 1000; // past the discovery TTL
-    await s.fetchGpuMetrics('gauges', { scope: [], summary: true });
-    expect(fake.mock.calls.length).toBeGreaterThan(first + 2);
+    const s = createMetricsSource({ request: fake });
+    const m1 = await s.fetchGpuMetrics('gauges', { scope: [], summary: true, small: true });
+    expect(fake.mock.calls.length).toBe(1); // exporter rows + totals + source probe, one answer
+    expect(decoded(fake)[0]).toContain('"agg", "hwmon"');
+    expect(m1.totals.gpus).toBe(0);
+    const m2 = await s.fetchGpuMetrics('gauges', { scope: [], summary: true, small: true });
+    expect(fake.mock.calls.length).toBe(2);
+    expect(s.source()).toBe(null);
+    // The Metrics page says so on every refresh, not only the first (zero totals, not "unknown").
+    for (const m of [m1, m2]) {
+      const vm = metricsView(makeContext({ nodes: [] }), { metrics: m, series: null, fetchError: null, fetching: false });
+      expect(sectionTitles(vm)).toContain('No AMD GPU Metrics in Prometheus');
+    }
+  });
+
+  it('the GPU Nodes page of a cluster without GPU telemetry asks once per refresh too', async () => {
+    const fake = prom({ data: {} });
+    const s = createMetricsSource({ request: fake });
+    await s.fetchGpuMetrics('topology', { scope: names(3), small: true });
+    await s.fetchGpuMetrics('topology', { scope: names(3) });
+    expect(fake.mock.calls.length).toBe(2);
+  });
+
+  it('a node-exporter-only cluster of one page gets its hwmon telemetry in the first answer', async () => {
+    const fake = prom({ data: {}, ne: neOf(names(2), 8) });
+    const s = createMetricsSource({ request: fake });
+    const m = await s.fetchGpuMetrics('gauges', { scope: [], summary: true, small: true });
+    expect(fake.mock.calls.length).toBe(1);
+    expect(s.source()).toBe('node-exporter');
+    expect(m.totals.gpus).toBe(16);
+    expect(m.totals.powerWatts).toBe(16 * 500);
+    // later refreshes ask node-exporter directly: one cluster-wide request
+    await s.fetchGpuMetrics('gauges', { scope: names(2), summary: true, small: true });
+    expect(fake.mock.calls.length).toBe(2);
+    expect(decoded(fake)[1]).not.toContain('gpu_power_usage');
+  });
+
+  it('a larger node-exporter cluster (more amdgpu chips than one page) reads cluster-wide in the second wave', async () => {
+    const fake = prom({ data: {}, ne: neOf(names(9), 8) });
+    const s = createMetricsSource({ request: fake });
+    const m = await s.fetchGpuMetrics('gauges', { scope: names(8), summary: true });
+    expect(fake.mock.calls.length).toBe(2);
+    expect(s.source()).toBe('node-exporter');
+    expect(m.totals.gpus).toBe(72);
+    expect(m.gpus.length).toBe(64);
   });
 });

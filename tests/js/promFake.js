@@ -101,14 +101,20 @@ function term(q, rows) {
   }
   const own = /^max by \([^)]*\) \(\{__name__="([a-z_]+)", pod!=""\}\)$/.exec(q);
   if (own) return rows.filter((r) => r.metric.__name__ === own[1] && r.metric.pod);
-  const agg = /^label_replace\((sum|count) by \(__name__\) \(\{__name__=~"(.*?)"\}\), "agg", "(\w+)", "", ""\)$/.exec(q);
+  // summaryQuery: sum / count by __name__ over one series per GPU (max by __name__, hostname, gpu_id).
+  const agg = /^label_replace\((sum|count) by \(__name__\) \((?:max by \(__name__, hostname, gpu_id\) \()?\{__name__=~"(.*?)"\}\)?\), "agg", "(\w+)", "", ""\)$/.exec(q);
   if (agg) {
     const re = new RegExp('^(?:' + agg[2] + ')$');
-    const by = {};
+    const perGpu = {};
     rows.filter((r) => re.test(r.metric.__name__ || '')).forEach((r) => {
-      const k = r.metric.__name__;
+      const g = r.metric.__name__ + '\u0000' + r.metric.hostname + '\u0000' + r.metric.gpu_id;
       const v = parseFloat(r.value[1]);
-      by[k] = (by[k] || 0) + (agg[1] === 'sum' ? v : 1);
+      perGpu[g] = g in perGpu ? Math.max(perGpu[g], v) : v;
+    });
+    const by = {};
+    Object.keys(perGpu).forEach((g) => {
+      const k = g.split('\u0000')[0];
+      by[k] = (by[k] || 0) + (agg[1] === 'sum' ? perGpu[g] : 1);
     });
     return Object.keys(by).map((k) => vec({ __name__: k, agg: agg[3] }, by[k]));
   }
@@ -141,7 +147,26 @@ function term(q, rows) {
 function powerSums(expr, rows) {
   const unesc = (v) => new RegExp('^(?:' + v.replace(/\\\\/g, '\\') + ')$');
   const m = /^sum by \(hostname\) \(\{__name__="([a-z_]+)"(?:, hostname=~"(.*)")?\}\)$/.exec(expr);
-  const p = m ? null : /^sum by \(namespace, pod\) \(\{__name__="([a-z_]+)", pod!=""(?:, pod=~"(.*)")?\}\)$/.exec(expr);
+  // promql.js podFilterMatchers: pod, namespace or node substring (`or` of three selectors), or "ns/name".
+  const alt = m ? null : /^sum by \(namespace, pod\) \(\{__name__="([a-z_]+)", pod!="", pod=~"(.*?)"\} or \{__name__="[a-z_]+", pod!="", namespace=~"(.*?)"\} or \{__name__="[a-z_]+", pod!="", hostname=~"(.*?)"\}\)$/.exec(expr);
+  const p = m || alt ? null : /^sum by \(namespace, pod\) \(\{__name__="([a-z_]+)", pod!=""(?:, pod=~"([^"]*)")?\}\)$/.exec(expr);
+  const nsName = m || p || alt ? null : /^sum by \(namespace, pod\) \(\{__name__="([a-z_]+)", pod!="", namespace=~"(.*?)", pod=~"(.*?)"\}\)$/.exec(expr);
+  if (alt || nsName) {
+    const un = (v) => new RegExp('^(?:' + v.replace(/\\\\/g, '\\') + ')$');
+    const keep = alt
+      ? (r) => un(alt[2]).test(r.metric.pod || '') || un(alt[3]).test(r.metric.namespace || '') || un(alt[4]).test(r.metric.hostname || '')
+      : (r) => un(nsName[2]).test(r.metric.namespace || '') && un(nsName[3]).test(r.metric.pod || '');
+    const name = (alt || nsName)[1];
+    const by = {};
+    const labels = {};
+    rows.forEach((r) => {
+      if (r.metric.__name__ !== name || !r.metric.pod || !keep(r)) return;
+      const k = r.metric.namespace + '/' + r.metric.pod;
+      by[k] = (by[k] || 0) + parseFloat(r.value[1]);
+      labels[k] = { namespace: r.metric.namespace, pod: r.metric.pod };
+    });
+    return Object.keys(by).map((k) => [k, by[k], labels[k]]);
+  }
   const x = m || p;
   if (!x) return null;
   const re = x[2] !== undefined ? unesc(x[2]) : null;
@@ -170,6 +195,14 @@ function rankOf(expr, rows) {
 
 /** metrics.js gpuNodeCount / gpuPodCount over `rows` (null for another shape). */
 function countOf(expr, rows) {
+  // promql.js hwmonGpuCount: node-exporter's amdgpu chips.
+  if (/^count\(count by \(instance, chip\) \(\{__name__="node_hwmon_chip_names", chip_name="amdgpu"\}\)\)$/.test(expr)) {
+    const chips = {};
+    rows.forEach((r) => {
+      if (r.metric.__name__ === 'node_hwmon_chip_names' && r.metric.chip_name === 'amdgpu') chips[r.metric.instance + '/' + r.metric.chip] = true;
+    });
+    return Object.keys(chips).length;
+  }
   const m = /^count\(count by \((hostname|namespace, pod)\) \(\{__name__="([a-z_]+)"(, pod!="")?\}\)\)$/.exec(expr);
   if (!m) return null;
   const seen = {};

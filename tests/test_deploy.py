@@ -9,7 +9,7 @@ import yaml
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DEPLOY = os.path.join(ROOT, "deploy")
 JS = open(os.path.join(ROOT, "src", "api", "amdgpu.js")).read()
-METRICS_JS = open(os.path.join(ROOT, "src", "api", "metrics.js")).read()
+METRICS_JS = open(os.path.join(ROOT, "src", "api", "series.js")).read()
 
 
 def docs(path):

@@ -357,3 +357,69 @@ def test_the_pod_power_ranked_page():
     assert ranks == {"infer-c": 200.0, "train-d": 100.0} and owners == {("web", "infer-c"), ("ml", "train-d")}
     owners, ranks, count = ranked(0, 2, "TRAIN-")
     assert ranks == {"train-a": 1200.0, "train-b": 1000.0} and count == 3
+    # The table's filter also matches the namespace and the node (the page filters "namespace/name node").
+    owners, ranks, count = ranked(0, 10, "web")
+    assert ranks == {"infer-c": 200.0} and count == 1
+    owners, ranks, count = ranked(0, 10, "n1")
+    assert set(ranks) == {"infer-c", "train-d"} and count == 2
+    owners, ranks, count = ranked(0, 10, "ml/train-")
+    assert set(ranks) == {"train-a", "train-b", "train-d"} and count == 3
+
+
+def _js(expr):
+    import subprocess
+
+    from headlamp_intel_gpu_plugin_amd.utils.nodebridge import ROOT, node_binary
+
+    js = "import('./src/api/metrics.js').then(m => process.stdout.write(JSON.stringify(%s)))" % expr
+    r = subprocess.run([node_binary(), "-e", js], cwd=ROOT, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    return json.loads(r.stdout)
+
+
+def test_summary_totals_fold_a_gpu_scraped_twice():
+    """summaryQuery folds duplicate scrapes of one GPU (two jobs / instances) before summing and counting."""
+    q = _js("m.summaryQuery()")
+    d = TSDB()
+    for job in ("servicemonitor", "annotations"):
+        for g in range(8):
+            lab = {"hostname": "a", "gpu_id": str(g), "job": job, "instance": job + ":5000"}
+            d.add(Series({"__name__": "gpu_power_usage", **lab}, fn=lambda t: 500.0))
+            d.add(Series({"__name__": "gpu_total_vram", **lab}, fn=lambda t: 294896.0))
+    got = {(r["metric"]["agg"], r["metric"]["__name__"]): float(r["value"][1]) for r in _vec(query(d, q, 100.0))}
+    assert got[("count", "gpu_power_usage")] == 8 and got[("sum", "gpu_power_usage")] == 8 * 500.0
+    assert got[("sum", "gpu_total_vram")] == 8 * 294896.0 and got[("nodes", "gpu_power_usage")] == 1
+
+
+def test_source_probe_decides_the_exporter_in_one_answer():
+    """sourceProbe: exporter hostnames, node-exporter's amdgpu chips and, up to SMALL_HWMON_GPUS chips, node-exporter's
+    GPU series — so one answer tells exporter / node-exporter / no GPU telemetry apart."""
+    q, limit = _js("[m.sourceProbe(true), m.SMALL_HWMON_GPUS]")
+
+    def hwmon(nodes, chips):
+        d = TSDB()
+        for i, node in enumerate(nodes):
+            inst = "10.0.0.%d:9100" % i
+            d.add(Series({"__name__": "node_uname_info", "instance": inst, "nodename": node}, fn=lambda t: 1.0))
+            d.add(Series({"__name__": "node_hwmon_chip_names", "instance": inst, "chip": "platform_coretemp_0",
+                          "chip_name": "coretemp"}, fn=lambda t: 1.0))
+            for c in range(chips):
+                chip = "0000_%02x_00_0" % (5 + c)
+                d.add(Series({"__name__": "node_hwmon_chip_names", "instance": inst, "chip": chip, "chip_name": "amdgpu"},
+                             fn=lambda t: 1.0))
+                d.add(Series({"__name__": "node_hwmon_power_input_watt", "instance": inst, "chip": chip,
+                              "sensor": "power1"}, fn=lambda t: 500.0))
+        return d
+
+    def agg(rows, tag):
+        vals = [float(r["value"][1]) for r in rows if r["metric"].get("agg") == tag]
+        return vals[0] if vals else 0
+
+    small = _vec(query(hwmon(["a", "b"], 8), q, 100.0))
+    assert agg(small, "hwmon") == 16 and agg(small, "gpu_nodes") == 0
+    data = [r for r in small if "agg" not in r["metric"]]
+    assert {r["metric"]["__name__"] for r in data} >= {"node_hwmon_chip_names", "node_hwmon_power_input_watt", "node_uname_info"}
+    assert all(set(r["metric"]) <= {"__name__", "instance", "node", "nodename", "chip", "chip_name", "card"} for r in data)
+    big = _vec(query(hwmon([str(i) for i in range(limit // 8 + 1)], 8), q, 100.0))
+    assert agg(big, "hwmon") == limit + 8 and [r for r in big if "agg" not in r["metric"]] == []
+    assert _vec(query(TSDB(), q, 100.0)) == []  # no exporter, no amdgpu hwmon: nothing at all
