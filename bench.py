@@ -287,17 +287,25 @@ def main(argv=None) -> int:
             "render_p50_ms": (round(summarize(result["amd"]["renderMs"])["p50"], 3)
                               if result["amd"].get("renderMs") else None),
             # Each page opened on an empty cache, as each is wired (reference: a
-            # fresh provider per route; Metrics then waits for it to load).
-            # amd = every wave done (GPU Nodes / GPU Pods / Metrics ask for their
-            # page's telemetry once the node / pod list is in: a second wave);
+            # fresh provider per route, a full-page Loader until every list and
+            # the serial chain are in; Metrics then waits for it to load).
+            # amd = the page complete: everything IT draws is in (Metrics: the
+            # node list + its telemetry, never the pod list; GPU Nodes / GPU
+            # Pods / Metrics ask for their page's telemetry once the node / pod
+            # list is in on a cluster larger than one page: a second wave);
+            # amd_first_content = the first render with content (progressive
+            # pages: a page waits only for the lists it draws);
             # amd_content = the lists + DeviceConfig committed, i.e. everything
-            # the reference's page shows rendered.
+            # the reference's page shows.
             "cold_open_per_page_p50_ms": {
                 pg: {"amd": round(summarize(result["amd_cold_pages"][pg]["latencies"])["p50"], 3),
+                     "amd_first_content": round(summarize(result["amd_cold_pages"][pg]["firstMs"])["p50"], 3),
                      "amd_content": round(summarize(result["amd_cold_pages"][pg]["contentMs"])["p50"], 3),
                      "reference": round(summarize(result["ref_cold_pages"][pg]["latencies"])["p50"], 3),
                      "requests": {"amd": result["amd_cold_pages"][pg]["requests"],
-                                  "reference": result["ref_cold_pages"][pg]["requests"]}}
+                                  "reference": result["ref_cold_pages"][pg]["requests"]},
+                     # the amd open's requests by kind (nodes, pods, crd, query, query_range, probe)
+                     "amd_requests_by_kind": {k: v["n"] for k, v in (result["amd_cold_pages"][pg].get("trace") or {}).items()}}
                 for pg in pages},
             # Per page, untimed: the page's view-model mounted in the harness
             # React through the shipped renderer (src/view/react.js), then

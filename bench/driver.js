@@ -32,7 +32,7 @@ import {
   overviewView, devicePluginsView, nodesView, podsView, metricsView,
   nodeDetailView, podDetailView, nodeColumns, nodePage, ownersScope, podPage, telemetryScope,
 } from '../src/view/pages.js';
-import { countRows } from '../src/view/ir.js';
+import { countRows, sections } from '../src/view/ir.js';
 import { renderPage, renderSection } from '../src/view/html.js';
 import { createReferenceSchedule } from './referenceSchedule.js';
 // The harness React (the Node-12 stand-in the spec suite renders the plugin
@@ -216,6 +216,18 @@ function pageVm(page, ctx, mstate, pageMetrics) {
   return metricsView(ctx, mstate, { pager: PAGER });
 }
 
+/**
+ * True when a page's view-model shows content rather than a loader: the
+ * full-page loader is gone (title set); on Metrics, whose header and static
+ * availability box render at once, a section of telemetry (or one saying
+ * there is none / Prometheus is unreachable) is there too.
+ */
+function hasContent(page, vm) {
+  if (!vm || vm.title === null) return false;
+  if (page !== 'metrics') return true;
+  return sections(vm).some(function (s) { return s.title !== 'Metric Availability'; });
+}
+
 /** Build and render ONE page; returns its row count. */
 function renderOne(page, ctx, mstate, pageMetrics) {
   const vm = pageVm(page, ctx, mstate, pageMetrics);
@@ -386,9 +398,10 @@ function amdSchedule(request, clock) {
    * of its first render and again only if the lists change that key (a
    * larger cluster's first page), as useMetricsFetch does.
    */
-  function pageOpen(page) {
+  function pageOpen(page, onData) {
     const keyOf = page === 'pods' ? ownersKey : function () { return scoped(false).key; };
-    const fetch = page === 'pods' ? fetchPodsPage : page === 'nodes' ? fetchNodesPage : fetchMetricsPage;
+    const fetch0 = page === 'pods' ? fetchPodsPage : page === 'nodes' ? fetchNodesPage : fetchMetricsPage;
+    const fetch = onData ? function () { return fetch0().then(onData); } : fetch0;
     const k0 = keyOf();
     const first = k0 === null ? Promise.resolve() : fetch();
     const second = listed(page === 'pods' ? 'podsState' : 'nodesState').then(function () {
@@ -411,6 +424,9 @@ function amdSchedule(request, clock) {
         }
       });
     });
+  }
+  function pageMetricsOf(page) {
+    return page in pageMetrics && pageMetrics[page] ? pageMetrics[page] : mstate.metrics;
   }
   function fetchPodsPage() {
     const o = ownersScope(store.getSnapshot(), PAGER);
@@ -459,20 +475,44 @@ function amdSchedule(request, clock) {
      * telemetry in one wave — all of it on a cluster of one page; a larger
      * cluster's GPU Nodes / Metrics (GPU Pods) ask for their first page of
      * nodes (pods) once the node (pod) list is there (a second wave).
+     *
+     * `marks` (all optional) are called as the page fills in:
+     *   first     the page's view-model first shows content (pages.js decides:
+     *             its full-page loader gone; on Metrics, telemetry or a state
+     *             saying there is none) — built and rendered on every store
+     *             commit and telemetry answer, as the mounted page re-renders;
+     *   content   the lists + DeviceConfig committed (the reference's content);
+     *   complete  everything THIS page draws is in (Metrics: the node list and
+     *             its telemetry, not the pod list; Device Plugins: the
+     *             DeviceConfigs and the pod list; the others: both lists, the
+     *             DeviceConfigs where shown, their telemetry).
+     * Resolves when every request has finished (the next open starts drained).
      */
-    coldOpenPage: function (page, onContent) {
-      // The provider's data (lists + DeviceConfig): the page renders
-      // everything the reference's page shows once it is in.
-      // (Not on Metrics: there the content IS the telemetry.)
-      const content = Promise.all([store.loadLists(), store.refresh()]).then(function () {
-        if (onContent && page !== 'metrics') onContent();
-      });
+    coldOpenPage: function (page, marks) {
+      const mk = marks || {};
+      let shown = !mk.first;
+      function check() {
+        if (shown) return;
+        const vm = pageVm(page, store.getSnapshot(), page === 'metrics' ? metricsPage : mstate, pageMetricsOf(page));
+        if (!hasContent(page, vm)) return;
+        shown = true;
+        renderPage(vm);
+        mk.first();
+      }
+      const off = store.subscribe(check);
+      const lists = store.loadLists();
+      const crd = store.refresh();
       // The page's metrics hook runs from the first render (pages.js
       // telemetryScope) and once more if the node list changes its key.
-      if (page === 'nodes' || page === 'metrics' || page === 'pods') return Promise.all([content, pageOpen(page)]);
-      return content;
+      const telemetry = page === 'nodes' || page === 'metrics' || page === 'pods' ? pageOpen(page, check) : Promise.resolve();
+      const content = Promise.all([lists, crd]).then(function () { if (mk.content) mk.content(); });
+      const needs = page === 'metrics' ? [listed('nodesState'), telemetry]
+        : page === 'devicePlugins' ? [crd, listed('podsState')]
+          : page === 'overview' ? [lists, crd] : [lists, telemetry];
+      const complete = Promise.all(needs).then(function () { if (mk.complete) mk.complete(); });
+      return Promise.all([lists, crd, telemetry, content, complete]).then(function () { off(); });
     },
-    pageMetrics: function (page) { return page in pageMetrics && pageMetrics[page] ? pageMetrics[page] : mstate.metrics; },
+    pageMetrics: pageMetricsOf,
     /** The Metrics page's own state (its hook), for rendering that page. */
     pageMstate: function () { return metricsPage; },
     /** Route switch: render from the shared store now, revalidate in the background. */
@@ -656,27 +696,41 @@ async function serve(a) {
           let req = 0;
           let trace = null;
           const content = [];
+          const first = [];
           for (let i = 0; i < n; i++) {
             const s = (name === 'reference' ? referenceSchedule : amdSchedule)(pool);
             const before = counter.n;
             const p0 = performance.now();
             const t0 = process.hrtime();
+            let tf = null;
             let tc = null;
-            await s.coldOpenPage(page, function () { tc = ms(process.hrtime(t0)); });
-            const t1 = process.hrtime();
-            renderOne(page, s.ctx(), page === 'metrics' ? s.pageMstate() : s.mstate(), s.pageMetrics(page));
-            renderMs.push(ms(process.hrtime(t1)));
-            lat.push(ms(process.hrtime(t0)));
-            // Time to the reference-equivalent content (lists + DeviceConfig);
-            // the reference's schedule has no later wave: its whole open.
-            content.push(tc === null ? lat[lat.length - 1] : tc);
+            let done = null;
+            const render = function () {
+              const t1 = process.hrtime();
+              renderOne(page, s.ctx(), page === 'metrics' ? s.pageMstate() : s.mstate(), s.pageMetrics(page));
+              renderMs.push(ms(process.hrtime(t1)));
+              done = ms(process.hrtime(t0));
+            };
+            await s.coldOpenPage(page, {
+              first: function () { tf = ms(process.hrtime(t0)); },
+              content: function () { tc = ms(process.hrtime(t0)); },
+              complete: render,
+            });
+            // The reference's schedule has no marks: one full-page loader
+            // until its whole open is in, then the page.
+            if (done === null) render();
+            lat.push(done);
+            // Time to the reference-equivalent content (lists + DeviceConfig),
+            // and to the first render with content (progressive pages).
+            content.push(tc === null ? done : tc);
+            first.push(tf === null ? done : tf);
             // observer entries are delivered asynchronously
             await new Promise(function (r) { setImmediate(r); });
             gcMs.push(gcBetween(p0, performance.now()));
             req = counter.n - before;
             if (s.spans) trace = traceSummary(s.spans);
           }
-          out.pages[page] = { latencies: lat, contentMs: content, renderMs: renderMs, gcMs: gcMs, requests: req, trace: trace };
+          out.pages[page] = { latencies: lat, contentMs: content, firstMs: first, renderMs: renderMs, gcMs: gcMs, requests: req, trace: trace };
         }
       } else if (c.cmd === 'steps') {
         const L = get(name);

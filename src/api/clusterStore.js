@@ -132,7 +132,13 @@ export function withTimeout(promise, ms, clock) {
  * @property {boolean} crdAvailable
  * @property {boolean} crdForbidden  the DeviceConfig list was refused (401 / 403) rather than absent (404)
  * @property {boolean} loading      true until the node and pod lists have settled (arrived or
- *                                  failed) and the first CRD/pod fetch is in
+ *                                  failed) and the first CRD/pod fetch is in (the reference's
+ *                                  rule, IntelGpuDataContext.tsx:214)
+ * @property {boolean} nodesLoading the node list has not settled yet
+ * @property {boolean} podsLoading  the pod list has not settled yet
+ * @property {boolean} crdLoading   the first DeviceConfig / operator-pod fetch is not in yet
+ *                                  (pages render what they can as each of the three settles:
+ *                                  a page waits only for the lists it draws)
  * @property {'unknown'|'pending'|'ready'|'error'} nodesState
  * @property {'unknown'|'pending'|'ready'|'error'} podsState
  * @property {boolean} refreshing   a refresh is in flight (data above is still valid)
@@ -273,6 +279,9 @@ export function createClusterStore(opts) {
       crdAvailable: s.crdAvailable,
       crdForbidden: s.crdForbidden,
       loading: !s.asyncLoaded || !settled(s.nodesState) || !settled(s.podsState),
+      nodesLoading: !settled(s.nodesState),
+      podsLoading: !settled(s.podsState),
+      crdLoading: !s.asyncLoaded,
       nodesState: s.nodesState,
       podsState: s.podsState,
       refreshing: s.refreshing,
@@ -520,14 +529,21 @@ export function resetSharedStores() {
   for (const k in shared) delete shared[k];
 }
 
-/** Path of one node's pods (a field selector: the apiserver filters, O(pods on the node)). */
+/** The field selector of one node's pods (the apiserver filters: O(pods on the node)). */
+export function nodePodsSelector(nodeName) {
+  return 'spec.nodeName=' + nodeName;
+}
+
+/** Path of one node's pods: the list request of a field-selected list + watch. */
 export function nodePodsPath(nodeName) {
-  return '/api/v1/pods?fieldSelector=' + encodeURIComponent('spec.nodeName=' + nodeName);
+  return '/api/v1/pods?fieldSelector=' + encodeURIComponent(nodePodsSelector(nodeName));
 }
 
 /**
- * The pods of ONE node, for a Node detail page opened on a cold store: one
- * field-selected list instead of the cluster-wide node + pod lists and the
+ * The pods of ONE node by one field-selected list: the request a cold Node
+ * detail page's scoped list + watch starts with (providerCore.js
+ * useNodePods), for clients without Headlamp's hooks (the benchmark, the
+ * terminal client) — instead of the cluster-wide node + pod lists and the
  * CRD / operator-pod requests the reference's provider mounts there
  * (reference src/index.tsx:152-160, IntelGpuDataContext.tsx:98-165).
  * Resolves to the node's pods; rejects with the request's error.

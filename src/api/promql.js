@@ -131,7 +131,8 @@ export function smallClusterQuery(withStatic, view, scope) {
  *     is hostname-scoped and matched nothing);
  *   * `agg="hwmon"`: node-exporter's amdgpu chips;
  *   * node-exporter's GPU series themselves while there are at most
- *     SMALL_HWMON_GPUS chips (a size guard, as smallClusterQuery).
+ *     SMALL_HWMON_GPUS chips (a size guard, as smallClusterQuery) and no
+ *     exporter reports.
  * A cluster without GPU telemetry (no exporter, no amdgpu hwmon) is then told
  * apart in the first wave; the reference probed and queried serially
  * (src/api/metrics.ts:77-116), and round 3 paid a second, cluster-wide
@@ -139,8 +140,11 @@ export function smallClusterQuery(withStatic, view, scope) {
  */
 export function sourceProbe(withGpuNodes) {
   const hw = hwmonGpuCount();
+  // node-exporter's series only where no exporter reports (`unless on()`):
+  // a cluster running both sends the exporter's alone.
   return (withGpuNodes ? sizeRow(gpuNodeCount(), 'gpu_nodes') + ' or ' : '') +
-    sizeRow(hw, 'hwmon') + ' or ' + sizeGuard(nodeExporterProjected(), true, hw, SMALL_HWMON_GPUS);
+    sizeRow(hw, 'hwmon') + ' or ' + sizeGuard(nodeExporterProjected(), true, hw, SMALL_HWMON_GPUS) +
+    ' unless on() (' + gpuNodeCount() + ')';
 }
 
 /** Node names are lowercase (RFC 1123): a name filter becomes a lowercase substring regex. */

@@ -39,7 +39,7 @@ export interface ClusterStore {
 export interface MetricsSource {
   /**
    * `scope`: node names of a paged view (hostname=~); `summary`: also the cluster totals (GpuMetrics.totals);
-   * `small`: every GPU when the cluster has at most SMALL_CLUSTER_GPUS, else `scope`'s (one request)
+   * `small`: every GPU when the cluster has at most SMALL_CLUSTER_NODES GPU nodes, else `scope`'s (one request)
    */
   fetchGpuMetrics(
     view?: 'all' | 'gauges' | 'topology',
@@ -77,10 +77,9 @@ export interface ProviderCore {
   ): GpuMetricsState;
   usePodGpuSeries(namespace: string | null, pod: string | null, enabled?: boolean): GpuMetricsState;
   useNodeGpuSeries(nodeName: string | null, enabled?: boolean): GpuMetricsState;
-  /** One node's pods for a Node detail section on a cold store (one field-selected request) */
+  /** One node's pods for a Node detail section on a cold store: the host's list + watch scoped by `spec.nodeName` */
   useNodePods(
-    nodeName: string | null,
-    enabled?: boolean
+    nodeName: string
   ): { loading: boolean; gpuPods: unknown[]; podsState: 'pending' | 'ready' | 'error'; error: string | null };
   /** The shared store already holds the node and pod lists (a plugin page fed it) */
   storeWarm(): boolean;

@@ -24,8 +24,8 @@
  *     (reference quirk Q7: every route mounted a cold provider).
  */
 
-import { createClusterStore, fetchNodePods, getSharedStore, storeIsWarm } from './clusterStore.js';
-import { filterGpuRequestingPods } from './amdgpu.js';
+import { createClusterStore, getSharedStore, nodePodsSelector, storeIsWarm } from './clusterStore.js';
+import { filterGpuRequestingPods, get, unwrapAll } from './amdgpu.js';
 import { createMetricsSource } from './metrics.js';
 import { clusterKey as defaultClusterKey } from './cluster.js';
 import { POLL_MISS, createPoller, loadSettings as defaultLoadSettings, prometheusCandidates, seriesStepSec } from './settings.js';
@@ -363,52 +363,40 @@ export function createProviderCore(React, lib, deps) {
   }
 
   /**
-   * The pods of one node for a Node detail section on a cold store: ONE
-   * field-selected request (clusterStore.js fetchNodePods), fetched in the
-   * same wave as the node's telemetry and history — O(pods on the node)
-   * instead of the reference's full provider on every Node detail page
-   * (src/index.tsx:152-160: both cluster-wide lists + 4 serial requests).
+   * The pods of one node for a Node detail section on a cold store: the
+   * host's list + watch hook SCOPED to the node (`fieldSelector
+   * spec.nodeName=<node>`, all namespaces), so the section is live like the
+   * reference's — a pod scheduled onto the node appears without a reload
+   * (reference src/index.tsx:152-160: a full provider with the cluster-wide
+   * Pod list + watch, IntelGpuDataContext.tsx:98-99) — at O(pods on the node)
+   * instead of O(pods in the cluster). The list request goes out in the same
+   * wave as the node's telemetry and power history. The pods are filtered by
+   * node here too, so a host that ignores the field selector is still correct
+   * (only slower). A list that stops answering after it delivered keeps the
+   * pods shown; only a first failure says the pods are unreadable.
    * Returns the slice of the context nodeDetailView reads.
    */
-  function useNodePods(nodeName, enabled) {
-    const active = (enabled === undefined ? true : enabled) && !!nodeName;
-    const refreshIntervalSec = loadSettings().refreshIntervalSec;
-    const st = useState({ node: null, pods: null, error: null });
-    const state = st[0];
-    const setState = st[1];
-    const sq = useState(0);
-    const seq = sq[0];
-    const setSeq = sq[1];
+  function useNodePods(nodeName) {
+    const res = useListOf(lib.K8s.ResourceClasses.Pod, { namespace: '', fieldSelector: nodePodsSelector(nodeName) });
+    const items = res[0];
+    const err = res[1];
+    const listed = useMemo(function () {
+      if (!items) return null;
+      return unwrapAll(items).filter(function (p) { return get(p, ['spec', 'nodeName'], null) === nodeName; });
+    }, [items, nodeName]);
+    // The last list delivered, for a watch that re-lists (or fails) after it
+    // delivered: what is shown stays instead of flapping to loading / error.
+    const last = React.useRef(null);
     useEffect(function () {
-      if (!active) return undefined;
-      let cancelled = false;
-      fetchNodePods(request, nodeName, loadSettings().requestTimeoutMs).then(
-        function (items) { if (!cancelled) setState({ node: nodeName, pods: items, error: null }); },
-        function (e) {
-          if (cancelled) return;
-          // A failed re-fetch keeps the pods already shown; only a first failure says so.
-          setState(function (s) { return s.node === nodeName && s.pods && !s.error ? s : { node: nodeName, pods: [], error: errorText(e) }; });
-        }
-      );
-      return function () { cancelled = true; };
-    }, [nodeName, active, seq]);
-    // No watch on this path: with auto-refresh on (settings) the list is re-read
-    // each period, like the pages' imperative track.
-    useEffect(function () {
-      if (!active) return undefined;
-      const poller = createPoller(refreshIntervalSec);
-      poller.start(function () { setSeq(function (x) { return x + 1; }); });
-      return function () { poller.stop(); };
-    }, [nodeName, active, refreshIntervalSec]);
+      if (listed) last.current = { node: nodeName, pods: listed };
+    }, [listed, nodeName]);
+    const kept = !listed && last.current && last.current.node === nodeName ? last.current.pods : null;
+    const pods = listed || kept;
     return useMemo(function () {
-      const mine = state.node === nodeName;
-      return {
-        loading: active && (!mine || state.pods === null),
-        gpuPods: mine && state.pods ? filterGpuRequestingPods(state.pods) : [],
-        podsState: mine && state.error ? 'error' : mine && state.pods ? 'ready' : 'pending',
-        error: mine ? state.error : null,
-      };
-    }, [state, nodeName, active]);
+      if (pods) return { loading: false, gpuPods: filterGpuRequestingPods(pods), podsState: 'ready', error: null };
+      if (err) return { loading: false, gpuPods: [], podsState: 'error', error: errorText(err) };
+      return { loading: true, gpuPods: [], podsState: 'pending', error: null };
+    }, [pods, err]);
   }
 
   /** One node's GPU power history for the native Node detail page (metrics.js fetchNodeSeries). */

@@ -225,6 +225,12 @@ export interface ClusterSnapshot {
   crdForbidden: boolean;
   /** true until the node and pod lists settled (arrived or failed) and the first CRD fetch is in */
   loading: boolean;
+  /** the node list has not settled yet (pages that draw nodes show their loader) */
+  nodesLoading: boolean;
+  /** the pod list has not settled yet (pod-derived sections show a loader; the rest renders) */
+  podsLoading: boolean;
+  /** the first DeviceConfig / operator-pod fetch is not in yet */
+  crdLoading: boolean;
   nodesState: ListState;
   podsState: ListState;
   /** a refresh is in flight; the data above is still valid */

@@ -176,25 +176,26 @@ export function createPlugin(env) {
 
   /**
    * The Node detail section on a cold store (no plugin page visited yet): the
-   * node's own pods by one field-selected request, with its telemetry and
-   * power history in the same wave — no cluster-wide watch is mounted.
+   * node's own pods by a list + watch scoped to the node (live, like the
+   * reference's section), with its telemetry and power history in the same
+   * wave — no cluster-wide watch is mounted. Mounted for AMD GPU nodes only.
    */
   function NodeDetailCold(props) {
-    const raw = unwrapKubeObject(props.resource);
-    const gpuNode = isAmdGpuNode(raw);
-    const name = gpuNode ? raw.metadata.name : null;
-    const ctx = core.useNodePods(name, gpuNode);
-    const m = core.useNodeGpuMetrics(name, gpuNode);
-    const ps = core.useNodeGpuSeries(name, gpuNode);
+    const name = unwrapKubeObject(props.resource).metadata.name;
+    const ctx = core.useNodePods(name);
+    const m = core.useNodeGpuMetrics(name, true);
+    const ps = core.useNodeGpuSeries(name, true);
     const section = nodeDetailView(props.resource, ctx, { metrics: m.metrics, series: ps.series });
     return section ? h(Section, { s: section }) : null;
   }
 
   /**
-   * Warm store (a plugin page loaded the cluster): the section reads it under
-   * the shared provider. Cold: NodeDetailCold, O(one node).
+   * Nothing for a node without AMD GPUs. Warm store (a plugin page loaded the
+   * cluster): the section reads it under the shared provider. Cold:
+   * NodeDetailCold, O(one node).
    */
   function NodeDetailHost(props) {
+    if (!isAmdGpuNode(unwrapKubeObject(props.resource))) return null;
     if (core.storeWarm()) return h(core.AmdGpuDataProvider, null, h(NodeDetailSection, props));
     return h(NodeDetailCold, props);
   }

@@ -1,0 +1,158 @@
+/**
+ * Device Plugins page view-model (reference
+ * src/components/DevicePluginsPage.tsx:20-219, SURVEY C6): one card per AMD
+ * GPU Operator DeviceConfig and one page of operator pods.
+ */
+
+import {
+  countsToStatus,
+  countsToText,
+  deviceConfigStatus,
+  deviceConfigStatusText,
+  formatComponent,
+  formatSelector,
+  get,
+  operandEnabled,
+  OPERANDS,
+  operandStatus,
+  pluginPodComponent,
+} from '../../api/amdgpu.js';
+import { kv, loader, page, pager, row, section, status, table } from '../ir.js';
+import {
+  ageText,
+  BRAND,
+  chunkedRows,
+  dpPluginRows,
+  errorSection,
+  memo,
+  nowOf,
+  podName,
+  podNode,
+  podNs,
+  readyLabel,
+  refreshButton,
+  restartsCell,
+  crdPending,
+  podsPending,
+} from './common.js';
+import { podPage } from './paging.js';
+
+function enabledCell(on, detail) {
+  return on ? status('success', detail ? 'Enabled — ' + detail : 'Enabled') : status('warning', 'Disabled');
+}
+
+/**
+ * One card per DeviceConfig (reference: one per GpuDevicePlugin). Per-operand
+ * DaemonSet counts replace the single desired/ready pair. The page needs no
+ * node list: it renders once the DeviceConfigs are in, with a loader where
+ * the operator pods go until the pod list is in (reference: a full-page
+ * Loader until every list is in, DevicePluginsPage.tsx:23-25).
+ */
+export function devicePluginsView(ctx, opts) {
+  const now = nowOf(opts);
+  if (crdPending(ctx)) return page(null, null, [loader('Loading device plugin data...')]);
+  const podsPend = podsPending(ctx);
+  // One page of the operator pod table (PODS_PER_PAGE; filter on
+  // namespace/name and node): three per GPU node on a real cluster.
+  const pg = podPage(ctx.pluginPods, opts && opts.pager, 'plugin-pod');
+  const items = memo(
+    'device-plugins',
+    [ctx.deviceConfigs, pg, ctx.crdAvailable, ctx.error, podsPend],
+    function () { return devicePluginsItems(ctx, now, pg, podsPend); },
+    now
+  );
+  return page(BRAND + ' — Device Plugins', refreshButton('Refresh device plugin data', ctx.refreshing), items);
+}
+
+function devicePluginsItems(ctx, now, pg, podsPend) {
+  const items = [];
+  if (ctx.error) items.push(errorSection(ctx.error));
+
+  if (!ctx.crdAvailable) {
+    items.push(
+      section('CRD Not Available', [
+        kv(ctx.crdForbidden
+          ? [
+            // 403: the operator may well be installed; this user cannot list its CRs.
+            row('Status', status('warning', 'DeviceConfig list forbidden for this user (HTTP 403)')),
+            row('Note', 'Grant list on deviceconfigs.amd.com (deploy/rbac/headlamp-amd-gpu-viewer.yaml). Device plugin daemon pods are shown below if detected.'),
+          ]
+          : [
+            row('Status', status('warning', 'DeviceConfig CRD (amd.com/v1alpha1) is not installed')),
+            row(
+              'Note',
+              'Install the AMD GPU Operator to manage DeviceConfig resources. Device plugin daemon pods are shown below if detected.'
+            ),
+          ]),
+      ])
+    );
+  }
+
+  if (ctx.crdAvailable && ctx.deviceConfigs.length === 0) {
+    items.push(
+      section('No Device Configs', [
+        kv([
+          row('Status', status('warning', 'No DeviceConfig resources found on this cluster')),
+          row('Create', 'kubectl apply -f deviceconfig.yaml (see the AMD GPU Operator documentation)'),
+        ]),
+      ])
+    );
+  }
+
+  for (let i = 0; i < ctx.deviceConfigs.length; i++) {
+    const dc = ctx.deviceConfigs[i];
+    const dp = operandStatus(dc, 'devicePlugin');
+    const rows = [
+      row('Status', status(deviceConfigStatus(dc), deviceConfigStatusText(dc))),
+      row('Namespace', dc.metadata.namespace || '—'),
+      row('Device Plugin Image', get(dc, ['spec', 'devicePlugin', 'devicePluginImage'], '—')),
+      row(
+        'Driver',
+        enabledCell(operandEnabled(dc, 'driver'), get(dc, ['spec', 'driver', 'version'], null))
+      ),
+      row('Node Labeller', enabledCell(operandEnabled(dc, 'nodeLabeller'))),
+      row(
+        'Metrics Exporter',
+        enabledCell(
+          operandEnabled(dc, 'metricsExporter'),
+          get(dc, ['spec', 'metricsExporter', 'port'], null) !== null ? 'port ' + get(dc, ['spec', 'metricsExporter', 'port'], '') : null
+        )
+      ),
+      row('Desired Nodes', String(dp.desired)),
+      row('Ready Nodes', String(dp.available)),
+    ];
+    if (dp.unavailable > 0) rows.push(row('Unavailable Nodes', status('error', dp.unavailable)));
+    for (let k = 0; k < OPERANDS.length; k++) {
+      const op = OPERANDS[k];
+      if (op.key === 'devicePlugin' || !operandEnabled(dc, op.key)) continue;
+      const st = operandStatus(dc, op.key);
+      rows.push(row(op.label + ' Pods', status(countsToStatus(st.desired, st.available), countsToText(st.desired, st.available))));
+    }
+    rows.push(row('Node Selector', formatSelector(get(dc, ['spec', 'selector'], null))));
+    rows.push(row('Age', ageText(dc.metadata.creationTimestamp, now)));
+    items.push(section('DeviceConfig: ' + dc.metadata.name, [kv(rows)], dc.metadata.uid || dc.metadata.name));
+  }
+
+  if (podsPend) {
+    items.push(loader('Loading operator pods...'));
+  } else if (ctx.pluginPods.length > 0) {
+    items.push(pager(pg, 'operator pods'));
+    items.push(
+      section('Plugin Daemon Pods', [
+        table(
+          ['Name', 'Namespace', 'Component', 'Node', 'Ready', 'Restarts', 'Age'],
+          chunkedRows('dp-plugin-rows', pg.nodes, [], function (p) {
+            return dpPluginRows(p, [], function () {
+              return [
+                podName(p), podNs(p), formatComponent(pluginPodComponent(p)), podNode(p), readyLabel(p),
+                restartsCell(p), ageText(p.metadata.creationTimestamp, now),
+              ];
+            }, now);
+          }, now)
+        ),
+      ])
+    );
+  }
+
+  return items;
+}

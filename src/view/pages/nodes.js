@@ -1,0 +1,357 @@
+/**
+ * GPU Nodes page view-model (reference src/components/NodesPage.tsx:145-293,
+ * SURVEY C7): summary table and per-node cards with the per-GPU allocation
+ * strip and the xGMI neighbour matrix, one page of nodes at a time, and what
+ * that page asks Prometheus for (telemetryScope).
+ */
+
+import {
+  formatBytes,
+  formatGpuModel,
+  formatGpuResourceName,
+  get,
+  getGpuResources,
+  getNodeGpuCount,
+  getNodeGpuModel,
+  getNodePhysicalGpuCount,
+  isNodeReady,
+  labellerValue,
+  MI355X,
+} from '../../api/amdgpu.js';
+import { SMALL_CLUSTER_NODES } from '../../api/metrics.js';
+import { buildGpuSlots, buildXgmiMatrix, isFullMesh } from '../../api/topology.js';
+import { kv, loader, page, pager, row, section, status, table } from '../ir.js';
+import {
+  ageText,
+  allocationBar,
+  BRAND,
+  chunkedRows,
+  errorSection,
+  memo,
+  NO_PODS,
+  nodeSummaryRows,
+  nowOf,
+  podName,
+  powerBar,
+  refreshButton,
+  nodesPending,
+  PODS_LOADING,
+  podsPending,
+} from './common.js';
+import { nodeNameOf, nodePage, NODES_PER_PAGE, nodeSortOf, RANKED_NODE_SORTS, rankedPage } from './paging.js';
+
+/** Names of the GPU nodes a paged view shows ([] while the node list is loading). */
+export function visibleNodeNames(ctx, state) {
+  if (!ctx || nodesPending(ctx) || !ctx.gpuNodes) return [];
+  return nodePage(ctx.gpuNodes, state, ctx.index).names;
+}
+
+/**
+ * What a paged page asks Prometheus for:
+ *   * while the node list is loading, and while every GPU node fits on one
+ *     page: `small` — the whole cluster if it has at most SMALL_CLUSTER_NODES
+ *     GPU nodes, else the page's nodes, decided by Prometheus in the same request
+ *     (metrics.js smallClusterQuery). A small cluster's page thus needs no
+ *     second wave after the node list, and keeps one query key (no refetch)
+ *     when the list arrives;
+ *   * the names on the page once a larger cluster is listed;
+ *   * cluster-wide (`scope` undefined) when the node list failed (e.g. RBAC
+ *     denies listing nodes), so telemetry still shows;
+ *   * with `ranked` (Metrics) and the power order: `rank`, the page Prometheus
+ *     is to pick (metrics.js rankedClusterQuery).
+ * @returns {{enabled: boolean, scope?: (string[]|undefined), small?: boolean,
+ *            rank?: {by: string, page: number, per: number, filter: string}}}
+ */
+export function telemetryScope(ctx, state, ranked) {
+  if (!ctx) return { enabled: false, scope: [] };
+  // Power order (Metrics): Prometheus picks the page — no node list needed.
+  if (ranked && nodeSortOf(state, RANKED_NODE_SORTS) === 'power') {
+    const st = state || {};
+    return {
+      enabled: true,
+      rank: { by: 'power', page: Math.max(0, Math.floor(st.page) || 0), per: NODES_PER_PAGE, filter: (st.filter || '').trim().toLowerCase() },
+    };
+  }
+  // The node list alone decides the page (the pod list of a large cluster
+  // arrives later: tens of MB against the node list's few).
+  const nodes = ctx.nodesState;
+  if (nodes === 'error') return { enabled: true, scope: undefined };
+  if (nodes !== 'ready' && nodesPending(ctx)) return { enabled: true, scope: [], small: true };
+  if (ctx.error && (!ctx.gpuNodes || ctx.gpuNodes.length === 0)) return { enabled: true, scope: undefined };
+  const names = nodePage(ctx.gpuNodes, state, ctx.index).names;
+  return ctx.gpuNodes.length <= SMALL_CLUSTER_NODES ? { enabled: true, scope: names, small: true } : { enabled: true, scope: names };
+}
+
+/** Per-GPU allocation strip block. */
+export function slotsBlock(node, podsOnNode, owners) {
+  const s = buildGpuSlots(node, podsOnNode, owners);
+  return { t: 'slots', slots: s.slots, exact: s.exact, partitionsPerGpu: s.partitionsPerGpu };
+}
+
+/** xGMI neighbour matrix block; `measuredTopology` when link hops came from the exporter. */
+export function matrixBlock(gpuCount, measured, probed) {
+  const hasProbe = !!probed && Object.keys(probed).length > 0;
+  const m = buildXgmiMatrix(gpuCount, measured, hasProbe ? probed : undefined);
+  return {
+    t: 'matrix',
+    matrix: m,
+    fullMesh: isFullMesh(m),
+    // Link types / hops come from the exporter's gpu_xgmi_link_hops (this
+    // repo's amdgpu-exporter); without them the matrix is the MI355X
+    // platform model, and only per-link throughput (stock exporter
+    // xgmi_neighbor_*_tx_throughput) is measured.
+    measuredTopology: hasProbe,
+    measuredThroughput: !!measured && Object.keys(measured).length > 0,
+  };
+}
+
+/**
+ * Readiness as `kubectl get nodes` words it: "Ready", "Not Ready", and
+ * ", SchedulingDisabled" on a cordoned node (spec.unschedulable) — whose free
+ * GPUs new pods cannot use, hence a warning.
+ */
+export function nodeReadyCell(node) {
+  const ready = isNodeReady(node);
+  const cordoned = get(node, ['spec', 'unschedulable'], false) === true;
+  const text = (ready ? 'Ready' : 'Not Ready') + (cordoned ? ', SchedulingDisabled' : '');
+  return status(!ready ? 'error' : cordoned ? 'warning' : 'success', text);
+}
+
+/** "key=value:Effect" per taint (the reference models NodeSpec.taints, k8s.ts:92-122, but never shows them). */
+export function formatTaints(node) {
+  const ts = get(node, ['spec', 'taints'], []);
+  if (!Array.isArray(ts) || ts.length === 0) return null;
+  return ts.map(function (t) { return (t.key || '') + (t.value ? '=' + t.value : '') + ':' + (t.effect || ''); }).join(', ');
+}
+
+function nodeCardRows(node, podsOnNode, stats, now, podsPend) {
+  const model = getNodeGpuModel(node);
+  const count = getNodeGpuCount(node);
+  const cap = getGpuResources(get(node, ['status', 'capacity'], null));
+  const alloc = getGpuResources(get(node, ['status', 'allocatable'], null));
+  const rows = [
+    row('Status', nodeReadyCell(node)),
+    row('GPU Model', model.product),
+  ];
+  const taints = formatTaints(node);
+  if (taints) rows.push(row('Taints', taints));
+  if (count > 0) {
+    const phys = getNodePhysicalGpuCount(node);
+    rows.push(row('GPU Devices (amd.com/gpu)', phys !== count ? count + ' (' + phys + ' × ' + model.shortName + ' in ' + model.computePartition + ')' : String(count)));
+    rows.push(row('HBM', formatBytes(phys * MI355X.hbmBytes) + ' (' + phys + ' × ' + model.vram + ')'));
+  }
+  for (const k in cap) rows.push(row(formatGpuResourceName(k) + ' (capacity)', cap[k]));
+  for (const k in alloc) rows.push(row(formatGpuResourceName(k) + ' (allocatable)', alloc[k]));
+  if (podsPend) rows.push(row('GPU Allocation', PODS_LOADING));
+  else if (stats) rows.push(row('GPU Allocation', allocationBar(stats.inUse, stats.allocatable || count)));
+  if (model.computePartition || model.memoryPartition) rows.push(row('Partition Mode', formatGpuModel(model)));
+  const drv = labellerValue(node, 'driver-version');
+  if (drv) rows.push(row('amdgpu Driver', drv));
+  rows.push(row('GPU Workload Pods', podsPend ? PODS_LOADING : podsOnNode.length > 0 ? podsOnNode.map(podName).join(', ') : '—'));
+  rows.push(row('OS Image', get(node, ['status', 'nodeInfo', 'osImage'], '—')));
+  rows.push(row('Kernel', get(node, ['status', 'nodeInfo', 'kernelVersion'], '—')));
+  rows.push(row('Kubelet', get(node, ['status', 'nodeInfo', 'kubeletVersion'], '—')));
+  rows.push(row('Age', ageText(node.metadata.creationTimestamp, now)));
+  return rows;
+}
+
+/**
+ * Differences: Allocation = GPUs held / allocatable GPUs (reference used the
+ * pod count, quirk Q2); each node card adds HBM, the per-GPU allocation
+ * strip and the xGMI neighbour matrix. `metrics` (optional) supplies exact
+ * per-GPU owners and measured xGMI throughput. The page renders from the
+ * node list: while the pod list is still loading, the cells that need pods
+ * (allocation, GPU pods, workload pods, the inferred slot strip) say so and
+ * fill in when it arrives (reference: a full-page Loader until every list is
+ * in, NodesPage.tsx:148-150).
+ */
+export function nodesView(ctx, opts) {
+  const now = nowOf(opts);
+  const metrics = opts && opts.metrics ? opts.metrics : null;
+  if (nodesPending(ctx)) return page(null, null, [loader('Loading GPU node data...')]);
+  const podsPend = podsPending(ctx);
+  // One page of nodes (NODES_PER_PAGE, name filter): the summary rows, the
+  // cards and the telemetry the page asks for are all O(page), not O(cluster).
+  // In power order Prometheus picked the page (metrics.js rankedSnapshot).
+  const pagerState = opts && opts.pager;
+  const sort = nodeSortOf(pagerState, RANKED_NODE_SORTS);
+  const pg = metrics && metrics.rank && sort === 'power' ? rankedNodePage(ctx, metrics, pagerState)
+    : nodePage(ctx.gpuNodes, pagerState, ctx.index);
+  // Live node power (the GPU Nodes query carries the power gauge for pod
+  // attribution anyway): "watts|cap" per node, whole watts, so the head and
+  // its rows rebuild only when a shown value changes.
+  const power = nodePowerKeys(metrics);
+  const head = memo('nodes-head', [pg, ctx.index, ctx.error, power.sig, podsPend], function () {
+    return nodesHeadItems(ctx, now, power.byNode, pg, sort, podsPend);
+  }, now);
+  const owners = ownersByNode(metrics);
+  const xgmi = metrics ? metrics.xgmi : undefined;
+  const links = metrics ? metrics.links : undefined;
+  // The card list as a whole holds while no input changed (most watch events
+  // touch no GPU node or pod); otherwise only changed cards are rebuilt.
+  const items = memo('nodes-cards', [head, pg, ctx.index, owners, xgmi, links, podsPend], function () {
+    const idx = ctx.index;
+    function inputs(n) {
+      const name = n.metadata.name;
+      return [idx.podsByNode.get(name) || NO_PODS, idx.nodeStats.get(name), owners[name],
+        xgmi ? xgmi[name] : undefined, links ? links[name] : undefined];
+    }
+    const cards = chunkedRows('node-cards', pg.nodes, [], function (n) {
+      const name = n.metadata.name;
+      const d = inputs(n);
+      const pods = d[0];
+      const stats = d[1];
+      const own = d[2];
+      const xg = d[3];
+      const lk = d[4];
+      // own / xg / lk keep their identity while their content is unchanged
+      // (ownersByNode + the metrics client's structural sharing).
+      return memo('node-card:' + name, [n, pods, stats, own, xg, lk, podsPend], function () {
+        const blocks = [kv(nodeCardRows(n, pods, stats, now, podsPend))];
+        const count = getNodeGpuCount(n);
+        if (count > 0) {
+          // Without the pods the strip is exact only from exporter owners.
+          if (!podsPend || own) blocks.push(slotsBlock(n, podsPend ? NO_PODS : pods, own));
+          blocks.push(matrixBlock(getNodePhysicalGpuCount(n), xg, lk));
+        }
+        return section(name, blocks, n.metadata.uid || name);
+      }, now);
+    }, now, inputs);
+    return head.concat(cards);
+  }, now);
+  return page(BRAND + ' — Nodes', refreshButton('Refresh node data', !!(opts && opts.fetching)), items);
+}
+
+const ownersCache = typeof WeakMap === 'function' ? new WeakMap() : null;
+
+let lastOwners = {};
+
+function sameOwners(a, b) {
+  if (!a || !b || a.length !== b.length) return false;
+  for (let i = 0; i < a.length; i++) {
+    if (a[i].gpu !== b[i].gpu || a[i].pod !== b[i].pod || a[i].namespace !== b[i].namespace) return false;
+  }
+  return true;
+}
+
+/**
+ * node → [{gpu, pod, namespace}] from exporter pod labels, computed once per
+ * GPU list; a node's array keeps its identity while its owners are unchanged
+ * (telemetry values change every scrape, GPU ownership rarely).
+ */
+const NO_OWNERS = Object.freeze({});
+
+export function ownersByNode(metrics) {
+  if (!metrics || !metrics.gpus) return NO_OWNERS;
+  if (ownersCache && ownersCache.has(metrics.gpus)) return ownersCache.get(metrics.gpus);
+  const out = {};
+  for (let i = 0; i < metrics.gpus.length; i++) {
+    const g = metrics.gpus[i];
+    if (!g.pod) continue;
+    if (!out[g.nodeName]) out[g.nodeName] = [];
+    out[g.nodeName].push({ gpu: g.gpu, pod: g.pod, namespace: g.namespace });
+  }
+  for (const k in out) {
+    if (sameOwners(lastOwners[k], out[k])) out[k] = lastOwners[k];
+  }
+  lastOwners = out;
+  if (ownersCache) ownersCache.set(metrics.gpus, out);
+  return out;
+}
+
+/** Per-node GPU power from a telemetry snapshot: {byNode: {node: "watts|cap"}, sig} (whole watts). */
+export function nodePowerKeys(metrics) {
+  const sum = {};
+  const gs = metrics && Array.isArray(metrics.gpus) ? metrics.gpus : [];
+  for (let i = 0; i < gs.length; i++) {
+    const g = gs[i];
+    if (typeof g.powerWatts !== 'number' || !isFinite(g.powerWatts)) continue;
+    const e = sum[g.nodeName] || (sum[g.nodeName] = [0, 0]);
+    e[0] += g.powerWatts;
+    e[1] += typeof g.powerCapWatts === 'number' && isFinite(g.powerCapWatts) ? g.powerCapWatts : 0;
+  }
+  const byNode = {};
+  const names = Object.keys(sum).sort();
+  for (let i = 0; i < names.length; i++) byNode[names[i]] = Math.round(sum[names[i]][0]) + '|' + Math.round(sum[names[i]][1]);
+  return { byNode: byNode, sig: names.map(function (n) { return n + '=' + byNode[n]; }).join(',') };
+}
+
+function nodePowerCell(key) {
+  if (!key) return '—';
+  const parts = key.split('|');
+  const cap = Number(parts[1]);
+  return powerBar(Number(parts[0]), cap > 0 ? cap : null);
+}
+
+function nodesHeadItems(ctx, now, powerByNode, pg, sort, podsPend) {
+  const pw = powerByNode || {};
+  const withPower = Object.keys(pw).length > 0;
+  const items = [];
+  if (ctx.error) items.push(errorSection(ctx.error));
+
+  if (ctx.gpuNodes.length === 0) {
+    items.push(
+      section('No GPU Nodes Found', [
+        kv([
+          row('Status', status('warning', 'No nodes with AMD GPU resources or labels were found')),
+          row(
+            'Note',
+            'Nodes appear here when they advertise amd.com/gpu or carry AMD node-feature-discovery / node-labeller labels. ' +
+              'Ensure the AMD GPU Operator (or the AMD k8s device plugin) and Node Feature Discovery are installed.'
+          ),
+        ]),
+      ])
+    );
+    return items;
+  }
+
+  items.push(pager(pg, pg.ranked ? 'GPU nodes reporting' : 'GPU nodes', { sort: sort, sorts: RANKED_NODE_SORTS, label: 'GPU nodes' }));
+  const idx = ctx.index;
+  if (pg.nodes.length > 0) {
+    items.push(
+      section('GPU Node Summary', [
+        table(
+          // "Power" (beyond the reference): the node's GPUs' live power against their summed cap.
+          ['Node', 'Ready', 'GPU Model', 'GPU Devices', 'Allocation', 'GPU Pods'].concat(withPower ? ['Power'] : [], ['Age']),
+          chunkedRows('node-summary-rows', pg.nodes, [withPower, podsPend], function (n) {
+            const st = idx.nodeStats.get(n.metadata.name);
+            const pk = pw[n.metadata.name];
+            // Per-node stats keep their identity while unchanged (buildClusterIndex).
+            return nodeSummaryRows(n, [st, withPower, pk, podsPend], function () {
+              const count = getNodeGpuCount(n);
+              return [
+                n.metadata.name,
+                nodeReadyCell(n),
+                formatGpuModel(getNodeGpuModel(n)),
+                count > 0 ? String(count) : '—',
+                podsPend ? PODS_LOADING : allocationBar(st ? st.inUse : 0, (st && st.allocatable) || count),
+                podsPend ? PODS_LOADING : String(st ? st.pods : 0),
+              ].concat(withPower ? [nodePowerCell(pk)] : [], [ageText(n.metadata.creationTimestamp, now)]);
+            }, now);
+          }, now, function (n) { return [idx.nodeStats.get(n.metadata.name), withPower, pw[n.metadata.name]]; }),
+          pg.nodes.map(function (n) { return n.metadata.uid || n.metadata.name; })
+        ),
+      ])
+    );
+  }
+
+  return items;
+}
+
+/**
+ * GPU Nodes in power order: the ranked page's names (metrics.rank) as the
+ * listed node objects; a ranked hostname that is no listed node is left out.
+ */
+function rankedNodePage(ctx, m, state) {
+  const byName = memo('nodes-by-name', [ctx.gpuNodes], function () {
+    const out = new Map();
+    for (let i = 0; i < ctx.gpuNodes.length; i++) out.set(ctx.gpuNodes[i].metadata.name, ctx.gpuNodes[i]);
+    return out;
+  });
+  return memo('nodes-ranked-page', [m, byName], function () {
+    const base = rankedPage(m, state);
+    const nodes = [];
+    for (let i = 0; i < base.names.length; i++) if (byName.has(base.names[i])) nodes.push(byName.get(base.names[i]));
+    return Object.assign({}, base, { nodes: nodes, names: nodes.map(nodeNameOf), ranked: true });
+  });
+}

@@ -1,0 +1,284 @@
+/**
+ * GPU Pods page view-model (reference src/components/PodsPage.tsx:94-270,
+ * SURVEY C8): one page of GPU pods, the pending pods, and which physical
+ * GPUs each pod holds when the exporter attributes them (ownersScope).
+ */
+
+import {
+  containerGpuEntries,
+  formatBytes,
+  formatGpuResourceName,
+  formatPodGpuRequests,
+  formatWatts,
+  gpuContainers,
+  gpuInitContainers,
+  phaseToStatus,
+  podFacts,
+  podPhase,
+  podWaitingMessage,
+  podWaitingReason,
+} from '../../api/amdgpu.js';
+import { SMALL_CLUSTER_PODS } from '../../api/metrics.js';
+import { kv, lines, loader, page, pager, row, section, status, table } from '../ir.js';
+import {
+  ageText,
+  BRAND,
+  chunkedFilter,
+  chunkedRows,
+  errorSection,
+  memo,
+  nowOf,
+  pendingRows,
+  podName,
+  podNode,
+  podNs,
+  podRows,
+  refreshButton,
+  restartsCell,
+  nodesPending,
+  podsPending,
+} from './common.js';
+import { podKeyOf, podPage, PODS_PER_PAGE, podSortOf, RANKED_POD_SORTS } from './paging.js';
+
+/** The rank of a power-ordered owners answer as a pager page: its pods, in rank order, out of the pods ranked. */
+function rankedPodPage(ctx, m, state) {
+  const byKey = memo('pods-by-key', [ctx.gpuPods], function () {
+    const out = new Map();
+    for (let i = 0; i < ctx.gpuPods.length; i++) out.set(podKeyOf(ctx.gpuPods[i]), ctx.gpuPods[i]);
+    return out;
+  });
+  return memo('pods-ranked-page', [m, byKey], function () {
+    const r = m.rank;
+    const pods = [];
+    for (let i = 0; i < r.order.length; i++) if (byKey.has(r.order[i])) pods.push(byKey.get(r.order[i]));
+    const count = Math.max(r.count, r.page * r.per + pods.length);
+    const from = Math.min(r.page * r.per, count);
+    return {
+      nodes: pods, names: pods.map(podKeyOf), page: r.page, pages: Math.max(1, Math.ceil(count / r.per)), from: from,
+      to: from + pods.length, total: count, matched: count, filter: (state && state.filter) || '', perPage: r.per, ranked: true,
+    };
+  });
+}
+
+let lastAssign = {};
+
+function sameAssign(a, b) {
+  if (!a || !b || a.length !== b.length) return false;
+  for (let i = 0; i < a.length; i++) if (a[i] !== b[i]) return false;
+  return true;
+}
+
+/**
+ * "namespace/pod" → the GPUs the exporter attributes to that pod (its
+ * pod/namespace labels), as GPU objects of the metrics snapshot. Kubernetes
+ * itself does not say which device a pod got; this is the exporter's view.
+ * A pod's array keeps its identity while its GPUs are the same objects
+ * (see the metrics client's structural sharing), and the whole map keeps
+ * its identity while no pod's list changed.
+ */
+export function podGpuAssignments(metrics) {
+  if (!metrics || !metrics.gpus) return {};
+  if (assignCache && assignCache.has(metrics.gpus)) return assignCache.get(metrics.gpus);
+  const out = {};
+  for (let i = 0; i < metrics.gpus.length; i++) {
+    const g = metrics.gpus[i];
+    if (!g.pod) continue;
+    const k = (g.namespace || '') + '/' + g.pod;
+    if (!out[k]) out[k] = [];
+    out[k].push(g);
+  }
+  let same = Object.keys(out).length === Object.keys(lastAssign).length;
+  for (const k in out) {
+    if (sameAssign(lastAssign[k], out[k])) out[k] = lastAssign[k];
+    else same = false;
+  }
+  const res = same ? lastAssign : out;
+  lastAssign = res;
+  if (assignCache) assignCache.set(metrics.gpus, res);
+  return res;
+}
+
+const assignCache = typeof WeakMap === 'function' ? new WeakMap() : null;
+
+export function assignedLines(gs) {
+  return lines(
+    gs.map(function (g) {
+      const parts = [];
+      if (g.powerWatts !== null && g.powerWatts !== undefined) parts.push(formatWatts(g.powerWatts));
+      if (g.gfxActivityPct !== null && g.gfxActivityPct !== undefined) parts.push(Math.round(g.gfxActivityPct) + '% GFX');
+      if (g.vramUsedBytes !== null && g.vramUsedBytes !== undefined) parts.push(formatBytes(g.vramUsedBytes) + ' HBM');
+      return { label: g.nodeName + ' GPU ' + g.gpu, text: parts.length ? parts.join(', ') : 'no telemetry' };
+    })
+  );
+}
+
+function assignedText(gs) {
+  if (!gs || gs.length === 0) return '—';
+  const byNode = {};
+  const order = [];
+  for (let i = 0; i < gs.length; i++) {
+    if (!byNode[gs[i].nodeName]) {
+      byNode[gs[i].nodeName] = [];
+      order.push(gs[i].nodeName);
+    }
+    byNode[gs[i].nodeName].push(gs[i].gpu);
+  }
+  return order.map(function (n) { return n + ': GPU ' + byNode[n].join(', '); }).join('; ');
+}
+
+/**
+ * The Pods page's owner query: `small` (every owner when at most
+ * SMALL_CLUSTER_PODS pods hold a GPU, else the page's pods) while the pod
+ * list loads or is that short; the pods of its page (namespace/name keys)
+ * once a longer list is in; cluster-wide when the pod list failed.
+ * @returns {{enabled: boolean, pods: (string[]|undefined), small?: boolean}}
+ */
+export function ownersScope(ctx, state) {
+  if (!ctx) return { enabled: false, pods: [] };
+  // Power order: Prometheus picks the page — no pod list needed.
+  if (podSortOf(state, RANKED_POD_SORTS) === 'power') {
+    const st = state || {};
+    return {
+      enabled: true,
+      rank: { by: 'power', page: Math.max(0, Math.floor(st.page) || 0), per: PODS_PER_PAGE, filter: (st.filter || '').trim().toLowerCase() },
+    };
+  }
+  if (ctx.podsState === 'error') return { enabled: true, pods: undefined };
+  // As telemetryScope: every owner of a small cluster in the first wave.
+  if (ctx.podsState !== 'ready' && podsPending(ctx)) return { enabled: true, pods: [], small: true };
+  if (ctx.error && (!ctx.gpuPods || ctx.gpuPods.length === 0)) return { enabled: true, pods: undefined };
+  const pods = podPage(ctx.gpuPods, state).names;
+  return ctx.gpuPods.length <= SMALL_CLUSTER_PODS ? { enabled: true, pods: pods, small: true } : { enabled: true, pods: pods };
+}
+
+/** Per-container GPU lines (reference GpuContainerList, PodsPage.tsx:49-88), init containers included. */
+export function gpuContainerLines(pod) {
+  const out = [];
+  function add(c, init) {
+    const es = containerGpuEntries(c);
+    const parts = [];
+    for (let i = 0; i < es.length; i++) {
+      const e = es[i];
+      const label = formatGpuResourceName(e.key);
+      if (e.request !== null && e.limit !== null && e.request === e.limit) parts.push(label + ': ' + e.request);
+      else parts.push(label + ': req=' + (e.request === null ? '—' : e.request) + ' lim=' + (e.limit === null ? '—' : e.limit));
+    }
+    out.push({ label: c.name + (init ? ' (init)' : ''), text: parts.join(', ') });
+  }
+  const ics = gpuInitContainers(pod);
+  for (let i = 0; i < ics.length; i++) add(ics[i], true);
+  const cs = gpuContainers(pod);
+  for (let i = 0; i < cs.length; i++) add(cs[i], false);
+  return out.length ? lines(out) : '—';
+}
+
+export function podsView(ctx, opts) {
+  const now = nowOf(opts);
+  // The page draws the pod list (and the index, built from the nodes too); it
+  // does not wait for the DeviceConfigs.
+  if (podsPending(ctx) || nodesPending(ctx)) return page(null, null, [loader('Loading GPU pod data...')]);
+  const assign = opts && opts.metrics ? podGpuAssignments(opts.metrics) : null;
+  // One page of the GPU pod table (PODS_PER_PAGE, filter on namespace/name
+  // and node): the reference lists every GPU pod (PodsPage.tsx:201-236).
+  const sort = podSortOf(opts && opts.pager, RANKED_POD_SORTS);
+  const m = opts && opts.metrics;
+  const ranked = sort === 'power' && m && m.rank && Array.isArray(m.rank.order);
+  const pg = ranked ? rankedPodPage(ctx, m, opts.pager) : podPage(ctx.gpuPods, opts && opts.pager);
+  const items = memo('pods', [pg, ctx.index, ctx.error, assign, sort], function () {
+    return podsItems(ctx, now, assign, pg, sort);
+  }, now);
+  return page(BRAND + ' — Pods', refreshButton('Refresh pod data', !!(opts && opts.fetching)), items);
+}
+
+function podsItems(ctx, now, assign, pg, sort) {
+  const items = [];
+  if (ctx.error) items.push(errorSection(ctx.error));
+  const pods = ctx.gpuPods;
+
+  if (pods.length === 0) {
+    items.push(
+      section('No GPU Pods Found', [
+        kv([
+          row('Status', status('warning', 'No pods requesting AMD GPU resources were found')),
+          row('Note', 'Pods appear here when they request resources like amd.com/gpu.'),
+        ]),
+      ])
+    );
+  }
+
+  const ph = ctx.index.phases;
+  const pending = ph.Pending > 0 ? chunkedFilter('pending-pods', pods, function (p) { return podFacts(p).phase === 'Pending'; }) : [];
+  if (pods.length > 0) {
+    const rows = [row('Total GPU Pods', String(pods.length))];
+    if (ph.Running > 0) rows.push(row('Running', status('success', ph.Running)));
+    if (ph.Pending > 0) rows.push(row('Pending', status('warning', ph.Pending)));
+    if (ph.Failed > 0) rows.push(row('Failed', status('error', ph.Failed)));
+    rows.push(row('GPUs Held', String(ctx.index.totals.heldGpus)));
+    items.push(section('Summary', [kv(rows)]));
+
+    // With exporter pod labels, show which physical GPUs each pod holds.
+    const exact = assign && Object.keys(assign).length > 0;
+    const cols = ['Name', 'Namespace', 'Node', 'Phase', 'GPU Resources', 'Restarts', 'Age'];
+    if (exact) cols.splice(5, 0, 'Assigned GPUs', 'GPU Power');
+    items.push(pager(pg, pg.ranked ? 'GPU pods drawing power' : 'GPU pods', { sort: sort, sorts: RANKED_POD_SORTS, label: 'GPU pods' }));
+    items.push(
+      section('All GPU Pods', [
+        table(
+          cols,
+          chunkedRows('pod-rows', pg.nodes, [exact, assign], function (p) {
+            // A pod's assignment keeps its identity while its GPUs are unchanged (podGpuAssignments).
+            const gs = exact ? assign[(p.metadata.namespace || '') + '/' + p.metadata.name] : undefined;
+            return podRows(p, [exact, gs], function () {
+              const phase = podPhase(p);
+              const r = [
+                podName(p), podNs(p), podNode(p), status(phaseToStatus(phase), phase), gpuContainerLines(p),
+                restartsCell(p), ageText(p.metadata.creationTimestamp, now),
+              ];
+              if (exact) r.splice(5, 0, assignedText(gs), podPowerText(gs));
+              return r;
+            }, now);
+          }, now),
+          pg.nodes.map(function (p) { return p.metadata.uid || (p.metadata.namespace + '/' + p.metadata.name); })
+        ),
+      ])
+    );
+  }
+
+  if (pending.length > 0) {
+    // The oldest PODS_PER_PAGE pending pods (a scheduler backlog can be
+    // thousands deep); the rest are counted, and found with the filter.
+    const shown = pending.length > PODS_PER_PAGE ? pending.slice(0, PODS_PER_PAGE) : pending;
+    const blocks = [
+      table(
+        // "Message" (beyond the reference): why the scheduler cannot place the pod.
+        ['Name', 'Namespace', 'GPU Resources', 'Waiting Reason', 'Message', 'Age'],
+        shown.map(function (p) {
+          return pendingRows(p, [], function () {
+            return [podName(p), podNs(p), formatPodGpuRequests(p), podWaitingReason(p) || '—', podWaitingMessage(p) || '—',
+              ageText(p.metadata.creationTimestamp, now)];
+          }, now);
+        })
+      ),
+    ];
+    if (shown.length < pending.length) {
+      blocks.push(kv([row('Not shown', (pending.length - shown.length) + ' more pending GPU pods (filter the table above by name)')]));
+    }
+    items.push(section('Attention: Pending GPU Pods', blocks));
+  }
+
+  return items;
+}
+
+/** Live power of the GPUs a pod holds (exporter pod labels), summed; "—" without a reading. */
+export function podPowerText(gs) {
+  if (!gs || !gs.length) return '—';
+  let w = 0;
+  let any = false;
+  for (let i = 0; i < gs.length; i++) {
+    if (typeof gs[i].powerWatts === 'number' && isFinite(gs[i].powerWatts)) {
+      w += gs[i].powerWatts;
+      any = true;
+    }
+  }
+  return any ? formatWatts(w) : '—';
+}

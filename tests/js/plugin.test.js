@@ -260,15 +260,15 @@ describe('detail sections', () => {
     expect(r.text()).toContain('Unavailable — the pod list could not be read');
   });
 
-  it('cold Node detail (no plugin page yet) reads its own pods: one field-selected request, no cluster-wide watch', async () => {
+  it('cold Node detail (no plugin page yet) reads its own pods: a list + watch scoped to the node, no cluster-wide watch', async () => {
     cluster();
     const r = render(nodeSection(makeGpuNode('mi355x-1')));
     await r.settle();
     expect(lib.lists.calls.Node).toHaveLength(0);
-    expect(lib.lists.calls.Pod).toHaveLength(0);
+    expect(lib.lists.calls.Pod.length).toBeGreaterThan(0);
+    expect(lib.lists.calls.Pod.every((o) => o && o.fieldSelector === 'spec.nodeName=mi355x-1' && o.namespace === '')).toBe(true);
     expect(lib.api.calls.filter((p) => p === DEVICE_CONFIG_LIST_PATH)).toHaveLength(0);
-    const own = lib.api.calls.filter((p) => p.indexOf('/api/v1/pods?') === 0);
-    expect(own).toEqual(['/api/v1/pods?fieldSelector=' + encodeURIComponent('spec.nodeName=mi355x-1')]);
+    expect(lib.api.calls.filter((p) => p.indexOf('/api/v1/pods') === 0)).toHaveLength(0); // the list is the hook's
     expect(r.html()).toContain('train-b');
     expect(r.html()).not.toContain('train-a'); // mi355x-0's pod
     r.unmount();

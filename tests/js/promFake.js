@@ -69,6 +69,12 @@ export function flatten(d) {
  * (__name__) …, "agg", …)). Unknown shapes answer no rows.
  */
 function term(q, rows) {
+  // `X unless on() (<count>)`: X only while the count has no sample.
+  const unless = /^(.*) unless on\(\) \((count\(count by .*\))\)$/.exec(q);
+  if (unless) {
+    const n = countOf(unless[2], rows);
+    return n ? [] : term(unless[1], rows);
+  }
   // sizeGuard: `(Q) and on() (<count> <= N)` keeps Q's rows when the count passes.
   const guard = /^\((.*)\) and on\(\) \((count\(count by .*\)) (<=|>) (\d+)\)$/.exec(q);
   if (guard) {

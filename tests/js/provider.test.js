@@ -150,36 +150,33 @@ describe('metrics hooks — auto-refresh back-off', () => {
   }
 });
 
-describe('useNodePods (cold Node detail) — auto-refresh', () => {
-  it('re-reads the node\'s pods each auto-refresh period and keeps them through a failed re-read', async () => {
-    vi.useFakeTimers();
-    settings.refreshIntervalSec = 15;
-    let pods = [makeGpuPod('a', { node: 'n1' })];
-    let fail = false;
-    const request = vi.fn((path) => {
-      if (fail) return Promise.reject(Object.assign(new Error('503'), { status: 503 }));
-      const m = /^\/api\/v1\/pods\?fieldSelector=(.*)$/.exec(path);
-      if (!m) return notFound();
-      const node = decodeURIComponent(m[1]).replace(/^spec\.nodeName=/, '');
-      return Promise.resolve(kubeList(pods.filter((p) => p.spec.nodeName === node)));
-    });
-    const c = core(request);
+describe('useNodePods (cold Node detail) — a scoped list + watch', () => {
+  it('follows the watch: pods scheduled later show up; a re-list or a failed watch keeps what is shown', async () => {
+    const c = core(vi.fn(() => notFound()));
+    let renders = 0;
     function S() {
-      const res = c.useNodePods('n1', true);
+      renders++;
+      const res = c.useNodePods('n1');
       return h('div', null, res.loading ? 'loading' : res.podsState + ':' + res.gpuPods.map((p) => p.metadata.name).join(','));
     }
+    lib.lists.Pod = [[makeGpuPod('a', { node: 'n1' }), makeGpuPod('b', { node: 'n2' })], null];
     const r = render(h(S));
     await r.settle();
     expect(r.text()).toBe('ready:a');
-    pods = [makeGpuPod('a', { node: 'n1' }), makeGpuPod('c', { node: 'n1' })];
-    await vi.advanceTimersByTimeAsync(15000);
+    expect(lib.lists.calls.Pod[0]).toEqual({ namespace: '', fieldSelector: 'spec.nodeName=n1' });
+    lib.lists.Pod = [[makeGpuPod('a', { node: 'n1' }), makeGpuPod('c', { node: 'n1' })], null];
+    r.rerender(h(S));
     await r.settle();
     expect(r.text()).toBe('ready:a,c');
-    fail = true;
-    await vi.advanceTimersByTimeAsync(15000);
+    lib.lists.Pod = [null, null]; // the host re-lists
+    r.rerender(h(S));
     await r.settle();
     expect(r.text()).toBe('ready:a,c');
-    expect(request.mock.calls.length).toBe(3);
+    lib.lists.Pod = [null, 'watch closed'];
+    r.rerender(h(S));
+    await r.settle();
+    expect(r.text()).toBe('ready:a,c');
+    expect(renders).toBeLessThan(12);
     r.unmount();
   });
 });

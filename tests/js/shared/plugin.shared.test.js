@@ -52,7 +52,8 @@ function cluster(o) {
     makePluginPod('amdgpu-dp-0'),
   ];
   lib.lists.Node = opt.loading ? [null, null] : [nodes, null];
-  lib.lists.Pod = opt.loading ? [null, null] : [pods, null];
+  // podsLoading: the node list is in, the all-namespaces pod list still in flight.
+  lib.lists.Pod = opt.loading || opt.podsLoading ? [null, null] : [pods, null];
   const fake = prom({ data: exporterData(opt.gpuNodes) });
   lib.api.handler = (path) => {
     if (path === DEVICE_CONFIG_LIST_PATH) return Promise.resolve({ kind: 'List', metadata: {}, items: [makeDeviceConfig()] });
@@ -64,6 +65,7 @@ function cluster(o) {
     }
     return Promise.reject(Object.assign(new Error('503 Service Unavailable'), { status: 503 }));
   };
+  fake.pods = pods;
   return fake;
 }
 
@@ -104,6 +106,70 @@ describe('shared: every route mounts and renders its page (' + tier + ')', () =>
     await r.settle();
     expect(r.text()).toContain('Loading AMD GPU data...');
     expect(r.text()).not.toContain('AMD GPU — Overview');
+    r.unmount();
+  });
+});
+
+describe('shared: progressive cold open — a page waits only for the lists it draws (' + tier + ')', () => {
+  it('Metrics renders its telemetry while the pod list is still pending', async () => {
+    cluster({ podsLoading: true });
+    const r = render(h(route('/amd-gpu/metrics')));
+    await r.settle();
+    expect(r.text()).toContain('AMD GPU — Metrics');
+    expect(r.text()).toContain('GPU Power Summary');
+    expect(r.text()).toContain('mi355x-000 — 8 × MI355X');
+    expect(r.text()).not.toContain('Loading AMD GPU data...');
+    r.unmount();
+  });
+
+  it('GPU Nodes renders its cards from the node list; the pod cells fill in when the pods arrive', async () => {
+    const fake = cluster({ podsLoading: true });
+    const r = render(h(route('/amd-gpu/nodes')));
+    await r.settle();
+    expect(r.text()).toContain('GPU Node Summary');
+    expect(r.text()).toContain('Loading…');
+    expect(r.text()).not.toContain('train-a');
+    lib.lists.Pod = [fake.pods, null];
+    r.rerender(h(route('/amd-gpu/nodes')));
+    await r.settle();
+    expect(r.text()).toContain('train-a');
+    expect(r.text()).not.toContain('Loading…');
+    r.unmount();
+  });
+
+  it('Overview shows nodes, capacity and DeviceConfigs first, a loader where the pods go', async () => {
+    const fake = cluster({ podsLoading: true });
+    const r = render(h(route('/amd-gpu')));
+    await r.settle();
+    expect(r.text()).toContain('AMD GPU — Overview');
+    expect(r.text()).toContain('Device Config Status');
+    expect(r.text()).toContain('Total GPU Devices');
+    expect(r.text()).toContain('Loading GPU pods...');
+    expect(r.text()).not.toContain('Plugin Not Detected');
+    expect(r.text()).not.toContain('GPU Workloads');
+    lib.lists.Pod = [fake.pods, null];
+    r.rerender(h(route('/amd-gpu')));
+    await r.settle();
+    expect(r.text()).toContain('GPU Workloads');
+    expect(r.text()).toContain('Active GPU Pods');
+    expect(r.text()).not.toContain('Loading GPU pods...');
+    r.unmount();
+  });
+
+  it('Device Plugins renders its DeviceConfig cards before either list', async () => {
+    cluster({ loading: true });
+    const r = render(h(route('/amd-gpu/device-plugins')));
+    await r.settle();
+    expect(r.text()).toContain('DeviceConfig: gpu-operator');
+    expect(r.text()).toContain('Loading operator pods...');
+    r.unmount();
+  });
+
+  it('GPU Pods waits for the pod list (the list is its content)', async () => {
+    cluster({ podsLoading: true });
+    const r = render(h(route('/amd-gpu/pods')));
+    await r.settle();
+    expect(r.text()).toContain('Loading GPU pod data...');
     r.unmount();
   });
 });
@@ -231,14 +297,29 @@ describe('shared: GPU Pods in power order (' + tier + ')', () => {
 });
 
 describe('shared: native-view sections (' + tier + ')', () => {
-  it('Node detail on a cold store: the node\'s own pods, no cluster-wide list', async () => {
+  it('Node detail on a cold store: the node\'s own pods by a scoped list + watch, no cluster-wide list', async () => {
     cluster();
     const r = render(reg.details[0]({ resource: { kind: 'Node', jsonData: makeGpuNode('mi355x-001') } }));
     await r.settle();
     expect(r.text()).toContain('AMD GPU');
     expect(r.text()).toContain('train-b');
-    expect(lib.lists.calls.Pod).toHaveLength(0);
-    expect(lib.api.calls.filter((p) => p.indexOf('/api/v1/pods?fieldSelector=') === 0)).toHaveLength(1);
+    expect(lib.lists.calls.Node).toHaveLength(0);
+    expect(lib.lists.calls.Pod.every((o) => o && o.fieldSelector === 'spec.nodeName=mi355x-001')).toBe(true);
+    r.unmount();
+  });
+
+  it('Node detail on a cold store is live: a pod scheduled onto the node after mount shows without remount', async () => {
+    const fake = cluster();
+    const el = () => reg.details[0]({ resource: { kind: 'Node', jsonData: makeGpuNode('mi355x-001') } });
+    const r = render(el());
+    await r.settle();
+    expect(r.text()).toContain('train-b');
+    expect(r.text()).not.toContain('late-job');
+    lib.lists.Pod = [fake.pods.concat([makeGpuPod('late-job', { gpus: 2, node: 'mi355x-001' })]), null];
+    r.rerender(el());
+    await r.settle();
+    expect(r.text()).toContain('late-job');
+    expect(r.text()).toContain('train-b');
     r.unmount();
   });
 

@@ -432,34 +432,32 @@ describe('shared: metrics hooks (' + tier + ')', () => {
 });
 
 describe('shared: useNodePods, the cold Node detail read (' + tier + ')', () => {
-  function nodePodsServer(pods) {
-    return vi.fn((path) => {
-      const m = /^\/api\/v1\/pods\?fieldSelector=(.*)$/.exec(path);
-      if (!m) return notFound();
-      const node = decodeURIComponent(m[1]).replace(/^spec\.nodeName=/, '');
-      return Promise.resolve(kubeList(pods().filter((p) => p.spec.nodeName === node)));
-    });
-  }
   function Section(c, node) {
     return function S() {
-      const r = c.useNodePods(node, true);
+      const r = c.useNodePods(node);
       return h('div', null, r.loading ? 'loading' : r.podsState + ':' + r.gpuPods.map((p) => p.metadata.name).join(','));
     };
   }
 
-  it('one field-selected request for the node, GPU pods only', async () => {
-    const request = nodePodsServer(() => [makeGpuPod('a', { node: 'n1' }), makeGpuPod('b', { node: 'n2' }), makePlainPod('web')]);
+  it('one list + watch scoped to the node (the host hook), GPU pods of that node only, no request of its own', async () => {
+    const request = vi.fn(() => notFound());
+    lib.lists.Pod = [[makeGpuPod('a', { node: 'n1' }), makeGpuPod('b', { node: 'n2' }), makePlainPod('web')], null];
     const r = render(h(Section(core(request), 'n1')));
-    expect(r.text()).toBe('loading');
     await r.settle();
     expect(r.text()).toBe('ready:a');
-    expect(request.mock.calls.map((c) => c[0])).toEqual(['/api/v1/pods?fieldSelector=' + encodeURIComponent('spec.nodeName=n1')]);
+    expect(lib.lists.calls.Pod.every((o) => o.fieldSelector === 'spec.nodeName=n1' && o.namespace === '')).toBe(true);
+    expect(request).not.toHaveBeenCalled();
     r.unmount();
   });
 
-  it('a first failure says the pods are unreadable', async () => {
-    const request = vi.fn(() => Promise.reject(Object.assign(new Error('pods is forbidden'), { status: 403 })));
-    const r = render(h(Section(core(request), 'n1')));
+  it('loading until the list is in; a first failure says the pods are unreadable', async () => {
+    lib.lists.Pod = [null, null];
+    const S = Section(core(vi.fn(() => notFound())), 'n1');
+    const r = render(h(S));
+    await r.settle();
+    expect(r.text()).toBe('loading');
+    lib.lists.Pod = [null, 'pods is forbidden'];
+    r.rerender(h(S));
     await r.settle();
     expect(r.text()).toBe('error:');
     r.unmount();

@@ -12,6 +12,7 @@ export const lists = {
   Node: [null, null],
   Pod: [null, null],
   calls: { Node: [], Pod: [] },
+  selected: {},
 };
 
 export const api = {
@@ -29,6 +30,7 @@ export function resetHeadlamp() {
   lists.Pod = [null, null];
   lists.calls.Node.length = 0;
   lists.calls.Pod.length = 0;
+  lists.selected = {};
   api.calls.length = 0;
   api.handler = function () { return Promise.reject(Object.assign(new Error('no handler'), { status: 404 })); };
 }
@@ -39,11 +41,29 @@ export function registerDetailsViewSection(f) { registry.details.push(f); }
 export function registerResourceTableColumnsProcessor(f) { registry.columns.push(f); }
 export function registerPluginSettings(name, component, showSave) { registry.settings.push({ name: name, component: component, showSave: showSave }); }
 
+/** `spec.nodeName=<n>` of a field selector, or null (the only selector the plugin sends). */
+function selectedNode(opts) {
+  const m = opts && typeof opts.fieldSelector === 'string' ? /^spec\.nodeName=(.*)$/.exec(opts.fieldSelector) : null;
+  return m ? m[1] : null;
+}
+
 function resourceClass(kind) {
   return {
     useList: function (opts) {
       lists.calls[kind].push(opts === undefined ? null : opts);
-      return lists[kind];
+      // A field-selected list holds what the apiserver would return for it:
+      // the objects on that node (identity kept while the list is unchanged).
+      const node = selectedNode(opts);
+      const res = lists[kind];
+      if (node === null || !res || !Array.isArray(res[0])) return res;
+      if (!lists.selected[kind] || lists.selected[kind].from !== res || lists.selected[kind].node !== node) {
+        const items = res[0].filter(function (o) {
+          const raw = o && o.jsonData ? o.jsonData : o;
+          return raw && raw.spec && raw.spec.nodeName === node;
+        });
+        lists.selected[kind] = { from: res, node: node, value: [items, res[1]] };
+      }
+      return lists.selected[kind].value;
     },
   };
 }

@@ -8,7 +8,7 @@ import yaml
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DEPLOY = os.path.join(ROOT, "deploy")
-JS = open(os.path.join(ROOT, "src", "api", "amdgpu.js")).read()
+JS = open(os.path.join(ROOT, "src", "api", "k8sCore.js")).read()
 METRICS_JS = open(os.path.join(ROOT, "src", "api", "series.js")).read()
 
 

@@ -423,3 +423,9 @@ def test_source_probe_decides_the_exporter_in_one_answer():
     big = _vec(query(hwmon([str(i) for i in range(limit // 8 + 1)], 8), q, 100.0))
     assert agg(big, "hwmon") == limit + 8 and [r for r in big if "agg" not in r["metric"]] == []
     assert _vec(query(TSDB(), q, 100.0)) == []  # no exporter, no amdgpu hwmon: nothing at all
+    # A Prometheus scraping both exporters: node-exporter's series are not sent (the exporter's win).
+    both = hwmon(["a"], 8)
+    for g in range(8):
+        both.add(Series({"__name__": "gpu_power_usage", "hostname": "a", "gpu_id": str(g)}, fn=lambda t: 500.0))
+    rows = _vec(query(both, q, 100.0))
+    assert agg(rows, "gpu_nodes") == 1 and agg(rows, "hwmon") == 8 and [r for r in rows if "agg" not in r["metric"]] == []

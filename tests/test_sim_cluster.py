@@ -16,7 +16,7 @@ from headlamp_intel_gpu_plugin_amd.sim.apiserver import (DEFAULT_PROM_SERVICE, F
                                                          parse_field_selector, parse_label_selector)
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-JS = open(os.path.join(ROOT, "src", "api", "amdgpu.js")).read()
+JS = open(os.path.join(ROOT, "src", "api", "k8sCore.js")).read()
 
 
 def js_const(name):

@@ -88,6 +88,28 @@ def table(rows):
     return md
 
 
+def cold_table(rows):
+    """Per page at each point: cold open, reference → new first content / new complete (ms), and the new open's
+    Prometheus requests (query + query_range + probe)."""
+    head = ["Config", "GPU nodes"] + [f"{t}: ref → first / complete (ms), Prometheus requests" for _, t in PAGE_COLS]
+    md = ["| " + " | ".join(head) + " |", "|---|---:|" + "---|" * (len(head) - 2)]
+    for r in rows:
+        l = r["line"]
+        cp = l.get("cold_open_per_page_p50_ms") or {}
+        label = f"{r['point']}-node scaling point" if r["kind"] == "nodes" else PRESET_LABEL[r["point"]]
+        cells = [label, str(l["config"]["nodes"])]
+        for k, _ in PAGE_COLS:
+            v = cp.get(k)
+            if not v or "amd_first_content" not in v:
+                cells.append("—")
+                continue
+            by = v.get("amd_requests_by_kind") or {}
+            prom = sum(by.get(x, 0) for x in ("query", "query_range", "probe"))
+            cells.append(f"{v['reference']:.0f} → {v['amd_first_content']:.0f} / {v['amd']:.0f}, {prom}")
+        md.append("| " + " | ".join(cells) + " |")
+    return md
+
+
 def render_table(rows):
     """Per page at each point: harness-React elements and mount / re-render ms, plus the cold Node detail open."""
     head = ["GPU nodes"] + [f"{t}: elements, mount / re-render ms" for _, t in PAGE_COLS] + [
@@ -191,7 +213,8 @@ def main():
         print(f"{kind}={val}: per-page p50 {line['value']} ms vs ref {line['baseline']['value_ms']} ms", flush=True)
         with open(os.path.join(args.out, "sweep.json"), "w") as f:
             json.dump(rows, f, indent=1)
-    md = (table(rows) + ["", "Render (harness React, first page of each view) and the cold Node detail open:", ""]
+    md = (table(rows) + ["", "Cold open per page (progressive: a page renders once the lists it draws are in):", ""]
+          + cold_table(rows) + ["", "Render (harness React, first page of each view) and the cold Node detail open:", ""]
           + render_table(rows) + react_dom_table(rows))
     with open(os.path.join(args.out, "sweep.md"), "w") as f:
         f.write("\n".join(md) + "\n")
