@@ -30,11 +30,13 @@ import { createMetricsSource } from '../src/api/metrics.js';
 import { filterGpuRequestingPods } from '../src/api/amdgpu.js';
 import {
   overviewView, devicePluginsView, nodesView, podsView, metricsView,
-  nodeDetailView, podDetailView, nodeColumns, nodePage, ownersScope, podPage, telemetryScope,
+  nodeDetailView, podDetailView, nodeColumns, nodePage, ownersScope, podPage, telemetryScope, clearViewMemo,
 } from '../src/view/pages.js';
 import { countRows, sections } from '../src/view/ir.js';
 import { renderPage, renderSection } from '../src/view/html.js';
 import { createReferenceSchedule } from './referenceSchedule.js';
+import { PAGE_NEEDS } from '../src/plugin.js';
+import { loadReferencePages, referenceContext, toGpuMetrics, toIntelNode, toIntelPod } from './referenceRender.js';
 // The harness React (the Node-12 stand-in the spec suite renders the plugin
 // with) and its CommonComponents: the pages are also mounted through the
 // shipped renderer (src/view/react.js) to count elements and time a
@@ -271,8 +273,8 @@ async function realReact(umdDir) {
     const umd = await import('../tests/js/harness/umd-load.js');
     const cc = await import('../tests/js/harness/commonComponents.js');
     const loaded = umd.loadUmdReact(umdDir, 'production');
-    realDom = { React: loaded.React, ReactDOM: loaded.ReactDOM,
-      view: createRenderer(loaded.React, cc.makeCommonComponents(loaded.React.createElement)) };
+    const CC = cc.makeCommonComponents(loaded.React.createElement);
+    realDom = { React: loaded.React, ReactDOM: loaded.ReactDOM, CC: CC, view: createRenderer(loaded.React, CC) };
   }
   return realDom;
 }
@@ -305,6 +307,114 @@ async function reactDomMeasure(umdDir, vm, vm2, reps) {
     document.body.removeChild(c);
   }
   return { mountMs: stats(mounts).p50, rerenderMs: stats(rerenders).p50, elements: elements, reps: reps };
+}
+
+/**
+ * Mount `make()` into a fresh root on real React (flushSync), wait until the
+ * container shows `waitText` when given (a page whose data arrives through an
+ * effect: the reference's MetricsPage fetches in useEffect), then call
+ * `beforeRerender()` (a watch event: a new context value) and render again.
+ * Median over `reps` cycles of the mount and re-render wall times.
+ */
+async function mountCycle(R, make, waitText, beforeRerender, reps, mustShow) {
+  const mounts = [];
+  const rerenders = [];
+  let elements = 0;
+  for (let i = 0; i < reps; i++) {
+    const c = document.createElement('div');
+    document.body.appendChild(c);
+    const root = R.ReactDOM.createRoot(c);
+    const t0 = process.hrtime();
+    R.ReactDOM.flushSync(function () { root.render(make()); });
+    for (let k = 0; waitText && k < 1000 && c.textContent.indexOf(waitText) < 0; k++) {
+      await new Promise(function (r) { setImmediate(r); });
+    }
+    if (waitText && c.textContent.indexOf(waitText) < 0) throw new Error('mountCycle: "' + waitText + '" never rendered');
+    mounts.push(ms(process.hrtime(t0)));
+    if (mustShow && c.textContent.indexOf(mustShow) < 0) throw new Error('mountCycle: the page does not show "' + mustShow + '"');
+    if (beforeRerender) beforeRerender();
+    const t1 = process.hrtime();
+    R.ReactDOM.flushSync(function () { root.render(make()); });
+    rerenders.push(ms(process.hrtime(t1)));
+    elements = c.querySelectorAll('*').length;
+    R.ReactDOM.flushSync(function () { root.unmount(); });
+    document.body.removeChild(c);
+  }
+  return { mountMs: stats(mounts).p50, rerenderMs: stats(rerenders).p50, elements: elements, reps: reps };
+}
+
+/**
+ * The reference's pages and this plugin's, each page mounted on real React
+ * 18.3.1 (production builds) from the same synthetic cluster (see
+ * ./referenceRender.js). Reference: mount with its data (its per-render
+ * aggregation included), re-render on a watch event (a new context value:
+ * new arrays of the same objects), and the provider's per-event filtering of
+ * the whole lists (IntelGpuDataContext.tsx:200-208) apart. This plugin: mount
+ * including the view-model built from a cold memo, re-render on the same
+ * watch event (a new snapshot of the same data), first page of each pager.
+ */
+/** The header each reference page shows once its data is in (its Loader gone). */
+const REFERENCE_TITLES = {
+  overview: 'Intel GPU — Overview', devicePlugins: 'Intel GPU — Device Plugins', nodes: 'Intel GPU — Nodes',
+  pods: 'Intel GPU — Pods', metrics: 'Intel GPU — Metrics',
+};
+
+async function compareRenders(c) {
+  const R = await realReact(c.umdDir);
+  const ref = loadReferencePages(c.referenceDir, R.React, R.CC);
+  const reps = c.reps || 5;
+  const s = amdSchedule(makeRequest(a0.url, { n: 0, bytes: 0 }));
+  await s.coldOpen();
+  await s.fetchAll();
+  const request = makeRequest(a0.url, { n: 0, bytes: 0 });
+  const lists = await Promise.all([request('/api/v1/nodes'), request('/api/v1/pods')]);
+  const snap = s.ctx();
+  const t0 = process.hrtime();
+  const refCtx = referenceContext(ref.k8s, {
+    nodes: lists[0].items, pods: lists[1].items, deviceConfigs: snap.deviceConfigs, pluginPods: snap.pluginPods,
+  });
+  const deriveMs = ms(process.hrtime(t0));
+  // the provider's useMemo filters, per watch event (the lists already in the reference's shapes)
+  const intelNodes = lists[0].items.map(toIntelNode);
+  const intelPods = lists[1].items.map(toIntelPod);
+  const d0 = process.hrtime();
+  ref.k8s.filterIntelGpuNodes(intelNodes);
+  ref.k8s.filterGpuRequestingPods(intelPods);
+  const filterMs = ms(process.hrtime(d0));
+  const refMetrics = toGpuMetrics(s.mstate().metrics);
+  const out = { pages: {}, referenceProviderFilterMs: filterMs, referenceContextBuildMs: deriveMs,
+    gpuNodes: refCtx.gpuNodes.length, gpuPods: refCtx.gpuPods.length, chips: refMetrics.chips.length };
+  for (let p = 0; p < PAGES.length; p++) {
+    const page = PAGES[p];
+    ref.setData(refCtx, refMetrics);
+    const reference = await mountCycle(R, function () { return R.React.createElement(ref.pages[page]); },
+      page === 'metrics' ? 'GPU Power Summary' : null, function () {
+        ref.setData(Object.assign({}, refCtx, {
+          gpuNodes: refCtx.gpuNodes.slice(), gpuPods: refCtx.gpuPods.slice(), pluginPods: refCtx.pluginPods.slice(),
+          devicePlugins: refCtx.devicePlugins.slice(),
+        }), refMetrics);
+      }, reps, REFERENCE_TITLES[page]);
+    const mstatePage = page === 'metrics' ? s.pageMstate() : s.mstate();
+    let ctx = snap;
+    const amd = await mountCycle(R, function () {
+      return R.React.createElement(R.view.Page, { vm: pageVm(page, ctx, mstatePage, s.pageMetrics(page)) });
+    }, null, function () { ctx = Object.assign({}, snap); }, 1);
+    // mount from a cold view memo each rep (the first page render of a session)
+    const colds = [];
+    for (let i = 0; i < reps; i++) {
+      clearViewMemo();
+      ctx = snap;
+      colds.push(await mountCycle(R, function () {
+        return R.React.createElement(R.view.Page, { vm: pageVm(page, ctx, mstatePage, s.pageMetrics(page)) });
+      }, null, function () { ctx = Object.assign({}, snap); }, 1));
+    }
+    out.pages[page] = {
+      reference: reference,
+      amd: { mountMs: stats(colds.map(function (x) { return x.mountMs; })).p50,
+        rerenderMs: stats(colds.map(function (x) { return x.rerenderMs; })).p50, elements: amd.elements, reps: reps },
+    };
+  }
+  return out;
 }
 
 const SNAPSHOT_CSS =
@@ -490,6 +600,8 @@ function amdSchedule(request, clock) {
      */
     coldOpenPage: function (page, marks) {
       const mk = marks || {};
+      // What the page's route mounts (src/plugin.js PAGE_NEEDS).
+      const needs = PAGE_NEEDS[page === 'devicePlugins' ? 'device-plugins' : page];
       let shown = !mk.first;
       function check() {
         if (shown) return;
@@ -500,16 +612,14 @@ function amdSchedule(request, clock) {
         mk.first();
       }
       const off = store.subscribe(check);
-      const lists = store.loadLists();
-      const crd = store.refresh();
+      const lists = store.loadLists({ nodes: needs.nodes, pods: needs.pods });
+      const crd = needs.crd ? store.refresh() : Promise.resolve();
       // The page's metrics hook runs from the first render (pages.js
       // telemetryScope) and once more if the node list changes its key.
       const telemetry = page === 'nodes' || page === 'metrics' || page === 'pods' ? pageOpen(page, check) : Promise.resolve();
       const content = Promise.all([lists, crd]).then(function () { if (mk.content) mk.content(); });
-      const needs = page === 'metrics' ? [listed('nodesState'), telemetry]
-        : page === 'devicePlugins' ? [crd, listed('podsState')]
-          : page === 'overview' ? [lists, crd] : [lists, telemetry];
-      const complete = Promise.all(needs).then(function () { if (mk.complete) mk.complete(); });
+      // Everything the page draws: what its route mounts, and its telemetry.
+      const complete = Promise.all([lists, crd, telemetry]).then(function () { if (mk.complete) mk.complete(); });
       return Promise.all([lists, crd, telemetry, content, complete]).then(function () { off(); });
     },
     pageMetrics: pageMetricsOf,
@@ -624,7 +734,11 @@ async function measure(name, factory, base, a) {
  *   {"cmd":"switch","schedule":"amd","n":3}
  *   {"cmd":"quit"}
  */
+/** The serve loop's arguments (compareRenders fetches from the same control plane). */
+let a0 = null;
+
 async function serve(a) {
+  a0 = a;
   // The views format "Last Fetched" with Date#toLocaleTimeString. Its first
   // call in a process builds an Intl formatter: V8 loads the ICU data the
   // Node binary carries, paged in from disk on a fresh host. A browser
@@ -968,6 +1082,9 @@ async function serve(a) {
         for (const k in modes) {
           out.detail[k] = { latencies: modes[k], bytesPerOpen: bytes[k] / Math.max(1, modes[k].length), requestsPerOpen: reqs[k] / Math.max(1, modes[k].length) };
         }
+      } else if (c.cmd === 'refRender') {
+        // The reference's own pages next to this plugin's, on real React (bench/referenceRender.js).
+        out.render = await compareRenders(c);
       } else if (c.cmd === 'switch') {
         const L = get(name);
         if (!L.opened) {

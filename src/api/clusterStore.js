@@ -436,20 +436,25 @@ export function createClusterStore(opts) {
 
   /**
    * Fetch nodes and pods directly (harness / cold start without Headlamp
-   * hooks). Runs in parallel with nothing else; callers usually do
+   * hooks); `which` ({nodes, pods}, default both) says which lists, as a
+   * route's provider mounts only the lists its page draws. Runs in parallel
+   * with nothing else; callers usually do
    * `Promise.all([store.loadLists(), store.refresh()])`.
    */
-  function loadLists() {
-    if (s.podsState === 'unknown') s.podsState = 'pending';
-    if (s.nodesState === 'unknown') s.nodesState = 'pending';
+  function loadLists(which) {
+    const w = which || {};
+    const wantNodes = w.nodes !== false;
+    const wantPods = w.pods !== false;
+    if (wantPods && s.podsState === 'unknown') s.podsState = 'pending';
+    if (wantNodes && s.nodesState === 'unknown') s.nodesState = 'pending';
     // Whole-cluster lists (what Headlamp's useList() delivers in the plugin;
     // loaded here by the terminal client and the harness) take far longer
     // than a CRD request on a large cluster: tens of MB at 1,000 nodes.
-    const nodesP = traced('nodes', '/api/v1/nodes', LIST_TIMEOUT_MS).then(
+    const nodesP = !wantNodes ? null : traced('nodes', '/api/v1/nodes', LIST_TIMEOUT_MS).then(
       function (l) { setNodes(isKubeList(l) ? l.items : [], null); },
       function (e) { setNodes([], e instanceof Error ? e.message : String(e)); }
     );
-    const podsP = traced('pods', '/api/v1/pods', LIST_TIMEOUT_MS).then(
+    const podsP = !wantPods ? null : traced('pods', '/api/v1/pods', LIST_TIMEOUT_MS).then(
       function (l) { setPods(isKubeList(l) ? l.items : [], null); },
       function (e) { setPods([], e instanceof Error ? e.message : String(e)); }
     );

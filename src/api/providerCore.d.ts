@@ -58,7 +58,10 @@ export interface MetricsSource {
 
 export interface ProviderCore {
   Context: Context<AmdGpuContextValue | null>;
-  AmdGpuDataProvider: ComponentType<{ children?: ReactNode }>;
+  /** `needs`: what the page draws — only those lists / requests are mounted (default: all) */
+  AmdGpuDataProvider: ComponentType<{ children?: ReactNode; needs?: { nodes?: boolean; pods?: boolean; crd?: boolean } }>;
+  /** Mounts the pod list + watch into the current cluster's store (a page whose provider does not feed pods) */
+  PodListHere: ComponentType<Record<string, never>>;
   useAmdGpuContext(): AmdGpuContextValue;
   useGpuMetrics(
     enabled?: boolean,

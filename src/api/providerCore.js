@@ -33,6 +33,9 @@ import { POLL_MISS, createPoller, loadSettings as defaultLoadSettings, prometheu
 /** Data younger than this is served from the shared store on mount without re-fetching. */
 export const STALE_MS = 5000;
 
+/** What a provider feeds by default: both lists and the DeviceConfigs (the reference's provider). */
+const ALL_NEEDS = Object.freeze({ nodes: true, pods: true, crd: true });
+
 export const PROMETHEUS_UNREACHABLE =
   'Could not reach Prometheus. Ensure kube-prometheus-stack is installed in the monitoring namespace.';
 
@@ -133,43 +136,83 @@ export function createProviderCore(React, lib, deps) {
     return listResult(res);
   }
 
-  function AmdGpuDataProvider(props) {
-    const store = storeFor(clusterKey());
-
-    // Track 1 — reactive lists from Headlamp (all namespaces for pods).
+  /** Feeds Headlamp's node list + watch into the store (its own component: the hook runs only where mounted). */
+  function NodeListFeed(props) {
+    const store = props.store;
     const nodes = useListOf(lib.K8s.ResourceClasses.Node);
-    const pods = useListOf(lib.K8s.ResourceClasses.Pod, { namespace: '' });
     const allNodes = nodes[0];
     const nodeError = nodes[1];
-    const allPods = pods[0];
-    const podError = pods[1];
-
     useEffect(function () {
       store.setNodes(allNodes === undefined ? null : allNodes, nodeError ? errorText(nodeError) : null);
     }, [store, allNodes, nodeError]);
+    return null;
+  }
+
+  /** Feeds Headlamp's all-namespaces pod list + watch into the store. */
+  function PodListFeed(props) {
+    const store = props.store;
+    const pods = useListOf(lib.K8s.ResourceClasses.Pod, { namespace: '' });
+    const allPods = pods[0];
+    const podError = pods[1];
     useEffect(function () {
       store.setPods(allPods === undefined ? null : allPods, podError ? errorText(podError) : null);
     }, [store, allPods, podError]);
+    return null;
+  }
+
+  /**
+   * The pod list + watch fed into the current cluster's store, mounted by a
+   * page whose provider does not feed pods when one of its views needs them
+   * after all (the Metrics page in an allocation order).
+   */
+  function PodListHere() {
+    return h(PodListFeed, { store: storeFor(clusterKey()) });
+  }
+
+  /**
+   * The cluster context of a page. `props.needs` says what the page draws
+   * ({nodes, pods, crd}, each default true): only those are subscribed to
+   * and fetched — the Metrics page mounts the node list alone, never the
+   * all-namespaces pod list (tens of MB, parsed on the browser's main thread
+   * on a large cluster) nor the DeviceConfig request; the reference mounts
+   * both lists and its CRD + 3 serial requests on every route
+   * (src/index.tsx:87-145, IntelGpuDataContext.tsx:98-165). What one page
+   * fed stays in the shared store for the next. `loading` is the reference's
+   * rule over what this provider feeds.
+   */
+  function AmdGpuDataProvider(props) {
+    const store = storeFor(clusterKey());
+    const needs = props.needs || ALL_NEEDS;
+    const wantNodes = needs.nodes !== false;
+    const wantPods = needs.pods !== false;
+    const wantCrd = needs.crd !== false;
 
     // Track 2 — imperative CRD / operator-pod fetch, shared and deduplicated.
     useEffect(function () {
-      store.revalidate(STALE_MS);
-    }, [store]);
+      if (wantCrd) store.revalidate(STALE_MS);
+    }, [store, wantCrd]);
 
     // Optional auto-refresh (settings; the reference only refreshes on click).
     const refreshIntervalSec = loadSettings().refreshIntervalSec;
     useEffect(function () {
+      if (!wantCrd) return undefined;
       const poller = createPoller(refreshIntervalSec);
       poller.start(function () { return store.revalidate(STALE_MS); });
       return function () { poller.stop(); };
-    }, [store, refreshIntervalSec]);
+    }, [store, refreshIntervalSec, wantCrd]);
 
     const snapshot = React.useSyncExternalStore(store.subscribe, store.getSnapshot);
     const value = useMemo(function () {
-      return Object.assign({}, snapshot, { refresh: function () { store.refresh(); } });
-    }, [snapshot, store]);
+      const loading = (wantCrd && snapshot.crdLoading) || (wantNodes && snapshot.nodesLoading) || (wantPods && snapshot.podsLoading);
+      return Object.assign({}, snapshot, { loading: !!loading, refresh: function () { store.refresh(); } });
+    }, [snapshot, store, wantCrd, wantNodes, wantPods]);
 
-    return h(Context.Provider, { value: value }, props.children);
+    // Track 1 — reactive lists from Headlamp (all namespaces for pods), as
+    // feed components next to the page, so a page mounts only the watches it draws.
+    return h(Context.Provider, { value: value },
+      wantNodes ? h(NodeListFeed, { store: store }) : null,
+      wantPods ? h(PodListFeed, { store: store }) : null,
+      props.children);
   }
 
   const IDLE = { metrics: null, series: null, fetchError: null, fetching: false };
@@ -441,6 +484,7 @@ export function createProviderCore(React, lib, deps) {
   return {
     Context: Context,
     AmdGpuDataProvider: AmdGpuDataProvider,
+    PodListHere: PodListHere,
     useAmdGpuContext: useAmdGpuContext,
     useGpuMetrics: useGpuMetrics,
     useNodeGpuMetrics: useNodeGpuMetrics,

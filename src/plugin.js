@@ -30,7 +30,9 @@ import {
   overviewView,
   podDetailView,
   podsView,
+  nodeSortOf,
   ownersScope,
+  RANKED_NODE_SORTS,
   telemetryScope,
 } from './view/pages.js';
 import { createRenderer } from './view/react.js';
@@ -40,6 +42,22 @@ import { processColumns, ROUTES, SIDEBAR } from './routes.js';
 
 /** Plugin name used for `registerPluginSettings`. */
 export const PLUGIN_NAME = 'amd-gpu';
+
+/**
+ * What each page draws, hence what its route mounts (providerCore.js
+ * AmdGpuDataProvider): Metrics needs the node list only (names of the page,
+ * nodes reporting); GPU Nodes and GPU Pods need both lists but not the
+ * DeviceConfigs; Device Plugins the DeviceConfigs and the pods (operator
+ * pods), not the node list; Overview everything. The reference mounts all of
+ * it on every route (src/index.tsx:87-145).
+ */
+export const PAGE_NEEDS = Object.freeze({
+  overview: Object.freeze({ nodes: true, pods: true, crd: true }),
+  'device-plugins': Object.freeze({ nodes: false, pods: true, crd: true }),
+  nodes: Object.freeze({ nodes: true, pods: true, crd: false }),
+  pods: Object.freeze({ nodes: true, pods: true, crd: false }),
+  metrics: Object.freeze({ nodes: true, pods: false, crd: false }),
+});
 
 /**
  * @param {{React: any, lib: any, CommonComponents: Record<string, Function>,
@@ -148,10 +166,14 @@ export function createPlugin(env) {
     const pager = usePager('metrics');
     const t = telemetryScope(ctx, pager.state, true);
     const m = core.useGpuMetrics(t.enabled, true, 'gauges', t.scope, t.small, t.rank);
-    return h(Page, {
+    // The route feeds the node list only (PAGE_NEEDS); the allocation orders
+    // rank nodes by the GPUs pods hold, so they mount the pod list too.
+    const sort = nodeSortOf(pager.state, RANKED_NODE_SORTS);
+    const needPods = sort === 'in-use' || sort === 'free';
+    return h(React.Fragment, null, needPods ? h(core.PodListHere, null) : null, h(Page, {
       vm: metricsView(ctx, m, { pager: pager.state }), onRefresh: m.refresh,
       onPage: pager.onPage, onFilter: pager.onFilter, onSort: pager.onSort,
-    });
+    }));
   }
 
   // -------------------------------------------------------------------------
@@ -233,12 +255,13 @@ export function createPlugin(env) {
     metrics: MetricsPage,
   };
 
-  /** Route component: the page under the (shared-store) provider. */
+  /** Route component: the page under the (shared-store) provider, mounting what the page draws. */
   function routeComponent(page) {
     const P = pages[page];
     if (!P) throw new Error('createPlugin: unknown page ' + page);
+    const needs = PAGE_NEEDS[page];
     function Route() {
-      return h(core.AmdGpuDataProvider, null, h(P, null));
+      return h(core.AmdGpuDataProvider, { needs: needs }, h(P, null));
     }
     Route.displayName = 'AmdGpuRoute(' + page + ')';
     return Route;

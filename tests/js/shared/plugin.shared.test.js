@@ -216,12 +216,49 @@ describe('shared: refresh and StrictMode (' + tier + ')', () => {
   });
 
   it('under StrictMode a route mounts with one CRD request and one live query', async () => {
-    const fake = cluster();
-    const r = render(h(route('/amd-gpu/metrics')), { strict: true });
+    let fake = cluster();
+    let r = render(h(route('/amd-gpu')), { strict: true });
     await r.settle();
     expect(crdCalls()).toBe(1);
+    r.unmount();
+    lib.resetHeadlamp();
+    resetSharedStores();
+    fake = cluster();
+    r = render(h(route('/amd-gpu/metrics')), { strict: true });
+    await r.settle();
     expect(promQueries(fake)).toHaveLength(1);
     expect(r.text()).toContain('GPU Power Summary');
+    r.unmount();
+  });
+
+  it('each route mounts only what its page draws: Metrics the node list alone, no pod list, no DeviceConfig request', async () => {
+    const expected = {
+      '/amd-gpu': [true, true, 1], '/amd-gpu/device-plugins': [false, true, 1], '/amd-gpu/nodes': [true, true, 0],
+      '/amd-gpu/pods': [true, true, 0], '/amd-gpu/metrics': [true, false, 0],
+    };
+    for (const path of Object.keys(expected)) {
+      lib.resetHeadlamp();
+      resetSharedStores();
+      cluster();
+      const r = render(h(route(path)));
+      await r.settle();
+      const [nodes, pods, crd] = expected[path];
+      expect([path, lib.lists.calls.Node.length > 0, lib.lists.calls.Pod.length > 0, crdCalls()]).toEqual([path, nodes, pods, crd]);
+      r.unmount();
+    }
+  });
+
+  it('Metrics in an allocation order mounts the pod list too, and ranks by the GPUs held', async () => {
+    cluster({ gpuNodes: nodeNames(12) }); // train-a (4 GPUs) on mi355x-000, train-b (2) on mi355x-001
+    lib.lists.Pod = [[makeGpuPod('hog', { gpus: 8, node: 'mi355x-010' })].concat(lib.lists.Pod[0]), null];
+    const r = render(h(route('/amd-gpu/metrics')));
+    await r.settle();
+    expect(lib.lists.calls.Pod).toHaveLength(0);
+    r.change(r.byLabel('Sort GPU nodes'), 'in-use');
+    await r.settle();
+    expect(lib.lists.calls.Pod.length).toBeGreaterThan(0);
+    const titles = r.byTag('h2').map((n) => r.textOf(n)).filter((t) => /^mi355x-/.test(t));
+    expect(titles[0]).toBe('mi355x-010 — 8 × MI355X');
     r.unmount();
   });
 });

@@ -52,9 +52,16 @@ def _check(line, n):
     for k in ("overview", "devicePlugins", "nodes", "pods"):
         assert cold[k]["requests"]["reference"] == 6
     assert cold["metrics"]["requests"]["reference"] == 6 + 5
-    assert cold["overview"]["requests"]["amd"] == 3 and cold["nodes"]["requests"]["amd"] == 4
+    # Each route mounts what its page draws (src/plugin.js PAGE_NEEDS): Overview both lists + the DeviceConfigs;
+    # GPU Nodes both lists + its telemetry query, no DeviceConfig request; Metrics the node list + its queries,
+    # never the all-namespaces pod list.
+    assert cold["overview"]["requests"]["amd"] == 3 and cold["nodes"]["requests"]["amd"] == 3
+    assert set(cold["metrics"]["amd_requests_by_kind"]) == {"nodes", "query", "query_range"}, cold["metrics"]
+    assert set(cold["devicePlugins"]["amd_requests_by_kind"]) == {"pods", "crd"}, cold["devicePlugins"]
     for v in cold.values():
         assert v["amd"] < v["reference"], cold
+        # progressive pages: the first render with content comes no later than the page complete
+        assert v["amd_first_content"] <= v["amd"] + 1e-6, cold
     # Every page mounted through the shipped renderer on the harness React and,
     # where this image vendors them, on real React 18.3.1 production builds:
     # the same IR mounts the same host elements on both.

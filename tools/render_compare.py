@@ -1,0 +1,97 @@
+#!/usr/bin/env python3
+"""The reference's own pages vs this plugin's, rendered on real React 18.3.1 at 1 to 1,000 GPU nodes.
+
+    python tools/render_compare.py [--sizes 1,2,4,8,16,64,256,1000] [--reps 5] [--out profiles/r4_render_compare]
+
+Per size: the fake control plane (no injected latency: this measures render, not requests) serves a synthetic
+cluster; bench/driver.js ``refRender`` mounts each of the five reference pages — read unmodified from
+``--reference`` (default /root/reference) and transpiled at run time by bench/tsx.js — and each of this plugin's,
+on the react@18.3.1 / react-dom@18.3.1 production UMD builds (bench/referenceRender.js has the data mapping).
+Writes ``<out>.json`` and ``<out>.md``.
+
+The reference's sources are not in this repository and not on the GPU box, so this runs where they are (this
+container's CPU); the figures of both plugins come from the same process on the same host.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+PAGES = [("overview", "Overview"), ("devicePlugins", "Device Plugins"), ("nodes", "GPU Nodes"), ("pods", "GPU Pods"),
+         ("metrics", "Metrics")]
+
+
+def measure(n: int, reference: str, reps: int) -> dict:
+    from headlamp_intel_gpu_plugin_amd.sim.serve import ControlPlaneProcess
+    from headlamp_intel_gpu_plugin_amd.utils.nodebridge import Driver
+    from headlamp_intel_gpu_plugin_amd.utils.reactumd import PROD_BUILDS, umd_dir
+
+    umd = umd_dir(PROD_BUILDS)
+    if not umd:
+        raise SystemExit("the React 18.3.1 production UMD builds are not available in this image")
+    with ControlPlaneProcess(n, source="both", latency_ms=0.0) as srv:
+        drv = Driver(srv.url)
+        try:
+            r = drv.call("refRender", referenceDir=reference, umdDir=umd, reps=reps, timeout=3000)
+        finally:
+            drv.close()
+    if r.get("error"):
+        raise RuntimeError(r["error"])
+    return r["render"]
+
+
+def table(rows) -> list:
+    head = ["GPU nodes", "GPU pods"] + [f"{t}: reference → new elements, mount ms, re-render ms" for _, t in PAGES] + [
+        "Reference provider filter per watch event (ms)"]
+    md = ["| " + " | ".join(head) + " |", "|---:|---:|" + "---|" * (len(head) - 2)]
+    for n, r in rows:
+        cells = [str(n), str(r["gpuPods"])]
+        for k, _ in PAGES:
+            a, ref = r["pages"][k]["amd"], r["pages"][k]["reference"]
+            cells.append(f"{ref['elements']} → {a['elements']}; {ref['mountMs']:.1f} → {a['mountMs']:.1f}; "
+                         f"{ref['rerenderMs']:.1f} → {a['rerenderMs']:.2f}")
+        cells.append(f"{r['referenceProviderFilterMs']:.1f}")
+        md.append("| " + " | ".join(cells) + " |")
+    return md
+
+
+def main() -> int:
+    p = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    p.add_argument("--sizes", default="1,2,4,8,16,64,256,1000")
+    p.add_argument("--reps", type=int, default=5)
+    p.add_argument("--reference", default="/root/reference")
+    p.add_argument("--out", default=os.path.join(ROOT, "profiles", "r4_render_compare"))
+    args = p.parse_args()
+    if not os.path.isdir(os.path.join(args.reference, "src", "components")):
+        raise SystemExit(f"no reference sources under {args.reference}")
+    rows = []
+    for s in args.sizes.split(","):
+        n = int(s)
+        t = time.time()
+        r = measure(n, args.reference, args.reps if n <= 256 else max(3, args.reps // 2))
+        rows.append((n, r))
+        print(f"[render_compare] {n} nodes: {time.time() - t:.1f} s", file=sys.stderr, flush=True)
+        with open(args.out + ".json", "w") as f:
+            json.dump({"host": os.uname().nodename, "node": "v12", "rows": [{"gpu_nodes": n, **r} for n, r in rows]}, f,
+                      indent=1)
+    md = ["Each page mounted on react@18.3.1 + react-dom@18.3.1 production UMD builds into a minimal JS DOM, "
+          "median of the reps. Reference = its page component (read from its sources, transpiled at run time) with "
+          "its data in context, its per-render aggregation included; re-render = a watch event (a new context "
+          "value). New = this plugin's page, mount including the view-model built from a cold memo; re-render = "
+          "the same watch event (a new store snapshot of the same data). First page of each pager. The last column "
+          "is the reference provider's re-filtering of both whole lists on every watch event "
+          "(IntelGpuDataContext.tsx:200-208), on top of the page's re-render.", ""] + table(rows)
+    with open(args.out + ".md", "w") as f:
+        f.write("\n".join(md) + "\n")
+    print("\n".join(md))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
