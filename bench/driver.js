@@ -326,10 +326,20 @@ async function mountCycle(R, make, waitText, beforeRerender, reps, mustShow) {
     const root = R.ReactDOM.createRoot(c);
     const t0 = process.hrtime();
     R.ReactDOM.flushSync(function () { root.render(make()); });
-    for (let k = 0; waitText && k < 1000 && c.textContent.indexOf(waitText) < 0; k++) {
-      await new Promise(function (r) { setImmediate(r); });
+    const errors = [];
+    const consoleError = console.error;
+    console.error = function () { errors.push(Array.prototype.join.call(arguments, ' ').slice(0, 500)); };
+    try {
+      const until = Date.now() + 60000;
+      while (waitText && c.textContent.indexOf(waitText) < 0 && Date.now() < until && !errors.length) {
+        await new Promise(function (r) { setImmediate(r); });
+      }
+    } finally {
+      console.error = consoleError;
     }
-    if (waitText && c.textContent.indexOf(waitText) < 0) throw new Error('mountCycle: "' + waitText + '" never rendered');
+    if (waitText && c.textContent.indexOf(waitText) < 0) {
+      throw new Error('mountCycle: "' + waitText + '" never rendered' + (errors.length ? ': ' + errors.join(' | ') : ''));
+    }
     mounts.push(ms(process.hrtime(t0)));
     if (mustShow && c.textContent.indexOf(mustShow) < 0) throw new Error('mountCycle: the page does not show "' + mustShow + '"');
     if (beforeRerender) beforeRerender();

@@ -727,7 +727,7 @@ export const HELPERS = 'function __oc(o, f) { return o === null || o === undefin
 /** `import` / `export` statements → `__import(spec)` / `__exports`. */
 export function lowerModules(src) {
   const exportsTail = [];
-  let s = src.replace(/^import\s+([\s\S]*?)\s+from\s+'([^']+)';?/gm, function (m, clause, spec) {
+  let s = src.replace(/^[ \t]*import\s+([\s\S]*?)\s+from\s+'([^']+)';?/gm, function (m, clause, spec) {
     const out = [];
     let c = clause.trim();
     const def = /^([A-Za-z_$][\w$]*)\s*(?:,\s*([\s\S]*))?$/.exec(c);
@@ -746,21 +746,21 @@ export function lowerModules(src) {
     }
     return out.join(' ');
   });
-  s = s.replace(/^import\s+'([^']+)';?/gm, function (m, spec) { return '__import(' + JSON.stringify(spec) + ');'; });
-  s = s.replace(/^export\s+default\s+function\s+([A-Za-z_$][\w$]*)/gm, function (m, name) {
+  s = s.replace(/^[ \t]*import\s+'([^']+)';?/gm, function (m, spec) { return '__import(' + JSON.stringify(spec) + ');'; });
+  s = s.replace(/^[ \t]*export\s+default\s+function\s+([A-Za-z_$][\w$]*)/gm, function (m, name) {
     exportsTail.push('__exports.default = ' + name + ';');
     return 'function ' + name;
   });
-  s = s.replace(/^export\s+(async\s+)?function\s+([A-Za-z_$][\w$]*)/gm, function (m, as, name) {
+  s = s.replace(/^[ \t]*export\s+(async\s+)?function\s+([A-Za-z_$][\w$]*)/gm, function (m, as, name) {
     exportsTail.push('__exports.' + name + ' = ' + name + ';');
     return (as || '') + 'function ' + name;
   });
-  s = s.replace(/^export\s+(const|let|var)\s+([A-Za-z_$][\w$]*)/gm, function (m, kw, name) {
+  s = s.replace(/^[ \t]*export\s+(const|let|var)\s+([A-Za-z_$][\w$]*)/gm, function (m, kw, name) {
     exportsTail.push('__exports.' + name + ' = ' + name + ';');
     return kw + ' ' + name;
   });
-  s = s.replace(/^export\s+default\s+/gm, '__exports.default = ');
-  const left = /^(import|export)\b.*$/m.exec(s);
+  s = s.replace(/^[ \t]*export\s+default\s+/gm, '__exports.default = ');
+  const left = /^[ \t]*(import|export)\b.*$/m.exec(s);
   if (left) throw new Error('tsx: unsupported module statement: ' + left[0]);
   return s + '\n' + exportsTail.join('\n') + '\n';
 }

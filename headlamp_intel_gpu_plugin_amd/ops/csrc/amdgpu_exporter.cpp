@@ -240,7 +240,7 @@ int main(int argc, char** argv) {
   } else if (!amdprobe::init_hip()) {
     // No device is not fatal: the exporter still answers (with no GPU series),
     // which is what the plugin's "No AMD GPU Metrics" state expects.
-    std::fprintf(stderr, "amdgpu-exporter: %s\n", amdprobe::g_error.c_str());
+    std::fprintf(stderr, "amdgpu-exporter: %s\n", amdprobe::last_error().c_str());
   }
   if (a.once) {
     std::fputs(amdprobe::render(a.render).c_str(), stdout);

@@ -37,7 +37,8 @@ using namespace amdprobe;
 // ---------------------------------------------------------------------------
 
 PyObject* raise_hip() {
-  PyErr_SetString(PyExc_RuntimeError, g_error.empty() ? "HIP unavailable" : g_error.c_str());
+  const std::string e = last_error();  // a copy: another thread may set a new one meanwhile
+  PyErr_SetString(PyExc_RuntimeError, e.empty() ? "HIP unavailable" : e.c_str());
   return nullptr;
 }
 
@@ -181,7 +182,7 @@ PyObject* py_render(PyObject*, PyObject* args) {
   return PyUnicode_FromStringAndSize(s.data(), static_cast<Py_ssize_t>(s.size()));
 }
 
-PyObject* py_last_error(PyObject*, PyObject*) { return PyUnicode_FromString(g_error.c_str()); }
+PyObject* py_last_error(PyObject*, PyObject*) { return PyUnicode_FromString(last_error().c_str()); }
 
 // RAS counters of a ras/ directory (no HIP needed: tests point it at a fixture tree).
 PyObject* py_read_ras(PyObject*, PyObject* args) {

@@ -18,6 +18,7 @@
 #include <cstring>
 #include <fstream>
 #include <sstream>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -70,7 +71,22 @@ struct Sample {
 
 inline bool g_hip_ok = false;
 inline int g_count = 0;
+
+// The last HIP error, written by whichever thread failed (device_info runs
+// with the GIL released, in the exporter's request threads too) and read by
+// another: every access goes through this mutex.
+inline std::mutex g_error_mu;
 inline std::string g_error;
+
+inline void set_error(const std::string& e) {
+  std::lock_guard<std::mutex> lk(g_error_mu);
+  g_error = e;
+}
+
+inline std::string last_error() {
+  std::lock_guard<std::mutex> lk(g_error_mu);
+  return g_error;
+}
 
 // Root of the sysfs tree (tests point it at a captured copy:
 // AMDGPU_EXPORTER_SYSFS_ROOT=/tmp/tree reads /tmp/tree/sys/...).
@@ -192,7 +208,7 @@ inline bool init_hip() {
   if (g_hip_ok) return true;
   hipError_t err = hipGetDeviceCount(&g_count);
   if (err != hipSuccess) {
-    g_error = std::string("hipGetDeviceCount: ") + hipGetErrorString(err);
+    set_error(std::string("hipGetDeviceCount: ") + hipGetErrorString(err));
     g_count = 0;
     return false;
   }
@@ -204,7 +220,7 @@ inline bool device_info(int dev, DeviceInfo* out) {
   hipDeviceProp_t p;
   hipError_t err = hipGetDeviceProperties(&p, dev);
   if (err != hipSuccess) {
-    g_error = std::string("hipGetDeviceProperties: ") + hipGetErrorString(err);
+    set_error(std::string("hipGetDeviceProperties: ") + hipGetErrorString(err));
     return false;
   }
   out->index = dev;

@@ -1,0 +1,138 @@
+/**
+ * bench/tsx.js — the benchmark's TSX → JavaScript transformer (it mounts the
+ * reference's own pages for the rows-rendered comparison,
+ * bench/referenceRender.js). Its transforms on small inputs, and, where the
+ * reference's sources are present (/root/reference), the reference's own
+ * unit tests of src/api/k8s.ts run through it against the transpiled module:
+ * the transpiler is right where the reference's tests say so.
+ */
+import fs from 'fs';
+import { loadModules, lowerModules, lowerOptional, stripTypes, transformJsx, transpile } from '../../bench/tsx.js';
+
+function run(src, imports) {
+  const exp = {};
+  new Function('__import', '__exports', transpile(src))(function (spec) { return imports[spec]; }, exp); // eslint-disable-line no-new-func
+  return exp;
+}
+
+const React = {
+  Fragment: 'F',
+  createElement: function (type, props) {
+    return { type: type, props: props, children: Array.prototype.slice.call(arguments, 2) };
+  },
+};
+
+describe('tsx: JSX → React.createElement', () => {
+  it('elements, attributes, spread, fragments, expression containers and JSX text', () => {
+    const m = run(`
+      import React from 'react';
+      export function view(p: { n: number; rest: Record<string, string> }) {
+        return (
+          <>
+            <div className="a" aria-label="x y" data-n={p.n} {...p.rest} hidden>
+              Hello &amp; welcome{' '}
+              <b>{p.n > 1 ? 'many' : 'one'}</b>
+              {/* a comment */}
+            </div>
+            <Child value={<i>nested</i>} />
+          </>
+        );
+      }
+      function Child() { return null; }
+    `, { react: React });
+    const el = m.view({ n: 2, rest: { id: 'r' } });
+    expect(el.type).toBe('F');
+    const div = el.children[0];
+    expect(div.type).toBe('div');
+    expect(div.props).toEqual({ className: 'a', 'aria-label': 'x y', 'data-n': 2, id: 'r', hidden: true });
+    expect(div.children[0]).toBe('Hello & welcome');
+    expect(div.children[1]).toBe(' ');
+    expect(div.children[2]).toEqual({ type: 'b', props: null, children: ['many'] });
+    expect(div.children).toHaveLength(3);
+    expect(el.children[1].props.value.type).toBe('i');
+  });
+
+  it('a < b is a comparison, Map<K, V>() a generic call, not JSX', () => {
+    const src = 'const a = 1 < 2;\nconst m = new Map<string, string[]>();\nconst s = useState<Foo | null>(null);';
+    const out = stripTypes(transformJsx(src));
+    expect(out).toContain('1 < 2');
+    expect(out).toContain('new Map()');
+    expect(out).toContain('useState(null)');
+  });
+});
+
+describe('tsx: TypeScript erasure', () => {
+  it('interfaces, type aliases, annotations, casts, type predicates, catch bindings, non-null', () => {
+    const src = `
+      export interface A { x: number; y?: string; z: Array<{ k: string }> }
+      export type T = 'a' | 'b';
+      export function f(value: unknown, n: number = 2, o?: A): value is A {
+        const r: Record<string, number> = { a: 1 };
+        const v = (value as Record<string, unknown>)['x'] as number | undefined;
+        try { throw new Error('e'); } catch (e: unknown) { r.c = 3; }
+        const g = (q: string): number => q.length;
+        return r.a + (v || 0) + g('ab') + new Map<string, number>([['k', n]]).get('k')!;
+      }
+      export const K = 'x' as const;
+    `;
+    const m = run(src, {});
+    expect(m.f({ x: 1 })).toBe(6);
+    expect(m.K).toBe('x');
+    expect(stripTypes(src)).not.toContain('interface');
+  });
+});
+
+describe('tsx: optional chaining and nullish coalescing → ES2019', () => {
+  it('chains, calls, index access, spread and nesting keep their semantics', () => {
+    const m = run(`
+      export function t(o: any) {
+        return [o?.a?.b ?? 'd', o?.list?.length ?? 0, o?.['k'], o?.f?.(2), { ...o?.s }, (o?.n ?? 1) + 1, o?.m.get('x') ?? 'none'];
+      }
+    `, {});
+    expect(m.t(null)).toEqual(['d', 0, undefined, undefined, {}, 2, 'none']);
+    expect(m.t({ a: { b: 0 }, list: [1, 2], k: 'v', f: (x) => x * 2, s: { z: 1 }, n: 0, m: new Map([['x', 'y']]) }))
+      .toEqual([0, 2, 'v', 4, { z: 1 }, 1, 'y']);
+  });
+
+  it('the left side is evaluated once', () => {
+    let calls = 0;
+    const m = run('export function t(f: () => any) { return f()?.x ?? f(); }', {});
+    expect(m.t(() => { calls++; return { x: 7 }; })).toBe(7);
+    expect(calls).toBe(1);
+  });
+
+  it('template literal expressions are lowered too', () => {
+    expect(lowerOptional('const s = `${a?.b ?? "x"}!`;')).not.toContain('?.');
+  });
+});
+
+describe('tsx: modules', () => {
+  it('imports (default, named, renamed, type-only) and exports', () => {
+    const out = lowerModules("import A, { b, type C, d as e } from 'm';\nexport default function F() {}\nexport const K = 1;");
+    expect(out).toContain("const A = __import(\"m\", true);");
+    expect(out).toContain('const { b, C, d: e } = __import("m");');
+    expect(out).toContain('__exports.default = F;');
+    expect(out).toContain('__exports.K = K;');
+  });
+
+  it('loadModules links a graph with external stand-ins', () => {
+    const exp = loadModules({
+      'a.ts': "import { two } from './b';\nimport X from 'ext';\nexport const three = two + X;",
+      'b.ts': 'export const two: number = 2;',
+    }, 'a.ts', (from, spec) => (spec === 'ext' ? { default: 1 } : spec.replace('./', '') + '.ts'));
+    expect(exp.three).toBe(3);
+  });
+});
+
+// The reference's own unit tests of its domain model (48 cases), run against
+// its k8s.ts as transpiled here — when its sources are in this container.
+const REF = '/root/reference/src/api/';
+const haveReference = fs.existsSync(REF + 'k8s.ts') && fs.existsSync(REF + 'k8s.test.ts');
+if (haveReference) {
+  const files = { 'k8s.ts': fs.readFileSync(REF + 'k8s.ts', 'utf8'), 'k8s.test.ts': fs.readFileSync(REF + 'k8s.test.ts', 'utf8') };
+  loadModules(files, 'k8s.test.ts', function (from, spec) {
+    if (spec === 'vitest') return { describe: describe, it: it, expect: expect, vi: vi, beforeEach: beforeEach };
+    if (spec === './k8s') return 'k8s.ts';
+    throw new Error('unexpected import ' + spec);
+  });
+}
