@@ -373,10 +373,14 @@ async function compareRenders(c) {
   const R = await realReact(c.umdDir);
   const ref = loadReferencePages(c.referenceDir, R.React, R.CC);
   const reps = c.reps || 5;
-  const s = amdSchedule(makeRequest(a0.url, { n: 0, bytes: 0 }));
+  // (no 2 s request limit: the fake Prometheus evaluates 8,000 GPUs in Python on this host)
+  const s = amdSchedule(makeRequest(a0.url, { n: 0, bytes: 0 }), null, 600000);
   await s.coldOpen();
-  await s.fetchAll();
   const request = makeRequest(a0.url, { n: 0, bytes: 0 });
+  // Every GPU's gauges for the reference's one-card-per-chip Metrics page (the
+  // fake Prometheus needs seconds for 8,000 GPUs: no 2 s request timeout here).
+  const every = await createMetricsSource({ request: request, timeoutMs: 600000 }).fetchGpuMetrics('gauges');
+  if (!every) throw new Error('compareRenders: no telemetry');
   const lists = await Promise.all([request('/api/v1/nodes'), request('/api/v1/pods')]);
   const snap = s.ctx();
   const t0 = process.hrtime();
@@ -391,7 +395,7 @@ async function compareRenders(c) {
   ref.k8s.filterIntelGpuNodes(intelNodes);
   ref.k8s.filterGpuRequestingPods(intelPods);
   const filterMs = ms(process.hrtime(d0));
-  const refMetrics = toGpuMetrics(s.mstate().metrics);
+  const refMetrics = toGpuMetrics(every);
   const out = { pages: {}, referenceProviderFilterMs: filterMs, referenceContextBuildMs: deriveMs,
     gpuNodes: refCtx.gpuNodes.length, gpuPods: refCtx.gpuPods.length, chips: refMetrics.chips.length };
   for (let p = 0; p < PAGES.length; p++) {
@@ -472,15 +476,15 @@ function writeSnapshots(ctx, mstate, dir, now, history) {
 // Schedules
 // ---------------------------------------------------------------------------
 
-function amdSchedule(request, clock) {
+function amdSchedule(request, clock, timeoutMs) {
   // Request spans from the data layer's tracing hook (clusterStore/metrics onTrace).
   const spans = [];
   function onTrace(span) {
     spans.push(span);
   }
   const clk = clock || hiResClock;
-  const store = createClusterStore({ request: request, onTrace: onTrace, clock: clk });
-  const metrics = createMetricsSource({ request: request, onTrace: onTrace, clock: clk });
+  const store = createClusterStore({ request: request, onTrace: onTrace, clock: clk, timeoutMs: timeoutMs });
+  const metrics = createMetricsSource({ request: request, onTrace: onTrace, clock: clk, timeoutMs: timeoutMs });
   const mstate = { metrics: null, fetchError: null, fetching: false, series: null };
   // Per-page metrics state, as each page's own hook holds it (plugin.js):
   // GPU Nodes → owners + xGMI links of the nodes on its first page

@@ -119,6 +119,19 @@ export function createPlugin(env) {
   }
 
   /**
+   * A power-ranked answer past the last page (the ranked count shrank while
+   * the user was on a later page): move to the last page, which asks again.
+   */
+  function useRankedPageClamp(metrics, pager) {
+    const r = metrics && metrics.rank;
+    const last = r && r.per > 0 ? Math.max(0, Math.ceil(r.count / r.per) - 1) : 0;
+    const beyond = !!r && r.page > last && r.page === pager.state.page;
+    React.useEffect(function () {
+      if (beyond) pager.onPage(last);
+    }, [beyond, last]);
+  }
+
+  /**
    * MI355X nodes: summary table, per-node cards with the per-GPU allocation
    * strip and the xGMI matrix (reference NodesPage.tsx, C7), one page of
    * nodes at a time. Exporter telemetry of the nodes on the page (no time
@@ -130,6 +143,7 @@ export function createPlugin(env) {
     const pager = usePager('nodes');
     const t = telemetryScope(ctx, pager.state, true);
     const m = core.useGpuMetrics(t.enabled, false, 'topology', t.scope, t.small, t.rank);
+    useRankedPageClamp(m.metrics, pager);
     // The node and pod lists are live watches; what Refresh can renew here is
     // the telemetry (the DeviceConfigs are not on this page).
     return h(Page, {
@@ -149,6 +163,7 @@ export function createPlugin(env) {
     const pager = usePager('pods');
     const o = ownersScope(ctx, pager.state);
     const m = core.useGpuOwners(o.enabled, o.pods, o.small, o.rank);
+    useRankedPageClamp(m.metrics, pager);
     // As on GPU Nodes: the lists are watches; Refresh renews the attribution.
     return h(Page, {
       vm: podsView(ctx, { metrics: m.metrics, pager: pager.state, fetching: m.fetching }), onRefresh: m.refresh,
@@ -166,6 +181,7 @@ export function createPlugin(env) {
     const pager = usePager('metrics');
     const t = telemetryScope(ctx, pager.state, true);
     const m = core.useGpuMetrics(t.enabled, true, 'gauges', t.scope, t.small, t.rank);
+    useRankedPageClamp(m.metrics, pager);
     // The route feeds the node list only (PAGE_NEEDS); the allocation orders
     // rank nodes by the GPUs pods hold, so they mount the pod list too.
     const sort = nodeSortOf(pager.state, RANKED_NODE_SORTS);

@@ -69,6 +69,7 @@ export function pager(p, noun, sorting) {
     t: 'pager', key: 'pager', noun: noun, label: (sorting && sorting.label) || noun, page: p.page, pages: p.pages, from: p.from, to: p.to,
     total: p.total, matched: p.matched, filter: p.filter, perPage: p.perPage,
   };
+  if (p.beyond) item.beyond = true;
   // Offered orders ({value, label}[]) and the current one, when the list can be ranked.
   if (sorting && sorting.sorts) {
     item.sort = sorting.sort;
@@ -82,6 +83,8 @@ export function pagerText(p) {
   const f = p.filter ? p.filter.trim() : '';
   const of = f ? p.matched + ' matching "' + f + '" (' + p.total + ' ' + p.noun + ')' : p.total + ' ' + p.noun;
   if (p.matched === 0) return 'No ' + p.noun + (f ? ' match "' + f + '"' : '');
+  // A ranked page past the end (the count shrank): the component moves to the last page.
+  if (p.beyond) return 'Moving to page ' + p.pages + ' of ' + p.pages + ' (' + of + ')';
   return 'Showing ' + (p.from + 1) + '–' + p.to + ' of ' + of + (p.pages > 1 ? ' · page ' + (p.page + 1) + ' of ' + p.pages : '');
 }
 

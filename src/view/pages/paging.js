@@ -198,12 +198,25 @@ function listPage(kind, all0, state, keyOf, textOf, perDefault) {
 /** The pager page of a power-ranked answer: its nodes, in rank order, out of the nodes ranked. */
 export function rankedPage(m, state) {
   return memo('metrics-ranked-page', [m], function () {
-    const r = m.rank;
-    const count = Math.max(r.count, r.page * r.per + m.scope.length);
-    const from = Math.min(r.page * r.per, count);
-    return {
-      nodes: m.scope, names: m.scope, page: r.page, pages: Math.max(1, Math.ceil(count / r.per)), from: from,
-      to: from + m.scope.length, total: count, matched: count, filter: (state && state.filter) || '', perPage: r.per,
-    };
+    return Object.assign(rankedSlice(m.rank, m.scope.length, state), { nodes: m.scope, names: m.scope });
   });
+}
+
+/**
+ * Pager fields of a ranked answer holding `shown` items of page `r.page`
+ * (`r.count` ranked in all). An answer past the last page (the ranked count
+ * shrank while the user was on a later page) is flagged `beyond`, with the
+ * last page's numbers; the page component then moves to the last page
+ * (plugin.js useRankedPageClamp).
+ */
+export function rankedSlice(r, shown, state) {
+  const count = shown ? Math.max(r.count, r.page * r.per + shown) : r.count;
+  const pages = Math.max(1, Math.ceil(count / r.per));
+  const beyond = !shown && r.page > pages - 1;
+  const page = beyond ? pages - 1 : r.page;
+  const from = Math.min(page * r.per, count);
+  return {
+    page: page, pages: pages, from: from, to: beyond ? from : from + shown, total: count, matched: count,
+    filter: (state && state.filter) || '', perPage: r.per, beyond: beyond,
+  };
 }

@@ -38,7 +38,7 @@ import {
   nodesPending,
   podsPending,
 } from './common.js';
-import { podKeyOf, podPage, PODS_PER_PAGE, podSortOf, RANKED_POD_SORTS } from './paging.js';
+import { podKeyOf, podPage, PODS_PER_PAGE, podSortOf, RANKED_POD_SORTS, rankedSlice } from './paging.js';
 
 /** The rank of a power-ordered owners answer as a pager page: its pods, in rank order, out of the pods ranked. */
 function rankedPodPage(ctx, m, state) {
@@ -51,12 +51,7 @@ function rankedPodPage(ctx, m, state) {
     const r = m.rank;
     const pods = [];
     for (let i = 0; i < r.order.length; i++) if (byKey.has(r.order[i])) pods.push(byKey.get(r.order[i]));
-    const count = Math.max(r.count, r.page * r.per + pods.length);
-    const from = Math.min(r.page * r.per, count);
-    return {
-      nodes: pods, names: pods.map(podKeyOf), page: r.page, pages: Math.max(1, Math.ceil(count / r.per)), from: from,
-      to: from + pods.length, total: count, matched: count, filter: (state && state.filter) || '', perPage: r.per, ranked: true,
-    };
+    return Object.assign(rankedSlice(r, pods.length, state), { nodes: pods, names: pods.map(podKeyOf), ranked: true });
   });
 }
 

@@ -21,6 +21,7 @@ import {
 } from '../../src/view/pages.js';
 import { renderText } from '../../src/view/text.js';
 import { countRows, findSection, pagerOf, pagerText, rowValue, sectionTitles } from '../../src/view/ir.js';
+import { rankedSlice } from '../../src/view/pages/paging.js';
 import { renderPage } from '../../src/view/html.js';
 import {
   SERIES, SMALL_CLUSTER_NODES, SMALL_CLUSTER_PODS, TOTAL_SERIES, createMetricsSource, powerRankQuery, hostnameMatcher, regexLiteral, scopedSeriesQuery, summarizeMetrics,
@@ -205,6 +206,31 @@ describe('GPU Pods in power order: Prometheus ranks the pods by the power of the
     expect(f.rank.order.every((k) => /^ml\/job-1\d$/.test(k))).toBe(true);
     const vm = podsView(ctx, { metrics: f, pager: { sort: 'power', filter: ' JOB-1' } });
     expect(findSection(vm, 'All GPU Pods').blocks[0].rows).toHaveLength(10);
+  });
+
+  it('a page past the end of the ranking (the count shrank) says so and the page moves to the last one', async () => {
+    const { ctx, fake } = cluster();
+    const p = rankedSlice({ page: 5, per: PODS_PER_PAGE, count: 30 }, 0, {});
+    expect(p).toMatchObject({ page: 1, pages: 2, from: 25, to: 25, beyond: true });
+    const t = pagerText({ noun: 'GPU pods drawing power', page: p.page, pages: p.pages, from: p.from, to: p.to, total: p.total,
+      matched: p.matched, filter: '', beyond: true });
+    expect(t).toBe('Moving to page 2 of 2 (30 GPU pods drawing power)');
+    expect(rankedSlice({ page: 1, per: PODS_PER_PAGE, count: 30 }, 5, {})).toMatchObject({ page: 1, from: 25, to: 30, beyond: false });
+    // The plugin: a stored page 6 in power order is moved to page 2, which is asked for and shown.
+    lib.resetHeadlamp();
+    lib.lists.Node = [ctx.gpuNodes, null];
+    lib.lists.Pod = [ctx.gpuPods, null];
+    lib.api.handler = (path) => (path.indexOf('/proxy/api/v1/') >= 0 ? fake(path)
+      : Promise.reject(Object.assign(new Error('404'), { status: 404 })));
+    const mem = {};
+    const storage = { getItem: (k) => (k in mem ? mem[k] : null), setItem: (k, v) => { mem[k] = v; } };
+    storage.setItem('headlamp-amd-gpu-plugin.view.__default__|pods', JSON.stringify({ page: 5, filter: '', sort: 'power' }));
+    const plugin = createPlugin({ React, lib, CommonComponents: CC, viewStorage: storage });
+    const view = render(h(plugin.routeComponent('pods')));
+    await view.settle(20);
+    expect(view.text()).toContain('Showing 26–30 of 30 GPU pods drawing power · page 2 of 2');
+    expect(JSON.parse(mem['headlamp-amd-gpu-plugin.view.__default__|pods']).page).toBe(1);
+    view.unmount();
   });
 
   it('before the ranked answer the page shows the name order; the client orders never ask Prometheus to rank', () => {
