@@ -17,172 +17,20 @@
  *     evaluate the left side once);
  *   * ES modules → a function module (`__import(spec)` / `__exports`).
  *
+ * The lexer is ./tsxLex.js, the `?.` / `??` and module lowering ./tsxLower.js.
+ *
  * It is a token-level transformer, not a full parser: the constructs above
  * are recognised from their context (what precedes a `<`, a `:` or a `?.`).
  * That is enough for the reference's 12 production files; it is not a
  * general TypeScript compiler and nothing shipped uses it.
  */
+import {
+  KEYWORD_BEFORE_EXPR, PUNCT2, PUNCT3, blank, exprPosition, isClose, isIdPart, isIdStart, isOpen, matchBrace, matching, scanRegex,
+  scanTemplate, sig, skipString, tokenize, typeArgsEnd, typeEnd,
+} from './tsxLex.js';
+import { HELPERS, lowerModules, lowerOptional } from './tsxLower.js';
 
-const PUNCT3 = ['...', '===', '!==', '**=', '<<=', '>>=', '>>>', '&&=', '||=', '??='];
-const PUNCT2 = ['=>', '==', '!=', '<=', '>=', '&&', '||', '??', '?.', '++', '--', '+=', '-=', '*=', '/=', '%=', '&=',
-  '|=', '^=', '<<', '>>', '**'];
-const KEYWORD_BEFORE_EXPR = { return: 1, case: 1, typeof: 1, void: 1, delete: 1, throw: 1, in: 1, of: 1, new: 1, else: 1,
-  do: 1, instanceof: 1, yield: 1, await: 1, default: 1 };
-
-function isIdStart(c) {
-  return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || c === '_' || c === '$';
-}
-function isIdPart(c) {
-  return isIdStart(c) || (c >= '0' && c <= '9');
-}
-
-/** True when the token `prev` (or the start) leaves the scanner in expression position. */
-function exprPosition(prev) {
-  if (!prev) return true;
-  if (prev.t === 'ident') return !!KEYWORD_BEFORE_EXPR[prev.v];
-  if (prev.t === 'punct') return [')', ']', '}', '++', '--'].indexOf(prev.v) < 0;
-  return false;
-}
-
-/**
- * Tokens of `src`: {t, v} with t in ws | comment | ident | num | str | tmpl |
- * regex | punct. A template literal is one token; `parts` alternates quasi
- * text and expression source.
- */
-export function tokenize(src) {
-  const out = [];
-  let i = 0;
-  let prev = null;
-  const n = src.length;
-  function push(t, v, extra) {
-    const tok = Object.assign({ t: t, v: v }, extra || {});
-    out.push(tok);
-    if (t !== 'ws' && t !== 'comment') prev = tok;
-  }
-  while (i < n) {
-    const c = src[i];
-    if (c === ' ' || c === '\t' || c === '\n' || c === '\r') {
-      let j = i;
-      while (j < n && /\s/.test(src[j])) j++;
-      push('ws', src.slice(i, j));
-      i = j;
-    } else if (c === '/' && src[i + 1] === '/') {
-      let j = src.indexOf('\n', i);
-      if (j < 0) j = n;
-      push('comment', src.slice(i, j));
-      i = j;
-    } else if (c === '/' && src[i + 1] === '*') {
-      const j = src.indexOf('*/', i + 2);
-      if (j < 0) throw new Error('tsx: unterminated comment');
-      push('comment', src.slice(i, j + 2));
-      i = j + 2;
-    } else if (c === '"' || c === "'") {
-      const j = skipString(src, i);
-      push('str', src.slice(i, j));
-      i = j;
-    } else if (c === '`') {
-      const r = scanTemplate(src, i);
-      push('tmpl', src.slice(i, r.end), { parts: r.parts });
-      i = r.end;
-    } else if (isIdStart(c)) {
-      let j = i;
-      while (j < n && isIdPart(src[j])) j++;
-      push('ident', src.slice(i, j));
-      i = j;
-    } else if (c >= '0' && c <= '9') {
-      let j = i;
-      while (j < n && /[0-9a-fA-FxXoObB._n]/.test(src[j])) j++;
-      push('num', src.slice(i, j));
-      i = j;
-    } else if (c === '/' && exprPosition(prev)) {
-      const j = scanRegex(src, i);
-      push('regex', src.slice(i, j));
-      i = j;
-    } else {
-      let p = null;
-      const three = src.substr(i, 3);
-      const two = src.substr(i, 2);
-      if (PUNCT3.indexOf(three) >= 0) p = three;
-      else if (PUNCT2.indexOf(two) >= 0 && !(two === '?.' && /[0-9]/.test(src[i + 2] || ''))) p = two;
-      else p = c;
-      push('punct', p);
-      i += p.length;
-    }
-  }
-  return out;
-}
-
-/** End of the regex literal at `i` (flags included). */
-function scanRegex(src, i) {
-  let j = i + 1;
-  let cls = false;
-  while (j < src.length) {
-    if (src[j] === '\\') { j += 2; continue; }
-    if (src[j] === '[') cls = true;
-    else if (src[j] === ']') cls = false;
-    else if (src[j] === '/' && !cls) break;
-    else if (src[j] === '\n') throw new Error('tsx: unterminated regex');
-    j++;
-  }
-  j++;
-  while (j < src.length && isIdPart(src[j])) j++;
-  return j;
-}
-
-function skipString(src, i) {
-  const q = src[i];
-  let j = i + 1;
-  while (j < src.length && src[j] !== q) {
-    if (src[j] === '\\') j++;
-    else if (src[j] === '\n') throw new Error('tsx: unterminated string');
-    j++;
-  }
-  return j + 1;
-}
-
-/** A template literal at `i`: {end, parts: [quasi, expr, quasi, ...]} (raw source). */
-function scanTemplate(src, i) {
-  const parts = [];
-  let j = i + 1;
-  let q = j;
-  while (j < src.length) {
-    if (src[j] === '\\') { j += 2; continue; }
-    if (src[j] === '`') {
-      parts.push(src.slice(q, j));
-      return { end: j + 1, parts: parts };
-    }
-    if (src[j] === '$' && src[j + 1] === '{') {
-      parts.push(src.slice(q, j));
-      const e = matchBrace(src, j + 1);
-      parts.push(src.slice(j + 2, e));
-      j = e + 1;
-      q = j;
-      continue;
-    }
-    j++;
-  }
-  throw new Error('tsx: unterminated template');
-}
-
-/** Index of the `}` closing the `{` at `open` (strings, templates and comments skipped). */
-function matchBrace(src, open) {
-  let depth = 0;
-  let j = open;
-  while (j < src.length) {
-    const c = src[j];
-    if (c === '"' || c === "'") { j = skipString(src, j); continue; }
-    if (c === '`') { j = scanTemplate(src, j).end; continue; }
-    if (c === '/' && src[j + 1] === '/') { j = src.indexOf('\n', j); if (j < 0) break; continue; }
-    if (c === '/' && src[j + 1] === '*') { j = src.indexOf('*/', j) + 2; continue; }
-    if (c === '{') depth++;
-    else if (c === '}') {
-      depth--;
-      if (depth === 0) return j;
-    }
-    j++;
-  }
-  throw new Error('tsx: unbalanced {');
-}
+export { HELPERS, lowerModules, lowerOptional, tokenize };
 
 // ---------------------------------------------------------------------------
 // JSX
@@ -377,73 +225,6 @@ function pushText(children, raw) {
 // TypeScript erasure (token level)
 // ---------------------------------------------------------------------------
 
-function sig(toks, k, dir) {
-  let j = k + dir;
-  while (j >= 0 && j < toks.length && (toks[j].t === 'ws' || toks[j].t === 'comment')) j += dir;
-  return j;
-}
-
-function isOpen(t) { return t.t === 'punct' && (t.v === '(' || t.v === '[' || t.v === '{'); }
-function isClose(t) { return t.t === 'punct' && (t.v === ')' || t.v === ']' || t.v === '}'); }
-
-/** Index of the token closing the bracket at `k`. */
-function matching(toks, k) {
-  let d = 0;
-  for (let j = k; j < toks.length; j++) {
-    if (isOpen(toks[j])) d++;
-    else if (isClose(toks[j])) {
-      d--;
-      if (d === 0) return j;
-    }
-  }
-  throw new Error('tsx: unbalanced ' + toks[k].v);
-}
-
-/** Index of the `>` closing a type-argument `<` at `k`, or -1 when it is no type argument list. */
-function typeArgsEnd(toks, k) {
-  let d = 0;
-  for (let j = k; j < toks.length; j++) {
-    const t = toks[j];
-    if (t.t === 'ws' || t.t === 'comment' || t.t === 'ident' || t.t === 'str' || t.t === 'num') continue;
-    if (t.t !== 'punct') return -1;
-    if (t.v === '<') d++;
-    else if (t.v === '>') {
-      d--;
-      if (d === 0) return j;
-    } else if (t.v === '>>') {
-      d -= 2;
-      if (d <= 0) return d === 0 ? j : -1;
-    } else if (['|', '&', ',', '[', ']', '.', '{', '}', ':', ';', '?', '(', ')', '=>'].indexOf(t.v) < 0) return -1;
-  }
-  return -1;
-}
-
-/**
- * End (exclusive) of a type starting at token `k`: the first token at depth 0
- * that is in `stops` (brackets and `<…>` nest).
- */
-function typeEnd(toks, k, stops) {
-  let d = 0;
-  let angle = 0;
-  for (let j = k; j < toks.length; j++) {
-    const t = toks[j];
-    if (t.t !== 'punct') continue;
-    if (d === 0 && angle === 0 && j > k && stops.indexOf(t.v) >= 0) return j;
-    if (isOpen(t)) d++;
-    else if (isClose(t)) {
-      if (d === 0) return j;
-      d--;
-    } else if (t.v === '<') angle++;
-    else if (t.v === '>' && angle > 0) angle--;
-    else if (t.v === '=>' && d === 0 && angle === 0 && stops.indexOf('=>') >= 0 && j > k) return j;
-  }
-  return toks.length;
-}
-
-function blank(toks, a, b) {
-  for (let j = a; j < b; j++) toks[j] = { t: 'ws', v: toks[j].t === 'ws' && /\n/.test(toks[j].v) ? '\n' : '' };
-}
-
 /** Erase TypeScript syntax from `src` (JSX already gone). */
 export function stripTypes(src) {
   const toks = tokenize(src);
@@ -582,188 +363,6 @@ function stripParams(toks, open) {
   }
 }
 
-// ---------------------------------------------------------------------------
-// ?. and ?? → ES2019
-// ---------------------------------------------------------------------------
-
-const NC_LEFT_STOPS = ['(', '[', '{', ',', ';', '=', ':', '?', '=>', '&&', '||', '??', '...', '!', '+=', '-='];
-const NC_RIGHT_STOPS = [')', ']', '}', ',', ';', ':', '?', '??', '||', '&&'];
-
-function text(toks, a, b) {
-  return toks.slice(a, b).map(function (x) { return x.v; }).join('');
-}
-
-/**
- * Start of the member / call chain ending at token `k` (inclusive):
- * primary ( .name | ?.name | (…) | […] )*, walked right to left.
- */
-function chainStart(toks, k) {
-  let j = k;
-  for (;;) {
-    const t = toks[j];
-    if (t.t === 'punct' && (t.v === ')' || t.v === ']')) {
-      const o = openOf(toks, j);
-      const p = sig(toks, o, -1);
-      const pv = p >= 0 ? toks[p] : null;
-      if (pv && pv.t === 'punct' && pv.v === '?.') { j = sig(toks, p, -1); continue; }
-      // a call or an index continues to the callee / object; else the bracket is the primary
-      if (pv && ((pv.t === 'ident' && !KEYWORD_BEFORE_EXPR[pv.v]) || (pv.t === 'punct' && (pv.v === ')' || pv.v === ']')))) {
-        j = p;
-        continue;
-      }
-      return o;
-    }
-    if (t.t === 'ident' || t.t === 'str' || t.t === 'num' || t.t === 'tmpl') {
-      if (t.t === 'ident' && KEYWORD_BEFORE_EXPR[t.v]) throw new Error('tsx: keyword in chain ' + t.v);
-      const p = sig(toks, j, -1);
-      if (p >= 0 && toks[p].t === 'punct' && (toks[p].v === '.' || toks[p].v === '?.')) {
-        j = sig(toks, p, -1);
-        continue;
-      }
-      return j;
-    }
-    throw new Error('tsx: cannot chain from ' + t.v);
-  }
-}
-
-function openOf(toks, close) {
-  let d = 0;
-  for (let j = close; j >= 0; j--) {
-    if (isClose(toks[j])) d++;
-    else if (isOpen(toks[j])) {
-      d--;
-      if (d === 0) return j;
-    }
-  }
-  throw new Error('tsx: unbalanced ' + toks[close].v);
-}
-
-/** End (exclusive) of the member / call chain continuing at token `k`. */
-function chainEnd(toks, k) {
-  let j = k;
-  for (;;) {
-    const n = sig(toks, j - 1, 1);
-    if (n >= toks.length) return j;
-    const t = toks[n];
-    if (t.t === 'punct' && (t.v === '.' || t.v === '?.')) {
-      const m = sig(toks, n, 1);
-      if (toks[m].t === 'ident') { j = m + 1; continue; }
-      if (toks[m].v === '(' || toks[m].v === '[') { j = matching(toks, m) + 1; continue; }
-      return j;
-    }
-    if (t.t === 'punct' && (t.v === '(' || t.v === '[')) { j = matching(toks, n) + 1; continue; }
-    return j;
-  }
-}
-
-/** Rewrite optional chains and nullish coalescing (innermost / leftmost first). */
-export function lowerOptional(src) {
-  for (let guard = 0; guard < 10000; guard++) {
-    const toks = tokenize(src);
-    // template literals: lower their expressions in place
-    let changed = false;
-    for (let k = 0; k < toks.length; k++) {
-      if (toks[k].t !== 'tmpl') continue;
-      const parts = toks[k].parts;
-      let v = '`';
-      for (let i = 0; i < parts.length; i++) v += i % 2 ? '${' + lowerOptional(parts[i]) + '}' : parts[i];
-      v += '`';
-      if (v !== toks[k].v) {
-        toks[k] = { t: 'tmpl', v: v, parts: parts };
-        changed = true;
-      }
-    }
-    if (changed) src = text(toks, 0, toks.length);
-    const T = tokenize(src);
-    let at = -1;
-    for (let k = 0; k < T.length; k++) {
-      if (T[k].t === 'punct' && (T[k].v === '?.' || T[k].v === '??')) { at = k; break; }
-    }
-    if (at < 0) return src;
-    if (T[at].v === '?.') {
-      const lhsEnd = sig(T, at, -1);
-      const lhsStart = chainStart(T, lhsEnd);
-      const restStart = sig(T, at, 1);
-      let restEnd;
-      if (T[restStart].t === 'ident') restEnd = chainEnd(T, restStart + 1);
-      else if (T[restStart].v === '(' || T[restStart].v === '[') restEnd = chainEnd(T, matching(T, restStart) + 1);
-      else throw new Error('tsx: bad optional chain');
-      const rest = text(T, restStart, restEnd);
-      const body = T[restStart].t === 'ident' ? '__o.' + rest : '__o' + rest;
-      src = text(T, 0, lhsStart) + '__oc(' + text(T, lhsStart, lhsEnd + 1) + ', function (__o) { return ' + body + '; })' +
-        text(T, restEnd, T.length);
-    } else {
-      // left operand: back to a lower-precedence token at depth 0
-      let a = at - 1;
-      for (; a >= 0; a--) {
-        const t = T[a];
-        if (isClose(t)) { a = openOf(T, a); continue; }
-        if (isOpen(t)) break;
-        if (t.t === 'punct' && NC_LEFT_STOPS.indexOf(t.v) >= 0) break;
-        if (t.t === 'ident' && (t.v === 'return' || t.v === 'case' || t.v === 'throw')) break;
-      }
-      let b = at + 1;
-      for (; b < T.length; b++) {
-        const t = T[b];
-        if (isOpen(t)) { b = matching(T, b); continue; }
-        if (isClose(t)) break;
-        if (t.t === 'punct' && NC_RIGHT_STOPS.indexOf(t.v) >= 0) break;
-      }
-      const left = text(T, a + 1, at).trim();
-      const right = text(T, at + 1, b).trim();
-      src = text(T, 0, a + 1) + ' __nc(' + left + ', function () { return ' + right + '; })' + text(T, b, T.length);
-    }
-  }
-  throw new Error('tsx: optional lowering did not converge');
-}
-
-// ---------------------------------------------------------------------------
-// ES module → function module
-// ---------------------------------------------------------------------------
-
-export const HELPERS = 'function __oc(o, f) { return o === null || o === undefined ? undefined : f(o); }\n' +
-  'function __nc(v, f) { return v === null || v === undefined ? f() : v; }\n';
-
-/** `import` / `export` statements → `__import(spec)` / `__exports`. */
-export function lowerModules(src) {
-  const exportsTail = [];
-  let s = src.replace(/^[ \t]*import\s+([\s\S]*?)\s+from\s+'([^']+)';?/gm, function (m, clause, spec) {
-    const out = [];
-    let c = clause.trim();
-    const def = /^([A-Za-z_$][\w$]*)\s*(?:,\s*([\s\S]*))?$/.exec(c);
-    if (def) {
-      out.push('const ' + def[1] + ' = __import(' + JSON.stringify(spec) + ', true);');
-      c = (def[2] || '').trim();
-    }
-    if (c) {
-      if (c[0] !== '{') throw new Error('tsx: unsupported import ' + m);
-      const names = c.slice(1, -1).split(',').map(function (x) { return x.trim(); }).filter(Boolean).map(function (x) {
-        const a = /^(?:type\s+)?([A-Za-z_$][\w$]*)(?:\s+as\s+([A-Za-z_$][\w$]*))?$/.exec(x);
-        if (!a) throw new Error('tsx: unsupported import name ' + x);
-        return a[2] ? a[1] + ': ' + a[2] : a[1];
-      });
-      out.push('const { ' + names.join(', ') + ' } = __import(' + JSON.stringify(spec) + ');');
-    }
-    return out.join(' ');
-  });
-  s = s.replace(/^[ \t]*import\s+'([^']+)';?/gm, function (m, spec) { return '__import(' + JSON.stringify(spec) + ');'; });
-  s = s.replace(/^[ \t]*export\s+default\s+function\s+([A-Za-z_$][\w$]*)/gm, function (m, name) {
-    exportsTail.push('__exports.default = ' + name + ';');
-    return 'function ' + name;
-  });
-  s = s.replace(/^[ \t]*export\s+(async\s+)?function\s+([A-Za-z_$][\w$]*)/gm, function (m, as, name) {
-    exportsTail.push('__exports.' + name + ' = ' + name + ';');
-    return (as || '') + 'function ' + name;
-  });
-  s = s.replace(/^[ \t]*export\s+(const|let|var)\s+([A-Za-z_$][\w$]*)/gm, function (m, kw, name) {
-    exportsTail.push('__exports.' + name + ' = ' + name + ';');
-    return kw + ' ' + name;
-  });
-  s = s.replace(/^[ \t]*export\s+default\s+/gm, '__exports.default = ');
-  const left = /^[ \t]*(import|export)\b.*$/m.exec(s);
-  if (left) throw new Error('tsx: unsupported module statement: ' + left[0]);
-  return s + '\n' + exportsTail.join('\n') + '\n';
-}
 
 /** The whole pipeline: TSX source → body of `function (__import, __exports) { … }`. */
 export function transpile(src) {

@@ -15,462 +15,19 @@ to serve every query the plugin and the reference-schedule replay issue:
 * ``label_replace(v, "dst", "replacement", "src", "regex")``;
 * number literals (the reference's discovery probe is ``query=1``).
 
-Series are stored either as a deterministic function of time sampled on a
-fixed scrape grid (synthetic telemetry) or as explicit pushed samples (live
-GPU telemetry from the native probe). Staleness/lookback follow Prometheus'
-5-minute default.
+Storage is :mod:`.tsdb` (series on a scrape grid or pushed samples, 5-minute
+lookback); the lexer / parser is :mod:`.promql_parse`. Both are re-exported
+here, the module the fake control plane and the tests import.
 """
 from __future__ import annotations
 
-import bisect
-import json
 import math
 import re
-from typing import Callable, Dict, List, Optional, Sequence, Tuple
+from typing import Dict, List, Optional, Tuple
 
-LOOKBACK_S = 300.0
-Labels = Dict[str, str]
-
-
-# ---------------------------------------------------------------------------
-# Storage
-# ---------------------------------------------------------------------------
-
-# Bumped on every sample push / series add: instant-query results cached by
-# :func:`query` are valid only while it is unchanged.
-_MUTATIONS = [0]
-
-
-class Series:
-    """One time series: labels + samples.
-
-    Either ``fn(t)`` sampled every ``interval`` seconds (aligned to the grid),
-    or explicit samples appended with :meth:`push` (kept sorted, bounded).
-    """
-
-    __slots__ = ("labels", "fn", "interval", "ts", "vs", "cap", "_key", "_json", "_memo", "seq")
-
-    def __init__(self, labels: Labels, fn: Optional[Callable[[float], float]] = None,
-                 interval: float = 15.0, cap: int = 4096):
-        self.labels = dict(labels)
-        self.fn = fn
-        self.interval = float(interval)
-        self.ts: List[float] = []
-        self.vs: List[float] = []
-        self.cap = cap
-        self._key = tuple(sorted(self.labels.items()))
-        self.seq = 0  # insertion order in its TSDB
-        self._json = None
-        self._memo: Dict[float, float] = {}  # fn value per sample time (fn series are deterministic)
-
-    def metric_json(self) -> str:
-        """JSON of the label set (cached — series labels never change once stored)."""
-        if self._json is None:
-            self._json = json.dumps(self.labels, separators=(",", ":"))
-        return self._json
-
-    def push(self, t: float, v: float) -> None:
-        _MUTATIONS[0] += 1
-        if self.ts and t <= self.ts[-1]:
-            if t == self.ts[-1]:
-                self.vs[-1] = v
-            return
-        self.ts.append(t)
-        self.vs.append(v)
-        if len(self.ts) > self.cap:
-            drop = len(self.ts) - self.cap
-            del self.ts[:drop]
-            del self.vs[:drop]
-
-    def _fn_at(self, ts: float) -> float:
-        v = self._memo.get(ts)
-        if v is None:
-            if len(self._memo) >= 4096:
-                self._memo.clear()
-            v = self._memo[ts] = self.fn(ts)
-        return v
-
-    def samples(self, start: float, end: float) -> List[Tuple[float, float]]:
-        """Samples with start < t <= end."""
-        if self.fn is not None:
-            iv = self.interval
-            k0 = math.floor(start / iv) + 1
-            k1 = math.floor(end / iv)
-            return [(k * iv, self._fn_at(k * iv)) for k in range(k0, k1 + 1)]
-        lo = bisect.bisect_right(self.ts, start)
-        hi = bisect.bisect_right(self.ts, end)
-        return list(zip(self.ts[lo:hi], self.vs[lo:hi]))
-
-    def at(self, t: float) -> Optional[Tuple[float, float]]:
-        """Latest sample within the lookback window ending at ``t``."""
-        if self.fn is not None:
-            k = math.floor(t / self.interval) * self.interval
-            return (k, self._fn_at(k))
-        i = bisect.bisect_right(self.ts, t) - 1
-        if i < 0 or t - self.ts[i] > LOOKBACK_S:
-            return None
-        return (self.ts[i], self.vs[i])
-
-
-class TSDB:
-    """Series indexed by metric name."""
-
-    def __init__(self) -> None:
-        self.by_name: Dict[str, List[Series]] = {}
-        self._index: Dict[tuple, Series] = {}
-        self._select_cache: Dict[tuple, List[Series]] = {}
-        self._by_labels_id: Dict[int, Series] = {}
-        # `by (...)` projections of stored label sets: (id(labels), by) → (key, projected, labels, json)
-        self._proj_cache: Dict[tuple, tuple] = {}
-        self._proj_json: Dict[int, tuple] = {}
-        self._fn_intervals: set = set()
-        self._query_cache: Dict[str, tuple] = {}
-        self._range_cache: Dict[str, tuple] = {}  # query → (mutation stamp, {t → rows})
-        # Inverted index (label, value) → series, as a real TSDB's postings:
-        # a `hostname=~"a|b|…"` page scope or `hostname="x"` detail query
-        # reads the matching series only, not every series of its names.
-        self._by_label: Dict[tuple, List[Series]] = {}
-        self._name_rank: Dict[str, int] = {}
-        # Aggregations over a plain selector: the function-backed series' part
-        # per (query part, sample-grid bucket); pushed series are added each time.
-        self._agg_cache: Dict[tuple, dict] = {}
-
-    def label_json(self, labels: Labels) -> str:
-        """JSON for a label set; cached when it is a stored series' own dict
-        or a cached ``by`` projection of one."""
-        s = self._by_labels_id.get(id(labels))
-        if s is not None and s.labels is labels:
-            return s.metric_json()
-        p = self._proj_json.get(id(labels))
-        if p is not None and p[0] is labels:
-            return p[1]
-        return json.dumps(labels, separators=(",", ":"))
-
-    def project(self, labels: Labels, by: tuple) -> tuple:
-        """(group key, projected labels) of ``labels`` onto ``by``, cached per
-        stored label set so a repeated aggregation query does no dict work."""
-        ck = (id(labels), by)
-        hit = self._proj_cache.get(ck)
-        if hit is not None and hit[2] is labels:
-            return hit[0], hit[1]
-        gl = {k: labels[k] for k in by if k in labels}
-        key = tuple(sorted(gl.items()))
-        if self._by_labels_id.get(id(labels)) is not None:
-            self._proj_cache[ck] = (key, gl, labels)
-            self._proj_json[id(gl)] = (gl, json.dumps(gl, separators=(",", ":")))
-        return key, gl
-
-    def add(self, series: Series) -> Series:
-        key = series._key
-        if key in self._index:
-            return self._index[key]
-        self._index[key] = series
-        _MUTATIONS[0] += 1
-        series.seq = len(self._index)
-        if series.fn is not None:
-            self._fn_intervals.add(series.interval)
-        name = series.labels.get("__name__", "")
-        if name not in self.by_name:
-            self._name_rank[name] = len(self._name_rank)
-        self.by_name.setdefault(name, []).append(series)
-        for kv in series.labels.items():
-            self._by_label.setdefault(kv, []).append(series)
-        self._by_labels_id[id(series.labels)] = series
-        self._select_cache.clear()
-        self._agg_cache.clear()
-        return series
-
-    def get_or_create(self, labels: Labels) -> Series:
-        key = tuple(sorted(labels.items()))
-        s = self._index.get(key)
-        if s is None:
-            s = self.add(Series(labels))
-        return s
-
-    def select(self, matchers: Sequence["Matcher"]) -> List[Series]:
-        """Series matching every matcher. The series set only grows via
-        :meth:`add`, so results are cached per matcher signature."""
-        sig = tuple((m.label, m.op, m.value) for m in matchers)
-        hit = self._select_cache.get(sig)
-        if hit is not None:
-            return hit
-        # The most selective indexable matcher (= or a =~ of literal
-        # alternatives) picks the candidates; every matcher then filters.
-        best = None
-        for m in matchers:
-            vals = m.literals()
-            if vals is None:
-                continue
-            lists = [self._by_label.get((m.label, v), []) for v in vals]
-            n = sum(len(x) for x in lists)
-            if best is None or n < best[0]:
-                best = (n, lists)
-        if best is not None:
-            cands = best[1][0] if len(best[1]) == 1 else [x for lst in best[1] for x in lst]
-            out = [x for x in cands if all(m.matches(x.labels.get(m.label, "")) for m in matchers)]
-            # the order a scan by name would give: names in insertion order, then series
-            rank = self._name_rank
-            out.sort(key=lambda x: (rank.get(x.labels.get("__name__", ""), 0), x.seq))
-            self._select_cache[sig] = out
-            return out
-        names = [m for m in matchers if m.label == "__name__" and m.op == "="]
-        if names:
-            cands = self.by_name.get(names[0].value, [])
-        else:
-            name_re = [m for m in matchers if m.label == "__name__" and m.op == "=~"]
-            if name_re:
-                cands = [s for n, lst in self.by_name.items() if name_re[0].matches(n) for s in lst]
-            else:
-                cands = [s for lst in self.by_name.values() for s in lst]
-        out = [s for s in cands if all(m.matches(s.labels.get(m.label, "")) for m in matchers)]
-        self._select_cache[sig] = out
-        return out
-
-    def __len__(self) -> int:
-        return len(self._index)
-
-
-# ---------------------------------------------------------------------------
-# Lexer / parser
-# ---------------------------------------------------------------------------
-
-class PromQLError(ValueError):
-    pass
-
-
-_TOKEN_RE = re.compile(r"""
-    (?P<ws>\s+)
-  | (?P<num>(?:\d+\.\d*|\.\d+|\d+)(?:[eE][+-]?\d+)?)
-  | (?P<dur>\[\s*\d+[smhdw]\s*\])
-  | (?P<str>"(?:[^"\\]|\\.)*"|'(?:[^'\\]|\\.)*')
-  | (?P<op>=~|!~|!=|==|>=|<=|[-+*/%^(){},=<>])
-  | (?P<ident>[a-zA-Z_:][a-zA-Z0-9_:]*)
-""", re.X)
-
-_DUR = {"s": 1, "m": 60, "h": 3600, "d": 86400, "w": 604800}
-AGGREGATIONS = {"sum", "avg", "max", "min", "count"}
-RANK_AGGREGATIONS = {"topk", "bottomk"}
-RANGE_FUNCS = {"rate", "irate", "increase", "avg_over_time", "max_over_time", "min_over_time",
-               "sum_over_time", "count_over_time", "last_over_time"}
-BIN_PREC = {"+": 1, "-": 1, "*": 2, "/": 2, "%": 2, "==": 0, "!=": 0, ">": 0, "<": 0, ">=": 0, "<=": 0,
-            "and": -1, "unless": -1, "or": -2}
-SET_OPS = {"and", "unless", "or"}
-MIN_PREC = min(BIN_PREC.values())
-
-
-def _tokenize(q: str) -> List[Tuple[str, str]]:
-    pos = 0
-    out = []
-    while pos < len(q):
-        m = _TOKEN_RE.match(q, pos)
-        if not m:
-            raise PromQLError(f"unexpected character {q[pos]!r} at {pos}")
-        pos = m.end()
-        kind = m.lastgroup
-        if kind == "ws":
-            continue
-        out.append((kind, m.group(kind)))
-    out.append(("eof", ""))
-    return out
-
-
-class Matcher:
-    __slots__ = ("label", "op", "value", "_re")
-
-    def __init__(self, label: str, op: str, value: str):
-        self.label, self.op, self.value = label, op, value
-        self._re = re.compile("^(?:" + value + ")$") if op in ("=~", "!~") else None
-
-    def literals(self) -> Optional[List[str]]:
-        """The exact values this matcher accepts, when it is `=` / a `=~` of
-        literal alternatives and none is empty (an empty value also matches
-        series without the label); else None."""
-        if self.op == "=":
-            return [self.value] if self.value else None
-        if self.op != "=~":
-            return None
-        out = []
-        for part in re.split(r"(?<!\\)\|", self.value):
-            if not part or re.search(r"(?<!\\)[.^$*+?()\[\]{}|]", part):
-                return None
-            out.append(re.sub(r"\\(.)", r"\1", part))
-        return out
-
-    def matches(self, v: str) -> bool:
-        if self.op == "=":
-            return v == self.value
-        if self.op == "!=":
-            return v != self.value
-        ok = bool(self._re.match(v))
-        return ok if self.op == "=~" else not ok
-
-
-# AST nodes are tuples: ("num", v) ("sel", matchers, range_s|None) ("func", name, arg)
-# ("agg", op, by|None, without|None, expr) ("bin", op, lhs, rhs, matching)
-
-class _Parser:
-    def __init__(self, q: str):
-        self.toks = _tokenize(q)
-        self.i = 0
-
-    def peek(self, k: int = 0):
-        return self.toks[self.i + k]
-
-    def take(self, kind: Optional[str] = None, val: Optional[str] = None):
-        t = self.toks[self.i]
-        if (kind and t[0] != kind) or (val is not None and t[1] != val):
-            raise PromQLError(f"expected {val or kind}, got {t[1]!r}")
-        self.i += 1
-        return t
-
-    def parse(self):
-        e = self.expr(MIN_PREC)
-        self.take("eof")
-        return e
-
-    def expr(self, min_prec: int):
-        lhs = self.unary()
-        while True:
-            k, v = self.peek()
-            is_op = (k == "op" and v in BIN_PREC) or (k == "ident" and v in SET_OPS)
-            if not is_op or BIN_PREC[v] < min_prec:
-                return lhs
-            self.i += 1
-            matching = self.vector_matching()
-            rhs = self.expr(BIN_PREC[v] + 1)
-            lhs = ("bin", v, lhs, rhs, matching)
-
-    def vector_matching(self):
-        k, v = self.peek()
-        if k == "ident" and v in ("on", "ignoring"):
-            self.i += 1
-            labels = self.label_list()
-            group = None
-            k2, v2 = self.peek()
-            if k2 == "ident" and v2 in ("group_left", "group_right"):
-                self.i += 1
-                extra = self.label_list() if self.peek()[1] == "(" else []
-                group = (v2, extra)
-            return (v, labels, group)
-        return None
-
-    def label_list(self) -> List[str]:
-        self.take("op", "(")
-        out = []
-        while self.peek()[1] != ")":
-            out.append(self.take("ident")[1])
-            if self.peek()[1] == ",":
-                self.i += 1
-        self.take("op", ")")
-        return out
-
-    def unary(self):
-        k, v = self.peek()
-        if k == "op" and v == "-":
-            self.i += 1
-            return ("bin", "*", ("num", -1.0), self.unary(), None)
-        return self.primary()
-
-    def primary(self):
-        k, v = self.peek()
-        if k == "num":
-            self.i += 1
-            return ("num", float(v))
-        if k == "op" and v == "(":
-            self.i += 1
-            e = self.expr(MIN_PREC)
-            self.take("op", ")")
-            return e
-        if k == "op" and v == "{":
-            return self.selector(None)
-        if k == "ident":
-            if v in AGGREGATIONS and self.peek(1)[1] in ("(", "by", "without"):
-                return self.aggregation()
-            if v in RANK_AGGREGATIONS and self.peek(1)[1] in ("(", "by", "without"):
-                return self.rank_aggregation()
-            if v == "label_replace" and self.peek(1)[1] == "(":
-                self.i += 2
-                arg = self.expr(MIN_PREC)
-                strs = []
-                for _ in range(4):
-                    self.take("op", ",")
-                    raw = self.take("str")[1]
-                    strs.append(bytes(raw[1:-1], "utf-8").decode("unicode_escape"))
-                self.take("op", ")")
-                return ("label_replace", arg, *strs)
-            if v in RANGE_FUNCS and self.peek(1)[1] == "(":
-                self.i += 2
-                arg = self.expr(MIN_PREC)
-                self.take("op", ")")
-                if arg[0] != "sel" or arg[2] is None:
-                    raise PromQLError(f"{v}() expects a range vector")
-                return ("func", v, arg)
-            self.i += 1
-            return self.selector(v)
-        raise PromQLError(f"unexpected token {v!r}")
-
-    def aggregation(self):
-        op = self.take("ident")[1]
-        by = without = None
-        if self.peek()[1] in ("by", "without"):
-            kw = self.take("ident")[1]
-            lst = self.label_list()
-            by, without = (lst, None) if kw == "by" else (None, lst)
-        self.take("op", "(")
-        e = self.expr(MIN_PREC)
-        self.take("op", ")")
-        if self.peek()[1] in ("by", "without"):
-            kw = self.take("ident")[1]
-            lst = self.label_list()
-            by, without = (lst, None) if kw == "by" else (None, lst)
-        return ("agg", op, by, without, e)
-
-    def rank_aggregation(self):
-        """`topk(k, expr)` / `bottomk(k, expr)`, optionally `by (…)` / `without (…)`."""
-        op = self.take("ident")[1]
-        by = without = None
-        if self.peek()[1] in ("by", "without"):
-            kw = self.take("ident")[1]
-            lst = self.label_list()
-            by, without = (lst, None) if kw == "by" else (None, lst)
-        self.take("op", "(")
-        k = self.expr(MIN_PREC)
-        self.take("op", ",")
-        e = self.expr(MIN_PREC)
-        self.take("op", ")")
-        if self.peek()[1] in ("by", "without"):
-            kw = self.take("ident")[1]
-            lst = self.label_list()
-            by, without = (lst, None) if kw == "by" else (None, lst)
-        return ("rank", op, k, by, without, e)
-
-    def selector(self, name: Optional[str]):
-        matchers = []
-        if name:
-            matchers.append(Matcher("__name__", "=", name))
-        if self.peek()[1] == "{":
-            self.i += 1
-            while self.peek()[1] != "}":
-                label = self.take("ident")[1]
-                op = self.take("op")[1]
-                if op not in ("=", "!=", "=~", "!~"):
-                    raise PromQLError(f"bad matcher op {op}")
-                raw = self.take("str")[1]
-                matchers.append(Matcher(label, op, bytes(raw[1:-1], "utf-8").decode("unicode_escape")))
-                if self.peek()[1] == ",":
-                    self.i += 1
-            self.take("op", "}")
-        if not matchers:
-            raise PromQLError("empty selector")
-        rng = None
-        if self.peek()[0] == "dur":
-            d = self.take("dur")[1].strip("[] ")
-            rng = float(d[:-1]) * _DUR[d[-1]]
-        return ("sel", matchers, rng)
-
-
-def parse(q: str):
-    return _Parser(q).parse()
+from .promql_parse import (AGGREGATIONS, BIN_PREC, RANGE_FUNCS, RANK_AGGREGATIONS, SET_OPS, Matcher,  # noqa: F401
+                           PromQLError, parse)
+from .tsdb import _MUTATIONS, LOOKBACK_S, Labels, Series, TSDB  # noqa: F401
 
 
 # ---------------------------------------------------------------------------
