@@ -5,35 +5,12 @@
  * range queries.
  */
 import {
-  PROMETHEUS_SERVICES,
-  stringLabels,
-  EXPORTER_JOIN_LABELS,
-  EXPORTER_LEAN_LABELS,
-  keyedByHostname,
-  SERIES,
-  createMetricsSource,
-  exporterQuery,
-  mergedQuery,
-  joinExporterResults,
-  joinNodeExporterResults,
-  servicePath,
-  shareGpus,
-  shareMap,
-  summarizeMetrics,
-  staticsOf,
-  applyStatics,
-  exporterNodeQuery,
-  nodeSlice,
-  ownersQuery,
-  promString,
-  METRIC_VIEWS,
-  nodePowerQuery,
-  podPowerQuery,
-  splitByName,
-  STALE_FAILURES,
+  PROMETHEUS_SERVICES, EXPORTER_JOIN_LABELS, EXPORTER_LEAN_LABELS, keyedByHostname, SERIES, createMetricsSource,
+  exporterQuery, mergedQuery, shareGpus, shareMap, staticsOf, applyStatics, exporterNodeQuery, METRIC_VIEWS,
+  splitByName, STALE_FAILURES,
 } from '../../src/api/metrics.js';
 
-import { BASE0, BASE1, exporterData, flatten, ok, prom, vec } from './promFake.js';
+import { BASE0, BASE1, exporterData, ok, prom, vec } from './promFake.js';
 
 describe('discovery', () => {
   it('probes all candidate services in parallel', async () => {

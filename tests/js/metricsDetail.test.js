@@ -6,36 +6,12 @@
  * metrics.test.js.
  */
 import {
-  PROMETHEUS_SERVICES,
-  stringLabels,
-  EXPORTER_JOIN_LABELS,
-  EXPORTER_LEAN_LABELS,
-  keyedByHostname,
-  SERIES,
-  createMetricsSource,
-  exporterQuery,
-  mergedQuery,
-  joinExporterResults,
-  joinNodeExporterResults,
-  servicePath,
-  shareGpus,
-  shareMap,
-  summarizeMetrics,
-  staticsOf,
-  applyStatics,
-  exporterNodeQuery,
-  nodeSlice,
-  ownersQuery,
-  promString,
-  METRIC_VIEWS,
-  nodePowerQuery,
+  stringLabels, EXPORTER_JOIN_LABELS, SERIES, createMetricsSource, exporterQuery, mergedQuery, joinExporterResults,
+  joinNodeExporterResults, summarizeMetrics, exporterNodeQuery, nodeSlice, ownersQuery, promString, nodePowerQuery,
   podPowerQuery,
-  splitByName,
-  STALE_FAILURES,
 } from '../../src/api/metrics.js';
 
-import { BASE0, BASE1, exporterData, flatten, ok, prom, vec } from './promFake.js';
-
+import { exporterData, flatten, ok, prom, vec } from './promFake.js';
 
 describe('fetchPodSeries (Pod detail power history)', () => {
   it('asks for one pod\'s power, summed per step, with escaped matchers', () => {

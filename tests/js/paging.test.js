@@ -15,17 +15,17 @@ import { createPlugin } from '../../src/plugin.js';
 import { resetSharedStores } from '../../src/api/clusterStore.js';
 import { DEVICE_CONFIG_LIST_PATH } from '../../src/api/amdgpu.js';
 import {
-  ALL_NODES_SERIES, RANKED_NODE_SORTS, NODE_SORTS, NODES_PER_PAGE, OVERVIEW_PLUGIN_PODS, PODS_PER_PAGE, clearViewMemo, devicePluginsView,
-  metricsView, nodePage, nodeSortOf, nodesView, overviewView, ownersScope, podPage, podSortOf, podsView, POD_SORTS,
-  RANKED_POD_SORTS, telemetryScope,
+  ALL_NODES_SERIES, RANKED_NODE_SORTS, NODE_SORTS, NODES_PER_PAGE, OVERVIEW_PLUGIN_PODS, PODS_PER_PAGE,
+  clearViewMemo, devicePluginsView, metricsView, nodePage, nodeSortOf, nodesView, overviewView, ownersScope, podPage,
+  podSortOf, podsView, POD_SORTS, RANKED_POD_SORTS, telemetryScope,
 } from '../../src/view/pages.js';
 import { renderText } from '../../src/view/text.js';
 import { countRows, findSection, pagerOf, pagerText, rowValue, sectionTitles } from '../../src/view/ir.js';
 import { rankedSlice } from '../../src/view/pages/paging.js';
 import { renderPage } from '../../src/view/html.js';
 import {
-  SERIES, SMALL_CLUSTER_NODES, SMALL_CLUSTER_PODS, TOTAL_SERIES, createMetricsSource, powerRankQuery, hostnameMatcher, regexLiteral, scopedSeriesQuery, summarizeMetrics,
-  summaryQuery, totalsFromRows, joinExporterResults, splitByName,
+  SERIES, TOTAL_SERIES, createMetricsSource, powerRankQuery, hostnameMatcher, regexLiteral, scopedSeriesQuery,
+  summarizeMetrics, summaryQuery, totalsFromRows, joinExporterResults, splitByName,
 } from '../../src/api/metrics.js';
 import { makeContext, makeDeviceConfig, makeGpuNode, makeGpuPod, makePluginPod } from './fixtures.js';
 import { BASE0, exporterData, flatten, prom } from './promFake.js';

@@ -4,32 +4,20 @@
  * scoped answer decides exporter / node-exporter / no telemetry in one wave).
  * The pager and the scoped queries themselves are in paging.test.js.
  */
-import React, { render, textOf as textOfNode } from './stubs/react.js';
+import React, { render } from './stubs/react.js';
 import * as lib from './stubs/headlamp-lib.js';
 import * as CC from './stubs/CommonComponents.js';
 import { createPlugin } from '../../src/plugin.js';
 import { resetSharedStores } from '../../src/api/clusterStore.js';
 import { DEVICE_CONFIG_LIST_PATH } from '../../src/api/amdgpu.js';
-import {
-  ALL_NODES_SERIES, RANKED_NODE_SORTS, NODE_SORTS, NODES_PER_PAGE, OVERVIEW_PLUGIN_PODS, PODS_PER_PAGE, clearViewMemo, devicePluginsView,
-  metricsView, nodePage, nodeSortOf, nodesView, overviewView, ownersScope, podPage, podSortOf, podsView, POD_SORTS,
-  RANKED_POD_SORTS, telemetryScope,
-} from '../../src/view/pages.js';
-import { renderText } from '../../src/view/text.js';
-import { countRows, findSection, pagerOf, pagerText, rowValue, sectionTitles } from '../../src/view/ir.js';
-import { rankedSlice } from '../../src/view/pages/paging.js';
-import { renderPage } from '../../src/view/html.js';
-import {
-  SERIES, SMALL_CLUSTER_NODES, SMALL_CLUSTER_PODS, TOTAL_SERIES, createMetricsSource, powerRankQuery, hostnameMatcher, regexLiteral, scopedSeriesQuery, summarizeMetrics,
-  summaryQuery, totalsFromRows, joinExporterResults, splitByName,
-} from '../../src/api/metrics.js';
-import { makeContext, makeDeviceConfig, makeGpuNode, makeGpuPod, makePluginPod } from './fixtures.js';
-import { BASE0, exporterData, flatten, prom } from './promFake.js';
+import { NODES_PER_PAGE, PODS_PER_PAGE, clearViewMemo, metricsView, ownersScope } from '../../src/view/pages.js';
+import { sectionTitles } from '../../src/view/ir.js';
+import { SERIES, SMALL_CLUSTER_NODES, SMALL_CLUSTER_PODS, createMetricsSource } from '../../src/api/metrics.js';
+import { makeContext, makeDeviceConfig, makeGpuNode, makeGpuPod } from './fixtures.js';
+import { exporterData, prom } from './promFake.js';
 
 const h = React.createElement;
 const names = (n) => Array.from({ length: n }, (_, i) => 'mi355x-' + String(i).padStart(3, '0'));
-const ctxOf = (n) => makeContext({ nodes: names(n).map((x) => makeGpuNode(x)), pods: [makeGpuPod('train-0', { node: 'mi355x-000' })] });
-const cards = (vm) => sectionTitles(vm).filter((t) => /^mi355x-/.test(t));
 const decoded = (fake) => fake.mock.calls.map((c) => decodeURIComponent(c[0]));
 
 beforeEach(() => {

@@ -26,7 +26,10 @@
  * testing-library style (getByText, getByLabelText, getByTestId, …),
  * clicked, and serialised to HTML. Only what the plugin needs is modelled:
  * no refs to host nodes, no portals, no suspense, no concurrent mode.
+ * The host tree's serialisation and queries are in ./hostTree.js.
  */
+
+import { hostQueries, htmlOf, textOf } from './hostTree.js';
 
 const ELEMENT = Symbol.for('stub.react.element');
 const MEMO = Symbol.for('stub.react.memo');
@@ -485,55 +488,10 @@ function unmount(inst) {
   removed.forEach(function (i) { i.root.unmounts++; });
 }
 
-function textOf(node) {
-  if (typeof node === 'string') return node;
-  let s = '';
-  for (let i = 0; i < node.children.length; i++) s += textOf(node.children[i]);
-  return s;
-}
-
-const VOID = { br: true, input: true, hr: true, img: true };
-
-function esc(s) {
-  return String(s).replace(/&/g, '&amp;').replace(/</g, '&lt;').replace(/>/g, '&gt;').replace(/"/g, '&quot;');
-}
-
-function attrs(props) {
-  let s = '';
-  const keys = Object.keys(props).sort();
-  for (let i = 0; i < keys.length; i++) {
-    const k = keys[i];
-    const v = props[k];
-    if (v === null || v === undefined || v === false || typeof v === 'function' || k === 'style') continue;
-    s += ' ' + k + (v === true ? '' : '="' + esc(v) + '"');
-  }
-  return s;
-}
-
-function htmlOf(node) {
-  if (typeof node === 'string') return esc(node);
-  const inner = node.children.map(htmlOf).join('');
-  if (VOID[node.tag]) return '<' + node.tag + attrs(node.props) + '>';
-  return '<' + node.tag + attrs(node.props) + '>' + inner + '</' + node.tag + '>';
-}
-
-function walk(nodes, fn) {
-  for (let i = 0; i < nodes.length; i++) {
-    const n = nodes[i];
-    if (typeof n === 'string') continue;
-    fn(n);
-    walk(n.children, fn);
-  }
-}
 
 function walkInstances(inst, fn) {
   fn(inst);
   for (let i = 0; i < inst.kids.length; i++) walkInstances(inst.kids[i], fn);
-}
-
-function matches(text, m) {
-  const t = text.replace(/\s+/g, ' ').trim();
-  return m instanceof RegExp ? m.test(t) : t === m;
 }
 
 function flushMicrotasks() {
@@ -642,7 +600,7 @@ export function render(element, options) {
   }
   flush();
 
-  const handle = {
+  const handle = Object.assign(hostQueries(function () { return root.top.out; }), {
     /** Synchronously apply pending state updates. */
     flush: function () {
       if (root.error) {
@@ -700,55 +658,6 @@ export function render(element, options) {
     html: function () { return root.top.out.map(htmlOf).join(''); },
     text: function () { return root.top.out.map(textOf).join(''); },
     stats: function () { return { commits: root.commits, unmounts: root.unmounts }; },
-    /** Host nodes (deepest first match semantics like testing-library). */
-    queryAll: function (pred) {
-      const out = [];
-      walk(root.top.out, function (n) { if (pred(n)) out.push(n); });
-      return out;
-    },
-    getAllByText: function (m) {
-      const hits = handle.queryAll(function (n) {
-        if (!matches(textOf(n), m)) return false;
-        // deepest: no host child matches as well
-        for (let i = 0; i < n.children.length; i++) {
-          const c = n.children[i];
-          if (typeof c !== 'string' && matches(textOf(c), m)) return false;
-        }
-        return true;
-      });
-      if (hits.length === 0) throw new Error('Unable to find an element with the text: ' + String(m));
-      return hits;
-    },
-    getByText: function (m) {
-      const hits = handle.getAllByText(m);
-      if (hits.length > 1) throw new Error('Found multiple elements with the text: ' + String(m));
-      return hits[0];
-    },
-    queryByText: function (m) {
-      try {
-        return handle.getByText(m);
-      } catch (e) {
-        return null;
-      }
-    },
-    getByLabelText: function (label) {
-      const hits = handle.queryAll(function (n) { return n.props['aria-label'] !== undefined && matches(String(n.props['aria-label']), label); });
-      if (hits.length !== 1) throw new Error((hits.length ? 'Found multiple' : 'Unable to find') + ' elements labelled ' + String(label));
-      return hits[0];
-    },
-    getAllByTestId: function (id) {
-      const hits = handle.queryAll(function (n) { return n.props['data-testid'] === id; });
-      if (hits.length === 0) throw new Error('Unable to find data-testid=' + id);
-      return hits;
-    },
-    getByTestId: function (id) {
-      const hits = handle.getAllByTestId(id);
-      if (hits.length > 1) throw new Error('Found multiple data-testid=' + id);
-      return hits[0];
-    },
-    byTag: function (tag) {
-      return handle.queryAll(function (n) { return n.tag === tag; });
-    },
     /** Component instances of `type` (function, memo or host tag). */
     instances: function (type) {
       const out = [];
@@ -784,7 +693,7 @@ export function render(element, options) {
       const v = node.instance.field;
       return v === undefined || v === null ? '' : String(v);
     },
-  };
+  });
   return handle;
 }
 
