@@ -139,6 +139,9 @@ export function withTimeout(promise, ms, clock) {
  * @property {boolean} crdLoading   the first DeviceConfig / operator-pod fetch is not in yet
  *                                  (pages render what they can as each of the three settles:
  *                                  a page waits only for the lists it draws)
+ * @property {boolean} pluginPodsLoading  the operator pods are not known yet: from the pod list
+ *                                  while a pod feed is mounted, else from the plugin-pod
+ *                                  requests (the Device Plugins route mounts no pod list)
  * @property {'unknown'|'pending'|'ready'|'error'} nodesState
  * @property {'unknown'|'pending'|'ready'|'error'} podsState
  * @property {boolean} refreshing   a refresh is in flight (data above is still valid)
@@ -171,7 +174,8 @@ export function createClusterStore(opts) {
     deviceConfigs: [],
     crdAvailable: false,
     crdForbidden: false, // the CRD list answered 401 / 403: RBAC, not a missing operator
-    pluginPods: [], // from the plugin-pod queries (used when the pod list is not available)
+    pluginPods: [], // from the plugin-pod queries (used when the pod list is not available or not watched)
+    pluginPodsKnown: false, // s.pluginPods holds an answer (queried, or the watched list's last word)
     // Where each list stands: 'unknown' (never fed: harness/tests),
     // 'pending' (a list/watch is in flight), 'ready', or 'error'. An errored
     // list (e.g. pods forbidden cluster-wide) is settled: the page leaves its
@@ -188,6 +192,14 @@ export function createClusterStore(opts) {
   let seq = 0;
   let inflight = null;
   let podsQueried = false; // the in-flight refresh includes the plugin-pod requests
+  // Pod list feeds mounted right now (providerCore.js PodListFeed). A store
+  // no feed ever attached to (harness, terminal client, tests feeding
+  // setPods / loadLists themselves) treats its pod list as current; once
+  // feeds attach, the list is current only while one is mounted — after the
+  // last unmounts nothing keeps it up to date, so operator pods come from the
+  // plugin-pod requests again.
+  let podFeeds = 0;
+  let feedsAttached = false;
   let version = 0;
   const listeners = [];
 
@@ -249,8 +261,16 @@ export function createClusterStore(opts) {
    * they come from the PLUGIN_POD_QUERIES requests.
    */
   function pluginPods() {
-    if (s.podsState !== 'ready' || !s.pods) return s.pluginPods;
+    if (s.podsState !== 'ready' || !s.pods || !podsLive()) return s.pluginPods;
     return memoPluginPods;
+  }
+  /** The pod list is kept current (a feed is mounted, or no feed ever was: see podFeeds). */
+  function podsLive() {
+    return podFeeds > 0 || !feedsAttached;
+  }
+  function pluginPodsLoading() {
+    if (podsLive() && s.podsState !== 'unknown') return !settled(s.podsState);
+    return !s.pluginPodsKnown;
   }
   function index(n, p) {
     if (memoIndexKey[0] !== n || memoIndexKey[1] !== p) {
@@ -282,6 +302,7 @@ export function createClusterStore(opts) {
       nodesLoading: !settled(s.nodesState),
       podsLoading: !settled(s.podsState),
       crdLoading: !s.asyncLoaded,
+      pluginPodsLoading: pluginPodsLoading(),
       nodesState: s.nodesState,
       podsState: s.podsState,
       refreshing: s.refreshing,
@@ -335,6 +356,7 @@ export function createClusterStore(opts) {
 
   function commitQueriedPods(pods) {
     s.pluginPods = sameObjects(s.pluginPods, pods) ? s.pluginPods : pods;
+    s.pluginPodsKnown = true;
   }
 
   /**
@@ -359,7 +381,7 @@ export function createClusterStore(opts) {
         return { ok: isAbsent(e) ? false : null, items: [], forbidden: st === 403 || st === 401 };
       }
     );
-    const needPods = s.podsState === 'unknown' || s.podsState === 'error';
+    const needPods = s.podsState === 'unknown' || s.podsState === 'error' || !podsLive();
     podsQueried = needPods;
     const pods = needPods ? queryPluginPods() : Promise.resolve(null);
     const run = Promise.all([crd, pods]).then(
@@ -461,6 +483,32 @@ export function createClusterStore(opts) {
     return Promise.all([nodesP, podsP]).then(function () {});
   }
 
+  /**
+   * A pod list feed mounted (providerCore.js PodListFeed); returns its
+   * detach. When the last feed detaches, the watched list's operator pods
+   * become the queried answer (the freshest known) until the next refresh
+   * asks the plugin-pod requests.
+   */
+  function attachPodFeed() {
+    const wasLive = podsLive();
+    podFeeds++;
+    feedsAttached = true;
+    let attached = true;
+    // The watched list is the operator pods' source again (a re-mounted feed).
+    if (podFeeds === 1 && !wasLive) emit();
+    return function detach() {
+      if (!attached) return;
+      attached = false;
+      podFeeds--;
+      if (podFeeds > 0) return;
+      if (s.podsState === 'ready' && s.pods) {
+        s.pluginPods = memoPluginPods;
+        s.pluginPodsKnown = true;
+      }
+      emit();
+    };
+  }
+
   function subscribe(fn) {
     listeners.push(fn);
     return function () {
@@ -480,9 +528,13 @@ export function createClusterStore(opts) {
    * together (a route + a Node detail section) cost one fetch, not N.
    */
   function revalidate(maxAgeMs) {
-    if (s.refreshing && inflight) return inflight;
+    // Operator pods nobody knows: no pod list is watched and no refresh asked
+    // the plugin-pod requests (a route without the pod list mounted after one
+    // whose list never arrived) — fresh DeviceConfigs alone do not do.
+    const podsMissing = !podsLive() && !s.pluginPodsKnown;
+    if (s.refreshing && inflight && !(podsMissing && !podsQueried)) return inflight;
     const age = s.lastUpdated === null ? Infinity : clock.now() - s.lastUpdated;
-    if (age < (maxAgeMs === undefined ? 0 : maxAgeMs)) return Promise.resolve();
+    if (age < (maxAgeMs === undefined ? 0 : maxAgeMs) && !podsMissing) return Promise.resolve();
     return refresh();
   }
 
@@ -491,6 +543,7 @@ export function createClusterStore(opts) {
     getSnapshot: getSnapshot,
     setNodes: setNodes,
     setPods: setPods,
+    attachPodFeed: attachPodFeed,
     refresh: refresh,
     revalidate: revalidate,
     loadLists: loadLists,

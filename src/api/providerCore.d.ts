@@ -29,6 +29,8 @@ export interface ClusterStore {
   getSnapshot(): Omit<AmdGpuContextValue, 'refresh'>;
   setNodes(items: unknown[] | null, error: string | null): void;
   setPods(items: unknown[] | null, error: string | null): void;
+  /** A pod list feed mounted; returns its detach (operator pods come from the plugin-pod requests once none is). */
+  attachPodFeed(): () => void;
   refresh(): Promise<void>;
   revalidate(maxAgeMs?: number): Promise<void>;
   loadLists(): Promise<void>;

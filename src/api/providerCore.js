@@ -148,9 +148,15 @@ export function createProviderCore(React, lib, deps) {
     return null;
   }
 
-  /** Feeds Headlamp's all-namespaces pod list + watch into the store. */
+  /**
+   * Feeds Headlamp's all-namespaces pod list + watch into the store. While
+   * one is mounted the store derives operator pods from it; after the last
+   * unmounts they come from the plugin-pod requests (clusterStore.js
+   * attachPodFeed).
+   */
   function PodListFeed(props) {
     const store = props.store;
+    useEffect(function () { return store.attachPodFeed(); }, [store]);
     const pods = useListOf(lib.K8s.ResourceClasses.Pod, { namespace: '' });
     const allPods = pods[0];
     const podError = pods[1];

@@ -231,6 +231,8 @@ export interface ClusterSnapshot {
   podsLoading: boolean;
   /** the first DeviceConfig / operator-pod fetch is not in yet */
   crdLoading: boolean;
+  /** the operator pods are not known yet (from the watched pod list, else from the plugin-pod requests) */
+  pluginPodsLoading: boolean;
   nodesState: ListState;
   podsState: ListState;
   /** a refresh is in flight; the data above is still valid */

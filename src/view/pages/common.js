@@ -62,6 +62,10 @@ export function podsPending(ctx) {
 export function crdPending(ctx) {
   return ctx.crdLoading !== undefined ? !!ctx.crdLoading : !!ctx.loading;
 }
+/** The operator pods: from the watched pod list, or from the plugin-pod requests where no pod list is mounted. */
+export function pluginPodsPending(ctx) {
+  return ctx.pluginPodsLoading !== undefined ? !!ctx.pluginPodsLoading : podsPending(ctx);
+}
 
 /** Text of a cell whose value needs the pod list while it is still loading. */
 export const PODS_LOADING = 'Loading…';

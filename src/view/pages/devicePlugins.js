@@ -33,7 +33,7 @@ import {
   refreshButton,
   restartsCell,
   crdPending,
-  podsPending,
+  pluginPodsPending,
 } from './common.js';
 import { podPage } from './paging.js';
 
@@ -44,14 +44,17 @@ function enabledCell(on, detail) {
 /**
  * One card per DeviceConfig (reference: one per GpuDevicePlugin). Per-operand
  * DaemonSet counts replace the single desired/ready pair. The page needs no
- * node list: it renders once the DeviceConfigs are in, with a loader where
- * the operator pods go until the pod list is in (reference: a full-page
- * Loader until every list is in, DevicePluginsPage.tsx:23-25).
+ * node list and no all-namespaces pod list: its route (plugin.js PAGE_NEEDS)
+ * asks for the operator pods with the plugin-pod requests, in the same wave
+ * as the DeviceConfigs, so it renders whole after one round trip on any
+ * cluster size (reference: a full-page Loader until both cluster-wide lists
+ * and its four serial requests are in, DevicePluginsPage.tsx:23-25,
+ * IntelGpuDataContext.tsx:98-165,214).
  */
 export function devicePluginsView(ctx, opts) {
   const now = nowOf(opts);
   if (crdPending(ctx)) return page(null, null, [loader('Loading device plugin data...')]);
-  const podsPend = podsPending(ctx);
+  const podsPend = pluginPodsPending(ctx);
   // One page of the operator pod table (PODS_PER_PAGE; filter on
   // namespace/name and node): three per GPU node on a real cluster.
   const pg = podPage(ctx.pluginPods, opts && opts.pager, 'plugin-pod');

@@ -435,6 +435,76 @@ describe('revalidate', () => {
   });
 });
 
+describe('pod list feeds: operator pods from the watched list, else from the plugin-pod requests', () => {
+  const ppNames = (store) => store.getSnapshot().pluginPods.map((p) => p.metadata.name).sort();
+  const queried = (request) => request.mock.calls.filter((c) => PLUGIN_POD_QUERIES.indexOf(c[0]) >= 0).length;
+
+  it('while a feed is mounted, a refresh is the CRD request alone and operator pods follow the list', async () => {
+    const request = router(baseRoutes());
+    const store = createClusterStore({ request });
+    const detach = store.attachPodFeed();
+    store.setPods([makePluginPod('dp-live'), makePlainPod('web')], null);
+    await store.refresh();
+    expect(queried(request)).toBe(0);
+    expect(ppNames(store)).toEqual(['dp-live']);
+    expect(store.getSnapshot().pluginPodsLoading).toBe(false);
+    detach();
+  });
+
+  it('after the last feed unmounts: the list\'s last word is kept, the next refresh asks the requests', async () => {
+    const request = router(baseRoutes());
+    const store = createClusterStore({ request });
+    const detach = store.attachPodFeed();
+    store.setPods([makePluginPod('dp-live')], null);
+    await store.refresh();
+    detach();
+    detach(); // idempotent
+    expect(ppNames(store)).toEqual(['dp-live']);
+    expect(store.getSnapshot().pluginPodsLoading).toBe(false);
+    await store.refresh();
+    expect(queried(request)).toBe(PLUGIN_POD_QUERIES.length);
+    expect(ppNames(store)).toEqual(['dp-0', 'dp-1']);
+  });
+
+  it('a feed mounted again makes the list the source again, without re-querying', async () => {
+    const request = router(baseRoutes());
+    const store = createClusterStore({ request });
+    store.attachPodFeed()();
+    store.setPods([makePluginPod('dp-live')], null);
+    const detach = store.attachPodFeed();
+    expect(ppNames(store)).toEqual(['dp-live']);
+    await store.refresh();
+    expect(queried(request)).toBe(0);
+    detach();
+  });
+
+  it('revalidate asks for operator pods nobody knows even when the DeviceConfigs are fresh', async () => {
+    const request = router(baseRoutes());
+    const store = createClusterStore({ request });
+    const detach = store.attachPodFeed(); // the pod list never arrives before the route unmounts
+    store.setPods(null, null); // what the feed reports while its list is in flight
+    await store.refresh();
+    expect(queried(request)).toBe(0);
+    detach();
+    expect(store.getSnapshot().pluginPodsLoading).toBe(true);
+    await store.revalidate(60000);
+    expect(queried(request)).toBe(PLUGIN_POD_QUERIES.length);
+    expect(store.getSnapshot().pluginPodsLoading).toBe(false);
+    expect(ppNames(store)).toEqual(['dp-0', 'dp-1']);
+    await store.revalidate(60000); // now known and fresh: nothing more
+    expect(request).toHaveBeenCalledTimes(2 + PLUGIN_POD_QUERIES.length);
+  });
+
+  it('a store no feed ever attached to (harness, terminal client) treats setPods / loadLists as current', async () => {
+    const request = router(baseRoutes());
+    const store = createClusterStore({ request });
+    await store.loadLists();
+    await store.refresh();
+    expect(queried(request)).toBe(0);
+    expect(store.getSnapshot().pluginPodsLoading).toBe(false);
+  });
+});
+
 describe('getSharedStore', () => {
   it('returns one store per cluster key', () => {
     resetSharedStores();

@@ -22,7 +22,7 @@ import { Page, Section } from '../../src/components/View.tsx';
 import { PLUGIN_NAME, createPlugin, registerPlugin } from '../../src/plugin.js';
 import { resetSharedStores } from '../../src/api/clusterStore.js';
 import { clearViewMemo } from '../../src/view/pages.js';
-import { DEVICE_CONFIG_LIST_PATH } from '../../src/api/amdgpu.js';
+import { DEVICE_CONFIG_LIST_PATH, PLUGIN_POD_QUERIES, isAmdGpuPluginPod } from '../../src/api/amdgpu.js';
 import { makeDeviceConfig, makeGpuNode, makeGpuPod, makeNode, makePlainPod, makePluginPod } from './fixtures.js';
 import { exporterData, prom } from './promFake.js';
 import { SERIES } from '../../src/api/metrics.js';
@@ -57,6 +57,14 @@ function cluster(o) {
       const list = lib.lists.Pod;
       if (!list || !list[0]) return Promise.reject(Object.assign(new Error(list && list[1] ? list[1] : 'pods is forbidden'), { status: 403 }));
       return Promise.resolve(kubeList(list[0].filter((p) => p.spec && p.spec.nodeName === node)));
+    }
+    // The plugin-pod requests (label selector across namespaces, the operator
+    // namespace), answered from the same pod list as an apiserver would.
+    const q = PLUGIN_POD_QUERIES.indexOf(path);
+    if (q >= 0) {
+      const list = lib.lists.Pod;
+      const all = list && list[0] ? list[0] : [];
+      return Promise.resolve(kubeList(all.filter((p) => (q === 0 ? isAmdGpuPluginPod(p) : p.metadata.namespace === 'kube-amd-gpu'))));
     }
     return Promise.reject(Object.assign(new Error('503 Service Unavailable'), { status: 503 }));
   };

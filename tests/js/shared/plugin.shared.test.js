@@ -24,7 +24,7 @@ import '../../../src/index.tsx';
 import { resetSharedStores } from '../../../src/api/clusterStore.js';
 import { clearViewMemo } from '../../../src/view/pages.js';
 import { invalidateSettings } from '../../../src/api/settings.js';
-import { DEVICE_CONFIG_LIST_PATH } from '../../../src/api/amdgpu.js';
+import { DEVICE_CONFIG_LIST_PATH, PLUGIN_POD_QUERIES, isAmdGpuPluginPod } from '../../../src/api/amdgpu.js';
 import { makeDeviceConfig, makeGpuNode, makeGpuPod, makeNode, makePlainPod, makePluginPod } from '../fixtures.js';
 import { exporterData, prom } from '../promFake.js';
 
@@ -62,6 +62,12 @@ function cluster(o) {
     if (fs) {
       const node = decodeURIComponent(fs[1]).replace(/^spec\.nodeName=/, '');
       return Promise.resolve({ kind: 'List', metadata: {}, items: pods.filter((p) => p.spec.nodeName === node) });
+    }
+    // The plugin-pod requests: operator pods by label across namespaces, and the operator namespace.
+    const q = PLUGIN_POD_QUERIES.indexOf(path);
+    if (q >= 0) {
+      const items = pods.filter((p) => (q === 0 ? isAmdGpuPluginPod(p) : p.metadata.namespace === 'kube-amd-gpu'));
+      return Promise.resolve({ kind: 'List', metadata: {}, items: items });
     }
     return Promise.reject(Object.assign(new Error('503 Service Unavailable'), { status: 503 }));
   };
@@ -156,13 +162,35 @@ describe('shared: progressive cold open — a page waits only for the lists it d
     r.unmount();
   });
 
-  it('Device Plugins renders its DeviceConfig cards before either list', async () => {
+  it('Device Plugins renders whole — DeviceConfig cards and operator pods — with both lists pending, no pod list mounted', async () => {
     cluster({ loading: true });
     const r = render(h(route('/amd-gpu/device-plugins')));
     await r.settle();
     expect(r.text()).toContain('DeviceConfig: gpu-operator');
-    expect(r.text()).toContain('Loading operator pods...');
+    expect(r.text()).toContain('amdgpu-dp-0');
+    expect(r.text()).not.toContain('Loading operator pods...');
+    expect(lib.lists.calls.Pod).toHaveLength(0);
+    PLUGIN_POD_QUERIES.forEach((q) => expect(lib.api.calls).toContain(q));
     r.unmount();
+  });
+
+  it('Device Plugins after a page that watched the pods: the list\'s operator pods at once, the requests on Refresh', async () => {
+    const fake = cluster();
+    const r1 = render(h(route('/amd-gpu')));
+    await r1.settle();
+    expect(PLUGIN_POD_QUERIES.some((q) => lib.api.calls.indexOf(q) >= 0)).toBe(false);
+    r1.unmount();
+    const r2 = render(h(route('/amd-gpu/device-plugins')));
+    await r2.settle();
+    expect(r2.text()).toContain('amdgpu-dp-0');
+    expect(PLUGIN_POD_QUERIES.some((q) => lib.api.calls.indexOf(q) >= 0)).toBe(false);
+    // A new operator pod: nothing watches the pod list on this route, Refresh asks the plugin-pod requests.
+    fake.pods.push(makePluginPod('amdgpu-dp-1', { node: 'mi355x-001' }));
+    r2.click(r2.byLabel('Refresh device plugin data'));
+    await r2.settle();
+    PLUGIN_POD_QUERIES.forEach((q) => expect(lib.api.calls).toContain(q));
+    expect(r2.text()).toContain('amdgpu-dp-1');
+    r2.unmount();
   });
 
   it('GPU Pods waits for the pod list (the list is its content)', async () => {
@@ -231,9 +259,9 @@ describe('shared: refresh and StrictMode (' + tier + ')', () => {
     r.unmount();
   });
 
-  it('each route mounts only what its page draws: Metrics the node list alone, no pod list, no DeviceConfig request', async () => {
+  it('each route mounts only what its page draws: Metrics the node list alone, Device Plugins no list at all', async () => {
     const expected = {
-      '/amd-gpu': [true, true, 1], '/amd-gpu/device-plugins': [false, true, 1], '/amd-gpu/nodes': [true, true, 0],
+      '/amd-gpu': [true, true, 1], '/amd-gpu/device-plugins': [false, false, 1], '/amd-gpu/nodes': [true, true, 0],
       '/amd-gpu/pods': [true, true, 0], '/amd-gpu/metrics': [true, false, 0],
     };
     for (const path of Object.keys(expected)) {

@@ -57,7 +57,8 @@ def _check(line, n):
     # never the all-namespaces pod list.
     assert cold["overview"]["requests"]["amd"] == 3 and cold["nodes"]["requests"]["amd"] == 3
     assert set(cold["metrics"]["amd_requests_by_kind"]) == {"nodes", "query", "query_range"}, cold["metrics"]
-    assert set(cold["devicePlugins"]["amd_requests_by_kind"]) == {"pods", "crd"}, cold["devicePlugins"]
+    # Device Plugins: the DeviceConfigs and the operator pods by the plugin-pod requests, one wave, no pod list.
+    assert set(cold["devicePlugins"]["amd_requests_by_kind"]) == {"plugin-pods", "crd"}, cold["devicePlugins"]
     for v in cold.values():
         assert v["amd"] < v["reference"], cold
         # progressive pages: the first render with content comes no later than the page complete
