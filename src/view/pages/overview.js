@@ -38,6 +38,7 @@ import {
   crdPending,
   nodesPending,
   PODS_LOADING,
+  pluginPodsPending,
   podsPending,
 } from './common.js';
 
@@ -65,10 +66,11 @@ export function overviewView(ctx, opts) {
   const now = nowOf(opts);
   if (nodesPending(ctx) || crdPending(ctx)) return page(null, null, [loader('Loading ' + BRAND + ' data...')]);
   const podsPend = podsPending(ctx);
+  const opPend = pluginPodsPending(ctx);
   const items = memo(
     'overview',
-    [ctx.deviceConfigs, ctx.pluginPods, ctx.pluginInstalled, ctx.crdAvailable, ctx.gpuNodes, ctx.gpuPods, ctx.index, ctx.error, podsPend],
-    function () { return overviewItems(ctx, now, podsPend); },
+    [ctx.deviceConfigs, ctx.pluginPods, ctx.pluginInstalled, ctx.crdAvailable, ctx.gpuNodes, ctx.gpuPods, ctx.index, ctx.error, podsPend, opPend],
+    function () { return overviewItems(ctx, now, podsPend, opPend); },
     now
   );
   return page(BRAND + ' — Overview', refreshButton('Refresh AMD GPU data', ctx.refreshing), items);
@@ -92,14 +94,15 @@ export function partitionModeDistribution(gpuNodes) {
   return order.map(function (k, i) { return { name: k, value: counts[k], fill: MODE_COLORS[i % MODE_COLORS.length] }; });
 }
 
-function overviewItems(ctx, now, podsPend) {
+function overviewItems(ctx, now, podsPend, opPend) {
   const items = [];
   const t = ctx.index.totals;
 
   if (ctx.error) items.push(errorSection(ctx.error));
 
-  // Operator pods come from the pod list: while it loads, "not detected" is not known yet.
-  if (!ctx.pluginInstalled && !podsPend) {
+  // Operator pods come from the pod list (or the plugin-pod requests): while
+  // they load, "not detected" is not known yet.
+  if (!ctx.pluginInstalled && !opPend) {
     items.push(
       section('Plugin Not Detected', [
         kv([
