@@ -24,6 +24,24 @@ export function amdSchedule(request, clock, timeoutMs) {
   }
   const clk = clock || hiResClock;
   const store = createClusterStore({ request: request, onTrace: onTrace, clock: clk, timeoutMs: timeoutMs });
+  // The pod list feed the routes that draw pods mount (providerCore.js
+  // PodListFeed): attached while such a page is shown. A route without it
+  // (Device Plugins, Metrics: plugin.js PAGE_NEEDS) runs with it detached, so
+  // its refresh asks what the shipped route asks (Device Plugins: the
+  // DeviceConfigs and the plugin-pod requests).
+  let detachFeed = store.attachPodFeed();
+  function needsOf(page) {
+    return PAGE_NEEDS[page === 'devicePlugins' ? 'device-plugins' : page];
+  }
+  function onRoute(page, run) {
+    if (needsOf(page).pods || !detachFeed) return run();
+    detachFeed();
+    detachFeed = null;
+    return run().then(function (v) {
+      detachFeed = store.attachPodFeed();
+      return v;
+    });
+  }
   const metrics = createMetricsSource({ request: request, onTrace: onTrace, clock: clk, timeoutMs: timeoutMs });
   const mstate = { metrics: null, fetchError: null, fetching: false, series: null };
   // Per-page metrics state, as each page's own hook holds it (plugin.js):
@@ -131,7 +149,7 @@ export function amdSchedule(request, clock, timeoutMs) {
       if (page === 'nodes') return fetchNodesPage();
       if (page === 'pods') return fetchPodsPage();
       if (page === 'metrics') return fetchMetricsPage();
-      return store.refresh();
+      return onRoute(page, function () { return store.refresh(); });
     },
     /**
      * One page opened on an empty cache, as src/plugin.js mounts it: the
@@ -155,7 +173,11 @@ export function amdSchedule(request, clock, timeoutMs) {
     coldOpenPage: function (page, marks) {
       const mk = marks || {};
       // What the page's route mounts (src/plugin.js PAGE_NEEDS).
-      const needs = PAGE_NEEDS[page === 'devicePlugins' ? 'device-plugins' : page];
+      const needs = needsOf(page);
+      if (!needs.pods && detachFeed) {
+        detachFeed();
+        detachFeed = null;
+      }
       let shown = !mk.first;
       function check() {
         if (shown) return;

@@ -71,11 +71,14 @@ export const AMD_NODE_LABELLER_POD_LABEL = 'amdgpu-labeller-ds';
  * Plugin-pod discovery requests. Issued in PARALLEL by the data layer
  * (the reference issues its three selectors serially,
  * src/api/IntelGpuDataContext.tsx:155-165). One set-based selector replaces
- * two equality selectors.
+ * two equality selectors, and it leaves out the operator namespace, which the
+ * second request lists whole: the two answers are disjoint, so on a large
+ * cluster (two or three operand pods per GPU node) no pod is sent twice.
  */
 export const PLUGIN_POD_QUERIES = [
   '/api/v1/pods?labelSelector=' +
-    encodeURIComponent('name in (' + AMD_DEVICE_PLUGIN_POD_LABEL + ',' + AMD_NODE_LABELLER_POD_LABEL + ')'),
+    encodeURIComponent('name in (' + AMD_DEVICE_PLUGIN_POD_LABEL + ',' + AMD_NODE_LABELLER_POD_LABEL + ')') +
+    '&fieldSelector=' + encodeURIComponent('metadata.namespace!=' + AMD_GPU_OPERATOR_NAMESPACE),
   '/api/v1/namespaces/' + AMD_GPU_OPERATOR_NAMESPACE + '/pods',
 ];
 

@@ -74,6 +74,8 @@ describe('constants', () => {
   });
   it('encodes the set-based plugin-pod selector', () => {
     expect(decodeURIComponent(PLUGIN_POD_QUERIES[0])).toContain('name in (amdgpu-dp-ds,amdgpu-labeller-ds)');
+    // disjoint from the namespace request: the operator namespace is left out of the selector's answer
+    expect(decodeURIComponent(PLUGIN_POD_QUERIES[0])).toContain('&fieldSelector=metadata.namespace!=kube-amd-gpu');
     expect(PLUGIN_POD_QUERIES[1]).toBe('/api/v1/namespaces/kube-amd-gpu/pods');
   });
 });

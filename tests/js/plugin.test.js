@@ -64,7 +64,7 @@ function cluster(o) {
     if (q >= 0) {
       const list = lib.lists.Pod;
       const all = list && list[0] ? list[0] : [];
-      return Promise.resolve(kubeList(all.filter((p) => (q === 0 ? isAmdGpuPluginPod(p) : p.metadata.namespace === 'kube-amd-gpu'))));
+      return Promise.resolve(kubeList(all.filter((p) => (q === 0 ? isAmdGpuPluginPod(p) && p.metadata.namespace !== 'kube-amd-gpu' : p.metadata.namespace === 'kube-amd-gpu'))));
     }
     return Promise.reject(Object.assign(new Error('503 Service Unavailable'), { status: 503 }));
   };

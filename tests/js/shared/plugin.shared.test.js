@@ -66,7 +66,7 @@ function cluster(o) {
     // The plugin-pod requests: operator pods by label across namespaces, and the operator namespace.
     const q = PLUGIN_POD_QUERIES.indexOf(path);
     if (q >= 0) {
-      const items = pods.filter((p) => (q === 0 ? isAmdGpuPluginPod(p) : p.metadata.namespace === 'kube-amd-gpu'));
+      const items = pods.filter((p) => (q === 0 ? isAmdGpuPluginPod(p) && p.metadata.namespace !== 'kube-amd-gpu' : p.metadata.namespace === 'kube-amd-gpu'));
       return Promise.resolve({ kind: 'List', metadata: {}, items: items });
     }
     return Promise.reject(Object.assign(new Error('503 Service Unavailable'), { status: 503 }));

@@ -193,6 +193,11 @@ def test_namespaced_pods_and_selectors(server):
     assert len(sel["items"]) == 5
     _, fs = get(server, "/api/v1/pods?fieldSelector=" + urllib.parse.quote("spec.nodeName=" + gpu_node_name(1)))
     assert all(p["spec"]["nodeName"] == gpu_node_name(1) for p in fs["items"])
+    # The plugin's label-selector request leaves out the operator namespace (disjoint from the namespace request).
+    _, every = get(server, "/api/v1/pods")
+    _, rest = get(server, "/api/v1/pods?fieldSelector=" + urllib.parse.quote("metadata.namespace!=kube-amd-gpu"))
+    assert rest["items"] and all(p["metadata"]["namespace"] != "kube-amd-gpu" for p in rest["items"])
+    assert len(rest["items"]) + len(ns["items"]) == len(every["items"])
 
 
 def test_bad_selector_is_400(server):
