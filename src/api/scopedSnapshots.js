@@ -149,7 +149,7 @@ export function createScopedSnapshots(client, state, snaps) {
    */
   function scoped(v, scope, summary, key, small) {
     const st = entry(key);
-    if (state.source === 'node-exporter') return snaps.cluster(v).then(function (m) { return cut(m, scope, summary, key); });
+    if (state.source === 'node-exporter') return snaps.cluster(v).then(function (m) { return cut(m, scope, summary, key, small); });
     return client.withPrometheus(function (base) {
       // Nothing cached yet for a small-cluster fetch before the node list: statics too.
       const withStatic = small && scope.length === 0 ? true : scope.length > 0 && needsStatic(scope);
@@ -177,7 +177,7 @@ export function createScopedSnapshots(client, state, snaps) {
           // came along on a small cluster (one wave); a larger one is read
           // cluster-wide once, then served from that snapshot.
           if (!joinNodeExporterResults(rows).gpus.length) return NOT_SCOPED;
-          return cut(snaps.commit(base, v, nodeExporterQuery(), rows, false), scope, summary, key);
+          return cut(snaps.commit(base, v, nodeExporterQuery(), rows, false), scope, summary, key, small);
         }
         // (No exporter and no amdgpu hwmon: no GPU telemetry — this answer stands.)
         scopeStatics(j, scope, withStatic);
@@ -187,7 +187,7 @@ export function createScopedSnapshots(client, state, snaps) {
     }, function () {
       return staleOrNull(st, STALE_FAILURES, client.invalidate);
     }).then(function (r) {
-      return r === NOT_SCOPED ? snaps.cluster(v).then(function (m) { return cut(m, scope, summary, key); }) : r;
+      return r === NOT_SCOPED ? snaps.cluster(v).then(function (m) { return cut(m, scope, summary, key, small); }) : r;
     });
   }
 
@@ -238,37 +238,43 @@ export function createScopedSnapshots(client, state, snaps) {
     }).then(function (r) { return r === NOT_SCOPED ? snaps.cluster(v) : r; });
   }
 
-  /** A cluster-wide snapshot cut to `scope` (node-exporter source), totals summed here. */
-  function cut(m, scope, summary, key) {
+  /**
+   * A cluster-wide snapshot cut to `scope` (node-exporter source), totals
+   * summed here. A small-cluster fetch (`small`) keeps its meaning: every GPU
+   * when at most SMALL_CLUSTER_NODES nodes report — the page may be asked
+   * before the node list names it, and its key then stays put — else
+   * `scope`'s, flagged `exceeded` so the caller's key follows the names.
+   */
+  function cut(m, scope, summary, key, small) {
     if (!m) return null;
     const st = entry(key);
     if (st.cutOf === m && st.last) return st.last;
-    const inScope = {};
-    for (let i = 0; i < scope.length; i++) inScope[scope[i]] = true;
+    const reporting = {};
+    let count = 0;
+    for (let i = 0; i < m.gpus.length; i++) {
+      if (!reporting[m.gpus[i].nodeName]) {
+        reporting[m.gpus[i].nodeName] = true;
+        count++;
+      }
+    }
+    const whole = !!small && count <= SMALL_CLUSTER_NODES;
+    const inScope = whole ? reporting : {};
+    if (!whole) for (let i = 0; i < scope.length; i++) inScope[scope[i]] = true;
+    const names = whole ? Object.keys(reporting) : scope;
     const xgmi = {};
     const links = {};
-    for (let i = 0; i < scope.length; i++) {
-      if (m.xgmi && m.xgmi[scope[i]]) xgmi[scope[i]] = m.xgmi[scope[i]];
-      if (m.links && m.links[scope[i]]) links[scope[i]] = m.links[scope[i]];
+    for (let i = 0; i < names.length; i++) {
+      if (m.xgmi && m.xgmi[names[i]]) xgmi[names[i]] = m.xgmi[names[i]];
+      if (m.links && m.links[names[i]]) links[names[i]] = m.links[names[i]];
     }
-    let totals;
-    if (summary) {
-      const seen = {};
-      let nodes = 0;
-      for (let i = 0; i < m.gpus.length; i++) {
-        if (!seen[m.gpus[i].nodeName]) {
-          seen[m.gpus[i].nodeName] = true;
-          nodes++;
-        }
-      }
-      totals = Object.assign(summarizeMetrics(m), { nodes: nodes });
-    }
+    const totals = summary ? Object.assign(summarizeMetrics(m), { nodes: count }) : undefined;
     const out = Object.assign({}, m, {
       gpus: m.gpus.filter(function (g) { return inScope[g.nodeName] === true; }),
       xgmi: xgmi,
       links: links,
       scope: scope,
       totals: totals,
+      small: small ? { count: count, limit: SMALL_CLUSTER_NODES, exceeded: !whole } : undefined,
     });
     st.cutOf = m;
     st.last = out;

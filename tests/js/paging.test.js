@@ -472,6 +472,32 @@ describe('metrics client: scoped snapshots', () => {
     expect(m.gpus.map((g) => g.nodeName)).toEqual(['mi355x-000']);
     expect(m.totals.gpus).toBe(1);
   });
+  it('node-exporter source, small-cluster fetch before the node list: every GPU of a small cluster, the page of a larger one', async () => {
+    function neData(nodes) {
+      const ne = { node_uname_info: [] };
+      ne[SERIES.nodeExporter.chips] = [];
+      nodes.forEach((n, k) => {
+        ne.node_uname_info.push({ metric: { __name__: 'node_uname_info', instance: 'i' + k, nodename: n }, value: [0, '1'] });
+        ne[SERIES.nodeExporter.chips].push({ metric: { __name__: 'node_hwmon_chip_names', chip_name: 'amdgpu', instance: 'i' + k, chip: '0000:05:00_0' }, value: [0, '1'] });
+      });
+      return ne;
+    }
+    // 2 nodes: the first answer (no names yet) holds the whole cluster, so the names arriving need no refetch.
+    let s = createMetricsSource({ request: prom({ data: {}, ne: neData(names(2)) }) });
+    let m = await s.fetchGpuMetrics('gauges', { scope: [], summary: true, small: true });
+    expect(m.source).toBe('node-exporter');
+    expect(m.gpus.map((g) => g.nodeName)).toEqual(names(2));
+    expect(m.small).toEqual({ count: 2, limit: 8, exceeded: false });
+    expect(m.totals.nodes).toBe(2);
+    // 12 nodes: more than a page — only the scope's, flagged so the caller's key follows the names.
+    s = createMetricsSource({ request: prom({ data: {}, ne: neData(names(12)) }) });
+    m = await s.fetchGpuMetrics('gauges', { scope: [], summary: true, small: true });
+    expect(m.gpus).toHaveLength(0);
+    expect(m.small.exceeded).toBe(true);
+    m = await s.fetchGpuMetrics('gauges', { scope: names(8), summary: true, small: true });
+    expect(Array.from(new Set(m.gpus.map((g) => g.nodeName)))).toEqual(names(8));
+    expect(m.totals.gpus).toBe(12);
+  });
   it('an empty scope with a summary asks for the totals only', async () => {
     const fake = prom({ data: exporterData(names(2)) });
     const m = await source(fake).fetchGpuMetrics('gauges', { scope: [], summary: true });

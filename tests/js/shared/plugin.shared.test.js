@@ -23,7 +23,7 @@ import * as lib from '@kinvolk/headlamp-plugin/lib';
 import '../../../src/index.tsx';
 import { resetSharedStores } from '../../../src/api/clusterStore.js';
 import { clearViewMemo } from '../../../src/view/pages.js';
-import { invalidateSettings } from '../../../src/api/settings.js';
+import { DEFAULT_SETTINGS, invalidateSettings, saveSettings } from '../../../src/api/settings.js';
 import { DEVICE_CONFIG_LIST_PATH, PLUGIN_POD_QUERIES, isAmdGpuPluginPod } from '../../../src/api/amdgpu.js';
 import { makeDeviceConfig, makeGpuNode, makeGpuPod, makeNode, makePlainPod, makePluginPod } from '../fixtures.js';
 import { exporterData, prom } from '../promFake.js';
@@ -54,7 +54,8 @@ function cluster(o) {
   lib.lists.Node = opt.loading ? [null, null] : [nodes, null];
   // podsLoading: the node list is in, the all-namespaces pod list still in flight.
   lib.lists.Pod = opt.loading || opt.podsLoading ? [null, null] : [pods, null];
-  const fake = prom({ data: exporterData(opt.gpuNodes) });
+  // nodeExporter: no exporter series, node-exporter's amdgpu hwmon chips instead (the fallback source).
+  const fake = opt.nodeExporter ? prom({ data: {}, ne: nodeExporterData(opt.gpuNodes) }) : prom({ data: exporterData(opt.gpuNodes) });
   lib.api.handler = (path) => {
     if (path === DEVICE_CONFIG_LIST_PATH) return Promise.resolve({ kind: 'List', metadata: {}, items: [makeDeviceConfig()] });
     if (path.indexOf('/proxy/api/v1/') >= 0) return fake(path);
@@ -73,6 +74,18 @@ function cluster(o) {
   };
   fake.pods = pods;
   return fake;
+}
+
+/** node-exporter series of GPU nodes: one amdgpu hwmon chip each, node_uname_info naming the node. */
+function nodeExporterData(nodes) {
+  const ne = { node_uname_info: [], node_hwmon_chip_names: [], node_hwmon_power_average_watt: [] };
+  nodes.forEach((n, k) => {
+    const inst = '10.0.0.' + (k + 1) + ':9100';
+    ne.node_uname_info.push({ metric: { __name__: 'node_uname_info', instance: inst, nodename: n }, value: [0, '1'] });
+    ne.node_hwmon_chip_names.push({ metric: { __name__: 'node_hwmon_chip_names', chip_name: 'amdgpu', instance: inst, chip: '0000:05:00_0' }, value: [0, '1'] });
+    ne.node_hwmon_power_average_watt.push({ metric: { __name__: 'node_hwmon_power_average_watt', instance: inst, chip: '0000:05:00_0' }, value: [0, '650'] });
+  });
+  return ne;
 }
 
 const crdCalls = () => lib.api.calls.filter((p) => p === DEVICE_CONFIG_LIST_PATH).length;
@@ -125,6 +138,21 @@ describe('shared: progressive cold open — a page waits only for the lists it d
     expect(r.text()).toContain('GPU Power Summary');
     expect(r.text()).toContain('mi355x-000 — 8 × MI355X');
     expect(r.text()).not.toContain('Loading AMD GPU data...');
+    r.unmount();
+  });
+
+  it('Metrics on a node-exporter-only cluster: the GPU cards from the first answer, one Prometheus query', async () => {
+    // A Prometheus this session has not met (its client is keyed by the settings that shape it).
+    saveSettings(Object.assign({}, DEFAULT_SETTINGS, { requestTimeoutMs: DEFAULT_SETTINGS.requestTimeoutMs + 1 }));
+    const fake = cluster({ nodeExporter: true });
+    const r = render(h(route('/amd-gpu/metrics')));
+    await r.settle();
+    saveSettings(DEFAULT_SETTINGS);
+    expect(r.text()).toContain('mi355x-000 — 1 × MI355X');
+    expect(r.text()).toContain('mi355x-001 — 1 × MI355X');
+    expect(r.text()).not.toContain('fetching telemetry');
+    expect(r.text()).not.toContain('No AMD GPU Metrics in Prometheus');
+    expect(promQueries(fake)).toHaveLength(1);
     r.unmount();
   });
 
