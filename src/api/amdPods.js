@@ -37,13 +37,38 @@ function containerAmdKeys(c) {
   return keys;
 }
 
-/** True if any container, init or regular, requests or limits an `amd.com/*` resource. */
+const hasOwn = Object.prototype.hasOwnProperty;
+
+/** `res` (requests or limits) names an `amd.com/*` resource — no allocation (runs on every pod of the cluster). */
+function hasAmdKey(res) {
+  if (res === null || typeof res !== 'object') return false;
+  for (const k in res) {
+    if (k.indexOf(AMD_RESOURCE_PREFIX) === 0 && hasOwn.call(res, k)) return true;
+  }
+  return false;
+}
+
+/** containerAmdKeys(c).length > 0, without building the list. */
+function containerHasAmd(c) {
+  const r = c !== null && typeof c === 'object' ? c.resources : undefined;
+  if (r === null || typeof r !== 'object') return false;
+  return hasAmdKey(r.requests) || hasAmdKey(r.limits);
+}
+
+/**
+ * True if any container, init or regular, requests or limits an `amd.com/*`
+ * resource. This is the classification every pod of the cluster goes
+ * through when the pod list arrives (37k pods at 1,000 nodes), so it reads
+ * the containers directly and allocates nothing.
+ */
 export function isGpuRequestingPod(pod) {
   if (!isNamedObject(pod)) return false;
-  const cs = get(pod, ['spec', 'containers'], []);
-  const ics = get(pod, ['spec', 'initContainers'], []);
-  for (let i = 0; i < cs.length; i++) if (containerAmdKeys(cs[i]).length > 0) return true;
-  for (let i = 0; i < ics.length; i++) if (containerAmdKeys(ics[i]).length > 0) return true;
+  const spec = pod.spec;
+  if (spec === null || typeof spec !== 'object') return false;
+  const cs = spec.containers;
+  if (cs !== null && cs !== undefined) for (let i = 0; i < cs.length; i++) if (containerHasAmd(cs[i])) return true;
+  const ics = spec.initContainers;
+  if (ics !== null && ics !== undefined) for (let i = 0; i < ics.length; i++) if (containerHasAmd(ics[i])) return true;
   return false;
 }
 
