@@ -27,7 +27,7 @@ from typing import Dict, List, Optional, Tuple
 
 from .promql_parse import (AGGREGATIONS, BIN_PREC, RANGE_FUNCS, RANK_AGGREGATIONS, SET_OPS, Matcher,  # noqa: F401
                            PromQLError, parse)
-from .tsdb import _MUTATIONS, LOOKBACK_S, Labels, Series, TSDB  # noqa: F401
+from .tsdb import _MUTATIONS, LOOKBACK_S, Labels, Series, TSDB, changes_since  # noqa: F401
 
 
 # ---------------------------------------------------------------------------
@@ -423,12 +423,27 @@ def query_range(db: TSDB, q: str, start: float, end: float, step: float):
         return {"status": "error", "errorType": "bad_data", "error": "invalid range"}
     if (end - start) / step > 11000:
         return {"status": "error", "errorType": "bad_data", "error": "exceeded maximum resolution of 11,000 points"}
-    # Per-step results are memoised while no series was pushed (same rule as
-    # query()): a window that slides by one step re-evaluates one step. A real
-    # Prometheus evaluates the whole window in milliseconds; evaluating it
-    # point by point in Python would otherwise dominate the fake's latency.
+    # Per-step results are memoised: a window that slides by one step
+    # re-evaluates one step, and samples pushed since (tsdb.changes_since)
+    # drop only the steps they can change — the ones at or after the pushed
+    # sample, not the whole window. A real Prometheus evaluates the whole
+    # window in milliseconds; evaluating it point by point in Python would
+    # otherwise dominate the fake's latency.
     memo = db._range_cache.get(q)
-    if memo is None or memo[0] != _MUTATIONS[0]:
+    if memo is not None and memo[0] != _MUTATIONS[0]:
+        changed = changes_since(memo[0])
+        if changed is None:
+            memo = None
+        else:
+            steps = memo[1]
+            # Changes are (T, inf): a sample pushed at T; (-inf, X): samples
+            # dropped, seen up to X; (-inf, inf): a new series.
+            lo = min((c[0] for c in changed if c[1] == math.inf), default=math.inf)
+            hi = max((c[1] for c in changed if c[1] != math.inf), default=-math.inf)
+            for t in [t for t in steps if t >= lo or t <= hi]:
+                del steps[t]
+            memo = db._range_cache[q] = (_MUTATIONS[0], steps)
+    if memo is None:
         memo = db._range_cache[q] = (_MUTATIONS[0], {})
     steps = memo[1]
     try:

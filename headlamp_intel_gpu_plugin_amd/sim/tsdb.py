@@ -25,6 +25,33 @@ Labels = Dict[str, str]
 # :func:`query` are valid only while it is unchanged.
 _MUTATIONS = [0]
 
+# What each mutation may have changed, as (mutation count, lo, hi): query
+# results at evaluation times in [lo, hi]. A pushed sample at T changes what
+# is seen at T and later only (samples are appended in time order); a sample
+# dropped from the front of a capped series changes what its lookback window
+# saw; a new series changes everything. Range-query memos (promql.query_range)
+# drop just those steps, so a scrape landing between two refreshes does not
+# make the fake re-evaluate a whole window in Python.
+_CHANGES: List[Tuple[int, float, float]] = []
+_CHANGES_MAX = 200_000
+
+
+def _changed(lo: float, hi: float) -> None:
+    _MUTATIONS[0] += 1
+    _CHANGES.append((_MUTATIONS[0], lo, hi))
+    if len(_CHANGES) > _CHANGES_MAX:
+        del _CHANGES[: _CHANGES_MAX // 2]
+
+
+def changes_since(stamp: int):
+    """The (lo, hi) ranges changed after mutation ``stamp``, or None when the log no longer reaches back that far."""
+    if stamp == _MUTATIONS[0]:
+        return []
+    if not _CHANGES or _CHANGES[0][0] > stamp + 1:
+        return None
+    i = bisect.bisect_right(_CHANGES, (stamp, math.inf, math.inf))
+    return [(lo, hi) for _, lo, hi in _CHANGES[i:]]
+
 
 class Series:
     """One time series: labels + samples.
@@ -55,15 +82,17 @@ class Series:
         return self._json
 
     def push(self, t: float, v: float) -> None:
-        _MUTATIONS[0] += 1
         if self.ts and t <= self.ts[-1]:
             if t == self.ts[-1]:
+                _changed(t, math.inf)
                 self.vs[-1] = v
             return
+        _changed(t, math.inf)
         self.ts.append(t)
         self.vs.append(v)
         if len(self.ts) > self.cap:
             drop = len(self.ts) - self.cap
+            _changed(-math.inf, self.ts[drop - 1] + LOOKBACK_S)
             del self.ts[:drop]
             del self.vs[:drop]
 
@@ -150,7 +179,7 @@ class TSDB:
         if key in self._index:
             return self._index[key]
         self._index[key] = series
-        _MUTATIONS[0] += 1
+        _changed(-math.inf, math.inf)
         series.seq = len(self._index)
         if series.fn is not None:
             self._fn_intervals.add(series.interval)

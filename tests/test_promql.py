@@ -189,6 +189,46 @@ def test_instant_cache_sees_pushes_and_interval_changes():
     assert body["data"]["result"][0]["value"][0] == 107.5  # eval timestamp is current, not cached
 
 
+
+def test_range_memo_keeps_steps_a_push_cannot_change():
+    """A push between two range queries re-evaluates only the steps at or after the pushed sample, and the
+    answer equals a fresh evaluation (cache cleared)."""
+    db = promql.TSDB()
+    live = db.add(promql.Series({"__name__": "gpu_power_usage", "hostname": "n0"}))
+    db.add(promql.Series({"__name__": "gpu_power_usage", "hostname": "n1"}, fn=lambda t: t, interval=15))
+    for t in range(0, 600, 10):
+        live.push(float(t), float(t) / 10)
+    q = "sum by (hostname) (gpu_power_usage)"
+    first = json.loads(promql.query_range(db, q, 0.0, 600.0, 30.0))
+    steps = db._range_cache[q][1]
+    assert len(steps) == 21
+    before = {t: steps[t] for t in steps}
+    live.push(605.0, 99.0)  # changes what is seen from t = 605 on
+    again = json.loads(promql.query_range(db, q, 0.0, 630.0, 30.0))
+    steps = db._range_cache[q][1]
+    assert all(steps[t] is before[t] for t in before if t < 605.0)  # reused, not re-evaluated
+    db._range_cache.clear()
+    fresh = json.loads(promql.query_range(db, q, 0.0, 630.0, 30.0))
+    assert again == fresh
+    assert first["data"]["result"][0]["values"][:21] == fresh["data"]["result"][0]["values"][:21]
+    # a new series changes every step
+    db.add(promql.Series({"__name__": "gpu_power_usage", "hostname": "n2"}, fn=lambda t: 1.0, interval=15))
+    promql.query_range(db, q, 0.0, 630.0, 30.0)
+    assert len(json.loads(promql.query_range(db, q, 0.0, 630.0, 30.0))["data"]["result"]) == 3
+
+
+def test_range_memo_drops_steps_that_saw_dropped_samples():
+    db = promql.TSDB()
+    s = db.add(promql.Series({"__name__": "x"}, cap=5))
+    for t in range(0, 50, 10):
+        s.push(float(t), 1.0)
+    assert len(json.loads(promql.query_range(db, "x", 0.0, 40.0, 10.0))["data"]["result"][0]["values"]) == 5
+    s.push(50.0, 2.0)  # drops the sample at 0: what t in [0, 300] saw may change
+    again = json.loads(promql.query_range(db, "x", 0.0, 50.0, 10.0))
+    db._range_cache.clear()
+    assert again == json.loads(promql.query_range(db, "x", 0.0, 50.0, 10.0))
+
+
 # ---- set operators and label_replace (the paged views' scoped + summary queries) ----
 
 def test_or_keeps_lhs_and_adds_unmatched_rhs_ignoring_the_name(db):
