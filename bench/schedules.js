@@ -24,21 +24,32 @@ export function amdSchedule(request, clock, timeoutMs) {
   }
   const clk = clock || hiResClock;
   const store = createClusterStore({ request: request, onTrace: onTrace, clock: clk, timeoutMs: timeoutMs });
-  // The pod list feed the routes that draw pods mount (providerCore.js
-  // PodListFeed): attached while such a page is shown. A route without it
-  // (Device Plugins, Metrics: plugin.js PAGE_NEEDS) runs with it detached, so
-  // its refresh asks what the shipped route asks (Device Plugins: the
-  // DeviceConfigs and the plugin-pod requests).
+  // The feeds a route mounts (providerCore.js PodListFeed / OperatorPodFeed,
+  // plugin.js PAGE_NEEDS): the all-namespaces pod list is attached while a
+  // page that draws pods is shown; Device Plugins mounts the operator pods'
+  // own lists instead. A page's refresh runs with its route's feeds, so it
+  // asks what the shipped route asks (Device Plugins: the DeviceConfigs alone,
+  // its operator pods being watched).
   let detachFeed = store.attachPodFeed();
   function needsOf(page) {
     return PAGE_NEEDS[page === 'devicePlugins' ? 'device-plugins' : page];
   }
-  function onRoute(page, run) {
-    if (needsOf(page).pods || !detachFeed) return run();
+  /** Switch the attached feeds to `page`'s route; returns a function restoring the pod list feed. */
+  function mountFeeds(page) {
+    const needs = needsOf(page);
+    if (needs.pods || !detachFeed) return function () {};
     detachFeed();
     detachFeed = null;
-    return run().then(function (v) {
+    const detachOps = needs.operatorPods ? store.attachOperatorFeed() : null;
+    return function () {
+      if (detachOps) detachOps();
       detachFeed = store.attachPodFeed();
+    };
+  }
+  function onRoute(page, run) {
+    const restore = mountFeeds(page);
+    return run().then(function (v) {
+      restore();
       return v;
     });
   }
@@ -174,10 +185,7 @@ export function amdSchedule(request, clock, timeoutMs) {
       const mk = marks || {};
       // What the page's route mounts (src/plugin.js PAGE_NEEDS).
       const needs = needsOf(page);
-      if (!needs.pods && detachFeed) {
-        detachFeed();
-        detachFeed = null;
-      }
+      mountFeeds(page); // a fresh schedule per open: nothing to restore
       let shown = !mk.first;
       function check() {
         if (shown) return;
@@ -188,7 +196,9 @@ export function amdSchedule(request, clock, timeoutMs) {
         mk.first();
       }
       const off = store.subscribe(check);
-      const lists = store.loadLists({ nodes: needs.nodes, pods: needs.pods });
+      // The list requests of the watches the route mounts.
+      const lists = Promise.all([store.loadLists({ nodes: needs.nodes, pods: needs.pods }),
+        needs.operatorPods && !needs.pods ? store.loadOperatorPods() : null]);
       const crd = needs.crd ? store.refresh() : Promise.resolve();
       // The page's metrics hook runs from the first render (pages.js
       // telemetryScope) and once more if the node list changes its key.

@@ -83,6 +83,7 @@ export {
   pct,
   pctToColor,
   pctToStatus,
+  OPERATOR_POD_LISTS,
   PLUGIN_POD_QUERIES,
   unwrapAll,
   unwrapKubeObject,

@@ -46,81 +46,12 @@ import {
   patchClusterIndex,
 } from './amdgpu.js';
 import { createListTracker } from './listCache.js';
+import { DEFAULT_REQUEST_TIMEOUT_MS, defaultClock, isAbsent, sameObjects, withTimeout } from './requests.js';
 
-export const DEFAULT_REQUEST_TIMEOUT_MS = 2000;
+export { DEFAULT_REQUEST_TIMEOUT_MS, fetchNodePods, isAbsent, nodePodsPath, nodePodsSelector, sameObjects, withTimeout } from './requests.js';
+
 /** Time limit of a whole-cluster node / pod list (loadLists). */
 export const LIST_TIMEOUT_MS = 60000;
-
-/**
- * True when two lists hold the same Kubernetes objects at the same versions
- * (uid + resourceVersion, falling back to a JSON comparison for objects
- * without a resourceVersion).
- */
-export function sameObjects(a, b) {
-  if (a === b) return true;
-  if (!a || !b || a.length !== b.length) return false;
-  for (let i = 0; i < a.length; i++) {
-    const ma = a[i] && a[i].metadata;
-    const mb = b[i] && b[i].metadata;
-    if (!ma || !mb) return false;
-    if (ma.resourceVersion && mb.resourceVersion) {
-      if (ma.uid !== mb.uid || ma.resourceVersion !== mb.resourceVersion) return false;
-    } else if (JSON.stringify(a[i]) !== JSON.stringify(b[i])) {
-      return false;
-    }
-  }
-  return true;
-}
-
-const defaultClock = {
-  setTimeout: function (fn, ms) { return setTimeout(fn, ms); },
-  clearTimeout: function (h) { clearTimeout(h); },
-  now: function () { return Date.now(); },
-};
-
-/**
- * True when a failed request proves the resource is not there for this user
- * (404 / 403 / 401), as opposed to a timeout or a server / network error.
- * Headlamp's ApiProxy errors carry the HTTP status in `status`.
- */
-export function isAbsent(err) {
-  const st = err && (err.status || (err.response && err.response.status));
-  return st === 404 || st === 403 || st === 401;
-}
-
-/**
- * Race `promise` against a timer; the timer is always cleared.
- * @template T
- * @param {Promise<T>} promise
- * @param {number} ms
- * @param {{setTimeout: Function, clearTimeout: Function}} [clock]
- * @returns {Promise<T>}
- */
-export function withTimeout(promise, ms, clock) {
-  const c = clock || defaultClock;
-  return new Promise(function (resolve, reject) {
-    let done = false;
-    const h = c.setTimeout(function () {
-      if (done) return;
-      done = true;
-      reject(new Error('Request timed out after ' + ms + 'ms'));
-    }, ms);
-    Promise.resolve(promise).then(
-      function (v) {
-        if (done) return;
-        done = true;
-        c.clearTimeout(h);
-        resolve(v);
-      },
-      function (e) {
-        if (done) return;
-        done = true;
-        c.clearTimeout(h);
-        reject(e);
-      }
-    );
-  });
-}
 
 /**
  * @typedef {Object} ClusterSnapshot
@@ -176,6 +107,11 @@ export function createClusterStore(opts) {
     crdForbidden: false, // the CRD list answered 401 / 403: RBAC, not a missing operator
     pluginPods: [], // from the plugin-pod queries (used when the pod list is not available or not watched)
     pluginPodsKnown: false, // s.pluginPods holds an answer (queried, or the watched list's last word)
+    // The operator pods by their own scoped lists + watches (providerCore.js
+    // OperatorPodFeed: the operator namespace, the plugin labels elsewhere) —
+    // what the Device Plugins route mounts instead of the all-namespaces list.
+    opPods: null,
+    opPodsState: 'unknown',
     // Where each list stands: 'unknown' (never fed: harness/tests),
     // 'pending' (a list/watch is in flight), 'ready', or 'error'. An errored
     // list (e.g. pods forbidden cluster-wide) is settled: the page leaves its
@@ -200,6 +136,7 @@ export function createClusterStore(opts) {
   // plugin-pod requests again.
   let podFeeds = 0;
   let feedsAttached = false;
+  let opFeeds = 0; // operator pod feeds mounted right now
   let version = 0;
   const listeners = [];
 
@@ -261,15 +198,26 @@ export function createClusterStore(opts) {
    * they come from the PLUGIN_POD_QUERIES requests.
    */
   function pluginPods() {
-    if (s.podsState !== 'ready' || !s.pods || !podsLive()) return s.pluginPods;
-    return memoPluginPods;
+    if (s.podsState === 'ready' && s.pods && podsLive()) return memoPluginPods;
+    if (opFeeds > 0 && s.opPodsState === 'ready') return s.opPods;
+    return s.pluginPods;
   }
   /** The pod list is kept current (a feed is mounted, or no feed ever was: see podFeeds). */
   function podsLive() {
     return podFeeds > 0 || !feedsAttached;
   }
+  /** The all-namespaces pod list is there or on its way, and kept current. */
+  function listLive() {
+    return s.podsState !== 'unknown' && s.podsState !== 'error' && podsLive();
+  }
+  /** An operator pod feed is mounted and has not failed: its watches keep the operator pods current. */
+  function opLive() {
+    return opFeeds > 0 && s.opPodsState !== 'error';
+  }
   function pluginPodsLoading() {
     if (podsLive() && s.podsState !== 'unknown') return !settled(s.podsState);
+    // While the operator feed's first lists are in flight, a known answer stays shown.
+    if (opLive() && s.opPodsState !== 'unknown') return s.opPodsState === 'pending' && !s.pluginPodsKnown;
     return !s.pluginPodsKnown;
   }
   function index(n, p) {
@@ -381,7 +329,9 @@ export function createClusterStore(opts) {
         return { ok: isAbsent(e) ? false : null, items: [], forbidden: st === 403 || st === 401 };
       }
     );
-    const needPods = s.podsState === 'unknown' || s.podsState === 'error' || !podsLive();
+    // The plugin-pod requests run only when no watch delivers operator pods:
+    // neither the all-namespaces pod list nor the operator pod feed.
+    const needPods = !listLive() && !opLive();
     podsQueried = needPods;
     const pods = needPods ? queryPluginPods() : Promise.resolve(null);
     const run = Promise.all([crd, pods]).then(
@@ -509,6 +459,75 @@ export function createClusterStore(opts) {
     };
   }
 
+  /**
+   * An operator pod feed mounted (providerCore.js OperatorPodFeed); returns
+   * its detach. While one is mounted its lists + watches are the operator
+   * pods' source (unless the all-namespaces list is watched too) and a
+   * refresh is the CRD request alone; after the last unmounts its answer is
+   * kept as the last known one, as for attachPodFeed.
+   */
+  function attachOperatorFeed() {
+    opFeeds++;
+    let attached = true;
+    if (opFeeds === 1 && s.opPodsState === 'ready') emit();
+    return function detach() {
+      if (!attached) return;
+      attached = false;
+      opFeeds--;
+      if (opFeeds > 0) return;
+      if (s.opPodsState === 'ready' && s.opPods) commitQueriedPods(s.opPods);
+      emit();
+    };
+  }
+
+  /**
+   * Feed the operator pod lists (already unwrapped, filtered to operator
+   * pods and deduplicated): `items` null while they are in flight. A list
+   * already held stays while a re-mounted feed reports "no items yet".
+   */
+  function setOperatorPods(items, error) {
+    const next = items ? (Array.isArray(items) ? items : []) : null;
+    const state = error ? 'error' : next ? 'ready' : 'pending';
+    if (state === 'pending' && (s.opPodsState === 'ready' || s.opPodsState === 'pending')) return;
+    const wasError = s.opPodsState === 'error';
+    s.opPodsState = state;
+    if (next) s.opPods = sameObjects(s.opPods, next) ? s.opPods : next;
+    emit();
+    // Both scoped lists failed: the plugin-pod requests are the fallback.
+    if (state === 'error' && !wasError && !listLive() && !(s.refreshing && podsQueried)) {
+      queryPluginPods().then(function (pods) {
+        if (s.opPodsState !== 'error') return;
+        commitQueriedPods(pods);
+        emit();
+      });
+    }
+  }
+
+  /**
+   * Fetch the operator pod lists directly (the list requests an operator pod
+   * feed's watches start with), for clients without Headlamp's hooks (the
+   * benchmark): the plugin-pod requests, fed through setOperatorPods.
+   */
+  function loadOperatorPods() {
+    if (s.opPodsState === 'unknown') s.opPodsState = 'pending';
+    const lists = podQueries.map(function (path, i) {
+      return traced('operator-pods-' + i, path).then(
+        function (list) { return { items: isKubeList(list) ? filterAmdGpuPluginPods(list.items) : [] }; },
+        function (e) { return { error: e instanceof Error ? e.message : String(e) }; }
+      );
+    });
+    return Promise.all(lists).then(function (rs) {
+      let found = [];
+      let failed = 0;
+      for (let i = 0; i < rs.length; i++) {
+        if (rs[i].error) failed++;
+        else found = found.concat(rs[i].items);
+      }
+      if (failed === rs.length) setOperatorPods(null, rs[0].error);
+      else setOperatorPods(dedupePods(found), null);
+    });
+  }
+
   function subscribe(fn) {
     listeners.push(fn);
     return function () {
@@ -531,7 +550,7 @@ export function createClusterStore(opts) {
     // Operator pods nobody knows: no pod list is watched and no refresh asked
     // the plugin-pod requests (a route without the pod list mounted after one
     // whose list never arrived) — fresh DeviceConfigs alone do not do.
-    const podsMissing = !podsLive() && !s.pluginPodsKnown;
+    const podsMissing = !podsLive() && !opLive() && !s.pluginPodsKnown;
     if (s.refreshing && inflight && !(podsMissing && !podsQueried)) return inflight;
     const age = s.lastUpdated === null ? Infinity : clock.now() - s.lastUpdated;
     if (age < (maxAgeMs === undefined ? 0 : maxAgeMs) && !podsMissing) return Promise.resolve();
@@ -544,6 +563,9 @@ export function createClusterStore(opts) {
     setNodes: setNodes,
     setPods: setPods,
     attachPodFeed: attachPodFeed,
+    attachOperatorFeed: attachOperatorFeed,
+    setOperatorPods: setOperatorPods,
+    loadOperatorPods: loadOperatorPods,
     refresh: refresh,
     revalidate: revalidate,
     loadLists: loadLists,
@@ -585,58 +607,6 @@ export function sharedStores() {
 
 export function resetSharedStores() {
   for (const k in shared) delete shared[k];
-}
-
-/** The field selector of one node's pods (the apiserver filters: O(pods on the node)). */
-export function nodePodsSelector(nodeName) {
-  return 'spec.nodeName=' + nodeName;
-}
-
-/** Path of one node's pods: the list request of a field-selected list + watch. */
-export function nodePodsPath(nodeName) {
-  return '/api/v1/pods?fieldSelector=' + encodeURIComponent(nodePodsSelector(nodeName));
-}
-
-/**
- * The pods of ONE node by one field-selected list: the request a cold Node
- * detail page's scoped list + watch starts with (providerCore.js
- * useNodePods), for clients without Headlamp's hooks (the benchmark, the
- * terminal client) — instead of the cluster-wide node + pod lists and the
- * CRD / operator-pod requests the reference's provider mounts there
- * (reference src/index.tsx:152-160, IntelGpuDataContext.tsx:98-165).
- * Resolves to the node's pods; rejects with the request's error.
- * @param {(path: string) => Promise<any>} request
- * @param {string} nodeName
- * @param {number} [timeoutMs]
- * @param {{setTimeout: Function, clearTimeout: Function}} [clock]
- * @returns {Promise<any[]>}
- */
-export function fetchNodePods(request, nodeName, timeoutMs, clock) {
-  return withTimeout(sharedRequest(request, nodePodsPath(nodeName)), timeoutMs || DEFAULT_REQUEST_TIMEOUT_MS,
-    clock || defaultClock).then(function (l) {
-    return isKubeList(l) ? l.items : [];
-  });
-}
-
-// In-flight requests per request function and path: callers asking for the
-// same path while it is in flight share one request (two sections of the same
-// node, or React 18 StrictMode mounting an effect twice in development).
-const inFlight = typeof WeakMap === 'function' ? new WeakMap() : null;
-
-function sharedRequest(request, path) {
-  if (!inFlight) return request(path);
-  let paths = inFlight.get(request);
-  if (!paths) {
-    paths = new Map();
-    inFlight.set(request, paths);
-  }
-  const pending = paths.get(path);
-  if (pending) return pending;
-  const p = Promise.resolve(request(path));
-  const done = function () { if (paths.get(path) === p) paths.delete(path); };
-  paths.set(path, p);
-  p.then(done, done);
-  return p;
 }
 
 /** True when the store has both cluster lists (a plugin page fed it): detail views can read it. */

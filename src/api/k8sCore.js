@@ -75,12 +75,25 @@ export const AMD_NODE_LABELLER_POD_LABEL = 'amdgpu-labeller-ds';
  * second request lists whole: the two answers are disjoint, so on a large
  * cluster (two or three operand pods per GPU node) no pod is sent twice.
  */
+export const PLUGIN_POD_LABEL_SELECTOR = 'name in (' + AMD_DEVICE_PLUGIN_POD_LABEL + ',' + AMD_NODE_LABELLER_POD_LABEL + ')';
+export const PLUGIN_POD_FIELD_SELECTOR = 'metadata.namespace!=' + AMD_GPU_OPERATOR_NAMESPACE;
+
 export const PLUGIN_POD_QUERIES = [
-  '/api/v1/pods?labelSelector=' +
-    encodeURIComponent('name in (' + AMD_DEVICE_PLUGIN_POD_LABEL + ',' + AMD_NODE_LABELLER_POD_LABEL + ')') +
-    '&fieldSelector=' + encodeURIComponent('metadata.namespace!=' + AMD_GPU_OPERATOR_NAMESPACE),
+  '/api/v1/pods?labelSelector=' + encodeURIComponent(PLUGIN_POD_LABEL_SELECTOR) +
+    '&fieldSelector=' + encodeURIComponent(PLUGIN_POD_FIELD_SELECTOR),
   '/api/v1/namespaces/' + AMD_GPU_OPERATOR_NAMESPACE + '/pods',
 ];
+
+/**
+ * The same two selections as list + watch options of Headlamp's
+ * `Pod.useList()` (providerCore.js OperatorPodFeed), in PLUGIN_POD_QUERIES
+ * order: what the Device Plugins route watches instead of every pod of the
+ * cluster. (Query options of `useList`: verify against the Headlamp release.)
+ */
+export const OPERATOR_POD_LISTS = Object.freeze([
+  Object.freeze({ namespace: '', labelSelector: PLUGIN_POD_LABEL_SELECTOR, fieldSelector: PLUGIN_POD_FIELD_SELECTOR }),
+  Object.freeze({ namespace: AMD_GPU_OPERATOR_NAMESPACE }),
+]);
 
 /** MI355X platform facts (MI355X_MICROARCH.md chip-level table). */
 export const MI355X = Object.freeze({

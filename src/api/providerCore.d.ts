@@ -31,6 +31,10 @@ export interface ClusterStore {
   setPods(items: unknown[] | null, error: string | null): void;
   /** A pod list feed mounted; returns its detach (operator pods come from the plugin-pod requests once none is). */
   attachPodFeed(): () => void;
+  /** An operator pod feed mounted (its own scoped lists + watches); returns its detach. */
+  attachOperatorFeed(): () => void;
+  /** Feed the operator pods of the scoped lists (null while in flight). */
+  setOperatorPods(items: unknown[] | null, error: string | null): void;
   refresh(): Promise<void>;
   revalidate(maxAgeMs?: number): Promise<void>;
   loadLists(): Promise<void>;

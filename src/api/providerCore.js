@@ -25,7 +25,7 @@
  */
 
 import { createClusterStore, getSharedStore, nodePodsSelector, storeIsWarm } from './clusterStore.js';
-import { filterGpuRequestingPods, get, unwrapAll } from './amdgpu.js';
+import { dedupePods, filterAmdGpuPluginPods, filterGpuRequestingPods, get, OPERATOR_POD_LISTS, unwrapAll } from './amdgpu.js';
 import { createMetricsSource } from './metrics.js';
 import { clusterKey as defaultClusterKey } from './cluster.js';
 import { POLL_MISS, createPoller, loadSettings as defaultLoadSettings, prometheusCandidates, seriesStepSec } from './settings.js';
@@ -34,7 +34,7 @@ import { POLL_MISS, createPoller, loadSettings as defaultLoadSettings, prometheu
 export const STALE_MS = 5000;
 
 /** What a provider feeds by default: both lists and the DeviceConfigs (the reference's provider). */
-const ALL_NEEDS = Object.freeze({ nodes: true, pods: true, crd: true });
+const ALL_NEEDS = Object.freeze({ nodes: true, pods: true, crd: true, operatorPods: false });
 
 export const PROMETHEUS_UNREACHABLE =
   'Could not reach Prometheus. Ensure kube-prometheus-stack is installed in the monitoring namespace.';
@@ -167,6 +167,41 @@ export function createProviderCore(React, lib, deps) {
   }
 
   /**
+   * The operator pods by their own lists + watches (amdgpu.js
+   * OPERATOR_POD_LISTS: the plugin labels outside the operator namespace,
+   * and the operator namespace) — what a page that draws operator pods but
+   * no other pod mounts (Device Plugins), instead of the all-namespaces list.
+   * Live like the reference's provider lists (IntelGpuDataContext.tsx:98-99),
+   * whose operator pods only changed on a Refresh click (:142-165). A
+   * failing list contributes nothing, as a failing selector request does in
+   * the reference (:162-164); both failing hand over to the plugin-pod
+   * requests (clusterStore.js setOperatorPods).
+   */
+  function OperatorPodFeed(props) {
+    const store = props.store;
+    useEffect(function () { return store.attachOperatorFeed(); }, [store]);
+    const a = useListOf(lib.K8s.ResourceClasses.Pod, OPERATOR_POD_LISTS[0]);
+    const b = useListOf(lib.K8s.ResourceClasses.Pod, OPERATOR_POD_LISTS[1]);
+    const fed = useMemo(function () {
+      const lists = [a, b];
+      let pending = false;
+      let failed = 0;
+      let found = [];
+      for (let i = 0; i < lists.length; i++) {
+        if (lists[i][1]) failed++;
+        else if (!lists[i][0]) pending = true;
+        else found = found.concat(filterAmdGpuPluginPods(unwrapAll(lists[i][0])));
+      }
+      if (failed === lists.length) return { items: null, error: errorText(a[1]) };
+      return { items: pending ? null : dedupePods(found), error: null };
+    }, [a[0], a[1], b[0], b[1]]);
+    useEffect(function () {
+      store.setOperatorPods(fed.items, fed.error);
+    }, [store, fed]);
+    return null;
+  }
+
+  /**
    * The pod list + watch fed into the current cluster's store, mounted by a
    * page whose provider does not feed pods when one of its views needs them
    * after all (the Metrics page in an allocation order).
@@ -177,7 +212,8 @@ export function createProviderCore(React, lib, deps) {
 
   /**
    * The cluster context of a page. `props.needs` says what the page draws
-   * ({nodes, pods, crd}, each default true): only those are subscribed to
+   * ({nodes, pods, crd}, each default true; `operatorPods`, default false:
+   * the operator pods' own lists where the pod list is not mounted): only those are subscribed to
    * and fetched — the Metrics page mounts the node list alone, never the
    * all-namespaces pod list (tens of MB, parsed on the browser's main thread
    * on a large cluster) nor the DeviceConfig request; the reference mounts
@@ -192,6 +228,7 @@ export function createProviderCore(React, lib, deps) {
     const wantNodes = needs.nodes !== false;
     const wantPods = needs.pods !== false;
     const wantCrd = needs.crd !== false;
+    const wantOps = needs.operatorPods === true && !wantPods;
 
     // Track 2 — imperative CRD / operator-pod fetch, shared and deduplicated.
     useEffect(function () {
@@ -209,15 +246,17 @@ export function createProviderCore(React, lib, deps) {
 
     const snapshot = React.useSyncExternalStore(store.subscribe, store.getSnapshot);
     const value = useMemo(function () {
-      const loading = (wantCrd && snapshot.crdLoading) || (wantNodes && snapshot.nodesLoading) || (wantPods && snapshot.podsLoading);
+      const loading = (wantCrd && snapshot.crdLoading) || (wantNodes && snapshot.nodesLoading) ||
+        (wantPods && snapshot.podsLoading) || (wantOps && snapshot.pluginPodsLoading);
       return Object.assign({}, snapshot, { loading: !!loading, refresh: function () { store.refresh(); } });
-    }, [snapshot, store, wantCrd, wantNodes, wantPods]);
+    }, [snapshot, store, wantCrd, wantNodes, wantPods, wantOps]);
 
     // Track 1 — reactive lists from Headlamp (all namespaces for pods), as
     // feed components next to the page, so a page mounts only the watches it draws.
     return h(Context.Provider, { value: value },
       wantNodes ? h(NodeListFeed, { store: store }) : null,
       wantPods ? h(PodListFeed, { store: store }) : null,
+      wantOps ? h(OperatorPodFeed, { store: store }) : null,
       props.children);
   }
 

@@ -7,7 +7,7 @@ import type { Renderer } from './view/react';
 export const PLUGIN_NAME: string;
 
 /** What each page draws, hence what its route mounts (lists, DeviceConfig request). */
-export const PAGE_NEEDS: Readonly<Record<'overview' | 'device-plugins' | 'nodes' | 'pods' | 'metrics', Readonly<{ nodes: boolean; pods: boolean; crd: boolean }>>>;
+export const PAGE_NEEDS: Readonly<Record<'overview' | 'device-plugins' | 'nodes' | 'pods' | 'metrics', Readonly<{ nodes: boolean; pods: boolean; crd: boolean; operatorPods?: boolean }>>>;
 
 export interface PluginEnv {
   React: unknown;

@@ -47,14 +47,15 @@ export const PLUGIN_NAME = 'amd-gpu';
  * What each page draws, hence what its route mounts (providerCore.js
  * AmdGpuDataProvider): Metrics needs the node list only (names of the page,
  * nodes reporting); GPU Nodes and GPU Pods need both lists but not the
- * DeviceConfigs; Device Plugins the DeviceConfigs only — its operator pods
- * come from the plugin-pod requests sent with them (clusterStore.js
- * attachPodFeed), not from the all-namespaces pod list; Overview everything.
+ * DeviceConfigs; Device Plugins the DeviceConfigs and the operator pods'
+ * own lists + watches (providerCore.js OperatorPodFeed: the operator
+ * namespace and the plugin labels), not the all-namespaces pod list;
+ * Overview everything.
  * The reference mounts all of it on every route (src/index.tsx:87-145).
  */
 export const PAGE_NEEDS = Object.freeze({
   overview: Object.freeze({ nodes: true, pods: true, crd: true }),
-  'device-plugins': Object.freeze({ nodes: false, pods: false, crd: true }),
+  'device-plugins': Object.freeze({ nodes: false, pods: false, crd: true, operatorPods: true }),
   nodes: Object.freeze({ nodes: true, pods: true, crd: false }),
   pods: Object.freeze({ nodes: true, pods: true, crd: false }),
   metrics: Object.freeze({ nodes: true, pods: false, crd: false }),

@@ -495,6 +495,46 @@ describe('pod list feeds: operator pods from the watched list, else from the plu
     expect(request).toHaveBeenCalledTimes(2 + PLUGIN_POD_QUERIES.length);
   });
 
+  it('an operator pod feed: its lists are the operator pods, a refresh is the CRD request alone', async () => {
+    const request = router(baseRoutes());
+    const store = createClusterStore({ request });
+    const detach = store.attachOperatorFeed();
+    store.setOperatorPods(null, null);
+    expect(store.getSnapshot().pluginPodsLoading).toBe(true);
+    store.setOperatorPods([makePluginPod('dp-watched')], null);
+    expect(store.getSnapshot().pluginPodsLoading).toBe(false);
+    expect(ppNames(store)).toEqual(['dp-watched']);
+    await store.refresh();
+    expect(queried(request)).toBe(0);
+    store.setOperatorPods(null, null); // a re-mounted list reporting "no items yet" keeps what is held
+    expect(ppNames(store)).toEqual(['dp-watched']);
+    detach();
+    expect(ppNames(store)).toEqual(['dp-watched']); // kept as the last known answer
+    await store.refresh(); // nothing watches them now
+    expect(queried(request)).toBe(PLUGIN_POD_QUERIES.length);
+  });
+
+  it('both operator pod lists failing hand over to the plugin-pod requests', async () => {
+    const request = router(baseRoutes());
+    const store = createClusterStore({ request });
+    store.attachOperatorFeed();
+    store.setOperatorPods(null, 'pods is forbidden');
+    await new Promise((r) => setTimeout(r, 0));
+    await store.settled();
+    expect(queried(request)).toBe(PLUGIN_POD_QUERIES.length);
+    expect(ppNames(store)).toEqual(['dp-0', 'dp-1']);
+  });
+
+  it('loadOperatorPods feeds the operator pod lists by their list requests', async () => {
+    const request = router(baseRoutes());
+    const store = createClusterStore({ request });
+    store.attachOperatorFeed();
+    await Promise.all([store.loadOperatorPods(), store.refresh()]);
+    expect(request).toHaveBeenCalledTimes(1 + PLUGIN_POD_QUERIES.length);
+    expect(ppNames(store)).toEqual(['dp-0', 'dp-1']);
+    expect(store.getSnapshot().pluginPodsLoading).toBe(false);
+  });
+
   it('a store no feed ever attached to (harness, terminal client) treats setPods / loadLists as current', async () => {
     const request = router(baseRoutes());
     const store = createClusterStore({ request });

@@ -88,6 +88,9 @@ function nodeExporterData(nodes) {
   return ne;
 }
 
+/** A list hook call for every pod of the cluster (all namespaces, no selector). */
+const allPods = (o) => !!o && o.namespace === '' && !o.labelSelector && !o.fieldSelector;
+
 const crdCalls = () => lib.api.calls.filter((p) => p === DEVICE_CONFIG_LIST_PATH).length;
 const promQueries = (fake) => fake.mock.calls.map((c) => decodeURIComponent(c[0])).filter((p) => /\/query\?query=(?!1$)/.test(p));
 
@@ -190,34 +193,57 @@ describe('shared: progressive cold open — a page waits only for the lists it d
     r.unmount();
   });
 
-  it('Device Plugins renders whole — DeviceConfig cards and operator pods — with both lists pending, no pod list mounted', async () => {
-    cluster({ loading: true });
+  it('Device Plugins watches the operator pods alone: no all-namespaces pod list, no node list, no plugin-pod requests', async () => {
+    cluster();
     const r = render(h(route('/amd-gpu/device-plugins')));
     await r.settle();
     expect(r.text()).toContain('DeviceConfig: gpu-operator');
     expect(r.text()).toContain('amdgpu-dp-0');
     expect(r.text()).not.toContain('Loading operator pods...');
-    expect(lib.lists.calls.Pod).toHaveLength(0);
-    PLUGIN_POD_QUERIES.forEach((q) => expect(lib.api.calls).toContain(q));
+    expect(lib.lists.calls.Node).toHaveLength(0);
+    expect(lib.lists.calls.Pod.some(allPods)).toBe(false);
+    expect(lib.lists.calls.Pod.some((o) => o && o.namespace === 'kube-amd-gpu')).toBe(true);
+    expect(lib.lists.calls.Pod.some((o) => o && o.labelSelector === 'name in (amdgpu-dp-ds,amdgpu-labeller-ds)')).toBe(true);
+    expect(PLUGIN_POD_QUERIES.some((q) => lib.api.calls.indexOf(q) >= 0)).toBe(false);
     r.unmount();
   });
 
-  it('Device Plugins after a page that watched the pods: the list\'s operator pods at once, the requests on Refresh', async () => {
+  it('Device Plugins: operator pods are live (a new one shows without Refresh) and Refresh is the DeviceConfig request alone', async () => {
     const fake = cluster();
+    const r = render(h(route('/amd-gpu/device-plugins')));
+    await r.settle();
+    const n = lib.api.calls.length;
+    lib.lists.Pod = [fake.pods.concat([makePluginPod('amdgpu-dp-1', { node: 'mi355x-001' })]), null];
+    r.rerender(h(route('/amd-gpu/device-plugins')));
+    await r.settle();
+    expect(r.text()).toContain('amdgpu-dp-1');
+    r.click(r.byLabel('Refresh device plugin data'));
+    await r.settle();
+    expect(lib.api.calls.slice(n)).toEqual([DEVICE_CONFIG_LIST_PATH]);
+    r.unmount();
+  });
+
+  it('Device Plugins: the operator pod lists refused, the plugin-pod requests stand in', async () => {
+    cluster();
+    lib.lists.Pod = [null, 'pods is forbidden'];
+    const r = render(h(route('/amd-gpu/device-plugins')));
+    await r.settle();
+    PLUGIN_POD_QUERIES.forEach((q) => expect(lib.api.calls).toContain(q));
+    expect(r.text()).toContain('DeviceConfig: gpu-operator');
+    expect(r.text()).not.toContain('Loading operator pods...');
+    r.unmount();
+  });
+
+  it('Device Plugins after a page that watched every pod: the operator pods at once, no plugin-pod request', async () => {
+    cluster();
     const r1 = render(h(route('/amd-gpu')));
     await r1.settle();
-    expect(PLUGIN_POD_QUERIES.some((q) => lib.api.calls.indexOf(q) >= 0)).toBe(false);
     r1.unmount();
     const r2 = render(h(route('/amd-gpu/device-plugins')));
+    expect(r2.text()).toContain('amdgpu-dp-0');
     await r2.settle();
     expect(r2.text()).toContain('amdgpu-dp-0');
     expect(PLUGIN_POD_QUERIES.some((q) => lib.api.calls.indexOf(q) >= 0)).toBe(false);
-    // A new operator pod: nothing watches the pod list on this route, Refresh asks the plugin-pod requests.
-    fake.pods.push(makePluginPod('amdgpu-dp-1', { node: 'mi355x-001' }));
-    r2.click(r2.byLabel('Refresh device plugin data'));
-    await r2.settle();
-    PLUGIN_POD_QUERIES.forEach((q) => expect(lib.api.calls).toContain(q));
-    expect(r2.text()).toContain('amdgpu-dp-1');
     r2.unmount();
   });
 
@@ -299,7 +325,7 @@ describe('shared: refresh and StrictMode (' + tier + ')', () => {
       const r = render(h(route(path)));
       await r.settle();
       const [nodes, pods, crd] = expected[path];
-      expect([path, lib.lists.calls.Node.length > 0, lib.lists.calls.Pod.length > 0, crdCalls()]).toEqual([path, nodes, pods, crd]);
+      expect([path, lib.lists.calls.Node.length > 0, lib.lists.calls.Pod.some(allPods), crdCalls()]).toEqual([path, nodes, pods, crd]);
       r.unmount();
     }
   });

@@ -57,8 +57,10 @@ def _check(line, n):
     # never the all-namespaces pod list.
     assert cold["overview"]["requests"]["amd"] == 3 and cold["nodes"]["requests"]["amd"] == 3
     assert set(cold["metrics"]["amd_requests_by_kind"]) == {"nodes", "query", "query_range"}, cold["metrics"]
-    # Device Plugins: the DeviceConfigs and the operator pods by the plugin-pod requests, one wave, no pod list.
-    assert set(cold["devicePlugins"]["amd_requests_by_kind"]) == {"plugin-pods", "crd"}, cold["devicePlugins"]
+    # Device Plugins: the DeviceConfigs and the operator pods' own lists (their watches' list requests), one wave,
+    # no all-namespaces pod list; its Refresh is the DeviceConfig request alone (the operator pods are watched).
+    assert set(cold["devicePlugins"]["amd_requests_by_kind"]) == {"operator-pods", "crd"}, cold["devicePlugins"]
+    assert pp["devicePlugins"]["requests"]["amd"] == 1
     for v in cold.values():
         assert v["amd"] < v["reference"], cold
         # progressive pages: the first render with content comes no later than the page complete
