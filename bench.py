@@ -15,7 +15,8 @@ cluster of 8×MI355X nodes (weak scaling: per-node work is fixed as N grows).
 * every rank with a GPU runs (unless ``--no-burn``) a workload "pod" running
   the MFMA GEMM + HBM triad kernels on its own MI355X; rank 0 starts the
   native ``amdgpu-exporter`` daemon (C++/HIP, one for the host) and scrapes
-  it every 2 s into the TSDB, HIP device r → GPU 0 of node r, so GPU 0 of
+  it every 15 s on the scrape grid (the interval of deploy/exporter's
+  ServiceMonitor) into the TSDB, HIP device r → GPU 0 of node r, so GPU 0 of
   every node reports real power / HBM / activity;
 * rank 0 drives the SHIPPED plugin data layer (src/, Node.js) over real HTTP:
   the reference plugin's request schedule is replayed first as the measured
@@ -139,7 +140,7 @@ def main(argv=None) -> int:
             live = live_series(list(node_of_device.values())) if node_of_device else None
             fc = make_fake(n_nodes, source="both", latency_ms=args.rtt_ms, live=live, preset=args.preset)
             n_nodes, gpus_per_node = len(fc.cluster.gpu_nodes), fc.cluster.spec.gpus_per_node
-            scraper = (Scraper([(exporter.url, device_to_node(node_of_device))], live, interval=2.0).start()
+            scraper = (Scraper([(exporter.url, device_to_node(node_of_device))], live, interval=15.0, align=True).start()
                        if node_of_device else None)
             server = ServerThread(fc).start()
         drv = Driver(server.url)
@@ -345,7 +346,7 @@ def main(argv=None) -> int:
                 rows[k] == result["ref"]["rows"][k]
                 for k in ("gpuNodes", "gpuPods", "gpusMonitored", "podTableRows", "detailSections")),
             "live_telemetry": bool(result["scrapes"]) and n_nodes > 0,
-            "telemetry_source": "native amdgpu-exporter (C++/HIP) scraped every 2 s" if exporter else "synthetic",
+            "telemetry_source": "native amdgpu-exporter (C++/HIP) scraped every 15 s (deploy/exporter ServiceMonitor interval)" if exporter else "synthetic",
             "host": socket.gethostname(),
         }
         print(json.dumps(line), flush=True)

@@ -14,6 +14,7 @@ physical device.
 from __future__ import annotations
 
 import http.server
+import math
 import os
 import signal
 import subprocess
@@ -169,18 +170,23 @@ class Scraper:
     """Pulls every target every ``interval`` s and appends to the live series.
 
     ``targets`` is ``{node: url}`` (per-node agents, labels used as-is) or a
-    list of ``(url, relabel)`` pairs.
+    list of ``(url, relabel)`` pairs. With ``align`` the scrapes land on the
+    ``interval`` grid and their samples carry the grid time, as Prometheus
+    stamps a target's scrapes on its scrape interval — and as the fake's
+    synthetic series are sampled — so the fake's query caches turn over once
+    per interval, not once per scrape of a faster loop.
     """
 
     def __init__(self, targets: Union[Dict[str, str], Sequence[Tuple[str, Relabel]]],
                  live: Dict[Tuple[str, int], Dict[str, Series]], interval: float = 2.0,
-                 now: Callable[[], float] = time.time):
+                 now: Callable[[], float] = time.time, align: bool = False):
         if isinstance(targets, dict):
             targets = [(url, _by_hostname(node)) for node, url in targets.items()]
         self.targets = list(targets)
         self.live = live
         self.interval = interval
         self.now = now
+        self.align = align
         self.scrapes = 0
         self.errors = 0
         self._stop = threading.Event()
@@ -188,6 +194,8 @@ class Scraper:
 
     def scrape_once(self) -> None:
         t = self.now()
+        if self.align:
+            t = math.floor(t / self.interval) * self.interval
         for url, relabel in self.targets:
             try:
                 with urllib.request.urlopen(url, timeout=2) as r:
@@ -204,6 +212,13 @@ class Scraper:
 
     def _loop(self) -> None:
         while not self._stop.is_set():
+            if self.align:
+                # Wake on the next grid point (a little after it, so the grid time has passed).
+                wait = self.interval - (self.now() % self.interval) + 0.01
+                if self._stop.wait(wait):
+                    break
+                self.scrape_once()
+                continue
             self.scrape_once()
             self._stop.wait(self.interval)
 

@@ -34,7 +34,8 @@ def main(argv=None) -> int:
     p.add_argument("--preset", default=None)
     p.add_argument("--exporter", default=None, help="amdgpu-exporter /metrics URL scraped into the live series")
     p.add_argument("--device-map", default="{}", help='JSON {"<hip device>": "<node>"}: device d → GPU 0 of that node')
-    p.add_argument("--interval", type=float, default=2.0, help="scrape interval (s)")
+    p.add_argument("--interval", type=float, default=15.0,
+                   help="scrape interval (s), on its grid: deploy/exporter's ServiceMonitor scrapes every 15 s")
     args = p.parse_args(argv)
 
     from ..parallel.agent import Scraper, device_to_node, live_series
@@ -43,7 +44,8 @@ def main(argv=None) -> int:
     node_of_device: Dict[str, str] = json.loads(args.device_map)
     live = live_series(list(node_of_device.values())) if args.exporter and node_of_device else None
     fc = make_fake(args.nodes, source=args.source, latency_ms=args.latency_ms, live=live, preset=args.preset)
-    scraper = (Scraper([(args.exporter, device_to_node(node_of_device))], live, interval=args.interval).start()
+    scraper = (Scraper([(args.exporter, device_to_node(node_of_device))], live, interval=args.interval,
+                       align=True).start()
                if live else None)
     server = ServerThread(fc).start()
     try:
@@ -75,7 +77,7 @@ class ControlPlaneProcess:
 
     def __init__(self, nodes: int, *, source: str = "both", latency_ms: float = 20.0, preset: Optional[str] = None,
                  exporter_url: Optional[str] = None, node_of_device: Optional[Dict[str, str]] = None,
-                 interval: float = 2.0):
+                 interval: float = 15.0):
         self.cmd = [sys.executable, "-m", "headlamp_intel_gpu_plugin_amd.sim.serve", "--nodes", str(nodes),
                     "--source", source, "--latency-ms", str(latency_ms), "--interval", str(interval)]
         if preset:
