@@ -269,6 +269,8 @@ export interface GpuTelemetry {
   eccUncorrectable: number | null;
   pod: string | null;
   namespace: string | null;
+  /** `powerCapWatts` is the MI355X board limit because the source reported no cap */
+  powerCapAssumed: boolean;
 }
 
 export interface GpuMetrics {
@@ -283,8 +285,10 @@ export interface GpuMetrics {
   prometheusPath: string;
   /** PromQL the snapshot came from (Metrics page "Query" row). */
   query?: string;
-  /** node names a paged snapshot covers (gpus holds only theirs) */
-  scope?: string[];
+  /** the series set the answer carries (metrics.js METRIC_VIEWS): every series, the Metrics page's, or GPU Nodes' */
+  view?: 'all' | 'gauges' | 'topology';
+  /** node names a paged snapshot covers (gpus holds only theirs); 'owners' on a pod → GPU attribution answer */
+  scope?: string[] | 'owners';
   /** cluster totals of a paged snapshot, from server-side aggregates */
   totals?: GpuTotals;
   /** a size-guarded (small-cluster) snapshot: GPU nodes (pods) reporting, and whether that was more than a page */

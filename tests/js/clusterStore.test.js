@@ -3,6 +3,7 @@
  * 8 cases) plus the parallel-fetch, SWR, race and shared-cache behaviour the
  * reference lacks.
  */
+import fs from 'fs';
 import { createClusterStore, fetchNodePods, getSharedStore, nodePodsPath, resetSharedStores, withTimeout } from '../../src/api/clusterStore.js';
 import { DEVICE_CONFIG_LIST_PATH, PLUGIN_POD_QUERIES } from '../../src/api/amdgpu.js';
 import { makeDeviceConfig, makeGpuNode, makeGpuPod, makeNode, makePlainPod, makePluginPod, NOW } from './fixtures.js';
@@ -542,6 +543,17 @@ describe('pod list feeds: operator pods from the watched list, else from the plu
     await store.refresh();
     expect(queried(request)).toBe(0);
     expect(store.getSnapshot().pluginPodsLoading).toBe(false);
+  });
+});
+
+describe('snapshot shape', () => {
+  it('has exactly the fields src/api/types.ts declares for ClusterSnapshot (no tsc offline: this pins the drift)', async () => {
+    const src = fs.readFileSync(new URL('../../src/api/types.ts', import.meta.url), 'utf8');
+    const body = /export interface ClusterSnapshot \{([\s\S]*?)\n\}/.exec(src)[1];
+    const declared = body.split('\n').map((l) => /^\s{2}(\w+)\??:/.exec(l)).filter(Boolean).map((m) => m[1]).sort();
+    const store = createClusterStore({ request: router(baseRoutes()) });
+    await store.refresh();
+    expect(Object.keys(store.getSnapshot()).sort()).toEqual(declared);
   });
 });
 

@@ -10,6 +10,7 @@ import {
   splitByName, STALE_FAILURES,
 } from '../../src/api/metrics.js';
 
+import fs from 'fs';
 import { BASE0, BASE1, exporterData, ok, prom, vec } from './promFake.js';
 
 describe('discovery', () => {
@@ -539,5 +540,50 @@ describe('failureReason (RBAC vs outage)', () => {
     mode = 200;
     await src.discover();
     expect(src.failureReason()).toBe('unreachable'); // no failure pending: the default wording
+  });
+});
+
+describe('answer shapes match src/api/types.ts (no tsc offline: this pins the drift)', () => {
+  const types = fs.readFileSync(new URL('../../src/api/types.ts', import.meta.url), 'utf8');
+  /** {required, optional} top-level field names of `export interface <name>`. */
+  function fields(name) {
+    const body = new RegExp('export interface ' + name + ' \\{([\\s\\S]*?)\\n\\}').exec(types)[1];
+    const out = { required: [], optional: [] };
+    body.split('\n').forEach((l) => {
+      const m = /^\s{2}(\w+)(\??):/.exec(l);
+      if (m) out[m[2] ? 'optional' : 'required'].push(m[1]);
+    });
+    return out;
+  }
+  function conforms(obj, name) {
+    const f = fields(name);
+    const keys = Object.keys(obj).filter((k) => obj[k] !== undefined);
+    f.required.forEach((k) => expect([name, k, k in obj]).toEqual([name, k, true]));
+    keys.forEach((k) => expect([name, k, f.required.concat(f.optional).indexOf(k) >= 0]).toEqual([name, k, true]));
+  }
+  it('GpuMetrics / GpuTelemetry / GpuTotals of a cluster-wide, a scoped and a summary answer', async () => {
+    const src = createMetricsSource({ request: prom({ data: exporterData(['n0', 'n1']) }) });
+    const all = await src.fetchGpuMetrics();
+    conforms(all, 'GpuMetrics');
+    all.gpus.forEach((g) => conforms(g, 'GpuTelemetry'));
+    const scoped = await src.fetchGpuMetrics('gauges', { scope: ['n0'], summary: true });
+    conforms(scoped, 'GpuMetrics');
+    conforms(scoped.totals, 'GpuTotals');
+    scoped.gpus.forEach((g) => conforms(g, 'GpuTelemetry'));
+    const owners = await src.fetchGpuOwners();
+    conforms(owners, 'GpuMetrics');
+    const sr = await src.fetchSeries(1800, 30, ['n0']);
+    conforms(sr, 'GpuSeries');
+  });
+  it('a node-exporter answer', async () => {
+    const i = '10.0.0.1:9100';
+    const ne = {
+      chips: [vec({ __name__: 'node_hwmon_chip_names', instance: i, chip: '0000:05:00_0', chip_name: 'amdgpu' }, 1)],
+      power: [vec({ __name__: 'node_hwmon_power_average_watt', instance: i, chip: '0000:05:00_0' }, 650)],
+      uname: [vec({ __name__: 'node_uname_info', instance: i, nodename: 'mi355x-0' }, 1)],
+    };
+    const m = await createMetricsSource({ request: prom({ data: null, ne }) }).fetchGpuMetrics();
+    conforms(m, 'GpuMetrics');
+    m.gpus.forEach((g) => conforms(g, 'GpuTelemetry'));
   });
 });
