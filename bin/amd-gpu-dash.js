@@ -26,6 +26,7 @@ import {
   nodeDetailView, nodesView, overviewView, podDetailView, podsView,
 } from '../src/view/pages.js';
 import { renderText, textSection } from '../src/view/text.js';
+import { PAGE_NEEDS } from '../src/plugin.js';
 
 const PAGES = ['overview', 'device-plugins', 'nodes', 'pods', 'metrics'];
 
@@ -204,6 +205,15 @@ async function main() {
       filter: (a.pager.filter || '').trim().toLowerCase() }
     : null;
 
+  // The lists the page draws, as its plugin route mounts them (PAGE_NEEDS):
+  // Device Plugins reads its operator pods with the plugin-pod requests
+  // (store.refresh, no pod list), Metrics the node list alone.
+  const byAllocation = a.pager.sort === 'in-use' || a.pager.sort === 'free'; // Metrics ranks nodes by GPUs pods hold
+  const needs = a.page === 'metrics' && byAllocation ? { nodes: true, pods: true } : PAGE_NEEDS[a.page] || { nodes: true, pods: true };
+  function loadLists() {
+    return needs.nodes || needs.pods ? store.loadLists({ nodes: needs.nodes, pods: needs.pods }) : Promise.resolve();
+  }
+
   async function fetchAll(first) {
     const jobs = [
       store.refresh(),
@@ -211,7 +221,7 @@ async function main() {
         : view ? metrics.fetchGpuMetrics(view, rank ? { rank: rank, summary: view === 'gauges' } : undefined) : Promise.resolve(null),
       view === 'all' || view === 'gauges' ? metrics.fetchSeries(1800, 30) : Promise.resolve(null),
     ];
-    if (first) jobs.push(store.loadLists());
+    if (first) jobs.push(loadLists());
     const r = await Promise.all(jobs);
     mstate.metrics = r[1];
     mstate.series = r[2];
@@ -232,7 +242,7 @@ async function main() {
   print();
   while (a.watch > 0) {
     await new Promise(function (r) { setTimeout(r, a.watch * 1000); });
-    await store.loadLists(); // no watch here: re-list nodes and pods each cycle
+    await loadLists(); // no watch here: re-list what the page draws each cycle
     await fetchAll(false);
     print();
   }

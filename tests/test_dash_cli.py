@@ -66,6 +66,19 @@ def test_overview_sends_no_prometheus_request():
         assert fc.stats().get("prometheus", 0) == 0 and fc.stats()["apiserver"] >= 3
 
 
+def test_device_plugins_lists_operator_pods_only():
+    """As its plugin route: the DeviceConfigs and the operator pods, never the node list or every pod."""
+    fc = make_fake(2, source="amd-exporter", latency_ms=1)
+    with ServerThread(fc) as srv:
+        r = run("--url", srv.url, "--page", "device-plugins")
+        assert r.returncode == 0, r.stderr
+        assert "DeviceConfig: gpu-operator" in r.stdout and "gpu-operator-device-plugin-" in r.stdout
+        with fc.lock:
+            paths = [p for p, _ in fc.requests]
+        assert "/api/v1/pods" not in paths and "/api/v1/nodes" not in paths, paths
+        assert "/api/v1/namespaces/kube-amd-gpu/pods" in paths
+
+
 def test_detail_sections_with_power_history(url):
     node = run("--url", url, "--page", "node:mi355x-001")
     assert node.returncode == 0, node.stderr
