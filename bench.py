@@ -68,6 +68,9 @@ def parse_args(argv=None):
     p.add_argument("--ref-steps", type=int, default=None, help="reference-schedule refreshes (default: --steps)")
     p.add_argument("--no-burn", action="store_true", help="do not run the GPU workload pods")
     p.add_argument("--no-live", action="store_true", help="synthetic telemetry only (no native probe)")
+    p.add_argument("--source", default="both", choices=["both", "amd-exporter", "node-exporter"],
+                   help="GPU series the fake Prometheus holds: the Device Metrics Exporter's, node-exporter's amdgpu "
+                        "hwmon / DRM series (the plugin's fallback source), or both")
     p.add_argument("--control-plane", default="process", choices=["process", "thread"],
                    help="run the fake apiserver/Prometheus in a child process (default) or a thread of rank 0")
     p.add_argument("--out", default=None, help="also write the full result JSON here")
@@ -88,7 +91,8 @@ def main(argv=None) -> int:
 
     # --- workload pod per rank; one native exporter for the host ----------
     burner = exporter = None
-    live_on = gpu and not args.no_live
+    # The live probe exports Device Metrics Exporter series: not on a node-exporter-only cluster.
+    live_on = gpu and not args.no_live and args.source != "node-exporter"
     if gpu and not args.no_burn:
         from headlamp_intel_gpu_plugin_amd.ops.workload import Burner
 
@@ -128,7 +132,7 @@ def main(argv=None) -> int:
             # hosts: no request waits for this process's GIL (workload pod).
             from headlamp_intel_gpu_plugin_amd.sim.serve import ControlPlaneProcess
 
-            server = ControlPlaneProcess(n_nodes, source="both", latency_ms=args.rtt_ms, preset=args.preset,
+            server = ControlPlaneProcess(n_nodes, source=args.source, latency_ms=args.rtt_ms, preset=args.preset,
                                          exporter_url=exporter.url if exporter else None,
                                          node_of_device=node_of_device).start()
             n_nodes, gpus_per_node = server.info["gpu_nodes"], server.info["gpus_per_node"]
@@ -138,7 +142,7 @@ def main(argv=None) -> int:
             from headlamp_intel_gpu_plugin_amd.sim.apiserver import ServerThread, make_fake
 
             live = live_series(list(node_of_device.values())) if node_of_device else None
-            fc = make_fake(n_nodes, source="both", latency_ms=args.rtt_ms, live=live, preset=args.preset)
+            fc = make_fake(n_nodes, source=args.source, latency_ms=args.rtt_ms, live=live, preset=args.preset)
             n_nodes, gpus_per_node = len(fc.cluster.gpu_nodes), fc.cluster.spec.gpus_per_node
             scraper = (Scraper([(exporter.url, device_to_node(node_of_device))], live, interval=15.0, align=True).start()
                        if node_of_device else None)
@@ -264,6 +268,7 @@ def main(argv=None) -> int:
                 "nodes": n_nodes,
                 "gpus_per_node": gpus_per_node,
                 "preset": args.preset,
+                "prometheus_series": args.source,
                 "global_batch": None,
                 "seq_len": None,
                 "parallelism": f"rank-per-node x{info.world}",

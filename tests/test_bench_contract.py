@@ -86,6 +86,21 @@ def test_bench_single_rank():
     _check(lines[0], 1)
 
 
+def test_bench_node_exporter_only_cluster_is_one_wave():
+    """A Prometheus with node-exporter's amdgpu hwmon series only (the fallback source): every GPU is monitored and
+    GPU Nodes / Metrics cold-open in one wave — one query (Metrics: plus its range query), no second cluster-wide read."""
+    r = subprocess.run([sys.executable, "bench.py", "--nodes", "2", "--source", "node-exporter", "--steps", "2",
+                        "--warmup", "1", "--rtt-ms", "5", "--no-burn"], cwd=ROOT, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = _json_lines(r.stdout)[-1]
+    assert line["config"]["prometheus_series"] == "node-exporter"
+    assert line["rendered"]["gpus_monitored"] == 16
+    cold = line["cold_open_per_page_p50_ms"]
+    assert cold["nodes"]["amd_requests_by_kind"].get("query") == 1, cold["nodes"]
+    assert cold["metrics"]["amd_requests_by_kind"].get("query") == 1, cold["metrics"]
+
+
 def test_bench_two_ranks_gloo():
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",

@@ -26,7 +26,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 POINTS = [("nodes", "1"), ("nodes", "2"), ("nodes", "4"), ("nodes", "8"),
-          ("preset", "cpu-only"), ("preset", "1x1"), ("preset", "1x8"), ("preset", "4x8"), ("preset", "8x8")]
+          ("preset", "cpu-only"), ("preset", "1x1"), ("preset", "1x8"), ("preset", "4x8"), ("preset", "8x8"),
+          ("hwmon", "8")]
 
 PRESET_LABEL = {
     "cpu-only": "#1 CPU-only cluster, 0 GPU nodes",
@@ -37,9 +38,19 @@ PRESET_LABEL = {
 }
 
 
+def label_of(r):
+    if r["kind"] == "nodes":
+        return f"{r['point']}-node scaling point"
+    if r["kind"] == "hwmon":
+        return f"{r['point']} nodes × 8 MI355X, node-exporter hwmon only (no exporter series)"
+    return PRESET_LABEL[r["point"]]
+
+
 def run(kind, val, args):
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", str(args.steps), "--warmup", str(args.warmup),
-           "--rtt-ms", str(args.rtt_ms), f"--{kind}", val]
+           "--rtt-ms", str(args.rtt_ms)]
+    # hwmon: a cluster whose Prometheus holds node-exporter's amdgpu series only (the plugin's fallback source)
+    cmd += ["--nodes", val, "--source", "node-exporter"] if kind == "hwmon" else [f"--{kind}", val]
     if args.extra:
         cmd += args.extra.split()
     # bench progress lines (stderr) pass through: a long point stays visibly alive
@@ -74,7 +85,7 @@ def table(rows):
         l = r["line"]
         pp = l["per_page_refresh_p50_ms"]
         comp = l["all_pages_refresh"]
-        label = f"{r['point']}-node scaling point" if r["kind"] == "nodes" else PRESET_LABEL[r["point"]]
+        label = label_of(r)
         cells = [label, str(l["config"]["nodes"])]
         cells += [f"{pp[k]['reference']:.1f} → {pp[k]['amd']:.1f}" for k, _ in PAGE_COLS]
         cells += [f"{l['baseline']['value_ms']:.1f} → {l['value']:.1f}", f"{l['baseline']['value_ms'] / l['value']:.1f}×",
@@ -96,7 +107,7 @@ def cold_table(rows):
     for r in rows:
         l = r["line"]
         cp = l.get("cold_open_per_page_p50_ms") or {}
-        label = f"{r['point']}-node scaling point" if r["kind"] == "nodes" else PRESET_LABEL[r["point"]]
+        label = label_of(r)
         cells = [label, str(l["config"]["nodes"])]
         for k, _ in PAGE_COLS:
             v = cp.get(k)
