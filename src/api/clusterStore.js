@@ -5,7 +5,8 @@
  * (src/api/IntelGpuDataContext.tsx:96-254, SURVEY.md C3) with a store that:
  *
  *   * refreshes with ONE request (the DeviceConfig list): operator pods are
- *     derived from the watched pod list, and the plugin-pod requests run —
+ *     derived from the watched pod list (or the operator pods' own watched
+ *     lists on a route that draws no other pod), and the plugin-pod requests run —
  *     in parallel, each time-boxed — only when that list is unavailable
  *     (reference: CRD + 3 selectors, serial, :122-165) — refresh latency is
  *     one RTT instead of Σ RTT;
@@ -191,11 +192,13 @@ export function createClusterStore(opts) {
     return memoGpuPods;
   }
   /**
-   * Operator pods. Once Headlamp's pod list (all namespaces) is in, they are
-   * derived from it: it already holds every pod the reference's three
-   * plugin-pod requests return, so a refresh needs only the CRD request.
-   * Without that list (forbidden cluster-wide, failed, or no watch at all)
-   * they come from the PLUGIN_POD_QUERIES requests.
+   * Operator pods, from whichever watch delivers them. While Headlamp's pod
+   * list (all namespaces) is watched they are derived from it: it already
+   * holds every pod the reference's three plugin-pod requests return, so a
+   * refresh needs only the CRD request. A route that watches the operator
+   * pods' own lists instead (Device Plugins: attachOperatorFeed) reads those.
+   * With neither (forbidden, failed, unmounted, or no watch at all) they come
+   * from the PLUGIN_POD_QUERIES requests.
    */
   function pluginPods() {
     if (s.podsState === 'ready' && s.pods && podsLive()) return memoPluginPods;
