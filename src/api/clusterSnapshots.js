@@ -16,10 +16,11 @@
  * then four instant queries on every fetch, power keyed by PCI chip only.
  */
 
-import { STALE_FAILURES } from './series.js';
-import { exporterNodeQuery, exporterQuery, mergedQuery, nodeExporterQuery } from './promql.js';
+import { SERIES, STALE_FAILURES } from './series.js';
+import { exporterNodeQuery, exporterQuery, mergedQuery, nodeExporterQuery, nodeExporterScopedQuery } from './promql.js';
 import {
   applyStatics,
+  isRow,
   joinExporterResults,
   joinNodeExporterResults,
   keyedByHostname,
@@ -143,7 +144,7 @@ export function createClusterSnapshots(client, state) {
     function clusterWide() {
       return cluster('all').then(function (m) { return m ? nodeSlice(m, key) : null; });
     }
-    if (state.source === 'node-exporter') return clusterWide();
+    if (state.source === 'node-exporter') return hwNode(st, key, clusterWide);
     return client.withPrometheus(function (base) {
       const withStatic = st.links === null || client.now() - st.staticAt >= client.ttl;
       return client.combined(base, exporterNodeQuery(key, withStatic)).then(function (res) {
@@ -168,6 +169,34 @@ export function createClusterSnapshots(client, state) {
           fetchedAt: client.fetchedAt(),
           prometheusPath: base,
           scope: key,
+        };
+        return st.last;
+      });
+    }, function () {
+      return staleOrNull(st, STALE_FAILURES, client.invalidate);
+    }).then(function (r) { return r === NOT_SCOPED ? clusterWide() : r; });
+  }
+
+  /**
+   * One node's GPUs on a node-exporter source: its series through
+   * node_uname_info (promql.js nodeExporterScopedQuery), O(GPUs per node);
+   * the cluster-wide snapshot cut to the node when no node_uname_info names
+   * it (node-exporter's `nodename` is not the Kubernetes node name there).
+   */
+  function hwNode(st, key, clusterWide) {
+    return client.withPrometheus(function (base) {
+      const q = nodeExporterScopedQuery([key]);
+      return client.combined(base, q).then(function (res) {
+        if (!res.ok) return UNREACHABLE;
+        st.failures = 0;
+        const un = res.rows[SERIES.nodeExporter.uname] || [];
+        if (!un.some(function (r) { return isRow(r) && r.metric.nodename === key; })) return NOT_SCOPED;
+        const j = joinNodeExporterResults(res.rows);
+        const gpus = j.gpus.filter(function (g) { return g.nodeName === key; });
+        const prev = st.last;
+        st.last = {
+          source: 'node-exporter', gpus: prev ? shareGpus(prev.gpus, gpus) : gpus, xgmi: {}, links: {},
+          fetchedAt: client.fetchedAt(), prometheusPath: base, scope: key,
         };
         return st.last;
       });

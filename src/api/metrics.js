@@ -68,6 +68,8 @@ export {
   mergedQuery,
   nodeExporterProjected,
   nodeExporterQuery,
+  nodeExporterScopedQuery,
+  nodeExporterSummaryQuery,
   nodePowerQuery,
   nodePowerSum,
   ownersQuery,
@@ -92,6 +94,7 @@ export {
   applyStatics,
   clusterPowerStats,
   gpuKey,
+  hwTotalsFromRows,
   isRow,
   joinExporterResults,
   joinNodeExporterResults,

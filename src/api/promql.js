@@ -319,6 +319,64 @@ export function nodeExporterProjected() {
 }
 
 /**
+ * `nodename=~"a|b|…"` on node_uname_info: node-exporter's GPU series carry
+ * `instance`, not the Kubernetes node name; node_uname_info names the node
+ * (telemetry.js joinNodeExporterResults maps instance → nodename). An empty
+ * scope matches nothing.
+ */
+function nodenameMatcher(names) {
+  if (!names.length) return 'nodename="."';
+  return 'nodename=~"' + promString(names.map(regexLiteral).join('|')) + '"';
+}
+
+/**
+ * node-exporter's series of the nodes a paged view shows, in ONE request:
+ * the GPU series of the instances whose node_uname_info names one of them
+ * (`and on(instance)`), plus those node_uname_info rows for the join —
+ * O(page) on a cluster that feeds Prometheus through node-exporter only
+ * (the reference's one source: src/api/metrics.ts:101-116, every chip of
+ * the cluster on every fetch).
+ */
+export function nodeExporterScopedQuery(names) {
+  const N = SERIES.nodeExporter;
+  const labels = NODE_EXPORTER_JOIN_LABELS.join(', ');
+  const gpuNames = nodeExporterNames().filter(function (n) { return n !== N.uname; });
+  const uname = N.uname + '{' + nodenameMatcher(names) + '}';
+  return 'max by (' + labels + ') ({__name__=~"' + gpuNames.join('|') + '"} and on(instance) ' + uname + ')' +
+    ' or max by (' + labels + ') (' + uname + ')';
+}
+
+/**
+ * Cluster totals of a node-exporter source as server-side aggregates, the
+ * figures summarizeMetrics takes from the per-GPU join (telemetry.js
+ * hwTotalsFromRows reads them back): amdgpu chips (GPUs) and the nodes
+ * reporting them; power per chip — the average where reported, else the
+ * instantaneous input (`or` keeps the first) — summed and counted; power
+ * caps; HBM used / total and GFX busy of the DRM cards of those nodes.
+ * A few rows whatever the cluster size.
+ */
+export function nodeExporterSummaryQuery() {
+  const N = SERIES.nodeExporter;
+  const chips = 'count by (instance, chip) (' + N.chips + ')';
+  const insts = 'count by (instance) (' + N.chips + ')';
+  const power = '(max by (instance, chip) (' + N.power + ') or max by (instance, chip) (' + N.powerInput + '))' +
+    ' and on(instance, chip) ' + chips;
+  const cap = 'max by (instance, chip) (' + N.powerCap + ') and on(instance, chip) ' + chips;
+  const card = function (n) { return 'max by (instance, card) (' + n + ') and on(instance) ' + insts; };
+  return [
+    sizeRow('count(' + chips + ')', 'hw_gpus'),
+    sizeRow('count(' + insts + ')', 'hw_nodes'),
+    sizeRow('sum(' + power + ')', 'hw_power'),
+    sizeRow('count(' + power + ')', 'hw_with_power'),
+    sizeRow('sum(' + cap + ')', 'hw_cap'),
+    sizeRow('sum(' + card(N.vramUsed) + ')', 'hw_vram_used'),
+    sizeRow('sum(' + card(N.vramTotal) + ')', 'hw_vram_total'),
+    sizeRow('sum(' + card(N.busy) + ')', 'hw_gfx_sum'),
+    sizeRow('count(' + card(N.busy) + ')', 'hw_gfx_n'),
+  ].join(' or ');
+}
+
+/**
  * First query of a session, while it is not yet known which exporter feeds
  * this Prometheus: both exporters' series in ONE request, projected onto the
  * union of the labels the two joins read. Later refreshes ask only the

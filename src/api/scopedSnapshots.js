@@ -16,8 +16,21 @@
  * every refresh (src/api/metrics.ts:96-155, MetricsPage.tsx:348-350).
  */
 
-import { SMALL_CLUSTER_NODES, STALE_FAILURES } from './series.js';
-import { exporterQuery, nodeExporterQuery, rankedClusterQuery, smallClusterQuery, sourceProbe, summaryQuery } from './promql.js';
+import { SERIES, SMALL_CLUSTER_NODES, SMALL_HWMON_GPUS, STALE_FAILURES } from './series.js';
+import {
+  exporterQuery,
+  gpuNodeCount,
+  hwmonGpuCount,
+  nodeExporterProjected,
+  nodeExporterScopedQuery,
+  nodeExporterSummaryQuery,
+  rankedClusterQuery,
+  sizeGuard,
+  sizeRow,
+  smallClusterQuery,
+  sourceProbe,
+  summaryQuery,
+} from './promql.js';
 import {
   applyStatics,
   gpuKey,
@@ -27,6 +40,8 @@ import {
   num,
   sameValue,
   shareGpus,
+  hwTotalsFromRows,
+  HW_TOTAL_TAGS,
   shareMap,
   sizeFromRows,
   staticsOf,
@@ -37,8 +52,9 @@ import {
 import { UNREACHABLE, staleOrNull } from './promClient.js';
 import { NOT_SCOPED } from './clusterSnapshots.js';
 
-/** `agg` tags of size / probe rows (not cluster totals). */
+/** `agg` tags of size / probe rows and of node-exporter totals (not exporter cluster totals). */
 const SIZE_TAGS = { gpu_nodes: true, hwmon: true, rank: true, ranked: true };
+for (let i = 0; i < HW_TOTAL_TAGS.length; i++) SIZE_TAGS[HW_TOTAL_TAGS[i]] = true;
 
 function totalsOf(rows) {
   return totalsFromRows(rows.__agg.filter(function (r) { return !SIZE_TAGS[r.metric.agg]; }));
@@ -149,7 +165,7 @@ export function createScopedSnapshots(client, state, snaps) {
    */
   function scoped(v, scope, summary, key, small) {
     const st = entry(key);
-    if (state.source === 'node-exporter') return snaps.cluster(v).then(function (m) { return cut(m, scope, summary, key, small); });
+    if (state.source === 'node-exporter') return hwScoped(st, v, scope, summary, key, small);
     return client.withPrometheus(function (base) {
       // Nothing cached yet for a small-cluster fetch before the node list: statics too.
       const withStatic = small && scope.length === 0 ? true : scope.length > 0 && needsStatic(scope);
@@ -159,7 +175,15 @@ export function createScopedSnapshots(client, state, snaps) {
       else if (scope.length) parts.push(exporterQuery(withStatic, true, v, scope));
       if (summary) parts.push(summaryQuery());
       // smallClusterQuery already carries the gpu_nodes row.
-      if (probing && parts.length) parts.push(sourceProbe(!small));
+      if (probing && parts.length) {
+        parts.push(sourceProbe(!small));
+        // node-exporter's page and totals too, where no exporter reports: a
+        // node-exporter cluster of any size is told apart AND served in this wave.
+        const hw = [];
+        if (scope.length) hw.push(nodeExporterScopedQuery(scope));
+        if (summary) hw.push(nodeExporterSummaryQuery());
+        if (hw.length) parts.push('(' + hw.join(' or ') + ') unless on() (' + gpuNodeCount() + ')');
+      }
       if (!parts.length) return Promise.resolve(result(st, base, null, { gpus: [], xgmi: {}, links: {} }, scope, undefined, v));
       const q = parts.join(' or ');
       return client.combined(base, q).then(function (res) {
@@ -174,10 +198,10 @@ export function createScopedSnapshots(client, state, snaps) {
           state.source = 'amd-exporter';
         } else if (probing && sizeFromRows(rows.__agg, 'hwmon') > 0) {
           // node-exporter's amdgpu hwmon feeds this Prometheus: its series
-          // came along on a small cluster (one wave); a larger one is read
-          // cluster-wide once, then served from that snapshot.
-          if (!joinNodeExporterResults(rows).gpus.length) return NOT_SCOPED;
-          return cut(snaps.commit(base, v, nodeExporterQuery(), rows, false), scope, summary, key, small);
+          // came along — every GPU on a small cluster, the page's on a larger
+          // one — with its totals (one wave).
+          state.source = 'node-exporter';
+          return hwAnswer(st, base, q, rows, v, scope, summary, small);
         }
         // (No exporter and no amdgpu hwmon: no GPU telemetry — this answer stands.)
         scopeStatics(j, scope, withStatic);
@@ -189,6 +213,60 @@ export function createScopedSnapshots(client, state, snaps) {
     }).then(function (r) {
       return r === NOT_SCOPED ? snaps.cluster(v).then(function (m) { return cut(m, scope, summary, key, small); }) : r;
     });
+  }
+
+  /**
+   * The page's telemetry on a node-exporter source: its nodes' series through
+   * node_uname_info (promql.js nodeExporterScopedQuery) and the totals as
+   * server-side aggregates (nodeExporterSummaryQuery) — O(page), like the
+   * exporter's `hostname=~` path. `small` keeps its meaning: every GPU while
+   * at most SMALL_HWMON_GPUS amdgpu chips report, else `scope`'s.
+   */
+  function hwScoped(st, v, scope, summary, key, small) {
+    return client.withPrometheus(function (base) {
+      const hw = hwmonGpuCount();
+      const parts = [];
+      if (small) {
+        parts.push(sizeGuard(nodeExporterProjected(), true, hw, SMALL_HWMON_GPUS));
+        if (scope.length) parts.push(sizeGuard(nodeExporterScopedQuery(scope), false, hw, SMALL_HWMON_GPUS));
+      } else if (scope.length) parts.push(nodeExporterScopedQuery(scope));
+      parts.push(sizeRow(hw, 'hwmon'));
+      if (summary) parts.push(nodeExporterSummaryQuery());
+      const q = parts.join(' or ');
+      return client.combined(base, q).then(function (res) {
+        if (!res.ok) return UNREACHABLE;
+        return hwAnswer(st, base, q, res.rows, v, scope, summary, small);
+      });
+    }, function () {
+      return staleOrNull(st, STALE_FAILURES, client.invalidate);
+    }).then(function (r) {
+      return r === NOT_SCOPED ? snaps.cluster(v).then(function (m) { return cut(m, scope, summary, key, small); }) : r;
+    });
+  }
+
+  /**
+   * A node-exporter answer (hwScoped, or the first query's probe) as the
+   * page's snapshot. NOT_SCOPED when the cluster reports amdgpu chips but no
+   * node_uname_info names a node of the page: node-exporter's `nodename` is
+   * not the Kubernetes node name there, so the page is cut from the
+   * cluster-wide snapshot instead (its join also tries `node` and `instance`).
+   */
+  function hwAnswer(st, base, q, rows, v, scope, summary, small) {
+    st.failures = 0;
+    const chips = sizeFromRows(rows.__agg, 'hwmon');
+    const whole = !!small && chips <= SMALL_HWMON_GPUS;
+    const j = joinNodeExporterResults(rows);
+    if (!whole) {
+      const inScope = {};
+      for (let i = 0; i < scope.length; i++) inScope[scope[i]] = true;
+      j.gpus = j.gpus.filter(function (g) { return inScope[g.nodeName] === true; });
+      const un = rows[SERIES.nodeExporter.uname] || [];
+      const named = un.some(function (r) { return isRow(r) && inScope[r.metric.nodename] === true; });
+      if (scope.length && !j.gpus.length && !named && chips > 0) return NOT_SCOPED;
+    }
+    const totals = summary ? hwTotalsFromRows(rows.__agg) || zeroTotals() : undefined;
+    const sized = small ? { count: chips, limit: SMALL_HWMON_GPUS, exceeded: !whole } : undefined;
+    return result(st, base, q, j, scope, totals, v, sized);
   }
 
   /**

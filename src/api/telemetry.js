@@ -271,6 +271,45 @@ export function totalsFromRows(rows) {
   };
 }
 
+/** `agg` tags of nodeExporterSummaryQuery rows (promql.js). */
+export const HW_TOTAL_TAGS = ['hw_gpus', 'hw_nodes', 'hw_power', 'hw_with_power', 'hw_cap', 'hw_vram_used',
+  'hw_vram_total', 'hw_gfx_sum', 'hw_gfx_n'];
+
+/**
+ * Rows of a nodeExporterSummaryQuery answer → the totals summarizeMetrics
+ * computes from the per-GPU node-exporter join (plus `nodes`); null when
+ * there are none. node-exporter reports no RAS counters and no throttle
+ * threshold, and a missing cap is not replaced (as in the join).
+ */
+export function hwTotalsFromRows(rows) {
+  const v = {};
+  let any = false;
+  for (let i = 0; i < rows.length; i++) {
+    const row = rows[i];
+    if (!isRow(row) || HW_TOTAL_TAGS.indexOf(row.metric.agg) < 0) continue;
+    const x = num(row.value[1]);
+    if (x === null) continue;
+    v[row.metric.agg] = x;
+    any = true;
+  }
+  if (!any) return null;
+  const g = function (k) { return v[k] || 0; };
+  return {
+    gpus: g('hw_gpus'),
+    withPower: g('hw_with_power'),
+    nodes: g('hw_nodes'),
+    powerWatts: g('hw_power'),
+    powerCapWatts: g('hw_cap'),
+    vramUsedBytes: g('hw_vram_used'),
+    vramTotalBytes: g('hw_vram_total'),
+    avgGfxActivityPct: g('hw_gfx_n') ? g('hw_gfx_sum') / g('hw_gfx_n') : null,
+    eccCorrectable: null,
+    eccUncorrectable: null,
+    powerCapAssumed: 0,
+    tempLimitAssumed: 0,
+  };
+}
+
 /**
  * The totals of a cluster where nothing reports: what a summary answer with
  * no aggregate rows means (summary asked, no exporter GPU anywhere), so the

@@ -69,6 +69,10 @@ export function flatten(d) {
  * (__name__) …, "agg", …)). Unknown shapes answer no rows.
  */
 function term(q, rows) {
+  // `a or b` at the top level: every term's rows; `(q)`: q.
+  const alts = splitOr(q);
+  if (alts.length > 1) return [].concat.apply([], alts.map((t) => term(t, rows)));
+  if (q[0] === '(' && closing(q, 0) === q.length - 1) return term(q.slice(1, -1), rows);
   // `X unless on() (<count>)`: X only while the count has no sample.
   const unless = /^(.*) unless on\(\) \((count\(count by .*\))\)$/.exec(q);
   if (unless) {
@@ -100,6 +104,12 @@ function term(q, rows) {
     const n = (powerSums(rankedCount[1], rows) || []).length;
     return n ? [vec({ agg: 'ranked' }, n)] : [];
   }
+  // promql.js nodeExporterSummaryQuery: node-exporter totals, computed here from the rows.
+  const hw = /^label_replace\((?:sum|count)\(.*\), "agg", "(hw_\w+)", "", ""\)$/.exec(q);
+  if (hw) {
+    const v = hwTotal(hw[1], rows);
+    return v === null ? [] : [vec({ agg: hw[1] }, v)];
+  }
   const sized = /^label_replace\((count\(count by .*\)), "agg", "(\w+)", "", ""\)$/.exec(q);
   if (sized) {
     const n = countOf(sized[1], rows);
@@ -130,6 +140,18 @@ function term(q, rows) {
     rows.filter((r) => r.metric.__name__ === nodes[1]).forEach((r) => (hs[r.metric.hostname] = true));
     const n = Object.keys(hs).length;
     return n ? [vec({ __name__: nodes[1], agg: 'nodes' }, n)] : [];
+  }
+  // promql.js nodeExporterScopedQuery: node-exporter series of the instances node_uname_info names.
+  const byNode = /^max by \([^)]*\) \((?:\{__name__=~"(.*?)"\} and on\(instance\) )?node_uname_info\{nodename(=~?)"((?:[^"\\]|\\.)*)"\}\)$/.exec(q);
+  if (byNode) {
+    const v = byNode[3].replace(/\\(.)/g, '$1');
+    const ok = byNode[2] === '=' ? (n) => n === v : (n) => new RegExp('^(?:' + v + ')$').test(n || '');
+    const named = rows.filter((r) => r.metric.__name__ === 'node_uname_info' && ok(r.metric.nodename));
+    if (byNode[1] === undefined) return named;
+    const insts = {};
+    named.forEach((r) => (insts[r.metric.instance] = true));
+    const re = new RegExp('^(?:' + byNode[1] + ')$');
+    return rows.filter((r) => re.test(r.metric.__name__ || '') && insts[r.metric.instance] === true);
   }
   const m = /^(?:max by \([^)]*\) \()?\{__name__=~"(.*?)"(?:, hostname(=~?)"((?:[^"\\]|\\.)*)")?\}\)?$/.exec(q);
   if (!m) return [];
@@ -217,6 +239,61 @@ function countOf(expr, rows) {
     seen[m[1] === 'hostname' ? r.metric.hostname : r.metric.namespace + '/' + r.metric.pod] = true;
   });
   return Object.keys(seen).length;
+}
+
+/** Index of the parenthesis closing the one at `open`. */
+function closing(q, open) {
+  let depth = 0;
+  for (let i = open; i < q.length; i++) {
+    if (q[i] === '(') depth++;
+    else if (q[i] === ')' && --depth === 0) return i;
+  }
+  return -1;
+}
+
+/**
+ * One nodeExporterSummaryQuery figure over `rows` (null: an empty vector):
+ * amdgpu chips, their instances, power (average, else input) summed and
+ * counted, caps, DRM HBM / busy of the cards of those instances.
+ */
+function hwTotal(tag, rows) {
+  const chips = {};
+  const insts = {};
+  rows.forEach((r) => {
+    if (r.metric.__name__ !== 'node_hwmon_chip_names' || r.metric.chip_name !== 'amdgpu') return;
+    chips[r.metric.instance + '/' + r.metric.chip] = true;
+    insts[r.metric.instance] = true;
+  });
+  const per = (name, keyOf, keep) => {
+    const out = {};
+    rows.forEach((r) => {
+      if (r.metric.__name__ !== name || !keep(r)) return;
+      const k = keyOf(r);
+      const v = parseFloat(r.value[1]);
+      out[k] = k in out ? Math.max(out[k], v) : v;
+    });
+    return out;
+  };
+  const chipKey = (r) => r.metric.instance + '/' + r.metric.chip;
+  const cardKey = (r) => r.metric.instance + '/' + r.metric.card;
+  const onChip = (r) => chips[chipKey(r)] === true;
+  const onInst = (r) => insts[r.metric.instance] === true;
+  const power = Object.assign(per('node_hwmon_power_input_watt', chipKey, onChip), per('node_hwmon_power_average_watt', chipKey, onChip));
+  const vals = (o) => Object.keys(o).map((k) => o[k]);
+  const sum = (a) => (a.length ? a.reduce((x, y) => x + y, 0) : null);
+  const count = (a) => (a.length ? a.length : null);
+  switch (tag) {
+    case 'hw_gpus': return count(Object.keys(chips));
+    case 'hw_nodes': return count(Object.keys(insts));
+    case 'hw_power': return sum(vals(power));
+    case 'hw_with_power': return count(vals(power));
+    case 'hw_cap': return sum(vals(per('node_hwmon_power_cap_watt', chipKey, onChip)));
+    case 'hw_vram_used': return sum(vals(per('node_drm_memory_vram_used_bytes', cardKey, onInst)));
+    case 'hw_vram_total': return sum(vals(per('node_drm_memory_vram_size_bytes', cardKey, onInst)));
+    case 'hw_gfx_sum': return sum(vals(per('node_drm_gpu_busy_percent', cardKey, onInst)));
+    case 'hw_gfx_n': return count(vals(per('node_drm_gpu_busy_percent', cardKey, onInst)));
+    default: return null;
+  }
 }
 
 /** `q` split at its top-level ` or ` (not inside parentheses). */

@@ -188,13 +188,18 @@ describe('scoped fetches: the first answer decides the telemetry source (one wav
     expect(decoded(fake)[1]).not.toContain('gpu_power_usage');
   });
 
-  it('a larger node-exporter cluster (more amdgpu chips than one page) reads cluster-wide in the second wave', async () => {
+  it('a larger node-exporter cluster (more amdgpu chips than one page) is served in the first wave, page-scoped', async () => {
     const fake = prom({ data: {}, ne: neOf(names(9), 8) });
     const s = createMetricsSource({ request: fake });
     const m = await s.fetchGpuMetrics('gauges', { scope: names(8), summary: true });
-    expect(fake.mock.calls.length).toBe(2);
+    expect(fake.mock.calls.length).toBe(1);
     expect(s.source()).toBe('node-exporter');
     expect(m.totals.gpus).toBe(72);
     expect(m.gpus.length).toBe(64);
+    // a refresh asks node-exporter for the page's nodes and the totals: nothing cluster-wide
+    await s.fetchGpuMetrics('gauges', { scope: names(8), summary: true });
+    expect(fake.mock.calls.length).toBe(2);
+    expect(decoded(fake)[1]).toContain('and on(instance) node_uname_info{nodename=~');
+    expect(decoded(fake)[1]).not.toMatch(/\{__name__=~"[^"]*"\}\)( or|$)/);
   });
 });

@@ -469,3 +469,37 @@ def test_source_probe_decides_the_exporter_in_one_answer():
         both.add(Series({"__name__": "gpu_power_usage", "hostname": "a", "gpu_id": str(g)}, fn=lambda t: 500.0))
     rows = _vec(query(both, q, 100.0))
     assert agg(rows, "gpu_nodes") == 1 and agg(rows, "hwmon") == 8 and [r for r in rows if "agg" not in r["metric"]] == []
+
+
+def test_node_exporter_summary_and_scoped_query_against_the_synthetic_cluster():
+    """nodeExporterSummaryQuery (server-side totals of a node-exporter-only Prometheus) against an oracle computed
+    from the stored series, and nodeExporterScopedQuery returning one node's series through node_uname_info."""
+    from headlamp_intel_gpu_plugin_amd.sim.apiserver import make_fake
+
+    summary, scoped = _js("[m.nodeExporterSummaryQuery(), m.nodeExporterScopedQuery(['mi355x-001'])]")
+    fc = make_fake(3, source="node-exporter", latency_ms=0)
+    d, t = fc.db, 1_000_000.0
+    chips = {(s.labels["instance"], s.labels["chip"]) for s in d.by_name["node_hwmon_chip_names"]
+             if s.labels.get("chip_name") == "amdgpu"}
+
+    def per(name, key):
+        return {key(s.labels): s.at(t)[1] for s in d.by_name.get(name, []) if s.at(t) is not None}
+
+    chip_key = lambda l: (l["instance"], l["chip"])
+    card_key = lambda l: (l["instance"], l["card"])
+    power = {**per("node_hwmon_power_input_watt", chip_key), **per("node_hwmon_power_average_watt", chip_key)}
+    power = {k: v for k, v in power.items() if k in chips}
+    insts = {i for i, _ in chips}
+    busy = {k: v for k, v in per("node_drm_gpu_busy_percent", card_key).items() if k[0] in insts}
+    got = {r["metric"]["agg"]: float(r["value"][1]) for r in _vec(query(d, summary, t))}
+    assert got["hw_gpus"] == len(chips) == 24 and got["hw_nodes"] == 3
+    assert got["hw_power"] == pytest.approx(sum(power.values())) and got["hw_with_power"] == len(power)
+    assert got["hw_cap"] == pytest.approx(sum(v for k, v in per("node_hwmon_power_cap_watt", chip_key).items() if k in chips))
+    assert got["hw_vram_used"] == pytest.approx(sum(per("node_drm_memory_vram_used_bytes", card_key).values()))
+    assert got["hw_gfx_sum"] == pytest.approx(sum(busy.values())) and got["hw_gfx_n"] == len(busy)
+    rows = _vec(query(d, scoped, t))
+    node_inst = {s.labels["instance"] for s in d.by_name["node_uname_info"] if s.labels["nodename"] == "mi355x-001"}
+    assert len(node_inst) == 1 and rows
+    assert {r["metric"]["instance"] for r in rows} == node_inst
+    names = {r["metric"]["__name__"] for r in rows}
+    assert {"node_uname_info", "node_hwmon_chip_names", "node_hwmon_power_input_watt", "node_drm_gpu_busy_percent"} <= names
