@@ -108,6 +108,8 @@ describe('fetchNodeMetrics (detail pages)', () => {
     await src.fetchNodeMetrics('mi355x-0');
     expect(paths(request, n)).toHaveLength(1);
     expect(paths(request, n)[0]).not.toContain('hostname=');
+    // ... and read that node alone, through node_uname_info
+    expect(paths(request, n)[0]).toContain('and on(instance) node_uname_info{nodename=~"mi355x-0"}');
   });
   it('serves the node\'s last snapshot stale through a transient failure, then null', async () => {
     let up = true;
