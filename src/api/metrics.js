@@ -33,12 +33,12 @@
  */
 
 import { METRIC_VIEWS } from './series.js';
-import { nodePowerQuery, podPowerQuery } from './promql.js';
+import { nodeExporterNodePowerQuery, nodePowerQuery, podPowerQuery } from './promql.js';
 import { createPromClient } from './promClient.js';
 import { createClusterSnapshots } from './clusterSnapshots.js';
 import { createScopedSnapshots } from './scopedSnapshots.js';
 import { createOwnerSnapshots } from './ownerSnapshots.js';
-import { createSeriesFetch } from './seriesFetch.js';
+import { createSeriesFetch, seriesQueryFor } from './seriesFetch.js';
 
 export {
   DISCOVERY_TTL_MS,
@@ -67,8 +67,11 @@ export {
   isExporterName,
   mergedQuery,
   nodeExporterProjected,
+  nodeExporterNodePowerQuery,
   nodeExporterQuery,
   nodeExporterScopedQuery,
+  nodeExporterScopedSeriesQuery,
+  nodeExporterSeriesQuery,
   nodeExporterSummaryQuery,
   nodePowerQuery,
   nodePowerSum,
@@ -133,7 +136,7 @@ export function createMetricsSource(opts) {
   const snaps = createClusterSnapshots(client, state);
   const scoped = createScopedSnapshots(client, state, snaps);
   const owners = createOwnerSnapshots(client, state);
-  const series = createSeriesFetch(client);
+  const series = createSeriesFetch(client, state);
 
   /**
    * One metrics snapshot of the series `view` needs (METRIC_VIEWS; default
@@ -190,7 +193,9 @@ export function createMetricsSource(opts) {
     },
     /** A node's GPU power over the last `rangeSec` (shape and nulls as fetchPodSeries). */
     fetchNodeSeries: function (nodeName, rangeSec, stepSec) {
-      return series.powerSeries('node|' + nodeName, nodePowerQuery(nodeName), rangeSec, stepSec);
+      return series.powerSeries('node|' + nodeName, function (source) {
+        return seriesQueryFor(source, nodePowerQuery(nodeName), nodeExporterNodePowerQuery(nodeName));
+      }, rangeSec, stepSec);
     },
     source: function () { return state.source; },
   };

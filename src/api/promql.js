@@ -346,6 +346,67 @@ export function nodeExporterScopedQuery(names) {
     ' or max by (' + labels + ') (' + uname + ')';
 }
 
+/** Each amdgpu chip's power: the average where node-exporter reports one, else the instantaneous input. */
+function hwChipPower() {
+  const N = SERIES.nodeExporter;
+  return '(max by (instance, chip) (' + N.power + ') or max by (instance, chip) (' + N.powerInput + '))' +
+    ' and on(instance, chip) count by (instance, chip) (' + N.chips + ')';
+}
+
+/** `q` renamed to `name` and tagged `series="<tag>"` (keeps `or`-ed lines apart: `or` ignores the name). */
+function asSeries(q, name, tag) {
+  return 'label_replace(label_replace(' + q + ', "__name__", "' + name + '", "", ""), "series", "' + tag + '", "", "")';
+}
+
+/**
+ * Power + HBM-used history of a node-exporter source in the exporter's
+ * shape (series.js names, per `hostname`, HBM in the exporter's MiB), so
+ * seriesFetch.js reads it unchanged: `nodes` — per node through
+ * node_uname_info, the nodes of `scope` or every node (`scope` null) — and
+ * `cluster` — the cluster-wide lines (`scope="cluster"`).
+ */
+function hwSeriesParts(scope) {
+  const N = SERIES.nodeExporter;
+  const E = SERIES.exporter;
+  const uname = 'max by (instance, nodename) (' + N.uname + (scope ? '{' + nodenameMatcher(scope) + '}' : '') + ')';
+  const perNode = function (q) {
+    return 'label_replace(sum by (nodename) ((' + q + ') * on(instance) group_left(nodename) ' + uname + '), "hostname", "$1", "nodename", "(.*)")';
+  };
+  const vram = 'max by (instance, card) (' + N.vramUsed + ') / ' + SERIES.exporterVramUnitBytes;
+  const cluster = function (q) { return 'label_replace(' + q + ', "scope", "cluster", "", "")'; };
+  return {
+    nodes: asSeries(perNode(hwChipPower()), E.power, 'power') + ' or ' + asSeries(perNode(vram), E.vramUsed, 'vram'),
+    cluster: cluster(asSeries('sum(' + hwChipPower() + ')', E.power, 'power')) + ' or ' +
+      cluster(asSeries('sum(' + vram + ' and on(instance) count by (instance) (' + N.chips + '))', E.vramUsed, 'vram')),
+  };
+}
+
+/** Every node's power + HBM lines of a node-exporter source (seriesQuery's counterpart). */
+export function nodeExporterSeriesQuery() {
+  return hwSeriesParts(null).nodes;
+}
+
+/**
+ * A paged view's lines of a node-exporter source, as scopedSeriesQuery: the
+ * page's nodes and the cluster line; `small` keeps every node's line while
+ * at most SMALL_HWMON_GPUS amdgpu chips report (the page may be asked before
+ * the node list names it), else the page's.
+ */
+export function nodeExporterScopedSeriesQuery(scope, small) {
+  const page = hwSeriesParts(scope).nodes;
+  const total = hwSeriesParts(null).cluster;
+  if (!small) return page + ' or ' + total;
+  const hw = hwmonGpuCount();
+  const all = sizeGuard(nodeExporterSeriesQuery(), true, hw, SMALL_HWMON_GPUS);
+  return (scope.length ? all + ' or ' + sizeGuard(page, false, hw, SMALL_HWMON_GPUS) : all) + ' or ' + total;
+}
+
+/** One node's total GPU power over time on a node-exporter source (Node detail history). */
+export function nodeExporterNodePowerQuery(nodeName) {
+  const uname = SERIES.nodeExporter.uname + '{nodename="' + promString(nodeName) + '"}';
+  return 'label_replace(sum(' + hwChipPower() + ' and on(instance) ' + uname + '), "__name__", "' + SERIES.exporter.power + '", "", "")';
+}
+
 /**
  * Cluster totals of a node-exporter source as server-side aggregates, the
  * figures summarizeMetrics takes from the per-GPU join (telemetry.js

@@ -14,14 +14,35 @@
  */
 
 import { SERIES, TOTAL_SERIES } from './series.js';
-import { scopedSeriesQuery, seriesQuery } from './promql.js';
+import {
+  gpuNodeCount,
+  nodeExporterScopedSeriesQuery,
+  nodeExporterSeriesQuery,
+  scopedSeriesQuery,
+  seriesQuery,
+} from './promql.js';
 import { num } from './telemetry.js';
 import { UNREACHABLE } from './promClient.js';
 
 /**
- * @param {PromClient} client
+ * The range query of a window on the known source: the exporter's, node-
+ * exporter's in the exporter's shape (promql.js nodeExporterSeriesQuery),
+ * or — while no answer has told which feeds Prometheus — both, node-
+ * exporter's only where no exporter reports, so the first window of a
+ * node-exporter cluster is not empty.
  */
-export function createSeriesFetch(client) {
+export function seriesQueryFor(source, exporterQ, hwQ) {
+  if (source === 'node-exporter') return hwQ;
+  if (source === 'amd-exporter') return exporterQ;
+  return exporterQ + ' or ((' + hwQ + ') unless on() (' + gpuNodeCount() + '))';
+}
+
+/**
+ * @param {PromClient} client
+ * @param {{source: ('amd-exporter'|'node-exporter'|null)}} [state]  which exporter feeds Prometheus (shared)
+ */
+export function createSeriesFetch(client, state) {
+  const st = state || { source: 'amd-exporter' };
   let cache = null; // { range, step, end, base, scope, data }
   client.onInvalidate(function () { cache = null; });
 
@@ -35,8 +56,11 @@ export function createSeriesFetch(client) {
     const E = SERIES.exporter;
     const parts = [['power', E.power, 1], ['vram', E.vramUsed, SERIES.exporterVramUnitBytes]];
     const scoped = Array.isArray(scope);
-    const sk = scoped ? (small ? 'small:' : '') + scope.map(String).join(',') : null;
-    const q = scoped ? scopedSeriesQuery(scope.map(String), !!small) : seriesQuery();
+    const src = st.source;
+    const sk = (src || '?') + '|' + (scoped ? (small ? 'small:' : '') + scope.map(String).join(',') : '*');
+    const q = seriesQueryFor(src,
+      scoped ? scopedSeriesQuery(scope.map(String), !!small) : seriesQuery(),
+      scoped ? nodeExporterScopedSeriesQuery(scope.map(String), !!small) : nodeExporterSeriesQuery());
     function from(base) {
       const end = Math.floor(client.now() / 1000 / step) * step;
       const fresh = !cache || cache.range !== range || cache.step !== step ||
@@ -88,10 +112,12 @@ export function createSeriesFetch(client) {
    * [[t, W]]}`; `power` is empty when nothing matches. Null when Prometheus is
    * unreachable.
    */
-  function powerSeries(scope, q, rangeSec, stepSec) {
+  function powerSeries(scope, query, rangeSec, stepSec) {
     const range = rangeSec || 1800;
     const step = stepSec || 30;
-    const key = 'power|' + scope + '|' + range + '|' + step;
+    // `query`: the PromQL, or a function of the source (the node history reads node-exporter too)
+    const q = typeof query === 'function' ? query(st.source) : query;
+    const key = 'power|' + scope + '|' + range + '|' + step + '|' + st.source;
     return client.shared(key, function () {
       return client.withPrometheus(function (base) {
         const end = Math.floor(client.now() / 1000 / step) * step;

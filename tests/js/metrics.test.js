@@ -587,3 +587,39 @@ describe('answer shapes match src/api/types.ts (no tsc offline: this pins the dr
     m.gpus.forEach((g) => conforms(g, 'GpuTelemetry'));
   });
 });
+
+describe('power / HBM series on either source', () => {
+  const ne = () => ({
+    chips: [vec({ __name__: 'node_hwmon_chip_names', instance: 'i0', chip: '0000:05:00_0', chip_name: 'amdgpu' }, 1)],
+    power: [vec({ __name__: 'node_hwmon_power_input_watt', instance: 'i0', chip: '0000:05:00_0' }, 650)],
+    uname: [vec({ __name__: 'node_uname_info', instance: 'i0', nodename: 'mi355x-0' }, 1)],
+  });
+  const ranges = (request) => request.mock.calls.map((c) => decodeURIComponent(c[0])).filter((p) => p.indexOf('/query_range') >= 0);
+  it('before any answer says which exporter feeds Prometheus, the window asks both (node-exporter where no exporter reports)', async () => {
+    const request = prom({ data: null, ne: ne() });
+    await createMetricsSource({ request }).fetchSeries(1800, 30, ['mi355x-0']);
+    const q = ranges(request)[0];
+    expect(q).toContain('sum by (__name__, hostname) ({__name__=~"gpu_power_usage|gpu_used_vram", hostname=~"mi355x-0"})');
+    expect(q).toContain('node_uname_info{nodename=~"mi355x-0"}');
+    expect(q).toContain('unless on() (count(count by (hostname)');
+  });
+  it('on a node-exporter source: node-exporter\'s lines alone, through node_uname_info', async () => {
+    const request = prom({ data: null, ne: ne() });
+    const src = createMetricsSource({ request });
+    await src.fetchGpuMetrics();
+    await src.fetchSeries(1800, 30, ['mi355x-0']);
+    await src.fetchNodeSeries('mi355x-0', 1800, 30);
+    const [page, node] = ranges(request);
+    expect(page).toContain('node_uname_info{nodename=~"mi355x-0"}');
+    expect(page).not.toContain('hostname=~');
+    expect(node).toContain('node_uname_info{nodename="mi355x-0"}');
+    expect(node).not.toContain('hostname=');
+  });
+  it('on an exporter source: the exporter\'s lines alone', async () => {
+    const request = prom({ data: exporterData(['n0']) });
+    const src = createMetricsSource({ request });
+    await src.fetchGpuMetrics();
+    await src.fetchSeries(1800, 30, ['n0']);
+    expect(ranges(request)[0]).not.toContain('node_uname_info');
+  });
+});

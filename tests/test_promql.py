@@ -503,3 +503,42 @@ def test_node_exporter_summary_and_scoped_query_against_the_synthetic_cluster():
     assert {r["metric"]["instance"] for r in rows} == node_inst
     names = {r["metric"]["__name__"] for r in rows}
     assert {"node_uname_info", "node_hwmon_chip_names", "node_hwmon_power_input_watt", "node_drm_gpu_busy_percent"} <= names
+
+
+def test_node_exporter_series_in_the_exporter_shape():
+    """nodeExporterScopedSeriesQuery: per-node power / HBM lines (exporter names, `hostname`, HBM in MiB) of the
+    page's nodes through node_uname_info, plus the cluster lines — what seriesFetch.js reads for the exporter."""
+    from headlamp_intel_gpu_plugin_amd.sim.apiserver import make_fake
+
+    q, node_q = _js("[m.nodeExporterScopedSeriesQuery(['mi355x-001'], false), m.nodeExporterNodePowerQuery('mi355x-001')]")
+    fc = make_fake(3, source="node-exporter", latency_ms=0)
+    d, t = fc.db, 1_000_000.0
+    body = json.loads(query_range(d, q, t - 60, t, 30.0))
+    assert body["status"] == "success", body
+    lines = {(r["metric"]["__name__"], r["metric"].get("hostname"), r["metric"].get("scope")): r["values"]
+             for r in body["data"]["result"]}
+    assert set(lines) == {("gpu_power_usage", "mi355x-001", None), ("gpu_used_vram", "mi355x-001", None),
+                          ("gpu_power_usage", None, "cluster"), ("gpu_used_vram", None, "cluster")}
+    inst = next(s.labels["instance"] for s in d.by_name["node_uname_info"] if s.labels["nodename"] == "mi355x-001")
+    chips = {s.labels["chip"] for s in d.by_name["node_hwmon_chip_names"]
+             if s.labels["instance"] == inst and s.labels.get("chip_name") == "amdgpu"}
+
+    def power_at(instances, ts):
+        tot = 0.0
+        for name in ("node_hwmon_power_input_watt",):
+            for s in d.by_name.get(name, []):
+                if s.labels["instance"] in instances and (s.labels["instance"] != inst or s.labels["chip"] in chips):
+                    tot += s.at(ts)[1]
+        return tot
+
+    ts, v = lines[("gpu_power_usage", "mi355x-001", None)][-1]
+    assert float(v) == pytest.approx(power_at({inst}, float(ts)))
+    all_insts = {s.labels["instance"] for s in d.by_name["node_uname_info"]}
+    ts, v = lines[("gpu_power_usage", None, "cluster")][-1]
+    assert float(v) == pytest.approx(power_at(all_insts, float(ts)))
+    vram = sum(s.at(t)[1] for s in d.by_name["node_drm_memory_vram_used_bytes"] if s.labels["instance"] == inst) / 1048576
+    assert float(lines[("gpu_used_vram", "mi355x-001", None)][-1][1]) == pytest.approx(vram)
+    node_body = json.loads(query_range(d, node_q, t - 60, t, 30.0))
+    (row,) = node_body["data"]["result"]
+    assert row["metric"]["__name__"] == "gpu_power_usage"
+    assert float(row["values"][-1][1]) == pytest.approx(power_at({inst}, float(row["values"][-1][0])))

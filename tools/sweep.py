@@ -210,14 +210,16 @@ def main():
     p.add_argument("--stress", action="store_true", help="watch-churn stress of the cluster-size axis instead")
     p.add_argument("--stress-nodes", default="16,64,256,1000")
     p.add_argument("--events", type=int, default=1000)
-    p.add_argument("--beyond", default="", help="extra node counts past the BASELINE configs, e.g. 16,32,64,256,1000")
+    p.add_argument("--beyond", default="", help="extra node counts past the BASELINE configs, e.g. 16,32,64,256,1000; hN = N nodes, node-exporter hwmon only")
     p.add_argument("--only-beyond", action="store_true", help="skip the BASELINE points (run --beyond only)")
     args = p.parse_args()
     if args.stress:
         return stress(args)
     os.makedirs(args.out, exist_ok=True)
     rows = []
-    points = ([] if args.only_beyond else POINTS) + [("nodes", v.strip()) for v in args.beyond.split(",") if v.strip()]
+    # --beyond 16,64,h256: "hN" is an N-node cluster whose Prometheus holds node-exporter's hwmon series only
+    points = ([] if args.only_beyond else POINTS) + [("hwmon", v.strip()[1:]) if v.strip().startswith("h") else ("nodes", v.strip())
+                                                     for v in args.beyond.split(",") if v.strip()]
     for kind, val in points:
         line = run(kind, val, args)
         rows.append({"kind": kind, "point": val, "line": line})
