@@ -64,6 +64,8 @@ export {
   gpuPodCount,
   hostnameMatcher,
   hwmonGpuCount,
+  hwNodePowerSum,
+  hwPowerRankQuery,
   isExporterName,
   mergedQuery,
   nodeExporterProjected,
@@ -83,6 +85,7 @@ export {
   powerRankQuery,
   promString,
   rankedClusterQuery,
+  rankedHwQuery,
   rankedOwnersQuery,
   regexLiteral,
   scopedSeriesQuery,

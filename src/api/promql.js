@@ -401,6 +401,40 @@ export function nodeExporterScopedSeriesQuery(scope, small) {
   return (scope.length ? all + ' or ' + sizeGuard(page, false, hw, SMALL_HWMON_GPUS) : all) + ' or ' + total;
 }
 
+/** Each node's total GPU power on a node-exporter source (the ranking key), per `nodename`; names matching `filter`. */
+export function hwNodePowerSum(filter) {
+  const N = SERIES.nodeExporter;
+  const f = String(filter || '').trim().toLowerCase();
+  const sel = f ? '{nodename=~".*' + promString(regexLiteral(f)) + '.*"}' : '';
+  return 'sum by (nodename) ((' + hwChipPower() + ') * on(instance) group_left(nodename) max by (instance, nodename) (' +
+    N.uname + sel + '))';
+}
+
+/** powerRankQuery on a node-exporter source: the page of nodes by total GPU power, ranked by Prometheus. */
+export function hwPowerRankQuery(page, per, filter) {
+  const r = hwNodePowerSum(filter);
+  const top = function (n) { return 'topk(' + n + ', ' + r + ')'; };
+  return page > 0 ? top(per * (page + 1)) + ' unless on(nodename) ' + top(per * page) : top(per);
+}
+
+/**
+ * rankedClusterQuery on a node-exporter source, in ONE request: the GPU
+ * series of the instances whose node_uname_info names a ranked node, those
+ * node_uname_info rows, the ranking as `agg="rank"` rows (with `hostname` =
+ * nodename, as the exporter's) and how many nodes are ranked.
+ */
+export function rankedHwQuery(rank) {
+  const N = SERIES.nodeExporter;
+  const s = hwPowerRankQuery(rank.page, rank.per, rank.filter);
+  const labels = NODE_EXPORTER_JOIN_LABELS.join(', ');
+  const gpuNames = nodeExporterNames().filter(function (n) { return n !== N.uname; });
+  const uname = N.uname + ' and on(nodename) (' + s + ')';
+  return 'max by (' + labels + ') ({__name__=~"' + gpuNames.join('|') + '"} and on(instance) (' + uname + '))' +
+    ' or max by (' + labels + ') (' + uname + ')' +
+    ' or ' + sizeRow('label_replace(' + s + ', "hostname", "$1", "nodename", "(.*)")', 'rank') +
+    ' or ' + sizeRow('count(' + hwNodePowerSum(rank.filter) + ')', 'ranked');
+}
+
 /** One node's total GPU power over time on a node-exporter source (Node detail history). */
 export function nodeExporterNodePowerQuery(nodeName) {
   const uname = SERIES.nodeExporter.uname + '{nodename="' + promString(nodeName) + '"}';

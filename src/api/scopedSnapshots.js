@@ -25,6 +25,7 @@ import {
   nodeExporterScopedQuery,
   nodeExporterSummaryQuery,
   rankedClusterQuery,
+  rankedHwQuery,
   sizeGuard,
   sizeRow,
   smallClusterQuery,
@@ -277,6 +278,7 @@ export function createScopedSnapshots(client, state, snaps) {
    */
   function ranked(v, rank, summary, key) {
     const st = entry(key);
+    if (state.source === 'node-exporter') return hwRanked(st, v, rank, summary);
     return client.withPrometheus(function (base) {
       // The page's names come with the answer: ask for the static series
       // while the nodes last shown (most likely shown again) lack a copy.
@@ -288,24 +290,16 @@ export function createScopedSnapshots(client, state, snaps) {
         st.failures = 0;
         const rows = res.rows;
         const j = joinExporterResults(rows);
-        const order = [];
-        const watts = {};
-        for (let i = 0; i < rows.__agg.length; i++) {
-          const r = rows.__agg[i];
-          if (!isRow(r) || r.metric.agg !== 'rank' || typeof r.metric.hostname !== 'string') continue;
-          const w = num(r.value[1]);
-          order.push([r.metric.hostname, w === null ? -Infinity : w]);
-          watts[r.metric.hostname] = w;
-        }
-        order.sort(function (a, b) { return b[1] - a[1] || (a[0] < b[0] ? -1 : a[0] > b[0] ? 1 : 0); });
-        const names = order.map(function (x) { return x[0]; });
+        const ro = rankOrder(rows);
+        const names = ro.names;
+        const watts = ro.watts;
         scopeStatics(j, names, withStatic);
         const count = sizeFromRows(rows.__agg, 'ranked');
         const totals = summary ? totalsOf(rows) || zeroTotals() : undefined;
         if (j.gpus.length > 0 || count > 0) state.source = 'amd-exporter';
         // Nothing ranked and no exporter seen: maybe node-exporter feeds this
         // Prometheus (no hostname label to rank by) — the cluster-wide
-        // snapshot instead, in name order.
+        // snapshot decides, and a node-exporter source is then ranked its way.
         else if (state.source !== 'amd-exporter') return NOT_SCOPED;
         const out = result(st, base, q, j, names, totals, v, undefined);
         out.rank = { by: rank.by, page: rank.page, per: rank.per, filter: rank.filter, count: count, watts: watts };
@@ -313,7 +307,56 @@ export function createScopedSnapshots(client, state, snaps) {
       });
     }, function () {
       return staleOrNull(st, STALE_FAILURES, client.invalidate);
-    }).then(function (r) { return r === NOT_SCOPED ? snaps.cluster(v) : r; });
+    }).then(function (r) {
+      if (r !== NOT_SCOPED) return r;
+      return snaps.cluster(v).then(function (m) {
+        return m && state.source === 'node-exporter' ? hwRanked(st, v, rank, summary) : m;
+      });
+    });
+  }
+
+  /** The `agg="rank"` rows of a ranked answer: node names highest power first, and each node's watts. */
+  function rankOrder(rows) {
+    const order = [];
+    const watts = {};
+    for (let i = 0; i < rows.__agg.length; i++) {
+      const r = rows.__agg[i];
+      if (!isRow(r) || r.metric.agg !== 'rank' || typeof r.metric.hostname !== 'string') continue;
+      const w = num(r.value[1]);
+      order.push([r.metric.hostname, w === null ? -Infinity : w]);
+      watts[r.metric.hostname] = w;
+    }
+    order.sort(function (a, b) { return b[1] - a[1] || (a[0] < b[0] ? -1 : a[0] > b[0] ? 1 : 0); });
+    return { names: order.map(function (x) { return x[0]; }), watts: watts };
+  }
+
+  /**
+   * A page of GPU nodes in power order on a node-exporter source (promql.js
+   * rankedHwQuery): Prometheus sums each node's amdgpu chips through
+   * node_uname_info and ranks them; the page's series, the ranking and the
+   * count come in one request, the totals with it.
+   */
+  function hwRanked(st, v, rank, summary) {
+    return client.withPrometheus(function (base) {
+      const q = rankedHwQuery(rank) + (summary ? ' or ' + nodeExporterSummaryQuery() : '');
+      return client.combined(base, q).then(function (res) {
+        if (!res.ok) return UNREACHABLE;
+        st.failures = 0;
+        const rows = res.rows;
+        const ro = rankOrder(rows);
+        const inRank = {};
+        for (let i = 0; i < ro.names.length; i++) inRank[ro.names[i]] = true;
+        const j = joinNodeExporterResults(rows);
+        j.gpus = j.gpus.filter(function (g) { return inRank[g.nodeName] === true; });
+        const totals = summary ? hwTotalsFromRows(rows.__agg) || zeroTotals() : undefined;
+        const out = result(st, base, q, j, ro.names, totals, v, undefined);
+        out.rank = { by: rank.by, page: rank.page, per: rank.per, filter: rank.filter,
+          count: sizeFromRows(rows.__agg, 'ranked'), watts: ro.watts };
+        return out;
+      });
+    }, function () {
+      return staleOrNull(st, STALE_FAILURES, client.invalidate);
+    });
   }
 
   /**

@@ -28,7 +28,7 @@ import {
   summarizeMetrics, summaryQuery, totalsFromRows, joinExporterResults, splitByName,
 } from '../../src/api/metrics.js';
 import { makeContext, makeDeviceConfig, makeGpuNode, makeGpuPod, makePluginPod } from './fixtures.js';
-import { BASE0, exporterData, flatten, prom, vec } from './promFake.js';
+import { BASE0, exporterData, flatten, prom } from './promFake.js';
 
 const h = React.createElement;
 const names = (n) => Array.from({ length: n }, (_, i) => 'mi355x-' + String(i).padStart(3, '0'));
@@ -279,18 +279,6 @@ describe('Metrics in power order: Prometheus ranks the page', () => {
     expect(pagePart(qs[2])).not.toContain(SERIES.exporter.vramTotal);
     expect(again.gpus[0].vramTotalBytes).toBeGreaterThan(0);
   });
-  it('a node-exporter Prometheus (nothing to rank by) answers with the cluster-wide snapshot in name order', async () => {
-    const ne = { node_uname_info: [{ metric: { __name__: 'node_uname_info', instance: 'i0', nodename: 'mi355x-000' }, value: [0, '1'] }] };
-    ne[SERIES.nodeExporter.chips] = [{ metric: { __name__: 'node_hwmon_chip_names', chip_name: 'amdgpu', instance: 'i0', chip: '0000:05:00_0' }, value: [0, '1'] }];
-    const s = createMetricsSource({ request: prom({ data: {}, ne: ne }) });
-    const m = await s.fetchGpuMetrics('gauges', { rank: rank(0), summary: true });
-    expect(m.source).toBe('node-exporter');
-    expect(m.rank).toBe(undefined);
-    expect(m.gpus.map((g) => g.nodeName)).toEqual(['mi355x-000']);
-    const vm = metricsView(ctxOf(1), { metrics: m, series: null, fetchError: null, fetching: false }, { pager: { sort: 'power' } });
-    expect(sectionTitles(vm)).not.toContain('No AMD GPU Metrics in Prometheus');
-    expect(cards(vm)).toEqual(['mi355x-000 — 1 × MI355X']);
-  });
   it('telemetryScope asks for the ranked page when the page can rank (GPU Nodes, Metrics)', () => {
     const ctx = ctxOf(12);
     expect(telemetryScope(ctx, { sort: 'power', page: 1, filter: ' X-0 ' }, true)).toEqual({ enabled: true, rank: { by: 'power', page: 1, per: 8, filter: 'x-0' } });
@@ -461,82 +449,6 @@ describe('metrics client: scoped snapshots', () => {
     // a new page of nodes needs their statics: asked for again
     await s.fetchGpuMetrics('topology', { scope: ['mi355x-002'] });
     expect(decoded(fake)[2]).toContain(SERIES.exporter.vramTotal);
-  });
-  it('falls back to the cluster-wide snapshot cut to the scope for a node-exporter source', async () => {
-    const ne = { node_uname_info: [{ metric: { __name__: 'node_uname_info', instance: 'i0', nodename: 'mi355x-000' }, value: [0, '1'] }] };
-    ne[SERIES.nodeExporter.chips] = [{ metric: { __name__: 'node_hwmon_chip_names', chip_name: 'amdgpu', instance: 'i0', chip: '0000:05:00_0' }, value: [0, '1'] }];
-    const fake = prom({ data: {}, ne: ne });
-    const s = source(fake);
-    const m = await s.fetchGpuMetrics('gauges', { scope: ['mi355x-000'], summary: true });
-    expect(m.source).toBe('node-exporter');
-    expect(m.gpus.map((g) => g.nodeName)).toEqual(['mi355x-000']);
-    expect(m.totals.gpus).toBe(1);
-  });
-  it('node-exporter source, small-cluster fetch before the node list: every GPU of a small cluster, the page of a larger one', async () => {
-    function neData(nodes) {
-      const ne = { node_uname_info: [] };
-      ne[SERIES.nodeExporter.chips] = [];
-      nodes.forEach((n, k) => {
-        ne.node_uname_info.push({ metric: { __name__: 'node_uname_info', instance: 'i' + k, nodename: n }, value: [0, '1'] });
-        for (let c = 0; c < 8; c++) {
-          const chip = '0000:' + (5 + c * 16).toString(16).padStart(2, '0') + ':00_0';
-          ne[SERIES.nodeExporter.chips].push({ metric: { __name__: 'node_hwmon_chip_names', chip_name: 'amdgpu', instance: 'i' + k, chip: chip }, value: [0, '1'] });
-        }
-      });
-      return ne;
-    }
-    // 2 nodes (16 chips): the first answer (no names yet) holds the whole cluster, so the names arriving need no refetch.
-    let request = prom({ data: {}, ne: neData(names(2)) });
-    let s = createMetricsSource({ request });
-    let m = await s.fetchGpuMetrics('gauges', { scope: [], summary: true, small: true });
-    expect(m.source).toBe('node-exporter');
-    expect(Array.from(new Set(m.gpus.map((g) => g.nodeName)))).toEqual(names(2));
-    expect(m.small).toEqual({ count: 16, limit: 64, exceeded: false });
-    expect([m.totals.gpus, m.totals.nodes]).toEqual([16, 2]);
-    expect(request.mock.calls).toHaveLength(1);
-    // 12 nodes (96 chips): more than a page — only the scope's, flagged so the caller's key follows the names.
-    request = prom({ data: {}, ne: neData(names(12)) });
-    s = createMetricsSource({ request });
-    m = await s.fetchGpuMetrics('gauges', { scope: [], summary: true, small: true });
-    expect(m.gpus).toHaveLength(0);
-    expect(m.small.exceeded).toBe(true);
-    expect([m.totals.gpus, m.totals.nodes]).toEqual([96, 12]);
-    m = await s.fetchGpuMetrics('gauges', { scope: names(8), summary: true, small: true });
-    expect(Array.from(new Set(m.gpus.map((g) => g.nodeName)))).toEqual(names(8));
-    expect(m.gpus).toHaveLength(64);
-    expect(m.totals.gpus).toBe(96);
-    // page-scoped through node_uname_info: nothing cluster-wide is read
-    const qs = request.mock.calls.map((c) => decodeURIComponent(c[0]));
-    expect(qs).toHaveLength(2);
-    expect(qs[1]).toContain('and on(instance) node_uname_info{nodename=~"mi355x-000|');
-  });
-  it('node-exporter: the page\'s totals from server-side aggregates equal the cluster-wide join\'s', async () => {
-    const ne = { node_uname_info: [] };
-    ['node_hwmon_chip_names', 'node_hwmon_power_input_watt', 'node_hwmon_power_average_watt', 'node_hwmon_power_cap_watt',
-      'node_drm_gpu_busy_percent', 'node_drm_memory_vram_used_bytes', 'node_drm_memory_vram_size_bytes'].forEach((n) => (ne[n] = []));
-    names(10).forEach((n, k) => {
-      const inst = '10.0.1.' + k + ':9100';
-      ne.node_uname_info.push(vec({ __name__: 'node_uname_info', instance: inst, nodename: n }, 1));
-      ne.node_hwmon_chip_names.push(vec({ __name__: 'node_hwmon_chip_names', instance: inst, chip: 'platform_coretemp_0', chip_name: 'coretemp' }, 1));
-      for (let c = 0; c < 8; c++) {
-        const chip = '0000:' + String(10 + c) + ':00_0';
-        ne.node_hwmon_chip_names.push(vec({ __name__: 'node_hwmon_chip_names', instance: inst, chip: chip, chip_name: 'amdgpu' }, 1));
-        ne.node_hwmon_power_input_watt.push(vec({ __name__: 'node_hwmon_power_input_watt', instance: inst, chip: chip }, 500 + k + c));
-        // some chips also report an average: it wins
-        if (c % 3 === 0) ne.node_hwmon_power_average_watt.push(vec({ __name__: 'node_hwmon_power_average_watt', instance: inst, chip: chip }, 700 + c));
-        if (k % 2 === 0) ne.node_hwmon_power_cap_watt.push(vec({ __name__: 'node_hwmon_power_cap_watt', instance: inst, chip: chip }, 1400));
-        ne.node_drm_gpu_busy_percent.push(vec({ __name__: 'node_drm_gpu_busy_percent', instance: inst, card: 'card' + c }, 10 * c));
-        ne.node_drm_memory_vram_used_bytes.push(vec({ __name__: 'node_drm_memory_vram_used_bytes', instance: inst, card: 'card' + c }, 1e9 * (c + 1)));
-        ne.node_drm_memory_vram_size_bytes.push(vec({ __name__: 'node_drm_memory_vram_size_bytes', instance: inst, card: 'card' + c }, 288e9));
-      }
-    });
-    const wide = await createMetricsSource({ request: prom({ data: {}, ne: ne }) }).fetchGpuMetrics();
-    const expected = Object.assign(summarizeMetrics(wide), { nodes: 10 });
-    const paged = await createMetricsSource({ request: prom({ data: {}, ne: ne }) })
-      .fetchGpuMetrics('gauges', { scope: names(10).slice(0, 8), summary: true });
-    expect(paged.source).toBe('node-exporter');
-    expect(Array.from(new Set(paged.gpus.map((g) => g.nodeName)))).toEqual(names(8));
-    Object.keys(expected).forEach((k) => expect([k, paged.totals[k]]).toEqual([k, expected[k]]));
   });
   it('an empty scope with a summary asks for the totals only', async () => {
     const fake = prom({ data: exporterData(names(2)) });

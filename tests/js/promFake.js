@@ -141,6 +141,25 @@ function term(q, rows) {
     const n = Object.keys(hs).length;
     return n ? [vec({ __name__: nodes[1], agg: 'nodes' }, n)] : [];
   }
+  // promql.js rankedHwQuery: node-exporter's page in power order, its ranking and its count.
+  const hwPage = /^max by \([^)]*\) \((?:\{__name__=~"(.*?)"\} and on\(instance\) \()?node_uname_info and on\(nodename\) \((topk\(.*)\)\)?\)$/.exec(q);
+  if (hwPage) {
+    const keep = {};
+    (hwRankOf(hwPage[2], rows) || []).forEach((x) => (keep[x[0]] = true));
+    const named = rows.filter((r) => r.metric.__name__ === 'node_uname_info' && keep[r.metric.nodename]);
+    if (hwPage[1] === undefined) return named;
+    const insts = {};
+    named.forEach((r) => (insts[r.metric.instance] = true));
+    const re = new RegExp('^(?:' + hwPage[1] + ')$');
+    return rows.filter((r) => re.test(r.metric.__name__ || '') && insts[r.metric.instance] === true);
+  }
+  const hwRankRow = /^label_replace\(label_replace\((topk\(.*\)), "hostname", "\$1", "nodename", "\(\.\*\)"\), "agg", "rank", "", ""\)$/.exec(q);
+  if (hwRankRow) return (hwRankOf(hwRankRow[1], rows) || []).map((x) => vec({ nodename: x[0], hostname: x[0], agg: 'rank' }, x[1]));
+  const hwRanked = /^label_replace\(count\((sum by \(nodename\) .*)\), "agg", "ranked", "", ""\)$/.exec(q);
+  if (hwRanked) {
+    const n = hwNodeSums(hwRanked[1], rows).length;
+    return n ? [vec({ agg: 'ranked' }, n)] : [];
+  }
   // promql.js nodeExporterScopedQuery: node-exporter series of the instances node_uname_info names.
   const byNode = /^max by \([^)]*\) \((?:\{__name__=~"(.*?)"\} and on\(instance\) )?node_uname_info\{nodename(=~?)"((?:[^"\\]|\\.)*)"\}\)$/.exec(q);
   if (byNode) {
@@ -239,6 +258,48 @@ function countOf(expr, rows) {
     seen[m[1] === 'hostname' ? r.metric.hostname : r.metric.namespace + '/' + r.metric.pod] = true;
   });
   return Object.keys(seen).length;
+}
+
+/**
+ * promql.js hwNodePowerSum over `rows`: [[nodename, watts]] — each node's
+ * amdgpu chips (power average, else input) through node_uname_info, names
+ * matching its `nodename=~` filter.
+ */
+function hwNodeSums(expr, rows) {
+  const f = /node_uname_info\{nodename=~"((?:[^"\\]|\\.)*)"\}/.exec(expr);
+  const re = f ? new RegExp('^(?:' + f[1].replace(/\\\\/g, '\\') + ')$') : null;
+  const nodeOf = {};
+  rows.forEach((r) => {
+    if (r.metric.__name__ === 'node_uname_info' && (!re || re.test(r.metric.nodename || ''))) nodeOf[r.metric.instance] = r.metric.nodename;
+  });
+  const chips = {};
+  rows.forEach((r) => {
+    if (r.metric.__name__ === 'node_hwmon_chip_names' && r.metric.chip_name === 'amdgpu') chips[r.metric.instance + '/' + r.metric.chip] = true;
+  });
+  const power = {};
+  ['node_hwmon_power_input_watt', 'node_hwmon_power_average_watt'].forEach((name) => rows.forEach((r) => {
+    const k = r.metric.instance + '/' + r.metric.chip;
+    if (r.metric.__name__ === name && chips[k]) power[k] = parseFloat(r.value[1]);
+  }));
+  const by = {};
+  Object.keys(power).forEach((k) => {
+    const node = nodeOf[k.split('/')[0]];
+    if (node !== undefined) by[node] = (by[node] || 0) + power[k];
+  });
+  return Object.keys(by).map((n) => [n, by[n]]);
+}
+
+/** promql.js hwPowerRankQuery: the ranked page, [[nodename, watts], …] (null for another shape). */
+function hwRankOf(expr, rows) {
+  if (expr.indexOf('topk(') !== 0) return null;
+  const close = closing(expr, 4);
+  const inner = expr.slice(5, close);
+  const comma = inner.indexOf(', ');
+  const n = Number(inner.slice(0, comma));
+  const rest = /^ unless on\(nodename\) topk\((\d+), /.exec(expr.slice(close + 1));
+  const all = hwNodeSums(inner.slice(comma + 2), rows);
+  all.sort((a, b) => b[1] - a[1] || (a[0] < b[0] ? -1 : 1));
+  return all.slice(rest ? Number(rest[1]) : 0, n);
 }
 
 /** Index of the parenthesis closing the one at `open`. */

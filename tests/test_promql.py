@@ -542,3 +542,26 @@ def test_node_exporter_series_in_the_exporter_shape():
     (row,) = node_body["data"]["result"]
     assert row["metric"]["__name__"] == "gpu_power_usage"
     assert float(row["values"][-1][1]) == pytest.approx(power_at({inst}, float(row["values"][-1][0])))
+
+
+def test_node_exporter_ranked_page_against_the_synthetic_cluster():
+    """rankedHwQuery: the page of nodes by their amdgpu chips' total power (through node_uname_info), the page's
+    series and uname rows, the ranking rows (hostname = nodename) and the count — against an oracle."""
+    from headlamp_intel_gpu_plugin_amd.sim.apiserver import make_fake
+
+    q = _js("m.rankedHwQuery({by: 'power', page: 1, per: 2, filter: ''})")
+    fc = make_fake(5, source="node-exporter", latency_ms=0)
+    d, t = fc.db, 1_000_000.0
+    node_of = {s.labels["instance"]: s.labels["nodename"] for s in d.by_name["node_uname_info"]}
+    per_node = {}
+    for s in d.by_name["node_hwmon_power_input_watt"]:
+        n = node_of[s.labels["instance"]]
+        per_node[n] = per_node.get(n, 0.0) + s.at(t)[1]
+    order = sorted(per_node, key=lambda n: (-per_node[n], n))
+    rows = _vec(query(d, q, t))
+    rank = {r["metric"]["hostname"]: float(r["value"][1]) for r in rows if r["metric"].get("agg") == "rank"}
+    assert sorted(rank, key=lambda n: -rank[n]) == order[2:4]
+    assert all(rank[n] == pytest.approx(per_node[n]) for n in rank)
+    assert [float(r["value"][1]) for r in rows if r["metric"].get("agg") == "ranked"] == [5.0]
+    page_insts = {i for i, n in node_of.items() if n in rank}
+    assert {r["metric"]["instance"] for r in rows if "agg" not in r["metric"]} == page_insts
