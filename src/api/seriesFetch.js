@@ -15,7 +15,6 @@
 
 import { SERIES, TOTAL_SERIES } from './series.js';
 import {
-  gpuNodeCount,
   nodeExporterScopedSeriesQuery,
   nodeExporterSeriesQuery,
   scopedSeriesQuery,
@@ -25,16 +24,32 @@ import { num } from './telemetry.js';
 import { UNREACHABLE } from './promClient.js';
 
 /**
- * The range query of a window on the known source: the exporter's, node-
- * exporter's in the exporter's shape (promql.js nodeExporterSeriesQuery),
- * or — while no answer has told which feeds Prometheus — both, node-
- * exporter's only where no exporter reports, so the first window of a
- * node-exporter cluster is not empty.
+ * The range queries of a window, in the order to try them: the known
+ * source's — the exporter's, or node-exporter's in the exporter's shape
+ * (promql.js nodeExporterSeriesQuery) — or, while no answer has told which
+ * feeds Prometheus, the exporter's and then, only if it found no series at
+ * all, node-exporter's. A cluster with the exporter never pays for
+ * node-exporter's joins (node-exporter runs on nearly every node); the first
+ * window of a node-exporter cluster costs one more round trip.
  */
 export function seriesQueryFor(source, exporterQ, hwQ) {
-  if (source === 'node-exporter') return hwQ;
-  if (source === 'amd-exporter') return exporterQ;
-  return exporterQ + ' or ((' + hwQ + ') unless on() (' + gpuNodeCount() + '))';
+  if (source === 'node-exporter') return [hwQ];
+  if (source === 'amd-exporter') return [exporterQ];
+  return [exporterQ, hwQ];
+}
+
+/** A range answer with no series at all. */
+function noSeries(got) {
+  for (const k in got) return false;
+  return true;
+}
+
+/** `client.range` of the first of `qs` that finds any series (UNREACHABLE stops). */
+function rangeOf(client, base, qs, start, end, step) {
+  return client.range(base, qs[0], start, end, step, TOTAL_SERIES).then(function (got) {
+    if (got === UNREACHABLE || qs.length < 2 || !noSeries(got)) return got;
+    return rangeOf(client, base, qs.slice(1), start, end, step);
+  });
 }
 
 /**
@@ -58,7 +73,7 @@ export function createSeriesFetch(client, state) {
     const scoped = Array.isArray(scope);
     const src = st.source;
     const sk = (src || '?') + '|' + (scoped ? (small ? 'small:' : '') + scope.map(String).join(',') : '*');
-    const q = seriesQueryFor(src,
+    const qs = seriesQueryFor(src,
       scoped ? scopedSeriesQuery(scope.map(String), !!small) : seriesQuery(),
       scoped ? nodeExporterScopedSeriesQuery(scope.map(String), !!small) : nodeExporterSeriesQuery());
     function from(base) {
@@ -67,7 +82,7 @@ export function createSeriesFetch(client, state) {
         cache.base !== base || cache.scope !== sk || end - cache.end >= range;
       const start = fresh ? end - range : cache.end + step;
       if (!fresh && start > end) return Promise.resolve(cache.data);
-      return client.range(base, q, start, end, step, TOTAL_SERIES).then(function (got) {
+      return rangeOf(client, base, qs, start, end, step).then(function (got) {
         if (got === UNREACHABLE) return UNREACHABLE;
         const data = { rangeSec: range, stepSec: step };
         if (scoped) {
@@ -115,13 +130,14 @@ export function createSeriesFetch(client, state) {
   function powerSeries(scope, query, rangeSec, stepSec) {
     const range = rangeSec || 1800;
     const step = stepSec || 30;
-    // `query`: the PromQL, or a function of the source (the node history reads node-exporter too)
+    // `query`: the PromQL, or a function of the source giving the queries to try (seriesQueryFor)
     const q = typeof query === 'function' ? query(st.source) : query;
+    const qs = Array.isArray(q) ? q : [q];
     const key = 'power|' + scope + '|' + range + '|' + step + '|' + st.source;
     return client.shared(key, function () {
       return client.withPrometheus(function (base) {
         const end = Math.floor(client.now() / 1000 / step) * step;
-        return client.range(base, q, end - range, end, step, TOTAL_SERIES).then(function (got) {
+        return rangeOf(client, base, qs, end - range, end, step).then(function (got) {
           if (got === UNREACHABLE) return UNREACHABLE;
           // Sum whatever rows came back per step (one row after `sum by (__name__)`).
           const total = {};

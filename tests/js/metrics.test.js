@@ -595,13 +595,19 @@ describe('power / HBM series on either source', () => {
     uname: [vec({ __name__: 'node_uname_info', instance: 'i0', nodename: 'mi355x-0' }, 1)],
   });
   const ranges = (request) => request.mock.calls.map((c) => decodeURIComponent(c[0])).filter((p) => p.indexOf('/query_range') >= 0);
-  it('before any answer says which exporter feeds Prometheus, the window asks both (node-exporter where no exporter reports)', async () => {
-    const request = prom({ data: null, ne: ne() });
+  it('before any answer says which exporter feeds Prometheus: the exporter\'s window, node-exporter\'s only if it finds nothing', async () => {
+    // (the JS fake answers every range query with exporter-shaped rows unless told otherwise)
+    const empty = vi.fn((path) => (path.indexOf('/query_range') >= 0 && path.indexOf('node_uname_info') < 0
+      ? Promise.resolve({ status: 'success', data: { resultType: 'matrix', result: [] } }) : prom({ data: null, ne: ne() })(path)));
+    await createMetricsSource({ request: empty }).fetchSeries(1800, 30, ['mi355x-0']);
+    const [first, second] = ranges(empty);
+    expect(first).toContain('sum by (__name__, hostname) ({__name__=~"gpu_power_usage|gpu_used_vram", hostname=~"mi355x-0"})');
+    expect(first).not.toContain('node_uname_info');
+    expect(second).toContain('node_uname_info{nodename=~"mi355x-0"}');
+    // an exporter cluster: one window, no node-exporter query
+    const request = prom({ data: exporterData(['mi355x-0']) });
     await createMetricsSource({ request }).fetchSeries(1800, 30, ['mi355x-0']);
-    const q = ranges(request)[0];
-    expect(q).toContain('sum by (__name__, hostname) ({__name__=~"gpu_power_usage|gpu_used_vram", hostname=~"mi355x-0"})');
-    expect(q).toContain('node_uname_info{nodename=~"mi355x-0"}');
-    expect(q).toContain('unless on() (count(count by (hostname)');
+    expect(ranges(request)).toHaveLength(1);
   });
   it('on a node-exporter source: node-exporter\'s lines alone, through node_uname_info', async () => {
     const request = prom({ data: null, ne: ne() });
