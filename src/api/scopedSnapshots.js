@@ -19,7 +19,6 @@
 import { SERIES, SMALL_CLUSTER_NODES, SMALL_HWMON_GPUS, STALE_FAILURES } from './series.js';
 import {
   exporterQuery,
-  gpuNodeCount,
   hwmonGpuCount,
   nodeExporterProjected,
   nodeExporterScopedQuery,
@@ -60,6 +59,9 @@ for (let i = 0; i < HW_TOTAL_TAGS.length; i++) SIZE_TAGS[HW_TOTAL_TAGS[i]] = tru
 function totalsOf(rows) {
   return totalsFromRows(rows.__agg.filter(function (r) { return !SIZE_TAGS[r.metric.agg]; }));
 }
+
+/** Marker: a node-exporter source found by the probe, too large for its series to have come along (ask hwScoped). */
+const HW_NEXT = Object.freeze({ hwNext: true });
 
 /** Scoped answers kept (stale fallbacks, structural sharing), most recent first. */
 const SCOPED_KEYS = 16;
@@ -176,15 +178,7 @@ export function createScopedSnapshots(client, state, snaps) {
       else if (scope.length) parts.push(exporterQuery(withStatic, true, v, scope));
       if (summary) parts.push(summaryQuery());
       // smallClusterQuery already carries the gpu_nodes row.
-      if (probing && parts.length) {
-        parts.push(sourceProbe(!small));
-        // node-exporter's page and totals too, where no exporter reports: a
-        // node-exporter cluster of any size is told apart AND served in this wave.
-        const hw = [];
-        if (scope.length) hw.push(nodeExporterScopedQuery(scope));
-        if (summary) hw.push(nodeExporterSummaryQuery());
-        if (hw.length) parts.push('(' + hw.join(' or ') + ') unless on() (' + gpuNodeCount() + ')');
-      }
+      if (probing && parts.length) parts.push(sourceProbe(!small));
       if (!parts.length) return Promise.resolve(result(st, base, null, { gpus: [], xgmi: {}, links: {} }, scope, undefined, v));
       const q = parts.join(' or ');
       return client.combined(base, q).then(function (res) {
@@ -198,11 +192,14 @@ export function createScopedSnapshots(client, state, snaps) {
         if (j.gpus.length > 0 || (!!totals && totals.gpus > 0) || reporting > 0) {
           state.source = 'amd-exporter';
         } else if (probing && sizeFromRows(rows.__agg, 'hwmon') > 0) {
-          // node-exporter's amdgpu hwmon feeds this Prometheus: its series
-          // came along — every GPU on a small cluster, the page's on a larger
-          // one — with its totals (one wave).
+          // node-exporter's amdgpu hwmon feeds this Prometheus: on a small
+          // cluster every GPU's series came along (one wave); a larger one is
+          // asked for its page and totals next (hwScoped) — the probe carries
+          // nothing more, so a cluster with the exporter, whose nodes run
+          // node-exporter too, never pays for node-exporter's joins.
           state.source = 'node-exporter';
-          return hwAnswer(st, base, q, rows, v, scope, summary, small);
+          if (!joinNodeExporterResults(rows).gpus.length) return HW_NEXT;
+          return hwAnswer(st, base, q, rows, v, scope, summary, small, true);
         }
         // (No exporter and no amdgpu hwmon: no GPU telemetry — this answer stands.)
         scopeStatics(j, scope, withStatic);
@@ -212,6 +209,7 @@ export function createScopedSnapshots(client, state, snaps) {
     }, function () {
       return staleOrNull(st, STALE_FAILURES, client.invalidate);
     }).then(function (r) {
+      if (r === HW_NEXT) return hwScoped(st, v, scope, summary, key, small);
       return r === NOT_SCOPED ? snaps.cluster(v).then(function (m) { return cut(m, scope, summary, key, small); }) : r;
     });
   }
@@ -252,11 +250,14 @@ export function createScopedSnapshots(client, state, snaps) {
    * not the Kubernetes node name there, so the page is cut from the
    * cluster-wide snapshot instead (its join also tries `node` and `instance`).
    */
-  function hwAnswer(st, base, q, rows, v, scope, summary, small) {
+  function hwAnswer(st, base, q, rows, v, scope, summary, small, everyGpu) {
     st.failures = 0;
     const chips = sizeFromRows(rows.__agg, 'hwmon');
     const whole = !!small && chips <= SMALL_HWMON_GPUS;
     const j = joinNodeExporterResults(rows);
+    // `everyGpu`: the rows hold every GPU (the probe on a small cluster), so
+    // the totals are summed here rather than asked for.
+    const allTotals = everyGpu && summary ? totalsOfAll(j) : null;
     if (!whole) {
       const inScope = {};
       for (let i = 0; i < scope.length; i++) inScope[scope[i]] = true;
@@ -265,9 +266,22 @@ export function createScopedSnapshots(client, state, snaps) {
       const named = un.some(function (r) { return isRow(r) && inScope[r.metric.nodename] === true; });
       if (scope.length && !j.gpus.length && !named && chips > 0) return NOT_SCOPED;
     }
-    const totals = summary ? hwTotalsFromRows(rows.__agg) || zeroTotals() : undefined;
+    const totals = summary ? hwTotalsFromRows(rows.__agg) || allTotals || zeroTotals() : undefined;
     const sized = small ? { count: chips, limit: SMALL_HWMON_GPUS, exceeded: !whole } : undefined;
     return result(st, base, q, j, scope, totals, v, sized);
+  }
+
+  /** summarizeMetrics of a join holding every GPU, plus the nodes reporting. */
+  function totalsOfAll(j) {
+    const seen = {};
+    let nodes = 0;
+    for (let i = 0; i < j.gpus.length; i++) {
+      if (!seen[j.gpus[i].nodeName]) {
+        seen[j.gpus[i].nodeName] = true;
+        nodes++;
+      }
+    }
+    return Object.assign(summarizeMetrics(j), { nodes: nodes });
   }
 
   /**

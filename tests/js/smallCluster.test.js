@@ -188,18 +188,22 @@ describe('scoped fetches: the first answer decides the telemetry source (one wav
     expect(decoded(fake)[1]).not.toContain('gpu_power_usage');
   });
 
-  it('a larger node-exporter cluster (more amdgpu chips than one page) is served in the first wave, page-scoped', async () => {
+  it('a larger node-exporter cluster (more amdgpu chips than one page) is asked for its page and totals next, page-scoped', async () => {
     const fake = prom({ data: {}, ne: neOf(names(9), 8) });
     const s = createMetricsSource({ request: fake });
     const m = await s.fetchGpuMetrics('gauges', { scope: names(8), summary: true });
-    expect(fake.mock.calls.length).toBe(1);
+    // the probe carries no node-exporter join (clusters with the exporter run node-exporter too): a second wave
+    expect(fake.mock.calls.length).toBe(2);
+    expect(decoded(fake)[0]).not.toContain('node_uname_info{nodename');
     expect(s.source()).toBe('node-exporter');
     expect(m.totals.gpus).toBe(72);
     expect(m.gpus.length).toBe(64);
-    // a refresh asks node-exporter for the page's nodes and the totals: nothing cluster-wide
+    // the page's nodes through node_uname_info and the totals: nothing cluster-wide, then and on every refresh
     await s.fetchGpuMetrics('gauges', { scope: names(8), summary: true });
-    expect(fake.mock.calls.length).toBe(2);
-    expect(decoded(fake)[1]).toContain('and on(instance) node_uname_info{nodename=~');
-    expect(decoded(fake)[1]).not.toMatch(/\{__name__=~"[^"]*"\}\)( or|$)/);
+    expect(fake.mock.calls.length).toBe(3);
+    [1, 2].forEach((i) => {
+      expect(decoded(fake)[i]).toContain('and on(instance) node_uname_info{nodename=~');
+      expect(decoded(fake)[i]).not.toMatch(/\{__name__=~"[^"]*"\}\)( or|$)/);
+    });
   });
 });
