@@ -304,6 +304,14 @@ class Evaluator:
             if lt != "vector" or rt != "vector":
                 raise PromQLError(f"set operator {op} needs vectors on both sides")
             return self._set_op(op, lv, rv, matching)
+        if op == "unless" and matching and matching[0] == "on" and not matching[1]:
+            # `x unless on() <non-empty>` is empty whatever x is (every row
+            # matches on no labels): answered without evaluating x, as `and`
+            # above — the client's first query appends node-exporter's page
+            # and totals this way, to be dropped where the exporter reports.
+            rt, rv = self.instant(rhs, t)
+            if rt == "vector" and rv:
+                return ("vector", [])
         lt, lv = self.instant(lhs, t)
         rt, rv = self.instant(rhs, t)
         if op in SET_OPS:

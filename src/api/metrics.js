@@ -131,10 +131,14 @@ export function createMetricsSource(opts) {
   // Which exporter answered ('amd-exporter' | 'node-exporter' | null: not
   // known yet), and whether every exporter series carries `hostname` (lean
   // live queries). Shared by every part; forgotten when Prometheus moves.
-  const state = { source: null, lean: false };
+  // `deciding`: the telemetry fetch in flight while the source is unknown
+  // (its answer decides it); a series window that found no exporter series
+  // waits for it before asking node-exporter (seriesFetch.js).
+  const state = { source: null, lean: false, deciding: null };
   client.onInvalidate(function () {
     state.source = null;
     state.lean = false;
+    state.deciding = null;
   });
   const snaps = createClusterSnapshots(client, state);
   const scoped = createScopedSnapshots(client, state, snaps);
@@ -154,6 +158,16 @@ export function createMetricsSource(opts) {
    * @returns {Promise<GpuMetrics|null>}
    */
   function fetchGpuMetrics(view, opts) {
+    const p = telemetry(view, opts);
+    if (state.source === null) {
+      const d = p.then(function () {}, function () {});
+      state.deciding = d;
+      d.then(function () { if (state.deciding === d) state.deciding = null; });
+    }
+    return p;
+  }
+
+  function telemetry(view, opts) {
     const v = view === undefined ? 'all' : view;
     if (METRIC_VIEWS.indexOf(v) < 0) return Promise.reject(new Error('fetchGpuMetrics: unknown view ' + JSON.stringify(view)));
     if (opts && opts.rank) {

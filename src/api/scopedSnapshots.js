@@ -19,6 +19,7 @@
 import { SERIES, SMALL_CLUSTER_NODES, SMALL_HWMON_GPUS, STALE_FAILURES } from './series.js';
 import {
   exporterQuery,
+  gpuNodeCount,
   hwmonGpuCount,
   nodeExporterProjected,
   nodeExporterScopedQuery,
@@ -59,9 +60,6 @@ for (let i = 0; i < HW_TOTAL_TAGS.length; i++) SIZE_TAGS[HW_TOTAL_TAGS[i]] = tru
 function totalsOf(rows) {
   return totalsFromRows(rows.__agg.filter(function (r) { return !SIZE_TAGS[r.metric.agg]; }));
 }
-
-/** Marker: a node-exporter source found by the probe, too large for its series to have come along (ask hwScoped). */
-const HW_NEXT = Object.freeze({ hwNext: true });
 
 /** Scoped answers kept (stale fallbacks, structural sharing), most recent first. */
 const SCOPED_KEYS = 16;
@@ -178,7 +176,16 @@ export function createScopedSnapshots(client, state, snaps) {
       else if (scope.length) parts.push(exporterQuery(withStatic, true, v, scope));
       if (summary) parts.push(summaryQuery());
       // smallClusterQuery already carries the gpu_nodes row.
-      if (probing && parts.length) parts.push(sourceProbe(!small));
+      if (probing && parts.length) {
+        parts.push(sourceProbe(!small));
+        // node-exporter's page and totals too, where no exporter reports (a
+        // few instant aggregates, cheap next to the range series): a
+        // node-exporter cluster of any size is told apart AND served here.
+        const hw = [];
+        if (scope.length) hw.push(nodeExporterScopedQuery(scope));
+        if (summary) hw.push(nodeExporterSummaryQuery());
+        if (hw.length) parts.push('(' + hw.join(' or ') + ') unless on() (' + gpuNodeCount() + ')');
+      }
       if (!parts.length) return Promise.resolve(result(st, base, null, { gpus: [], xgmi: {}, links: {} }, scope, undefined, v));
       const q = parts.join(' or ');
       return client.combined(base, q).then(function (res) {
@@ -192,14 +199,11 @@ export function createScopedSnapshots(client, state, snaps) {
         if (j.gpus.length > 0 || (!!totals && totals.gpus > 0) || reporting > 0) {
           state.source = 'amd-exporter';
         } else if (probing && sizeFromRows(rows.__agg, 'hwmon') > 0) {
-          // node-exporter's amdgpu hwmon feeds this Prometheus: on a small
-          // cluster every GPU's series came along (one wave); a larger one is
-          // asked for its page and totals next (hwScoped) — the probe carries
-          // nothing more, so a cluster with the exporter, whose nodes run
-          // node-exporter too, never pays for node-exporter's joins.
+          // node-exporter's amdgpu hwmon feeds this Prometheus: every GPU's
+          // series came along on a small cluster, the page's and the totals
+          // on any (one wave).
           state.source = 'node-exporter';
-          if (!joinNodeExporterResults(rows).gpus.length) return HW_NEXT;
-          return hwAnswer(st, base, q, rows, v, scope, summary, small, true);
+          return hwAnswer(st, base, q, rows, v, scope, summary, small, joinNodeExporterResults(rows).gpus.length > 0);
         }
         // (No exporter and no amdgpu hwmon: no GPU telemetry — this answer stands.)
         scopeStatics(j, scope, withStatic);
@@ -209,7 +213,6 @@ export function createScopedSnapshots(client, state, snaps) {
     }, function () {
       return staleOrNull(st, STALE_FAILURES, client.invalidate);
     }).then(function (r) {
-      if (r === HW_NEXT) return hwScoped(st, v, scope, summary, key, small);
       return r === NOT_SCOPED ? snaps.cluster(v).then(function (m) { return cut(m, scope, summary, key, small); }) : r;
     });
   }
@@ -255,8 +258,8 @@ export function createScopedSnapshots(client, state, snaps) {
     const chips = sizeFromRows(rows.__agg, 'hwmon');
     const whole = !!small && chips <= SMALL_HWMON_GPUS;
     const j = joinNodeExporterResults(rows);
-    // `everyGpu`: the rows hold every GPU (the probe on a small cluster), so
-    // the totals are summed here rather than asked for.
+    // `everyGpu`: the rows hold every GPU (the probe on a small cluster): the
+    // totals can be summed here when no aggregate rows came along.
     const allTotals = everyGpu && summary ? totalsOfAll(j) : null;
     if (!whole) {
       const inScope = {};

@@ -24,13 +24,10 @@ import { num } from './telemetry.js';
 import { UNREACHABLE } from './promClient.js';
 
 /**
- * The range queries of a window, in the order to try them: the known
- * source's — the exporter's, or node-exporter's in the exporter's shape
- * (promql.js nodeExporterSeriesQuery) — or, while no answer has told which
- * feeds Prometheus, the exporter's and then, only if it found no series at
- * all, node-exporter's. A cluster with the exporter never pays for
- * node-exporter's joins (node-exporter runs on nearly every node); the first
- * window of a node-exporter cluster costs one more round trip.
+ * The range queries of a window: the known source's — the exporter's, or
+ * node-exporter's in the exporter's shape (promql.js nodeExporterSeriesQuery)
+ * — or, while no answer has told which feeds Prometheus, the exporter's
+ * first and node-exporter's second (rangeOf).
  */
 export function seriesQueryFor(source, exporterQ, hwQ) {
   if (source === 'node-exporter') return [hwQ];
@@ -44,11 +41,21 @@ function noSeries(got) {
   return true;
 }
 
-/** `client.range` of the first of `qs` that finds any series (UNREACHABLE stops). */
-function rangeOf(client, base, qs, start, end, step) {
+/**
+ * `client.range` of qs[0]; when it finds no series and a node-exporter query
+ * follows (the source was unknown), qs[1] — but only once the telemetry
+ * answer in flight (`st.deciding`) has named node-exporter the source. A
+ * cluster with the exporter never pays for node-exporter's joins
+ * (node-exporter runs on nearly every node), one without GPU telemetry sends
+ * nothing more, and the first window of a node-exporter cluster costs one
+ * more round trip.
+ */
+function rangeOf(client, st, base, qs, start, end, step) {
   return client.range(base, qs[0], start, end, step, TOTAL_SERIES).then(function (got) {
     if (got === UNREACHABLE || qs.length < 2 || !noSeries(got)) return got;
-    return rangeOf(client, base, qs.slice(1), start, end, step);
+    return Promise.resolve(st.deciding).then(function () {
+      return st.source === 'node-exporter' ? client.range(base, qs[1], start, end, step, TOTAL_SERIES) : got;
+    });
   });
 }
 
@@ -82,7 +89,7 @@ export function createSeriesFetch(client, state) {
         cache.base !== base || cache.scope !== sk || end - cache.end >= range;
       const start = fresh ? end - range : cache.end + step;
       if (!fresh && start > end) return Promise.resolve(cache.data);
-      return rangeOf(client, base, qs, start, end, step).then(function (got) {
+      return rangeOf(client, st, base, qs, start, end, step).then(function (got) {
         if (got === UNREACHABLE) return UNREACHABLE;
         const data = { rangeSec: range, stepSec: step };
         if (scoped) {
@@ -137,7 +144,7 @@ export function createSeriesFetch(client, state) {
     return client.shared(key, function () {
       return client.withPrometheus(function (base) {
         const end = Math.floor(client.now() / 1000 / step) * step;
-        return rangeOf(client, base, qs, end - range, end, step).then(function (got) {
+        return rangeOf(client, st, base, qs, end - range, end, step).then(function (got) {
           if (got === UNREACHABLE) return UNREACHABLE;
           // Sum whatever rows came back per step (one row after `sum by (__name__)`).
           const total = {};

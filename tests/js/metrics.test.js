@@ -599,7 +599,9 @@ describe('power / HBM series on either source', () => {
     // (the JS fake answers every range query with exporter-shaped rows unless told otherwise)
     const empty = vi.fn((path) => (path.indexOf('/query_range') >= 0 && path.indexOf('node_uname_info') < 0
       ? Promise.resolve({ status: 'success', data: { resultType: 'matrix', result: [] } }) : prom({ data: null, ne: ne() })(path)));
-    await createMetricsSource({ request: empty }).fetchSeries(1800, 30, ['mi355x-0']);
+    // as the pages fetch: the telemetry (whose answer decides the source) next to the window
+    const src = createMetricsSource({ request: empty });
+    await Promise.all([src.fetchGpuMetrics('gauges', { scope: ['mi355x-0'], summary: true }), src.fetchSeries(1800, 30, ['mi355x-0'])]);
     const [first, second] = ranges(empty);
     expect(first).toContain('sum by (__name__, hostname) ({__name__=~"gpu_power_usage|gpu_used_vram", hostname=~"mi355x-0"})');
     expect(first).not.toContain('node_uname_info');
@@ -608,6 +610,12 @@ describe('power / HBM series on either source', () => {
     const request = prom({ data: exporterData(['mi355x-0']) });
     await createMetricsSource({ request }).fetchSeries(1800, 30, ['mi355x-0']);
     expect(ranges(request)).toHaveLength(1);
+    // no GPU telemetry at all: the empty window stands, nothing more is asked
+    const none = vi.fn((path) => (path.indexOf('/query_range') >= 0
+      ? Promise.resolve({ status: 'success', data: { resultType: 'matrix', result: [] } }) : prom({ data: {} })(path)));
+    const s2 = createMetricsSource({ request: none });
+    await Promise.all([s2.fetchGpuMetrics('gauges', { scope: ['mi355x-0'], summary: true }), s2.fetchSeries(1800, 30, ['mi355x-0'])]);
+    expect(ranges(none)).toHaveLength(1);
   });
   it('on a node-exporter source: node-exporter\'s lines alone, through node_uname_info', async () => {
     const request = prom({ data: null, ne: ne() });

@@ -96,10 +96,10 @@ describe('node-exporter source: paged, totalled and ranked by Prometheus', () =>
     expect(Array.from(new Set(m.gpus.map((g) => g.nodeName)))).toEqual(names(8));
     expect(m.gpus).toHaveLength(64);
     expect(m.totals.gpus).toBe(96);
-    // the probe, node-exporter's first answer (totals, no page yet), then the page through node_uname_info
+    // the probe (with the totals), then the page through node_uname_info
     const qs = request.mock.calls.map((c) => decodeURIComponent(c[0]));
-    expect(qs).toHaveLength(3);
-    expect(qs[2]).toContain('and on(instance) node_uname_info{nodename=~"mi355x-000|');
+    expect(qs).toHaveLength(2);
+    expect(qs[1]).toContain('and on(instance) node_uname_info{nodename=~"mi355x-000|');
   });
   it('node-exporter: the page\'s totals from server-side aggregates equal the cluster-wide join\'s', async () => {
     const ne = { node_uname_info: [] };

@@ -188,20 +188,20 @@ describe('scoped fetches: the first answer decides the telemetry source (one wav
     expect(decoded(fake)[1]).not.toContain('gpu_power_usage');
   });
 
-  it('a larger node-exporter cluster (more amdgpu chips than one page) is asked for its page and totals next, page-scoped', async () => {
+  it('a larger node-exporter cluster (more amdgpu chips than one page) is served in the first wave, page-scoped', async () => {
     const fake = prom({ data: {}, ne: neOf(names(9), 8) });
     const s = createMetricsSource({ request: fake });
     const m = await s.fetchGpuMetrics('gauges', { scope: names(8), summary: true });
-    // the probe carries no node-exporter join (clusters with the exporter run node-exporter too): a second wave
-    expect(fake.mock.calls.length).toBe(2);
-    expect(decoded(fake)[0]).not.toContain('node_uname_info{nodename');
+    // the probe carries node-exporter's page and totals, dropped where the exporter reports (`unless on()`)
+    expect(fake.mock.calls.length).toBe(1);
+    expect(decoded(fake)[0]).toContain(') unless on() (count(count by (hostname)');
     expect(s.source()).toBe('node-exporter');
     expect(m.totals.gpus).toBe(72);
     expect(m.gpus.length).toBe(64);
     // the page's nodes through node_uname_info and the totals: nothing cluster-wide, then and on every refresh
     await s.fetchGpuMetrics('gauges', { scope: names(8), summary: true });
-    expect(fake.mock.calls.length).toBe(3);
-    [1, 2].forEach((i) => {
+    expect(fake.mock.calls.length).toBe(2);
+    [0, 1].forEach((i) => {
       expect(decoded(fake)[i]).toContain('and on(instance) node_uname_info{nodename=~');
       expect(decoded(fake)[i]).not.toMatch(/\{__name__=~"[^"]*"\}\)( or|$)/);
     });
