@@ -94,7 +94,7 @@ export function amdSchedule(request, clock, timeoutMs) {
   function pageOpen(page, onData) {
     const keyOf = page === 'pods' ? ownersKey : function () { return scoped(false).key; };
     const fetch0 = page === 'pods' ? fetchPodsPage : page === 'nodes' ? fetchNodesPage : fetchMetricsPage;
-    const fetch = onData ? function () { return fetch0().then(onData); } : fetch0;
+    const fetch = onData ? function () { return fetch0(onData).then(onData); } : fetch0;
     const k0 = keyOf();
     const first = k0 === null ? Promise.resolve() : fetch();
     const second = listed(page === 'pods' ? 'podsState' : 'nodesState').then(function () {
@@ -128,9 +128,17 @@ export function amdSchedule(request, clock, timeoutMs) {
   function fetchNodesPage() {
     return metrics.fetchGpuMetrics('topology', scoped(false).opts).then(function (m) { pageMetrics.nodes = m; });
   }
-  function fetchMetricsPage() {
+  /** The Metrics page's hook (providerCore.js useGpuMetrics): telemetry shown as it comes (`early`), then the series. */
+  function fetchMetricsPage(early) {
     const sc = scoped(true);
-    return Promise.all([metrics.fetchGpuMetrics('gauges', sc.opts), metrics.fetchSeries(1800, 30, sc.scope, sc.small)]).then(function (r) {
+    const mp = metrics.fetchGpuMetrics('gauges', sc.opts);
+    mp.then(function (m) {
+      if (!m || !early) return;
+      metricsPage.metrics = m;
+      metricsPage.fetchError = null;
+      early();
+    });
+    return Promise.all([mp, metrics.fetchSeries(1800, 30, sc.scope, sc.small)]).then(function (r) {
       metricsPage.metrics = r[0];
       metricsPage.series = r[1];
       metricsPage.fetchError = r[0] ? null : 'Could not reach Prometheus';

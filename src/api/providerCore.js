@@ -268,7 +268,8 @@ export function createProviderCore(React, lib, deps) {
    * unmount) drops the previous key's in-flight answer (the reference's
    * `cancelled` flag, MetricsPage.tsx:206-230).
    * @param {string|null} key
-   * @param {() => Promise<[any, any]>} fetchPair  resolves [metrics, series]
+   * @param {(early: (metrics: any) => void) => Promise<[any, any]>} fetchPair  resolves [metrics, series];
+   *   may call `early(metrics)` when the telemetry is in before the series (the page shows it at once)
    * @param {boolean} [seriesOnly]  the fetch returns series only: unreachable = no series
    * @param {{failureReason?: () => string}} [source]  says whether a failure was RBAC (403) or an outage
    */
@@ -285,7 +286,12 @@ export function createProviderCore(React, lib, deps) {
       if (key === null) return undefined;
       let cancelled = false;
       setState(function (s) { return Object.assign({}, s, { fetching: true, fetchError: null }); });
-      fetchPair().then(
+      fetchPair(function early(metrics) {
+        if (cancelled || !metrics) return;
+        // Telemetry ahead of its range series: shown now, the series (and
+        // `fetching`) follow with the pair.
+        setState(function (s) { return Object.assign({}, s, { metrics: metrics, fetchError: null }); });
+      }).then(
         function (pair) {
           if (cancelled) return;
           const metrics = pair[0];
@@ -367,18 +373,22 @@ export function createProviderCore(React, lib, deps) {
     const rk = rank ? rank.by + ':' + rank.page + ':' + rank.per + ':' + rank.filter : null;
     const key = 'gpus|' + sourceKey(cluster, settings) + '|' + v + '|' + series + '|' + settings.seriesMinutes +
       (rk ? '|rank:' + rk : sm ? smallKey(ex[0], names) : scoped ? '|scope:' + names.join(',') : '');
-    const res = useMetricsFetch(on ? key : null, function () {
+    const res = useMetricsFetch(on ? key : null, function (early) {
       if (rk) {
         // The ranked page's names come with the answer: its series follow it.
         return source.fetchGpuMetrics(v, { rank: rank, summary: v === 'gauges' }).then(function (m) {
           if (!series || !m) return [m, null];
+          early(m);
           return source.fetchSeries(settings.seriesMinutes * 60, seriesStepSec(settings), m.scope || [])
             .then(function (sr) { return [m, sr]; });
         });
       }
       const opts = scoped ? { scope: names, summary: v === 'gauges', small: sm } : undefined;
+      const mp = source.fetchGpuMetrics(v, opts);
+      // The range series usually answer after the instant telemetry: the page shows the telemetry first.
+      if (series) mp.then(early, function () {});
       return Promise.all([
-        source.fetchGpuMetrics(v, opts),
+        mp,
         series ? source.fetchSeries(settings.seriesMinutes * 60, seriesStepSec(settings), names || undefined, sm) : Promise.resolve(null),
       ]);
     }, false, source);

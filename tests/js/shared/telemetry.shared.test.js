@@ -48,6 +48,25 @@ describe('shared: telemetry on the detail and Metrics pages (' + tier + ')', () 
     r.unmount();
   });
 
+  it('Metrics shows the instant telemetry while its range series are still in flight, then the series', async () => {
+    const fake = prom({ data: exporterData(['mi355x-0', 'mi355x-1']) });
+    const held = [];
+    cluster((p) => (p.indexOf('/query_range') >= 0
+      ? new Promise((res) => { held.push(() => res(fake(p))); })
+      : fake(p)));
+    const fresh = createPlugin({ React, lib, CommonComponents: CC });
+    const r = render(h(fresh.AmdGpuDataProvider, null, h(fresh.MetricsPage)));
+    await r.settle();
+    expect(held.length).toBeGreaterThan(0);
+    expect(r.text()).toContain('GPUs Monitored');
+    expect(r.text()).not.toContain('Power & HBM (last');
+    held.splice(0).forEach((go) => go());
+    await r.settle();
+    expect(r.text()).toContain('GPUs Monitored');
+    expect(r.text()).toContain('Power & HBM (last');
+    r.unmount();
+  });
+
   it('Metrics without RBAC for the Prometheus proxy says access was denied and which permission is missing', async () => {
     cluster(() => Promise.reject(Object.assign(new Error('services "kube-prometheus-stack-prometheus" is forbidden'), { status: 403 })));
     // A fresh plugin: no metrics client state from earlier specs.
