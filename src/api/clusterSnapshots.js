@@ -17,7 +17,16 @@
  */
 
 import { SERIES, STALE_FAILURES } from './series.js';
-import { exporterNodeQuery, exporterQuery, mergedQuery, nodeExporterQuery, nodeExporterScopedQuery } from './promql.js';
+import {
+  exporterNodeQuery,
+  exporterQuery,
+  gpuNodeCount,
+  hwmonGpuCount,
+  mergedQuery,
+  nodeExporterQuery,
+  nodeExporterScopedQuery,
+  sizeRow,
+} from './promql.js';
 import {
   applyStatics,
   isRow,
@@ -27,6 +36,7 @@ import {
   nodeSlice,
   shareGpus,
   shareMap,
+  sizeFromRows,
   staticsOf,
 } from './telemetry.js';
 import { UNREACHABLE, staleOrNull } from './promClient.js';
@@ -147,10 +157,26 @@ export function createClusterSnapshots(client, state) {
     if (state.source === 'node-exporter') return hwNode(st, key, clusterWide);
     return client.withPrometheus(function (base) {
       const withStatic = st.links === null || client.now() - st.staticAt >= client.ttl;
-      return client.combined(base, exporterNodeQuery(key, withStatic)).then(function (res) {
+      // Source not known yet (a detail page opened first): the same request
+      // carries the source probe's counts and node-exporter's series of this
+      // node — O(one node) either way, one wave on a cluster of either
+      // exporter or of none.
+      const probing = state.source === null;
+      const q = exporterNodeQuery(key, withStatic) + (probing
+        ? ' or ' + sizeRow(gpuNodeCount(), 'gpu_nodes') + ' or ' + sizeRow(hwmonGpuCount(), 'hwmon') +
+          ' or (' + nodeExporterScopedQuery([key]) + ') unless on() (' + gpuNodeCount() + ')'
+        : '');
+      return client.combined(base, q).then(function (res) {
         if (!res.ok) return UNREACHABLE;
         st.failures = 0;
         const j = joinExporterResults(res.rows);
+        if (probing) {
+          if (j.gpus.length || sizeFromRows(res.rows.__agg, 'gpu_nodes') > 0) state.source = 'amd-exporter';
+          else if (sizeFromRows(res.rows.__agg, 'hwmon') > 0) {
+            state.source = 'node-exporter';
+            return hwNodeAnswer(st, key, base, res.rows);
+          } else return nodeAnswer(st, key, base, { gpus: [] }, 'none'); // no GPU telemetry in this Prometheus
+        }
         if (!j.gpus.length) return NOT_SCOPED;
         if (withStatic) {
           st.links = j.links;
@@ -160,21 +186,28 @@ export function createClusterSnapshots(client, state) {
           j.links = st.links;
           if (!applyStatics(j.gpus, st.statics)) st.staticAt = -Infinity;
         }
-        const prev = st.last;
-        st.last = {
-          source: 'amd-exporter',
-          gpus: prev ? shareGpus(prev.gpus, j.gpus) : j.gpus,
-          xgmi: prev ? shareMap(prev.xgmi, j.xgmi) : j.xgmi,
-          links: prev ? shareMap(prev.links, j.links || {}) : j.links || {},
-          fetchedAt: client.fetchedAt(),
-          prometheusPath: base,
-          scope: key,
-        };
-        return st.last;
+        return nodeAnswer(st, key, base, j, 'amd-exporter');
       });
     }, function () {
       return staleOrNull(st, STALE_FAILURES, client.invalidate);
     }).then(function (r) { return r === NOT_SCOPED ? clusterWide() : r; });
+  }
+
+  /** One node's snapshot from its joined rows `j` ([] : no GPU telemetry at all), sharing structure with the last. */
+  function nodeAnswer(st, key, base, j, source) {
+    const gpus = j.gpus || [];
+    const prev = st.last;
+    const same = prev && prev.source === (source === 'none' ? null : source);
+    st.last = {
+      source: source === 'none' ? null : source,
+      gpus: same ? shareGpus(prev.gpus, gpus) : gpus,
+      xgmi: same ? shareMap(prev.xgmi, j.xgmi || {}) : j.xgmi || {},
+      links: same ? shareMap(prev.links, j.links || {}) : j.links || {},
+      fetchedAt: client.fetchedAt(),
+      prometheusPath: base,
+      scope: key,
+    };
+    return st.last;
   }
 
   /**
@@ -188,21 +221,20 @@ export function createClusterSnapshots(client, state) {
       const q = nodeExporterScopedQuery([key]);
       return client.combined(base, q).then(function (res) {
         if (!res.ok) return UNREACHABLE;
-        st.failures = 0;
-        const un = res.rows[SERIES.nodeExporter.uname] || [];
-        if (!un.some(function (r) { return isRow(r) && r.metric.nodename === key; })) return NOT_SCOPED;
-        const j = joinNodeExporterResults(res.rows);
-        const gpus = j.gpus.filter(function (g) { return g.nodeName === key; });
-        const prev = st.last;
-        st.last = {
-          source: 'node-exporter', gpus: prev ? shareGpus(prev.gpus, gpus) : gpus, xgmi: {}, links: {},
-          fetchedAt: client.fetchedAt(), prometheusPath: base, scope: key,
-        };
-        return st.last;
+        return hwNodeAnswer(st, key, base, res.rows);
       });
     }, function () {
       return staleOrNull(st, STALE_FAILURES, client.invalidate);
     }).then(function (r) { return r === NOT_SCOPED ? clusterWide() : r; });
+  }
+
+  /** hwNode's answer (or the probing node query's node-exporter rows): NOT_SCOPED when no node_uname_info names the node. */
+  function hwNodeAnswer(st, key, base, rows) {
+    st.failures = 0;
+    const un = rows[SERIES.nodeExporter.uname] || [];
+    if (!un.some(function (r) { return isRow(r) && r.metric.nodename === key; })) return NOT_SCOPED;
+    const j = joinNodeExporterResults(rows);
+    return nodeAnswer(st, key, base, { gpus: j.gpus.filter(function (g) { return g.nodeName === key; }) }, 'node-exporter');
   }
 
   return {

@@ -211,6 +211,10 @@ export function createMetricsSource(opts) {
     /** A node's GPU power over the last `rangeSec` (shape and nulls as fetchPodSeries). */
     fetchNodeSeries: function (nodeName, rangeSec, stepSec) {
       return series.powerSeries('node|' + nodeName, function (source) {
+        // Source unknown (a detail page opened first): both in one query — each
+        // selects this node only, and `or` keeps the exporter's line at a step
+        // where both report (one row, the same label set).
+        if (source === null) return nodePowerQuery(nodeName) + ' or ' + nodeExporterNodePowerQuery(nodeName);
         return seriesQueryFor(source, nodePowerQuery(nodeName), nodeExporterNodePowerQuery(nodeName));
       }, rangeSec, stepSec);
     },

@@ -63,6 +63,30 @@ describe('node-exporter source: paged, totalled and ranked by Prometheus', () =>
     expect(m.gpus.map((g) => g.nodeName)).toEqual(['mi355x-000']);
     expect(m.totals.gpus).toBe(1);
   });
+  it('a Node detail opened first (source unknown) reads its node in ONE request on node-exporter, and on a Prometheus with no GPU series', async () => {
+    const ne = { node_uname_info: [] };
+    ne[SERIES.nodeExporter.chips] = [];
+    ['mi355x-000', 'mi355x-001'].forEach((n, k) => {
+      ne.node_uname_info.push({ metric: { __name__: 'node_uname_info', instance: 'i' + k, nodename: n }, value: [0, '1'] });
+      ne[SERIES.nodeExporter.chips].push({ metric: { __name__: 'node_hwmon_chip_names', chip_name: 'amdgpu', instance: 'i' + k, chip: '0000:05:00_0' }, value: [0, '1'] });
+    });
+    const fake = prom({ data: {}, ne: ne });
+    const s = source(fake);
+    const m = await s.fetchNodeMetrics('mi355x-001');
+    expect(m.source).toBe('node-exporter');
+    expect(m.gpus.map((g) => g.nodeName)).toEqual(['mi355x-001']);
+    const queries = fake.mock.calls.map((c) => decodeURIComponent(c[0])).filter((p) => p.indexOf('/api/v1/query') >= 0);
+    expect(queries).toHaveLength(1);
+    expect(s.source()).toBe('node-exporter');
+
+    const none = prom({ data: {} });
+    const s2 = source(none);
+    const m2 = await s2.fetchNodeMetrics('mi355x-000');
+    expect(m2).not.toBeNull();
+    expect(m2.gpus).toEqual([]);
+    expect(none.mock.calls.map((c) => decodeURIComponent(c[0])).filter((p) => p.indexOf('/api/v1/query') >= 0)).toHaveLength(1);
+  });
+
   it('node-exporter source, small-cluster fetch before the node list: every GPU of a small cluster, the page of a larger one', async () => {
     function neData(nodes) {
       const ne = { node_uname_info: [] };
