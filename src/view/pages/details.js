@@ -100,7 +100,8 @@ function nodeDetailSection(raw, name, cap, alloc, podsOnNode, loading, own, xg, 
   let blocks = [kv(rows)];
   if (count > 0) {
     blocks.push(slotsBlock(raw, podsOnNode, own));
-    blocks.push(matrixBlock(phys, xg, lk));
+    // xGMI links join the GPUs of a node: a single-GPU node has no matrix to show.
+    if (phys > 1) blocks.push(matrixBlock(phys, xg, lk));
   }
   if (series) blocks = blocks.concat(powerHistoryBlocks(name, 'Node', series));
   return section('AMD GPU', blocks);

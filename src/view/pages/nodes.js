@@ -212,7 +212,8 @@ export function nodesView(ctx, opts) {
         if (count > 0) {
           // Without the pods the strip is exact only from exporter owners.
           if (!podsPend || own) blocks.push(slotsBlock(n, podsPend ? NO_PODS : pods, own));
-          blocks.push(matrixBlock(getNodePhysicalGpuCount(n), xg, lk));
+          const phys = getNodePhysicalGpuCount(n);
+          if (phys > 1) blocks.push(matrixBlock(phys, xg, lk)); // no xGMI peers on a single-GPU node
         }
         return section(name, blocks, n.metadata.uid || name);
       }, now);

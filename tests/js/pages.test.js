@@ -10,6 +10,7 @@ import {
   nodesView,
   podsView,
   podDetailView,
+  nodeDetailView,
   podGpuAssignments,
   tempCell,
   eccCell,
@@ -297,6 +298,16 @@ describe('nodesView', () => {
     const m = firstBlock(s, 'matrix');
     expect(m.matrix.size).toBe(8);
     expect(m.fullMesh).toBe(true);
+  });
+  it('a single-GPU node has slots but no xGMI matrix (no peers), on its card and its detail section', () => {
+    const ctx = makeContext({ nodes: [makeGpuNode('g1', { gpus: 1 })], pods: [makeGpuPod('a', { node: 'g1', gpus: 1 })] });
+    const s = findSection(nodesView(ctx, opts), 'g1');
+    expect(firstBlock(s, 'slots').slots).toHaveLength(1);
+    expect(firstBlock(s, 'matrix')).toBeFalsy();
+    const d = nodeDetailView(makeGpuNode('g1', { gpus: 1 }), ctx);
+    expect(firstBlock(d, 'slots')).toBeTruthy();
+    expect(firstBlock(d, 'matrix')).toBeFalsy();
+    expect(renderPage(nodesView(ctx, opts))).not.toContain('xgmi-matrix');
   });
   it('uses exporter pod labels for exact slots when metrics are given', () => {
     const E = SERIES.exporter;
