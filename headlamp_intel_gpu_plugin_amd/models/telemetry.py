@@ -78,6 +78,16 @@ def populate(db: TSDB, cluster: SyntheticCluster, source: str = "amd-exporter", 
         if source == "node-exporter":
             db.add(Series({"__name__": "node_uname_info", "instance": f"{instance}:9100", "nodename": node,
                            "job": "node-exporter"}, fn=lambda t: 1.0, interval=interval))
+            # The host CPU's hwmon chip: temperatures the plugin must not take for a GPU's.
+            cpu = {"chip": "platform_coretemp_0", "instance": f"{instance}:9100"}
+            db.add(Series(dict(cpu, __name__="node_hwmon_chip_names", chip_name="coretemp"), fn=lambda t: 1.0,
+                          interval=interval))
+            db.add(Series(dict(cpu, __name__="node_hwmon_temp_celsius", sensor="temp1"), fn=lambda t: 47.0,
+                          interval=interval))
+            db.add(Series(dict(cpu, __name__="node_hwmon_temp_crit_celsius", sensor="temp1"), fn=lambda t: 100.0,
+                          interval=interval))
+            db.add(Series(dict(cpu, __name__="node_hwmon_sensor_label", sensor="temp1", label="Package id 0"),
+                          fn=lambda t: 1.0, interval=interval))
         for g in range(spec.gpus_per_node):
             owner = cluster.gpu_owner.get((node, g))
             busy = owner is not None
@@ -148,6 +158,16 @@ def populate(db: TSDB, cluster: SyntheticCluster, source: str = "amd-exporter", 
                                "instance": inst}, fn=power, interval=interval))
                 db.add(Series({"__name__": "node_hwmon_power_cap_watt", "chip": chip, "sensor": "power1",
                                "instance": inst}, fn=lambda t: BOARD_POWER_W, interval=interval))
+                # amdgpu hwmon temperatures: temp2 "junction" (its crit is the throttle threshold) and
+                # temp3 "mem"; an MI355X reports no edge temperature.
+                for sensor, label, fn, crit in (("temp2", "junction", temp, JUNCTION_SLOWDOWN_C),
+                                                ("temp3", "mem", lambda t, f=temp: f(t) - 6.0, 95.0)):
+                    hw = {"chip": chip, "sensor": sensor, "instance": inst}
+                    db.add(Series(dict(hw, __name__="node_hwmon_temp_celsius"), fn=fn, interval=interval))
+                    db.add(Series(dict(hw, __name__="node_hwmon_temp_crit_celsius"), fn=lambda t, c=crit: c,
+                                  interval=interval))
+                    db.add(Series(dict(hw, __name__="node_hwmon_sensor_label", label=label), fn=lambda t: 1.0,
+                                  interval=interval))
                 card = f"card{g}"
                 db.add(Series({"__name__": "node_drm_gpu_busy_percent", "card": card, "instance": inst},
                               fn=gfx, interval=interval))

@@ -75,6 +75,7 @@ export {
   nodeExporterScopedSeriesQuery,
   nodeExporterSeriesQuery,
   nodeExporterSummaryQuery,
+  nodeExporterTempQuery,
   nodePowerQuery,
   nodePowerSum,
   ownersQuery,

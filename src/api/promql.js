@@ -309,8 +309,23 @@ function nodeExporterNames() {
   return [N.chips.split('{')[0], N.power, N.powerInput, N.powerCap, N.busy, N.vramUsed, N.vramTotal, N.uname];
 }
 
+/**
+ * amdgpu junction temperature and its crit (throttle) limit through
+ * node-exporter: the hwmon temperatures whose sensor node_hwmon_sensor_label
+ * names "junction", on amdgpu chips only — two series per GPU, not every
+ * sensor of every chip of the node. `uname` (a node_uname_info selector):
+ * only the instances it names. The rows keep `sensor`, so `or`-ed next to
+ * the power rows of the same chip (which `or` would match, ignoring the
+ * name) they stay apart.
+ */
+export function nodeExporterTempQuery(uname) {
+  const N = SERIES.nodeExporter;
+  return '{__name__=~"' + N.temp + '|' + N.tempCrit + '"} and on(instance, chip, sensor) ' + N.sensorLabel +
+    '{label="junction"} and on(instance, chip) ' + N.chips + (uname ? ' and on(instance) (' + uname + ')' : '');
+}
+
 export function nodeExporterQuery() {
-  return '{__name__=~"' + nodeExporterNames().join('|') + '"}';
+  return '{__name__=~"' + nodeExporterNames().join('|') + '"} or ' + nodeExporterTempQuery();
 }
 
 /** nodeExporterQuery projected onto the labels its join reads. */
@@ -342,7 +357,8 @@ export function nodeExporterScopedQuery(names) {
   const labels = NODE_EXPORTER_JOIN_LABELS.join(', ');
   const gpuNames = nodeExporterNames().filter(function (n) { return n !== N.uname; });
   const uname = N.uname + '{' + nodenameMatcher(names) + '}';
-  return 'max by (' + labels + ') ({__name__=~"' + gpuNames.join('|') + '"} and on(instance) ' + uname + ')' +
+  return 'max by (' + labels + ') ({__name__=~"' + gpuNames.join('|') + '"} and on(instance) ' + uname +
+    ' or ' + nodeExporterTempQuery(uname) + ')' +
     ' or max by (' + labels + ') (' + uname + ')';
 }
 
@@ -429,7 +445,8 @@ export function rankedHwQuery(rank) {
   const labels = NODE_EXPORTER_JOIN_LABELS.join(', ');
   const gpuNames = nodeExporterNames().filter(function (n) { return n !== N.uname; });
   const uname = N.uname + ' and on(nodename) (' + s + ')';
-  return 'max by (' + labels + ') ({__name__=~"' + gpuNames.join('|') + '"} and on(instance) (' + uname + '))' +
+  return 'max by (' + labels + ') ({__name__=~"' + gpuNames.join('|') + '"} and on(instance) (' + uname + ')' +
+    ' or ' + nodeExporterTempQuery(uname) + ')' +
     ' or max by (' + labels + ') (' + uname + ')' +
     ' or ' + sizeRow('label_replace(' + s + ', "hostname", "$1", "nodename", "(.*)")', 'rank') +
     ' or ' + sizeRow('count(' + hwNodePowerSum(rank.filter) + ')', 'ranked');
@@ -483,7 +500,7 @@ export function mergedQuery(withStatic, view) {
   for (let i = 0; i < NODE_EXPORTER_JOIN_LABELS.length; i++) {
     if (labels.indexOf(NODE_EXPORTER_JOIN_LABELS[i]) < 0) labels.push(NODE_EXPORTER_JOIN_LABELS[i]);
   }
-  return 'max by (' + labels.join(', ') + ') ({__name__=~"' + names.join('|') + '"})';
+  return 'max by (' + labels.join(', ') + ') ({__name__=~"' + names.join('|') + '"} or ' + nodeExporterTempQuery() + ')';
 }
 
 /**

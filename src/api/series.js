@@ -51,6 +51,11 @@ export const SERIES = {
     busy: 'node_drm_gpu_busy_percent',
     vramUsed: 'node_drm_memory_vram_used_bytes',
     vramTotal: 'node_drm_memory_vram_size_bytes',
+    // hwmon temperatures (m°C read as °C) and their labels: amdgpu's junction
+    // sensor is the one labelled "junction" (temp2 on an MI355X; edge reads N/A).
+    temp: 'node_hwmon_temp_celsius',
+    tempCrit: 'node_hwmon_temp_crit_celsius',
+    sensorLabel: 'node_hwmon_sensor_label',
     uname: 'node_uname_info',
   },
 };

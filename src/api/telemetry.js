@@ -215,6 +215,9 @@ export function joinNodeExporterResults(r) {
   each(r[N.busy], cardKey, function (g, v) { g.gfxActivityPct = v; });
   each(r[N.vramUsed], cardKey, function (g, v) { g.vramUsedBytes = v; });
   each(r[N.vramTotal], cardKey, function (g, v) { g.vramTotalBytes = v; });
+  // The query keeps the amdgpu "junction" sensor only (promql.js nodeExporterTempQuery).
+  each(r[N.temp], chipKey, function (g, v) { g.tempC = v; });
+  each(r[N.tempCrit], chipKey, function (g, v) { if (v !== null && v > 0) g.tempSlowdownC = v; });
   gpus.sort(byNodeGpu);
   return { gpus: gpus, xgmi: {}, links: {} };
 }

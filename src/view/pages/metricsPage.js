@@ -96,8 +96,44 @@ function noTelemetrySection(name) {
   ], name);
 }
 
-/** Static availability box (reference MetricRequirements, MetricsPage.tsx:125-185) — on AMD everything is available. */
-export function metricAvailabilitySection() {
+/**
+ * What each telemetry source provides: [row, field of a joined GPU (null: the snapshot's xGMI map), exporter
+ * series, node-exporter series (null: the exporter alone has it)].
+ */
+const AVAILABILITY = [
+  ['Power (W)', 'powerWatts', 'gpu_power_usage', 'node_hwmon_power_average_watt / power_input_watt (amdgpu hwmon)'],
+  ['HBM used / total', 'vramUsedBytes', 'gpu_used_vram / gpu_total_vram', 'node_drm_memory_vram_used_bytes / size_bytes (--collector.drm)'],
+  ['GFX activity (%)', 'gfxActivityPct', 'gpu_gfx_activity', 'node_drm_gpu_busy_percent (--collector.drm)'],
+  ['HBM controller activity (%)', 'memActivityPct', 'gpu_umc_activity', null],
+  ['Junction temperature', 'tempC', 'gpu_junction_temperature', 'node_hwmon_temp_celsius, the sensor labelled "junction" (amdgpu hwmon)'],
+  ['xGMI link throughput', null, 'xgmi_neighbor_N_tx_throughput (7 links per GPU)', null],
+  ['Per-GPU pod owner', 'pod', 'pod / namespace labels (exporter pod association)', null],
+];
+
+/**
+ * The reference's MetricRequirements box (MetricsPage.tsx:125-185), said of
+ * the source that answered: each figure is "Reporting" when a GPU of the
+ * page carries it, else why not and what would provide it. Before any
+ * answer (or with no GPU series) the static list of what each source offers.
+ * @param {any} [m]  the page's telemetry snapshot
+ */
+export function metricAvailabilitySection(m) {
+  if (m && m.gpus && m.gpus.length && (m.source === 'amd-exporter' || m.source === 'node-exporter')) {
+    const ne = m.source === 'node-exporter';
+    const rows = [];
+    for (let i = 0; i < AVAILABILITY.length; i++) {
+      const a = AVAILABILITY[i];
+      let seen = a[1] === null && Object.keys(m.xgmi || {}).length > 0;
+      for (let k = 0; a[1] !== null && k < m.gpus.length && !seen; k++) seen = m.gpus[k][a[1]] !== null && m.gpus[k][a[1]] !== undefined;
+      const series = ne ? a[3] : a[2];
+      rows.push(row(a[0], seen
+        ? status('success', 'Reporting — ' + series)
+        : ne && series === null
+          ? status('warning', 'Not available from node-exporter — the AMD Device Metrics Exporter reports ' + a[2])
+          : status('warning', 'Not reported on this page — ' + series)));
+    }
+    return section('Metric Availability', [kv(rows)]);
+  }
   return section('Metric Availability', [
     kv([
       row('Power (W)', lines([
@@ -131,8 +167,8 @@ export function metricsView(ctx, mstate, opts) {
   // whole context, MetricsPage.tsx:203-205).
   const nodesPend = nodesPending(ctx);
   if (nodesPend) items.push(loader('Loading ' + BRAND + ' data...'));
-  items.push(metricAvailabilitySection());
   const m = mstate.metrics;
+  items.push(metricAvailabilitySection(m));
   if (mstate.fetching && !m) items.push(loader('Querying Prometheus for GPU metrics...'));
 
   if (mstate.fetchError) {

@@ -87,6 +87,32 @@ describe('node-exporter source: paged, totalled and ranked by Prometheus', () =>
     expect(none.mock.calls.map((c) => decodeURIComponent(c[0])).filter((p) => p.indexOf('/api/v1/query') >= 0)).toHaveLength(1);
   });
 
+  it('junction temperature and its throttle limit come from the amdgpu hwmon sensor labelled "junction" (not mem, not the CPU)', async () => {
+    const i = '10.0.0.1:9100';
+    const chip = '0000:05:00_0';
+    const cpu = 'platform_coretemp_0';
+    const t = (name, c, sensor, v) => vec({ __name__: name, instance: i, chip: c, sensor: sensor }, v);
+    const lab = (c, sensor, label) => vec({ __name__: 'node_hwmon_sensor_label', instance: i, chip: c, sensor: sensor, label: label }, 1);
+    const ne = {
+      node_uname_info: [vec({ __name__: 'node_uname_info', instance: i, nodename: 'mi355x-000' }, 1)],
+      chips: [vec({ __name__: 'node_hwmon_chip_names', instance: i, chip: chip, chip_name: 'amdgpu' }, 1),
+        vec({ __name__: 'node_hwmon_chip_names', instance: i, chip: cpu, chip_name: 'coretemp' }, 1)],
+      power: [vec({ __name__: 'node_hwmon_power_input_watt', instance: i, chip: chip, sensor: 'power1' }, 900)],
+      temps: [t('node_hwmon_temp_celsius', chip, 'temp2', 71), t('node_hwmon_temp_crit_celsius', chip, 'temp2', 100),
+        t('node_hwmon_temp_celsius', chip, 'temp3', 64), t('node_hwmon_temp_crit_celsius', chip, 'temp3', 95),
+        t('node_hwmon_temp_celsius', cpu, 'temp1', 47)],
+      labels: [lab(chip, 'temp2', 'junction'), lab(chip, 'temp3', 'mem'), lab(cpu, 'temp1', 'Package id 0')],
+    };
+    // Cluster-wide, paged and single-node reads all carry it.
+    const m = await source(prom({ data: {}, ne: ne })).fetchGpuMetrics();
+    expect(m.source).toBe('node-exporter');
+    expect(m.gpus.map((g) => [g.nodeName, g.tempC, g.tempSlowdownC, g.powerWatts])).toEqual([['mi355x-000', 71, 100, 900]]);
+    const p = await source(prom({ data: {}, ne: ne })).fetchGpuMetrics('gauges', { scope: ['mi355x-000'], summary: true });
+    expect(p.gpus.map((g) => g.tempC)).toEqual([71]);
+    const d = await source(prom({ data: {}, ne: ne })).fetchNodeMetrics('mi355x-000');
+    expect(d.gpus.map((g) => [g.tempC, g.tempSlowdownC])).toEqual([[71, 100]]);
+  });
+
   it('node-exporter source, small-cluster fetch before the node list: every GPU of a small cluster, the page of a larger one', async () => {
     function neData(nodes) {
       const ne = { node_uname_info: [] };

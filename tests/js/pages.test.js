@@ -481,6 +481,27 @@ describe('metricsView', () => {
     expect(sectionTitles(vm)).toEqual(['Metric Availability']);
     expect(vm.refresh.ariaLabel).toBe('Refresh metrics');
   });
+  it('availability says what the answering source reports: node-exporter has no HBM activity, xGMI or pod owner', () => {
+    const g = { nodeName: 'n0', gpu: '0', powerWatts: 900, powerCapWatts: 1400, vramUsedBytes: 1, vramTotalBytes: 2,
+      gfxActivityPct: 50, memActivityPct: null, tempC: 70, tempSlowdownC: 100, pod: null };
+    const cell = (m, name) => {
+      const sec = findSection(metricsView(ctx, { metrics: m, fetchError: null, fetching: false }, opts), 'Metric Availability');
+      return sec.blocks[0].rows.filter((r) => r.name === name)[0].value;
+    };
+    const ne = { source: 'node-exporter', gpus: [g], xgmi: {}, fetchedAt: new Date(NOW).toISOString(), prometheusPath: '/p' };
+    expect(cell(ne, 'Junction temperature').status).toBe('success');
+    expect(cell(ne, 'Junction temperature').text).toContain('"junction"');
+    expect(cell(ne, 'HBM controller activity (%)')).toEqual({ t: 'status', status: 'warning',
+      text: 'Not available from node-exporter — the AMD Device Metrics Exporter reports gpu_umc_activity' });
+    expect(cell(ne, 'xGMI link throughput').status).toBe('warning');
+    const ex = { source: 'amd-exporter', gpus: [Object.assign({}, g, { memActivityPct: 30 })], xgmi: { n0: { 0: [50e9] } },
+      fetchedAt: new Date(NOW).toISOString(), prometheusPath: '/p' };
+    expect(cell(ex, 'HBM controller activity (%)').text).toBe('Reporting — gpu_umc_activity');
+    expect(cell(ex, 'xGMI link throughput').status).toBe('success');
+    expect(cell(ex, 'Per-GPU pod owner').text).toBe('Not reported on this page — pod / namespace labels (exporter pod association)');
+    // Before an answer: what each source offers.
+    expect(text(cell(null, 'Power (W)'))).toContain('Available — gpu_power_usage');
+  });
   it('shows the context loader while the store loads', () => {
     const vm = metricsView(makeContext({ loading: true, lastUpdated: null }), { metrics: null, fetchError: null, fetching: false }, opts);
     expect(loaders(vm)).toEqual(['Loading AMD GPU data...']);

@@ -73,6 +73,33 @@ function term(q, rows) {
   const alts = splitOr(q);
   if (alts.length > 1) return [].concat.apply([], alts.map((t) => term(t, rows)));
   if (q[0] === '(' && closing(q, 0) === q.length - 1) return term(q.slice(1, -1), rows);
+  // `max by (…) (a or b)`: each alternative under the same projection (the fake does not project).
+  const mb = /^max by \([^)]*\) \(/.exec(q);
+  if (mb && closing(q, mb[0].length - 1) === q.length - 1) {
+    const parts = splitOr(q.slice(mb[0].length, -1));
+    if (parts.length > 1) return [].concat.apply([], parts.map((t) => term(mb[0] + t + ')', rows)));
+  }
+  // promql.js nodeExporterTempQuery: amdgpu temperatures of the sensor labelled "junction" (of the instances a
+  // node_uname_info selection names).
+  const bare = mb && closing(q, mb[0].length - 1) === q.length - 1 ? q.slice(mb[0].length, -1) : q;
+  const temp = /^\{__name__=~"(node_hwmon_temp_celsius\|node_hwmon_temp_crit_celsius)"\} and on\(instance, chip, sensor\) node_hwmon_sensor_label\{label="junction"\} and on\(instance, chip\) node_hwmon_chip_names\{chip_name="amdgpu"\}(?: and on\(instance\) \((.*)\))?$/.exec(bare);
+  if (temp) {
+    const key = (r) => r.metric.instance + '/' + r.metric.chip;
+    const junction = {};
+    const amd = {};
+    rows.forEach((r) => {
+      if (r.metric.__name__ === 'node_hwmon_sensor_label' && r.metric.label === 'junction') junction[key(r) + '/' + r.metric.sensor] = true;
+      if (r.metric.__name__ === 'node_hwmon_chip_names' && r.metric.chip_name === 'amdgpu') amd[key(r)] = true;
+    });
+    let insts = null;
+    if (temp[2] !== undefined) {
+      insts = {};
+      term('max by (instance) (' + temp[2] + ')', rows).forEach((r) => (insts[r.metric.instance] = true));
+    }
+    const re = new RegExp('^(?:' + temp[1] + ')$');
+    return rows.filter((r) => re.test(r.metric.__name__ || '') && junction[key(r) + '/' + r.metric.sensor] &&
+      amd[key(r)] && (!insts || insts[r.metric.instance]));
+  }
   // `X unless on() (<count>)`: X only while the count has no sample.
   const unless = /^(.*) unless on\(\) \((count\(count by .*\))\)$/.exec(q);
   if (unless) {

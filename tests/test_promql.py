@@ -565,3 +565,33 @@ def test_node_exporter_ranked_page_against_the_synthetic_cluster():
     assert [float(r["value"][1]) for r in rows if r["metric"].get("agg") == "ranked"] == [5.0]
     page_insts = {i for i, n in node_of.items() if n in rank}
     assert {r["metric"]["instance"] for r in rows if "agg" not in r["metric"]} == page_insts
+
+
+def test_node_exporter_junction_temperature_against_the_synthetic_cluster():
+    """nodeExporterTempQuery on the Python fake: the amdgpu sensor labelled "junction" and its crit limit, one pair
+    per GPU — not the "mem" sensor of the same chip, not the host CPU's coretemp chip; scoped through
+    node_uname_info when asked (nodeExporterScopedQuery carries it)."""
+    from headlamp_intel_gpu_plugin_amd.sim.apiserver import make_fake
+
+    fc = make_fake(3, source="node-exporter", latency_ms=0)
+    d, t = fc.db, 1_000_000.0
+    junction = {(s.labels["instance"], s.labels["chip"]) for s in d.by_name["node_hwmon_sensor_label"]
+                if s.labels["label"] == "junction"}
+    assert len(junction) == 24
+    rows = _vec(query(d, _js("m.nodeExporterTempQuery()"), t))
+    assert sorted(r["metric"]["__name__"] for r in rows) == ["node_hwmon_temp_celsius"] * 24 + \
+        ["node_hwmon_temp_crit_celsius"] * 24
+    assert {(r["metric"]["instance"], r["metric"]["chip"]) for r in rows} == junction
+    assert {r["metric"]["sensor"] for r in rows} == {"temp2"}
+    by_key = {(s.labels["instance"], s.labels["chip"], s.labels["sensor"]): s for s in d.by_name["node_hwmon_temp_celsius"]}
+    for r in rows:
+        if r["metric"]["__name__"] == "node_hwmon_temp_celsius":
+            k = (r["metric"]["instance"], r["metric"]["chip"], "temp2")
+            assert float(r["value"][1]) == pytest.approx(by_key[k].at(t)[1])
+    # The page of one node: its 8 GPUs' pairs alone, next to its power rows (`or` keeps them apart by `sensor`).
+    node = "mi355x-001"
+    inst = [s.labels["instance"] for s in d.by_name["node_uname_info"] if s.labels["nodename"] == node][0]
+    page = _vec(query(d, _js(f"m.nodeExporterScopedQuery(['{node}'])"), t))
+    temps = [r for r in page if r["metric"]["__name__"] == "node_hwmon_temp_celsius"]
+    assert len(temps) == 8 and {r["metric"]["instance"] for r in temps} == {inst}
+    assert len([r for r in page if r["metric"]["__name__"] == "node_hwmon_power_input_watt"]) == 8
