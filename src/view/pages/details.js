@@ -32,6 +32,7 @@ import {
 import { clusterPowerStats } from '../../api/metrics.js';
 import { kv, row, section, status } from '../ir.js';
 import { formatWindow, memo, podDetailCache, podName, podsPending, seriesMeans } from './common.js';
+import { gpuTelemetryTable } from './metricsPage.js';
 import { matrixBlock, ownersByNode, slotsBlock } from './nodes.js';
 import { assignedLines, podGpuAssignments } from './pods.js';
 
@@ -62,12 +63,15 @@ export function nodeDetailView(resource, ctx, opts) {
   const lk = metrics && metrics.links ? metrics.links[name] : undefined;
   const podsUnreadable = ctx.podsState === 'error';
   const series = opts && opts.series && opts.series.power && opts.series.power.length ? opts.series : null;
-  return memo('node-detail:' + name, [raw, podsOnNode, podsPend, podsUnreadable, own, xg, lk, series], function () {
-    return nodeDetailSection(raw, name, cap, alloc, podsOnNode, podsPend, own, xg, lk, podsUnreadable, series);
+  // This node's GPUs from the node-scoped snapshot (metrics.js fetchNodeMetrics): the live telemetry table.
+  const gs = metrics && metrics.gpus ? metrics.gpus.filter(function (g) { return g.nodeName === name; }) : [];
+  const deps = [raw, podsOnNode, podsPend, podsUnreadable, own, xg, lk, series].concat(gs);
+  return memo('node-detail:' + name, deps, function () {
+    return nodeDetailSection(raw, name, cap, alloc, podsOnNode, podsPend, own, xg, lk, podsUnreadable, series, gs);
   });
 }
 
-function nodeDetailSection(raw, name, cap, alloc, podsOnNode, loading, own, xg, lk, podsUnreadable, series) {
+function nodeDetailSection(raw, name, cap, alloc, podsOnNode, loading, own, xg, lk, podsUnreadable, series, gs) {
   const allocatable = parseInt(alloc[AMD_GPU_RESOURCE] || '0', 10) || 0;
   let inUse = 0;
   for (let i = 0; i < podsOnNode.length; i++) {
@@ -100,6 +104,7 @@ function nodeDetailSection(raw, name, cap, alloc, podsOnNode, loading, own, xg, 
   let blocks = [kv(rows)];
   if (count > 0) {
     blocks.push(slotsBlock(raw, podsOnNode, own));
+    if (gs.length) blocks.push(gpuTelemetryTable(gs));
     // xGMI links join the GPUs of a node: a single-GPU node has no matrix to show.
     if (phys > 1) blocks.push(matrixBlock(phys, xg, lk));
   }

@@ -320,27 +320,26 @@ function limitsRows(sum) {
   return parts.length ? [row('Assumed Limits', status('warning', parts.join('; ')))] : [];
 }
 
-function metricsNodeSection(name, gs) {
-  return section(
-    name + ' — ' + gs.length + ' × ' + MI355X.shortName,
-    [
-      table(
-        ['GPU', 'Power', 'HBM Used', 'GFX', 'HBM Activity', 'Temp', 'ECC', 'Pod'],
-        gs.map(function (g) {
-          return [
-            'GPU ' + g.gpu,
-            g.powerWatts !== null ? powerBar(g.powerWatts, g.powerCapWatts) : status('warning', 'No data'),
-            hbmBar(g.vramUsedBytes, g.vramTotalBytes),
-            pctText(g.gfxActivityPct),
-            pctText(g.memActivityPct),
-            tempCell(g),
-            eccCell(g),
-            g.pod ? (g.namespace ? g.namespace + '/' : '') + g.pod : '—',
-          ];
-        }),
-        gs.map(function (g) { return g.nodeName + '-' + g.gpu; })
-      ),
-    ],
-    name
+/** One node's GPUs as a table: power against cap, HBM, activity, junction temperature, ECC, owning pod. */
+export function gpuTelemetryTable(gs) {
+  return table(
+    ['GPU', 'Power', 'HBM Used', 'GFX', 'HBM Activity', 'Temp', 'ECC', 'Pod'],
+    gs.map(function (g) {
+      return [
+        'GPU ' + g.gpu,
+        g.powerWatts !== null ? powerBar(g.powerWatts, g.powerCapWatts) : status('warning', 'No data'),
+        hbmBar(g.vramUsedBytes, g.vramTotalBytes),
+        pctText(g.gfxActivityPct),
+        pctText(g.memActivityPct),
+        tempCell(g),
+        eccCell(g),
+        g.pod ? (g.namespace ? g.namespace + '/' : '') + g.pod : '—',
+      ];
+    }),
+    gs.map(function (g) { return g.nodeName + '-' + g.gpu; })
   );
+}
+
+function metricsNodeSection(name, gs) {
+  return section(name + ' — ' + gs.length + ' × ' + MI355X.shortName, [gpuTelemetryTable(gs)], name);
 }

@@ -309,6 +309,19 @@ describe('nodesView', () => {
     expect(firstBlock(d, 'matrix')).toBeFalsy();
     expect(renderPage(nodesView(ctx, opts))).not.toContain('xgmi-matrix');
   });
+  it('the Node detail section shows its GPUs\' live telemetry from the node-scoped snapshot, and no table without one', () => {
+    const E = SERIES.exporter;
+    const r = {};
+    r[E.power] = [0, 1].map((g) => ({ metric: { hostname: 'g0', gpu_id: String(g) }, value: [0, String(700 + g)] }));
+    r[E.temp] = [0, 1].map((g) => ({ metric: { hostname: 'g0', gpu_id: String(g) }, value: [0, '66'] }));
+    const metrics = joinExporterResults(r);
+    const ctx = makeContext({ nodes: [makeGpuNode('g0')], pods: [] });
+    const d = nodeDetailView(makeGpuNode('g0'), ctx, { metrics: metrics });
+    const t = firstBlock(d, 'table');
+    expect(t.columns.slice(0, 2)).toEqual(['GPU', 'Power']);
+    expect(t.rows.map((x) => [x[0], text(x[5])])).toEqual([['GPU 0', '66 °C'], ['GPU 1', '66 °C']]);
+    expect(firstBlock(nodeDetailView(makeGpuNode('g0'), ctx), 'table')).toBeFalsy();
+  });
   it('uses exporter pod labels for exact slots when metrics are given', () => {
     const E = SERIES.exporter;
     const r = {};
