@@ -102,6 +102,7 @@ export function assignedLines(gs) {
       if (g.powerWatts !== null && g.powerWatts !== undefined) parts.push(formatWatts(g.powerWatts));
       if (g.gfxActivityPct !== null && g.gfxActivityPct !== undefined) parts.push(Math.round(g.gfxActivityPct) + '% GFX');
       if (g.vramUsedBytes !== null && g.vramUsedBytes !== undefined) parts.push(formatBytes(g.vramUsedBytes) + ' HBM');
+      if (g.tempC !== null && g.tempC !== undefined) parts.push(Math.round(g.tempC) + ' °C');
       return { label: g.nodeName + ' GPU ' + g.gpu, text: parts.length ? parts.join(', ') : 'no telemetry' };
     })
   );

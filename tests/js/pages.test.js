@@ -30,6 +30,7 @@ import { renderPage, textContent } from '../../src/view/html.js';
 import { clusterPowerStats, joinExporterResults, SERIES } from '../../src/api/metrics.js';
 import { NOW, makeContext, makeDeviceConfig, makeGpuNode, makeGpuPod, makeNode, makePlainPod, makePluginPod } from './fixtures.js';
 import { MI355X } from '../../src/api/amdgpu.js';
+import { assignedLines } from '../../src/view/pages/pods.js';
 
 const opts = { now: NOW };
 
@@ -459,6 +460,7 @@ describe('pod → GPU assignment (exporter pod labels)', () => {
     const v = rowValue(s, 'Assigned GPUs');
     expect(v.t).toBe('lines');
     expect(v.lines[0]).toEqual({ label: 'g0 GPU 0', text: '1000.0 W, 90% GFX, 64 GiB HBM' });
+    expect(assignedLines([Object.assign({}, metrics.gpus[0], { tempC: 81.6 })]).lines[0].text).toBe('1000.0 W, 90% GFX, 64 GiB HBM, 82 °C');
     expect(rowValue(podDetailView(pods[1], { metrics }), 'Assigned GPUs')).toBeUndefined();
   });
   it('keeps assignment identity across snapshots with unchanged ownership', () => {
