@@ -123,9 +123,14 @@ export function metricAvailabilitySection(m) {
     const rows = [];
     for (let i = 0; i < AVAILABILITY.length; i++) {
       const a = AVAILABILITY[i];
+      const series = ne ? a[3] : a[2];
+      // This page's snapshot ('gauges') does not ask for link throughput: GPU Nodes draws it.
+      if (a[1] === null && !ne && m.view === 'gauges') {
+        rows.push(row(a[0], lines([{ label: '', text: 'On GPU Nodes (xGMI matrix) — ' + series }])));
+        continue;
+      }
       let seen = a[1] === null && Object.keys(m.xgmi || {}).length > 0;
       for (let k = 0; a[1] !== null && k < m.gpus.length && !seen; k++) seen = m.gpus[k][a[1]] !== null && m.gpus[k][a[1]] !== undefined;
-      const series = ne ? a[3] : a[2];
       rows.push(row(a[0], seen
         ? status('success', 'Reporting — ' + series)
         : ne && series === null

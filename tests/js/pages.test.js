@@ -514,6 +514,8 @@ describe('metricsView', () => {
     expect(cell(ex, 'HBM controller activity (%)').text).toBe('Reporting — gpu_umc_activity');
     expect(cell(ex, 'xGMI link throughput').status).toBe('success');
     expect(cell(ex, 'Per-GPU pod owner').text).toBe('Not reported on this page — pod / namespace labels (exporter pod association)');
+    // The Metrics page's own snapshot ('gauges') asks for no link throughput: it points to GPU Nodes instead.
+    expect(text(cell(Object.assign({}, ex, { view: 'gauges', xgmi: {} }), 'xGMI link throughput'))).toContain('On GPU Nodes');
     // Before an answer: what each source offers.
     expect(text(cell(null, 'Power (W)'))).toContain('Available — gpu_power_usage');
   });
