@@ -159,7 +159,16 @@ export function createMetricsSource(opts) {
    * @returns {Promise<GpuMetrics|null>}
    */
   function fetchGpuMetrics(view, opts) {
-    const p = telemetry(view, opts);
+    return deciding(telemetry(view, opts));
+  }
+
+  /**
+   * While the source is unknown, a telemetry answer in flight is what
+   * decides it: range windows asked meanwhile wait for it before asking
+   * node-exporter (seriesFetch.js rangeOf), so a cluster with the exporter
+   * never evaluates node-exporter's range joins.
+   */
+  function deciding(p) {
     if (state.source === null) {
       const d = p.then(function () {}, function () {});
       state.deciding = d;
@@ -200,7 +209,7 @@ export function createMetricsSource(opts) {
     failureReason: client.failureReason,
     fetchGpuMetrics: fetchGpuMetrics,
     /** Telemetry of ONE node's GPUs (native Node / Pod detail pages), `hostname`-scoped. */
-    fetchNodeMetrics: snaps.node,
+    fetchNodeMetrics: function (nodeName) { return deciding(snaps.node(nodeName)); },
     /** Pod → GPU attribution (ownerSnapshots.js). */
     fetchGpuOwners: owners.owners,
     /** Per-node power / HBM series over the last `rangeSec` (seriesFetch.js). */
@@ -212,10 +221,6 @@ export function createMetricsSource(opts) {
     /** A node's GPU power over the last `rangeSec` (shape and nulls as fetchPodSeries). */
     fetchNodeSeries: function (nodeName, rangeSec, stepSec) {
       return series.powerSeries('node|' + nodeName, function (source) {
-        // Source unknown (a detail page opened first): both in one query — each
-        // selects this node only, and `or` keeps the exporter's line at a step
-        // where both report (one row, the same label set).
-        if (source === null) return nodePowerQuery(nodeName) + ' or ' + nodeExporterNodePowerQuery(nodeName);
         return seriesQueryFor(source, nodePowerQuery(nodeName), nodeExporterNodePowerQuery(nodeName));
       }, rangeSec, stepSec);
     },
