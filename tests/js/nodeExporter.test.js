@@ -11,7 +11,7 @@ import { createMetricsSource, SERIES, summarizeMetrics } from '../../src/api/met
 import { clearViewMemo, metricsView } from '../../src/view/pages.js';
 import { sectionTitles } from '../../src/view/ir.js';
 import { makeContext, makeGpuNode, makeGpuPod } from './fixtures.js';
-import { prom, vec } from './promFake.js';
+import { exporterData, prom, vec } from './promFake.js';
 
 const names = (n) => Array.from({ length: n }, (_, i) => 'mi355x-' + String(i).padStart(3, '0'));
 const ctxOf = (n) => makeContext({ nodes: names(n).map((x) => makeGpuNode(x)), pods: [makeGpuPod('train-0', { node: 'mi355x-000' })] });
@@ -85,6 +85,16 @@ describe('node-exporter source: paged, totalled and ranked by Prometheus', () =>
     expect(m2).not.toBeNull();
     expect(m2.gpus).toEqual([]);
     expect(none.mock.calls.map((c) => decodeURIComponent(c[0])).filter((p) => p.indexOf('/api/v1/query') >= 0)).toHaveLength(1);
+  });
+
+  it('a cold Node detail on an exporter cluster never asks node-exporter for its history (the node query decides first)', async () => {
+    const fake = prom({ data: exporterData(['mi355x-000']) });
+    const s = source(fake);
+    const r = await Promise.all([s.fetchNodeMetrics('mi355x-000'), s.fetchNodeSeries('mi355x-000', 1800, 30)]);
+    expect(r[0].source).toBe('amd-exporter');
+    const ranges = fake.mock.calls.map((c) => decodeURIComponent(c[0])).filter((p) => p.indexOf('/query_range') >= 0);
+    expect(ranges).toHaveLength(1);
+    expect(ranges[0]).not.toContain('node_hwmon');
   });
 
   it('junction temperature and its throttle limit come from the amdgpu hwmon sensor labelled "junction" (not mem, not the CPU)', async () => {
