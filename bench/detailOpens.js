@@ -29,7 +29,16 @@ export async function detailOpens(url, counter, ctx, n) {
   const reqs = {};
   MODES.forEach(function (k) { modes[k] = []; bytes[k] = 0; reqs[k] = 0; });
   const slow = [];
-  const detailRequest = makeRequest(url, counter);
+  // Each mode's own request function and counter: a request still in flight
+  // when its open ends (the reference's 2 s-capped requests on a 1,000-node
+  // cluster) lands its bytes on the mode that sent it, not on whichever open
+  // it completes during.
+  const own = {};
+  const reqOf = {};
+  MODES.forEach(function (k) {
+    own[k] = { n: 0, bytes: 0 };
+    reqOf[k] = makeRequest(url, own[k]);
+  });
   for (let i = 0; i < n && pods.length; i++) {
     const pod = pods[i % pods.length];
     const node = ctx.gpuNodes.filter(function (x) { return x.metadata.name === pod.spec.nodeName; })[0];
@@ -59,7 +68,7 @@ export async function detailOpens(url, counter, ctx, n) {
       // history, one wave.
       ['nodeDetailCold', function (src) {
         const nm = pod.spec.nodeName;
-        return Promise.all([fetchNodePods(detailRequest, nm), src.fetchNodeMetrics(nm), src.fetchNodeSeries(nm, 1800, 30)])
+        return Promise.all([fetchNodePods(reqOf.nodeDetailCold, nm), src.fetchNodeMetrics(nm), src.fetchNodeSeries(nm, 1800, 30)])
           .then(function (r) {
             const cold = { loading: false, gpuPods: filterGpuRequestingPods(r[0]), podsState: 'ready', error: null };
             return node ? nodeDetailView(node, cold, { metrics: r[1], series: r[2] }) : null;
@@ -69,7 +78,7 @@ export async function detailOpens(url, counter, ctx, n) {
       // cluster-wide lists alongside CRD + 3 serial selector requests,
       // src/index.tsx:152-160), then its section from that context.
       ['nodeDetailColdReference', function () {
-        const ref = createReferenceSchedule(detailRequest);
+        const ref = createReferenceSchedule(reqOf.nodeDetailColdReference);
         return ref.coldOpenPage('nodes').then(function () { return node ? nodeDetailView(node, ref.snapshot()) : null; });
       }],
       // GPU Pods page: pod → GPU attribution of its first page of pods only.
@@ -87,10 +96,8 @@ export async function detailOpens(url, counter, ctx, n) {
       // connection pool: a browser keeps its keep-alive sockets to the
       // Headlamp origin across in-app navigations.
       const src = createMetricsSource({
-        request: detailRequest, clock: hiResClock, onTrace: function (sp) { spans.push(sp); },
+        request: reqOf[runs[r][0]], clock: hiResClock, onTrace: function (sp) { spans.push(sp); },
       });
-      const b0 = counter.bytes;
-      const n0 = counter.n;
       const t0 = process.hrtime();
       const start = hiResClock.now();
       const s = await runs[r][1](src);
@@ -103,10 +110,14 @@ export async function detailOpens(url, counter, ctx, n) {
           return { name: sp.name, startMs: sp.start - start, durMs: sp.end - sp.start, ok: sp.ok };
         }) });
       }
-      bytes[runs[r][0]] += counter.bytes - b0;
-      reqs[runs[r][0]] += counter.n - n0;
     }
   }
+  MODES.forEach(function (k) {
+    bytes[k] = own[k].bytes;
+    reqs[k] = own[k].n;
+    counter.n += own[k].n;
+    counter.bytes += own[k].bytes;
+  });
   out.detail = {};
   out.detailSlow = slow;
   for (const k in modes) {
