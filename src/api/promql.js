@@ -500,7 +500,9 @@ export function mergedQuery(withStatic, view) {
   for (let i = 0; i < NODE_EXPORTER_JOIN_LABELS.length; i++) {
     if (labels.indexOf(NODE_EXPORTER_JOIN_LABELS[i]) < 0) labels.push(NODE_EXPORTER_JOIN_LABELS[i]);
   }
-  return 'max by (' + labels.join(', ') + ') ({__name__=~"' + names.join('|') + '"} or ' + nodeExporterTempQuery() + ')';
+  // node-exporter's temperatures only where no exporter reports (its join would be read for nothing).
+  return 'max by (' + labels.join(', ') + ') ({__name__=~"' + names.join('|') + '"} or (' + nodeExporterTempQuery() +
+    ') unless on() (' + gpuNodeCount() + '))';
 }
 
 /**

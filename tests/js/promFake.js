@@ -76,8 +76,11 @@ function term(q, rows) {
   // `max by (…) (a or b)`: each alternative under the same projection (the fake does not project).
   const mb = /^max by \([^)]*\) \(/.exec(q);
   if (mb && closing(q, mb[0].length - 1) === q.length - 1) {
-    const parts = splitOr(q.slice(mb[0].length, -1));
+    const inner = q.slice(mb[0].length, -1);
+    const parts = splitOr(inner);
     if (parts.length > 1) return [].concat.apply([], parts.map((t) => term(mb[0] + t + ')', rows)));
+    // `max by (…) ((x) unless on() (count))`: the guard decides (no projection in the fake).
+    if (/^\(.*\) unless on\(\) \(count\(count by .*\)\)$/.test(inner) && closing(inner, 0) === inner.indexOf(') unless on() (')) return term(inner, rows);
   }
   // promql.js nodeExporterTempQuery: amdgpu temperatures of the sensor labelled "junction" (of the instances a
   // node_uname_info selection names).
