@@ -37,6 +37,12 @@ import {
 } from './common.js';
 import { podPage } from './paging.js';
 
+/** DeviceConfig operands of later AMD GPU Operator releases (`spec.<key>.enable`). */
+const EXTRA_OPERANDS = [
+  { key: 'testRunner', label: 'Test Runner' },
+  { key: 'configManager', label: 'Config Manager' },
+];
+
 function enabledCell(on, detail) {
   return on ? status('success', detail ? 'Enabled — ' + detail : 'Enabled') : status('warning', 'Disabled');
 }
@@ -130,6 +136,18 @@ function devicePluginsItems(ctx, now, pg, podsPend) {
       if (op.key === 'devicePlugin' || !operandEnabled(dc, op.key)) continue;
       const st = operandStatus(dc, op.key);
       rows.push(row(op.label + ' Pods', status(countsToStatus(st.desired, st.available), countsToText(st.desired, st.available))));
+    }
+    // Later operator releases' operands (GPU test runner, partition config
+    // manager): shown when the DeviceConfig names them, their DaemonSet
+    // counts when its status reports them.
+    for (let k = 0; k < EXTRA_OPERANDS.length; k++) {
+      const op = EXTRA_OPERANDS[k];
+      if (get(dc, ['spec', op.key], null) === null) continue;
+      rows.push(row(op.label, enabledCell(operandEnabled(dc, op.key))));
+      if (operandEnabled(dc, op.key) && get(dc, ['status', op.key], null) !== null) {
+        const st = operandStatus(dc, op.key);
+        rows.push(row(op.label + ' Pods', status(countsToStatus(st.desired, st.available), countsToText(st.desired, st.available))));
+      }
     }
     rows.push(row('Node Selector', formatSelector(get(dc, ['spec', 'selector'], null))));
     rows.push(row('Age', ageText(dc.metadata.creationTimestamp, now)));

@@ -166,6 +166,19 @@ describe('devicePluginsView', () => {
     const absent = findSection(devicePluginsView(makeContext({ crdAvailable: false }), opts), 'CRD Not Available');
     expect(rowValue(absent, 'Status').text).toContain('not installed');
   });
+  it('test runner / config manager operands show when the DeviceConfig names them, pods when its status counts them', () => {
+    const dc = makeDeviceConfig('gpu-operator');
+    dc.spec.testRunner = { enable: true };
+    dc.spec.configManager = { enable: false };
+    dc.status.testRunner = { nodesMatchingSelectorNumber: 2, desiredNumber: 2, availableNumber: 1 };
+    const s = findSection(devicePluginsView(makeContext({ deviceConfigs: [dc] }), opts), 'DeviceConfig: gpu-operator');
+    expect(rowValue(s, 'Test Runner')).toEqual({ t: 'status', status: 'success', text: 'Enabled' });
+    expect(rowValue(s, 'Test Runner Pods').text).toBe('1/2 ready');
+    expect(rowValue(s, 'Config Manager')).toEqual({ t: 'status', status: 'warning', text: 'Disabled' });
+    expect(rowValue(s, 'Config Manager Pods')).toBeUndefined();
+    const plain = findSection(devicePluginsView(makeContext({ deviceConfigs: [makeDeviceConfig('gpu-operator')] }), opts), 'DeviceConfig: gpu-operator');
+    expect(rowValue(plain, 'Test Runner')).toBeUndefined();
+  });
   it('shows the loader on first load', () => {
     expect(loaders(devicePluginsView(makeContext({ loading: true, lastUpdated: null }), opts))).toEqual(['Loading device plugin data...']);
   });
