@@ -28,7 +28,7 @@ import {
 export function exporterNames(withStatic, view) {
   const E = SERIES.exporter;
   const gauges = [E.power, E.vramUsed, E.gfx, E.umc, E.temp, E.eccCorrect, E.eccUncorrect];
-  const names = view === 'gauges' ? gauges : view === 'topology' ? [E.power, E.xgmiRe] : gauges.concat([E.xgmiRe]);
+  const names = view === 'gauges' ? gauges : view === 'topology' ? [E.power, E.temp, E.xgmiRe] : gauges.concat([E.xgmiRe]);
   if (withStatic !== false) names.push(E.powerCap, E.vramTotal, E.tempSlowdown, E.linkHops);
   return names;
 }

@@ -116,7 +116,8 @@ export const NODE_EXPORTER_JOIN_LABELS = ['__name__', 'instance', 'node', 'noden
  *   all       every live gauge and every xGMI link (terminal client, detail fallback);
  *   gauges    the Metrics page: per-GPU power / HBM / activity / temperature /
  *             RAS, no xGMI links (7 of the 14 live series of a GPU);
- *   topology  the GPU Nodes page: per-GPU pod owners (from the power gauge)
+ *   topology  the GPU Nodes page: per-GPU pod owners and node power (from the
+ *             power gauge), the junction temperature (each node's hottest GPU)
  *             and the per-link xGMI throughput of the neighbour matrix.
  */
 export const METRIC_VIEWS = ['all', 'gauges', 'topology'];

@@ -59,6 +59,7 @@ export {
   formatTaints,
   matrixBlock,
   nodePowerKeys,
+  nodeTempKeys,
   nodeReadyCell,
   nodesView,
   slotsBlock,

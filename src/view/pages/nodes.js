@@ -37,6 +37,7 @@ import {
   nodesPending,
   PODS_LOADING,
   podsPending,
+  tempCell,
 } from './common.js';
 import { nodeNameOf, nodePage, NODES_PER_PAGE, nodeSortOf, RANKED_NODE_SORTS, rankedPage } from './paging.js';
 
@@ -181,8 +182,9 @@ export function nodesView(ctx, opts) {
   // attribution anyway): "watts|cap" per node, whole watts, so the head and
   // its rows rebuild only when a shown value changes.
   const power = nodePowerKeys(metrics);
-  const head = memo('nodes-head', [pg, ctx.index, ctx.error, power.sig, podsPend], function () {
-    return nodesHeadItems(ctx, now, power.byNode, pg, sort, podsPend);
+  const temps = nodeTempKeys(metrics);
+  const head = memo('nodes-head', [pg, ctx.index, ctx.error, power.sig, temps.sig, podsPend], function () {
+    return nodesHeadItems(ctx, now, power.byNode, pg, sort, podsPend, temps.byNode);
   }, now);
   const owners = ownersByNode(metrics);
   const xgmi = metrics ? metrics.xgmi : undefined;
@@ -277,6 +279,33 @@ export function nodePowerKeys(metrics) {
   return { byNode: byNode, sig: names.map(function (n) { return n + '=' + byNode[n]; }).join(',') };
 }
 
+/**
+ * The hottest GPU of each node (junction °C, whole degrees) and its throttle
+ * limit: "temp|limit" per node (limit 0 when the source reports none), so
+ * the summary rebuilds only when a shown value changes.
+ */
+export function nodeTempKeys(metrics) {
+  const hot = {};
+  const gs = metrics && Array.isArray(metrics.gpus) ? metrics.gpus : [];
+  for (let i = 0; i < gs.length; i++) {
+    const g = gs[i];
+    if (typeof g.tempC !== 'number' || !isFinite(g.tempC)) continue;
+    const lim = typeof g.tempSlowdownC === 'number' && g.tempSlowdownC > 0 ? g.tempSlowdownC : 0;
+    const e = hot[g.nodeName];
+    if (!e || g.tempC > e[0]) hot[g.nodeName] = [g.tempC, lim];
+  }
+  const byNode = {};
+  const names = Object.keys(hot).sort();
+  for (let i = 0; i < names.length; i++) byNode[names[i]] = Math.round(hot[names[i]][0]) + '|' + Math.round(hot[names[i]][1]);
+  return { byNode: byNode, sig: names.map(function (n) { return n + '=' + byNode[n]; }).join(',') };
+}
+
+function nodeTempCell(key) {
+  if (!key) return '—';
+  const parts = key.split('|');
+  return tempCell({ tempC: Number(parts[0]), tempSlowdownC: Number(parts[1]) });
+}
+
 function nodePowerCell(key) {
   if (!key) return '—';
   const parts = key.split('|');
@@ -284,9 +313,11 @@ function nodePowerCell(key) {
   return powerBar(Number(parts[0]), cap > 0 ? cap : null);
 }
 
-function nodesHeadItems(ctx, now, powerByNode, pg, sort, podsPend) {
+function nodesHeadItems(ctx, now, powerByNode, pg, sort, podsPend, tempByNode) {
   const pw = powerByNode || {};
   const withPower = Object.keys(pw).length > 0;
+  const tp = tempByNode || {};
+  const withTemp = Object.keys(tp).length > 0;
   const items = [];
   if (ctx.error) items.push(errorSection(ctx.error));
 
@@ -312,13 +343,16 @@ function nodesHeadItems(ctx, now, powerByNode, pg, sort, podsPend) {
     items.push(
       section('GPU Node Summary', [
         table(
-          // "Power" (beyond the reference): the node's GPUs' live power against their summed cap.
-          ['Node', 'Ready', 'GPU Model', 'GPU Devices', 'Allocation', 'GPU Pods'].concat(withPower ? ['Power'] : [], ['Age']),
-          chunkedRows('node-summary-rows', pg.nodes, [withPower, podsPend], function (n) {
+          // "Power" and "Hottest GPU" (beyond the reference): the node's GPUs'
+          // live power against their summed cap; its hottest junction temperature.
+          ['Node', 'Ready', 'GPU Model', 'GPU Devices', 'Allocation', 'GPU Pods'].concat(withPower ? ['Power'] : [],
+            withTemp ? ['Hottest GPU'] : [], ['Age']),
+          chunkedRows('node-summary-rows', pg.nodes, [withPower, withTemp, podsPend], function (n) {
             const st = idx.nodeStats.get(n.metadata.name);
             const pk = pw[n.metadata.name];
+            const tk = tp[n.metadata.name];
             // Per-node stats keep their identity while unchanged (buildClusterIndex).
-            return nodeSummaryRows(n, [st, withPower, pk, podsPend], function () {
+            return nodeSummaryRows(n, [st, withPower, pk, withTemp, tk, podsPend], function () {
               const count = getNodeGpuCount(n);
               return [
                 n.metadata.name,
@@ -327,9 +361,10 @@ function nodesHeadItems(ctx, now, powerByNode, pg, sort, podsPend) {
                 count > 0 ? String(count) : '—',
                 podsPend ? PODS_LOADING : allocationBar(st ? st.inUse : 0, (st && st.allocatable) || count),
                 podsPend ? PODS_LOADING : String(st ? st.pods : 0),
-              ].concat(withPower ? [nodePowerCell(pk)] : [], [ageText(n.metadata.creationTimestamp, now)]);
+              ].concat(withPower ? [nodePowerCell(pk)] : [], withTemp ? [nodeTempCell(tk)] : [],
+                [ageText(n.metadata.creationTimestamp, now)]);
             }, now);
-          }, now, function (n) { return [idx.nodeStats.get(n.metadata.name), withPower, pw[n.metadata.name]]; }),
+          }, now, function (n) { return [idx.nodeStats.get(n.metadata.name), withPower, pw[n.metadata.name], tp[n.metadata.name]]; }),
           pg.nodes.map(function (n) { return n.metadata.uid || n.metadata.name; })
         ),
       ])

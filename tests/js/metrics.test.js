@@ -389,11 +389,12 @@ describe('page views (each page asks only for what it draws)', () => {
     expect(mergedQuery(true, 'gauges')).not.toContain(E.xgmiRe);
   });
 
-  it("'topology' (GPU Nodes page) asks for the owner-bearing power gauge and the xGMI links only", () => {
+  it("'topology' (GPU Nodes page) asks for the owner-bearing power gauge, the junction temperature and the xGMI links only", () => {
     const q = exporterQuery(false, true, 'topology');
     expect(q).toContain(E.power);
+    expect(q).toContain(E.temp);
     expect(q).toContain(E.xgmiRe);
-    [E.vramUsed, E.gfx, E.umc, E.temp, E.eccCorrect].forEach((n) => expect(q).not.toContain(n));
+    [E.vramUsed, E.gfx, E.umc, E.eccCorrect].forEach((n) => expect(q).not.toContain(n));
     // static series (link hops, caps) still ride along when the cached copy is stale
     expect(exporterQuery(true, false, 'topology')).toContain(E.linkHops);
   });

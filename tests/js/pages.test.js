@@ -24,6 +24,7 @@ import {
   formatTaints,
   nodeReadyCell,
   nodePowerKeys,
+  nodeTempKeys,
 } from '../../src/view/pages.js';
 import { countRows, findSection, firstBlock, firstTable, loaders, rowNames, rowValue, sectionTitles, text } from '../../src/view/ir.js';
 import { renderPage, textContent } from '../../src/view/html.js';
@@ -255,6 +256,22 @@ describe('nodesView: live node power', () => {
     expect(nodePowerKeys(metrics).byNode).toEqual({ g0: '1400|2800' });
     const plain = firstTable(findSection(nodesView(ctx, { now: NOW }), 'GPU Node Summary'));
     expect(plain.columns).not.toContain('Power');
+  });
+});
+
+describe('nodesView: hottest GPU', () => {
+  it('adds a Hottest GPU column (max junction °C per node, coloured against its throttle limit) when temperatures are there', () => {
+    const ctx = makeContext({ nodes: [makeGpuNode('g0'), makeGpuNode('g1')] });
+    const g = (node, i, t) => ({ nodeName: node, gpu: String(i), powerWatts: 700, powerCapWatts: 1400, tempC: t, tempSlowdownC: 100 });
+    const metrics = { source: 'amd-exporter', gpus: [g('g0', 0, 61.2), g('g0', 1, 93.6), g('g1', 0, null)], xgmi: {}, links: {} };
+    const t = firstTable(findSection(nodesView(ctx, { now: NOW, metrics }), 'GPU Node Summary'));
+    const col = t.columns.indexOf('Hottest GPU');
+    expect(col).toBe(t.columns.length - 2); // after Power, before Age
+    expect(t.rows[0][col]).toEqual({ t: 'status', status: 'warning', text: '94 °C' });
+    expect(t.rows[1][col]).toBe('—');
+    expect(nodeTempKeys(metrics).byNode).toEqual({ g0: '94|100' });
+    const plain = firstTable(findSection(nodesView(ctx, { now: NOW }), 'GPU Node Summary'));
+    expect(plain.columns).not.toContain('Hottest GPU');
   });
 });
 
