@@ -339,8 +339,14 @@ def main(argv=None) -> int:
                                     "reference": round(summarize(result["ref_switch"]["latencies"])["p50"], 3)},
             # Native Pod / Node detail page opened on a warm cluster: the node's
             # telemetry by a hostname-scoped query vs the cluster-wide snapshot.
-            "detail_open": {k: {"p50_ms": round(summarize(v["latencies"])["p50"], 3) if v["latencies"] else None,
-                                "bytes": round(v["bytesPerOpen"]), "requests": v["requestsPerOpen"]}
+            # The *Wired modes mount the shipped Node detail wiring and also count its list hooks.
+            "detail_open": {k: dict({"p50_ms": round(summarize(v["latencies"])["p50"], 3) if v["latencies"] else None,
+                                     "bytes": round(v["bytesPerOpen"]), "requests": v["requestsPerOpen"]},
+                                    **{o: v[i] for i, o in (("listsPerOpen", "lists"),
+                                                            ("clusterWideListsPerOpen", "cluster_wide_lists"),
+                                                            ("deviceConfigRequestsPerOpen", "deviceconfig_requests"),
+                                                            ("listPaths", "list_paths"), ("rendered", "rendered"))
+                                       if i in v})
                             for k, v in result["detail"].items()},
             "rendered": {"gpu_nodes": rows["gpuNodes"], "gpu_pods": rows["gpuPods"],
                          "gpus_monitored": rows["gpusMonitored"], "gpu_cells": rows["gpuCells"],

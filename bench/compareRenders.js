@@ -10,7 +10,7 @@
  * Driven by tools/render_compare.py (driver command 'refRender').
  */
 import { createMetricsSource } from '../src/api/metrics.js';
-import { clearViewMemo } from '../src/view/pages.js';
+import { clearViewMemo } from '../src/view/pages/common.js';
 import { loadReferencePages, referenceContext, toGpuMetrics, toIntelNode, toIntelPod } from './referenceRender.js';
 import { amdSchedule } from './schedules.js';
 import { makeRequest, ms, stats } from './common.js';

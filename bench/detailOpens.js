@@ -8,12 +8,17 @@
  */
 import { fetchNodePods } from '../src/api/clusterStore.js';
 import { createMetricsSource } from '../src/api/metrics.js';
-import { filterGpuRequestingPods } from '../src/api/amdgpu.js';
-import { nodeDetailView, ownersScope, podDetailView, podsView } from '../src/view/pages.js';
+import { filterGpuRequestingPods } from '../src/api/amdPods.js';
+import { nodeDetailView, podDetailView } from '../src/view/pages/details.js';
+import { ownersScope, podsView } from '../src/view/pages/pods.js';
 import { renderPage, renderSection } from '../src/view/html.js';
 import { createReferenceSchedule } from './referenceSchedule.js';
 import { hiResClock, makeRequest, ms } from './common.js';
 import { PAGER } from './pageRender.js';
+import { wiredNodeDetailOpen } from './wiredDetail.js';
+
+/** Opens per wired mode: the 'after a page' mode downloads that page's lists first (untimed). */
+const WIRED_OPENS = 3;
 
 /**
  * `n` opens of each mode over the pods of `ctx` (a warm store's snapshot).
@@ -122,6 +127,30 @@ export async function detailOpens(url, counter, ctx, n) {
   out.detailSlow = slow;
   for (const k in modes) {
     out.detail[k] = { latencies: modes[k], bytesPerOpen: bytes[k] / Math.max(1, modes[k].length), requestsPerOpen: reqs[k] / Math.max(1, modes[k].length) };
+  }
+  // The Node detail section through the plugin's own wiring (bench/wiredDetail.js):
+  // after GPU Nodes was visited and unmounted, and on a cold start. Its list
+  // hooks are counted next to its requests and bytes.
+  const wired = [['nodeDetailWired', 'nodes'], ['nodeDetailWiredCold', null]];
+  for (let w = 0; w < wired.length; w++) {
+    const runs = [];
+    for (let i = 0; i < Math.min(n, WIRED_OPENS) && pods.length; i++) {
+      const pod = pods[i % pods.length];
+      const node = ctx.gpuNodes.filter(function (x) { return x.metadata.name === pod.spec.nodeName; })[0];
+      if (node) runs.push(await wiredNodeDetailOpen(url, node, wired[w][1], wired[w][0] + '-' + i));
+    }
+    const k = runs.length || 1;
+    const sum = function (f) { return runs.reduce(function (a, r) { return a + f(r); }, 0) / k; };
+    out.detail[wired[w][0]] = {
+      latencies: runs.map(function (r) { return r.ms; }),
+      bytesPerOpen: sum(function (r) { return r.bytes; }),
+      requestsPerOpen: sum(function (r) { return r.requests; }),
+      listsPerOpen: sum(function (r) { return r.lists.length; }),
+      clusterWideListsPerOpen: sum(function (r) { return r.clusterWideLists; }),
+      deviceConfigRequestsPerOpen: sum(function (r) { return r.deviceConfigRequests; }),
+      listPaths: runs.length ? runs[runs.length - 1].lists : [],
+      rendered: runs.every(function (r) { return r.section && !r.loading; }),
+    };
   }
   return out;
 }

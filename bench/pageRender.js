@@ -6,10 +6,13 @@
  */
 import fs from 'fs';
 import path from 'path';
-import {
-  overviewView, devicePluginsView, nodesView, podsView, metricsView,
-  nodeDetailView, podDetailView, nodeColumns, nodePage, podPage,
-} from '../src/view/pages.js';
+import { nodeColumns, nodeDetailView, podDetailView } from '../src/view/pages/details.js';
+import { devicePluginsView } from '../src/view/pages/devicePlugins.js';
+import { metricsView } from '../src/view/pages/metricsPage.js';
+import { nodesView } from '../src/view/pages/nodes.js';
+import { overviewView } from '../src/view/pages/overview.js';
+import { nodePage, podPage } from '../src/view/pages/paging.js';
+import { podsView } from '../src/view/pages/pods.js';
 import { countRows, sections } from '../src/view/ir.js';
 import { renderPage, renderSection } from '../src/view/html.js';
 // The harness React (the Node-12 stand-in the spec suite renders the plugin

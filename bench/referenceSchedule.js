@@ -21,18 +21,12 @@
  * reference source.
  */
 
-import {
-  DEVICE_CONFIG_LIST_PATH,
-  AMD_GPU_OPERATOR_NAMESPACE,
-  isKubeList,
-  isDeviceConfig,
-  filterAmdGpuPluginPods,
-  filterAmdGpuNodes,
-  filterGpuRequestingPods,
-  buildClusterIndex,
-} from '../src/api/amdgpu.js';
+import { filterAmdGpuNodes, isDeviceConfig } from '../src/api/amdNodes.js';
+import { filterAmdGpuPluginPods, filterGpuRequestingPods } from '../src/api/amdPods.js';
+import { buildClusterIndex } from '../src/api/clusterIndex.js';
+import { AMD_GPU_OPERATOR_NAMESPACE, DEVICE_CONFIG_LIST_PATH, isKubeList } from '../src/api/k8sCore.js';
 import { withTimeout } from '../src/api/clusterStore.js';
-import { PROMETHEUS_SERVICES, servicePath } from '../src/api/metrics.js';
+import { PROMETHEUS_SERVICES, servicePath } from '../src/api/series.js';
 
 export const REF_TIMEOUT_MS = 2000;
 

@@ -9,7 +9,8 @@
  */
 import { createClusterStore } from '../src/api/clusterStore.js';
 import { createMetricsSource } from '../src/api/metrics.js';
-import { ownersScope, telemetryScope } from '../src/view/pages.js';
+import { telemetryScope } from '../src/view/pages/nodes.js';
+import { ownersScope } from '../src/view/pages/pods.js';
 import { renderPage } from '../src/view/html.js';
 import { PAGE_NEEDS } from '../src/plugin.js';
 import { createReferenceSchedule } from './referenceSchedule.js';

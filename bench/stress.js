@@ -19,7 +19,7 @@
  *              view-models (Overview, Device Plugins, GPU Nodes, GPU Pods,
  *              Metrics) and the Node-detail section of the node the event
  *              touched — the shipped code (src/api/clusterStore.js,
- *              src/view/pages.js);
+ *              src/view/pages/*.js);
  *   reference  a replay of what the reference recomputes on the same event:
  *              jsonData extraction + GPU-pod filter over every pod
  *              (IntelGpuDataContext.tsx:200-208) and the Overview page's
@@ -37,25 +37,17 @@
  * the churn, and bytes per pod / node list.
  */
 
-import {
-  filterGpuRequestingPods,
-  getNodeGpuCount,
-  isNodeReady,
-  getPodGpuRequests,
-  unwrapAll,
-  filterAmdGpuNodes,
-  getNodeGpuModel,
-} from '../src/api/amdgpu.js';
+import { filterAmdGpuNodes, getNodeGpuCount, getNodeGpuModel, isNodeReady } from '../src/api/amdNodes.js';
+import { filterGpuRequestingPods, getPodGpuRequests } from '../src/api/amdPods.js';
+import { unwrapAll } from '../src/api/k8sCore.js';
 import { createClusterStore } from '../src/api/clusterStore.js';
-import {
-  overviewView,
-  devicePluginsView,
-  nodesView,
-  podsView,
-  metricsView,
-  nodeDetailView,
-  clearViewMemo,
-} from '../src/view/pages.js';
+import { clearViewMemo } from '../src/view/pages/common.js';
+import { nodeDetailView } from '../src/view/pages/details.js';
+import { devicePluginsView } from '../src/view/pages/devicePlugins.js';
+import { metricsView } from '../src/view/pages/metricsPage.js';
+import { nodesView } from '../src/view/pages/nodes.js';
+import { overviewView } from '../src/view/pages/overview.js';
+import { podsView } from '../src/view/pages/pods.js';
 import fs from 'fs';
 
 function parseArgs(argv) {

@@ -3,7 +3,7 @@
  * amd-gpu-dash — the plugin's dashboard in a terminal.
  *
  * Runs the plugin's own data layer (src/api: cluster store, metrics client)
- * and view-models (src/view/pages.js) against a cluster reached through
+ * and view-models (src/view/pages/*.js) against a cluster reached through
  * `kubectl proxy` (or any URL that speaks the Kubernetes API with the
  * caller's credentials), and prints the pages with the text renderer. Same
  * requests, same degradation rules, same numbers as the Headlamp pages.
@@ -21,10 +21,20 @@ import https from 'https';
 import { createClusterStore } from '../src/api/clusterStore.js';
 import { createMetricsSource } from '../src/api/metrics.js';
 import { parsePrometheus, prometheusCandidates } from '../src/api/settings.js';
+import { nodeDetailView, podDetailView } from '../src/view/pages/details.js';
+import { devicePluginsView } from '../src/view/pages/devicePlugins.js';
+import { metricsView } from '../src/view/pages/metricsPage.js';
+import { nodesView } from '../src/view/pages/nodes.js';
+import { overviewView } from '../src/view/pages/overview.js';
 import {
-  NODES_PER_PAGE, NODE_SORTS, PODS_PER_PAGE, POD_SORTS, RANKED_NODE_SORTS, RANKED_POD_SORTS, devicePluginsView, metricsView,
-  nodeDetailView, nodesView, overviewView, podDetailView, podsView,
-} from '../src/view/pages.js';
+  NODE_SORTS,
+  NODES_PER_PAGE,
+  POD_SORTS,
+  PODS_PER_PAGE,
+  RANKED_NODE_SORTS,
+  RANKED_POD_SORTS,
+} from '../src/view/pages/paging.js';
+import { podsView } from '../src/view/pages/pods.js';
 import { renderText, textSection } from '../src/view/text.js';
 import { PAGE_NEEDS } from '../src/plugin.js';
 

@@ -15,7 +15,7 @@ clusters of N nodes × 8 MI355X with:
 
 BASELINE.json configs map to ``PRESETS``.
 
-Label, CRD and pod-naming conventions must match ``src/api/amdgpu.js``; the
+Label, CRD and pod-naming conventions must match ``src/api/k8sCore.js`` / ``amdNodes.js``; the
 JS constants are the single source of truth and tests cross-check them.
 """
 from __future__ import annotations
@@ -27,7 +27,7 @@ import hashlib
 from typing import Dict, List, Optional
 
 GPUS_PER_NODE = 8
-#: devices per MI355X board in each compute-partition mode (src/api/amdgpu.js COMPUTE_PARTITIONS)
+#: devices per MI355X board in each compute-partition mode (src/api/amdNodes.js COMPUTE_PARTITIONS)
 COMPUTE_PARTITIONS = {"SPX": 1, "DPX": 2, "QPX": 4, "CPX": 8}
 HBM_BYTES = 294896 * 2**20  # 288 GiB less 16 MiB, as the device reports it (309,220,868,096 B)
 OPERATOR_NS = "kube-amd-gpu"

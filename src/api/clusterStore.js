@@ -33,19 +33,10 @@
  * `useSyncExternalStore`; snapshots are immutable objects.
  */
 
-import {
-  DEVICE_CONFIG_LIST_PATH,
-  PLUGIN_POD_QUERIES,
-  buildClusterIndex,
-  dedupePods,
-  filterAmdGpuPluginPods,
-  isAmdGpuNode,
-  isAmdGpuPluginPod,
-  isDeviceConfig,
-  isGpuRequestingPod,
-  isKubeList,
-  patchClusterIndex,
-} from './amdgpu.js';
+import { isAmdGpuNode, isDeviceConfig } from './amdNodes.js';
+import { dedupePods, filterAmdGpuPluginPods, isAmdGpuPluginPod, isGpuRequestingPod } from './amdPods.js';
+import { buildClusterIndex, patchClusterIndex } from './clusterIndex.js';
+import { DEVICE_CONFIG_LIST_PATH, isKubeList, PLUGIN_POD_QUERIES } from './k8sCore.js';
 import { createListTracker } from './listCache.js';
 import { DEFAULT_REQUEST_TIMEOUT_MS, defaultClock, isAbsent, sameObjects, withTimeout } from './requests.js';
 
@@ -138,6 +129,13 @@ export function createClusterStore(opts) {
   let podFeeds = 0;
   let feedsAttached = false;
   let opFeeds = 0; // operator pod feeds mounted right now
+  // Objects a scoped list + watch delivered OUTSIDE the selection it asked
+  // for (providerCore.js NodePodsWatch / OperatorPodFeed): a host whose
+  // useList() drops the list options. Once seen, those views read their
+  // scoped requests instead (ADR 012).
+  const ignored = { nodePods: 0, operatorPods: 0 };
+  const noted = typeof WeakSet === 'function' ? new WeakSet() : null; // deliveries already counted
+  let opLoad = null; // loadOperatorPods in flight
   let version = 0;
   const listeners = [];
 
@@ -512,6 +510,8 @@ export function createClusterStore(opts) {
    * benchmark): the plugin-pod requests, fed through setOperatorPods.
    */
   function loadOperatorPods() {
+    // Callers asking while a load is in flight share it (an effect run twice).
+    if (opLoad) return opLoad;
     if (s.opPodsState === 'unknown') s.opPodsState = 'pending';
     const lists = podQueries.map(function (path, i) {
       return traced('operator-pods-' + i, path).then(
@@ -519,7 +519,8 @@ export function createClusterStore(opts) {
         function (e) { return { error: e instanceof Error ? e.message : String(e) }; }
       );
     });
-    return Promise.all(lists).then(function (rs) {
+    const run = Promise.all(lists).then(function (rs) {
+      opLoad = null;
       let found = [];
       let failed = 0;
       for (let i = 0; i < rs.length; i++) {
@@ -529,6 +530,26 @@ export function createClusterStore(opts) {
       if (failed === rs.length) setOperatorPods(null, rs[0].error);
       else setOperatorPods(dedupePods(found), null);
     });
+    opLoad = run;
+    return run;
+  }
+
+  /**
+   * A scoped list + watch of `kind` delivered `n` objects outside its
+   * selection: the host ignored the list options. Counted (counters()
+   * .selectorIgnored); the first report notifies subscribers, so the views
+   * switch to their scoped requests.
+   */
+  function noteSelectorIgnored(kind, n, delivery) {
+    if (!(kind in ignored) || !(n > 0)) return;
+    // One delivery is counted once, however often its effect runs (StrictMode).
+    if (delivery && noted) {
+      if (noted.has(delivery)) return;
+      noted.add(delivery);
+    }
+    const first = ignored[kind] === 0;
+    ignored[kind] += n;
+    if (first) emit();
   }
 
   function subscribe(fn) {
@@ -582,8 +603,17 @@ export function createClusterStore(opts) {
      * and the views subscribed right now.
      */
     counters: function () {
-      return Object.assign({}, counters, { pods: podTracker.stats(), nodes: nodeTracker.stats(), subscribers: listeners.length });
+      return Object.assign({}, counters, {
+        pods: podTracker.stats(), nodes: nodeTracker.stats(), subscribers: listeners.length,
+        podFeeds: podFeeds, operatorFeeds: opFeeds,
+        selectorIgnored: ignored.nodePods || ignored.operatorPods ? Object.assign({}, ignored) : null,
+      });
     },
+    /** A pod list feed is mounted right now: the store's pod list is being kept current. */
+    podFeedMounted: function () { return podFeeds > 0; },
+    noteSelectorIgnored: noteSelectorIgnored,
+    /** True once a scoped list of `kind` ('nodePods' | 'operatorPods') came back unscoped. */
+    selectorsIgnored: function (kind) { return ignored[kind] > 0; },
   };
 }
 
@@ -612,8 +642,13 @@ export function resetSharedStores() {
   for (const k in shared) delete shared[k];
 }
 
-/** True when the store has both cluster lists (a plugin page fed it): detail views can read it. */
-export function storeIsWarm(store) {
-  const s = store && store.getSnapshot();
-  return !!s && s.nodesState === 'ready' && s.podsState === 'ready';
+/**
+ * True while a mounted pod feed keeps the store's pod list current and that
+ * list is in: a Node detail section can then read the store. A list fed once
+ * and no longer watched (every plugin page unmounted, as when the user went
+ * to Headlamp's own Node page) is a seed, not a live source.
+ */
+export function storeIsLive(store) {
+  if (!store || !store.podFeedMounted()) return false;
+  return store.getSnapshot().podsState === 'ready';
 }

@@ -34,7 +34,7 @@
  * object re-created) is handled the same way, by lookups instead of compares.
  */
 
-import { unwrapKubeObject } from './amdgpu.js';
+import { unwrapKubeObject } from './k8sCore.js';
 
 function keyOf(raw) {
   const m = raw && raw.metadata;

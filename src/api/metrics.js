@@ -28,8 +28,8 @@
  * transient failures. Metric and label names are pinned by captures from a
  * real MI355X (tests/fixtures/mi355x).
  *
- * Every name the parts export is re-exported here, so callers import the
- * telemetry API from one module.
+ * Callers import names, PromQL builders and joins from those modules
+ * directly; this module only assembles the client.
  */
 
 import { METRIC_VIEWS } from './series.js';
@@ -40,85 +40,6 @@ import { createScopedSnapshots } from './scopedSnapshots.js';
 import { createOwnerSnapshots } from './ownerSnapshots.js';
 import { createSeriesFetch, seriesQueryFor } from './seriesFetch.js';
 
-export {
-  DISCOVERY_TTL_MS,
-  EXPORTER_JOIN_LABELS,
-  EXPORTER_LEAN_LABELS,
-  METRIC_VIEWS,
-  NODE_EXPORTER_JOIN_LABELS,
-  PROMETHEUS_SERVICES,
-  SERIES,
-  SMALL_CLUSTER_NODES,
-  SMALL_CLUSTER_PODS,
-  SMALL_HWMON_GPUS,
-  STALE_FAILURES,
-  STATIC_GPU_FIELDS,
-  TOTAL_SERIES,
-  servicePath,
-} from './series.js';
-export {
-  exporterNames,
-  exporterNodeQuery,
-  exporterQuery,
-  gpuNodeCount,
-  gpuPodCount,
-  hostnameMatcher,
-  hwmonGpuCount,
-  hwNodePowerSum,
-  hwPowerRankQuery,
-  isExporterName,
-  mergedQuery,
-  nodeExporterProjected,
-  nodeExporterNodePowerQuery,
-  nodeExporterQuery,
-  nodeExporterScopedQuery,
-  nodeExporterScopedSeriesQuery,
-  nodeExporterSeriesQuery,
-  nodeExporterSummaryQuery,
-  nodeExporterTempQuery,
-  nodePowerQuery,
-  nodePowerSum,
-  ownersQuery,
-  podFilterMatchers,
-  podPowerQuery,
-  podPowerRankQuery,
-  podPowerSum,
-  powerRankQuery,
-  promString,
-  rankedClusterQuery,
-  rankedHwQuery,
-  rankedOwnersQuery,
-  regexLiteral,
-  scopedSeriesQuery,
-  seriesQuery,
-  sizeGuard,
-  sizeRow,
-  smallClusterQuery,
-  sourceProbe,
-  summaryQuery,
-} from './promql.js';
-export {
-  applyStatics,
-  clusterPowerStats,
-  gpuKey,
-  hwTotalsFromRows,
-  isRow,
-  joinExporterResults,
-  joinNodeExporterResults,
-  keyedByHostname,
-  nodeSlice,
-  num,
-  sameValue,
-  shareGpus,
-  shareMap,
-  sizeFromRows,
-  splitByName,
-  staticsOf,
-  stringLabels,
-  summarizeMetrics,
-  totalsFromRows,
-  zeroTotals,
-} from './telemetry.js';
 
 /**
  * @param {{ request: (path: string) => Promise<any>, timeoutMs?: number,

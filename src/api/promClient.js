@@ -16,7 +16,7 @@
 
 import { DEFAULT_REQUEST_TIMEOUT_MS, withTimeout } from './clusterStore.js';
 import { DISCOVERY_TTL_MS, PROMETHEUS_SERVICES, servicePath } from './series.js';
-import { isObject } from './amdgpu.js';
+import { isObject } from './k8sCore.js';
 import { splitByName, stringLabels } from './telemetry.js';
 
 /** Marker for "the request did not reach a Prometheus". */

@@ -6,12 +6,23 @@ export const STALE_MS: number;
 export const PROMETHEUS_UNREACHABLE: string;
 export const PROMETHEUS_FORBIDDEN: string;
 export const OUTSIDE_PROVIDER: string;
+/** Needs of a provider that reads the store and mounts nothing. */
+export const READ_ONLY_NEEDS: { nodes: false; pods: false; crd: false; operatorPods: false };
+/** Re-read period (s) of a scoped request standing in for an unscoped watch, when auto-refresh is off. */
+export const SCOPED_POLL_SEC: number;
+
+/** List options of a scoped list + watch (the apiserver applies them; ADR 012 checks the host passed them on). */
+export interface ListOptions {
+  namespace?: string;
+  labelSelector?: string;
+  fieldSelector?: string;
+}
 
 export interface HeadlampLibLike {
   K8s: {
     ResourceClasses: {
-      Node: { useList: (opts?: { namespace?: string }) => [unknown[] | null, unknown, ...unknown[]] };
-      Pod: { useList: (opts?: { namespace?: string }) => [unknown[] | null, unknown, ...unknown[]] };
+      Node: { useList: (opts?: ListOptions) => [unknown[] | null, unknown, ...unknown[]] };
+      Pod: { useList: (opts?: ListOptions) => [unknown[] | null, unknown, ...unknown[]] };
     };
   };
   ApiProxy: { request: (path: string) => Promise<unknown> };
@@ -35,11 +46,27 @@ export interface ClusterStore {
   attachOperatorFeed(): () => void;
   /** Feed the operator pods of the scoped lists (null while in flight). */
   setOperatorPods(items: unknown[] | null, error: string | null): void;
+  /** The operator pods by the plugin-pod requests (a client without list hooks, or a host ignoring list options). */
+  loadOperatorPods(): Promise<void>;
   refresh(): Promise<void>;
   revalidate(maxAgeMs?: number): Promise<void>;
-  loadLists(): Promise<void>;
+  loadLists(which?: { nodes?: boolean; pods?: boolean }): Promise<void>;
   settled(): Promise<void>;
   hasLoaded(): boolean;
+  /** A pod list feed is mounted right now. */
+  podFeedMounted(): boolean;
+  /** A scoped list of `kind` delivered `n` objects outside its selection (the host ignored the options). */
+  noteSelectorIgnored(kind: 'nodePods' | 'operatorPods', n: number, delivery?: object): void;
+  selectorsIgnored(kind: 'nodePods' | 'operatorPods'): boolean;
+  counters(): {
+    indexBuilds: number;
+    indexPatches: number;
+    subscribers: number;
+    podFeeds: number;
+    operatorFeeds: number;
+    selectorIgnored: { nodePods: number; operatorPods: number } | null;
+    [k: string]: unknown;
+  };
 }
 
 export interface MetricsSource {
@@ -65,7 +92,7 @@ export interface MetricsSource {
 export interface ProviderCore {
   Context: Context<AmdGpuContextValue | null>;
   /** `needs`: what the page draws — only those lists / requests are mounted (default: all) */
-  AmdGpuDataProvider: ComponentType<{ children?: ReactNode; needs?: { nodes?: boolean; pods?: boolean; crd?: boolean } }>;
+  AmdGpuDataProvider: ComponentType<{ children?: ReactNode; needs?: { nodes?: boolean; pods?: boolean; crd?: boolean; operatorPods?: boolean } }>;
   /** Mounts the pod list + watch into the current cluster's store (a page whose provider does not feed pods) */
   PodListHere: ComponentType<Record<string, never>>;
   useAmdGpuContext(): AmdGpuContextValue;
@@ -86,12 +113,16 @@ export interface ProviderCore {
   ): GpuMetricsState;
   usePodGpuSeries(namespace: string | null, pod: string | null, enabled?: boolean): GpuMetricsState;
   useNodeGpuSeries(nodeName: string | null, enabled?: boolean): GpuMetricsState;
-  /** One node's pods for a Node detail section on a cold store: the host's list + watch scoped by `spec.nodeName` */
+  /**
+   * One node's pods for a Node detail section no page feeds: the host's list + watch scoped by `spec.nodeName`
+   * (or, on a host ignoring list options, the field-selected request re-read), seeded by the store's last list.
+   * Returns [what nodeDetailView reads, the feed element the caller must render].
+   */
   useNodePods(
     nodeName: string
-  ): { loading: boolean; gpuPods: unknown[]; podsState: 'pending' | 'ready' | 'error'; error: string | null };
-  /** The shared store already holds the node and pod lists (a plugin page fed it) */
-  storeWarm(): boolean;
+  ): [{ loading: boolean; gpuPods: unknown[]; podsState: 'pending' | 'ready' | 'error'; error: string | null }, ReactNode];
+  /** A mounted pod feed keeps the shared store current (re-renders the caller when that flips). */
+  usePodsLive(): boolean;
   storeFor(cluster: string): ClusterStore;
   metricsSourceFor(cluster: string): MetricsSource;
   /** The current cluster's key (per-cluster state: stores, view state). */

@@ -24,9 +24,11 @@
  *     (reference quirk Q7: every route mounted a cold provider).
  */
 
-import { createClusterStore, getSharedStore, nodePodsSelector, storeIsWarm } from './clusterStore.js';
-import { dedupePods, filterAmdGpuPluginPods, filterGpuRequestingPods, get, OPERATOR_POD_LISTS, unwrapAll } from './amdgpu.js';
+import { createClusterStore, fetchNodePods, getSharedStore, nodePodsSelector, storeIsLive } from './clusterStore.js';
+import { dedupePods, filterAmdGpuPluginPods, filterGpuRequestingPods } from './amdPods.js';
+import { get, OPERATOR_POD_LISTS, unwrapAll } from './k8sCore.js';
 import { createMetricsSource } from './metrics.js';
+import { countOutside } from './selectors.js';
 import { clusterKey as defaultClusterKey } from './cluster.js';
 import { POLL_MISS, createPoller, loadSettings as defaultLoadSettings, prometheusCandidates, seriesStepSec } from './settings.js';
 
@@ -35,6 +37,16 @@ export const STALE_MS = 5000;
 
 /** What a provider feeds by default: both lists and the DeviceConfigs (the reference's provider). */
 const ALL_NEEDS = Object.freeze({ nodes: true, pods: true, crd: true, operatorPods: false });
+
+/** A provider that reads the store and mounts nothing (a Node detail section next to a page that feeds it). */
+export const READ_ONLY_NEEDS = Object.freeze({ nodes: false, pods: false, crd: false, operatorPods: false });
+
+/**
+ * Period (s) of a scoped request that stands in for a list + watch the host
+ * would not scope (ADR 012) when auto-refresh is off: a watch is live, so
+ * its stand-in is re-read rather than read once.
+ */
+export const SCOPED_POLL_SEC = 30;
 
 export const PROMETHEUS_UNREACHABLE =
   'Could not reach Prometheus. Ensure kube-prometheus-stack is installed in the monitoring namespace.';
@@ -167,7 +179,7 @@ export function createProviderCore(React, lib, deps) {
   }
 
   /**
-   * The operator pods by their own lists + watches (amdgpu.js
+   * The operator pods by their own lists + watches (k8sCore.js
    * OPERATOR_POD_LISTS: the plugin labels outside the operator namespace,
    * and the operator namespace) — what a page that draws operator pods but
    * no other pod mounts (Device Plugins), instead of the all-namespaces list.
@@ -187,17 +199,52 @@ export function createProviderCore(React, lib, deps) {
       let pending = false;
       let failed = 0;
       let found = [];
+      let outside = 0;
       for (let i = 0; i < lists.length; i++) {
         if (lists[i][1]) failed++;
         else if (!lists[i][0]) pending = true;
-        else found = found.concat(filterAmdGpuPluginPods(unwrapAll(lists[i][0])));
+        else {
+          const raw = unwrapAll(lists[i][0]);
+          outside += countOutside(raw, OPERATOR_POD_LISTS[i]);
+          found = found.concat(filterAmdGpuPluginPods(raw));
+        }
       }
-      if (failed === lists.length) return { items: null, error: errorText(a[1]) };
-      return { items: pending ? null : dedupePods(found), error: null };
+      if (failed === lists.length) return { items: null, error: errorText(a[1]), outside: outside };
+      // A host that dropped the list options delivered every pod: the answer
+      // is still right (the plugin-pod filter), but the provider swaps this
+      // feed for the scoped requests (OperatorPodPoll).
+      return { items: pending ? null : dedupePods(found), error: null, outside: outside };
     }, [a[0], a[1], b[0], b[1]]);
     useEffect(function () {
       store.setOperatorPods(fed.items, fed.error);
+      if (fed.outside > 0) store.noteSelectorIgnored('operatorPods', fed.outside, fed);
     }, [store, fed]);
+    return null;
+  }
+
+  /** How often a scoped request standing in for a watch is re-read: the refresh period, else SCOPED_POLL_SEC. */
+  function scopedPollSec() {
+    const sec = loadSettings().refreshIntervalSec;
+    return sec > 0 ? sec : SCOPED_POLL_SEC;
+  }
+
+  /**
+   * The operator pods by the plugin-pod requests (PLUGIN_POD_QUERIES: the
+   * same two selections, applied by the apiserver as query parameters),
+   * re-read every scopedPollSec(): what the provider mounts instead of
+   * OperatorPodFeed on a host that ignores useList() options, so Device
+   * Plugins never mounts the unscoped lists such a host would deliver.
+   */
+  function OperatorPodPoll(props) {
+    const store = props.store;
+    const period = scopedPollSec();
+    useEffect(function () { return store.attachOperatorFeed(); }, [store]);
+    useEffect(function () {
+      store.loadOperatorPods();
+      const poller = createPoller(period);
+      poller.start(function () { return store.loadOperatorPods(); });
+      return function () { poller.stop(); };
+    }, [store, period]);
     return null;
   }
 
@@ -256,7 +303,7 @@ export function createProviderCore(React, lib, deps) {
     return h(Context.Provider, { value: value },
       wantNodes ? h(NodeListFeed, { store: store }) : null,
       wantPods ? h(PodListFeed, { store: store }) : null,
-      wantOps ? h(OperatorPodFeed, { store: store }) : null,
+      wantOps ? h(store.selectorsIgnored('operatorPods') ? OperatorPodPoll : OperatorPodFeed, { store: store }) : null,
       props.children);
   }
 
@@ -451,50 +498,134 @@ export function createProviderCore(React, lib, deps) {
   }
 
   /**
-   * True when the cluster's shared store already holds the node and pod lists
-   * (a plugin page fed it): a Node detail section then reads it; otherwise it
-   * reads its own node's pods (useNodePods) instead of mounting the
-   * cluster-wide watches.
+   * True while a mounted pod feed keeps the cluster's shared store current
+   * (clusterStore.js storeIsLive: a plugin page that draws pods is mounted
+   * next to the caller). A Node detail section then reads the store;
+   * otherwise it reads its own node's pods (useNodePods) and never mounts a
+   * cluster-wide watch. Re-renders the caller when that flips (the page
+   * unmounts, or its list arrives).
    */
-  function storeWarm() {
-    return storeIsWarm(storeFor(clusterKey()));
+  function usePodsLive() {
+    const store = storeFor(clusterKey());
+    return React.useSyncExternalStore(store.subscribe, function () { return storeIsLive(store); });
+  }
+
+  /** Raw pods of `items` (list-hook items or raw objects) bound to `nodeName`. */
+  function onNode(items, nodeName) {
+    return unwrapAll(items).filter(function (p) { return get(p, ['spec', 'nodeName'], null) === nodeName; });
   }
 
   /**
-   * The pods of one node for a Node detail section on a cold store: the
-   * host's list + watch hook SCOPED to the node (`fieldSelector
-   * spec.nodeName=<node>`, all namespaces), so the section is live like the
-   * reference's — a pod scheduled onto the node appears without a reload
-   * (reference src/index.tsx:152-160: a full provider with the cluster-wide
-   * Pod list + watch, IntelGpuDataContext.tsx:98-99) — at O(pods on the node)
-   * instead of O(pods in the cluster). The list request goes out in the same
-   * wave as the node's telemetry and power history. The pods are filtered by
-   * node here too, so a host that ignores the field selector is still correct
-   * (only slower). A list that stops answering after it delivered keeps the
-   * pods shown; only a first failure says the pods are unreadable.
-   * Returns the slice of the context nodeDetailView reads.
+   * One node's pods by the host's list + watch hook SCOPED to the node
+   * (`fieldSelector spec.nodeName=<node>`, all namespaces), delivered to
+   * `props.onList(node, pods | null, error | null)`. The pods are filtered by
+   * node here too; objects of other nodes mean the host ignored the field
+   * selector (store.noteSelectorIgnored), and useNodePods swaps this feed for
+   * NodePodsPoll.
    */
-  function useNodePods(nodeName) {
-    const res = useListOf(lib.K8s.ResourceClasses.Pod, { namespace: '', fieldSelector: nodePodsSelector(nodeName) });
+  function NodePodsWatch(props) {
+    const node = props.node;
+    const opts = useMemo(function () { return { namespace: '', fieldSelector: nodePodsSelector(node) }; }, [node]);
+    const res = useListOf(lib.K8s.ResourceClasses.Pod, opts);
     const items = res[0];
     const err = res[1];
-    const listed = useMemo(function () {
-      if (!items) return null;
-      return unwrapAll(items).filter(function (p) { return get(p, ['spec', 'nodeName'], null) === nodeName; });
-    }, [items, nodeName]);
-    // The last list delivered, for a watch that re-lists (or fails) after it
-    // delivered: what is shown stays instead of flapping to loading / error.
-    const last = React.useRef(null);
+    const got = useMemo(function () {
+      if (!items) return { pods: null, outside: 0 };
+      const raw = unwrapAll(items);
+      return { pods: onNode(raw, node), outside: countOutside(raw, opts) };
+    }, [items, node, opts]);
     useEffect(function () {
-      if (listed) last.current = { node: nodeName, pods: listed };
-    }, [listed, nodeName]);
-    const kept = !listed && last.current && last.current.node === nodeName ? last.current.pods : null;
-    const pods = listed || kept;
-    return useMemo(function () {
+      if (got.outside > 0) props.store.noteSelectorIgnored('nodePods', got.outside, got);
+      props.onList(node, got.pods, got.pods ? null : err ? errorText(err) : null);
+    }, [got, err, node]);
+    return null;
+  }
+
+  /**
+   * One node's pods by the field-selected request (requests.js
+   * fetchNodePods: the apiserver applies the selector as a query parameter),
+   * re-read every scopedPollSec(): what a Node detail section reads on a host
+   * that ignores useList() options, instead of the cluster-wide list such a
+   * host would deliver.
+   */
+  function NodePodsPoll(props) {
+    const node = props.node;
+    const onList = props.onList;
+    const period = scopedPollSec();
+    useEffect(function () {
+      let live = true;
+      const timeoutMs = loadSettings().requestTimeoutMs;
+      function read() {
+        return fetchNodePods(request, node, timeoutMs).then(
+          function (items) { if (live) onList(node, onNode(items, node), null); },
+          function (e) { if (live) onList(node, null, errorText(e)); }
+        );
+      }
+      read();
+      const poller = createPoller(period);
+      poller.start(read);
+      return function () {
+        live = false;
+        poller.stop();
+      };
+    }, [node, period]);
+    return null;
+  }
+
+  /** The GPU pods of `nodeName` in the store's last pod list (any age), or null when it holds none. */
+  function seedPods(store, nodeName) {
+    const snap = store.getSnapshot();
+    if (snap.podsState !== 'ready') return null;
+    const byNode = snap.index && snap.index.podsByNode ? snap.index.podsByNode.get(nodeName) : undefined;
+    return byNode || snap.gpuPods.filter(function (p) { return get(p, ['spec', 'nodeName'], null) === nodeName; });
+  }
+
+  /**
+   * The pods of one node for a Node detail section that no mounted page
+   * feeds: a list + watch scoped to the node (NodePodsWatch), live like the
+   * reference's section — a pod scheduled onto the node appears without a
+   * reload (reference src/index.tsx:152-160: a full provider with the
+   * cluster-wide Pod list + watch, IntelGpuDataContext.tsx:98-99) — at O(pods
+   * on the node) instead of O(pods in the cluster); on a host that ignores
+   * list options, the field-selected request re-read (NodePodsPoll). The
+   * list request goes out in the same wave as the node's telemetry and power
+   * history.
+   *
+   * Until the node's own list delivers, the store's last pod list (a plugin
+   * page visited earlier, no longer watched) seeds the section, so it paints
+   * at once. A list that stops answering after it delivered keeps the pods
+   * shown; only a first failure says the pods are unreadable.
+   *
+   * Returns [the slice of the context nodeDetailView reads, the feed element
+   * the caller renders].
+   */
+  function useNodePods(nodeName) {
+    const store = storeFor(clusterKey());
+    const ignored = React.useSyncExternalStore(store.subscribe, function () { return store.selectorsIgnored('nodePods'); });
+    const seed = useMemo(function () { return seedPods(store, nodeName); }, [store, nodeName]);
+    const st = useState(null);
+    const got = st[0];
+    const setGot = st[1];
+    const onList = useMemo(function () {
+      return function (node, pods, error) {
+        setGot(function (prev) {
+          const same = prev && prev.node === node;
+          if (pods) return { node: node, pods: pods, error: null };
+          // A re-list or a failure after a delivery keeps what is shown.
+          if (same && prev.pods) return prev;
+          return error ? { node: node, pods: null, error: error } : same ? prev : null;
+        });
+      };
+    }, []);
+    const cur = got && got.node === nodeName ? got : null;
+    const pods = cur && cur.pods ? cur.pods : cur && cur.error ? null : seed;
+    const ctx = useMemo(function () {
       if (pods) return { loading: false, gpuPods: filterGpuRequestingPods(pods), podsState: 'ready', error: null };
-      if (err) return { loading: false, gpuPods: [], podsState: 'error', error: errorText(err) };
+      if (cur && cur.error) return { loading: false, gpuPods: [], podsState: 'error', error: cur.error };
       return { loading: true, gpuPods: [], podsState: 'pending', error: null };
-    }, [pods, err]);
+    }, [pods, cur && cur.error]);
+    const feed = h(ignored ? NodePodsPoll : NodePodsWatch, { node: nodeName, onList: onList, store: store });
+    return [ctx, feed];
   }
 
   /** One node's GPU power history for the native Node detail page (metrics.js fetchNodeSeries). */
@@ -547,7 +678,7 @@ export function createProviderCore(React, lib, deps) {
     usePodGpuSeries: usePodGpuSeries,
     useNodeGpuSeries: useNodeGpuSeries,
     useNodePods: useNodePods,
-    storeWarm: storeWarm,
+    usePodsLive: usePodsLive,
     storeFor: storeFor,
     metricsSourceFor: metricsSourceFor,
     /** The current cluster's key (per-cluster state: stores, view state). */

@@ -6,7 +6,7 @@
  * reads, shared by callers asking for the same node at once.
  */
 
-import { isKubeList } from './amdgpu.js';
+import { isKubeList } from './k8sCore.js';
 
 export const DEFAULT_REQUEST_TIMEOUT_MS = 2000;
 

@@ -12,8 +12,8 @@
  * falls back to the defaults field by field instead of breaking the plugin.
  */
 
-import { PROMETHEUS_SERVICES } from './metrics.js';
-import { isObject } from './amdgpu.js';
+import { PROMETHEUS_SERVICES } from './series.js';
+import { isObject } from './k8sCore.js';
 
 export const SETTINGS_KEY = 'headlamp-amd-gpu-plugin.settings';
 

@@ -9,7 +9,7 @@
  * by (node, gpu index).
  */
 
-import { MI355X, isObject } from './amdgpu.js';
+import { isObject, MI355X } from './k8sCore.js';
 import { SERIES, STATIC_GPU_FIELDS } from './series.js';
 import { isExporterName } from './promql.js';
 

@@ -12,7 +12,9 @@
  * exact; otherwise they are filled in pod order and flagged `inferred`.
  */
 
-import { MI355X, getNodeGpuCount, getPodGpuCount, get, partitionsPerGpu } from './amdgpu.js';
+import { getNodeGpuCount, partitionsPerGpu } from './amdNodes.js';
+import { getPodGpuCount } from './amdPods.js';
+import { get, MI355X } from './k8sCore.js';
 
 /**
  * One schedulable device. On a partitioned node (DPX/QPX/CPX) device `index`

@@ -1,7 +1,7 @@
 /**
  * Typed shapes of the Kubernetes / AMD objects the plugin reads — the fields
  * it actually uses, nothing more. Runtime narrowing from `unknown` happens in
- * the `is*` guards of ./amdgpu.js; these interfaces describe what a value is
+ * the `is*` guards of ./k8sCore.js, ./amdNodes.js and ./amdPods.js; these interfaces describe what a value is
  * once a guard has accepted it.
  *
  * Reference analog: src/api/k8s.ts:37-50 (KubeObjectMeta, KubeObject),

@@ -1,6 +1,6 @@
 /**
  * The plugin, assembled: every page, detail section, table column and the
- * settings page, built from the pure view-models (./view/pages.js), the IR
+ * settings page, built from the pure view-models (./view/pages/*.js), the IR
  * renderer (./view/react.js) and the provider core (./api/providerCore.js)
  * against an INJECTED React + Headlamp library. `registerPlugin` performs the
  * registration the reference does at module load (src/index.tsx:35-182,
@@ -19,22 +19,17 @@
  * in the background (reference quirk Q7).
  */
 
-import { createProviderCore } from './api/providerCore.js';
-import { get, isAmdGpuNode, isGpuRequestingPod, unwrapKubeObject } from './api/amdgpu.js';
-import {
-  devicePluginsView,
-  metricsView,
-  nodeColumns,
-  nodeDetailView,
-  nodesView,
-  overviewView,
-  podDetailView,
-  podsView,
-  nodeSortOf,
-  ownersScope,
-  RANKED_NODE_SORTS,
-  telemetryScope,
-} from './view/pages.js';
+import { createProviderCore, READ_ONLY_NEEDS } from './api/providerCore.js';
+import { isAmdGpuNode } from './api/amdNodes.js';
+import { isGpuRequestingPod } from './api/amdPods.js';
+import { get, unwrapKubeObject } from './api/k8sCore.js';
+import { nodeColumns, nodeDetailView, podDetailView } from './view/pages/details.js';
+import { devicePluginsView } from './view/pages/devicePlugins.js';
+import { metricsView } from './view/pages/metricsPage.js';
+import { nodesView, telemetryScope } from './view/pages/nodes.js';
+import { overviewView } from './view/pages/overview.js';
+import { nodeSortOf, RANKED_NODE_SORTS } from './view/pages/paging.js';
+import { ownersScope, podsView } from './view/pages/pods.js';
 import { createRenderer } from './view/react.js';
 import { createSettingsPage } from './view/settingsPage.js';
 import { loadViewState, saveViewState } from './api/settings.js';
@@ -215,28 +210,35 @@ export function createPlugin(env) {
   }
 
   /**
-   * The Node detail section on a cold store (no plugin page visited yet): the
-   * node's own pods by a list + watch scoped to the node (live, like the
-   * reference's section), with its telemetry and power history in the same
-   * wave — no cluster-wide watch is mounted. Mounted for AMD GPU nodes only.
+   * The Node detail section when no mounted page feeds the store — the usual
+   * case: Headlamp reaches a Node's page from its own Nodes list, after any
+   * plugin page unmounted. The node's own pods by a list + watch scoped to
+   * the node (live, like the reference's section; seeded by the store's last
+   * pod list for the first paint), with its telemetry and power history in
+   * the same wave — no cluster-wide watch and no DeviceConfig request.
+   * Mounted for AMD GPU nodes only.
    */
   function NodeDetailCold(props) {
     const name = unwrapKubeObject(props.resource).metadata.name;
-    const ctx = core.useNodePods(name);
+    const np = core.useNodePods(name);
     const m = core.useNodeGpuMetrics(name, true);
     const ps = core.useNodeGpuSeries(name, true);
-    const section = nodeDetailView(props.resource, ctx, { metrics: m.metrics, series: ps.series });
-    return section ? h(Section, { s: section }) : null;
+    const section = nodeDetailView(props.resource, np[0], { metrics: m.metrics, series: ps.series });
+    return h(React.Fragment, null, np[1], section ? h(Section, { s: section }) : null);
   }
 
   /**
-   * Nothing for a node without AMD GPUs. Warm store (a plugin page loaded the
-   * cluster): the section reads it under the shared provider. Cold:
-   * NodeDetailCold, O(one node).
+   * Nothing for a node without AMD GPUs. While a plugin page that draws pods
+   * is mounted next to it (its pod feed keeps the store current), the section
+   * reads the store under a provider that mounts nothing (READ_ONLY_NEEDS);
+   * otherwise NodeDetailCold, O(one node). The reference mounts a full
+   * provider — both cluster-wide lists and the CRD + 3 serial requests — on
+   * every Node detail page (src/index.tsx:152-160).
    */
   function NodeDetailHost(props) {
+    const live = core.usePodsLive();
     if (!isAmdGpuNode(unwrapKubeObject(props.resource))) return null;
-    if (core.storeWarm()) return h(core.AmdGpuDataProvider, null, h(NodeDetailSection, props));
+    if (live) return h(core.AmdGpuDataProvider, { needs: READ_ONLY_NEEDS }, h(NodeDetailSection, props));
     return h(NodeDetailCold, props);
   }
 

@@ -5,6 +5,7 @@
  * draw (allocation, power, HBM, temperature, RAS).
  */
 
+import { getPodRestarts, isPodReady } from '../../api/amdPods.js';
 import {
   BAR_COLORS,
   formatAge,
@@ -12,13 +13,11 @@ import {
   formatPercent,
   formatWatts,
   get,
-  getPodRestarts,
-  isPodReady,
   MI355X,
   nextAgeChange,
   pct,
   pctToColor,
-} from '../../api/amdgpu.js';
+} from '../../api/k8sCore.js';
 import { bar, createMemo, createObjectCache, kv, noteExpiry, row, section, status } from '../ir.js';
 
 export const BRAND = 'AMD GPU';

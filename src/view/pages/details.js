@@ -6,30 +6,34 @@
  */
 
 import {
-  AMD_GPU_RESOURCE,
-  containerGpuEntries,
-  formatBytes,
   formatGpuModel,
-  formatGpuResourceName,
-  formatWatts,
-  get,
   getGpuResources,
   getNodeGpuCount,
   getNodeGpuModel,
   getNodePhysicalGpuCount,
+  isAmdGpuNode,
+} from '../../api/amdNodes.js';
+import {
+  containerGpuEntries,
   getPodGpuCount,
   getPodGpuDemand,
   gpuContainers,
   gpuInitContainers,
-  isAmdGpuNode,
   isGpuRequestingPod,
+  podPhase,
+} from '../../api/amdPods.js';
+import {
+  AMD_GPU_RESOURCE,
+  formatBytes,
+  formatGpuResourceName,
+  formatWatts,
+  get,
   MI355X,
   pct,
   pctToStatus,
-  podPhase,
   unwrapKubeObject,
-} from '../../api/amdgpu.js';
-import { clusterPowerStats } from '../../api/metrics.js';
+} from '../../api/k8sCore.js';
+import { clusterPowerStats } from '../../api/telemetry.js';
 import { kv, row, section, status } from '../ir.js';
 import { formatWindow, memo, podDetailCache, podName, podsPending, seriesMeans } from './common.js';
 import { gpuTelemetryTable } from './metricsPage.js';

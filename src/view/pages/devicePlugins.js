@@ -9,14 +9,13 @@ import {
   countsToText,
   deviceConfigStatus,
   deviceConfigStatusText,
-  formatComponent,
   formatSelector,
-  get,
   operandEnabled,
   OPERANDS,
   operandStatus,
-  pluginPodComponent,
-} from '../../api/amdgpu.js';
+} from '../../api/amdNodes.js';
+import { formatComponent, pluginPodComponent } from '../../api/amdPods.js';
+import { get } from '../../api/k8sCore.js';
 import { kv, loader, page, pager, row, section, status, table } from '../ir.js';
 import {
   ageText,

@@ -4,8 +4,9 @@
  * the page with a per-GPU table.
  */
 
-import { formatWatts, MI355X } from '../../api/amdgpu.js';
-import { clusterPowerStats, PROMETHEUS_SERVICES, summarizeMetrics } from '../../api/metrics.js';
+import { formatWatts, MI355X } from '../../api/k8sCore.js';
+import { PROMETHEUS_SERVICES } from '../../api/series.js';
+import { clusterPowerStats, summarizeMetrics } from '../../api/telemetry.js';
 import { kv, lines, loader, page, pager, row, section, status, table } from '../ir.js';
 import {
   BRAND,

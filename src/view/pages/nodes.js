@@ -6,19 +6,16 @@
  */
 
 import {
-  formatBytes,
   formatGpuModel,
-  formatGpuResourceName,
-  get,
   getGpuResources,
   getNodeGpuCount,
   getNodeGpuModel,
   getNodePhysicalGpuCount,
   isNodeReady,
   labellerValue,
-  MI355X,
-} from '../../api/amdgpu.js';
-import { SMALL_CLUSTER_NODES } from '../../api/metrics.js';
+} from '../../api/amdNodes.js';
+import { formatBytes, formatGpuResourceName, get, MI355X } from '../../api/k8sCore.js';
+import { SMALL_CLUSTER_NODES } from '../../api/series.js';
 import { buildGpuSlots, buildXgmiMatrix, isFullMesh } from '../../api/topology.js';
 import { kv, loader, page, pager, row, section, status, table } from '../ir.js';
 import {

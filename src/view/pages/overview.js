@@ -4,22 +4,15 @@
  */
 
 import {
-  AMD_GPU_OPERATOR_NAMESPACE,
-  BAR_COLORS,
   deviceConfigStatus,
   deviceConfigStatusText,
-  formatBytes,
-  formatComponent,
-  formatPodGpuRequests,
   formatSelector,
-  get,
   getNodeGpuModel,
-  isPodReady,
-  MI355X,
   operandEnabled,
-  pluginPodComponent,
-  podFacts,
-} from '../../api/amdgpu.js';
+} from '../../api/amdNodes.js';
+import { formatComponent, formatPodGpuRequests, isPodReady, pluginPodComponent } from '../../api/amdPods.js';
+import { podFacts } from '../../api/clusterIndex.js';
+import { AMD_GPU_OPERATOR_NAMESPACE, BAR_COLORS, formatBytes, get, MI355X } from '../../api/k8sCore.js';
 import { kv, loader, page, pctbar, row, section, status, table } from '../ir.js';
 import {
   ageText,

@@ -6,7 +6,9 @@
  * the telemetry of those only.
  */
 
-import { get, isNodeReady, podFacts } from '../../api/amdgpu.js';
+import { isNodeReady } from '../../api/amdNodes.js';
+import { podFacts } from '../../api/clusterIndex.js';
+import { get } from '../../api/k8sCore.js';
 import { memo, NO_PODS } from './common.js';
 
 /** GPU nodes per page on the GPU Nodes and Metrics pages. */

@@ -6,19 +6,17 @@
 
 import {
   containerGpuEntries,
-  formatBytes,
-  formatGpuResourceName,
   formatPodGpuRequests,
-  formatWatts,
   gpuContainers,
   gpuInitContainers,
   phaseToStatus,
-  podFacts,
   podPhase,
   podWaitingMessage,
   podWaitingReason,
-} from '../../api/amdgpu.js';
-import { SMALL_CLUSTER_PODS } from '../../api/metrics.js';
+} from '../../api/amdPods.js';
+import { podFacts } from '../../api/clusterIndex.js';
+import { formatBytes, formatGpuResourceName, formatWatts } from '../../api/k8sCore.js';
+import { SMALL_CLUSTER_PODS } from '../../api/series.js';
 import { kv, lines, loader, page, pager, row, section, status, table } from '../ir.js';
 import {
   ageText,

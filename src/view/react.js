@@ -25,7 +25,7 @@
  * for the inline bar idiom).
  */
 
-import { BAR_COLORS, formatWatts } from '../api/amdgpu.js';
+import { BAR_COLORS, formatWatts } from '../api/k8sCore.js';
 import { matrixCaption, pagerText } from './ir.js';
 
 /** CommonComponents the renderer needs (reference src/components/OverviewPage.tsx:8-16). */

@@ -2,60 +2,64 @@
  * Domain-model specs (analog of reference src/api/k8s.test.ts, 48 cases).
  */
 import {
-  AMD_GPU_RESOURCE,
-  DEVICE_CONFIG_LIST_PATH,
-  MI355X,
-  PLUGIN_POD_QUERIES,
-  buildClusterIndex,
-  containerGpuEntries,
   countsToStatus,
   countsToText,
-  dedupePods,
   deviceConfigStatus,
   deviceConfigStatusText,
   filterAmdGpuNodes,
-  filterAmdGpuPluginPods,
-  filterGpuRequestingPods,
-  formatAge,
-  nextAgeChange,
-  formatBytes,
   formatGpuModel,
-  shortProductName,
-  formatGpuResourceName,
-  formatPercent,
-  formatPodGpuRequests,
   formatSelector,
-  formatWatts,
   getGpuResources,
   getNodeGpuAllocatable,
   getNodeGpuCount,
   getNodeGpuModel,
   getNodePartitionCount,
+  isAmdGpuNode,
+  isDeviceConfig,
+  isNodeReady,
+  operandEnabled,
+  operandStatus,
+  shortProductName,
+} from '../../src/api/amdNodes.js';
+import {
+  containerGpuEntries,
+  dedupePods,
+  filterAmdGpuPluginPods,
+  filterGpuRequestingPods,
+  formatPodGpuRequests,
   getPodGpuCount,
   getPodGpuDemand,
   getPodGpuRequests,
   getPodRestarts,
-  isAmdGpuNode,
   isAmdGpuPluginPod,
-  isDeviceConfig,
   isGpuRequestingPod,
-  isNamedObject,
-  isKubeList,
-  isNodeReady,
   isPodReady,
-  operandEnabled,
-  operandStatus,
-  parseCount,
-  pct,
-  pctToColor,
-  pctToStatus,
   phaseToStatus,
   pluginPodComponent,
   podWaitingMessage,
   podWaitingReason,
+} from '../../src/api/amdPods.js';
+import { buildClusterIndex } from '../../src/api/clusterIndex.js';
+import {
+  AMD_GPU_RESOURCE,
+  DEVICE_CONFIG_LIST_PATH,
+  formatAge,
+  formatBytes,
+  formatGpuResourceName,
+  formatPercent,
+  formatWatts,
+  isKubeList,
+  isNamedObject,
+  MI355X,
+  nextAgeChange,
+  parseCount,
+  pct,
+  pctToColor,
+  pctToStatus,
+  PLUGIN_POD_QUERIES,
   unwrapAll,
   unwrapKubeObject,
-} from '../../src/api/amdgpu.js';
+} from '../../src/api/k8sCore.js';
 import { NOW, ago, makeDeviceConfig, makeGpuNode, makeGpuPod, makeNode, makePlainPod, makePluginPod } from './fixtures.js';
 
 describe('constants', () => {

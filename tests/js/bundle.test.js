@@ -13,7 +13,7 @@ import React, { render } from './stubs/react.js';
 import * as lib from './stubs/headlamp-lib.js';
 import * as CC from './stubs/CommonComponents.js';
 import { bundle, transformModule, EXTERNALS } from '../../tools/bundle.js';
-import { DEVICE_CONFIG_LIST_PATH } from '../../src/api/amdgpu.js';
+import { DEVICE_CONFIG_LIST_PATH } from '../../src/api/k8sCore.js';
 import { makeDeviceConfig, makeGpuNode, makeGpuPod, makeNode, makePlainPod, makePluginPod } from './fixtures.js';
 
 const ROOT = path.resolve(path.dirname(fileURLToPath(import.meta.url)), '..', '..');
@@ -51,12 +51,12 @@ beforeEach(() => {
 describe('tools/bundle.js', () => {
   it('bundles the entry and the modules it imports, nothing from the harness', () => {
     expect(built.modules[built.modules.length - 1]).toBe('src/index.tsx');
-    ['src/headlamp.ts', 'src/plugin.js', 'src/api/providerCore.js', 'src/api/clusterStore.js', 'src/api/metrics.js', 'src/view/pages.js', 'src/view/react.js'].forEach((m) => {
+    ['src/headlamp.ts', 'src/plugin.js', 'src/api/providerCore.js', 'src/api/clusterStore.js', 'src/api/metrics.js', 'src/view/pages/overview.js', 'src/view/react.js'].forEach((m) => {
       expect(built.modules).toContain(m);
     });
     built.modules.forEach((m) => expect(m.indexOf('tests/')).toBe(-1));
     // dependencies before dependants
-    expect(built.modules.indexOf('src/api/amdgpu.js')).toBeLessThan(built.modules.indexOf('src/api/clusterStore.js'));
+    expect(built.modules.indexOf('src/api/amdNodes.js')).toBeLessThan(built.modules.indexOf('src/api/clusterStore.js'));
   });
 
   it('leaves no module syntax and only host modules outside', () => {

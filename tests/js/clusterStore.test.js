@@ -5,9 +5,10 @@
  */
 import fs from 'fs';
 import { createClusterStore, fetchNodePods, getSharedStore, nodePodsPath, resetSharedStores, withTimeout } from '../../src/api/clusterStore.js';
-import { DEVICE_CONFIG_LIST_PATH, PLUGIN_POD_QUERIES } from '../../src/api/amdgpu.js';
+import { DEVICE_CONFIG_LIST_PATH, PLUGIN_POD_QUERIES } from '../../src/api/k8sCore.js';
 import { makeDeviceConfig, makeGpuNode, makeGpuPod, makeNode, makePlainPod, makePluginPod, NOW } from './fixtures.js';
-import { metricsView, nodeDetailView } from '../../src/view/pages.js';
+import { nodeDetailView } from '../../src/view/pages/details.js';
+import { metricsView } from '../../src/view/pages/metricsPage.js';
 import { rowValue, text } from '../../src/view/ir.js';
 
 function deferred() {

@@ -127,7 +127,9 @@ export function makePluginPod(name, o) {
 }
 
 /** A snapshot shaped like ClusterStore.getSnapshot(), built from raw objects. */
-import { buildClusterIndex, filterAmdGpuNodes, filterGpuRequestingPods } from '../../src/api/amdgpu.js';
+import { filterAmdGpuNodes } from '../../src/api/amdNodes.js';
+import { filterGpuRequestingPods } from '../../src/api/amdPods.js';
+import { buildClusterIndex } from '../../src/api/clusterIndex.js';
 
 export function makeContext(over) {
   const o = over || {};

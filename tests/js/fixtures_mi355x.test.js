@@ -6,8 +6,10 @@
  */
 import fs from 'fs';
 import path from 'path';
-import { SERIES, joinExporterResults, splitByName } from '../../src/api/metrics.js';
-import { MI355X, formatBytes, shortProductName } from '../../src/api/amdgpu.js';
+import { SERIES } from '../../src/api/series.js';
+import { joinExporterResults, splitByName } from '../../src/api/telemetry.js';
+import { shortProductName } from '../../src/api/amdNodes.js';
+import { formatBytes, MI355X } from '../../src/api/k8sCore.js';
 import { parseExposition } from './promFake.js';
 
 const DIR = path.join(process.cwd(), 'tests', 'fixtures', 'mi355x');

@@ -4,18 +4,20 @@
  * (PodDetailSection.test.tsx, 10 cases), the Nodes-table columns (untested in
  * the reference) and the topology model (new).
  */
-import { formatEnergy, nodeColumns, nodeDetailView, podDetailView, seriesEnergyJoules } from '../../src/view/pages.js';
+import {
+  formatEnergy,
+  nodeColumns,
+  nodeDetailView,
+  podDetailView,
+  seriesEnergyJoules,
+} from '../../src/view/pages/details.js';
 import { findSection, firstBlock, rowNames, rowValue, text } from '../../src/view/ir.js';
 import { buildGpuSlots, buildXgmiMatrix, isFullMesh } from '../../src/api/topology.js';
 import { NOW, makeContext, makeGpuNode, makeGpuPod, makeNode, makePlainPod } from './fixtures.js';
-import {
-  MI355X,
-  buildClusterIndex,
-  getNodeGpuCount,
-  getNodePhysicalGpuCount,
-  getPodGpuCount,
-  partitionsPerGpu,
-} from '../../src/api/amdgpu.js';
+import { getNodeGpuCount, getNodePhysicalGpuCount, partitionsPerGpu } from '../../src/api/amdNodes.js';
+import { getPodGpuCount } from '../../src/api/amdPods.js';
+import { buildClusterIndex } from '../../src/api/clusterIndex.js';
+import { MI355X } from '../../src/api/k8sCore.js';
 
 describe('nodeDetailView', () => {
   const node = makeGpuNode('g0');

@@ -9,15 +9,14 @@
  */
 import { createListTracker } from '../../src/api/listCache.js';
 import { createClusterStore } from '../../src/api/clusterStore.js';
+import { filterAmdGpuNodes } from '../../src/api/amdNodes.js';
 import {
-  buildClusterIndex,
-  filterAmdGpuNodes,
   filterAmdGpuPluginPods,
   filterGpuRequestingPods,
   isAmdGpuPluginPod,
   isGpuRequestingPod,
-  patchClusterIndex,
-} from '../../src/api/amdgpu.js';
+} from '../../src/api/amdPods.js';
+import { buildClusterIndex, patchClusterIndex } from '../../src/api/clusterIndex.js';
 import { makeGpuNode, makeGpuPod, makeNode, makePlainPod, makePluginPod } from './fixtures.js';
 
 function rng(seed) {

@@ -4,10 +4,15 @@
  * inputs → recomputed sections.
  */
 import { createMemo, sections } from '../../src/view/ir.js';
-import { clearViewMemo, metricsView, nodesView, overviewView, podDetailView, podsView } from '../../src/view/pages.js';
+import { clearViewMemo } from '../../src/view/pages/common.js';
+import { podDetailView } from '../../src/view/pages/details.js';
+import { metricsView } from '../../src/view/pages/metricsPage.js';
+import { nodesView } from '../../src/view/pages/nodes.js';
+import { overviewView } from '../../src/view/pages/overview.js';
+import { podsView } from '../../src/view/pages/pods.js';
 import { renderSection } from '../../src/view/html.js';
 import { createClusterStore, sameObjects } from '../../src/api/clusterStore.js';
-import { DEVICE_CONFIG_LIST_PATH, PLUGIN_POD_QUERIES } from '../../src/api/amdgpu.js';
+import { DEVICE_CONFIG_LIST_PATH, PLUGIN_POD_QUERIES } from '../../src/api/k8sCore.js';
 import { NOW, makeContext, makeDeviceConfig, makeGpuNode, makeGpuPod, makeNode, makePlainPod, makePluginPod } from './fixtures.js';
 
 describe('createMemo', () => {

@@ -4,11 +4,17 @@
  * exporter and node-exporter joins, the per-(node, gpu) key, caching and
  * range queries.
  */
+import { createMetricsSource } from '../../src/api/metrics.js';
+import { exporterNodeQuery, exporterQuery, mergedQuery } from '../../src/api/promql.js';
 import {
-  PROMETHEUS_SERVICES, EXPORTER_JOIN_LABELS, EXPORTER_LEAN_LABELS, keyedByHostname, SERIES, createMetricsSource,
-  exporterQuery, mergedQuery, shareGpus, shareMap, staticsOf, applyStatics, exporterNodeQuery, METRIC_VIEWS,
-  splitByName, STALE_FAILURES,
-} from '../../src/api/metrics.js';
+  EXPORTER_JOIN_LABELS,
+  EXPORTER_LEAN_LABELS,
+  METRIC_VIEWS,
+  PROMETHEUS_SERVICES,
+  SERIES,
+  STALE_FAILURES,
+} from '../../src/api/series.js';
+import { applyStatics, keyedByHostname, shareGpus, shareMap, splitByName, staticsOf } from '../../src/api/telemetry.js';
 
 import fs from 'fs';
 import { BASE0, BASE1, exporterData, ok, prom, vec } from './promFake.js';

@@ -5,11 +5,24 @@
  * Discovery, the page views, sharing and failure handling are in
  * metrics.test.js.
  */
+import { createMetricsSource } from '../../src/api/metrics.js';
 import {
-  stringLabels, EXPORTER_JOIN_LABELS, SERIES, createMetricsSource, exporterQuery, mergedQuery, joinExporterResults,
-  joinNodeExporterResults, summarizeMetrics, exporterNodeQuery, nodeSlice, ownersQuery, promString, nodePowerQuery,
+  exporterNodeQuery,
+  exporterQuery,
+  mergedQuery,
+  nodePowerQuery,
+  ownersQuery,
   podPowerQuery,
-} from '../../src/api/metrics.js';
+  promString,
+} from '../../src/api/promql.js';
+import { EXPORTER_JOIN_LABELS, SERIES } from '../../src/api/series.js';
+import {
+  joinExporterResults,
+  joinNodeExporterResults,
+  nodeSlice,
+  stringLabels,
+  summarizeMetrics,
+} from '../../src/api/telemetry.js';
 
 import { exporterData, flatten, ok, prom, vec } from './promFake.js';
 

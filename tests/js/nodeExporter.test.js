@@ -7,8 +7,11 @@
  * (promql.js nodeExporterScopedQuery / nodeExporterSummaryQuery /
  * rankedHwQuery, scopedSnapshots.js hwScoped / hwRanked).
  */
-import { createMetricsSource, SERIES, summarizeMetrics } from '../../src/api/metrics.js';
-import { clearViewMemo, metricsView } from '../../src/view/pages.js';
+import { createMetricsSource } from '../../src/api/metrics.js';
+import { SERIES } from '../../src/api/series.js';
+import { summarizeMetrics } from '../../src/api/telemetry.js';
+import { clearViewMemo } from '../../src/view/pages/common.js';
+import { metricsView } from '../../src/view/pages/metricsPage.js';
 import { sectionTitles } from '../../src/view/ir.js';
 import { makeContext, makeGpuNode, makeGpuPod } from './fixtures.js';
 import { exporterData, prom, vec } from './promFake.js';

@@ -4,33 +4,19 @@
  * PodsPage.test.tsx 6, MetricsPage.test.tsx 9). Assertions target section
  * titles, row labels, status values and refresh aria-labels, as there.
  */
-import {
-  overviewView,
-  devicePluginsView,
-  nodesView,
-  podsView,
-  podDetailView,
-  nodeDetailView,
-  podGpuAssignments,
-  tempCell,
-  eccCell,
-  metricsView,
-  formatWindow,
-  allocationBar,
-  powerBar,
-  hbmBar,
-  gpuContainerLines,
-  ACTIVE_PODS_LIMIT,
-  formatTaints,
-  nodeReadyCell,
-  nodePowerKeys,
-  nodeTempKeys,
-} from '../../src/view/pages.js';
+import { allocationBar, eccCell, formatWindow, hbmBar, powerBar, tempCell } from '../../src/view/pages/common.js';
+import { nodeDetailView, podDetailView } from '../../src/view/pages/details.js';
+import { devicePluginsView } from '../../src/view/pages/devicePlugins.js';
+import { metricsView } from '../../src/view/pages/metricsPage.js';
+import { formatTaints, nodePowerKeys, nodeReadyCell, nodesView, nodeTempKeys } from '../../src/view/pages/nodes.js';
+import { ACTIVE_PODS_LIMIT, overviewView } from '../../src/view/pages/overview.js';
+import { gpuContainerLines, podGpuAssignments, podsView } from '../../src/view/pages/pods.js';
 import { countRows, findSection, firstBlock, firstTable, loaders, rowNames, rowValue, sectionTitles, text } from '../../src/view/ir.js';
 import { renderPage, textContent } from '../../src/view/html.js';
-import { clusterPowerStats, joinExporterResults, SERIES } from '../../src/api/metrics.js';
+import { SERIES } from '../../src/api/series.js';
+import { clusterPowerStats, joinExporterResults } from '../../src/api/telemetry.js';
 import { NOW, makeContext, makeDeviceConfig, makeGpuNode, makeGpuPod, makeNode, makePlainPod, makePluginPod } from './fixtures.js';
-import { MI355X } from '../../src/api/amdgpu.js';
+import { MI355X } from '../../src/api/k8sCore.js';
 import { assignedLines } from '../../src/view/pages/pods.js';
 
 const opts = { now: NOW };

@@ -13,20 +13,39 @@ import * as lib from './stubs/headlamp-lib.js';
 import * as CC from './stubs/CommonComponents.js';
 import { createPlugin } from '../../src/plugin.js';
 import { resetSharedStores } from '../../src/api/clusterStore.js';
-import { DEVICE_CONFIG_LIST_PATH } from '../../src/api/amdgpu.js';
+import { DEVICE_CONFIG_LIST_PATH } from '../../src/api/k8sCore.js';
+import { clearViewMemo } from '../../src/view/pages/common.js';
+import { devicePluginsView } from '../../src/view/pages/devicePlugins.js';
+import { ALL_NODES_SERIES, metricsView } from '../../src/view/pages/metricsPage.js';
+import { nodesView, telemetryScope } from '../../src/view/pages/nodes.js';
+import { OVERVIEW_PLUGIN_PODS, overviewView } from '../../src/view/pages/overview.js';
 import {
-  ALL_NODES_SERIES, RANKED_NODE_SORTS, NODE_SORTS, NODES_PER_PAGE, OVERVIEW_PLUGIN_PODS, PODS_PER_PAGE,
-  clearViewMemo, devicePluginsView, metricsView, nodePage, nodeSortOf, nodesView, overviewView, ownersScope, podPage,
-  podSortOf, podsView, POD_SORTS, RANKED_POD_SORTS, telemetryScope,
-} from '../../src/view/pages.js';
+  NODE_SORTS,
+  nodePage,
+  NODES_PER_PAGE,
+  nodeSortOf,
+  POD_SORTS,
+  podPage,
+  PODS_PER_PAGE,
+  podSortOf,
+  RANKED_NODE_SORTS,
+  RANKED_POD_SORTS,
+} from '../../src/view/pages/paging.js';
+import { ownersScope, podsView } from '../../src/view/pages/pods.js';
 import { renderText } from '../../src/view/text.js';
 import { countRows, findSection, pagerOf, pagerText, rowValue, sectionTitles } from '../../src/view/ir.js';
 import { rankedSlice } from '../../src/view/pages/paging.js';
 import { renderPage } from '../../src/view/html.js';
+import { createMetricsSource } from '../../src/api/metrics.js';
 import {
-  SERIES, TOTAL_SERIES, createMetricsSource, powerRankQuery, hostnameMatcher, regexLiteral, scopedSeriesQuery,
-  summarizeMetrics, summaryQuery, totalsFromRows, joinExporterResults, splitByName,
-} from '../../src/api/metrics.js';
+  hostnameMatcher,
+  powerRankQuery,
+  regexLiteral,
+  scopedSeriesQuery,
+  summaryQuery,
+} from '../../src/api/promql.js';
+import { SERIES, TOTAL_SERIES } from '../../src/api/series.js';
+import { joinExporterResults, splitByName, summarizeMetrics, totalsFromRows } from '../../src/api/telemetry.js';
 import { makeContext, makeDeviceConfig, makeGpuNode, makeGpuPod, makePluginPod } from './fixtures.js';
 import { BASE0, exporterData, flatten, prom } from './promFake.js';
 

@@ -21,11 +21,12 @@ import { AmdGpuDataProvider, useAmdGpuContext } from '../../src/api/AmdGpuDataCo
 import { Page, Section } from '../../src/components/View.tsx';
 import { PLUGIN_NAME, createPlugin, registerPlugin } from '../../src/plugin.js';
 import { resetSharedStores } from '../../src/api/clusterStore.js';
-import { clearViewMemo } from '../../src/view/pages.js';
-import { DEVICE_CONFIG_LIST_PATH, PLUGIN_POD_QUERIES, isAmdGpuPluginPod } from '../../src/api/amdgpu.js';
+import { clearViewMemo } from '../../src/view/pages/common.js';
+import { isAmdGpuPluginPod } from '../../src/api/amdPods.js';
+import { DEVICE_CONFIG_LIST_PATH, PLUGIN_POD_QUERIES } from '../../src/api/k8sCore.js';
 import { makeDeviceConfig, makeGpuNode, makeGpuPod, makeNode, makePlainPod, makePluginPod } from './fixtures.js';
 import { exporterData, prom } from './promFake.js';
-import { SERIES } from '../../src/api/metrics.js';
+import { SERIES } from '../../src/api/series.js';
 
 const h = React.createElement;
 
@@ -299,7 +300,51 @@ describe('detail sections', () => {
     cluster();
     const r = render(h('div', null, h(route('/amd-gpu/nodes')), nodeSection(makeGpuNode('mi355x-0'))));
     await r.settle();
-    expect(lib.api.calls.filter((p) => p === DEVICE_CONFIG_LIST_PATH)).toHaveLength(1);
+    // GPU Nodes draws no DeviceConfig, and the section next to it reads the store.
+    expect(lib.api.calls.filter((p) => p === DEVICE_CONFIG_LIST_PATH)).toHaveLength(0);
+    expect(r.html()).toContain('train-a');
+  });
+
+  it.each(['/amd-gpu', '/amd-gpu/nodes', '/amd-gpu/pods', '/amd-gpu/metrics', '/amd-gpu/device-plugins'])(
+    'Node detail after %s unmounted mounts no cluster-wide watch and no DeviceConfig request', async (path) => {
+      cluster();
+      const page = render(h(route(path)));
+      await page.settle();
+      page.unmount();
+      lib.lists.calls.Node.length = 0;
+      lib.lists.calls.Pod.length = 0;
+      const before = lib.api.calls.length;
+      const r = render(nodeSection(makeGpuNode('mi355x-1')));
+      await r.settle();
+      expect(lib.lists.calls.Node).toHaveLength(0);
+      expect(lib.lists.calls.Pod.length).toBeGreaterThan(0);
+      lib.lists.calls.Pod.forEach((o) => expect(o && o.fieldSelector).toBe('spec.nodeName=mi355x-1'));
+      expect(lib.api.calls.slice(before).filter((p) => p === DEVICE_CONFIG_LIST_PATH)).toHaveLength(0);
+      expect(r.html()).toContain('train-b');
+      expect(r.html()).not.toContain('train-a');
+      r.unmount();
+    });
+
+  it('Node detail next to a mounted page reads the store; when the page unmounts it moves to its node-scoped watch', async () => {
+    cluster();
+    const page = render(h(route('/amd-gpu/nodes')));
+    await page.settle();
+    lib.lists.calls.Node.length = 0;
+    lib.lists.calls.Pod.length = 0;
+    const r = render(nodeSection(makeGpuNode('mi355x-0')));
+    await r.settle();
+    expect(lib.lists.calls.Pod.filter((o) => o && o.fieldSelector)).toHaveLength(0); // the store, no list of its own
+    page.unmount();
+    await r.settle();
+    lib.lists.calls.Node.length = 0;
+    lib.lists.calls.Pod.length = 0;
+    r.rerender(nodeSection(makeGpuNode('mi355x-0')));
+    await r.settle();
+    expect(lib.lists.calls.Node).toHaveLength(0);
+    lib.lists.calls.Pod.forEach((o) => expect(o && o.fieldSelector).toBe('spec.nodeName=mi355x-0'));
+    expect(lib.lists.calls.Pod.length).toBeGreaterThan(0);
+    expect(r.html()).toContain('train-a');
+    r.unmount();
   });
 
   it('Pod detail: GPU pod renders without a provider or a cluster request', async () => {

@@ -5,7 +5,7 @@
  * hostname-scoped), the pod-owner query and `query_range`, from exporter
  * rows built by `exporterData`.
  */
-import { PROMETHEUS_SERVICES, SERIES, servicePath } from '../../src/api/metrics.js';
+import { PROMETHEUS_SERVICES, SERIES, servicePath } from '../../src/api/series.js';
 
 export const BASE0 = servicePath(PROMETHEUS_SERVICES[0]);
 export const BASE1 = servicePath(PROMETHEUS_SERVICES[1]);

@@ -3,11 +3,21 @@
  * model and the structural-sharing helpers against independent oracles
  * over a few hundred generated nodes / pods / snapshots each.
  */
-import { buildClusterIndex, formatBytes, getPodGpuDemand } from '../../src/api/amdgpu.js';
-import { shareGpus, shareMap } from '../../src/api/metrics.js';
+import { getPodGpuDemand } from '../../src/api/amdPods.js';
+import { buildClusterIndex } from '../../src/api/clusterIndex.js';
+import { formatBytes } from '../../src/api/k8sCore.js';
+import { shareGpus, shareMap } from '../../src/api/telemetry.js';
 import { buildXgmiMatrix, isFullMesh } from '../../src/api/topology.js';
 import { makeGpuNode } from './fixtures.js';
 import { int, mutate, pick, rng } from './fuzzlib.js';
+
+/** Every page view-model module, merged (what the fuzz cases call by name). */
+async function loadPages() {
+  const mods = ['common', 'details', 'devicePlugins', 'metricsPage', 'nodes', 'overview', 'paging', 'pods'];
+  const out = {};
+  for (let i = 0; i < mods.length; i++) Object.assign(out, await import('../../src/view/pages/' + mods[i] + '.js'));
+  return out;
+}
 
 const RES = ['amd.com/gpu', 'amd.com/cpx_nps4'];
 
@@ -160,7 +170,7 @@ describe('properties', () => {
 
 describe('malformed cluster objects (what a real apiserver, an old CRD version or a half-written object can hand over)', () => {
   it('no page, detail section, column or index throws on them', async () => {
-    const pages = await import('../../src/view/pages.js');
+    const pages = await loadPages();
     const html = await import('../../src/view/html.js');
     const text = await import('../../src/view/text.js');
     const { createClusterStore } = await import('../../src/api/clusterStore.js');
@@ -203,8 +213,8 @@ describe('malformed cluster objects (what a real apiserver, an old CRD version o
 
 describe('malformed Prometheus answers', () => {
   it('joins and telemetry views never throw on wrong-shaped rows', async () => {
-    const pages = await import('../../src/view/pages.js');
-    const { joinExporterResults, joinNodeExporterResults, splitByName, summarizeMetrics, clusterPowerStats } = await import('../../src/api/metrics.js');
+    const pages = await loadPages();
+    const { joinExporterResults, joinNodeExporterResults, splitByName, summarizeMetrics, clusterPowerStats } = await import('../../src/api/telemetry.js');
     const { exporterData, flatten } = await import('./promFake.js');
     const { makeContext, makeGpuNode, makeGpuPod } = await import('./fixtures.js');
     const r = rng(77);
@@ -238,7 +248,7 @@ describe('malformed Prometheus answers', () => {
   });
 
   it('ranked and size-guarded answers with hostile rows never throw, in the client or the Metrics view', async () => {
-    const pages = await import('../../src/view/pages.js');
+    const pages = await loadPages();
     const { createMetricsSource } = await import('../../src/api/metrics.js');
     const { exporterData, flatten, ok } = await import('./promFake.js');
     const { makeContext, makeGpuNode } = await import('./fixtures.js');

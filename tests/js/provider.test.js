@@ -11,7 +11,7 @@ import React, { render } from './stubs/react.js';
 import * as lib from './stubs/headlamp-lib.js';
 import { PROMETHEUS_FORBIDDEN, PROMETHEUS_UNREACHABLE, STALE_MS, createProviderCore, listResult } from '../../src/api/providerCore.js';
 import { resetSharedStores } from '../../src/api/clusterStore.js';
-import { DEVICE_CONFIG_LIST_PATH, PLUGIN_POD_QUERIES } from '../../src/api/amdgpu.js';
+import { DEVICE_CONFIG_LIST_PATH, PLUGIN_POD_QUERIES } from '../../src/api/k8sCore.js';
 import { DEFAULT_SETTINGS } from '../../src/api/settings.js';
 import { makeDeviceConfig, makeGpuPod } from './fixtures.js';
 
@@ -156,8 +156,9 @@ describe('useNodePods (cold Node detail) — a scoped list + watch', () => {
     let renders = 0;
     function S() {
       renders++;
-      const res = c.useNodePods('n1');
-      return h('div', null, res.loading ? 'loading' : res.podsState + ':' + res.gpuPods.map((p) => p.metadata.name).join(','));
+      const np = c.useNodePods('n1');
+      const res = np[0];
+      return h('div', null, np[1], res.loading ? 'loading' : res.podsState + ':' + res.gpuPods.map((p) => p.metadata.name).join(','));
     }
     lib.lists.Pod = [[makeGpuPod('a', { node: 'n1' }), makeGpuPod('b', { node: 'n2' })], null];
     const r = render(h(S));

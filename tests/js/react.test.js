@@ -11,7 +11,9 @@ import React, { render } from './stubs/react.js';
 import * as CC from './stubs/CommonComponents.js';
 import { createRenderer, REQUIRED_COMPONENTS, buttonStyle, matrixCaption, matrixCellColor, sparklinePath } from '../../src/view/react.js';
 import { bar, kv, lines, loader, page, pctbar, row, section, status, table } from '../../src/view/ir.js';
-import { clearViewMemo, matrixBlock, overviewView, slotsBlock } from '../../src/view/pages.js';
+import { clearViewMemo } from '../../src/view/pages/common.js';
+import { matrixBlock, slotsBlock } from '../../src/view/pages/nodes.js';
+import { overviewView } from '../../src/view/pages/overview.js';
 import { makeContext, makeGpuNode, makeGpuPod } from './fixtures.js';
 
 const h = React.createElement;

@@ -18,7 +18,7 @@ import {
   saveSettings,
   seriesStepSec,
 } from '../../src/api/settings.js';
-import { PROMETHEUS_SERVICES } from '../../src/api/metrics.js';
+import { PROMETHEUS_SERVICES } from '../../src/api/series.js';
 
 function memStorage() {
   const m = new Map();

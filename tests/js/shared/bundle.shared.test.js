@@ -13,9 +13,9 @@ import { React, render, tier } from 'amd-test-harness';
 import * as lib from '@kinvolk/headlamp-plugin/lib';
 import * as CC from '@kinvolk/headlamp-plugin/lib/CommonComponents';
 import { bundle } from '../../../tools/bundle.js';
-import { DEVICE_CONFIG_LIST_PATH } from '../../../src/api/amdgpu.js';
+import { DEVICE_CONFIG_LIST_PATH } from '../../../src/api/k8sCore.js';
 import { resetSharedStores } from '../../../src/api/clusterStore.js';
-import { clearViewMemo } from '../../../src/view/pages.js';
+import { clearViewMemo } from '../../../src/view/pages/common.js';
 import { makeDeviceConfig, makeGpuNode, makeGpuPod, makeNode, makePlainPod, makePluginPod } from '../fixtures.js';
 
 const ROOT = path.resolve(path.dirname(fileURLToPath(import.meta.url)), '..', '..', '..');

@@ -11,7 +11,17 @@
 import { React, render, tier } from 'amd-test-harness';
 import * as CC from '@kinvolk/headlamp-plugin/lib/CommonComponents';
 import { createRenderer } from '../../../src/view/react.js';
-import * as pages from '../../../src/view/pages.js';
+import { clearViewMemo } from '../../../src/view/pages/common.js';
+import { nodeColumns, nodeDetailView, podDetailView } from '../../../src/view/pages/details.js';
+import { devicePluginsView } from '../../../src/view/pages/devicePlugins.js';
+import { metricsView } from '../../../src/view/pages/metricsPage.js';
+import { nodesView } from '../../../src/view/pages/nodes.js';
+import { overviewView } from '../../../src/view/pages/overview.js';
+import { podsView } from '../../../src/view/pages/pods.js';
+
+const pages = {
+  clearViewMemo, devicePluginsView, metricsView, nodeColumns, nodeDetailView, nodesView, overviewView, podDetailView, podsView,
+};
 import { createClusterStore } from '../../../src/api/clusterStore.js';
 import { createMetricsSource } from '../../../src/api/metrics.js';
 import { makeContext, makeDeviceConfig, makeGpuNode, makeGpuPod, makeNode, makePlainPod, makePluginPod } from '../fixtures.js';

@@ -22,9 +22,10 @@ import { React, render, tier } from 'amd-test-harness';
 import * as lib from '@kinvolk/headlamp-plugin/lib';
 import '../../../src/index.tsx';
 import { resetSharedStores } from '../../../src/api/clusterStore.js';
-import { clearViewMemo } from '../../../src/view/pages.js';
+import { clearViewMemo } from '../../../src/view/pages/common.js';
 import { DEFAULT_SETTINGS, invalidateSettings, saveSettings } from '../../../src/api/settings.js';
-import { DEVICE_CONFIG_LIST_PATH, PLUGIN_POD_QUERIES, isAmdGpuPluginPod } from '../../../src/api/amdgpu.js';
+import { isAmdGpuPluginPod } from '../../../src/api/amdPods.js';
+import { DEVICE_CONFIG_LIST_PATH, PLUGIN_POD_QUERIES } from '../../../src/api/k8sCore.js';
 import { makeDeviceConfig, makeGpuNode, makeGpuPod, makeNode, makePlainPod, makePluginPod } from '../fixtures.js';
 import { exporterData, prom } from '../promFake.js';
 

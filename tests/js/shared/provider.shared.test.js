@@ -12,7 +12,7 @@ import { React, render, tier } from 'amd-test-harness';
 import * as lib from '@kinvolk/headlamp-plugin/lib';
 import { OUTSIDE_PROVIDER, PROMETHEUS_UNREACHABLE, createProviderCore } from '../../../src/api/providerCore.js';
 import { resetSharedStores } from '../../../src/api/clusterStore.js';
-import { DEVICE_CONFIG_LIST_PATH, PLUGIN_POD_QUERIES } from '../../../src/api/amdgpu.js';
+import { DEVICE_CONFIG_LIST_PATH, PLUGIN_POD_QUERIES } from '../../../src/api/k8sCore.js';
 import { DEFAULT_SETTINGS } from '../../../src/api/settings.js';
 import { makeDeviceConfig, makeGpuNode, makeGpuPod, makeNode, makePlainPod, makePluginPod } from '../fixtures.js';
 import { BASE0, exporterData, prom } from '../promFake.js';
@@ -434,9 +434,20 @@ describe('shared: metrics hooks (' + tier + ')', () => {
 describe('shared: useNodePods, the cold Node detail read (' + tier + ')', () => {
   function Section(c, node) {
     return function S() {
-      const r = c.useNodePods(node);
-      return h('div', null, r.loading ? 'loading' : r.podsState + ':' + r.gpuPods.map((p) => p.metadata.name).join(','));
+      const np = c.useNodePods(node);
+      const r = np[0];
+      return h('div', null, np[1], r.loading ? 'loading' : r.podsState + ':' + r.gpuPods.map((p) => p.metadata.name).join(','));
     };
+  }
+
+  /** The scoped request of one node's pods, answered from lib.lists.Pod as an apiserver would. */
+  function nodePodsServer() {
+    return vi.fn((path) => {
+      const m = /^\/api\/v1\/pods\?fieldSelector=(.*)$/.exec(path);
+      if (!m) return notFound();
+      const node = decodeURIComponent(m[1]).replace(/^spec\.nodeName=/, '');
+      return Promise.resolve(kubeList((lib.lists.Pod[0] || []).filter((p) => p.spec && p.spec.nodeName === node)));
+    });
   }
 
   it('one list + watch scoped to the node (the host hook), GPU pods of that node only, no request of its own', async () => {
@@ -460,6 +471,84 @@ describe('shared: useNodePods, the cold Node detail read (' + tier + ')', () => 
     r.rerender(h(S));
     await r.settle();
     expect(r.text()).toBe('error:');
+    r.unmount();
+  });
+
+  it('the store\'s last pod list (no feed mounted) seeds the first paint; the node\'s own list then replaces it', async () => {
+    const c = core(vi.fn(() => notFound()));
+    const store = c.storeFor(c.clusterKey());
+    store.setPods([makeGpuPod('old', { node: 'n1' }), makeGpuPod('x', { node: 'n2' })], null);
+    lib.lists.Pod = [null, null];
+    const S = Section(c, 'n1');
+    const r = render(h(S));
+    expect(r.text()).toBe('ready:old');
+    lib.lists.Pod = [[makeGpuPod('new', { node: 'n1' })], null];
+    r.rerender(h(S));
+    await r.settle();
+    expect(r.text()).toBe('ready:new');
+    r.unmount();
+  });
+
+  it('a host that ignores the field selector: counted, the watch unmounted, the field-selected request read instead', async () => {
+    const request = nodePodsServer();
+    const c = core(request);
+    lib.lists.ignoreOptions = true;
+    lib.lists.Pod = [[makeGpuPod('a', { node: 'n1' }), makeGpuPod('b', { node: 'n2' }), makePlainPod('web', { node: 'n2' })], null];
+    const S = Section(c, 'n1');
+    const r = render(h(S));
+    await r.settle();
+    expect(r.text()).toBe('ready:a');
+    expect(c.storeFor(c.clusterKey()).counters().selectorIgnored).toEqual({ nodePods: 2, operatorPods: 0 });
+    expect(request.mock.calls.map((x) => x[0])).toEqual(['/api/v1/pods?fieldSelector=' + encodeURIComponent('spec.nodeName=n1')]);
+    // No list hook is mounted any more: a re-render calls none.
+    lib.lists.calls.Pod.length = 0;
+    r.rerender(h(S));
+    await r.settle();
+    expect(lib.lists.calls.Pod).toHaveLength(0);
+    expect(r.text()).toBe('ready:a');
+    // A later section on this cluster reads the request from the start.
+    r.unmount();
+    const r2 = render(h(Section(c, 'n2')));
+    await r2.settle();
+    expect(lib.lists.calls.Pod).toHaveLength(0);
+    expect(r2.text()).toBe('ready:b');
+    r2.unmount();
+  });
+});
+
+describe('shared: the operator pods on a host that ignores list options (' + tier + ')', () => {
+  const OPS = { nodes: false, pods: false, crd: true, operatorPods: true };
+
+  it('the operator pod feed is swapped for the plugin-pod requests: same pods, no unscoped list left mounted', async () => {
+    const dp = makePluginPod('amdgpu-dp-0');
+    const all = [dp, makePlainPod('web-0'), makeGpuPod('train-a')];
+    lib.lists.ignoreOptions = true;
+    lib.lists.Pod = [all, null];
+    const request = apiServer({ pluginPods: [dp] });
+    const c = core(request);
+    const p = probe(c);
+    const r = render(h(c.AmdGpuDataProvider, { needs: OPS }, h(p.Probe)));
+    await r.settle();
+    const counters = c.storeFor(c.clusterKey()).counters();
+    expect(counters.selectorIgnored.operatorPods).toBeGreaterThan(0);
+    expect(p.last().pluginPods.map((x) => x.metadata.name)).toEqual(['amdgpu-dp-0']);
+    expect(request.mock.calls.filter((x) => PLUGIN_POD_QUERIES.indexOf(x[0]) >= 0).length).toBe(PLUGIN_POD_QUERIES.length);
+    lib.lists.calls.Pod.length = 0;
+    r.rerender(h(c.AmdGpuDataProvider, { needs: OPS }, h(p.Probe)));
+    await r.settle();
+    expect(lib.lists.calls.Pod).toHaveLength(0);
+    expect(p.last().pluginPods.map((x) => x.metadata.name)).toEqual(['amdgpu-dp-0']);
+    r.unmount();
+  });
+
+  it('a host that applies the options is not flagged', async () => {
+    lib.lists.Pod = [[makePluginPod('amdgpu-dp-0'), makePlainPod('web-0')], null];
+    const c = core(apiServer());
+    const p = probe(c);
+    const r = render(h(c.AmdGpuDataProvider, { needs: OPS }, h(p.Probe)));
+    await r.settle();
+    expect(c.storeFor(c.clusterKey()).counters().selectorIgnored).toBeNull();
+    expect(lib.lists.calls.Pod.length).toBeGreaterThan(0);
     r.unmount();
   });
 });

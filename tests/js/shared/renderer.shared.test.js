@@ -13,7 +13,10 @@ import { React, render, tier } from 'amd-test-harness';
 import * as CC from '@kinvolk/headlamp-plugin/lib/CommonComponents';
 import { createRenderer, sparklinePath } from '../../../src/view/react.js';
 import { bar, kv, lines, loader, page, pager, pctbar, row, section, status, table } from '../../../src/view/ir.js';
-import { clearViewMemo, matrixBlock, nodePage, overviewView, slotsBlock } from '../../../src/view/pages.js';
+import { clearViewMemo } from '../../../src/view/pages/common.js';
+import { matrixBlock, slotsBlock } from '../../../src/view/pages/nodes.js';
+import { overviewView } from '../../../src/view/pages/overview.js';
+import { nodePage } from '../../../src/view/pages/paging.js';
 import { makeContext, makeGpuNode, makeGpuPod } from '../fixtures.js';
 
 const h = React.createElement;

@@ -10,8 +10,8 @@ import * as CC from '@kinvolk/headlamp-plugin/lib/CommonComponents';
 import '../../../src/index.tsx';
 import { createPlugin } from '../../../src/plugin.js';
 import { resetSharedStores } from '../../../src/api/clusterStore.js';
-import { clearViewMemo } from '../../../src/view/pages.js';
-import { DEVICE_CONFIG_LIST_PATH } from '../../../src/api/amdgpu.js';
+import { clearViewMemo } from '../../../src/view/pages/common.js';
+import { DEVICE_CONFIG_LIST_PATH } from '../../../src/api/k8sCore.js';
 import { makeDeviceConfig, makeGpuNode, makeGpuPod } from '../fixtures.js';
 import { exporterData, prom } from '../promFake.js';
 

@@ -11,7 +11,7 @@ import * as lib from '@kinvolk/headlamp-plugin/lib';
 import * as CC from '@kinvolk/headlamp-plugin/lib/CommonComponents';
 import { createPlugin } from '../../../src/plugin.js';
 import { resetSharedStores } from '../../../src/api/clusterStore.js';
-import { clearViewMemo } from '../../../src/view/pages.js';
+import { clearViewMemo } from '../../../src/view/pages/common.js';
 import { makeGpuNode } from '../fixtures.js';
 
 const h = React.createElement;

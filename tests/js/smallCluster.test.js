@@ -9,10 +9,14 @@ import * as lib from './stubs/headlamp-lib.js';
 import * as CC from './stubs/CommonComponents.js';
 import { createPlugin } from '../../src/plugin.js';
 import { resetSharedStores } from '../../src/api/clusterStore.js';
-import { DEVICE_CONFIG_LIST_PATH } from '../../src/api/amdgpu.js';
-import { NODES_PER_PAGE, PODS_PER_PAGE, clearViewMemo, metricsView, ownersScope } from '../../src/view/pages.js';
+import { DEVICE_CONFIG_LIST_PATH } from '../../src/api/k8sCore.js';
+import { clearViewMemo } from '../../src/view/pages/common.js';
+import { metricsView } from '../../src/view/pages/metricsPage.js';
+import { NODES_PER_PAGE, PODS_PER_PAGE } from '../../src/view/pages/paging.js';
+import { ownersScope } from '../../src/view/pages/pods.js';
 import { sectionTitles } from '../../src/view/ir.js';
-import { SERIES, SMALL_CLUSTER_NODES, SMALL_CLUSTER_PODS, createMetricsSource } from '../../src/api/metrics.js';
+import { createMetricsSource } from '../../src/api/metrics.js';
+import { SERIES, SMALL_CLUSTER_NODES, SMALL_CLUSTER_PODS } from '../../src/api/series.js';
 import { makeContext, makeDeviceConfig, makeGpuNode, makeGpuPod } from './fixtures.js';
 import { exporterData, prom } from './promFake.js';
 

@@ -14,8 +14,9 @@ import * as lib from './stubs/headlamp-lib.js';
 import * as CC from './stubs/CommonComponents.js';
 import { createPlugin } from '../../src/plugin.js';
 import { resetSharedStores } from '../../src/api/clusterStore.js';
-import { DEVICE_CONFIG_LIST_PATH } from '../../src/api/amdgpu.js';
-import { NODE_SORTS, clearViewMemo, nodePage } from '../../src/view/pages.js';
+import { DEVICE_CONFIG_LIST_PATH } from '../../src/api/k8sCore.js';
+import { clearViewMemo } from '../../src/view/pages/common.js';
+import { NODE_SORTS, nodePage } from '../../src/view/pages/paging.js';
 import { makeContext, makeGpuNode, makeGpuPod } from './fixtures.js';
 import { exporterData, prom } from './promFake.js';
 

@@ -10,9 +10,14 @@
  */
 import fs from 'fs';
 import path from 'path';
-import { createMetricsSource, splitByName } from '../../src/api/metrics.js';
-import { MI355X } from '../../src/api/amdgpu.js';
-import { metricsView, nodeDetailView, nodesView, podsView, clearViewMemo } from '../../src/view/pages.js';
+import { createMetricsSource } from '../../src/api/metrics.js';
+import { splitByName } from '../../src/api/telemetry.js';
+import { MI355X } from '../../src/api/k8sCore.js';
+import { clearViewMemo } from '../../src/view/pages/common.js';
+import { nodeDetailView } from '../../src/view/pages/details.js';
+import { metricsView } from '../../src/view/pages/metricsPage.js';
+import { nodesView } from '../../src/view/pages/nodes.js';
+import { podsView } from '../../src/view/pages/pods.js';
 import { findSection, firstBlock, firstTable, rowValue, sections } from '../../src/view/ir.js';
 import { renderPage } from '../../src/view/html.js';
 import { renderText } from '../../src/view/text.js';

@@ -13,6 +13,9 @@ export const lists = {
   Pod: [null, null],
   calls: { Node: [], Pod: [] },
   selected: {},
+  // A host whose useList() drops its options (an older Headlamp): every list
+  // holds every object, whatever namespace / selector was asked for.
+  ignoreOptions: false,
 };
 
 export const api = {
@@ -31,6 +34,7 @@ export function resetHeadlamp() {
   lists.calls.Node.length = 0;
   lists.calls.Pod.length = 0;
   lists.selected = {};
+  lists.ignoreOptions = false;
   api.calls.length = 0;
   api.handler = function () { return Promise.reject(Object.assign(new Error('no handler'), { status: 404 })); };
 }
@@ -117,7 +121,7 @@ function resourceClass(kind) {
       lists.calls[kind].push(opts === undefined ? null : opts);
       // A namespaced or selected list holds what the apiserver would return
       // for it (identity kept while the underlying list is unchanged).
-      const pred = selection(opts);
+      const pred = lists.ignoreOptions ? null : selection(opts);
       const res = lists[kind];
       if (pred === null || !res || !Array.isArray(res[0])) return res;
       const sig = JSON.stringify(opts);

@@ -2,7 +2,8 @@
  * Terminal renderer (src/view/text.js) — the third renderer of the view IR.
  */
 import { renderText, sparkline, textSection, textValue } from '../../src/view/text.js';
-import { nodesView, podDetailView } from '../../src/view/pages.js';
+import { podDetailView } from '../../src/view/pages/details.js';
+import { nodesView } from '../../src/view/pages/nodes.js';
 import { bar, kv, lines, row, section, status, table } from '../../src/view/ir.js';
 import { NOW, makeContext, makeGpuNode, makeGpuPod } from './fixtures.js';
 

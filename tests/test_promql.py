@@ -280,7 +280,7 @@ def test_summary_query_of_the_metrics_page():
 
     from headlamp_intel_gpu_plugin_amd.utils.nodebridge import ROOT, node_binary
 
-    q = subprocess.run([node_binary(), "-e", "import('./src/api/metrics.js').then(m => process.stdout.write(m.summaryQuery()))"],
+    q = subprocess.run([node_binary(), "-e", "Promise.all([import('./src/api/promql.js'), import('./src/api/series.js')]).then(ms => Object.assign({}, ...ms)).then(m => process.stdout.write(m.summaryQuery()))"],
                        cwd=ROOT, capture_output=True, text=True, timeout=60).stdout
     d = TSDB()
     for node in ("a", "b", "c"):
@@ -304,7 +304,7 @@ def test_size_guarded_small_cluster_query():
 
     from headlamp_intel_gpu_plugin_amd.utils.nodebridge import ROOT, node_binary
 
-    js = ("import('./src/api/metrics.js').then(m => process.stdout.write(JSON.stringify("
+    js = ("Promise.all([import('./src/api/promql.js'), import('./src/api/series.js')]).then(ms => Object.assign({}, ...ms)).then(m => process.stdout.write(JSON.stringify("
           "[m.smallClusterQuery(true, 'topology', ['b']), m.SMALL_CLUSTER_NODES])))")
     q, limit = json.loads(subprocess.run([node_binary(), "-e", js], cwd=ROOT, capture_output=True, text=True,
                                          timeout=60).stdout)
@@ -351,7 +351,7 @@ def test_topk_bottomk_and_the_power_ranked_page():
     low = _vec(query(d, "bottomk by (hostname) (1, gpu_power_usage)", 100.0))
     assert len(low) == 5 and all(r["metric"]["__name__"] == "gpu_power_usage" for r in low)
 
-    js = ("import('./src/api/metrics.js').then(m => process.stdout.write("
+    js = ("Promise.all([import('./src/api/promql.js'), import('./src/api/series.js')]).then(ms => Object.assign({}, ...ms)).then(m => process.stdout.write("
           "m.rankedClusterQuery('gauges', {page: 1, per: 2, filter: ''})))")
     q = subprocess.run([node_binary(), "-e", js], cwd=ROOT, capture_output=True, text=True, timeout=60).stdout
     rows = _vec(query(d, q, 100.0))
@@ -380,7 +380,7 @@ def test_the_pod_power_ranked_page():
     d.add(Series({"__name__": "gpu_power_usage", "hostname": "n1", "gpu_id": "7"}, fn=lambda t: 90.0))  # idle GPU
 
     def ranked(page, per, flt):
-        js = ("import('./src/api/metrics.js').then(m => process.stdout.write(m.rankedOwnersQuery("
+        js = ("Promise.all([import('./src/api/promql.js'), import('./src/api/series.js')]).then(ms => Object.assign({}, ...ms)).then(m => process.stdout.write(m.rankedOwnersQuery("
               "{by: 'power', page: %d, per: %d, filter: %s})))" % (page, per, json.dumps(flt)))
         q = subprocess.run([node_binary(), "-e", js], cwd=ROOT, capture_output=True, text=True, timeout=60).stdout
         rows = _vec(query(d, q, 100.0))
@@ -411,7 +411,7 @@ def _js(expr):
 
     from headlamp_intel_gpu_plugin_amd.utils.nodebridge import ROOT, node_binary
 
-    js = "import('./src/api/metrics.js').then(m => process.stdout.write(JSON.stringify(%s)))" % expr
+    js = "Promise.all([import('./src/api/promql.js'), import('./src/api/series.js')]).then(ms => Object.assign({}, ...ms)).then(m => process.stdout.write(JSON.stringify(%s)))" % expr
     r = subprocess.run([node_binary(), "-e", js], cwd=ROOT, capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stderr
     return json.loads(r.stdout)

@@ -3,7 +3,7 @@
     python tools/screenshots.py [--nodes 2] [--out docs/screenshots]
 
 The reference ships hand-drawn SVG mock-ups (docs/screenshots/*.svg); these
-are the real view-models (src/view/pages.js) of a fake 2-node cluster
+are the real view-models (src/view/pages/*.js) of a fake 2-node cluster
 rendered through src/view/html.js — the same path the benchmark counts rows
 on — so they stay in sync with the code.
 """
