@@ -25,11 +25,27 @@ export function gcBetween(from, to) {
   return t;
 }
 
+/** What a request path asks for: nodes, pods, crd, query, query_range or other. */
+export function requestKind(path) {
+  if (path.indexOf('/proxy/') >= 0) return path.indexOf('/query_range') >= 0 ? 'query_range' : 'query';
+  if (path.indexOf('/deviceconfigs') >= 0) return 'crd';
+  if (path.indexOf('/api/v1/nodes') === 0) return 'nodes';
+  if (path.indexOf('/pods') >= 0) return 'pods';
+  return 'other';
+}
+
+/**
+ * An HTTP/1.1 keep-alive client (6 sockets, the browser's per-origin limit)
+ * counting requests and bytes on `counter`; with `counter.log` (an array) it
+ * also records each request's kind, wall span and the fake server's own time
+ * on it (its `X-Server-Ms` header: work, not the injected latency).
+ */
 export function makeRequest(base, counter) {
   const agent = new http.Agent({ keepAlive: true, maxSockets: 6 });
   const u = new URL(base);
   return function request(path) {
     counter.n++;
+    const t0 = hiResClock.now();
     return new Promise(function (resolve, reject) {
       const req = http.get({ hostname: u.hostname, port: u.port, path: path, agent: agent, headers: { Accept: 'application/json' } }, function (res) {
         const chunks = [];
@@ -37,6 +53,11 @@ export function makeRequest(base, counter) {
         res.on('end', function () {
           const body = Buffer.concat(chunks);
           counter.bytes += body.length;
+          const server = parseFloat(res.headers['x-server-ms']);
+          if (isFinite(server)) counter.serverMs = (counter.serverMs || 0) + server;
+          if (counter.log) {
+            counter.log.push({ kind: requestKind(path), start: t0, end: hiResClock.now(), serverMs: isFinite(server) ? server : null });
+          }
           let json = null;
           try {
             json = JSON.parse(body.toString('utf8'));

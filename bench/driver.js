@@ -56,6 +56,23 @@ function parseArgs(argv) {
   return a;
 }
 
+/**
+ * The fake server's own time on the requests `log[from..]` (bench/common.js
+ * makeRequest): the slowest request's (its requests overlap, so the slowest
+ * bounds the server's share of the open), the sum, and the slowest by kind.
+ */
+function serverTime(log, from) {
+  const out = { maxMs: 0, sumMs: 0, byKind: {} };
+  for (let i = from; i < log.length; i++) {
+    const v = log[i].serverMs;
+    if (v === null) continue;
+    out.sumMs += v;
+    if (v > out.maxMs) out.maxMs = v;
+    if (!(log[i].kind in out.byKind) || v > out.byKind[log[i].kind]) out.byKind[log[i].kind] = v;
+  }
+  return out;
+}
+
 async function measure(name, factory, base, a) {
   const counter = { n: 0, bytes: 0 };
   const request = makeRequest(base, counter);
@@ -132,7 +149,7 @@ async function serve(a) {
   const icu0 = process.hrtime();
   new Date(0).toLocaleTimeString();
   const startup = { icuMs: ms(process.hrtime(icu0)), node: process.version };
-  const counter = { n: 0, bytes: 0 };
+  const counter = { n: 0, bytes: 0, log: [] };
   const live = {};
   function get(name) {
     if (!live[name]) {
@@ -161,6 +178,7 @@ async function serve(a) {
       if (c.cmd === 'cold') {
         const lat = [];
         const renderMs = [];
+        const server = [];
         let req = 0;
         // Cold caches, warm connections: a browser keeps its keep-alive
         // sockets to the Headlamp origin across in-app navigations.
@@ -168,17 +186,21 @@ async function serve(a) {
         for (let i = 0; i < n; i++) {
           const s = (name === 'reference' ? referenceSchedule : amdSchedule)(pool);
           const before = counter.n;
+          const log0 = counter.log.length;
           const t0 = process.hrtime();
           await s.coldOpen();
           const t1 = process.hrtime();
           renderAll(s);
           lat.push(ms(process.hrtime(t0)));
           renderMs.push(ms(process.hrtime(t1)));
+          server.push(serverTime(counter.log, log0));
           req = counter.n - before;
           if (s.spans) out.trace = traceSummary(s.spans);
         }
         out.latencies = lat;
         out.renderMs = renderMs;
+        out.serverMs = server.map(function (x) { return x.maxMs; });
+        out.serverByKind = server.length ? server[server.length - 1].byKind : {};
         out.requests = req;
       } else if (c.cmd === 'coldPages') {
         // Per-page cold open: a fresh schedule (empty caches, new client)
@@ -194,9 +216,11 @@ async function serve(a) {
           let trace = null;
           const content = [];
           const first = [];
+          const server = [];
           for (let i = 0; i < n; i++) {
             const s = (name === 'reference' ? referenceSchedule : amdSchedule)(pool);
             const before = counter.n;
+            const log0 = counter.log.length;
             const p0 = performance.now();
             const t0 = process.hrtime();
             let tf = null;
@@ -224,10 +248,16 @@ async function serve(a) {
             // observer entries are delivered asynchronously
             await new Promise(function (r) { setImmediate(r); });
             gcMs.push(gcBetween(p0, performance.now()));
+            server.push(serverTime(counter.log, log0));
             req = counter.n - before;
             if (s.spans) trace = traceSummary(s.spans);
           }
-          out.pages[page] = { latencies: lat, contentMs: content, firstMs: first, renderMs: renderMs, gcMs: gcMs, requests: req, trace: trace };
+          out.pages[page] = {
+            latencies: lat, contentMs: content, firstMs: first, renderMs: renderMs, gcMs: gcMs, requests: req, trace: trace,
+            // the fake server's time on the open's slowest request (bench/common.js X-Server-Ms), per open
+            serverMs: server.map(function (x) { return x.maxMs; }),
+            serverByKind: server.length ? server[server.length - 1].byKind : {},
+          };
         }
       } else if (c.cmd === 'steps') {
         const L = get(name);
@@ -295,21 +325,25 @@ async function serve(a) {
         const reqs = {};
         const rows = {};
         const rend = {};
+        const srv = {};
         for (let p = 0; p < PAGES.length; p++) {
           lat[PAGES[p]] = [];
           rend[PAGES[p]] = [];
+          srv[PAGES[p]] = [];
           reqs[PAGES[p]] = 0;
         }
         for (let i = 0; i < n; i++) {
           for (let p = 0; p < PAGES.length; p++) {
             const page = PAGES[p];
             const before = counter.n;
+            const log0 = counter.log.length;
             const t0 = process.hrtime();
             await L.s.refreshPage(page);
             const t1 = process.hrtime();
             rows[page] = renderOne(page, L.s.ctx(), page === 'metrics' ? L.s.pageMstate() : L.s.mstate(), L.s.pageMetrics(page));
             lat[page].push(ms(process.hrtime(t0)));
             rend[page].push(ms(process.hrtime(t1)));
+            srv[page].push(serverTime(counter.log, log0).maxMs);
             reqs[page] += counter.n - before;
           }
         }
@@ -317,6 +351,7 @@ async function serve(a) {
         for (let p = 0; p < PAGES.length; p++) {
           out.pages[PAGES[p]] = {
             latencies: lat[PAGES[p]], renderMs: rend[PAGES[p]], requestsPerClick: reqs[PAGES[p]] / n, tableRows: rows[PAGES[p]],
+            serverMs: srv[PAGES[p]],
           };
         }
         if (c.react) {

@@ -18,12 +18,28 @@ schedule and the reference's replayed schedule are compared on equal terms
 (BASELINE.md "How the comparison will be made"). List bodies are
 serialised once per cluster version and cached, like a watch cache.
 
+Every response carries ``X-Server-Ms``: the time the fake spent on it
+(handler work, including a Prometheus evaluation and its wait for the
+evaluation thread), not the injected latency — so a client figure can be
+split into plugin time and fake-server time.
+
+With ``rules=True`` (the benchmark's control plane) the fake Prometheus
+answers instant queries like one with recording rules: every query it was
+asked is re-evaluated in the background when its inputs change (a scrape
+lands, or the synthetic series' 15 s sample grid ticks), and a request is
+served the latest evaluation at once — at most one evaluation behind, as a
+real Prometheus answer is at most one scrape behind. A real Prometheus
+evaluates these selectors in milliseconds; this Python one needs up to
+seconds at 1,000 nodes, which would otherwise land on whichever client
+request first follows a tick (VERDICT r4 Weak #4).
+
 Runs on its own asyncio loop in a daemon thread (:class:`ServerThread`).
 """
 from __future__ import annotations
 
 import asyncio
 import concurrent.futures
+import heapq
 import random
 import json
 import re
@@ -39,12 +55,18 @@ from . import promql
 
 DEFAULT_PROM_SERVICE = ("monitoring", "kube-prometheus-stack-prometheus", "9090")
 
+#: A recording-rule query nobody asked for this long is dropped (``rules=True``).
+RULE_TTL_S = 300.0
+
 
 # ---------------------------------------------------------------------------
 # Label / field selectors
 # ---------------------------------------------------------------------------
 
 _SET_RE = re.compile(r"^\s*([A-Za-z0-9_./-]+)\s+(in|notin)\s+\(([^)]*)\)\s*$")
+
+
+_NODE_FIELD_RE = re.compile(r"^spec\.nodeName==?([^,!=]+)$")
 
 
 def _split_terms(sel: str) -> List[str]:
@@ -117,8 +139,13 @@ class FakeCluster:
     def __init__(self, cluster: SyntheticCluster, db: Optional[promql.TSDB] = None, *, latency_ms: float = 20.0,
                  crd_installed: bool = True, prometheus_up: Iterable[Tuple[str, str, str]] = (DEFAULT_PROM_SERVICE,),
                  per_kb_us: float = 0.0, now=time.time, fail_rate: float = 0.0, hang_rate: float = 0.0,
-                 seed: int = 0):
+                 seed: int = 0, rules: bool = False):
         self.cluster = cluster
+        # Instant queries as recording rules (module docstring): query → [stamp, body, last asked].
+        self.rules = rules
+        self.answers: Dict[str, list] = {}
+        self.refreshing: set = set()
+        self.rule_evals = 0
         # Fault injection: each request independently fails with a 503 Status
         # (fail_rate) or never answers within the client's 2 s budget
         # (hang_rate, held 3 s) — seeded, so a failing run reproduces.
@@ -173,11 +200,24 @@ class FakeCluster:
         def build():
             lp = parse_label_selector(label_sel)
             fp = parse_field_selector(field_sel)
-            items = [p for p in self.cluster.pods
+            # One node's pods (a Node detail's scoped list) from a per-node index, as the apiserver's watch cache
+            # indexes pods by spec.nodeName: not a pass over every pod of the cluster.
+            m = _NODE_FIELD_RE.match(field_sel or "")
+            pool = self._pods_by_node().get(m.group(1), []) if m else self.cluster.pods
+            items = [p for p in pool
                      if (ns is None or p["metadata"]["namespace"] == ns) and lp(p["metadata"].get("labels", {})) and fp(p)]
             return self._list("PodList", items)
 
         return self._cached(key, build)
+
+    def _pods_by_node(self) -> Dict[str, list]:
+        idx = self._cache.get("__pods_by_node__")
+        if idx is None:
+            idx = {}
+            for p in self.cluster.pods:
+                idx.setdefault(p["spec"].get("nodeName") or "", []).append(p)
+            self._cache["__pods_by_node__"] = idx
+        return idx
 
     def nodes_body(self, label_sel: str) -> bytes:
         def build():
@@ -193,6 +233,48 @@ class FakeCluster:
                                "metadata": {"resourceVersion": str(self.version)}, "items": items}).encode()
 
         return self._cached(f"dc|{ns}", build)
+
+
+class PriorityPool:
+    """One evaluation thread taking work by priority: what a client request waits for (0) before background
+    recording-rule refreshes (1) — so a query nobody asked before, or a range query, never queues behind a pass
+    over every rule at 1,000 nodes."""
+
+    def __init__(self, name: str = "fake-prometheus"):
+        self._heap: list = []
+        self._seq = 0
+        self._cv = threading.Condition()
+        self._stop = False
+        self._thread = threading.Thread(target=self._run, daemon=True, name=name)
+        self._thread.start()
+
+    def submit(self, priority: int, fn, *args) -> concurrent.futures.Future:
+        fut: concurrent.futures.Future = concurrent.futures.Future()
+        with self._cv:
+            self._seq += 1
+            heapq.heappush(self._heap, (priority, self._seq, fn, args, fut))
+            self._cv.notify()
+        return fut
+
+    def _run(self) -> None:
+        while True:
+            with self._cv:
+                while not self._heap and not self._stop:
+                    self._cv.wait()
+                if self._stop:
+                    return
+                _, _, fn, args, fut = heapq.heappop(self._heap)
+            if not fut.set_running_or_notify_cancel():
+                continue
+            try:
+                fut.set_result(fn(*args))
+            except BaseException as e:  # surfaced to the awaiting request
+                fut.set_exception(e)
+
+    def shutdown(self) -> None:
+        with self._cv:
+            self._stop = True
+            self._cv.notify_all()
 
 
 def _status(code: int, reason: str, message: str) -> web.Response:
@@ -217,6 +299,7 @@ def build_app(fc: FakeCluster) -> web.Application:
                                          status=503)
         resp = await handler(request)
         work = time.perf_counter() - t0
+        resp.headers["X-Server-Ms"] = f"{work * 1e3:.3f}"
         delay = fc.latency_ms / 1000.0
         if fc.per_kb_us and getattr(resp, "body", None) is not None:
             delay += len(resp.body) / 1024.0 * fc.per_kb_us / 1e6
@@ -257,13 +340,21 @@ def build_app(fc: FakeCluster) -> web.Application:
         if q is None:
             return web.json_response({"status": "error", "errorType": "bad_data", "error": "missing query"}, status=400)
         now = fc.now()
-        loop = asyncio.get_running_loop()
         # Prometheus is its own server: its evaluation runs on its own thread,
         # so a slow (Python) evaluation does not hold the apiserver's list
         # responses on this event loop.
-        if sub == "api/v1/query":
+        if sub == "api/v1/query" and fc.rules and "time" not in req.query:
+            ent = fc.answers.get(q)
+            if ent is None:
+                body = await asyncio.wrap_future(prom_pool.submit(0, evaluate_rule, q))
+            else:
+                ent[2] = now
+                if ent[0] != promql.cache_stamp(fc.db, now):
+                    schedule_rule(q)
+                body = ent[1]
+        elif sub == "api/v1/query":
             t = float(req.query.get("time", now))
-            body = await loop.run_in_executor(prom_pool, promql.query, fc.db, q, t)
+            body = await asyncio.wrap_future(prom_pool.submit(0, promql.query, fc.db, q, t))
         elif sub == "api/v1/query_range":
             try:
                 rng = float(req.query["start"]), float(req.query["end"]), float(req.query["step"])
@@ -272,7 +363,7 @@ def build_app(fc: FakeCluster) -> web.Application:
             if rng is None:
                 body = {"status": "error", "errorType": "bad_data", "error": "bad range parameters"}
             else:
-                body = await loop.run_in_executor(prom_pool, promql.query_range, fc.db, q, *rng)
+                body = await asyncio.wrap_future(prom_pool.submit(0, promql.query_range, fc.db, q, *rng))
         else:
             return _status(404, "NotFound", sub)
         if isinstance(body, promql.RawJSON):
@@ -280,13 +371,49 @@ def build_app(fc: FakeCluster) -> web.Application:
         return web.json_response(body, status=200 if body["status"] == "success" else 400)
 
     # One evaluation thread: the TSDB's lazily built indexes and caches are not
-    # shared between concurrent evaluations.
-    prom_pool = concurrent.futures.ThreadPoolExecutor(max_workers=1, thread_name_prefix="fake-prometheus")
+    # shared between concurrent evaluations. Client requests before rule refreshes.
+    prom_pool = PriorityPool()
+
+    def evaluate_rule(q):
+        """Evaluate ``q`` now and keep the answer (runs on the evaluation thread)."""
+        t = fc.now()
+        stamp = promql.cache_stamp(fc.db, t)
+        body = promql.query(fc.db, q, t)
+        prev = fc.answers.get(q)
+        fc.answers[q] = [stamp, body, prev[2] if prev else t]
+        fc.rule_evals += 1
+        fc.refreshing.discard(q)
+        return body
+
+    def schedule_rule(q):
+        if q not in fc.refreshing:
+            fc.refreshing.add(q)
+            prom_pool.submit(1, evaluate_rule, q)
+
+    async def rule_ticker(_app):
+        """Re-evaluate every query asked in the last RULE_TTL_S once its inputs changed."""
+        async def tick():
+            while True:
+                await asyncio.sleep(0.25)
+                now = fc.now()
+                stamp = promql.cache_stamp(fc.db, now)
+                for q, ent in list(fc.answers.items()):
+                    if now - ent[2] > RULE_TTL_S:
+                        fc.answers.pop(q, None)
+                    elif ent[0] != stamp:
+                        schedule_rule(q)
+
+        if fc.rules:
+            _app["rule_ticker"] = asyncio.get_running_loop().create_task(tick())
 
     async def stop_pool(_app):
-        prom_pool.shutdown(wait=False)
+        task = _app.get("rule_ticker")
+        if task is not None:
+            task.cancel()
+        prom_pool.shutdown()
 
     app = web.Application(middlewares=[latency])
+    app.on_startup.append(rule_ticker)
     app.on_cleanup.append(stop_pool)
     app.router.add_get("/api/v1/nodes", nodes)
     app.router.add_get("/api/v1/pods", pods)
@@ -363,7 +490,7 @@ class ServerThread:
 
 def make_fake(nodes: int, *, source: str = "amd-exporter", latency_ms: float = 20.0, crd_installed: bool = True,
               prometheus_up=(DEFAULT_PROM_SERVICE,), live=None, preset: Optional[str] = None,
-              fail_rate: float = 0.0, hang_rate: float = 0.0, seed: int = 0) -> FakeCluster:
+              fail_rate: float = 0.0, hang_rate: float = 0.0, seed: int = 0, rules: bool = False) -> FakeCluster:
     """Convenience: synthetic cluster of ``nodes`` × 8 MI355X (or a BASELINE ``preset``) + telemetry + fake control plane."""
     import copy
 
@@ -376,7 +503,7 @@ def make_fake(nodes: int, *, source: str = "amd-exporter", latency_ms: float = 2
     for src in (("amd-exporter", "node-exporter") if source == "both" else (source,)):
         populate(db, cluster, source=src, live=live)
     return FakeCluster(cluster, db, latency_ms=latency_ms, crd_installed=crd_installed, prometheus_up=prometheus_up,
-                       fail_rate=fail_rate, hang_rate=hang_rate, seed=seed)
+                       fail_rate=fail_rate, hang_rate=hang_rate, seed=seed, rules=rules)
 
 
 __all__ = ["FakeCluster", "ServerThread", "build_app", "make_fake", "parse_label_selector", "parse_field_selector",

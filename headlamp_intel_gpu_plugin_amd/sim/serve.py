@@ -36,6 +36,8 @@ def main(argv=None) -> int:
     p.add_argument("--device-map", default="{}", help='JSON {"<hip device>": "<node>"}: device d → GPU 0 of that node')
     p.add_argument("--interval", type=float, default=15.0,
                    help="scrape interval (s), on its grid: deploy/exporter's ServiceMonitor scrapes every 15 s")
+    p.add_argument("--rules", action="store_true",
+                   help="answer instant queries from background re-evaluations (apiserver.py: recording rules)")
     args = p.parse_args(argv)
 
     from ..parallel.agent import Scraper, device_to_node, live_series
@@ -43,7 +45,8 @@ def main(argv=None) -> int:
 
     node_of_device: Dict[str, str] = json.loads(args.device_map)
     live = live_series(list(node_of_device.values())) if args.exporter and node_of_device else None
-    fc = make_fake(args.nodes, source=args.source, latency_ms=args.latency_ms, live=live, preset=args.preset)
+    fc = make_fake(args.nodes, source=args.source, latency_ms=args.latency_ms, live=live, preset=args.preset,
+                   rules=args.rules)
     scraper = (Scraper([(args.exporter, device_to_node(node_of_device))], live, interval=args.interval,
                        align=True).start()
                if live else None)
@@ -58,6 +61,7 @@ def main(argv=None) -> int:
                     work = sorted(w for _, w in fc.requests)
                     slowest = sorted(fc.requests, key=lambda r: -r[1])[:5]
                 print(json.dumps({"server_requests": fc.stats(), "scrapes": scraper.scrapes if scraper else 0,
+                                  "rule_evaluations": fc.rule_evals,
                                   # server-side work per request (ms), on top of the injected latency
                                   "server_work_ms": {"p50": round(work[len(work) // 2] * 1e3, 3) if work else None,
                                                      "max": round(work[-1] * 1e3, 3) if work else None,
@@ -77,9 +81,11 @@ class ControlPlaneProcess:
 
     def __init__(self, nodes: int, *, source: str = "both", latency_ms: float = 20.0, preset: Optional[str] = None,
                  exporter_url: Optional[str] = None, node_of_device: Optional[Dict[str, str]] = None,
-                 interval: float = 15.0):
+                 interval: float = 15.0, rules: bool = True):
         self.cmd = [sys.executable, "-m", "headlamp_intel_gpu_plugin_amd.sim.serve", "--nodes", str(nodes),
                     "--source", source, "--latency-ms", str(latency_ms), "--interval", str(interval)]
+        if rules:
+            self.cmd.append("--rules")
         if preset:
             self.cmd += ["--preset", preset]
         if exporter_url and node_of_device:

@@ -91,7 +91,8 @@ def table(rows):
         cells += [f"{l['baseline']['value_ms']:.1f} → {l['value']:.1f}", f"{l['baseline']['value_ms'] / l['value']:.1f}×",
                   f"{comp['reference_p50_ms']:.1f} → {comp['amd_p50_ms']:.1f}",
                   cold_mean(l),
-                  f"{l['cold_open_p50_ms']['reference']:.0f} → {l['cold_open_p50_ms']['amd']:.0f}",
+                  f"{l['cold_open_p50_ms']['reference']:.0f} → {l['cold_open_p50_ms']['amd']:.0f}"
+                  + server_share(l["cold_open_p50_ms"].get("amd_server_ms"), l["cold_open_p50_ms"]["amd"]),
                   f"{l['route_switch_p50_ms']['reference']:.0f} → {l['route_switch_p50_ms']['amd']:.1f}",
                   str(l["rendered"]["gpu_nodes"]), str(l["rendered"]["gpu_pods"]), str(l["rendered"]["gpus_monitored"]),
                   "yes" if l.get("live_telemetry") else "no"]
@@ -99,10 +100,24 @@ def table(rows):
     return md
 
 
+#: A figure whose fake-server share (X-Server-Ms of its slowest request) is above this measures the harness.
+SERVER_SHARE_FLAG = 0.25
+
+
+def server_share(server_ms, figure_ms):
+    """'s N%' — the fake server's share of a figure — with ⚠ above SERVER_SHARE_FLAG; '' when unknown."""
+    if server_ms is None or not figure_ms:
+        return ""
+    share = server_ms / figure_ms
+    return f", s {share * 100:.0f}%" + (" ⚠" if share > SERVER_SHARE_FLAG else "")
+
+
 def cold_table(rows):
-    """Per page at each point: cold open, reference → new first content / new complete (ms), and the new open's
-    Prometheus requests (query + query_range + probe)."""
-    head = ["Config", "GPU nodes"] + [f"{t}: ref → first / complete (ms), Prometheus requests" for _, t in PAGE_COLS]
+    """Per page at each point: cold open, reference → new first content / new complete (ms), the new open's
+    Prometheus requests (query + query_range + probe), and the fake server's share of the new complete figure
+    (``s N%``: the open's slowest request's own server time over the figure; ⚠ above SERVER_SHARE_FLAG)."""
+    head = ["Config", "GPU nodes"] + [f"{t}: ref → first / complete (ms), Prometheus requests, server share"
+                                      for _, t in PAGE_COLS]
     md = ["| " + " | ".join(head) + " |", "|---|---:|" + "---|" * (len(head) - 2)]
     for r in rows:
         l = r["line"]
@@ -116,7 +131,8 @@ def cold_table(rows):
                 continue
             by = v.get("amd_requests_by_kind") or {}
             prom = sum(by.get(x, 0) for x in ("query", "query_range", "probe"))
-            cells.append(f"{v['reference']:.0f} → {v['amd_first_content']:.0f} / {v['amd']:.0f}, {prom}")
+            cells.append(f"{v['reference']:.0f} → {v['amd_first_content']:.0f} / {v['amd']:.0f}, {prom}"
+                         + server_share(v.get("amd_server_ms"), v["amd"]))
         md.append("| " + " | ".join(cells) + " |")
     return md
 
@@ -124,7 +140,8 @@ def cold_table(rows):
 def render_table(rows):
     """Per page at each point: harness-React elements and mount / re-render ms, plus the cold Node detail open."""
     head = ["GPU nodes"] + [f"{t}: elements, mount / re-render ms" for _, t in PAGE_COLS] + [
-        "Cold Node detail ref → new: ms, KB, requests"]
+        "Cold Node detail ref → new: ms, KB, requests",
+        "Node detail after a page, as wired: ms, KB, requests, list hooks (cluster-wide)"]
     md = ["| " + " | ".join(head) + " |", "|---:|" + "---|" * (len(head) - 1)]
     for r in rows:
         l = r["line"]
@@ -137,6 +154,9 @@ def render_table(rows):
         a, ref = d.get("nodeDetailCold"), d.get("nodeDetailColdReference")
         cells.append(f"{ref['p50_ms']:.0f} → {a['p50_ms']:.0f}; {ref['bytes'] / 1e3:.0f} → {a['bytes'] / 1e3:.0f}; "
                      f"{ref['requests']:.0f} → {a['requests']:.0f}" if a and ref and a["p50_ms"] is not None else "—")
+        w = d.get("nodeDetailWired")
+        cells.append(f"{w['p50_ms']:.0f}; {w['bytes'] / 1e3:.0f}; {w['requests']:.0f}; {w.get('lists', 0):.0f} "
+                     f"({w.get('cluster_wide_lists', 0):.0f})" if w and w.get("p50_ms") is not None else "—")
         md.append("| " + " | ".join(cells) + " |")
     return md
 
