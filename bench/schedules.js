@@ -124,7 +124,8 @@ export function amdSchedule(request, clock, timeoutMs) {
   }
   function fetchPodsPage() {
     const o = ownersScope(store.getSnapshot(), PAGER);
-    return metrics.fetchGpuOwners(o.pods === undefined ? undefined : { pods: o.pods, small: !!o.small }).then(function (m) { pageMetrics.pods = m; });
+    const opts = o.pods === undefined ? undefined : { pods: o.pods, small: !!o.small, preview: o.preview };
+    return metrics.fetchGpuOwners(opts).then(function (m) { pageMetrics.pods = m; });
   }
   function fetchNodesPage() {
     return metrics.fetchGpuMetrics('topology', scoped(false).opts).then(function (m) { pageMetrics.nodes = m; });

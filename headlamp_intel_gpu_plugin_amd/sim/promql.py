@@ -199,12 +199,13 @@ class Evaluator:
         db = self.db
         iv = next(iter(db._fn_intervals)) if db._fn_intervals else 1.0
         sig = tuple((m.label, m.op, m.value) for m in e[1])
-        key = (sig, byt, wt, math.floor(t / iv))
+        counting = op == "count"  # a function-backed series always has a sample: no value needed
+        # A count's partials hold 1.0 per series, not its values: they are kept apart from the value partials.
+        key = (sig, byt, wt, math.floor(t / iv), counting)
         hit = db._agg_cache.get(key)
         if hit is None:
             parts: Dict[tuple, list] = {}
             pushed = []
-            counting = op == "count"  # a function-backed series always has a sample: no value needed
             for s in db.select(e[1]):
                 if s.fn is None:
                     pushed.append(s)
@@ -391,6 +392,16 @@ class RawJSON(str):
     """A pre-encoded JSON response body (served as-is by the fake apiserver)."""
 
 
+def cache_stamp(db: TSDB, t: float):
+    """What an instant answer at ``t`` depends on: the function-backed series' sample-grid bucket and the TSDB's
+    mutation count (pushes). Two evaluations with the same stamp give the same answer; None when the TSDB mixes
+    sample intervals (no stamp is cheap to compute)."""
+    if len(db._fn_intervals) > 1:
+        return None
+    iv = next(iter(db._fn_intervals)) if db._fn_intervals else 1.0
+    return (math.floor(t / iv), _MUTATIONS[0])
+
+
 def query(db: TSDB, q: str, t: float):
     """Prometheus ``/api/v1/query`` response body (dict on error/scalar, RawJSON for vectors).
 
@@ -400,10 +411,9 @@ def query(db: TSDB, q: str, t: float):
     cost of a Python TSDB would otherwise dominate the fake's latency, where
     a real Prometheus answers such a selector in well under a millisecond.
     """
-    cacheable = len(db._fn_intervals) <= 1
+    stamp = cache_stamp(db, t)
+    cacheable = stamp is not None
     if cacheable:
-        iv = next(iter(db._fn_intervals)) if db._fn_intervals else 1.0
-        stamp = (math.floor(t / iv), _MUTATIONS[0])
         hit = db._query_cache.get(q)
         if hit is not None and hit[0] == stamp:
             return _vector_body(hit[1], t)

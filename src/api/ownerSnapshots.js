@@ -36,10 +36,13 @@ export function createOwnerSnapshots(client, state) {
   }
 
   /**
-   * @param {{pods?: string[], small?: boolean, rank?: {by: string, page: number, per: number, filter: string}}} [opts]
+   * @param {{pods?: string[], small?: boolean, preview?: number,
+   *          rank?: {by: string, page: number, per: number, filter: string}}} [opts]
    *   `pods`: "namespace/name" keys of the page; `small`: every owner when at
-   *   most SMALL_CLUSTER_PODS pods own a GPU, else the page's; `rank`: the
-   *   page of pods ranked by the power of the GPUs they hold.
+   *   most SMALL_CLUSTER_PODS pods own a GPU, else the page's; `preview` (with
+   *   `small` and no page yet): on a larger cluster, the `preview` pods
+   *   drawing the most power instead, as `preview` = {order, watts, count};
+   *   `rank`: the page of pods ranked by the power of the GPUs they hold.
    */
   function owners(opts) {
     const rank = opts && opts.rank;
@@ -50,8 +53,9 @@ export function createOwnerSnapshots(client, state) {
     const pods = opts && Array.isArray(opts.pods) ? opts.pods.map(String) : null;
     const small = !!(opts && opts.small);
     if (small) {
-      const sk = 'owners|small|' + (pods || []).join(',');
-      return client.shared(sk, function () { return ownersOf(pods || [], true, sk); });
+      const pre = !(pods && pods.length) && opts.preview > 0 ? Math.min(200, Math.floor(opts.preview)) : 0;
+      const sk = 'owners|small|' + (pre ? 'preview:' + pre + '|' : '') + (pods || []).join(',');
+      return client.shared(sk, function () { return ownersOf(pods || [], true, sk, pre); });
     }
     if (pods && pods.length === 0) {
       return Promise.resolve({ source: state.source, gpus: [], xgmi: {}, links: {}, fetchedAt: client.fetchedAt(),
@@ -76,17 +80,36 @@ export function createOwnerSnapshots(client, state) {
     return st.last;
   }
 
-  function ownersOf(pods, small, key) {
+  function ownersOf(pods, small, key, preview) {
     const st = entry(key);
     return client.withPrometheus(function (base) {
-      return client.combined(base, ownersQuery(pods, small)).then(function (res) {
+      return client.combined(base, ownersQuery(pods, small, preview)).then(function (res) {
         if (!res.ok) return UNREACHABLE;
         const owning = small ? sizeFromRows(res.rows.__agg, 'gpu_pods') : 0;
+        const exceeded = owning > SMALL_CLUSTER_PODS;
+        const r = preview && exceeded ? rankRows(res.rows) : null;
         return answer(st, base, joinExporterResults(res.rows), {
-          small: small ? { count: owning, limit: SMALL_CLUSTER_PODS, exceeded: owning > SMALL_CLUSTER_PODS } : undefined,
+          small: small ? { count: owning, limit: SMALL_CLUSTER_PODS, exceeded: exceeded } : undefined,
+          preview: r ? { per: preview, count: owning, order: r.order, watts: r.watts } : undefined,
         });
       });
     }, function () { return staleOrNull(st, STALE_FAILURES, client.invalidate); });
+  }
+
+  /** The `agg="rank"` rows of an answer: "namespace/pod" keys highest power first, and the watts per key. */
+  function rankRows(rows) {
+    const ranked = [];
+    const watts = {};
+    for (let i = 0; i < rows.__agg.length; i++) {
+      const r = rows.__agg[i];
+      if (!isRow(r) || r.metric.agg !== 'rank' || typeof r.metric.pod !== 'string') continue;
+      const k = (typeof r.metric.namespace === 'string' ? r.metric.namespace : '') + '/' + r.metric.pod;
+      const w = num(r.value[1]);
+      ranked.push([k, w === null ? -Infinity : w]);
+      watts[k] = w;
+    }
+    ranked.sort(function (a, b) { return b[1] - a[1] || (a[0] < b[0] ? -1 : a[0] > b[0] ? 1 : 0); });
+    return { order: ranked.map(function (x) { return x[0]; }), watts: watts };
   }
 
   /**
@@ -100,20 +123,10 @@ export function createOwnerSnapshots(client, state) {
       return client.combined(base, rankedOwnersQuery(rank)).then(function (res) {
         if (!res.ok) return UNREACHABLE;
         const rows = res.rows;
-        const ranked = [];
-        const watts = {};
-        for (let i = 0; i < rows.__agg.length; i++) {
-          const r = rows.__agg[i];
-          if (!isRow(r) || r.metric.agg !== 'rank' || typeof r.metric.pod !== 'string') continue;
-          const k = (typeof r.metric.namespace === 'string' ? r.metric.namespace : '') + '/' + r.metric.pod;
-          const w = num(r.value[1]);
-          ranked.push([k, w === null ? -Infinity : w]);
-          watts[k] = w;
-        }
-        ranked.sort(function (a, b) { return b[1] - a[1] || (a[0] < b[0] ? -1 : a[0] > b[0] ? 1 : 0); });
+        const r = rankRows(rows);
         return answer(st, base, joinExporterResults(rows), {
           rank: { by: rank.by, page: rank.page, per: rank.per, filter: rank.filter, count: sizeFromRows(rows.__agg, 'ranked'),
-            order: ranked.map(function (x) { return x[0]; }), watts: watts },
+            order: r.order, watts: r.watts },
         });
       });
     }, function () { return staleOrNull(st, STALE_FAILURES, client.invalidate); });

@@ -232,14 +232,18 @@ export function exporterNodeQuery(nodeName, withStatic) {
  * `pod` label is set — one series per allocated GPU, instead of every live
  * gauge and xGMI link of every GPU.
  */
-export function ownersQuery(pods, small) {
+export function ownersQuery(pods, small, preview) {
   const sel = '{__name__="' + SERIES.exporter.power + '", ';
   if (small) {
     // Every owner when they fit on one page of the Pods table, else the page's pods (smallClusterQuery).
     const n = gpuPodCount();
     const all = sizeGuard(ownersQuery(null), true, n, SMALL_CLUSTER_PODS);
     const page = pods && pods.length ? ' or ' + sizeGuard(ownersQuery(pods), false, n, SMALL_CLUSTER_PODS) : '';
-    return all + page + ' or ' + sizeRow(n, 'gpu_pods');
+    // No page yet (the pod list is on its way) on a larger cluster: the
+    // `preview` pods drawing the most power, ranked, so the page has rows to
+    // show before the list is in (pods.js podsPreview).
+    const pre = preview > 0 && !(pods && pods.length) ? ' or ' + sizeGuard(previewOwners(preview), false, n, SMALL_CLUSTER_PODS) : '';
+    return all + page + pre + ' or ' + sizeRow(n, 'gpu_pods');
   }
   if (!pods) return 'max by (' + EXPORTER_JOIN_LABELS.join(', ') + ') (' + sel + 'pod!=""})';
   // The pods of one page of the Pods table ("namespace/name" keys): O(page).
@@ -253,6 +257,16 @@ export function ownersQuery(pods, small) {
   }
   const alt = function (o) { return promString(Object.keys(o).map(regexLiteral).join('|')); };
   return 'max by (' + EXPORTER_JOIN_LABELS.join(', ') + ') (' + sel + 'pod=~"' + alt(names) + '", namespace=~"' + alt(nss) + '"})';
+}
+
+/**
+ * The owner series of the `per` pods drawing the most GPU power and their
+ * ranking as `agg="rank"` rows: page 0 of rankedOwnersQuery without its
+ * count (the size row of the small query counts the owners).
+ */
+function previewOwners(per) {
+  const s = podPowerRankQuery(0, per, '');
+  return '(' + ownersQuery(null) + ') and on(namespace, pod) (' + s + ') or ' + sizeRow(s, 'rank');
 }
 
 /**

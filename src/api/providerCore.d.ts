@@ -81,7 +81,7 @@ export interface MetricsSource {
   fetchNodeMetrics(nodeName: string): Promise<GpuMetrics | null>;
   /** `pods`: "namespace/name" keys of one page of the Pods table; `small` as in fetchGpuMetrics */
   fetchGpuOwners(
-    opts?: { pods?: string[]; small?: boolean; rank?: { by: 'power'; page: number; per: number; filter: string } }
+    opts?: { pods?: string[]; small?: boolean; preview?: number; rank?: { by: 'power'; page: number; per: number; filter: string } }
   ): Promise<GpuMetrics | null>;
   failureReason(): 'forbidden' | 'unreachable';
   fetchPodSeries(namespace: string, pod: string, rangeSec: number, stepSec: number): Promise<{ rangeSec: number; stepSec: number; power: Array<[number, number]> } | null>;
@@ -109,7 +109,9 @@ export interface ProviderCore {
     enabled?: boolean,
     pods?: string[],
     small?: boolean,
-    rank?: { by: 'power'; page: number; per: number; filter: string }
+    rank?: { by: 'power'; page: number; per: number; filter: string },
+    /** with `small` and no page yet: the pods drawing the most power on a larger cluster (a partial page) */
+    preview?: number
   ): GpuMetricsState;
   usePodGpuSeries(namespace: string | null, pod: string | null, enabled?: boolean): GpuMetricsState;
   useNodeGpuSeries(nodeName: string | null, enabled?: boolean): GpuMetricsState;

@@ -645,9 +645,11 @@ export function createProviderCore(React, lib, deps) {
    * Pod → GPU attribution for the Pods page (metrics.js fetchGpuOwners): one
    * series per allocated GPU — of the pods on the page when `pods` (their
    * "namespace/name" keys) is given, else of every pod; `small` as in
-   * useGpuMetrics (pages.js ownersScope).
+   * useGpuMetrics (pages.js ownersScope); `preview` (small, no page yet): on a
+   * larger cluster the `preview` pods drawing the most power (a partial page
+   * before the pod list is in).
    */
-  function useGpuOwners(enabled, pods, small, rank) {
+  function useGpuOwners(enabled, pods, small, rank, preview) {
     const cluster = clusterKey();
     const source = metricsSourceFor(cluster);
     const on = enabled === undefined ? true : enabled;
@@ -657,10 +659,13 @@ export function createProviderCore(React, lib, deps) {
     const ex = useState(false);
     // Power order (ownersScope rank): Prometheus picks the page's pods.
     const rk = rank ? rank.by + ':' + rank.page + ':' + rank.per + ':' + rank.filter : null;
+    // The preview is asked with the first small query but is not part of its
+    // key: on a small cluster the pod list arriving keeps the key (no refetch).
+    const pre = sm && !keys.length && preview > 0 ? preview : 0;
     const key = 'owners|' + sourceKey(cluster, loadSettings()) +
       (rk ? '|rank:' + rk : sm ? smallKey(ex[0], keys) : scoped ? '|pods:' + keys.join(',') : '');
     const res = useMetricsFetch(on ? key : null, function () {
-      const opts = rank ? { rank: rank } : scoped ? { pods: keys, small: sm } : undefined;
+      const opts = rank ? { rank: rank } : scoped ? { pods: keys, small: sm, preview: pre } : undefined;
       return source.fetchGpuOwners(opts).then(function (m) { return [m, null]; });
     }, false, source);
     useExceeded(sm, res, ex);

@@ -293,6 +293,11 @@ export interface GpuMetrics {
   totals?: GpuTotals;
   /** a size-guarded (small-cluster) snapshot: GPU nodes (pods) reporting, and whether that was more than a page */
   small?: { count: number; limit: number; exceeded: boolean };
+  /**
+   * an owners answer asked before the pod list (ownersScope `preview`) on a cluster of more than one page of owners:
+   * the `per` pods drawing the most power, "namespace/pod" keys highest first, out of `count` pods holding GPUs
+   */
+  preview?: { per: number; count: number; order: string[]; watts: Record<string, number | null> };
   /** a power-ranked page (metrics.js rankedSnapshot): `scope` is in rank order */
   /** power order: the page Prometheus ranked; `order` ("namespace/pod" keys, highest first) on an owners answer */
   rank?: {

@@ -159,7 +159,7 @@ export function createPlugin(env) {
     const ctx = core.useAmdGpuContext();
     const pager = usePager('pods');
     const o = ownersScope(ctx, pager.state);
-    const m = core.useGpuOwners(o.enabled, o.pods, o.small, o.rank);
+    const m = core.useGpuOwners(o.enabled, o.pods, o.small, o.rank, o.preview);
     useRankedPageClamp(m.metrics, pager);
     // As on GPU Nodes: the lists are watches; Refresh renews the attribution.
     return h(Page, {

@@ -5,17 +5,14 @@
  */
 
 import {
-  containerGpuEntries,
   formatPodGpuRequests,
-  gpuContainers,
-  gpuInitContainers,
   phaseToStatus,
   podPhase,
   podWaitingMessage,
   podWaitingReason,
 } from '../../api/amdPods.js';
 import { podFacts } from '../../api/clusterIndex.js';
-import { formatBytes, formatGpuResourceName, formatWatts } from '../../api/k8sCore.js';
+import { formatBytes, formatWatts } from '../../api/k8sCore.js';
 import { SMALL_CLUSTER_PODS } from '../../api/series.js';
 import { kv, lines, loader, page, pager, row, section, status, table } from '../ir.js';
 import {
@@ -125,7 +122,7 @@ function assignedText(gs) {
  * SMALL_CLUSTER_PODS pods hold a GPU, else the page's pods) while the pod
  * list loads or is that short; the pods of its page (namespace/name keys)
  * once a longer list is in; cluster-wide when the pod list failed.
- * @returns {{enabled: boolean, pods: (string[]|undefined), small?: boolean}}
+ * @returns {{enabled: boolean, pods: (string[]|undefined), small?: boolean, preview?: number}}
  */
 export function ownersScope(ctx, state) {
   if (!ctx) return { enabled: false, pods: [] };
@@ -138,39 +135,36 @@ export function ownersScope(ctx, state) {
     };
   }
   if (ctx.podsState === 'error') return { enabled: true, pods: undefined };
-  // As telemetryScope: every owner of a small cluster in the first wave.
-  if (ctx.podsState !== 'ready' && podsPending(ctx)) return { enabled: true, pods: [], small: true };
+  // As telemetryScope: every owner of a small cluster in the first wave; on a
+  // larger one the PODS_PER_PAGE pods drawing the most power, so the page has
+  // rows before the pod list is in (podsPreview).
+  if (ctx.podsState !== 'ready' && podsPending(ctx)) return { enabled: true, pods: [], small: true, preview: PODS_PER_PAGE };
   if (ctx.error && (!ctx.gpuPods || ctx.gpuPods.length === 0)) return { enabled: true, pods: undefined };
   const pods = podPage(ctx.gpuPods, state).names;
   return ctx.gpuPods.length <= SMALL_CLUSTER_PODS ? { enabled: true, pods: pods, small: true } : { enabled: true, pods: pods };
 }
 
-/** Per-container GPU lines (reference GpuContainerList, PodsPage.tsx:49-88), init containers included. */
+/**
+ * Per-container GPU lines (reference GpuContainerList, PodsPage.tsx:49-88),
+ * init containers included — derived with the pod's facts when the pod list
+ * arrived (clusterIndex.js podFacts). One container is plain text.
+ */
 export function gpuContainerLines(pod) {
-  const out = [];
-  function add(c, init) {
-    const es = containerGpuEntries(c);
-    const parts = [];
-    for (let i = 0; i < es.length; i++) {
-      const e = es[i];
-      const label = formatGpuResourceName(e.key);
-      if (e.request !== null && e.limit !== null && e.request === e.limit) parts.push(label + ': ' + e.request);
-      else parts.push(label + ': req=' + (e.request === null ? '—' : e.request) + ' lim=' + (e.limit === null ? '—' : e.limit));
-    }
-    out.push({ label: c.name + (init ? ' (init)' : ''), text: parts.join(', ') });
-  }
-  const ics = gpuInitContainers(pod);
-  for (let i = 0; i < ics.length; i++) add(ics[i], true);
-  const cs = gpuContainers(pod);
-  for (let i = 0; i < cs.length; i++) add(cs[i], false);
-  return out.length ? lines(out) : '—';
+  const cs = podFacts(pod).containers;
+  if (!cs.length) return '—';
+  return cs.length === 1 ? cs[0].label + ': ' + cs[0].text : lines(cs);
 }
 
 export function podsView(ctx, opts) {
   const now = nowOf(opts);
   // The page draws the pod list (and the index, built from the nodes too); it
-  // does not wait for the DeviceConfigs.
-  if (podsPending(ctx) || nodesPending(ctx)) return page(null, null, [loader('Loading GPU pod data...')]);
+  // does not wait for the DeviceConfigs. Until the lists are in, the
+  // exporter's owner answer (when it came first) is shown as a partial page.
+  if (podsPending(ctx) || nodesPending(ctx)) {
+    const pv = podsPreview(opts && opts.metrics);
+    if (!pv) return page(null, null, [loader('Loading GPU pod data...')]);
+    return page(BRAND + ' — Pods', refreshButton('Refresh pod data', !!(opts && opts.fetching)), pv);
+  }
   const assign = opts && opts.metrics ? podGpuAssignments(opts.metrics) : null;
   // One page of the GPU pod table (PODS_PER_PAGE, filter on namespace/name
   // and node): the reference lists every GPU pod (PodsPage.tsx:201-236).
@@ -261,6 +255,47 @@ function podsItems(ctx, now, assign, pg, sort) {
   }
 
   return items;
+}
+
+/**
+ * The GPU Pods page while the pod list is on its way (ADR 013): rows for the
+ * pods the exporter attributes GPUs to — on a small cluster every owner in
+ * namespace / name order, on a larger one the PODS_PER_PAGE pods drawing the
+ * most power (ownersScope `preview`) — marked partial. Kubernetes facts the
+ * exporter does not carry (requests, restarts, age, pending pods) follow with
+ * the list, which then replaces these rows. Null when the answer names no
+ * owner (or has not come).
+ */
+export function podsPreview(metrics) {
+  if (!metrics || !metrics.gpus) return null;
+  const assign = podGpuAssignments(metrics);
+  const pv = metrics.preview;
+  return memo('pods-preview', [assign, pv], function () {
+    const keys = pv && Array.isArray(pv.order) ? pv.order.filter(function (k) { return assign[k]; })
+      : Object.keys(assign).sort().slice(0, PODS_PER_PAGE);
+    if (!keys.length) return null;
+    const total = pv ? pv.count : Object.keys(assign).length;
+    const held = pv ? null : metrics.gpus.filter(function (g) { return !!g.pod; }).length;
+    const sum = [
+      row('Status', status('warning', 'Partial — the pod list is loading; these rows come from the GPU exporter')),
+      row('Pods Holding GPUs', String(total)),
+    ];
+    if (held !== null) sum.push(row('GPUs Held', String(held)));
+    const rows = keys.map(function (k) {
+      const gs = assign[k];
+      const slash = k.indexOf('/');
+      const nodes = [];
+      for (let i = 0; i < gs.length; i++) if (nodes.indexOf(gs[i].nodeName) < 0) nodes.push(gs[i].nodeName);
+      return [k.slice(slash + 1), k.slice(0, slash), nodes.join(', '), status('success', 'Running'),
+        gs.length + ' GPU' + (gs.length === 1 ? '' : 's') + ' held', assignedText(gs), podPowerText(gs), '—', '—'];
+    });
+    return [
+      section('Summary (partial)', [kv(sum)]),
+      section(pv ? 'GPU Pods Drawing the Most Power (partial)' : 'GPU Pods (partial)', [
+        table(['Name', 'Namespace', 'Node', 'Phase', 'GPU Resources', 'Assigned GPUs', 'GPU Power', 'Restarts', 'Age'], rows, keys),
+      ]),
+    ];
+  });
 }
 
 /** Live power of the GPUs a pod holds (exporter pod labels), summed; "—" without a reading. */

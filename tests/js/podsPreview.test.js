@@ -1,0 +1,115 @@
+/**
+ * The GPU Pods page before the pod list is in (ADR 013): the owner query's
+ * preview branch (promql.js ownersQuery), its answer (ownerSnapshots.js) and
+ * the partial page (pods.js podsPreview / podsView).
+ */
+import { createMetricsSource } from '../../src/api/metrics.js';
+import { ownersQuery } from '../../src/api/promql.js';
+import { SERIES, SMALL_CLUSTER_PODS } from '../../src/api/series.js';
+import { clearViewMemo } from '../../src/view/pages/common.js';
+import { ownersScope, podsPreview, podsView } from '../../src/view/pages/pods.js';
+import { PODS_PER_PAGE } from '../../src/view/pages/paging.js';
+import { sectionTitles } from '../../src/view/ir.js';
+import { renderPage } from '../../src/view/html.js';
+import { ok, vec } from './promFake.js';
+
+const E = SERIES.exporter;
+
+function owner(ns, pod, node, gpu, w) {
+  return vec({ __name__: E.power, namespace: ns, pod: pod, hostname: node, gpu_id: String(gpu) }, w);
+}
+
+/** A pending pod list: what the GPU Pods page sees on a cold open. */
+const PENDING = { podsState: 'pending', podsLoading: true, nodesState: 'ready', nodesLoading: false, gpuPods: [], loading: true };
+
+beforeEach(() => clearViewMemo());
+
+describe('ownersScope before the pod list', () => {
+  it('asks the small owner query with a preview of one page', () => {
+    expect(ownersScope(PENDING, { page: 0, filter: '' })).toEqual({ enabled: true, pods: [], small: true, preview: PODS_PER_PAGE });
+  });
+  it('the preview branch is a power ranking guarded to clusters of more than one page of owners', () => {
+    const q = ownersQuery([], true, 25);
+    expect(q).toContain('topk(25, sum by (namespace, pod)');
+    expect(q).toContain('> ' + SMALL_CLUSTER_PODS);
+    expect(q).toContain('"agg", "rank"');
+    // a page of pods asked: no preview
+    expect(ownersQuery(['ml/a'], true, 25)).not.toContain('topk(');
+    expect(ownersQuery([], true)).not.toContain('topk(');
+  });
+});
+
+describe('the preview answer (ownerSnapshots.js)', () => {
+  it('large cluster: the ranked pods, their watts and the owner count', async () => {
+    const asked = [];
+    const request = (path) => {
+      asked.push(decodeURIComponent(path));
+      if (path.indexOf('query=1') >= 0) return Promise.resolve(ok([]));
+      return Promise.resolve(ok([
+        owner('ml', 'big', 'n1', 0, 700), owner('ml', 'big', 'n1', 1, 700), owner('ml', 'mid', 'n2', 0, 500),
+        vec({ namespace: 'ml', pod: 'big', agg: 'rank' }, 1400), vec({ namespace: 'ml', pod: 'mid', agg: 'rank' }, 500),
+        vec({ agg: 'gpu_pods' }, 300),
+      ]));
+    };
+    const m = await createMetricsSource({ request }).fetchGpuOwners({ pods: [], small: true, preview: 25 });
+    expect(asked.some((p) => p.indexOf('topk(25,') >= 0)).toBe(true);
+    expect(m.small).toEqual({ count: 300, limit: SMALL_CLUSTER_PODS, exceeded: true });
+    expect(m.preview.order).toEqual(['ml/big', 'ml/mid']);
+    expect(m.preview.count).toBe(300);
+    expect(m.preview.watts['ml/big']).toBe(1400);
+    expect(m.gpus.filter((g) => g.pod === 'big')).toHaveLength(2);
+  });
+
+  it('small cluster: every owner, no preview ranking', async () => {
+    const request = () => Promise.resolve(ok([owner('ml', 'a', 'n1', 0, 300), vec({ agg: 'gpu_pods' }, 1)]));
+    const m = await createMetricsSource({ request }).fetchGpuOwners({ pods: [], small: true, preview: 25 });
+    expect(m.small.exceeded).toBe(false);
+    expect(m.preview).toBeUndefined();
+  });
+});
+
+describe('podsPreview / podsView with the pod list pending', () => {
+  function metrics(gpus, preview) {
+    return { gpus: gpus, xgmi: {}, links: {}, scope: 'owners', preview: preview };
+  }
+  function g(ns, pod, node, gpu, w) {
+    return { namespace: ns, pod: pod, nodeName: node, gpu: String(gpu), powerWatts: w };
+  }
+
+  it('nothing to show without an owner answer: the loader', () => {
+    expect(podsPreview(null)).toBeNull();
+    expect(podsPreview(metrics([g('', '', 'n1', 0, 100)].filter((x) => x.pod)))).toBeNull();
+    const vm = podsView(PENDING, { metrics: null });
+    expect(renderPage(vm)).toContain('Loading GPU pod data...');
+  });
+
+  it('small cluster: every owner in namespace / name order, marked partial, with GPUs held', () => {
+    const m = metrics([g('ml', 'b', 'n1', 0, 300), g('ml', 'a', 'n1', 1, 200), g('ml', 'a', 'n2', 0, 200), g('', null, 'n2', 1, 90)]);
+    const vm = podsView(PENDING, { metrics: m });
+    const html = renderPage(vm);
+    expect(sectionTitles(vm)).toEqual(['Summary (partial)', 'GPU Pods (partial)']);
+    expect(html).toContain('Partial — the pod list is loading');
+    expect(html.indexOf('>a<')).toBeLessThan(html.indexOf('>b<'));
+    expect(html).toContain('n1, n2');
+    expect(html).toContain('2 GPUs held');
+    expect(html).toContain('400.0 W');
+    expect(html).not.toContain('Loading GPU pod data...');
+  });
+
+  it('large cluster: the ranked pods in power order, out of every pod holding a GPU', () => {
+    const m = metrics([g('ml', 'low', 'n1', 0, 100), g('ml', 'high', 'n2', 0, 700)],
+      { per: 25, count: 4000, order: ['ml/high', 'ml/low'], watts: { 'ml/high': 700, 'ml/low': 100 } });
+    const vm = podsView(PENDING, { metrics: m });
+    const html = renderPage(vm);
+    expect(sectionTitles(vm)).toEqual(['Summary (partial)', 'GPU Pods Drawing the Most Power (partial)']);
+    expect(html).toContain('4000');
+    expect(html.indexOf('>high<')).toBeLessThan(html.indexOf('>low<'));
+  });
+
+  it('the pod list in: the partial sections give way to the full page', () => {
+    const m = metrics([g('ml', 'a', 'n1', 0, 200)]);
+    const ready = { podsState: 'ready', podsLoading: false, nodesState: 'ready', nodesLoading: false, gpuPods: [], loading: false,
+      index: { phases: { Running: 0, Pending: 0, Failed: 0 }, totals: { heldGpus: 0 } } };
+    expect(sectionTitles(podsView(ready, { metrics: m }))).toEqual(['No GPU Pods Found']);
+  });
+});

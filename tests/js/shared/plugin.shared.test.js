@@ -248,10 +248,31 @@ describe('shared: progressive cold open — a page waits only for the lists it d
     r2.unmount();
   });
 
-  it('GPU Pods waits for the pod list (the list is its content)', async () => {
-    cluster({ podsLoading: true });
+  it('GPU Pods: while the pod list loads, the exporter\'s GPU owners as a partial page; the list then replaces it', async () => {
+    const fake = cluster({ podsLoading: true });
     const r = render(h(route('/amd-gpu/pods')));
     await r.settle();
+    expect(r.text()).not.toContain('Loading GPU pod data...');
+    expect(r.text()).toContain('Partial — the pod list is loading');
+    expect(r.text()).toContain('train-0');
+    lib.lists.Pod = [fake.pods, null];
+    r.rerender(h(route('/amd-gpu/pods')));
+    await r.settle();
+    expect(r.text()).not.toContain('Partial');
+    expect(r.text()).toContain('train-a');
+    r.unmount();
+  });
+
+  it('GPU Pods without telemetry waits for the pod list (the list is its content)', async () => {
+    // A Prometheus this session has not met (no earlier answer to serve stale).
+    saveSettings(Object.assign({}, DEFAULT_SETTINGS, { requestTimeoutMs: DEFAULT_SETTINGS.requestTimeoutMs + 2 }));
+    cluster({ podsLoading: true });
+    const api = lib.api.handler;
+    lib.api.handler = (path) => (path.indexOf('/proxy/') >= 0
+      ? Promise.reject(Object.assign(new Error('503 Service Unavailable'), { status: 503 })) : api(path));
+    const r = render(h(route('/amd-gpu/pods')));
+    await r.settle();
+    saveSettings(DEFAULT_SETTINGS);
     expect(r.text()).toContain('Loading GPU pod data...');
     r.unmount();
   });
@@ -403,6 +424,9 @@ describe('shared: GPU Pods in power order (' + tier + ')', () => {
     // the exporter fixture labels GPU 0 / 1 of each node with pods ml/train-0 (700 W) and ml/train-1 (701 W)
     lib.lists.Pod = [[makeGpuPod('train-0', { gpus: 1, node: 'mi355x-000' }), makeGpuPod('train-1', { gpus: 1, node: 'mi355x-001' })], null];
     const r = render(h(route('/amd-gpu/pods')));
+    await r.settle();
+    expect(r.byLabel('Filter or sort GPU pods')).toBeTruthy(); // one page: the count line and this button
+    r.click(r.byLabel('Filter or sort GPU pods'));
     await r.settle();
     r.change(r.byLabel('Sort GPU pods'), 'power');
     await r.settle();

@@ -595,3 +595,40 @@ def test_node_exporter_junction_temperature_against_the_synthetic_cluster():
     temps = [r for r in page if r["metric"]["__name__"] == "node_hwmon_temp_celsius"]
     assert len(temps) == 8 and {r["metric"]["instance"] for r in temps} == {inst}
     assert len([r for r in page if r["metric"]["__name__"] == "node_hwmon_power_input_watt"]) == 8
+
+
+def test_the_owners_preview_before_the_pod_list():
+    """promql.js ownersQuery([], small, preview): every owner on a cluster of at most SMALL_CLUSTER_PODS owners;
+    on a larger one the `preview` pods drawing the most power (their owner series and rank rows) and the count."""
+    def cluster(n_pods):
+        d = TSDB()
+        for i in range(n_pods):
+            for g in range(2):
+                d.add(Series({"__name__": "gpu_power_usage", "hostname": f"n{i // 4}", "gpu_id": str(2 * (i % 4) + g),
+                              "pod": f"p{i:03d}", "namespace": "ml"}, fn=lambda t, w=100.0 + i: w))
+        return d
+
+    q, limit = _js("[m.ownersQuery([], true, 5), m.SMALL_CLUSTER_PODS]")
+    small = _vec(query(cluster(limit), q, 100.0))
+    owners = {r["metric"]["pod"] for r in small if "agg" not in r["metric"]}
+    assert len(owners) == limit and not [r for r in small if r["metric"].get("agg") == "rank"]
+    big = _vec(query(cluster(limit + 36), q, 100.0))
+    owners = {r["metric"]["pod"] for r in big if "agg" not in r["metric"]}
+    ranks = {r["metric"]["pod"]: float(r["value"][1]) for r in big if r["metric"].get("agg") == "rank"}
+    (count,) = [float(r["value"][1]) for r in big if r["metric"].get("agg") == "gpu_pods"]
+    top = {f"p{i:03d}" for i in range(limit + 31, limit + 36)}
+    assert owners == top and set(ranks) == top and count == limit + 36
+    assert ranks[f"p{limit + 35:03d}"] == 2 * (100.0 + limit + 35)
+    # Without `preview` (or with a page of pods) the large cluster answers the count alone, as before.
+    q0 = _js("m.ownersQuery([], true)")
+    assert [r["metric"].get("agg") for r in _vec(query(cluster(limit + 36), q0, 100.0))] == ["gpu_pods"]
+
+
+def test_count_and_sum_of_the_same_selector_do_not_share_partials():
+    """The fake's per-grid aggregation cache keys a count's partials (1.0 per series) apart from the values."""
+    d = TSDB()
+    for i in range(3):
+        d.add(Series({"__name__": "gpu_power_usage", "pod": "p", "gpu_id": str(i)}, fn=lambda t, w=100.0 * (i + 1): w))
+    sel = '{__name__="gpu_power_usage", pod!=""}'
+    assert [r["value"][1] for r in _vec(query(d, f"count by (pod) ({sel})", 100.0))] == ["3"]
+    assert [r["value"][1] for r in _vec(query(d, f"sum by (pod) ({sel})", 100.0))] == ["600"]
