@@ -91,5 +91,5 @@ export async function mountCycle(R, make, waitText, beforeRerender, reps, mustSh
     R.ReactDOM.flushSync(function () { root.unmount(); });
     document.body.removeChild(c);
   }
-  return { mountMs: stats(mounts).p50, rerenderMs: stats(rerenders).p50, elements: elements, reps: reps };
+  return { mountMs: stats(mounts).p50, rerenderMs: stats(rerenders).p50, elements: elements, reps: reps, mounts: mounts, rerenders: rerenders };
 }

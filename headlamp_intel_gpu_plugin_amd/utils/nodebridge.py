@@ -20,13 +20,14 @@ def node_binary() -> str:
 class Driver:
     """A long-lived ``bench/driver.js --serve`` process speaking JSON lines."""
 
-    def __init__(self, url: str):
+    def __init__(self, url: str, node_flags=(), env: Optional[Dict[str, str]] = None):
         # HEADLAMP_AMD_NODE_FLAGS: extra node flags for diagnostics, e.g. "--cpu-prof --cpu-prof-dir=/tmp/p"
-        # (node 12 refuses --cpu-prof in NODE_OPTIONS).
-        flags = os.environ.get("HEADLAMP_AMD_NODE_FLAGS", "").split()
+        # (node 12 refuses --cpu-prof in NODE_OPTIONS). `node_flags` / `env`: the opt-in render comparison runs the
+        # driver with --disallow-code-generation-from-strings and a minimal environment (tools/render_compare.py).
+        flags = list(node_flags) + os.environ.get("HEADLAMP_AMD_NODE_FLAGS", "").split()
         self.proc = subprocess.Popen([node_binary(), *flags, os.path.join(ROOT, "bench", "driver.js"), "--serve", "--url", url],
                                      cwd=ROOT, stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
-                                     text=True, bufsize=1)
+                                     text=True, bufsize=1, env=env)
 
     def call(self, cmd: str, schedule: str = "amd", n: int = 1, timeout: Optional[float] = None, **extra) -> Dict:
         assert self.proc.stdin and self.proc.stdout

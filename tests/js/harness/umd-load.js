@@ -11,6 +11,7 @@
  */
 import fs from 'fs';
 import path from 'path';
+import vm from 'vm';
 import { createWindow } from './minidom.js';
 
 const FILES = {
@@ -58,7 +59,9 @@ export function loadUmdReact(dir, build) {
     // The UMD wrapper registers on `this` when neither CommonJS nor AMD is
     // around — on `self` in the .min.js builds, whose strict-mode IIFE leaves
     // `this` undefined: both are the sandbox.
-    new Function('self', src).call(sandbox, sandbox); // eslint-disable-line no-new-func
+    // Compiled as a script (not by the Function constructor), so it also loads in a process started with
+    // --disallow-code-generation-from-strings (the opt-in render comparison, bench/compareRenders.js).
+    vm.runInThisContext('(function (self) {' + src + '\n})', { filename: files[i] }).call(sandbox, sandbox);
   }
   const React = sandbox.React;
   const ReactDOM = sandbox.ReactDOM;

@@ -1,18 +1,15 @@
 /**
- * bench/tsx.js — the benchmark's TSX → JavaScript transformer (it mounts the
- * reference's own pages for the rows-rendered comparison,
- * bench/referenceRender.js). Its transforms on small inputs, and, where the
- * reference's sources are present (/root/reference), the reference's own
- * unit tests of src/api/k8s.ts run through it against the transpiled module:
- * the transpiler is right where the reference's tests say so.
+ * bench/tsx.js — the benchmark's TSX → JavaScript transformer (the opt-in
+ * render comparison mounts the reference's own pages with it,
+ * bench/referenceRender.js). Its transforms on small inputs of this
+ * repository's own, and the sandbox it loads modules into. Nothing here
+ * reads or runs the reference's sources: they are untrusted public content
+ * (ADR 013), executed only by tools/render_compare.py --allow-reference-exec.
  */
-import fs from 'fs';
-import { loadModules, lowerModules, lowerOptional, stripTypes, transformJsx, transpile } from '../../bench/tsx.js';
+import { loadModules, lowerModules, lowerOptional, stripTypes, transformJsx } from '../../bench/tsx.js';
 
 function run(src, imports) {
-  const exp = {};
-  new Function('__import', '__exports', transpile(src))(function (spec) { return imports[spec]; }, exp); // eslint-disable-line no-new-func
-  return exp;
+  return loadModules({ 'm.tsx': src }, 'm.tsx', function (from, spec) { return imports[spec]; });
 }
 
 const React = {
@@ -124,15 +121,34 @@ describe('tsx: modules', () => {
   });
 });
 
-// The reference's own unit tests of its domain model (48 cases), run against
-// its k8s.ts as transpiled here — when its sources are in this container.
-const REF = '/root/reference/src/api/';
-const haveReference = fs.existsSync(REF + 'k8s.ts') && fs.existsSync(REF + 'k8s.test.ts');
-if (haveReference) {
-  const files = { 'k8s.ts': fs.readFileSync(REF + 'k8s.ts', 'utf8'), 'k8s.test.ts': fs.readFileSync(REF + 'k8s.test.ts', 'utf8') };
-  loadModules(files, 'k8s.test.ts', function (from, spec) {
-    if (spec === 'vitest') return { describe: describe, it: it, expect: expect, vi: vi, beforeEach: beforeEach };
-    if (spec === './k8s') return 'k8s.ts';
-    throw new Error('unexpected import ' + spec);
+describe('tsx: the module sandbox', () => {
+  it('a module sees the language built-ins and its imports, not Node', () => {
+    const m = run([
+      "import ext from 'ext';",
+      'export const seen = [typeof process, typeof require, typeof setTimeout, typeof Buffer, typeof fetch, typeof ext.v];',
+      'export const builtins = [typeof Map, typeof Promise, typeof JSON.parse, typeof Date.now];',
+    ].join('\n'), { ext: { default: { v: 1 } } });
+    expect(m.seen).toEqual(['undefined', 'undefined', 'undefined', 'undefined', 'undefined', 'number']);
+    expect(m.builtins).toEqual(['function', 'function', 'function', 'function']);
   });
-}
+
+  it('eval and the Function constructor of its own realm are refused', () => {
+    const m = run([
+      'export function viaEval() { return eval("1 + 1"); }',
+      'export function viaFunction() { return (function () {}).constructor("return 1")(); }',
+    ].join('\n'), {});
+    expect(() => m.viaEval()).toThrow('Code generation from strings disallowed');
+    expect(() => m.viaFunction()).toThrow('Code generation from strings disallowed');
+  });
+
+  it('dynamic import() is refused', async () => {
+    const m = run("export function load() { return import('fs'); }", {});
+    let err = null;
+    try {
+      await m.load();
+    } catch (e) {
+      err = e;
+    }
+    expect(err).not.toBeNull();
+  });
+});

@@ -1,7 +1,17 @@
 #!/usr/bin/env python3
 """The reference's own pages vs this plugin's, rendered on real React 18.3.1 at 1 to 1,000 GPU nodes.
 
-    python tools/render_compare.py [--sizes 1,2,4,8,16,64,256,1000] [--reps 5] [--out profiles/r4_render_compare]
+    python tools/render_compare.py --allow-reference-exec [--sizes 1,2,4,8] [--reps 15] [--warm 5]
+                                   [--out profiles/r5_render_compare]
+
+OPT-IN: this runs the reference's page components, which are untrusted public content (ADR 013). Without
+``--allow-reference-exec`` it refuses. With it, bench/driver.js runs in a child process started with
+``--disallow-code-generation-from-strings`` and only PATH in its environment, and the reference's modules are
+compiled into bench/tsx.js's sandbox: a vm context of their own, with no ``process``, ``require``, ``import()``,
+timers, file system or network, and no code generation from strings there or through any host function.
+
+Per page and size: ``--warm`` untimed mounts of each side, then ``--reps`` (at least 15) interleaved
+reference / new pairs, the order alternating; mount and re-render p50 with the interquartile range.
 
 Per size: the fake control plane (no injected latency: this measures render, not requests) serves a synthetic
 cluster; bench/driver.js ``refRender`` mounts each of the five reference pages — read unmodified from
@@ -27,7 +37,7 @@ PAGES = [("overview", "Overview"), ("devicePlugins", "Device Plugins"), ("nodes"
          ("metrics", "Metrics")]
 
 
-def measure(n: int, reference: str, reps: int) -> dict:
+def measure(n: int, reference: str, reps: int, warm: int) -> dict:
     from headlamp_intel_gpu_plugin_amd.sim.serve import ControlPlaneProcess
     from headlamp_intel_gpu_plugin_amd.utils.nodebridge import Driver
     from headlamp_intel_gpu_plugin_amd.utils.reactumd import PROD_BUILDS, umd_dir
@@ -36,9 +46,11 @@ def measure(n: int, reference: str, reps: int) -> dict:
     if not umd:
         raise SystemExit("the React 18.3.1 production UMD builds are not available in this image")
     with ControlPlaneProcess(n, source="both", latency_ms=0.0) as srv:
-        drv = Driver(srv.url)
+        drv = Driver(srv.url, node_flags=["--disallow-code-generation-from-strings"],
+                     env={"PATH": os.environ.get("PATH", "/usr/bin:/bin")})
         try:
-            r = drv.call("refRender", referenceDir=reference, umdDir=umd, reps=reps, timeout=3000)
+            r = drv.call("refRender", referenceDir=reference, umdDir=umd, reps=reps, warm=warm, allowReferenceExec=True,
+                         timeout=3000)
         finally:
             drv.close()
     if r.get("error"):
@@ -46,16 +58,25 @@ def measure(n: int, reference: str, reps: int) -> dict:
     return r["render"]
 
 
+def verdict(a: dict, ref: dict) -> str:
+    """'≤' when the new mount p50 is at most the reference's, '≈' within its interquartile range, else '>'."""
+    if a["mountMs"] <= ref["mountMs"]:
+        return "≤"
+    return "≈" if a["mountMs"] <= ref.get("mountQ3", ref["mountMs"]) else ">"
+
+
 def table(rows) -> list:
-    head = ["GPU nodes", "GPU pods"] + [f"{t}: reference → new elements, mount ms, re-render ms" for _, t in PAGES] + [
-        "Reference provider filter per watch event (ms)"]
+    head = ["GPU nodes", "GPU pods"] + [f"{t}: elements ref → new; mount p50 [IQR] ref → new (ms); re-render p50 ref → new"
+                                        for _, t in PAGES] + ["Reference provider filter per watch event (ms)"]
     md = ["| " + " | ".join(head) + " |", "|---:|---:|" + "---|" * (len(head) - 2)]
     for n, r in rows:
         cells = [str(n), str(r["gpuPods"])]
         for k, _ in PAGES:
             a, ref = r["pages"][k]["amd"], r["pages"][k]["reference"]
-            cells.append(f"{ref['elements']} → {a['elements']}; {ref['mountMs']:.1f} → {a['mountMs']:.1f}; "
-                         f"{ref['rerenderMs']:.1f} → {a['rerenderMs']:.2f}")
+            iqr = lambda x: f"[{x['mountQ1']:.2f}–{x['mountQ3']:.2f}]" if "mountQ1" in x else ""
+            split = f" (vm {a['vmBuildMs']:.2f} + React {a['reactOnlyMs']:.2f})" if "vmBuildMs" in a else ""
+            cells.append(f"{ref['elements']} → {a['elements']}; {ref['mountMs']:.2f} {iqr(ref)} → {a['mountMs']:.2f} {iqr(a)} "
+                         f"{verdict(a, ref)}{split}; {ref['rerenderMs']:.2f} → {a['rerenderMs']:.2f}")
         cells.append(f"{r['referenceProviderFilterMs']:.1f}")
         md.append("| " + " | ".join(cells) + " |")
     return md
@@ -63,25 +84,33 @@ def table(rows) -> list:
 
 def main() -> int:
     p = argparse.ArgumentParser(description=__doc__.split("\n")[0])
-    p.add_argument("--sizes", default="1,2,4,8,16,64,256,1000")
-    p.add_argument("--reps", type=int, default=5)
+    p.add_argument("--sizes", default="1,2,4,8")
+    p.add_argument("--reps", type=int, default=31)
+    p.add_argument("--warm", type=int, default=50)
     p.add_argument("--reference", default="/root/reference")
-    p.add_argument("--out", default=os.path.join(ROOT, "profiles", "r4_render_compare"))
+    p.add_argument("--out", default=os.path.join(ROOT, "profiles", "r5_render_compare"))
+    p.add_argument("--allow-reference-exec", action="store_true",
+                   help="run the reference's page components (untrusted) in the sandboxed child process")
     args = p.parse_args()
+    if not args.allow_reference_exec:
+        raise SystemExit("render_compare runs the reference's sources (untrusted public content): "
+                         "pass --allow-reference-exec to run them in the sandboxed driver process (ADR 013)")
     if not os.path.isdir(os.path.join(args.reference, "src", "components")):
         raise SystemExit(f"no reference sources under {args.reference}")
     rows = []
     for s in args.sizes.split(","):
         n = int(s)
         t = time.time()
-        r = measure(n, args.reference, args.reps if n <= 256 else max(3, args.reps // 2))
+        r = measure(n, args.reference, args.reps, args.warm)
         rows.append((n, r))
         print(f"[render_compare] {n} nodes: {time.time() - t:.1f} s", file=sys.stderr, flush=True)
         with open(args.out + ".json", "w") as f:
             json.dump({"host": os.uname().nodename, "node": "v12", "rows": [{"gpu_nodes": n, **r} for n, r in rows]}, f,
                       indent=1)
-    md = ["Each page mounted on react@18.3.1 + react-dom@18.3.1 production UMD builds into a minimal JS DOM, "
-          "median of the reps. Reference = its page component (read from its sources, transpiled at run time) with "
+    md = ["Each page mounted on react@18.3.1 + react-dom@18.3.1 production UMD builds into a minimal JS DOM: "
+          f"{args.warm} untimed warm mounts of each side, then {max(15, args.reps)} interleaved reference / new pairs "
+          "(order alternating); p50 with the interquartile range. ≤: new p50 at most the reference's; ≈: within its "
+          "IQR; >: above it. Reference = its page component (read from its sources, transpiled at run time) with "
           "its data in context, its per-render aggregation included; re-render = a watch event (a new context "
           "value). New = this plugin's page, mount including the view-model built from a cold memo; re-render = "
           "the same watch event (a new store snapshot of the same data). First page of each pager. The last column "
