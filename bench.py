@@ -74,7 +74,16 @@ def parse_args(argv=None):
     p.add_argument("--control-plane", default="process", choices=["process", "thread"],
                    help="run the fake apiserver/Prometheus in a child process (default) or a thread of rank 0")
     p.add_argument("--out", default=None, help="also write the full result JSON here")
+    p.add_argument("--order", default="reference-first", choices=["reference-first", "amd-first"],
+                   help="which schedule's phases run first (the figures must not depend on it)")
     return p.parse_args(argv)
+
+
+def _p50(xs):
+    """p50 of a list of ms (rounded), None for none."""
+    from headlamp_intel_gpu_plugin_amd.utils.stats import summarize
+
+    return round(summarize(xs)["p50"], 3) if xs else None
 
 
 def main(argv=None) -> int:
@@ -163,14 +172,18 @@ def main(argv=None) -> int:
             # 30-minute window of 1,000 nodes take seconds each (up to 10 s of
             # server work, queued on its one evaluation thread; cached afterwards),
             # which a real Prometheus does not. Both schedules are warmed the same way.
-            call("cold", "reference", n=2)
-            # Measured baseline: the reference plugin's schedule (untimed region).
-            ref_cold = call("cold", "reference", n=3)
-            ref_cold_pages = call("coldPages", "reference", n=5)
-            call("pages", "reference", n=max(1, args.warmup))
-            ref_pages = call("pages", "reference", n=ref_steps)
-            ref = call("steps", "reference", n=max(3, ref_steps // 2))
-            ref_switch = call("switch", "reference", n=3)
+            def reference_phases():
+                """Measured baseline: the reference plugin's schedule (untimed region)."""
+                call("cold", "reference", n=2)
+                out = {"ref_cold": call("cold", "reference", n=3), "ref_cold_pages": call("coldPages", "reference", n=5)}
+                call("pages", "reference", n=max(1, args.warmup))
+                out["ref_pages"] = call("pages", "reference", n=ref_steps)
+                out["ref"] = call("steps", "reference", n=max(3, ref_steps // 2))
+                out["ref_switch"] = call("switch", "reference", n=3)
+                return out
+
+            if args.order == "reference-first":
+                R = reference_phases()
             # Flagship schedule.
             call("cold", "amd", n=2)
             amd_cold = call("cold", "amd", n=3)
@@ -196,6 +209,10 @@ def main(argv=None) -> int:
             amd_switch = call("switch", "amd", n=5)
             detail_out = call("detail", "amd", n=5)
             detail = detail_out["detail"]
+            if args.order == "amd-first":
+                R = reference_phases()
+            ref_cold, ref_cold_pages, ref_pages, ref, ref_switch = (R[k] for k in (
+                "ref_cold", "ref_cold_pages", "ref_pages", "ref", "ref_switch"))
             served = (server.stats() if args.control_plane == "process"
                       else {"server_requests": fc.stats(), "scrapes": scraper.scrapes if scraper else 0})
             for r in (ref_pages, amd_pages, ref, amd, ref_cold_pages, amd_cold_pages):
@@ -239,7 +256,9 @@ def main(argv=None) -> int:
                             "amd_p95": round(a["p95"], 3), "reference_p95": round(r["p95"], 3),
                             "requests": {"amd": result["amd_pages"][pg]["requestsPerClick"],
                                          "reference": result["ref_pages"][pg]["requestsPerClick"]},
-                            "speedup": round(r["p50"] / a["p50"], 2)}
+                            "speedup": round(r["p50"] / a["p50"], 2),
+                            "server_ms": {"amd": _p50(result["amd_pages"][pg].get("serverMs")),
+                                          "reference": _p50(result["ref_pages"][pg].get("serverMs"))}}
         value = sum(per_page[pg]["amd"] for pg in pages) / len(pages)
         ref_value = sum(per_page[pg]["reference"] for pg in pages) / len(pages)
         line = {
@@ -308,6 +327,10 @@ def main(argv=None) -> int:
                 pg: {"amd": round(summarize(result["amd_cold_pages"][pg]["latencies"])["p50"], 3),
                      "amd_first_content": round(summarize(result["amd_cold_pages"][pg]["firstMs"])["p50"], 3),
                      "amd_content": round(summarize(result["amd_cold_pages"][pg]["contentMs"])["p50"], 3),
+                     # the fake server's own time on the open's slowest request (X-Server-Ms), p50 over the opens:
+                     # the part of the figure that is the synthetic apiserver / Prometheus, not the plugin
+                     "amd_server_ms": _p50(result["amd_cold_pages"][pg].get("serverMs")),
+                     "reference_server_ms": _p50(result["ref_cold_pages"][pg].get("serverMs")),
                      "reference": round(summarize(result["ref_cold_pages"][pg]["latencies"])["p50"], 3),
                      "requests": {"amd": result["amd_cold_pages"][pg]["requests"],
                                   "reference": result["ref_cold_pages"][pg]["requests"]},
@@ -331,7 +354,10 @@ def main(argv=None) -> int:
                                            for pg, v in result["react_dom"].items()} or None),
             # Secondary: every page's data (all telemetry + series) in one cold open.
             "cold_open_p50_ms": {"amd": round(summarize(result["amd_cold"]["latencies"])["p50"], 3),
-                                 "reference": round(summarize(result["ref_cold"]["latencies"])["p50"], 3)},
+                                 "reference": round(summarize(result["ref_cold"]["latencies"])["p50"], 3),
+                                 "amd_server_ms": _p50(result["amd_cold"].get("serverMs")),
+                                 "reference_server_ms": _p50(result["ref_cold"].get("serverMs"))},
+            "schedule_order": args.order,
             # Part of the cold open spent rebuilding every view from an empty memo.
             "cold_render_p50_ms": (round(summarize(result["amd_cold"]["renderMs"])["p50"], 3)
                                    if result["amd_cold"].get("renderMs") else None),
@@ -346,7 +372,8 @@ def main(argv=None) -> int:
                                                             ("clusterWideListsPerOpen", "cluster_wide_lists"),
                                                             ("deviceConfigRequestsPerOpen", "deviceconfig_requests"),
                                                             ("listPaths", "list_paths"), ("rendered", "rendered"))
-                                       if i in v})
+                                       if i in v},
+                                    **({"server_ms": _p50(v["serverMs"])} if v.get("serverMs") else {}))
                             for k, v in result["detail"].items()},
             "rendered": {"gpu_nodes": rows["gpuNodes"], "gpu_pods": rows["gpuPods"],
                          "gpus_monitored": rows["gpusMonitored"], "gpu_cells": rows["gpuCells"],

@@ -258,6 +258,17 @@ export function shortProductName(deviceId, product) {
  * @returns {{ product: string, shortName: string, fromLabels: boolean, computePartition: string|null, memoryPartition: string|null, vram: string, cuCount: number }}
  */
 export function getNodeGpuModel(node) {
+  // A node object is an immutable snapshot of the watch: its model is read once.
+  const key = node && typeof node === 'object' ? node : null;
+  if (modelCache && key && modelCache.has(key)) return modelCache.get(key);
+  const m = readGpuModel(node);
+  if (modelCache && key) modelCache.set(key, m);
+  return m;
+}
+
+const modelCache = typeof WeakMap === 'function' ? new WeakMap() : null;
+
+function readGpuModel(node) {
   const productLabel = labellerValue(node, 'product-name');
   const labels = labelsOf(node);
   const cp = labels[LABEL_COMPUTE_PARTITION] || labellerValue(node, 'compute-partitioning-mode');
@@ -265,7 +276,7 @@ export function getNodeGpuModel(node) {
   const vram = labellerValue(node, 'vram');
   const cu = labellerValue(node, 'cu-count');
   const deviceId = labellerValue(node, 'device-id');
-  return {
+  return Object.freeze({
     product: productLabel ? String(productLabel).replace(/_/g, ' ') : MI355X.product,
     shortName: shortProductName(deviceId, productLabel),
     fromLabels: !!productLabel,
@@ -273,7 +284,7 @@ export function getNodeGpuModel(node) {
     memoryPartition: mp ? String(mp).toUpperCase() : null,
     vram: vram ? String(vram) : MI355X.hbmLabel,
     cuCount: cu ? parseCount(cu) : MI355X.computeUnits,
-  };
+  });
 }
 
 /** Column / row text for the node's GPU model, e.g. "MI355X" or "MI355X (CPX/NPS4)". */

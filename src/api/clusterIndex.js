@@ -9,14 +9,18 @@
  */
 
 import {
+  formatGpuModel,
+  getGpuResources,
   getNodeGpuAllocatable,
   getNodeGpuCount,
+  getNodeGpuModel,
   getNodePartitionCount,
   isNodeReady,
+  labellerValue,
   partitionsPerGpu,
 } from './amdNodes.js';
-import { getPodGpuCount, podPhase } from './amdPods.js';
-import { get, MI355X, pct } from './k8sCore.js';
+import { containerGpuEntries, getPodGpuCount, gpuContainers, gpuInitContainers, podPhase } from './amdPods.js';
+import { formatGpuResourceName, get, MI355X, pct } from './k8sCore.js';
 
 // Per-object facts the index needs, cached on the (immutable) object: a
 // watch event that changes one pod re-derives that pod only.
@@ -24,11 +28,19 @@ const nodeFactCache = new WeakMap();
 
 const podFactCache = new WeakMap();
 
-function nodeFacts(n) {
+/**
+ * What a GPU node object says, derived once per object — when the index is
+ * built, i.e. when the node list arrives, not when a page mounts: its GPU
+ * accounting, readiness, GPU model, resources, taints and node info (what the
+ * GPU Nodes summary rows and cards draw).
+ */
+export function nodeFacts(n) {
   let f = nodeFactCache.get(n);
   if (!f) {
     const cap = getNodeGpuCount(n);
     const pp = partitionsPerGpu(n);
+    const model = getNodeGpuModel(n);
+    const info = get(n, ['status', 'nodeInfo'], null) || {};
     f = {
       capacity: cap,
       allocatable: getNodeGpuAllocatable(n),
@@ -37,10 +49,24 @@ function nodeFacts(n) {
       partitionsPerGpu: pp,
       physicalGpus: cap > 0 ? Math.ceil(cap / pp) : 0,
       partitions: getNodePartitionCount(n),
+      model: model,
+      modelText: formatGpuModel(model),
+      capacityResources: getGpuResources(get(n, ['status', 'capacity'], null)),
+      allocatableResources: getGpuResources(get(n, ['status', 'allocatable'], null)),
+      taints: taintsText(n),
+      driverVersion: labellerValue(n, 'driver-version'),
+      osText: [info.osImage || '—', info.kernelVersion || '—', info.kubeletVersion || '—'].join(' · '),
     };
     nodeFactCache.set(n, f);
   }
   return f;
+}
+
+/** "key=value:Effect" per taint, or null (the reference models NodeSpec.taints, k8s.ts:92-122, but never shows them). */
+export function taintsText(node) {
+  const ts = get(node, ['spec', 'taints'], []);
+  if (!Array.isArray(ts) || ts.length === 0) return null;
+  return ts.map(function (t) { return (t.key || '') + (t.value ? '=' + t.value : '') + ':' + (t.effect || ''); }).join(', ');
 }
 
 /**
@@ -57,10 +83,37 @@ export function podFacts(p) {
       // The kubelet allocates devices at admission and releases them when the
       // pod terminates, so a bound non-terminal pod holds its GPUs.
       gpus: phase !== 'Succeeded' && phase !== 'Failed' ? getPodGpuCount(p) : 0,
+      // Its GPU containers' requests as the GPU Pods table lists them (pages/pods.js gpuContainerLines).
+      containers: containerLines(p),
     };
     podFactCache.set(p, f);
   }
   return f;
+}
+
+/**
+ * One {label, text} per GPU container, init containers first ("trainer",
+ * "GPU: 2"; "req=1 lim=2" when they differ) — the reference's
+ * GpuContainerList (PodsPage.tsx:49-88), init containers included.
+ */
+function containerLines(pod) {
+  const out = [];
+  function add(c, init) {
+    const es = containerGpuEntries(c);
+    const parts = [];
+    for (let i = 0; i < es.length; i++) {
+      const e = es[i];
+      const label = formatGpuResourceName(e.key);
+      if (e.request !== null && e.limit !== null && e.request === e.limit) parts.push(label + ': ' + e.request);
+      else parts.push(label + ': req=' + (e.request === null ? '—' : e.request) + ' lim=' + (e.limit === null ? '—' : e.limit));
+    }
+    out.push({ label: c.name + (init ? ' (init)' : ''), text: parts.join(', ') });
+  }
+  const ics = gpuInitContainers(pod);
+  for (let i = 0; i < ics.length; i++) add(ics[i], true);
+  const cs = gpuContainers(pod);
+  for (let i = 0; i < cs.length; i++) add(cs[i], false);
+  return out;
 }
 
 function sameArray(a, b) {

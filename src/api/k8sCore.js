@@ -195,7 +195,7 @@ export function pctToStatus(p) {
 }
 
 /** Bar colours matching the thresholds (AMD red for healthy "in use"). */
-export const BAR_COLORS = { ok: '#ed1c24', warn: '#f57c00', err: '#d32f2f', track: '#e0e0e0', mute: '#9e9e9e' };
+export const BAR_COLORS = { ok: '#ed1c24', okInferred: '#f27478', warn: '#f57c00', err: '#d32f2f', track: '#e0e0e0', mute: '#9e9e9e' };
 
 export function pctToColor(p) {
   if (p >= ERROR_PCT) return BAR_COLORS.err;

@@ -117,6 +117,66 @@ export function buildXgmiMatrix(gpuCount, measured, probed) {
   };
 }
 
+/** "i-j" link keys of the maps, made once: a lookup by an interned string skips hashing a new one. */
+const LINK_KEYS = [];
+function linkKey(i, j) {
+  const row = LINK_KEYS[i] || (LINK_KEYS[i] = []);
+  return row[j] || (row[j] = i + '-' + j);
+}
+
+const factCache = typeof WeakMap === 'function' ? new WeakMap() : null;
+
+/**
+ * What buildXgmiMatrix + isFullMesh say of a node's links, without the grid:
+ * {fullMesh, linksPerGpu, stats: {links, meanGBs, maxGBs} | null} — `stats`
+ * over the measured throughput of the xGMI links (every pair of distinct GPUs
+ * in the platform model; the pairs `probed` types XGMI otherwise). Cached on
+ * the map objects (the metrics client keeps a map's identity while its
+ * values are unchanged; the measured topology is static), so a page that
+ * re-renders, or mounts again, reads it once per answer.
+ * @param {number} n  GPUs of the node
+ * @param {Record<string, number>|null} measured
+ * @param {Record<string, {type: string, hops: number}>|null} probed  (non-empty, or null)
+ */
+export function linkFacts(n, measured, probed) {
+  const key = measured || probed;
+  if (factCache && key) {
+    const hit = factCache.get(key);
+    if (hit && hit.n === n && hit.measured === measured && hit.probed === probed) return hit.facts;
+  }
+  let linksPerGpu = probed ? 0 : Math.max(0, n - 1);
+  let full = n > 1;
+  let cnt = 0;
+  let sum = 0;
+  let max = 0;
+  if (probed || measured) {
+    for (let i = 0; i < n; i++) {
+      let links = 0;
+      for (let j = 0; j < n; j++) {
+        if (i === j) continue;
+        const k = linkKey(i, j);
+        let xgmi = true;
+        if (probed) {
+          const p = probed[k];
+          xgmi = !!p && p.type === 'XGMI';
+          if (!xgmi || p.hops !== 1) full = false;
+          if (xgmi) links++;
+        }
+        const v = measured && xgmi ? measured[k] : undefined;
+        if (typeof v === 'number') {
+          cnt++;
+          sum += v;
+          if (v > max) max = v;
+        }
+      }
+      if (probed && links > linksPerGpu) linksPerGpu = links;
+    }
+  }
+  const facts = { fullMesh: full, linksPerGpu: linksPerGpu, stats: cnt ? { links: cnt, meanGBs: sum / cnt, maxGBs: max } : null };
+  if (factCache && key) factCache.set(key, { n: n, measured: measured, probed: probed, facts: facts });
+  return facts;
+}
+
 /** True when the matrix is the full point-to-point mesh an 8×MI355X node should have. */
 export function isFullMesh(matrix) {
   if (matrix.size < 2) return false;

@@ -12,7 +12,7 @@
  * (src/components/View.tsx).
  */
 
-import { matrixCaption, pagerText } from './ir.js';
+import { matrixCaption, matrixSummary, pagerIdle, pagerText } from './ir.js';
 
 const NEEDS_ESC = /[&<>"]/;
 
@@ -85,9 +85,11 @@ function renderBlock(b) {
       );
     case 'matrix': {
       const m = b.matrix;
-      let h = '<table data-testid="xgmi-matrix" data-full-mesh="' + (b.fullMesh ? 'true' : 'false') + '" data-topology="' +
-        (b.measuredTopology ? 'measured' : 'assumed') + '" data-throughput="' + (b.measuredThroughput ? 'measured' : 'none') +
-        '"><caption>' + esc(matrixCaption(b)) + '</caption><thead><tr><th></th>';
+      const attrs = 'data-testid="xgmi-matrix" data-full-mesh="' + (b.fullMesh ? 'true' : 'false') + '" data-topology="' +
+        (b.measuredTopology ? 'measured' : 'assumed') + '" data-throughput="' + (b.measuredThroughput ? 'measured' : 'none') + '"';
+      // A closed matrix (GPU Nodes cards) is its summary, as the React renderer draws it.
+      if (b.open === false) return '<details ' + attrs + '><summary>' + esc(matrixCaption(b) + matrixSummary(b)) + '</summary></details>';
+      let h = '<table ' + attrs + '><caption>' + esc(matrixCaption(b) + matrixSummary(b)) + '</caption><thead><tr><th></th>';
       for (let j = 0; j < m.size; j++) h += '<th>GPU ' + j + '</th>';
       h += '</tr></thead><tbody>';
       for (let i = 0; i < m.size; i++) {
@@ -136,7 +138,10 @@ export function renderSection(s) {
 
 /** Pager → <nav>: the range shown, the name filter and previous / next buttons. */
 export function renderPager(p) {
-  return '<nav data-testid="pager" data-page="' + p.page + '" data-pages="' + p.pages + '" data-total="' + p.total + '">' +
+  const head = '<nav data-testid="pager" data-page="' + p.page + '" data-pages="' + p.pages + '" data-total="' + p.total + '"';
+  // Nothing to control (one page, no filter, default order): the count alone, as the React renderer draws it.
+  if (pagerIdle(p)) return head + ' data-idle="true"><span>' + esc(pagerText(p)) + '</span></nav>';
+  return head + '>' +
     '<input aria-label="Filter ' + esc(p.label || p.noun) + ' by name" value="' + esc(p.filter) + '">' +
     (p.sorts
       ? '<select aria-label="Sort ' + esc(p.label || p.noun) + '">' + p.sorts.map(function (o) {

@@ -105,6 +105,15 @@ export interface MatrixBlock {
   measuredTopology: boolean;
   /** Per-link throughput was measured (stock exporter xgmi_neighbor_* series). */
   measuredThroughput: boolean;
+  /** Renderers draw the grid (true) or its summary line with the grid one click away (false). */
+  open: boolean;
+  /** Facts pages/nodes.js matrixBlock reads from the link maps (topology.js linkFacts) without building
+   * the grid; absent on a hand-made block, where matrixCaption / matrixSummary read `matrix`. */
+  size?: number;
+  linksPerGpu?: number;
+  linkGBs?: number;
+  ringBusGBs?: number;
+  linkStats?: { links: number; maxGBs: number; meanGBs: number } | null;
 }
 
 /** [unix seconds, value] */
@@ -155,6 +164,8 @@ export interface PagerItem {
   /** the current order, when the list offers several (`sorts`) */
   sort?: string;
   sorts?: ReadonlyArray<{ value: string; label: string }>;
+  /** a ranked page past the end (the count shrank): the component moves to the last page */
+  beyond?: boolean;
 }
 
 export interface RefreshButton {
@@ -182,12 +193,14 @@ export function section(title: string, blocks: Block[], key?: string): Section;
 export function loader(title: string): LoaderItem;
 export function page(title: string | null, refresh: RefreshButton | null, items: Array<Section | LoaderItem | PagerItem>): PageVM;
 export function pager(
-  p: { page: number; pages: number; from: number; to: number; total: number; matched: number; filter: string; perPage: number },
+  p: { page: number; pages: number; from: number; to: number; total: number; matched: number; filter: string; perPage: number; beyond?: boolean },
   noun: string,
   sorting?: { sort?: string; sorts?: ReadonlyArray<{ value: string; label: string }>; label?: string }
 ): PagerItem;
 /** "Showing 17–24 of 1000 GPU nodes · page 3 of 125" */
 export function pagerText(p: PagerItem): string;
+/** One page, no filter, the default order: renderers show the count with the controls one click away. */
+export function pagerIdle(p: PagerItem): boolean;
 export function pagerOf(vm: PageVM | null): PagerItem | null;
 
 export interface Memo {
@@ -210,6 +223,12 @@ export function noteExpiry(t: number | null | undefined): void;
 
 /** Caption of the xGMI matrix: measured topology, or the platform model with measured throughput. */
 export function matrixCaption(b: MatrixBlock): string;
+/** " · measured: max X, mean Y GB/s over N links", or '' without measured throughput. */
+export function matrixSummary(b: MatrixBlock): string;
+/** "namespace/pod" or "free". */
+export function slotOwner(s: GpuSlot): string;
+/** Owners in runs: "GPU 0–3 ml/train-a · GPU 4–7 free". */
+export function slotsText(slots: GpuSlot[]): string;
 
 export function sections(vm: PageVM | Section | null): Section[];
 export function sectionTitles(vm: PageVM | Section | null): string[];

@@ -78,6 +78,18 @@ export function pager(p, noun, sorting) {
   return item;
 }
 
+/**
+ * True when a pager has nothing to control: the whole list on one page, no
+ * filter typed and the default order. Renderers then draw its count line
+ * alone (a cluster of a few nodes mounts no filter box, order menu or
+ * previous / next buttons); any of the three brings the controls back.
+ */
+export function pagerIdle(p) {
+  const filtered = typeof p.filter === 'string' && p.filter.trim() !== '';
+  const sorted = !!p.sorts && p.sorts.length > 0 && !!p.sort && p.sort !== p.sorts[0].value;
+  return p.pages <= 1 && !filtered && !sorted && !p.beyond;
+}
+
 /** "Showing 17–32 of 1000 GPU nodes" (with the filter's match count when one is set). */
 export function pagerText(p) {
   const f = p.filter ? p.filter.trim() : '';
@@ -196,8 +208,9 @@ export function createObjectCache() {
 
 /** Caption of the xGMI matrix: says whether the link topology was measured or is the platform model. */
 export function matrixCaption(b) {
-  const m = b.matrix;
-  const peak = m.size > 1 ? ' ' + m.cells[0][1].peakGBs : '';
+  // Blocks of pages/nodes.js matrixBlock carry the facts; a hand-made block only its grid.
+  const m = b.linksPerGpu !== undefined ? b : b.matrix;
+  const peak = m.size > 1 ? ' ' + (b.linkGBs !== undefined ? b.linkGBs : m.cells[0][1].peakGBs) : '';
   const kind = b.measuredTopology
     ? 'measured'
     : b.measuredThroughput
@@ -208,6 +221,62 @@ export function matrixCaption(b) {
     (b.fullMesh ? 'full mesh, ' + m.linksPerGpu + ' links/GPU' : 'partial') +
     ' · ' + m.linksPerGpu + '×' + peak + ' GB/s per GPU · ring collectives bound at ' + m.ringBusGBs + ' GB/s per link'
   );
+}
+
+/**
+ * The measured side of an xGMI matrix in one phrase (" · measured: max X,
+ * mean Y GB/s over N links"), '' when no link throughput was measured: what
+ * a closed matrix still says.
+ */
+export function matrixSummary(b) {
+  // pages/nodes.js matrixBlock reads the statistics from the link maps; a
+  // hand-made block (tests, text renderer) has only its grid.
+  const st = b.linkStats !== undefined ? b.linkStats : gridLinkStats(b.matrix);
+  return st ? ' · measured: max ' + st.maxGBs.toFixed(0) + ', mean ' + st.meanGBs.toFixed(0) + ' GB/s over ' + st.links + ' links' : '';
+}
+
+function gridLinkStats(m) {
+  let n = 0;
+  let sum = 0;
+  let max = 0;
+  for (let i = 0; i < m.size; i++) {
+    for (let j = 0; j < m.size; j++) {
+      const c = m.cells[i][j];
+      if (c.kind !== 'xgmi' || typeof c.measuredGBs !== 'number') continue;
+      n++;
+      sum += c.measuredGBs;
+      if (c.measuredGBs > max) max = c.measuredGBs;
+    }
+  }
+  return n ? { links: n, meanGBs: sum / n, maxGBs: max } : null;
+}
+
+/** One slot's owner as `data-slots` lists it: "namespace/pod", or "free". */
+export function slotOwner(s) {
+  return s.pod ? (s.namespace ? s.namespace + '/' : '') + s.pod : 'free';
+}
+
+function slotLabel(s) {
+  return s.partition === null || s.partition === undefined ? String(s.index) : s.board + '·' + s.partition;
+}
+
+/**
+ * A slot strip's owners in runs: "GPU 0–3 ml/train-a · GPU 4 free · …"
+ * (consecutive slots of one owner fold into one run).
+ */
+export function slotsText(slots) {
+  const runs = [];
+  for (let i = 0; i < slots.length; i++) {
+    const o = slotOwner(slots[i]);
+    const last = runs[runs.length - 1];
+    if (last && last.owner === o) last.to = slots[i];
+    else runs.push({ owner: o, from: slots[i], to: slots[i] });
+  }
+  return runs.map(function (r) {
+    const a = slotLabel(r.from);
+    const z = slotLabel(r.to);
+    return 'GPU ' + (a === z ? a : a + '–' + z) + ' ' + r.owner;
+  }).join(' · ');
 }
 
 // ---------------------------------------------------------------------------

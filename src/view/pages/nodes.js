@@ -5,18 +5,10 @@
  * that page asks Prometheus for (telemetryScope).
  */
 
-import {
-  formatGpuModel,
-  getGpuResources,
-  getNodeGpuCount,
-  getNodeGpuModel,
-  getNodePhysicalGpuCount,
-  isNodeReady,
-  labellerValue,
-} from '../../api/amdNodes.js';
-import { formatBytes, formatGpuResourceName, get, MI355X } from '../../api/k8sCore.js';
+import { nodeFacts } from '../../api/clusterIndex.js';
+import { AMD_GPU_RESOURCE, formatBytes, formatGpuResourceName, get, MI355X } from '../../api/k8sCore.js';
 import { SMALL_CLUSTER_NODES } from '../../api/series.js';
-import { buildGpuSlots, buildXgmiMatrix, isFullMesh } from '../../api/topology.js';
+import { buildGpuSlots, buildXgmiMatrix, linkFacts } from '../../api/topology.js';
 import { kv, loader, page, pager, row, section, status, table } from '../ir.js';
 import {
   ageText,
@@ -34,7 +26,6 @@ import {
   nodesPending,
   PODS_LOADING,
   podsPending,
-  tempCell,
 } from './common.js';
 import { nodeNameOf, nodePage, NODES_PER_PAGE, nodeSortOf, RANKED_NODE_SORTS, rankedPage } from './paging.js';
 
@@ -86,22 +77,69 @@ export function slotsBlock(node, podsOnNode, owners) {
   return { t: 'slots', slots: s.slots, exact: s.exact, partitionsPerGpu: s.partitionsPerGpu };
 }
 
-/** xGMI neighbour matrix block; `measuredTopology` when link hops came from the exporter. */
-export function matrixBlock(gpuCount, measured, probed) {
-  const hasProbe = !!probed && Object.keys(probed).length > 0;
-  const m = buildXgmiMatrix(gpuCount, measured, hasProbe ? probed : undefined);
-  return {
-    t: 'matrix',
-    matrix: m,
-    fullMesh: isFullMesh(m),
-    // Link types / hops come from the exporter's gpu_xgmi_link_hops (this
-    // repo's amdgpu-exporter); without them the matrix is the MI355X
-    // platform model, and only per-link throughput (stock exporter
-    // xgmi_neighbor_*_tx_throughput) is measured.
-    measuredTopology: hasProbe,
-    measuredThroughput: !!measured && Object.keys(measured).length > 0,
-  };
+/**
+ * xGMI neighbour matrix block; `measuredTopology` when link hops came from
+ * the exporter. `open` (default true): the renderers draw the 8 × 8 grid;
+ * false: its one-line summary, the grid one click away (a GPU Nodes card:
+ * eight grids per page would be most of the page's elements).
+ */
+export function matrixBlock(gpuCount, measured, probed, open) {
+  const n = gpuCount > 0 ? gpuCount : 0;
+  // The caption and summary come from the link maps, in one pass; the 8 × 8
+  // grid of cells is built on first read (a closed card never reads it).
+  return new MatrixBlock(n, measured && typeof measured === 'object' ? measured : null, hasKey(probed) ? probed : null,
+    open === undefined ? true : !!open);
 }
+
+const nonEmpty = typeof WeakMap === 'function' ? new WeakMap() : null;
+
+/** `o` has an own key (answered once per map object: a link map is a 56-key dictionary, slow to enumerate). */
+function hasKey(o) {
+  if (!o || typeof o !== 'object') return false;
+  if (nonEmpty && nonEmpty.has(o)) return nonEmpty.get(o);
+  let any = false;
+  for (const k in o) {
+    if (Object.prototype.hasOwnProperty.call(o, k)) {
+      any = true;
+      break;
+    }
+  }
+  if (nonEmpty) nonEmpty.set(o, any);
+  return any;
+}
+
+/**
+ * An xGMI matrix block (IR `matrix`): `fullMesh`, `linksPerGpu`,
+ * `ringBusGBs` and the measured-link statistics (`linkStats`) read from the
+ * maps (topology.js linkFacts, cached on them), as buildXgmiMatrix +
+ * isFullMesh would say; `matrix`, the grid itself, built when first read.
+ */
+function MatrixBlock(n, measured, probed, open) {
+  const f = linkFacts(n, measured, probed);
+  this.t = 'matrix';
+  this.fullMesh = f.fullMesh;
+  // Link types / hops come from the exporter's gpu_xgmi_link_hops (this
+  // repo's amdgpu-exporter); without them the matrix is the MI355X
+  // platform model, and only per-link throughput (stock exporter
+  // xgmi_neighbor_*_tx_throughput) is measured.
+  this.measuredTopology = !!probed;
+  this.measuredThroughput = !!f.stats;
+  this.open = open;
+  this.size = n;
+  this.linksPerGpu = f.linksPerGpu;
+  this.linkGBs = MI355X.xgmiLinkGBs;
+  this.ringBusGBs = f.linksPerGpu > 0 ? MI355X.xgmiLinkGBs : 0;
+  this.linkStats = f.stats;
+  this.measured = f.stats ? measured : null;
+  this.probed = probed;
+  this.grid = null;
+}
+
+Object.defineProperty(MatrixBlock.prototype, 'matrix', {
+  get: function () {
+    return this.grid || (this.grid = buildXgmiMatrix(this.size, this.measured || undefined, this.probed || undefined));
+  },
+});
 
 /**
  * Readiness as `kubectl get nodes` words it: "Ready", "Not Ready", and
@@ -109,48 +147,73 @@ export function matrixBlock(gpuCount, measured, probed) {
  * GPUs new pods cannot use, hence a warning.
  */
 export function nodeReadyCell(node) {
-  const ready = isNodeReady(node);
-  const cordoned = get(node, ['spec', 'unschedulable'], false) === true;
+  // One cell per node object (the summary row and the card both show it).
+  const key = node && typeof node === 'object' ? node : null;
+  if (readyCells && key && readyCells.has(key)) return readyCells.get(key);
+  const cell = readyCellOf(node);
+  if (readyCells && key) readyCells.set(key, cell);
+  return cell;
+}
+
+const readyCells = typeof WeakMap === 'function' ? new WeakMap() : null;
+
+function readyCellOf(node) {
+  const f = nodeFacts(node);
+  const ready = f.ready;
+  const cordoned = f.cordoned;
   const text = (ready ? 'Ready' : 'Not Ready') + (cordoned ? ', SchedulingDisabled' : '');
   return status(!ready ? 'error' : cordoned ? 'warning' : 'success', text);
 }
 
-/** "key=value:Effect" per taint (the reference models NodeSpec.taints, k8s.ts:92-122, but never shows them). */
+/** "key=value:Effect" per taint (clusterIndex.js taintsText, cached per node object). */
 export function formatTaints(node) {
-  const ts = get(node, ['spec', 'taints'], []);
-  if (!Array.isArray(ts) || ts.length === 0) return null;
-  return ts.map(function (t) { return (t.key || '') + (t.value ? '=' + t.value : '') + ':' + (t.effect || ''); }).join(', ');
+  return nodeFacts(node).taints;
 }
 
-function nodeCardRows(node, podsOnNode, stats, now, podsPend) {
-  const model = getNodeGpuModel(node);
-  const count = getNodeGpuCount(node);
-  const cap = getGpuResources(get(node, ['status', 'capacity'], null));
-  const alloc = getGpuResources(get(node, ['status', 'allocatable'], null));
-  const rows = [
-    row('Status', nodeReadyCell(node)),
-    row('GPU Model', model.product),
-  ];
-  const taints = formatTaints(node);
-  if (taints) rows.push(row('Taints', taints));
+function nodeCardRows(node, podsOnNode, now, podsPend) {
+  // Everything but the pods and the age was derived when the node list
+  // arrived (clusterIndex.js nodeFacts), not on this render.
+  const f = nodeFacts(node);
+  const model = f.model;
+  const count = f.capacity;
+  const cap = f.capacityResources;
+  const alloc = f.allocatableResources;
+  // Readiness, GPU model and age are the node's summary row on this page
+  // (the reference repeats them on its card, NodesPage.tsx:69-139); the card
+  // holds what the row does not.
+  const rows = [];
+  if (f.taints) rows.push(row('Taints', f.taints));
+  // One resource (the usual amd.com/gpu): its capacity and allocatable are
+  // said on the device row (the reference gives them a row each,
+  // NodesPage.tsx:98-113); several (partitioned resources) keep their rows.
+  const capKeys = Object.keys(cap);
+  const single = capKeys.length === 1 && capKeys[0] === AMD_GPU_RESOURCE && Object.keys(alloc).length <= 1;
   if (count > 0) {
-    const phys = getNodePhysicalGpuCount(node);
-    rows.push(row('GPU Devices (amd.com/gpu)', phys !== count ? count + ' (' + phys + ' × ' + model.shortName + ' in ' + model.computePartition + ')' : String(count)));
-    rows.push(row('HBM', formatBytes(phys * MI355X.hbmBytes) + ' (' + phys + ' × ' + model.vram + ')'));
+    const phys = f.physicalGpus;
+    const devices = phys !== count ? count + ' (' + phys + ' × ' + model.shortName + ' in ' + model.computePartition + ')' : String(count);
+    rows.push(row('GPU Devices (amd.com/gpu)', single
+      ? devices + ' · capacity ' + cap[AMD_GPU_RESOURCE] + ', allocatable ' + (alloc[AMD_GPU_RESOURCE] !== undefined ? alloc[AMD_GPU_RESOURCE] : '—')
+      : devices));
+    rows.push(row('HBM', hbmText(phys) + ' (' + phys + ' × ' + model.vram + ')'));
   }
-  for (const k in cap) rows.push(row(formatGpuResourceName(k) + ' (capacity)', cap[k]));
-  for (const k in alloc) rows.push(row(formatGpuResourceName(k) + ' (allocatable)', alloc[k]));
-  if (podsPend) rows.push(row('GPU Allocation', PODS_LOADING));
-  else if (stats) rows.push(row('GPU Allocation', allocationBar(stats.inUse, stats.allocatable || count)));
-  if (model.computePartition || model.memoryPartition) rows.push(row('Partition Mode', formatGpuModel(model)));
-  const drv = labellerValue(node, 'driver-version');
-  if (drv) rows.push(row('amdgpu Driver', drv));
+  if (!single || count === 0) {
+    for (const k in cap) rows.push(row(formatGpuResourceName(k) + ' (capacity)', cap[k]));
+    for (const k in alloc) rows.push(row(formatGpuResourceName(k) + ' (allocatable)', alloc[k]));
+  }
+  // The node's allocation bar is its summary row's (the reference's card has none either, NodesPage.tsx:69-139).
+  if (model.computePartition || model.memoryPartition) rows.push(row('Partition Mode', f.modelText));
+  if (f.driverVersion) rows.push(row('amdgpu Driver', f.driverVersion));
   rows.push(row('GPU Workload Pods', podsPend ? PODS_LOADING : podsOnNode.length > 0 ? podsOnNode.map(podName).join(', ') : '—'));
-  rows.push(row('OS Image', get(node, ['status', 'nodeInfo', 'osImage'], '—')));
-  rows.push(row('Kernel', get(node, ['status', 'nodeInfo', 'kernelVersion'], '—')));
-  rows.push(row('Kubelet', get(node, ['status', 'nodeInfo', 'kubeletVersion'], '—')));
-  rows.push(row('Age', ageText(node.metadata.creationTimestamp, now)));
+  // OS image, kernel and kubelet on one row (the reference: a row each, NodesPage.tsx:124-126).
+  rows.push(row('OS / Kernel / Kubelet', f.osText));
   return rows;
+}
+
+const hbmTexts = {};
+
+/** HBM of `phys` MI355X boards, formatted once per board count. */
+function hbmText(phys) {
+  return hbmTexts[phys] || (hbmTexts[phys] = formatBytes(phys * MI355X.hbmBytes));
 }
 
 /**
@@ -199,20 +262,19 @@ export function nodesView(ctx, opts) {
       const name = n.metadata.name;
       const d = inputs(n);
       const pods = d[0];
-      const stats = d[1];
       const own = d[2];
       const xg = d[3];
       const lk = d[4];
       // own / xg / lk keep their identity while their content is unchanged
       // (ownersByNode + the metrics client's structural sharing).
-      return memo('node-card:' + name, [n, pods, stats, own, xg, lk, podsPend], function () {
-        const blocks = [kv(nodeCardRows(n, pods, stats, now, podsPend))];
-        const count = getNodeGpuCount(n);
-        if (count > 0) {
+      return memo('node-card:' + name, [n, pods, own, xg, lk, podsPend], function () {
+        const blocks = [kv(nodeCardRows(n, pods, now, podsPend))];
+        const facts = nodeFacts(n);
+        if (facts.capacity > 0) {
           // Without the pods the strip is exact only from exporter owners.
           if (!podsPend || own) blocks.push(slotsBlock(n, podsPend ? NO_PODS : pods, own));
-          const phys = getNodePhysicalGpuCount(n);
-          if (phys > 1) blocks.push(matrixBlock(phys, xg, lk)); // no xGMI peers on a single-GPU node
+          const phys = facts.physicalGpus;
+          if (phys > 1) blocks.push(matrixBlock(phys, xg, lk, false)); // no xGMI peers on a single-GPU node
         }
         return section(name, blocks, n.metadata.uid || name);
       }, now);
@@ -259,10 +321,26 @@ export function ownersByNode(metrics) {
   return out;
 }
 
+const powerKeyCache = typeof WeakMap === 'function' ? new WeakMap() : null;
+const tempKeyCache = typeof WeakMap === 'function' ? new WeakMap() : null;
+
+/** `compute(gs)` once per GPU list of a telemetry snapshot (the client keeps the list's identity while unchanged). */
+function perGpuList(cache, metrics, compute) {
+  const gs = metrics && Array.isArray(metrics.gpus) ? metrics.gpus : null;
+  if (!gs) return compute([]);
+  if (cache && cache.has(gs)) return cache.get(gs);
+  const v = compute(gs);
+  if (cache) cache.set(gs, v);
+  return v;
+}
+
 /** Per-node GPU power from a telemetry snapshot: {byNode: {node: "watts|cap"}, sig} (whole watts). */
 export function nodePowerKeys(metrics) {
+  return perGpuList(powerKeyCache, metrics, powerKeys);
+}
+
+function powerKeys(gs) {
   const sum = {};
-  const gs = metrics && Array.isArray(metrics.gpus) ? metrics.gpus : [];
   for (let i = 0; i < gs.length; i++) {
     const g = gs[i];
     if (typeof g.powerWatts !== 'number' || !isFinite(g.powerWatts)) continue;
@@ -277,30 +355,43 @@ export function nodePowerKeys(metrics) {
 }
 
 /**
- * The hottest GPU of each node (junction °C, whole degrees) and its throttle
- * limit: "temp|limit" per node (limit 0 when the source reports none), so
- * the summary rebuilds only when a shown value changes.
+ * The hottest GPU of each node (junction °C, whole degrees), its throttle
+ * limit (the source's, else the MI355X's) and the status level its UNROUNDED
+ * reading has against that limit (common.js tempCell): "temp|limit|level"
+ * per node, so the summary rebuilds only when a shown value changes, and a
+ * GPU at 99.6 °C under a 100 °C limit is a warning here as on the Metrics
+ * page, not an error after rounding.
  */
 export function nodeTempKeys(metrics) {
+  return perGpuList(tempKeyCache, metrics, tempKeys);
+}
+
+function tempKeys(gs) {
   const hot = {};
-  const gs = metrics && Array.isArray(metrics.gpus) ? metrics.gpus : [];
   for (let i = 0; i < gs.length; i++) {
     const g = gs[i];
     if (typeof g.tempC !== 'number' || !isFinite(g.tempC)) continue;
-    const lim = typeof g.tempSlowdownC === 'number' && g.tempSlowdownC > 0 ? g.tempSlowdownC : 0;
+    const lim = typeof g.tempSlowdownC === 'number' && g.tempSlowdownC > 0 ? g.tempSlowdownC : MI355X.junctionSlowdownC;
     const e = hot[g.nodeName];
     if (!e || g.tempC > e[0]) hot[g.nodeName] = [g.tempC, lim];
   }
   const byNode = {};
   const names = Object.keys(hot).sort();
-  for (let i = 0; i < names.length; i++) byNode[names[i]] = Math.round(hot[names[i]][0]) + '|' + Math.round(hot[names[i]][1]);
+  for (let i = 0; i < names.length; i++) {
+    const t = hot[names[i]][0];
+    const lim = hot[names[i]][1];
+    const level = t >= lim ? 'error' : t >= lim - 10 ? 'warning' : 'ok';
+    byNode[names[i]] = Math.round(t) + '|' + Math.round(lim) + '|' + level;
+  }
   return { byNode: byNode, sig: names.map(function (n) { return n + '=' + byNode[n]; }).join(',') };
 }
 
 function nodeTempCell(key) {
   if (!key) return '—';
   const parts = key.split('|');
-  return tempCell({ tempC: Number(parts[0]), tempSlowdownC: Number(parts[1]) });
+  const text = parts[0] + ' °C';
+  if (parts[2] === 'error') return status('error', text + ' (throttling at ' + parts[1] + ' °C)');
+  return parts[2] === 'warning' ? status('warning', text) : text;
 }
 
 function nodePowerCell(key) {
@@ -350,11 +441,12 @@ function nodesHeadItems(ctx, now, powerByNode, pg, sort, podsPend, tempByNode) {
             const tk = tp[n.metadata.name];
             // Per-node stats keep their identity while unchanged (buildClusterIndex).
             return nodeSummaryRows(n, [st, withPower, pk, withTemp, tk, podsPend], function () {
-              const count = getNodeGpuCount(n);
+              const f = nodeFacts(n);
+              const count = f.capacity;
               return [
                 n.metadata.name,
                 nodeReadyCell(n),
-                formatGpuModel(getNodeGpuModel(n)),
+                f.modelText,
                 count > 0 ? String(count) : '—',
                 podsPend ? PODS_LOADING : allocationBar(st ? st.inUse : 0, (st && st.allocatable) || count),
                 podsPend ? PODS_LOADING : String(st ? st.pods : 0),

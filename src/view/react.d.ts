@@ -4,7 +4,7 @@
  * (tests/js/stubs/react.js) both satisfy it.
  */
 import type { ComponentType, CSSProperties, ReactElement, ReactNode } from 'react';
-import type { Block as IRBlock, Cell, MatrixBlock, PageVM, PagerItem, Section as IRSection, SeriesPoint } from './ir';
+import type { Block as IRBlock, Cell, GpuSlot, MatrixBlock, PageVM, PagerItem, Section as IRSection, SeriesPoint } from './ir';
 
 export interface ReactLike {
   createElement: (...args: never[]) => ReactElement;
@@ -25,7 +25,12 @@ export interface CommonComponentsLike {
 
 export const REQUIRED_COMPONENTS: ReadonlyArray<keyof CommonComponentsLike>;
 
-export function buttonStyle(disabled: boolean): CSSProperties;
+/** The renderer's stylesheet (classes amdgpu-*), added to the document once by ensureStyles. */
+export const PLUGIN_CSS: string;
+export const BUTTON_CLASS: string;
+export function ensureStyles(doc?: Document | null): boolean;
+export function barStyle(pct: number, color: string): CSSProperties;
+export function slotsGradient(slots: GpuSlot[]): string;
 export function sparklinePath(points: SeriesPoint[] | null | undefined, w: number, h: number): string | null;
 export function matrixCellColor(c: MatrixBlock['matrix']['cells'][number][number]): string;
 export function matrixCaption(b: MatrixBlock): string;

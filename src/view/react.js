@@ -26,7 +26,7 @@
  */
 
 import { BAR_COLORS, formatWatts } from '../api/k8sCore.js';
-import { matrixCaption, pagerText } from './ir.js';
+import { matrixCaption, matrixSummary, pagerIdle, pagerText, slotOwner, slotsText } from './ir.js';
 
 /** CommonComponents the renderer needs (reference src/components/OverviewPage.tsx:8-16). */
 export const REQUIRED_COMPONENTS = [
@@ -39,22 +39,61 @@ export const REQUIRED_COMPONENTS = [
   'StatusLabel',
 ];
 
-const MUTED = { fontSize: '13px', marginBottom: '6px', color: 'var(--mui-palette-text-secondary)' };
+/**
+ * The renderer's own styles, as classes of one stylesheet added to the
+ * document once (ensureStyles) instead of a style object on every element:
+ * a page mounts a few hundred elements, and react-dom sets an inline style
+ * property by property on each. Colours follow Headlamp's MUI theme through
+ * its CSS variables, as the inline styles did.
+ */
+export const PLUGIN_CSS = [
+  '.amdgpu-btn{padding:6px 16px;background-color:transparent;color:var(--mui-palette-primary-main,#ed1c24);' +
+    'border:1px solid var(--mui-palette-primary-main,#ed1c24);border-radius:4px;cursor:pointer;font-size:13px;font-weight:500}',
+  '.amdgpu-btn:disabled{cursor:not-allowed;opacity:.6}',
+  '.amdgpu-head{display:flex;justify-content:space-between;align-items:center;margin-bottom:20px}',
+  '.amdgpu-num{font-size:12px;font-variant-numeric:tabular-nums}',
+  '.amdgpu-bar{display:inline-block;padding-left:108px;line-height:16px;background-size:100px 8px;' +
+    'background-repeat:no-repeat;background-position:left center;font-size:12px;font-variant-numeric:tabular-nums}',
+  '.amdgpu-line{margin-bottom:2px;font-size:13px}',
+  '.amdgpu-muted{font-size:13px;margin-bottom:6px;color:var(--mui-palette-text-secondary)}',
+  '.amdgpu-slots{margin-top:12px;padding-top:18px;font-size:12px;background-size:100% 12px;background-repeat:no-repeat;' +
+    'background-position:left top}',
+  '.amdgpu-mx{margin-top:12px;overflow-x:auto}',
+  '.amdgpu-mx-closed{margin-top:12px;font-size:13px;color:var(--mui-palette-text-secondary)}',
+  '.amdgpu-mx table{border-collapse:collapse;font-size:11px}',
+  '.amdgpu-mx th{padding:2px 6px}',
+  '.amdgpu-mx tbody th{text-align:right}',
+  '.amdgpu-mx td{padding:2px 6px;text-align:center;border:1px solid var(--mui-palette-divider,#e0e0e0)}',
+  '.amdgpu-pct{margin-bottom:16px}',
+  '.amdgpu-pct-label{margin-bottom:8px;font-size:14px;color:var(--mui-palette-text-secondary)}',
+  '.amdgpu-pager{display:flex;align-items:center;gap:8px;flex-wrap:wrap;margin:0 0 16px}',
+  '.amdgpu-pager input{padding:4px 6px;font-size:13px;min-width:180px}',
+  '.amdgpu-pager select{padding:4px 6px;font-size:13px}',
+  '.amdgpu-pager span{font-size:13px;color:var(--mui-palette-text-secondary)}',
+  '.amdgpu-count{margin:0 0 16px;font-size:13px;color:var(--mui-palette-text-secondary)}',
+].join('\n');
 
-/** Style of the page refresh button (disabled while a refresh is in flight). */
-export function buttonStyle(disabled) {
-  return {
-    padding: '6px 16px',
-    backgroundColor: 'transparent',
-    color: 'var(--mui-palette-primary-main, #ed1c24)',
-    border: '1px solid var(--mui-palette-primary-main, #ed1c24)',
-    borderRadius: '4px',
-    cursor: disabled ? 'not-allowed' : 'pointer',
-    fontSize: '13px',
-    fontWeight: 500,
-    opacity: disabled ? 0.6 : 1,
-  };
+const styledDocuments = typeof WeakSet === 'function' ? new WeakSet() : null;
+
+/**
+ * Add PLUGIN_CSS to `doc` (default: the global document) once; nothing
+ * without a DOM (the harness React, server-side HTML). Returns true when the
+ * document holds the stylesheet.
+ */
+export function ensureStyles(doc) {
+  const d = doc || (typeof document !== 'undefined' ? document : null);
+  if (!d || !d.head || typeof d.createElement !== 'function' || !styledDocuments) return false;
+  if (styledDocuments.has(d)) return true;
+  const el = d.createElement('style');
+  el.setAttribute('data-amdgpu-styles', '');
+  el.textContent = PLUGIN_CSS;
+  d.head.appendChild(el);
+  styledDocuments.add(d);
+  return true;
 }
+
+/** Class of the refresh / pager / matrix buttons (PLUGIN_CSS: `:disabled` dims it). */
+export const BUTTON_CLASS = 'amdgpu-btn';
 
 /** SVG path of a sparkline over `points` ([t, v] pairs) in a w×h box; null below 2 points. */
 export function sparklinePath(points, w, h) {
@@ -78,6 +117,39 @@ export function sparklinePath(points, w, h) {
   return d;
 }
 
+/** Inline style of a one-element bar (InlineBar, class amdgpu-bar): `pct` of its 100 × 8 px track in `color`. */
+export function barStyle(pct, color) {
+  const p = Math.max(0, Math.min(100, pct));
+  return { backgroundImage: 'linear-gradient(to right, ' + color + ' ' + p + '%, ' + BAR_COLORS.track + ' ' + p + '%)' };
+}
+
+/** Background of a slot strip: one hard-edged segment per slot, held (dimmed when inferred) or free. */
+export function slotsGradient(slots) {
+  const pos = gradientStops(slots.length);
+  let out = 'linear-gradient(to right';
+  for (let i = 0; i < slots.length; i++) {
+    const s = slots[i];
+    const c = s.pod ? (s.inferred ? BAR_COLORS.okInferred : BAR_COLORS.ok) : BAR_COLORS.track;
+    out += ', ' + c + pos[i][0] + ', ' + c + pos[i][1] + pos[i][2];
+  }
+  return out + ')';
+}
+
+const stopCache = {};
+
+/** Per slot of an `n`-slot strip: its start, its end less a 1 px gap, and the gap ("transparent …"). */
+function gradientStops(n) {
+  if (stopCache[n]) return stopCache[n];
+  const out = [];
+  for (let i = 0; i < n; i++) {
+    const a = (100 * i / n).toFixed(3);
+    const z = (100 * (i + 1) / n).toFixed(3);
+    out.push([' ' + a + '%', ' calc(' + z + '% - 1px)', ', transparent calc(' + z + '% - 1px), transparent ' + z + '%']);
+  }
+  stopCache[n] = out;
+  return out;
+}
+
 /** Background of one xGMI matrix cell: measured utilisation shades it, otherwise link kind. */
 export function matrixCellColor(c) {
   if (c.kind === 'self') return 'transparent';
@@ -99,36 +171,36 @@ export function createRenderer(React, CC) {
   }
   const h = React.createElement;
   const Fragment = React.Fragment;
+  ensureStyles();
 
+  /**
+   * A 100 × 8 px bar and its text as ONE element: the bar is the element's
+   * background (a two-stop gradient: fill up to `pct`, track after), drawn in
+   * its left padding. A page holds two bars per GPU node row; four DOM nodes
+   * each (track, fill, text, wrapper) were a tenth of GPU Nodes' elements.
+   */
   function InlineBar(props) {
-    const track = props.pct === null
-      ? null
-      : h(
-        'div',
-        { style: { width: '100px', height: '8px', backgroundColor: BAR_COLORS.track, borderRadius: '4px', overflow: 'hidden', flexShrink: 0 } },
-        h('div', {
-          'data-pct': props.pct,
-          style: { width: props.pct + '%', height: '100%', backgroundColor: props.color, borderRadius: '4px', transition: 'width 0.4s ease' },
-        })
-      );
-    return h(
-      'div',
-      { style: { display: 'flex', alignItems: 'center', gap: '8px' } },
-      track,
-      h('span', { style: { fontSize: '12px', fontVariantNumeric: 'tabular-nums' } }, props.text)
-    );
+    return barNode(props.pct, props.color, props.text);
   }
 
-  /** One table / name-value cell. */
-  function Value(props) {
-    const v = props.v;
+  function barNode(pct, color, text) {
+    if (pct === null) return h('span', { className: 'amdgpu-num' }, text);
+    return h('span', { className: 'amdgpu-bar', 'data-pct': pct, 'data-color': color, style: barStyle(pct, color) }, text);
+  }
+
+  /**
+   * One table / name-value cell as React nodes, built inline: a plain string
+   * stays a string, and no component instance wraps a cell (a page holds a
+   * few hundred cells; a component per cell cost more than the elements).
+   */
+  function valueNode(v) {
     if (v === null || v === undefined) return null;
     if (typeof v === 'string' || typeof v === 'number') return String(v);
     switch (v.t) {
       case 'status':
         return h(CC.StatusLabel, { status: v.status }, v.text);
       case 'bar':
-        return h(InlineBar, { pct: v.pct, color: v.color, text: v.text });
+        return barNode(v.pct, v.color, v.text);
       case 'lines':
         return h(
           Fragment,
@@ -136,7 +208,7 @@ export function createRenderer(React, CC) {
           v.lines.map(function (l, i) {
             return h(
               'div',
-              { key: i, style: { marginBottom: '2px', fontSize: '13px' } },
+              { key: i, className: 'amdgpu-line' },
               l.label ? h('strong', null, l.label) : null,
               l.label ? ': ' : null,
               l.text
@@ -148,51 +220,62 @@ export function createRenderer(React, CC) {
     }
   }
 
+  /** One table / name-value cell (valueNode as a component: the Nodes-table columns, tests). */
+  function Value(props) {
+    return valueNode(props.v);
+  }
+
+  /**
+   * The per-GPU allocation strip as ONE element: one coloured segment per GPU
+   * (or partition) in its background, the owners as text under it ("GPU 0–3
+   * ml/train-a · GPU 4–7 free"), each slot's owner in `data-slots`.
+   */
   function Slots(props) {
-    const b = props.b;
-    const cols = Math.min(8, b.partitionsPerGpu > 1 ? b.partitionsPerGpu : 8);
+    return slotsNode(props.b);
+  }
+
+  function slotsNode(b, key) {
+    const caption = 'Per-GPU allocation' + (b.exact ? '' : ' (inferred from pod order — exporter pod labels unavailable)');
     return h(
       'div',
-      { style: { marginTop: '12px' } },
-      h('div', { style: MUTED }, 'Per-GPU allocation' + (b.exact ? '' : ' (inferred from pod order — exporter pod labels unavailable)')),
-      h(
-        'div',
-        { style: { display: 'grid', gridTemplateColumns: 'repeat(' + cols + ', minmax(0, 1fr))', gap: '4px' } },
-        b.slots.map(function (s) {
-          const label = s.partition === null || s.partition === undefined ? 'GPU ' + s.index : 'GPU ' + s.board + '·' + s.partition;
-          return h(
-            'div',
-            {
-              key: s.index,
-              'data-slot': s.index,
-              title: s.pod ? (s.namespace ? s.namespace + '/' : '') + s.pod : 'free',
-              style: {
-                padding: '6px 4px', borderRadius: '4px', fontSize: '11px', textAlign: 'center', overflow: 'hidden',
-                textOverflow: 'ellipsis', whiteSpace: 'nowrap', color: s.pod ? '#fff' : 'inherit',
-                backgroundColor: s.pod ? BAR_COLORS.ok : BAR_COLORS.track, opacity: s.inferred ? 0.8 : 1,
-              },
-            },
-            label,
-            h('br', null),
-            s.pod || 'free'
-          );
-        })
-      )
+      {
+        key: key,
+        'data-slots': b.slots.map(slotOwner).join(','),
+        title: caption,
+        className: 'amdgpu-slots',
+        style: { backgroundImage: slotsGradient(b.slots) },
+      },
+      slotsText(b.slots) + (b.exact ? '' : ' (inferred)')
     );
   }
 
+  /**
+   * The xGMI matrix: its caption and summary line, and the 8 × 8 grid when
+   * open. A block built closed (a GPU Nodes card) opens on click; the state
+   * stays with the mounted section.
+   */
   function Matrix(props) {
     const b = props.b;
+    const st = React.useState(b.open !== false);
+    const open = st[0];
+    const setOpen = st[1];
+    const toggle = h('button', {
+      'aria-expanded': open ? 'true' : 'false', className: BUTTON_CLASS,
+      onClick: function () { setOpen(!open); },
+    }, open ? 'Hide xGMI matrix' : 'Show xGMI matrix');
+    if (!open) {
+      return h('div', { 'data-matrix': 'closed', className: 'amdgpu-mx-closed' },
+        matrixCaption(b) + matrixSummary(b) + ' ', toggle);
+    }
     const m = b.matrix;
-    const cell = { padding: '2px 6px' };
     return h(
       'div',
-      { style: { marginTop: '12px', overflowX: 'auto' } },
-      h('div', { style: MUTED }, matrixCaption(b)),
+      { 'data-matrix': 'open', className: 'amdgpu-mx' },
+      h('div', { className: 'amdgpu-muted' }, matrixCaption(b) + matrixSummary(b) + ' ', toggle),
       h(
         'table',
-        { style: { borderCollapse: 'collapse', fontSize: '11px' } },
-        h('thead', null, h('tr', null, h('th', null), m.cells.map(function (_, j) { return h('th', { key: j, style: cell }, 'GPU ' + j); }))),
+        null,
+        h('thead', null, h('tr', null, h('th', null), m.cells.map(function (_, j) { return h('th', { key: j }, 'GPU ' + j); }))),
         h(
           'tbody',
           null,
@@ -200,7 +283,7 @@ export function createRenderer(React, CC) {
             return h(
               'tr',
               { key: i },
-              h('th', { style: { padding: '2px 6px', textAlign: 'right' } }, 'GPU ' + i),
+              h('th', null, 'GPU ' + i),
               rowCells.map(function (c, j) {
                 const txt = c.kind === 'self' ? '—' : c.measuredGBs !== null ? c.measuredGBs.toFixed(0) : c.kind === 'xgmi' ? '•' : c.kind;
                 return h(
@@ -208,10 +291,7 @@ export function createRenderer(React, CC) {
                   {
                     key: j,
                     title: c.kind === 'xgmi' ? c.hops + ' hop · ' + c.peakGBs + ' GB/s peak' : c.kind,
-                    style: {
-                      padding: '2px 6px', textAlign: 'center', border: '1px solid var(--mui-palette-divider, #e0e0e0)',
-                      backgroundColor: matrixCellColor(c),
-                    },
+                    style: { backgroundColor: matrixCellColor(c) },
                   },
                   txt
                 );
@@ -261,32 +341,40 @@ export function createRenderer(React, CC) {
   /** Column descriptors of a `table` block: getter i reads cell i of the row array. */
   function tableColumns(b) {
     return b.columns.map(function (label, i) {
-      return { label: label, getter: function (r) { return h(Value, { v: r[i] }); } };
+      return { label: label, getter: function (r) { return valueNode(r[i]); } };
     });
   }
 
   function Block(props) {
-    const b = props.b;
+    return blockNode(props.b);
+  }
+
+  /**
+   * One IR block as React nodes, built inline (no component of its own; the
+   * matrix, which keeps open / closed state, is the one that has one).
+   */
+  function blockNode(b, key) {
     switch (b.t) {
       case 'kv':
         return h(CC.NameValueTable, {
-          rows: b.rows.map(function (r) { return { name: r.name, value: h(Value, { v: r.value }) }; }),
+          key: key,
+          rows: b.rows.map(function (r) { return { name: r.name, value: valueNode(r.value) }; }),
         });
       case 'table':
-        return h(CC.SimpleTable, { columns: tableColumns(b), data: b.rows });
+        return h(CC.SimpleTable, { key: key, columns: tableColumns(b), data: b.rows });
       case 'pctbar':
         return h(
           'div',
-          { style: { marginBottom: '16px' } },
-          h('div', { style: { marginBottom: '8px', fontSize: '14px', color: 'var(--mui-palette-text-secondary)' } }, b.label),
+          { key: key, className: 'amdgpu-pct' },
+          h('div', { className: 'amdgpu-pct-label' }, b.label),
           h(CC.PercentageBar, { data: b.data, total: b.total })
         );
       case 'slots':
-        return h(Slots, { b: b });
+        return slotsNode(b, key);
       case 'matrix':
-        return h(Matrix, { b: b });
+        return h(Matrix, { key: key, b: b });
       case 'series':
-        return h(Series, { b: b });
+        return h(Series, { key: key, b: b });
       default:
         return null;
     }
@@ -298,7 +386,7 @@ export function createRenderer(React, CC) {
     return h(
       CC.SectionBox,
       { title: s.title },
-      s.blocks.map(function (b, i) { return h(Block, { key: i, b: b }); })
+      s.blocks.map(function (b, i) { return blockNode(b, i); })
     );
   }
   // View-models return the same section object while its inputs are
@@ -314,16 +402,25 @@ export function createRenderer(React, CC) {
    */
   function Pager(props) {
     const p = props.p;
+    const shown = React.useState(false);
+    // Nothing to control (ir.js pagerIdle): the count line and one button
+    // that brings up the filter box and the order menu.
+    if (pagerIdle(p) && !shown[0]) {
+      return h('div', { 'data-pager': p.label || p.noun, 'data-idle': 'true', className: 'amdgpu-count' }, pagerText(p) + ' ',
+        h('button', {
+          'aria-label': 'Filter or sort ' + (p.label || p.noun), className: BUTTON_CLASS,
+          onClick: function () { shown[1](true); },
+        }, p.sorts ? 'Filter / sort' : 'Filter'));
+    }
     const prev = p.page > 0;
     const next = p.page + 1 < p.pages;
     return h(
       'div',
-      { 'data-pager': p.label || p.noun, style: { display: 'flex', alignItems: 'center', gap: '8px', flexWrap: 'wrap', margin: '0 0 16px' } },
+      { 'data-pager': p.label || p.noun, className: 'amdgpu-pager' },
       h('input', {
         'aria-label': 'Filter ' + (p.label || p.noun) + ' by name',
         placeholder: 'Filter by name',
         value: p.filter,
-        style: { padding: '4px 6px', fontSize: '13px', minWidth: '180px' },
         onChange: function (e) { if (props.onFilter) props.onFilter(e.target.value); },
       }),
       p.sorts
@@ -332,19 +429,18 @@ export function createRenderer(React, CC) {
           {
             'aria-label': 'Sort ' + (p.label || p.noun),
             value: p.sort,
-            style: { padding: '4px 6px', fontSize: '13px' },
             onChange: function (e) { if (props.onSort) props.onSort(e.target.value); },
           },
           p.sorts.map(function (o) { return h('option', { key: o.value, value: o.value }, o.label); })
         )
         : null,
-      h('span', { style: { fontSize: '13px', color: 'var(--mui-palette-text-secondary)' } }, pagerText(p)),
+      h('span', null, pagerText(p)),
       h('button', {
-        'aria-label': 'Previous page', disabled: !prev, style: buttonStyle(!prev),
+        'aria-label': 'Previous page', disabled: !prev, className: BUTTON_CLASS,
         onClick: function () { if (prev && props.onPage) props.onPage(p.page - 1); },
       }, '‹ Prev'),
       h('button', {
-        'aria-label': 'Next page', disabled: !next, style: buttonStyle(!next),
+        'aria-label': 'Next page', disabled: !next, className: BUTTON_CLASS,
         onClick: function () { if (next && props.onPage) props.onPage(p.page + 1); },
       }, 'Next ›')
     );
@@ -356,7 +452,7 @@ export function createRenderer(React, CC) {
     const header = vm.title
       ? h(
         'div',
-        { style: { display: 'flex', justifyContent: 'space-between', alignItems: 'center', marginBottom: '20px' } },
+        { className: 'amdgpu-head' },
         h(CC.SectionHeader, { title: vm.title }),
         vm.refresh
           ? h(
@@ -365,7 +461,7 @@ export function createRenderer(React, CC) {
               onClick: function () { if (onRefresh) onRefresh(); },
               disabled: vm.refresh.disabled,
               'aria-label': vm.refresh.ariaLabel,
-              style: buttonStyle(vm.refresh.disabled),
+              className: BUTTON_CLASS,
             },
             vm.refresh.label
           )
@@ -386,6 +482,7 @@ export function createRenderer(React, CC) {
 
   return {
     Value: Value,
+    valueNode: valueNode,
     InlineBar: InlineBar,
     Slots: Slots,
     Matrix: Matrix,

@@ -28,7 +28,7 @@ export function render(element, options) {
     byAttr: function (name) { return r.queryAll(function (n) { return n.props[name] !== undefined; }); },
     /** An attribute as the DOM reports it (a string), or null. */
     attr: function (node, name) {
-      const v = node.props[name];
+      const v = node.props[name === 'class' ? 'className' : name];
       return v === undefined || v === null || v === false ? null : String(v);
     },
     style: function (node) { return node.props.style || {}; },

@@ -255,9 +255,21 @@ describe('nodesView: hottest GPU', () => {
     expect(col).toBe(t.columns.length - 2); // after Power, before Age
     expect(t.rows[0][col]).toEqual({ t: 'status', status: 'warning', text: '94 °C' });
     expect(t.rows[1][col]).toBe('—');
-    expect(nodeTempKeys(metrics).byNode).toEqual({ g0: '94|100' });
+    expect(nodeTempKeys(metrics).byNode).toEqual({ g0: '94|100|warning' });
     const plain = firstTable(findSection(nodesView(ctx, { now: NOW }), 'GPU Node Summary'));
     expect(plain.columns).not.toContain('Hottest GPU');
+  });
+
+  it('classifies the hottest GPU from its unrounded reading, as the Metrics page does (99.6 °C under 100 °C is a warning)', () => {
+    const ctx = makeContext({ nodes: [makeGpuNode('g0'), makeGpuNode('g1'), makeGpuNode('g2')] });
+    const g = (node, t) => ({ nodeName: node, gpu: '0', powerWatts: 700, powerCapWatts: 1400, tempC: t, tempSlowdownC: 100 });
+    const metrics = { source: 'amd-exporter', gpus: [g('g0', 99.6), g('g1', 100), g('g2', 89.5)], xgmi: {}, links: {} };
+    const t = firstTable(findSection(nodesView(ctx, { now: NOW, metrics }), 'GPU Node Summary'));
+    const col = t.columns.indexOf('Hottest GPU');
+    expect(t.rows[0][col]).toEqual({ t: 'status', status: 'warning', text: '100 °C' });
+    expect(tempCell(metrics.gpus[0])).toEqual({ t: 'status', status: 'warning', text: '100 °C' });
+    expect(t.rows[1][col]).toEqual({ t: 'status', status: 'error', text: '100 °C (throttling at 100 °C)' });
+    expect(t.rows[2][col]).toBe('90 °C'); // 89.5 is below the warning band, though it rounds to 90
   });
 });
 
@@ -270,7 +282,9 @@ describe('nodesView', () => {
     expect(t.rows[0][1]).toEqual({ t: 'status', status: 'warning', text: 'Ready, SchedulingDisabled' });
     const card = findSection(vm, 'g0');
     expect(rowValue(card, 'Taints')).toBe('amd.com/gpu=present:NoSchedule, node.kubernetes.io/unschedulable:NoSchedule');
-    expect(rowValue(card, 'Status').text).toBe('Ready, SchedulingDisabled');
+    // readiness, model and age are the summary row's, not repeated on the card
+    expect(rowValue(card, 'Status')).toBeUndefined();
+    expect(rowValue(card, 'GPU Model')).toBeUndefined();
     // an untainted, schedulable node: plain "Ready", no Taints row
     const plain = nodesView(makeContext({ nodes: [makeGpuNode('g1')] }), opts);
     expect(rowValue(findSection(plain, 'g1'), 'Taints')).toBeUndefined();
@@ -300,11 +314,12 @@ describe('nodesView', () => {
   it('renders one card per node with HBM and workload pods', () => {
     const ctx = makeContext({ nodes: [makeGpuNode('g0')], pods: [makeGpuPod('a', { node: 'g0', gpus: 2 })] });
     const s = findSection(nodesView(ctx, opts), 'g0');
-    expect(rowValue(s, 'GPU Devices (amd.com/gpu)')).toBe('8');
+    // one amd.com/gpu resource: capacity and allocatable on the device row; OS, kernel and kubelet on one row
+    expect(rowValue(s, 'GPU Devices (amd.com/gpu)')).toBe('8 · capacity 8, allocatable 8');
     expect(rowValue(s, 'HBM')).toBe('2.25 TiB (8 × 288G)');
     expect(rowValue(s, 'GPU Workload Pods')).toBe('a');
-    expect(rowValue(s, 'GPU (capacity)')).toBe('8');
-    expect(rowValue(s, 'Kubelet')).toBe('v1.31.2');
+    expect(rowValue(s, 'GPU (capacity)')).toBeUndefined();
+    expect(rowValue(s, 'OS / Kernel / Kubelet')).toContain(' · v1.31.2');
   });
   it('adds per-GPU slots and the xGMI matrix to each card', () => {
     const ctx = makeContext({ nodes: [makeGpuNode('g0')], pods: [makeGpuPod('a', { node: 'g0', gpus: 3 })] });

@@ -188,7 +188,9 @@ describe('route components', () => {
     expect(html).toContain('mi355x-0');
     expect(html).toContain('mi355x-1');
     expect(html).not.toContain('cpu-0');
-    expect(r.queryAll((n) => n.props['data-slot'] !== undefined)).toHaveLength(16);
+    // one slot strip and one (closed) xGMI matrix per node
+    expect(r.queryAll((n) => n.props['data-slots'] !== undefined)).toHaveLength(2);
+    expect(r.queryAll((n) => n.props['data-matrix'] === 'closed')).toHaveLength(2);
   });
 
   it('Pods page lists GPU pods only', async () => {

@@ -166,6 +166,32 @@ describe('properties', () => {
       expect(isFullMesh(buildXgmiMatrix(n))).toBe(n > 1);
     }
   });
+
+  it('a matrix block\'s facts and summary, read from the link maps, are what its grid says', async () => {
+    const { matrixBlock } = await import('../../src/view/pages/nodes.js');
+    const { matrixSummary } = await import('../../src/view/ir.js');
+    const r = rng(77);
+    for (let round = 0; round < 200; round++) {
+      const n = int(r, 0, 9);
+      const probed = r() < 0.5 ? {} : null;
+      const measured = r() < 0.7 ? {} : null;
+      for (let i = 0; i < n; i++) {
+        for (let j = 0; j < n; j++) {
+          if (i === j) continue;
+          if (probed && r() < 0.85) probed[i + '-' + j] = { type: r() < 0.8 ? 'XGMI' : 'PCIE', hops: r() < 0.9 ? 1 : 2 };
+          if (measured && r() < 0.6) measured[i + '-' + j] = Math.round(r() * 100);
+        }
+      }
+      const b = matrixBlock(n, measured, probed, false);
+      const grid = buildXgmiMatrix(n, measured, probed && Object.keys(probed).length ? probed : undefined);
+      expect(b.fullMesh).toBe(isFullMesh(grid));
+      expect(b.linksPerGpu).toBe(grid.linksPerGpu);
+      expect(b.ringBusGBs).toBe(grid.ringBusGBs);
+      // the summary from the maps = the summary from the cells
+      expect(matrixSummary(b)).toBe(matrixSummary({ matrix: grid }));
+      expect(b.matrix.cells).toEqual(grid.cells);
+    }
+  });
 });
 
 describe('malformed cluster objects (what a real apiserver, an old CRD version or a half-written object can hand over)', () => {

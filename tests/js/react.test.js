@@ -9,7 +9,7 @@
  */
 import React, { render } from './stubs/react.js';
 import * as CC from './stubs/CommonComponents.js';
-import { createRenderer, REQUIRED_COMPONENTS, buttonStyle, matrixCaption, matrixCellColor, sparklinePath } from '../../src/view/react.js';
+import { BUTTON_CLASS, createRenderer, ensureStyles, PLUGIN_CSS, REQUIRED_COMPONENTS, matrixCaption, matrixCellColor, sparklinePath } from '../../src/view/react.js';
 import { bar, kv, lines, loader, page, pctbar, row, section, status, table } from '../../src/view/ir.js';
 import { clearViewMemo } from '../../src/view/pages/common.js';
 import { matrixBlock, slotsBlock } from '../../src/view/pages/nodes.js';
@@ -70,17 +70,31 @@ describe('Page', () => {
     expect(onRefresh).toHaveBeenCalledTimes(2);
   });
 
-  it('disabled refresh button does not fire and uses the not-allowed style', () => {
+  it('disabled refresh button does not fire; its class dims it and shows the not-allowed cursor', () => {
     const v = setup();
     const onRefresh = vi.fn();
     const vm = page('T', { label: 'Refreshing...', ariaLabel: 'Refresh metrics', disabled: true }, []);
     const r = render(h(v.Page, { vm, onRefresh }));
     const btn = r.getByLabelText('Refresh metrics');
     expect(btn.props.disabled).toBe(true);
-    expect(btn.props.style).toEqual(buttonStyle(true));
-    expect(btn.props.style.cursor).toBe('not-allowed');
+    expect(btn.props.className).toBe(BUTTON_CLASS);
+    expect(PLUGIN_CSS).toContain('.' + BUTTON_CLASS + ':disabled{cursor:not-allowed;opacity:.6}');
     r.click(btn);
     expect(onRefresh).not.toHaveBeenCalled();
+  });
+
+  it('the stylesheet is added to a document once; nothing without a DOM', () => {
+    const appended = [];
+    const doc = {
+      head: { appendChild: (el) => appended.push(el) },
+      createElement: (tag) => ({ tag, attrs: {}, setAttribute(k, v) { this.attrs[k] = v; }, textContent: '' }),
+    };
+    expect(ensureStyles(doc)).toBe(true);
+    expect(ensureStyles(doc)).toBe(true);
+    expect(appended).toHaveLength(1);
+    expect(appended[0].tag).toBe('style');
+    expect(appended[0].textContent).toBe(PLUGIN_CSS);
+    expect(ensureStyles({})).toBe(false);
   });
 
   it('maps loader and section items in order', () => {
@@ -112,8 +126,10 @@ describe('blocks', () => {
     const p = only(r, CC.SimpleTable);
     expect(p.columns.map((c) => c.label)).toEqual(['Node', 'GPUs']);
     expect(p.data).toBe(rows);
-    expect(p.columns[0].getter(rows[0]).props.v).toBe('n0');
-    expect(p.columns[1].getter(rows[1]).props.v).toEqual(status('warning', '4'));
+    // cells are built inline: a string stays a string, a status cell is the StatusLabel itself
+    expect(p.columns[0].getter(rows[0])).toBe('n0');
+    expect(p.columns[1].getter(rows[1]).type).toBe(CC.StatusLabel);
+    expect(p.columns[1].getter(rows[1]).props.status).toBe('warning');
     expect(r.byTag('tr')).toHaveLength(3);
     expect(r.byTag('th').map((n) => n.children[0])).toEqual(['Node', 'GPUs']);
   });
@@ -129,14 +145,15 @@ describe('blocks', () => {
     expect(r.getByTestId('percentage-bar').props['data-total']).toBe(8);
   });
 
-  it('bar cell → inline track with its fill width and text', () => {
+  it('bar cell → ONE element: its fill as a gradient background up to the percentage, and its text', () => {
     const v = setup();
     const r = render(h(v.Value, { v: bar(3, 8, 38, '#4caf50', '3/8 (38%)') }));
     const fill = r.queryAll((n) => n.props['data-pct'] !== undefined);
     expect(fill).toHaveLength(1);
-    expect(fill[0].props.style.width).toBe('38%');
-    expect(fill[0].props.style.backgroundColor).toBe('#4caf50');
+    expect(fill[0].props.style.backgroundImage).toBe('linear-gradient(to right, #4caf50 38%, #e0e0e0 38%)');
+    expect(fill[0].props['data-color']).toBe('#4caf50');
     expect(r.text()).toBe('3/8 (38%)');
+    expect(r.queryAll((n) => typeof n.tag === 'string')).toHaveLength(1);
   });
 
   it('bar cell without a percentage draws only the text', () => {
@@ -167,17 +184,32 @@ describe('blocks', () => {
     expect(r.text()).toBe('S');
   });
 
-  it('slots → one tile per GPU, pod owners and free slots labelled', () => {
+  it('slots → ONE element: a segment per GPU in its background, owners in runs as its text', () => {
     const v = setup();
     const node = makeGpuNode('mi355x-0');
     const pods = [makeGpuPod('train-a', { gpus: 2 }), makeGpuPod('train-b', { gpus: 1 })];
     const b = slotsBlock(node, pods, null);
     const r = render(h(v.Block, { b }));
-    const tiles = r.queryAll((n) => n.props['data-slot'] !== undefined);
-    expect(tiles).toHaveLength(8);
-    expect(tiles.filter((t) => t.props.title === 'free')).toHaveLength(5);
-    expect(r.text()).toContain('inferred from pod order');
-    expect(tiles[0].props.title).toBe('ml/train-a');
+    const strip = r.queryAll((n) => n.props['data-slots'] !== undefined);
+    expect(strip).toHaveLength(1);
+    expect(strip[0].props['data-slots'].split(',')).toEqual(['ml/train-a', 'ml/train-a', 'ml/train-b', 'free', 'free', 'free', 'free', 'free']);
+    expect(r.text()).toBe('GPU 0–1 ml/train-a · GPU 2 ml/train-b · GPU 3–7 free (inferred)');
+    expect(strip[0].props.title).toContain('inferred from pod order');
+    expect(strip[0].props.style.backgroundImage.split('#e0e0e0').length - 1).toBe(10); // 5 free segments, 2 stops each
+    expect(r.queryAll((n) => typeof n.tag === 'string')).toHaveLength(1);
+  });
+
+  it('a matrix built closed shows its summary and opens on click', () => {
+    const v = setup();
+    const r = render(h(v.Block, { b: matrixBlock(8, { '0-1': 40, '1-0': 60 }, null, false) }));
+    expect(r.queryAll((n) => n.tag === 'td')).toHaveLength(0);
+    expect(r.text()).toContain('measured: max 60, mean 50 GB/s over 2 links');
+    const btn = r.queryAll((n) => n.tag === 'button')[0];
+    expect(btn.props['aria-expanded']).toBe('false');
+    r.click(btn);
+    expect(r.queryAll((n) => n.tag === 'td')).toHaveLength(64);
+    r.click(r.queryAll((n) => n.tag === 'button')[0]);
+    expect(r.queryAll((n) => n.tag === 'td')).toHaveLength(0);
   });
 
   it('matrix → 8×8 table, self cells dashed, caption says the topology is assumed', () => {

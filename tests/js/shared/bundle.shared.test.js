@@ -65,6 +65,9 @@ describe('shared: the built bundle on the host React (' + tier + ')', () => {
     const a = render(h(nodes));
     await a.settle();
     expect(a.text()).toContain('GPU Node Summary');
+    // one page of nodes: the pager is its count line until asked for its controls
+    a.click(a.byLabel('Filter or sort GPU nodes'));
+    await a.settle();
     expect(a.byLabel('Sort GPU nodes')).toBeTruthy();
     a.unmount();
     const b = render(lib.registry.details[0]({ resource: { kind: 'Node', jsonData: makeGpuNode('mi355x-1') } }));

@@ -49,13 +49,13 @@ describe('shared: Page (' + tier + ')', () => {
     r.unmount();
   });
 
-  it('a disabled Refresh button does not fire and shows the not-allowed cursor', () => {
+  it('a disabled Refresh button does not fire and carries the button class (its :disabled style)', () => {
     const onRefresh = vi.fn();
     const vm = page('T', { label: 'Refreshing...', ariaLabel: 'Refresh metrics', disabled: true }, []);
     const r = render(h(v().Page, { vm, onRefresh }));
     const btn = r.byLabel('Refresh metrics');
     expect(r.isDisabled(btn)).toBe(true);
-    expect(r.style(btn).cursor).toBe('not-allowed');
+    expect(r.attr(btn, 'class')).toBe('amdgpu-btn');
     r.click(btn);
     expect(onRefresh).not.toHaveBeenCalled();
     r.unmount();
@@ -98,11 +98,12 @@ describe('shared: blocks (' + tier + ')', () => {
     r.unmount();
   });
 
-  it('bar cell → a fill of its percentage width and colour, and its text', () => {
+  it('bar cell → one element carrying its percentage and colour, and its text', () => {
     const r = render(h(v().Value, { v: bar(3, 8, 38, '#4caf50', '3/8 (38%)') }));
     const fill = r.byAttr('data-pct');
     expect(fill).toHaveLength(1);
-    expect(r.style(fill[0]).width).toBe('38%');
+    expect(r.attr(fill[0], 'data-pct')).toBe('38');
+    expect(r.attr(fill[0], 'data-color')).toBe('#4caf50');
     expect(r.text()).toBe('3/8 (38%)');
     r.unmount();
   });
@@ -135,14 +136,15 @@ describe('shared: blocks (' + tier + ')', () => {
     r.unmount();
   });
 
-  it('slots → one tile per GPU, owners and free slots titled, inferred allocation said so', () => {
+  it('slots → one strip: each slot\'s owner, the owners in runs as text, inferred allocation said so', () => {
     const b = slotsBlock(makeGpuNode('mi355x-0'), [makeGpuPod('train-a', { gpus: 2 }), makeGpuPod('train-b', { gpus: 1 })], null);
     const r = render(h(v().Block, { b }));
-    const tiles = r.byAttr('data-slot');
-    expect(tiles).toHaveLength(8);
-    expect(tiles.filter((t) => r.attr(t, 'title') === 'free')).toHaveLength(5);
-    expect(r.attr(tiles[0], 'title')).toBe('ml/train-a');
-    expect(r.text()).toContain('inferred from pod order');
+    const strip = r.byAttr('data-slots');
+    expect(strip).toHaveLength(1);
+    expect(r.attr(strip[0], 'data-slots').split(',').filter((o) => o === 'free')).toHaveLength(5);
+    expect(r.attr(strip[0], 'data-slots').split(',')[0]).toBe('ml/train-a');
+    expect(r.attr(strip[0], 'title')).toContain('inferred from pod order');
+    expect(r.text()).toBe('GPU 0–1 ml/train-a · GPU 2 ml/train-b · GPU 3–7 free (inferred)');
     r.unmount();
   });
 
