@@ -148,6 +148,7 @@ export async function detailOpens(url, counter, ctx, n) {
       listsPerOpen: sum(function (r) { return r.lists.length; }),
       clusterWideListsPerOpen: sum(function (r) { return r.clusterWideLists; }),
       deviceConfigRequestsPerOpen: sum(function (r) { return r.deviceConfigRequests; }),
+      serverMs: runs.map(function (r) { return r.serverMs; }),
       listPaths: runs.length ? runs[runs.length - 1].lists : [],
       rendered: runs.every(function (r) { return r.section && !r.loading; }),
     };

@@ -67,9 +67,11 @@ function httpLib(request, rec) {
   };
 }
 
-/** Wait until every request of `counter` has answered and the tree is quiet. */
+/** Wait until every request in flight has answered and the tree is quiet (at most QUIET_MS). */
+const QUIET_MS = 120000;
 async function quiet(handle, inflight) {
-  for (let i = 0; i < 2000; i++) {
+  const until = Date.now() + QUIET_MS;
+  while (Date.now() < until) {
     await handle.settle(2);
     if (inflight.n === 0) {
       await handle.settle(2);
@@ -77,7 +79,7 @@ async function quiet(handle, inflight) {
     }
     await new Promise(function (r) { setTimeout(r, 1); });
   }
-  throw new Error('wiredDetail: requests did not settle');
+  throw new Error('wiredDetail: requests did not settle within ' + QUIET_MS + ' ms (' + inflight.n + ' in flight)');
 }
 
 /**
@@ -87,7 +89,7 @@ async function quiet(handle, inflight) {
  * requests / bytes, and the list hooks it mounted.
  */
 export async function wiredNodeDetailOpen(url, node, after, tag) {
-  const counter = { n: 0, bytes: 0 };
+  const counter = { n: 0, bytes: 0, log: [] };
   const raw = makeRequest(url, counter);
   const inflight = { n: 0 };
   const paths = [];
@@ -117,7 +119,7 @@ export async function wiredNodeDetailOpen(url, node, after, tag) {
     await quiet(page, inflight);
     page.unmount();
   }
-  const before = { n: counter.n, bytes: counter.bytes, lists: rec.lists.length, paths: paths.length };
+  const before = { n: counter.n, bytes: counter.bytes, lists: rec.lists.length, paths: paths.length, log: counter.log.length };
   const t0 = process.hrtime();
   const r = HarnessReact.render(plugin.nodeDetailSectionFor({ resource: Object.assign({ kind: 'Node' }, node) }));
   await quiet(r, inflight);
@@ -132,6 +134,8 @@ export async function wiredNodeDetailOpen(url, node, after, tag) {
     lists: lists.map(function (l) { return l.path; }),
     clusterWideLists: lists.filter(function (l) { return clusterWide(l.opts); }).length,
     deviceConfigRequests: paths.slice(before.paths).filter(function (p) { return p === DEVICE_CONFIG_LIST_PATH; }).length,
+    // the fake server's own time on the open's slowest request (X-Server-Ms)
+    serverMs: counter.log.slice(before.log).reduce(function (m, r) { return Math.max(m, r.serverMs || 0); }, 0),
     section: html.indexOf('AMD GPU') >= 0,
     loading: html.indexOf('Loading…') >= 0,
   };
