@@ -15,6 +15,7 @@ import { nodePage, podPage } from '../src/view/pages/paging.js';
 import { podsView } from '../src/view/pages/pods.js';
 import { countRows, sections } from '../src/view/ir.js';
 import { renderPage, renderSection } from '../src/view/html.js';
+import { renderPageSvg, renderSectionSvg } from '../src/view/svg.js';
 // The harness React (the Node-12 stand-in the spec suite renders the plugin
 // with) and its CommonComponents: the pages are also mounted through the
 // shipped renderer to count elements and time a mount / re-render, next to
@@ -158,30 +159,36 @@ export function writeSnapshots(ctx, mstate, dir, now, history) {
   const hist = history || {};
   fs.mkdirSync(dir, { recursive: true });
   const opts = { metrics: mstate.metrics, now: now };
+  // [file name, page view-model] or [file name, section, true]
   const views = [
-    ['01-overview', renderPage(overviewView(ctx, opts))],
-    ['02-device-plugins', renderPage(devicePluginsView(ctx, opts))],
-    ['03-gpu-nodes', renderPage(nodesView(ctx, opts))],
-    ['04-gpu-pods', renderPage(podsView(ctx, opts))],
-    ['05-metrics', renderPage(metricsView(ctx, Object.assign({}, mstate, { now: now })))],
+    ['01-overview', overviewView(ctx, opts)],
+    ['02-device-plugins', devicePluginsView(ctx, opts)],
+    ['03-gpu-nodes', nodesView(ctx, opts)],
+    ['04-gpu-pods', podsView(ctx, opts)],
+    ['05-metrics', metricsView(ctx, Object.assign({}, mstate, { now: now }))],
   ];
   if (ctx.gpuNodes.length) {
     const s = nodeDetailView(ctx.gpuNodes[0], ctx, Object.assign({}, opts, { series: hist.node }));
-    if (s) views.push(['06-node-detail', renderSection(s)]);
+    if (s) views.push(['06-node-detail', s, true]);
   }
   if (ctx.gpuPods.length) {
     const s = podDetailView(ctx.gpuPods[0], Object.assign({}, opts, { series: hist.pod }));
-    if (s) views.push(['07-pod-detail', renderSection(s)]);
+    if (s) views.push(['07-pod-detail', s, true]);
   }
   const files = [];
   for (let i = 0; i < views.length; i++) {
-    const f = path.join(dir, views[i][0] + '.html');
+    const v = views[i];
+    const f = path.join(dir, v[0] + '.html');
     fs.writeFileSync(
       f,
-      '<!doctype html><html><head><meta charset="utf-8"><title>amd-gpu — ' + views[i][0] + '</title><style>' +
-        SNAPSHOT_CSS + '</style></head><body>\n' + views[i][1] + '\n</body></html>\n'
+      '<!doctype html><html><head><meta charset="utf-8"><title>amd-gpu — ' + v[0] + '</title><style>' +
+        SNAPSHOT_CSS + '</style></head><body>\n' + (v[2] ? renderSection(v[1]) : renderPage(v[1])) + '\n</body></html>\n'
     );
     files.push(f);
+    // The same view-model as a picture (ArtifactHub and README cannot show HTML).
+    const g = path.join(dir, v[0] + '.svg');
+    fs.writeFileSync(g, v[2] ? renderSectionSvg(v[1]) : renderPageSvg(v[1]));
+    files.push(g);
   }
   return files;
 }

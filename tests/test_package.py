@@ -132,6 +132,12 @@ def test_artifacthub_metadata_is_valid_and_matches_the_manifest(tmp_path):
     assert any("checksum" in e for e in broken(lambda m: m["annotations"].update({"headlamp/plugin/archive-checksum": "sha256:xyz"})))
     assert any("v9.9.9" in e for e in broken(lambda m: m.update(version="9.9.9")))
     assert any("license" in e for e in broken(lambda m: m.pop("license")))
+    # screenshots: present, raw URLs of this repository, files that exist (here: none under tmp_path)
+    assert "missing screenshots" in broken(lambda m: m.pop("screenshots"))
+    assert any("does not exist" in e for e in broken(lambda m: None))
+    assert any("not in amd-gpu-headlamp" in e for e in broken(
+        lambda m: m["screenshots"][0].update(url=m["screenshots"][0]["url"].replace("amd-gpu-headlamp/", "someone-else/"))))
+    assert any("raw.githubusercontent.com" in e for e in broken(lambda m: m["screenshots"][0].update(url="https://x/y.png")))
     assert validate(str(tmp_path / "missing.yml")) == [f"{tmp_path / 'missing.yml'} not found"]
 
 

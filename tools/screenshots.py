@@ -1,11 +1,13 @@
-"""Render every plugin view of a synthetic MI355X cluster to static HTML.
+"""Render every plugin view of a synthetic MI355X cluster to static HTML and SVG.
 
     python tools/screenshots.py [--nodes 2] [--out docs/screenshots]
 
-The reference ships hand-drawn SVG mock-ups (docs/screenshots/*.svg); these
-are the real view-models (src/view/pages/*.js) of a fake 2-node cluster
-rendered through src/view/html.js — the same path the benchmark counts rows
-on — so they stay in sync with the code.
+The reference ships hand-drawn SVG mock-ups (docs/screenshots/*.svg, published
+through artifacthub-pkg.yml's `screenshots:`); these are the real view-models
+(src/view/pages/*.js) of a fake 2-node cluster, rendered through
+src/view/html.js — the same path the benchmark counts rows on — and drawn by
+src/view/svg.js as the pictures ArtifactHub and the README show, so they stay
+in sync with the code.
 """
 import argparse
 import os

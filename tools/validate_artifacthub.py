@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
-"""Validate artifacthub-pkg.yml (required fields, SemVer, archive annotations).
+"""Validate artifacthub-pkg.yml (required fields, SemVer, archive annotations, screenshots).
 
 Used by CI; exits non-zero with one line per problem.
 """
+import os
 import re
 import sys
 
@@ -35,6 +36,37 @@ def validate(path="artifacthub-pkg.yml"):
         errors.append(f"archive-checksum {checksum!r} is not sha256:<64 hex>")
     if not ann.get("headlamp/plugin/version-compat"):
         errors.append("missing annotation headlamp/plugin/version-compat")
+    errors.extend(screenshot_errors(pkg, os.path.dirname(os.path.abspath(path))))
+    return errors
+
+
+# ArtifactHub shows what `url` serves; the files are this repository's docs/screenshots, published from main.
+RAW_RE = re.compile(r"^https://raw\.githubusercontent\.com/([^/]+)/([^/]+)/[^/]+/(docs/screenshots/[\w.-]+\.(?:svg|png))$")
+
+
+def screenshot_errors(pkg, root):
+    """`screenshots:` — at least one; each a title and a raw.githubusercontent.com URL of this repository
+    (homeURL's owner/name) naming a file that exists under docs/screenshots."""
+    shots = pkg.get("screenshots")
+    if not shots:
+        return ["missing screenshots"]
+    if not isinstance(shots, list):
+        return ["screenshots is not a list"]
+    home = re.match(r"^https://github\.com/([^/]+)/([^/]+?)/?$", str(pkg.get("homeURL", "")))
+    errors = []
+    for i, s in enumerate(shots):
+        if not isinstance(s, dict) or not str(s.get("title", "")).strip():
+            errors.append(f"screenshots[{i}] has no title")
+            continue
+        url = str(s.get("url", ""))
+        m = RAW_RE.match(url)
+        if not m:
+            errors.append(f"screenshots[{i}] url {url!r} is not a raw.githubusercontent.com docs/screenshots/*.svg|png URL")
+            continue
+        if home and (m.group(1), m.group(2)) != (home.group(1), home.group(2)):
+            errors.append(f"screenshots[{i}] url is not in {home.group(1)}/{home.group(2)} (homeURL)")
+        if not os.path.isfile(os.path.join(root, m.group(3))):
+            errors.append(f"screenshots[{i}] file {m.group(3)} does not exist")
     return errors
 
 
