@@ -29,11 +29,13 @@ import { get, MI355X } from './k8sCore.js';
  * @param {any[]} podsOnNode  GPU pods bound to the node
  * @param {Array<{gpu: string, pod?: string|null, namespace?: string|null}>} [perGpuOwners]
  *        exporter-derived owners keyed by gpu index (as string)
+ * @param {{capacity: number, partitionsPerGpu: number}} [dims]  the node's device count and partitions per
+ *        board when the caller has them (clusterIndex.js nodeFacts), instead of reading the node's labels again
  * @returns {{ slots: GpuSlot[], exact: boolean, partitionsPerGpu: number }}
  */
-export function buildGpuSlots(node, podsOnNode, perGpuOwners) {
-  const n = getNodeGpuCount(node) || 0;
-  const pp = partitionsPerGpu(node);
+export function buildGpuSlots(node, podsOnNode, perGpuOwners, dims) {
+  const n = (dims ? dims.capacity : getNodeGpuCount(node)) || 0;
+  const pp = dims ? dims.partitionsPerGpu : partitionsPerGpu(node);
   const slots = [];
   for (let i = 0; i < n; i++) {
     slots.push({

@@ -256,6 +256,12 @@ export function slotOwner(s) {
   return s.pod ? (s.namespace ? s.namespace + '/' : '') + s.pod : 'free';
 }
 
+/** slotOwner(a) === slotOwner(b), without building the strings. */
+function sameOwner(a, b) {
+  if (!a.pod || !b.pod) return !a.pod && !b.pod;
+  return a.pod === b.pod && (a.namespace || '') === (b.namespace || '');
+}
+
 function slotLabel(s) {
   return s.partition === null || s.partition === undefined ? String(s.index) : s.board + '·' + s.partition;
 }
@@ -265,18 +271,18 @@ function slotLabel(s) {
  * (consecutive slots of one owner fold into one run).
  */
 export function slotsText(slots) {
-  const runs = [];
-  for (let i = 0; i < slots.length; i++) {
-    const o = slotOwner(slots[i]);
-    const last = runs[runs.length - 1];
-    if (last && last.owner === o) last.to = slots[i];
-    else runs.push({ owner: o, from: slots[i], to: slots[i] });
+  // Runs compare the owners' fields (no owner string per slot: a strip is
+  // drawn per GPU node card on every mount).
+  let out = '';
+  for (let i = 0; i < slots.length;) {
+    const from = slots[i];
+    let j = i + 1;
+    while (j < slots.length && sameOwner(slots[j], from)) j++;
+    const a = slotLabel(from);
+    out += (i ? ' · GPU ' : 'GPU ') + (j - 1 === i ? a : a + '–' + slotLabel(slots[j - 1])) + ' ' + slotOwner(from);
+    i = j;
   }
-  return runs.map(function (r) {
-    const a = slotLabel(r.from);
-    const z = slotLabel(r.to);
-    return 'GPU ' + (a === z ? a : a + '–' + z) + ' ' + r.owner;
-  }).join(' · ');
+  return out;
 }
 
 // ---------------------------------------------------------------------------

@@ -11,7 +11,6 @@ import {
   deviceConfigStatusText,
   formatSelector,
   operandEnabled,
-  OPERANDS,
   operandStatus,
 } from '../../api/amdNodes.js';
 import { formatComponent, pluginPodComponent } from '../../api/amdPods.js';
@@ -42,8 +41,18 @@ const EXTRA_OPERANDS = [
   { key: 'configManager', label: 'Config Manager' },
 ];
 
-function enabledCell(on, detail) {
-  return on ? status('success', detail ? 'Enabled — ' + detail : 'Enabled') : status('warning', 'Disabled');
+/**
+ * An operand's row: "Disabled", or "Enabled" (— its version / port) and, when
+ * the DeviceConfig's status counts its DaemonSet, "· ready/desired" in the
+ * same cell, coloured by the pods (one row per operand; the reference has no
+ * operand rows, DevicePluginsPage.tsx:115-180).
+ */
+function operandCell(dc, key, detail, counted) {
+  if (!operandEnabled(dc, key)) return status('warning', 'Disabled');
+  const head = detail ? 'Enabled — ' + detail : 'Enabled';
+  if (!counted) return status('success', head);
+  const st = operandStatus(dc, key);
+  return status(countsToStatus(st.desired, st.available), head + ' · ' + countsToText(st.desired, st.available));
 }
 
 /**
@@ -114,39 +123,24 @@ function devicePluginsItems(ctx, now, pg, podsPend) {
       row('Status', status(deviceConfigStatus(dc), deviceConfigStatusText(dc))),
       row('Namespace', dc.metadata.namespace || '—'),
       row('Device Plugin Image', get(dc, ['spec', 'devicePlugin', 'devicePluginImage'], '—')),
-      row(
-        'Driver',
-        enabledCell(operandEnabled(dc, 'driver'), get(dc, ['spec', 'driver', 'version'], null))
-      ),
-      row('Node Labeller', enabledCell(operandEnabled(dc, 'nodeLabeller'))),
+      row('Driver', operandCell(dc, 'driver', get(dc, ['spec', 'driver', 'version'], null), true)),
+      row('Node Labeller', operandCell(dc, 'nodeLabeller', null, true)),
       row(
         'Metrics Exporter',
-        enabledCell(
-          operandEnabled(dc, 'metricsExporter'),
-          get(dc, ['spec', 'metricsExporter', 'port'], null) !== null ? 'port ' + get(dc, ['spec', 'metricsExporter', 'port'], '') : null
-        )
+        operandCell(dc, 'metricsExporter',
+          get(dc, ['spec', 'metricsExporter', 'port'], null) !== null ? 'port ' + get(dc, ['spec', 'metricsExporter', 'port'], '') : null, true)
       ),
       row('Desired Nodes', String(dp.desired)),
       row('Ready Nodes', String(dp.available)),
     ];
     if (dp.unavailable > 0) rows.push(row('Unavailable Nodes', status('error', dp.unavailable)));
-    for (let k = 0; k < OPERANDS.length; k++) {
-      const op = OPERANDS[k];
-      if (op.key === 'devicePlugin' || !operandEnabled(dc, op.key)) continue;
-      const st = operandStatus(dc, op.key);
-      rows.push(row(op.label + ' Pods', status(countsToStatus(st.desired, st.available), countsToText(st.desired, st.available))));
-    }
     // Later operator releases' operands (GPU test runner, partition config
     // manager): shown when the DeviceConfig names them, their DaemonSet
     // counts when its status reports them.
     for (let k = 0; k < EXTRA_OPERANDS.length; k++) {
       const op = EXTRA_OPERANDS[k];
       if (get(dc, ['spec', op.key], null) === null) continue;
-      rows.push(row(op.label, enabledCell(operandEnabled(dc, op.key))));
-      if (operandEnabled(dc, op.key) && get(dc, ['status', op.key], null) !== null) {
-        const st = operandStatus(dc, op.key);
-        rows.push(row(op.label + ' Pods', status(countsToStatus(st.desired, st.available), countsToText(st.desired, st.available))));
-      }
+      rows.push(row(op.label, operandCell(dc, op.key, null, get(dc, ['status', op.key], null) !== null)));
     }
     rows.push(row('Node Selector', formatSelector(get(dc, ['spec', 'selector'], null))));
     rows.push(row('Age', ageText(dc.metadata.creationTimestamp, now)));

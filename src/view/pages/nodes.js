@@ -73,7 +73,7 @@ export function telemetryScope(ctx, state, ranked) {
 
 /** Per-GPU allocation strip block. */
 export function slotsBlock(node, podsOnNode, owners) {
-  const s = buildGpuSlots(node, podsOnNode, owners);
+  const s = buildGpuSlots(node, podsOnNode, owners, nodeFacts(node));
   return { t: 'slots', slots: s.slots, exact: s.exact, partitionsPerGpu: s.partitionsPerGpu };
 }
 

@@ -159,10 +159,11 @@ describe('devicePluginsView', () => {
     dc.spec.configManager = { enable: false };
     dc.status.testRunner = { nodesMatchingSelectorNumber: 2, desiredNumber: 2, availableNumber: 1 };
     const s = findSection(devicePluginsView(makeContext({ deviceConfigs: [dc] }), opts), 'DeviceConfig: gpu-operator');
-    expect(rowValue(s, 'Test Runner')).toEqual({ t: 'status', status: 'success', text: 'Enabled' });
-    expect(rowValue(s, 'Test Runner Pods').text).toBe('1/2 ready');
+    expect(rowValue(s, 'Test Runner')).toEqual({ t: 'status', status: 'warning', text: 'Enabled · 1/2 ready' });
     expect(rowValue(s, 'Config Manager')).toEqual({ t: 'status', status: 'warning', text: 'Disabled' });
-    expect(rowValue(s, 'Config Manager Pods')).toBeUndefined();
+    delete dc.status.testRunner;
+    const uncounted = findSection(devicePluginsView(makeContext({ deviceConfigs: [dc] }), opts), 'DeviceConfig: gpu-operator');
+    expect(rowValue(uncounted, 'Test Runner')).toEqual({ t: 'status', status: 'success', text: 'Enabled' });
     const plain = findSection(devicePluginsView(makeContext({ deviceConfigs: [makeDeviceConfig('gpu-operator')] }), opts), 'DeviceConfig: gpu-operator');
     expect(rowValue(plain, 'Test Runner')).toBeUndefined();
   });
@@ -187,8 +188,9 @@ describe('devicePluginsView', () => {
     const vm = devicePluginsView(makeContext({ crdAvailable: true, deviceConfigs: [makeDeviceConfig('a'), makeDeviceConfig('b', { exporter: false })] }), opts);
     const a = findSection(vm, 'DeviceConfig: a');
     expect(rowValue(a, 'Status')).toEqual({ t: 'status', status: 'success', text: '2/2 ready' });
-    expect(rowValue(a, 'Metrics Exporter')).toEqual({ t: 'status', status: 'success', text: 'Enabled — port 5000' });
-    expect(rowNames(a)).toContain('Metrics Exporter Pods');
+    // the operand and its DaemonSet's pods in one row
+    expect(rowValue(a, 'Metrics Exporter')).toEqual({ t: 'status', status: 'success', text: 'Enabled — port 5000 · 2/2 ready' });
+    expect(rowNames(a).filter((n) => / Pods$/.test(n))).toEqual([]);
     expect(rowValue(findSection(vm, 'DeviceConfig: b'), 'Metrics Exporter').status).toBe('warning');
     expect(rowValue(a, 'Node Selector')).toBe('feature.node.kubernetes.io/amd-gpu=true');
   });

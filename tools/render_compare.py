@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """The reference's own pages vs this plugin's, rendered on real React 18.3.1 at 1 to 1,000 GPU nodes.
 
-    python tools/render_compare.py --allow-reference-exec [--sizes 1,2,4,8] [--reps 15] [--warm 5]
+    python tools/render_compare.py --allow-reference-exec [--sizes 1,2,4,8] [--reps 101] [--warm 50]
                                    [--out profiles/r5_render_compare]
 
 OPT-IN: this runs the reference's page components, which are untrusted public content (ADR 013). Without
@@ -85,7 +85,7 @@ def table(rows) -> list:
 def main() -> int:
     p = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     p.add_argument("--sizes", default="1,2,4,8")
-    p.add_argument("--reps", type=int, default=31)
+    p.add_argument("--reps", type=int, default=101)
     p.add_argument("--warm", type=int, default=50)
     p.add_argument("--reference", default="/root/reference")
     p.add_argument("--out", default=os.path.join(ROOT, "profiles", "r5_render_compare"))
