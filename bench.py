@@ -157,11 +157,15 @@ def main(argv=None) -> int:
                        if node_of_device else None)
             server = ServerThread(fc).start()
         drv = Driver(server.url)
+        # The reference schedule runs in a Node process of its own: neither
+        # schedule's figures depend on the heap and JIT state the other left
+        # (the 1,000-node composite moved by 18% with the order otherwise).
+        ref_drv = Driver(server.url)
 
-        def call(*a, **k):
+        def call(*a, driver=None, **k):
             """drv.call + a progress line on stderr (a long 1,000-node run stays visibly alive)."""
             t = time.perf_counter()
-            r = drv.call(*a, **k)
+            r = (driver or drv).call(*a, **k)
             print(f"[bench] {a[0]} {a[1] if len(a) > 1 else ''} {time.perf_counter() - t:.1f} s", file=sys.stderr, flush=True)
             return r
 
@@ -173,13 +177,15 @@ def main(argv=None) -> int:
             # server work, queued on its one evaluation thread; cached afterwards),
             # which a real Prometheus does not. Both schedules are warmed the same way.
             def reference_phases():
-                """Measured baseline: the reference plugin's schedule (untimed region)."""
-                call("cold", "reference", n=2)
-                out = {"ref_cold": call("cold", "reference", n=3), "ref_cold_pages": call("coldPages", "reference", n=5)}
-                call("pages", "reference", n=max(1, args.warmup))
-                out["ref_pages"] = call("pages", "reference", n=ref_steps)
-                out["ref"] = call("steps", "reference", n=max(3, ref_steps // 2))
-                out["ref_switch"] = call("switch", "reference", n=3)
+                """Measured baseline: the reference plugin's schedule (untimed region), in its own driver process."""
+                call("cold", "reference", n=2, driver=ref_drv)
+                out = {"ref_cold": call("cold", "reference", n=3, driver=ref_drv),
+                       "ref_cold_pages": call("coldPages", "reference", n=5, driver=ref_drv)}
+                call("pages", "reference", n=max(1, args.warmup), driver=ref_drv)
+                out["ref_pages"] = call("pages", "reference", n=ref_steps, driver=ref_drv)
+                out["ref"] = call("steps", "reference", n=max(3, ref_steps // 2), driver=ref_drv)
+                out["ref_switch"] = call("switch", "reference", n=3, driver=ref_drv)
+                ref_drv.close()
                 return out
 
             if args.order == "reference-first":
@@ -225,6 +231,7 @@ def main(argv=None) -> int:
                       **served}
         finally:
             drv.close()
+            ref_drv.close()
             server.stop()
             if scraper:
                 scraper.stop()

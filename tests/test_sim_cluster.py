@@ -2,6 +2,7 @@
 import json
 import os
 import re
+import time
 import urllib.error
 import urllib.parse
 import urllib.request
@@ -259,3 +260,61 @@ def test_list_cache_invalidation():
     fc.cluster.nodes.pop()
     fc.bump()
     assert fc.nodes_body("") != a
+
+
+def test_recording_rule_answers_and_server_time(monkeypatch):
+    """rules=True (the benchmark's control plane): the first instant query is evaluated for its caller, later ones
+    are served the kept answer; the ticker re-evaluates it once its inputs changed, in a lull of client requests and
+    no more often than RULE_EVAL_S; every response says its server time (X-Server-Ms)."""
+    from headlamp_intel_gpu_plugin_amd.sim import apiserver
+
+    monkeypatch.setattr(apiserver, "RULE_EVAL_S", 0.0)
+    monkeypatch.setattr(apiserver, "RULE_IDLE_S", 0.2)
+    fc = make_fake(1, source="amd-exporter", latency_ms=0, rules=True)
+    clock = [fc.now()]
+    fc.now = lambda: clock[0]
+    q = PROM + "query?query=" + urllib.parse.quote("sum(gpu_power_usage)")
+    with ServerThread(fc) as s:
+        with urllib.request.urlopen(s.url + q, timeout=10) as r:
+            first = json.loads(r.read())
+            assert float(r.headers["X-Server-Ms"]) >= 0
+        assert fc.rule_evals == 1 and first["status"] == "success"
+        for _ in range(3):
+            assert get(s, q)[1] == first
+        assert fc.rule_evals == 1  # served, not evaluated
+        clock[0] += 60.0  # the sample grid ticks: the kept answer is behind its inputs
+        deadline = time.time() + 10
+        while fc.rule_evals == 1 and time.time() < deadline:
+            time.sleep(0.05)
+        assert fc.rule_evals == 2
+        assert get(s, q)[1]["data"]["result"]
+        # A request of any kind says its server time.
+        with urllib.request.urlopen(s.url + "/api/v1/nodes", timeout=10) as r:
+            assert float(r.headers["X-Server-Ms"]) >= 0
+
+
+def test_rule_refreshes_wait_for_a_lull(monkeypatch):
+    """A refresh does not start while client requests keep arriving (the evaluation thread cannot pre-empt it),
+    unless the answer is RULE_STALE_S old."""
+    from headlamp_intel_gpu_plugin_amd.sim import apiserver
+
+    monkeypatch.setattr(apiserver, "RULE_EVAL_S", 0.0)
+    monkeypatch.setattr(apiserver, "RULE_IDLE_S", 5.0)
+    fc = make_fake(1, source="amd-exporter", latency_ms=0, rules=True)
+    clock = [fc.now()]
+    fc.now = lambda: clock[0]
+    q = PROM + "query?query=" + urllib.parse.quote("count(gpu_power_usage)")
+    with ServerThread(fc) as s:
+        get(s, q)
+        clock[0] += 60.0
+        end = time.time() + 1.5
+        while time.time() < end:  # a steady stream of requests: no lull of 5 s
+            get(s, "/api/v1/nodes")
+            time.sleep(0.1)
+        assert fc.rule_evals == 1
+        monkeypatch.setattr(apiserver, "RULE_STALE_S", 0.0)  # an answer this old is refreshed whatever the load
+        end = time.time() + 10
+        while fc.rule_evals == 1 and time.time() < end:
+            get(s, "/api/v1/nodes")
+            time.sleep(0.05)
+        assert fc.rule_evals == 2
