@@ -71,7 +71,8 @@ export function taintsText(node) {
 
 /**
  * {phase, nodeName, gpus} of a GPU pod, derived once per object; `gpus` is
- * what the pod holds (0 once it terminated).
+ * what the pod holds (0 once it terminated). `containers` is filled in by
+ * podContainerLines, for the pods a page shows.
  */
 export function podFacts(p) {
   let f = podFactCache.get(p);
@@ -83,12 +84,21 @@ export function podFacts(p) {
       // The kubelet allocates devices at admission and releases them when the
       // pod terminates, so a bound non-terminal pod holds its GPUs.
       gpus: phase !== 'Succeeded' && phase !== 'Failed' ? getPodGpuCount(p) : 0,
-      // Its GPU containers' requests as the GPU Pods table lists them (pages/pods.js gpuContainerLines).
-      containers: containerLines(p),
+      containers: null,
     };
     podFactCache.set(p, f);
   }
   return f;
+}
+
+/**
+ * A GPU pod's containers as the GPU Pods table lists them (pages/pods.js
+ * gpuContainerLines): derived on first read and kept with the pod's facts —
+ * not when the list arrives (a page shows 25 of 5,000 GPU pods).
+ */
+export function podContainerLines(p) {
+  const f = podFacts(p);
+  return f.containers || (f.containers = containerLines(p));
 }
 
 /**

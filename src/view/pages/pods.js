@@ -11,7 +11,7 @@ import {
   podWaitingMessage,
   podWaitingReason,
 } from '../../api/amdPods.js';
-import { podFacts } from '../../api/clusterIndex.js';
+import { podContainerLines, podFacts } from '../../api/clusterIndex.js';
 import { formatBytes, formatWatts } from '../../api/k8sCore.js';
 import { SMALL_CLUSTER_PODS } from '../../api/series.js';
 import { kv, lines, loader, page, pager, row, section, status, table } from '../ir.js';
@@ -146,11 +146,12 @@ export function ownersScope(ctx, state) {
 
 /**
  * Per-container GPU lines (reference GpuContainerList, PodsPage.tsx:49-88),
- * init containers included — derived with the pod's facts when the pod list
- * arrived (clusterIndex.js podFacts). One container is plain text.
+ * init containers included — derived once per pod object, the first time a
+ * page shows the pod (clusterIndex.js podContainerLines). One container is
+ * plain text.
  */
 export function gpuContainerLines(pod) {
-  const cs = podFacts(pod).containers;
+  const cs = podContainerLines(pod);
   if (!cs.length) return '—';
   return cs.length === 1 ? cs[0].label + ': ' + cs[0].text : lines(cs);
 }
