@@ -29,7 +29,7 @@ export const NO_CODEGEN_FLAG = '--disallow-code-generation-from-strings';
 /**
  * Refuses unless the caller opted in (`allowReferenceExec`) and this process
  * runs with NO_CODEGEN_FLAG: the reference's sources are untrusted public
- * content, run only in bench/tsx.js's sandbox under that flag (ADR 013).
+ * content, run only in bench/tsx.js's sandbox under that flag (ADR 014).
  */
 export function assertReferenceSandbox(c) {
   if (!c || c.allowReferenceExec !== true) {

@@ -31,7 +31,7 @@
  * are untrusted public content: they are loaded only by the opt-in render
  * comparison (tools/render_compare.py --allow-reference-exec), in a child
  * process started with --disallow-code-generation-from-strings, so that
- * no host function's constructor compiles code either (ADR 013).
+ * no host function's constructor compiles code either (ADR 014).
  */
 import vm from 'vm';
 import {

@@ -166,15 +166,23 @@ def device_to_node(node_of_device: Dict[str, str]) -> Relabel:
     return lambda labels: (node_of_device[labels["gpu_id"]], 0) if labels.get("gpu_id") in node_of_device else None
 
 
+#: A grid-scheduled scrape this late after its grid point is still stamped with it.
+ALIGN_SLACK_S = 0.5
+
+
 class Scraper:
     """Pulls every target every ``interval`` s and appends to the live series.
 
     ``targets`` is ``{node: url}`` (per-node agents, labels used as-is) or a
-    list of ``(url, relabel)`` pairs. With ``align`` the scrapes land on the
-    ``interval`` grid and their samples carry the grid time, as Prometheus
-    stamps a target's scrapes on its scrape interval — and as the fake's
-    synthetic series are sampled — so the fake's query caches turn over once
-    per interval, not once per scrape of a faster loop.
+    list of ``(url, relabel)`` pairs. With ``align`` the scrapes are scheduled
+    on the ``interval`` grid (a target's scrapes are one interval apart in
+    Prometheus too, and the fake's synthetic series are sampled on the same
+    grid), so the fake's query caches turn over once per interval, not once
+    per scrape of a faster loop. A scrape taken on the grid (within
+    ALIGN_SLACK_S after a grid point, the loop's wake-up delay) is stamped
+    with the grid time; one taken off it — the first, when the scraper starts
+    — keeps its own time, so no sample is dated more than ALIGN_SLACK_S
+    before it was read.
     """
 
     def __init__(self, targets: Union[Dict[str, str], Sequence[Tuple[str, Relabel]]],
@@ -195,7 +203,9 @@ class Scraper:
     def scrape_once(self) -> None:
         t = self.now()
         if self.align:
-            t = math.floor(t / self.interval) * self.interval
+            grid = math.floor(t / self.interval) * self.interval
+            if t - grid <= ALIGN_SLACK_S:
+                t = grid
         for url, relabel in self.targets:
             try:
                 with urllib.request.urlopen(url, timeout=2) as r:

@@ -59,11 +59,14 @@ function operandCell(dc, key, detail, counted) {
  * One card per DeviceConfig (reference: one per GpuDevicePlugin). Per-operand
  * DaemonSet counts replace the single desired/ready pair. The page needs no
  * node list and no all-namespaces pod list: its route (plugin.js PAGE_NEEDS)
- * asks for the operator pods with the plugin-pod requests, in the same wave
- * as the DeviceConfigs, so it renders whole after one round trip on any
- * cluster size (reference: a full-page Loader until both cluster-wide lists
- * and its four serial requests are in, DevicePluginsPage.tsx:23-25,
- * IntelGpuDataContext.tsx:98-165,214).
+ * mounts OperatorPodFeed, a list + watch of the operator namespace and one of
+ * the device plugin / labeller labels elsewhere (providerCore.js), in the
+ * same wave as the DeviceConfig request, so it renders whole after one round
+ * trip on any cluster size. The plugin-pod requests (requests.js
+ * PLUGIN_POD_QUERIES) stand in when both lists fail, or re-read on a timer
+ * when the host ignores list selectors (ADR 012). Reference: a full-page
+ * Loader until both cluster-wide lists and its four serial requests are in,
+ * DevicePluginsPage.tsx:23-25, IntelGpuDataContext.tsx:98-165,214.
  */
 export function devicePluginsView(ctx, opts) {
   const now = nowOf(opts);

@@ -4,7 +4,7 @@
  * bench/referenceRender.js). Its transforms on small inputs of this
  * repository's own, and the sandbox it loads modules into. Nothing here
  * reads or runs the reference's sources: they are untrusted public content
- * (ADR 013), executed only by tools/render_compare.py --allow-reference-exec.
+ * (ADR 014), executed only by tools/render_compare.py --allow-reference-exec.
  */
 import { loadModules, lowerModules, lowerOptional, stripTypes, transformJsx } from '../../bench/tsx.js';
 

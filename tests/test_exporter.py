@@ -116,11 +116,16 @@ def test_exporter_process_and_device_relabel(exe):
         assert live[("mi355x-003", 0)]["gpu_power_usage"].at(100.0)[1] == 321.0
         assert live[("mi355x-003", 0)]["gpu_total_vram"].at(100.0)[1] == 1024.0
         assert device_to_node({"0": "n"})({"gpu_id": "5"}) is None
-        # On the scrape grid (the ServiceMonitor's 15 s): a scrape at 107.3 s is stamped 105 s.
-        aligned = Scraper([(agent.url, device_to_node({"0": "mi355x-003"}))], live, interval=15.0, now=lambda: 107.3,
+        # On the scrape grid (the ServiceMonitor's 15 s): a scrape just after a grid point is stamped with it; one
+        # off the grid (the first, at start) keeps its time, so no value is dated seconds before it was read.
+        clock = [120.02]
+        aligned = Scraper([(agent.url, device_to_node({"0": "mi355x-003"}))], live, interval=15.0, now=lambda: clock[0],
                           align=True)
         aligned.scrape_once()
-        assert live[("mi355x-003", 0)]["gpu_power_usage"].ts[-1] == 105.0
+        assert live[("mi355x-003", 0)]["gpu_power_usage"].ts[-1] == 120.0
+        clock[0] = 127.3
+        aligned.scrape_once()
+        assert live[("mi355x-003", 0)]["gpu_power_usage"].ts[-1] == 127.3
     finally:
         agent.stop()
 

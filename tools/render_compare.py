@@ -4,7 +4,7 @@
     python tools/render_compare.py --allow-reference-exec [--sizes 1,2,4,8] [--reps 101] [--warm 50]
                                    [--out profiles/r5_render_compare]
 
-OPT-IN: this runs the reference's page components, which are untrusted public content (ADR 013). Without
+OPT-IN: this runs the reference's page components, which are untrusted public content (ADR 014). Without
 ``--allow-reference-exec`` it refuses. With it, bench/driver.js runs in a child process started with
 ``--disallow-code-generation-from-strings`` and only PATH in its environment, and the reference's modules are
 compiled into bench/tsx.js's sandbox: a vm context of their own, with no ``process``, ``require``, ``import()``,
@@ -94,7 +94,7 @@ def main() -> int:
     args = p.parse_args()
     if not args.allow_reference_exec:
         raise SystemExit("render_compare runs the reference's sources (untrusted public content): "
-                         "pass --allow-reference-exec to run them in the sandboxed driver process (ADR 013)")
+                         "pass --allow-reference-exec to run them in the sandboxed driver process (ADR 014)")
     if not os.path.isdir(os.path.join(args.reference, "src", "components")):
         raise SystemExit(f"no reference sources under {args.reference}")
     rows = []
