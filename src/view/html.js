@@ -9,7 +9,7 @@
  *
  * Used by the Node-side tests and by the benchmark to measure "rows
  * rendered" on real output; the shipped plugin renders the IR with React
- * (src/components/View.tsx).
+ * (src/view/react.js, bound in src/headlamp.ts).
  */
 
 import { matrixCaption, matrixSummary, pagerIdle, pagerText } from './ir.js';

@@ -14,11 +14,9 @@ import * as lib from './stubs/headlamp-lib.js';
 import * as CC from './stubs/CommonComponents.js';
 import { registered } from '../../src/index.tsx';
 import { plugin } from '../../src/headlamp.ts';
-import OverviewTsx from '../../src/components/OverviewPage.tsx';
-import MetricsTsx from '../../src/components/MetricsPage.tsx';
-import { buildNodeGpuColumns } from '../../src/components/integrations/NodeColumns.tsx';
-import { AmdGpuDataProvider, useAmdGpuContext } from '../../src/api/AmdGpuDataContext.tsx';
-import { Page, Section } from '../../src/components/View.tsx';
+import {
+  AmdGpuDataProvider, buildNodeGpuColumns, MetricsPage as MetricsTsx, OverviewPage as OverviewTsx, Page, Section, useAmdGpuContext,
+} from '../../src/headlamp.ts';
 import { PLUGIN_NAME, createPlugin, registerPlugin } from '../../src/plugin.js';
 import { resetSharedStores } from '../../src/api/clusterStore.js';
 import { clearViewMemo } from '../../src/view/pages/common.js';

@@ -22,7 +22,7 @@ SPECS = sorted(os.path.relpath(p, ROOT) for p in glob.glob(os.path.join(ROOT, "t
 RUNNER = os.path.join("tools", "minitest.js")
 # Resolves 'react' / '@kinvolk/headlamp-plugin/lib' to the harness stand-ins
 # and loads the TypeScript entry shims, so the specs import src/index.tsx and
-# src/components/*.tsx exactly as Headlamp bundles them.
+# src/headlamp.ts exactly as Headlamp bundles them.
 LOADER = ["--no-warnings", "--experimental-loader", "./tools/plugin-loader.js"]
 
 

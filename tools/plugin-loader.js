@@ -1,6 +1,6 @@
 /**
  * ESM loader that lets Node execute the plugin's TypeScript entry shims
- * (src/index.tsx, src/headlamp.ts, src/components/*.tsx, …) against the
+ * (src/index.tsx, src/headlamp.ts) against the
  * harness stand-ins, so the files Headlamp bundles are the files the specs
  * run:
  *
