@@ -318,3 +318,30 @@ def test_rule_refreshes_wait_for_a_lull(monkeypatch):
             get(s, "/api/v1/nodes")
             time.sleep(0.05)
         assert fc.rule_evals == 2
+
+
+def test_priority_pool_runs_client_work_before_queued_rule_refreshes():
+    """The fake Prometheus's one evaluation thread takes a client request (priority 0) before rule refreshes
+    (priority 1) that were queued earlier; equal priorities keep their order."""
+    import threading
+
+    from headlamp_intel_gpu_plugin_amd.sim.apiserver import PriorityPool
+
+    pool = PriorityPool("test-pool")
+    try:
+        gate = threading.Event()
+        order = []
+        first = pool.submit(1, gate.wait, 10)  # occupies the thread until released
+        queued = [pool.submit(1, order.append, f"rule{i}") for i in range(3)]
+        client = pool.submit(0, order.append, "client")
+        gate.set()
+        for f in [first, client] + queued:
+            f.result(timeout=10)
+        assert order == ["client", "rule0", "rule1", "rule2"]
+        # An exception reaches the caller and the thread keeps serving.
+        bad = pool.submit(0, lambda: 1 / 0)
+        with pytest.raises(ZeroDivisionError):
+            bad.result(timeout=10)
+        assert pool.submit(0, lambda: 42).result(timeout=10) == 42
+    finally:
+        pool.shutdown()
