@@ -156,6 +156,25 @@ describe('shared: blocks (' + tier + ')', () => {
     r.unmount();
   });
 
+  it('a matrix built closed (a GPU Nodes card) is its summary line; the toggle opens the grid and closes it', () => {
+    const measured = {};
+    for (let i = 0; i < 8; i++) for (let j = 0; j < 8; j++) if (i !== j) measured[i + '-' + j] = 40;
+    const r = render(h(v().Block, { b: matrixBlock(8, measured, null, false) }));
+    expect(r.byTag('td')).toHaveLength(0);
+    expect(r.text()).toContain('measured: max 40, mean 40 GB/s over 56 links');
+    const toggle = () => r.byTag('button')[0];
+    expect(r.attr(toggle(), 'aria-expanded')).toBe('false');
+    expect(r.textOf(toggle())).toBe('Show xGMI matrix');
+    r.click(toggle());
+    expect(r.byTag('td')).toHaveLength(64);
+    expect(r.byTag('td').filter((n) => r.textOf(n) === '40')).toHaveLength(56);
+    expect(r.attr(toggle(), 'aria-expanded')).toBe('true');
+    r.click(toggle());
+    expect(r.byTag('td')).toHaveLength(0);
+    expect(r.textOf(toggle())).toBe('Show xGMI matrix');
+    r.unmount();
+  });
+
   it('series → per-node sparklines labelled for screen readers', () => {
     const pts = [[0, 100], [30, 300], [60, 200]];
     const b = { t: 'series', power: { n0: pts, n1: [] }, vram: { n0: pts }, avgPower: { n0: 200 } };
