@@ -49,6 +49,7 @@ function clip(s, n) {
 
 /** `s` broken into lines of at most `n` characters, at spaces where it can. */
 export function wrap(s, n) {
+  n = Math.max(1, Math.floor(n));
   const words = String(s).split(' ');
   const out = [];
   let line = '';

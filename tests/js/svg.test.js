@@ -24,6 +24,7 @@ describe('text layout', () => {
     expect(wrap('a bb ccc dddd', 6)).toEqual(['a bb', 'ccc', 'dddd']);
     expect(wrap('abcdefghij', 4)).toEqual(['abcd', 'efgh', 'ij']);
     expect(wrap('', 10)).toEqual(['']);
+    expect(wrap('ab', 0)).toEqual(['a', 'b']); // a width below one character still makes progress
     // counted in code points, not UTF-16 units
     expect(wrap('°C °C °C', 5)).toEqual(['°C °C', '°C']);
   });
