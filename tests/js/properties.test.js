@@ -199,6 +199,7 @@ describe('malformed cluster objects (what a real apiserver, an old CRD version o
     const pages = await loadPages();
     const html = await import('../../src/view/html.js');
     const text = await import('../../src/view/text.js');
+    const svg = await import('../../src/view/svg.js');
     const { createClusterStore } = await import('../../src/api/clusterStore.js');
     const { makeGpuPod, makePlainPod, makePluginPod, makeNode, makeDeviceConfig } = await import('./fixtures.js');
     const r = rng(4242);
@@ -220,15 +221,19 @@ describe('malformed cluster objects (what a real apiserver, an old CRD version o
       const vms = [pages.overviewView(ctx, opts), pages.devicePluginsView(ctx, opts), pages.nodesView(ctx, opts),
         pages.podsView(ctx, opts), pages.metricsView(ctx, { metrics: null, fetchError: null, fetching: false }, opts)];
       const sections = nodes.map((n) => pages.nodeDetailView(n, ctx, opts)).concat(pods.map((p) => pages.podDetailView(p, opts)));
-      // The HTML (bench, snapshots) and terminal (bin/amd-gpu-dash.js) renderers take them too.
+      // The HTML (bench, snapshots), terminal (bin/amd-gpu-dash.js) and SVG (screenshots) renderers take them too.
       vms.forEach((vm) => {
         expect(typeof html.renderPage(vm)).toBe('string');
         expect(typeof text.renderText(vm, { color: false })).toBe('string');
+        const picture = svg.renderPageSvg(vm);
+        expect(picture).toMatch(/^<svg [^>]*height="\d+(\.\d)?"[\s\S]*<\/svg>\n$/);
+        expect(picture.indexOf('NaN')).toBe(-1);
       });
       sections.forEach((sec) => {
         if (!sec) return;
         expect(typeof html.renderSection(sec)).toBe('string');
         expect(text.textSection(sec, false).every((l) => typeof l === 'string')).toBe(true);
+        expect(svg.renderSectionSvg(sec).indexOf('NaN')).toBe(-1);
       });
       const cols = pages.nodeColumns();
       nodes.forEach((n) => cols.forEach((c) => c.getter(n)));
