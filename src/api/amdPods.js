@@ -21,19 +21,22 @@ import {
   parseCount,
 } from './k8sCore.js';
 
+const NO_RESOURCES = Object.freeze({});
+
+/** A container's `resources.requests` / `resources.limits` map, or an empty one. */
+function resourcesOf(c, which) {
+  const r = c !== null && typeof c === 'object' ? c.resources : undefined;
+  const m = r !== null && typeof r === 'object' ? r[which] : undefined;
+  return m !== null && typeof m === 'object' ? m : NO_RESOURCES;
+}
+
+/** The container's `amd.com/*` resource names: requested ones first, then limits-only ones. */
 function containerAmdKeys(c) {
-  const req = get(c, ['resources', 'requests'], {});
-  const lim = get(c, ['resources', 'limits'], {});
+  const req = resourcesOf(c, 'requests');
+  const lim = resourcesOf(c, 'limits');
   const keys = [];
-  const seen = {};
-  const all = Object.keys(req).concat(Object.keys(lim));
-  for (let i = 0; i < all.length; i++) {
-    const k = all[i];
-    if (k.indexOf(AMD_RESOURCE_PREFIX) === 0 && !seen[k]) {
-      seen[k] = true;
-      keys.push(k);
-    }
-  }
+  for (const k in req) if (k.indexOf(AMD_RESOURCE_PREFIX) === 0 && hasOwn.call(req, k)) keys.push(k);
+  for (const k in lim) if (k.indexOf(AMD_RESOURCE_PREFIX) === 0 && hasOwn.call(lim, k) && !hasOwn.call(req, k)) keys.push(k);
   return keys;
 }
 
@@ -83,7 +86,7 @@ export function filterGpuRequestingPods(items) {
 export function gpuContainers(pod) {
   const cs = get(pod, ['spec', 'containers'], []);
   const out = [];
-  for (let i = 0; i < cs.length; i++) if (containerAmdKeys(cs[i]).length > 0) out.push(cs[i]);
+  for (let i = 0; i < cs.length; i++) if (containerHasAmd(cs[i])) out.push(cs[i]);
   return out;
 }
 
@@ -91,7 +94,7 @@ export function gpuContainers(pod) {
 export function gpuInitContainers(pod) {
   const cs = get(pod, ['spec', 'initContainers'], []);
   const out = [];
-  for (let i = 0; i < cs.length; i++) if (containerAmdKeys(cs[i]).length > 0) out.push(cs[i]);
+  for (let i = 0; i < cs.length; i++) if (containerHasAmd(cs[i])) out.push(cs[i]);
   return out;
 }
 
@@ -101,8 +104,8 @@ export function gpuInitContainers(pod) {
  * @returns {Array<{ key: string, request: string|null, limit: string|null, effective: number }>}
  */
 export function containerGpuEntries(c) {
-  const req = get(c, ['resources', 'requests'], {});
-  const lim = get(c, ['resources', 'limits'], {});
+  const req = resourcesOf(c, 'requests');
+  const lim = resourcesOf(c, 'limits');
   const keys = containerAmdKeys(c);
   const out = [];
   for (let i = 0; i < keys.length; i++) {

@@ -20,6 +20,7 @@ import {
   partitionsPerGpu,
 } from './amdNodes.js';
 import { containerGpuEntries, getPodGpuCount, gpuContainers, gpuInitContainers, podPhase } from './amdPods.js';
+import { derivedCache } from './derivedCache.js';
 import { formatGpuResourceName, get, MI355X, pct } from './k8sCore.js';
 
 // Per-object facts the index needs, cached on the (immutable) object: a
@@ -71,8 +72,7 @@ export function taintsText(node) {
 
 /**
  * {phase, nodeName, gpus} of a GPU pod, derived once per object; `gpus` is
- * what the pod holds (0 once it terminated). `containers` is filled in by
- * podContainerLines, for the pods a page shows.
+ * what the pod holds (0 once it terminated).
  */
 export function podFacts(p) {
   let f = podFactCache.get(p);
@@ -84,7 +84,6 @@ export function podFacts(p) {
       // The kubelet allocates devices at admission and releases them when the
       // pod terminates, so a bound non-terminal pod holds its GPUs.
       gpus: phase !== 'Succeeded' && phase !== 'Failed' ? getPodGpuCount(p) : 0,
-      containers: null,
     };
     podFactCache.set(p, f);
   }
@@ -97,9 +96,10 @@ export function podFacts(p) {
  * not when the list arrives (a page shows 25 of 5,000 GPU pods).
  */
 export function podContainerLines(p) {
-  const f = podFacts(p);
-  return f.containers || (f.containers = containerLines(p));
+  return containerCache.has(p) ? containerCache.get(p) : containerCache.set(p, containerLines(p));
 }
+
+const containerCache = derivedCache();
 
 /**
  * One {label, text} per GPU container, init containers first ("trainer",

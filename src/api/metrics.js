@@ -17,6 +17,8 @@
  *   ./scopedSnapshots.js   one page of nodes (by name, small-cluster, ranked)
  *   ./ownerSnapshots.js    pod → GPU attribution (GPU Pods page)
  *   ./seriesFetch.js       power / HBM `query_range` series
+ *   ./nodeSummaries.js     per-node power / temperature / owner keys and link
+ *                          facts, derived as each snapshot arrives
  *
  * In short: the first query goes straight to the preferred service (its
  * answer is the discovery), then parallel time-boxed probes only if that
@@ -39,6 +41,7 @@ import { createClusterSnapshots } from './clusterSnapshots.js';
 import { createScopedSnapshots } from './scopedSnapshots.js';
 import { createOwnerSnapshots } from './ownerSnapshots.js';
 import { createSeriesFetch, seriesQueryFor } from './seriesFetch.js';
+import { primeSnapshot } from './nodeSummaries.js';
 
 
 /**
@@ -80,7 +83,7 @@ export function createMetricsSource(opts) {
    * @returns {Promise<GpuMetrics|null>}
    */
   function fetchGpuMetrics(view, opts) {
-    return deciding(telemetry(view, opts));
+    return deciding(telemetry(view, opts)).then(primeSnapshot);
   }
 
   /**
@@ -130,9 +133,9 @@ export function createMetricsSource(opts) {
     failureReason: client.failureReason,
     fetchGpuMetrics: fetchGpuMetrics,
     /** Telemetry of ONE node's GPUs (native Node / Pod detail pages), `hostname`-scoped. */
-    fetchNodeMetrics: function (nodeName) { return deciding(snaps.node(nodeName)); },
+    fetchNodeMetrics: function (nodeName) { return deciding(snaps.node(nodeName)).then(primeSnapshot); },
     /** Pod → GPU attribution (ownerSnapshots.js). */
-    fetchGpuOwners: owners.owners,
+    fetchGpuOwners: function (o) { return owners.owners(o).then(primeSnapshot); },
     /** Per-node power / HBM series over the last `rangeSec` (seriesFetch.js). */
     fetchSeries: series.series,
     /** A pod's GPU power over the last `rangeSec`: {rangeSec, stepSec, power: [[t, W]]}, or null. */

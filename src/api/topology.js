@@ -135,7 +135,8 @@ const factCache = typeof WeakMap === 'function' ? new WeakMap() : null;
  * in the platform model; the pairs `probed` types XGMI otherwise). Cached on
  * the map objects (the metrics client keeps a map's identity while its
  * values are unchanged; the measured topology is static), so a page that
- * re-renders, or mounts again, reads it once per answer.
+ * re-renders reads it once per answer. The metrics client derives them when
+ * an answer arrives (nodeSummaries.js primeSnapshot).
  * @param {number} n  GPUs of the node
  * @param {Record<string, number>|null} measured
  * @param {Record<string, {type: string, hops: number}>|null} probed  (non-empty, or null)

@@ -18,6 +18,7 @@ import {
   pct,
   pctToColor,
 } from '../../api/k8sCore.js';
+import { derivedCache, resetDerivedCaches } from '../../api/derivedCache.js';
 import { bar, createMemo, createObjectCache, kv, noteExpiry, row, section, status } from '../ir.js';
 
 export const BRAND = 'AMD GPU';
@@ -40,7 +41,7 @@ export const podRows = createObjectCache();
 export const pendingRows = createObjectCache();
 const ROW_CACHES = [ovPluginRows, dpPluginRows, nodeSummaryRows, podRows, pendingRows];
 
-export const podDetailCache = typeof WeakMap === 'function' ? new WeakMap() : null;
+export const podDetailCache = derivedCache();
 
 /**
  * Progressive loading: what has settled. A page waits only for the lists it
@@ -120,10 +121,11 @@ export function formatWindow(sec) {
   return sec + ' s';
 }
 
-/** Drop memoised sections (tests; cluster switch). */
+/** Drop memoised sections and the first-use derived caches (derivedCache.js): tests, a cluster switch, a cold mount. */
 export function clearViewMemo() {
   memo.clear();
   for (let i = 0; i < ROW_CACHES.length; i++) ROW_CACHES[i].clear();
+  resetDerivedCaches();
 }
 
 export function nowOf(opts) {

@@ -6,6 +6,8 @@
  */
 
 import { nodeFacts } from '../../api/clusterIndex.js';
+import { derivedCache } from '../../api/derivedCache.js';
+import { nodePowerKeys, nodeTempKeys, nonEmptyMap, ownersByNode } from '../../api/nodeSummaries.js';
 import { AMD_GPU_RESOURCE, formatBytes, formatGpuResourceName, get, MI355X } from '../../api/k8sCore.js';
 import { SMALL_CLUSTER_NODES } from '../../api/series.js';
 import { buildGpuSlots, buildXgmiMatrix, linkFacts } from '../../api/topology.js';
@@ -87,25 +89,8 @@ export function matrixBlock(gpuCount, measured, probed, open) {
   const n = gpuCount > 0 ? gpuCount : 0;
   // The caption and summary come from the link maps, in one pass; the 8 × 8
   // grid of cells is built on first read (a closed card never reads it).
-  return new MatrixBlock(n, measured && typeof measured === 'object' ? measured : null, hasKey(probed) ? probed : null,
+  return new MatrixBlock(n, measured && typeof measured === 'object' ? measured : null, nonEmptyMap(probed) ? probed : null,
     open === undefined ? true : !!open);
-}
-
-const nonEmpty = typeof WeakMap === 'function' ? new WeakMap() : null;
-
-/** `o` has an own key (answered once per map object: a link map is a 56-key dictionary, slow to enumerate). */
-function hasKey(o) {
-  if (!o || typeof o !== 'object') return false;
-  if (nonEmpty && nonEmpty.has(o)) return nonEmpty.get(o);
-  let any = false;
-  for (const k in o) {
-    if (Object.prototype.hasOwnProperty.call(o, k)) {
-      any = true;
-      break;
-    }
-  }
-  if (nonEmpty) nonEmpty.set(o, any);
-  return any;
 }
 
 /**
@@ -155,7 +140,7 @@ export function nodeReadyCell(node) {
   return cell;
 }
 
-const readyCells = typeof WeakMap === 'function' ? new WeakMap() : null;
+const readyCells = derivedCache();
 
 function readyCellOf(node) {
   const f = nodeFacts(node);
@@ -284,107 +269,9 @@ export function nodesView(ctx, opts) {
   return page(BRAND + ' — Nodes', refreshButton('Refresh node data', !!(opts && opts.fetching)), items);
 }
 
-const ownersCache = typeof WeakMap === 'function' ? new WeakMap() : null;
-
-let lastOwners = {};
-
-function sameOwners(a, b) {
-  if (!a || !b || a.length !== b.length) return false;
-  for (let i = 0; i < a.length; i++) {
-    if (a[i].gpu !== b[i].gpu || a[i].pod !== b[i].pod || a[i].namespace !== b[i].namespace) return false;
-  }
-  return true;
-}
-
-/**
- * node → [{gpu, pod, namespace}] from exporter pod labels, computed once per
- * GPU list; a node's array keeps its identity while its owners are unchanged
- * (telemetry values change every scrape, GPU ownership rarely).
- */
-const NO_OWNERS = Object.freeze({});
-
-export function ownersByNode(metrics) {
-  if (!metrics || !metrics.gpus) return NO_OWNERS;
-  if (ownersCache && ownersCache.has(metrics.gpus)) return ownersCache.get(metrics.gpus);
-  const out = {};
-  for (let i = 0; i < metrics.gpus.length; i++) {
-    const g = metrics.gpus[i];
-    if (!g.pod) continue;
-    if (!out[g.nodeName]) out[g.nodeName] = [];
-    out[g.nodeName].push({ gpu: g.gpu, pod: g.pod, namespace: g.namespace });
-  }
-  for (const k in out) {
-    if (sameOwners(lastOwners[k], out[k])) out[k] = lastOwners[k];
-  }
-  lastOwners = out;
-  if (ownersCache) ownersCache.set(metrics.gpus, out);
-  return out;
-}
-
-const powerKeyCache = typeof WeakMap === 'function' ? new WeakMap() : null;
-const tempKeyCache = typeof WeakMap === 'function' ? new WeakMap() : null;
-
-/** `compute(gs)` once per GPU list of a telemetry snapshot (the client keeps the list's identity while unchanged). */
-function perGpuList(cache, metrics, compute) {
-  const gs = metrics && Array.isArray(metrics.gpus) ? metrics.gpus : null;
-  if (!gs) return compute([]);
-  if (cache && cache.has(gs)) return cache.get(gs);
-  const v = compute(gs);
-  if (cache) cache.set(gs, v);
-  return v;
-}
-
-/** Per-node GPU power from a telemetry snapshot: {byNode: {node: "watts|cap"}, sig} (whole watts). */
-export function nodePowerKeys(metrics) {
-  return perGpuList(powerKeyCache, metrics, powerKeys);
-}
-
-function powerKeys(gs) {
-  const sum = {};
-  for (let i = 0; i < gs.length; i++) {
-    const g = gs[i];
-    if (typeof g.powerWatts !== 'number' || !isFinite(g.powerWatts)) continue;
-    const e = sum[g.nodeName] || (sum[g.nodeName] = [0, 0]);
-    e[0] += g.powerWatts;
-    e[1] += typeof g.powerCapWatts === 'number' && isFinite(g.powerCapWatts) ? g.powerCapWatts : 0;
-  }
-  const byNode = {};
-  const names = Object.keys(sum).sort();
-  for (let i = 0; i < names.length; i++) byNode[names[i]] = Math.round(sum[names[i]][0]) + '|' + Math.round(sum[names[i]][1]);
-  return { byNode: byNode, sig: names.map(function (n) { return n + '=' + byNode[n]; }).join(',') };
-}
-
-/**
- * The hottest GPU of each node (junction °C, whole degrees), its throttle
- * limit (the source's, else the MI355X's) and the status level its UNROUNDED
- * reading has against that limit (common.js tempCell): "temp|limit|level"
- * per node, so the summary rebuilds only when a shown value changes, and a
- * GPU at 99.6 °C under a 100 °C limit is a warning here as on the Metrics
- * page, not an error after rounding.
- */
-export function nodeTempKeys(metrics) {
-  return perGpuList(tempKeyCache, metrics, tempKeys);
-}
-
-function tempKeys(gs) {
-  const hot = {};
-  for (let i = 0; i < gs.length; i++) {
-    const g = gs[i];
-    if (typeof g.tempC !== 'number' || !isFinite(g.tempC)) continue;
-    const lim = typeof g.tempSlowdownC === 'number' && g.tempSlowdownC > 0 ? g.tempSlowdownC : MI355X.junctionSlowdownC;
-    const e = hot[g.nodeName];
-    if (!e || g.tempC > e[0]) hot[g.nodeName] = [g.tempC, lim];
-  }
-  const byNode = {};
-  const names = Object.keys(hot).sort();
-  for (let i = 0; i < names.length; i++) {
-    const t = hot[names[i]][0];
-    const lim = hot[names[i]][1];
-    const level = t >= lim ? 'error' : t >= lim - 10 ? 'warning' : 'ok';
-    byNode[names[i]] = Math.round(t) + '|' + Math.round(lim) + '|' + level;
-  }
-  return { byNode: byNode, sig: names.map(function (n) { return n + '=' + byNode[n]; }).join(',') };
-}
+// ownersByNode, nodePowerKeys, nodeTempKeys: per-node summaries of a
+// telemetry snapshot, derived when it arrives (api/nodeSummaries.js).
+export { nodePowerKeys, nodeTempKeys, ownersByNode };
 
 function nodeTempCell(key) {
   if (!key) return '—';

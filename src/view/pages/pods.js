@@ -12,6 +12,7 @@ import {
   podWaitingReason,
 } from '../../api/amdPods.js';
 import { podContainerLines, podFacts } from '../../api/clusterIndex.js';
+import { podGpuAssignments } from '../../api/nodeSummaries.js';
 import { formatBytes, formatWatts } from '../../api/k8sCore.js';
 import { SMALL_CLUSTER_PODS } from '../../api/series.js';
 import { kv, lines, loader, page, pager, row, section, status, table } from '../ir.js';
@@ -50,45 +51,9 @@ function rankedPodPage(ctx, m, state) {
   });
 }
 
-let lastAssign = {};
-
-function sameAssign(a, b) {
-  if (!a || !b || a.length !== b.length) return false;
-  for (let i = 0; i < a.length; i++) if (a[i] !== b[i]) return false;
-  return true;
-}
-
-/**
- * "namespace/pod" → the GPUs the exporter attributes to that pod (its
- * pod/namespace labels), as GPU objects of the metrics snapshot. Kubernetes
- * itself does not say which device a pod got; this is the exporter's view.
- * A pod's array keeps its identity while its GPUs are the same objects
- * (see the metrics client's structural sharing), and the whole map keeps
- * its identity while no pod's list changed.
- */
-export function podGpuAssignments(metrics) {
-  if (!metrics || !metrics.gpus) return {};
-  if (assignCache && assignCache.has(metrics.gpus)) return assignCache.get(metrics.gpus);
-  const out = {};
-  for (let i = 0; i < metrics.gpus.length; i++) {
-    const g = metrics.gpus[i];
-    if (!g.pod) continue;
-    const k = (g.namespace || '') + '/' + g.pod;
-    if (!out[k]) out[k] = [];
-    out[k].push(g);
-  }
-  let same = Object.keys(out).length === Object.keys(lastAssign).length;
-  for (const k in out) {
-    if (sameAssign(lastAssign[k], out[k])) out[k] = lastAssign[k];
-    else same = false;
-  }
-  const res = same ? lastAssign : out;
-  lastAssign = res;
-  if (assignCache) assignCache.set(metrics.gpus, res);
-  return res;
-}
-
-const assignCache = typeof WeakMap === 'function' ? new WeakMap() : null;
+// podGpuAssignments: "namespace/pod" → the GPUs the exporter attributes to
+// the pod, derived when a telemetry snapshot arrives (api/nodeSummaries.js).
+export { podGpuAssignments };
 
 export function assignedLines(gs) {
   return lines(

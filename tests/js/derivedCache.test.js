@@ -1,0 +1,72 @@
+/**
+ * What a cold mount pays for (api/derivedCache.js) and what the data layer
+ * derived on arrival (api/nodeSummaries.js, clusterIndex.js facts): the view
+ * memo's reset (clearViewMemo — a cluster switch, tests, the render
+ * comparison's first-render-of-a-session mount) empties the first; the second
+ * stays with its objects.
+ */
+import { derivedCache, resetDerivedCaches } from '../../src/api/derivedCache.js';
+import { nodeFacts, podContainerLines } from '../../src/api/clusterIndex.js';
+import { nodePowerKeys, ownersByNode, podGpuAssignments, primeSnapshot } from '../../src/api/nodeSummaries.js';
+import { linkFacts } from '../../src/api/topology.js';
+import { clearViewMemo } from '../../src/view/pages/common.js';
+import { nodeReadyCell } from '../../src/view/pages/nodes.js';
+import { makeGpuNode, makeGpuPod } from './fixtures.js';
+
+function snapshot() {
+  const gpus = [];
+  for (let i = 0; i < 8; i++) {
+    gpus.push({ nodeName: 'n1', gpu: String(i), powerWatts: 1000 + i, powerCapWatts: 1400, tempC: 60 + i, pod: i < 2 ? 'train' : null, namespace: 'ml' });
+  }
+  const xgmi = { n1: {} };
+  for (let i = 0; i < 8; i++) for (let j = 0; j < 8; j++) if (i !== j) xgmi.n1[i + '-' + j] = 10;
+  return { gpus: gpus, xgmi: xgmi, links: {} };
+}
+
+describe('derivedCache', () => {
+  it('resetDerivedCaches empties every registered cache and runs its reset hook', () => {
+    const c = derivedCache();
+    let hook = 0;
+    c.onReset = () => { hook++; };
+    const k = {};
+    expect(c.set(k, 1)).toBe(1);
+    expect(c.has(k)).toBe(true);
+    resetDerivedCaches();
+    expect(c.has(k)).toBe(false);
+    expect(hook).toBe(1);
+  });
+
+  it('clearViewMemo drops first-use view facts: a ready cell, a pod\'s container lines', () => {
+    const node = makeGpuNode('n1');
+    const pod = makeGpuPod('a', { gpus: 2 });
+    const cell = nodeReadyCell(node);
+    const lines = podContainerLines(pod);
+    expect(nodeReadyCell(node)).toBe(cell);
+    expect(podContainerLines(pod)).toBe(lines);
+    clearViewMemo();
+    expect(nodeReadyCell(node)).not.toBe(cell);
+    expect(nodeReadyCell(node)).toEqual(cell);
+    expect(podContainerLines(pod)).not.toBe(lines);
+    expect(podContainerLines(pod)).toEqual(lines);
+  });
+
+  it('facts derived on arrival stay: node facts, and a primed snapshot\'s summaries and link facts', () => {
+    const node = makeGpuNode('n1');
+    const f = nodeFacts(node);
+    const m = primeSnapshot(snapshot());
+    const power = nodePowerKeys(m);
+    const owners = ownersByNode(m);
+    const assign = podGpuAssignments(m);
+    const links = linkFacts(8, m.xgmi.n1, null);
+    clearViewMemo();
+    expect(nodeFacts(node)).toBe(f);
+    expect(nodePowerKeys(m)).toBe(power);
+    expect(ownersByNode(m)).toBe(owners);
+    expect(podGpuAssignments(m)).toBe(assign);
+    expect(linkFacts(8, m.xgmi.n1, null)).toBe(links);
+    expect(power.byNode.n1).toBe('8028|11200');
+    expect(owners.n1.map((o) => o.gpu)).toEqual(['0', '1']);
+    expect(assign['ml/train']).toHaveLength(2);
+    expect(links).toEqual({ fullMesh: true, linksPerGpu: 7, stats: { links: 56, meanGBs: 10, maxGBs: 10 } });
+  });
+});
