@@ -21,7 +21,7 @@ import {
 } from './amdNodes.js';
 import { containerGpuEntries, getPodGpuCount, gpuContainers, gpuInitContainers, podPhase } from './amdPods.js';
 import { derivedCache } from './derivedCache.js';
-import { formatGpuResourceName, get, MI355X, pct } from './k8sCore.js';
+import { AMD_GPU_RESOURCE, formatBytes, formatGpuResourceName, get, MI355X, pct } from './k8sCore.js';
 
 // Per-object facts the index needs, cached on the (immutable) object: a
 // watch event that changes one pod re-derives that pod only.
@@ -58,9 +58,61 @@ export function nodeFacts(n) {
       driverVersion: labellerValue(n, 'driver-version'),
       osText: [info.osImage || '—', info.kernelVersion || '—', info.kubeletVersion || '—'].join(' · '),
     };
+    // Readiness as `kubectl get nodes` words it; a cordoned node's free GPUs
+    // are not schedulable, hence a warning.
+    f.readyText = (f.ready ? 'Ready' : 'Not Ready') + (f.cordoned ? ', SchedulingDisabled' : '');
+    f.readyLevel = !f.ready ? 'error' : f.cordoned ? 'warning' : 'success';
+    f.card = cardRows(f);
     nodeFactCache.set(n, f);
   }
   return f;
+}
+
+const hbmTexts = {};
+
+/** HBM of `phys` MI355X boards, formatted once per board count. */
+function hbmText(phys) {
+  return hbmTexts[phys] || (hbmTexts[phys] = formatBytes(phys * MI355X.hbmBytes));
+}
+
+/**
+ * A GPU Nodes card's rows that the node alone decides, as {name, value}:
+ * `before` the workload pods (taints, devices, HBM, per-resource capacity /
+ * allocatable, partition mode, driver), `after` them (node info). The
+ * summary row on the same page carries readiness, model and age (the
+ * reference repeats them on its card, NodesPage.tsx:69-139).
+ */
+function cardRows(f) {
+  const model = f.model;
+  const count = f.capacity;
+  const cap = f.capacityResources;
+  const alloc = f.allocatableResources;
+  const before = [];
+  if (f.taints) before.push({ name: 'Taints', value: f.taints });
+  // One resource (the usual amd.com/gpu): its capacity and allocatable are
+  // said on the device row (the reference gives them a row each,
+  // NodesPage.tsx:98-113); several (partitioned resources) keep their rows.
+  const capKeys = Object.keys(cap);
+  const single = capKeys.length === 1 && capKeys[0] === AMD_GPU_RESOURCE && Object.keys(alloc).length <= 1;
+  if (count > 0) {
+    const phys = f.physicalGpus;
+    const devices = phys !== count ? count + ' (' + phys + ' × ' + model.shortName + ' in ' + model.computePartition + ')' : String(count);
+    before.push({
+      name: 'GPU Devices (amd.com/gpu)',
+      value: single
+        ? devices + ' · capacity ' + cap[AMD_GPU_RESOURCE] + ', allocatable ' + (alloc[AMD_GPU_RESOURCE] !== undefined ? alloc[AMD_GPU_RESOURCE] : '—')
+        : devices,
+    });
+    before.push({ name: 'HBM', value: hbmText(phys) + ' (' + phys + ' × ' + model.vram + ')' });
+  }
+  if (!single || count === 0) {
+    for (const k in cap) before.push({ name: formatGpuResourceName(k) + ' (capacity)', value: cap[k] });
+    for (const k in alloc) before.push({ name: formatGpuResourceName(k) + ' (allocatable)', value: alloc[k] });
+  }
+  if (model.computePartition || model.memoryPartition) before.push({ name: 'Partition Mode', value: f.modelText });
+  if (f.driverVersion) before.push({ name: 'amdgpu Driver', value: f.driverVersion });
+  // OS image, kernel and kubelet on one row (the reference: a row each, NodesPage.tsx:124-126).
+  return { before: before, after: [{ name: 'OS / Kernel / Kubelet', value: f.osText }] };
 }
 
 /** "key=value:Effect" per taint, or null (the reference models NodeSpec.taints, k8s.ts:92-122, but never shows them). */

@@ -38,6 +38,7 @@ import { dedupePods, filterAmdGpuPluginPods, isAmdGpuPluginPod, isGpuRequestingP
 import { buildClusterIndex, patchClusterIndex } from './clusterIndex.js';
 import { DEVICE_CONFIG_LIST_PATH, isKubeList, PLUGIN_POD_QUERIES } from './k8sCore.js';
 import { createListTracker } from './listCache.js';
+import { primeOperatorFacts } from './operatorFacts.js';
 import { DEFAULT_REQUEST_TIMEOUT_MS, defaultClock, isAbsent, sameObjects, withTimeout } from './requests.js';
 
 export { DEFAULT_REQUEST_TIMEOUT_MS, fetchNodePods, isAbsent, nodePodsPath, nodePodsSelector, sameObjects, withTimeout } from './requests.js';
@@ -230,6 +231,9 @@ export function createClusterStore(opts) {
     return memoIndex;
   }
 
+  let primedConfigs = null;
+  let primedOperatorPods = null;
+
   function build() {
     const n = gpuNodes();
     const p = gpuPods();
@@ -238,6 +242,13 @@ export function createClusterStore(opts) {
     if (s.podError) errors.push(String(s.podError));
     if (s.asyncError) errors.push(s.asyncError);
     const pp = pluginPods();
+    // The operator's objects' facts, once per list (operatorFacts.js; the
+    // index build does the same for GPU nodes and pods).
+    if (s.deviceConfigs !== primedConfigs || pp !== primedOperatorPods) {
+      primeOperatorFacts(s.deviceConfigs, pp);
+      primedConfigs = s.deviceConfigs;
+      primedOperatorPods = pp;
+    }
     version++;
     return Object.freeze({
       deviceConfigs: s.deviceConfigs,

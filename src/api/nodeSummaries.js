@@ -4,11 +4,13 @@
  * snapshot's objects (the client keeps them by identity while unchanged):
  *
  *   * nodePowerKeys: each node's GPU power against its summed caps,
- *     "watts|cap" in whole watts;
+ *     "watts|cap" in whole watts, and the bar the GPU Nodes summary draws;
  *   * nodeTempKeys: each node's hottest junction temperature, its throttle
- *     limit and the level of the unrounded reading, "temp|limit|level";
+ *     limit and the level of the unrounded reading, "temp|limit|level", and
+ *     the cell's text;
  *   * ownersByNode: node → [{gpu, pod, namespace}] from exporter pod labels;
- *   * podGpuAssignments: "namespace/pod" → the GPUs attributed to the pod;
+ *   * podGpuAssignments: "namespace/pod" → the GPUs attributed to the pod,
+ *     and assignmentTexts, the GPU Pods row's "Assigned GPUs" and "GPU Power";
  *   * nonEmptyMap / topology.js linkFacts of every node's link maps.
  *
  * They are data-layer facts, like clusterIndex.js nodeFacts at list arrival:
@@ -16,7 +18,7 @@
  * snapshot made elsewhere (a test) derives them on first read.
  */
 
-import { MI355X } from './k8sCore.js';
+import { BAR_COLORS, formatPercent, formatWatts, MI355X, pct, pctToColor } from './k8sCore.js';
 import { linkFacts } from './topology.js';
 
 const powerKeyCache = new WeakMap();
@@ -24,6 +26,7 @@ const tempKeyCache = new WeakMap();
 const ownersCache = new WeakMap();
 const nonEmpty = new WeakMap();
 const assignCache = new WeakMap();
+const textCache = new WeakMap();
 
 /** `compute(gs)` once per GPU list of a telemetry snapshot. */
 function perGpuList(cache, metrics, compute) {
@@ -35,7 +38,10 @@ function perGpuList(cache, metrics, compute) {
   return v;
 }
 
-/** Per-node GPU power from a telemetry snapshot: {byNode: {node: "watts|cap"}, sig} (whole watts). */
+/**
+ * Per-node GPU power from a telemetry snapshot: {byNode: {node: "watts|cap"}, sig, bars: {node: {watts, cap, pct,
+ * color, text}}} in whole watts; `cap` null without a cap (pages/common.js powerBar's text and colours).
+ */
 export function nodePowerKeys(metrics) {
   return perGpuList(powerKeyCache, metrics, powerKeys);
 }
@@ -50,9 +56,28 @@ function powerKeys(gs) {
     e[1] += typeof g.powerCapWatts === 'number' && isFinite(g.powerCapWatts) ? g.powerCapWatts : 0;
   }
   const byNode = {};
+  const bars = {};
   const names = Object.keys(sum).sort();
-  for (let i = 0; i < names.length; i++) byNode[names[i]] = Math.round(sum[names[i]][0]) + '|' + Math.round(sum[names[i]][1]);
-  return { byNode: byNode, sig: names.map(function (n) { return n + '=' + byNode[n]; }).join(',') };
+  for (let i = 0; i < names.length; i++) {
+    const w = Math.round(sum[names[i]][0]);
+    const c = Math.round(sum[names[i]][1]);
+    byNode[names[i]] = w + '|' + c;
+    bars[names[i]] = powerBarFacts(w, c > 0 ? c : null);
+  }
+  return { byNode: byNode, sig: names.map(function (n) { return n + '=' + byNode[n]; }).join(','), bars: bars };
+}
+
+/** The power bar's numbers and text: "X W / Y W (Z%)", coloured at 70 / 90 % (reference PowerBar, MetricsPage.tsx:50-89). */
+export function powerBarFacts(watts, capWatts) {
+  const hasCap = capWatts !== null && capWatts > 0;
+  const p = hasCap ? Math.min(100, pct(watts, capWatts)) : null;
+  return {
+    watts: watts,
+    cap: hasCap ? capWatts : null,
+    pct: p,
+    color: p === null ? BAR_COLORS.ok : pctToColor(p),
+    text: formatWatts(watts) + (hasCap ? ' / ' + formatWatts(capWatts) + ' (' + formatPercent(watts, capWatts) + ')' : ''),
+  };
 }
 
 /**
@@ -77,14 +102,17 @@ function tempKeys(gs) {
     if (!e || g.tempC > e[0]) hot[g.nodeName] = [g.tempC, lim];
   }
   const byNode = {};
+  const cells = {};
   const names = Object.keys(hot).sort();
   for (let i = 0; i < names.length; i++) {
     const t = hot[names[i]][0];
     const lim = hot[names[i]][1];
     const level = t >= lim ? 'error' : t >= lim - 10 ? 'warning' : 'ok';
     byNode[names[i]] = Math.round(t) + '|' + Math.round(lim) + '|' + level;
+    const text = Math.round(t) + ' °C';
+    cells[names[i]] = { level: level, text: level === 'error' ? text + ' (throttling at ' + Math.round(lim) + ' °C)' : text };
   }
-  return { byNode: byNode, sig: names.map(function (n) { return n + '=' + byNode[n]; }).join(',') };
+  return { byNode: byNode, sig: names.map(function (n) { return n + '=' + byNode[n]; }).join(','), cells: cells };
 }
 
 let lastOwners = {};
@@ -160,6 +188,50 @@ export function podGpuAssignments(metrics) {
   return res;
 }
 
+/** A pod's summed GPU power ("2393.4 W"), or "—" without a reading. */
+export function podPowerText(gs) {
+  if (!gs || !gs.length) return '—';
+  let w = 0;
+  let any = false;
+  for (let i = 0; i < gs.length; i++) {
+    if (typeof gs[i].powerWatts === 'number' && isFinite(gs[i].powerWatts)) {
+      w += gs[i].powerWatts;
+      any = true;
+    }
+  }
+  return any ? formatWatts(w) : '—';
+}
+
+function assignedText(gs) {
+  const byNode = {};
+  const order = [];
+  for (let i = 0; i < gs.length; i++) {
+    if (!byNode[gs[i].nodeName]) {
+      byNode[gs[i].nodeName] = [];
+      order.push(gs[i].nodeName);
+    }
+    byNode[gs[i].nodeName].push(gs[i].gpu);
+  }
+  return order.map(function (n) { return n + ': GPU ' + byNode[n].join(', '); }).join('; ');
+}
+
+const NO_ASSIGNMENT = Object.freeze({ assigned: '—', power: '—' });
+
+/**
+ * A pod's GPUs as its GPU Pods row says them: {assigned: "n1: GPU 2, 3",
+ * power: "2393.4 W"}, once per assignment array (podGpuAssignments keeps an
+ * unchanged pod's array).
+ */
+export function assignmentTexts(gs) {
+  if (!gs || !gs.length) return NO_ASSIGNMENT;
+  let t = textCache.get(gs);
+  if (!t) {
+    t = { assigned: assignedText(gs), power: podPowerText(gs) };
+    textCache.set(gs, t);
+  }
+  return t;
+}
+
 /** `o` is an object with an own key (answered once per map: a link map is a 56-key dictionary, slow to enumerate). */
 export function nonEmptyMap(o) {
   if (!o || typeof o !== 'object') return false;
@@ -186,7 +258,8 @@ export function primeSnapshot(m) {
   nodePowerKeys(m);
   nodeTempKeys(m);
   ownersByNode(m);
-  podGpuAssignments(m);
+  const assign = podGpuAssignments(m);
+  for (const k in assign) assignmentTexts(assign[k]);
   const xgmi = m.xgmi || {};
   const links = m.links || {};
   const nodes = {};

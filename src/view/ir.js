@@ -117,25 +117,38 @@ export function page(title, refresh, items) {
 // the first label it shows changes. While a section or row is built, the
 // earliest such instant is collected here (noteExpiry), so a cached value can
 // be reused until then instead of being rebuilt on every clock tick.
-let horizon = null;
+// `building`: a value is being built; `until`: its earliest label change so
+// far; `lastUntil`: the horizon of the value computeWithHorizon just built.
+// Plain variables, saved and restored around nested builds: a cold page
+// build makes a few dozen memo entries, and an object per entry for its
+// horizon was a measurable share of it.
+let building = false;
+let until = Infinity;
+let lastUntil = Infinity;
 
 /** Record that the value being built changes at epoch-ms `t`. */
 export function noteExpiry(t) {
-  if (horizon !== null && t < horizon.until) horizon.until = t;
+  if (building && t < until) until = t;
 }
 
+/** `compute()`, noting the earliest label change inside it in `lastUntil` (and in the enclosing build). */
 function computeWithHorizon(compute) {
-  const saved = horizon;
-  const h = { until: Infinity };
-  horizon = h;
+  const savedBuilding = building;
+  const savedUntil = until;
+  building = true;
+  until = Infinity;
   let value;
+  let mine;
   try {
     value = compute();
   } finally {
-    horizon = saved;
+    mine = until;
+    building = savedBuilding;
+    until = savedUntil;
   }
-  noteExpiry(h.until); // a nested value bounds the enclosing one
-  return { value: value, until: h.until };
+  noteExpiry(mine); // a nested value bounds the enclosing one
+  lastUntil = mine;
+  return value;
 }
 
 function sameDeps(a, b) {
@@ -169,11 +182,12 @@ export function createMemo(limit) {
       noteExpiry(e.until);
       return e.value;
     }
-    const r = computeWithHorizon(compute);
-    slots.delete(key);
-    slots.set(key, { deps: deps, value: r.value, until: r.until, from: now === undefined ? -Infinity : now });
+    const value = computeWithHorizon(compute);
+    // Most recently built last (the LRU order): an entry being replaced moves to the end.
+    if (e) slots.delete(key);
+    slots.set(key, { deps: deps, value: value, until: lastUntil, from: now === undefined ? -Infinity : now });
     if (slots.size > max) slots.delete(slots.keys().next().value);
-    return r.value;
+    return value;
   }
   memo.clear = function () { slots.clear(); };
   memo.size = function () { return slots.size; };
@@ -194,9 +208,9 @@ export function createObjectCache() {
       noteExpiry(e.until);
       return e.value;
     }
-    const r = computeWithHorizon(compute);
-    cache.set(obj, { deps: deps, value: r.value, until: r.until, from: now === undefined ? -Infinity : now });
-    return r.value;
+    const value = computeWithHorizon(compute);
+    cache.set(obj, { deps: deps, value: value, until: lastUntil, from: now === undefined ? -Infinity : now });
+    return value;
   }
   cached.clear = function () { cache = new WeakMap(); };
   return cached;

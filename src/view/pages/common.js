@@ -7,11 +7,8 @@
 
 import { getPodRestarts, isPodReady } from '../../api/amdPods.js';
 import {
-  BAR_COLORS,
   formatAge,
   formatBytes,
-  formatPercent,
-  formatWatts,
   get,
   MI355X,
   nextAgeChange,
@@ -19,6 +16,7 @@ import {
   pctToColor,
 } from '../../api/k8sCore.js';
 import { derivedCache, resetDerivedCaches } from '../../api/derivedCache.js';
+import { powerBarFacts } from '../../api/nodeSummaries.js';
 import { bar, createMemo, createObjectCache, kv, noteExpiry, row, section, status } from '../ir.js';
 
 export const BRAND = 'AMD GPU';
@@ -191,10 +189,8 @@ export function seriesMeans(byNode) {
 
 /** Power bar: "X W / Y W (Z%)" with 70/90 colouring (reference PowerBar, MetricsPage.tsx:50-89). */
 export function powerBar(watts, capWatts) {
-  const hasCap = capWatts !== null && capWatts > 0;
-  const p = hasCap ? Math.min(100, pct(watts, capWatts)) : null;
-  const txt = formatWatts(watts) + (hasCap ? ' / ' + formatWatts(capWatts) + ' (' + formatPercent(watts, capWatts) + ')' : '');
-  return bar(watts, hasCap ? capWatts : null, p, p === null ? BAR_COLORS.ok : pctToColor(p), txt);
+  const f = powerBarFacts(watts, capWatts);
+  return bar(f.watts, f.cap, f.pct, f.color, f.text);
 }
 
 export function hbmBar(used, total) {

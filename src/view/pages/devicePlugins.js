@@ -4,17 +4,7 @@
  * GPU Operator DeviceConfig and one page of operator pods.
  */
 
-import {
-  countsToStatus,
-  countsToText,
-  deviceConfigStatus,
-  deviceConfigStatusText,
-  formatSelector,
-  operandEnabled,
-  operandStatus,
-} from '../../api/amdNodes.js';
-import { formatComponent, pluginPodComponent } from '../../api/amdPods.js';
-import { get } from '../../api/k8sCore.js';
+import { deviceConfigFacts, operatorPodFacts } from '../../api/operatorFacts.js';
 import { kv, loader, page, pager, row, section, status, table } from '../ir.js';
 import {
   ageText,
@@ -25,35 +15,14 @@ import {
   memo,
   nowOf,
   podName,
-  podNode,
   podNs,
-  readyLabel,
   refreshButton,
-  restartsCell,
   crdPending,
   pluginPodsPending,
 } from './common.js';
 import { podPage } from './paging.js';
 
-/** DeviceConfig operands of later AMD GPU Operator releases (`spec.<key>.enable`). */
-const EXTRA_OPERANDS = [
-  { key: 'testRunner', label: 'Test Runner' },
-  { key: 'configManager', label: 'Config Manager' },
-];
-
-/**
- * An operand's row: "Disabled", or "Enabled" (— its version / port) and, when
- * the DeviceConfig's status counts its DaemonSet, "· ready/desired" in the
- * same cell, coloured by the pods (one row per operand; the reference has no
- * operand rows, DevicePluginsPage.tsx:115-180).
- */
-function operandCell(dc, key, detail, counted) {
-  if (!operandEnabled(dc, key)) return status('warning', 'Disabled');
-  const head = detail ? 'Enabled — ' + detail : 'Enabled';
-  if (!counted) return status('success', head);
-  const st = operandStatus(dc, key);
-  return status(countsToStatus(st.desired, st.available), head + ' · ' + countsToText(st.desired, st.available));
-}
+const READY = status('success', 'Ready');
 
 /**
  * One card per DeviceConfig (reference: one per GpuDevicePlugin). Per-operand
@@ -121,31 +90,24 @@ function devicePluginsItems(ctx, now, pg, podsPend) {
 
   for (let i = 0; i < ctx.deviceConfigs.length; i++) {
     const dc = ctx.deviceConfigs[i];
-    const dp = operandStatus(dc, 'devicePlugin');
+    // Derived when the store took the list (api/operatorFacts.js).
+    const f = deviceConfigFacts(dc);
     const rows = [
-      row('Status', status(deviceConfigStatus(dc), deviceConfigStatusText(dc))),
-      row('Namespace', dc.metadata.namespace || '—'),
-      row('Device Plugin Image', get(dc, ['spec', 'devicePlugin', 'devicePluginImage'], '—')),
-      row('Driver', operandCell(dc, 'driver', get(dc, ['spec', 'driver', 'version'], null), true)),
-      row('Node Labeller', operandCell(dc, 'nodeLabeller', null, true)),
-      row(
-        'Metrics Exporter',
-        operandCell(dc, 'metricsExporter',
-          get(dc, ['spec', 'metricsExporter', 'port'], null) !== null ? 'port ' + get(dc, ['spec', 'metricsExporter', 'port'], '') : null, true)
-      ),
-      row('Desired Nodes', String(dp.desired)),
-      row('Ready Nodes', String(dp.available)),
+      row('Status', status(f.level, f.text)),
+      row('Namespace', f.namespace),
+      row('Device Plugin Image', f.image),
+      row('Driver', status(f.driver.level, f.driver.text)),
+      row('Node Labeller', status(f.nodeLabeller.level, f.nodeLabeller.text)),
+      row('Metrics Exporter', status(f.metricsExporter.level, f.metricsExporter.text)),
+      row('Desired Nodes', String(f.plugin.desired)),
+      row('Ready Nodes', String(f.plugin.available)),
     ];
-    if (dp.unavailable > 0) rows.push(row('Unavailable Nodes', status('error', dp.unavailable)));
+    if (f.plugin.unavailable > 0) rows.push(row('Unavailable Nodes', status('error', f.plugin.unavailable)));
     // Later operator releases' operands (GPU test runner, partition config
     // manager): shown when the DeviceConfig names them, their DaemonSet
     // counts when its status reports them.
-    for (let k = 0; k < EXTRA_OPERANDS.length; k++) {
-      const op = EXTRA_OPERANDS[k];
-      if (get(dc, ['spec', op.key], null) === null) continue;
-      rows.push(row(op.label, operandCell(dc, op.key, null, get(dc, ['status', op.key], null) !== null)));
-    }
-    rows.push(row('Node Selector', formatSelector(get(dc, ['spec', 'selector'], null))));
+    for (let k = 0; k < f.extra.length; k++) rows.push(row(f.extra[k].label, status(f.extra[k].level, f.extra[k].text)));
+    rows.push(row('Node Selector', f.selector));
     rows.push(row('Age', ageText(dc.metadata.creationTimestamp, now)));
     items.push(section('DeviceConfig: ' + dc.metadata.name, [kv(rows)], dc.metadata.uid || dc.metadata.name));
   }
@@ -160,9 +122,10 @@ function devicePluginsItems(ctx, now, pg, podsPend) {
           ['Name', 'Namespace', 'Component', 'Node', 'Ready', 'Restarts', 'Age'],
           chunkedRows('dp-plugin-rows', pg.nodes, [], function (p) {
             return dpPluginRows(p, [], function () {
+              const f = operatorPodFacts(p);
               return [
-                podName(p), podNs(p), formatComponent(pluginPodComponent(p)), podNode(p), readyLabel(p),
-                restartsCell(p), ageText(p.metadata.creationTimestamp, now),
+                podName(p), podNs(p), f.component, f.node, f.ready ? READY : status('warning', f.phase),
+                f.restarts > 0 ? status('warning', f.restarts) : String(f.restarts), ageText(p.metadata.creationTimestamp, now),
               ];
             }, now);
           }, now)

@@ -6,12 +6,11 @@
  */
 
 import { nodeFacts } from '../../api/clusterIndex.js';
-import { derivedCache } from '../../api/derivedCache.js';
 import { nodePowerKeys, nodeTempKeys, nonEmptyMap, ownersByNode } from '../../api/nodeSummaries.js';
-import { AMD_GPU_RESOURCE, formatBytes, formatGpuResourceName, get, MI355X } from '../../api/k8sCore.js';
+import { MI355X } from '../../api/k8sCore.js';
 import { SMALL_CLUSTER_NODES } from '../../api/series.js';
 import { buildGpuSlots, buildXgmiMatrix, linkFacts } from '../../api/topology.js';
-import { kv, loader, page, pager, row, section, status, table } from '../ir.js';
+import { bar, kv, loader, page, pager, row, section, status, table } from '../ir.js';
 import {
   ageText,
   allocationBar,
@@ -23,7 +22,6 @@ import {
   nodeSummaryRows,
   nowOf,
   podName,
-  powerBar,
   refreshButton,
   nodesPending,
   PODS_LOADING,
@@ -126,28 +124,17 @@ Object.defineProperty(MatrixBlock.prototype, 'matrix', {
   },
 });
 
+const READY_CELLS = {};
+
 /**
  * Readiness as `kubectl get nodes` words it: "Ready", "Not Ready", and
  * ", SchedulingDisabled" on a cordoned node (spec.unschedulable) — whose free
- * GPUs new pods cannot use, hence a warning.
+ * GPUs new pods cannot use, hence a warning (clusterIndex.js nodeFacts). One
+ * cell per wording.
  */
 export function nodeReadyCell(node) {
-  // One cell per node object (the summary row and the card both show it).
-  const key = node && typeof node === 'object' ? node : null;
-  if (readyCells && key && readyCells.has(key)) return readyCells.get(key);
-  const cell = readyCellOf(node);
-  if (readyCells && key) readyCells.set(key, cell);
-  return cell;
-}
-
-const readyCells = derivedCache();
-
-function readyCellOf(node) {
   const f = nodeFacts(node);
-  const ready = f.ready;
-  const cordoned = f.cordoned;
-  const text = (ready ? 'Ready' : 'Not Ready') + (cordoned ? ', SchedulingDisabled' : '');
-  return status(!ready ? 'error' : cordoned ? 'warning' : 'success', text);
+  return READY_CELLS[f.readyText] || (READY_CELLS[f.readyText] = status(f.readyLevel, f.readyText));
 }
 
 /** "key=value:Effect" per taint (clusterIndex.js taintsText, cached per node object). */
@@ -156,49 +143,13 @@ export function formatTaints(node) {
 }
 
 function nodeCardRows(node, podsOnNode, now, podsPend) {
-  // Everything but the pods and the age was derived when the node list
-  // arrived (clusterIndex.js nodeFacts), not on this render.
-  const f = nodeFacts(node);
-  const model = f.model;
-  const count = f.capacity;
-  const cap = f.capacityResources;
-  const alloc = f.allocatableResources;
-  // Readiness, GPU model and age are the node's summary row on this page
-  // (the reference repeats them on its card, NodesPage.tsx:69-139); the card
-  // holds what the row does not.
-  const rows = [];
-  if (f.taints) rows.push(row('Taints', f.taints));
-  // One resource (the usual amd.com/gpu): its capacity and allocatable are
-  // said on the device row (the reference gives them a row each,
-  // NodesPage.tsx:98-113); several (partitioned resources) keep their rows.
-  const capKeys = Object.keys(cap);
-  const single = capKeys.length === 1 && capKeys[0] === AMD_GPU_RESOURCE && Object.keys(alloc).length <= 1;
-  if (count > 0) {
-    const phys = f.physicalGpus;
-    const devices = phys !== count ? count + ' (' + phys + ' × ' + model.shortName + ' in ' + model.computePartition + ')' : String(count);
-    rows.push(row('GPU Devices (amd.com/gpu)', single
-      ? devices + ' · capacity ' + cap[AMD_GPU_RESOURCE] + ', allocatable ' + (alloc[AMD_GPU_RESOURCE] !== undefined ? alloc[AMD_GPU_RESOURCE] : '—')
-      : devices));
-    rows.push(row('HBM', hbmText(phys) + ' (' + phys + ' × ' + model.vram + ')'));
-  }
-  if (!single || count === 0) {
-    for (const k in cap) rows.push(row(formatGpuResourceName(k) + ' (capacity)', cap[k]));
-    for (const k in alloc) rows.push(row(formatGpuResourceName(k) + ' (allocatable)', alloc[k]));
-  }
-  // The node's allocation bar is its summary row's (the reference's card has none either, NodesPage.tsx:69-139).
-  if (model.computePartition || model.memoryPartition) rows.push(row('Partition Mode', f.modelText));
-  if (f.driverVersion) rows.push(row('amdgpu Driver', f.driverVersion));
-  rows.push(row('GPU Workload Pods', podsPend ? PODS_LOADING : podsOnNode.length > 0 ? podsOnNode.map(podName).join(', ') : '—'));
-  // OS image, kernel and kubelet on one row (the reference: a row each, NodesPage.tsx:124-126).
-  rows.push(row('OS / Kernel / Kubelet', f.osText));
-  return rows;
-}
-
-const hbmTexts = {};
-
-/** HBM of `phys` MI355X boards, formatted once per board count. */
-function hbmText(phys) {
-  return hbmTexts[phys] || (hbmTexts[phys] = formatBytes(phys * MI355X.hbmBytes));
+  // Everything but the pods was derived when the node list arrived
+  // (clusterIndex.js nodeFacts `card`), not on this render.
+  const card = nodeFacts(node).card;
+  return card.before.concat(
+    [row('GPU Workload Pods', podsPend ? PODS_LOADING : podsOnNode.length > 0 ? podsOnNode.map(podName).join(', ') : '—')],
+    card.after
+  );
 }
 
 /**
@@ -229,7 +180,7 @@ export function nodesView(ctx, opts) {
   const power = nodePowerKeys(metrics);
   const temps = nodeTempKeys(metrics);
   const head = memo('nodes-head', [pg, ctx.index, ctx.error, power.sig, temps.sig, podsPend], function () {
-    return nodesHeadItems(ctx, now, power.byNode, pg, sort, podsPend, temps.byNode);
+    return nodesHeadItems(ctx, now, power, pg, sort, podsPend, temps);
   }, now);
   const owners = ownersByNode(metrics);
   const xgmi = metrics ? metrics.xgmi : undefined;
@@ -273,26 +224,22 @@ export function nodesView(ctx, opts) {
 // telemetry snapshot, derived when it arrives (api/nodeSummaries.js).
 export { nodePowerKeys, nodeTempKeys, ownersByNode };
 
-function nodeTempCell(key) {
-  if (!key) return '—';
-  const parts = key.split('|');
-  const text = parts[0] + ' °C';
-  if (parts[2] === 'error') return status('error', text + ' (throttling at ' + parts[1] + ' °C)');
-  return parts[2] === 'warning' ? status('warning', text) : text;
+/** The Hottest GPU cell from its snapshot facts (nodeSummaries.js nodeTempKeys): a status when warm or throttling. */
+function nodeTempCell(c) {
+  if (!c) return '—';
+  return c.level === 'ok' ? c.text : status(c.level, c.text);
 }
 
-function nodePowerCell(key) {
-  if (!key) return '—';
-  const parts = key.split('|');
-  const cap = Number(parts[1]);
-  return powerBar(Number(parts[0]), cap > 0 ? cap : null);
+/** The Power cell from its snapshot facts (nodeSummaries.js nodePowerKeys). */
+function nodePowerCell(b) {
+  return b ? bar(b.watts, b.cap, b.pct, b.color, b.text) : '—';
 }
 
-function nodesHeadItems(ctx, now, powerByNode, pg, sort, podsPend, tempByNode) {
-  const pw = powerByNode || {};
-  const withPower = Object.keys(pw).length > 0;
-  const tp = tempByNode || {};
-  const withTemp = Object.keys(tp).length > 0;
+function nodesHeadItems(ctx, now, power, pg, sort, podsPend, temps) {
+  const pw = power.byNode;
+  const withPower = power.sig !== '';
+  const tp = temps.byNode;
+  const withTemp = temps.sig !== '';
   const items = [];
   if (ctx.error) items.push(errorSection(ctx.error));
 
@@ -337,7 +284,7 @@ function nodesHeadItems(ctx, now, powerByNode, pg, sort, podsPend, tempByNode) {
                 count > 0 ? String(count) : '—',
                 podsPend ? PODS_LOADING : allocationBar(st ? st.inUse : 0, (st && st.allocatable) || count),
                 podsPend ? PODS_LOADING : String(st ? st.pods : 0),
-              ].concat(withPower ? [nodePowerCell(pk)] : [], withTemp ? [nodeTempCell(tk)] : [],
+              ].concat(withPower ? [nodePowerCell(power.bars[n.metadata.name])] : [], withTemp ? [nodeTempCell(temps.cells[n.metadata.name])] : [],
                 [ageText(n.metadata.creationTimestamp, now)]);
             }, now);
           }, now, function (n) { return [idx.nodeStats.get(n.metadata.name), withPower, pw[n.metadata.name], tp[n.metadata.name]]; }),

@@ -3,16 +3,11 @@
  * SURVEY C5).
  */
 
-import {
-  deviceConfigStatus,
-  deviceConfigStatusText,
-  formatSelector,
-  getNodeGpuModel,
-  operandEnabled,
-} from '../../api/amdNodes.js';
-import { formatComponent, formatPodGpuRequests, isPodReady, pluginPodComponent } from '../../api/amdPods.js';
+import { getNodeGpuModel } from '../../api/amdNodes.js';
+import { formatPodGpuRequests } from '../../api/amdPods.js';
 import { podFacts } from '../../api/clusterIndex.js';
-import { AMD_GPU_OPERATOR_NAMESPACE, BAR_COLORS, formatBytes, get, MI355X } from '../../api/k8sCore.js';
+import { AMD_GPU_OPERATOR_NAMESPACE, BAR_COLORS, formatBytes, MI355X } from '../../api/k8sCore.js';
+import { deviceConfigFacts, operatorPodFacts } from '../../api/operatorFacts.js';
 import { kv, loader, page, pctbar, row, section, status, table } from '../ir.js';
 import {
   ageText,
@@ -26,7 +21,6 @@ import {
   podName,
   podNode,
   podNs,
-  readyLabel,
   refreshButton,
   crdPending,
   nodesPending,
@@ -146,18 +140,24 @@ function overviewItems(ctx, now, podsPend, opPend) {
   return items;
 }
 
+const ENABLED = status('success', 'Enabled');
+const DISABLED = status('warning', 'Disabled');
+const READY = status('success', 'Ready');
+
 function overviewDeviceConfigs(dcs, now) {
   return section('Device Config Status', [
     table(
       ['Name', 'Namespace', 'Status', 'Metrics Exporter', 'Node Labeller', 'Selector', 'Age'],
       dcs.map(function (dc) {
+        // Derived when the store took the list (api/operatorFacts.js).
+        const f = deviceConfigFacts(dc);
         return [
           dc.metadata.name,
-          dc.metadata.namespace || '—',
-          status(deviceConfigStatus(dc), deviceConfigStatusText(dc)),
-          operandEnabled(dc, 'metricsExporter') ? status('success', 'Enabled') : status('warning', 'Disabled'),
-          operandEnabled(dc, 'nodeLabeller') ? status('success', 'Enabled') : status('warning', 'Disabled'),
-          formatSelector(get(dc, ['spec', 'selector'], null)),
+          f.namespace,
+          status(f.level, f.text),
+          f.metricsExporter.enabled ? ENABLED : DISABLED,
+          f.nodeLabeller.enabled ? ENABLED : DISABLED,
+          f.selector,
           ageText(dc.metadata.creationTimestamp, now),
         ];
       }),
@@ -176,12 +176,12 @@ export const OVERVIEW_PLUGIN_PODS = 10;
  * thousands of rows on a large cluster.
  */
 function overviewPluginPods(pods, now) {
-  const notReady = chunkedFilter('ov-plugin-not-ready', pods, function (p) { return !isPodReady(p); });
+  const notReady = chunkedFilter('ov-plugin-not-ready', pods, function (p) { return !operatorPodFacts(p).ready; });
   let shown = pods;
   if (pods.length > OVERVIEW_PLUGIN_PODS) {
     shown = notReady.slice(0, OVERVIEW_PLUGIN_PODS);
     for (let i = 0; i < pods.length && shown.length < OVERVIEW_PLUGIN_PODS; i++) {
-      if (isPodReady(pods[i])) shown.push(pods[i]);
+      if (operatorPodFacts(pods[i]).ready) shown.push(pods[i]);
     }
   }
   const blocks = [
@@ -189,7 +189,8 @@ function overviewPluginPods(pods, now) {
       ['Name', 'Namespace', 'Component', 'Node', 'Status', 'Age'],
       chunkedRows('ov-plugin-rows', shown, [], function (p) {
         return ovPluginRows(p, [], function () {
-          return [podName(p), podNs(p), formatComponent(pluginPodComponent(p)), podNode(p), readyLabel(p), ageText(p.metadata.creationTimestamp, now)];
+          const f = operatorPodFacts(p);
+          return [podName(p), podNs(p), f.component, f.node, f.ready ? READY : status('warning', f.phase), ageText(p.metadata.creationTimestamp, now)];
         }, now);
       }, now)
     ),

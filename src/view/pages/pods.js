@@ -12,7 +12,7 @@ import {
   podWaitingReason,
 } from '../../api/amdPods.js';
 import { podContainerLines, podFacts } from '../../api/clusterIndex.js';
-import { podGpuAssignments } from '../../api/nodeSummaries.js';
+import { assignmentTexts, podGpuAssignments, podPowerText } from '../../api/nodeSummaries.js';
 import { formatBytes, formatWatts } from '../../api/k8sCore.js';
 import { SMALL_CLUSTER_PODS } from '../../api/series.js';
 import { kv, lines, loader, page, pager, row, section, status, table } from '../ir.js';
@@ -53,7 +53,7 @@ function rankedPodPage(ctx, m, state) {
 
 // podGpuAssignments: "namespace/pod" → the GPUs the exporter attributes to
 // the pod, derived when a telemetry snapshot arrives (api/nodeSummaries.js).
-export { podGpuAssignments };
+export { podGpuAssignments, podPowerText };
 
 export function assignedLines(gs) {
   return lines(
@@ -66,20 +66,6 @@ export function assignedLines(gs) {
       return { label: g.nodeName + ' GPU ' + g.gpu, text: parts.length ? parts.join(', ') : 'no telemetry' };
     })
   );
-}
-
-function assignedText(gs) {
-  if (!gs || gs.length === 0) return '—';
-  const byNode = {};
-  const order = [];
-  for (let i = 0; i < gs.length; i++) {
-    if (!byNode[gs[i].nodeName]) {
-      byNode[gs[i].nodeName] = [];
-      order.push(gs[i].nodeName);
-    }
-    byNode[gs[i].nodeName].push(gs[i].gpu);
-  }
-  return order.map(function (n) { return n + ': GPU ' + byNode[n].join(', '); }).join('; ');
 }
 
 /**
@@ -188,7 +174,10 @@ function podsItems(ctx, now, assign, pg, sort) {
                 podName(p), podNs(p), podNode(p), status(phaseToStatus(phase), phase), gpuContainerLines(p),
                 restartsCell(p), ageText(p.metadata.creationTimestamp, now),
               ];
-              if (exact) r.splice(5, 0, assignedText(gs), podPowerText(gs));
+              if (exact) {
+                const t = assignmentTexts(gs);
+                r.splice(5, 0, t.assigned, t.power);
+              }
               return r;
             }, now);
           }, now),
@@ -253,7 +242,7 @@ export function podsPreview(metrics) {
       const nodes = [];
       for (let i = 0; i < gs.length; i++) if (nodes.indexOf(gs[i].nodeName) < 0) nodes.push(gs[i].nodeName);
       return [k.slice(slash + 1), k.slice(0, slash), nodes.join(', '), status('success', 'Running'),
-        gs.length + ' GPU' + (gs.length === 1 ? '' : 's') + ' held', assignedText(gs), podPowerText(gs), '—', '—'];
+        gs.length + ' GPU' + (gs.length === 1 ? '' : 's') + ' held', assignmentTexts(gs).assigned, assignmentTexts(gs).power, '—', '—'];
     });
     return [
       section('Summary (partial)', [kv(sum)]),
@@ -265,15 +254,3 @@ export function podsPreview(metrics) {
 }
 
 /** Live power of the GPUs a pod holds (exporter pod labels), summed; "—" without a reading. */
-export function podPowerText(gs) {
-  if (!gs || !gs.length) return '—';
-  let w = 0;
-  let any = false;
-  for (let i = 0; i < gs.length; i++) {
-    if (typeof gs[i].powerWatts === 'number' && isFinite(gs[i].powerWatts)) {
-      w += gs[i].powerWatts;
-      any = true;
-    }
-  }
-  return any ? formatWatts(w) : '—';
-}

@@ -8,10 +8,11 @@
 import { derivedCache, resetDerivedCaches } from '../../src/api/derivedCache.js';
 import { nodeFacts, podContainerLines } from '../../src/api/clusterIndex.js';
 import { nodePowerKeys, ownersByNode, podGpuAssignments, primeSnapshot } from '../../src/api/nodeSummaries.js';
+import { deviceConfigFacts, operatorPodFacts } from '../../src/api/operatorFacts.js';
 import { linkFacts } from '../../src/api/topology.js';
 import { clearViewMemo } from '../../src/view/pages/common.js';
 import { nodeReadyCell } from '../../src/view/pages/nodes.js';
-import { makeGpuNode, makeGpuPod } from './fixtures.js';
+import { makeDeviceConfig, makeGpuNode, makeGpuPod, makePluginPod } from './fixtures.js';
 
 function snapshot() {
   const gpus = [];
@@ -36,16 +37,11 @@ describe('derivedCache', () => {
     expect(hook).toBe(1);
   });
 
-  it('clearViewMemo drops first-use view facts: a ready cell, a pod\'s container lines', () => {
-    const node = makeGpuNode('n1');
+  it('clearViewMemo drops first-use view facts: a pod\'s container lines', () => {
     const pod = makeGpuPod('a', { gpus: 2 });
-    const cell = nodeReadyCell(node);
     const lines = podContainerLines(pod);
-    expect(nodeReadyCell(node)).toBe(cell);
     expect(podContainerLines(pod)).toBe(lines);
     clearViewMemo();
-    expect(nodeReadyCell(node)).not.toBe(cell);
-    expect(nodeReadyCell(node)).toEqual(cell);
     expect(podContainerLines(pod)).not.toBe(lines);
     expect(podContainerLines(pod)).toEqual(lines);
   });
@@ -53,6 +49,7 @@ describe('derivedCache', () => {
   it('facts derived on arrival stay: node facts, and a primed snapshot\'s summaries and link facts', () => {
     const node = makeGpuNode('n1');
     const f = nodeFacts(node);
+    const ready = nodeReadyCell(node);
     const m = primeSnapshot(snapshot());
     const power = nodePowerKeys(m);
     const owners = ownersByNode(m);
@@ -60,6 +57,8 @@ describe('derivedCache', () => {
     const links = linkFacts(8, m.xgmi.n1, null);
     clearViewMemo();
     expect(nodeFacts(node)).toBe(f);
+    expect(nodeReadyCell(node)).toBe(ready); // one cell per wording, from the node's facts
+    expect(f.card.after).toEqual([{ name: 'OS / Kernel / Kubelet', value: f.osText }]);
     expect(nodePowerKeys(m)).toBe(power);
     expect(ownersByNode(m)).toBe(owners);
     expect(podGpuAssignments(m)).toBe(assign);
@@ -68,5 +67,24 @@ describe('derivedCache', () => {
     expect(owners.n1.map((o) => o.gpu)).toEqual(['0', '1']);
     expect(assign['ml/train']).toHaveLength(2);
     expect(links).toEqual({ fullMesh: true, linksPerGpu: 7, stats: { links: 56, meanGBs: 10, maxGBs: 10 } });
+  });
+
+  it('the store derives the operator objects\' facts when it takes their lists', async () => {
+    const { createClusterStore } = await import('../../src/api/clusterStore.js');
+    const dc = makeDeviceConfig('gpu-operator');
+    const op = makePluginPod('dp-0');
+    const store = createClusterStore({ request: (path) => Promise.resolve({ kind: 'List', items: path.indexOf('deviceconfigs') >= 0 ? [dc] : [op] }) });
+    store.setNodes([], null);
+    store.setPods([op], null);
+    await store.refresh();
+    const ctx = store.getSnapshot();
+    expect(ctx.deviceConfigs).toEqual([dc]);
+    const f = deviceConfigFacts(ctx.deviceConfigs[0]);
+    const pf = operatorPodFacts(op);
+    clearViewMemo();
+    expect(deviceConfigFacts(ctx.deviceConfigs[0])).toBe(f);
+    expect(operatorPodFacts(op)).toBe(pf);
+    expect(f.metricsExporter).toEqual({ enabled: true, level: 'success', text: 'Enabled — port 5000 · 2/2 ready' });
+    expect(pf.ready).toBe(true);
   });
 });

@@ -161,8 +161,10 @@ describe('devicePluginsView', () => {
     const s = findSection(devicePluginsView(makeContext({ deviceConfigs: [dc] }), opts), 'DeviceConfig: gpu-operator');
     expect(rowValue(s, 'Test Runner')).toEqual({ t: 'status', status: 'warning', text: 'Enabled · 1/2 ready' });
     expect(rowValue(s, 'Config Manager')).toEqual({ t: 'status', status: 'warning', text: 'Disabled' });
-    delete dc.status.testRunner;
-    const uncounted = findSection(devicePluginsView(makeContext({ deviceConfigs: [dc] }), opts), 'DeviceConfig: gpu-operator');
+    // a new object (the store's objects are immutable snapshots; their facts are derived once)
+    const dc2 = JSON.parse(JSON.stringify(dc));
+    delete dc2.status.testRunner;
+    const uncounted = findSection(devicePluginsView(makeContext({ deviceConfigs: [dc2] }), opts), 'DeviceConfig: gpu-operator');
     expect(rowValue(uncounted, 'Test Runner')).toEqual({ t: 'status', status: 'success', text: 'Enabled' });
     const plain = findSection(devicePluginsView(makeContext({ deviceConfigs: [makeDeviceConfig('gpu-operator')] }), opts), 'DeviceConfig: gpu-operator');
     expect(rowValue(plain, 'Test Runner')).toBeUndefined();

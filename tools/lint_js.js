@@ -32,10 +32,22 @@ function walk(p, out) {
 function identifiers(src) {
   const used = {};
   (function scan(s) {
-    tokenize(s).forEach(function (t) {
-      if (t.t === 'ident') used[t.v] = (used[t.v] || 0) + 1;
-      else if (t.t === 'tmpl') t.parts.forEach(function (p, i) { if (i % 2) scan(p); });
-    });
+    // Significant tokens (no whitespace / comments), to look one back and one ahead.
+    const ts = tokenize(s).filter(function (t) { return t.t !== 'ws' && t.t !== 'comment'; });
+    for (let i = 0; i < ts.length; i++) {
+      const t = ts[i];
+      if (t.t === 'tmpl') {
+        t.parts.forEach(function (p, k) { if (k % 2) scan(p); });
+        continue;
+      }
+      if (t.t !== 'ident') continue;
+      const prev = ts[i - 1];
+      const next = ts[i + 1];
+      // `x.get(…)` and `{ get: … }` name a property, not an imported `get`.
+      if (prev && prev.v === '.') continue;
+      if (prev && (prev.v === '{' || prev.v === ',') && next && next.v === ':') continue;
+      used[t.v] = (used[t.v] || 0) + 1;
+    }
   })(src);
   return used;
 }
