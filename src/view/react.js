@@ -5,7 +5,7 @@
  * real React inside Headlamp and under the Node-12 test harness's stand-in
  * (tests/js/stubs/react.js). No JSX: the file needs no transpiler.
  *
- * One IR node → one component (src/view/ir.js; typed in ir.d.ts):
+ * IR nodes → React (src/view/ir.js; typed in ir.d.ts):
  *   page     → SectionHeader + refresh <button aria-label> + items
  *   loader   → Loader
  *   section  → SectionBox (memoised: unchanged section IR is not re-rendered)
@@ -13,16 +13,21 @@
  *   table    → SimpleTable (one getter per column reading row[i])
  *   pctbar   → PercentageBar
  *   status   → StatusLabel
- *   bar      → inline allocation / power bar (reference NodesPage.tsx:35-63,
- *              MetricsPage.tsx:50-89)
- *   slots    → per-GPU allocation strip (MI355X, new)
- *   matrix   → xGMI neighbour matrix (MI355X, new)
+ *   bar      → one element: the bar is its background, the text its content
+ *              (reference NodesPage.tsx:35-63, MetricsPage.tsx:50-89)
+ *   slots    → per-GPU allocation strip, one element (MI355X, new)
+ *   matrix   → xGMI neighbour matrix: a summary line with the grid one click
+ *              away when built closed (MI355X, new)
  *   series   → inline SVG sparklines of per-node power / HBM (new)
- *   pager    → name filter + "Showing 1–16 of N" + previous / next (page item)
+ *   pager    → name filter + "Showing 1–16 of N" + previous / next (page
+ *              item); a count line and one button while it has nothing to do
+ * Cells and blocks are built inline (valueNode / blockNode), not as a
+ * component each; the matrix and the pager, which keep state, are components.
  *
- * Only CommonComponents plus inline-styled elements are used, like the
- * reference (reference CLAUDE.md conventions; src/components/NodesPage.tsx:35-63
- * for the inline bar idiom).
+ * Only CommonComponents and plain elements are used, like the reference
+ * (reference CLAUDE.md conventions). The plain elements take their styles
+ * from one stylesheet (PLUGIN_CSS, added once per document) rather than an
+ * inline style object each, except a bar's or strip's background.
  */
 
 import { BAR_COLORS, formatWatts } from '../api/k8sCore.js';
