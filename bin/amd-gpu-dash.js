@@ -13,6 +13,7 @@
  *   node bin/amd-gpu-dash.js --page all --watch 10 --color
  *   node bin/amd-gpu-dash.js --prometheus monitoring/my-prom:9090 --page metrics
  *   node bin/amd-gpu-dash.js --json --page pods          # the view-model IR
+ *   node bin/amd-gpu-dash.js --svg --page nodes > nodes.svg   # a picture of the page
  *
  * Plain ES2019 modules: runs on the Node 12 of the development image.
  */
@@ -35,6 +36,7 @@ import {
   RANKED_POD_SORTS,
 } from '../src/view/pages/paging.js';
 import { podsView } from '../src/view/pages/pods.js';
+import { renderPageSvg, renderSectionSvg } from '../src/view/svg.js';
 import { renderText, textSection } from '../src/view/text.js';
 import { PAGE_NEEDS } from '../src/plugin.js';
 
@@ -47,14 +49,14 @@ function usage(msg) {
       '                    [--watch SECONDS] [--filter TEXT] [--page-number N] [--per-page N]\n' +
       '                    [--sort name|in-use|free|attention (nodes) | gpus|newest|attention (pods) | power (nodes, metrics, pods)]\n' +
       '                    [--prometheus NAMESPACE/SERVICE:PORT] [--timeout MS] [--token TOKEN] [--insecure]\n' +
-      '                    [--color] [--json]\n'
+      '                    [--color] [--json | --svg]\n'
   );
   process.exit(2);
 }
 
 export function parseArgs(argv) {
   const a = { url: 'http://127.0.0.1:8001', page: 'overview', watch: 0, prometheus: null, timeout: 2000,
-    token: null, insecure: false, color: false, json: false, pager: { page: 0, filter: '' } };
+    token: null, insecure: false, color: false, json: false, svg: false, pager: { page: 0, filter: '' } };
   for (let i = 0; i < argv.length; i++) {
     const k = argv[i];
     const v = argv[i + 1];
@@ -82,6 +84,10 @@ export function parseArgs(argv) {
     } else if (k === '--json') {
       a.json = true;
       continue;
+    } else if (k === '--svg') {
+      // One page or detail section as an SVG picture (src/view/svg.js), once.
+      a.svg = true;
+      continue;
     } else if (k === '--help' || k === '-h') return { error: '' };
     else return { error: 'unknown argument ' + k };
     if (v === undefined) return { error: 'missing value for ' + k };
@@ -94,6 +100,7 @@ export function parseArgs(argv) {
   else if (pod) a.detail = { kind: 'pod', namespace: pod[1], name: pod[2] };
   else if (a.page !== 'all' && PAGES.indexOf(a.page) < 0) return { error: 'unknown page ' + a.page };
   if (!(a.watch >= 0) || !(a.timeout > 0)) return { error: 'bad --watch / --timeout' };
+  if (a.svg && (a.json || a.watch > 0 || a.page === 'all')) return { error: '--svg draws one page once (no --json, --watch or --page all)' };
   if (!(a.pager.page >= 0) || (a.pager.perPage !== undefined && !(a.pager.perPage > 0))) return { error: 'bad --page-number / --per-page' };
   // Node orders apply to the GPU node pages, pod orders to GPU Pods ('name' to both).
   const sorts = NODE_SORTS.concat(POD_SORTS, RANKED_NODE_SORTS, RANKED_POD_SORTS).map(function (o) { return o.value; })
@@ -196,6 +203,10 @@ async function main() {
       process.stdout.write(JSON.stringify(section) + '\n');
       return;
     }
+    if (a.svg) {
+      process.stdout.write(renderSectionSvg(section || { t: 'section', title: 'No AMD GPU section for ' + what, key: 'none', blocks: [] }));
+      return;
+    }
     if (a.watch > 0) process.stdout.write('\u001b[2J\u001b[H');
     process.stdout.write(section ? textSection(section, a.color).join('\n') + '\n' : 'No AMD GPU section for ' + what + '\n');
   }
@@ -242,6 +253,10 @@ async function main() {
     const vms = views(store.getSnapshot(), mstate, a.page, a.pager);
     if (a.json) {
       process.stdout.write(JSON.stringify(vms.length === 1 ? vms[0] : vms) + '\n');
+      return;
+    }
+    if (a.svg) {
+      process.stdout.write(renderPageSvg(vms[0]));
       return;
     }
     if (a.watch > 0) process.stdout.write('\u001b[2J\u001b[H');

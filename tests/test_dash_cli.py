@@ -129,3 +129,19 @@ def test_sort_power_lets_prometheus_rank_the_page(url):
         assert pager["total"] > 0, (page, pager)
     text = run("--url", url, "--page", "pods", "--sort", "power")
     assert text.returncode == 0 and "sorted: Highest GPU power" in text.stdout, text.stdout[-800:]
+
+
+def test_svg_draws_a_page_or_a_detail_section(url):
+    """--svg: the page's view-model as the SVG picture docs/screenshots holds (src/view/svg.js), once."""
+    import xml.etree.ElementTree as ET
+
+    r = run("--url", url, "--page", "nodes", "--svg")
+    assert r.returncode == 0, r.stderr
+    root = ET.fromstring(r.stdout)
+    texts = [t.text for t in root.iter("{http://www.w3.org/2000/svg}text")]
+    assert texts[0] == "AMD GPU — Nodes" and "GPU Node Summary" in texts and "mi355x-001" in texts
+    d = run("--url", url, "--page", "node:mi355x-000", "--svg")
+    assert d.returncode == 0, d.stderr
+    assert "AMD GPU" in [t.text for t in ET.fromstring(d.stdout).iter("{http://www.w3.org/2000/svg}text")]
+    for bad in (["--svg", "--json"], ["--svg", "--page", "all"], ["--svg", "--watch", "5"]):
+        assert run("--url", url, *bad).returncode == 2
