@@ -149,6 +149,8 @@ export async function compareRenders(url, c) {
     out.pages[page] = {
       reference: summary(samples.reference),
       amd: Object.assign(summary(samples.amd), { reactOnlyMs: spread(prebuilt.mount).p50, vmBuildMs: spread(prebuilt.vm).p50 }),
+      // The samples themselves, so runs in several processes can be pooled (tools/render_compare.py --runs).
+      samples: { reference: samples.reference, amd: samples.amd, prebuilt: prebuilt },
     };
   }
   return out;

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """The reference's own pages vs this plugin's, rendered on real React 18.3.1 at 1 to 1,000 GPU nodes.
 
-    python tools/render_compare.py --allow-reference-exec [--sizes 1,2,4,8] [--reps 101] [--warm 50]
+    python tools/render_compare.py --allow-reference-exec [--sizes 1,2,4,8] [--reps 101] [--warm 50] [--runs 3]
                                    [--out profiles/r5_render_compare]
 
 OPT-IN: this runs the reference's page components, which are untrusted public content (ADR 014). Without
@@ -11,7 +11,9 @@ compiled into bench/tsx.js's sandbox: a vm context of their own, with no ``proce
 timers, file system or network, and no code generation from strings there or through any host function.
 
 Per page and size: ``--warm`` untimed mounts of each side, then ``--reps`` (at least 15) interleaved
-reference / new pairs, the order alternating; mount and re-render p50 with the interquartile range.
+reference / new pairs, the order alternating; mount and re-render p50 with the interquartile range. ``--runs``
+driver processes measure each size, and their samples are pooled: a process's JIT and heap state moves every figure
+it takes, so one process is one draw of that state.
 
 Per size: the fake control plane (no injected latency: this measures render, not requests) serves a synthetic
 cluster; bench/driver.js ``refRender`` mounts each of the five reference pages — read unmodified from
@@ -58,6 +60,36 @@ def measure(n: int, reference: str, reps: int, warm: int) -> dict:
     return r["render"]
 
 
+def quantile(xs, p):
+    v = sorted(xs)
+    idx = (len(v) - 1) * p
+    lo, hi = int(idx), min(int(idx) + 1, len(v) - 1)
+    return v[lo] + (v[hi] - v[lo]) * (idx - lo)
+
+
+def pooled(runs: list) -> dict:
+    """One size's result from several driver processes: each page's samples pooled, p50 / IQR recomputed."""
+    out = {k: v for k, v in runs[0].items() if k != "pages"}
+    out["runs"] = len(runs)
+    out["pages"] = {}
+    for page in runs[0]["pages"]:
+        per = [r["pages"][page] for r in runs]
+        res = {}
+        for side in ("reference", "amd"):
+            mount = [x for p in per for x in p["samples"][side]["mount"]]
+            rer = [x for p in per for x in p["samples"][side]["rerender"]]
+            res[side] = {"elements": per[0][side]["elements"], "reps": len(mount),
+                         "mountMs": quantile(mount, 0.5), "mountQ1": quantile(mount, 0.25), "mountQ3": quantile(mount, 0.75),
+                         "rerenderMs": quantile(rer, 0.5), "rerenderQ1": quantile(rer, 0.25), "rerenderQ3": quantile(rer, 0.75)}
+        res["amd"]["reactOnlyMs"] = quantile([x for p in per for x in p["samples"]["prebuilt"]["mount"]], 0.5)
+        res["amd"]["vmBuildMs"] = quantile([x for p in per for x in p["samples"]["prebuilt"]["vm"]], 0.5)
+        # each process's own p50s, to show the spread between processes
+        res["amd"]["runMountMs"] = [p["amd"]["mountMs"] for p in per]
+        res["reference"]["runMountMs"] = [p["reference"]["mountMs"] for p in per]
+        out["pages"][page] = res
+    return out
+
+
 def verdict(a: dict, ref: dict) -> str:
     """'≤' when the new mount p50 is at most the reference's, '≈' within its interquartile range, else '>'."""
     if a["mountMs"] <= ref["mountMs"]:
@@ -87,6 +119,7 @@ def main() -> int:
     p.add_argument("--sizes", default="1,2,4,8")
     p.add_argument("--reps", type=int, default=101)
     p.add_argument("--warm", type=int, default=50)
+    p.add_argument("--runs", type=int, default=3, help="driver processes per size, their samples pooled")
     p.add_argument("--reference", default="/root/reference")
     p.add_argument("--out", default=os.path.join(ROOT, "profiles", "r5_render_compare"))
     p.add_argument("--allow-reference-exec", action="store_true",
@@ -101,7 +134,7 @@ def main() -> int:
     for s in args.sizes.split(","):
         n = int(s)
         t = time.time()
-        r = measure(n, args.reference, args.reps, args.warm)
+        r = pooled([measure(n, args.reference, args.reps, args.warm) for _ in range(max(1, args.runs))])
         rows.append((n, r))
         print(f"[render_compare] {n} nodes: {time.time() - t:.1f} s", file=sys.stderr, flush=True)
         with open(args.out + ".json", "w") as f:
@@ -109,7 +142,8 @@ def main() -> int:
                       indent=1)
     md = ["Each page mounted on react@18.3.1 + react-dom@18.3.1 production UMD builds into a minimal JS DOM: "
           f"{args.warm} untimed warm mounts of each side, then {max(15, args.reps)} interleaved reference / new pairs "
-          "(order alternating); p50 with the interquartile range. ≤: new p50 at most the reference's; ≈: within its "
+          f"(order alternating), in each of {max(1, args.runs)} driver processes, samples pooled; p50 with the "
+          "interquartile range. ≤: new p50 at most the reference's; ≈: within its "
           "IQR; >: above it. Reference = its page component (read from its sources, transpiled at run time) with "
           "its data in context, its per-render aggregation included; re-render = a watch event (a new context "
           "value). New = this plugin's page, mount including the view-model built from a cold memo; re-render = "
