@@ -152,3 +152,13 @@ describe('tsx: the module sandbox', () => {
     expect(err).not.toBeNull();
   });
 });
+
+describe('the render comparison refuses to run the reference unless asked, in a sandboxed process', () => {
+  it('assertReferenceSandbox: the opt-in, then the process flag', async () => {
+    const { assertReferenceSandbox } = await import('../../bench/compareRenders.js');
+    expect(() => assertReferenceSandbox({})).toThrow('--allow-reference-exec');
+    expect(() => assertReferenceSandbox({ allowReferenceExec: 'yes' })).toThrow('--allow-reference-exec');
+    // The spec runner is not started with --disallow-code-generation-from-strings.
+    expect(() => assertReferenceSandbox({ allowReferenceExec: true })).toThrow('--disallow-code-generation-from-strings');
+  });
+});
