@@ -88,3 +88,27 @@ describe('derivedCache', () => {
     expect(pf.ready).toBe(true);
   });
 });
+
+describe('arrival facts change no output', () => {
+  it('a page built from a primed snapshot equals one built from fresh, unprimed copies of the same data', async () => {
+    const { nodesView } = await import('../../src/view/pages/nodes.js');
+    const { podsView } = await import('../../src/view/pages/pods.js');
+    const { makeContext } = await import('./fixtures.js');
+    const nodes = [makeGpuNode('n1'), makeGpuNode('n2')];
+    const pods = [makeGpuPod('train', { node: 'n1', gpus: 2 }), makeGpuPod('eval', { node: 'n2', gpus: 1 })];
+    const now = Date.parse('2026-10-16T00:00:00Z');
+    function metrics() {
+      const m = snapshot();
+      m.gpus.forEach((g, i) => { if (i < 2) g.pod = 'train'; });
+      return m;
+    }
+    const primed = primeSnapshot(metrics());
+    const a = [nodesView(makeContext({ nodes, pods }), { metrics: primed, now }), podsView(makeContext({ nodes, pods }), { metrics: primed, now })];
+    clearViewMemo();
+    const copy = (x) => JSON.parse(JSON.stringify(x));
+    const fresh = metrics(); // never primed: every summary derived on first read
+    const b = [nodesView(makeContext({ nodes: copy(nodes), pods: copy(pods) }), { metrics: fresh, now }),
+      podsView(makeContext({ nodes: copy(nodes), pods: copy(pods) }), { metrics: fresh, now })];
+    expect(JSON.stringify(b)).toBe(JSON.stringify(a));
+  });
+});
