@@ -94,7 +94,7 @@ export const PAGES = ['overview', 'devicePlugins', 'nodes', 'pods', 'metrics'];
 
 /** Build ONE page's view-model (the one whose Refresh was clicked), first page of the pager. */
 export function pageVm(page, ctx, mstate, pageMetrics) {
-  if (page === 'overview') return overviewView(ctx);
+  if (page === 'overview') return overviewView(ctx, { metrics: pageMetrics });
   if (page === 'devicePlugins') return devicePluginsView(ctx, { pager: PAGER });
   if (page === 'nodes') return nodesView(ctx, { metrics: pageMetrics, pager: PAGER });
   if (page === 'pods') return podsView(ctx, { metrics: pageMetrics, pager: PAGER });

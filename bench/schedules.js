@@ -11,6 +11,7 @@ import { createClusterStore } from '../src/api/clusterStore.js';
 import { createMetricsSource } from '../src/api/metrics.js';
 import { telemetryScope } from '../src/view/pages/nodes.js';
 import { ownersScope } from '../src/view/pages/pods.js';
+import { overviewOwnersScope } from '../src/view/pages/overview.js';
 import { renderPage } from '../src/view/html.js';
 import { PAGE_NEEDS } from '../src/plugin.js';
 import { createReferenceSchedule } from './referenceSchedule.js';
@@ -62,7 +63,7 @@ export function amdSchedule(request, clock, timeoutMs) {
   // cluster totals + per-GPU gauges + series of the nodes on its first page
   // ('gauges', scoped). Cold open / route switch / the all-pages composite
   // fetch every live series in one query ('all').
-  const pageMetrics = { nodes: null, pods: null };
+  const pageMetrics = { nodes: null, pods: null, overview: null };
   const metricsPage = { metrics: null, fetchError: null, fetching: false, series: null };
   function fetchMetrics(view) {
     return Promise.all([metrics.fetchGpuMetrics(view), metrics.fetchSeries(1800, 30)]).then(function (r) {
@@ -120,7 +121,24 @@ export function amdSchedule(request, clock, timeoutMs) {
     });
   }
   function pageMetricsOf(page) {
+    if (page === 'overview') return pageMetrics.overview;
     return page in pageMetrics && pageMetrics[page] ? pageMetrics[page] : mstate.metrics;
+  }
+  /**
+   * Overview's owner hook (plugin.js OverviewPage): once the node list says the
+   * cluster is larger than one page and while its pod list is still loading
+   * (overview.js overviewOwnersScope), the exporter's owners with a preview.
+   */
+  function overviewOpen(onData) {
+    pageMetrics.overview = null;
+    return listed('nodesState').then(function () {
+      const o = overviewOwnersScope(store.getSnapshot());
+      if (!o.enabled) return undefined;
+      return metrics.fetchGpuOwners({ pods: o.pods, small: o.small, preview: o.preview }).then(function (m) {
+        pageMetrics.overview = m;
+        if (onData) onData();
+      });
+    });
   }
   function fetchPodsPage() {
     const o = ownersScope(store.getSnapshot(), PAGER);
@@ -213,10 +231,13 @@ export function amdSchedule(request, clock, timeoutMs) {
       // The page's metrics hook runs from the first render (pages.js
       // telemetryScope) and once more if the node list changes its key.
       const telemetry = page === 'nodes' || page === 'metrics' || page === 'pods' ? pageOpen(page, check) : Promise.resolve();
+      // Overview's stand-in for its pod sections while a large cluster's pod
+      // list loads: shown as it comes, not part of what the page draws when complete.
+      const interim = page === 'overview' ? overviewOpen(check) : Promise.resolve();
       const content = Promise.all([lists, crd]).then(function () { if (mk.content) mk.content(); });
       // Everything the page draws: what its route mounts, and its telemetry.
       const complete = Promise.all([lists, crd, telemetry]).then(function () { if (mk.complete) mk.complete(); });
-      return Promise.all([lists, crd, telemetry, content, complete]).then(function () { off(); });
+      return Promise.all([lists, crd, telemetry, interim, content, complete]).then(function () { off(); });
     },
     pageMetrics: pageMetricsOf,
     /** The Metrics page's own state (its hook), for rendering that page. */

@@ -27,7 +27,7 @@ import { nodeColumns, nodeDetailView, podDetailView } from './view/pages/details
 import { devicePluginsView } from './view/pages/devicePlugins.js';
 import { metricsView } from './view/pages/metricsPage.js';
 import { nodesView, telemetryScope } from './view/pages/nodes.js';
-import { overviewView } from './view/pages/overview.js';
+import { overviewOwnersScope, overviewView } from './view/pages/overview.js';
 import { nodeSortOf, RANKED_NODE_SORTS } from './view/pages/paging.js';
 import { ownersScope, podsView } from './view/pages/pods.js';
 import { createRenderer } from './view/react.js';
@@ -75,10 +75,17 @@ export function createPlugin(env) {
   // Pages (reference src/components/*Page.tsx, SURVEY.md C5–C9)
   // -------------------------------------------------------------------------
 
-  /** Cluster-level MI355X dashboard (reference OverviewPage.tsx, C5). */
+  /**
+   * Cluster-level MI355X dashboard (reference OverviewPage.tsx, C5). On a
+   * cluster of more than one page of GPU nodes, the exporter's owner answer
+   * stands in for the pod-derived sections while the pod list loads
+   * (overviewOwnersScope); no Prometheus request otherwise.
+   */
   function OverviewPage() {
     const ctx = core.useAmdGpuContext();
-    return h(Page, { vm: overviewView(ctx), onRefresh: ctx.refresh });
+    const o = overviewOwnersScope(ctx);
+    const m = core.useGpuOwners(o.enabled, o.pods, o.small, undefined, o.preview);
+    return h(Page, { vm: overviewView(ctx, { metrics: o.enabled ? m.metrics : null }), onRefresh: ctx.refresh });
   }
 
   /** AMD GPU Operator DeviceConfigs and operand pods (reference DevicePluginsPage.tsx, C6). */

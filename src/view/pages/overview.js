@@ -7,7 +7,9 @@ import { getNodeGpuModel } from '../../api/amdNodes.js';
 import { formatPodGpuRequests } from '../../api/amdPods.js';
 import { podFacts } from '../../api/clusterIndex.js';
 import { AMD_GPU_OPERATOR_NAMESPACE, BAR_COLORS, formatBytes, MI355X } from '../../api/k8sCore.js';
+import { assignmentTexts, podGpuAssignments } from '../../api/nodeSummaries.js';
 import { deviceConfigFacts, operatorPodFacts } from '../../api/operatorFacts.js';
+import { SMALL_CLUSTER_NODES } from '../../api/series.js';
 import { kv, loader, page, pctbar, row, section, status, table } from '../ir.js';
 import {
   ageText,
@@ -47,17 +49,22 @@ export const OPERATOR_DOCS = 'https://instinct.docs.amd.com/projects/gpu-operato
  * shows a full-page Loader until every list is in (OverviewPage.tsx:67-69,
  * IntelGpuDataContext.tsx:214). Aggregates come from the store's memoised
  * index. In-use counts GPUs held by bound, non-terminated pods (the
- * scheduler's view), and Free is clamped at 0.
+ * scheduler's view), and Free is clamped at 0. On a cluster of more than one
+ * page of GPU nodes, `opts.metrics` (the exporter's owner answer,
+ * overviewOwnersScope) shows the pods drawing the most power while the pod
+ * list is still on its way (ADR 013).
  */
 export function overviewView(ctx, opts) {
   const now = nowOf(opts);
   if (nodesPending(ctx) || crdPending(ctx)) return page(null, null, [loader('Loading ' + BRAND + ' data...')]);
   const podsPend = podsPending(ctx);
   const opPend = pluginPodsPending(ctx);
+  const owners = podsPend && opts && opts.metrics && Array.isArray(opts.metrics.gpus) ? opts.metrics : null;
   const items = memo(
     'overview',
-    [ctx.deviceConfigs, ctx.pluginPods, ctx.pluginInstalled, ctx.crdAvailable, ctx.gpuNodes, ctx.gpuPods, ctx.index, ctx.error, podsPend, opPend],
-    function () { return overviewItems(ctx, now, podsPend, opPend); },
+    [ctx.deviceConfigs, ctx.pluginPods, ctx.pluginInstalled, ctx.crdAvailable, ctx.gpuNodes, ctx.gpuPods, ctx.index, ctx.error, podsPend, opPend,
+      owners && owners.gpus],
+    function () { return overviewItems(ctx, now, podsPend, opPend, owners); },
     now
   );
   return page(BRAND + ' — Overview', refreshButton('Refresh AMD GPU data', ctx.refreshing), items);
@@ -81,7 +88,51 @@ export function partitionModeDistribution(gpuNodes) {
   return order.map(function (k, i) { return { name: k, value: counts[k], fill: MODE_COLORS[i % MODE_COLORS.length] }; });
 }
 
-function overviewItems(ctx, now, podsPend, opPend) {
+/**
+ * Overview's exporter query (plugin.js OverviewPage): only while a cluster
+ * of more than one page of GPU nodes has its node list and not yet its pod
+ * list. The owner answer shows the pods drawing the most power until the list
+ * is in (overviewPodsPreview). A smaller cluster's pod list comes in the first
+ * wave with its nodes: the page sends no Prometheus request there.
+ * @returns {{enabled: boolean, pods?: string[], small?: boolean, preview?: number}}
+ */
+export function overviewOwnersScope(ctx) {
+  if (!ctx || ctx.nodesState !== 'ready' || !podsPending(ctx) || !ctx.gpuNodes || ctx.gpuNodes.length <= SMALL_CLUSTER_NODES) {
+    return { enabled: false };
+  }
+  return { enabled: true, pods: [], small: true, preview: ACTIVE_PODS_LIMIT };
+}
+
+/**
+ * The pods holding GPUs as the exporter's owner answer names them, while
+ * the pod list loads: the ACTIVE_PODS_LIMIT drawing the most power on a
+ * cluster with more owners than that (the answer's preview ranking), else
+ * every owner in namespace / name order. Null without owners.
+ */
+export function overviewPodsPreview(metrics) {
+  if (!metrics || !Array.isArray(metrics.gpus)) return null;
+  const assign = podGpuAssignments(metrics);
+  const pv = metrics.preview;
+  return memo('overview-preview', [assign, pv], function () {
+    const keys = (pv && Array.isArray(pv.order) ? pv.order.filter(function (k) { return assign[k]; })
+      : Object.keys(assign).sort()).slice(0, ACTIVE_PODS_LIMIT);
+    if (!keys.length) return null;
+    const count = pv ? pv.count : Object.keys(assign).length;
+    return section(pv ? 'GPU Pods Drawing the Most Power (partial)' : 'GPU Pods (partial)', [
+      kv([
+        row('Status', status('warning', 'Partial — the pod list is loading; these rows come from the GPU exporter')),
+        row('Pods Holding GPUs', String(count)),
+      ]),
+      table(['Name', 'Namespace', 'Assigned GPUs', 'GPU Power'], keys.map(function (k) {
+        const slash = k.indexOf('/');
+        const t = assignmentTexts(assign[k]);
+        return [k.slice(slash + 1), k.slice(0, slash) || '—', t.assigned, t.power];
+      }), keys),
+    ]);
+  });
+}
+
+function overviewItems(ctx, now, podsPend, opPend, owners) {
   const items = [];
   const t = ctx.index.totals;
 
@@ -129,6 +180,8 @@ function overviewItems(ctx, now, podsPend, opPend) {
   if (podsPend) {
     // Capacity is known from the nodes; what is in use needs the pods.
     if (t.capacity > 0) items.push(memo('overview-alloc-nodes', [t], function () { return overviewCapacity(t); }));
+    const preview = owners ? overviewPodsPreview(owners) : null;
+    if (preview) items.push(preview);
     items.push(loader('Loading GPU pods...'));
     return items;
   }

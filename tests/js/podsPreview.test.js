@@ -113,3 +113,37 @@ describe('podsPreview / podsView with the pod list pending', () => {
     expect(sectionTitles(podsView(ready, { metrics: m }))).toEqual(['No GPU Pods Found']);
   });
 });
+
+describe('Overview before the pod list (overview.js overviewOwnersScope / overviewPodsPreview)', () => {
+  const nodesOf = (n) => Array.from({ length: n }, (_, i) => ({ metadata: { name: 'n' + i } }));
+  const base = { nodesState: 'ready', podsState: 'pending', podsLoading: true, nodesLoading: false };
+
+  it('asks the exporter only on a cluster of more than one page of GPU nodes, and only while its pod list loads', async () => {
+    const { overviewOwnersScope, ACTIVE_PODS_LIMIT } = await import('../../src/view/pages/overview.js');
+    const { SMALL_CLUSTER_NODES: per } = await import('../../src/api/series.js');
+    expect(overviewOwnersScope(Object.assign({}, base, { gpuNodes: nodesOf(per) })).enabled).toBe(false);
+    expect(overviewOwnersScope(Object.assign({}, base, { gpuNodes: nodesOf(per + 1) })))
+      .toEqual({ enabled: true, pods: [], small: true, preview: ACTIVE_PODS_LIMIT });
+    expect(overviewOwnersScope(Object.assign({}, base, { gpuNodes: nodesOf(per + 1), podsState: 'ready', podsLoading: false })).enabled).toBe(false);
+    expect(overviewOwnersScope(Object.assign({}, base, { gpuNodes: [], nodesState: 'pending' })).enabled).toBe(false);
+    expect(overviewOwnersScope(null).enabled).toBe(false);
+  });
+
+  it('the ranked owners, at most ACTIVE_PODS_LIMIT, with their GPUs and power; nothing without owners', async () => {
+    const { overviewPodsPreview, ACTIVE_PODS_LIMIT } = await import('../../src/view/pages/overview.js');
+    const gpus = [];
+    const order = [];
+    for (let i = 0; i < 12; i++) {
+      gpus.push({ namespace: 'ml', pod: 'p' + i, nodeName: 'n' + i, gpu: '0', powerWatts: 100 + i });
+      order.push('ml/p' + (11 - i));
+    }
+    const s = overviewPodsPreview({ gpus: gpus, preview: { per: ACTIVE_PODS_LIMIT, count: 300, order: order, watts: {} } });
+    expect(s.title).toBe('GPU Pods Drawing the Most Power (partial)');
+    const t = s.blocks[1];
+    expect(t.rows).toHaveLength(ACTIVE_PODS_LIMIT);
+    expect(t.rows[0]).toEqual(['p11', 'ml', 'n11: GPU 0', '111.0 W']);
+    expect(s.blocks[0].rows[1]).toEqual({ name: 'Pods Holding GPUs', value: '300' });
+    expect(overviewPodsPreview({ gpus: [{ namespace: '', pod: null, nodeName: 'n0', gpu: '0' }] })).toBeNull();
+    expect(overviewPodsPreview(null)).toBeNull();
+  });
+});

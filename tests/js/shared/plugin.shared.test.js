@@ -263,6 +263,30 @@ describe('shared: progressive cold open — a page waits only for the lists it d
     r.unmount();
   });
 
+  it('Overview on a cluster of more than one page: the exporter\'s GPU owners stand in for the pod sections while the list loads', async () => {
+    const fake = cluster({ gpuNodes: Array.from({ length: 9 }, (_, i) => 'mi355x-' + String(i).padStart(3, '0')), podsLoading: true });
+    const r = render(h(route('/amd-gpu')));
+    await r.settle();
+    expect(r.text()).toContain('Partial — the pod list is loading');
+    expect(r.text()).toContain('train-0');
+    expect(r.text()).toContain('Loading GPU pods...');
+    lib.lists.Pod = [fake.pods, null];
+    r.rerender(h(route('/amd-gpu')));
+    await r.settle();
+    expect(r.text()).not.toContain('Partial');
+    expect(r.text()).toContain('Active GPU Pods');
+    r.unmount();
+  });
+
+  it('Overview on a one-page cluster sends no Prometheus request, its pod list pending or not', async () => {
+    cluster({ podsLoading: true });
+    const r = render(h(route('/amd-gpu')));
+    await r.settle();
+    expect(lib.api.calls.filter((c) => c.indexOf('/proxy/') >= 0)).toEqual([]);
+    expect(r.text()).not.toContain('Partial');
+    r.unmount();
+  });
+
   it('GPU Pods without telemetry waits for the pod list (the list is its content)', async () => {
     // A Prometheus this session has not met (no earlier answer to serve stale).
     saveSettings(Object.assign({}, DEFAULT_SETTINGS, { requestTimeoutMs: DEFAULT_SETTINGS.requestTimeoutMs + 2 }));
