@@ -131,7 +131,7 @@ export function createClusterStore(opts) {
   let feedsAttached = false;
   let opFeeds = 0; // operator pod feeds mounted right now
   // Objects a scoped list + watch delivered OUTSIDE the selection it asked
-  // for (providerCore.js NodePodsWatch / OperatorPodFeed): a host whose
+  // for (nodePodHooks.js NodePodsWatch, providerCore.js OperatorPodFeed): a host whose
   // useList() drops the list options. Once seen, those views read their
   // scoped requests instead (ADR 012).
   const ignored = { nodePods: 0, operatorPods: 0 };

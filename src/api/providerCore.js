@@ -24,11 +24,12 @@
  *     (reference quirk Q7: every route mounted a cold provider).
  */
 
-import { createClusterStore, fetchNodePods, getSharedStore, nodePodsSelector, storeIsLive } from './clusterStore.js';
-import { dedupePods, filterAmdGpuPluginPods, filterGpuRequestingPods } from './amdPods.js';
-import { get, OPERATOR_POD_LISTS, unwrapAll } from './k8sCore.js';
+import { createClusterStore, getSharedStore } from './clusterStore.js';
+import { dedupePods, filterAmdGpuPluginPods } from './amdPods.js';
+import { OPERATOR_POD_LISTS, unwrapAll } from './k8sCore.js';
 import { createMetricsSource } from './metrics.js';
 import { countOutside } from './selectors.js';
+import { createNodePodHooks } from './nodePodHooks.js';
 import { clusterKey as defaultClusterKey } from './cluster.js';
 import { POLL_MISS, createPoller, loadSettings as defaultLoadSettings, prometheusCandidates, seriesStepSec } from './settings.js';
 
@@ -497,137 +498,6 @@ export function createProviderCore(React, lib, deps) {
     }, true);
   }
 
-  /**
-   * True while a mounted pod feed keeps the cluster's shared store current
-   * (clusterStore.js storeIsLive: a plugin page that draws pods is mounted
-   * next to the caller). A Node detail section then reads the store;
-   * otherwise it reads its own node's pods (useNodePods) and never mounts a
-   * cluster-wide watch. Re-renders the caller when that flips (the page
-   * unmounts, or its list arrives).
-   */
-  function usePodsLive() {
-    const store = storeFor(clusterKey());
-    return React.useSyncExternalStore(store.subscribe, function () { return storeIsLive(store); });
-  }
-
-  /** Raw pods of `items` (list-hook items or raw objects) bound to `nodeName`. */
-  function onNode(items, nodeName) {
-    return unwrapAll(items).filter(function (p) { return get(p, ['spec', 'nodeName'], null) === nodeName; });
-  }
-
-  /**
-   * One node's pods by the host's list + watch hook SCOPED to the node
-   * (`fieldSelector spec.nodeName=<node>`, all namespaces), delivered to
-   * `props.onList(node, pods | null, error | null)`. The pods are filtered by
-   * node here too; objects of other nodes mean the host ignored the field
-   * selector (store.noteSelectorIgnored), and useNodePods swaps this feed for
-   * NodePodsPoll.
-   */
-  function NodePodsWatch(props) {
-    const node = props.node;
-    const opts = useMemo(function () { return { namespace: '', fieldSelector: nodePodsSelector(node) }; }, [node]);
-    const res = useListOf(lib.K8s.ResourceClasses.Pod, opts);
-    const items = res[0];
-    const err = res[1];
-    const got = useMemo(function () {
-      if (!items) return { pods: null, outside: 0 };
-      const raw = unwrapAll(items);
-      return { pods: onNode(raw, node), outside: countOutside(raw, opts) };
-    }, [items, node, opts]);
-    useEffect(function () {
-      if (got.outside > 0) props.store.noteSelectorIgnored('nodePods', got.outside, got);
-      props.onList(node, got.pods, got.pods ? null : err ? errorText(err) : null);
-    }, [got, err, node]);
-    return null;
-  }
-
-  /**
-   * One node's pods by the field-selected request (requests.js
-   * fetchNodePods: the apiserver applies the selector as a query parameter),
-   * re-read every scopedPollSec(): what a Node detail section reads on a host
-   * that ignores useList() options, instead of the cluster-wide list such a
-   * host would deliver.
-   */
-  function NodePodsPoll(props) {
-    const node = props.node;
-    const onList = props.onList;
-    const period = scopedPollSec();
-    useEffect(function () {
-      let live = true;
-      const timeoutMs = loadSettings().requestTimeoutMs;
-      function read() {
-        return fetchNodePods(request, node, timeoutMs).then(
-          function (items) { if (live) onList(node, onNode(items, node), null); },
-          function (e) { if (live) onList(node, null, errorText(e)); }
-        );
-      }
-      read();
-      const poller = createPoller(period);
-      poller.start(read);
-      return function () {
-        live = false;
-        poller.stop();
-      };
-    }, [node, period]);
-    return null;
-  }
-
-  /** The GPU pods of `nodeName` in the store's last pod list (any age), or null when it holds none. */
-  function seedPods(store, nodeName) {
-    const snap = store.getSnapshot();
-    if (snap.podsState !== 'ready') return null;
-    const byNode = snap.index && snap.index.podsByNode ? snap.index.podsByNode.get(nodeName) : undefined;
-    return byNode || snap.gpuPods.filter(function (p) { return get(p, ['spec', 'nodeName'], null) === nodeName; });
-  }
-
-  /**
-   * The pods of one node for a Node detail section that no mounted page
-   * feeds: a list + watch scoped to the node (NodePodsWatch), live like the
-   * reference's section — a pod scheduled onto the node appears without a
-   * reload (reference src/index.tsx:152-160: a full provider with the
-   * cluster-wide Pod list + watch, IntelGpuDataContext.tsx:98-99) — at O(pods
-   * on the node) instead of O(pods in the cluster); on a host that ignores
-   * list options, the field-selected request re-read (NodePodsPoll). The
-   * list request goes out in the same wave as the node's telemetry and power
-   * history.
-   *
-   * Until the node's own list delivers, the store's last pod list (a plugin
-   * page visited earlier, no longer watched) seeds the section, so it paints
-   * at once. A list that stops answering after it delivered keeps the pods
-   * shown; only a first failure says the pods are unreadable.
-   *
-   * Returns [the slice of the context nodeDetailView reads, the feed element
-   * the caller renders].
-   */
-  function useNodePods(nodeName) {
-    const store = storeFor(clusterKey());
-    const ignored = React.useSyncExternalStore(store.subscribe, function () { return store.selectorsIgnored('nodePods'); });
-    const seed = useMemo(function () { return seedPods(store, nodeName); }, [store, nodeName]);
-    const st = useState(null);
-    const got = st[0];
-    const setGot = st[1];
-    const onList = useMemo(function () {
-      return function (node, pods, error) {
-        setGot(function (prev) {
-          const same = prev && prev.node === node;
-          if (pods) return { node: node, pods: pods, error: null };
-          // A re-list or a failure after a delivery keeps what is shown.
-          if (same && prev.pods) return prev;
-          return error ? { node: node, pods: null, error: error } : same ? prev : null;
-        });
-      };
-    }, []);
-    const cur = got && got.node === nodeName ? got : null;
-    const pods = cur && cur.pods ? cur.pods : cur && cur.error ? null : seed;
-    const ctx = useMemo(function () {
-      if (pods) return { loading: false, gpuPods: filterGpuRequestingPods(pods), podsState: 'ready', error: null };
-      if (cur && cur.error) return { loading: false, gpuPods: [], podsState: 'error', error: cur.error };
-      return { loading: true, gpuPods: [], podsState: 'pending', error: null };
-    }, [pods, cur && cur.error]);
-    const feed = h(ignored ? NodePodsPoll : NodePodsWatch, { node: nodeName, onList: onList, store: store });
-    return [ctx, feed];
-  }
-
   /** One node's GPU power history for the native Node detail page (metrics.js fetchNodeSeries). */
   function useNodeGpuSeries(nodeName, enabled) {
     const cluster = clusterKey();
@@ -672,6 +542,12 @@ export function createProviderCore(React, lib, deps) {
     return res;
   }
 
+  // The Node detail section's pods (nodePodHooks.js).
+  const nodePods = createNodePodHooks(React, lib, {
+    storeFor: storeFor, clusterKey: clusterKey, request: request, loadSettings: loadSettings,
+    scopedPollSec: scopedPollSec, useListOf: useListOf, errorText: errorText,
+  });
+
   return {
     Context: Context,
     AmdGpuDataProvider: AmdGpuDataProvider,
@@ -682,8 +558,8 @@ export function createProviderCore(React, lib, deps) {
     useGpuOwners: useGpuOwners,
     usePodGpuSeries: usePodGpuSeries,
     useNodeGpuSeries: useNodeGpuSeries,
-    useNodePods: useNodePods,
-    usePodsLive: usePodsLive,
+    useNodePods: nodePods.useNodePods,
+    usePodsLive: nodePods.usePodsLive,
     storeFor: storeFor,
     metricsSourceFor: metricsSourceFor,
     /** The current cluster's key (per-cluster state: stores, view state). */
