@@ -13,8 +13,8 @@
  */
 
 import { getNodeGpuCount, partitionsPerGpu } from './amdNodes.js';
-import { getPodGpuCount } from './amdPods.js';
-import { get, MI355X } from './k8sCore.js';
+import { podFacts } from './clusterIndex.js';
+import { MI355X } from './k8sCore.js';
 
 /**
  * One schedulable device. On a partitioned node (DPX/QPX/CPX) device `index`
@@ -56,9 +56,8 @@ export function buildGpuSlots(node, podsOnNode, perGpuOwners, dims) {
   let next = 0;
   for (let p = 0; p < podsOnNode.length; p++) {
     const pod = podsOnNode[p];
-    const phase = get(pod, ['status', 'phase'], '');
-    if (phase === 'Succeeded' || phase === 'Failed') continue;
-    const g = getPodGpuCount(pod);
+    // What the pod holds (0 once terminated), derived when the pod list arrived.
+    const g = podFacts(pod).gpus;
     for (let k = 0; k < g && next < n; k++, next++) {
       slots[next].pod = pod.metadata.name;
       slots[next].namespace = pod.metadata.namespace || null;

@@ -174,7 +174,9 @@ export function metricsView(ctx, mstate, opts) {
   const nodesPend = nodesPending(ctx);
   if (nodesPend) items.push(loader('Loading ' + BRAND + ' data...'));
   const m = mstate.metrics;
-  items.push(metricAvailabilitySection(m));
+  // The sections below that read the snapshot alone are memoised on it: a
+  // watch event (a new store snapshot, same telemetry) re-renders none of them.
+  items.push(memo('metrics-availability', [m], function () { return metricAvailabilitySection(m); }));
   if (mstate.fetching && !m) items.push(loader('Querying Prometheus for GPU metrics...'));
 
   if (mstate.fetchError) {
@@ -212,9 +214,9 @@ export function metricsView(ctx, mstate, opts) {
   if (m && (m.gpus.length > 0 || (tot && tot.gpus > 0))) {
     // Cluster totals: server-side aggregates on a paged (scoped) snapshot,
     // else summed here from every GPU of the snapshot.
-    const sum = tot || summarizeMetrics(m);
-    items.push(
-      section('GPU Power Summary', [
+    const sum = tot || memo('metrics-sum', [m], function () { return summarizeMetrics(m); });
+    items.push(memo('metrics-summary', [m, sum, ctx.gpuNodes], function () {
+      return section('GPU Power Summary', [
         kv([
           row('GPUs Monitored', String(sum.gpus)),
           row('Nodes Reporting', tot ? nodesReportingCount(tot.nodes, ctx) : nodesReporting(m, ctx)),
@@ -232,19 +234,12 @@ export function metricsView(ctx, mstate, opts) {
               : new Date(m.fetchedAt).toLocaleTimeString()
           ),
         ], m.query ? [row('Query', m.query)] : [])),
-      ])
-    );
+      ]);
+    }));
 
-    const byNode = {};
-    const order = [];
-    for (let i = 0; i < m.gpus.length; i++) {
-      const g = m.gpus[i];
-      if (!byNode[g.nodeName]) {
-        byNode[g.nodeName] = [];
-        order.push(g.nodeName);
-      }
-      byNode[g.nodeName].push(g);
-    }
+    const grouped = memo('metrics-by-node', [m], function () { return gpusByNode(m.gpus); });
+    const byNode = grouped.byNode;
+    const order = grouped.order;
     // One page of per-node cards. A paged snapshot covers the GPU nodes of
     // the page (m.scope); a cluster-wide one is paged over the nodes reporting.
     const scoped = Array.isArray(m.scope);
@@ -257,26 +252,8 @@ export function metricsView(ctx, mstate, opts) {
 
     const sr = mstate.series;
     if (sr && sr.power) {
-      const win = formatWindow(sr.rangeSec || 1800);
-      // A paged snapshot's series carry the cluster line apart (series.total);
-      // a cluster-wide one is summed here. Peak / average are the cluster's;
-      // the table shows the cluster line and the nodes of the page.
-      const total = sr.total || seriesTotal(sr);
-      const ps = clusterPowerStats({ cluster: total.power || [] });
       const cap = sum.powerCapWatts > 0 ? sum.powerCapWatts : null;
-      const statRows = ps
-        ? [kv([
-          row('Peak Power (' + win + ')', powerBar(ps.peakWatts, cap)),
-          row('Average Power (' + win + ')', powerBar(ps.avgWatts, cap)),
-        ])]
-        : [];
-      const power = Object.assign(withTotal(total.power), pick(sr.power, pg.names));
-      const vram = Object.assign(withTotal(total.vram), pick(sr.vram || {}, pg.names));
-      items.push(
-        section('Power & HBM (last ' + win + ')', statRows.concat([
-          { t: 'series', power: power, vram: vram, avgPower: seriesMeans(power) },
-        ]))
-      );
+      items.push(memo('metrics-series', [sr, cap].concat(pg.names), function () { return seriesSection(sr, cap, pg.names); }));
     }
 
     items.push(rankedView ? pager(pg, 'GPU nodes reporting', { sort: 'power', sorts: RANKED_NODE_SORTS, label: 'GPU nodes' })
@@ -310,6 +287,42 @@ export function metricsView(ctx, mstate, opts) {
 
   void now;
   return page(BRAND + ' — Metrics', refreshButton('Refresh metrics', mstate.fetching || nodesPend), items);
+}
+
+/** The snapshot's GPUs grouped by node, nodes in order of first appearance. */
+function gpusByNode(gpus) {
+  const byNode = {};
+  const order = [];
+  for (let i = 0; i < gpus.length; i++) {
+    const g = gpus[i];
+    if (!byNode[g.nodeName]) {
+      byNode[g.nodeName] = [];
+      order.push(g.nodeName);
+    }
+    byNode[g.nodeName].push(g);
+  }
+  return { byNode: byNode, order: order };
+}
+
+/** The power / HBM history of the cluster line and the nodes of the page (`names`). */
+function seriesSection(sr, cap, names) {
+  const win = formatWindow(sr.rangeSec || 1800);
+  // A paged snapshot's series carry the cluster line apart (series.total);
+  // a cluster-wide one is summed here. Peak / average are the cluster's;
+  // the table shows the cluster line and the nodes of the page.
+  const total = sr.total || seriesTotal(sr);
+  const ps = clusterPowerStats({ cluster: total.power || [] });
+  const statRows = ps
+    ? [kv([
+      row('Peak Power (' + win + ')', powerBar(ps.peakWatts, cap)),
+      row('Average Power (' + win + ')', powerBar(ps.avgWatts, cap)),
+    ])]
+    : [];
+  const power = Object.assign(withTotal(total.power), pick(sr.power, names));
+  const vram = Object.assign(withTotal(total.vram), pick(sr.vram || {}, names));
+  return section('Power & HBM (last ' + win + ')', statRows.concat([
+    { t: 'series', power: power, vram: vram, avgPower: seriesMeans(power) },
+  ]));
 }
 
 /** Says which limits are MI355X platform values because the source reports none. */

@@ -125,6 +125,24 @@ describe('view memoisation', () => {
     expect(b).toBe(a);
   });
 
+  it('metrics page: a watch event (new context, same snapshot) rebuilds none of its sections; a new snapshot rebuilds the summary', () => {
+    const ctx = makeContext({ nodes: [makeGpuNode('g0')] });
+    const g = { nodeName: 'g0', gpu: '0', pod: null, namespace: null, powerWatts: 900, powerCapWatts: 1400,
+      vramUsedBytes: 1, vramTotalBytes: 2, gfxActivityPct: 50, memActivityPct: 20, tempC: 60 };
+    const m1 = { source: 'amd-exporter', gpus: [g], xgmi: {}, links: {}, fetchedAt: new Date(NOW).toISOString() };
+    const series = { rangeSec: 1800, power: { g0: [[1, 900], [2, 950]] }, vram: { g0: [[1, 1], [2, 1]] } };
+    const st = { metrics: m1, series, fetchError: null, fetching: false };
+    const a = sections(metricsView(ctx, st, { now: NOW }));
+    const b = sections(metricsView(Object.assign({}, ctx), st, { now: NOW + 1000 }));
+    expect(a.map((s) => s.title)).toEqual(['Metric Availability', 'GPU Power Summary', 'Power & HBM (last 30 min)', 'g0 — 1 × MI355X']);
+    b.forEach((s, i) => expect(s).toBe(a[i]));
+    const m2 = Object.assign({}, m1, { fetchedAt: new Date(NOW + 5000).toISOString() });
+    const c = sections(metricsView(ctx, Object.assign({}, st, { metrics: m2 }), { now: NOW }));
+    expect(c[1]).not.toBe(a[1]);
+    expect(c[2]).toBe(a[2]); // same series window
+    expect(c[3]).toBe(a[3]); // same GPU objects
+  });
+
   it('pod detail sections are cached per pod object', () => {
     const p = makeGpuPod('p');
     expect(podDetailView(p)).toBe(podDetailView({ jsonData: p }));
