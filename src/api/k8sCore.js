@@ -88,7 +88,9 @@ export const PLUGIN_POD_QUERIES = [
  * The same two selections as list + watch options of Headlamp's
  * `Pod.useList()` (providerCore.js OperatorPodFeed), in PLUGIN_POD_QUERIES
  * order: what the Device Plugins route watches instead of every pod of the
- * cluster. (Query options of `useList`: verify against the Headlamp release.)
+ * cluster. A host whose `useList` does not apply these options delivers
+ * objects outside them: the feed counts those (selectors.js countOutside),
+ * and the provider swaps the watches for the scoped requests (ADR 012).
  */
 export const OPERATOR_POD_LISTS = Object.freeze([
   Object.freeze({ namespace: '', labelSelector: PLUGIN_POD_LABEL_SELECTOR, fieldSelector: PLUGIN_POD_FIELD_SELECTOR }),
