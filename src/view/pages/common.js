@@ -126,6 +126,22 @@ export function clearViewMemo() {
   resetDerivedCaches();
 }
 
+let timeFormat = null;
+
+/**
+ * `new Date(t).toLocaleTimeString()` (the reference's "Last Fetched",
+ * MetricsPage.tsx:336-338) through one cached formatter with the same
+ * options: the method builds a formatter per call, ≈30 µs on Node.
+ */
+export function localTimeText(t) {
+  if (!timeFormat) {
+    timeFormat = typeof Intl === 'object' && Intl.DateTimeFormat
+      ? new Intl.DateTimeFormat(undefined, { hour: 'numeric', minute: 'numeric', second: 'numeric' })
+      : { format: function (d) { return d.toLocaleTimeString(); } };
+  }
+  return timeFormat.format(new Date(t));
+}
+
 export function nowOf(opts) {
   return opts && typeof opts.now === 'number' ? opts.now : Date.now();
 }

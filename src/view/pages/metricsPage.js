@@ -13,6 +13,7 @@ import {
   eccCell,
   formatWindow,
   hbmBar,
+  localTimeText,
   memo,
   nowOf,
   pctText,
@@ -230,8 +231,8 @@ export function metricsView(ctx, mstate, opts) {
           row(
             'Last Fetched',
             m.stale
-              ? status('warning', new Date(m.fetchedAt).toLocaleTimeString() + ' (stale: the latest refresh failed)')
-              : new Date(m.fetchedAt).toLocaleTimeString()
+              ? status('warning', localTimeText(m.fetchedAt) + ' (stale: the latest refresh failed)')
+              : localTimeText(m.fetchedAt)
           ),
         ], m.query ? [row('Query', m.query)] : [])),
       ]);

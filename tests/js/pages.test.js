@@ -4,7 +4,7 @@
  * PodsPage.test.tsx 6, MetricsPage.test.tsx 9). Assertions target section
  * titles, row labels, status values and refresh aria-labels, as there.
  */
-import { allocationBar, eccCell, formatWindow, hbmBar, powerBar, tempCell } from '../../src/view/pages/common.js';
+import { allocationBar, eccCell, formatWindow, hbmBar, localTimeText, powerBar, tempCell } from '../../src/view/pages/common.js';
 import { nodeDetailView, podDetailView } from '../../src/view/pages/details.js';
 import { devicePluginsView } from '../../src/view/pages/devicePlugins.js';
 import { metricsView } from '../../src/view/pages/metricsPage.js';
@@ -634,6 +634,14 @@ describe('metricsView', () => {
     expect(sectionTitles(vm)).toContain('Power & HBM (last 6 h)');
     expect(formatWindow(90)).toBe('90 s');
     expect(formatWindow(900)).toBe('15 min');
+  });
+  it('"Last Fetched" reads as toLocaleTimeString() does, through one cached formatter', () => {
+    const t0 = Date.parse('2026-10-16T13:04:05Z');
+    for (let i = 0; i < 48; i++) {
+      const t = t0 + i * 3599 * 1000;
+      expect(localTimeText(t)).toBe(new Date(t).toLocaleTimeString());
+      expect(localTimeText(new Date(t).toISOString())).toBe(new Date(t).toLocaleTimeString());
+    }
   });
   it('powerBar without a cap shows watts only', () => {
     expect(powerBar(512.25, null).text).toBe('512.3 W');
