@@ -264,24 +264,31 @@ export function formatGpuResourceName(key) {
  * Bytes → "288 GiB" / "2.3 TiB". Binary units: the MI355X's "288 GB" of HBM3E
  * is 288 GiB (measured on the device), and the exporter reports MiB.
  */
+const BYTE_UNITS = ['B', 'KiB', 'MiB', 'GiB', 'TiB', 'PiB'];
+
 export function formatBytes(b) {
   if (!(b >= 0) || b === null) return '—';
-  const units = ['B', 'KiB', 'MiB', 'GiB', 'TiB', 'PiB'];
   let v = b;
   let u = 0;
-  while (v >= 1024 && u < units.length - 1) {
+  while (v >= 1024 && u < BYTE_UNITS.length - 1) {
     v /= 1024;
     u++;
   }
   // Three significant digits, trailing zeros dropped: "288 GiB", "2.25 TiB", "4.5 TiB".
   const digits = v >= 100 || u === 0 ? 0 : v >= 10 ? 1 : 2;
   let t = v.toFixed(digits);
-  if (digits > 0) t = t.replace(/\.?0+$/, '');
-  return t + ' ' + units[u];
+  if (digits > 0) {
+    let end = t.length;
+    while (t.charCodeAt(end - 1) === 48) end--; // '0'
+    if (t.charCodeAt(end - 1) === 46) end--; // '.'
+    t = t.slice(0, end);
+  }
+  return t + ' ' + BYTE_UNITS[u];
 }
 
+/** Watts with one decimal, as `toFixed(1)` writes them (whole watts, the usual reading, without the call). */
 export function formatWatts(w) {
-  return w.toFixed(1) + ' W';
+  return (Number.isSafeInteger(w) ? w + '.0' : w.toFixed(1)) + ' W';
 }
 
 export function formatPercent(used, max) {

@@ -509,30 +509,41 @@ export function applyStatics(gpus, statics) {
  * @returns {{peakWatts: number, peakAt: number, avgWatts: number, steps: number} | null}
  */
 export function clusterPowerStats(powerByNode) {
-  const total = {};
-  for (const node in powerByNode || {}) {
-    const pts = powerByNode[node] || [];
+  const names = Object.keys(powerByNode || {});
+  // One series (the cluster line the Metrics page passes) is its own sum.
+  if (names.length === 1) return windowStats(powerByNode[names[0]] || []);
+  const total = new Map();
+  for (let n = 0; n < names.length; n++) {
+    const pts = powerByNode[names[n]] || [];
     for (let i = 0; i < pts.length; i++) {
-      const t = pts[i][0];
       const v = pts[i][1];
       if (typeof v !== 'number' || !isFinite(v)) continue;
-      total[t] = (total[t] || 0) + v;
+      total.set(pts[i][0], (total.get(pts[i][0]) || 0) + v);
     }
   }
-  const ts = Object.keys(total);
-  if (!ts.length) return null;
+  const steps = [];
+  total.forEach(function (v, t) { steps.push([t, v]); });
+  steps.sort(function (a, b) { return a[0] - b[0]; });
+  return windowStats(steps);
+}
+
+/** Peak (the earliest step holding it) and mean of one time-ordered series; null without a finite sample. */
+function windowStats(pts) {
   let peak = -Infinity;
   let peakAt = 0;
   let sum = 0;
-  for (let i = 0; i < ts.length; i++) {
-    const v = total[ts[i]];
+  let steps = 0;
+  for (let i = 0; i < pts.length; i++) {
+    const v = pts[i][1];
+    if (typeof v !== 'number' || !isFinite(v)) continue;
     sum += v;
+    steps++;
     if (v > peak) {
       peak = v;
-      peakAt = Number(ts[i]);
+      peakAt = Number(pts[i][0]);
     }
   }
-  return { peakWatts: peak, peakAt: peakAt, avgWatts: sum / ts.length, steps: ts.length };
+  return steps ? { peakWatts: peak, peakAt: peakAt, avgWatts: sum / steps, steps: steps } : null;
 }
 
 /** Cluster totals for the summary box. */

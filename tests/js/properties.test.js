@@ -5,8 +5,8 @@
  */
 import { getPodGpuDemand } from '../../src/api/amdPods.js';
 import { buildClusterIndex } from '../../src/api/clusterIndex.js';
-import { formatBytes } from '../../src/api/k8sCore.js';
-import { shareGpus, shareMap } from '../../src/api/telemetry.js';
+import { formatBytes, formatWatts } from '../../src/api/k8sCore.js';
+import { clusterPowerStats, shareGpus, shareMap } from '../../src/api/telemetry.js';
 import { buildXgmiMatrix, isFullMesh } from '../../src/api/topology.js';
 import { makeGpuNode } from './fixtures.js';
 import { int, mutate, pick, rng } from './fuzzlib.js';
@@ -313,6 +313,86 @@ describe('malformed Prometheus answers', () => {
         pages.podsView(ctx, { metrics: m, now: 0 });
       }
       pages.clearViewMemo();
+    }
+  });
+});
+
+describe('clusterPowerStats', () => {
+  // The per-step sum as a plain object keyed by step (integer keys iterate in
+  // ascending order): the definition the faster implementation must match.
+  function oracle(byNode) {
+    const total = {};
+    for (const n in byNode) {
+      for (const [t, v] of byNode[n]) if (typeof v === 'number' && isFinite(v)) total[t] = (total[t] || 0) + v;
+    }
+    const ts = Object.keys(total);
+    if (!ts.length) return null;
+    let peak = -Infinity;
+    let peakAt = 0;
+    let sum = 0;
+    for (const t of ts) {
+      sum += total[t];
+      if (total[t] > peak) {
+        peak = total[t];
+        peakAt = Number(t);
+      }
+    }
+    return { peakWatts: peak, peakAt: peakAt, avgWatts: sum / ts.length, steps: ts.length };
+  }
+
+  it('equals the per-step sum over nodes, for one series and for several, with gaps and non-numbers', () => {
+    const r = rng(2026);
+    let compared = 0;
+    for (let round = 0; round < 400; round++) {
+      const byNode = {};
+      const nodes = int(r, 1, 3);
+      for (let n = 0; n < nodes; n++) {
+        const pts = [];
+        const start = 1760000000 + 15 * int(r, 0, 4);
+        const len = int(r, 0, 40);
+        for (let i = 0; i < len; i++) {
+          if (r() < 0.2) continue; // a missing step
+          pts.push([start + 15 * i, pick(r, [int(r, 0, 1400), int(r, 0, 1400) + 0.5, 700, 700, NaN, null, Infinity, '5'])]);
+        }
+        byNode['n' + n] = pts;
+      }
+      const got = clusterPowerStats(byNode);
+      const want = oracle(byNode);
+      if (want === null) expect(got).toBeNull();
+      else {
+        expect(got.peakWatts).toBe(want.peakWatts);
+        expect(got.peakAt).toBe(want.peakAt);
+        expect(got.steps).toBe(want.steps);
+        expect(Math.abs(got.avgWatts - want.avgWatts)).toBeLessThan(1e-9 * Math.max(1, Math.abs(want.avgWatts)));
+        compared++;
+      }
+    }
+    expect(compared).toBeGreaterThan(300);
+  });
+});
+
+describe('formatters', () => {
+  it('formatWatts writes what toFixed(1) writes, and formatBytes trims as the regex /\\.?0+$/ does', () => {
+    const r = rng(355);
+    const xs = [0, -0, 1, -3, 0.05, 0.15, 2.5, 1023.95, 2 ** 53, 2 ** 53 + 2, -(2 ** 53), 1e21, 294896 * 1048576];
+    for (let i = 0; i < 5000; i++) {
+      xs.push(r() * Math.pow(2, r() * 70), Math.round(r() * Math.pow(2, r() * 70)), Math.round(r() * 30000) / 10, -r() * 100);
+    }
+    const units = ['B', 'KiB', 'MiB', 'GiB', 'TiB', 'PiB'];
+    function bytesOracle(b) {
+      let v = b;
+      let u = 0;
+      while (v >= 1024 && u < units.length - 1) {
+        v /= 1024;
+        u++;
+      }
+      const digits = v >= 100 || u === 0 ? 0 : v >= 10 ? 1 : 2;
+      const t = v.toFixed(digits);
+      return (digits > 0 ? t.replace(/\.?0+$/, '') : t) + ' ' + units[u];
+    }
+    for (const x of xs) {
+      expect(formatWatts(x)).toBe(x.toFixed(1) + ' W');
+      if (x >= 0) expect(formatBytes(x)).toBe(bytesOracle(x));
     }
   });
 });
