@@ -106,6 +106,174 @@ def test_offline_plugin_archive_is_installable_and_reproducible(tmp_path):
     assert meta["name"] == pkg["name"] and meta["version"] == pkg["version"] and meta["main"] == "main.js"
 
 
+def _node():
+    from headlamp_intel_gpu_plugin_amd.utils.nodebridge import node_binary
+
+    return node_binary()
+
+
+def _validator():
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    try:
+        import validate_artifacthub
+    finally:
+        sys.path.pop(0)
+    return validate_artifacthub
+
+
+def _committed_digest():
+    meta = yaml.safe_load(open(os.path.join(ROOT, "artifacthub-pkg.yml")))
+    return meta["annotations"]["headlamp/plugin/archive-checksum"].split(":", 1)[1]
+
+
+def test_committed_archive_checksum_is_this_trees_archive():
+    """artifacthub-pkg.yml's archive-checksum is the sha256 of the archive this tree builds (tools/bundle.js is
+    deterministic), recomputed here from the sources; `--check` says the same. A source change without
+    `node tools/bundle.js --package --stamp` fails this test (reference /root/reference/artifacthub-pkg.yml:101-105)."""
+    import subprocess
+
+    v = _validator()
+    digest = v.tree_digest(ROOT)
+    assert digest == _committed_digest()
+    assert v.validate(os.path.join(ROOT, "artifacthub-pkg.yml"), digest) == []
+    r = subprocess.run([_node(), os.path.join(ROOT, "tools", "bundle.js"), "--check"], cwd=ROOT, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_validator_rejects_placeholder_and_foreign_digests(tmp_path):
+    v = _validator()
+    shipped = os.path.join(ROOT, "artifacthub-pkg.yml")
+
+    def with_checksum(hexd):
+        m = yaml.safe_load(open(shipped))
+        m["annotations"]["headlamp/plugin/archive-checksum"] = "sha256:" + hexd
+        p = tmp_path / "pkg.yml"
+        p.write_text(yaml.safe_dump(m))
+        # screenshots resolve against the file's directory: put them beside it
+        if not (tmp_path / "docs").exists():
+            os.symlink(os.path.join(ROOT, "docs"), tmp_path / "docs")
+        return v.validate(str(p), _committed_digest())
+
+    for placeholder in ("0" * 64, "f" * 64, "ab" * 32, "deadbeef" * 8):
+        errs = with_checksum(placeholder)
+        assert len(errs) == 1 and "placeholder" in errs[0], (placeholder, errs)
+    errs = with_checksum("1" + _committed_digest()[1:] if _committed_digest()[0] != "1" else "2" + _committed_digest()[1:])
+    assert len(errs) == 1 and "not this tree's archive" in errs[0], errs
+    assert with_checksum(_committed_digest()) == []
+
+
+def test_the_archive_the_release_uploads_loads_and_registers_every_extension_point(tmp_path):
+    """The release's steps, in order, on a scratch copy of the output: bundle + package, then tools/verify_archive.js on
+    that file — gunzip, untar, evaluate the archive's own main.js with the host library as `pluginLib`: 6 sidebar
+    entries, 5 exact routes, 2 detail sections, 1 column processor, each route and section mounted."""
+    import subprocess
+
+    pkg = json.load(open(os.path.join(ROOT, "package.json")))
+    r = subprocess.run([_node(), os.path.join(ROOT, "tools", "bundle.js"), "--out", str(tmp_path / "main.js"), "--package"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    arc = tmp_path / f"{pkg['name']}-{pkg['version']}.tar.gz"
+    r = subprocess.run([_node(), os.path.join(ROOT, "tools", "verify_archive.js"), str(arc), "--version", pkg["version"],
+                        "--sha256", _committed_digest()], cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["ok"] and out["errors"] == []
+    assert out["registered"] == {"sidebar": 6, "routes": 5, "detailSections": 2, "columnProcessors": 1}
+    assert out["mounted"] == ["/amd-gpu", "/amd-gpu/device-plugins", "/amd-gpu/nodes", "/amd-gpu/pods", "/amd-gpu/metrics",
+                              "node-detail", "pod-detail", "headlamp-nodes columns"]
+    assert out["entries"] == [f"{pkg['name']}/main.js", f"{pkg['name']}/package.json"]
+
+
+def test_archive_verifier_fails_an_archive_that_does_not_register_everything(tmp_path):
+    import gzip
+    import io
+    import subprocess
+    import tarfile
+
+    pkg = json.load(open(os.path.join(ROOT, "package.json")))
+
+    def archive(main_js, extra=None):
+        buf = io.BytesIO()
+        with tarfile.open(fileobj=buf, mode="w", format=tarfile.USTAR_FORMAT) as t:
+            files = [(f"{pkg['name']}/main.js", main_js.encode()),
+                     (f"{pkg['name']}/package.json", json.dumps({"name": pkg["name"], "version": pkg["version"],
+                                                                 "main": "main.js"}).encode())] + (extra or [])
+            for name, body in files:
+                info = tarfile.TarInfo(name)
+                info.size = len(body)
+                t.addfile(info, io.BytesIO(body))
+        p = tmp_path / "a.tar.gz"
+        p.write_bytes(gzip.compress(buf.getvalue()))
+        r = subprocess.run([_node(), os.path.join(ROOT, "tools", "verify_archive.js"), str(p)], cwd=ROOT,
+                           capture_output=True, text=True, timeout=120)
+        return r.returncode, json.loads(r.stdout.strip().splitlines()[-1]) if r.stdout.strip() else None
+
+    one_route = ("(function (pluginLib) { pluginLib.registerRoute({ path: '/amd-gpu', exact: true, component: function () "
+                 "{ return null; } }); return { registered: { routes: 1 } }; })(pluginLib)")
+    rc, out = archive(one_route)
+    assert rc == 1 and not out["ok"]
+    assert any(e.startswith("sidebar") for e in out["errors"]) and any(e.startswith("routes") for e in out["errors"])
+    rc, out = archive("throw new Error('boom')")
+    assert rc == 1 and any("does not evaluate" in e for e in out["errors"])
+    dist = open(os.path.join(ROOT, "dist-offline", "main.js")).read() if os.path.exists(
+        os.path.join(ROOT, "dist-offline", "main.js")) else None
+    if dist:
+        rc, out = archive(dist, [(f"{pkg['name']}/extra.js", b"1")])
+        assert rc == 1 and any("entries" in e for e in out["errors"])
+
+
+def test_deflate_is_deterministic_and_standard():
+    """tools/deflate.js: any inflater reads it, and its bytes are pinned (a zlib build would vary across Node versions,
+    and the committed archive digest must be reproducible on the release runner)."""
+    import gzip
+    import hashlib
+    import subprocess
+
+    script = ("import { gzipStable } from './tools/deflate.js';"
+              "const parts = []; for (let i = 0; i < 4000; i++) parts.push('line ' + (i * 7919 % 1000) + ' of the MI355X fixture\\n');"
+              "process.stdout.write(gzipStable(Buffer.from(parts.join(''))).toString('base64'));")
+    r = subprocess.run([_node(), "--input-type=module", "-e", script], cwd=ROOT, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    import base64
+
+    gz = base64.b64decode(r.stdout)
+    text = "".join(f"line {i * 7919 % 1000} of the MI355X fixture\n" for i in range(4000)).encode()
+    assert gzip.decompress(gz) == text
+    assert gz[:4] == b"\x1f\x8b\x08\x00" and gz[4:8] == b"\0\0\0\0"  # no mtime
+    assert len(gz) < len(text) // 4
+    assert hashlib.sha256(gz).hexdigest() == DEFLATE_GOLDEN
+
+
+DEFLATE_GOLDEN = "42ae0ea4b2f2995f90011e16f1f66fe0572206d93bc7e80b800a047f20cc20f7"
+
+
+def test_release_publishes_the_verified_archive_and_commits_its_digest_before_tagging():
+    wf = yaml.safe_load(open(os.path.join(ROOT, ".github", "workflows", "release.yaml")))
+    steps = wf["jobs"]["release"]["steps"]
+    runs = [s.get("run", "") for s in steps]
+    names = [s.get("name", "") for s in steps]
+
+    def idx(pred):
+        return next(i for i, s in enumerate(steps) if pred(s))
+
+    pack = idx(lambda s: "tools/bundle.js" in s.get("run", "") and "--stamp" in s.get("run", ""))
+    verify = idx(lambda s: "tools/verify_archive.js" in s.get("run", ""))
+    commit = idx(lambda s: "git push origin HEAD:main" in s.get("run", ""))
+    tag = idx(lambda s: "git tag" in s.get("run", ""))
+    publish = idx(lambda s: "action-gh-release" in s.get("uses", ""))
+    assert pack < verify < commit < tag < publish, names
+    assert "dist-offline/amd-gpu-$VERSION.tar.gz" in runs[verify]
+    assert steps[publish]["with"]["files"] == "dist-offline/amd-gpu-${{ inputs.version }}.tar.gz"
+    assert "artifacthub-pkg.yml" in runs[commit]
+    assert not any("headlamp-plugin" in r or "npm run build" in r or "npm run package" in r for r in runs)
+    ci = yaml.safe_load(open(os.path.join(ROOT, ".github", "workflows", "ci.yaml")))
+    ci_runs = " ".join(s.get("run", "") for s in ci["jobs"]["plugin"]["steps"])
+    assert "validate_artifacthub.py --tree" in ci_runs and "tools/verify_archive.js" in ci_runs
+
+
 def test_artifacthub_metadata_is_valid_and_matches_the_manifest(tmp_path):
     """CI's ArtifactHub gate (reference .github/workflows/ci.yaml:25-72) accepts the shipped metadata, whose version is
     package.json's, and rejects the mistakes it exists to catch."""

@@ -4,7 +4,9 @@
  * self-contained script (default `dist-offline/main.js`; `headlamp-plugin build`
  * writes `dist/main.js`), the file Headlamp loads for a plugin.
  *
- *   node tools/bundle.js [--entry src/index.tsx] [--out dist-offline/main.js] [--package]
+ *   node tools/bundle.js [--entry src/index.tsx] [--out dist-offline/main.js] [--package] [--stamp]
+ *   node tools/bundle.js --digest      # print the archive's sha256 for this tree, write nothing
+ *   node tools/bundle.js --check       # exit 1 unless artifacthub-pkg.yml carries that digest
  *
  * The reference builds its bundle with `headlamp-plugin build` (vite;
  * /root/reference/package.json:16-18, CI /root/reference/.github/workflows/ci.yaml:169-170).
@@ -24,15 +26,22 @@
  *
  * Anything else (an `import`/`export` form this does not understand, a bare
  * specifier that is not a host module) is an error, not a silent pass-through.
- * CI still runs the real `npm run build`; this bundle is what the offline
- * checks load (tests/js/bundle.test.js evaluates it against the harness
- * stand-ins and mounts every registered component).
+ *
+ * This bundle is the shipped artifact: `--package` wraps it into the archive
+ * the release uploads (.github/workflows/release.yaml), `--stamp` writes that
+ * archive's version, URL and sha256 into artifacthub-pkg.yml (the reference
+ * commits the real digest, /root/reference/artifacthub-pkg.yml:101-105), and
+ * tools/verify_archive.js evaluates the archive's own main.js and checks
+ * every registration. The archive is a function of the tree alone (fixed
+ * tar headers, tools/deflate.js instead of zlib), so the CPU gate re-derives
+ * the committed digest. CI still runs `npm run build` (headlamp-plugin's
+ * vite build) as a check that the real toolchain compiles the sources.
  */
 import crypto from 'crypto';
 import fs from 'fs';
 import path from 'path';
 import { fileURLToPath } from 'url';
-import zlib from 'zlib';
+import { gzipStable } from './deflate.js';
 
 const ROOT = path.resolve(path.dirname(fileURLToPath(import.meta.url)), '..');
 
@@ -235,10 +244,11 @@ function tarEntry(name, body, mtime) {
 /**
  * The installable plugin archive: `<name>/main.js` + `<name>/package.json`,
  * the layout Headlamp loads from its plugins directory and `headlamp-plugin
- * package` produces; gzip-compressed, deterministic (fixed mtime). Returns
- * {file, sha256} — the checksum artifacthub-pkg.yml's archive-checksum takes.
+ * package` produces; gzip-compressed by tools/deflate.js with fixed tar
+ * headers (mtime 0), so the bytes depend on the bundle and package.json only.
+ * Returns {name, bytes, sha256}.
  */
-export function packageArchive(code, outDir) {
+export function archiveOf(code) {
   const pkg = JSON.parse(fs.readFileSync(path.join(ROOT, 'package.json'), 'utf8'));
   const meta = { name: pkg.name, version: pkg.version, description: pkg.description, license: pkg.license, main: 'main.js' };
   const mtime = 0;
@@ -247,26 +257,77 @@ export function packageArchive(code, outDir) {
     tarEntry(pkg.name + '/package.json', Buffer.from(JSON.stringify(meta, null, 2) + '\n', 'utf8'), mtime),
     Buffer.alloc(1024, 0),
   ]);
-  const gz = zlib.gzipSync(tar, { level: 9 });
-  // gzip header bytes 4-7 hold an mtime; zlib writes 0, so the archive is reproducible.
-  const file = path.join(outDir, pkg.name + '-' + pkg.version + '.tar.gz');
+  const gz = gzipStable(tar);
+  return { name: pkg.name + '-' + pkg.version + '.tar.gz', version: pkg.version, bytes: gz, sha256: crypto.createHash('sha256').update(gz).digest('hex') };
+}
+
+/** Write archiveOf(code) into outDir → {file, sha256} (the checksum artifacthub-pkg.yml's archive-checksum takes). */
+export function packageArchive(code, outDir) {
+  const a = archiveOf(code);
+  const file = path.join(outDir, a.name);
   fs.mkdirSync(outDir, { recursive: true });
-  fs.writeFileSync(file, gz);
-  return { file: file, sha256: crypto.createHash('sha256').update(gz).digest('hex') };
+  fs.writeFileSync(file, a.bytes);
+  return { file: file, sha256: a.sha256 };
+}
+
+/** The archive this tree ships: src/index.tsx bundled and packaged, in memory. */
+export function treeArchive() {
+  return archiveOf(bundle(path.join(ROOT, 'src', 'index.tsx')).code);
+}
+
+const PKG_YML = path.join(ROOT, 'artifacthub-pkg.yml');
+const CHECKSUM_RE = /^(\s*headlamp\/plugin\/archive-checksum:\s*)"sha256:[0-9a-f]{64}"\s*$/m;
+const URL_RE = /^(\s*headlamp\/plugin\/archive-url:\s*")([^"]*\/)v\d+\.\d+\.\d+\/([^"/]*?)-\d+\.\d+\.\d+\.tar\.gz"\s*$/m;
+
+/** artifacthub-pkg.yml text with version, archive URL and checksum set to archive `a`. */
+export function stampText(text, a) {
+  if (!CHECKSUM_RE.test(text)) throw new Error('bundle: no archive-checksum "sha256:<64 hex>" line in artifacthub-pkg.yml');
+  if (!URL_RE.test(text)) throw new Error('bundle: no archive-url ".../vX.Y.Z/<name>-X.Y.Z.tar.gz" line in artifacthub-pkg.yml');
+  if (!/^version: "[^"]*"\s*$/m.test(text)) throw new Error('bundle: no top-level version: "X.Y.Z" line in artifacthub-pkg.yml');
+  return text
+    .replace(/^version: "[^"]*"/m, 'version: "' + a.version + '"')
+    .replace(URL_RE, function (m, pre, base) { return pre + base + 'v' + a.version + '/' + a.name + '"'; })
+    .replace(CHECKSUM_RE, function (m, pre) { return pre + '"sha256:' + a.sha256 + '"'; });
+}
+
+/** The archive-checksum artifacthub-pkg.yml carries (hex), or null. */
+export function committedDigest(text) {
+  const m = /headlamp\/plugin\/archive-checksum:\s*"sha256:([0-9a-f]{64})"/.exec(text);
+  return m ? m[1] : null;
 }
 
 function main(argv) {
   let entry = path.join(ROOT, 'src', 'index.tsx');
   let out = path.join(ROOT, 'dist-offline', 'main.js');
   let pack = false;
+  let stamp = false;
+  let mode = 'build';
   for (let i = 0; i < argv.length; i++) {
     if (argv[i] === '--entry') entry = path.resolve(argv[++i]);
     else if (argv[i] === '--out') out = path.resolve(argv[++i]);
     else if (argv[i] === '--package') pack = true;
+    else if (argv[i] === '--stamp') pack = stamp = true;
+    else if (argv[i] === '--digest') mode = 'digest';
+    else if (argv[i] === '--check') mode = 'check';
     else {
-      process.stderr.write('usage: node tools/bundle.js [--entry src/index.tsx] [--out dist-offline/main.js] [--package]\n');
+      process.stderr.write('usage: node tools/bundle.js [--entry src/index.tsx] [--out dist-offline/main.js] [--package] [--stamp] | --digest | --check\n');
       return 2;
     }
+  }
+  if (mode !== 'build') {
+    const a = treeArchive();
+    if (mode === 'digest') {
+      process.stdout.write('sha256:' + a.sha256 + '\n');
+      return 0;
+    }
+    const text = fs.readFileSync(PKG_YML, 'utf8');
+    if (stampText(text, a) !== text) {
+      process.stderr.write('artifacthub-pkg.yml does not describe this tree\'s archive ' + a.name + ' (sha256:' + a.sha256 +
+        ', committed ' + committedDigest(text) + '); run: node tools/bundle.js --package --stamp\n');
+      return 1;
+    }
+    process.stdout.write('artifacthub-pkg.yml matches ' + a.name + ' sha256:' + a.sha256 + '\n');
+    return 0;
   }
   const b = bundle(entry);
   fs.mkdirSync(path.dirname(out), { recursive: true });
@@ -277,6 +338,11 @@ function main(argv) {
   if (pack) {
     const a = packageArchive(b.code, path.dirname(out));
     process.stdout.write(path.relative(process.cwd(), a.file) + ': sha256:' + a.sha256 + '\n');
+    if (stamp) {
+      if (entry !== path.join(ROOT, 'src', 'index.tsx')) throw new Error('bundle: --stamp describes the shipped entry, src/index.tsx');
+      fs.writeFileSync(PKG_YML, stampText(fs.readFileSync(PKG_YML, 'utf8'), archiveOf(b.code)));
+      process.stdout.write('artifacthub-pkg.yml: stamped sha256:' + a.sha256 + '\n');
+    }
   }
   return 0;
 }
