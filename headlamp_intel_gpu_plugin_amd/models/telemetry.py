@@ -6,7 +6,8 @@ Two sources fill the TSDB, mirroring the two exporters the plugin reads
 * ``amd-exporter`` — AMD Device Metrics Exporter style ``gpu_*`` gauges keyed
   by ``hostname`` + ``gpu_id``, with ``pod``/``namespace`` labels on GPUs a
   workload holds, ``xgmi_neighbor_N_tx_throughput`` per link and the
-  native exporter's ``gpu_xgmi_link_hops`` per peer;
+  native exporter's ``gpu_xgmi_link_hops`` per peer (with its ``neighbor``
+  order, which places the per-neighbour throughput on a peer);
 * ``node-exporter`` — ``node_hwmon_*`` (chip = PCI address, chip_name
   ``amdgpu``) and ``node_drm_*`` (card) series plus ``node_uname_info``.
 
@@ -145,8 +146,10 @@ def populate(db: TSDB, cluster: SyntheticCluster, source: str = "amd-exporter", 
 
                     db.add(Series(dict(base, __name__=f"xgmi_neighbor_{k}_tx_throughput"), fn=xgmi, interval=interval))
                     # Link hop count as the framework's amdgpu-exporter reports it
-                    # (ops/csrc/probe_core.h): one hop to every peer on the mesh.
-                    db.add(Series(dict(base, __name__="gpu_xgmi_link_hops", peer_gpu_id=str(peer)),
+                    # (ops/csrc/probe_core.h, --sysfs-only): one hop to every peer on
+                    # the mesh, and the link's place in the GPU's neighbour order (KFD
+                    # io_link order), which pins xgmi_neighbor_<k> to its peer.
+                    db.add(Series(dict(base, __name__="gpu_xgmi_link_hops", peer_gpu_id=str(peer), neighbor=str(k)),
                                   fn=lambda t: 1.0, interval=interval))
             else:
                 chip = pci_address(i, g)

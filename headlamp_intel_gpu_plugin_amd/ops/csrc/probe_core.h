@@ -415,12 +415,23 @@ inline std::string kfd_bdf(long long domain, long long location_id) {
   return b;
 }
 
-// Direct xGMI links between GPU ordinals (indices into `bdfs`), one pair per
+// One direct xGMI link between GPU ordinals, and its position among the
+// source node's xGMI io_links in io_link number order (io_links/0, /1, ...,
+// counting links to GPUs this process cannot read too): the neighbour order
+// the exporter publishes as the `neighbor` label, so a consumer can place a
+// per-neighbour series (xgmi_neighbor_<k>_*) on its peer.
+struct XgmiLink {
+  int from;
+  int to;
+  int neighbor;
+};
+
+// Direct xGMI links between GPU ordinals (indices into `bdfs`), one per
 // direction, from the KFD nodes this process may read.
-inline std::vector<std::pair<int, int>> kfd_xgmi_links(const std::vector<std::string>& bdfs) {
+inline std::vector<XgmiLink> kfd_xgmi_links(const std::vector<std::string>& bdfs) {
   const std::string base = sysfs_root() + "/sys/class/kfd/kfd/topology/nodes";
   std::vector<int> ordinal_of_node;  // KFD node → GPU ordinal (-1: CPU or unreadable)
-  std::vector<std::vector<std::pair<int, int>>> links;  // per node: (type, node_to)
+  std::vector<std::vector<std::pair<int, int>>> links;  // per node: (type, node_to), in io_link order
   for (int n : numbered_entries(base, "")) {
     if (n >= static_cast<int>(ordinal_of_node.size())) {
       ordinal_of_node.resize(n + 1, -1);
@@ -436,17 +447,21 @@ inline std::vector<std::pair<int, int>> kfd_xgmi_links(const std::vector<std::st
     ordinal_of_node[n] = static_cast<int>(it - bdfs.begin());
     for (int l : numbered_entries(nd + "/io_links", "")) {
       std::vector<std::pair<std::string, double>> lp;
-      if (!kfd_props(nd + "/io_links/" + std::to_string(l) + "/properties", &lp)) continue;
+      // An unreadable link keeps its place (type 0) so later neighbours keep their numbers.
+      if (!kfd_props(nd + "/io_links/" + std::to_string(l) + "/properties", &lp)) lp.clear();
       links[n].emplace_back(static_cast<int>(kfd_get(lp, "type", 0)), static_cast<int>(kfd_get(lp, "node_to", -1)));
     }
   }
-  std::vector<std::pair<int, int>> out;
+  std::vector<XgmiLink> out;
   for (size_t n = 0; n < links.size(); ++n) {
     if (ordinal_of_node[n] < 0) continue;
+    int k = 0;
     for (const auto& tl : links[n]) {
-      if (tl.first != kKfdIoLinkXgmi || tl.second < 0 || tl.second >= static_cast<int>(ordinal_of_node.size())) continue;
+      if (tl.first != kKfdIoLinkXgmi) continue;
+      const int neighbor = k++;
+      if (tl.second < 0 || tl.second >= static_cast<int>(ordinal_of_node.size())) continue;
       const int peer = ordinal_of_node[tl.second];
-      if (peer >= 0 && peer != ordinal_of_node[n]) out.emplace_back(ordinal_of_node[n], peer);
+      if (peer >= 0 && peer != ordinal_of_node[n]) out.push_back({ordinal_of_node[n], peer, neighbor});
     }
   }
   return out;
@@ -575,21 +590,23 @@ inline std::string render(const RenderOptions& opt) {
     }
   }
   if (opt.topology && opt.only_device < 0) {
-    auto link = [&](int a, int b, double hops) {
+    // `neighbor` (sysfs mode): the link's place in the KFD io_link order of gpu_id's node.
+    auto link = [&](int a, int b, double hops, int neighbor) {
       append_metric(&out, "gpu_xgmi_link_hops",
                     "hostname=\"" + escape_label(opt.hostname) + "\",gpu_id=\"" + std::to_string(a) +
-                        "\",peer_gpu_id=\"" + std::to_string(b) + "\"",
+                        "\",peer_gpu_id=\"" + std::to_string(b) + "\"" +
+                        (neighbor >= 0 ? ",neighbor=\"" + std::to_string(neighbor) + "\"" : std::string()),
                     hops);
     };
     if (from_sysfs) {
-      for (const auto& ab : kfd_xgmi_links(bdfs)) link(ab.first, ab.second, 1.0);
+      for (const auto& l : kfd_xgmi_links(bdfs)) link(l.from, l.to, 1.0, l.neighbor);
     } else {
       for (int a = 0; a < g_count; ++a) {
         for (int b = 0; b < g_count; ++b) {
           if (a == b) continue;
           uint32_t type = 0, hops = 0;
           if (hipExtGetLinkTypeAndHopCount(a, b, &type, &hops) != hipSuccess || type != kLinkTypeXgmi) continue;
-          link(a, b, static_cast<double>(hops));
+          link(a, b, static_cast<double>(hops), -1);  // HIP reports no neighbour order
         }
       }
     }

@@ -95,8 +95,11 @@ export const SMALL_HWMON_GPUS = SMALL_CLUSTER_NODES * 8;
  * dozen of those to every gauge, which would otherwise dominate the bytes
  * moved through the Headlamp proxy on each refresh. `max` also folds
  * duplicate scrapes of one GPU (two jobs scraping one exporter).
+ * `neighbor` is on this repo's exporter's link series only: the link's place
+ * in the GPU's neighbour order, which pins the stock exporter's per-neighbour
+ * throughput to a peer (topology.js placeThroughput).
  */
-export const EXPORTER_JOIN_LABELS = ['__name__', 'hostname', 'node', 'instance', 'gpu_id', 'peer_gpu_id', 'pod', 'namespace'];
+export const EXPORTER_JOIN_LABELS = ['__name__', 'hostname', 'node', 'instance', 'gpu_id', 'peer_gpu_id', 'neighbor', 'pod', 'namespace'];
 
 /**
  * The projection of the per-refresh (live-only) query once the static query

@@ -34,9 +34,11 @@ import { isExporterName } from './promql.js';
  * @typedef {Object} GpuMetrics
  * @property {'amd-exporter'|'node-exporter'|null} source
  * @property {GpuTelemetry[]} gpus
- * @property {Record<string, Record<string, number>>} xgmi  node → "src-dst" → GB/s
- * @property {Record<string, Record<string, {type: string, hops: number}>>} links  node → "src-dst" →
- *           measured link (gpu_xgmi_link_hops); empty when the exporter does not report topology
+ * @property {Record<string, Record<string, number>>} xgmi  node → GB/s sent over xGMI, keyed "src-dst" when
+ *           the series named the peer, "src>k" for neighbour k (placed by topology.js placeThroughput)
+ * @property {Record<string, Record<string, {type: string, hops: number, neighbor?: number}>>} links  node →
+ *           "src-dst" → measured link (gpu_xgmi_link_hops; `neighbor` when the exporter publishes its neighbour
+ *           order); empty when the exporter does not report topology
  * @property {string} fetchedAt
  * @property {boolean} [stale]  the latest fetch failed; this is the previous snapshot
  * @property {string} prometheusPath
@@ -127,7 +129,14 @@ export function joinExporterResults(r) {
   }
   gpus.sort(byNodeGpu);
 
-  // xGMI: neighbour k of GPU i is the k-th peer in index order, skipping i (verify).
+  // xGMI throughput as the series state it, placed on no peer yet:
+  // `src-dst` when the row names its peer (a `peer_gpu_id` label), else
+  // `src>k` for neighbour k of the stock exporter's
+  // xgmi_neighbor_<k>_tx_throughput, whose neighbour numbering no series
+  // documents. topology.js placeThroughput puts `src>k` on a peer only when a
+  // link series pins neighbour k (this repo's amdgpu-exporter: the `neighbor`
+  // label, from the KFD io_link order); otherwise it counts towards GPU src's
+  // xGMI total alone.
   const xgmi = {};
   const xr = r.__xgmi;
   if (Array.isArray(xr)) {
@@ -139,15 +148,16 @@ export function joinExporterResults(r) {
       if (!mm) continue;
       const src = parseInt(m.gpu_id, 10);
       if (!isFinite(src)) continue;
-      const k = parseInt(mm[1], 10);
-      const dst = k < src ? k : k + 1;
+      const peer = typeof m.peer_gpu_id === 'string' && m.peer_gpu_id !== '' ? parseInt(m.peer_gpu_id, 10) : NaN;
+      if (peer === src) continue;
       const node = labelStr(m.hostname) || labelStr(m.instance);
       if (!xgmi[node]) xgmi[node] = {};
       const v = num(xr[i].value[1]);
-      if (v !== null) xgmi[node][src + '-' + dst] = v / 1e9;
+      if (v !== null) xgmi[node][isFinite(peer) ? src + '-' + peer : src + '>' + mm[1]] = v / 1e9;
     }
   }
-  // Measured topology: gpu_xgmi_link_hops{gpu_id, peer_gpu_id} per xGMI-connected pair.
+  // Measured topology: gpu_xgmi_link_hops{gpu_id, peer_gpu_id[, neighbor]} per
+  // xGMI-connected pair; `neighbor`: the link's place in gpu_id's neighbour order.
   const links = {};
   const lr = r[E.linkHops];
   if (Array.isArray(lr)) {
@@ -158,7 +168,8 @@ export function joinExporterResults(r) {
       const v = num(lr[i].value[1]);
       if (v === null || m.gpu_id === undefined || m.peer_gpu_id === undefined) continue;
       if (!links[node]) links[node] = {};
-      links[node][m.gpu_id + '-' + m.peer_gpu_id] = { type: 'XGMI', hops: v };
+      const nb = typeof m.neighbor === 'string' && /^\d+$/.test(m.neighbor) ? parseInt(m.neighbor, 10) : -1;
+      links[node][m.gpu_id + '-' + m.peer_gpu_id] = nb >= 0 ? { type: 'XGMI', hops: v, neighbor: nb } : { type: 'XGMI', hops: v };
     }
   }
   return { gpus: gpus, xgmi: xgmi, links: links };

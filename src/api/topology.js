@@ -67,30 +67,99 @@ export function buildGpuSlots(node, podsOnNode, perGpuOwners, dims) {
   return { slots: slots, exact: false, partitionsPerGpu: pp };
 }
 
+const placeCache = typeof WeakMap === 'function' ? new WeakMap() : null;
+
+/**
+ * Measured xGMI throughput of one node (telemetry.js join: "src-dst" when the
+ * series named the peer, "src>k" for neighbour k) placed on the matrix:
+ *   * "src-dst" as given;
+ *   * "src>k" on the peer whose link series carries `neighbor: k` (this
+ *     repo's amdgpu-exporter publishes its KFD io_link order) — else on no
+ *     peer: the stock exporter does not say which peer its neighbour k is,
+ *     and KFD does not promise index order;
+ *   * "i-i": GPU i's throughput summed over all its rows, placed or not —
+ *     the figure that needs no neighbour order.
+ * → {map, pinned: a row landed on a peer, perGpu: a total exists}; null
+ * without measurements. Cached on the maps (their identity holds while the
+ * values do).
+ * @param {Record<string, number>|null|undefined} measured
+ * @param {Record<string, {type: string, hops: number, neighbor?: number}>|null|undefined} probed
+ */
+export function placeThroughput(measured, probed) {
+  if (!measured || typeof measured !== 'object') return null;
+  if (placeCache) {
+    const hit = placeCache.get(measured);
+    if (hit && hit.probed === (probed || null)) return hit.placed;
+  }
+  let byNeighbor = null;
+  if (probed) {
+    for (const k in probed) {
+      const p = probed[k];
+      const dash = k.indexOf('-');
+      if (!p || typeof p.neighbor !== 'number' || dash <= 0) continue;
+      (byNeighbor || (byNeighbor = {}))[k.slice(0, dash) + '>' + p.neighbor] = k.slice(dash + 1);
+    }
+  }
+  const map = {};
+  let pinned = false;
+  let perGpu = false;
+  for (const key in measured) {
+    const v = measured[key];
+    if (typeof v !== 'number') continue;
+    const dash = key.indexOf('-');
+    let src;
+    let dst;
+    if (dash > 0) {
+      src = key.slice(0, dash);
+      dst = key.slice(dash + 1);
+      if (dst === src) continue;
+    } else {
+      const gt = key.indexOf('>');
+      if (gt <= 0) continue;
+      src = key.slice(0, gt);
+      dst = byNeighbor ? byNeighbor[key] : undefined;
+    }
+    if (dst !== undefined) {
+      map[src + '-' + dst] = v;
+      pinned = true;
+    }
+    const self = src + '-' + src;
+    map[self] = (map[self] || 0) + v;
+    perGpu = true;
+  }
+  const placed = perGpu ? { map: map, pinned: pinned, perGpu: perGpu } : null;
+  if (placeCache) placeCache.set(measured, { probed: probed || null, placed: placed });
+  return placed;
+}
+
 /**
  * xGMI neighbour matrix for one node.
  *
  * @param {number} gpuCount
- * @param {Record<string, number>} [measured]  `${src}-${dst}` → GB/s observed
- *        (exporter xGMI throughput series), optional
- * @param {Record<string, {type: string, hops: number}>} [probed]  `${src}-${dst}` →
- *        link type/hops from the native probe (hipExtGetLinkTypeAndHopCount)
+ * @param {Record<string, number>} [measured]  GB/s observed (exporter xGMI
+ *        throughput series, telemetry.js keys), optional; placed by placeThroughput
+ * @param {Record<string, {type: string, hops: number, neighbor?: number}>} [probed]  `${src}-${dst}` →
+ *        link type/hops from the exporter's link series (KFD io_links / hipExtGetLinkTypeAndHopCount)
  * @returns {{ size: number, cells: Array<Array<{ kind: 'self'|'xgmi'|'pcie'|'none', hops: number, peakGBs: number, measuredGBs: number|null }>>,
  *             linksPerGpu: number, perGpuPeakGBs: number, ringBusGBs: number }}
+ *          a `self` cell's measuredGBs is the GPU's xGMI throughput summed over its links
  */
 export function buildXgmiMatrix(gpuCount, measured, probed) {
   const n = gpuCount > 0 ? gpuCount : 0;
+  const placed = placeThroughput(measured, probed);
+  const pm = placed ? placed.map : null;
   const cells = [];
   let linksPerGpu = 0;
   for (let i = 0; i < n; i++) {
     const row = [];
     let links = 0;
     for (let j = 0; j < n; j++) {
+      const key = i + '-' + j;
+      const m = pm && typeof pm[key] === 'number' ? pm[key] : null;
       if (i === j) {
-        row.push({ kind: 'self', hops: 0, peakGBs: 0, measuredGBs: null });
+        row.push({ kind: 'self', hops: 0, peakGBs: 0, measuredGBs: m });
         continue;
       }
-      const key = i + '-' + j;
       let kind = 'xgmi';
       let hops = 1;
       if (probed) {
@@ -100,7 +169,6 @@ export function buildXgmiMatrix(gpuCount, measured, probed) {
         kind = !p ? 'none' : p.type === 'XGMI' ? 'xgmi' : p.type === 'PCIE' ? 'pcie' : 'none';
         hops = p ? p.hops : 0;
       }
-      const m = measured && typeof measured[key] === 'number' ? measured[key] : null;
       if (kind === 'xgmi') links++;
       row.push({ kind: kind, hops: hops, peakGBs: kind === 'xgmi' ? MI355X.xgmiLinkGBs : 0, measuredGBs: m });
     }
@@ -129,16 +197,18 @@ const factCache = typeof WeakMap === 'function' ? new WeakMap() : null;
 
 /**
  * What buildXgmiMatrix + isFullMesh say of a node's links, without the grid:
- * {fullMesh, linksPerGpu, stats: {links, meanGBs, maxGBs} | null} — `stats`
- * over the measured throughput of the xGMI links (every pair of distinct GPUs
- * in the platform model; the pairs `probed` types XGMI otherwise). Cached on
- * the map objects (the metrics client keeps a map's identity while its
- * values are unchanged; the measured topology is static), so a page that
- * re-renders reads it once per answer. The metrics client derives them when
- * an answer arrives (nodeSummaries.js primeSnapshot).
+ * {fullMesh, linksPerGpu, stats, gpuStats} — `stats` ({links, meanGBs,
+ * maxGBs} | null) over the throughput placed on xGMI links (every pair of
+ * distinct GPUs in the platform model; the pairs `probed` types XGMI
+ * otherwise), `gpuStats` ({gpus, meanGBs, maxGBs} | null) over the per-GPU
+ * totals (placeThroughput). Cached on the map objects (the metrics client
+ * keeps a map's identity while its values are unchanged; the measured
+ * topology is static), so a page that re-renders reads it once per answer.
+ * The metrics client derives them when an answer arrives
+ * (nodeSummaries.js primeSnapshot).
  * @param {number} n  GPUs of the node
  * @param {Record<string, number>|null} measured
- * @param {Record<string, {type: string, hops: number}>|null} probed  (non-empty, or null)
+ * @param {Record<string, {type: string, hops: number, neighbor?: number}>|null} probed  (non-empty, or null)
  */
 export function linkFacts(n, measured, probed) {
   const key = measured || probed;
@@ -151,12 +221,25 @@ export function linkFacts(n, measured, probed) {
   let cnt = 0;
   let sum = 0;
   let max = 0;
-  if (probed || measured) {
+  let gCnt = 0;
+  let gSum = 0;
+  let gMax = 0;
+  const placed = placeThroughput(measured, probed);
+  const pm = placed ? placed.map : null;
+  if (probed || pm) {
     for (let i = 0; i < n; i++) {
       let links = 0;
       for (let j = 0; j < n; j++) {
-        if (i === j) continue;
         const k = linkKey(i, j);
+        if (i === j) {
+          const t = pm ? pm[k] : undefined;
+          if (typeof t === 'number') {
+            gCnt++;
+            gSum += t;
+            if (t > gMax) gMax = t;
+          }
+          continue;
+        }
         let xgmi = true;
         if (probed) {
           const p = probed[k];
@@ -164,7 +247,7 @@ export function linkFacts(n, measured, probed) {
           if (!xgmi || p.hops !== 1) full = false;
           if (xgmi) links++;
         }
-        const v = measured && xgmi ? measured[k] : undefined;
+        const v = pm && placed.pinned && xgmi ? pm[k] : undefined;
         if (typeof v === 'number') {
           cnt++;
           sum += v;
@@ -174,7 +257,12 @@ export function linkFacts(n, measured, probed) {
       if (probed && links > linksPerGpu) linksPerGpu = links;
     }
   }
-  const facts = { fullMesh: full, linksPerGpu: linksPerGpu, stats: cnt ? { links: cnt, meanGBs: sum / cnt, maxGBs: max } : null };
+  const facts = {
+    fullMesh: full,
+    linksPerGpu: linksPerGpu,
+    stats: cnt ? { links: cnt, meanGBs: sum / cnt, maxGBs: max } : null,
+    gpuStats: gCnt ? { gpus: gCnt, meanGBs: gSum / gCnt, maxGBs: gMax } : null,
+  };
   if (factCache && key) factCache.set(key, { n: n, measured: measured, probed: probed, facts: facts });
   return facts;
 }

@@ -48,6 +48,12 @@ export function renderValue(v) {
   }
 }
 
+/** Whether a grid's diagonal carries per-GPU xGMI totals (a hand-made block has no throughputPerGpu). */
+function selfMeasured(m) {
+  for (let i = 0; i < m.size; i++) if (m.cells[i][i].measuredGBs !== null && m.cells[i][i].measuredGBs !== undefined) return true;
+  return false;
+}
+
 function renderBlock(b) {
   switch (b.t) {
     case 'kv':
@@ -86,7 +92,7 @@ function renderBlock(b) {
     case 'matrix': {
       const m = b.matrix;
       const attrs = 'data-testid="xgmi-matrix" data-full-mesh="' + (b.fullMesh ? 'true' : 'false') + '" data-topology="' +
-        (b.measuredTopology ? 'measured' : 'assumed') + '" data-throughput="' + (b.measuredThroughput ? 'measured' : 'none') + '"';
+        (b.measuredTopology ? 'measured' : 'assumed') + '" data-throughput="' + (b.measuredThroughput ? 'measured' : (b.throughputPerGpu !== undefined ? b.throughputPerGpu : selfMeasured(m)) ? 'per-gpu' : 'none') + '"';
       // A closed matrix (GPU Nodes cards) is its summary, as the React renderer draws it.
       if (b.open === false) return '<details ' + attrs + '><summary>' + esc(matrixCaption(b) + matrixSummary(b)) + '</summary></details>';
       let h = '<table ' + attrs + '><caption>' + esc(matrixCaption(b) + matrixSummary(b)) + '</caption><thead><tr><th></th>';
@@ -96,7 +102,7 @@ function renderBlock(b) {
         h += '<tr><th>GPU ' + i + '</th>';
         for (let j = 0; j < m.size; j++) {
           const c = m.cells[i][j];
-          h += '<td data-kind="' + c.kind + '">' + (c.kind === 'self' ? '—' : c.kind === 'xgmi'
+          h += '<td data-kind="' + c.kind + '">' + (c.kind === 'self' ? (c.measuredGBs !== null ? '\u03a3 ' + c.measuredGBs.toFixed(1) + ' GB/s' : '—') : c.kind === 'xgmi'
             ? (c.measuredGBs !== null ? c.measuredGBs.toFixed(1) + '/' : '') + c.peakGBs + ' GB/s'
             : c.kind) + '</td>';
         }

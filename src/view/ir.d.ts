@@ -86,6 +86,7 @@ export interface XgmiCell {
   kind: 'self' | 'xgmi' | 'pcie' | 'none';
   hops: number;
   peakGBs: number;
+  /** GB/s placed on this link (a series pinned its peer); on a `self` cell, the GPU's xGMI total over all links. */
   measuredGBs: number | null;
 }
 
@@ -103,8 +104,10 @@ export interface MatrixBlock {
   fullMesh: boolean;
   /** Link types / hops were measured (exporter link series) rather than assumed. */
   measuredTopology: boolean;
-  /** Per-link throughput was measured (stock exporter xgmi_neighbor_* series). */
+  /** Throughput sits on links: a series pinned each xgmi_neighbor_<k> row to its peer (topology.js placeThroughput). */
   measuredThroughput: boolean;
+  /** Per-GPU xGMI totals were measured (the diagonal cells); true whenever any throughput was. */
+  throughputPerGpu?: boolean;
   /** Renderers draw the grid (true) or its summary line with the grid one click away (false). */
   open: boolean;
   /** Facts pages/nodes.js matrixBlock reads from the link maps (topology.js linkFacts) without building
@@ -114,6 +117,7 @@ export interface MatrixBlock {
   linkGBs?: number;
   ringBusGBs?: number;
   linkStats?: { links: number; maxGBs: number; meanGBs: number } | null;
+  gpuStats?: { gpus: number; maxGBs: number; meanGBs: number } | null;
 }
 
 /** [unix seconds, value] */
@@ -221,10 +225,12 @@ export function createObjectCache(): ObjectCache;
 /** Record that the value being built changes at epoch-ms `t` (age labels). */
 export function noteExpiry(t: number | null | undefined): void;
 
-/** Caption of the xGMI matrix: measured topology, or the platform model with measured throughput. */
+/** Caption of the xGMI matrix: measured topology or the platform model; link or per-GPU throughput. */
 export function matrixCaption(b: MatrixBlock): string;
-/** " · measured: max X, mean Y GB/s over N links", or '' without measured throughput. */
+/** " · measured: max X, mean Y GB/s over N links", the per-GPU form, or '' without measured throughput. */
 export function matrixSummary(b: MatrixBlock): string;
+/** Text of one matrix cell: "Σ N" for a GPU's total, GB/s on a link, `xgmiMark` on an unmeasured xGMI link. */
+export function matrixCellText(c: XgmiCell, xgmiMark: string): string;
 /** "namespace/pod" or "free". */
 export function slotOwner(s: GpuSlot): string;
 /** Owners in runs: "GPU 0–3 ml/train-a · GPU 4–7 free". */

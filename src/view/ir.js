@@ -220,16 +220,19 @@ export function createObjectCache() {
 // Shared captions (React, HTML and text renderers)
 // ---------------------------------------------------------------------------
 
-/** Caption of the xGMI matrix: says whether the link topology was measured or is the platform model. */
+/**
+ * Caption of the xGMI matrix: whether the link topology was measured or is
+ * the platform model, and what throughput was measured — per link only when
+ * a series pinned each row to its peer (topology.js placeThroughput), else
+ * per GPU with the neighbour order said to be unknown.
+ */
 export function matrixCaption(b) {
   // Blocks of pages/nodes.js matrixBlock carry the facts; a hand-made block only its grid.
   const m = b.linksPerGpu !== undefined ? b : b.matrix;
   const peak = m.size > 1 ? ' ' + (b.linkGBs !== undefined ? b.linkGBs : m.cells[0][1].peakGBs) : '';
-  const kind = b.measuredTopology
-    ? 'measured'
-    : b.measuredThroughput
-      ? 'assumed MI355X full mesh; link throughput measured'
-      : 'assumed MI355X full mesh';
+  const perGpu = b.throughputPerGpu !== undefined ? b.throughputPerGpu : !!gridGpuStats(b.matrix);
+  const kind = (b.measuredTopology ? 'measured' : 'assumed MI355X full mesh') +
+    (b.measuredThroughput ? '; link throughput measured' : perGpu ? '; xGMI throughput measured per GPU, neighbour order not reported' : '');
   return (
     'xGMI topology (' + kind + ') — ' +
     (b.fullMesh ? 'full mesh, ' + m.linksPerGpu + ' links/GPU' : 'partial') +
@@ -238,15 +241,18 @@ export function matrixCaption(b) {
 }
 
 /**
- * The measured side of an xGMI matrix in one phrase (" · measured: max X,
- * mean Y GB/s over N links"), '' when no link throughput was measured: what
- * a closed matrix still says.
+ * The measured side of an xGMI matrix in one phrase — " · measured: max X,
+ * mean Y GB/s over N links" when throughput sits on links, " · measured per
+ * GPU: max X, mean Y GB/s over N GPUs" when only totals do, '' when nothing
+ * was measured: what a closed matrix still says.
  */
 export function matrixSummary(b) {
   // pages/nodes.js matrixBlock reads the statistics from the link maps; a
   // hand-made block (tests, text renderer) has only its grid.
   const st = b.linkStats !== undefined ? b.linkStats : gridLinkStats(b.matrix);
-  return st ? ' · measured: max ' + st.maxGBs.toFixed(0) + ', mean ' + st.meanGBs.toFixed(0) + ' GB/s over ' + st.links + ' links' : '';
+  if (st) return ' · measured: max ' + st.maxGBs.toFixed(0) + ', mean ' + st.meanGBs.toFixed(0) + ' GB/s over ' + st.links + ' links';
+  const gs = b.gpuStats !== undefined ? b.gpuStats : gridGpuStats(b.matrix);
+  return gs ? ' · measured per GPU: max ' + gs.maxGBs.toFixed(0) + ', mean ' + gs.meanGBs.toFixed(0) + ' GB/s over ' + gs.gpus + ' GPUs' : '';
 }
 
 function gridLinkStats(m) {
@@ -263,6 +269,27 @@ function gridLinkStats(m) {
     }
   }
   return n ? { links: n, meanGBs: sum / n, maxGBs: max } : null;
+}
+
+/** Per-GPU totals of a grid (its `self` cells). */
+function gridGpuStats(m) {
+  let n = 0;
+  let sum = 0;
+  let max = 0;
+  for (let i = 0; i < m.size; i++) {
+    const v = m.cells[i][i].measuredGBs;
+    if (typeof v !== 'number') continue;
+    n++;
+    sum += v;
+    if (v > max) max = v;
+  }
+  return n ? { gpus: n, meanGBs: sum / n, maxGBs: max } : null;
+}
+
+/** Text of one xGMI matrix cell: a GPU's total "Σ N" on the diagonal, GB/s on a link, else its kind. */
+export function matrixCellText(c, xgmiMark) {
+  if (c.kind === 'self') return c.measuredGBs !== null && c.measuredGBs !== undefined ? '\u03a3' + c.measuredGBs.toFixed(0) : '\u2014';
+  return c.measuredGBs !== null ? c.measuredGBs.toFixed(0) : c.kind === 'xgmi' ? xgmiMark : c.kind;
 }
 
 /** One slot's owner as `data-slots` lists it: "namespace/pod", or "free". */

@@ -108,7 +108,7 @@ const AVAILABILITY = [
   ['GFX activity (%)', 'gfxActivityPct', 'gpu_gfx_activity', 'node_drm_gpu_busy_percent (--collector.drm)'],
   ['HBM controller activity (%)', 'memActivityPct', 'gpu_umc_activity', null],
   ['Junction temperature', 'tempC', 'gpu_junction_temperature', 'node_hwmon_temp_celsius, the sensor labelled "junction" (amdgpu hwmon)'],
-  ['xGMI link throughput', null, 'xgmi_neighbor_N_tx_throughput (7 links per GPU)', null],
+  ['xGMI link throughput', null, 'xgmi_neighbor_N_tx_throughput (7 links per GPU; per link where gpu_xgmi_link_hops gives the neighbour order, else per GPU)', null],
   ['Per-GPU pod owner', 'pod', 'pod / namespace labels (exporter pod association)', null],
 ];
 
@@ -151,7 +151,8 @@ export function metricAvailabilitySection(m) {
       ])),
       row('GFX activity (%)', lines([{ label: '', text: 'Available — gpu_gfx_activity, or node_drm_gpu_busy_percent' }])),
       row('HBM controller activity (%)', lines([{ label: '', text: 'Available — gpu_umc_activity (exporter only)' }])),
-      row('xGMI link throughput', lines([{ label: '', text: 'Available — xgmi_neighbor_N_tx_throughput (exporter only; 7 links per GPU)' }])),
+      row('xGMI link throughput', lines([{ label: '', text: 'Available — xgmi_neighbor_N_tx_throughput (exporter only; 7 links per GPU). ' +
+        'Drawn per link where gpu_xgmi_link_hops gives the neighbour order (this repo\'s amdgpu-exporter), else as each GPU\'s total' }])),
       row('Per-GPU pod owner', lines([{ label: '', text: 'Available when the exporter runs with pod association (pod / namespace labels)' }])),
     ]),
   ]);

@@ -93,9 +93,12 @@ export function matrixBlock(gpuCount, measured, probed, open) {
 
 /**
  * An xGMI matrix block (IR `matrix`): `fullMesh`, `linksPerGpu`,
- * `ringBusGBs` and the measured-link statistics (`linkStats`) read from the
- * maps (topology.js linkFacts, cached on them), as buildXgmiMatrix +
- * isFullMesh would say; `matrix`, the grid itself, built when first read.
+ * `ringBusGBs` and the throughput statistics (`linkStats` over throughput
+ * placed on links, `gpuStats` over per-GPU totals) read from the maps
+ * (topology.js linkFacts, cached on them), as buildXgmiMatrix + isFullMesh
+ * would say; `matrix`, the grid itself, built when first read. toJSON gives
+ * the plain IR shape (the grid built, the link maps left out), so the JSON
+ * a consumer reads (`amd-gpu-dash --json`) renders like the block.
  */
 function MatrixBlock(n, measured, probed, open) {
   const f = linkFacts(n, measured, probed);
@@ -103,17 +106,20 @@ function MatrixBlock(n, measured, probed, open) {
   this.fullMesh = f.fullMesh;
   // Link types / hops come from the exporter's gpu_xgmi_link_hops (this
   // repo's amdgpu-exporter); without them the matrix is the MI355X
-  // platform model, and only per-link throughput (stock exporter
-  // xgmi_neighbor_*_tx_throughput) is measured.
+  // platform model. Throughput (stock exporter xgmi_neighbor_*_tx_throughput)
+  // sits on a link only where a series pins its peer (topology.js
+  // placeThroughput); otherwise only each GPU's total is measured.
   this.measuredTopology = !!probed;
   this.measuredThroughput = !!f.stats;
+  this.throughputPerGpu = !!f.gpuStats;
   this.open = open;
   this.size = n;
   this.linksPerGpu = f.linksPerGpu;
   this.linkGBs = MI355X.xgmiLinkGBs;
   this.ringBusGBs = f.linksPerGpu > 0 ? MI355X.xgmiLinkGBs : 0;
   this.linkStats = f.stats;
-  this.measured = f.stats ? measured : null;
+  this.gpuStats = f.gpuStats;
+  this.measured = f.stats || f.gpuStats ? measured : null;
   this.probed = probed;
   this.grid = null;
 }
@@ -123,6 +129,15 @@ Object.defineProperty(MatrixBlock.prototype, 'matrix', {
     return this.grid || (this.grid = buildXgmiMatrix(this.size, this.measured || undefined, this.probed || undefined));
   },
 });
+
+MatrixBlock.prototype.toJSON = function () {
+  return {
+    t: 'matrix', matrix: this.matrix, fullMesh: this.fullMesh, measuredTopology: this.measuredTopology,
+    measuredThroughput: this.measuredThroughput, throughputPerGpu: this.throughputPerGpu, open: this.open, size: this.size,
+    linksPerGpu: this.linksPerGpu, linkGBs: this.linkGBs, ringBusGBs: this.ringBusGBs, linkStats: this.linkStats,
+    gpuStats: this.gpuStats,
+  };
+};
 
 const READY_CELLS = {};
 

@@ -31,7 +31,7 @@
  */
 
 import { BAR_COLORS, formatWatts } from '../api/k8sCore.js';
-import { matrixCaption, matrixSummary, pagerIdle, pagerText, slotOwner, slotsText } from './ir.js';
+import { matrixCaption, matrixCellText, matrixSummary, pagerIdle, pagerText, slotOwner, slotsText } from './ir.js';
 
 /** CommonComponents the renderer needs (reference src/components/OverviewPage.tsx:8-16). */
 export const REQUIRED_COMPONENTS = [
@@ -290,12 +290,13 @@ export function createRenderer(React, CC) {
               { key: i },
               h('th', null, 'GPU ' + i),
               rowCells.map(function (c, j) {
-                const txt = c.kind === 'self' ? '—' : c.measuredGBs !== null ? c.measuredGBs.toFixed(0) : c.kind === 'xgmi' ? '•' : c.kind;
+                const txt = matrixCellText(c, '•');
                 return h(
                   'td',
                   {
                     key: j,
-                    title: c.kind === 'xgmi' ? c.hops + ' hop · ' + c.peakGBs + ' GB/s peak' : c.kind,
+                    title: c.kind === 'xgmi' ? c.hops + ' hop · ' + c.peakGBs + ' GB/s peak'
+                      : c.kind === 'self' && c.measuredGBs !== null ? 'GPU ' + i + ' xGMI throughput, all links (GB/s)' : c.kind,
                     style: { backgroundColor: matrixCellColor(c) },
                   },
                   txt

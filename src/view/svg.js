@@ -14,7 +14,7 @@
  */
 
 import { BAR_COLORS } from '../api/k8sCore.js';
-import { matrixCaption, matrixSummary, pagerText, slotsText } from './ir.js';
+import { matrixCaption, matrixCellText, matrixSummary, pagerText, slotsText } from './ir.js';
 import { matrixCellColor, sparklinePath } from './react.js';
 
 export const SVG_WIDTH = 1200;
@@ -266,7 +266,7 @@ function drawBlock(out, b, x, y, cols) {
         row.forEach(function (c, j) {
           const fill = matrixCellColor(c);
           out.push(rect(x + 60 + j * cw, y + h, cw - 2, LINE, fill === 'transparent' ? 'none' : fill, ' stroke="#e0e0e0"'));
-          const t = c.kind === 'self' ? '—' : c.measuredGBs !== null ? c.measuredGBs.toFixed(0) : c.kind === 'xgmi' ? '•' : c.kind;
+          const t = matrixCellText(c, '•');
           out.push(text(x + 60 + j * cw + (cw - 2 - width(t) * CHAR_W) / 2, y + h + 15, t));
         });
         h += LINE + 2;

@@ -121,7 +121,7 @@ function blockLines(b, color) {
       out.push('  ' + matrixCaption(b));
       m.cells.forEach(function (row, i) {
         out.push('    ' + pad('GPU ' + i, 6) + row.map(function (c) {
-          const v = c.kind === 'self' ? '-' : c.measuredGBs !== null ? String(Math.round(c.measuredGBs))
+          const v = c.kind === 'self' ? (c.measuredGBs !== null ? 'S' + Math.round(c.measuredGBs) : '-') : c.measuredGBs !== null ? String(Math.round(c.measuredGBs))
             : c.kind === 'xgmi' ? 'x' : '.';
           return ' '.repeat(Math.max(1, 4 - v.length)) + v; // right-aligned, 4 columns per cell
         }).join(''));

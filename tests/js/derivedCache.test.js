@@ -66,7 +66,7 @@ describe('derivedCache', () => {
     expect(power.byNode.n1).toBe('8028|11200');
     expect(owners.n1.map((o) => o.gpu)).toEqual(['0', '1']);
     expect(assign['ml/train']).toHaveLength(2);
-    expect(links).toEqual({ fullMesh: true, linksPerGpu: 7, stats: { links: 56, meanGBs: 10, maxGBs: 10 } });
+    expect(links).toEqual({ fullMesh: true, linksPerGpu: 7, stats: { links: 56, meanGBs: 10, maxGBs: 10 }, gpuStats: { gpus: 8, meanGBs: 70, maxGBs: 70 } });
   });
 
   it('the store derives the operator objects\' facts when it takes their lists', async () => {

@@ -11,8 +11,11 @@ import {
   podDetailView,
   seriesEnergyJoules,
 } from '../../src/view/pages/details.js';
-import { findSection, firstBlock, rowNames, rowValue, text } from '../../src/view/ir.js';
-import { buildGpuSlots, buildXgmiMatrix, isFullMesh } from '../../src/api/topology.js';
+import { findSection, firstBlock, matrixCaption, matrixSummary, rowNames, rowValue, text } from '../../src/view/ir.js';
+import { buildGpuSlots, buildXgmiMatrix, isFullMesh, placeThroughput } from '../../src/api/topology.js';
+import { matrixBlock, nodesView } from '../../src/view/pages/nodes.js';
+import { renderPage, renderSection } from '../../src/view/html.js';
+import { renderText } from '../../src/view/text.js';
 import { NOW, makeContext, makeGpuNode, makeGpuPod, makeNode, makePlainPod } from './fixtures.js';
 import { getNodeGpuCount, getNodePhysicalGpuCount, partitionsPerGpu } from '../../src/api/amdNodes.js';
 import { getPodGpuCount } from '../../src/api/amdPods.js';
@@ -46,6 +49,15 @@ describe('nodeDetailView', () => {
   it('computes allocation from pods on this node with threshold status', () => {
     const s = nodeDetailView(node, ctx);
     expect(rowValue(s, 'GPU Allocation')).toEqual({ t: 'status', status: 'warning', text: '6/8 (75%)' });
+  });
+  it('pods seeded from an earlier store list are marked as being refreshed, not shown as current', () => {
+    const s = nodeDetailView(node, Object.assign({}, ctx, { podsSeeded: true }));
+    expect(rowValue(s, 'GPU Workload Pods')).toBe('a, b (from an earlier pod list; refreshing…)');
+    expect(rowValue(s, 'GPU Allocation').text).toBe('6/8 (75%) (from an earlier pod list; refreshing…)');
+    const none = makeContext({ nodes: [node], pods: [] });
+    expect(rowValue(nodeDetailView(node, Object.assign({}, none, { podsSeeded: true })), 'GPU Workload Pods'))
+      .toBe('None (from an earlier pod list; refreshing…)');
+    expect(rowValue(nodeDetailView(node, ctx), 'GPU Workload Pods')).toBe('a, b');
   });
   it('escalates to error at 90%', () => {
     const c2 = makeContext({ nodes: [node], pods: [makeGpuPod('a', { node: 'g0', gpus: 8 })] });
@@ -237,6 +249,68 @@ describe('topology', () => {
     expect(m.cells[0][2].kind).toBe('none');
     expect(m.linksPerGpu).toBe(1);
     expect(isFullMesh(m)).toBe(false);
+  });
+  it('xGMI throughput sits on a link only where a series pins neighbour k to its peer; else only per GPU', () => {
+    // stock exporter rows: GPU 0 neighbours 0 and 1, GPU 1 neighbour 0 — which peers, no series says
+    const measured = { '0>0': 10, '0>1': 20, '1>0': 5 };
+    const unpinned = matrixBlock(8, measured, null, true);
+    expect(unpinned.measuredThroughput).toBe(false);
+    expect(unpinned.throughputPerGpu).toBe(true);
+    expect(matrixCaption(unpinned)).not.toContain('link throughput measured');
+    expect(matrixCaption(unpinned)).toContain('xGMI throughput measured per GPU, neighbour order not reported');
+    expect(matrixSummary(unpinned)).toBe(' · measured per GPU: max 30, mean 18 GB/s over 2 GPUs');
+    const ug = unpinned.matrix;
+    ug.cells.forEach((row, i) => row.forEach((c, j) => { if (i !== j) expect(c.measuredGBs).toBeNull(); }));
+    expect([ug.cells[0][0].measuredGBs, ug.cells[1][1].measuredGBs, ug.cells[2][2].measuredGBs]).toEqual([30, 5, null]);
+    // this repo's exporter: link series with the KFD neighbour order (GPU 0's listed in reverse)
+    const probed = {};
+    for (let i = 0; i < 8; i++) {
+      const peers = [];
+      for (let j = 0; j < 8; j++) if (j !== i) peers.push(j);
+      if (i === 0) peers.reverse();
+      peers.forEach((j, k) => { probed[i + '-' + j] = { type: 'XGMI', hops: 1, neighbor: k }; });
+    }
+    const pinned = matrixBlock(8, measured, probed, true);
+    expect(pinned.measuredThroughput).toBe(true);
+    expect(matrixCaption(pinned)).toBe('xGMI topology (measured; link throughput measured) — full mesh, 7 links/GPU · 7× 153 GB/s per GPU · ' +
+      'ring collectives bound at 153 GB/s per link');
+    expect(matrixSummary(pinned)).toBe(' · measured: max 20, mean 12 GB/s over 3 links');
+    const pg = pinned.matrix;
+    expect([pg.cells[0][7].measuredGBs, pg.cells[0][6].measuredGBs, pg.cells[1][0].measuredGBs, pg.cells[0][1].measuredGBs]).toEqual([10, 20, 5, null]);
+    expect(pg.cells[0][0].measuredGBs).toBe(30);
+    // a link series without the order pins nothing
+    const noOrder = {};
+    Object.keys(probed).forEach((k) => { noOrder[k] = { type: 'XGMI', hops: 1 }; });
+    expect(placeThroughput(measured, noOrder).pinned).toBe(false);
+    expect(matrixCaption(matrixBlock(8, measured, noOrder, false))).toBe('xGMI topology (measured; xGMI throughput measured per GPU, ' +
+      'neighbour order not reported) — full mesh, 7 links/GPU · 7× 153 GB/s per GPU · ring collectives bound at 153 GB/s per link');
+    // a row that names its own peer is placed as named
+    expect(placeThroughput({ '5-1': 7 }, null).map).toEqual({ '5-1': 7, '5-5': 7 });
+  });
+  it('a matrix block goes through JSON (amd-gpu-dash --json) with its grid and without the link maps', () => {
+    const b = matrixBlock(8, { '0>0': 10, '2-3': 4 }, null, false);
+    const j = JSON.parse(JSON.stringify(b));
+    expect(Object.keys(j).sort()).toEqual(['fullMesh', 'gpuStats', 'linkGBs', 'linkStats', 'linksPerGpu', 'matrix', 'measuredThroughput',
+      'measuredTopology', 'open', 'ringBusGBs', 'size', 't', 'throughputPerGpu']);
+    expect(j.matrix.cells[2][3].measuredGBs).toBe(4);
+    expect(j.matrix.cells[0][0].measuredGBs).toBe(10);
+    expect(renderSection({ title: 'n', blocks: [j] })).toBe(renderSection({ title: 'n', blocks: [b] }));
+    const open = JSON.parse(JSON.stringify(matrixBlock(8, { '0>0': 10 }, null, true)));
+    expect(renderText({ title: 'x', actions: null, items: [{ title: 'n', blocks: [open] }] })).toContain('S10');
+  });
+  it('a GPU Nodes and a Node detail view-model render the same after a JSON round trip', () => {
+    const nodes = [makeGpuNode('g0'), makeGpuNode('g1')];
+    const ctx = makeContext({ nodes: nodes, pods: [makeGpuPod('a', { node: 'g0', gpus: 4 })] });
+    const metrics = { source: 'amd-exporter', gpus: [], xgmi: { g0: { '0>0': 12, '1>3': 7 } }, links: {}, fetchedAt: new Date(NOW).toISOString() };
+    const vm = nodesView(ctx, { now: NOW, metrics: metrics });
+    const back = JSON.parse(JSON.stringify(vm));
+    expect(renderPage(back)).toBe(renderPage(vm));
+    expect(renderText(back)).toBe(renderText(vm));
+    const card = back.items.find((x) => x.title === 'g0');
+    expect(firstBlock(card, 'matrix').matrix.cells).toHaveLength(8);
+    const sec = nodeDetailView(nodes[0], ctx, { now: NOW, metrics: metrics });
+    const sback = JSON.parse(JSON.stringify(sec));
+    expect(renderSection(sback)).toBe(renderSection(sec));
   });
   it('a single GPU is not a mesh', () => {
     expect(isFullMesh(buildXgmiMatrix(1))).toBe(false);

@@ -111,11 +111,25 @@ describe('fetchGpuMetrics', () => {
     expect(m.gpus[0].namespace).toBe('ml');
     expect(m.gpus[4].pod).toBeNull();
   });
-  it('maps xGMI neighbour series onto peer indices', async () => {
+  it('keeps xGMI neighbour series per neighbour: no series says which peer neighbour k is', async () => {
     const src = createMetricsSource({ request: prom() });
     const m = await src.fetchGpuMetrics();
-    expect(m.xgmi.n0['0-1']).toBe(50);
-    expect(m.xgmi.n0['3-0']).toBe(50);
+    expect(m.xgmi.n0['0>0']).toBe(50);
+    expect(m.xgmi.n0['3>0']).toBe(50);
+    expect(m.xgmi.n0['0-1']).toBeUndefined();
+  });
+  it('places a neighbour row on the peer its own peer_gpu_id label names', async () => {
+    const d = exporterData(['n0']);
+    d.__xgmi = [vec({ __name__: 'xgmi_neighbor_2_tx_throughput', hostname: 'n0', gpu_id: '5', peer_gpu_id: '1' }, 30e9)];
+    const m = await createMetricsSource({ request: prom({ data: d }) }).fetchGpuMetrics();
+    expect(m.xgmi.n0).toEqual({ '5-1': 30 });
+  });
+  it('reads the neighbour order of the native exporter\'s link series', async () => {
+    const d = exporterData(['n0']);
+    d.gpu_xgmi_link_hops = [vec({ __name__: 'gpu_xgmi_link_hops', hostname: 'n0', gpu_id: '0', peer_gpu_id: '6', neighbor: '0' }, 1),
+      vec({ __name__: 'gpu_xgmi_link_hops', hostname: 'n0', gpu_id: '0', peer_gpu_id: '1', neighbor: 'x' }, 1)];
+    const m = await createMetricsSource({ request: prom({ data: d }) }).fetchGpuMetrics();
+    expect(m.links.n0).toEqual({ '0-6': { type: 'XGMI', hops: 1, neighbor: 0 }, '0-1': { type: 'XGMI', hops: 1 } });
   });
   it('reads measured xGMI link hops from the native exporter', async () => {
     const d = exporterData(['n0']);

@@ -62,8 +62,10 @@ describe('stock AMD Device Metrics Exporter (no repo-specific series)', () => {
       expect(g.vramTotalBytes).toBe(MI355X.hbmBytes);
     });
     expect(m.links).toEqual({});
-    expect(m.xgmi[HOST]['0-1']).toBeCloseTo(61.2, 6);
-    expect(m.xgmi[HOST]['4-5']).toBe(0);
+    // no series says which peer neighbour k is: the rows stay per neighbour, placed on no peer
+    expect(m.xgmi[HOST]['0>0']).toBeCloseTo(61.2, 6);
+    expect(m.xgmi[HOST]['4>4']).toBe(0);
+    expect(Object.keys(m.xgmi[HOST]).filter((k) => k.indexOf('-') >= 0)).toEqual([]);
   });
 
   it('Metrics page: summary says which limits are assumed; every per-GPU cell', async () => {
@@ -107,7 +109,7 @@ describe('stock AMD Device Metrics Exporter (no repo-specific series)', () => {
     expect(r(7)[7]).toBe('—');
   });
 
-  it('GPU Nodes page: exact per-GPU owners, assumed full mesh with measured link throughput', async () => {
+  it('GPU Nodes page: exact per-GPU owners, assumed full mesh, xGMI throughput per GPU only (neighbour order unknown)', async () => {
     const m = await fetchStock();
     const vm = nodesView(cluster(), { now: NOW, metrics: m });
     const card = sections(vm).find((x) => x.title === HOST);
@@ -116,22 +118,29 @@ describe('stock AMD Device Metrics Exporter (no repo-specific series)', () => {
     expect(slots.slots.map((x) => x.pod)).toEqual(['train-a', 'train-a', 'train-a', 'train-a', 'infer-b', null, null, null]);
     const mx = firstBlock(card, 'matrix');
     expect(mx.measuredTopology).toBe(false);
-    expect(mx.measuredThroughput).toBe(true);
+    expect(mx.measuredThroughput).toBe(false);
+    expect(mx.throughputPerGpu).toBe(true);
     expect(mx.fullMesh).toBe(true);
     expect(mx.matrix.cells[0][1].kind).toBe('xgmi');
-    expect(mx.matrix.cells[0][1].measuredGBs).toBeCloseTo(61.2, 6);
-    expect(mx.matrix.cells[4][5].measuredGBs).toBe(0);
+    // no link cell claims a measurement; each GPU's total sits on the diagonal
+    mx.matrix.cells.forEach((row, i) => row.forEach((c, j) => { if (i !== j) expect(c.measuredGBs).toBeNull(); }));
+    const sent = {};
+    m.gpus.forEach((g) => { sent[g.gpu] = 0; });
+    Object.keys(m.xgmi[HOST]).forEach((k) => { sent[k.split('>')[0]] += m.xgmi[HOST][k]; });
+    mx.matrix.cells.forEach((row, i) => expect(row[i].measuredGBs).toBeCloseTo(sent[String(i)], 6));
     const html = renderPage(vm);
-    expect(html).toContain('data-topology="assumed" data-throughput="measured"');
-    expect(html).toContain('xGMI topology (assumed MI355X full mesh; link throughput measured)');
-    expect(renderText(vm)).toContain('xGMI topology (assumed MI355X full mesh; link throughput measured) — full mesh, 7 links/GPU');
+    expect(html).toContain('data-topology="assumed" data-throughput="per-gpu"');
+    expect(html).not.toContain('link throughput measured');
+    expect(html).toContain('xGMI topology (assumed MI355X full mesh; xGMI throughput measured per GPU, neighbour order not reported)');
+    expect(renderText(vm)).toContain('xGMI topology (assumed MI355X full mesh; xGMI throughput measured per GPU, neighbour order not reported) — full mesh, 7 links/GPU');
   });
 
   it('Node detail and GPU Pods pages use the same stock series', async () => {
     const m = await fetchStock();
     const ctx = cluster();
     const sec = nodeDetailView(ctx.gpuNodes[0], ctx, { now: NOW, metrics: m });
-    expect(firstBlock(sec, 'matrix').measuredThroughput).toBe(true);
+    expect(firstBlock(sec, 'matrix').measuredThroughput).toBe(false);
+    expect(firstBlock(sec, 'matrix').throughputPerGpu).toBe(true);
     expect(firstBlock(sec, 'slots').exact).toBe(true);
     const pods = firstTable(findSection(podsView(ctx, { now: NOW, metrics: m }), 'All GPU Pods'));
     expect(pods.columns).toContain('Assigned GPUs');

@@ -110,6 +110,12 @@ describe('renderSectionSvg: the xGMI matrix', () => {
     const t = texts(svg);
     expect(t.filter((x) => x === 'GPU 7')).toHaveLength(2); // column and row header
     expect(t).toContain('117');
-    expect(t.filter((x) => x === '—')).toHaveLength(8); // the diagonal
+    // the diagonal: each GPU's xGMI total (GPU 2 sends 117 GB/s, the others nothing)
+    expect(t.filter((x) => /^\u03a3/.test(x))).toEqual(['\u03a30', '\u03a30', '\u03a3117', '\u03a30', '\u03a30', '\u03a30', '\u03a30', '\u03a30']);
+  });
+
+  it('no measurements: an em dash on the diagonal', () => {
+    const t = texts(renderSectionSvg(section('n1', [matrixBlock(8, null, null, true)])));
+    expect(t.filter((x) => x === '\u2014')).toHaveLength(8);
   });
 });

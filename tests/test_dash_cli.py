@@ -29,7 +29,7 @@ def test_all_pages_render(url):
     for title in ("AMD GPU — Overview", "AMD GPU — Device Plugins", "AMD GPU — Nodes", "AMD GPU — Pods",
                   "AMD GPU — Metrics"):
         assert "# " + title in r.stdout
-    assert "mi355x-001" in r.stdout and "xGMI topology (measured)" in r.stdout and "Assigned GPUs" in r.stdout
+    assert "mi355x-001" in r.stdout and "xGMI topology (measured; link throughput measured)" in r.stdout and "Assigned GPUs" in r.stdout
 
 
 def test_json_is_the_view_model(url):
@@ -55,7 +55,7 @@ def test_single_pages_ask_only_for_their_telemetry(url):
     pods = run("--url", url, "--page", "pods")
     assert pods.returncode == 0 and "Assigned GPUs" in pods.stdout and "mi355x-000: GPU 0" in pods.stdout
     nodes = run("--url", url, "--page", "nodes")
-    assert nodes.returncode == 0 and "xGMI topology (measured)" in nodes.stdout
+    assert nodes.returncode == 0 and "xGMI topology (measured; link throughput measured)" in nodes.stdout
 
 
 def test_overview_sends_no_prometheus_request():

@@ -220,25 +220,57 @@ def test_sysfs_only_reads_xgmi_links_from_a_readable_kfd_topology(exe, tmp_path)
     # Every GPU node readable (a pod whose device cgroup admits the render
     # nodes): node 2's captured properties as the template, each node at its
     # card's PCI address, every GPU linked to the 7 others (io_link type 11).
+    # GPU 0 (KFD node 2) keeps its captured io_links verbatim: a PCIe link to
+    # its CPU node, then xGMI to nodes 3..9 in that order. The others list a
+    # PCIe link, then their peers ROTATED (GPU k: k+1, k+2, ... mod 8), so the
+    # exporter's `neighbor` label must follow io_link order, not GPU index.
     # SYNTHETIC beyond node 2: the capture could read only its own GPU.
     captured = {n: (p, l) for n, p, l in _kfd_nodes(os.path.join(FIX, "kfd_topology.txt"))}
     template = [l for l in captured[2][0] if not l.startswith(("location_id ", "domain "))]
     xgmi_tmpl = next(lp for name, lp in captured[2][1].items() if lp and "type 11" in lp)
+    pcie_tmpl = captured[2][1]["io_links/0"]
     nodes = [(0, captured[0][0], {}), (1, captured[1][0], {})]
     cards = _drm_cards()
+    order = {}
     for k, (_, bdf) in enumerate(cards):
         bus, dev, fn = int(bdf[5:7], 16), int(bdf[8:10], 16), int(bdf[11], 16)
         props = template + [f"location_id {bus << 8 | dev << 3 | fn}", "domain 0"]
-        links = {}
-        for j in range(len(cards)):
-            if j != k:
-                links[f"io_links/{len(links)}"] = [l if not l.startswith("node_to ") else f"node_to {j + 2}"
-                                                   for l in xgmi_tmpl]
+        if k == 0:
+            links = {name: lp for name, lp in captured[2][1].items() if name.startswith("io_links")}
+        else:
+            links = {"io_links/0": pcie_tmpl}
+            for j in ((k + d) % len(cards) for d in range(1, len(cards))):
+                links[f"io_links/{len(links)}"] = [l if not l.startswith("node_to ") else f"node_to {j + 2}" for l in xgmi_tmpl]
+        # expected neighbour order: the xGMI io_links' node_to, in io_link number order
+        xg = [dict(x.split(" ", 1) for x in links[f"io_links/{i}"]) for i in range(len(links))]
+        order[k] = [int(l["node_to"]) - 2 for l in xg if l["type"] == "11"]
         nodes.append((k + 2, props, links))
+    assert order[0] == [1, 2, 3, 4, 5, 6, 7]  # the capture: node 2 → nodes 3..9
+    assert order[3] == [4, 5, 6, 7, 0, 1, 2]
     rows = _scrape_sysfs_only(exe, _sysfs_tree(tmp_path, nodes))
     hops = {(l["gpu_id"], l["peer_gpu_id"]): v for n, l, v in rows if n == "gpu_xgmi_link_hops"}
     assert len(hops) == 56 and set(hops.values()) == {1.0}
     assert all((str(a), str(b)) in hops for a in range(8) for b in range(8) if a != b)
+    neighbor = {(int(l["gpu_id"]), int(l["neighbor"])): int(l["peer_gpu_id"]) for n, l, v in rows if n == "gpu_xgmi_link_hops"}
+    assert neighbor == {(a, k): order[a][k] for a in range(8) for k in range(7)}
+
+
+def test_neighbor_numbers_count_links_to_unreadable_peers(exe, tmp_path):
+    """A link whose peer this process cannot read is not exported, but it keeps its place: the next readable peer's
+    `neighbor` is its io_link position among ALL xGMI links (what a per-neighbour series from another exporter counts)."""
+    captured = {n: (p, l) for n, p, l in _kfd_nodes(os.path.join(FIX, "kfd_topology.txt"))}
+    template = [l for l in captured[2][0] if not l.startswith(("location_id ", "domain "))]
+    cards = _drm_cards()
+    nodes = [(0, captured[0][0], {}), (1, captured[1][0], {})]
+    readable = {0, 4}  # GPUs 0 and 4 only: GPU 0 reaches GPU 4 as its 4th xGMI neighbour (nodes 3,4,5 unreadable)
+    for k, (_, bdf) in enumerate(cards):
+        bus, dev, fn = int(bdf[5:7], 16), int(bdf[8:10], 16), int(bdf[11], 16)
+        props = (template + [f"location_id {bus << 8 | dev << 3 | fn}", "domain 0"]) if k in readable else []
+        links = {name: lp for name, lp in captured[2][1].items() if name.startswith("io_links")} if k == 0 else {}
+        nodes.append((k + 2, props, links))
+    rows = _scrape_sysfs_only(exe, _sysfs_tree(tmp_path, nodes))
+    links = [(l["gpu_id"], l["peer_gpu_id"], l["neighbor"]) for n, l, v in rows if n == "gpu_xgmi_link_hops"]
+    assert links == [("0", "4", "3")]
 
 
 def test_captured_kfd_topology_links_this_gpu_to_seven_peers_over_xgmi():
