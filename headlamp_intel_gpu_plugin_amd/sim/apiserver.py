@@ -46,6 +46,7 @@ import concurrent.futures
 import heapq
 import random
 import json
+import logging
 import re
 import threading
 import time
@@ -56,6 +57,8 @@ from aiohttp import web
 
 from ..models.cluster import SyntheticCluster
 from . import promql
+
+log = logging.getLogger(__name__)
 
 DEFAULT_PROM_SERVICE = ("monitoring", "kube-prometheus-stack-prometheus", "9090")
 
@@ -388,16 +391,23 @@ def build_app(fc: FakeCluster) -> web.Application:
     prom_pool = PriorityPool()
 
     def evaluate_rule(q):
-        """Evaluate ``q`` now and keep the answer (runs on the evaluation thread)."""
-        t = fc.now()
-        stamp = promql.cache_stamp(fc.db, t)
-        body = promql.query(fc.db, q, t)
-        prev = fc.answers.get(q)
-        # [inputs' stamp, body, last asked (fake clock), evaluated at (monotonic)]
-        fc.answers[q] = [stamp, body, prev[2] if prev else t, time.monotonic()]
-        fc.rule_evals += 1
-        fc.refreshing.discard(q)
-        return body
+        """Evaluate ``q`` now and keep the answer (runs on the evaluation thread). A failed evaluation is logged and
+        raised to its caller; either way ``q`` leaves ``fc.refreshing``, so the ticker can schedule it again (a
+        background refresh's future has no one awaiting it)."""
+        try:
+            t = fc.now()
+            stamp = promql.cache_stamp(fc.db, t)
+            body = promql.query(fc.db, q, t)
+            prev = fc.answers.get(q)
+            # [inputs' stamp, body, last asked (fake clock), evaluated at (monotonic)]
+            fc.answers[q] = [stamp, body, prev[2] if prev else t, time.monotonic()]
+            fc.rule_evals += 1
+            return body
+        except Exception:
+            log.exception("rule evaluation failed: %s", q)
+            raise
+        finally:
+            fc.refreshing.discard(q)
 
     def schedule_rule(q):
         if q not in fc.refreshing:
@@ -417,7 +427,10 @@ def build_app(fc: FakeCluster) -> web.Application:
                 for q, ent in list(fc.answers.items()):
                     if now - ent[2] > RULE_TTL_S:
                         fc.answers.pop(q, None)
-                    elif ent[0] != stamp and (mono - ent[3] >= RULE_STALE_S or (lull and mono - ent[3] >= RULE_EVAL_S)):
+                    # No stamp (series sampled at mixed intervals): the inputs may have changed at
+                    # any time, so the answer counts as changed and the age limits decide.
+                    elif (stamp is None or ent[0] != stamp) and (mono - ent[3] >= RULE_STALE_S or
+                                                                 (lull and mono - ent[3] >= RULE_EVAL_S)):
                         schedule_rule(q)
 
         if fc.rules:

@@ -121,8 +121,10 @@ export function createNodePodHooks(React, lib, env) {
    *
    * Until the node's own list delivers, the store's last pod list (a plugin
    * page visited earlier, no longer watched) seeds the section, so it paints
-   * at once. A list that stops answering after it delivered keeps the pods
-   * shown; only a first failure says the pods are unreadable.
+   * at once; that list can be of any age, so the context says so
+   * (`podsSeeded`) and the section marks its pods as being refreshed. A list
+   * that stops answering after it delivered keeps the pods shown; only a
+   * first failure says the pods are unreadable.
    *
    * Returns [the slice of the context nodeDetailView reads, the feed element
    * the caller renders].
@@ -146,9 +148,10 @@ export function createNodePodHooks(React, lib, env) {
       };
     }, []);
     const cur = got && got.node === nodeName ? got : null;
-    const pods = cur && cur.pods ? cur.pods : cur && cur.error ? null : seed;
+    const own = cur && cur.pods ? cur.pods : null;
+    const pods = own || (cur && cur.error ? null : seed);
     const ctx = useMemo(function () {
-      if (pods) return { loading: false, gpuPods: filterGpuRequestingPods(pods), podsState: 'ready', error: null };
+      if (pods) return { loading: false, gpuPods: filterGpuRequestingPods(pods), podsState: 'ready', error: null, podsSeeded: !own };
       if (cur && cur.error) return { loading: false, gpuPods: [], podsState: 'error', error: cur.error };
       return { loading: true, gpuPods: [], podsState: 'pending', error: null };
     }, [pods, cur && cur.error]);

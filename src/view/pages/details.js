@@ -66,16 +66,20 @@ export function nodeDetailView(resource, ctx, opts) {
   const xg = metrics && metrics.xgmi ? metrics.xgmi[name] : undefined;
   const lk = metrics && metrics.links ? metrics.links[name] : undefined;
   const podsUnreadable = ctx.podsState === 'error';
+  // Pods from the store's last list while the node's own list is on its way (nodePodHooks.js useNodePods).
+  const seeded = !!ctx.podsSeeded && !podsPend;
   const series = opts && opts.series && opts.series.power && opts.series.power.length ? opts.series : null;
   // This node's GPUs from the node-scoped snapshot (metrics.js fetchNodeMetrics): the live telemetry table.
   const gs = metrics && metrics.gpus ? metrics.gpus.filter(function (g) { return g.nodeName === name; }) : [];
-  const deps = [raw, podsOnNode, podsPend, podsUnreadable, own, xg, lk, series].concat(gs);
+  const deps = [raw, podsOnNode, podsPend, podsUnreadable, seeded, own, xg, lk, series].concat(gs);
   return memo('node-detail:' + name, deps, function () {
-    return nodeDetailSection(raw, name, cap, alloc, podsOnNode, podsPend, own, xg, lk, podsUnreadable, series, gs);
+    return nodeDetailSection(raw, name, cap, alloc, podsOnNode, podsPend, own, xg, lk, podsUnreadable, series, gs, seeded);
   });
 }
 
-function nodeDetailSection(raw, name, cap, alloc, podsOnNode, loading, own, xg, lk, podsUnreadable, series, gs) {
+const SEEDED_NOTE = ' (from an earlier pod list; refreshing…)';
+
+function nodeDetailSection(raw, name, cap, alloc, podsOnNode, loading, own, xg, lk, podsUnreadable, series, gs, seeded) {
   const allocatable = parseInt(alloc[AMD_GPU_RESOURCE] || '0', 10) || 0;
   let inUse = 0;
   for (let i = 0; i < podsOnNode.length; i++) {
@@ -91,7 +95,7 @@ function nodeDetailSection(raw, name, cap, alloc, podsOnNode, loading, own, xg, 
   const phys = getNodePhysicalGpuCount(raw);
   if (count > 0) rows.push(row('HBM', formatBytes(phys * MI355X.hbmBytes)));
   if (allocatable > 0 && !podsUnreadable) {
-    rows.push(row('GPU Allocation', status(pctToStatus(p), inUse + '/' + allocatable + ' (' + p + '%)')));
+    rows.push(row('GPU Allocation', status(pctToStatus(p), inUse + '/' + allocatable + ' (' + p + '%)' + (seeded ? SEEDED_NOTE : ''))));
   }
   // With the pod list unreadable (RBAC) the node's pods are unknown, not
   // absent: say so rather than "None" or an endless "Loading…".
@@ -99,10 +103,10 @@ function nodeDetailSection(raw, name, cap, alloc, podsOnNode, loading, own, xg, 
     row(
       'GPU Workload Pods',
       podsOnNode.length > 0
-        ? podsOnNode.map(podName).join(', ')
+        ? podsOnNode.map(podName).join(', ') + (seeded ? SEEDED_NOTE : '')
         : podsUnreadable
           ? status('warning', 'Unavailable — the pod list could not be read')
-          : loading ? 'Loading…' : 'None'
+          : loading ? 'Loading…' : seeded ? 'None' + SEEDED_NOTE : 'None'
     )
   );
   let blocks = [kv(rows)];

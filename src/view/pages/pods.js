@@ -221,6 +221,8 @@ function podsItems(ctx, now, assign, pg, sort) {
  * the list, which then replaces these rows. Null when the answer names no
  * owner (or has not come).
  */
+const HOLDS_GPUS = 'Holds GPUs';
+
 export function podsPreview(metrics) {
   if (!metrics || !metrics.gpus) return null;
   const assign = podGpuAssignments(metrics);
@@ -241,7 +243,9 @@ export function podsPreview(metrics) {
       const slash = k.indexOf('/');
       const nodes = [];
       for (let i = 0; i < gs.length; i++) if (nodes.indexOf(gs[i].nodeName) < 0) nodes.push(gs[i].nodeName);
-      return [k.slice(slash + 1), k.slice(0, slash), nodes.join(', '), status('success', 'Running'),
+      // The exporter says the pod holds GPUs, not its phase: devices are bound at
+      // admission, so a pod still in ContainerCreating (Pending) is attributed too.
+      return [k.slice(slash + 1), k.slice(0, slash), nodes.join(', '), HOLDS_GPUS,
         gs.length + ' GPU' + (gs.length === 1 ? '' : 's') + ' held', assignmentTexts(gs).assigned, assignmentTexts(gs).power, '—', '—'];
     });
     return [

@@ -96,6 +96,14 @@ describe('podsPreview / podsView with the pod list pending', () => {
     expect(html).not.toContain('Loading GPU pod data...');
   });
 
+  it('the Phase cell says what the exporter knows (the pod holds GPUs), not Running', () => {
+    // Devices are bound at admission: a pod in ContainerCreating (Pending) is attributed too.
+    const vm = podsView(PENDING, { metrics: metrics([g('ml', 'starting', 'n1', 0, 0)]) });
+    const t = vm.items[1].blocks[0];
+    expect(t.rows[0][t.columns.indexOf('Phase')]).toBe('Holds GPUs');
+    expect(renderPage(vm)).not.toContain('Running');
+  });
+
   it('large cluster: the ranked pods in power order, out of every pod holding a GPU', () => {
     const m = metrics([g('ml', 'low', 'n1', 0, 100), g('ml', 'high', 'n2', 0, 700)],
       { per: 25, count: 4000, order: ['ml/high', 'ml/low'], watts: { 'ml/high': 700, 'ml/low': 100 } });

@@ -436,7 +436,8 @@ describe('shared: useNodePods, the cold Node detail read (' + tier + ')', () => 
     return function S() {
       const np = c.useNodePods(node);
       const r = np[0];
-      return h('div', null, np[1], r.loading ? 'loading' : r.podsState + ':' + r.gpuPods.map((p) => p.metadata.name).join(','));
+      return h('div', null, np[1], r.loading ? 'loading'
+        : r.podsState + ':' + r.gpuPods.map((p) => p.metadata.name).join(',') + (r.podsSeeded ? ' (seeded)' : ''));
     };
   }
 
@@ -481,7 +482,8 @@ describe('shared: useNodePods, the cold Node detail read (' + tier + ')', () => 
     lib.lists.Pod = [null, null];
     const S = Section(c, 'n1');
     const r = render(h(S));
-    expect(r.text()).toBe('ready:old');
+    // the store's list can be of any age: the context says these pods are seeded, not current
+    expect(r.text()).toBe('ready:old (seeded)');
     lib.lists.Pod = [[makeGpuPod('new', { node: 'n1' })], null];
     r.rerender(h(S));
     await r.settle();

@@ -320,6 +320,44 @@ def test_rule_refreshes_wait_for_a_lull(monkeypatch):
         assert fc.rule_evals == 2
 
 
+def test_a_failed_rule_refresh_is_retried_and_an_unstamped_answer_still_refreshes(monkeypatch):
+    """A background refresh that raises (its future has no one awaiting it) leaves the query schedulable: the next
+    tick evaluates it again. With no input stamp (series sampled at mixed intervals) the answer counts as changed, so
+    the age limits still refresh it."""
+    from headlamp_intel_gpu_plugin_amd.sim import apiserver
+
+    monkeypatch.setattr(apiserver, "RULE_EVAL_S", 0.0)
+    monkeypatch.setattr(apiserver, "RULE_IDLE_S", 0.0)
+    fc = make_fake(1, source="amd-exporter", latency_ms=0, rules=True)
+    clock = [fc.now()]
+    fc.now = lambda: clock[0]
+    real = apiserver.promql.query
+    calls = []
+
+    def flaky(db, q, t):
+        calls.append(q)
+        if len(calls) == 2:
+            raise RuntimeError("evaluation failed once")
+        return real(db, q, t)
+
+    monkeypatch.setattr(apiserver.promql, "query", flaky)
+    q = PROM + "query?query=" + urllib.parse.quote("max(gpu_power_usage)")
+    with ServerThread(fc) as s:
+        assert get(s, q)[1]["status"] == "success"
+        clock[0] += 60.0
+        deadline = time.time() + 10
+        while fc.rule_evals < 2 and time.time() < deadline:
+            time.sleep(0.05)
+        assert len(calls) >= 3 and fc.rule_evals == 2  # the failure, then the retry
+        assert not fc.refreshing or fc.refreshing == {urllib.parse.unquote(q.split("query=")[1])}
+        monkeypatch.setattr(apiserver.promql, "cache_stamp", lambda db, t: None)
+        before = fc.rule_evals
+        deadline = time.time() + 10
+        while fc.rule_evals == before and time.time() < deadline:  # clock unchanged: only the missing stamp
+            time.sleep(0.05)
+        assert fc.rule_evals > before
+
+
 def test_priority_pool_runs_client_work_before_queued_rule_refreshes():
     """The fake Prometheus's one evaluation thread takes a client request (priority 0) before rule refreshes
     (priority 1) that were queued earlier; equal priorities keep their order."""
