@@ -388,6 +388,13 @@ def _fmt(v: float) -> str:
     return r[:-2] if r.endswith(".0") else r
 
 
+def _fmt_ts(t: float) -> str:
+    """A sample timestamp as Prometheus's JSON writes it: seconds, then the milliseconds (3 digits) unless zero."""
+    ms = int(round(float(t) * 1000.0))
+    sec, frac = divmod(ms, 1000)
+    return f"{sec}.{frac:03d}" if frac else str(sec)
+
+
 class RawJSON(str):
     """A pre-encoded JSON response body (served as-is by the fake apiserver)."""
 
@@ -430,7 +437,7 @@ def query(db: TSDB, q: str, t: float):
 
 
 def _vector_body(rows, t: float) -> "RawJSON":
-    ts = repr(float(t))
+    ts = _fmt_ts(t)
     parts = ['{"metric":' + lj + ',"value":[' + ts + ',"' + fv + '"]}' for lj, fv in rows]
     return RawJSON('{"status":"success","data":{"resultType":"vector","result":[' + ",".join(parts) + "]}}")
 
@@ -476,7 +483,7 @@ def query_range(db: TSDB, q: str, start: float, end: float, step: float):
                 typ, val = ev.instant(node, t)
                 if typ == "scalar":
                     val = [({}, val)]
-                tsr = repr(float(t))
+                tsr = _fmt_ts(t)
                 rows = [(tuple(sorted(labels.items())), labels, "[" + tsr + ',"' + _fmt(v) + '"]') for labels, v in val]
                 steps[t] = rows
             for k, labels, cell in rows:

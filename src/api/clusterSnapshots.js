@@ -169,7 +169,7 @@ export function createClusterSnapshots(client, state) {
       return client.combined(base, q).then(function (res) {
         if (!res.ok) return UNREACHABLE;
         st.failures = 0;
-        const j = joinExporterResults(res.rows);
+        const j = joinExporterResults(res.rows, key);
         if (probing) {
           if (j.gpus.length || sizeFromRows(res.rows.__agg, 'gpu_nodes') > 0) state.source = 'amd-exporter';
           else if (sizeFromRows(res.rows.__agg, 'hwmon') > 0) {

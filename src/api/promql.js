@@ -9,6 +9,7 @@
  * cluster totals and size guards Prometheus evaluates in the same request.
  */
 
+import { MI355X } from './k8sCore.js';
 import {
   EXPORTER_JOIN_LABELS,
   EXPORTER_LEAN_LABELS,
@@ -214,17 +215,56 @@ export function summaryQuery() {
     ' or label_replace(count by (__name__) (count by (__name__, hostname) ({__name__="' + E.power + '"})), "agg", "nodes", "", "")';
 }
 
+/** Labels of the one-node query's per-GPU rows: `hostname` is its matcher (the client puts it back), `instance` unread. */
+export const NODE_GAUGE_LABELS = ['__name__', 'gpu_id', 'pod', 'namespace'];
+
 /**
  * The exporter query scoped to ONE node (`hostname` label = Kubernetes node
  * name, the same key the joins and views use): what the native Node / Pod
- * detail pages ask for, O(GPUs per node) series whatever the cluster size.
+ * detail pages ask for, O(GPUs per node) series whatever the cluster size,
+ * shaped so each row carries only what the page reads (ADR 006):
+ *   * per-GPU gauges projected onto NODE_GAUGE_LABELS;
+ *   * xGMI throughput placed on its peer by Prometheus — the stock
+ *     exporter's xgmi_neighbor_<k>_tx_throughput joined on the link series'
+ *     `neighbor` (this repo's amdgpu-exporter), or a row's own peer_gpu_id —
+ *     and, per GPU, the sum of what no series places (the client's
+ *     topology.js placeThroughput rules, evaluated where the rows are);
+ *   * with `withStatic`, the link topology as a count of one-hop links per
+ *     GPU, plus the link rows of any GPU that does not have the full MI355X
+ *     mesh of MI355X.xgmiLinksPerGpu (telemetry.js expands the count).
  */
 export function exporterNodeQuery(nodeName, withStatic) {
-  const names = exporterNames(withStatic);
-  // Every row matches the hostname matcher: the live-only query needs no fallback keys.
-  const labels = withStatic === false ? EXPORTER_LEAN_LABELS : EXPORTER_JOIN_LABELS;
-  return 'max by (' + labels.join(', ') + ') ({__name__=~"' + names.join('|') + '", hostname="' +
-    promString(nodeName) + '"})';
+  const E = SERIES.exporter;
+  const S = SERIES.nodeShaped;
+  const host = 'hostname="' + promString(nodeName) + '"';
+  const names = exporterNames(withStatic, 'gauges').filter(function (n) { return n !== E.linkHops; });
+  const hops = E.linkHops + '{' + host + '}';
+  const xgmi = '{__name__=~"' + E.xgmiRe + '", ' + host;
+  const byNeighbor = 'label_replace(' + xgmi + ', peer_gpu_id=""}, "neighbor", "$1", "__name__", "xgmi_neighbor_([0-9]+)_tx_throughput")';
+  // one link row per (gpu_id, neighbor): a bad duplicate cannot turn the join many-to-many
+  const pins = 'topk by (gpu_id, neighbor) (1, max by (gpu_id, neighbor, peer_gpu_id) (' + hops + '))';
+  // `or` keeps a right-hand row only when no left-hand row has its labels
+  // other than __name__: a GPU's total and link count would collide with its
+  // gauges ({gpu_id}), a non-mesh link row with its placed throughput
+  // ({gpu_id, peer_gpu_id}) — an `xgmi` label tells them apart.
+  function named(expr, name, tag) {
+    const e = 'label_replace(' + expr + ', "__name__", "' + name + '", "", "")';
+    return tag ? 'label_replace(' + e + ', "xgmi", "' + tag + '", "", "")' : e;
+  }
+  const parts = [
+    'max by (' + NODE_GAUGE_LABELS.join(', ') + ') ({__name__=~"' + names.join('|') + '", ' + host + '})',
+    named('max by (gpu_id, peer_gpu_id) (' + byNeighbor + ' * on (gpu_id, neighbor) group_left (peer_gpu_id) (0 * ' + pins + ' + 1))',
+      S.xgmiLink),
+    named('max by (gpu_id, peer_gpu_id) (' + xgmi + ', peer_gpu_id!=""})', S.xgmiLink),
+    named('sum by (gpu_id) (max by (gpu_id, neighbor) (' + byNeighbor + ' unless on (gpu_id, neighbor) ' + pins + '))', S.xgmiGpu, 'gpu'),
+  ];
+  if (withStatic !== false) {
+    const oneHop = 'count by (gpu_id) (max by (gpu_id, peer_gpu_id) (' + hops + ') == 1)';
+    parts.push(named(oneHop, S.oneHopLinks, '1hop'));
+    parts.push('label_replace(max by (__name__, gpu_id, peer_gpu_id) (' + hops + '), "xgmi", "hops", "", "") unless on (gpu_id) (' + oneHop +
+      ' == ' + MI355X.xgmiLinksPerGpu + ')');
+  }
+  return parts.join(' or ');
 }
 
 /**

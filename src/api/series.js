@@ -39,6 +39,15 @@ export const SERIES = {
     xgmiRe: 'xgmi_neighbor_[0-6]_tx_throughput', // bytes/s per neighbour
     linkHops: 'gpu_xgmi_link_hops', // measured link topology (this repo's native amdgpu-exporter)
   },
+  // Rows the ONE-node query (promql.js exporterNodeQuery) shapes server-side:
+  // xGMI throughput placed on its peer, each GPU's unplaced total, and the
+  // count of one-hop xGMI links per GPU (recording-rule style names: they
+  // exist only in that answer, no exporter emits them).
+  nodeShaped: {
+    xgmiLink: 'amdgpu:xgmi_link_tx', // bytes/s on link gpu_id → peer_gpu_id
+    xgmiGpu: 'amdgpu:xgmi_gpu_tx', // bytes/s of gpu_id over the links no series pins to a peer
+    oneHopLinks: 'amdgpu:xgmi_1hop_links', // one-hop xGMI links of gpu_id
+  },
   exporterVramUnitBytes: 1024 * 1024,
   nodeExporter: {
     chips: 'node_hwmon_chip_names{chip_name="amdgpu"}',

@@ -79,14 +79,21 @@ function byNodeGpu(a, b) {
 
 /**
  * Join AMD Device Metrics Exporter instant vectors into per-GPU telemetry.
- * Keyed by (hostname, gpu_id). Exported for direct unit tests.
+ * Keyed by (hostname, gpu_id). `nodeName`: the node a one-node answer
+ * (promql.js exporterNodeQuery) is about — its rows leave out `hostname`, the
+ * query's matcher. Exported for direct unit tests.
  */
-export function joinExporterResults(r) {
+export function joinExporterResults(r, nodeName) {
   const E = SERIES.exporter;
+  const S = SERIES.nodeShaped;
+  const fallback = typeof nodeName === 'string' ? nodeName : '';
   const map = {};
+  function nodeOf(m) {
+    return labelStr(m.hostname) || labelStr(m.node) || labelStr(m.instance) || fallback;
+  }
   function slot(m) {
     // Label values are strings; anything else in a malformed answer is ignored.
-    const node = labelStr(m.hostname) || labelStr(m.node) || labelStr(m.instance);
+    const node = nodeOf(m);
     const gpu = m.gpu_id !== undefined ? String(m.gpu_id) : '0';
     const k = node + '\u0000' + gpu;
     if (!map[k]) map[k] = emptyGpu(node, gpu, m.instance || '');
@@ -150,12 +157,36 @@ export function joinExporterResults(r) {
       if (!isFinite(src)) continue;
       const peer = typeof m.peer_gpu_id === 'string' && m.peer_gpu_id !== '' ? parseInt(m.peer_gpu_id, 10) : NaN;
       if (peer === src) continue;
-      const node = labelStr(m.hostname) || labelStr(m.instance);
+      const node = labelStr(m.hostname) || labelStr(m.instance) || fallback;
       if (!xgmi[node]) xgmi[node] = {};
       const v = num(xr[i].value[1]);
       if (v !== null) xgmi[node][isFinite(peer) ? src + '-' + peer : src + '>' + mm[1]] = v / 1e9;
     }
   }
+  // The one-node answer's rows placed by Prometheus: on a link ("src-dst"),
+  // or a GPU's total over the links nothing places ("src>*": counted towards
+  // the GPU alone, topology.js placeThroughput).
+  function shaped(list, keyOf) {
+    if (!Array.isArray(list)) return;
+    for (let i = 0; i < list.length; i++) {
+      if (!isRow(list[i])) continue;
+      const m = list[i].metric;
+      const k = keyOf(m);
+      const v = num(list[i].value[1]);
+      if (k === null || v === null) continue;
+      const node = nodeOf(m);
+      (xgmi[node] || (xgmi[node] = {}))[k] = v / 1e9;
+    }
+  }
+  shaped(r[S.xgmiLink], function (m) {
+    const a = parseInt(m.gpu_id, 10);
+    const b = parseInt(m.peer_gpu_id, 10);
+    return isFinite(a) && isFinite(b) && a !== b ? a + '-' + b : null;
+  });
+  shaped(r[S.xgmiGpu], function (m) {
+    const a = parseInt(m.gpu_id, 10);
+    return isFinite(a) ? a + '>*' : null;
+  });
   // Measured topology: gpu_xgmi_link_hops{gpu_id, peer_gpu_id[, neighbor]} per
   // xGMI-connected pair; `neighbor`: the link's place in gpu_id's neighbour order.
   const links = {};
@@ -164,12 +195,27 @@ export function joinExporterResults(r) {
     for (let i = 0; i < lr.length; i++) {
       if (!isRow(lr[i])) continue;
       const m = lr[i].metric;
-      const node = labelStr(m.hostname) || labelStr(m.instance);
+      const node = labelStr(m.hostname) || labelStr(m.instance) || fallback;
       const v = num(lr[i].value[1]);
       if (v === null || m.gpu_id === undefined || m.peer_gpu_id === undefined) continue;
       if (!links[node]) links[node] = {};
       const nb = typeof m.neighbor === 'string' && /^\d+$/.test(m.neighbor) ? parseInt(m.neighbor, 10) : -1;
       links[node][m.gpu_id + '-' + m.peer_gpu_id] = nb >= 0 ? { type: 'XGMI', hops: v, neighbor: nb } : { type: 'XGMI', hops: v };
+    }
+  }
+  // A GPU with the full MI355X mesh arrives as its one-hop link count alone
+  // (exporterNodeQuery): every other GPU of the node at one hop.
+  const oh = r[S.oneHopLinks];
+  if (Array.isArray(oh)) {
+    const per = MI355X.xgmiLinksPerGpu;
+    for (let i = 0; i < oh.length; i++) {
+      if (!isRow(oh[i])) continue;
+      const m = oh[i].metric;
+      const a = parseInt(m.gpu_id, 10);
+      if (num(oh[i].value[1]) !== per || !(a >= 0 && a <= per)) continue;
+      const node = nodeOf(m);
+      const l = links[node] || (links[node] = {});
+      for (let b = 0; b <= per; b++) if (b !== a && !l[a + '-' + b]) l[a + '-' + b] = { type: 'XGMI', hops: 1 };
     }
   }
   return { gpus: gpus, xgmi: xgmi, links: links };

@@ -5,7 +5,7 @@
  * range queries.
  */
 import { createMetricsSource } from '../../src/api/metrics.js';
-import { exporterNodeQuery, exporterQuery, mergedQuery } from '../../src/api/promql.js';
+import { exporterNodeQuery, exporterQuery, mergedQuery, NODE_GAUGE_LABELS } from '../../src/api/promql.js';
 import {
   EXPORTER_JOIN_LABELS,
   EXPORTER_LEAN_LABELS,
@@ -288,9 +288,32 @@ describe('fetchGpuMetrics', () => {
     await src.fetchGpuMetrics();
     expect(/max by \(([^)]*)\)/.exec(decodeURIComponent(request.mock.calls[1][0]))[1]).toBe(EXPORTER_JOIN_LABELS.join(', '));
   });
-  it('scopes live-only node queries with the lean projection', () => {
-    expect(exporterNodeQuery('n0', false)).toContain('max by (' + EXPORTER_LEAN_LABELS.join(', ') + ')');
-    expect(exporterNodeQuery('n0', true)).toContain('max by (' + EXPORTER_JOIN_LABELS.join(', ') + ')');
+  it('projects one node\'s gauges onto what the detail pages read: no hostname (the matcher), no instance', () => {
+    [true, false].forEach((withStatic) => {
+      const q = exporterNodeQuery('n0', withStatic);
+      expect(q.indexOf('max by (' + NODE_GAUGE_LABELS.join(', ') + ') ({__name__=~"gpu_power_usage|')).toBe(0);
+      expect(q).not.toContain('max by (' + EXPORTER_JOIN_LABELS.join(', ') + ')');
+      expect(q).not.toContain('max by (' + EXPORTER_LEAN_LABELS.join(', ') + ')');
+      // xGMI throughput comes placed (or summed per GPU), never as per-neighbour rows
+      expect(q).toContain('"__name__", "' + SERIES.nodeShaped.xgmiLink + '"');
+      expect(q).toContain('"__name__", "' + SERIES.nodeShaped.xgmiGpu + '"');
+      // the topology only with the static series
+      expect(q.indexOf(SERIES.nodeShaped.oneHopLinks) >= 0).toBe(withStatic);
+    });
+    expect(NODE_GAUGE_LABELS).toEqual(['__name__', 'gpu_id', 'pod', 'namespace']);
+  });
+  it('one node\'s answer: gauges keyed by the asked node, throughput placed by the link series, the mesh from its counts', async () => {
+    const d = exporterData(['n0', 'n1']);
+    // n1 GPU 0's neighbour 0 is GPU 5 (this repo's exporter says so); the others have no link series
+    d.gpu_xgmi_link_hops = [vec({ __name__: 'gpu_xgmi_link_hops', hostname: 'n1', gpu_id: '0', peer_gpu_id: '5', neighbor: '0' }, 1)];
+    for (let p = 1; p < 8; p++) if (p !== 5) d.gpu_xgmi_link_hops.push(vec({ __name__: 'gpu_xgmi_link_hops', hostname: 'n1', gpu_id: '0', peer_gpu_id: String(p), neighbor: String(p) }, 1));
+    const m = await createMetricsSource({ request: prom({ data: d }) }).fetchNodeMetrics('n1');
+    expect(m.gpus.map((g) => g.nodeName)).toEqual(Array(8).fill('n1'));
+    expect(m.xgmi.n1['0-5']).toBe(50);
+    expect(m.xgmi.n1['3>*']).toBe(50); // GPU 3: no link series, its total only
+    expect(m.xgmi.n1['0>*']).toBeUndefined();
+    // GPU 0 has its 7 one-hop links: counted by Prometheus, expanded here
+    expect(Object.keys(m.links.n1).sort()).toEqual(['0-1', '0-2', '0-3', '0-4', '0-5', '0-6', '0-7']);
   });
   it('refetches the static series when a GPU appears that the copy does not know', async () => {
     const E = SERIES.exporter;

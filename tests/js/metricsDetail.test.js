@@ -25,6 +25,10 @@ import {
 } from '../../src/api/telemetry.js';
 
 import { exporterData, flatten, ok, prom, vec } from './promFake.js';
+import { nodeDetailView } from '../../src/view/pages/details.js';
+import { clearViewMemo } from '../../src/view/pages/common.js';
+import { renderSection } from '../../src/view/html.js';
+import { makeContext, makeGpuNode, makeGpuPod, NOW } from './fixtures.js';
 
 describe('fetchPodSeries (Pod detail power history)', () => {
   it('asks for one pod\'s power, summed per step, with escaped matchers', () => {
@@ -326,3 +330,48 @@ describe('stringLabels: label values are strings or absent', () => {
     expect([...hosts].every((x) => typeof x === 'string')).toBe(true);
   });
 });
+
+describe('the one-node answer draws the Node detail section the cluster-wide answer draws', () => {
+  /** n1's 8 GPUs on the full mesh, neighbour k of GPU g = GPU (g + 1 + k) % 8, each link a distinct throughput. */
+  function meshData(withLinks) {
+    const d = exporterData(['n0', 'n1']);
+    d.__xgmi = [];
+    d.gpu_xgmi_link_hops = [];
+    ['n0', 'n1'].forEach((h) => {
+      for (let g = 0; g < 8; g++) {
+        for (let k = 0; k < 7; k++) {
+          const peer = (g + 1 + k) % 8;
+          d.__xgmi.push(vec({ __name__: 'xgmi_neighbor_' + k + '_tx_throughput', hostname: h, gpu_id: String(g), instance: h + ':5000' },
+            (10 * g + k + 1) * 1e9));
+          if (withLinks) {
+            d.gpu_xgmi_link_hops.push(vec({ __name__: 'gpu_xgmi_link_hops', hostname: h, gpu_id: String(g), peer_gpu_id: String(peer),
+              neighbor: String(k) }, 1));
+          }
+        }
+      }
+    });
+    return d;
+  }
+
+  [true, false].forEach((withLinks) => {
+    it((withLinks ? 'links pin the neighbours: throughput per link' : 'no link series: throughput per GPU') + ', the same HTML', async () => {
+      const d = meshData(withLinks);
+      const node = makeGpuNode('n1');
+      const ctx = makeContext({ nodes: [node], pods: [makeGpuPod('train-0', { node: 'n1', gpus: 2 })] });
+      const scoped = await createMetricsSource({ request: prom({ data: d }) }).fetchNodeMetrics('n1');
+      const wide = nodeSlice(await createMetricsSource({ request: prom({ data: d }) }).fetchGpuMetrics(), 'n1');
+      clearViewMemo();
+      const a = renderSection(nodeDetailView(node, ctx, { now: NOW, metrics: scoped }));
+      clearViewMemo();
+      const b = renderSection(nodeDetailView(node, ctx, { now: NOW, metrics: wide }));
+      expect(a).toBe(b);
+      expect(a).toContain(withLinks ? 'data-throughput="measured"' : 'data-throughput="per-gpu"');
+      expect(a).toContain(withLinks ? 'data-topology="measured"' : 'data-topology="assumed"');
+      // GPU 2's neighbour 3 is GPU 6: 24 GB/s on that link when pinned; GPU 2's total is 21 + … + 27 = 168
+      expect(a).toContain('\u03a3 168.0 GB/s');
+      if (withLinks) expect(Object.keys(scoped.xgmi.n1)).toContain('2-6');
+      if (withLinks) expect(scoped.xgmi.n1['2-6']).toBe(24);
+    });
+  });
+});
+

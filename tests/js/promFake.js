@@ -6,6 +6,7 @@
  * rows built by `exporterData`.
  */
 import { PROMETHEUS_SERVICES, SERIES, servicePath } from '../../src/api/series.js';
+import { MI355X } from '../../src/api/k8sCore.js';
 
 export const BASE0 = servicePath(PROMETHEUS_SERVICES[0]);
 export const BASE1 = servicePath(PROMETHEUS_SERVICES[1]);
@@ -68,11 +69,58 @@ export function flatten(d) {
  * pod-owner query, and the summary aggregates (label_replace(sum|count by
  * (__name__) …, "agg", …)). Unknown shapes answer no rows.
  */
+/**
+ * promql.js exporterNodeQuery's server-shaped xGMI terms, evaluated the way
+ * Prometheus would (tests/test_promql.py checks the real PromQL against the
+ * fake Prometheus of the Python harness): throughput placed by the link
+ * series' `neighbor` or a row's own peer_gpu_id, each GPU's unplaced sum, the
+ * one-hop link count per GPU, the link rows of a GPU off the full mesh.
+ * Null for any other term.
+ */
+function nodeShaped(q, rows) {
+  const S = SERIES.nodeShaped;
+  const host = /hostname="((?:[^"\\]|\\.)*)"/.exec(q);
+  if (!host || q.indexOf('gpu_xgmi_link_hops') < 0 && q.indexOf('xgmi_neighbor_') < 0) return null;
+  const h = host[1];
+  const mine = rows.filter((r) => r.metric.hostname === h);
+  const links = mine.filter((r) => r.metric.__name__ === 'gpu_xgmi_link_hops');
+  const pin = {};
+  links.forEach((r) => { if (r.metric.neighbor !== undefined) pin[r.metric.gpu_id + '>' + r.metric.neighbor] = r.metric.peer_gpu_id; });
+  const tx = [];
+  mine.forEach((r) => {
+    const m = /^xgmi_neighbor_(\d+)_tx_throughput$/.exec(r.metric.__name__ || '');
+    if (m) tx.push({ gpu: r.metric.gpu_id, k: m[1], peer: r.metric.peer_gpu_id, v: parseFloat(r.value[1]) });
+  });
+  if (q.indexOf('"__name__", "' + S.xgmiLink + '"') >= 0) {
+    const own = q.indexOf('peer_gpu_id!=""') >= 0;
+    return tx.filter((x) => (own ? !!x.peer : !x.peer && pin[x.gpu + '>' + x.k] !== undefined))
+      .map((x) => vec({ __name__: S.xgmiLink, gpu_id: x.gpu, peer_gpu_id: own ? x.peer : pin[x.gpu + '>' + x.k] }, x.v));
+  }
+  if (q.indexOf('"__name__", "' + S.xgmiGpu + '"') >= 0) {
+    const sum = {};
+    tx.forEach((x) => { if (!x.peer && pin[x.gpu + '>' + x.k] === undefined) sum[x.gpu] = (sum[x.gpu] || 0) + x.v; });
+    return Object.keys(sum).map((g) => vec({ __name__: S.xgmiGpu, gpu_id: g, xgmi: 'gpu' }, sum[g]));
+  }
+  const oneHop = {};
+  links.forEach((r) => { if (parseFloat(r.value[1]) === 1) oneHop[r.metric.gpu_id] = (oneHop[r.metric.gpu_id] || 0) + 1; });
+  if (q.indexOf('"__name__", "' + S.oneHopLinks + '"') >= 0) {
+    return Object.keys(oneHop).map((g) => vec({ __name__: S.oneHopLinks, gpu_id: g, xgmi: '1hop' }, oneHop[g]));
+  }
+  if (q.indexOf('label_replace(max by (__name__, gpu_id, peer_gpu_id) (gpu_xgmi_link_hops{') === 0) {
+    return links.filter((r) => oneHop[r.metric.gpu_id] !== MI355X.xgmiLinksPerGpu)
+      .map((r) => vec({ __name__: 'gpu_xgmi_link_hops', gpu_id: r.metric.gpu_id, peer_gpu_id: r.metric.peer_gpu_id, xgmi: 'hops' },
+        parseFloat(r.value[1])));
+  }
+  return null;
+}
+
 function term(q, rows) {
   // `a or b` at the top level: every term's rows; `(q)`: q.
   const alts = splitOr(q);
   if (alts.length > 1) return [].concat.apply([], alts.map((t) => term(t, rows)));
   if (q[0] === '(' && closing(q, 0) === q.length - 1) return term(q.slice(1, -1), rows);
+  const shaped = nodeShaped(q, rows);
+  if (shaped) return shaped;
   // `max by (…) (a or b)`: each alternative under the same projection (the fake does not project).
   const mb = /^max by \([^)]*\) \(/.exec(q);
   if (mb && closing(q, mb[0].length - 1) === q.length - 1) {

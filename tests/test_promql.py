@@ -632,3 +632,13 @@ def test_count_and_sum_of_the_same_selector_do_not_share_partials():
     sel = '{__name__="gpu_power_usage", pod!=""}'
     assert [r["value"][1] for r in _vec(query(d, f"count by (pod) ({sel})", 100.0))] == ["3"]
     assert [r["value"][1] for r in _vec(query(d, f"sum by (pod) ({sel})", 100.0))] == ["600"]
+
+
+def test_sample_timestamps_are_written_as_prometheus_writes_them(db):
+    """Prometheus's JSON: seconds, then '.' and 3 millisecond digits unless the milliseconds are 0."""
+    assert '"value":[1000.5,' not in query(db, "gpu_power_usage", 1000.5)
+    assert '"value":[1000.500,' in query(db, "gpu_power_usage", 1000.5)
+    assert '"value":[1000,' in query(db, "gpu_power_usage", 1000.0)
+    assert '"value":[1000.042,' in query(db, "gpu_power_usage", 1000.0421)
+    body = json.loads(query_range(db, "gpu_power_usage", 1000.0, 1030.0, 15.0))
+    assert [p[0] for p in body["data"]["result"][0]["values"]] == [1000, 1015, 1030]
