@@ -8,14 +8,44 @@
  * including the view-model built from a cold memo, re-render on the same
  * watch event (a new snapshot of the same data), first page of each pager.
  * Driven by tools/render_compare.py (driver command 'refRender').
+ *
+ * The reference's pages run in bench/refWorker.cjs's realm, in the process
+ * ./refIsolated.js starts without network or writes; this process only sends
+ * it text and reads back its timings (ADR 014). Both realms mount the same
+ * calibration tree, so the two environments' React speed is on record.
  */
 import { createMetricsSource } from '../src/api/metrics.js';
 import { clearViewMemo } from '../src/view/pages/common.js';
-import { loadReferencePages, referenceContext, toGpuMetrics, toIntelNode, toIntelPod } from './referenceRender.js';
+import { referenceData } from './referenceRender.js';
+import { referenceWorker } from './refIsolated.js';
 import { amdSchedule } from './schedules.js';
 import { makeRequest, ms, stats } from './common.js';
 import { PAGES, pageVm } from './pageRender.js';
 import { mountCycle, realReact } from './reactMount.js';
+
+/** Rows of the calibration table both realms mount (bench/refWorker.cjs `calibrate`). */
+const CALIBRATION_ROWS = 100;
+
+/** The calibration tree mounted in this realm, as the worker's realm does (ms per mount). */
+function calibrateHere(R, reps) {
+  const h = R.React.createElement;
+  const times = [];
+  let elements = 0;
+  for (let i = 0; i < reps; i++) {
+    const t0 = process.hrtime();
+    const trs = [];
+    for (let k = 0; k < CALIBRATION_ROWS; k++) trs.push(h('tr', { key: k }, h('td', null, 'node-' + k), h('td', null, String(k * 7))));
+    const c = document.createElement('div');
+    document.body.appendChild(c);
+    const root = R.ReactDOM.createRoot(c);
+    R.ReactDOM.flushSync(function () { root.render(h('table', null, h('tbody', null, trs))); });
+    elements = c.querySelectorAll('*').length;
+    R.ReactDOM.flushSync(function () { root.unmount(); });
+    document.body.removeChild(c);
+    times.push(ms(process.hrtime(t0)));
+  }
+  return { times: times, elements: elements };
+}
 
 /** The header each reference page shows once its data is in (its Loader gone). */
 const REFERENCE_TITLES = {
@@ -29,7 +59,9 @@ export const NO_CODEGEN_FLAG = '--disallow-code-generation-from-strings';
 /**
  * Refuses unless the caller opted in (`allowReferenceExec`) and this process
  * runs with NO_CODEGEN_FLAG: the reference's sources are untrusted public
- * content, run only in bench/tsx.js's sandbox under that flag (ADR 014).
+ * content. This process runs none of them; it starts the worker that does,
+ * without network or writes, in a realm of their own (./refIsolated.js,
+ * ./refWorker.cjs; ADR 014).
  */
 export function assertReferenceSandbox(c) {
   if (!c || c.allowReferenceExec !== true) {
@@ -65,7 +97,15 @@ function summary(x) {
 export async function compareRenders(url, c) {
   assertReferenceSandbox(c);
   const R = await realReact(c.umdDir);
-  const ref = loadReferencePages(c.referenceDir, R.React, R.CC);
+  const ref = await referenceWorker(c.referenceDir, c.umdDir);
+  try {
+    return await measure(url, c, R, ref);
+  } finally {
+    await ref.close();
+  }
+}
+
+async function measure(url, c, R, ref) {
   const reps = Math.max(15, c.reps || 15);
   const warm = c.warm === undefined ? 5 : c.warm;
   // (no 2 s request limit: the fake Prometheus evaluates 8,000 GPUs in Python on this host)
@@ -78,35 +118,25 @@ export async function compareRenders(url, c) {
   if (!every) throw new Error('compareRenders: no telemetry');
   const lists = await Promise.all([request('/api/v1/nodes'), request('/api/v1/pods')]);
   const snap = s.ctx();
-  const t0 = process.hrtime();
-  const refCtx = referenceContext(ref.k8s, {
-    nodes: lists[0].items, pods: lists[1].items, deviceConfigs: snap.deviceConfigs, pluginPods: snap.pluginPods,
+  const refInfo = await ref.call('setData', {
+    json: referenceData({ nodes: lists[0].items, pods: lists[1].items, deviceConfigs: snap.deviceConfigs, pluginPods: snap.pluginPods }, every),
   });
-  const deriveMs = ms(process.hrtime(t0));
   // the provider's useMemo filters, per watch event (the lists already in the reference's shapes)
-  const intelNodes = lists[0].items.map(toIntelNode);
-  const intelPods = lists[1].items.map(toIntelPod);
-  const d0 = process.hrtime();
-  ref.k8s.filterIntelGpuNodes(intelNodes);
-  ref.k8s.filterGpuRequestingPods(intelPods);
-  const filterMs = ms(process.hrtime(d0));
-  const refMetrics = toGpuMetrics(every);
-  const out = { pages: {}, referenceProviderFilterMs: filterMs, referenceContextBuildMs: deriveMs,
-    gpuNodes: refCtx.gpuNodes.length, gpuPods: refCtx.gpuPods.length, chips: refMetrics.chips.length, reps: reps, warm: warm };
-  const refEvent = function () {
-    ref.setData(Object.assign({}, refCtx, {
-      gpuNodes: refCtx.gpuNodes.slice(), gpuPods: refCtx.gpuPods.slice(), pluginPods: refCtx.pluginPods.slice(),
-      devicePlugins: refCtx.devicePlugins.slice(),
-    }), refMetrics);
-  };
+  const filterMs = await ref.call('filter');
+  const calReps = Math.max(31, warm);
+  const calRef = await ref.call('calibrate', { rows: CALIBRATION_ROWS, reps: calReps });
+  const calHere = calibrateHere(R, calReps);
+  const out = { pages: {}, referenceProviderFilterMs: filterMs, referenceContextBuildMs: refInfo.contextBuildMs,
+    gpuNodes: refInfo.gpuNodes, gpuPods: refInfo.gpuPods, chips: refInfo.chips, reps: reps, warm: warm,
+    calibration: { rows: CALIBRATION_ROWS, elements: calHere.elements, referenceRealmMs: spread(calRef.times.slice(5)).p50,
+      driverRealmMs: spread(calHere.times.slice(5)).p50 } };
   for (let p = 0; p < PAGES.length; p++) {
     const page = PAGES[p];
     const mstatePage = page === 'metrics' ? s.pageMstate() : s.mstate();
     let ctx = snap;
     function referenceOnce() {
-      ref.setData(refCtx, refMetrics);
-      return mountCycle(R, function () { return R.React.createElement(ref.pages[page]); },
-        page === 'metrics' ? 'GPU Power Summary' : null, refEvent, 1, REFERENCE_TITLES[page]);
+      return ref.call('cycle', { page: page, waitText: page === 'metrics' ? 'GPU Power Summary' : null, mustShow: REFERENCE_TITLES[page] })
+        .then(function (r) { return { mounts: [r.mount], rerenders: [r.rerender], elements: r.elements }; });
     }
     // Mount from a cold view memo each time (the first page render of a session).
     function amdOnce() {

@@ -25,12 +25,15 @@
  * reference's own filterIntelGpuNodes / filterGpuRequestingPods, as its
  * provider does (IntelGpuDataContext.tsx:200-208).
  *
- * Only source files are read; nothing prebuilt from the reference is run.
+ * This module only reads and transforms text: the reference's code runs in
+ * bench/refWorker.cjs's realm, in the isolated process bench/refIsolated.js
+ * starts (ADR 014). Only source files are read; nothing prebuilt from the
+ * reference is run.
  */
 
 import fs from 'fs';
 import path from 'path';
-import { loadModules } from './tsx.js';
+import { transpile } from './tsx.js';
 
 export const REFERENCE_PAGES = {
   overview: 'components/OverviewPage.tsx',
@@ -140,71 +143,58 @@ export function toGpuMetrics(m) {
 }
 
 /**
- * Load the reference's page components against `React` (real), the
- * CommonComponents stand-ins and data stand-ins. Returns {pages, k8s, setData}.
+ * The reference's modules for the realm (bench/refWorker.cjs): k8s.ts,
+ * metrics.ts and the five pages read UNMODIFIED from `referenceDir` and
+ * transpiled here (./tsx.js: a pure text transform), with each import
+ * resolved to another of these files or to a stand-in the realm builds
+ * (React, the CommonComponents, the Headlamp library, the data context, the
+ * metrics client's fetch). → {modules: {id: body}, resolve: {id: {spec:
+ * {file} | {ext}}}, pages: {key: id}}
  */
-export function loadReferencePages(referenceDir, React, CommonComponents) {
+export function referenceModules(referenceDir) {
   const src = path.join(referenceDir, 'src');
-  const files = {};
   const ids = ['api/k8s.ts', 'api/metrics.ts'].concat(Object.keys(REFERENCE_PAGES).map(function (k) { return REFERENCE_PAGES[k]; }));
+  const files = {};
   for (let i = 0; i < ids.length; i++) files[ids[i]] = fs.readFileSync(path.join(src, ids[i]), 'utf8');
-  const data = { ctx: null, metrics: null };
-  const contextStandIn = {
-    useIntelGpuContext: function () {
-      if (!data.ctx) throw new Error('useIntelGpuContext must be used within an IntelGpuDataProvider');
-      return data.ctx;
-    },
-  };
-  const lib = { ApiProxy: { request: function () { return Promise.reject(new Error('no network in the render bench')); } } };
-  function resolver(metricsStandIn) {
-    return function (from, spec) {
-      if (spec === 'react') return React;
-      if (spec === '@kinvolk/headlamp-plugin/lib/CommonComponents') return CommonComponents;
-      if (spec === '@kinvolk/headlamp-plugin/lib') return lib;
-      if (spec === '../api/IntelGpuDataContext') return contextStandIn;
-      if (spec === '../api/metrics' && metricsStandIn) return metricsStandIn;
-      const base = path.posix.normalize(path.posix.join(path.posix.dirname(from), spec));
-      for (const ext of ['.ts', '.tsx']) if (files[base + ext] !== undefined) return base + ext;
-      throw new Error('referenceRender: cannot resolve ' + spec + ' from ' + from);
-    };
+  const modules = {};
+  const resolve = {};
+  for (let i = 0; i < ids.length; i++) {
+    const id = ids[i];
+    modules[id] = transpile(files[id]);
+    resolve[id] = {};
+    const re = /__import\("([^"]+)"/g;
+    let m;
+    while ((m = re.exec(modules[id]))) {
+      const spec = m[1];
+      if (REALM_EXTERNALS.indexOf(spec) >= 0) {
+        resolve[id][spec] = { ext: spec };
+        continue;
+      }
+      const base = path.posix.normalize(path.posix.join(path.posix.dirname(id), spec));
+      const hit = ['.ts', '.tsx'].map(function (e) { return base + e; }).filter(function (f) { return files[f] !== undefined; })[0];
+      if (!hit) throw new Error('referenceRender: cannot resolve ' + spec + ' from ' + id);
+      resolve[id][spec] = { file: hit };
+    }
   }
-  const k8s = loadModules(files, 'api/k8s.ts', resolver(null));
-  const realMetrics = loadModules(files, 'api/metrics.ts', resolver(null));
-  // fetchGpuMetrics answers from the synthetic cluster (as MetricsPage.test.tsx mocks it); the formatters are the reference's.
-  const metricsStandIn = Object.assign({}, realMetrics, {
-    fetchGpuMetrics: function () { return Promise.resolve(data.metrics); },
-  });
-  const pages = {};
-  for (const k in REFERENCE_PAGES) pages[k] = loadModules(files, REFERENCE_PAGES[k], resolver(metricsStandIn)).default;
-  return {
-    pages: pages,
-    k8s: k8s,
-    setData: function (ctx, metrics) {
-      data.ctx = ctx;
-      data.metrics = metrics;
-    },
-  };
+  return { modules: modules, resolve: resolve, pages: Object.assign({}, REFERENCE_PAGES) };
 }
 
+/** Imports the realm answers with its own stand-ins (bench/refWorker.cjs realmBench). */
+export const REALM_EXTERNALS = ['react', '@kinvolk/headlamp-plugin/lib/CommonComponents', '@kinvolk/headlamp-plugin/lib',
+  '../api/IntelGpuDataContext', '../api/metrics'];
+
 /**
- * The reference's context value for the synthetic cluster: what its provider
- * computes (IntelGpuDataContext.tsx:200-251) from the lists, the CRs and the
- * plugin pods, once loaded.
+ * The cluster as the reference's shapes, as JSON text for the realm: nodes,
+ * pods, CRs and plugin pods mapped onto the Intel model; telemetry as its
+ * GpuMetrics. The realm's own copy of the reference's filters makes the
+ * context value from it (IntelGpuDataContext.tsx:200-251).
  */
-export function referenceContext(k8s, lists) {
-  const nodes = lists.nodes.map(toIntelNode);
-  const pods = lists.pods.map(toIntelPod);
-  const devicePlugins = lists.deviceConfigs.map(toGpuDevicePlugin);
-  const pluginPods = lists.pluginPods.map(toIntelPluginPod);
-  return {
-    devicePlugins: devicePlugins,
-    pluginInstalled: devicePlugins.length > 0 || pluginPods.length > 0,
-    gpuNodes: k8s.filterIntelGpuNodes(nodes),
-    gpuPods: k8s.filterGpuRequestingPods(pods),
-    pluginPods: pluginPods,
-    crdAvailable: true,
-    loading: false,
-    error: null,
-    refresh: function () {},
-  };
+export function referenceData(lists, telemetry) {
+  return JSON.stringify({
+    nodes: lists.nodes.map(toIntelNode),
+    pods: lists.pods.map(toIntelPod),
+    devicePlugins: lists.deviceConfigs.map(toGpuDevicePlugin),
+    pluginPods: lists.pluginPods.map(toIntelPluginPod),
+    metrics: toGpuMetrics(telemetry),
+  });
 }

@@ -24,16 +24,12 @@
  * That is enough for the reference's 12 production files; it is not a
  * general TypeScript compiler and nothing shipped uses it.
  *
- * Modules are compiled with `vm.Script` into a context of their own with
- * string code generation and WebAssembly off (`loadModules`): the code sees
- * the language's built-ins and what its imports resolve to, and no
- * `process`, `require`, `import()`, timers or file system. Reference sources
- * are untrusted public content: they are loaded only by the opt-in render
- * comparison (tools/render_compare.py --allow-reference-exec), in a child
- * process started with --disallow-code-generation-from-strings, so that
- * no host function's constructor compiles code either (ADR 014).
+ * This file only transforms text. The transpiled modules run in
+ * bench/refWorker.cjs's realm, in the isolated process bench/refIsolated.js
+ * starts, and only for the opt-in render comparison
+ * (tools/render_compare.py --allow-reference-exec; ADR 014): reference
+ * sources are untrusted public content.
  */
-import vm from 'vm';
 import {
   KEYWORD_BEFORE_EXPR, PUNCT2, PUNCT3, blank, exprPosition, isClose, isIdPart, isIdStart, isOpen, matchBrace, matching, scanRegex,
   scanTemplate, sig, skipString, tokenize, typeArgsEnd, typeEnd,
@@ -377,41 +373,4 @@ function stripParams(toks, open) {
 /** The whole pipeline: TSX source → body of `function (__import, __exports) { … }`. */
 export function transpile(src) {
   return HELPERS + lowerModules(lowerOptional(stripTypes(transformJsx(src))));
-}
-
-/**
- * A fresh context for a module graph: the ECMAScript built-ins of its own
- * realm, nothing of Node's, and no code generation from strings (eval /
- * Function) inside it.
- */
-export function sandboxContext() {
-  return vm.createContext(Object.create(null), { name: 'tsx-sandbox', codeGeneration: { strings: false, wasm: false } });
-}
-
-/**
- * Load a graph of TSX / TS modules: `files` maps a module id to its source;
- * `resolve(fromId, spec)` returns a module id or an object (an external
- * module: React, a stand-in). Returns the export object of `entry`. Every
- * module runs in `context` (default: a fresh sandboxContext()).
- */
-export function loadModules(files, entry, resolve, context) {
-  const cache = {};
-  const ctx = context || sandboxContext();
-  function load(id) {
-    if (cache[id]) return cache[id];
-    if (!(id in files)) throw new Error('tsx: no module ' + id);
-    const exp = {};
-    cache[id] = exp;
-    const body = transpile(files[id]);
-    const script = new vm.Script('(function (__import, __exports) {"use strict";\n' + body + '\n})', { filename: 'tsx:' + id });
-    const fn = script.runInContext(ctx, { timeout: 10000 });
-    fn(function (spec, wantDefault) {
-      const r = resolve(id, spec);
-      const m = typeof r === 'string' ? load(r) : r;
-      if (!wantDefault) return m;
-      return m && m.default !== undefined ? m.default : m;
-    }, exp);
-    return exp;
-  }
-  return load(entry);
 }

@@ -5,10 +5,11 @@
                                    [--out profiles/r5_render_compare]
 
 OPT-IN: this runs the reference's page components, which are untrusted public content (ADR 014). Without
-``--allow-reference-exec`` it refuses. With it, bench/driver.js runs in a child process started with
-``--disallow-code-generation-from-strings`` and only PATH in its environment, and the reference's modules are
-compiled into bench/tsx.js's sandbox: a vm context of their own, with no ``process``, ``require``, ``import()``,
-timers, file system or network, and no code generation from strings there or through any host function.
+``--allow-reference-exec`` it refuses. With it, bench/driver.js (this plugin's pages) starts the process that runs the
+reference's (bench/refIsolated.js): no network, read-only mounts, no capabilities, no file it can open, V8's
+``--disallow-code-generation-from-strings``; inside it the reference's modules, React and the DOM stand-in are built
+from source text in a realm of their own (bench/refWorker.cjs), with no ``process``, ``require``, ``import()``,
+timers, file system or network, and no code generation from strings. It gets text and answers with numbers.
 
 Per page and size: ``--warm`` untimed mounts of each side, then ``--reps`` (at least 15) interleaved
 reference / new pairs, the order alternating; mount and re-render p50 with the interquartile range. ``--runs``
@@ -22,7 +23,9 @@ on the react@18.3.1 / react-dom@18.3.1 production UMD builds (bench/referenceRen
 Writes ``<out>.json`` and ``<out>.md``.
 
 The reference's sources are not in this repository and not on the GPU box, so this runs where they are (this
-container's CPU); the figures of both plugins come from the same process on the same host.
+container's CPU); the figures of both plugins come from the same host, each side's from its own process, the pairs
+interleaved. Both processes also mount one calibration tree (a 100-row table) on their own React, so the two
+environments' speed is on record next to the figures.
 """
 from __future__ import annotations
 
@@ -71,6 +74,11 @@ def pooled(runs: list) -> dict:
     """One size's result from several driver processes: each page's samples pooled, p50 / IQR recomputed."""
     out = {k: v for k, v in runs[0].items() if k != "pages"}
     out["runs"] = len(runs)
+    cal = [r["calibration"] for r in runs if "calibration" in r]
+    if cal:
+        out["calibration"] = {"rows": cal[0]["rows"], "elements": cal[0]["elements"],
+                              "referenceRealmMs": [c["referenceRealmMs"] for c in cal],
+                              "driverRealmMs": [c["driverRealmMs"] for c in cal]}
     out["pages"] = {}
     for page in runs[0]["pages"]:
         per = [r["pages"][page] for r in runs]
@@ -99,7 +107,8 @@ def verdict(a: dict, ref: dict) -> str:
 
 def table(rows) -> list:
     head = ["GPU nodes", "GPU pods"] + [f"{t}: elements ref → new; mount p50 [IQR] ref → new (ms); re-render p50 ref → new"
-                                        for _, t in PAGES] + ["Reference provider filter per watch event (ms)"]
+                                        for _, t in PAGES] + ["Reference provider filter per watch event (ms)",
+                                                              "Calibration tree mount, reference's realm / driver's (ms)"]
     md = ["| " + " | ".join(head) + " |", "|---:|---:|" + "---|" * (len(head) - 2)]
     for n, r in rows:
         cells = [str(n), str(r["gpuPods"])]
@@ -110,6 +119,8 @@ def table(rows) -> list:
             cells.append(f"{ref['elements']} → {a['elements']}; {ref['mountMs']:.2f} {iqr(ref)} → {a['mountMs']:.2f} {iqr(a)} "
                          f"{verdict(a, ref)}{split}; {ref['rerenderMs']:.2f} → {a['rerenderMs']:.2f}")
         cells.append(f"{r['referenceProviderFilterMs']:.1f}")
+        cal = r.get("calibration")
+        cells.append(" · ".join(f"{a:.2f} / {b:.2f}" for a, b in zip(cal["referenceRealmMs"], cal["driverRealmMs"])) if cal else "—")
         md.append("| " + " | ".join(cells) + " |")
     return md
 
@@ -123,11 +134,11 @@ def main() -> int:
     p.add_argument("--reference", default="/root/reference")
     p.add_argument("--out", default=os.path.join(ROOT, "profiles", "r5_render_compare"))
     p.add_argument("--allow-reference-exec", action="store_true",
-                   help="run the reference's page components (untrusted) in the sandboxed child process")
+                   help="run the reference's page components (untrusted) in the isolated worker process")
     args = p.parse_args()
     if not args.allow_reference_exec:
         raise SystemExit("render_compare runs the reference's sources (untrusted public content): "
-                         "pass --allow-reference-exec to run them in the sandboxed driver process (ADR 014)")
+                         "pass --allow-reference-exec to run them in the isolated worker process (ADR 014)")
     if not os.path.isdir(os.path.join(args.reference, "src", "components")):
         raise SystemExit(f"no reference sources under {args.reference}")
     rows = []
