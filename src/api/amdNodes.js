@@ -200,6 +200,18 @@ export function partitionsPerGpu(node) {
   return (cp && COMPUTE_PARTITIONS[String(cp).toUpperCase()]) || 1;
 }
 
+/**
+ * The node's partition mode as the Overview counts it, "SPX/NPS1" when
+ * unlabelled (the same labels getNodeGpuModel reads, without the rest of the
+ * model).
+ */
+export function partitionModeKey(node) {
+  const labels = labelsOf(node);
+  const cp = labels[LABEL_COMPUTE_PARTITION] || labellerValue(node, 'compute-partitioning-mode');
+  const mp = labels[LABEL_MEMORY_PARTITION] || labellerValue(node, 'memory-partitioning-mode');
+  return (cp ? String(cp).toUpperCase() : 'SPX') + '/' + (mp ? String(mp).toUpperCase() : 'NPS1');
+}
+
 /** MI355X boards on the node: devices ÷ partitions per board. */
 export function getNodePhysicalGpuCount(node) {
   const d = getNodeGpuCount(node);

@@ -17,11 +17,13 @@ import {
   getNodePartitionCount,
   isNodeReady,
   labellerValue,
+  partitionModeKey,
   partitionsPerGpu,
 } from './amdNodes.js';
 import { containerGpuEntries, getPodGpuCount, gpuContainers, gpuInitContainers, podPhase } from './amdPods.js';
 import { derivedCache } from './derivedCache.js';
 import { AMD_GPU_RESOURCE, formatBytes, formatGpuResourceName, get, MI355X, pct } from './k8sCore.js';
+import { SMALL_CLUSTER_NODES } from './series.js';
 
 // Per-object facts the index needs, cached on the (immutable) object: a
 // watch event that changes one pod re-derives that pod only.
@@ -30,26 +32,51 @@ const nodeFactCache = new WeakMap();
 const podFactCache = new WeakMap();
 
 /**
- * What a GPU node object says, derived once per object — when the index is
- * built, i.e. when the node list arrives, not when a page mounts: its GPU
- * accounting, readiness, GPU model, resources, taints and node info (what the
- * GPU Nodes summary rows and cards draw).
+ * What a GPU node object says, derived once per object. Its GPU accounting
+ * and readiness — what the index and every page's totals need — when the
+ * index is built, i.e. when the node list arrives. The rest — GPU model,
+ * resources, taints, driver, node info, the GPU Nodes card rows — for the
+ * first page of nodes with the list (primeFirstPage), for any other node on
+ * first read (a page shows eight of up to 1,000 nodes): those fields are
+ * prototype getters over one display object made once per node object.
  */
 export function nodeFacts(n) {
   let f = nodeFactCache.get(n);
   if (!f) {
-    const cap = getNodeGpuCount(n);
-    const pp = partitionsPerGpu(n);
+    f = new NodeFacts(n);
+    nodeFactCache.set(n, f);
+  }
+  return f;
+}
+
+function NodeFacts(n) {
+  const cap = getNodeGpuCount(n);
+  const pp = partitionsPerGpu(n);
+  this.node = n;
+  this.capacity = cap;
+  this.allocatable = getNodeGpuAllocatable(n);
+  this.ready = isNodeReady(n);
+  this.cordoned = get(n, ['spec', 'unschedulable'], false) === true;
+  this.partitionsPerGpu = pp;
+  this.physicalGpus = cap > 0 ? Math.ceil(cap / pp) : 0;
+  this.partitions = getNodePartitionCount(n);
+  // Overview counts nodes per partition mode (its distribution bar).
+  this.partitionMode = partitionModeKey(n);
+  // Readiness as `kubectl get nodes` words it; a cordoned node's free GPUs
+  // are not schedulable, hence a warning.
+  this.readyText = (this.ready ? 'Ready' : 'Not Ready') + (this.cordoned ? ', SchedulingDisabled' : '');
+  this.readyLevel = !this.ready ? 'error' : this.cordoned ? 'warning' : 'success';
+  this.shown = null;
+}
+
+/** The display facts of the node, made on first read. */
+NodeFacts.prototype.display = function () {
+  let d = this.shown;
+  if (!d) {
+    const n = this.node;
     const model = getNodeGpuModel(n);
     const info = get(n, ['status', 'nodeInfo'], null) || {};
-    f = {
-      capacity: cap,
-      allocatable: getNodeGpuAllocatable(n),
-      ready: isNodeReady(n),
-      cordoned: get(n, ['spec', 'unschedulable'], false) === true,
-      partitionsPerGpu: pp,
-      physicalGpus: cap > 0 ? Math.ceil(cap / pp) : 0,
-      partitions: getNodePartitionCount(n),
+    d = this.shown = {
       model: model,
       modelText: formatGpuModel(model),
       capacityResources: getGpuResources(get(n, ['status', 'capacity'], null)),
@@ -57,15 +84,39 @@ export function nodeFacts(n) {
       taints: taintsText(n),
       driverVersion: labellerValue(n, 'driver-version'),
       osText: [info.osImage || '—', info.kernelVersion || '—', info.kubeletVersion || '—'].join(' · '),
+      card: null,
     };
-    // Readiness as `kubectl get nodes` words it; a cordoned node's free GPUs
-    // are not schedulable, hence a warning.
-    f.readyText = (f.ready ? 'Ready' : 'Not Ready') + (f.cordoned ? ', SchedulingDisabled' : '');
-    f.readyLevel = !f.ready ? 'error' : f.cordoned ? 'warning' : 'success';
-    f.card = cardRows(f);
-    nodeFactCache.set(n, f);
+    d.card = cardRows(this, d);
   }
-  return f;
+  return d;
+};
+
+['model', 'modelText', 'capacityResources', 'allocatableResources', 'taints', 'driverVersion', 'osText', 'card'].forEach(function (k) {
+  Object.defineProperty(NodeFacts.prototype, k, { enumerable: true, get: function () { return this.display()[k]; } });
+});
+
+/**
+ * The display facts of the nodes the GPU Nodes page opens on — the first
+ * page in its default (name) order, SMALL_CLUSTER_NODES of them — derived
+ * with the list, as their accounting is; every other node's on first read.
+ */
+function primeFirstPage(gpuNodes) {
+  if (gpuNodes.length <= SMALL_CLUSTER_NODES) {
+    for (let i = 0; i < gpuNodes.length; i++) nodeFacts(gpuNodes[i]).display();
+    return;
+  }
+  const first = [];
+  for (let i = 0; i < gpuNodes.length; i++) {
+    const name = gpuNodes[i].metadata.name;
+    if (first.length === SMALL_CLUSTER_NODES && !(name < first[first.length - 1].metadata.name)) continue;
+    let k = first.length === SMALL_CLUSTER_NODES ? first.length - 1 : first.length;
+    while (k > 0 && first[k - 1].metadata.name > name) {
+      first[k] = first[k - 1];
+      k--;
+    }
+    first[k] = gpuNodes[i];
+  }
+  for (let i = 0; i < first.length; i++) nodeFacts(first[i]).display();
 }
 
 const hbmTexts = {};
@@ -82,13 +133,13 @@ function hbmText(phys) {
  * summary row on the same page carries readiness, model and age (the
  * reference repeats them on its card, NodesPage.tsx:69-139).
  */
-function cardRows(f) {
-  const model = f.model;
+function cardRows(f, d) {
+  const model = d.model;
   const count = f.capacity;
-  const cap = f.capacityResources;
-  const alloc = f.allocatableResources;
+  const cap = d.capacityResources;
+  const alloc = d.allocatableResources;
   const before = [];
-  if (f.taints) before.push({ name: 'Taints', value: f.taints });
+  if (d.taints) before.push({ name: 'Taints', value: d.taints });
   // One resource (the usual amd.com/gpu): its capacity and allocatable are
   // said on the device row (the reference gives them a row each,
   // NodesPage.tsx:98-113); several (partitioned resources) keep their rows.
@@ -109,10 +160,10 @@ function cardRows(f) {
     for (const k in cap) before.push({ name: formatGpuResourceName(k) + ' (capacity)', value: cap[k] });
     for (const k in alloc) before.push({ name: formatGpuResourceName(k) + ' (allocatable)', value: alloc[k] });
   }
-  if (model.computePartition || model.memoryPartition) before.push({ name: 'Partition Mode', value: f.modelText });
-  if (f.driverVersion) before.push({ name: 'amdgpu Driver', value: f.driverVersion });
+  if (model.computePartition || model.memoryPartition) before.push({ name: 'Partition Mode', value: d.modelText });
+  if (d.driverVersion) before.push({ name: 'amdgpu Driver', value: d.driverVersion });
   // OS image, kernel and kubelet on one row (the reference: a row each, NodesPage.tsx:124-126).
-  return { before: before, after: [{ name: 'OS / Kernel / Kubelet', value: f.osText }] };
+  return { before: before, after: [{ name: 'OS / Kernel / Kubelet', value: d.osText }] };
 }
 
 /** "key=value:Effect" per taint, or null (the reference models NodeSpec.taints, k8s.ts:92-122, but never shows them). */
@@ -239,6 +290,7 @@ export function buildClusterIndex(gpuNodes, gpuPods, prev) {
     });
     podsByNode.set(name, []);
   }
+  primeFirstPage(gpuNodes);
   for (let i = 0; i < gpuPods.length; i++) {
     const p = gpuPods[i];
     const f = podFacts(p);

@@ -232,7 +232,6 @@ export function createClusterStore(opts) {
   }
 
   let primedConfigs = null;
-  let primedOperatorPods = null;
 
   function build() {
     const n = gpuNodes();
@@ -242,12 +241,11 @@ export function createClusterStore(opts) {
     if (s.podError) errors.push(String(s.podError));
     if (s.asyncError) errors.push(s.asyncError);
     const pp = pluginPods();
-    // The operator's objects' facts, once per list (operatorFacts.js; the
-    // index build does the same for GPU nodes and pods).
-    if (s.deviceConfigs !== primedConfigs || pp !== primedOperatorPods) {
-      primeOperatorFacts(s.deviceConfigs, pp);
+    // The DeviceConfigs' facts, once per list (operatorFacts.js); operator
+    // pods' when a page shows their row.
+    if (s.deviceConfigs !== primedConfigs) {
+      primeOperatorFacts(s.deviceConfigs);
       primedConfigs = s.deviceConfigs;
-      primedOperatorPods = pp;
     }
     version++;
     return Object.freeze({

@@ -1,13 +1,15 @@
 /**
- * Facts of the AMD GPU Operator's objects, derived once per object when the
- * store takes the list (clusterStore.js build — as the index build derives
- * node and pod facts, ADR 015) and read by Overview and Device Plugins:
+ * Facts of the AMD GPU Operator's objects, derived once per object and read
+ * by Overview and Device Plugins:
  *
  *   * deviceConfigFacts: a DeviceConfig's status (worst operand) and its
  *     device-plugin counts, image, each operand's row (enabled, version /
- *     port, its DaemonSet's ready / desired) and node selector;
+ *     port, its DaemonSet's ready / desired) and node selector — when the
+ *     store takes the list (clusterStore.js build; a handful of objects);
  *   * operatorPodFacts: an operator pod's component, node, readiness and
- *     restarts.
+ *     restarts — on first read: the pages show one page of the operator pods
+ *     (three per GPU node: 3,000 on a 1,000-node cluster), so only the rows
+ *     shown pay for them (ADR 015).
  *
  * Reference: the same derivations run on every render of its pages
  * (DevicePluginsPage.tsx:110-182, OverviewPage.tsx:222-272).
@@ -93,8 +95,7 @@ export function operatorPodFacts(p) {
   return f;
 }
 
-/** Derive the facts of every DeviceConfig and operator pod of a snapshot (once per object). */
-export function primeOperatorFacts(deviceConfigs, operatorPods) {
+/** Derive the facts of every DeviceConfig of a snapshot (once per object); operator pods' on first read. */
+export function primeOperatorFacts(deviceConfigs) {
   for (let i = 0; i < deviceConfigs.length; i++) deviceConfigFacts(deviceConfigs[i]);
-  for (let i = 0; i < operatorPods.length; i++) operatorPodFacts(operatorPods[i]);
 }

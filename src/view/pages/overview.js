@@ -3,9 +3,8 @@
  * SURVEY C5).
  */
 
-import { getNodeGpuModel } from '../../api/amdNodes.js';
-import { formatPodGpuRequests } from '../../api/amdPods.js';
-import { podFacts } from '../../api/clusterIndex.js';
+import { formatPodGpuRequests, isPodReady } from '../../api/amdPods.js';
+import { nodeFacts, podFacts } from '../../api/clusterIndex.js';
 import { AMD_GPU_OPERATOR_NAMESPACE, BAR_COLORS, formatBytes, MI355X } from '../../api/k8sCore.js';
 import { assignmentTexts, podGpuAssignments } from '../../api/nodeSummaries.js';
 import { deviceConfigFacts, operatorPodFacts } from '../../api/operatorFacts.js';
@@ -42,10 +41,11 @@ export const OPERATOR_DOCS = 'https://instinct.docs.amd.com/projects/gpu-operato
 /**
  * Differences: the loader only replaces the page on the FIRST load — later
  * refreshes keep the data (stale-while-revalidate). It waits for the node
- * list and the DeviceConfigs only: the node, capacity and DeviceConfig
- * sections render while the all-namespaces pod list is still arriving (tens
- * of MB on a large cluster), and the pod-derived ones (in use, workloads,
- * active pods, operator pods) show a loader until it is in — the reference
+ * list only: the node and capacity sections render while the DeviceConfig
+ * request (up to its timeout when the CRD is slow or absent) and the
+ * all-namespaces pod list (tens of MB on a large cluster) are still out; the
+ * DeviceConfig section and the pod-derived ones (in use, workloads, active
+ * pods, operator pods) show a loader until theirs is in — the reference
  * shows a full-page Loader until every list is in (OverviewPage.tsx:67-69,
  * IntelGpuDataContext.tsx:214). Aggregates come from the store's memoised
  * index. In-use counts GPUs held by bound, non-terminated pods (the
@@ -56,15 +56,16 @@ export const OPERATOR_DOCS = 'https://instinct.docs.amd.com/projects/gpu-operato
  */
 export function overviewView(ctx, opts) {
   const now = nowOf(opts);
-  if (nodesPending(ctx) || crdPending(ctx)) return page(null, null, [loader('Loading ' + BRAND + ' data...')]);
+  if (nodesPending(ctx)) return page(null, null, [loader('Loading ' + BRAND + ' data...')]);
   const podsPend = podsPending(ctx);
   const opPend = pluginPodsPending(ctx);
+  const crdPend = crdPending(ctx);
   const owners = podsPend && opts && opts.metrics && Array.isArray(opts.metrics.gpus) ? opts.metrics : null;
   const items = memo(
     'overview',
     [ctx.deviceConfigs, ctx.pluginPods, ctx.pluginInstalled, ctx.crdAvailable, ctx.gpuNodes, ctx.gpuPods, ctx.index, ctx.error, podsPend, opPend,
-      owners && owners.gpus],
-    function () { return overviewItems(ctx, now, podsPend, opPend, owners); },
+      crdPend, owners && owners.gpus],
+    function () { return overviewItems(ctx, now, podsPend, opPend, owners, crdPend); },
     now
   );
   return page(BRAND + ' — Overview', refreshButton('Refresh AMD GPU data', ctx.refreshing), items);
@@ -77,8 +78,7 @@ export function partitionModeDistribution(gpuNodes) {
   const counts = {};
   const order = [];
   for (let i = 0; i < gpuNodes.length; i++) {
-    const m = getNodeGpuModel(gpuNodes[i]);
-    const k = (m.computePartition || 'SPX') + '/' + (m.memoryPartition || 'NPS1');
+    const k = nodeFacts(gpuNodes[i]).partitionMode;
     if (!(k in counts)) {
       counts[k] = 0;
       order.push(k);
@@ -132,15 +132,16 @@ export function overviewPodsPreview(metrics) {
   });
 }
 
-function overviewItems(ctx, now, podsPend, opPend, owners) {
+function overviewItems(ctx, now, podsPend, opPend, owners, crdPend) {
   const items = [];
   const t = ctx.index.totals;
 
   if (ctx.error) items.push(errorSection(ctx.error));
 
-  // Operator pods come from the pod list (or the plugin-pod requests): while
-  // they load, "not detected" is not known yet.
-  if (!ctx.pluginInstalled && !opPend) {
+  // Operator pods come from the pod list (or the plugin-pod requests), the
+  // DeviceConfigs from their request: while either loads, "not detected" is
+  // not known yet.
+  if (!ctx.pluginInstalled && !opPend && !crdPend) {
     items.push(
       section('Plugin Not Detected', [
         kv([
@@ -152,7 +153,9 @@ function overviewItems(ctx, now, podsPend, opPend, owners) {
     );
   }
 
-  if (!ctx.crdAvailable && ctx.pluginInstalled) {
+  if (crdPend) {
+    items.push(loader('Loading DeviceConfigs...'));
+  } else if (!ctx.crdAvailable && ctx.pluginInstalled) {
     items.push(
       section('Notice', [
         kv([
@@ -229,12 +232,13 @@ export const OVERVIEW_PLUGIN_PODS = 10;
  * thousands of rows on a large cluster.
  */
 function overviewPluginPods(pods, now) {
-  const notReady = chunkedFilter('ov-plugin-not-ready', pods, function (p) { return !operatorPodFacts(p).ready; });
+  // Readiness of every pod (the not-ready count), the other facts of the rows shown only.
+  const notReady = chunkedFilter('ov-plugin-not-ready', pods, function (p) { return !isPodReady(p); });
   let shown = pods;
   if (pods.length > OVERVIEW_PLUGIN_PODS) {
     shown = notReady.slice(0, OVERVIEW_PLUGIN_PODS);
     for (let i = 0; i < pods.length && shown.length < OVERVIEW_PLUGIN_PODS; i++) {
-      if (operatorPodFacts(pods[i]).ready) shown.push(pods[i]);
+      if (isPodReady(pods[i])) shown.push(pods[i]);
     }
   }
   const blocks = [

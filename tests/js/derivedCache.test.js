@@ -6,7 +6,7 @@
  * stays with its objects.
  */
 import { derivedCache, resetDerivedCaches } from '../../src/api/derivedCache.js';
-import { nodeFacts, podContainerLines } from '../../src/api/clusterIndex.js';
+import { buildClusterIndex, nodeFacts, podContainerLines } from '../../src/api/clusterIndex.js';
 import { nodePowerKeys, ownersByNode, podGpuAssignments, primeSnapshot } from '../../src/api/nodeSummaries.js';
 import { deviceConfigFacts, operatorPodFacts } from '../../src/api/operatorFacts.js';
 import { linkFacts } from '../../src/api/topology.js';
@@ -69,7 +69,26 @@ describe('derivedCache', () => {
     expect(links).toEqual({ fullMesh: true, linksPerGpu: 7, stats: { links: 56, meanGBs: 10, maxGBs: 10 }, gpuStats: { gpus: 8, meanGBs: 70, maxGBs: 70 } });
   });
 
-  it('the store derives the operator objects\' facts when it takes their lists', async () => {
+  it('the index derives every node\'s accounting with the list, display facts only for the first page in name order', () => {
+    const nodes = [];
+    for (let i = 0; i < 20; i++) nodes.push(makeGpuNode('node-' + String(19 - i).padStart(2, '0')));
+    buildClusterIndex(nodes, []);
+    const primed = nodes.filter((n) => nodeFacts(n).shown !== null).map((n) => n.metadata.name).sort();
+    expect(primed).toEqual(['node-00', 'node-01', 'node-02', 'node-03', 'node-04', 'node-05', 'node-06', 'node-07']);
+    expect(nodes.every((n) => nodeFacts(n).capacity === 8)).toBe(true);
+    // any other node's display facts on first read, kept with its object (not reset with the memo)
+    const late = nodes.find((n) => n.metadata.name === 'node-15');
+    expect(nodeFacts(late).modelText).toBe('MI355X');
+    const shown = nodeFacts(late).shown;
+    clearViewMemo();
+    expect(nodeFacts(late).shown).toBe(shown);
+    // a small cluster: every node
+    const few = [makeGpuNode('b'), makeGpuNode('a')];
+    buildClusterIndex(few, []);
+    expect(few.every((n) => nodeFacts(n).shown !== null)).toBe(true);
+  });
+
+  it('the store derives the DeviceConfigs\' facts when it takes their list; an operator pod\'s when a row reads them', async () => {
     const { createClusterStore } = await import('../../src/api/clusterStore.js');
     const dc = makeDeviceConfig('gpu-operator');
     const op = makePluginPod('dp-0');
@@ -81,6 +100,7 @@ describe('derivedCache', () => {
     expect(ctx.deviceConfigs).toEqual([dc]);
     const f = deviceConfigFacts(ctx.deviceConfigs[0]);
     const pf = operatorPodFacts(op);
+    expect(operatorPodFacts(makePluginPod('dp-1'))).not.toBe(pf);
     clearViewMemo();
     expect(deviceConfigFacts(ctx.deviceConfigs[0])).toBe(f);
     expect(operatorPodFacts(op)).toBe(pf);
