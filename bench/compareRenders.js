@@ -130,8 +130,9 @@ async function measure(url, c, R, ref) {
     gpuNodes: refInfo.gpuNodes, gpuPods: refInfo.gpuPods, chips: refInfo.chips, reps: reps, warm: warm,
     calibration: { rows: CALIBRATION_ROWS, elements: calHere.elements, referenceRealmMs: spread(calRef.times.slice(5)).p50,
       driverRealmMs: spread(calHere.times.slice(5)).p50 } };
-  for (let p = 0; p < PAGES.length; p++) {
-    const page = PAGES[p];
+  const pages = Array.isArray(c.pages) && c.pages.length ? PAGES.filter(function (x) { return c.pages.indexOf(x) >= 0; }) : PAGES;
+  for (let p = 0; p < pages.length; p++) {
+    const page = pages[p];
     const mstatePage = page === 'metrics' ? s.pageMstate() : s.mstate();
     let ctx = snap;
     function referenceOnce() {

@@ -195,9 +195,17 @@ export const COMPUTE_PARTITIONS = Object.freeze({ SPX: 1, DPX: 2, QPX: 4, CPX: 8
 
 /** Devices per physical GPU on this node (1 unless the labeller reports a partition mode). */
 export function partitionsPerGpu(node) {
-  const labels = labelsOf(node);
-  const cp = labels[LABEL_COMPUTE_PARTITION] || labellerValue(node, 'compute-partitioning-mode');
+  return partitionsOfMode(computePartitionLabel(node));
+}
+
+/** Devices per board for a compute partition label value (null: SPX). */
+export function partitionsOfMode(cp) {
   return (cp && COMPUTE_PARTITIONS[String(cp).toUpperCase()]) || 1;
+}
+
+/** The node's compute partition mode label (the GPU operator's, else the labeller's), or null. */
+export function computePartitionLabel(node) {
+  return labelsOf(node)[LABEL_COMPUTE_PARTITION] || labellerValue(node, 'compute-partitioning-mode');
 }
 
 /**
@@ -205,11 +213,10 @@ export function partitionsPerGpu(node) {
  * unlabelled (the same labels getNodeGpuModel reads, without the rest of the
  * model).
  */
-export function partitionModeKey(node) {
-  const labels = labelsOf(node);
-  const cp = labels[LABEL_COMPUTE_PARTITION] || labellerValue(node, 'compute-partitioning-mode');
-  const mp = labels[LABEL_MEMORY_PARTITION] || labellerValue(node, 'memory-partitioning-mode');
-  return (cp ? String(cp).toUpperCase() : 'SPX') + '/' + (mp ? String(mp).toUpperCase() : 'NPS1');
+export function partitionModeKey(node, cp) {
+  const c = cp === undefined ? computePartitionLabel(node) : cp;
+  const mp = labelsOf(node)[LABEL_MEMORY_PARTITION] || labellerValue(node, 'memory-partitioning-mode');
+  return (c ? String(c).toUpperCase() : 'SPX') + '/' + (mp ? String(mp).toUpperCase() : 'NPS1');
 }
 
 /** MI355X boards on the node: devices ÷ partitions per board. */
@@ -236,12 +243,16 @@ export function isNodeReady(node) {
   return false;
 }
 
+/** [current, legacy] label key of each labeller property, made once. */
+const LABELLER_KEYS = Object.create(null);
+
 /** Look up a labeller property under the current or the legacy prefix. */
 export function labellerValue(node, prop) {
   const labels = labelsOf(node);
-  const v = labels[AMD_LABELLER_PREFIX + prop];
+  const keys = LABELLER_KEYS[prop] || (LABELLER_KEYS[prop] = [AMD_LABELLER_PREFIX + prop, AMD_LABELLER_LEGACY_PREFIX + prop]);
+  const v = labels[keys[0]];
   if (v !== undefined) return v;
-  const legacy = labels[AMD_LABELLER_LEGACY_PREFIX + prop];
+  const legacy = labels[keys[1]];
   return legacy !== undefined ? legacy : null;
 }
 

@@ -296,13 +296,19 @@ export function filterAmdGpuPluginPods(items) {
  * to namespace/name so uid-less fixtures are kept (fixes reference Q5).
  */
 export function dedupePods(pods) {
-  const seen = {};
+  const uids = new Set();
+  const names = new Set();
   const out = [];
   for (let i = 0; i < pods.length; i++) {
     const m = pods[i].metadata || {};
-    const key = m.uid ? 'u:' + m.uid : 'n:' + (m.namespace || '') + '/' + (m.name || '');
-    if (seen[key]) continue;
-    seen[key] = true;
+    if (m.uid) {
+      if (uids.has(m.uid)) continue;
+      uids.add(m.uid);
+    } else {
+      const key = (m.namespace || '') + '/' + (m.name || '');
+      if (names.has(key)) continue;
+      names.add(key);
+    }
     out.push(pods[i]);
   }
   return out;

@@ -17,8 +17,9 @@ import {
   getNodePartitionCount,
   isNodeReady,
   labellerValue,
+  computePartitionLabel,
   partitionModeKey,
-  partitionsPerGpu,
+  partitionsOfMode,
 } from './amdNodes.js';
 import { containerGpuEntries, getPodGpuCount, gpuContainers, gpuInitContainers, podPhase } from './amdPods.js';
 import { derivedCache } from './derivedCache.js';
@@ -51,7 +52,8 @@ export function nodeFacts(n) {
 
 function NodeFacts(n) {
   const cap = getNodeGpuCount(n);
-  const pp = partitionsPerGpu(n);
+  const cp = computePartitionLabel(n);
+  const pp = partitionsOfMode(cp);
   this.node = n;
   this.capacity = cap;
   this.allocatable = getNodeGpuAllocatable(n);
@@ -61,7 +63,7 @@ function NodeFacts(n) {
   this.physicalGpus = cap > 0 ? Math.ceil(cap / pp) : 0;
   this.partitions = getNodePartitionCount(n);
   // Overview counts nodes per partition mode (its distribution bar).
-  this.partitionMode = partitionModeKey(n);
+  this.partitionMode = partitionModeKey(n, cp);
   // Readiness as `kubectl get nodes` words it; a cordoned node's free GPUs
   // are not schedulable, hence a warning.
   this.readyText = (this.ready ? 'Ready' : 'Not Ready') + (this.cordoned ? ', SchedulingDisabled' : '');
@@ -148,22 +150,26 @@ function cardRows(f, d) {
   if (count > 0) {
     const phys = f.physicalGpus;
     const devices = phys !== count ? count + ' (' + phys + ' × ' + model.shortName + ' in ' + model.computePartition + ')' : String(count);
+    // The devices and the HBM they carry on one row (a card is a row less to mount).
     before.push({
-      name: 'GPU Devices (amd.com/gpu)',
-      value: single
+      name: 'GPU Devices (amd.com/gpu) · HBM',
+      value: (single
         ? devices + ' · capacity ' + cap[AMD_GPU_RESOURCE] + ', allocatable ' + (alloc[AMD_GPU_RESOURCE] !== undefined ? alloc[AMD_GPU_RESOURCE] : '—')
-        : devices,
+        : devices) + ' · HBM ' + hbmText(phys) + ' (' + phys + ' × ' + model.vram + ')',
     });
-    before.push({ name: 'HBM', value: hbmText(phys) + ' (' + phys + ' × ' + model.vram + ')' });
   }
   if (!single || count === 0) {
     for (const k in cap) before.push({ name: formatGpuResourceName(k) + ' (capacity)', value: cap[k] });
     for (const k in alloc) before.push({ name: formatGpuResourceName(k) + ' (allocatable)', value: alloc[k] });
   }
   if (model.computePartition || model.memoryPartition) before.push({ name: 'Partition Mode', value: d.modelText });
-  if (d.driverVersion) before.push({ name: 'amdgpu Driver', value: d.driverVersion });
-  // OS image, kernel and kubelet on one row (the reference: a row each, NodesPage.tsx:124-126).
-  return { before: before, after: [{ name: 'OS / Kernel / Kubelet', value: d.osText }] };
+  // The node's software on one row: OS image, kernel, kubelet (the reference: a row each, NodesPage.tsx:124-126)
+  // and the amdgpu driver the labeller reports.
+  return {
+    before: before,
+    after: [d.driverVersion ? { name: 'OS / Kernel / Kubelet / amdgpu', value: d.osText + ' · amdgpu ' + d.driverVersion }
+      : { name: 'OS / Kernel / Kubelet', value: d.osText }],
+  };
 }
 
 /** "key=value:Effect" per taint, or null (the reference models NodeSpec.taints, k8s.ts:92-122, but never shows them). */

@@ -231,6 +231,8 @@ export function matrixCaption(b: MatrixBlock): string;
 export function matrixSummary(b: MatrixBlock): string;
 /** Text of one matrix cell: "Σ N" for a GPU's total, GB/s on a link, `xgmiMark` on an unmeasured xGMI link. */
 export function matrixCellText(c: XgmiCell, xgmiMark: string): string;
+/** matrixCaption(b) + matrixSummary(b), formatted once per distinct content (the facts; the statistics object). */
+export function matrixLine(b: MatrixBlock): string;
 /** "namespace/pod" or "free". */
 export function slotOwner(s: GpuSlot): string;
 /** Owners in runs: "GPU 0–3 ml/train-a · GPU 4–7 free". */

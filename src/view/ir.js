@@ -255,6 +255,34 @@ export function matrixSummary(b) {
   return gs ? ' · measured per GPU: max ' + gs.maxGBs.toFixed(0) + ', mean ' + gs.meanGBs.toFixed(0) + ' GB/s over ' + gs.gpus + ' GPUs' : '';
 }
 
+const captionCache = new Map();
+const summaryCache = typeof WeakMap === 'function' ? new WeakMap() : null;
+
+/**
+ * matrixCaption(b) + matrixSummary(b), the line a matrix shows open or
+ * closed, formatted once per distinct content: the caption per combination
+ * of its facts, the summary per statistics object (topology.js linkFacts
+ * keeps one per link map). A hand-made block (no facts) is formatted as is.
+ */
+export function matrixLine(b) {
+  if (b.linksPerGpu === undefined) return matrixCaption(b) + matrixSummary(b);
+  const key = (b.measuredTopology ? 1 : 0) + (b.measuredThroughput ? 2 : 0) + (b.throughputPerGpu ? 4 : 0) + (b.fullMesh ? 8 : 0) +
+    '|' + b.linksPerGpu + '|' + b.linkGBs + '|' + b.ringBusGBs;
+  let caption = captionCache.get(key);
+  if (caption === undefined) {
+    caption = matrixCaption(b);
+    captionCache.set(key, caption);
+  }
+  const st = b.linkStats || b.gpuStats;
+  if (!st || !summaryCache) return caption + (st ? matrixSummary(b) : '');
+  let summary = summaryCache.get(st);
+  if (summary === undefined) {
+    summary = matrixSummary(b);
+    summaryCache.set(st, summary);
+  }
+  return caption + summary;
+}
+
 function gridLinkStats(m) {
   let n = 0;
   let sum = 0;

@@ -31,7 +31,7 @@
  */
 
 import { BAR_COLORS, formatWatts } from '../api/k8sCore.js';
-import { matrixCaption, matrixCellText, matrixSummary, pagerIdle, pagerText, slotOwner, slotsText } from './ir.js';
+import { matrixCaption, matrixCellText, matrixLine, pagerIdle, pagerText, slotOwner, slotsText } from './ir.js';
 
 /** CommonComponents the renderer needs (reference src/components/OverviewPage.tsx:8-16). */
 export const REQUIRED_COMPONENTS = [
@@ -64,7 +64,8 @@ export const PLUGIN_CSS = [
   '.amdgpu-slots{margin-top:12px;padding-top:18px;font-size:12px;background-size:100% 12px;background-repeat:no-repeat;' +
     'background-position:left top}',
   '.amdgpu-mx{margin-top:12px;overflow-x:auto}',
-  '.amdgpu-mx-closed{margin-top:12px;font-size:13px;color:var(--mui-palette-text-secondary)}',
+  '.amdgpu-mx-closed{display:block;margin-top:12px;padding:0;border:0;background:none;font:inherit;font-size:13px;text-align:left;' +
+    'cursor:pointer;color:var(--mui-palette-text-secondary)}',
   '.amdgpu-mx table{border-collapse:collapse;font-size:11px}',
   '.amdgpu-mx th{padding:2px 6px}',
   '.amdgpu-mx tbody th{text-align:right}',
@@ -264,19 +265,19 @@ export function createRenderer(React, CC) {
     const st = React.useState(b.open !== false);
     const open = st[0];
     const setOpen = st[1];
-    const toggle = h('button', {
-      'aria-expanded': open ? 'true' : 'false', className: BUTTON_CLASS,
-      onClick: function () { setOpen(!open); },
-    }, open ? 'Hide xGMI matrix' : 'Show xGMI matrix');
+    const flip = function () { setOpen(!open); };
     if (!open) {
-      return h('div', { 'data-matrix': 'closed', className: 'amdgpu-mx-closed' },
-        matrixCaption(b) + matrixSummary(b) + ' ', toggle);
+      // Closed (a GPU Nodes card): the summary line is itself the toggle — one element.
+      return h('button', {
+        'data-matrix': 'closed', 'aria-expanded': 'false', className: 'amdgpu-mx-closed', onClick: flip,
+      }, matrixLine(b) + ' · Show xGMI matrix');
     }
+    const toggle = h('button', { 'aria-expanded': 'true', className: BUTTON_CLASS, onClick: flip }, 'Hide xGMI matrix');
     const m = b.matrix;
     return h(
       'div',
       { 'data-matrix': 'open', className: 'amdgpu-mx' },
-      h('div', { className: 'amdgpu-muted' }, matrixCaption(b) + matrixSummary(b) + ' ', toggle),
+      h('div', { className: 'amdgpu-muted' }, matrixLine(b) + ' ', toggle),
       h(
         'table',
         null,

@@ -58,7 +58,7 @@ describe('derivedCache', () => {
     clearViewMemo();
     expect(nodeFacts(node)).toBe(f);
     expect(nodeReadyCell(node)).toBe(ready); // one cell per wording, from the node's facts
-    expect(f.card.after).toEqual([{ name: 'OS / Kernel / Kubelet', value: f.osText }]);
+    expect(f.card.after).toEqual([{ name: 'OS / Kernel / Kubelet / amdgpu', value: f.osText + ' · amdgpu ' + f.driverVersion }]);
     expect(nodePowerKeys(m)).toBe(power);
     expect(ownersByNode(m)).toBe(owners);
     expect(podGpuAssignments(m)).toBe(assign);

@@ -319,11 +319,10 @@ describe('nodesView', () => {
     const ctx = makeContext({ nodes: [makeGpuNode('g0')], pods: [makeGpuPod('a', { node: 'g0', gpus: 2 })] });
     const s = findSection(nodesView(ctx, opts), 'g0');
     // one amd.com/gpu resource: capacity and allocatable on the device row; OS, kernel and kubelet on one row
-    expect(rowValue(s, 'GPU Devices (amd.com/gpu)')).toBe('8 · capacity 8, allocatable 8');
-    expect(rowValue(s, 'HBM')).toBe('2.25 TiB (8 × 288G)');
+    expect(rowValue(s, 'GPU Devices (amd.com/gpu) · HBM')).toBe('8 · capacity 8, allocatable 8 · HBM 2.25 TiB (8 × 288G)');
     expect(rowValue(s, 'GPU Workload Pods')).toBe('a');
     expect(rowValue(s, 'GPU (capacity)')).toBeUndefined();
-    expect(rowValue(s, 'OS / Kernel / Kubelet')).toContain(' · v1.31.2');
+    expect(rowValue(s, 'OS / Kernel / Kubelet / amdgpu')).toBe('Ubuntu 24.04 LTS · 6.8.0-45-generic · v1.31.2 · amdgpu 6.12.12');
   });
   it('adds per-GPU slots and the xGMI matrix to each card', () => {
     const ctx = makeContext({ nodes: [makeGpuNode('g0')], pods: [makeGpuPod('a', { node: 'g0', gpus: 3 })] });

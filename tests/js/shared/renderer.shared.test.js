@@ -163,15 +163,18 @@ describe('shared: blocks (' + tier + ')', () => {
     expect(r.byTag('td')).toHaveLength(0);
     expect(r.text()).toContain('measured: max 40, mean 40 GB/s over 56 links');
     const toggle = () => r.byTag('button')[0];
+    // closed: the summary line is the toggle (one element)
+    expect(r.byTag('button')).toHaveLength(1);
     expect(r.attr(toggle(), 'aria-expanded')).toBe('false');
-    expect(r.textOf(toggle())).toBe('Show xGMI matrix');
+    expect(r.textOf(toggle())).toMatch(/^xGMI topology \(.* · Show xGMI matrix$/);
     r.click(toggle());
     expect(r.byTag('td')).toHaveLength(64);
     expect(r.byTag('td').filter((n) => r.textOf(n) === '40')).toHaveLength(56);
     expect(r.attr(toggle(), 'aria-expanded')).toBe('true');
+    expect(r.textOf(toggle())).toBe('Hide xGMI matrix');
     r.click(toggle());
     expect(r.byTag('td')).toHaveLength(0);
-    expect(r.textOf(toggle())).toBe('Show xGMI matrix');
+    expect(r.textOf(toggle())).toMatch(/ · Show xGMI matrix$/);
     r.unmount();
   });
 

@@ -42,7 +42,7 @@ PAGES = [("overview", "Overview"), ("devicePlugins", "Device Plugins"), ("nodes"
          ("metrics", "Metrics")]
 
 
-def measure(n: int, reference: str, reps: int, warm: int) -> dict:
+def measure(n: int, reference: str, reps: int, warm: int, pages=None) -> dict:
     from headlamp_intel_gpu_plugin_amd.sim.serve import ControlPlaneProcess
     from headlamp_intel_gpu_plugin_amd.utils.nodebridge import Driver
     from headlamp_intel_gpu_plugin_amd.utils.reactumd import PROD_BUILDS, umd_dir
@@ -55,7 +55,7 @@ def measure(n: int, reference: str, reps: int, warm: int) -> dict:
                      env={"PATH": os.environ.get("PATH", "/usr/bin:/bin")})
         try:
             r = drv.call("refRender", referenceDir=reference, umdDir=umd, reps=reps, warm=warm, allowReferenceExec=True,
-                         timeout=3000)
+                         pages=pages, timeout=3000)
         finally:
             drv.close()
     if r.get("error"):
@@ -132,6 +132,7 @@ def main() -> int:
     p.add_argument("--warm", type=int, default=50)
     p.add_argument("--runs", type=int, default=3, help="driver processes per size, their samples pooled")
     p.add_argument("--reference", default="/root/reference")
+    p.add_argument("--pages", default=None, help="comma-separated page keys (default: all five); a partial run prints no table")
     p.add_argument("--out", default=os.path.join(ROOT, "profiles", "r5_render_compare"))
     p.add_argument("--allow-reference-exec", action="store_true",
                    help="run the reference's page components (untrusted) in the isolated worker process")
@@ -145,7 +146,16 @@ def main() -> int:
     for s in args.sizes.split(","):
         n = int(s)
         t = time.time()
-        r = pooled([measure(n, args.reference, args.reps, args.warm) for _ in range(max(1, args.runs))])
+        pages = args.pages.split(",") if args.pages else None
+        r = pooled([measure(n, args.reference, args.reps, args.warm, pages) for _ in range(max(1, args.runs))])
+        if pages:
+            for k, v in r["pages"].items():
+                a, ref = v["amd"], v["reference"]
+                print(f"[render_compare] {n} nodes {k}: ref {ref['mountMs']:.3f} [{ref['mountQ1']:.3f}-{ref['mountQ3']:.3f}] "
+                      f"({ref['elements']} el) new {a['mountMs']:.3f} [{a['mountQ1']:.3f}-{a['mountQ3']:.3f}] ({a['elements']} el) "
+                      f"{verdict(a, ref)} vm {a['vmBuildMs']:.3f} react {a['reactOnlyMs']:.3f}; cal {r.get('calibration')}",
+                      file=sys.stderr, flush=True)
+            continue
         rows.append((n, r))
         print(f"[render_compare] {n} nodes: {time.time() - t:.1f} s", file=sys.stderr, flush=True)
         with open(args.out + ".json", "w") as f:
