@@ -10,4 +10,4 @@ package holds everything around it that runs outside the browser:
 * ``parallel`` — one-process-per-GPU launch helpers for the benchmark;
 * ``utils``    — statistics and the Node.js bridge.
 """
-__version__ = "0.5.0"
+__version__ = "0.6.0"
