@@ -40,10 +40,17 @@ export function workerCommand() {
   return ['unshare', ['--net', '--mount', '--propagation', 'private', '--', 'sh', '-c', LOCKDOWN, process.execPath, boot]];
 }
 
+/** How long one call may take before the worker is killed (ms): building the realm, and anything after it. */
+export const INIT_TIMEOUT_MS = 120000;
+export const CALL_TIMEOUT_MS = 60000;
+
 /**
- * Start the worker → {call(cmd, fields): Promise, close()}. A start that
- * fails (no unshare / setpriv, or no permission for them) rejects the first
- * call with the process's stderr.
+ * Start the worker → {call(cmd, fields, timeoutMs): Promise, close()}. A start
+ * that fails (no unshare / setpriv, or no permission for them) rejects the
+ * first call with the process's stderr. A call not answered in time (a
+ * reference render that never returns, say) kills the worker and rejects
+ * every call waiting and every later one: the realm's own timeout covers its
+ * module code only, not the renders React runs afterwards.
  */
 export function startWorker() {
   const cmd = workerCommand();
@@ -64,25 +71,32 @@ export function startWorker() {
       const w = waiting.get(m.id);
       if (!w) continue;
       waiting.delete(m.id);
+      clearTimeout(w.timer);
       if (m.ok) w.resolve(m.result);
       else w.reject(new Error('reference worker: ' + m.error));
     }
   });
+  child.stdin.on('error', function () {}); // a killed worker's pipe: the call is already rejected
   child.stderr.setEncoding('utf8');
   child.stderr.on('data', function (c) { err = (err + c).slice(-4000); });
   function fail(why) {
-    dead = new Error('reference worker ' + why + (err ? ': ' + err.trim() : ''));
-    waiting.forEach(function (w) { w.reject(dead); });
+    if (!dead) dead = new Error('reference worker ' + why + (err ? ': ' + err.trim() : ''));
+    waiting.forEach(function (w) { clearTimeout(w.timer); w.reject(dead); });
     waiting.clear();
   }
   child.on('error', function (e) { fail('did not start (' + e.message + ')'); });
   child.on('exit', function (code, sig) { fail('exited (' + (sig || code) + ')'); });
   return {
-    call: function (cmd, fields) {
+    call: function (cmd, fields, timeoutMs) {
       if (dead) return Promise.reject(dead);
       const id = ++next;
+      const limit = timeoutMs || (cmd === 'init' ? INIT_TIMEOUT_MS : CALL_TIMEOUT_MS);
       return new Promise(function (resolve, reject) {
-        waiting.set(id, { resolve: resolve, reject: reject });
+        const timer = setTimeout(function () {
+          fail('timed out after ' + limit + ' ms on ' + cmd);
+          child.kill('SIGKILL');
+        }, limit);
+        waiting.set(id, { resolve: resolve, reject: reject, timer: timer });
         child.stdin.write(JSON.stringify(Object.assign({ id: id, cmd: cmd }, fields || {})) + '\n');
       });
     },

@@ -128,6 +128,11 @@ const [fixture, umd] = process.argv.slice(2);
   out.cycle = await w.call('cycle', { page: 'metrics', waitText: 'GPU Power Summary', mustShow: 'Intel GPU' });
   out.audit = await w.call('audit');
   await w.close();
+  // a call answered late kills the worker: this one, and every later call, rejects
+  const w2 = startWorker();
+  out.late = await w2.call('init', realmInit(fixture, umd), 1).then(() => 'answered', (e) => e.message);
+  out.after = await w2.call('probe').then(() => 'answered', (e) => e.message);
+  await w2.close();
   process.stdout.write(JSON.stringify(out));
 })().catch((e) => { console.error(e.stack); process.exit(1); });
 """
@@ -144,7 +149,7 @@ def _can_isolate():
 def test_the_reference_worker_has_no_network_and_writes_nothing(tmp_path):
     """The process bench/refIsolated.js starts for the reference's pages: its writes fail on every mount it tries
     (read-only namespace, RLIMIT_FSIZE 0), its TCP connection out fails (empty network namespace), and its realm
-    still renders a page and audits clean. Skipped where the container allows no namespaces (ADR 014)."""
+    still renders a page and audits clean. A call answered late kills the worker and fails every later call. Skipped where the container allows no namespaces (ADR 014)."""
     import json
 
     import pytest
@@ -164,5 +169,7 @@ def test_the_reference_worker_has_no_network_and_writes_nothing(tmp_path):
     assert out["probe"]["connect"] in ("ENETUNREACH", "EHOSTUNREACH", "ENETDOWN"), out["probe"]
     assert out["cycle"]["elements"] > 0
     assert out["audit"]["leaks"] == []
+    assert out["late"].startswith("reference worker timed out after 1 ms on init"), out["late"]
+    assert out["after"] == out["late"]
     for f in ("/tmp/.ref-probe", "/dev/shm/.ref-probe"):
         assert not os.path.exists(f)
